@@ -1,0 +1,42 @@
+# Build of the product library (HIP, gfx950) and the CPU oracle (test infrastructure).
+#   make            -> orb_slam3_comments_ghr_amd/liborbslam3_amd.so + oracle/liboracle.so
+HIPCC ?= hipcc
+ARCH ?= gfx950
+PKG = orb_slam3_comments_ghr_amd
+CSRC = $(PKG)/csrc
+LIB = $(PKG)/liborbslam3_amd.so
+OBJDIR = build/obj
+HIPFLAGS = --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-function
+# bit-exact float geometry in the matcher: no FMA contraction in those translation units
+EXACT = -ffp-contract=off
+HDRS = include/osg.h include/osg_ba.h $(CSRC)/osg_internal.h
+
+OBJS = $(OBJDIR)/runtime.o $(OBJDIR)/hamming.o $(OBJDIR)/match.o $(OBJDIR)/pose.o $(OBJDIR)/ba.o
+
+all: $(LIB) oracle
+
+$(OBJDIR):
+	mkdir -p $(OBJDIR)
+
+$(OBJDIR)/runtime.o: $(CSRC)/runtime.hip $(HDRS) | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+$(OBJDIR)/hamming.o: $(CSRC)/hamming.hip $(HDRS) | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) $(EXACT) -c $< -o $@
+$(OBJDIR)/match.o: $(CSRC)/match.hip $(HDRS) $(CSRC)/match_common.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) $(EXACT) -c $< -o $@
+$(OBJDIR)/pose.o: $(CSRC)/pose.hip $(HDRS) $(CSRC)/ba_common.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+$(OBJDIR)/ba.o: $(CSRC)/ba.hip $(HDRS) $(CSRC)/ba_common.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf build $(LIB)
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean

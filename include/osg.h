@@ -1,0 +1,226 @@
+/*
+ * osg.h — C ABI of the MI355X-native ORB-SLAM3 matching + bundle-adjustment hot path.
+ *
+ * This is the drop-in boundary.  Every entry point replaces one reference operator
+ * (Herong1212/ORB_SLAM3_comments_ghr, cited as ref:<file>:<line>) and takes plain
+ * pointers and sizes only — no torch, OpenCV, Eigen or Sophus types cross it.
+ *
+ *   osg_descriptor_distance*   ← ORBmatcher::DescriptorDistance       ref:src/ORBmatcher.cc:2388-2408
+ *   osg_hamming_top2*          ← the top-2 candidate loop shared by every matcher
+ *                                (brute force over a train set, semantics of
+ *                                ref:src/ORBmatcher.cc:327-355: strict '<', first index wins ties,
+ *                                sentinel distance 256, best index -1)
+ *   osg_search_by_bow_kf_f     ← ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&)
+ *                                ref:src/ORBmatcher.cc:262-496
+ *   osg_search_by_bow_kf_kf    ← ORBmatcher::SearchByBoW(KeyFrame*, KeyFrame*, vector<MapPoint*>&)
+ *                                ref:src/ORBmatcher.cc:890-1043
+ *   osg_search_by_projection_mps   ← ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th, bFarPoints, thFar)
+ *                                ref:src/ORBmatcher.cc:44-242
+ *   osg_search_by_projection_last  ← ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono)
+ *                                ref:src/ORBmatcher.cc:1957-2191
+ *   osg_search_by_projection_kf    ← ORBmatcher::SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist)
+ *                                ref:src/ORBmatcher.cc:2203-2330
+ *   osg_pose_optimization*     ← Optimizer::PoseOptimization(Frame*)   ref:src/Optimizer.cc:71-420
+ *   osg_local_bundle_adjustment← Optimizer::LocalBundleAdjustment(...) ref:src/Optimizer.cc:1758-2206
+ *                                (graph already gathered; g2o LM + BlockSolver_6_3 inner loop on device)
+ *
+ * Conventions
+ *  - Functions return >= 0 on success (a match / inlier count where the reference returns one)
+ *    or a negative OSG_E_* code.  Nothing throws across the ABI.
+ *  - Host-pointer entry points copy inputs to device memory owned by the context, run, and copy
+ *    the outputs back (the reference hands host memory in).  *_dev entry points take device
+ *    pointers (inputs already resident in HBM) and run asynchronously on the context's stream.
+ *  - One osg_ctx per host thread (the reference calls matchers concurrently from Tracking,
+ *    LocalMapping and LoopClosing).  A context owns a HIP stream and pooled device scratch.
+ *  - Descriptors are ORB rows: 32 bytes, row-major, as cv::Mat CV_8UC1 rows
+ *    (ref:src/ORBextractor.cc:1538), read as 8 x int32 (ref:src/ORBmatcher.cc:2390-2391).
+ */
+#ifndef OSG_H
+#define OSG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- constants (ref:src/ORBmatcher.cc:34-36, ref:include/Frame.h:44-45) ------------------- */
+#define OSG_TH_HIGH 100
+#define OSG_TH_LOW 50
+#define OSG_HISTO_LENGTH 30
+#define OSG_GRID_COLS 64
+#define OSG_GRID_ROWS 48
+#define OSG_GRID_CELLS (OSG_GRID_COLS * OSG_GRID_ROWS)
+#define OSG_DESC_BYTES 32
+
+/* ---- error codes --------------------------------------------------------------------------- */
+#define OSG_OK 0
+#define OSG_E_INVALID (-1)     /* bad argument / shape */
+#define OSG_E_HIP (-2)         /* HIP runtime error */
+#define OSG_E_NOMEM (-3)       /* device allocation failed */
+#define OSG_E_UNSUPPORTED (-4) /* configuration not implemented */
+#define OSG_E_NODEVICE (-5)    /* no gfx950 device visible */
+
+typedef struct osg_ctx osg_ctx;
+
+/* ---- context ------------------------------------------------------------------------------- */
+int osg_ctx_create(int device, osg_ctx **out);
+int osg_ctx_destroy(osg_ctx *ctx);
+/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL restores the
+ * context's own stream. */
+int osg_ctx_set_stream(osg_ctx *ctx, void *hip_stream);
+void *osg_ctx_stream(osg_ctx *ctx);
+int osg_ctx_synchronize(osg_ctx *ctx);
+const char *osg_strerror(int code);
+const char *osg_ctx_last_error(osg_ctx *ctx);
+/* Library build identifier, e.g. "osg 0.1 gfx950". */
+const char *osg_version(void);
+
+/* ---- a1: DescriptorDistance ---------------------------------------------------------------- */
+/* Host scalar form (SWAR popcount of 8 x int32 XOR, ref:src/ORBmatcher.cc:2397-2405). */
+int osg_descriptor_distance(const uint8_t *a, const uint8_t *b);
+/* Row-pairwise distances on device: out[i] = DescriptorDistance(a[i], b[i]), i < n. */
+int osg_descriptor_distance_pairs(osg_ctx *ctx, const uint8_t *a, const uint8_t *b, int32_t n,
+                                  int32_t *out);
+
+/* ---- a1+a2: brute-force top-2 --------------------------------------------------------------
+ * For every query row q: best_idx[q] = the first train index (train order) with the minimum
+ * distance, best_dist[q] = that distance, second_dist[q] = the second smallest distance counted
+ * with multiplicity.  Sentinels: best_idx -1, distances 256 (train empty).  Exactly the
+ * (bestDist1, bestIdx, bestDist2) of ref:src/ORBmatcher.cc:316-355 with every train row a
+ * candidate.  nt <= 2^24. */
+int osg_hamming_top2(osg_ctx *ctx, const uint8_t *query, int32_t nq, const uint8_t *train,
+                     int32_t nt, int32_t *best_idx, int32_t *best_dist, int32_t *second_dist);
+/* Device form: d_query/d_train/d_out are device pointers; d_out holds nq x int32[3]
+ * {best_idx, best_dist, second_dist}.  Asynchronous on the context stream. */
+int osg_hamming_top2_dev(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d_train,
+                         int32_t nt, void *d_out);
+
+/* ---- frame view (SoA gather of ORB_SLAM3::Frame / KeyFrame fields) ----------------------------
+ * Grid: ref:src/Frame.cc:469-507 (AssignFeaturesToGrid), cells in CSR with cell = ix*48 + iy and
+ * items in insertion (ascending feature index) order, which is GetFeaturesInArea's candidate
+ * enumeration order (ix outer, iy inner; ref:src/Frame.cc:922-957). */
+typedef struct osg_frame {
+    int32_t n;                  /* Frame::N (left + right keypoints for a two-camera rig) */
+    int32_t nleft;              /* Frame::Nleft, -1 for mono / rectified stereo */
+    const uint8_t *desc;        /* n x 32 */
+    const float *kp_x;          /* mvKeysUn[i].pt.x (nleft == -1) / mvKeys, mvKeysRight */
+    const float *kp_y;
+    const float *kp_angle;      /* cv::KeyPoint::angle, same indexing */
+    const int32_t *kp_octave;   /* cv::KeyPoint::octave, same indexing */
+    const float *u_right;       /* mvuRight[n] (may be NULL: treated as all < 0) */
+    const int32_t *grid_start;  /* OSG_GRID_CELLS + 1 offsets into grid_idx (left camera) */
+    const int32_t *grid_idx;
+    const int32_t *grid_start_r;/* right camera grid (nleft != -1), indices relative to nleft */
+    const int32_t *grid_idx_r;
+    const int32_t *left_to_right; /* mvLeftToRightMatch[nleft] or NULL */
+    const int32_t *right_to_left; /* mvRightToLeftMatch[n - nleft] or NULL */
+    float min_x, max_x, min_y, max_y; /* mnMinX, mnMaxX, mnMinY, mnMaxY */
+    float grid_inv_w, grid_inv_h;     /* mfGridElementWidthInv, mfGridElementHeightInv */
+    const float *scale_factors;       /* mvScaleFactors[n_levels] */
+    int32_t n_levels;
+    float mb, mbf;                    /* baseline (m), baseline * fx */
+} osg_frame;
+
+/* Slot state of the frame being matched into (Frame::mvpMapPoints):
+ *   slot_mp[i]     in/out  caller's MapPoint id in slot i, -1 = NULL
+ *   slot_taken[i]  in      1 if the slot's current MapPoint blocks matching
+ *                          (SearchByProjection: mvpMapPoints[i] && Observations() > 0). */
+
+/* ---- a5: SearchByProjection(Frame&, const vector<MapPoint*>&, th, bFarPoints, thFarPoints) -----
+ * Query fields are those Frame::isInFrustum stored on each MapPoint (ref:src/Frame.cc:676-782). */
+typedef struct osg_mp_queries {
+    int32_t n;
+    const int32_t *mp_id;          /* caller MapPoint id written into slot_mp on a match */
+    const uint8_t *desc;           /* n x 32 : MapPoint::GetDescriptor() */
+    const uint8_t *usable;         /* !isBad() */
+    const uint8_t *has_obs;        /* Observations() > 0 (claimed slots then block later queries) */
+    const uint8_t *in_view;        /* mbTrackInView */
+    const float *proj_x, *proj_y;  /* mTrackProjX, mTrackProjY */
+    const float *proj_xr;          /* mTrackProjXR (stereo ur check / right-camera x) */
+    const float *view_cos;         /* mTrackViewCos */
+    const int32_t *pred_level;     /* mnTrackScaleLevel */
+    const float *track_depth;      /* mTrackDepth (bFarPoints filter) */
+    /* right camera (nleft != -1) */
+    const uint8_t *in_view_r;      /* mbTrackInViewR */
+    const float *proj_yr;          /* mTrackProjYR */
+    const float *view_cos_r;       /* mTrackViewCosR */
+    const int32_t *pred_level_r;   /* mnTrackScaleLevelR */
+} osg_mp_queries;
+
+int osg_search_by_projection_mps(osg_ctx *ctx, const osg_frame *F, const osg_mp_queries *mps,
+                                 float nnratio, float th, int far_points, float th_far_points,
+                                 int32_t *slot_mp, const uint8_t *slot_taken);
+
+/* ---- a6: SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th, bMono) ------------
+ * Per LastFrame slot i with a non-outlier MapPoint the caller supplies the projection the
+ * reference computes with Sophus/Eigen float math (ref:src/ORBmatcher.cc:1993-2009):
+ * u, v = mpCamera->project(Tcw * x3Dw), invz = 1/x3Dc(2); valid = MapPoint present, not outlier.
+ * For a two-camera rig also the right-camera projection (ref:src/ORBmatcher.cc:2096-2100). */
+typedef struct osg_last_queries {
+    int32_t n;                     /* LastFrame.N */
+    const int32_t *mp_id;          /* LastFrame.mvpMapPoints[i] id, -1 = NULL */
+    const uint8_t *desc;           /* n x 32 : MapPoint::GetDescriptor() */
+    const uint8_t *valid;          /* pMP && !mvbOutlier[i] */
+    const uint8_t *has_obs;        /* pMP->Observations() > 0 */
+    const float *u, *v, *invz;     /* projection into CurrentFrame (left camera) */
+    const float *u_r, *v_r;        /* projection into right camera (nleft != -1) */
+    const int32_t *octave;         /* LastFrame keypoint octave (nLastOctave) */
+    const float *angle;            /* LastFrame keypoint angle (kpLF) */
+    float tlc_z;                   /* (Tlw * twc)(2): forward/backward test */
+} osg_last_queries;
+
+int osg_search_by_projection_last(osg_ctx *ctx, const osg_frame *CF, const osg_last_queries *last,
+                                  float th, int mono, int check_orientation, int32_t *slot_mp,
+                                  const uint8_t *slot_taken);
+
+/* ---- a7: SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>& sAlreadyFound, th, ORBdist)
+ * Per KF slot: valid = pMP && !isBad() && !sAlreadyFound.count(pMP) && uv inside image &&
+ * dist3D inside [minDist, maxDist]; u, v and pred_level = PredictScale(dist3D, &F) are computed
+ * by the caller (ref:src/ORBmatcher.cc:2238-2262).  A match requires an empty slot
+ * (ref:src/ORBmatcher.cc:2272-2273). */
+typedef struct osg_kf_queries {
+    int32_t n;
+    const int32_t *mp_id;
+    const uint8_t *desc;
+    const uint8_t *valid;
+    const float *u, *v;
+    const int32_t *pred_level;
+    const float *angle;            /* pKF->mvKeysUn[i].angle */
+} osg_kf_queries;
+
+int osg_search_by_projection_kf(osg_ctx *ctx, const osg_frame *CF, const osg_kf_queries *kfq,
+                                float th, int orb_dist, int check_orientation, int32_t *slot_mp);
+
+/* ---- a3/a4: SearchByBoW -----------------------------------------------------------------------
+ * DBoW2::FeatureVector (std::map<NodeId, vector<unsigned>>, ref:Thirdparty/DBoW2/DBoW2/FeatureVector.h:24)
+ * as CSR: node_id[k] ascending, feature indices feat[node_start[k] .. node_start[k+1]). */
+typedef struct osg_featvec {
+    int32_t n_nodes;
+    const uint32_t *node_id;
+    const int32_t *node_start;     /* n_nodes + 1 */
+    const int32_t *feat;
+} osg_featvec;
+
+typedef struct osg_bow_side {
+    int32_t n;                     /* keypoints */
+    int32_t nleft;                 /* -1, or NLeft for a two-camera rig */
+    const uint8_t *desc;           /* n x 32 */
+    const float *angle;            /* keypoint angle as indexed by the reference at that call */
+    const int32_t *mp_id;          /* GetMapPointMatches(): id, -1 = NULL (Frame side: unused) */
+    const uint8_t *mp_good;        /* pMP && !pMP->isBad() */
+    osg_featvec fv;
+} osg_bow_side;
+
+/* out_mp[F.n]: MapPoint id matched to each Frame keypoint, -1 = NULL. Returns nmatches. */
+int osg_search_by_bow_kf_f(osg_ctx *ctx, const osg_bow_side *kf, const osg_bow_side *f,
+                           float nnratio, int check_orientation, int32_t *out_mp);
+/* out_mp12[kf1.n]: KF2 MapPoint id matched to each KF1 keypoint, -1 = NULL. */
+int osg_search_by_bow_kf_kf(osg_ctx *ctx, const osg_bow_side *kf1, const osg_bow_side *kf2,
+                            float nnratio, int check_orientation, int32_t *out_mp12);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OSG_H */

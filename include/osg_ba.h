@@ -1,0 +1,111 @@
+/*
+ * osg_ba.h — C ABI of the bundle-adjustment half of the hot path.
+ *
+ *   osg_pose_optimization[_batch]  ← Optimizer::PoseOptimization(Frame*)        ref:src/Optimizer.cc:71-420
+ *   osg_local_bundle_adjustment    ← the g2o part of Optimizer::LocalBundleAdjustment
+ *                                    (ref:src/Optimizer.cc:1877-2203: graph → optimize(10) →
+ *                                    outlier classification → estimates out)
+ *
+ * The caller (the ORB-SLAM3 side adapter) gathers the graph exactly as the
+ * reference builds it — the same vertices, the same edges in the same insertion order, the same
+ * float→double casts — and applies the returned estimates / outlier flags under the reference's
+ * locks.  Inside, the g2o LM + BlockSolver_6_3 semantics are reproduced:
+ * ref:Thirdparty/g2o/g2o/core/optimization_algorithm_levenberg.cpp:61-194,
+ * ref:Thirdparty/g2o/g2o/core/block_solver.hpp:143-604, ref:Thirdparty/g2o/g2o/core/sparse_optimizer.cpp:61-552.
+ *
+ * Poses are SE3 as 7 doubles {qx, qy, qz, qw, tx, ty, tz} (g2o::SE3Quat; Tcw = world→camera).
+ */
+#ifndef OSG_BA_H
+#define OSG_BA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+struct osg_ctx;
+
+/* camera model, ref:include/CameraModels/GeometricCamera.h:115 (vector<float> mvParameters) */
+#define OSG_CAM_PINHOLE 0 /* ref:src/CameraModels/Pinhole.cpp:50-133 */
+#define OSG_CAM_KB8 1     /* ref:src/CameraModels/KannalaBrandt8.cpp:62-260 */
+
+/* edge kinds (ref:include/OptimizableTypes.h:32-158, ref:Thirdparty/g2o/g2o/types/types_six_dof_expmap.h:146-235) */
+#define OSG_EDGE_MONO 0   /* EdgeSE3ProjectXYZ[OnlyPose]: 2-D, pCamera->project */
+#define OSG_EDGE_STEREO 1 /* EdgeStereoSE3ProjectXYZ[OnlyPose]: 3-D (u, v, ur), fx fy cx cy bf */
+#define OSG_EDGE_BODY 2   /* EdgeSE3ProjectXYZ[OnlyPose]ToBody: 2-D, right camera through mTrl */
+
+typedef struct osg_camera {
+    int32_t type;        /* OSG_CAM_* */
+    float p[8];          /* mvParameters: fx fy cx cy [k1 k2 k3 k4] */
+    float fx, fy, cx, cy, bf; /* Frame/KeyFrame fx..mbf (stereo edges copy these into doubles) */
+    double trl[7];       /* right-from-left SE3 (GetRelativePoseTrl) for BODY edges */
+} osg_camera;
+
+/* ---- PoseOptimization ---------------------------------------------------------------------- */
+typedef struct osg_pose_problem {
+    double pose[7];           /* pFrame->GetPose() cast to double */
+    int32_t n_edges;          /* one per Frame slot with a MapPoint, in slot order */
+    const int8_t *kind;       /* OSG_EDGE_* per edge */
+    const double *xw;         /* 3 per edge: GetWorldPos().cast<double>() */
+    const double *obs;        /* 3 per edge: (u, v, ur) — ur only read for STEREO */
+    const float *inv_sigma2;  /* mvInvLevelSigma2[octave] per edge */
+    osg_camera cam;           /* mpCamera + stereo parameters */
+    osg_camera cam2;          /* mpCamera2 + mTrl (BODY edges) */
+} osg_pose_problem;
+
+typedef struct osg_pose_result {
+    double pose[7];           /* optimised Tcw (input pose when fewer than 3 edges) */
+    uint8_t *outlier;         /* n_edges flags (mvbOutlier of each edge's slot) */
+    int32_t n_inliers;        /* the reference's return value: nInitial - nBad */
+    int32_t lm_iterations;    /* solve() calls over the 4 rounds */
+    int32_t lm_trials;        /* linear solves (incl. rejected steps) */
+} osg_pose_result;
+
+int osg_pose_optimization(struct osg_ctx *ctx, const osg_pose_problem *p, osg_pose_result *r);
+/* n independent frames in one launch (frame-batched tracking, sequences sharded over GPUs). */
+int osg_pose_optimization_batch(struct osg_ctx *ctx, const osg_pose_problem *p, int32_t n,
+                                osg_pose_result *r);
+
+/* ---- LocalBundleAdjustment ------------------------------------------------------------------
+ * Vertices are given sorted by g2o vertex id (KeyFrames: mnId; MapPoints: mnId + maxKFid + 1),
+ * which fixes the Hessian index order (ref:Thirdparty/g2o/g2o/core/sparse_optimizer.cpp:181-211,
+ * 547-552).  Edges are given in insertion order (internalId order). */
+typedef struct osg_ba_graph {
+    int32_t n_poses;
+    const double *pose;        /* 7 per pose */
+    const uint8_t *pose_fixed; /* setFixed(...) */
+    int32_t n_points;
+    const double *point;       /* 3 per point (marginalised) */
+    int32_t n_edges;
+    const int32_t *e_point;    /* point index per edge (vertex 0) */
+    const int32_t *e_pose;     /* pose index per edge (vertex 1) */
+    const int8_t *e_kind;      /* OSG_EDGE_* */
+    const int32_t *e_cam;      /* index into cams */
+    const double *e_obs;       /* 3 per edge */
+    const float *e_inv_sigma2;
+    int32_t n_cams;
+    const osg_camera *cams;
+    int32_t iterations;        /* optimize(iterations): 10 in LocalBundleAdjustment */
+    double user_lambda_init;   /* 0 → tau·max(diag H); 100 when the map is inertial */
+} osg_ba_graph;
+
+typedef struct osg_ba_result {
+    double *pose;              /* 7 per pose (fixed poses returned unchanged) */
+    double *point;             /* 3 per point */
+    uint8_t *edge_bad;         /* chi2 > 5.991 (mono/body) / 7.815 (stereo) || !isDepthPositive() */
+    int32_t iterations;        /* LM solve() calls executed */
+    int32_t trials;            /* linear solves incl. rejected steps */
+    double chi2_initial;       /* activeRobustChi2 before the first iteration */
+    double chi2_final;         /* activeRobustChi2 of the accepted state */
+    int32_t aborted;           /* stop flag observed */
+} osg_ba_result;
+
+/* stop_flag: the reference's pbStopFlag, polled between LM iterations and trials (may be NULL). */
+int osg_local_bundle_adjustment(struct osg_ctx *ctx, const osg_ba_graph *g, osg_ba_result *r,
+                                const volatile int *stop_flag);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

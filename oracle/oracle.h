@@ -1,0 +1,43 @@
+/* oracle.h — CPU restatement of the reference hot path.  TEST INFRASTRUCTURE ONLY (see
+ * oracle_match.c / oracle_ba.c headers).  Never linked into the product library. */
+#ifndef OSG_ORACLE_H
+#define OSG_ORACLE_H
+#include <stdint.h>
+#include "../include/osg.h"
+#include "../include/osg_ba.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int oracle_descriptor_distance(const uint8_t *a, const uint8_t *b);
+void oracle_hamming_top2(const uint8_t *q, int nq, const uint8_t *t, int nt, int32_t *best_idx,
+                         int32_t *best_dist, int32_t *second_dist);
+void oracle_hamming_top2_mt(const uint8_t *q, int nq, const uint8_t *t, int nt, int32_t *best_idx,
+                            int32_t *best_dist, int32_t *second_dist, int nthreads);
+int oracle_frame_features_in_area(const osg_frame *F, float x, float y, float r, int minLevel,
+                                  int maxLevel, int bRight, int32_t *out);
+void oracle_compute_three_maxima(const int *histo_size, int L, int *ind1, int *ind2, int *ind3);
+int oracle_rot_bin(float angle_a, float angle_b);
+int oracle_search_by_projection_mps(const osg_frame *F, const osg_mp_queries *Q, float nnratio,
+                                    float th, int bFarPoints, float thFarPoints, int32_t *slot_mp,
+                                    const uint8_t *slot_taken_in);
+int oracle_search_by_projection_last(const osg_frame *CF, const osg_last_queries *L, float th,
+                                     int bMono, int checkOri, int32_t *slot_mp,
+                                     const uint8_t *slot_taken_in);
+int oracle_search_by_projection_kf(const osg_frame *CF, const osg_kf_queries *K, float th,
+                                   int ORBdist, int checkOri, int32_t *slot_mp);
+int oracle_search_by_bow_kf_f(const osg_bow_side *KF, const osg_bow_side *F, float nnratio,
+                              int checkOri, int32_t *out_mp);
+int oracle_search_by_bow_kf_kf(const osg_bow_side *K1, const osg_bow_side *K2, float nnratio,
+                               int checkOri, int32_t *out_mp12);
+
+/* bundle adjustment (oracle_ba.c) */
+int oracle_pose_optimization(const osg_pose_problem *P, osg_pose_result *R);
+int oracle_local_bundle_adjustment(const osg_ba_graph *G, osg_ba_result *R,
+                                   const volatile int *stop_flag);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,196 @@
+"""ctypes mirror of the C ABI in include/osg.h and include/osg_ba.h.
+
+Only plain pointers and sizes cross the boundary; every pointer field is a ``c_void_p`` filled
+from a numpy array's address by the helpers in this package.  The structures are shared by the
+product bindings (liborbslam3_amd.so) and the tests' oracle bindings (oracle/liboracle.so).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liborbslam3_amd.so")
+
+OSG_OK = 0
+OSG_E_INVALID = -1
+OSG_E_HIP = -2
+OSG_E_NOMEM = -3
+OSG_E_UNSUPPORTED = -4
+OSG_E_NODEVICE = -5
+
+TH_HIGH = 100
+TH_LOW = 50
+HISTO_LENGTH = 30
+GRID_COLS = 64
+GRID_ROWS = 48
+GRID_CELLS = GRID_COLS * GRID_ROWS
+
+CAM_PINHOLE = 0
+CAM_KB8 = 1
+EDGE_MONO = 0
+EDGE_STEREO = 1
+EDGE_BODY = 2
+
+P = C.c_void_p
+i32 = C.c_int32
+f32 = C.c_float
+f64 = C.c_double
+
+
+class OsgFrame(C.Structure):
+    _fields_ = [
+        ("n", i32), ("nleft", i32), ("desc", P), ("kp_x", P), ("kp_y", P), ("kp_angle", P),
+        ("kp_octave", P), ("u_right", P), ("grid_start", P), ("grid_idx", P),
+        ("grid_start_r", P), ("grid_idx_r", P), ("left_to_right", P), ("right_to_left", P),
+        ("min_x", f32), ("max_x", f32), ("min_y", f32), ("max_y", f32),
+        ("grid_inv_w", f32), ("grid_inv_h", f32), ("scale_factors", P), ("n_levels", i32),
+        ("mb", f32), ("mbf", f32),
+    ]
+
+
+class OsgMpQueries(C.Structure):
+    _fields_ = [
+        ("n", i32), ("mp_id", P), ("desc", P), ("usable", P), ("has_obs", P), ("in_view", P),
+        ("proj_x", P), ("proj_y", P), ("proj_xr", P), ("view_cos", P), ("pred_level", P),
+        ("track_depth", P), ("in_view_r", P), ("proj_yr", P), ("view_cos_r", P),
+        ("pred_level_r", P),
+    ]
+
+
+class OsgLastQueries(C.Structure):
+    _fields_ = [
+        ("n", i32), ("mp_id", P), ("desc", P), ("valid", P), ("has_obs", P), ("u", P),
+        ("v", P), ("invz", P), ("u_r", P), ("v_r", P), ("octave", P), ("angle", P),
+        ("tlc_z", f32),
+    ]
+
+
+class OsgKfQueries(C.Structure):
+    _fields_ = [
+        ("n", i32), ("mp_id", P), ("desc", P), ("valid", P), ("u", P), ("v", P),
+        ("pred_level", P), ("angle", P),
+    ]
+
+
+class OsgFeatVec(C.Structure):
+    _fields_ = [("n_nodes", i32), ("node_id", P), ("node_start", P), ("feat", P)]
+
+
+class OsgBowSide(C.Structure):
+    _fields_ = [
+        ("n", i32), ("nleft", i32), ("desc", P), ("angle", P), ("mp_id", P), ("mp_good", P),
+        ("fv", OsgFeatVec),
+    ]
+
+
+class OsgCamera(C.Structure):
+    _fields_ = [
+        ("type", i32), ("p", f32 * 8), ("fx", f32), ("fy", f32), ("cx", f32), ("cy", f32),
+        ("bf", f32), ("trl", f64 * 7),
+    ]
+
+
+class OsgPoseProblem(C.Structure):
+    _fields_ = [
+        ("pose", f64 * 7), ("n_edges", i32), ("kind", P), ("xw", P), ("obs", P),
+        ("inv_sigma2", P), ("cam", OsgCamera), ("cam2", OsgCamera),
+    ]
+
+
+class OsgPoseResult(C.Structure):
+    _fields_ = [
+        ("pose", f64 * 7), ("outlier", P), ("n_inliers", i32), ("lm_iterations", i32),
+        ("lm_trials", i32),
+    ]
+
+
+class OsgBaGraph(C.Structure):
+    _fields_ = [
+        ("n_poses", i32), ("pose", P), ("pose_fixed", P), ("n_points", i32), ("point", P),
+        ("n_edges", i32), ("e_point", P), ("e_pose", P), ("e_kind", P), ("e_cam", P),
+        ("e_obs", P), ("e_inv_sigma2", P), ("n_cams", i32), ("cams", P), ("iterations", i32),
+        ("user_lambda_init", f64),
+    ]
+
+
+class OsgBaResult(C.Structure):
+    _fields_ = [
+        ("pose", P), ("point", P), ("edge_bad", P), ("iterations", i32), ("trials", i32),
+        ("chi2_initial", f64), ("chi2_final", f64), ("aborted", i32),
+    ]
+
+
+# Every symbol include/osg.h and include/osg_ba.h declare (checked by tests/test_abi.py).
+EXPORTS = [
+    "osg_ctx_create", "osg_ctx_destroy", "osg_ctx_set_stream", "osg_ctx_stream",
+    "osg_ctx_synchronize", "osg_strerror", "osg_ctx_last_error", "osg_version",
+    "osg_descriptor_distance", "osg_descriptor_distance_pairs", "osg_hamming_top2",
+    "osg_hamming_top2_dev", "osg_search_by_projection_mps", "osg_search_by_projection_last",
+    "osg_search_by_projection_kf", "osg_search_by_bow_kf_f", "osg_search_by_bow_kf_kf",
+    "osg_pose_optimization", "osg_pose_optimization_batch", "osg_local_bundle_adjustment",
+]
+
+
+def declare(lib: C.CDLL) -> C.CDLL:
+    """Attach argtypes/restypes for the product library."""
+    vp = C.c_void_p
+    lib.osg_ctx_create.argtypes = [C.c_int, C.POINTER(vp)]
+    lib.osg_ctx_destroy.argtypes = [vp]
+    lib.osg_ctx_set_stream.argtypes = [vp, vp]
+    lib.osg_ctx_stream.argtypes = [vp]
+    lib.osg_ctx_stream.restype = vp
+    lib.osg_ctx_synchronize.argtypes = [vp]
+    lib.osg_strerror.argtypes = [C.c_int]
+    lib.osg_strerror.restype = C.c_char_p
+    lib.osg_ctx_last_error.argtypes = [vp]
+    lib.osg_ctx_last_error.restype = C.c_char_p
+    lib.osg_version.restype = C.c_char_p
+    lib.osg_descriptor_distance.argtypes = [vp, vp]
+    lib.osg_descriptor_distance_pairs.argtypes = [vp, vp, vp, i32, vp]
+    lib.osg_hamming_top2.argtypes = [vp, vp, i32, vp, i32, vp, vp, vp]
+    lib.osg_hamming_top2_dev.argtypes = [vp, vp, i32, vp, i32, vp]
+    lib.osg_search_by_projection_mps.argtypes = [vp, C.POINTER(OsgFrame), C.POINTER(OsgMpQueries),
+                                                 f32, f32, C.c_int, f32, vp, vp]
+    lib.osg_search_by_projection_last.argtypes = [vp, C.POINTER(OsgFrame),
+                                                  C.POINTER(OsgLastQueries), f32, C.c_int, C.c_int,
+                                                  vp, vp]
+    lib.osg_search_by_projection_kf.argtypes = [vp, C.POINTER(OsgFrame), C.POINTER(OsgKfQueries),
+                                                f32, C.c_int, C.c_int, vp]
+    lib.osg_search_by_bow_kf_f.argtypes = [vp, C.POINTER(OsgBowSide), C.POINTER(OsgBowSide), f32,
+                                           C.c_int, vp]
+    lib.osg_search_by_bow_kf_kf.argtypes = [vp, C.POINTER(OsgBowSide), C.POINTER(OsgBowSide), f32,
+                                            C.c_int, vp]
+    lib.osg_pose_optimization.argtypes = [vp, C.POINTER(OsgPoseProblem), C.POINTER(OsgPoseResult)]
+    lib.osg_pose_optimization_batch.argtypes = [vp, C.POINTER(OsgPoseProblem), i32,
+                                                C.POINTER(OsgPoseResult)]
+    lib.osg_local_bundle_adjustment.argtypes = [vp, C.POINTER(OsgBaGraph), C.POINTER(OsgBaResult),
+                                                vp]
+    return lib
+
+
+def declare_oracle(lib: C.CDLL) -> C.CDLL:
+    """argtypes for oracle/liboracle.so (test infrastructure)."""
+    vp = C.c_void_p
+    lib.oracle_descriptor_distance.argtypes = [vp, vp]
+    lib.oracle_hamming_top2.argtypes = [vp, C.c_int, vp, C.c_int, vp, vp, vp]
+    lib.oracle_hamming_top2_mt.argtypes = [vp, C.c_int, vp, C.c_int, vp, vp, vp, C.c_int]
+    lib.oracle_frame_features_in_area.argtypes = [C.POINTER(OsgFrame), f32, f32, f32, C.c_int,
+                                                  C.c_int, C.c_int, vp]
+    lib.oracle_compute_three_maxima.argtypes = [vp, C.c_int, vp, vp, vp]
+    lib.oracle_rot_bin.argtypes = [f32, f32]
+    lib.oracle_search_by_projection_mps.argtypes = [C.POINTER(OsgFrame), C.POINTER(OsgMpQueries),
+                                                    f32, f32, C.c_int, f32, vp, vp]
+    lib.oracle_search_by_projection_last.argtypes = [C.POINTER(OsgFrame),
+                                                     C.POINTER(OsgLastQueries), f32, C.c_int,
+                                                     C.c_int, vp, vp]
+    lib.oracle_search_by_projection_kf.argtypes = [C.POINTER(OsgFrame), C.POINTER(OsgKfQueries),
+                                                   f32, C.c_int, C.c_int, vp]
+    lib.oracle_search_by_bow_kf_f.argtypes = [C.POINTER(OsgBowSide), C.POINTER(OsgBowSide), f32,
+                                              C.c_int, vp]
+    lib.oracle_search_by_bow_kf_kf.argtypes = [C.POINTER(OsgBowSide), C.POINTER(OsgBowSide), f32,
+                                               C.c_int, vp]
+    lib.oracle_pose_optimization.argtypes = [C.POINTER(OsgPoseProblem), C.POINTER(OsgPoseResult)]
+    lib.oracle_local_bundle_adjustment.argtypes = [C.POINTER(OsgBaGraph), C.POINTER(OsgBaResult),
+                                                   vp]
+    return lib

@@ -1,0 +1,433 @@
+// hamming.hip — 256-bit Hamming distance and brute-force top-2 kernels for gfx950.
+//
+// Replaces ORBmatcher::DescriptorDistance (ref:src/ORBmatcher.cc:2388-2408) evaluated inside the
+// top-2 candidate loop every matcher runs (ref:src/ORBmatcher.cc:316-355 is the canonical form):
+//   bestDist1 = bestDist2 = 256, bestIdx = -1;
+//   for each candidate j: d = dist(q, t_j);
+//       if (d < bestDist1) { bestDist2 = bestDist1; bestDist1 = d; bestIdx = j; }
+//       else if (d < bestDist2) bestDist2 = d;
+// which is: best = smallest distance, first index among ties; second = 2nd smallest distance
+// counted with multiplicity; a distance of 256 never enters.  On the GPU this is an
+// order-independent min over packed keys  key = dist << 23 | local_index  (smaller key = smaller
+// distance, then earlier index), kept as (k1 = smallest key, k2 = second smallest key) with
+// k2' = min(k2, max(k1, key)), k1' = min(k1, key) — 2 VALU ops (v_max/v_min3 or v_med3).
+//
+// Two shapes (same semantics, chosen by osg_launch_top2):
+//  * tile   — lane = query (its 8 words in VGPRs); every train row is wave-uniform and comes in
+//             through scalar loads (s_load_dwordx8: one 32-byte row broadcast to 64 queries), so a
+//             pair costs 8 v_xor + 8 v_bcnt(accumulate) + 1 v_lshl_or + 2 min = 19 VALU and no
+//             vector-memory traffic.  INT32-VALU bound.  Train rows split over WAVES waves of a
+//             workgroup (merged in LDS) and over G workgroups (merged by the last-arriving
+//             workgroup: agent-scope release/acquire through a self-resetting counter).
+//  * stream — few queries (<= 8) against a huge train set (C2', M = 2^24): lane = train row,
+//             queries in SGPRs, rows read once with coalesced 16-B loads.  HBM bound.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
+#include "osg_internal.h"
+
+namespace {
+
+constexpr int KEY_SHIFT = 23;
+constexpr uint32_t IDX_MASK = (1u << KEY_SHIFT) - 1u;
+constexpr uint32_t KEY_EMPTY = 0xFFFFFFFFu;
+constexpr uint32_t D_EMPTY = 511u;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// v_bcnt_u32_b32 with its accumulate operand chained (hipcc otherwise splits the sum into
+// bcnt(x,0) + v_add3, 3 extra VALU per pair).
+__device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc)
+{
+    uint32_t r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+    return r;
+}
+
+__device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c)
+{
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+__device__ __forceinline__ uint32_t hamming8(const uint32_t (&a)[8], const uint32_t *__restrict__ b)
+{
+    uint32_t d = __popc(a[0] ^ b[0]);
+    d = bcnt_acc(a[1] ^ b[1], d);
+    d = bcnt_acc(a[2] ^ b[2], d);
+    d = bcnt_acc(a[3] ^ b[3], d);
+    d = bcnt_acc(a[4] ^ b[4], d);
+    d = bcnt_acc(a[5] ^ b[5], d);
+    d = bcnt_acc(a[6] ^ b[6], d);
+    d = bcnt_acc(a[7] ^ b[7], d);
+    return d;
+}
+
+// (k1, k2) = two smallest keys seen; k1 <= k2 always, so the new second is med3(k1, key, k2).
+__device__ __forceinline__ void key_push(uint32_t &k1, uint32_t &k2, uint32_t key)
+{
+    k2 = med3_u32(k1, key, k2);
+    k1 = min(k1, key);
+}
+
+__device__ __forceinline__ void key_merge(uint32_t &k1, uint32_t &k2, uint32_t a1, uint32_t a2)
+{
+    const uint32_t hi = max(k1, a1);
+    k1 = min(k1, a1);
+    k2 = min(min(k2, a2), hi);
+}
+
+// partial = {global idx of best, d1 << 16 | d2}
+__device__ __forceinline__ uint2 key_to_part(uint32_t k1, uint32_t k2, uint32_t base)
+{
+    const uint32_t d1 = k1 >> KEY_SHIFT, d2 = k2 >> KEY_SHIFT;
+    const uint32_t i1 = (k1 == KEY_EMPTY) ? 0xFFFFFFFFu : base + (k1 & IDX_MASK);
+    return make_uint2(i1, (d1 << 16) | d2);
+}
+
+__device__ __forceinline__ void part_merge(uint32_t &D1, uint32_t &I1, uint32_t &D2, uint2 p)
+{
+    const uint32_t d1 = p.y >> 16, d2 = p.y & 0xFFFFu, i1 = p.x;
+    if (d1 < D1 || (d1 == D1 && i1 < I1)) {
+        D2 = min(D1, d2);
+        D1 = d1;
+        I1 = i1;
+    } else {
+        D2 = min(D2, d1);
+    }
+}
+
+__device__ __forceinline__ void write_result(int32_t *__restrict__ out, int q, uint32_t D1, uint32_t I1,
+                                             uint32_t D2)
+{
+    const int32_t d1 = (int32_t)min(D1, 256u);
+    out[3 * q + 0] = (D1 < 256u) ? (int32_t)I1 : -1;
+    out[3 * q + 1] = d1;
+    out[3 * q + 2] = (int32_t)min(D2, 256u);
+}
+
+// ------------------------------------------------------------------------------- tile kernel
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void k_top2_tile(const uint4 *__restrict__ query, int nq,
+                                                          const uint32_t *__restrict__ train, int nt,
+                                                          int rows_per_chunk, int G,
+                                                          uint2 *__restrict__ part,
+                                                          uint32_t *__restrict__ counters,
+                                                          int32_t *__restrict__ out)
+{
+    __shared__ uint32_t s_k1[WAVES][64];
+    __shared__ uint32_t s_k2[WAVES][64];
+    __shared__ int s_last;
+
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int qb = blockIdx.x;
+    const int c = blockIdx.y;
+    const int qi = qb * 64 + lane;
+
+    uint32_t qd[8];
+    {
+        const int qq = qi < nq ? qi : nq - 1;
+        const uint4 a = query[2 * qq], b = query[2 * qq + 1];
+        qd[0] = a.x; qd[1] = a.y; qd[2] = a.z; qd[3] = a.w;
+        qd[4] = b.x; qd[5] = b.y; qd[6] = b.z; qd[7] = b.w;
+    }
+    const int r0 = c * rows_per_chunk;
+    const int r1 = min(nt, r0 + rows_per_chunk);
+    uint32_t k1 = KEY_EMPTY, k2 = KEY_EMPTY;
+
+    // rows r0 + w + WAVES*j: wave-uniform, consumed from SGPRs (scalar loads)
+    int r = r0 + w;
+    for (; r + 3 * WAVES < r1; r += 4 * WAVES) {
+        const uint32_t *t0 = train + (size_t)r * 8;
+        const uint32_t *t1 = t0 + 8 * WAVES;
+        const uint32_t *t2 = t1 + 8 * WAVES;
+        const uint32_t *t3 = t2 + 8 * WAVES;
+        const uint32_t l = (uint32_t)(r - r0);
+        key_push(k1, k2, (hamming8(qd, t0) << KEY_SHIFT) | l);
+        key_push(k1, k2, (hamming8(qd, t1) << KEY_SHIFT) | (l + WAVES));
+        key_push(k1, k2, (hamming8(qd, t2) << KEY_SHIFT) | (l + 2 * WAVES));
+        key_push(k1, k2, (hamming8(qd, t3) << KEY_SHIFT) | (l + 3 * WAVES));
+    }
+    for (; r < r1; r += WAVES) {
+        const uint32_t *t0 = train + (size_t)r * 8;
+        key_push(k1, k2, (hamming8(qd, t0) << KEY_SHIFT) | (uint32_t)(r - r0));
+    }
+
+    if (WAVES > 1) {
+        s_k1[w][lane] = k1;
+        s_k2[w][lane] = k2;
+        __syncthreads();
+        if (w == 0) {
+#pragma unroll
+            for (int o = 1; o < WAVES; o++) key_merge(k1, k2, s_k1[o][lane], s_k2[o][lane]);
+        }
+    }
+    if (G == 1) {
+        if (w == 0 && qi < nq) {
+            const uint2 p = key_to_part(k1, k2, (uint32_t)r0);
+            write_result(out, qi, p.y >> 16, p.x, p.y & 0xFFFFu);
+        }
+        return;
+    }
+    // publish this chunk's partial, then the last-arriving workgroup of this query block merges
+    if (w == 0 && qi < nq) part[(size_t)c * nq + qi] = key_to_part(k1, k2, (uint32_t)r0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t prev =
+            __hip_atomic_fetch_add(&counters[qb], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = (prev == (uint32_t)(G - 1));
+    }
+    __syncthreads();
+    if (!s_last) return;
+    if (w == 0 && qi < nq) {
+        uint32_t D1 = D_EMPTY, I1 = 0xFFFFFFFFu, D2 = D_EMPTY;
+        for (int cc = 0; cc < G; cc++) part_merge(D1, I1, D2, part[(size_t)cc * nq + qi]);
+        write_result(out, qi, D1, I1, D2);
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(&counters[qb], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+
+// ----------------------------------------------------------------------------- stream kernel
+template <int NQ>
+__global__ __launch_bounds__(256) void k_top2_stream(const uint32_t *__restrict__ query, int nq,
+                                                     const uint4 *__restrict__ train, int nt,
+                                                     int rows_per_block, int G,
+                                                     uint2 *__restrict__ part,
+                                                     uint32_t *__restrict__ counter,
+                                                     int32_t *__restrict__ out)
+{
+    __shared__ uint32_t s_k1[4][NQ], s_k2[4][NQ];
+    __shared__ uint32_t s_D1[4][NQ], s_I1[4][NQ], s_D2[4][NQ];
+    __shared__ int s_last;
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+
+    uint32_t qd[NQ][8];
+#pragma unroll
+    for (int j = 0; j < NQ; j++) {
+        const int jj = j < nq ? j : nq - 1;
+#pragma unroll
+        for (int i = 0; i < 8; i++) qd[j][i] = query[jj * 8 + i]; // uniform: SGPRs
+    }
+    const int r0 = blockIdx.x * rows_per_block;
+    const int r1 = min(nt, r0 + rows_per_block);
+    uint32_t k1[NQ], k2[NQ];
+#pragma unroll
+    for (int j = 0; j < NQ; j++) k1[j] = k2[j] = KEY_EMPTY;
+
+    constexpr int U = 4;
+    int r = r0 + threadIdx.x;
+    for (; r + (U - 1) * 256 < r1; r += U * 256) {
+        u32x4 ta[U], tb[U];
+        const u32x4 *tv = (const u32x4 *)train;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            ta[u] = __builtin_nontemporal_load(&tv[2 * (size_t)(r + u * 256)]);
+            tb[u] = __builtin_nontemporal_load(&tv[2 * (size_t)(r + u * 256) + 1]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t t[8] = {ta[u].x, ta[u].y, ta[u].z, ta[u].w, tb[u].x, tb[u].y, tb[u].z, tb[u].w};
+            const uint32_t l = (uint32_t)(r + u * 256 - r0);
+#pragma unroll
+            for (int j = 0; j < NQ; j++) key_push(k1[j], k2[j], (hamming8(qd[j], t) << KEY_SHIFT) | l);
+        }
+    }
+    for (; r < r1; r += 256) {
+        const uint4 a = train[2 * (size_t)r], b = train[2 * (size_t)r + 1];
+        const uint32_t t[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        const uint32_t l = (uint32_t)(r - r0);
+#pragma unroll
+        for (int j = 0; j < NQ; j++) key_push(k1[j], k2[j], (hamming8(qd[j], t) << KEY_SHIFT) | l);
+    }
+    // wave butterfly, then across the 4 waves in LDS
+#pragma unroll
+    for (int j = 0; j < NQ; j++) {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const uint32_t a1 = __shfl_xor(k1[j], off), a2 = __shfl_xor(k2[j], off);
+            key_merge(k1[j], k2[j], a1, a2);
+        }
+        if (lane == 0) {
+            s_k1[w][j] = k1[j];
+            s_k2[w][j] = k2[j];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < nq) {
+        const int j = threadIdx.x;
+        uint32_t a1 = s_k1[0][j], a2 = s_k2[0][j];
+        for (int o = 1; o < 4; o++) key_merge(a1, a2, s_k1[o][j], s_k2[o][j]);
+        const uint2 p = key_to_part(a1, a2, (uint32_t)r0);
+        if (G == 1) write_result(out, j, p.y >> 16, p.x, p.y & 0xFFFFu);
+        else part[(size_t)blockIdx.x * nq + j] = p;
+    }
+    if (G == 1) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = (prev == (uint32_t)(G - 1));
+    }
+    __syncthreads();
+    if (!s_last) return;
+    for (int j = 0; j < nq; j++) {
+        uint32_t D1 = D_EMPTY, I1 = 0xFFFFFFFFu, D2 = D_EMPTY;
+        for (int b = threadIdx.x; b < G; b += 256) part_merge(D1, I1, D2, part[(size_t)b * nq + j]);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const uint2 o = make_uint2(__shfl_xor(I1, off), (__shfl_xor(D1, off) << 16) | __shfl_xor(D2, off));
+            part_merge(D1, I1, D2, o);
+        }
+        if (lane == 0) {
+            s_D1[w][0] = D1;
+            s_I1[w][0] = I1;
+            s_D2[w][0] = D2;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int o = 1; o < 4; o++) part_merge(D1, I1, D2, make_uint2(s_I1[o][0], (s_D1[o][0] << 16) | s_D2[o][0]));
+            write_result(out, j, D1, I1, D2);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// --------------------------------------------------------------------------- pairwise distance
+__global__ __launch_bounds__(256) void k_pair_dist(const uint4 *__restrict__ a, const uint4 *__restrict__ b,
+                                                   int n, int32_t *__restrict__ out)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint4 a0 = a[2 * i], a1 = a[2 * i + 1], b0 = b[2 * i], b1 = b[2 * i + 1];
+    out[i] = __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+             __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+int env_int(const char *name, int dflt)
+{
+    const char *v = getenv(name);
+    return (v && *v) ? atoi(v) : dflt;
+}
+
+}  // namespace
+
+// Device-pointer launcher shared by the C ABI and the matcher engine.
+int osg_launch_top2(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d_train, int32_t nt,
+                    void *d_out)
+{
+    if (nq <= 0) return OSG_OK;
+    OSG_REQUIRE(ctx, nt >= 0 && nt <= (1 << 24), "nt=%d out of range [0, 2^24]", nt);
+    if (nt == 0) {
+        // no candidates: (-1, 256, 256) for every query
+        static const int32_t sentinel[3] = {-1, 256, 256};
+        int32_t *h = (int32_t *)osg_pinned(ctx, sizeof(int32_t) * 3 * (size_t)nq);
+        if (!h) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
+        OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+        for (int i = 0; i < nq; i++) memcpy(h + 3 * i, sentinel, sizeof sentinel);
+        OSG_HIP_CHECK(ctx, hipMemcpyAsync(d_out, h, sizeof(int32_t) * 3 * (size_t)nq, hipMemcpyHostToDevice, ctx->stream));
+        return OSG_OK;
+    }
+    const int cus = ctx->num_cus;
+    if (nq <= 8 && nt >= 65536) {
+        // streaming shape: lane = train row
+        int G = env_int("OSG_TOP2_STREAM_G", 8 * cus);
+        int rpb = (nt + G - 1) / G;
+        rpb = ((rpb + 1023) / 1024) * 1024;
+        G = (nt + rpb - 1) / rpb;
+        uint2 *part = nullptr;
+        OSG_ALLOC(ctx, part, SLOT_PART, sizeof(uint2) * (size_t)G * nq);
+        uint32_t *counter = ctx->counters + (OSG_N_COUNTERS - 1);
+        const uint32_t *q = (const uint32_t *)d_query;
+        const uint4 *t = (const uint4 *)d_train;
+        int32_t *o = (int32_t *)d_out;
+        if (nq == 1) hipLaunchKernelGGL(k_top2_stream<1>, dim3(G), dim3(256), 0, ctx->stream, q, nq, t, nt, rpb, G, part, counter, o);
+        else if (nq == 2) hipLaunchKernelGGL(k_top2_stream<2>, dim3(G), dim3(256), 0, ctx->stream, q, nq, t, nt, rpb, G, part, counter, o);
+        else if (nq <= 4) hipLaunchKernelGGL(k_top2_stream<4>, dim3(G), dim3(256), 0, ctx->stream, q, nq, t, nt, rpb, G, part, counter, o);
+        else hipLaunchKernelGGL(k_top2_stream<8>, dim3(G), dim3(256), 0, ctx->stream, q, nq, t, nt, rpb, G, part, counter, o);
+        OSG_HIP_CHECK(ctx, hipGetLastError());
+        return OSG_OK;
+    }
+    constexpr int WAVES = 4;
+    const int nqb = (nq + 63) / 64;
+    OSG_REQUIRE(ctx, nqb <= OSG_N_COUNTERS - 1, "too many queries (%d)", nq);
+    const int target_wg = env_int("OSG_TOP2_WG", 4 * cus);
+    const int min_rows = env_int("OSG_TOP2_MIN_ROWS", WAVES * 32);
+    int G = (target_wg + nqb - 1) / nqb;
+    G = std::min(G, std::max(1, nt / min_rows));
+    G = std::max(G, (nt + (int)IDX_MASK) / ((int)IDX_MASK + 1)); // chunk-local index fits 23 bits
+    G = std::max(1, std::min(G, 65535));
+    const int rpc = (nt + G - 1) / G;
+    G = (nt + rpc - 1) / rpc;
+    uint2 *part = nullptr;
+    if (G > 1) OSG_ALLOC(ctx, part, SLOT_PART, sizeof(uint2) * (size_t)G * nq);
+    hipLaunchKernelGGL(k_top2_tile<WAVES>, dim3(nqb, G), dim3(WAVES * 64), 0, ctx->stream,
+                       (const uint4 *)d_query, nq, (const uint32_t *)d_train, nt, rpc, G, part,
+                       ctx->counters, (int32_t *)d_out);
+    OSG_HIP_CHECK(ctx, hipGetLastError());
+    return OSG_OK;
+}
+
+extern "C" {
+
+int osg_hamming_top2_dev(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d_train, int32_t nt,
+                         void *d_out)
+{
+    if (!ctx) return OSG_E_INVALID;
+    OSG_REQUIRE(ctx, nq >= 0 && (nq == 0 || (d_query && d_out)) && (nt == 0 || d_train), "null pointer");
+    return osg_launch_top2(ctx, d_query, nq, d_train, nt, d_out);
+}
+
+int osg_hamming_top2(osg_ctx *ctx, const uint8_t *query, int32_t nq, const uint8_t *train, int32_t nt,
+                     int32_t *best_idx, int32_t *best_dist, int32_t *second_dist)
+{
+    if (!ctx) return OSG_E_INVALID;
+    OSG_REQUIRE(ctx, nq >= 0 && nt >= 0, "negative size");
+    if (nq == 0) return OSG_OK;
+    OSG_REQUIRE(ctx, query && best_idx && best_dist && second_dist && (nt == 0 || train), "null pointer");
+    void *dq, *dt, *dout;
+    OSG_ALLOC(ctx, dq, SLOT_Q, (size_t)nq * 32);
+    OSG_ALLOC(ctx, dt, SLOT_T, (size_t)std::max(nt, 1) * 32);
+    OSG_ALLOC(ctx, dout, SLOT_OUT, (size_t)nq * 12);
+    OSG_HIP_CHECK(ctx, hipMemcpyAsync(dq, query, (size_t)nq * 32, hipMemcpyHostToDevice, ctx->stream));
+    if (nt > 0) OSG_HIP_CHECK(ctx, hipMemcpyAsync(dt, train, (size_t)nt * 32, hipMemcpyHostToDevice, ctx->stream));
+    int rc = osg_launch_top2(ctx, dq, nq, dt, nt, dout);
+    if (rc < 0) return rc;
+    int32_t *h = (int32_t *)osg_pinned(ctx, (size_t)nq * 12);
+    if (!h) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
+    OSG_HIP_CHECK(ctx, hipMemcpyAsync(h, dout, (size_t)nq * 12, hipMemcpyDeviceToHost, ctx->stream));
+    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    for (int i = 0; i < nq; i++) {
+        best_idx[i] = h[3 * i];
+        best_dist[i] = h[3 * i + 1];
+        second_dist[i] = h[3 * i + 2];
+    }
+    return OSG_OK;
+}
+
+int osg_descriptor_distance_pairs(osg_ctx *ctx, const uint8_t *a, const uint8_t *b, int32_t n, int32_t *out)
+{
+    if (!ctx) return OSG_E_INVALID;
+    OSG_REQUIRE(ctx, n >= 0, "negative size");
+    if (n == 0) return OSG_OK;
+    OSG_REQUIRE(ctx, a && b && out, "null pointer");
+    void *da, *db, *dout;
+    OSG_ALLOC(ctx, da, SLOT_Q, (size_t)n * 32);
+    OSG_ALLOC(ctx, db, SLOT_T, (size_t)n * 32);
+    OSG_ALLOC(ctx, dout, SLOT_OUT, (size_t)n * 4);
+    OSG_HIP_CHECK(ctx, hipMemcpyAsync(da, a, (size_t)n * 32, hipMemcpyHostToDevice, ctx->stream));
+    OSG_HIP_CHECK(ctx, hipMemcpyAsync(db, b, (size_t)n * 32, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_pair_dist, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, (const uint4 *)da,
+                       (const uint4 *)db, n, (int32_t *)dout);
+    OSG_HIP_CHECK(ctx, hipGetLastError());
+    OSG_HIP_CHECK(ctx, hipMemcpyAsync(out, dout, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    return OSG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,65 @@
+// osg_internal.h — shared host/device internals of liborbslam3_amd (not part of the ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/osg.h"
+#include "../../include/osg_ba.h"
+
+// Scratch slots: each entry point owns a few named device buffers that grow on demand and are
+// reused across calls (no hipMalloc on the steady-state path).
+enum osg_slot {
+    SLOT_Q = 0, SLOT_T, SLOT_OUT, SLOT_PART, SLOT_TMP0, SLOT_TMP1, SLOT_TMP2, SLOT_TMP3,
+    SLOT_TMP4, SLOT_TMP5, SLOT_TMP6, SLOT_TMP7, SLOT_TMP8, SLOT_TMP9, SLOT_TMP10, SLOT_TMP11,
+    SLOT_BA0, SLOT_BA1, SLOT_BA2, SLOT_BA3, SLOT_BA4, SLOT_BA5, SLOT_BA6, SLOT_BA7,
+    SLOT_BA8, SLOT_BA9, SLOT_BA10, SLOT_BA11, SLOT_BA12, SLOT_BA13, SLOT_BA14, SLOT_BA15,
+    SLOT_PINNED0, SLOT_COUNT
+};
+
+// Counters for in-launch last-arriver merges: zero at allocation, each launch leaves them zero.
+#define OSG_N_COUNTERS 65536
+
+struct osg_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    void *buf[SLOT_COUNT] = {};
+    size_t cap[SLOT_COUNT] = {};
+    void *host_pinned = nullptr;
+    size_t host_pinned_cap = 0;
+    uint32_t *counters = nullptr;
+    int num_cus = 256;
+    std::string last_error;
+};
+
+int osg_set_error(osg_ctx *ctx, int code, const char *fmt, ...);
+// device buffer of at least `bytes` for `slot` (grows, never shrinks)
+void *osg_scratch(osg_ctx *ctx, int slot, size_t bytes);
+void *osg_pinned(osg_ctx *ctx, size_t bytes);
+
+#define OSG_HIP_CHECK(ctx, expr)                                                             \
+    do {                                                                                     \
+        hipError_t _e = (expr);                                                              \
+        if (_e != hipSuccess)                                                                \
+            return osg_set_error((ctx), OSG_E_HIP, "%s failed: %s (%s:%d)", #expr,          \
+                                 hipGetErrorString(_e), __FILE__, __LINE__);                 \
+    } while (0)
+
+#define OSG_REQUIRE(ctx, cond, ...)                                                          \
+    do {                                                                                     \
+        if (!(cond)) return osg_set_error((ctx), OSG_E_INVALID, __VA_ARGS__);               \
+    } while (0)
+
+#define OSG_ALLOC(ctx, ptr, slot, bytes)                                                     \
+    do {                                                                                     \
+        ptr = (decltype(ptr))osg_scratch((ctx), (slot), (bytes));                            \
+        if (!(ptr)) return osg_set_error((ctx), OSG_E_NOMEM, "scratch alloc %zu B failed",  \
+                                         (size_t)(bytes));                                   \
+    } while (0)
+
+// internal device-pointer launchers shared between translation units
+int osg_launch_top2(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d_train, int32_t nt,
+                    void *d_out);

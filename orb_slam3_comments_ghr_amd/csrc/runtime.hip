@@ -1,0 +1,152 @@
+// runtime.hip — context lifecycle, scratch pool, errors (C ABI: include/osg.h "context").
+#include <cstdarg>
+#include <cstring>
+
+#include "osg_internal.h"
+
+int osg_set_error(osg_ctx *ctx, int code, const char *fmt, ...)
+{
+    if (ctx) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        ctx->last_error = buf;
+    }
+    return code;
+}
+
+void *osg_scratch(osg_ctx *ctx, int slot, size_t bytes)
+{
+    if (bytes == 0) bytes = 16;
+    if (ctx->cap[slot] >= bytes) return ctx->buf[slot];
+    if (ctx->buf[slot]) {
+        // the previous buffer may still be read by queued work on this stream
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipFree(ctx->buf[slot]);
+        ctx->buf[slot] = nullptr;
+        ctx->cap[slot] = 0;
+    }
+    size_t cap = bytes + bytes / 4 + 256;
+    cap = (cap + 255) & ~size_t(255);
+    void *p = nullptr;
+    if (hipMalloc(&p, cap) != hipSuccess) return nullptr;
+    ctx->buf[slot] = p;
+    ctx->cap[slot] = cap;
+    return p;
+}
+
+void *osg_pinned(osg_ctx *ctx, size_t bytes)
+{
+    if (ctx->host_pinned_cap >= bytes) return ctx->host_pinned;
+    if (ctx->host_pinned) {
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipHostFree(ctx->host_pinned);
+        ctx->host_pinned = nullptr;
+        ctx->host_pinned_cap = 0;
+    }
+    size_t cap = bytes + bytes / 4 + 4096;
+    void *p = nullptr;
+    if (hipHostMalloc(&p, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+    ctx->host_pinned = p;
+    ctx->host_pinned_cap = cap;
+    return p;
+}
+
+extern "C" {
+
+const char *osg_version(void) { return "osg 0.1 gfx950 (orb_slam3_comments_ghr_amd)"; }
+
+const char *osg_strerror(int code)
+{
+    switch (code) {
+    case OSG_OK: return "ok";
+    case OSG_E_INVALID: return "invalid argument";
+    case OSG_E_HIP: return "HIP runtime error";
+    case OSG_E_NOMEM: return "device allocation failed";
+    case OSG_E_UNSUPPORTED: return "unsupported configuration";
+    case OSG_E_NODEVICE: return "no gfx950 device";
+    default: return code >= 0 ? "ok" : "unknown error";
+    }
+}
+
+int osg_ctx_create(int device, osg_ctx **out)
+{
+    if (!out) return OSG_E_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return OSG_E_NODEVICE;
+    if (device < 0 || device >= n) return OSG_E_INVALID;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return OSG_E_HIP;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return OSG_E_NODEVICE;
+    if (hipSetDevice(device) != hipSuccess) return OSG_E_HIP;
+    osg_ctx *ctx = new osg_ctx();
+    ctx->device = device;
+    ctx->num_cus = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return OSG_E_HIP;
+    }
+    ctx->stream = ctx->own_stream;
+    if (hipMalloc(&ctx->counters, sizeof(uint32_t) * OSG_N_COUNTERS) != hipSuccess ||
+        hipMemset(ctx->counters, 0, sizeof(uint32_t) * OSG_N_COUNTERS) != hipSuccess) {
+        (void)hipStreamDestroy(ctx->own_stream);
+        delete ctx;
+        return OSG_E_NOMEM;
+    }
+    *out = ctx;
+    return OSG_OK;
+}
+
+int osg_ctx_destroy(osg_ctx *ctx)
+{
+    if (!ctx) return OSG_E_INVALID;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (int i = 0; i < SLOT_COUNT; i++)
+        if (ctx->buf[i]) (void)hipFree(ctx->buf[i]);
+    if (ctx->host_pinned) (void)hipHostFree(ctx->host_pinned);
+    if (ctx->counters) (void)hipFree(ctx->counters);
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+    return OSG_OK;
+}
+
+int osg_ctx_set_stream(osg_ctx *ctx, void *hip_stream)
+{
+    if (!ctx) return OSG_E_INVALID;
+    ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own_stream;
+    return OSG_OK;
+}
+
+void *osg_ctx_stream(osg_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+int osg_ctx_synchronize(osg_ctx *ctx)
+{
+    if (!ctx) return OSG_E_INVALID;
+    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    return OSG_OK;
+}
+
+const char *osg_ctx_last_error(osg_ctx *ctx) { return ctx ? ctx->last_error.c_str() : ""; }
+
+// ref:src/ORBmatcher.cc:2388-2408 — host scalar form (the SWAR popcount as written).
+int osg_descriptor_distance(const uint8_t *a, const uint8_t *b)
+{
+    if (!a || !b) return OSG_E_INVALID;
+    int dist = 0;
+    for (int i = 0; i < 8; i++) {
+        int32_t wa, wb;
+        std::memcpy(&wa, a + 4 * i, 4);
+        std::memcpy(&wb, b + 4 * i, 4);
+        unsigned int v = (unsigned int)(wa ^ wb);
+        v = v - ((v >> 1) & 0x55555555u);
+        v = (v & 0x33333333u) + ((v >> 2) & 0x33333333u);
+        dist += (int)((((v + (v >> 4)) & 0xF0F0F0Fu) * 0x1010101u) >> 24);
+    }
+    return dist;
+}
+
+}  // extern "C"
