@@ -63,7 +63,9 @@ def main():
     from orb_slam3_comments_ghr_amd import Context, synth
 
     ctx = Context(local_rank)
-    stream = torch.cuda.current_stream(dev)
+    # a dedicated (non-null) stream: the kernels and the HIP events below share it
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
 
     def barrier():

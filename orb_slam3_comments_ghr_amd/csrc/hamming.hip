@@ -108,7 +108,17 @@ __device__ __forceinline__ void write_result(int32_t *__restrict__ out, int q, u
 }
 
 // ------------------------------------------------------------------------------- tile kernel
-template <int WAVES>
+// STAGE 0: train rows come straight from memory through scalar loads (wave-uniform address).
+// STAGE 1: the workgroup first copies its chunk into LDS with one coalesced 16-B load per thread,
+//          then every wave reads rows with wave-uniform (broadcast) ds_read_b128.
+// MERGE 0: partials published with plain stores + agent release, consumed after agent acquire.
+// MERGE 1: partials published with write-through (sc1) 8-B stores, drained (vmcnt(0)) before a
+//          relaxed agent-scope counter add; the last arriver reads them with sc1 loads
+//          (MI355X_MICROARCH.md "Valid forms", first table row).
+constexpr int TILE_MAX_ROWS = 512;  // STAGE 1 chunk capacity (16 KiB of LDS)
+constexpr int TILE_MAX_G = 64;      // partials staged in LDS by the merging workgroup
+
+template <int WAVES, int STAGE, int MERGE>
 __global__ __launch_bounds__(WAVES * 64) void k_top2_tile(const uint4 *__restrict__ query, int nq,
                                                           const uint32_t *__restrict__ train, int nt,
                                                           int rows_per_chunk, int G,
@@ -118,6 +128,8 @@ __global__ __launch_bounds__(WAVES * 64) void k_top2_tile(const uint4 *__restric
 {
     __shared__ uint32_t s_k1[WAVES][64];
     __shared__ uint32_t s_k2[WAVES][64];
+    __shared__ uint4 s_rows[STAGE ? 2 * TILE_MAX_ROWS : 1];
+    __shared__ uint2 s_part[TILE_MAX_G * 64];
     __shared__ int s_last;
 
     const int lane = threadIdx.x & 63;
@@ -125,7 +137,13 @@ __global__ __launch_bounds__(WAVES * 64) void k_top2_tile(const uint4 *__restric
     const int qb = blockIdx.x;
     const int c = blockIdx.y;
     const int qi = qb * 64 + lane;
+    const int r0 = c * rows_per_chunk;
+    const int r1 = min(nt, r0 + rows_per_chunk);
 
+    if (STAGE) {
+        const uint4 *tv = (const uint4 *)train + 2 * (size_t)r0;
+        for (int i = threadIdx.x; i < 2 * (r1 - r0); i += WAVES * 64) s_rows[i] = tv[i];
+    }
     uint32_t qd[8];
     {
         const int qq = qi < nq ? qi : nq - 1;
@@ -133,26 +151,46 @@ __global__ __launch_bounds__(WAVES * 64) void k_top2_tile(const uint4 *__restric
         qd[0] = a.x; qd[1] = a.y; qd[2] = a.z; qd[3] = a.w;
         qd[4] = b.x; qd[5] = b.y; qd[6] = b.z; qd[7] = b.w;
     }
-    const int r0 = c * rows_per_chunk;
-    const int r1 = min(nt, r0 + rows_per_chunk);
     uint32_t k1 = KEY_EMPTY, k2 = KEY_EMPTY;
-
-    // rows r0 + w + WAVES*j: wave-uniform, consumed from SGPRs (scalar loads)
-    int r = r0 + w;
-    for (; r + 3 * WAVES < r1; r += 4 * WAVES) {
-        const uint32_t *t0 = train + (size_t)r * 8;
-        const uint32_t *t1 = t0 + 8 * WAVES;
-        const uint32_t *t2 = t1 + 8 * WAVES;
-        const uint32_t *t3 = t2 + 8 * WAVES;
-        const uint32_t l = (uint32_t)(r - r0);
-        key_push(k1, k2, (hamming8(qd, t0) << KEY_SHIFT) | l);
-        key_push(k1, k2, (hamming8(qd, t1) << KEY_SHIFT) | (l + WAVES));
-        key_push(k1, k2, (hamming8(qd, t2) << KEY_SHIFT) | (l + 2 * WAVES));
-        key_push(k1, k2, (hamming8(qd, t3) << KEY_SHIFT) | (l + 3 * WAVES));
-    }
-    for (; r < r1; r += WAVES) {
-        const uint32_t *t0 = train + (size_t)r * 8;
-        key_push(k1, k2, (hamming8(qd, t0) << KEY_SHIFT) | (uint32_t)(r - r0));
+    if (STAGE) {
+        __syncthreads();
+        const int nr = r1 - r0;
+        int j = w;
+        for (; j + 3 * WAVES < nr; j += 4 * WAVES) {
+            uint32_t t[4][8];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint4 a = s_rows[2 * (j + u * WAVES)], b = s_rows[2 * (j + u * WAVES) + 1];
+                t[u][0] = a.x; t[u][1] = a.y; t[u][2] = a.z; t[u][3] = a.w;
+                t[u][4] = b.x; t[u][5] = b.y; t[u][6] = b.z; t[u][7] = b.w;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                key_push(k1, k2, (hamming8(qd, t[u]) << KEY_SHIFT) | (uint32_t)(j + u * WAVES));
+        }
+        for (; j < nr; j += WAVES) {
+            const uint4 a = s_rows[2 * j], b = s_rows[2 * j + 1];
+            const uint32_t t[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+            key_push(k1, k2, (hamming8(qd, t) << KEY_SHIFT) | (uint32_t)j);
+        }
+    } else {
+        // rows r0 + w + WAVES*j: wave-uniform, consumed from SGPRs (scalar loads)
+        int r = r0 + w;
+        for (; r + 3 * WAVES < r1; r += 4 * WAVES) {
+            const uint32_t *t0 = train + (size_t)r * 8;
+            const uint32_t *t1 = t0 + 8 * WAVES;
+            const uint32_t *t2 = t1 + 8 * WAVES;
+            const uint32_t *t3 = t2 + 8 * WAVES;
+            const uint32_t l = (uint32_t)(r - r0);
+            key_push(k1, k2, (hamming8(qd, t0) << KEY_SHIFT) | l);
+            key_push(k1, k2, (hamming8(qd, t1) << KEY_SHIFT) | (l + WAVES));
+            key_push(k1, k2, (hamming8(qd, t2) << KEY_SHIFT) | (l + 2 * WAVES));
+            key_push(k1, k2, (hamming8(qd, t3) << KEY_SHIFT) | (l + 3 * WAVES));
+        }
+        for (; r < r1; r += WAVES) {
+            const uint32_t *t0 = train + (size_t)r * 8;
+            key_push(k1, k2, (hamming8(qd, t0) << KEY_SHIFT) | (uint32_t)(r - r0));
+        }
     }
 
     if (WAVES > 1) {
@@ -171,25 +209,50 @@ __global__ __launch_bounds__(WAVES * 64) void k_top2_tile(const uint4 *__restric
         }
         return;
     }
-    // publish this chunk's partial, then the last-arriving workgroup of this query block merges
-    if (w == 0 && qi < nq) part[(size_t)c * nq + qi] = key_to_part(k1, k2, (uint32_t)r0);
+    // publish this chunk's partial; the last-arriving workgroup of this query block merges
+    if (w == 0 && qi < nq) {
+        const uint2 p = key_to_part(k1, k2, (uint32_t)r0);
+        if (MERGE == 1) {
+            const unsigned long long v = ((unsigned long long)p.y << 32) | p.x;
+            __hip_atomic_store((unsigned long long *)&part[(size_t)c * nq + qi], v, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            part[(size_t)c * nq + qi] = p;
+        }
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        const uint32_t prev =
-            __hip_atomic_fetch_add(&counters[qb], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t prev;
+        if (MERGE == 1)
+            prev = __hip_atomic_fetch_add(&counters[qb], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            prev = __hip_atomic_fetch_add(&counters[qb], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
         s_last = (prev == (uint32_t)(G - 1));
     }
     __syncthreads();
     if (!s_last) return;
+    // stage all G partials of this query block in LDS with one round of parallel loads
+    for (int i = threadIdx.x; i < G * 64; i += WAVES * 64) {
+        const int cc = i >> 6, l = i & 63, qq = qb * 64 + l;
+        if (qq < nq) {
+            if (MERGE == 1) {
+                const unsigned long long v = __hip_atomic_load(
+                    (unsigned long long *)&part[(size_t)cc * nq + qq], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_part[i] = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+            } else {
+                s_part[i] = part[(size_t)cc * nq + qq];
+            }
+        }
+    }
+    __syncthreads();
     if (w == 0 && qi < nq) {
         uint32_t D1 = D_EMPTY, I1 = 0xFFFFFFFFu, D2 = D_EMPTY;
-        for (int cc = 0; cc < G; cc++) part_merge(D1, I1, D2, part[(size_t)cc * nq + qi]);
+        for (int cc = 0; cc < G; cc++) part_merge(D1, I1, D2, s_part[cc * 64 + lane]);
         write_result(out, qi, D1, I1, D2);
     }
     if (threadIdx.x == 0) __hip_atomic_store(&counters[qb], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-
 
 // ----------------------------------------------------------------------------- stream kernel
 template <int NQ>
@@ -356,19 +419,30 @@ int osg_launch_top2(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d
     constexpr int WAVES = 4;
     const int nqb = (nq + 63) / 64;
     OSG_REQUIRE(ctx, nqb <= OSG_N_COUNTERS - 1, "too many queries (%d)", nq);
+    const int variant = env_int("OSG_TOP2_VARIANT", 2);
     const int target_wg = env_int("OSG_TOP2_WG", 4 * cus);
     const int min_rows = env_int("OSG_TOP2_MIN_ROWS", WAVES * 32);
     int G = (target_wg + nqb - 1) / nqb;
     G = std::min(G, std::max(1, nt / min_rows));
     G = std::max(G, (nt + (int)IDX_MASK) / ((int)IDX_MASK + 1)); // chunk-local index fits 23 bits
-    G = std::max(1, std::min(G, 65535));
-    const int rpc = (nt + G - 1) / G;
+    const bool staged = (variant == 2) && (nt + G - 1) / G <= TILE_MAX_ROWS;
+    if (variant == 2 && !staged) G = std::max(G, (nt + TILE_MAX_ROWS - 1) / TILE_MAX_ROWS);
+    G = std::max(1, std::min(G, TILE_MAX_G));
+    int rpc = (nt + G - 1) / G;
     G = (nt + rpc - 1) / rpc;
+    const bool use_stage = (variant == 2) && rpc <= TILE_MAX_ROWS;
     uint2 *part = nullptr;
     if (G > 1) OSG_ALLOC(ctx, part, SLOT_PART, sizeof(uint2) * (size_t)G * nq);
-    hipLaunchKernelGGL(k_top2_tile<WAVES>, dim3(nqb, G), dim3(WAVES * 64), 0, ctx->stream,
-                       (const uint4 *)d_query, nq, (const uint32_t *)d_train, nt, rpc, G, part,
-                       ctx->counters, (int32_t *)d_out);
+    const dim3 grid(nqb, G), block(WAVES * 64);
+    const uint4 *q = (const uint4 *)d_query;
+    const uint32_t *t = (const uint32_t *)d_train;
+    int32_t *o = (int32_t *)d_out;
+    if (use_stage)
+        hipLaunchKernelGGL((k_top2_tile<WAVES, 1, 1>), grid, block, 0, ctx->stream, q, nq, t, nt, rpc, G, part, ctx->counters, o);
+    else if (variant == 0)
+        hipLaunchKernelGGL((k_top2_tile<WAVES, 0, 0>), grid, block, 0, ctx->stream, q, nq, t, nt, rpc, G, part, ctx->counters, o);
+    else
+        hipLaunchKernelGGL((k_top2_tile<WAVES, 0, 1>), grid, block, 0, ctx->stream, q, nq, t, nt, rpc, G, part, ctx->counters, o);
     OSG_HIP_CHECK(ctx, hipGetLastError());
     return OSG_OK;
 }

@@ -88,3 +88,26 @@ def test_pairwise_distance(ctx, oracle):
     got = ctx.descriptor_distance_pairs(a, b)
     ref = np.array([oracle.oracle_descriptor_distance(ptr(a[i]), ptr(b[i])) for i in range(len(a))])
     np.testing.assert_array_equal(got, ref)
+
+
+def test_alternating_problems_no_stale_partials(ctx, oracle):
+    """Partials and counters are reused between calls: alternate two different problems so a
+    stale partial from the previous call would show up as a mismatch."""
+    p1 = synth.descriptors_c2(2000, 2000, seed=21)
+    p2 = synth.descriptors_c2(2000, 2000, seed=22)
+    r1 = otop2(oracle, *p1)
+    r2 = otop2(oracle, *p2)
+    for i in range(30):
+        q, t = (p1, p2)[i % 2]
+        ref = (r1, r2)[i % 2]
+        got = ctx.hamming_top2(q, t)
+        for g, r in zip(got, ref):
+            np.testing.assert_array_equal(g, r)
+
+
+@pytest.mark.parametrize("variant", ["0", "1", "2"])
+def test_tile_variants(ctx, oracle, variant, monkeypatch):
+    monkeypatch.setenv("OSG_TOP2_VARIANT", variant)
+    for seed, (nq, nt) in enumerate([(2000, 2000), (300, 20000), (5000, 600)]):
+        q, t = synth.descriptors_c2(nq, nt, seed=900 + seed)
+        check(ctx, oracle, q, t)

@@ -1,0 +1,64 @@
+"""Time the top-2 kernels under different launch configurations (env knobs read per launch)."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from orb_slam3_comments_ghr_amd import Context, synth  # noqa: E402
+
+
+def time_cfg(ctx, stream, dq, nq, dt, nt, dout, n=300):
+    for _ in range(20):
+        ctx.hamming_top2_dev(dq, nq, dt, nt, dout)
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+    for a, b in evs:
+        a.record(stream)
+        ctx.hamming_top2_dev(dq, nq, dt, nt, dout)
+        b.record(stream)
+    torch.cuda.synchronize()
+    ks = np.array([a.elapsed_time(b) for a, b in evs]) * 1e3
+    # back-to-back wall per launch
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record(stream)
+    for _ in range(n):
+        ctx.hamming_top2_dev(dq, nq, dt, nt, dout)
+    e.record(stream)
+    torch.cuda.synchronize()
+    return float(np.median(ks)), float(s.elapsed_time(e) * 1e3 / n)
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    ctx = Context(0)
+    ctx.set_stream(stream.cuda_stream)
+    res = []
+    for (nq, nt) in [(2000, 2000), (20000, 20000)]:
+        q, t = synth.descriptors_c2(nq, nt)
+        dq = torch.from_numpy(q).to(dev)
+        dt = torch.from_numpy(t).to(dev)
+        dout = torch.empty((nq, 3), dtype=torch.int32, device=dev)
+        ref = ctx.hamming_top2(q, t)
+        for variant in sys.argv[1].split(","):
+            for wg in [int(x) for x in sys.argv[2].split(",")]:
+                for mr in [int(x) for x in sys.argv[3].split(",")]:
+                    os.environ["OSG_TOP2_VARIANT"] = variant
+                    os.environ["OSG_TOP2_WG"] = str(wg)
+                    os.environ["OSG_TOP2_MIN_ROWS"] = str(mr)
+                    k_us, wall_us = time_cfg(ctx, stream, dq, nq, dt, nt, dout)
+                    o = dout.cpu().numpy()
+                    ok = all(np.array_equal(o[:, i], ref[i]) for i in range(3))
+                    r = dict(nq=nq, nt=nt, variant=variant, wg=wg, min_rows=mr, kernel_us=round(k_us, 2),
+                             wall_us=round(wall_us, 2), tops=round(nq * nt * 19 / k_us / 1e6, 2), ok=ok)
+                    print(json.dumps(r), flush=True)
+                    res.append(r)
+
+
+if __name__ == "__main__":
+    main()
