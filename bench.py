@@ -104,6 +104,9 @@ def main():
     # ---- dominant kernel roofline: per-launch HIP events on the launch stream ----------------
     n_ev = max(50, min(args.steps, 500))
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
+    # pre-fill the stream with a spin kernel so the host enqueues every (event, kernel, event)
+    # before the GPU reaches them: each bracket then holds the kernel, not host launch gaps
+    torch.cuda._sleep(int(2e6 + n_ev * 2e4))
     for a, b in evs:
         a.record(stream)
         step()
@@ -158,6 +161,7 @@ def main():
             ctx.hamming_top2_dev(sq, Q, st, M, so)
         torch.cuda.synchronize(dev)
         sev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+        torch.cuda._sleep(2_000_000)
         for a, b in sev:
             a.record(stream)
             ctx.hamming_top2_dev(sq, Q, st, M, so)

@@ -124,7 +124,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_top2_tile(const uint4 *__restric
                                                           int rows_per_chunk, int G,
                                                           uint2 *__restrict__ part,
                                                           uint32_t *__restrict__ counters,
-                                                          int32_t *__restrict__ out)
+                                                          int32_t *__restrict__ out, int dbg)
 {
     __shared__ uint32_t s_k1[WAVES][64];
     __shared__ uint32_t s_k2[WAVES][64];
@@ -154,7 +154,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_top2_tile(const uint4 *__restric
     uint32_t k1 = KEY_EMPTY, k2 = KEY_EMPTY;
     if (STAGE) {
         __syncthreads();
-        const int nr = r1 - r0;
+        const int nr = (dbg & 1) ? 0 : r1 - r0;
         int j = w;
         for (; j + 3 * WAVES < nr; j += 4 * WAVES) {
             uint32_t t[4][8];
@@ -231,7 +231,9 @@ __global__ __launch_bounds__(WAVES * 64) void k_top2_tile(const uint4 *__restric
         s_last = (prev == (uint32_t)(G - 1));
     }
     __syncthreads();
-    if (!s_last) return;
+    if (s_last && (dbg & 2) && threadIdx.x == 0)
+        __hip_atomic_store(&counters[qb], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!s_last || (dbg & 2)) return;
     // stage all G partials of this query block in LDS with one round of parallel loads
     for (int i = threadIdx.x; i < G * 64; i += WAVES * 64) {
         const int cc = i >> 6, l = i & 63, qq = qb * 64 + l;
@@ -372,10 +374,21 @@ __global__ __launch_bounds__(256) void k_pair_dist(const uint4 *__restrict__ a, 
              __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
 }
 
+// tuning knobs (environment, read once per process; defaults from the r01 sweeps on MI355X)
 int env_int(const char *name, int dflt)
 {
     const char *v = getenv(name);
     return (v && *v) ? atoi(v) : dflt;
+}
+struct top2_knobs {
+    int variant, waves, target_wg, min_rows, dbg, stream_g;
+};
+const top2_knobs &knobs(int cus)
+{
+    static const top2_knobs k = {env_int("OSG_TOP2_VARIANT", 2), env_int("OSG_TOP2_WAVES", 0),
+                                 env_int("OSG_TOP2_WG", cus), env_int("OSG_TOP2_MIN_ROWS", 64),
+                                 env_int("OSG_TOP2_DEBUG", 0), env_int("OSG_TOP2_STREAM_G", 8 * cus)};
+    return k;
 }
 
 }  // namespace
@@ -399,7 +412,7 @@ int osg_launch_top2(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d
     const int cus = ctx->num_cus;
     if (nq <= 8 && nt >= 65536) {
         // streaming shape: lane = train row
-        int G = env_int("OSG_TOP2_STREAM_G", 8 * cus);
+        int G = knobs(cus).stream_g;
         int rpb = (nt + G - 1) / G;
         rpb = ((rpb + 1023) / 1024) * 1024;
         G = (nt + rpb - 1) / rpb;
@@ -416,17 +429,19 @@ int osg_launch_top2(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d
         OSG_HIP_CHECK(ctx, hipGetLastError());
         return OSG_OK;
     }
-    constexpr int WAVES = 4;
+    const top2_knobs &kn = knobs(cus);
+    const int waves = kn.waves > 0 ? kn.waves : (nq <= 4096 ? 16 : 8);
+    const int WAVES = (waves >= 16) ? 16 : (waves >= 8 ? 8 : 4);
     const int nqb = (nq + 63) / 64;
     OSG_REQUIRE(ctx, nqb <= OSG_N_COUNTERS - 1, "too many queries (%d)", nq);
-    const int variant = env_int("OSG_TOP2_VARIANT", 2);
-    const int target_wg = env_int("OSG_TOP2_WG", 4 * cus);
-    const int min_rows = env_int("OSG_TOP2_MIN_ROWS", WAVES * 32);
+    const int variant = kn.variant;
+    const int dbg = kn.dbg;
+    const int target_wg = kn.target_wg;
+    const int min_rows = kn.min_rows;
     int G = (target_wg + nqb - 1) / nqb;
     G = std::min(G, std::max(1, nt / min_rows));
     G = std::max(G, (nt + (int)IDX_MASK) / ((int)IDX_MASK + 1)); // chunk-local index fits 23 bits
-    const bool staged = (variant == 2) && (nt + G - 1) / G <= TILE_MAX_ROWS;
-    if (variant == 2 && !staged) G = std::max(G, (nt + TILE_MAX_ROWS - 1) / TILE_MAX_ROWS);
+    if (variant == 2) G = std::max(G, (nt + TILE_MAX_ROWS - 1) / TILE_MAX_ROWS);
     G = std::max(1, std::min(G, TILE_MAX_G));
     int rpc = (nt + G - 1) / G;
     G = (nt + rpc - 1) / rpc;
@@ -437,12 +452,20 @@ int osg_launch_top2(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d
     const uint4 *q = (const uint4 *)d_query;
     const uint32_t *t = (const uint32_t *)d_train;
     int32_t *o = (int32_t *)d_out;
-    if (use_stage)
-        hipLaunchKernelGGL((k_top2_tile<WAVES, 1, 1>), grid, block, 0, ctx->stream, q, nq, t, nt, rpc, G, part, ctx->counters, o);
-    else if (variant == 0)
-        hipLaunchKernelGGL((k_top2_tile<WAVES, 0, 0>), grid, block, 0, ctx->stream, q, nq, t, nt, rpc, G, part, ctx->counters, o);
-    else
-        hipLaunchKernelGGL((k_top2_tile<WAVES, 0, 1>), grid, block, 0, ctx->stream, q, nq, t, nt, rpc, G, part, ctx->counters, o);
+#define OSG_TILE_LAUNCH(W)                                                                                     \
+    if (use_stage)                                                                                             \
+        hipLaunchKernelGGL((k_top2_tile<W, 1, 1>), grid, block, 0, ctx->stream, q, nq, t, nt, rpc, G, part,   \
+                           ctx->counters, o, dbg);                                                            \
+    else if (variant == 0)                                                                                     \
+        hipLaunchKernelGGL((k_top2_tile<W, 0, 0>), grid, block, 0, ctx->stream, q, nq, t, nt, rpc, G, part,   \
+                           ctx->counters, o, dbg);                                                            \
+    else                                                                                                       \
+        hipLaunchKernelGGL((k_top2_tile<W, 0, 1>), grid, block, 0, ctx->stream, q, nq, t, nt, rpc, G, part,   \
+                           ctx->counters, o, dbg);
+    if (WAVES == 16) { OSG_TILE_LAUNCH(16) }
+    else if (WAVES == 8) { OSG_TILE_LAUNCH(8) }
+    else { OSG_TILE_LAUNCH(4) }
+#undef OSG_TILE_LAUNCH
     OSG_HIP_CHECK(ctx, hipGetLastError());
     return OSG_OK;
 }

@@ -105,9 +105,27 @@ def test_alternating_problems_no_stale_partials(ctx, oracle):
             np.testing.assert_array_equal(g, r)
 
 
-@pytest.mark.parametrize("variant", ["0", "1", "2"])
-def test_tile_variants(ctx, oracle, variant, monkeypatch):
-    monkeypatch.setenv("OSG_TOP2_VARIANT", variant)
+@pytest.mark.parametrize("variant,waves", [("0", "4"), ("1", "8"), ("2", "16"), ("2", "4")])
+def test_tile_variants(oracle, variant, waves):
+    """Every tile variant (scalar/LDS staging x fence/write-through merge x 4/8/16 waves) in a
+    fresh process: the knobs are read once per process."""
+    import subprocess, sys, os, json
+    code = (
+        "import numpy as np, json\n"
+        "from orb_slam3_comments_ghr_amd import Context, synth\n"
+        "c = Context(0)\n"
+        "out = []\n"
+        "for seed, (nq, nt) in enumerate([(2000, 2000), (300, 20000), (5000, 600)]):\n"
+        "    q, t = synth.descriptors_c2(nq, nt, seed=900 + seed)\n"
+        "    out.append([a.tolist() for a in c.hamming_top2(q, t)])\n"
+        "print(json.dumps(out))\n")
+    env = dict(os.environ, OSG_TOP2_VARIANT=variant, OSG_TOP2_WAVES=waves)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = json.loads(r.stdout.strip().splitlines()[-1])
     for seed, (nq, nt) in enumerate([(2000, 2000), (300, 20000), (5000, 600)]):
         q, t = synth.descriptors_c2(nq, nt, seed=900 + seed)
-        check(ctx, oracle, q, t)
+        ref = otop2(oracle, q, t)
+        for g, rr in zip(got[seed], ref):
+            np.testing.assert_array_equal(np.array(g, np.int32), rr)
