@@ -1,0 +1,384 @@
+"""Structure-of-arrays views of the reference's Frame / KeyFrame / MapPoint fields.
+
+These are what the ORB-SLAM3-side adapter gathers before calling the C ABI (see
+INTEGRATION.md): plain numpy arrays with the reference's field meaning, plus ``.struct()``
+builders for the ctypes mirrors in ``_abi``.  Also the seeded synthetic generators for the
+matching configs.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _abi
+from .synth import EUROC_BF, EUROC_FX, EUROC_H, EUROC_W
+
+
+def _p(a):
+    return None if a is None else int(a.ctypes.data)
+
+
+def _c(a, dt):
+    return None if a is None else np.ascontiguousarray(a, dtype=dt)
+
+
+def pos_in_grid(x, y, min_x, min_y, inv_w, inv_h):
+    """Frame::PosInGrid (ref:src/Frame.cc:973-989): round() of float products."""
+    vx = ((np.float32(x) - np.float32(min_x)) * np.float32(inv_w)).astype(np.float32)
+    vy = ((np.float32(y) - np.float32(min_y)) * np.float32(inv_h)).astype(np.float32)
+
+    def cround(v):  # C round(): half away from zero, on the exact float value
+        v = v.astype(np.float64)
+        return np.where(v >= 0, np.floor(v + 0.5), np.ceil(v - 0.5)).astype(np.int64)
+
+    return cround(vx), cround(vy)
+
+
+def build_grid(kp_x, kp_y, min_x, min_y, inv_w, inv_h):
+    """Frame::AssignFeaturesToGrid (ref:src/Frame.cc:469-507) as CSR, cell = ix*48 + iy."""
+    px, py = pos_in_grid(kp_x, kp_y, min_x, min_y, inv_w, inv_h)
+    ok = (px >= 0) & (px < _abi.GRID_COLS) & (py >= 0) & (py < _abi.GRID_ROWS)
+    cell = np.where(ok, px * _abi.GRID_ROWS + py, -1)
+    idx = np.nonzero(ok)[0]
+    order = np.argsort(cell[idx], kind="stable")  # stable: ascending feature index inside a cell
+    items = idx[order].astype(np.int32)
+    counts = np.bincount(cell[idx], minlength=_abi.GRID_CELLS)
+    start = np.zeros(_abi.GRID_CELLS + 1, np.int32)
+    start[1:] = np.cumsum(counts)
+    return start, items
+
+
+def scale_factors(n_levels=8, factor=1.2):
+    s = np.ones(n_levels, np.float32)
+    for i in range(1, n_levels):
+        s[i] = np.float32(s[i - 1] * np.float32(factor))
+    return s
+
+
+@dataclass
+class FrameSoA:
+    desc: np.ndarray          # n x 32 uint8
+    kp_x: np.ndarray
+    kp_y: np.ndarray
+    kp_angle: np.ndarray
+    kp_octave: np.ndarray
+    u_right: np.ndarray | None = None
+    min_x: float = 0.0
+    max_x: float = float(EUROC_W)
+    min_y: float = 0.0
+    max_y: float = float(EUROC_H)
+    scale: np.ndarray = field(default_factory=scale_factors)
+    mb: float = EUROC_BF / EUROC_FX
+    mbf: float = EUROC_BF
+    nleft: int = -1
+    grid_start: np.ndarray | None = None
+    grid_idx: np.ndarray | None = None
+
+    def __post_init__(self):
+        self.desc = _c(self.desc, np.uint8).reshape(-1, 32)
+        self.kp_x = _c(self.kp_x, np.float32)
+        self.kp_y = _c(self.kp_y, np.float32)
+        self.kp_angle = _c(self.kp_angle, np.float32)
+        self.kp_octave = _c(self.kp_octave, np.int32)
+        self.u_right = _c(self.u_right, np.float32)
+        self.scale = _c(self.scale, np.float32)
+        self.inv_w = np.float32(np.float32(_abi.GRID_COLS) / np.float32(self.max_x - self.min_x))
+        self.inv_h = np.float32(np.float32(_abi.GRID_ROWS) / np.float32(self.max_y - self.min_y))
+        if self.grid_start is None:
+            self.grid_start, self.grid_idx = build_grid(self.kp_x, self.kp_y, self.min_x, self.min_y,
+                                                        self.inv_w, self.inv_h)
+
+    @property
+    def n(self):
+        return self.desc.shape[0]
+
+    def struct(self):
+        s = _abi.OsgFrame()
+        s.n = self.n
+        s.nleft = self.nleft
+        s.desc = _p(self.desc)
+        s.kp_x = _p(self.kp_x)
+        s.kp_y = _p(self.kp_y)
+        s.kp_angle = _p(self.kp_angle)
+        s.kp_octave = _p(self.kp_octave)
+        s.u_right = _p(self.u_right)
+        s.grid_start = _p(self.grid_start)
+        s.grid_idx = _p(self.grid_idx)
+        s.min_x, s.max_x, s.min_y, s.max_y = self.min_x, self.max_x, self.min_y, self.max_y
+        s.grid_inv_w = float(self.inv_w)
+        s.grid_inv_h = float(self.inv_h)
+        s.scale_factors = _p(self.scale)
+        s.n_levels = len(self.scale)
+        s.mb = self.mb
+        s.mbf = self.mbf
+        return s
+
+
+@dataclass
+class MPQueries:
+    """Local map points after Frame::isInFrustum (a5)."""
+    mp_id: np.ndarray
+    desc: np.ndarray
+    usable: np.ndarray
+    has_obs: np.ndarray
+    in_view: np.ndarray
+    proj_x: np.ndarray
+    proj_y: np.ndarray
+    proj_xr: np.ndarray
+    view_cos: np.ndarray
+    pred_level: np.ndarray
+    track_depth: np.ndarray
+
+    def __post_init__(self):
+        for k, dt in [("mp_id", np.int32), ("desc", np.uint8), ("usable", np.uint8), ("has_obs", np.uint8),
+                      ("in_view", np.uint8), ("proj_x", np.float32), ("proj_y", np.float32),
+                      ("proj_xr", np.float32), ("view_cos", np.float32), ("pred_level", np.int32),
+                      ("track_depth", np.float32)]:
+            setattr(self, k, _c(getattr(self, k), dt))
+
+    def struct(self):
+        s = _abi.OsgMpQueries()
+        s.n = len(self.mp_id)
+        for k in ["mp_id", "desc", "usable", "has_obs", "in_view", "proj_x", "proj_y", "proj_xr",
+                  "view_cos", "pred_level", "track_depth"]:
+            setattr(s, k, _p(getattr(self, k)))
+        return s
+
+
+@dataclass
+class LastQueries:
+    """LastFrame map points projected into the current frame (a6)."""
+    mp_id: np.ndarray
+    desc: np.ndarray
+    valid: np.ndarray
+    has_obs: np.ndarray
+    u: np.ndarray
+    v: np.ndarray
+    invz: np.ndarray
+    octave: np.ndarray
+    angle: np.ndarray
+    tlc_z: float = 0.0
+
+    def __post_init__(self):
+        for k, dt in [("mp_id", np.int32), ("desc", np.uint8), ("valid", np.uint8), ("has_obs", np.uint8),
+                      ("u", np.float32), ("v", np.float32), ("invz", np.float32), ("octave", np.int32),
+                      ("angle", np.float32)]:
+            setattr(self, k, _c(getattr(self, k), dt))
+
+    def struct(self):
+        s = _abi.OsgLastQueries()
+        s.n = len(self.mp_id)
+        for k in ["mp_id", "desc", "valid", "has_obs", "u", "v", "invz", "octave", "angle"]:
+            setattr(s, k, _p(getattr(self, k)))
+        s.tlc_z = float(self.tlc_z)
+        return s
+
+
+@dataclass
+class KFQueries:
+    """KeyFrame map points projected into the current frame (a7, relocalisation)."""
+    mp_id: np.ndarray
+    desc: np.ndarray
+    valid: np.ndarray
+    u: np.ndarray
+    v: np.ndarray
+    pred_level: np.ndarray
+    angle: np.ndarray
+
+    def __post_init__(self):
+        for k, dt in [("mp_id", np.int32), ("desc", np.uint8), ("valid", np.uint8), ("u", np.float32),
+                      ("v", np.float32), ("pred_level", np.int32), ("angle", np.float32)]:
+            setattr(self, k, _c(getattr(self, k), dt))
+
+    def struct(self):
+        s = _abi.OsgKfQueries()
+        s.n = len(self.mp_id)
+        for k in ["mp_id", "desc", "valid", "u", "v", "pred_level", "angle"]:
+            setattr(s, k, _p(getattr(self, k)))
+        return s
+
+
+@dataclass
+class BowSide:
+    """One side of SearchByBoW: descriptors, angles, map-point slots and the FeatureVector."""
+    desc: np.ndarray
+    angle: np.ndarray
+    mp_id: np.ndarray
+    mp_good: np.ndarray
+    node_id: np.ndarray
+    node_start: np.ndarray
+    feat: np.ndarray
+    nleft: int = -1
+
+    def __post_init__(self):
+        self.desc = _c(self.desc, np.uint8).reshape(-1, 32)
+        self.angle = _c(self.angle, np.float32)
+        self.mp_id = _c(self.mp_id, np.int32)
+        self.mp_good = _c(self.mp_good, np.uint8)
+        self.node_id = _c(self.node_id, np.uint32)
+        self.node_start = _c(self.node_start, np.int32)
+        self.feat = _c(self.feat, np.int32)
+
+    @property
+    def n(self):
+        return self.desc.shape[0]
+
+    def struct(self):
+        s = _abi.OsgBowSide()
+        s.n = self.n
+        s.nleft = self.nleft
+        s.desc = _p(self.desc)
+        s.angle = _p(self.angle)
+        s.mp_id = _p(self.mp_id)
+        s.mp_good = _p(self.mp_good)
+        s.fv.n_nodes = len(self.node_id)
+        s.fv.node_id = _p(self.node_id)
+        s.fv.node_start = _p(self.node_start)
+        s.fv.feat = _p(self.feat)
+        return s
+
+
+# ------------------------------------------------------------------------------- generators
+
+def _flip(rng, rows, p):
+    bits = np.unpackbits(rows, axis=1)
+    return np.packbits(bits ^ (rng.random(bits.shape) < p).astype(np.uint8), axis=1)
+
+
+def synth_frame(rng, n=1200, stereo=True, n_levels=8):
+    """Keypoints uniform in 752x480, octave ~ geometric(1/1.2) truncated to 8 levels,
+    angle U[0,360), 60 % with a stereo u_R (bf = 47.9)."""
+    x = rng.uniform(0, EUROC_W, n).astype(np.float32)
+    y = rng.uniform(0, EUROC_H, n).astype(np.float32)
+    p = np.array([1.2 ** -i for i in range(n_levels)])
+    oct_ = rng.choice(n_levels, size=n, p=p / p.sum()).astype(np.int32)
+    ang = rng.uniform(0, 360, n).astype(np.float32)
+    desc = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    ur = None
+    if stereo:
+        depth = rng.uniform(1, 10, n)
+        ur = np.where(rng.random(n) < 0.6, x - EUROC_BF / depth, -1.0).astype(np.float32)
+    return FrameSoA(desc=desc, kp_x=x, kp_y=y, kp_angle=ang, kp_octave=oct_, u_right=ur,
+                    scale=scale_factors(n_levels))
+
+
+def synth_mp_queries(rng, F: FrameSoA, m=3000, noise_px=3.0, match_frac=0.6):
+    """Local map points whose projections land near frame keypoints (a5)."""
+    n = F.n
+    tgt = rng.integers(0, n, m)
+    is_match = rng.random(m) < match_frac
+    px = np.where(is_match, F.kp_x[tgt] + rng.normal(0, noise_px, m), rng.uniform(0, EUROC_W, m))
+    py = np.where(is_match, F.kp_y[tgt] + rng.normal(0, noise_px, m), rng.uniform(0, EUROC_H, m))
+    desc = rng.integers(0, 256, (m, 32), dtype=np.uint8)
+    desc[is_match] = _flip(rng, F.desc[tgt[is_match]], 0.06)
+    lvl = np.clip(F.kp_octave[tgt] + rng.integers(-1, 2, m), 0, len(F.scale) - 1)
+    depth = rng.uniform(0.5, 60.0, m)
+    pxr = (px - EUROC_BF / depth).astype(np.float32)
+    if F.u_right is not None:
+        pxr = np.where(is_match & (F.u_right[tgt] > 0), F.u_right[tgt] + rng.normal(0, 1.0, m), pxr)
+    return MPQueries(
+        mp_id=np.arange(1000, 1000 + m), desc=desc, usable=rng.random(m) < 0.98,
+        has_obs=rng.random(m) < 0.93, in_view=rng.random(m) < 0.85, proj_x=px, proj_y=py,
+        proj_xr=pxr, view_cos=rng.uniform(0.99, 1.0, m), pred_level=lvl, track_depth=depth)
+
+
+def synth_slots(rng, n, frac_assigned=0.1, frac_taken=0.7, id_base=500000):
+    slot_mp = np.where(rng.random(n) < frac_assigned, id_base + np.arange(n), -1).astype(np.int32)
+    slot_taken = ((slot_mp >= 0) & (rng.random(n) < frac_taken)).astype(np.uint8)
+    return slot_mp, slot_taken
+
+
+def synth_last_queries(rng, F: FrameSoA, n_last=1000, noise_px=2.0, match_frac=0.7, tlc_z=0.0):
+    n = F.n
+    tgt = rng.integers(0, n, n_last)
+    is_match = rng.random(n_last) < match_frac
+    u = np.where(is_match, F.kp_x[tgt] + rng.normal(0, noise_px, n_last), rng.uniform(-20, EUROC_W + 20, n_last))
+    v = np.where(is_match, F.kp_y[tgt] + rng.normal(0, noise_px, n_last), rng.uniform(-20, EUROC_H + 20, n_last))
+    desc = rng.integers(0, 256, (n_last, 32), dtype=np.uint8)
+    desc[is_match] = _flip(rng, F.desc[tgt[is_match]], 0.06)
+    depth = rng.uniform(1, 20, n_last)
+    invz = (1.0 / depth * np.where(rng.random(n_last) < 0.02, -1, 1)).astype(np.float32)
+    if F.u_right is not None:
+        # make the stereo check pass for most true matches: u_R(target) ~ u - mbf*invz
+        pass
+    octv = np.where(is_match, F.kp_octave[tgt], rng.integers(0, len(F.scale), n_last)).astype(np.int32)
+    ang = np.where(is_match, F.kp_angle[tgt] + 7.0 + rng.normal(0, 3, n_last), rng.uniform(0, 360, n_last))
+    ang = np.mod(ang, 360).astype(np.float32)
+    mp_id = np.where(rng.random(n_last) < 0.9, 2000 + np.arange(n_last), -1)
+    valid = (mp_id >= 0) & (rng.random(n_last) < 0.9)
+    return LastQueries(mp_id=mp_id, desc=desc, valid=valid, has_obs=rng.random(n_last) < 0.9, u=u, v=v,
+                       invz=invz, octave=octv, angle=ang, tlc_z=tlc_z)
+
+
+def synth_kf_queries(rng, F: FrameSoA, n_kf=1000, noise_px=2.0, match_frac=0.6):
+    n = F.n
+    tgt = rng.integers(0, n, n_kf)
+    is_match = rng.random(n_kf) < match_frac
+    u = np.where(is_match, F.kp_x[tgt] + rng.normal(0, noise_px, n_kf), rng.uniform(0, EUROC_W, n_kf))
+    v = np.where(is_match, F.kp_y[tgt] + rng.normal(0, noise_px, n_kf), rng.uniform(0, EUROC_H, n_kf))
+    desc = rng.integers(0, 256, (n_kf, 32), dtype=np.uint8)
+    desc[is_match] = _flip(rng, F.desc[tgt[is_match]], 0.06)
+    lvl = np.clip(F.kp_octave[tgt] + rng.integers(-1, 2, n_kf), 0, len(F.scale) - 1)
+    ang = np.where(is_match, F.kp_angle[tgt] + 7.0 + rng.normal(0, 3, n_kf), rng.uniform(0, 360, n_kf))
+    return KFQueries(mp_id=3000 + np.arange(n_kf), desc=desc, valid=rng.random(n_kf) < 0.7, u=u, v=v,
+                     pred_level=lvl, angle=np.mod(ang, 360))
+
+
+def _featvec(rng, n, n_nodes, zipf=1.1, node_base=0):
+    w = 1.0 / np.arange(1, n_nodes + 1) ** zipf
+    node_of = rng.choice(n_nodes, size=n, p=w / w.sum())
+    ids = np.sort(rng.choice(np.arange(node_base, node_base + 10 * n_nodes), size=n_nodes, replace=False))
+    used = np.unique(node_of)
+    node_id = ids[used].astype(np.uint32)
+    node_start = np.zeros(len(used) + 1, np.int32)
+    feat = []
+    for k, nd in enumerate(used):
+        f = np.nonzero(node_of == nd)[0]
+        feat.append(f)
+        node_start[k + 1] = node_start[k] + len(f)
+    return node_id, node_start, np.concatenate(feat).astype(np.int32), node_of, ids
+
+
+def synth_bow_pair(rng, n_kf=1200, n_f=1200, n_nodes=100, mp_frac=0.7, copy_frac=0.6, flip=0.06,
+                   f_is_kf=False):
+    """KF and F (or KF2) sharing a vocabulary: 60 % of the second side's descriptors are noisy copies
+    of KF features (same node), angle offset +7 deg +- 3."""
+    kf_desc = rng.integers(0, 256, (n_kf, 32), dtype=np.uint8)
+    kf_ang = rng.uniform(0, 360, n_kf).astype(np.float32)
+    w = 1.0 / np.arange(1, n_nodes + 1) ** 1.1
+    node_ids = np.sort(rng.choice(np.arange(0, 10 * n_nodes), size=n_nodes, replace=False)).astype(np.uint32)
+    kf_node = rng.choice(n_nodes, size=n_kf, p=w / w.sum())
+    f_desc = rng.integers(0, 256, (n_f, 32), dtype=np.uint8)
+    f_ang = rng.uniform(0, 360, n_f).astype(np.float32)
+    f_node = rng.choice(n_nodes, size=n_f, p=w / w.sum())
+    src = rng.integers(0, n_kf, n_f)
+    cp = rng.random(n_f) < copy_frac
+    f_desc[cp] = _flip(rng, kf_desc[src[cp]], flip)
+    f_node[cp] = kf_node[src[cp]]
+    f_ang[cp] = np.mod(kf_ang[src[cp]] - 7.0 - rng.normal(0, 3, cp.sum()), 360).astype(np.float32)
+
+    def fv(node_of):
+        used = np.unique(node_of)
+        start = np.zeros(len(used) + 1, np.int32)
+        feats = []
+        for k, nd in enumerate(used):
+            f = np.nonzero(node_of == nd)[0]
+            feats.append(f)
+            start[k + 1] = start[k] + len(f)
+        return node_ids[used], start, np.concatenate(feats).astype(np.int32)
+
+    a = fv(kf_node)
+    b = fv(f_node)
+    kf_mp = np.where(rng.random(n_kf) < mp_frac, 10000 + np.arange(n_kf), -1).astype(np.int32)
+    kf_good = ((kf_mp >= 0) & (rng.random(n_kf) < 0.98)).astype(np.uint8)
+    KF = BowSide(kf_desc, kf_ang, kf_mp, kf_good, *a)
+    if f_is_kf:
+        f_mp = np.where(rng.random(n_f) < mp_frac, 20000 + np.arange(n_f), -1).astype(np.int32)
+        f_good = ((f_mp >= 0) & (rng.random(n_f) < 0.98)).astype(np.uint8)
+    else:
+        f_mp = np.full(n_f, -1, np.int32)
+        f_good = np.zeros(n_f, np.uint8)
+    Fb = BowSide(f_desc, f_ang, f_mp, f_good, *b)
+    return KF, Fb

@@ -1,0 +1,81 @@
+"""Host mirror of the reference operator API ``ORB_SLAM3::ORBmatcher`` (ref:include/ORBmatcher.h:34-99)
+on top of the C ABI.  Same names, argument meaning, defaults and in-place outputs; every search
+runs on the GPU (there is no CPU fallback).
+
+    m = ORBmatcher(ctx, nnratio=0.6, checkOri=True)
+    n = m.SearchByProjection(F, mps, th=3, slot_mp=slots, slot_taken=taken)     # (Frame&, vector<MapPoint*>)
+    n = m.SearchByProjection(CF, last, th, bMono, slot_mp=slots, slot_taken=t)  # (Frame&, const Frame&)
+    n = m.SearchByProjection(CF, kfq, th, ORBdist, slot_mp=slots)               # (Frame&, KeyFrame*, set)
+    n, vpMapPointMatches = m.SearchByBoW(KF, F)                                 # (KeyFrame*, Frame&)
+    n, vpMatches12 = m.SearchByBoW(KF1, KF2, kf2=True)                          # (KeyFrame*, KeyFrame*)
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import Context, _abi, descriptor_distance
+from .frames import BowSide, FrameSoA, KFQueries, LastQueries, MPQueries
+
+
+class ORBmatcher:
+    TH_HIGH = _abi.TH_HIGH
+    TH_LOW = _abi.TH_LOW
+    HISTO_LENGTH = _abi.HISTO_LENGTH
+
+    def __init__(self, ctx: Context, nnratio: float = 0.6, checkOri: bool = True):
+        self.ctx = ctx
+        self.mfNNratio = float(nnratio)
+        self.mbCheckOrientation = bool(checkOri)
+
+    @staticmethod
+    def DescriptorDistance(a, b) -> int:
+        return descriptor_distance(a, b)
+
+    def SearchByProjection(self, F: FrameSoA, q, *args, slot_mp=None, slot_taken=None, **kw) -> int:
+        lib, h = self.ctx.lib, self.ctx.handle
+        fs = F.struct()
+        if slot_mp is None:
+            slot_mp = np.full(F.n, -1, np.int32)
+        assert slot_mp.dtype == np.int32 and slot_mp.flags["C_CONTIGUOUS"] and len(slot_mp) == F.n
+        if isinstance(q, MPQueries):
+            th = args[0] if len(args) > 0 else kw.get("th", 3.0)
+            far = args[1] if len(args) > 1 else kw.get("bFarPoints", False)
+            thfar = args[2] if len(args) > 2 else kw.get("thFarPoints", 50.0)
+            taken = np.ascontiguousarray(slot_taken if slot_taken is not None else np.zeros(F.n), np.uint8)
+            qs = q.struct()
+            rc = lib.osg_search_by_projection_mps(h, C.byref(fs), C.byref(qs), self.mfNNratio, float(th),
+                                                  int(bool(far)), float(thfar), slot_mp.ctypes.data,
+                                                  taken.ctypes.data)
+            return self.ctx.check(rc, "SearchByProjection(Frame, vector<MapPoint*>)")
+        if isinstance(q, LastQueries):
+            th = args[0] if len(args) > 0 else kw["th"]
+            mono = args[1] if len(args) > 1 else kw["bMono"]
+            taken = np.ascontiguousarray(slot_taken if slot_taken is not None else np.zeros(F.n), np.uint8)
+            qs = q.struct()
+            rc = lib.osg_search_by_projection_last(h, C.byref(fs), C.byref(qs), float(th), int(bool(mono)),
+                                                   int(self.mbCheckOrientation), slot_mp.ctypes.data,
+                                                   taken.ctypes.data)
+            return self.ctx.check(rc, "SearchByProjection(Frame, Frame)")
+        if isinstance(q, KFQueries):
+            th = args[0] if len(args) > 0 else kw["th"]
+            orb = args[1] if len(args) > 1 else kw["ORBdist"]
+            qs = q.struct()
+            rc = lib.osg_search_by_projection_kf(h, C.byref(fs), C.byref(qs), float(th), int(orb),
+                                                 int(self.mbCheckOrientation), slot_mp.ctypes.data)
+            return self.ctx.check(rc, "SearchByProjection(Frame, KeyFrame, set)")
+        raise TypeError(f"no SearchByProjection overload for {type(q).__name__}")
+
+    def SearchByBoW(self, KF: BowSide, other: BowSide, kf2: bool = False):
+        lib, h = self.ctx.lib, self.ctx.handle
+        a, b = KF.struct(), other.struct()
+        if not kf2:
+            out = np.full(other.n, -1, np.int32)
+            rc = lib.osg_search_by_bow_kf_f(h, C.byref(a), C.byref(b), self.mfNNratio,
+                                            int(self.mbCheckOrientation), out.ctypes.data)
+            return self.ctx.check(rc, "SearchByBoW(KeyFrame, Frame)"), out
+        out = np.full(KF.n, -1, np.int32)
+        rc = lib.osg_search_by_bow_kf_kf(h, C.byref(a), C.byref(b), self.mfNNratio,
+                                         int(self.mbCheckOrientation), out.ctypes.data)
+        return self.ctx.check(rc, "SearchByBoW(KeyFrame, KeyFrame)"), out

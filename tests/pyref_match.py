@@ -1,0 +1,271 @@
+"""Second, independent restatement of the reference matchers in pure Python (float32 scalars for
+the reference's float arithmetic).  Slow — small inputs only.  Used to pin the C oracle
+(tests/test_oracle_match.py); never used by the product."""
+import math
+
+import numpy as np
+
+f32 = np.float32
+TH_HIGH, TH_LOW, HISTO = 100, 50, 30
+
+
+def dist(a, b):
+    return int(np.bitwise_count(np.bitwise_xor(a, b)).sum())
+
+
+def features_in_area(F, x, y, r, minL=-1, maxL=-1):
+    x, y, r = f32(x), f32(y), f32(r)
+    out = []
+    minCX = max(0, int(math.floor(f32(f32(x - f32(F.min_x)) - r) * F.inv_w)))
+    if minCX >= 64:
+        return out
+    maxCX = min(63, int(math.ceil(f32(f32(x - f32(F.min_x)) + r) * F.inv_w)))
+    if maxCX < 0:
+        return out
+    minCY = max(0, int(math.floor(f32(f32(y - f32(F.min_y)) - r) * F.inv_h)))
+    if minCY >= 48:
+        return out
+    maxCY = min(47, int(math.ceil(f32(f32(y - f32(F.min_y)) + r) * F.inv_h)))
+    if maxCY < 0:
+        return out
+    chk = (minL > 0) or (maxL >= 0)
+    for ix in range(minCX, maxCX + 1):
+        for iy in range(minCY, maxCY + 1):
+            c = ix * 48 + iy
+            for j in range(F.grid_start[c], F.grid_start[c + 1]):
+                idx = int(F.grid_idx[j])
+                o = int(F.kp_octave[idx])
+                if chk:
+                    if o < minL:
+                        continue
+                    if maxL >= 0 and o > maxL:
+                        continue
+                if abs(f32(F.kp_x[idx] - x)) < r and abs(f32(F.kp_y[idx] - y)) < r:
+                    out.append(idx)
+    return out
+
+
+def rot_bin(a, b):
+    rot = f32(f32(a) - f32(b))
+    if rot < 0.0:
+        rot = f32(rot + f32(360.0))
+    v = float(f32(rot * f32(f32(1.0) / f32(30))))
+    b_ = int(math.floor(v + 0.5))  # round half away from zero, v >= 0
+    return 0 if b_ == 30 else b_
+
+
+def three_maxima(sizes):
+    m1 = m2 = m3 = 0
+    i1 = i2 = i3 = -1
+    for i, s in enumerate(sizes):
+        if s > m1:
+            m3, m2, m1 = m2, m1, s
+            i3, i2, i1 = i2, i1, i
+        elif s > m2:
+            m3, m2 = m2, s
+            i3, i2 = i2, i
+        elif s > m3:
+            m3, i3 = s, i
+    if m2 < f32(0.1) * f32(m1):
+        i2 = i3 = -1
+    elif m3 < f32(0.1) * f32(m1):
+        i3 = -1
+    return i1, i2, i3
+
+
+def apply_hist(hist, slots, nm):
+    keep = three_maxima([len(h) for h in hist])
+    for i in range(HISTO):
+        if i in keep:
+            continue
+        for s in hist[i]:
+            slots[s] = -1
+            nm -= 1
+    return nm
+
+
+def search_mps(F, Q, nn, th, far, thfar, slot_mp, slot_taken):
+    slots = slot_mp.copy()
+    taken = slot_taken.copy()
+    nm = 0
+    nn = f32(nn)
+    for i in range(len(Q.mp_id)):
+        if not Q.in_view[i]:
+            continue
+        if far and Q.track_depth[i] > f32(thfar):
+            continue
+        if not Q.usable[i]:
+            continue
+        lvl = int(Q.pred_level[i])
+        r = f32(2.5) if float(Q.view_cos[i]) > 0.998 else f32(4.0)
+        if f32(th) != f32(1.0):
+            r = f32(r * f32(th))
+        R = f32(r * F.scale[lvl])
+        cands = features_in_area(F, Q.proj_x[i], Q.proj_y[i], R, lvl - 1, lvl)
+        if not cands:
+            continue
+        b, bl, b2, bl2, bi = 256, -1, 256, -1, -1
+        for idx in cands:
+            if slots[idx] >= 0 and taken[idx]:
+                continue
+            if F.u_right is not None and F.u_right[idx] > 0:
+                if abs(f32(Q.proj_xr[i] - F.u_right[idx])) > R:
+                    continue
+            d = dist(Q.desc[i], F.desc[idx])
+            if d < b:
+                b2, bl2, b, bl, bi = b, bl, d, int(F.kp_octave[idx]), idx
+            elif d < b2:
+                b2, bl2 = d, int(F.kp_octave[idx])
+        if b <= TH_HIGH:
+            if bl == bl2 and f32(b) > nn * f32(b2):
+                continue
+            slots[bi] = Q.mp_id[i]
+            taken[bi] = Q.has_obs[i]
+            nm += 1
+    return nm, slots
+
+
+def search_last(F, L, th, mono, ori, slot_mp, slot_taken):
+    slots = slot_mp.copy()
+    taken = slot_taken.copy()
+    hist = [[] for _ in range(HISTO)]
+    nm = 0
+    fwd = f32(L.tlc_z) > f32(F.mb) and not mono
+    bwd = -f32(L.tlc_z) > f32(F.mb) and not mono
+    for i in range(len(L.mp_id)):
+        if not L.valid[i]:
+            continue
+        invz = L.invz[i]
+        if invz < 0:
+            continue
+        u, v = L.u[i], L.v[i]
+        if u < f32(F.min_x) or u > f32(F.max_x) or v < f32(F.min_y) or v > f32(F.max_y):
+            continue
+        o = int(L.octave[i])
+        rad = f32(f32(th) * F.scale[o])
+        if fwd:
+            c = features_in_area(F, u, v, rad, o)
+        elif bwd:
+            c = features_in_area(F, u, v, rad, 0, o)
+        else:
+            c = features_in_area(F, u, v, rad, o - 1, o + 1)
+        if not c:
+            continue
+        b, bi = 256, -1
+        for i2 in c:
+            if slots[i2] >= 0 and taken[i2]:
+                continue
+            if F.u_right is not None and F.u_right[i2] > 0:
+                ur = f32(u - f32(f32(F.mbf) * invz))
+                if abs(f32(ur - F.u_right[i2])) > rad:
+                    continue
+            d = dist(L.desc[i], F.desc[i2])
+            if d < b:
+                b, bi = d, i2
+        if b <= TH_HIGH:
+            slots[bi] = L.mp_id[i]
+            taken[bi] = L.has_obs[i]
+            nm += 1
+            if ori:
+                hist[rot_bin(L.angle[i], F.kp_angle[bi])].append(bi)
+    if ori:
+        nm = apply_hist(hist, slots, nm)
+    return nm, slots
+
+
+def search_kf(F, K, th, orb, ori, slot_mp):
+    slots = slot_mp.copy()
+    hist = [[] for _ in range(HISTO)]
+    nm = 0
+    for i in range(len(K.mp_id)):
+        if not K.valid[i]:
+            continue
+        lvl = int(K.pred_level[i])
+        rad = f32(f32(th) * F.scale[lvl])
+        c = features_in_area(F, K.u[i], K.v[i], rad, lvl - 1, lvl + 1)
+        if not c:
+            continue
+        b, bi = 256, -1
+        for i2 in c:
+            if slots[i2] >= 0:
+                continue
+            d = dist(K.desc[i], F.desc[i2])
+            if d < b:
+                b, bi = d, i2
+        if b <= orb:
+            slots[bi] = K.mp_id[i]
+            nm += 1
+            if ori:
+                hist[rot_bin(K.angle[i], F.kp_angle[bi])].append(bi)
+    if ori:
+        nm = apply_hist(hist, slots, nm)
+    return nm, slots
+
+
+def _shared_nodes(A, B):
+    ma = {int(n): (A.node_start[k], A.node_start[k + 1]) for k, n in enumerate(A.node_id)}
+    mb = {int(n): (B.node_start[k], B.node_start[k + 1]) for k, n in enumerate(B.node_id)}
+    for n in sorted(set(ma) & set(mb)):
+        yield ma[n], mb[n]
+
+
+def search_bow_kf_f(KF, F, nn, ori):
+    out = np.full(F.n, -1, np.int32)
+    hist = [[] for _ in range(HISTO)]
+    nm = 0
+    nn = f32(nn)
+    for (a0, a1), (b0, b1) in _shared_nodes(KF, F):
+        for a in range(a0, a1):
+            ik = int(KF.feat[a])
+            if not KF.mp_good[ik]:
+                continue
+            b, bi, b2 = 256, -1, 256
+            for j in range(b0, b1):
+                jf = int(F.feat[j])
+                if out[jf] >= 0:
+                    continue
+                d = dist(KF.desc[ik], F.desc[jf])
+                if d < b:
+                    b2, b, bi = b, d, jf
+                elif d < b2:
+                    b2 = d
+            if b <= TH_LOW and f32(b) < nn * f32(b2):
+                out[bi] = KF.mp_id[ik]
+                nm += 1
+                if ori:
+                    hist[rot_bin(KF.angle[ik], F.angle[bi])].append(bi)
+    if ori:
+        nm = apply_hist(hist, out, nm)
+    return nm, out
+
+
+def search_bow_kf_kf(K1, K2, nn, ori):
+    out = np.full(K1.n, -1, np.int32)
+    matched2 = np.zeros(K2.n, bool)
+    hist = [[] for _ in range(HISTO)]
+    nm = 0
+    nn = f32(nn)
+    for (a0, a1), (b0, b1) in _shared_nodes(K1, K2):
+        for a in range(a0, a1):
+            i1 = int(K1.feat[a])
+            if not K1.mp_good[i1]:
+                continue
+            b, bi, b2 = 256, -1, 256
+            for j in range(b0, b1):
+                i2 = int(K2.feat[j])
+                if matched2[i2] or K2.mp_id[i2] < 0 or not K2.mp_good[i2]:
+                    continue
+                d = dist(K1.desc[i1], K2.desc[i2])
+                if d < b:
+                    b2, b, bi = b, d, i2
+                elif d < b2:
+                    b2 = d
+            if b < TH_LOW and f32(b) < nn * f32(b2):
+                out[i1] = K2.mp_id[bi]
+                matched2[bi] = True
+                nm += 1
+                if ori:
+                    hist[rot_bin(K1.angle[i1], K2.angle[bi])].append(i1)
+    if ori:
+        nm = apply_hist(hist, out, nm)
+    return nm, out

@@ -1,0 +1,126 @@
+"""CPU: pin the C oracle's matcher restatements against an independent pure-Python restatement
+(tests/pyref_match.py) on small seeded inputs, plus hand-derived known answers for the grid
+enumeration order, the rotation-bin quirk and ComputeThreeMaxima, and the committed golden
+fixtures."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from tests import oracle_calls as oc
+from tests import pyref_match as pr
+from orb_slam3_comments_ghr_amd import frames as fr
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def small_frame(rng, n=220, stereo=True):
+    return fr.synth_frame(rng, n=n, stereo=stereo)
+
+
+def test_rot_bin_quirk(oracle):
+    # factor = 1/30 applied to degrees (upstream bug kept): rot 45 deg -> bin round(1.5) = 2
+    cases = [(45.0, 0.0), (0.0, 45.0), (359.0, 0.0), (15.0, 0.0), (14.999, 0.0), (0.0, 0.0), (10.0, 370.0)]
+    for a, b in cases:
+        assert oracle.oracle_rot_bin(a, b) == pr.rot_bin(a, b)
+    assert oracle.oracle_rot_bin(45.0, 0.0) == 2
+    assert oracle.oracle_rot_bin(0.0, 45.0) == 11   # (360-45)/30 = 10.5 -> 11
+    assert max(oracle.oracle_rot_bin(float(a), 0.0) for a in np.linspace(0, 359.99, 2000)) == 12
+
+
+def test_three_maxima(oracle):
+    rng = np.random.default_rng(0)
+    for _ in range(300):
+        h = rng.integers(0, 12, 30).astype(np.int32)
+        if rng.random() < 0.3:
+            h[:] = 0
+            h[rng.integers(0, 30)] = 50
+        out = np.zeros(3, np.int32) - 1
+        oracle.oracle_compute_three_maxima(h.ctypes.data, 30, out[0:].ctypes.data, out[1:].ctypes.data,
+                                           out[2:].ctypes.data)
+        assert tuple(out) == pr.three_maxima(list(h))
+
+
+def test_features_in_area_order_and_filters(oracle):
+    rng = np.random.default_rng(3)
+    F = small_frame(rng, n=800)
+    fs = F.struct()
+    buf = np.zeros(F.n, np.int32)
+    for _ in range(300):
+        x, y = rng.uniform(-30, 780), rng.uniform(-30, 510)
+        r = rng.uniform(1, 80)
+        lo, hi = int(rng.integers(-1, 8)), int(rng.integers(-1, 8))
+        n = oracle.oracle_frame_features_in_area(C.byref(fs), x, y, r, lo, hi, 0, buf.ctypes.data)
+        assert list(buf[:n]) == pr.features_in_area(F, x, y, r, lo, hi)
+
+
+def test_features_in_area_hand_case(oracle):
+    # enumeration follows cells (ix outer, iy inner), insertion order inside a cell — not the
+    # feature index: kp2 rounds into column 8 (99.7*64/752 = 8.485), kp0/kp1 into column 9
+    x = np.array([100.0, 100.5, 99.7, 112.0], np.float32)
+    y = np.array([100.0, 100.2, 99.9, 80.0], np.float32)
+    F = fr.FrameSoA(desc=np.zeros((4, 32), np.uint8), kp_x=x, kp_y=y, kp_angle=np.zeros(4),
+                    kp_octave=np.zeros(4, np.int32))
+    fs = F.struct()
+    buf = np.zeros(4, np.int32)
+    n = oracle.oracle_frame_features_in_area(C.byref(fs), 101.0, 95.0, 20.0, -1, -1, 0, buf.ctypes.data)
+    assert list(buf[:n]) == [2, 0, 1, 3] == pr.features_in_area(F, 101.0, 95.0, 20.0)
+    # strict '<': a point exactly r away is out
+    n = oracle.oracle_frame_features_in_area(C.byref(fs), 100.0, 90.0, 10.0, -1, -1, 0, buf.ctypes.data)
+    assert 0 not in list(buf[:n])
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_oracle_mps_vs_python(oracle, seed):
+    rng = np.random.default_rng(100 + seed)
+    F = small_frame(rng, stereo=seed % 2 == 0)
+    Q = fr.synth_mp_queries(rng, F, m=300)
+    slot_mp, taken = fr.synth_slots(rng, F.n)
+    for th, nn, far in [(1.0, 0.8, False), (5.0, 0.6, True)]:
+        got = oc.mps(oracle, F, Q, nn, th, far, 20.0, slot_mp, taken)
+        ref = pr.search_mps(F, Q, nn, th, far, 20.0, slot_mp, taken)
+        assert got[0] == ref[0]
+        np.testing.assert_array_equal(got[1], ref[1])
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_oracle_last_vs_python(oracle, seed):
+    rng = np.random.default_rng(200 + seed)
+    F = small_frame(rng, stereo=seed % 2 == 0)
+    L = fr.synth_last_queries(rng, F, n_last=250, tlc_z=[0.0, 1.0, -1.0, 0.0][seed])
+    slot_mp, taken = fr.synth_slots(rng, F.n)
+    for th, mono, ori in [(7.0, False, True), (15.0, True, False), (7.0, False, False)]:
+        got = oc.last(oracle, F, L, th, mono, ori, slot_mp, taken)
+        ref = pr.search_last(F, L, th, mono, ori, slot_mp, taken)
+        assert got[0] == ref[0]
+        np.testing.assert_array_equal(got[1], ref[1])
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_oracle_kf_vs_python(oracle, seed):
+    rng = np.random.default_rng(300 + seed)
+    F = small_frame(rng)
+    K = fr.synth_kf_queries(rng, F, n_kf=250)
+    slot_mp, _ = fr.synth_slots(rng, F.n, frac_assigned=0.2)
+    for th, orb, ori in [(10.0, 100, True), (3.0, 64, False)]:
+        got = oc.kf(oracle, F, K, th, orb, ori, slot_mp)
+        ref = pr.search_kf(F, K, th, orb, ori, slot_mp)
+        assert got[0] == ref[0]
+        np.testing.assert_array_equal(got[1], ref[1])
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_oracle_bow_vs_python(oracle, seed):
+    rng = np.random.default_rng(400 + seed)
+    KF, F = fr.synth_bow_pair(rng, n_kf=300, n_f=300, n_nodes=30)
+    K1, K2 = fr.synth_bow_pair(rng, n_kf=300, n_f=320, n_nodes=30, f_is_kf=True)
+    for nn, ori in [(0.7, True), (0.9, False)]:
+        got = oc.bow_kf_f(oracle, KF, F, nn, ori)
+        ref = pr.search_bow_kf_f(KF, F, nn, ori)
+        assert got[0] == ref[0]
+        np.testing.assert_array_equal(got[1], ref[1])
+        got = oc.bow_kf_kf(oracle, K1, K2, nn, ori)
+        ref = pr.search_bow_kf_kf(K1, K2, nn, ori)
+        assert got[0] == ref[0]
+        np.testing.assert_array_equal(got[1], ref[1])
