@@ -1,6 +1,861 @@
-// ba.hip — placeholder (filled in next)
-#include "osg_internal.h"
+// ba.hip — the g2o inner loop of Optimizer::LocalBundleAdjustment on gfx950.
+//
+// Reference: ref:src/Optimizer.cc:1877-2203 (graph → optimize(10) → classification), running
+// g2o's LM (ref:Thirdparty/g2o/g2o/core/optimization_algorithm_levenberg.cpp:61-194) over a
+// BlockSolver<6,3> with the points marginalised (ref:Thirdparty/g2o/g2o/core/block_solver.hpp:143-604).
+//
+// Structure (built once per call, host, like BlockSolver::buildStructure):
+//   Hessian order: free poses with >= 1 edge, then points (vertex-id order); one Hpl block per
+//   (free pose, point) pair; CSR of edges per point and per pose; for every pose pair (i <= j)
+//   the list of (block_i, block_j) contributions in landmark order (the Schur outer loop order).
+//
+// Per LM iteration (device):
+//   k_errors      per edge: error, Huber rho -> per-workgroup chi2 partials        (HBM/latency)
+//   k_jacobians   per edge: J_pose (3x6), J_point (3x3), weights                 (FP64 VALU)
+//   k_point_red   per point: Hll, b_l and its Hpl blocks from its edges            (segmented, no atomics)
+//   k_pose_red    per pose: Hpp, b_p from its edges (workgroup reduction)
+// Per LM trial (lambda known on the host):
+//   k_schur_point per point: Dinv = (Hll + lambda I)^-1, BDinv = Hpl Dinv, coef = Hpl Dinv b_l
+//   k_schur_pairs per pose pair (i <= j), one wave: S_ij = sum_p BDinv_ip Hpl_jp^T ; writes the
+//                 dense reduced camera matrix Hpp + lambda I - S and b_schur
+//   k_chol        one workgroup: blocked Cholesky of the reduced system (n = 6 x free poses)
+//                 and the two triangular solves
+//   k_update      per point: x_l = Dinv (b_l - Hpl^T x_p), new estimates (poses: exp(x) * T)
+//                 and the LM scale sum;  then k_errors on the new estimates -> tempChi
+// The host reads back 3 scalars per trial and runs the accept / reject / lambda logic exactly as
+// the reference; push/pop is a swap of the current / trial estimate buffers.
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <vector>
+
 #include "ba_common.h"
-extern "C" {
-int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *, osg_ba_result *, const volatile int *) { return osg_set_error(ctx, OSG_E_UNSUPPORTED, "not built"); }
+#include "match_common.h"
+
+using namespace osgba;
+
+namespace {
+
+constexpr int EB = 256;      // edge-parallel kernels
+constexpr int NPART = 1024;  // max chi2 / scale partials
+
+struct LbaDev {
+    // sizes
+    int np, npt, ne, nhp, nhl, nblk, npairs, n_cams;
+    // inputs
+    const uint8_t *pose_fixed;
+    const int32_t *e_pose, *e_point, *e_cam;
+    const int8_t *e_kind;
+    const double *e_obs;
+    const float *e_isig2;
+    const osg_camera *cams;
+    // structure
+    const int32_t *pose_h;        // per pose: hessian index or -1
+    const int32_t *hp_pose;       // per hessian pose: pose index
+    const int32_t *point_h;       // per point: landmark index or -1
+    const int32_t *hl_point;      // per landmark: point index
+    const int32_t *lm_e_start, *lm_e;    // edges per landmark
+    const int32_t *lm_b_start;           // blocks per landmark (blocks are numbered landmark-major)
+    const int32_t *blk_pose;             // per block: hessian pose index
+    const int32_t *edge_blk;             // per edge: block or -1
+    const int32_t *hp_e_start, *hp_e;    // edges per hessian pose
+    const int32_t *hp_b_start, *hp_b;    // blocks per hessian pose
+    const int32_t *pair_start;           // dense (i <= j) pairs
+    const int32_t *pair_ab;              // 2 ints per contribution
+    // state
+    const double *pose_cur, *point_cur;
+    double *pose_new, *point_new;
+    double *err;                         // 3 per edge
+    double *J;                           // 32 per edge
+    double *Hll, *bl, *Hpl, *Hpp, *bp;
+    double *Dinv, *BDinv, *coef;
+    double *Hs, *bs, *x;
+    double *part;                        // [0..NPART): chi partials, [NPART..2NPART): scale, [2NPART..]: max diag
+    int *flag;                           // [0] cholesky ok
+};
+
+__device__ inline double edge_w(const LbaDev &D, int e) { return (double)D.e_isig2[e]; }
+
+__device__ inline void kind_delta(int kind, double &delta, float &dsqr)
+{
+    const float dm = (float)sqrt(5.991), ds = (float)sqrt(7.815);
+    const float d = (kind == OSG_EDGE_STEREO) ? ds : dm;
+    delta = (double)d;
+    dsqr = (float)((double)d * (double)d);
+}
+
+__device__ inline double block_sum_d(double v, double *s)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    v = wave_sum(v);
+    if (lane == 0) s[w] = v;
+    __syncthreads();
+    double t = 0;
+    for (int i = 0; i < nw; i++) t += s[i];
+    __syncthreads();
+    return t;
+}
+
+// per edge error + robust chi2 -> partial sums per workgroup (deterministic order)
+__global__ __launch_bounds__(EB) void k_errors(LbaDev D, const double *__restrict__ poses,
+                                               const double *__restrict__ points, int part_off)
+{
+    __shared__ double s[EB / 64];
+    const int e = blockIdx.x * EB + threadIdx.x;
+    double rho0 = 0.0;
+    if (e < D.ne) {
+        const int k = D.e_kind[e];
+        const SE3 T = se3_from7(poses + 7 * (size_t)D.e_pose[e]);
+        const double *X = points + 3 * (size_t)D.e_point[e];
+        double ev[3];
+        edge_error(k, true, D.cams[D.e_cam[e]], T, X, D.e_obs + 3 * (size_t)e, ev);
+        D.err[3 * e] = ev[0];
+        D.err[3 * e + 1] = ev[1];
+        D.err[3 * e + 2] = ev[2];
+        const int dim = (k == OSG_EDGE_STEREO) ? 3 : 2;
+        const double c = chi2_of(ev, dim, edge_w(D, e));
+        double delta, r1;
+        float dsqr;
+        kind_delta(k, delta, dsqr);
+        huber(c, delta, dsqr, rho0, r1);
+    }
+    const double t = block_sum_d(rho0, s);
+    if (threadIdx.x == 0) D.part[part_off + blockIdx.x] = t;
+}
+
+// per edge Jacobians and weights: J[e] = {Jp[3][6], Jx[3][3], ww, omega_r[3], rho1}
+__global__ __launch_bounds__(EB) void k_jacobians(LbaDev D)
+{
+    const int e = blockIdx.x * EB + threadIdx.x;
+    if (e >= D.ne) return;
+    const int k = D.e_kind[e];
+    const SE3 T = se3_from7(D.pose_cur + 7 * (size_t)D.e_pose[e]);
+    const double *X = D.point_cur + 3 * (size_t)D.e_point[e];
+    double Jp[3][6], Jx[3][3];
+    edge_jacobians(k, true, D.cams[D.e_cam[e]], T, X, Jp, Jx);
+    const int dim = (k == OSG_EDGE_STEREO) ? 3 : 2;
+    const double w = edge_w(D, e);
+    const double ev[3] = {D.err[3 * e], D.err[3 * e + 1], D.err[3 * e + 2]};
+    double delta, r0, rho1;
+    float dsqr;
+    kind_delta(k, delta, dsqr);
+    huber(chi2_of(ev, dim, w), delta, dsqr, r0, rho1);
+    double *o = D.J + 32 * (size_t)e;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 6; j++) o[i * 6 + j] = (i < dim) ? Jp[i][j] : 0.0;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) o[18 + i * 3 + j] = (i < dim) ? Jx[i][j] : 0.0;
+    o[27] = rho1 * w;
+    for (int i = 0; i < 3; i++) o[28 + i] = (i < dim) ? -(w * ev[i]) * rho1 : 0.0;
+    o[31] = (double)dim;
+}
+
+// per landmark: Hll (3x3), b_l and the Hpl blocks (6x3) of its (free pose) edges
+__global__ __launch_bounds__(EB) void k_point_red(LbaDev D)
+{
+    __shared__ double s[EB / 64];
+    const int l = blockIdx.x * EB + threadIdx.x;
+    double md = 0.0;
+    if (l < D.nhl) {
+        double H[9] = {0}, b[3] = {0};
+        const int b0 = D.lm_b_start[l], b1 = D.lm_b_start[l + 1];
+        for (int blk = b0; blk < b1; blk++)
+            for (int i = 0; i < 18; i++) D.Hpl[18 * (size_t)blk + i] = 0.0;
+        for (int q = D.lm_e_start[l]; q < D.lm_e_start[l + 1]; q++) {
+            const int e = D.lm_e[q];
+            const double *J = D.J + 32 * (size_t)e;
+            const double *Jp = J, *Jx = J + 18;
+            const double ww = J[27];
+            const double *om = J + 28;
+            for (int i = 0; i < 3; i++) {
+                double sb = 0;
+                for (int d = 0; d < 3; d++) sb += Jx[d * 3 + i] * om[d];
+                b[i] += sb;
+                for (int j = 0; j < 3; j++) {
+                    double h = 0;
+                    for (int d = 0; d < 3; d++) h += Jx[d * 3 + i] * ww * Jx[d * 3 + j];
+                    H[i * 3 + j] += h;
+                }
+            }
+            const int blk = D.edge_blk[e];
+            if (blk >= 0) {
+                double *Hb = D.Hpl + 18 * (size_t)blk;
+                for (int i = 0; i < 6; i++)
+                    for (int j = 0; j < 3; j++) {
+                        double h = 0;
+                        for (int d = 0; d < 3; d++) h += Jp[d * 6 + i] * ww * Jx[d * 3 + j];
+                        Hb[i * 3 + j] += h;
+                    }
+            }
+        }
+        for (int i = 0; i < 9; i++) D.Hll[9 * (size_t)l + i] = H[i];
+        for (int i = 0; i < 3; i++) D.bl[3 * (size_t)l + i] = b[i];
+        md = fmax(fabs(H[0]), fmax(fabs(H[4]), fabs(H[8])));
+    }
+    // max |diag| per workgroup for computeLambdaInit
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int off = 32; off >= 1; off >>= 1) md = fmax(md, __shfl_xor(md, off));
+    if (lane == 0) s[w] = md;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double m = 0;
+        for (int i = 0; i < EB / 64; i++) m = fmax(m, s[i]);
+        D.part[2 * NPART + blockIdx.x] = m;
+    }
+}
+
+// per free pose (one workgroup): Hpp (6x6) and b_p from its edges
+__global__ __launch_bounds__(EB) void k_pose_red(LbaDev D, int diag_off)
+{
+    __shared__ double s[EB / 64][27];
+    const int i = blockIdx.x;
+    double acc[27];
+    for (int k = 0; k < 27; k++) acc[k] = 0.0;
+    for (int q = D.hp_e_start[i] + threadIdx.x; q < D.hp_e_start[i + 1]; q += EB) {
+        const int e = D.hp_e[q];
+        const double *J = D.J + 32 * (size_t)e;
+        const double ww = J[27];
+        const double *om = J + 28;
+        int c = 0;
+        for (int a = 0; a < 6; a++)
+            for (int b = a; b < 6; b++) {
+                double h = 0;
+                for (int d = 0; d < 3; d++) h += J[d * 6 + a] * ww * J[d * 6 + b];
+                acc[c++] += h;
+            }
+        for (int a = 0; a < 6; a++) {
+            double sb = 0;
+            for (int d = 0; d < 3; d++) sb += J[d * 6 + a] * om[d];
+            acc[21 + a] += sb;
+        }
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int k = 0; k < 27; k++) acc[k] = wave_sum(acc[k]);
+    if (lane == 0)
+        for (int k = 0; k < 27; k++) s[w][k] = acc[k];
+    __syncthreads();
+    if (threadIdx.x < 27) {
+        double t = 0;
+        for (int ww = 0; ww < EB / 64; ww++) t += s[ww][threadIdx.x];
+        s[0][threadIdx.x] = t;  // only wave 0's slot is reused after all reads below
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double H[36];
+        int c = 0;
+        double md = 0;
+        for (int a = 0; a < 6; a++)
+            for (int b = a; b < 6; b++) {
+                H[a * 6 + b] = s[0][c];
+                H[b * 6 + a] = s[0][c];
+                c++;
+            }
+        for (int k = 0; k < 36; k++) D.Hpp[36 * (size_t)i + k] = H[k];
+        for (int a = 0; a < 6; a++) {
+            D.bp[6 * (size_t)i + a] = s[0][21 + a];
+            md = fmax(md, fabs(H[a * 7]));
+        }
+        D.part[diag_off + i] = md;
+    }
+}
+
+__device__ inline void inv3(const double *m, double *o)
+{  // Eigen compute_inverse<Matrix3>: cofactors, determinant along column 0
+#define M_(i, j) m[(i)*3 + (j)]
+#define COF(i, j) (M_(((i) + 1) % 3, ((j) + 1) % 3) * M_(((i) + 2) % 3, ((j) + 2) % 3) - M_(((i) + 1) % 3, ((j) + 2) % 3) * M_(((i) + 2) % 3, ((j) + 1) % 3))
+    const double c00 = COF(0, 0), c10 = COF(1, 0), c20 = COF(2, 0);
+    const double det = c00 * M_(0, 0) + c10 * M_(1, 0) + c20 * M_(2, 0);
+    const double invdet = 1.0 / det;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) o[i * 3 + j] = COF(j, i) * invdet;
+#undef COF
+#undef M_
+}
+
+__global__ __launch_bounds__(EB) void k_schur_point(LbaDev D, double lambda)
+{
+    const int l = blockIdx.x * EB + threadIdx.x;
+    if (l >= D.nhl) return;
+    double Dm[9];
+    for (int i = 0; i < 9; i++) Dm[i] = D.Hll[9 * (size_t)l + i];
+    Dm[0] += lambda;
+    Dm[4] += lambda;
+    Dm[8] += lambda;
+    double Di[9];
+    inv3(Dm, Di);
+    for (int i = 0; i < 9; i++) D.Dinv[9 * (size_t)l + i] = Di[i];
+    const double *b = D.bl + 3 * (size_t)l;
+    double db[3];
+    for (int r = 0; r < 3; r++) db[r] = Di[3 * r] * b[0] + Di[3 * r + 1] * b[1] + Di[3 * r + 2] * b[2];
+    for (int blk = D.lm_b_start[l]; blk < D.lm_b_start[l + 1]; blk++) {
+        const double *B = D.Hpl + 18 * (size_t)blk;
+        double *BD = D.BDinv + 18 * (size_t)blk;
+        double *cf = D.coef + 6 * (size_t)blk;
+        for (int r = 0; r < 6; r++) {
+            for (int c = 0; c < 3; c++) BD[3 * r + c] = B[3 * r] * Di[c] + B[3 * r + 1] * Di[3 + c] + B[3 * r + 2] * Di[6 + c];
+            cf[r] = B[3 * r] * db[0] + B[3 * r + 1] * db[1] + B[3 * r + 2] * db[2];
+        }
+    }
+}
+
+// one wave per pose pair (i <= j): S = sum BDinv_a Hpl_b^T ; writes the dense reduced system
+__global__ __launch_bounds__(256) void k_schur_pairs(LbaDev D, double lambda)
+{
+    const int wave = (blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (wave >= D.npairs) return;
+    // decode dense pair index -> (i, j), i <= j
+    int i = 0, rem = wave;
+    while (rem >= D.nhp - i) {
+        rem -= D.nhp - i;
+        i++;
+    }
+    const int j = i + rem;
+    double S[36];
+    for (int k = 0; k < 36; k++) S[k] = 0.0;
+    for (int q = D.pair_start[wave] + lane; q < D.pair_start[wave + 1]; q += 64) {
+        const int a = D.pair_ab[2 * q], b = D.pair_ab[2 * q + 1];
+        const double *BD = D.BDinv + 18 * (size_t)a;
+        const double *Bj = D.Hpl + 18 * (size_t)b;
+        for (int r = 0; r < 6; r++)
+            for (int c = 0; c < 6; c++)
+                S[r * 6 + c] += BD[3 * r] * Bj[3 * c] + BD[3 * r + 1] * Bj[3 * c + 1] + BD[3 * r + 2] * Bj[3 * c + 2];
+    }
+    for (int k = 0; k < 36; k++) S[k] = wave_sum(S[k]);
+    const int n = 6 * D.nhp;
+    if (lane < 36) {
+        const int r = lane / 6, c = lane % 6;
+        double v = -S[lane];
+        if (i == j) {
+            v += D.Hpp[36 * (size_t)i + lane];
+            if (r == c) v += lambda;
+        }
+        D.Hs[(size_t)(6 * i + r) * n + 6 * j + c] = v;
+        if (i != j) D.Hs[(size_t)(6 * j + c) * n + 6 * i + r] = v;
+    }
+    if (i == j && lane < 6) {
+        double cs = 0.0;
+        for (int q = D.hp_b_start[i]; q < D.hp_b_start[i + 1]; q++) cs += D.coef[6 * (size_t)D.hp_b[q] + lane];
+        D.bs[6 * i + lane] = D.bp[6 * (size_t)i + lane] - cs;
+    }
+}
+
+// Dense Cholesky (LL^T, lower, in place) + forward/back substitution, one 1024-thread workgroup.
+// Right-looking, panel width CB: the panel is factored wave-synchronously from LDS, the trailing
+// lower triangle is updated with the panel held in LDS.
+constexpr int CB = 32;
+constexpr int CT = 1024;
+constexpr int CMAX = 384;  // max reduced dimension (64 free poses)
+
+__global__ __launch_bounds__(CT) void k_chol(LbaDev D)
+{
+    __shared__ double s_panel[CMAX * CB];  // rows k0.. n of the current panel (n - k0) x CB
+    __shared__ int s_ok;
+    const int n = 6 * D.nhp;
+    double *A = D.Hs;
+    const int tid = threadIdx.x;
+    if (tid == 0) s_ok = 1;
+    __syncthreads();
+    for (int k0 = 0; k0 < n; k0 += CB) {
+        const int nb = min(CB, n - k0);
+        const int m = n - k0;  // rows in the panel (incl. the diagonal block)
+        // load panel columns k0..k0+nb of rows k0..n into LDS
+        for (int idx = tid; idx < m * nb; idx += CT) {
+            const int r = idx / nb, c = idx % nb;
+            s_panel[r * CB + c] = A[(size_t)(k0 + r) * n + k0 + c];
+        }
+        __syncthreads();
+        // unblocked right-looking factorisation of the panel (columns k0..k0+nb)
+        for (int c = 0; c < nb; c++) {
+            if (tid == 0) {
+                const double d = s_panel[c * CB + c];
+                if (!(d > 0.0)) s_ok = 0;
+                s_panel[c * CB + c] = sqrt(fmax(d, 1e-300));
+            }
+            __syncthreads();
+            const double piv = s_panel[c * CB + c];
+            for (int r = c + 1 + tid; r < m; r += CT) s_panel[r * CB + c] /= piv;
+            __syncthreads();
+            // update the remaining panel columns c+1..nb for rows > c
+            const int w = nb - c - 1;
+            for (int idx = tid; idx < (m - c - 1) * w; idx += CT) {
+                const int r = c + 1 + idx / w, cc = c + 1 + idx % w;
+                if (r >= cc) s_panel[r * CB + cc] -= s_panel[r * CB + c] * s_panel[cc * CB + c];
+            }
+            __syncthreads();
+        }
+        // write the factored panel back (lower part)
+        for (int idx = tid; idx < m * nb; idx += CT) {
+            const int r = idx / nb, c = idx % nb;
+            if (r >= c) A[(size_t)(k0 + r) * n + k0 + c] = s_panel[r * CB + c];
+        }
+        // trailing update: A[r][cc] -= sum_k L[r][k] L[cc][k], k0+nb <= cc <= r < n
+        const int t0 = nb;  // first trailing row inside the panel indexing
+        const int mt = m - t0;
+        const long long tri = (long long)mt * (mt + 1) / 2;
+        for (long long idx = tid; idx < tri; idx += CT) {
+            // map idx -> (r, cc) in the lower triangle, row-major
+            int r = (int)((sqrt(8.0 * (double)idx + 1.0) - 1.0) * 0.5);
+            while ((long long)(r + 1) * (r + 2) / 2 <= idx) r++;
+            while ((long long)r * (r + 1) / 2 > idx) r--;
+            const int cc = (int)(idx - (long long)r * (r + 1) / 2);
+            const double *Lr = s_panel + (t0 + r) * CB;
+            const double *Lc = s_panel + (t0 + cc) * CB;
+            double sum = 0.0;
+            for (int k = 0; k < nb; k++) sum += Lr[k] * Lc[k];
+            A[(size_t)(k0 + t0 + r) * n + k0 + t0 + cc] -= sum;
+        }
+        __syncthreads();
+    }
+    // forward substitution L y = b, back substitution L^T x = y (column-oriented, one column per step)
+    double *y = D.x;  // reuse x[0..n) for y then x
+    for (int i = tid; i < n; i += CT) y[i] = D.bs[i];
+    __syncthreads();
+    for (int c = 0; c < n; c++) {
+        if (tid == 0) y[c] /= A[(size_t)c * n + c];
+        __syncthreads();
+        const double yc = y[c];
+        for (int r = c + 1 + tid; r < n; r += CT) y[r] -= A[(size_t)r * n + c] * yc;
+        __syncthreads();
+    }
+    for (int c = n - 1; c >= 0; c--) {
+        if (tid == 0) y[c] /= A[(size_t)c * n + c];
+        __syncthreads();
+        const double yc = y[c];
+        for (int r = tid; r < c; r += CT) y[r] -= A[(size_t)c * n + r] * yc;
+        __syncthreads();
+    }
+    if (tid == 0) D.flag[0] = s_ok;
+}
+
+// landmark back-substitution + new estimates + LM scale partials
+__global__ __launch_bounds__(EB) void k_update(LbaDev D, double lambda)
+{
+    __shared__ double s[EB / 64];
+    const int t = blockIdx.x * EB + threadIdx.x;
+    const int sp = 6 * D.nhp;
+    double sc = 0.0;
+    if (t < D.nhl) {
+        const int l = t;
+        double cl[3] = {D.bl[3 * (size_t)l], D.bl[3 * (size_t)l + 1], D.bl[3 * (size_t)l + 2]};
+        for (int blk = D.lm_b_start[l]; blk < D.lm_b_start[l + 1]; blk++) {
+            const int i1 = D.blk_pose[blk];
+            const double *B = D.Hpl + 18 * (size_t)blk;
+            for (int c = 0; c < 3; c++) {
+                double s_ = 0;
+                for (int r = 0; r < 6; r++) s_ += B[3 * r + c] * (-D.x[6 * i1 + r]);
+                cl[c] += s_;
+            }
+        }
+        const double *Di = D.Dinv + 9 * (size_t)l;
+        const int p = D.hl_point[l];
+        for (int r = 0; r < 3; r++) {
+            const double xl = Di[3 * r] * cl[0] + Di[3 * r + 1] * cl[1] + Di[3 * r + 2] * cl[2];
+            D.x[sp + 3 * l + r] = xl;
+            D.point_new[3 * (size_t)p + r] = D.point_cur[3 * (size_t)p + r] + xl;
+            sc += xl * (lambda * xl + D.bl[3 * (size_t)l + r]);
+        }
+    }
+    if (t < D.np) {  // poses: exp(x) * T for free active poses, copy otherwise
+        const int hi = D.pose_h[t];
+        if (hi >= 0) {
+            SE3 T = se3_from7(D.pose_cur + 7 * (size_t)t);
+            double upd[6];
+            for (int k = 0; k < 6; k++) {
+                upd[k] = D.x[6 * hi + k];
+                sc += upd[k] * (lambda * upd[k] + D.bp[6 * (size_t)hi + k]);
+            }
+            se3_oplus(T, upd);
+            se3_to7(T, D.pose_new + 7 * (size_t)t);
+        } else {
+            for (int k = 0; k < 7; k++) D.pose_new[7 * (size_t)t + k] = D.pose_cur[7 * (size_t)t + k];
+        }
+    }
+    // points without a landmark index (no edges) keep their estimate
+    if (t < D.npt && D.point_h[t] < 0)
+        for (int k = 0; k < 3; k++) D.point_new[3 * (size_t)t + k] = D.point_cur[3 * (size_t)t + k];
+    const double tot = block_sum_d(sc, s);
+    if (threadIdx.x == 0) D.part[NPART + blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(EB) void k_classify(LbaDev D, const double *__restrict__ poses,
+                                                 const double *__restrict__ points, uint8_t *__restrict__ bad)
+{
+    const int e = blockIdx.x * EB + threadIdx.x;
+    if (e >= D.ne) return;
+    const int k = D.e_kind[e];
+    const int dim = (k == OSG_EDGE_STEREO) ? 3 : 2;
+    const double ev[3] = {D.err[3 * e], D.err[3 * e + 1], D.err[3 * e + 2]};
+    const double th = (k == OSG_EDGE_STEREO) ? 7.815 : 5.991;
+    const SE3 T = se3_from7(poses + 7 * (size_t)D.e_pose[e]);
+    const bool pos = edge_depth_positive(k, D.cams[D.e_cam[e]], T, points + 3 * (size_t)D.e_point[e]);
+    bad[e] = (chi2_of(ev, dim, edge_w(D, e)) > th || !pos) ? 1 : 0;
+}
+
+template <typename T>
+T *carve(char *base, size_t &off, size_t count)
+{
+    off = (off + 255) & ~size_t(255);
+    T *p = (T *)(base + off);
+    off += sizeof(T) * std::max<size_t>(count, 1);
+    return p;
+}
+
+}  // namespace
+
+extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, osg_ba_result *R,
+                                           const volatile int *stop)
+{
+    if (!ctx) return OSG_E_INVALID;
+    OSG_REQUIRE(ctx, G && R, "null argument");
+    const int np = G->n_poses, npt = G->n_points, ne = G->n_edges;
+    OSG_REQUIRE(ctx, np >= 0 && npt >= 0 && ne >= 0 && G->n_cams >= 0, "sizes");
+    OSG_REQUIRE(ctx, R->pose && R->point && (ne == 0 || R->edge_bad), "result buffers");
+    R->iterations = 0;
+    R->trials = 0;
+    R->aborted = 0;
+    R->chi2_initial = R->chi2_final = 0.0;
+    std::memcpy(R->pose, G->pose, sizeof(double) * 7 * np);
+    std::memcpy(R->point, G->point, sizeof(double) * 3 * npt);
+    if (ne > 0) std::memset(R->edge_bad, 0, ne);
+    if (stop && *stop) {  // ref:src/Optimizer.cc:2112-2114
+        R->aborted = 1;
+        return 0;
+    }
+    if (ne == 0) return 0;
+    for (int e = 0; e < ne; e++) {
+        if (G->e_pose[e] < 0 || G->e_pose[e] >= np || G->e_point[e] < 0 || G->e_point[e] >= npt ||
+            G->e_cam[e] < 0 || G->e_cam[e] >= G->n_cams)
+            return osg_set_error(ctx, OSG_E_INVALID, "edge %d references out of range", e);
+    }
+    // ---------------------------------------------------------------- structure (host)
+    std::vector<int32_t> pose_cnt(np, 0), point_cnt(npt, 0);
+    for (int e = 0; e < ne; e++) {
+        pose_cnt[G->e_pose[e]]++;
+        point_cnt[G->e_point[e]]++;
+    }
+    std::vector<int32_t> pose_h(np, -1), hp_pose, point_h(npt, -1), hl_point;
+    for (int i = 0; i < np; i++)
+        if (!G->pose_fixed[i] && pose_cnt[i] > 0) {
+            pose_h[i] = (int)hp_pose.size();
+            hp_pose.push_back(i);
+        }
+    for (int i = 0; i < npt; i++)
+        if (point_cnt[i] > 0) {
+            point_h[i] = (int)hl_point.size();
+            hl_point.push_back(i);
+        }
+    const int nhp = (int)hp_pose.size(), nhl = (int)hl_point.size();
+    if (nhp + nhl == 0) return 0;
+    OSG_REQUIRE(ctx, 6 * nhp <= CMAX, "%d free poses exceed the dense reduced-system limit (%d)", nhp, CMAX / 6);
+    // edges per landmark (stable in edge order)
+    std::vector<int32_t> lm_e_start(nhl + 1, 0), lm_e(ne);
+    for (int e = 0; e < ne; e++) lm_e_start[point_h[G->e_point[e]] + 1]++;
+    for (int l = 0; l < nhl; l++) lm_e_start[l + 1] += lm_e_start[l];
+    {
+        std::vector<int32_t> fill(lm_e_start.begin(), lm_e_start.end() - 1);
+        for (int e = 0; e < ne; e++) lm_e[fill[point_h[G->e_point[e]]]++] = e;
+    }
+    // blocks per landmark: unique free poses sorted by hessian index
+    std::vector<int32_t> lm_b_start(nhl + 1, 0), blk_pose, edge_blk(ne, -1);
+    blk_pose.reserve(ne);
+    std::vector<int32_t> tmp;
+    for (int l = 0; l < nhl; l++) {
+        tmp.clear();
+        for (int q = lm_e_start[l]; q < lm_e_start[l + 1]; q++) {
+            const int ph = pose_h[G->e_pose[lm_e[q]]];
+            if (ph >= 0) tmp.push_back(ph);
+        }
+        std::sort(tmp.begin(), tmp.end());
+        tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
+        const int base = (int)blk_pose.size();
+        for (int ph : tmp) blk_pose.push_back(ph);
+        lm_b_start[l + 1] = (int)blk_pose.size();
+        for (int q = lm_e_start[l]; q < lm_e_start[l + 1]; q++) {
+            const int e = lm_e[q];
+            const int ph = pose_h[G->e_pose[e]];
+            if (ph < 0) continue;
+            for (int k = 0; k < (int)tmp.size(); k++)
+                if (tmp[k] == ph) {
+                    edge_blk[e] = base + k;
+                    break;
+                }
+        }
+    }
+    const int nblk = (int)blk_pose.size();
+    // edges / blocks per hessian pose
+    std::vector<int32_t> hp_e_start(nhp + 1, 0), hp_e, hp_b_start(nhp + 1, 0), hp_b(nblk);
+    for (int e = 0; e < ne; e++)
+        if (pose_h[G->e_pose[e]] >= 0) hp_e_start[pose_h[G->e_pose[e]] + 1]++;
+    for (int i = 0; i < nhp; i++) hp_e_start[i + 1] += hp_e_start[i];
+    hp_e.resize(hp_e_start[nhp]);
+    {
+        std::vector<int32_t> fill(hp_e_start.begin(), hp_e_start.end() - 1);
+        for (int e = 0; e < ne; e++)
+            if (pose_h[G->e_pose[e]] >= 0) hp_e[fill[pose_h[G->e_pose[e]]]++] = e;
+    }
+    for (int b = 0; b < nblk; b++) hp_b_start[blk_pose[b] + 1]++;
+    for (int i = 0; i < nhp; i++) hp_b_start[i + 1] += hp_b_start[i];
+    {
+        std::vector<int32_t> fill(hp_b_start.begin(), hp_b_start.end() - 1);
+        for (int b = 0; b < nblk; b++) hp_b[fill[blk_pose[b]]++] = b;
+    }
+    // pose pairs (i <= j), dense index; contributions in landmark order
+    const int npairs = nhp * (nhp + 1) / 2;
+    auto pid = [nhp](int i, int j) { return i * nhp - i * (i - 1) / 2 + (j - i); };
+    std::vector<int32_t> pair_start(npairs + 1, 0);
+    for (int l = 0; l < nhl; l++)
+        for (int a = lm_b_start[l]; a < lm_b_start[l + 1]; a++)
+            for (int b = a; b < lm_b_start[l + 1]; b++) pair_start[pid(blk_pose[a], blk_pose[b]) + 1]++;
+    for (int k = 0; k < npairs; k++) pair_start[k + 1] += pair_start[k];
+    std::vector<int32_t> pair_ab(2 * (size_t)std::max(pair_start[npairs], 1));
+    {
+        std::vector<int32_t> fill(pair_start.begin(), pair_start.end() - 1);
+        for (int l = 0; l < nhl; l++)
+            for (int a = lm_b_start[l]; a < lm_b_start[l + 1]; a++)
+                for (int b = a; b < lm_b_start[l + 1]; b++) {
+                    const int k = fill[pid(blk_pose[a], blk_pose[b])]++;
+                    pair_ab[2 * k] = a;
+                    pair_ab[2 * k + 1] = b;
+                }
+    }
+    // ---------------------------------------------------------------- device layout
+    osg_packer pk;
+    const size_t o_fixed = pk.add(G->pose_fixed, np);
+    const size_t o_epose = pk.add(G->e_pose, 4 * (size_t)ne);
+    const size_t o_epoint = pk.add(G->e_point, 4 * (size_t)ne);
+    const size_t o_ecam = pk.add(G->e_cam, 4 * (size_t)ne);
+    const size_t o_ekind = pk.add(G->e_kind, ne);
+    const size_t o_eobs = pk.add(G->e_obs, 24 * (size_t)ne);
+    const size_t o_eisig = pk.add(G->e_inv_sigma2, 4 * (size_t)ne);
+    const size_t o_cams = pk.add(G->cams, sizeof(osg_camera) * G->n_cams);
+    const size_t o_poseh = pk.add(pose_h.data(), 4 * (size_t)np);
+    const size_t o_hppose = pk.add(hp_pose.data(), 4 * (size_t)nhp);
+    const size_t o_pointh = pk.add(point_h.data(), 4 * (size_t)npt);
+    const size_t o_hlpoint = pk.add(hl_point.data(), 4 * (size_t)nhl);
+    const size_t o_lmes = pk.add(lm_e_start.data(), 4 * (size_t)(nhl + 1));
+    const size_t o_lme = pk.add(lm_e.data(), 4 * (size_t)ne);
+    const size_t o_lmbs = pk.add(lm_b_start.data(), 4 * (size_t)(nhl + 1));
+    const size_t o_blkpose = pk.add(blk_pose.data(), 4 * (size_t)nblk);
+    const size_t o_eblk = pk.add(edge_blk.data(), 4 * (size_t)ne);
+    const size_t o_hpes = pk.add(hp_e_start.data(), 4 * (size_t)(nhp + 1));
+    const size_t o_hpe = pk.add(hp_e.data(), 4 * hp_e.size());
+    const size_t o_hpbs = pk.add(hp_b_start.data(), 4 * (size_t)(nhp + 1));
+    const size_t o_hpb = pk.add(hp_b.data(), 4 * (size_t)nblk);
+    const size_t o_pairs = pk.add(pair_start.data(), 4 * (size_t)(npairs + 1));
+    const size_t o_pairab = pk.add(pair_ab.data(), 4 * pair_ab.size());
+    const size_t o_pose0 = pk.add(G->pose, 56 * (size_t)np);
+    const size_t o_point0 = pk.add(G->point, 24 * (size_t)npt);
+    char *pin = (char *)osg_pinned(ctx, pk.total + 4096 + sizeof(double) * (3 * NPART + 64));
+    if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
+    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    pk.fill(pin);
+    char *din = nullptr;
+    OSG_ALLOC(ctx, din, SLOT_BA2, pk.total + 256);
+    OSG_HIP_CHECK(ctx, hipMemcpyAsync(din, pin, pk.total, hipMemcpyHostToDevice, ctx->stream));
+    // state buffers
+    const int sp = 6 * nhp;
+    size_t off = 0;
+    size_t st_bytes = 0;
+    {  // size pass
+        char *z = nullptr;
+        carve<double>(z, st_bytes, 7 * (size_t)np);      // pose A
+        carve<double>(z, st_bytes, 7 * (size_t)np);      // pose B
+        carve<double>(z, st_bytes, 3 * (size_t)npt);     // point A
+        carve<double>(z, st_bytes, 3 * (size_t)npt);     // point B
+        carve<double>(z, st_bytes, 3 * (size_t)ne);      // err
+        carve<double>(z, st_bytes, 32 * (size_t)ne);     // J
+        carve<double>(z, st_bytes, 9 * (size_t)nhl);     // Hll
+        carve<double>(z, st_bytes, 3 * (size_t)nhl);     // bl
+        carve<double>(z, st_bytes, 18 * (size_t)nblk);   // Hpl
+        carve<double>(z, st_bytes, 36 * (size_t)nhp);    // Hpp
+        carve<double>(z, st_bytes, 6 * (size_t)nhp);     // bp
+        carve<double>(z, st_bytes, 9 * (size_t)nhl);     // Dinv
+        carve<double>(z, st_bytes, 18 * (size_t)nblk);   // BDinv
+        carve<double>(z, st_bytes, 6 * (size_t)nblk);    // coef
+        carve<double>(z, st_bytes, (size_t)sp * sp);     // Hs
+        carve<double>(z, st_bytes, (size_t)sp);          // bs
+        carve<double>(z, st_bytes, (size_t)sp + 3 * (size_t)nhl);  // x
+        carve<double>(z, st_bytes, 3 * (size_t)NPART + 64);        // partials
+        carve<int>(z, st_bytes, 16);                                // flags
+        carve<uint8_t>(z, st_bytes, ne);                            // edge_bad
+        st_bytes += 256;
+    }
+    char *dst = nullptr;
+    OSG_ALLOC(ctx, dst, SLOT_BA3, st_bytes);
+    double *poseA = carve<double>(dst, off, 7 * (size_t)np);
+    double *poseB = carve<double>(dst, off, 7 * (size_t)np);
+    double *pointA = carve<double>(dst, off, 3 * (size_t)npt);
+    double *pointB = carve<double>(dst, off, 3 * (size_t)npt);
+    LbaDev D = {};
+    D.np = np;
+    D.npt = npt;
+    D.ne = ne;
+    D.nhp = nhp;
+    D.nhl = nhl;
+    D.nblk = nblk;
+    D.npairs = npairs;
+    D.n_cams = G->n_cams;
+    D.pose_fixed = osg_dptr<uint8_t>(din, o_fixed);
+    D.e_pose = osg_dptr<int32_t>(din, o_epose);
+    D.e_point = osg_dptr<int32_t>(din, o_epoint);
+    D.e_cam = osg_dptr<int32_t>(din, o_ecam);
+    D.e_kind = osg_dptr<int8_t>(din, o_ekind);
+    D.e_obs = osg_dptr<double>(din, o_eobs);
+    D.e_isig2 = osg_dptr<float>(din, o_eisig);
+    D.cams = osg_dptr<osg_camera>(din, o_cams);
+    D.pose_h = osg_dptr<int32_t>(din, o_poseh);
+    D.hp_pose = osg_dptr<int32_t>(din, o_hppose);
+    D.point_h = osg_dptr<int32_t>(din, o_pointh);
+    D.hl_point = osg_dptr<int32_t>(din, o_hlpoint);
+    D.lm_e_start = osg_dptr<int32_t>(din, o_lmes);
+    D.lm_e = osg_dptr<int32_t>(din, o_lme);
+    D.lm_b_start = osg_dptr<int32_t>(din, o_lmbs);
+    D.blk_pose = osg_dptr<int32_t>(din, o_blkpose);
+    D.edge_blk = osg_dptr<int32_t>(din, o_eblk);
+    D.hp_e_start = osg_dptr<int32_t>(din, o_hpes);
+    D.hp_e = osg_dptr<int32_t>(din, o_hpe);
+    D.hp_b_start = osg_dptr<int32_t>(din, o_hpbs);
+    D.hp_b = osg_dptr<int32_t>(din, o_hpb);
+    D.pair_start = osg_dptr<int32_t>(din, o_pairs);
+    D.pair_ab = osg_dptr<int32_t>(din, o_pairab);
+    D.err = carve<double>(dst, off, 3 * (size_t)ne);
+    D.J = carve<double>(dst, off, 32 * (size_t)ne);
+    D.Hll = carve<double>(dst, off, 9 * (size_t)nhl);
+    D.bl = carve<double>(dst, off, 3 * (size_t)nhl);
+    D.Hpl = carve<double>(dst, off, 18 * (size_t)nblk);
+    D.Hpp = carve<double>(dst, off, 36 * (size_t)nhp);
+    D.bp = carve<double>(dst, off, 6 * (size_t)nhp);
+    D.Dinv = carve<double>(dst, off, 9 * (size_t)nhl);
+    D.BDinv = carve<double>(dst, off, 18 * (size_t)nblk);
+    D.coef = carve<double>(dst, off, 6 * (size_t)nblk);
+    D.Hs = carve<double>(dst, off, (size_t)sp * sp);
+    D.bs = carve<double>(dst, off, (size_t)sp);
+    D.x = carve<double>(dst, off, (size_t)sp + 3 * (size_t)nhl);
+    D.part = carve<double>(dst, off, 3 * (size_t)NPART + 64);
+    D.flag = carve<int>(dst, off, 16);
+    uint8_t *d_bad = carve<uint8_t>(dst, off, ne);
+    OSG_HIP_CHECK(ctx, hipMemcpyAsync(poseA, din + o_pose0, 56 * (size_t)np, hipMemcpyDeviceToDevice, ctx->stream));
+    OSG_HIP_CHECK(ctx, hipMemcpyAsync(pointA, din + o_point0, 24 * (size_t)npt, hipMemcpyDeviceToDevice, ctx->stream));
+
+    const int ge = (ne + EB - 1) / EB;
+    const int gl = (nhl + EB - 1) / EB;
+    const int gu = (std::max(std::max(nhl, np), npt) + EB - 1) / EB;
+    OSG_REQUIRE(ctx, ge <= NPART && gu <= NPART && gl + nhp <= NPART, "graph too large for the partial buffers");
+    double *h_part = (double *)(pin + ((pk.total + 255) & ~size_t(255)));
+    double *cur_pose = poseA, *cur_point = pointA, *new_pose = poseB, *new_point = pointB;
+
+    auto errors = [&](const double *poses, const double *points) -> int {
+        hipLaunchKernelGGL(k_errors, dim3(ge), dim3(EB), 0, ctx->stream, D, poses, points, 0);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    };
+    auto fetch = [&](size_t first, size_t count) -> int {
+        if (hipMemcpyAsync(h_part + first, D.part + first, sizeof(double) * count, hipMemcpyDeviceToHost,
+                           ctx->stream) != hipSuccess)
+            return -1;
+        return hipStreamSynchronize(ctx->stream) == hipSuccess ? 0 : -1;
+    };
+    auto sum_part = [&](size_t first, int count) {
+        double s = 0;
+        for (int i = 0; i < count; i++) s += h_part[first + i];
+        return s;
+    };
+
+    // initial chi2 (activeRobustChi2 before optimising)
+    D.pose_cur = cur_pose;
+    D.point_cur = cur_point;
+    if (errors(cur_pose, cur_point) || fetch(0, ge)) return osg_set_error(ctx, OSG_E_HIP, "k_errors");
+    double currentChi = sum_part(0, ge);
+    R->chi2_initial = currentChi;
+    bool errors_current = true;  // err[] holds the current estimate's errors
+    double lambda = 0, ni = 2;
+    int nBad = 0, iters = 0, trials = 0;
+    const int max_it = G->iterations;
+    bool ok = true;
+    for (int it = 0; it < max_it && !(stop && *stop) && ok; it++) {
+        D.pose_cur = cur_pose;
+        D.point_cur = cur_point;
+        if (!errors_current) {
+            if (errors(cur_pose, cur_point) || fetch(0, ge)) return osg_set_error(ctx, OSG_E_HIP, "k_errors");
+            currentChi = sum_part(0, ge);
+        }
+        const double iniChi = currentChi;
+        hipLaunchKernelGGL(k_jacobians, dim3(ge), dim3(EB), 0, ctx->stream, D);
+        hipLaunchKernelGGL(k_point_red, dim3(std::max(gl, 1)), dim3(EB), 0, ctx->stream, D);
+        if (nhp > 0) hipLaunchKernelGGL(k_pose_red, dim3(nhp), dim3(EB), 0, ctx->stream, D, 2 * NPART + gl);
+        OSG_HIP_CHECK(ctx, hipGetLastError());
+        if (it == 0) {
+            if (fetch(2 * NPART, (size_t)gl + nhp)) return osg_set_error(ctx, OSG_E_HIP, "diag fetch");
+            if (G->user_lambda_init > 0) lambda = G->user_lambda_init;
+            else {
+                double md = 0;
+                for (int i = 0; i < gl + nhp; i++) md = std::max(md, h_part[2 * NPART + i]);
+                lambda = 1e-5 * md;
+            }
+            ni = 2;
+            nBad = 0;
+        }
+        double rho = 0;
+        int qmax = 0;
+        do {
+            trials++;
+            hipLaunchKernelGGL(k_schur_point, dim3(std::max(gl, 1)), dim3(EB), 0, ctx->stream, D, lambda);
+            if (nhp > 0) {
+                hipLaunchKernelGGL(k_schur_pairs, dim3((npairs * 64 + 255) / 256), dim3(256), 0, ctx->stream, D, lambda);
+                hipLaunchKernelGGL(k_chol, dim3(1), dim3(CT), 0, ctx->stream, D);
+            }
+            D.pose_new = new_pose;
+            D.point_new = new_point;
+            hipLaunchKernelGGL(k_update, dim3(gu), dim3(EB), 0, ctx->stream, D, lambda);
+            OSG_HIP_CHECK(ctx, hipGetLastError());
+            if (errors(new_pose, new_point)) return osg_set_error(ctx, OSG_E_HIP, "k_errors");
+            // one download: chi partials, scale partials, cholesky flag
+            OSG_HIP_CHECK(ctx, hipMemcpyAsync(h_part, D.part, sizeof(double) * 2 * NPART, hipMemcpyDeviceToHost, ctx->stream));
+            int hflag = 1;
+            if (nhp > 0) OSG_HIP_CHECK(ctx, hipMemcpyAsync(&hflag, D.flag, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+            OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+            double tempChi = sum_part(0, ge);
+            if (!hflag) tempChi = DBL_MAX;
+            rho = currentChi - tempChi;
+            double scale = sum_part(NPART, gu) + 1e-3;
+            rho /= scale;
+            if (rho > 0 && std::isfinite(tempChi)) {
+                double alpha = 1. - std::pow((2 * rho - 1), 3);
+                alpha = std::min(alpha, 2. / 3.);
+                const double scaleFactor = std::max(1. / 3., alpha);
+                lambda *= scaleFactor;
+                ni = 2;
+                currentChi = tempChi;
+                std::swap(cur_pose, new_pose);
+                std::swap(cur_point, new_point);
+                errors_current = true;
+            } else {
+                lambda *= ni;
+                ni *= 2;
+                errors_current = false;  // err[] holds the rejected estimate's errors
+            }
+            qmax++;
+        } while (rho < 0 && qmax < 10 && !(stop && *stop));
+        iters++;
+        if (qmax == 10 || rho == 0) ok = false;
+        else {
+            if ((iniChi - currentChi) * 1e3 < iniChi) nBad++;
+            else nBad = 0;
+            if (nBad >= 3) ok = false;
+        }
+    }
+    R->iterations = iters;
+    R->trials = trials;
+    R->aborted = (stop && *stop) ? 1 : 0;
+    R->chi2_final = currentChi;
+    // classification with the last computed errors; estimates out
+    D.pose_cur = cur_pose;
+    D.point_cur = cur_point;
+    hipLaunchKernelGGL(k_classify, dim3(ge), dim3(EB), 0, ctx->stream, D, cur_pose, cur_point, d_bad);
+    OSG_HIP_CHECK(ctx, hipGetLastError());
+    OSG_HIP_CHECK(ctx, hipMemcpyAsync(R->pose, cur_pose, 56 * (size_t)np, hipMemcpyDeviceToHost, ctx->stream));
+    OSG_HIP_CHECK(ctx, hipMemcpyAsync(R->point, cur_point, 24 * (size_t)npt, hipMemcpyDeviceToHost, ctx->stream));
+    OSG_HIP_CHECK(ctx, hipMemcpyAsync(R->edge_bad, d_bad, ne, hipMemcpyDeviceToHost, ctx->stream));
+    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    return iters;
 }

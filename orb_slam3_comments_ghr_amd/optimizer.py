@@ -1,0 +1,370 @@
+"""Host mirror of ``ORB_SLAM3::Optimizer::PoseOptimization`` / ``LocalBundleAdjustment``
+(ref:include/Optimizer.h:55,77) on the C ABI in include/osg_ba.h, plus the seeded synthetic
+problems of SURVEY.md §8d (C3 PoseOptimization, C4 LocalBA 50 KF x 10k points).
+
+The graph gathering that the reference does from Frame / KeyFrame / MapPoint (window selection,
+vertex ids, edge insertion order, float->double casts) is the adapter's job; here a problem is
+given directly as those arrays.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import Context, _abi
+from .synth import EUROC_BF, EUROC_CX, EUROC_CY, EUROC_FX, EUROC_FY, EUROC_H, EUROC_W
+
+
+def _p(a):
+    return None if a is None else int(a.ctypes.data)
+
+
+def pinhole_camera(fx=EUROC_FX, fy=EUROC_FY, cx=EUROC_CX, cy=EUROC_CY, bf=EUROC_BF, trl=None):
+    c = _abi.OsgCamera()
+    c.type = _abi.CAM_PINHOLE
+    for i, v in enumerate([fx, fy, cx, cy, 0, 0, 0, 0]):
+        c.p[i] = v
+    c.fx, c.fy, c.cx, c.cy, c.bf = fx, fy, cx, cy, bf
+    t = trl if trl is not None else [0, 0, 0, 1, 0, 0, 0]
+    for i in range(7):
+        c.trl[i] = t[i]
+    return c
+
+
+def kb8_camera(fx=190.98, fy=190.97, cx=254.93, cy=256.90, k=(3.48e-3, 7.15e-4, -2.05e-3, 2.03e-4), trl=None):
+    c = _abi.OsgCamera()
+    c.type = _abi.CAM_KB8
+    for i, v in enumerate([fx, fy, cx, cy, *k]):
+        c.p[i] = v
+    c.fx, c.fy, c.cx, c.cy, c.bf = fx, fy, cx, cy, 0.0
+    t = trl if trl is not None else [0, 0, 0, 1, 0, 0, 0]
+    for i in range(7):
+        c.trl[i] = t[i]
+    return c
+
+
+# ----------------------------------------------------------------------------- geometry helpers
+def rot_to_quat(m):
+    """Eigen Quaternion(Matrix3) (trace method), coeffs (x, y, z, w)."""
+    q = np.zeros(4)
+    t = m[0, 0] + m[1, 1] + m[2, 2]
+    if t > 0:
+        s = np.sqrt(t + 1.0)
+        q[3] = 0.5 * s
+        s = 0.5 / s
+        q[0] = (m[2, 1] - m[1, 2]) * s
+        q[1] = (m[0, 2] - m[2, 0]) * s
+        q[2] = (m[1, 0] - m[0, 1]) * s
+    else:
+        i = 0
+        if m[1, 1] > m[0, 0]:
+            i = 1
+        if m[2, 2] > m[i, i]:
+            i = 2
+        j, k = (i + 1) % 3, (i + 2) % 3
+        s = np.sqrt(m[i, i] - m[j, j] - m[k, k] + 1.0)
+        q[i] = 0.5 * s
+        s = 0.5 / s
+        q[3] = (m[k, j] - m[j, k]) * s
+        q[j] = (m[j, i] + m[i, j]) * s
+        q[k] = (m[k, i] + m[i, k]) * s
+    if q[3] < 0:
+        q = -q
+    return q / np.linalg.norm(q)
+
+
+def quat_to_rot(q):
+    x, y, z, w = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+def look_at(center, target, up=(0, -1, 0)):
+    """Tcw (world->camera) for a camera at `center` looking at `target` (z forward, y down)."""
+    z = np.asarray(target, float) - np.asarray(center, float)
+    z /= np.linalg.norm(z)
+    x = np.cross(np.asarray(up, float), z)
+    x /= np.linalg.norm(x)
+    y = np.cross(z, x)
+    Rcw = np.stack([x, y, z])
+    tcw = -Rcw @ np.asarray(center, float)
+    return Rcw, tcw
+
+
+def small_rotation(rng, deg):
+    axis = rng.normal(size=3)
+    axis /= np.linalg.norm(axis)
+    a = np.deg2rad(deg) * rng.normal()
+    K = np.array([[0, -axis[2], axis[1]], [axis[2], 0, -axis[0]], [-axis[1], axis[0], 0]])
+    return np.eye(3) + np.sin(a) * K + (1 - np.cos(a)) * K @ K
+
+
+def pose7(R, t):
+    """Sophus SE3f -> g2o SE3Quat as the reference does: float quaternion / translation cast to
+    double (ref:src/Optimizer.cc:97)."""
+    q = rot_to_quat(R).astype(np.float32).astype(np.float64)
+    return np.concatenate([q, np.asarray(t, np.float32).astype(np.float64)])
+
+
+def inv_level_sigma2(n_levels=8, factor=1.2):
+    s = np.ones(n_levels, np.float32)
+    for i in range(1, n_levels):
+        s[i] = np.float32(s[i - 1] * np.float32(factor))
+    return (np.float32(1.0) / (s * s)).astype(np.float32)
+
+
+# ----------------------------------------------------------------------------- problem containers
+@dataclass
+class PoseProblem:
+    pose: np.ndarray          # 7 doubles (q xyzw, t)
+    kind: np.ndarray          # int8 per edge
+    xw: np.ndarray            # n x 3 double
+    obs: np.ndarray           # n x 3 double
+    inv_sigma2: np.ndarray    # float32 per edge
+    cam: object = field(default_factory=pinhole_camera)
+    cam2: object = field(default_factory=pinhole_camera)
+
+    def __post_init__(self):
+        self.pose = np.ascontiguousarray(self.pose, np.float64)
+        self.kind = np.ascontiguousarray(self.kind, np.int8)
+        self.xw = np.ascontiguousarray(self.xw, np.float64).reshape(-1, 3)
+        self.obs = np.ascontiguousarray(self.obs, np.float64).reshape(-1, 3)
+        self.inv_sigma2 = np.ascontiguousarray(self.inv_sigma2, np.float32)
+
+    @property
+    def n(self):
+        return len(self.kind)
+
+    def struct(self):
+        s = _abi.OsgPoseProblem()
+        for i in range(7):
+            s.pose[i] = float(self.pose[i])
+        s.n_edges = self.n
+        s.kind, s.xw, s.obs, s.inv_sigma2 = _p(self.kind), _p(self.xw), _p(self.obs), _p(self.inv_sigma2)
+        s.cam = self.cam
+        s.cam2 = self.cam2
+        return s
+
+
+@dataclass
+class PoseResult:
+    pose: np.ndarray
+    outlier: np.ndarray
+    n_inliers: int
+    lm_iterations: int
+    lm_trials: int
+
+
+@dataclass
+class BAGraph:
+    pose: np.ndarray          # np x 7
+    pose_fixed: np.ndarray    # np uint8
+    point: np.ndarray         # npt x 3
+    e_point: np.ndarray
+    e_pose: np.ndarray
+    e_kind: np.ndarray
+    e_cam: np.ndarray
+    e_obs: np.ndarray         # ne x 3
+    e_inv_sigma2: np.ndarray
+    cams: list
+    iterations: int = 10
+    user_lambda_init: float = 0.0
+
+    def __post_init__(self):
+        self.pose = np.ascontiguousarray(self.pose, np.float64).reshape(-1, 7)
+        self.pose_fixed = np.ascontiguousarray(self.pose_fixed, np.uint8)
+        self.point = np.ascontiguousarray(self.point, np.float64).reshape(-1, 3)
+        self.e_point = np.ascontiguousarray(self.e_point, np.int32)
+        self.e_pose = np.ascontiguousarray(self.e_pose, np.int32)
+        self.e_kind = np.ascontiguousarray(self.e_kind, np.int8)
+        self.e_cam = np.ascontiguousarray(self.e_cam, np.int32)
+        self.e_obs = np.ascontiguousarray(self.e_obs, np.float64).reshape(-1, 3)
+        self.e_inv_sigma2 = np.ascontiguousarray(self.e_inv_sigma2, np.float32)
+        self._cams = (_abi.OsgCamera * max(1, len(self.cams)))(*self.cams)
+
+    def struct(self):
+        s = _abi.OsgBaGraph()
+        s.n_poses = len(self.pose)
+        s.pose, s.pose_fixed = _p(self.pose), _p(self.pose_fixed)
+        s.n_points = len(self.point)
+        s.point = _p(self.point)
+        s.n_edges = len(self.e_point)
+        s.e_point, s.e_pose, s.e_kind = _p(self.e_point), _p(self.e_pose), _p(self.e_kind)
+        s.e_cam, s.e_obs, s.e_inv_sigma2 = _p(self.e_cam), _p(self.e_obs), _p(self.e_inv_sigma2)
+        s.n_cams = len(self.cams)
+        s.cams = C.addressof(self._cams)
+        s.iterations = self.iterations
+        s.user_lambda_init = self.user_lambda_init
+        return s
+
+
+@dataclass
+class BAResult:
+    pose: np.ndarray
+    point: np.ndarray
+    edge_bad: np.ndarray
+    iterations: int
+    trials: int
+    chi2_initial: float
+    chi2_final: float
+    aborted: int
+
+
+def run_pose(fn, problems, handle=None):
+    """Call a PoseOptimization entry point (product batch API or the oracle) on problems."""
+    res_structs = (_abi.OsgPoseResult * len(problems))()
+    outl = [np.zeros(p.n, np.uint8) for p in problems]
+    for r, o in zip(res_structs, outl):
+        r.outlier = _p(o)
+    probs = (_abi.OsgPoseProblem * len(problems))(*[p.struct() for p in problems])
+    rc = fn(probs, res_structs) if handle is None else fn(handle, probs, len(problems), res_structs)
+    out = [PoseResult(np.array(list(r.pose)), o, r.n_inliers, r.lm_iterations, r.lm_trials)
+           for r, o in zip(res_structs, outl)]
+    return rc, out
+
+
+def make_ba_result(G: BAGraph):
+    R = _abi.OsgBaResult()
+    pose = np.zeros_like(G.pose)
+    point = np.zeros_like(G.point)
+    bad = np.zeros(len(G.e_point), np.uint8)
+    R.pose, R.point, R.edge_bad = _p(pose), _p(point), _p(bad)
+    return R, pose, point, bad
+
+
+class Optimizer:
+    """``Optimizer::PoseOptimization`` / ``LocalBundleAdjustment`` on the GPU."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+
+    def PoseOptimization(self, problems):
+        """Batch form: one launch for all frames.  Returns the per-frame results (the reference's
+        return value is ``n_inliers``)."""
+        single = isinstance(problems, PoseProblem)
+        probs = [problems] if single else list(problems)
+        lib, h = self.ctx.lib, self.ctx.handle
+        rc, out = run_pose(lib.osg_pose_optimization_batch, probs, handle=h)
+        self.ctx.check(rc, "PoseOptimization")
+        return out[0] if single else out
+
+    def LocalBundleAdjustment(self, G: BAGraph, stop_flag: np.ndarray | None = None) -> BAResult:
+        lib, h = self.ctx.lib, self.ctx.handle
+        R, pose, point, bad = make_ba_result(G)
+        gs = G.struct()
+        sf = None if stop_flag is None else _p(stop_flag)
+        rc = lib.osg_local_bundle_adjustment(h, C.byref(gs), C.byref(R), sf)
+        self.ctx.check(rc, "LocalBundleAdjustment")
+        return BAResult(pose, point, bad, R.iterations, R.trials, R.chi2_initial, R.chi2_final, R.aborted)
+
+
+def oracle_lba(oracle, G: BAGraph, stop_flag=None) -> BAResult:
+    R, pose, point, bad = make_ba_result(G)
+    gs = G.struct()
+    oracle.oracle_local_bundle_adjustment(C.byref(gs), C.byref(R), None if stop_flag is None else _p(stop_flag))
+    return BAResult(pose, point, bad, R.iterations, R.trials, R.chi2_initial, R.chi2_final, R.aborted)
+
+
+def oracle_pose(oracle, problems):
+    fn = lambda probs, res: [oracle.oracle_pose_optimization(C.byref(probs[i]), C.byref(res[i]))  # noqa: E731
+                             for i in range(len(probs))]
+    _, out = run_pose(fn, problems)
+    return out
+
+
+# ----------------------------------------------------------------------------- generators
+def synth_pose_problem(rng, n_edges=400, stereo_frac=0.6, outlier_frac=0.1, n_levels=8, cam=None):
+    """C3 PoseOptimization: Xw depth U[1,10] m in front of the camera, pose perturbed by
+    1 cm / 0.5 deg, pixel noise 1 px * 1.2^octave, 10 % outliers (+20..50 px), stereo u_R for
+    60 % of the edges (bf = 47.9)."""
+    cam = cam or pinhole_camera()
+    Rcw = small_rotation(rng, 20.0)
+    tcw = rng.normal(0, 1.0, 3)
+    u = rng.uniform(20, EUROC_W - 20, n_edges)
+    v = rng.uniform(20, EUROC_H - 20, n_edges)
+    z = rng.uniform(1.0, 10.0, n_edges)
+    Xc = np.stack([(u - EUROC_CX) / EUROC_FX * z, (v - EUROC_CY) / EUROC_FY * z, z], 1)
+    Xw = (Xc - tcw) @ Rcw  # Rcw^T (Xc - t)
+    Xw = Xw.astype(np.float32).astype(np.float64)
+    octv = rng.choice(n_levels, n_edges, p=np.array([1.2 ** -i for i in range(n_levels)]) / sum(1.2 ** -i for i in range(n_levels)))
+    sig = 1.2 ** octv
+    obs = np.zeros((n_edges, 3))
+    obs[:, 0] = u + rng.normal(0, 1, n_edges) * sig
+    obs[:, 1] = v + rng.normal(0, 1, n_edges) * sig
+    out = rng.random(n_edges) < outlier_frac
+    obs[out, 0] += rng.uniform(20, 50, out.sum()) * rng.choice([-1, 1], out.sum())
+    obs[out, 1] += rng.uniform(20, 50, out.sum()) * rng.choice([-1, 1], out.sum())
+    stereo = rng.random(n_edges) < stereo_frac
+    obs[:, 2] = np.where(stereo, obs[:, 0] - EUROC_BF / z + rng.normal(0, 0.5, n_edges), 0.0)
+    obs = obs.astype(np.float32).astype(np.float64)  # keypoints are float
+    kind = np.where(stereo, _abi.EDGE_STEREO, _abi.EDGE_MONO).astype(np.int8)
+    # perturbed initial pose
+    R0 = small_rotation(rng, 0.5) @ Rcw
+    t0 = tcw + rng.normal(0, 0.01, 3)
+    isig = inv_level_sigma2(n_levels)[octv]
+    return PoseProblem(pose7(R0, t0), kind, Xw, obs, isig, cam=cam, cam2=cam)
+
+
+def synth_lba_graph(rng, n_kf=50, n_points=10000, k_range=(2, 8), n_fixed=2, stereo_frac=0.0,
+                    outlier_frac=0.01, n_levels=8, radius=6.0, arc_deg=50.0):
+    """C4 LocalBundleAdjustment: n_kf keyframes on an arc (radius 6 m, ~5 m long) looking at a
+    4 x 4 x 2 m box of points; each point observed by k ~ U{2..8} keyframes that see it; pixel
+    noise 1 px * 1.2^octave; pose noise 1 cm / 0.3 deg; point noise 2 cm; 1 % gross outliers.
+    KeyFrames 0..n_fixed-1 are fixed (init KF + fixed observers)."""
+    cam = pinhole_camera()
+    ang = np.deg2rad(np.linspace(-arc_deg / 2, arc_deg / 2, n_kf))
+    centers = np.stack([radius * np.sin(ang), 0.3 * np.sin(3 * ang), -radius * np.cos(ang)], 1)
+    Rs, ts = [], []
+    for c in centers:
+        R, t = look_at(c, [0, 0, 0])
+        Rs.append(R)
+        ts.append(t)
+    P = np.stack([rng.uniform(-2, 2, n_points), rng.uniform(-2, 2, n_points), rng.uniform(-1, 1, n_points)], 1)
+    isig_tab = inv_level_sigma2(n_levels)
+    e_point, e_pose, e_obs, e_isig, e_kind = [], [], [], [], []
+    for p in range(n_points):
+        # keyframes that see the point inside the image
+        Xc = np.einsum("kij,j->ki", np.array(Rs), P[p]) + np.array(ts)
+        u = EUROC_FX * Xc[:, 0] / Xc[:, 2] + EUROC_CX
+        v = EUROC_FY * Xc[:, 1] / Xc[:, 2] + EUROC_CY
+        vis = np.nonzero((Xc[:, 2] > 0.5) & (u > 0) & (u < EUROC_W) & (v > 0) & (v < EUROC_H))[0]
+        if len(vis) < 2:
+            continue
+        k = min(len(vis), int(rng.integers(k_range[0], k_range[1] + 1)))
+        obs_kf = np.sort(rng.choice(vis, k, replace=False))
+        for kf in obs_kf:
+            octv = int(rng.choice(n_levels, p=np.array([1.2 ** -i for i in range(n_levels)]) / sum(1.2 ** -i for i in range(n_levels))))
+            s = 1.2 ** octv
+            uu = u[kf] + rng.normal() * s
+            vv = v[kf] + rng.normal() * s
+            if rng.random() < outlier_frac:
+                uu += rng.uniform(20, 50) * rng.choice([-1, 1])
+                vv += rng.uniform(20, 50) * rng.choice([-1, 1])
+            st = rng.random() < stereo_frac
+            ur = uu - EUROC_BF / Xc[kf, 2] + rng.normal() * 0.5 if st else 0.0
+            e_point.append(p)
+            e_pose.append(kf)
+            e_obs.append([uu, vv, ur])
+            e_isig.append(isig_tab[octv])
+            e_kind.append(_abi.EDGE_STEREO if st else _abi.EDGE_MONO)
+    e_point = np.array(e_point)
+    used = np.unique(e_point)
+    remap = -np.ones(n_points, int)
+    remap[used] = np.arange(len(used))
+    e_point = remap[e_point]
+    P = P[used]
+    poses = []
+    for i, (R, t) in enumerate(zip(Rs, ts)):
+        if i >= n_fixed:
+            R = small_rotation(rng, 0.3) @ R
+            t = t + rng.normal(0, 0.01, 3)
+        poses.append(pose7(R, t))
+    Pn = (P + rng.normal(0, 0.02, P.shape)).astype(np.float32).astype(np.float64)
+    fixed = np.zeros(n_kf, np.uint8)
+    fixed[:n_fixed] = 1
+    obs = np.array(e_obs, np.float32).astype(np.float64)
+    return BAGraph(np.array(poses), fixed, Pn, e_point, np.array(e_pose), np.array(e_kind, np.int8),
+                   np.zeros(len(e_point), np.int32), obs, np.array(e_isig, np.float32), [cam])
