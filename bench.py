@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-stream", action="store_true")
     ap.add_argument("--no-ba", action="store_true")
+    ap.add_argument("--ba-reps", type=int, default=20)
     return ap.parse_args()
 
 
@@ -184,11 +185,69 @@ def main():
         out["cpu_baseline"] = cpu_baseline(q_np, t_np, args.cpu_seconds)
         out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
 
+    # ---- LocalBA iters/s on C4 (50 KF x 10k points), the second half of the metric ----------
+    if not args.no_ba:
+        out["local_ba"] = bench_lba(ctx, rank, world, dist, dev, args)
+
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_lba(ctx, rank, world, dist, dev, args):
+    """osg_local_bundle_adjustment on the C4 graph (host API: graph upload, structure build,
+    optimize(10), classification, download), repeated; iterations / wall second.  Each rank runs
+    its own window (replicas)."""
+    import torch
+    from orb_slam3_comments_ghr_amd import optimizer as op
+    rng = np.random.default_rng(0x0B5EED04 + rank)
+    G = op.synth_lba_graph(rng, n_kf=50, n_points=10000)
+    opt = op.Optimizer(ctx)
+    for _ in range(2):
+        r = opt.LocalBundleAdjustment(G)
+    reps = args.ba_reps
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    iters = 0
+    for _ in range(reps):
+        r = opt.LocalBundleAdjustment(G)
+        iters += r.iterations
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el, iters], dtype=torch.float64, device=dev)
+        mx = tt.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = tt.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        el, iters = float(mx[0].item()), int(sm[1].item())
+    res = {
+        "metric": "LocalBA iters/s", "value": round(iters / el, 1), "unit": "LM iterations/s",
+        "workload": f"C4: {len(G.pose)} KF x {len(G.point)} points x {len(G.e_point)} mono edges, optimize(10), {reps} LBAs per rank",
+        "ms_per_lba": round(el / reps * 1e3, 3), "iterations_per_lba": r.iterations,
+        "trials_per_lba": r.trials, "n_gpus": world, "dtype": "f64",
+        "flop_per_iter_survey_formula": 72.6e6,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        so = os.path.join(ROOT, "oracle", "liboracle.so")
+        from orb_slam3_comments_ghr_amd import _abi
+        lib = _abi.declare_oracle(ctypes.CDLL(so))
+        t0 = time.perf_counter()
+        n = 0
+        ci = 0
+        while time.perf_counter() - t0 < args.cpu_seconds / 2 or n == 0:
+            rr = op.oracle_lba(lib, G)
+            ci += rr.iterations
+            n += 1
+        cel = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": round(ci / cel, 2), "unit": "LM iterations/s", "cores": 1, "kind": "port",
+                               "sample": f"{n} x C4 LBA (oracle_local_bundle_adjustment, gcc -O3, 1 thread, dense LDL^T) in {cel:.1f} s"}
+        res["speedup_vs_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
+    return res
 
 
 def cpu_baseline(q_np, t_np, seconds):
