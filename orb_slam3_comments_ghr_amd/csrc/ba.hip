@@ -11,15 +11,15 @@
 //
 // Per LM iteration (device):
 //   k_errors      per edge: error, Huber rho -> per-workgroup chi2 partials        (HBM/latency)
-//   k_jacobians   per edge: J_pose (3x6), J_point (3x3), weights                 (FP64 VALU)
-//   k_point_red   per point: Hll, b_l and its Hpl blocks from its edges            (segmented, no atomics)
+//   k_linearize   per edge: Jacobians -> the edge's Hpp/b_p/Hll/b_l/Hpl terms      (FP64 VALU)
+//   k_point_red   per point: sums Hll, b_l and its Hpl blocks                      (segmented, no atomics)
 //   k_pose_red    per pose: Hpp, b_p from its edges (workgroup reduction)
 // Per LM trial (lambda known on the host):
 //   k_schur_point per point: Dinv = (Hll + lambda I)^-1, BDinv = Hpl Dinv, coef = Hpl Dinv b_l
 //   k_schur_pairs per pose pair (i <= j), one wave: S_ij = sum_p BDinv_ip Hpl_jp^T ; writes the
 //                 dense reduced camera matrix Hpp + lambda I - S and b_schur
-//   k_chol        one workgroup: blocked Cholesky of the reduced system (n = 6 x free poses)
-//                 and the two triangular solves
+//   k_chol_*      blocked Cholesky of the reduced system (n = 6 x free poses): panel kernel,
+//                 FP64-MFMA trailing SYRK, blocked triangular solves
 //   k_update      per point: x_l = Dinv (b_l - Hpl^T x_p), new estimates (poses: exp(x) * T)
 //                 and the LM scale sum;  then k_errors on the new estimates -> tempChi
 // The host reads back 3 scalars per trial and runs the accept / reject / lambda logic exactly as
@@ -66,7 +66,7 @@ struct LbaDev {
     const double *pose_cur, *point_cur;
     double *pose_new, *point_new;
     double *err;                         // 3 per edge
-    double *J;                           // 32 per edge
+    double *J;                           // EC per edge: quadratic-form contributions
     double *Hll, *bl, *Hpl, *Hpp, *bp;
     double *Dinv, *BDinv, *coef;
     double *Hs, *bs, *x;
@@ -123,8 +123,11 @@ __global__ __launch_bounds__(EB) void k_errors(LbaDev D, const double *__restric
     if (threadIdx.x == 0) D.part[part_off + blockIdx.x] = t;
 }
 
-// per edge Jacobians and weights: J[e] = {Jp[3][6], Jx[3][3], ww, omega_r[3], rho1}
-__global__ __launch_bounds__(EB) void k_jacobians(LbaDev D)
+// per edge: Jacobians and the edge's quadratic-form contributions (ref:Thirdparty/g2o/g2o/core/
+// base_binary_edge.hpp:55-120, robust branch): C[e] = {Hpp 21 (upper), b_p 6, Hll 6 (upper),
+// b_l 3, Hpl 18 (6x3)} = 54 doubles; the reductions below only sum them.
+constexpr int EC = 54;
+__global__ __launch_bounds__(EB) void k_linearize(LbaDev D)
 {
     const int e = blockIdx.x * EB + threadIdx.x;
     if (e >= D.ne) return;
@@ -140,54 +143,58 @@ __global__ __launch_bounds__(EB) void k_jacobians(LbaDev D)
     float dsqr;
     kind_delta(k, delta, dsqr);
     huber(chi2_of(ev, dim, w), delta, dsqr, r0, rho1);
-    double *o = D.J + 32 * (size_t)e;
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 6; j++) o[i * 6 + j] = (i < dim) ? Jp[i][j] : 0.0;
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) o[18 + i * 3 + j] = (i < dim) ? Jx[i][j] : 0.0;
-    o[27] = rho1 * w;
-    for (int i = 0; i < 3; i++) o[28 + i] = (i < dim) ? -(w * ev[i]) * rho1 : 0.0;
-    o[31] = (double)dim;
+    const double ww = rho1 * w;
+    double om[3];
+    for (int d = 0; d < 3; d++) om[d] = (d < dim) ? -(w * ev[d]) * rho1 : 0.0;
+    if (dim == 2) {
+        for (int j = 0; j < 6; j++) Jp[2][j] = 0.0;
+        for (int j = 0; j < 3; j++) Jx[2][j] = 0.0;
+    }
+    double *o = D.J + EC * (size_t)e;
+    int c = 0;
+    for (int a = 0; a < 6; a++)
+        for (int bb = a; bb < 6; bb++)
+            o[c++] = Jp[0][a] * ww * Jp[0][bb] + Jp[1][a] * ww * Jp[1][bb] + Jp[2][a] * ww * Jp[2][bb];
+    for (int a = 0; a < 6; a++) o[c++] = Jp[0][a] * om[0] + Jp[1][a] * om[1] + Jp[2][a] * om[2];
+    for (int a = 0; a < 3; a++)
+        for (int bb = a; bb < 3; bb++)
+            o[c++] = Jx[0][a] * ww * Jx[0][bb] + Jx[1][a] * ww * Jx[1][bb] + Jx[2][a] * ww * Jx[2][bb];
+    for (int a = 0; a < 3; a++) o[c++] = Jx[0][a] * om[0] + Jx[1][a] * om[1] + Jx[2][a] * om[2];
+    for (int a = 0; a < 6; a++)
+        for (int bb = 0; bb < 3; bb++)
+            o[c++] = Jp[0][a] * ww * Jx[0][bb] + Jp[1][a] * ww * Jx[1][bb] + Jp[2][a] * ww * Jx[2][bb];
 }
 
-// per landmark: Hll (3x3), b_l and the Hpl blocks (6x3) of its (free pose) edges
+// per landmark: Hll (3x3), b_l and the Hpl blocks of its edges (sums of edge contributions)
 __global__ __launch_bounds__(EB) void k_point_red(LbaDev D)
 {
     __shared__ double s[EB / 64];
     const int l = blockIdx.x * EB + threadIdx.x;
     double md = 0.0;
     if (l < D.nhl) {
-        double H[9] = {0}, b[3] = {0};
-        const int b0 = D.lm_b_start[l], b1 = D.lm_b_start[l + 1];
-        for (int blk = b0; blk < b1; blk++)
-            for (int i = 0; i < 18; i++) D.Hpl[18 * (size_t)blk + i] = 0.0;
+        double H6[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
+        int last_blk = -1;
         for (int q = D.lm_e_start[l]; q < D.lm_e_start[l + 1]; q++) {
             const int e = D.lm_e[q];
-            const double *J = D.J + 32 * (size_t)e;
-            const double *Jp = J, *Jx = J + 18;
-            const double ww = J[27];
-            const double *om = J + 28;
-            for (int i = 0; i < 3; i++) {
-                double sb = 0;
-                for (int d = 0; d < 3; d++) sb += Jx[d * 3 + i] * om[d];
-                b[i] += sb;
-                for (int j = 0; j < 3; j++) {
-                    double h = 0;
-                    for (int d = 0; d < 3; d++) h += Jx[d * 3 + i] * ww * Jx[d * 3 + j];
-                    H[i * 3 + j] += h;
-                }
-            }
+            const double *C = D.J + EC * (size_t)e;
+            for (int i = 0; i < 6; i++) H6[i] += C[27 + i];
+            for (int i = 0; i < 3; i++) b[i] += C[33 + i];
             const int blk = D.edge_blk[e];
             if (blk >= 0) {
                 double *Hb = D.Hpl + 18 * (size_t)blk;
-                for (int i = 0; i < 6; i++)
-                    for (int j = 0; j < 3; j++) {
-                        double h = 0;
-                        for (int d = 0; d < 3; d++) h += Jp[d * 6 + i] * ww * Jx[d * 3 + j];
-                        Hb[i * 3 + j] += h;
-                    }
+                // blocks of one landmark are distinct per pose; parallel edges (mono + body of one
+                // keyframe) share a block and are summed in edge order
+                bool seen = false;
+                for (int q2 = D.lm_e_start[l]; q2 < q; q2++) seen |= (D.edge_blk[D.lm_e[q2]] == blk);
+                if (!seen)
+                    for (int i = 0; i < 18; i++) Hb[i] = C[36 + i];
+                else
+                    for (int i = 0; i < 18; i++) Hb[i] += C[36 + i];
+                last_blk = blk;
             }
         }
+        (void)last_blk;
+        const double H[9] = {H6[0], H6[1], H6[2], H6[1], H6[3], H6[4], H6[2], H6[4], H6[5]};
         for (int i = 0; i < 9; i++) D.Hll[9 * (size_t)l + i] = H[i];
         for (int i = 0; i < 3; i++) D.bl[3 * (size_t)l + i] = b[i];
         md = fmax(fabs(H[0]), fmax(fabs(H[4]), fabs(H[8])));
@@ -213,21 +220,8 @@ __global__ __launch_bounds__(EB) void k_pose_red(LbaDev D, int diag_off)
     for (int k = 0; k < 27; k++) acc[k] = 0.0;
     for (int q = D.hp_e_start[i] + threadIdx.x; q < D.hp_e_start[i + 1]; q += EB) {
         const int e = D.hp_e[q];
-        const double *J = D.J + 32 * (size_t)e;
-        const double ww = J[27];
-        const double *om = J + 28;
-        int c = 0;
-        for (int a = 0; a < 6; a++)
-            for (int b = a; b < 6; b++) {
-                double h = 0;
-                for (int d = 0; d < 3; d++) h += J[d * 6 + a] * ww * J[d * 6 + b];
-                acc[c++] += h;
-            }
-        for (int a = 0; a < 6; a++) {
-            double sb = 0;
-            for (int d = 0; d < 3; d++) sb += J[d * 6 + a] * om[d];
-            acc[21 + a] += sb;
-        }
+        const double *C = D.J + EC * (size_t)e;
+        for (int k = 0; k < 27; k++) acc[k] += C[k];
     }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int k = 0; k < 27; k++) acc[k] = wave_sum(acc[k]);
@@ -298,34 +292,51 @@ __global__ __launch_bounds__(EB) void k_schur_point(LbaDev D, double lambda)
     }
 }
 
-// one wave per pose pair (i <= j): S = sum BDinv_a Hpl_b^T ; writes the dense reduced system
+// One wave per pose pair (i <= j).  Lane (r, c) < 36 owns S_ij[r][c] and runs over the pair's
+// contributions in landmark order — the order of g2o's Schur loop (ref:Thirdparty/g2o/g2o/core/
+// block_solver.hpp:381-432) — so the sum is deterministic and needs no cross-lane reduction:
+//   S[r][c] = sum_q  BDinv_a[r][:] . Hpl_b[c][:]
+// Writes Hs = Hpp + lambda I - S (both triangles) and b_schur.
 __global__ __launch_bounds__(256) void k_schur_pairs(LbaDev D, double lambda)
 {
     const int wave = (blockIdx.x * 256 + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (wave >= D.npairs) return;
-    // decode dense pair index -> (i, j), i <= j
     int i = 0, rem = wave;
     while (rem >= D.nhp - i) {
         rem -= D.nhp - i;
         i++;
     }
     const int j = i + rem;
-    double S[36];
-    for (int k = 0; k < 36; k++) S[k] = 0.0;
-    for (int q = D.pair_start[wave] + lane; q < D.pair_start[wave + 1]; q += 64) {
-        const int a = D.pair_ab[2 * q], b = D.pair_ab[2 * q + 1];
-        const double *BD = D.BDinv + 18 * (size_t)a;
-        const double *Bj = D.Hpl + 18 * (size_t)b;
-        for (int r = 0; r < 6; r++)
-            for (int c = 0; c < 6; c++)
-                S[r * 6 + c] += BD[3 * r] * Bj[3 * c] + BD[3 * r + 1] * Bj[3 * c + 1] + BD[3 * r + 2] * Bj[3 * c + 2];
-    }
-    for (int k = 0; k < 36; k++) S[k] = wave_sum(S[k]);
+    if (wave == 0 && lane == 0) D.flag[0] = 1;  // the Cholesky of this trial clears it on failure
     const int n = 6 * D.nhp;
-    if (lane < 36) {
-        const int r = lane / 6, c = lane % 6;
-        double v = -S[lane];
+    const int r = lane / 6, c = lane % 6;
+    const bool act = lane < 36;
+    double acc = 0.0;
+    const int q0 = D.pair_start[wave], q1 = D.pair_start[wave + 1];
+    int q = q0;
+    for (; q + 3 < q1; q += 4) {
+        double t[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int a = D.pair_ab[2 * (q + u)], b = D.pair_ab[2 * (q + u) + 1];
+            const double *BD = D.BDinv + 18 * (size_t)a + 3 * r;
+            const double *Bj = D.Hpl + 18 * (size_t)b + 3 * c;
+            t[u] = act ? (BD[0] * Bj[0] + BD[1] * Bj[1] + BD[2] * Bj[2]) : 0.0;
+        }
+        acc += t[0];
+        acc += t[1];
+        acc += t[2];
+        acc += t[3];
+    }
+    for (; q < q1; q++) {
+        const int a = D.pair_ab[2 * q], b = D.pair_ab[2 * q + 1];
+        const double *BD = D.BDinv + 18 * (size_t)a + 3 * r;
+        const double *Bj = D.Hpl + 18 * (size_t)b + 3 * c;
+        if (act) acc += BD[0] * Bj[0] + BD[1] * Bj[1] + BD[2] * Bj[2];
+    }
+    if (act) {
+        double v = -acc;
         if (i == j) {
             v += D.Hpp[36 * (size_t)i + lane];
             if (r == c) v += lambda;
@@ -335,97 +346,181 @@ __global__ __launch_bounds__(256) void k_schur_pairs(LbaDev D, double lambda)
     }
     if (i == j && lane < 6) {
         double cs = 0.0;
-        for (int q = D.hp_b_start[i]; q < D.hp_b_start[i + 1]; q++) cs += D.coef[6 * (size_t)D.hp_b[q] + lane];
+        for (int qq = D.hp_b_start[i]; qq < D.hp_b_start[i + 1]; qq++) cs += D.coef[6 * (size_t)D.hp_b[qq] + lane];
         D.bs[6 * i + lane] = D.bp[6 * (size_t)i + lane] - cs;
     }
 }
 
-// Dense Cholesky (LL^T, lower, in place) + forward/back substitution, one 1024-thread workgroup.
-// Right-looking, panel width CB: the panel is factored wave-synchronously from LDS, the trailing
-// lower triangle is updated with the panel held in LDS.
+// ---------------------------------------------------------------------------------------------
+// Reduced camera system: blocked right-looking Cholesky (LL^T, lower, in place in Hs) over
+// panels of CB = 32 columns, then blocked triangular solves.  Per panel:
+//   k_chol_panel  one workgroup: the 32x32 diagonal block factored by one wave with the rows in
+//                 registers (shuffles, no barriers), then the panel rows below solved against it;
+//   k_chol_syrk   trailing update A22 -= L21 L21^T on 32x32 lower tiles, one workgroup per tile,
+//                 one wave per 16x16 quadrant on FP64 MFMA (v_mfma_f64_16x16x4_f64, K = 32 as
+//                 8 MFMAs) — the only MFMA use on the path (the dense Schur GEMM).
+// The factorisation reports failure on a non-positive pivot (g2o's solvers then reject the step).
 constexpr int CB = 32;
-constexpr int CT = 1024;
 constexpr int CMAX = 384;  // max reduced dimension (64 free poses)
+typedef double d4 __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(CT) void k_chol(LbaDev D)
+__global__ __launch_bounds__(256) void k_chol_panel(LbaDev D, int k0)
 {
-    __shared__ double s_panel[CMAX * CB];  // rows k0.. n of the current panel (n - k0) x CB
-    __shared__ int s_ok;
+    __shared__ double s_d[CB][CB + 1];
     const int n = 6 * D.nhp;
     double *A = D.Hs;
+    const int nb = min(CB, n - k0);
     const int tid = threadIdx.x;
-    if (tid == 0) s_ok = 1;
+    if (tid < 64) {
+        // wave 0: rows of the diagonal block in registers (lane = row)
+        double a[CB];
+        const int r = tid;
+#pragma unroll
+        for (int c = 0; c < CB; c++) a[c] = (r < nb && c <= r && c < nb) ? A[(size_t)(k0 + r) * n + k0 + c] : 0.0;
+        int ok = 1;
+#pragma unroll
+        for (int c = 0; c < CB; c++) {
+            if (c < nb) {
+                const double d = __shfl(a[c], c);
+                ok &= d > 0.0;
+                const double piv = sqrt(fmax(d, 1e-300));
+                if (r == c) a[c] = piv;
+                else if (r > c) a[c] /= piv;
+                const double lrc = a[c];
+#pragma unroll
+                for (int cc = c + 1; cc < CB; cc++) {
+                    const double lcc = __shfl(a[c], cc);  // L[cc][c]
+                    if (cc < nb && r >= cc) a[cc] -= lrc * lcc;
+                }
+            }
+        }
+        if (r < CB)
+#pragma unroll
+            for (int c = 0; c < CB; c++) s_d[r][c] = a[c];
+        if (tid == 0 && !ok) D.flag[0] = 0;
+        if (r < nb)
+#pragma unroll
+            for (int c = 0; c < CB; c++)
+                if (c <= r && c < nb) A[(size_t)(k0 + r) * n + k0 + c] = a[c];
+    }
+    __syncthreads();
+    // rows below the diagonal block: L[row][0:nb] = A[row][0:nb] L_kk^-T (forward substitution)
+    for (int row = k0 + nb + tid; row < n; row += 256) {
+        double x[CB];
+        double *Ar = A + (size_t)row * n + k0;
+#pragma unroll
+        for (int c = 0; c < CB; c++) x[c] = (c < nb) ? Ar[c] : 0.0;
+#pragma unroll
+        for (int c = 0; c < CB; c++) {
+            if (c < nb) {
+                double v = x[c];
+#pragma unroll
+                for (int k = 0; k < c; k++) v -= x[k] * s_d[c][k];
+                x[c] = v / s_d[c][c];
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < CB; c++)
+            if (c < nb) Ar[c] = x[c];
+    }
+}
+
+// tile (ti, tj), ti >= tj, of the trailing matrix starting at t0 = k0 + CB
+__global__ __launch_bounds__(256) void k_chol_syrk(LbaDev D, int k0)
+{
+    const int n = 6 * D.nhp;
+    double *A = D.Hs;
+    const int t0 = k0 + CB;
+    // decode lower-triangular tile index
+    int ti = 0, rem = blockIdx.x;
+    while (rem > ti) {
+        rem -= ti + 1;
+        ti++;
+    }
+    const int tj = rem;
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int R0 = t0 + ti * CB + (w >> 1) * 16;  // quadrant rows
+    const int C0 = t0 + tj * CB + (w & 1) * 16;   // quadrant cols
+    if (R0 >= n || C0 >= n) return;
+    if (ti == tj && (w & 1) > (w >> 1)) return;   // strictly upper quadrant of a diagonal tile
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    const int ra = R0 + (l & 15), cb = C0 + (l & 15);
+#pragma unroll
+    for (int ks = 0; ks < CB / 4; ks++) {
+        const int kk = k0 + ks * 4 + (l >> 4);
+        const double a = (ra < n) ? A[(size_t)ra * n + kk] : 0.0;  // L[R0+i][k]
+        const double b = (cb < n) ? A[(size_t)cb * n + kk] : 0.0;  // L[C0+j][k] (= B[k][j])
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    }
+    const int col = C0 + (l & 15);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int row = R0 + (l >> 4) + 4 * q;
+        if (row < n && col < n && col <= row) A[(size_t)row * n + col] -= acc[q];
+    }
+}
+
+// blocked forward (L y = b) and backward (L^T x = y) substitution, one workgroup
+__global__ __launch_bounds__(1024) void k_chol_solve(LbaDev D)
+{
+    __shared__ double s_x[CMAX];
+    __shared__ double s_blk[CB];
+    const int n = 6 * D.nhp;
+    const double *A = D.Hs;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < n; i += 1024) s_x[i] = D.bs[i];
     __syncthreads();
     for (int k0 = 0; k0 < n; k0 += CB) {
         const int nb = min(CB, n - k0);
-        const int m = n - k0;  // rows in the panel (incl. the diagonal block)
-        // load panel columns k0..k0+nb of rows k0..n into LDS
-        for (int idx = tid; idx < m * nb; idx += CT) {
-            const int r = idx / nb, c = idx % nb;
-            s_panel[r * CB + c] = A[(size_t)(k0 + r) * n + k0 + c];
-        }
-        __syncthreads();
-        // unblocked right-looking factorisation of the panel (columns k0..k0+nb)
-        for (int c = 0; c < nb; c++) {
-            if (tid == 0) {
-                const double d = s_panel[c * CB + c];
-                if (!(d > 0.0)) s_ok = 0;
-                s_panel[c * CB + c] = sqrt(fmax(d, 1e-300));
+        if (tid < 64) {
+            const int r = tid;
+            double xv = (r < nb) ? s_x[k0 + r] : 0.0;
+            for (int c = 0; c < nb; c++) {
+                double xc = __shfl(xv, c);
+                xc /= A[(size_t)(k0 + c) * n + k0 + c];
+                if (r == c) xv = xc;
+                if (r > c && r < nb) xv -= A[(size_t)(k0 + r) * n + k0 + c] * xc;
             }
-            __syncthreads();
-            const double piv = s_panel[c * CB + c];
-            for (int r = c + 1 + tid; r < m; r += CT) s_panel[r * CB + c] /= piv;
-            __syncthreads();
-            // update the remaining panel columns c+1..nb for rows > c
-            const int w = nb - c - 1;
-            for (int idx = tid; idx < (m - c - 1) * w; idx += CT) {
-                const int r = c + 1 + idx / w, cc = c + 1 + idx % w;
-                if (r >= cc) s_panel[r * CB + cc] -= s_panel[r * CB + c] * s_panel[cc * CB + c];
+            if (r < nb) {
+                s_x[k0 + r] = xv;
+                s_blk[r] = xv;
             }
-            __syncthreads();
         }
-        // write the factored panel back (lower part)
-        for (int idx = tid; idx < m * nb; idx += CT) {
-            const int r = idx / nb, c = idx % nb;
-            if (r >= c) A[(size_t)(k0 + r) * n + k0 + c] = s_panel[r * CB + c];
-        }
-        // trailing update: A[r][cc] -= sum_k L[r][k] L[cc][k], k0+nb <= cc <= r < n
-        const int t0 = nb;  // first trailing row inside the panel indexing
-        const int mt = m - t0;
-        const long long tri = (long long)mt * (mt + 1) / 2;
-        for (long long idx = tid; idx < tri; idx += CT) {
-            // map idx -> (r, cc) in the lower triangle, row-major
-            int r = (int)((sqrt(8.0 * (double)idx + 1.0) - 1.0) * 0.5);
-            while ((long long)(r + 1) * (r + 2) / 2 <= idx) r++;
-            while ((long long)r * (r + 1) / 2 > idx) r--;
-            const int cc = (int)(idx - (long long)r * (r + 1) / 2);
-            const double *Lr = s_panel + (t0 + r) * CB;
-            const double *Lc = s_panel + (t0 + cc) * CB;
-            double sum = 0.0;
-            for (int k = 0; k < nb; k++) sum += Lr[k] * Lc[k];
-            A[(size_t)(k0 + t0 + r) * n + k0 + t0 + cc] -= sum;
+        __syncthreads();
+        for (int row = k0 + nb + tid; row < n; row += 1024) {
+            double v = 0.0;
+            for (int c = 0; c < nb; c++) v += A[(size_t)row * n + k0 + c] * s_blk[c];
+            s_x[row] -= v;
         }
         __syncthreads();
     }
-    // forward substitution L y = b, back substitution L^T x = y (column-oriented, one column per step)
-    double *y = D.x;  // reuse x[0..n) for y then x
-    for (int i = tid; i < n; i += CT) y[i] = D.bs[i];
-    __syncthreads();
-    for (int c = 0; c < n; c++) {
-        if (tid == 0) y[c] /= A[(size_t)c * n + c];
+    const int nblk = (n + CB - 1) / CB;
+    for (int bi = nblk - 1; bi >= 0; bi--) {
+        const int k0 = bi * CB;
+        const int nb = min(CB, n - k0);
+        if (tid < 64) {
+            const int r = tid;
+            double xv = (r < nb) ? s_x[k0 + r] : 0.0;
+            for (int c = nb - 1; c >= 0; c--) {
+                double xc = __shfl(xv, c);
+                xc /= A[(size_t)(k0 + c) * n + k0 + c];
+                if (r == c) xv = xc;
+                if (r < c) xv -= A[(size_t)(k0 + c) * n + k0 + r] * xc;  // L^T[r][c] = L[c][r]
+            }
+            if (r < nb) {
+                s_x[k0 + r] = xv;
+                s_blk[r] = xv;
+            }
+        }
         __syncthreads();
-        const double yc = y[c];
-        for (int r = c + 1 + tid; r < n; r += CT) y[r] -= A[(size_t)r * n + c] * yc;
+        for (int row = tid; row < k0; row += 1024) {
+            double v = 0.0;
+            for (int c = 0; c < nb; c++) v += A[(size_t)(k0 + c) * n + row] * s_blk[c];
+            s_x[row] -= v;
+        }
         __syncthreads();
     }
-    for (int c = n - 1; c >= 0; c--) {
-        if (tid == 0) y[c] /= A[(size_t)c * n + c];
-        __syncthreads();
-        const double yc = y[c];
-        for (int r = tid; r < c; r += CT) y[r] -= A[(size_t)c * n + r] * yc;
-        __syncthreads();
-    }
-    if (tid == 0) D.flag[0] = s_ok;
+    for (int i = tid; i < n; i += 1024) D.x[i] = s_x[i];
 }
 
 // landmark back-substitution + new estimates + LM scale partials
@@ -664,7 +759,7 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
         carve<double>(z, st_bytes, 3 * (size_t)npt);     // point A
         carve<double>(z, st_bytes, 3 * (size_t)npt);     // point B
         carve<double>(z, st_bytes, 3 * (size_t)ne);      // err
-        carve<double>(z, st_bytes, 32 * (size_t)ne);     // J
+        carve<double>(z, st_bytes, EC * (size_t)ne);     // per-edge contributions
         carve<double>(z, st_bytes, 9 * (size_t)nhl);     // Hll
         carve<double>(z, st_bytes, 3 * (size_t)nhl);     // bl
         carve<double>(z, st_bytes, 18 * (size_t)nblk);   // Hpl
@@ -720,7 +815,7 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
     D.pair_start = osg_dptr<int32_t>(din, o_pairs);
     D.pair_ab = osg_dptr<int32_t>(din, o_pairab);
     D.err = carve<double>(dst, off, 3 * (size_t)ne);
-    D.J = carve<double>(dst, off, 32 * (size_t)ne);
+    D.J = carve<double>(dst, off, EC * (size_t)ne);
     D.Hll = carve<double>(dst, off, 9 * (size_t)nhl);
     D.bl = carve<double>(dst, off, 3 * (size_t)nhl);
     D.Hpl = carve<double>(dst, off, 18 * (size_t)nblk);
@@ -780,7 +875,7 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
             currentChi = sum_part(0, ge);
         }
         const double iniChi = currentChi;
-        hipLaunchKernelGGL(k_jacobians, dim3(ge), dim3(EB), 0, ctx->stream, D);
+        hipLaunchKernelGGL(k_linearize, dim3(ge), dim3(EB), 0, ctx->stream, D);
         hipLaunchKernelGGL(k_point_red, dim3(std::max(gl, 1)), dim3(EB), 0, ctx->stream, D);
         if (nhp > 0) hipLaunchKernelGGL(k_pose_red, dim3(nhp), dim3(EB), 0, ctx->stream, D, 2 * NPART + gl);
         OSG_HIP_CHECK(ctx, hipGetLastError());
@@ -802,7 +897,13 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
             hipLaunchKernelGGL(k_schur_point, dim3(std::max(gl, 1)), dim3(EB), 0, ctx->stream, D, lambda);
             if (nhp > 0) {
                 hipLaunchKernelGGL(k_schur_pairs, dim3((npairs * 64 + 255) / 256), dim3(256), 0, ctx->stream, D, lambda);
-                hipLaunchKernelGGL(k_chol, dim3(1), dim3(CT), 0, ctx->stream, D);
+                const int nred = 6 * nhp;
+                for (int k0 = 0; k0 < nred; k0 += CB) {
+                    hipLaunchKernelGGL(k_chol_panel, dim3(1), dim3(256), 0, ctx->stream, D, k0);
+                    const int t = (nred - k0 - CB + CB - 1) / CB;
+                    if (t > 0) hipLaunchKernelGGL(k_chol_syrk, dim3(t * (t + 1) / 2), dim3(256), 0, ctx->stream, D, k0);
+                }
+                hipLaunchKernelGGL(k_chol_solve, dim3(1), dim3(1024), 0, ctx->stream, D);
             }
             D.pose_new = new_pose;
             D.point_new = new_point;
