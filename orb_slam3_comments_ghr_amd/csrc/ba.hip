@@ -26,6 +26,8 @@
 // the reference; push/pop is a swap of the current / trial estimate buffers.
 #include <algorithm>
 #include <cfloat>
+#include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <vector>
 
@@ -62,6 +64,10 @@ struct LbaDev {
     const int32_t *hp_b_start, *hp_b;    // blocks per hessian pose
     const int32_t *pair_start;           // dense (i <= j) pairs
     const int32_t *pair_ab;              // 2 ints per contribution
+    int nchunks;
+    const int32_t *chunk_start;          // contribution range of each chunk (chunks never span pairs)
+    const int32_t *pair_chunk;           // per pair: first chunk (npairs + 1)
+    double *chunk_part;                  // 36 per chunk
     // state
     const double *pose_cur, *point_cur;
     double *pose_new, *point_new;
@@ -292,11 +298,53 @@ __global__ __launch_bounds__(EB) void k_schur_point(LbaDev D, double lambda)
     }
 }
 
-// One wave per pose pair (i <= j).  Lane (r, c) < 36 owns S_ij[r][c] and runs over the pair's
-// contributions in landmark order — the order of g2o's Schur loop (ref:Thirdparty/g2o/g2o/core/
-// block_solver.hpp:381-432) — so the sum is deterministic and needs no cross-lane reduction:
-//   S[r][c] = sum_q  BDinv_a[r][:] . Hpl_b[c][:]
-// Writes Hs = Hpp + lambda I - S (both triangles) and b_schur.
+// Schur accumulation S_ij = sum_p BDinv_ip Hpl_jp^T over the (block_i, block_j) contributions of
+// every pose pair (i <= j), in landmark order — the order of g2o's Schur loop
+// (ref:Thirdparty/g2o/g2o/core/block_solver.hpp:381-432).  Diagonal pairs carry ~10x the
+// contributions of off-diagonal ones, so the lists are cut into chunks of <= SCH contributions:
+//   k_schur_chunks  one wave per chunk, lane (r, c) < 36 owns S[r][c] (no cross-lane reduction),
+//                   8 contributions' loads in flight per step -> chunk partial;
+//   k_schur_pairs   one wave per pair: sums its chunk partials in chunk order (deterministic),
+//                   writes Hs = Hpp + lambda I - S (both triangles) and b_schur.
+constexpr int SCH = 32;
+__global__ __launch_bounds__(256) void k_schur_chunks(LbaDev D)
+{
+    const int ch = (blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (ch >= D.nchunks) return;
+    const int r = (lane < 36) ? lane / 6 : 0, c = (lane < 36) ? lane % 6 : 0;
+    const double *__restrict__ BDv = D.BDinv;
+    const double *__restrict__ Hv = D.Hpl;
+    const int *__restrict__ ab = D.pair_ab;
+    const int q0 = D.chunk_start[ch], q1 = D.chunk_start[ch + 1];
+    double acc = 0.0;
+    int q = q0;
+    for (; q + 7 < q1; q += 8) {
+        int a[8], b[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            a[u] = ab[2 * (q + u)];
+            b[u] = ab[2 * (q + u) + 1];
+        }
+        double t[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const double *BD = BDv + 18 * (size_t)a[u] + 3 * r;
+            const double *Bj = Hv + 18 * (size_t)b[u] + 3 * c;
+            t[u] = BD[0] * Bj[0] + BD[1] * Bj[1] + BD[2] * Bj[2];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) acc += t[u];
+    }
+    for (; q < q1; q++) {
+        const int a = ab[2 * q], b = ab[2 * q + 1];
+        const double *BD = BDv + 18 * (size_t)a + 3 * r;
+        const double *Bj = Hv + 18 * (size_t)b + 3 * c;
+        acc += BD[0] * Bj[0] + BD[1] * Bj[1] + BD[2] * Bj[2];
+    }
+    if (lane < 36) D.chunk_part[36 * (size_t)ch + lane] = acc;
+}
+
 __global__ __launch_bounds__(256) void k_schur_pairs(LbaDev D, double lambda)
 {
     const int wave = (blockIdx.x * 256 + threadIdx.x) >> 6;
@@ -310,32 +358,10 @@ __global__ __launch_bounds__(256) void k_schur_pairs(LbaDev D, double lambda)
     const int j = i + rem;
     if (wave == 0 && lane == 0) D.flag[0] = 1;  // the Cholesky of this trial clears it on failure
     const int n = 6 * D.nhp;
-    const int r = lane / 6, c = lane % 6;
-    const bool act = lane < 36;
-    double acc = 0.0;
-    const int q0 = D.pair_start[wave], q1 = D.pair_start[wave + 1];
-    int q = q0;
-    for (; q + 3 < q1; q += 4) {
-        double t[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int a = D.pair_ab[2 * (q + u)], b = D.pair_ab[2 * (q + u) + 1];
-            const double *BD = D.BDinv + 18 * (size_t)a + 3 * r;
-            const double *Bj = D.Hpl + 18 * (size_t)b + 3 * c;
-            t[u] = act ? (BD[0] * Bj[0] + BD[1] * Bj[1] + BD[2] * Bj[2]) : 0.0;
-        }
-        acc += t[0];
-        acc += t[1];
-        acc += t[2];
-        acc += t[3];
-    }
-    for (; q < q1; q++) {
-        const int a = D.pair_ab[2 * q], b = D.pair_ab[2 * q + 1];
-        const double *BD = D.BDinv + 18 * (size_t)a + 3 * r;
-        const double *Bj = D.Hpl + 18 * (size_t)b + 3 * c;
-        if (act) acc += BD[0] * Bj[0] + BD[1] * Bj[1] + BD[2] * Bj[2];
-    }
-    if (act) {
+    if (lane < 36) {
+        const int r = lane / 6, c = lane % 6;
+        double acc = 0.0;
+        for (int ch = D.pair_chunk[wave]; ch < D.pair_chunk[wave + 1]; ch++) acc += D.chunk_part[36 * (size_t)ch + lane];
         double v = -acc;
         if (i == j) {
             v += D.Hpp[36 * (size_t)i + lane];
@@ -349,6 +375,14 @@ __global__ __launch_bounds__(256) void k_schur_pairs(LbaDev D, double lambda)
         for (int qq = D.hp_b_start[i]; qq < D.hp_b_start[i + 1]; qq++) cs += D.coef[6 * (size_t)D.hp_b[qq] + lane];
         D.bs[6 * i + lane] = D.bp[6 * (size_t)i + lane] - cs;
     }
+}
+
+__device__ inline double readlane_d(double v, int lane)
+{  // wave-uniform lane index: two v_readlane_b32 instead of a ds_bpermute round trip
+    const unsigned long long u = __double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, lane);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), lane);
+    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -381,7 +415,7 @@ __global__ __launch_bounds__(256) void k_chol_panel(LbaDev D, int k0)
 #pragma unroll
         for (int c = 0; c < CB; c++) {
             if (c < nb) {
-                const double d = __shfl(a[c], c);
+                const double d = readlane_d(a[c], c);
                 ok &= d > 0.0;
                 const double piv = sqrt(fmax(d, 1e-300));
                 if (r == c) a[c] = piv;
@@ -389,7 +423,7 @@ __global__ __launch_bounds__(256) void k_chol_panel(LbaDev D, int k0)
                 const double lrc = a[c];
 #pragma unroll
                 for (int cc = c + 1; cc < CB; cc++) {
-                    const double lcc = __shfl(a[c], cc);  // L[cc][c]
+                    const double lcc = readlane_d(a[c], cc);  // L[cc][c]
                     if (cc < nb && r >= cc) a[cc] -= lrc * lcc;
                 }
             }
@@ -475,11 +509,19 @@ __global__ __launch_bounds__(1024) void k_chol_solve(LbaDev D)
         if (tid < 64) {
             const int r = tid;
             double xv = (r < nb) ? s_x[k0 + r] : 0.0;
-            for (int c = 0; c < nb; c++) {
-                double xc = __shfl(xv, c);
-                xc /= A[(size_t)(k0 + c) * n + k0 + c];
-                if (r == c) xv = xc;
-                if (r > c && r < nb) xv -= A[(size_t)(k0 + r) * n + k0 + c] * xc;
+            double Lr[CB], dg[CB];
+#pragma unroll
+            for (int c = 0; c < CB; c++) {
+                Lr[c] = (r < nb && c < nb) ? A[(size_t)(k0 + r) * n + k0 + c] : 0.0;  // row r of the block
+                dg[c] = (c < nb) ? A[(size_t)(k0 + c) * n + k0 + c] : 1.0;
+            }
+#pragma unroll
+            for (int c = 0; c < CB; c++) {
+                if (c < nb) {
+                    const double xc = readlane_d(xv, c) / dg[c];
+                    if (r == c) xv = xc;
+                    if (r > c) xv -= Lr[c] * xc;
+                }
             }
             if (r < nb) {
                 s_x[k0 + r] = xv;
@@ -501,11 +543,19 @@ __global__ __launch_bounds__(1024) void k_chol_solve(LbaDev D)
         if (tid < 64) {
             const int r = tid;
             double xv = (r < nb) ? s_x[k0 + r] : 0.0;
-            for (int c = nb - 1; c >= 0; c--) {
-                double xc = __shfl(xv, c);
-                xc /= A[(size_t)(k0 + c) * n + k0 + c];
-                if (r == c) xv = xc;
-                if (r < c) xv -= A[(size_t)(k0 + c) * n + k0 + r] * xc;  // L^T[r][c] = L[c][r]
+            double Lc[CB], dg[CB];
+#pragma unroll
+            for (int c = 0; c < CB; c++) {
+                Lc[c] = (r < nb && c < nb) ? A[(size_t)(k0 + c) * n + k0 + r] : 0.0;  // L[c][r] = L^T[r][c]
+                dg[c] = (c < nb) ? A[(size_t)(k0 + c) * n + k0 + c] : 1.0;
+            }
+#pragma unroll
+            for (int c = CB - 1; c >= 0; c--) {
+                if (c < nb) {
+                    const double xc = readlane_d(xv, c) / dg[c];
+                    if (r == c) xv = xc;
+                    if (r < c) xv -= Lc[c] * xc;
+                }
             }
             if (r < nb) {
                 s_x[k0 + r] = xv;
@@ -624,6 +674,11 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
             return osg_set_error(ctx, OSG_E_INVALID, "edge %d references out of range", e);
     }
     // ---------------------------------------------------------------- structure (host)
+    static const bool prof = getenv("OSG_LBA_PROFILE") && atoi(getenv("OSG_LBA_PROFILE"));
+    const auto tp0 = std::chrono::steady_clock::now();
+    auto ms_since = [&](std::chrono::steady_clock::time_point t) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+    };
     std::vector<int32_t> pose_cnt(np, 0), point_cnt(npt, 0);
     for (int e = 0; e < ne; e++) {
         pose_cnt[G->e_pose[e]]++;
@@ -714,6 +769,16 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
                     pair_ab[2 * k + 1] = b;
                 }
     }
+    const double t_struct = ms_since(tp0);
+    // chunks of <= SCH contributions, never spanning two pairs
+    std::vector<int32_t> chunk_start, pair_chunk(npairs + 1, 0);
+    for (int k = 0; k < npairs; k++) {
+        pair_chunk[k] = (int)chunk_start.size();
+        for (int q = pair_start[k]; q < pair_start[k + 1]; q += SCH) chunk_start.push_back(q);
+    }
+    pair_chunk[npairs] = (int)chunk_start.size();
+    const int nchunks = (int)chunk_start.size();
+    chunk_start.push_back(pair_start[npairs]);
     // ---------------------------------------------------------------- device layout
     osg_packer pk;
     const size_t o_fixed = pk.add(G->pose_fixed, np);
@@ -739,6 +804,8 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
     const size_t o_hpb = pk.add(hp_b.data(), 4 * (size_t)nblk);
     const size_t o_pairs = pk.add(pair_start.data(), 4 * (size_t)(npairs + 1));
     const size_t o_pairab = pk.add(pair_ab.data(), 4 * pair_ab.size());
+    const size_t o_chs = pk.add(chunk_start.data(), 4 * chunk_start.size());
+    const size_t o_pch = pk.add(pair_chunk.data(), 4 * pair_chunk.size());
     const size_t o_pose0 = pk.add(G->pose, 56 * (size_t)np);
     const size_t o_point0 = pk.add(G->point, 24 * (size_t)npt);
     char *pin = (char *)osg_pinned(ctx, pk.total + 4096 + sizeof(double) * (3 * NPART + 64));
@@ -772,6 +839,7 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
         carve<double>(z, st_bytes, (size_t)sp);          // bs
         carve<double>(z, st_bytes, (size_t)sp + 3 * (size_t)nhl);  // x
         carve<double>(z, st_bytes, 3 * (size_t)NPART + 64);        // partials
+        carve<double>(z, st_bytes, 36 * (size_t)std::max(nchunks, 1));  // chunk partials
         carve<int>(z, st_bytes, 16);                                // flags
         carve<uint8_t>(z, st_bytes, ne);                            // edge_bad
         st_bytes += 256;
@@ -828,6 +896,10 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
     D.bs = carve<double>(dst, off, (size_t)sp);
     D.x = carve<double>(dst, off, (size_t)sp + 3 * (size_t)nhl);
     D.part = carve<double>(dst, off, 3 * (size_t)NPART + 64);
+    D.chunk_part = carve<double>(dst, off, 36 * (size_t)std::max(nchunks, 1));
+    D.nchunks = nchunks;
+    D.chunk_start = osg_dptr<int32_t>(din, o_chs);
+    D.pair_chunk = osg_dptr<int32_t>(din, o_pch);
     D.flag = carve<int>(dst, off, 16);
     uint8_t *d_bad = carve<uint8_t>(dst, off, ne);
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(poseA, din + o_pose0, 56 * (size_t)np, hipMemcpyDeviceToDevice, ctx->stream));
@@ -856,6 +928,8 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
         return s;
     };
 
+    const double t_upload = ms_since(tp0) - t_struct;
+    const auto tp1 = std::chrono::steady_clock::now();
     // initial chi2 (activeRobustChi2 before optimising)
     D.pose_cur = cur_pose;
     D.point_cur = cur_point;
@@ -896,6 +970,8 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
             trials++;
             hipLaunchKernelGGL(k_schur_point, dim3(std::max(gl, 1)), dim3(EB), 0, ctx->stream, D, lambda);
             if (nhp > 0) {
+                if (nchunks > 0)
+                    hipLaunchKernelGGL(k_schur_chunks, dim3((nchunks * 64 + 255) / 256), dim3(256), 0, ctx->stream, D);
                 hipLaunchKernelGGL(k_schur_pairs, dim3((npairs * 64 + 255) / 256), dim3(256), 0, ctx->stream, D, lambda);
                 const int nred = 6 * nhp;
                 for (int k0 = 0; k0 < nred; k0 += CB) {
@@ -945,6 +1021,9 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
             if (nBad >= 3) ok = false;
         }
     }
+    if (prof)
+        fprintf(stderr, "[osg lba] structure %.3f ms, pack+upload %.3f ms, LM %.3f ms (%d it, %d trials), pairs %d contrib %d\n",
+                t_struct, t_upload, ms_since(tp1), iters, trials, npairs, pair_start[npairs]);
     R->iterations = iters;
     R->trials = trials;
     R->aborted = (stop && *stop) ? 1 : 0;
