@@ -60,6 +60,8 @@ struct LbaDev {
     const int32_t *lm_b_start;           // blocks per landmark (blocks are numbered landmark-major)
     const int32_t *blk_pose;             // per block: hessian pose index
     const int32_t *edge_blk;             // per edge: block or -1
+    const int32_t *blk_lm;               // per block: landmark
+    const int32_t *blk_e_start, *blk_e;  // edges per block (edge order)
     const int32_t *hp_e_start, *hp_e;    // edges per hessian pose
     const int32_t *hp_b_start, *hp_b;    // blocks per hessian pose
     const int32_t *pair_start;           // dense (i <= j) pairs
@@ -74,7 +76,7 @@ struct LbaDev {
     double *err;                         // 3 per edge
     double *J;                           // EC per edge: quadratic-form contributions
     double *Hll, *bl, *Hpl, *Hpp, *bp;
-    double *Dinv, *BDinv, *coef;
+    double *Dinv, *db, *BDinv, *coef;
     double *Hs, *bs, *x;
     double *part;                        // [0..NPART): chi partials, [NPART..2NPART): scale, [2NPART..]: max diag
     int *flag;                           // [0] cholesky ok
@@ -171,7 +173,22 @@ __global__ __launch_bounds__(EB) void k_linearize(LbaDev D)
             o[c++] = Jp[0][a] * ww * Jx[0][bb] + Jp[1][a] * ww * Jx[1][bb] + Jp[2][a] * ww * Jx[2][bb];
 }
 
-// per landmark: Hll (3x3), b_l and the Hpl blocks of its edges (sums of edge contributions)
+// per block: Hpl = sum of its edges' contributions (usually one edge; mono + body of one
+// keyframe share a block)
+__global__ __launch_bounds__(EB) void k_block_red(LbaDev D)
+{
+    const int blk = blockIdx.x * EB + threadIdx.x;
+    if (blk >= D.nblk) return;
+    double h[18];
+    for (int i = 0; i < 18; i++) h[i] = 0.0;
+    for (int q = D.blk_e_start[blk]; q < D.blk_e_start[blk + 1]; q++) {
+        const double *C = D.J + EC * (size_t)D.blk_e[q];
+        for (int i = 0; i < 18; i++) h[i] += C[36 + i];
+    }
+    for (int i = 0; i < 18; i++) D.Hpl[18 * (size_t)blk + i] = h[i];
+}
+
+// per landmark: Hll (3x3) and b_l (sums of edge contributions)
 __global__ __launch_bounds__(EB) void k_point_red(LbaDev D)
 {
     __shared__ double s[EB / 64];
@@ -179,27 +196,12 @@ __global__ __launch_bounds__(EB) void k_point_red(LbaDev D)
     double md = 0.0;
     if (l < D.nhl) {
         double H6[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
-        int last_blk = -1;
         for (int q = D.lm_e_start[l]; q < D.lm_e_start[l + 1]; q++) {
             const int e = D.lm_e[q];
             const double *C = D.J + EC * (size_t)e;
             for (int i = 0; i < 6; i++) H6[i] += C[27 + i];
             for (int i = 0; i < 3; i++) b[i] += C[33 + i];
-            const int blk = D.edge_blk[e];
-            if (blk >= 0) {
-                double *Hb = D.Hpl + 18 * (size_t)blk;
-                // blocks of one landmark are distinct per pose; parallel edges (mono + body of one
-                // keyframe) share a block and are summed in edge order
-                bool seen = false;
-                for (int q2 = D.lm_e_start[l]; q2 < q; q2++) seen |= (D.edge_blk[D.lm_e[q2]] == blk);
-                if (!seen)
-                    for (int i = 0; i < 18; i++) Hb[i] = C[36 + i];
-                else
-                    for (int i = 0; i < 18; i++) Hb[i] += C[36 + i];
-                last_blk = blk;
-            }
         }
-        (void)last_blk;
         const double H[9] = {H6[0], H6[1], H6[2], H6[1], H6[3], H6[4], H6[2], H6[4], H6[5]};
         for (int i = 0; i < 9; i++) D.Hll[9 * (size_t)l + i] = H[i];
         for (int i = 0; i < 3; i++) D.bl[3 * (size_t)l + i] = b[i];
@@ -285,16 +287,24 @@ __global__ __launch_bounds__(EB) void k_schur_point(LbaDev D, double lambda)
     inv3(Dm, Di);
     for (int i = 0; i < 9; i++) D.Dinv[9 * (size_t)l + i] = Di[i];
     const double *b = D.bl + 3 * (size_t)l;
-    double db[3];
-    for (int r = 0; r < 3; r++) db[r] = Di[3 * r] * b[0] + Di[3 * r + 1] * b[1] + Di[3 * r + 2] * b[2];
-    for (int blk = D.lm_b_start[l]; blk < D.lm_b_start[l + 1]; blk++) {
-        const double *B = D.Hpl + 18 * (size_t)blk;
-        double *BD = D.BDinv + 18 * (size_t)blk;
-        double *cf = D.coef + 6 * (size_t)blk;
-        for (int r = 0; r < 6; r++) {
-            for (int c = 0; c < 3; c++) BD[3 * r + c] = B[3 * r] * Di[c] + B[3 * r + 1] * Di[3 + c] + B[3 * r + 2] * Di[6 + c];
-            cf[r] = B[3 * r] * db[0] + B[3 * r + 1] * db[1] + B[3 * r + 2] * db[2];
-        }
+    for (int r = 0; r < 3; r++) D.db[3 * (size_t)l + r] = Di[3 * r] * b[0] + Di[3 * r + 1] * b[1] + Di[3 * r + 2] * b[2];
+}
+
+// per block: BDinv = Hpl Dinv, coef = Hpl Dinv b_l
+__global__ __launch_bounds__(EB) void k_schur_block(LbaDev D)
+{
+    const int blk = blockIdx.x * EB + threadIdx.x;
+    if (blk >= D.nblk) return;
+    const int l = D.blk_lm[blk];
+    double Di[9], db[3], B[18];
+    for (int i = 0; i < 9; i++) Di[i] = D.Dinv[9 * (size_t)l + i];
+    for (int i = 0; i < 3; i++) db[i] = D.db[3 * (size_t)l + i];
+    for (int i = 0; i < 18; i++) B[i] = D.Hpl[18 * (size_t)blk + i];
+    double *BD = D.BDinv + 18 * (size_t)blk;
+    double *cf = D.coef + 6 * (size_t)blk;
+    for (int r = 0; r < 6; r++) {
+        for (int c = 0; c < 3; c++) BD[3 * r + c] = B[3 * r] * Di[c] + B[3 * r + 1] * Di[3 + c] + B[3 * r + 2] * Di[6 + c];
+        cf[r] = B[3 * r] * db[0] + B[3 * r + 1] * db[1] + B[3 * r + 2] * db[2];
     }
 }
 
@@ -370,10 +380,26 @@ __global__ __launch_bounds__(256) void k_schur_pairs(LbaDev D, double lambda)
         D.Hs[(size_t)(6 * i + r) * n + 6 * j + c] = v;
         if (i != j) D.Hs[(size_t)(6 * j + c) * n + 6 * i + r] = v;
     }
-    if (i == j && lane < 6) {
-        double cs = 0.0;
-        for (int qq = D.hp_b_start[i]; qq < D.hp_b_start[i + 1]; qq++) cs += D.coef[6 * (size_t)D.hp_b[qq] + lane];
-        D.bs[6 * i + lane] = D.bp[6 * (size_t)i + lane] - cs;
+}
+
+// b_schur_i = b_p,i - sum over pose i's blocks of Hpl Dinv b_l: one workgroup per pose
+__global__ __launch_bounds__(256) void k_bschur(LbaDev D)
+{
+    __shared__ double s[4][6];
+    const int i = blockIdx.x;
+    double acc[6] = {0, 0, 0, 0, 0, 0};
+    for (int q = D.hp_b_start[i] + threadIdx.x; q < D.hp_b_start[i + 1]; q += 256) {
+        const double *cf = D.coef + 6 * (size_t)D.hp_b[q];
+        for (int k = 0; k < 6; k++) acc[k] += cf[k];
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int k = 0; k < 6; k++) acc[k] = wave_sum(acc[k]);
+    if (lane == 0)
+        for (int k = 0; k < 6; k++) s[w][k] = acc[k];
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const int k = threadIdx.x;
+        D.bs[6 * i + k] = D.bp[6 * (size_t)i + k] - (((s[0][k] + s[1][k]) + s[2][k]) + s[3][k]);
     }
 }
 
@@ -401,61 +427,55 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void k_chol_panel(LbaDev D, int k0)
 {
     __shared__ double s_d[CB][CB + 1];
+    __shared__ double s_x[256][CB + 1];
+    __shared__ int s_ok;
     const int n = 6 * D.nhp;
     double *A = D.Hs;
     const int nb = min(CB, n - k0);
     const int tid = threadIdx.x;
-    if (tid < 64) {
-        // wave 0: rows of the diagonal block in registers (lane = row)
-        double a[CB];
-        const int r = tid;
-#pragma unroll
-        for (int c = 0; c < CB; c++) a[c] = (r < nb && c <= r && c < nb) ? A[(size_t)(k0 + r) * n + k0 + c] : 0.0;
-        int ok = 1;
-#pragma unroll
-        for (int c = 0; c < CB; c++) {
-            if (c < nb) {
-                const double d = readlane_d(a[c], c);
-                ok &= d > 0.0;
-                const double piv = sqrt(fmax(d, 1e-300));
-                if (r == c) a[c] = piv;
-                else if (r > c) a[c] /= piv;
-                const double lrc = a[c];
-#pragma unroll
-                for (int cc = c + 1; cc < CB; cc++) {
-                    const double lcc = readlane_d(a[c], cc);  // L[cc][c]
-                    if (cc < nb && r >= cc) a[cc] -= lrc * lcc;
-                }
-            }
+    for (int idx = tid; idx < CB * CB; idx += 256) {
+        const int r = idx / CB, c = idx % CB;
+        s_d[r][c] = (r < nb && c < nb && c <= r) ? A[(size_t)(k0 + r) * n + k0 + c] : 0.0;
+    }
+    if (tid == 0) s_ok = 1;
+    __syncthreads();
+    // right-looking LL^T of the diagonal block, one barrier per column: the update of columns > c
+    // uses the unscaled column c (L_rc L_kc = A_rc A_kc / d); column c is scaled afterwards, which
+    // no later column step reads.
+    for (int c = 0; c < nb; c++) {
+        const double d = s_d[c][c];
+        const double inv_d = 1.0 / d;
+        for (int idx = tid; idx < CB * CB; idx += 256) {
+            const int r = idx / CB, k = idx % CB;
+            if (k > c && r >= k && r < nb) s_d[r][k] -= s_d[r][c] * s_d[k][c] * inv_d;
         }
-        if (r < CB)
-#pragma unroll
-            for (int c = 0; c < CB; c++) s_d[r][c] = a[c];
-        if (tid == 0 && !ok) D.flag[0] = 0;
-        if (r < nb)
-#pragma unroll
-            for (int c = 0; c < CB; c++)
-                if (c <= r && c < nb) A[(size_t)(k0 + r) * n + k0 + c] = a[c];
+        __syncthreads();
+        const double piv = sqrt(fmax(d, 1e-300));
+        if (tid == 0 && !(d > 0.0)) s_ok = 0;
+        for (int r = c + tid; r < nb; r += 256) s_d[r][c] = (r == c) ? piv : s_d[r][c] / piv;
     }
     __syncthreads();
-    // rows below the diagonal block: L[row][0:nb] = A[row][0:nb] L_kk^-T (forward substitution)
-    for (int row = k0 + nb + tid; row < n; row += 256) {
-        double x[CB];
-        double *Ar = A + (size_t)row * n + k0;
-#pragma unroll
-        for (int c = 0; c < CB; c++) x[c] = (c < nb) ? Ar[c] : 0.0;
-#pragma unroll
-        for (int c = 0; c < CB; c++) {
-            if (c < nb) {
-                double v = x[c];
-#pragma unroll
-                for (int k = 0; k < c; k++) v -= x[k] * s_d[c][k];
-                x[c] = v / s_d[c][c];
+    if (tid == 0 && !s_ok) D.flag[0] = 0;
+    for (int idx = tid; idx < nb * nb; idx += 256) {
+        const int r = idx / nb, c = idx % nb;
+        if (c <= r) A[(size_t)(k0 + r) * n + k0 + c] = s_d[r][c];
+    }
+    // rows below the diagonal block: L[row][0:nb] = A[row][0:nb] L_kk^-T (forward substitution);
+    // each thread keeps its row in LDS (no register array, no spills)
+    for (int row0 = k0 + nb; row0 < n; row0 += 256) {
+        const int row = row0 + tid;
+        double *xr = s_x[tid];
+        if (row < n) {
+            const double *Ar = A + (size_t)row * n + k0;
+            for (int c = 0; c < nb; c++) xr[c] = Ar[c];
+            for (int c = 0; c < nb; c++) {
+                double v = xr[c];
+                for (int k = 0; k < c; k++) v -= xr[k] * s_d[c][k];
+                xr[c] = v / s_d[c][c];
             }
+            double *Aw = A + (size_t)row * n + k0;
+            for (int c = 0; c < nb; c++) Aw[c] = xr[c];
         }
-#pragma unroll
-        for (int c = 0; c < CB; c++)
-            if (c < nb) Ar[c] = x[c];
     }
 }
 
@@ -733,6 +753,18 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
         }
     }
     const int nblk = (int)blk_pose.size();
+    std::vector<int32_t> blk_lm(nblk), blk_e_start(nblk + 1, 0), blk_e;
+    for (int l = 0; l < nhl; l++)
+        for (int b = lm_b_start[l]; b < lm_b_start[l + 1]; b++) blk_lm[b] = l;
+    for (int e = 0; e < ne; e++)
+        if (edge_blk[e] >= 0) blk_e_start[edge_blk[e] + 1]++;
+    for (int b = 0; b < nblk; b++) blk_e_start[b + 1] += blk_e_start[b];
+    blk_e.resize(blk_e_start[nblk]);
+    {
+        std::vector<int32_t> fill(blk_e_start.begin(), blk_e_start.end() - 1);
+        for (int e = 0; e < ne; e++)
+            if (edge_blk[e] >= 0) blk_e[fill[edge_blk[e]]++] = e;
+    }
     // edges / blocks per hessian pose
     std::vector<int32_t> hp_e_start(nhp + 1, 0), hp_e, hp_b_start(nhp + 1, 0), hp_b(nblk);
     for (int e = 0; e < ne; e++)
@@ -805,6 +837,9 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
     const size_t o_pairs = pk.add(pair_start.data(), 4 * (size_t)(npairs + 1));
     const size_t o_pairab = pk.add(pair_ab.data(), 4 * pair_ab.size());
     const size_t o_chs = pk.add(chunk_start.data(), 4 * chunk_start.size());
+    const size_t o_blklm = pk.add(blk_lm.data(), 4 * (size_t)nblk);
+    const size_t o_blkes = pk.add(blk_e_start.data(), 4 * (size_t)(nblk + 1));
+    const size_t o_blke = pk.add(blk_e.data(), 4 * blk_e.size());
     const size_t o_pch = pk.add(pair_chunk.data(), 4 * pair_chunk.size());
     const size_t o_pose0 = pk.add(G->pose, 56 * (size_t)np);
     const size_t o_point0 = pk.add(G->point, 24 * (size_t)npt);
@@ -840,6 +875,7 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
         carve<double>(z, st_bytes, (size_t)sp + 3 * (size_t)nhl);  // x
         carve<double>(z, st_bytes, 3 * (size_t)NPART + 64);        // partials
         carve<double>(z, st_bytes, 36 * (size_t)std::max(nchunks, 1));  // chunk partials
+        carve<double>(z, st_bytes, 3 * (size_t)nhl);                     // db
         carve<int>(z, st_bytes, 16);                                // flags
         carve<uint8_t>(z, st_bytes, ne);                            // edge_bad
         st_bytes += 256;
@@ -899,6 +935,10 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
     D.chunk_part = carve<double>(dst, off, 36 * (size_t)std::max(nchunks, 1));
     D.nchunks = nchunks;
     D.chunk_start = osg_dptr<int32_t>(din, o_chs);
+    D.blk_lm = osg_dptr<int32_t>(din, o_blklm);
+    D.blk_e_start = osg_dptr<int32_t>(din, o_blkes);
+    D.blk_e = osg_dptr<int32_t>(din, o_blke);
+    D.db = carve<double>(dst, off, 3 * (size_t)nhl);
     D.pair_chunk = osg_dptr<int32_t>(din, o_pch);
     D.flag = carve<int>(dst, off, 16);
     uint8_t *d_bad = carve<uint8_t>(dst, off, ne);
@@ -951,6 +991,7 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
         const double iniChi = currentChi;
         hipLaunchKernelGGL(k_linearize, dim3(ge), dim3(EB), 0, ctx->stream, D);
         hipLaunchKernelGGL(k_point_red, dim3(std::max(gl, 1)), dim3(EB), 0, ctx->stream, D);
+        if (nblk > 0) hipLaunchKernelGGL(k_block_red, dim3((nblk + EB - 1) / EB), dim3(EB), 0, ctx->stream, D);
         if (nhp > 0) hipLaunchKernelGGL(k_pose_red, dim3(nhp), dim3(EB), 0, ctx->stream, D, 2 * NPART + gl);
         OSG_HIP_CHECK(ctx, hipGetLastError());
         if (it == 0) {
@@ -969,10 +1010,12 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
         do {
             trials++;
             hipLaunchKernelGGL(k_schur_point, dim3(std::max(gl, 1)), dim3(EB), 0, ctx->stream, D, lambda);
+            if (nblk > 0) hipLaunchKernelGGL(k_schur_block, dim3((nblk + EB - 1) / EB), dim3(EB), 0, ctx->stream, D);
             if (nhp > 0) {
                 if (nchunks > 0)
                     hipLaunchKernelGGL(k_schur_chunks, dim3((nchunks * 64 + 255) / 256), dim3(256), 0, ctx->stream, D);
                 hipLaunchKernelGGL(k_schur_pairs, dim3((npairs * 64 + 255) / 256), dim3(256), 0, ctx->stream, D, lambda);
+                hipLaunchKernelGGL(k_bschur, dim3(nhp), dim3(256), 0, ctx->stream, D);
                 const int nred = 6 * nhp;
                 for (int k0 = 0; k0 < nred; k0 += CB) {
                     hipLaunchKernelGGL(k_chol_panel, dim3(1), dim3(256), 0, ctx->stream, D, k0);
