@@ -78,6 +78,7 @@ struct LbaDev {
     double *Hll, *bl, *Hpl, *Hpp, *bp;
     double *Dinv, *db, *BDinv, *coef;
     double *Hs, *bs, *x;
+    double *Lkk;                         // factored 32x32 diagonal blocks, row-major per block row
     double *part;                        // [0..NPART): chi partials, [NPART..2NPART): scale, [2NPART..]: max diag
     int *flag;                           // [0] cholesky ok
 };
@@ -413,9 +414,10 @@ __device__ inline double readlane_d(double v, int lane)
 
 // ---------------------------------------------------------------------------------------------
 // Reduced camera system: blocked right-looking Cholesky (LL^T, lower, in place in Hs) over
-// panels of CB = 32 columns, then blocked triangular solves.  Per panel:
-//   k_chol_panel  one workgroup: the 32x32 diagonal block factored by one wave with the rows in
-//                 registers (shuffles, no barriers), then the panel rows below solved against it;
+// panels of CB = 32 columns with the forward substitution fused, then a blocked backward solve.
+// Per panel:
+//   k_chol_panel  one wave per 32-row block: diagonal block factored in registers (readlane),
+//                 rows below solved against it, b updated;
 //   k_chol_syrk   trailing update A22 -= L21 L21^T on 32x32 lower tiles, one workgroup per tile,
 //                 one wave per 16x16 quadrant on FP64 MFMA (v_mfma_f64_16x16x4_f64, K = 32 as
 //                 8 MFMAs) — the only MFMA use on the path (the dense Schur GEMM).
@@ -424,58 +426,77 @@ constexpr int CB = 32;
 constexpr int CMAX = 384;  // max reduced dimension (64 free poses)
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(256) void k_chol_panel(LbaDev D, int k0)
+// Panel step k0, one 64-thread workgroup per 32-row block at or below the diagonal block.  Every
+// workgroup factors the 32x32 diagonal block itself (lane = row, registers, v_readlane
+// broadcasts, no barriers) and solves y_k = L_kk^-1 b_k; workgroup 0 stores L_kk and y_k,
+// workgroup t > 0 turns its 32 rows into L21 rows (x L_kk^T = a) and updates b for them
+// (b_row -= L_row . y_k).  Workgroup 0 writes L_kk to Lkk and y_k to x (forward substitution fused).
+__global__ __launch_bounds__(64) void k_chol_panel(LbaDev D, int k0)
 {
-    __shared__ double s_d[CB][CB + 1];
-    __shared__ double s_x[256][CB + 1];
-    __shared__ int s_ok;
     const int n = 6 * D.nhp;
     double *A = D.Hs;
+    double *bs = D.bs;
     const int nb = min(CB, n - k0);
-    const int tid = threadIdx.x;
-    for (int idx = tid; idx < CB * CB; idx += 256) {
-        const int r = idx / CB, c = idx % CB;
-        s_d[r][c] = (r < nb && c < nb && c <= r) ? A[(size_t)(k0 + r) * n + k0 + c] : 0.0;
-    }
-    if (tid == 0) s_ok = 1;
-    __syncthreads();
-    // right-looking LL^T of the diagonal block, one barrier per column: the update of columns > c
-    // uses the unscaled column c (L_rc L_kc = A_rc A_kc / d); column c is scaled afterwards, which
-    // no later column step reads.
-    for (int c = 0; c < nb; c++) {
-        const double d = s_d[c][c];
-        const double inv_d = 1.0 / d;
-        for (int idx = tid; idx < CB * CB; idx += 256) {
-            const int r = idx / CB, k = idx % CB;
-            if (k > c && r >= k && r < nb) s_d[r][k] -= s_d[r][c] * s_d[k][c] * inv_d;
-        }
-        __syncthreads();
-        const double piv = sqrt(fmax(d, 1e-300));
-        if (tid == 0 && !(d > 0.0)) s_ok = 0;
-        for (int r = c + tid; r < nb; r += 256) s_d[r][c] = (r == c) ? piv : s_d[r][c] / piv;
-    }
-    __syncthreads();
-    if (tid == 0 && !s_ok) D.flag[0] = 0;
-    for (int idx = tid; idx < nb * nb; idx += 256) {
-        const int r = idx / nb, c = idx % nb;
-        if (c <= r) A[(size_t)(k0 + r) * n + k0 + c] = s_d[r][c];
-    }
-    // rows below the diagonal block: L[row][0:nb] = A[row][0:nb] L_kk^-T (forward substitution);
-    // each thread keeps its row in LDS (no register array, no spills)
-    for (int row0 = k0 + nb; row0 < n; row0 += 256) {
-        const int row = row0 + tid;
-        double *xr = s_x[tid];
-        if (row < n) {
-            const double *Ar = A + (size_t)row * n + k0;
-            for (int c = 0; c < nb; c++) xr[c] = Ar[c];
-            for (int c = 0; c < nb; c++) {
-                double v = xr[c];
-                for (int k = 0; k < c; k++) v -= xr[k] * s_d[c][k];
-                xr[c] = v / s_d[c][c];
+    const int r = threadIdx.x;  // lane
+    double a[CB];
+#pragma unroll
+    for (int c = 0; c < CB; c++) a[c] = (r < nb && c < nb && c <= r) ? A[(size_t)(k0 + r) * n + k0 + c] : 0.0;
+    double yv = (r < nb) ? bs[k0 + r] : 0.0;
+    int ok = 1;
+#pragma unroll
+    for (int c = 0; c < CB; c++) {
+        if (c < nb) {
+            const double d = readlane_d(a[c], c);
+            ok &= d > 0.0;
+            const double piv = sqrt(fmax(d, 1e-300));
+            if (r == c) a[c] = piv;
+            else if (r > c) a[c] /= piv;
+            const double lrc = a[c];
+#pragma unroll
+            for (int cc = c + 1; cc < CB; cc++) {
+                const double lcc = readlane_d(a[c], cc);  // L[cc][c]
+                if (cc < nb && r >= cc) a[cc] -= lrc * lcc;
             }
-            double *Aw = A + (size_t)row * n + k0;
-            for (int c = 0; c < nb; c++) Aw[c] = xr[c];
+            // forward substitution of b inside the block
+            const double yc = readlane_d(yv, c) / piv;
+            if (r == c) yv = yc;
+            else if (r > c && r < nb) yv -= lrc * yc;
         }
+    }
+    if (blockIdx.x == 0) {
+        if (r == 0 && !ok) D.flag[0] = 0;
+        // the diagonal block of Hs and b_k stay untouched: the other workgroups of this launch read them
+        if (r < nb) {
+#pragma unroll
+            for (int c = 0; c < CB; c++) D.Lkk[(size_t)(k0 + r) * CB + c] = a[c];
+            D.x[k0 + r] = yv;
+        }
+        return;
+    }
+    // rows of block t: x L_kk^T = a_row  ->  x_c = (a_c - sum_{k<c} x_k L[c][k]) / L[c][c]
+    const int row = k0 + blockIdx.x * CB + r;
+    const bool has = r < CB && row < n;
+    double x[CB];
+#pragma unroll
+    for (int c = 0; c < CB; c++) x[c] = (has && c < nb) ? A[(size_t)row * n + k0 + c] : 0.0;
+#pragma unroll
+    for (int c = 0; c < CB; c++) {
+        if (c < nb) {
+            double v = x[c];
+#pragma unroll
+            for (int k = 0; k < c; k++) v -= x[k] * readlane_d(a[k], c);  // L[c][k] lives in lane c
+            x[c] = v / readlane_d(a[c], c);
+        }
+    }
+    double dot = 0.0;
+#pragma unroll
+    for (int c = 0; c < CB; c++)
+        if (c < nb) dot += x[c] * readlane_d(yv, c);
+    if (has) {
+#pragma unroll
+        for (int c = 0; c < CB; c++)
+            if (c < nb) A[(size_t)row * n + k0 + c] = x[c];
+        bs[row] -= dot;
     }
 }
 
@@ -514,79 +535,52 @@ __global__ __launch_bounds__(256) void k_chol_syrk(LbaDev D, int k0)
     }
 }
 
-// blocked forward (L y = b) and backward (L^T x = y) substitution, one workgroup
-__global__ __launch_bounds__(1024) void k_chol_solve(LbaDev D)
+// Backward substitution L^T x = y (y in x after the fused forward pass), one 1024-thread
+// workgroup, blocked by 32: for block k (last to first) the right-hand side
+// y_k - sum_{rows below} L[row][k-block]^T x_row is reduced by all threads (LDS), then one wave
+// solves the 32x32 upper-triangular block with readlane broadcasts.
+__global__ __launch_bounds__(1024) void k_chol_back(LbaDev D)
 {
     __shared__ double s_x[CMAX];
-    __shared__ double s_blk[CB];
+    __shared__ double s_part[32][33];
     const int n = 6 * D.nhp;
     const double *A = D.Hs;
     const int tid = threadIdx.x;
-    for (int i = tid; i < n; i += 1024) s_x[i] = D.bs[i];
+    for (int i = tid; i < n; i += 1024) s_x[i] = 0.0;
     __syncthreads();
-    for (int k0 = 0; k0 < n; k0 += CB) {
-        const int nb = min(CB, n - k0);
-        if (tid < 64) {
-            const int r = tid;
-            double xv = (r < nb) ? s_x[k0 + r] : 0.0;
-            double Lr[CB], dg[CB];
-#pragma unroll
-            for (int c = 0; c < CB; c++) {
-                Lr[c] = (r < nb && c < nb) ? A[(size_t)(k0 + r) * n + k0 + c] : 0.0;  // row r of the block
-                dg[c] = (c < nb) ? A[(size_t)(k0 + c) * n + k0 + c] : 1.0;
-            }
-#pragma unroll
-            for (int c = 0; c < CB; c++) {
-                if (c < nb) {
-                    const double xc = readlane_d(xv, c) / dg[c];
-                    if (r == c) xv = xc;
-                    if (r > c) xv -= Lr[c] * xc;
-                }
-            }
-            if (r < nb) {
-                s_x[k0 + r] = xv;
-                s_blk[r] = xv;
-            }
-        }
-        __syncthreads();
-        for (int row = k0 + nb + tid; row < n; row += 1024) {
-            double v = 0.0;
-            for (int c = 0; c < nb; c++) v += A[(size_t)row * n + k0 + c] * s_blk[c];
-            s_x[row] -= v;
-        }
-        __syncthreads();
-    }
     const int nblk = (n + CB - 1) / CB;
     for (int bi = nblk - 1; bi >= 0; bi--) {
         const int k0 = bi * CB;
         const int nb = min(CB, n - k0);
+        {
+            const int c = tid & 31, g = tid >> 5;  // 32 groups of rows
+            double acc = 0.0;
+            if (c < nb)
+                for (int row = k0 + nb + g; row < n; row += 32) acc += A[(size_t)row * n + k0 + c] * s_x[row];
+            s_part[c][g] = acc;
+        }
+        __syncthreads();
         if (tid < 64) {
             const int r = tid;
-            double xv = (r < nb) ? s_x[k0 + r] : 0.0;
-            double Lc[CB], dg[CB];
-#pragma unroll
-            for (int c = 0; c < CB; c++) {
-                Lc[c] = (r < nb && c < nb) ? A[(size_t)(k0 + c) * n + k0 + r] : 0.0;  // L[c][r] = L^T[r][c]
-                dg[c] = (c < nb) ? A[(size_t)(k0 + c) * n + k0 + c] : 1.0;
+            double rhs = 0.0;
+            if (r < nb) {
+                double t = 0.0;
+                for (int g = 0; g < 32; g++) t += s_part[r][g];
+                rhs = D.x[k0 + r] - t;  // y_k from the panel pass
             }
+            double Lc[CB];
+#pragma unroll
+            for (int c = 0; c < CB; c++) Lc[c] = (r < nb && c < nb && c >= r) ? D.Lkk[(size_t)(k0 + c) * CB + r] : 0.0;
+            double xv = rhs;
 #pragma unroll
             for (int c = CB - 1; c >= 0; c--) {
                 if (c < nb) {
-                    const double xc = readlane_d(xv, c) / dg[c];
+                    const double xc = readlane_d(xv, c) / readlane_d(Lc[c], c);  // L[c][c] in lane c
                     if (r == c) xv = xc;
-                    if (r < c) xv -= Lc[c] * xc;
+                    else if (r < c) xv -= Lc[c] * xc;  // L^T[r][c] = L[c][r]
                 }
             }
-            if (r < nb) {
-                s_x[k0 + r] = xv;
-                s_blk[r] = xv;
-            }
-        }
-        __syncthreads();
-        for (int row = tid; row < k0; row += 1024) {
-            double v = 0.0;
-            for (int c = 0; c < nb; c++) v += A[(size_t)(k0 + c) * n + row] * s_blk[c];
-            s_x[row] -= v;
+            if (r < nb) s_x[k0 + r] = xv;
         }
         __syncthreads();
     }
@@ -876,6 +870,7 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
         carve<double>(z, st_bytes, 3 * (size_t)NPART + 64);        // partials
         carve<double>(z, st_bytes, 36 * (size_t)std::max(nchunks, 1));  // chunk partials
         carve<double>(z, st_bytes, 3 * (size_t)nhl);                     // db
+        carve<double>(z, st_bytes, (size_t)sp * CB);                     // Lkk
         carve<int>(z, st_bytes, 16);                                // flags
         carve<uint8_t>(z, st_bytes, ne);                            // edge_bad
         st_bytes += 256;
@@ -940,6 +935,7 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
     D.blk_e = osg_dptr<int32_t>(din, o_blke);
     D.db = carve<double>(dst, off, 3 * (size_t)nhl);
     D.pair_chunk = osg_dptr<int32_t>(din, o_pch);
+    D.Lkk = carve<double>(dst, off, (size_t)sp * CB);
     D.flag = carve<int>(dst, off, 16);
     uint8_t *d_bad = carve<uint8_t>(dst, off, ne);
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(poseA, din + o_pose0, 56 * (size_t)np, hipMemcpyDeviceToDevice, ctx->stream));
@@ -1018,11 +1014,12 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
                 hipLaunchKernelGGL(k_bschur, dim3(nhp), dim3(256), 0, ctx->stream, D);
                 const int nred = 6 * nhp;
                 for (int k0 = 0; k0 < nred; k0 += CB) {
-                    hipLaunchKernelGGL(k_chol_panel, dim3(1), dim3(256), 0, ctx->stream, D, k0);
+                    const int rb = (nred - k0 + CB - 1) / CB;  // row blocks at and below the diagonal
+                    hipLaunchKernelGGL(k_chol_panel, dim3(rb), dim3(64), 0, ctx->stream, D, k0);
                     const int t = (nred - k0 - CB + CB - 1) / CB;
                     if (t > 0) hipLaunchKernelGGL(k_chol_syrk, dim3(t * (t + 1) / 2), dim3(256), 0, ctx->stream, D, k0);
                 }
-                hipLaunchKernelGGL(k_chol_solve, dim3(1), dim3(1024), 0, ctx->stream, D);
+                hipLaunchKernelGGL(k_chol_back, dim3(1), dim3(1024), 0, ctx->stream, D);
             }
             D.pose_new = new_pose;
             D.point_new = new_point;
