@@ -97,6 +97,10 @@ int osg_hamming_top2(osg_ctx *ctx, const uint8_t *query, int32_t nq, const uint8
 int osg_hamming_top2_dev(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d_train,
                          int32_t nt, void *d_out);
 
+/* Diagnostics: name and grid of the kernel osg_hamming_top2[_dev] would launch for (nq, nt) in
+ * this process (the launch knobs are read once).  No reference counterpart. */
+int osg_hamming_top2_plan(osg_ctx *ctx, int32_t nq, int32_t nt, char *name, int32_t len);
+
 /* ---- frame view (SoA gather of ORB_SLAM3::Frame / KeyFrame fields) ----------------------------
  * Grid: ref:src/Frame.cc:469-507 (AssignFeaturesToGrid), cells in CSR with cell = ix*48 + iy and
  * items in insertion (ascending feature index) order, which is GetFeaturesInArea's candidate

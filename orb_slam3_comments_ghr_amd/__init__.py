@@ -108,6 +108,13 @@ class Context:
                                                  _ptr(d_train), int(nt), _ptr(d_out)),
                    "osg_hamming_top2_dev")
 
+    def hamming_top2_plan(self, nq: int, nt: int) -> str:
+        """Name and grid of the kernel a (nq, nt) top-2 launch uses in this process."""
+        import ctypes
+        buf = ctypes.create_string_buffer(160)
+        self.check(self.lib.osg_hamming_top2_plan(self.handle, int(nq), int(nt), buf, 160), "osg_hamming_top2_plan")
+        return buf.value.decode()
+
     def descriptor_distance_pairs(self, a: np.ndarray, b: np.ndarray) -> np.ndarray:
         a = np.ascontiguousarray(a, dtype=np.uint8).reshape(-1, 32)
         b = np.ascontiguousarray(b, dtype=np.uint8).reshape(-1, 32)

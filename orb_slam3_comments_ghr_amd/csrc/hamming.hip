@@ -12,16 +12,18 @@
 // distance, then earlier index), kept as (k1 = smallest key, k2 = second smallest key) with
 // k2' = min(k2, max(k1, key)), k1' = min(k1, key) — 2 VALU ops (v_max/v_min3 or v_med3).
 //
-// Two shapes (same semantics, chosen by osg_launch_top2):
-//  * tile   — lane = query (its 8 words in VGPRs); every train row is wave-uniform and comes in
-//             through scalar loads (s_load_dwordx8: one 32-byte row broadcast to 64 queries), so a
-//             pair costs 8 v_xor + 8 v_bcnt(accumulate) + 1 v_lshl_or + 2 min = 19 VALU and no
-//             vector-memory traffic.  INT32-VALU bound.  Train rows split over WAVES waves of a
-//             workgroup (merged in LDS) and over G workgroups (merged by the last-arriving
-//             workgroup: agent-scope release/acquire through a self-resetting counter).
-//  * stream — few queries (<= 8) against a huge train set (C2', M = 2^24): lane = train row,
-//             queries in SGPRs, rows read once with coalesced 16-B loads.  HBM bound.
+// Three shapes (same semantics, chosen by osg_launch_top2):
+//  * qsplit — small query sets (nq <= 32 x CUs, e.g. C2 2000 x 2000): a workgroup owns a few
+//             queries against the whole train set staged through LDS; no cross-workgroup merge.
+//  * tile   — large query sets: lane = query (its 8 words in VGPRs); every train row is
+//             wave-uniform (scalar loads or LDS broadcast), so a pair costs 8 v_xor +
+//             8 v_bcnt(accumulate) + 1 v_lshl_or + 2 min = 19 VALU.  INT32-VALU bound.  Train rows
+//             split over WAVES waves (merged in LDS) and over G workgroups (merged by the
+//             last-arriving workgroup through a self-resetting counter).
+//  * stream — few queries (<= 8) against a huge train set (C2', M = 2^24): a lane pair per train
+//             row, queries in VGPRs, every row read once with fully coalesced 16-B loads.  HBM bound.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -256,64 +258,201 @@ __global__ __launch_bounds__(WAVES * 64) void k_top2_tile(const uint4 *__restric
     if (threadIdx.x == 0) __hip_atomic_store(&counters[qb], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ------------------------------------------------------------------- query-split (qsplit) kernel
+// Small query sets (C2: 2000 x 2000): one workgroup owns QB queries against the WHOLE train set,
+// staged through LDS in chunks of QS_ROWS rows, so no partial keys leave the workgroup (no
+// cross-workgroup merge, no atomics).  Thread t handles query t % QB over train rows
+// r = t / QB + k * (1024 / QB); a wave therefore reads 64 / QB distinct rows per step (each
+// broadcast to QB lanes, conflict-free ds_read_b128).  Reduction: xor-shuffles over the lanes of
+// one query inside the wave, then across the 16 waves in LDS.  Keys carry the global row index
+// (nt <= 2^23).
+constexpr int QS_ROWS = 2048;  // 64 KiB of LDS per chunk
+
+// rows [0, n) of the staged chunk, slice sl of S; keys carry row index base + r
+template <int S>
+__device__ __forceinline__ void qs_scan(const uint4 *rows, int n, int sl, uint32_t base, const uint32_t (&qd)[8],
+                                        uint32_t &k1, uint32_t &k2)
+{
+    int r = sl;
+    for (; r + 3 * S < n; r += 4 * S) {
+        uint32_t tr[4][8];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint4 a = rows[2 * (r + u * S)], b = rows[2 * (r + u * S) + 1];
+            tr[u][0] = a.x; tr[u][1] = a.y; tr[u][2] = a.z; tr[u][3] = a.w;
+            tr[u][4] = b.x; tr[u][5] = b.y; tr[u][6] = b.z; tr[u][7] = b.w;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) key_push(k1, k2, (hamming8(qd, tr[u]) << KEY_SHIFT) | (base + r + u * S));
+    }
+    for (; r < n; r += S) {
+        const uint4 a = rows[2 * r], b = rows[2 * r + 1];
+        const uint32_t tr[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        key_push(k1, k2, (hamming8(qd, tr) << KEY_SHIFT) | (base + r));
+    }
+}
+
+// (Measured on MI355X at 2000 x 2000, kernel average over back-to-back launches: this register
+// staging 5.75 us; LDS-DMA staging (global_load_lds_dwordx4) with per-quarter counted waits
+// 6.1 us, whether the rows are then read with compiler-scheduled or inline-asm ds_reads.)
+template <int QB>
+__global__ __launch_bounds__(1024) void k_top2_qsplit(const uint4 *__restrict__ query, int nq,
+                                                      const uint4 *__restrict__ train, int nt,
+                                                      int32_t *__restrict__ out)
+{
+    constexpr int S = 1024 / QB;  // row slices
+    __shared__ uint4 s_rows[2 * QS_ROWS];
+    __shared__ uint32_t s_k1[16][QB], s_k2[16][QB];
+    const int t = threadIdx.x;
+    const int w = t >> 6, lane = t & 63;
+    const int qi = t % QB;
+    const int sl = t / QB;
+    const int q = blockIdx.x * QB + qi;
+    uint32_t qd[8];
+    {
+        const int qq = q < nq ? q : nq - 1;
+        const uint4 a = query[2 * qq], b = query[2 * qq + 1];
+        qd[0] = a.x; qd[1] = a.y; qd[2] = a.z; qd[3] = a.w;
+        qd[4] = b.x; qd[5] = b.y; qd[6] = b.z; qd[7] = b.w;
+    }
+    uint32_t k1 = KEY_EMPTY, k2 = KEY_EMPTY;
+    for (int c0 = 0; c0 < nt; c0 += QS_ROWS) {
+        const int n = min(QS_ROWS, nt - c0);
+        const uint4 *src = train + 2 * (size_t)c0;
+        const int last = 2 * n - 1;  // past n: clamped copies, never read
+        const uint4 v0 = src[min(t, last)], v1 = src[min(1024 + t, last)];
+        const uint4 v2 = src[min(2048 + t, last)], v3 = src[min(3072 + t, last)];
+        if (c0 > 0) __syncthreads();  // previous chunk fully consumed
+        s_rows[t] = v0;
+        s_rows[1024 + t] = v1;
+        s_rows[2048 + t] = v2;
+        s_rows[3072 + t] = v3;
+        __syncthreads();
+        qs_scan<S>(s_rows, n, sl, (uint32_t)c0, qd, k1, k2);
+    }
+    // lanes of one query inside the wave: lane ^ QB, ^ 2QB, ... < 64
+#pragma unroll
+    for (int off = QB; off < 64; off <<= 1) {
+        const uint32_t a1 = __shfl_xor(k1, off), a2 = __shfl_xor(k2, off);
+        key_merge(k1, k2, a1, a2);
+    }
+    if (lane < QB) {
+        s_k1[w][lane] = k1;
+        s_k2[w][lane] = k2;
+    }
+    __syncthreads();
+    if (t < QB && q < nq) {
+        uint32_t a1 = s_k1[0][t], a2 = s_k2[0][t];
+#pragma unroll
+        for (int o = 1; o < 16; o++) key_merge(a1, a2, s_k1[o][t], s_k2[o][t]);
+        const uint2 p = key_to_part(a1, a2, 0u);
+        write_result(out, q, p.y >> 16, p.x, p.y & 0xFFFFu);
+    }
+}
+
 // ----------------------------------------------------------------------------- stream kernel
+// Completion counters of the stream kernels: 8 group counters and one top counter, each on its
+// own 128-B line at the end of ctx->counters (the tile kernel uses the first nqb entries).
+constexpr int STREAM_CNT_BASE = OSG_N_COUNTERS - 512;
+constexpr int STREAM_GROUPS = 8;
+
+// Arrival of one workgroup: group counter (blockIdx % 8), the last of a group bumps the top
+// counter; returns true in the workgroup that completes the whole grid.  Relaxed agent-scope
+// atomics after write-through partial stores drained with vmcnt(0): no L2 writeback fences.
+// Fan-in per counter is G / 8 instead of G (one device-scope atomic costs ~12 ns serialised).
+__device__ __forceinline__ bool stream_arrive(uint32_t *counters, int G)
+{
+    const int g = blockIdx.x % STREAM_GROUPS;
+    const int members = G / STREAM_GROUPS + (g < G % STREAM_GROUPS ? 1 : 0);
+    const int groups = min(G, STREAM_GROUPS);
+    uint32_t *gc = counters + STREAM_CNT_BASE + 32 * g;
+    uint32_t *top = counters + STREAM_CNT_BASE + 32 * STREAM_GROUPS;
+    const uint32_t prev = __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev != (uint32_t)(members - 1)) return false;
+    __hip_atomic_store(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t tprev = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tprev != (uint32_t)(groups - 1)) return false;
+    __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
+
+// Stream kernel, lane-pair layout: lane = one 16-B half of a train row, so every load
+// instruction of a wave reads 1 KiB contiguous (32 rows); the half distances of a row meet with
+// one DPP add (quad_perm [1,0,3,2]).  Both lanes of a pair then hold the same keys, so the
+// butterfly starts at offset 2.  Rows double-buffered in registers (U steps of 128 rows per
+// workgroup in flight while the previous U are consumed).
 template <int NQ>
 __global__ __launch_bounds__(256) void k_top2_stream(const uint32_t *__restrict__ query, int nq,
-                                                     const uint4 *__restrict__ train, int nt,
-                                                     int rows_per_block, int G,
-                                                     uint2 *__restrict__ part,
-                                                     uint32_t *__restrict__ counter,
-                                                     int32_t *__restrict__ out)
+                                                      const u32x4 *__restrict__ train, int nt,
+                                                      int rows_per_block, int G,
+                                                      uint2 *__restrict__ part,
+                                                      uint32_t *__restrict__ counters,
+                                                      int32_t *__restrict__ out)
 {
+    constexpr int U = 4;
     __shared__ uint32_t s_k1[4][NQ], s_k2[4][NQ];
-    __shared__ uint32_t s_D1[4][NQ], s_I1[4][NQ], s_D2[4][NQ];
+    __shared__ uint32_t s_D1[4], s_I1[4], s_D2[4];
     __shared__ int s_last;
-    const int lane = threadIdx.x & 63;
-    const int w = threadIdx.x >> 6;
+    const int t = threadIdx.x;
+    const int lane = t & 63, w = t >> 6, h = t & 1;
 
-    uint32_t qd[NQ][8];
+    uint32_t qh[NQ][4];
 #pragma unroll
     for (int j = 0; j < NQ; j++) {
         const int jj = j < nq ? j : nq - 1;
 #pragma unroll
-        for (int i = 0; i < 8; i++) qd[j][i] = query[jj * 8 + i]; // uniform: SGPRs
+        for (int i = 0; i < 4; i++) qh[j][i] = query[jj * 8 + 4 * h + i];
     }
-    const int r0 = blockIdx.x * rows_per_block;
-    const int r1 = min(nt, r0 + rows_per_block);
     uint32_t k1[NQ], k2[NQ];
 #pragma unroll
     for (int j = 0; j < NQ; j++) k1[j] = k2[j] = KEY_EMPTY;
 
-    constexpr int U = 4;
-    int r = r0 + threadIdx.x;
-    for (; r + (U - 1) * 256 < r1; r += U * 256) {
-        u32x4 ta[U], tb[U];
-        const u32x4 *tv = (const u32x4 *)train;
+    const int r0 = blockIdx.x * rows_per_block;
+    const int r1 = min(nt, r0 + rows_per_block);
+    const int nr = r1 - r0;
+    const u32x4 *base = train + 2 * (size_t)r0;
+    auto consume = [&](const u32x4 &v, uint32_t rl) {
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            ta[u] = __builtin_nontemporal_load(&tv[2 * (size_t)(r + u * 256)]);
-            tb[u] = __builtin_nontemporal_load(&tv[2 * (size_t)(r + u * 256) + 1]);
+        for (int j = 0; j < NQ; j++) {
+            uint32_t p = __popc(qh[j][0] ^ v.x);
+            p = bcnt_acc(qh[j][1] ^ v.y, p);
+            p = bcnt_acc(qh[j][2] ^ v.z, p);
+            p = bcnt_acc(qh[j][3] ^ v.w, p);
+            const uint32_t d = p + (uint32_t)__builtin_amdgcn_mov_dpp((int)p, 0xB1, 0xF, 0xF, false);
+            key_push(k1[j], k2[j], (d << KEY_SHIFT) | rl);
+        }
+    };
+    // full batches: U steps of 128 rows (256 16-B elements) each
+    const int nfull = nr / (128 * U);
+    int b = 0;
+    if (nfull > 0) {
+        u32x4 cur[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) cur[u] = __builtin_nontemporal_load(&base[256 * u + t]);
+        for (; b + 1 < nfull; b++) {
+            u32x4 nxt[U];
+            const u32x4 *nb = base + 256 * U * (b + 1);
+#pragma unroll
+            for (int u = 0; u < U; u++) nxt[u] = __builtin_nontemporal_load(&nb[256 * u + t]);
+#pragma unroll
+            for (int u = 0; u < U; u++) consume(cur[u], (uint32_t)(128 * (U * b + u) + (t >> 1)));
+#pragma unroll
+            for (int u = 0; u < U; u++) cur[u] = nxt[u];
         }
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint32_t t[8] = {ta[u].x, ta[u].y, ta[u].z, ta[u].w, tb[u].x, tb[u].y, tb[u].z, tb[u].w};
-            const uint32_t l = (uint32_t)(r + u * 256 - r0);
-#pragma unroll
-            for (int j = 0; j < NQ; j++) key_push(k1[j], k2[j], (hamming8(qd[j], t) << KEY_SHIFT) | l);
-        }
+        for (int u = 0; u < U; u++) consume(cur[u], (uint32_t)(128 * (U * b + u) + (t >> 1)));
+        b++;
     }
-    for (; r < r1; r += 256) {
-        const uint4 a = train[2 * (size_t)r], b = train[2 * (size_t)r + 1];
-        const uint32_t t[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-        const uint32_t l = (uint32_t)(r - r0);
-#pragma unroll
-        for (int j = 0; j < NQ; j++) key_push(k1[j], k2[j], (hamming8(qd[j], t) << KEY_SHIFT) | l);
+    // tail steps of 128 rows
+    for (int rs = 128 * U * b; rs < nr; rs += 128) {
+        const int rl = rs + (t >> 1);
+        const u32x4 v = base[2 * min(rl, nr - 1) + h];
+        if (rl < nr) consume(v, (uint32_t)rl);  // both lanes of a pair share rl: DPP partner active
     }
-    // wave butterfly, then across the 4 waves in LDS
 #pragma unroll
     for (int j = 0; j < NQ; j++) {
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
+        for (int off = 2; off < 64; off <<= 1) {
             const uint32_t a1 = __shfl_xor(k1[j], off), a2 = __shfl_xor(k2[j], off);
             key_merge(k1[j], k2[j], a1, a2);
         }
@@ -323,44 +462,49 @@ __global__ __launch_bounds__(256) void k_top2_stream(const uint32_t *__restrict_
         }
     }
     __syncthreads();
-    if (threadIdx.x < nq) {
-        const int j = threadIdx.x;
+    if (t < nq) {
+        const int j = t;
         uint32_t a1 = s_k1[0][j], a2 = s_k2[0][j];
         for (int o = 1; o < 4; o++) key_merge(a1, a2, s_k1[o][j], s_k2[o][j]);
         const uint2 p = key_to_part(a1, a2, (uint32_t)r0);
-        if (G == 1) write_result(out, j, p.y >> 16, p.x, p.y & 0xFFFFu);
-        else part[(size_t)blockIdx.x * nq + j] = p;
+        if (G == 1) {
+            write_result(out, j, p.y >> 16, p.x, p.y & 0xFFFFu);
+        } else {
+            const unsigned long long v = ((unsigned long long)p.y << 32) | p.x;
+            __hip_atomic_store((unsigned long long *)&part[(size_t)blockIdx.x * nq + j], v, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     if (G == 1) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = (prev == (uint32_t)(G - 1));
-    }
+    if (t == 0) s_last = stream_arrive(counters, G);
     __syncthreads();
     if (!s_last) return;
     for (int j = 0; j < nq; j++) {
         uint32_t D1 = D_EMPTY, I1 = 0xFFFFFFFFu, D2 = D_EMPTY;
-        for (int b = threadIdx.x; b < G; b += 256) part_merge(D1, I1, D2, part[(size_t)b * nq + j]);
+        for (int bb = t; bb < G; bb += 256) {
+            const unsigned long long v = __hip_atomic_load((unsigned long long *)&part[(size_t)bb * nq + j],
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            part_merge(D1, I1, D2, make_uint2((uint32_t)v, (uint32_t)(v >> 32)));
+        }
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
             const uint2 o = make_uint2(__shfl_xor(I1, off), (__shfl_xor(D1, off) << 16) | __shfl_xor(D2, off));
             part_merge(D1, I1, D2, o);
         }
         if (lane == 0) {
-            s_D1[w][0] = D1;
-            s_I1[w][0] = I1;
-            s_D2[w][0] = D2;
+            s_D1[w] = D1;
+            s_I1[w] = I1;
+            s_D2[w] = D2;
         }
         __syncthreads();
-        if (threadIdx.x == 0) {
-            for (int o = 1; o < 4; o++) part_merge(D1, I1, D2, make_uint2(s_I1[o][0], (s_D1[o][0] << 16) | s_D2[o][0]));
+        if (t == 0) {
+            for (int o = 1; o < 4; o++) part_merge(D1, I1, D2, make_uint2(s_I1[o], (s_D1[o] << 16) | s_D2[o]));
             write_result(out, j, D1, I1, D2);
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // --------------------------------------------------------------------------- pairwise distance
@@ -381,13 +525,14 @@ int env_int(const char *name, int dflt)
     return (v && *v) ? atoi(v) : dflt;
 }
 struct top2_knobs {
-    int variant, waves, target_wg, min_rows, dbg, stream_g;
+    int variant, waves, target_wg, min_rows, dbg, stream_g, qs_wg;
 };
 const top2_knobs &knobs(int cus)
 {
     static const top2_knobs k = {env_int("OSG_TOP2_VARIANT", 2), env_int("OSG_TOP2_WAVES", 0),
                                  env_int("OSG_TOP2_WG", cus), env_int("OSG_TOP2_MIN_ROWS", 64),
-                                 env_int("OSG_TOP2_DEBUG", 0), env_int("OSG_TOP2_STREAM_G", 8 * cus)};
+                                 env_int("OSG_TOP2_DEBUG", 0), env_int("OSG_TOP2_STREAM_G", 2 * cus),
+                                 env_int("OSG_TOP2_QS_WG", cus * 9 / 10)};
     return k;
 }
 
@@ -411,29 +556,53 @@ int osg_launch_top2(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d
     }
     const int cus = ctx->num_cus;
     if (nq <= 8 && nt >= 65536) {
-        // streaming shape: lane = train row
+        // streaming shape: a lane pair per train row
         int G = knobs(cus).stream_g;
         int rpb = (nt + G - 1) / G;
         rpb = ((rpb + 1023) / 1024) * 1024;
         G = (nt + rpb - 1) / rpb;
         uint2 *part = nullptr;
         OSG_ALLOC(ctx, part, SLOT_PART, sizeof(uint2) * (size_t)G * nq);
-        uint32_t *counter = ctx->counters + (OSG_N_COUNTERS - 1);
         const uint32_t *q = (const uint32_t *)d_query;
-        const uint4 *t = (const uint4 *)d_train;
         int32_t *o = (int32_t *)d_out;
-        if (nq == 1) hipLaunchKernelGGL(k_top2_stream<1>, dim3(G), dim3(256), 0, ctx->stream, q, nq, t, nt, rpb, G, part, counter, o);
-        else if (nq == 2) hipLaunchKernelGGL(k_top2_stream<2>, dim3(G), dim3(256), 0, ctx->stream, q, nq, t, nt, rpb, G, part, counter, o);
-        else if (nq <= 4) hipLaunchKernelGGL(k_top2_stream<4>, dim3(G), dim3(256), 0, ctx->stream, q, nq, t, nt, rpb, G, part, counter, o);
-        else hipLaunchKernelGGL(k_top2_stream<8>, dim3(G), dim3(256), 0, ctx->stream, q, nq, t, nt, rpb, G, part, counter, o);
+        const u32x4 *t2 = (const u32x4 *)d_train;
+        uint32_t *cn = ctx->counters;
+        if (nq == 1) hipLaunchKernelGGL(k_top2_stream<1>, dim3(G), dim3(256), 0, ctx->stream, q, nq, t2, nt, rpb, G, part, cn, o);
+        else if (nq == 2) hipLaunchKernelGGL(k_top2_stream<2>, dim3(G), dim3(256), 0, ctx->stream, q, nq, t2, nt, rpb, G, part, cn, o);
+        else if (nq <= 4) hipLaunchKernelGGL(k_top2_stream<4>, dim3(G), dim3(256), 0, ctx->stream, q, nq, t2, nt, rpb, G, part, cn, o);
+        else hipLaunchKernelGGL(k_top2_stream<8>, dim3(G), dim3(256), 0, ctx->stream, q, nq, t2, nt, rpb, G, part, cn, o);
         OSG_HIP_CHECK(ctx, hipGetLastError());
         return OSG_OK;
     }
     const top2_knobs &kn = knobs(cus);
+    // OSG_TOP2_VARIANT: 2 = auto (default), 3 = query-split only, 4 = LDS-staged tile only,
+    // 1 = scalar-load tile + write-through merge, 0 = scalar-load tile + fenced merge.
+    // Query-split shape: enough workgroups of QB queries to cover the CUs (OSG_TOP2_QS_WG), whole
+    // train set per workgroup
+    const bool qsplit = (kn.variant == 3 || (kn.variant == 2 && nq <= 32 * cus)) && nt <= (int)IDX_MASK;
+    if (qsplit) {
+        int qb = 64;
+        while (qb > 1 && (nq + qb - 1) / qb < kn.qs_wg) qb >>= 1;
+        const dim3 grid((nq + qb - 1) / qb), block(1024);
+        const uint4 *q = (const uint4 *)d_query;
+        const uint4 *t = (const uint4 *)d_train;
+        int32_t *o = (int32_t *)d_out;
+        switch (qb) {
+        case 64: hipLaunchKernelGGL(k_top2_qsplit<64>, grid, block, 0, ctx->stream, q, nq, t, nt, o); break;
+        case 32: hipLaunchKernelGGL(k_top2_qsplit<32>, grid, block, 0, ctx->stream, q, nq, t, nt, o); break;
+        case 16: hipLaunchKernelGGL(k_top2_qsplit<16>, grid, block, 0, ctx->stream, q, nq, t, nt, o); break;
+        case 8: hipLaunchKernelGGL(k_top2_qsplit<8>, grid, block, 0, ctx->stream, q, nq, t, nt, o); break;
+        case 4: hipLaunchKernelGGL(k_top2_qsplit<4>, grid, block, 0, ctx->stream, q, nq, t, nt, o); break;
+        case 2: hipLaunchKernelGGL(k_top2_qsplit<2>, grid, block, 0, ctx->stream, q, nq, t, nt, o); break;
+        default: hipLaunchKernelGGL(k_top2_qsplit<1>, grid, block, 0, ctx->stream, q, nq, t, nt, o); break;
+        }
+        OSG_HIP_CHECK(ctx, hipGetLastError());
+        return OSG_OK;
+    }
     const int waves = kn.waves > 0 ? kn.waves : (nq <= 4096 ? 16 : 8);
     const int WAVES = (waves >= 16) ? 16 : (waves >= 8 ? 8 : 4);
     const int nqb = (nq + 63) / 64;
-    OSG_REQUIRE(ctx, nqb <= OSG_N_COUNTERS - 1, "too many queries (%d)", nq);
+    OSG_REQUIRE(ctx, nqb <= STREAM_CNT_BASE, "too many queries (%d)", nq);
     const int variant = kn.variant;
     const int dbg = kn.dbg;
     const int target_wg = kn.target_wg;
@@ -441,11 +610,11 @@ int osg_launch_top2(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d
     int G = (target_wg + nqb - 1) / nqb;
     G = std::min(G, std::max(1, nt / min_rows));
     G = std::max(G, (nt + (int)IDX_MASK) / ((int)IDX_MASK + 1)); // chunk-local index fits 23 bits
-    if (variant == 2) G = std::max(G, (nt + TILE_MAX_ROWS - 1) / TILE_MAX_ROWS);
+    if (variant == 2 || variant == 4) G = std::max(G, (nt + TILE_MAX_ROWS - 1) / TILE_MAX_ROWS);
     G = std::max(1, std::min(G, TILE_MAX_G));
     int rpc = (nt + G - 1) / G;
     G = (nt + rpc - 1) / rpc;
-    const bool use_stage = (variant == 2) && rpc <= TILE_MAX_ROWS;
+    const bool use_stage = (variant == 2 || variant == 4) && rpc <= TILE_MAX_ROWS;
     uint2 *part = nullptr;
     if (G > 1) OSG_ALLOC(ctx, part, SLOT_PART, sizeof(uint2) * (size_t)G * nq);
     const dim3 grid(nqb, G), block(WAVES * 64);
@@ -471,6 +640,30 @@ int osg_launch_top2(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d
 }
 
 extern "C" {
+
+int osg_hamming_top2_plan(osg_ctx *ctx, int32_t nq, int32_t nt, char *name, int32_t len)
+{
+    if (!ctx || !name || len <= 0) return OSG_E_INVALID;
+    const int cus = ctx->num_cus;
+    const top2_knobs &kn = knobs(cus);
+    char buf[160];
+    if (nq <= 0 || nt <= 0) {
+        snprintf(buf, sizeof buf, "none");
+    } else if (nq <= 8 && nt >= 65536) {
+        int G = kn.stream_g, rpb = (nt + G - 1) / G;
+        rpb = ((rpb + 1023) / 1024) * 1024;
+        snprintf(buf, sizeof buf, "k_top2_stream<%d> grid=%d x 256", nq == 1 ? 1 : nq == 2 ? 2 : nq <= 4 ? 4 : 8,
+                 (nt + rpb - 1) / rpb);
+    } else if ((kn.variant == 3 || (kn.variant == 2 && nq <= 32 * cus)) && nt <= (int)IDX_MASK) {
+        int qb = 64;
+        while (qb > 1 && (nq + qb - 1) / qb < kn.qs_wg) qb >>= 1;
+        snprintf(buf, sizeof buf, "k_top2_qsplit<%d> grid=%d x 1024", qb, (nq + qb - 1) / qb);
+    } else {
+        snprintf(buf, sizeof buf, "k_top2_tile (variant %d)", kn.variant);
+    }
+    snprintf(name, (size_t)len, "%s", buf);
+    return OSG_OK;
+}
 
 int osg_hamming_top2_dev(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d_train, int32_t nt,
                          void *d_out)

@@ -105,26 +105,32 @@ def test_alternating_problems_no_stale_partials(ctx, oracle):
             np.testing.assert_array_equal(g, r)
 
 
-@pytest.mark.parametrize("variant,waves", [("0", "4"), ("1", "8"), ("2", "16"), ("2", "4")])
-def test_tile_variants(oracle, variant, waves):
-    """Every tile variant (scalar/LDS staging x fence/write-through merge x 4/8/16 waves) in a
-    fresh process: the knobs are read once per process."""
+@pytest.mark.parametrize("variant,waves,wg", [("0", "4", ""), ("1", "8", ""), ("4", "16", ""), ("4", "4", ""),
+                                               ("3", "16", ""), ("3", "16", "64"), ("3", "16", "4096"),
+                                               ("2", "8", "")])
+def test_tile_variants(oracle, variant, waves, wg):
+    """Every top-2 variant in a fresh process (the knobs are read once per process): tile kernel
+    with scalar/LDS staging x fence/write-through merge x 4/8/16 waves, and the query-split kernel
+    at several queries-per-workgroup (OSG_TOP2_QS_WG target 64 -> 32 queries per workgroup at
+    nq = 2000, 4096 -> 1 query per workgroup)."""
     import subprocess, sys, os, json
     code = (
         "import numpy as np, json\n"
         "from orb_slam3_comments_ghr_amd import Context, synth\n"
         "c = Context(0)\n"
         "out = []\n"
-        "for seed, (nq, nt) in enumerate([(2000, 2000), (300, 20000), (5000, 600)]):\n"
+        "for seed, (nq, nt) in enumerate([(2000, 2000), (300, 20000), (5000, 600), (70, 4097)]):\n"
         "    q, t = synth.descriptors_c2(nq, nt, seed=900 + seed)\n"
         "    out.append([a.tolist() for a in c.hamming_top2(q, t)])\n"
         "print(json.dumps(out))\n")
     env = dict(os.environ, OSG_TOP2_VARIANT=variant, OSG_TOP2_WAVES=waves)
+    if wg:
+        env["OSG_TOP2_WG"] = env["OSG_TOP2_QS_WG"] = wg
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300,
                        cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert r.returncode == 0, r.stderr[-2000:]
     got = json.loads(r.stdout.strip().splitlines()[-1])
-    for seed, (nq, nt) in enumerate([(2000, 2000), (300, 20000), (5000, 600)]):
+    for seed, (nq, nt) in enumerate([(2000, 2000), (300, 20000), (5000, 600), (70, 4097)]):
         q, t = synth.descriptors_c2(nq, nt, seed=900 + seed)
         ref = otop2(oracle, q, t)
         for g, rr in zip(got[seed], ref):
