@@ -78,9 +78,10 @@ struct LbaDev {
     double *Hll, *bl, *Hpl, *Hpp, *bp;
     double *Dinv, *db, *BDinv, *coef;
     double *Hs, *bs, *x;
-    double *Lkk;                         // factored 32x32 diagonal blocks, row-major per block row
+    double *Linv;                        // inverses of the 32x32 diagonal blocks of L, row-major per block row
     double *part;                        // [0..NPART): chi partials, [NPART..2NPART): scale, [2NPART..]: max diag
     int *flag;                           // [0] cholesky ok
+    unsigned long long *tstamp;          // phase timestamps (OSG_LBA_PROFILE=2), else null
 };
 
 __device__ inline double edge_w(const LbaDev &D, int e) { return (double)D.e_isig2[e]; }
@@ -404,186 +405,408 @@ __global__ __launch_bounds__(256) void k_bschur(LbaDev D)
     }
 }
 
-__device__ inline double readlane_d(double v, int lane)
-{  // wave-uniform lane index: two v_readlane_b32 instead of a ds_bpermute round trip
-    const unsigned long long u = __double_as_longlong(v);
-    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, lane);
-    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), lane);
-    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
-}
-
 // ---------------------------------------------------------------------------------------------
-// Reduced camera system: blocked right-looking Cholesky (LL^T, lower, in place in Hs) over
-// panels of CB = 32 columns with the forward substitution fused, then a blocked backward solve.
-// Per panel:
-//   k_chol_panel  one wave per 32-row block: diagonal block factored in registers (readlane),
-//                 rows below solved against it, b updated;
-//   k_chol_syrk   trailing update A22 -= L21 L21^T on 32x32 lower tiles, one workgroup per tile,
-//                 one wave per 16x16 quadrant on FP64 MFMA (v_mfma_f64_16x16x4_f64, K = 32 as
-//                 8 MFMAs) — the only MFMA use on the path (the dense Schur GEMM).
-// The factorisation reports failure on a non-positive pivot (g2o's solvers then reject the step).
+// Reduced camera system: blocked left-looking Cholesky (L L^T, lower, in place in Hs) over column
+// blocks of CB = 32, one launch per column block (k_chol_col: FP64-MFMA update of the block's
+// tiles from all previous columns, LDS factorisation of the diagonal tile, its inverse, L21 as
+// X L^-T, forward substitution fused), then k_chol_back.  The MFMA tile updates are the dense
+// Schur GEMM of the path.  A non-positive pivot clears flag[0] (g2o's solvers then reject the step).
 constexpr int CB = 32;
 constexpr int CMAX = 384;  // max reduced dimension (64 free poses)
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-// Panel step k0, one 64-thread workgroup per 32-row block at or below the diagonal block.  Every
-// workgroup factors the 32x32 diagonal block itself (lane = row, registers, v_readlane
-// broadcasts, no barriers) and solves y_k = L_kk^-1 b_k; workgroup 0 stores L_kk and y_k,
-// workgroup t > 0 turns its 32 rows into L21 rows (x L_kk^T = a) and updates b for them
-// (b_row -= L_row . y_k).  Workgroup 0 writes L_kk to Lkk and y_k to x (forward substitution fused).
-__global__ __launch_bounds__(64) void k_chol_panel(LbaDev D, int k0)
-{
-    const int n = 6 * D.nhp;
-    double *A = D.Hs;
-    double *bs = D.bs;
-    const int nb = min(CB, n - k0);
-    const int r = threadIdx.x;  // lane
-    double a[CB];
-#pragma unroll
-    for (int c = 0; c < CB; c++) a[c] = (r < nb && c < nb && c <= r) ? A[(size_t)(k0 + r) * n + k0 + c] : 0.0;
-    double yv = (r < nb) ? bs[k0 + r] : 0.0;
-    int ok = 1;
-#pragma unroll
-    for (int c = 0; c < CB; c++) {
-        if (c < nb) {
-            const double d = readlane_d(a[c], c);
-            ok &= d > 0.0;
-            const double piv = sqrt(fmax(d, 1e-300));
-            if (r == c) a[c] = piv;
-            else if (r > c) a[c] /= piv;
-            const double lrc = a[c];
-#pragma unroll
-            for (int cc = c + 1; cc < CB; cc++) {
-                const double lcc = readlane_d(a[c], cc);  // L[cc][c]
-                if (cc < nb && r >= cc) a[cc] -= lrc * lcc;
-            }
-            // forward substitution of b inside the block
-            const double yc = readlane_d(yv, c) / piv;
-            if (r == c) yv = yc;
-            else if (r > c && r < nb) yv -= lrc * yc;
-        }
-    }
-    if (blockIdx.x == 0) {
-        if (r == 0 && !ok) D.flag[0] = 0;
-        // the diagonal block of Hs and b_k stay untouched: the other workgroups of this launch read them
-        if (r < nb) {
-#pragma unroll
-            for (int c = 0; c < CB; c++) D.Lkk[(size_t)(k0 + r) * CB + c] = a[c];
-            D.x[k0 + r] = yv;
-        }
-        return;
-    }
-    // rows of block t: x L_kk^T = a_row  ->  x_c = (a_c - sum_{k<c} x_k L[c][k]) / L[c][c]
-    const int row = k0 + blockIdx.x * CB + r;
-    const bool has = r < CB && row < n;
-    double x[CB];
-#pragma unroll
-    for (int c = 0; c < CB; c++) x[c] = (has && c < nb) ? A[(size_t)row * n + k0 + c] : 0.0;
-#pragma unroll
-    for (int c = 0; c < CB; c++) {
-        if (c < nb) {
-            double v = x[c];
-#pragma unroll
-            for (int k = 0; k < c; k++) v -= x[k] * readlane_d(a[k], c);  // L[c][k] lives in lane c
-            x[c] = v / readlane_d(a[c], c);
-        }
-    }
-    double dot = 0.0;
-#pragma unroll
-    for (int c = 0; c < CB; c++)
-        if (c < nb) dot += x[c] * readlane_d(yv, c);
-    if (has) {
-#pragma unroll
-        for (int c = 0; c < CB; c++)
-            if (c < nb) A[(size_t)row * n + k0 + c] = x[c];
-        bs[row] -= dot;
-    }
-}
+// Left-looking tile updates of column block j on FP64 MFMA (v_mfma_f64_16x16x4f64):
+//   sT = A_jj - sum_{m < K} L_jm L_jm^T      (the diagonal tile)
+//   sX = A_tj - sum_{m < K} L_tm L_jm^T      (row block t, when R0 >= 0)
+//   s_rp[w][r] = partial of sum_{m < K} L_jm[r][m] y_m   (when y != null: forward substitution)
+// K (= 32 j) is split over the 4 waves; each wave issues every load of its K-slice before its
+// first MFMA (one memory latency per launch instead of one per 16-wide step), computes all 4
+// quadrants of each tile, and the 4 partial tiles are summed through LDS.  MFMA operand layout:
+// lane l holds row (l & 15) and k-group (l >> 4); per 16-wide step a lane loads the 4
+// consecutive elements m0 + 4 (l >> 4) .. + 3 and MFMA i consumes element i, so each step covers
+// m0 .. m0 + 15 once.  The L_j rows serve as both operands of the diagonal tile.  Rows past n
+// read as zero; tile entries past n become the identity (keeps the padded factorisation finite).
+constexpr int LU_STEPS = CMAX / 64;  // 16-wide steps per wave at most
 
-// tile (ti, tj), ti >= tj, of the trailing matrix starting at t0 = k0 + CB
-__global__ __launch_bounds__(256) void k_chol_syrk(LbaDev D, int k0)
+__device__ __forceinline__ void tile_left_update2(const double *__restrict__ A, int n, int C0, int R0, int K,
+                                                  const double *__restrict__ y,
+                                                  double (*sT)[CB + 1], double (*sX)[CB + 1],
+                                                  double (*sP)[CB][CB + 1], double (*s_rp)[CB])
 {
-    const int n = 6 * D.nhp;
-    double *A = D.Hs;
-    const int t0 = k0 + CB;
-    // decode lower-triangular tile index
-    int ti = 0, rem = blockIdx.x;
-    while (rem > ti) {
-        rem -= ti + 1;
-        ti++;
-    }
-    const int tj = rem;
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const int R0 = t0 + ti * CB + (w >> 1) * 16;  // quadrant rows
-    const int C0 = t0 + tj * CB + (w & 1) * 16;   // quadrant cols
-    if (R0 >= n || C0 >= n) return;
-    if (ti == tj && (w & 1) > (w >> 1)) return;   // strictly upper quadrant of a diagonal tile
-    d4 acc = {0.0, 0.0, 0.0, 0.0};
-    const int ra = R0 + (l & 15), cb = C0 + (l & 15);
-#pragma unroll
-    for (int ks = 0; ks < CB / 4; ks++) {
-        const int kk = k0 + ks * 4 + (l >> 4);
-        const double a = (ra < n) ? A[(size_t)ra * n + kk] : 0.0;  // L[R0+i][k]
-        const double b = (cb < n) ? A[(size_t)cb * n + kk] : 0.0;  // L[C0+j][k] (= B[k][j])
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
-    }
-    const int col = C0 + (l & 15);
+    const bool two = R0 >= 0;
+    // originals first: their latency overlaps the GEMM
+    double aT[4], aX[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-        const int row = R0 + (l >> 4) + 4 * q;
-        if (row < n && col < n && col <= row) A[(size_t)row * n + col] -= acc[q];
+        const int e = threadIdx.x + 256 * q, r = e >> 5, c = e & 31;
+        aT[q] = (C0 + r < n && C0 + c < n) ? A[(size_t)(C0 + r) * n + C0 + c] : 0.0;
+        aX[q] = (two && R0 + r < n && C0 + c < n) ? A[(size_t)(R0 + r) * n + C0 + c] : 0.0;
+    }
+    const int kq = ((K + 63) / 64) * 16;  // per-wave slice, multiple of 16
+    const int mb = w * kq, me = min(K, mb + kq);
+    const int g4 = 4 * (l >> 4);
+    const int rj0 = C0 + (l & 15), rj1 = C0 + 16 + (l & 15);
+    const int rt0 = R0 + (l & 15), rt1 = R0 + 16 + (l & 15);
+    const bool vj0 = rj0 < n, vj1 = rj1 < n, vt0 = two && rt0 < n, vt1 = two && rt1 < n;
+    const double *pj0 = A + (size_t)(vj0 ? rj0 : 0) * n + g4, *pj1 = A + (size_t)(vj1 ? rj1 : 0) * n + g4;
+    const double *pt0 = A + (size_t)(vt0 ? rt0 : 0) * n + g4, *pt1 = A + (size_t)(vt1 ? rt1 : 0) * n + g4;
+    double2 j0[LU_STEPS][2], j1[LU_STEPS][2], t0[LU_STEPS][2], t1[LU_STEPS][2], yy[LU_STEPS][2];
+    const int nst = max(0, (me - mb) / 16);  // wave-uniform step count of this slice
+#pragma unroll
+    for (int s = 0; s < LU_STEPS; s++) {
+        if (s >= nst) break;
+        const int m = mb + 16 * s;
+        j0[s][0] = *(const double2 *)(pj0 + m); j0[s][1] = *(const double2 *)(pj0 + m + 2);
+        j1[s][0] = *(const double2 *)(pj1 + m); j1[s][1] = *(const double2 *)(pj1 + m + 2);
+        if (two) {
+            t0[s][0] = *(const double2 *)(pt0 + m); t0[s][1] = *(const double2 *)(pt0 + m + 2);
+            t1[s][0] = *(const double2 *)(pt1 + m); t1[s][1] = *(const double2 *)(pt1 + m + 2);
+        }
+        if (y) {
+            yy[s][0] = *(const double2 *)(y + g4 + m); yy[s][1] = *(const double2 *)(y + g4 + m + 2);
+        }
+    }
+    d4 accT[2][2], accX[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) accT[a][b] = accX[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+    double rp0 = 0.0, rp1 = 0.0;
+#pragma unroll
+    for (int s = 0; s < LU_STEPS; s++) {
+        if (s < nst) {
+            double ja[2][4], ta[2][4];
+            const bool z0 = !vj0, z1 = !vj1, y0 = !vt0, y1 = !vt1;
+            ja[0][0] = z0 ? 0.0 : j0[s][0].x; ja[0][1] = z0 ? 0.0 : j0[s][0].y;
+            ja[0][2] = z0 ? 0.0 : j0[s][1].x; ja[0][3] = z0 ? 0.0 : j0[s][1].y;
+            ja[1][0] = z1 ? 0.0 : j1[s][0].x; ja[1][1] = z1 ? 0.0 : j1[s][0].y;
+            ja[1][2] = z1 ? 0.0 : j1[s][1].x; ja[1][3] = z1 ? 0.0 : j1[s][1].y;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                accT[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(ja[0][i], ja[0][i], accT[0][0], 0, 0, 0);
+                accT[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(ja[1][i], ja[0][i], accT[1][0], 0, 0, 0);
+                accT[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(ja[1][i], ja[1][i], accT[1][1], 0, 0, 0);
+            }
+            if (y) {
+                const double yv[4] = {yy[s][0].x, yy[s][0].y, yy[s][1].x, yy[s][1].y};
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    rp0 += ja[0][i] * yv[i];
+                    rp1 += ja[1][i] * yv[i];
+                }
+            }
+            if (two) {
+                ta[0][0] = y0 ? 0.0 : t0[s][0].x; ta[0][1] = y0 ? 0.0 : t0[s][0].y;
+                ta[0][2] = y0 ? 0.0 : t0[s][1].x; ta[0][3] = y0 ? 0.0 : t0[s][1].y;
+                ta[1][0] = y1 ? 0.0 : t1[s][0].x; ta[1][1] = y1 ? 0.0 : t1[s][0].y;
+                ta[1][2] = y1 ? 0.0 : t1[s][1].x; ta[1][3] = y1 ? 0.0 : t1[s][1].y;
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int a = 0; a < 2; a++)
+#pragma unroll
+                        for (int b = 0; b < 2; b++)
+                            accX[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(ta[a][i], ja[b][i], accX[a][b], 0, 0, 0);
+            }
+        }
+    }
+    if (y) {  // sum the 4 k-groups of a row (lanes l, l ^ 16, l ^ 32, l ^ 48)
+        rp0 += __shfl_xor(rp0, 16);
+        rp0 += __shfl_xor(rp0, 32);
+        rp1 += __shfl_xor(rp1, 16);
+        rp1 += __shfl_xor(rp1, 32);
+        if (l < 16) {
+            s_rp[w][l] = rp0;
+            s_rp[w][16 + l] = rp1;
+        }
+    }
+    // diagonal tile: lower quadrants only (the upper one mirrors (1,0))
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) {
+            if (b > a) continue;
+#pragma unroll
+            for (int q = 0; q < 4; q++) sP[w][16 * a + (l >> 4) + 4 * q][16 * b + (l & 15)] = accT[a][b][q];
+        }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int e = threadIdx.x + 256 * q, r = e >> 5, c = e & 31;
+        const double sum = (c <= r) ? ((sP[0][r][c] + sP[1][r][c]) + sP[2][r][c]) + sP[3][r][c] : 0.0;
+        sT[r][c] = (C0 + r < n && C0 + c < n) ? aT[q] - sum : (r == c ? 1.0 : 0.0);
+    }
+    if (!two) return;
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) sP[w][16 * a + (l >> 4) + 4 * q][16 * b + (l & 15)] = accX[a][b][q];
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int e = threadIdx.x + 256 * q, r = e >> 5, c = e & 31;
+        const double sum = ((sP[0][r][c] + sP[1][r][c]) + sP[2][r][c]) + sP[3][r][c];
+        sX[r][c] = (R0 + r < n && C0 + c < n) ? aX[q] - sum : 0.0;
     }
 }
 
-// Backward substitution L^T x = y (y in x after the fused forward pass), one 1024-thread
-// workgroup, blocked by 32: for block k (last to first) the right-hand side
-// y_k - sum_{rows below} L[row][k-block]^T x_row is reduced by all threads (LDS), then one wave
-// solves the 32x32 upper-triangular block with readlane broadcasts.
+// 1 / d to full double precision: v_rcp_f64 and two Newton steps
+__device__ __forceinline__ double rcp_nr(double d)
+{
+    double r = __builtin_amdgcn_rcp(d);
+    r = fma(r, fma(-d, r, 1.0), r);
+    r = fma(r, fma(-d, r, 1.0), r);
+    return r;
+}
+
+// Column block j (rows/cols k0 = 32 j ..), left-looking: every previous column block is final.
+//  1. T = A_jj - sum_{m < k0} L_jm L_jm^T (every workgroup) and, in workgroup t > 0,
+//     X = A_tj - sum_{m < k0} L_tm L_jm^T (tile_left_update2, FP64 MFMA); workgroup 0 also
+//     reduces b_j - sum_{m < k0} L_jm y_m from the same operand registers.
+//  2. T = Lt D Lt^T by elimination in LDS, one barrier per column; the same row operations
+//     applied to the identity give M = Lt^-1, so L_jj^-1 = D^-1/2 M without a triangular solve.
+//  3. workgroup 0: L_jj^-1 -> Linv, y_j = L_jj^-1 rhs -> x;  workgroup t > 0: L_tj = X L_jj^-T
+//     (MFMA) written over A_tj.  A_jj itself is never written (nothing downstream needs L_jj).
+__global__ __launch_bounds__(256) void k_chol_col(LbaDev D, int j)
+{
+    __shared__ double sP[4][CB][CB + 1];  // per-wave partial tiles
+    __shared__ double sG[CB][CB + 1];     // T under elimination
+    __shared__ double sM[CB][CB + 1];     // Lt^-1, then L_jj^-1
+    __shared__ double sX[CB][CB + 1];     // X (t > 0)
+    __shared__ double s_rsq[CB];          // D^-1/2
+    __shared__ double s_d[CB];            // pivots
+    __shared__ double s_rp[4][CB];
+    __shared__ double s_rhs[CB];
+    const int n = 6 * D.nhp;
+    const double *A = D.Hs;
+    const int k0 = j * CB;
+    const int nb = min(CB, n - k0);
+    const int t = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int R0 = k0 + t * CB;
+    unsigned long long *ts = (D.tstamp && t < 2 && tid == 0) ? D.tstamp + 8 * (2 * j + t) : nullptr;
+    if (ts) ts[0] = wall_clock64();
+
+    const double bj = (t == 0 && tid < nb) ? D.bs[k0 + tid] : 0.0;
+    for (int e = tid; e < CB * (CB + 1); e += 256) (&sM[0][0])[e] = 0.0;
+    tile_left_update2(A, n, k0, t > 0 ? R0 : -1, k0, t == 0 ? D.x : nullptr, sG, sX, sP, s_rp);
+    if (tid < CB) sM[tid][tid] = 1.0;
+    __syncthreads();
+    if (ts) ts[1] = wall_clock64();
+
+    // Elimination two columns per barrier (2x2 pivot block c, c + 1, redundantly in every thread):
+    //   d0 = g_cc, l10 = g_c+1,c / d0, d1 = g_c+1,c+1 - g_c+1,c l10, g'_i,c+1 = g_i,c+1 - g_ic l10
+    //   G: g_i,jj -= g_ic g_jj,c / d0 + g'_i,c+1 g'_jj,c+1 / d1        (c + 1 < jj <= i)
+    //   M: m_i,m  -= g_ic / d0 m_c,m + g'_i,c+1 / d1 (m_c+1,m - l10 m_c,m)  (i > c + 1, m <= c + 1)
+    //      m_c+1,m -= l10 m_c,m (m <= c): written one step later (other threads read row c + 1 now;
+    //      nothing reads it in the next step).  Pivots go to s_d (the diagonal of G is read now).
+    // An odd nb pairs its last column with padding column nb (identity: l10 = 0, d1 = 1).
+    const int jj = tid & 31, ib = tid >> 5;
+    int ok = 1;
+    double defer_val = 0.0;
+    int defer_at = -1;  // index into sM of the deferred row-(c+1) value
+    for (int c = 0; c < nb; c += 2) {
+        if (defer_at >= 0) (&sM[0][0])[defer_at] = defer_val;
+        defer_at = -1;
+        const double d0 = sG[c][c], e = sG[c + 1][c], d1r = sG[c + 1][c + 1];
+        const double gj0 = sG[jj][c], gj1 = sG[jj][c + 1];
+        const double mc = sM[c][jj], mc1 = sM[c + 1][jj];
+        double *const base = (jj > c + 1) ? &sG[0][0] : &sM[0][0];
+        double gi0[4], gi1[4], cur[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int i = ib + 8 * q;
+            gi0[q] = sG[i][c];
+            gi1[q] = sG[i][c + 1];
+            cur[q] = base[i * (CB + 1) + jj];
+        }
+        const double r0 = rcp_nr(d0 > 0.0 ? d0 : 1.0);
+        const double l10 = e * r0;
+        const double d1 = d1r - e * l10;
+        ok &= (d0 > 0.0) & (d1 > 0.0);
+        const double r1 = rcp_nr(d1 > 0.0 ? d1 : 1.0);
+        if (tid == 0) {
+            s_d[c] = d0;
+            s_d[c + 1] = d1;
+        }
+        const double gj1p = gj1 - gj0 * l10;
+        const double mc1p = mc1 - l10 * mc;
+        const bool gcol = jj > c + 1;
+        const double a0 = gcol ? gj0 * r0 : mc * r0;     // coefficient of g_ic
+        const double a1 = gcol ? gj1p * r1 : mc1p * r1;  // coefficient of g'_i,c+1
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int i = ib + 8 * q;
+            const double gi1p = gi1[q] - gi0[q] * l10;
+            const double v = cur[q] - gi0[q] * a0 - gi1p * a1;
+            if (i < nb && i > c + 1 && jj <= i) base[i * (CB + 1) + jj] = v;
+            if (i == c + 1 && i < nb && jj <= c) {
+                defer_val = mc1p;
+                defer_at = i * (CB + 1) + jj;
+            }
+        }
+        __syncthreads();
+    }
+    if (defer_at >= 0) (&sM[0][0])[defer_at] = defer_val;
+    __syncthreads();
+    if (tid < CB) {
+        const double d = s_d[tid];
+        s_rsq[tid] = (tid < nb && d > 0.0) ? 1.0 / sqrt(d) : 1.0;
+    }
+    __syncthreads();
+    // L_jj^-1 = D^-1/2 M (lower)
+    for (int e = tid; e < CB * CB; e += 256) {
+        const int i = e >> 5, m = e & 31;
+        sM[i][m] = (m <= i) ? sM[i][m] * s_rsq[i] : 0.0;
+    }
+    __syncthreads();
+    if (ts) ts[2] = wall_clock64();
+
+    if (t == 0) {
+        if (tid == 0 && !ok) D.flag[0] = 0;
+        for (int e = tid; e < CB * CB; e += 256) {
+            const int r = e >> 5, c = e & 31;
+            if (k0 + r < n) D.Linv[(size_t)(k0 + r) * CB + c] = sM[r][c];
+        }
+        if (tid < CB) s_rhs[tid] = (tid < nb) ? bj - (((s_rp[0][tid] + s_rp[1][tid]) + s_rp[2][tid]) + s_rp[3][tid]) : 0.0;
+        __syncthreads();
+        // y_i = sum_{m <= i} Linv[i][m] rhs_m, 8 threads per row
+        {
+            const int i = tid >> 3, p = tid & 7;
+            double acc = 0.0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) acc += sM[i][p + 8 * q] * s_rhs[p + 8 * q];
+            acc += __shfl_xor(acc, 1);
+            acc += __shfl_xor(acc, 2);
+            acc += __shfl_xor(acc, 4);
+            if (p == 0 && i < nb) D.x[k0 + i] = acc;
+        }
+        if (ts) ts[3] = ts[4] = wall_clock64();
+        return;
+    }
+    // L_tj = X L_jj^-T on MFMA: quadrant (qr, qc) per wave, A = X rows, B[k][c] = Linv[c][k]
+    {
+        const int w = tid >> 6, l = tid & 63;
+        const int qr = (w >> 1) * 16, qc = (w & 1) * 16;
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int ks = 0; ks < CB / 4; ks++) {
+            const int k = 4 * ks + (l >> 4);
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sX[qr + (l & 15)][k], sM[qc + (l & 15)][k], acc, 0, 0, 0);
+        }
+        const int c = qc + (l & 15);
+        double *Aw = D.Hs;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int r = qr + (l >> 4) + 4 * q;
+            if (R0 + r < n && c < nb) Aw[(size_t)(R0 + r) * n + k0 + c] = acc[q];
+        }
+    }
+    if (ts) ts[3] = ts[4] = wall_clock64();
+}
+
+// Backward substitution L^T x = y (y in x after the column launches), one 1024-thread
+// workgroup, blocked by 32 from the last block: rhs_k = y_k - sum_{rows below} L[row][k]^T x_row
+// (all threads, LDS partials), then x_k = L_kk^-T rhs_k (32 threads).  Linv and y are staged in
+// LDS once; the L rows of the next block are loaded while the current block is being solved.
+constexpr int BK_ROWS = CMAX / 32;  // rows per thread per block at most
+
+// Workgroup barrier for LDS traffic only: __syncthreads() also waits for every outstanding global
+// load (vmcnt(0)), which would drain the prefetch of the next block's rows each block.
+__device__ __forceinline__ void lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 __global__ __launch_bounds__(1024) void k_chol_back(LbaDev D)
 {
     __shared__ double s_x[CMAX];
+    __shared__ double s_y[CMAX];
+    __shared__ double s_li[CMAX * CB];
     __shared__ double s_part[32][33];
+    __shared__ double s_rhs[CB];
     const int n = 6 * D.nhp;
     const double *A = D.Hs;
     const int tid = threadIdx.x;
-    for (int i = tid; i < n; i += 1024) s_x[i] = 0.0;
-    __syncthreads();
+    // staging: every load issued before the first LDS store (a load -> store loop would pay one
+    // memory latency per iteration)
+    {
+        constexpr int NL = CMAX * CB / 1024;
+        double v[NL];
+#pragma unroll
+        for (int k = 0; k < NL; k++) v[k] = D.Linv[min(tid + 1024 * k, n * CB - 1)];
+        const double yv = D.x[min(tid, n - 1)];
+#pragma unroll
+        for (int k = 0; k < NL; k++)
+            if (tid + 1024 * k < n * CB) s_li[tid + 1024 * k] = v[k];
+        if (tid < n) {
+            s_x[tid] = 0.0;
+            s_y[tid] = yv;
+        }
+    }
     const int nblk = (n + CB - 1) / CB;
-    for (int bi = nblk - 1; bi >= 0; bi--) {
+    const int c = tid & 31, g = tid >> 5;  // 32 groups of rows
+    double cur[BK_ROWS];
+    // unconditional (clamped) loads: branch-free, so the prefetch keeps counted waits
+    auto load_block = [&](int bi, double (&v)[BK_ROWS]) {
+        const int k0 = bi * CB, nb = min(CB, n - k0);
+        const int cc = k0 + min(c, nb - 1);
+#pragma unroll
+        for (int i = 0; i < BK_ROWS; i++) {
+            const int row = min(k0 + nb + g + 32 * i, n - 1);
+            v[i] = A[(size_t)row * n + cc];
+        }
+    };
+    // one block: rows below from v (loaded one block earlier), the next block's rows into w
+    unsigned long long *ts = (D.tstamp && tid == 0) ? D.tstamp + 8 * 2 * 32 : nullptr;  // after k_chol_col's
+    if (ts) ts[0] = wall_clock64();
+    auto solve_block = [&](int bi, const double (&v)[BK_ROWS], double (&w)[BK_ROWS]) {
+        if (ts) ts[1 + bi] = wall_clock64();
         const int k0 = bi * CB;
         const int nb = min(CB, n - k0);
-        {
-            const int c = tid & 31, g = tid >> 5;  // 32 groups of rows
-            double acc = 0.0;
-            if (c < nb)
-                for (int row = k0 + nb + g; row < n; row += 32) acc += A[(size_t)row * n + k0 + c] * s_x[row];
-            s_part[c][g] = acc;
-        }
-        __syncthreads();
-        if (tid < 64) {
-            const int r = tid;
-            double rhs = 0.0;
-            if (r < nb) {
-                double t = 0.0;
-                for (int g = 0; g < 32; g++) t += s_part[r][g];
-                rhs = D.x[k0 + r] - t;  // y_k from the panel pass
-            }
-            double Lc[CB];
+        load_block(max(bi - 1, 0), w);  // unconditional; stays in flight: only LDS barriers below
+        double acc = 0.0;
 #pragma unroll
-            for (int c = 0; c < CB; c++) Lc[c] = (r < nb && c < nb && c >= r) ? D.Lkk[(size_t)(k0 + c) * CB + r] : 0.0;
-            double xv = rhs;
-#pragma unroll
-            for (int c = CB - 1; c >= 0; c--) {
-                if (c < nb) {
-                    const double xc = readlane_d(xv, c) / readlane_d(Lc[c], c);  // L[c][c] in lane c
-                    if (r == c) xv = xc;
-                    else if (r < c) xv -= Lc[c] * xc;  // L^T[r][c] = L[c][r]
-                }
-            }
-            if (r < nb) s_x[k0 + r] = xv;
+        for (int i = 0; i < BK_ROWS; i++) {
+            const int row = k0 + nb + g + 32 * i;
+            const bool ok = row < n && c < nb;
+            acc += (ok ? v[i] : 0.0) * s_x[ok ? row : 0];
         }
-        __syncthreads();
+        s_part[c][g] = acc;
+        lds_barrier();
+        if (tid < CB) {
+            double s = 0.0;
+#pragma unroll
+            for (int gg = 0; gg < 32; gg++) s += s_part[tid][gg];
+            s_rhs[tid] = (tid < nb) ? s_y[k0 + tid] - s : 0.0;  // zero-padded past nb
+        }
+        lds_barrier();
+        if (tid < nb) {
+            // Linv is zero above its diagonal and s_rhs past nb: no predicates, so the 32 LDS
+            // reads pipeline instead of one branch + wait each
+            double xv = 0.0;
+#pragma unroll
+            for (int r = 0; r < CB; r++) xv += s_li[min(k0 + r, n - 1) * CB + tid] * s_rhs[r];
+            s_x[k0 + tid] = xv;
+        }
+        lds_barrier();
+    };
+    double alt[BK_ROWS];
+    load_block(nblk - 1, cur);
+    __syncthreads();
+    if (ts) ts[41] = wall_clock64();
+    // ping-pong between cur and alt (a register copy would wait for the prefetch to land)
+    for (int bi = nblk - 1; bi >= 0; bi -= 2) {
+        solve_block(bi, cur, alt);
+        if (bi - 1 >= 0) solve_block(bi - 1, alt, cur);
     }
+    if (ts) ts[40] = wall_clock64();
     for (int i = tid; i < n; i += 1024) D.x[i] = s_x[i];
 }
 
@@ -688,7 +911,10 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
             return osg_set_error(ctx, OSG_E_INVALID, "edge %d references out of range", e);
     }
     // ---------------------------------------------------------------- structure (host)
-    static const bool prof = getenv("OSG_LBA_PROFILE") && atoi(getenv("OSG_LBA_PROFILE"));
+    static const int prof_level = getenv("OSG_LBA_PROFILE") ? atoi(getenv("OSG_LBA_PROFILE")) : 0;
+    static const bool prof = prof_level > 0;
+    const bool prof_ts = prof_level >= 2;
+    int ts_printed = 0;
     const auto tp0 = std::chrono::steady_clock::now();
     auto ms_since = [&](std::chrono::steady_clock::time_point t) {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
@@ -870,8 +1096,9 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
         carve<double>(z, st_bytes, 3 * (size_t)NPART + 64);        // partials
         carve<double>(z, st_bytes, 36 * (size_t)std::max(nchunks, 1));  // chunk partials
         carve<double>(z, st_bytes, 3 * (size_t)nhl);                     // db
-        carve<double>(z, st_bytes, (size_t)sp * CB);                     // Lkk
+        carve<double>(z, st_bytes, (size_t)sp * CB);                     // Linv
         carve<int>(z, st_bytes, 16);                                // flags
+        if (prof_ts) carve<unsigned long long>(z, st_bytes, 8 * 2 * 64 + 64);  // phase timestamps
         carve<uint8_t>(z, st_bytes, ne);                            // edge_bad
         st_bytes += 256;
     }
@@ -935,8 +1162,10 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
     D.blk_e = osg_dptr<int32_t>(din, o_blke);
     D.db = carve<double>(dst, off, 3 * (size_t)nhl);
     D.pair_chunk = osg_dptr<int32_t>(din, o_pch);
-    D.Lkk = carve<double>(dst, off, (size_t)sp * CB);
+    D.Linv = carve<double>(dst, off, (size_t)sp * CB);
     D.flag = carve<int>(dst, off, 16);
+    D.tstamp = nullptr;
+    if (prof_ts) D.tstamp = carve<unsigned long long>(dst, off, 8 * 2 * 64 + 64);
     uint8_t *d_bad = carve<uint8_t>(dst, off, ne);
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(poseA, din + o_pose0, 56 * (size_t)np, hipMemcpyDeviceToDevice, ctx->stream));
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(pointA, din + o_point0, 24 * (size_t)npt, hipMemcpyDeviceToDevice, ctx->stream));
@@ -1013,12 +1242,9 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
                 hipLaunchKernelGGL(k_schur_pairs, dim3((npairs * 64 + 255) / 256), dim3(256), 0, ctx->stream, D, lambda);
                 hipLaunchKernelGGL(k_bschur, dim3(nhp), dim3(256), 0, ctx->stream, D);
                 const int nred = 6 * nhp;
-                for (int k0 = 0; k0 < nred; k0 += CB) {
-                    const int rb = (nred - k0 + CB - 1) / CB;  // row blocks at and below the diagonal
-                    hipLaunchKernelGGL(k_chol_panel, dim3(rb), dim3(64), 0, ctx->stream, D, k0);
-                    const int t = (nred - k0 - CB + CB - 1) / CB;
-                    if (t > 0) hipLaunchKernelGGL(k_chol_syrk, dim3(t * (t + 1) / 2), dim3(256), 0, ctx->stream, D, k0);
-                }
+                const int nblk_red = (nred + CB - 1) / CB;
+                for (int jb = 0; jb < nblk_red; jb++)  // row blocks at and below the diagonal block
+                    hipLaunchKernelGGL(k_chol_col, dim3(nblk_red - jb), dim3(256), 0, ctx->stream, D, jb);
                 hipLaunchKernelGGL(k_chol_back, dim3(1), dim3(1024), 0, ctx->stream, D);
             }
             D.pose_new = new_pose;
@@ -1031,6 +1257,26 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
             int hflag = 1;
             if (nhp > 0) OSG_HIP_CHECK(ctx, hipMemcpyAsync(&hflag, D.flag, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
             OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+            if (prof_ts && !ts_printed && nhp > 0) {
+                ts_printed = 1;
+                const int nbr = (6 * nhp + CB - 1) / CB;
+                std::vector<unsigned long long> h(8 * 2 * nbr);
+                OSG_HIP_CHECK(ctx, hipMemcpy(h.data(), D.tstamp, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+                {
+                    std::vector<unsigned long long> hb(64);
+                    OSG_HIP_CHECK(ctx, hipMemcpy(hb.data(), D.tstamp + 8 * 2 * 32, sizeof(unsigned long long) * 64, hipMemcpyDeviceToHost));
+                    fprintf(stderr, "[osg back] staging %.2f us;", (hb[41] - hb[0]) * 0.01);
+                    for (int bb = nbr - 1; bb >= 0; bb--)
+                        fprintf(stderr, " b%d@%.2f", bb, (hb[1 + bb] - hb[0]) * 0.01);
+                    fprintf(stderr, " end@%.2f\n", (hb[40] - hb[0]) * 0.01);
+                }
+                for (int jb = 0; jb < nbr; jb++)
+                    for (int tt = 0; tt < 2 && tt < nbr - jb; tt++) {
+                        const unsigned long long *q = &h[8 * (2 * jb + tt)];
+                        fprintf(stderr, "[osg chol] j=%d wg=%d gemm %.2f factor+inverse %.2f tail %.2f us\n", jb, tt,
+                                (q[1] - q[0]) * 0.01, (q[2] - q[1]) * 0.01, (q[3] - q[2]) * 0.01);
+                    }
+            }
             double tempChi = sum_part(0, ge);
             if (!hflag) tempChi = DBL_MAX;
             rho = currentChi - tempChi;
