@@ -1,0 +1,636 @@
+// osg_orbslam3.h — ORB-SLAM3 side of the drop-in: gathers the reference's objects into the
+// plain arrays of the C ABI (include/osg.h, include/osg_ba.h), calls it, and writes the results
+// back the way the reference does.  Header-only C++17 templates over the reference's own member
+// names (Frame, KeyFrame, MapPoint, cv::Mat, cv::KeyPoint, DBoW2::FeatureVector), so the same code
+// compiles inside an ORB-SLAM3 tree (adapters/orbslam3/ORBmatcher_osg.cc, Optimizer_osg.cc) and
+// against the POD mocks of tests/adapter/mock_orbslam3.h.
+//
+// The few places where the reference uses Sophus / Eigen / its camera classes go through a hook
+// policy H (static member functions), defined by the integration with the reference's own code:
+//
+//   static void  H::pose(const Frame|KeyFrame&, double q[7])         GetPose() -> {qx qy qz qw tx ty tz}
+//   static void  H::set_pose(Frame|KeyFrame&, const double q[7])     SetPose(SE3f(q, t))
+//   static void  H::world_pos(MapPoint*, double x[3])                GetWorldPos().cast<double>()
+//   static void  H::set_world_pos(MapPoint*, const double x[3])      SetWorldPos + UpdateNormalAndDepth
+//   static void  H::camera(const Frame|KeyFrame&, bool right, osg_camera&)
+//                mpCamera / mpCamera2 type + parameters, fx fy cx cy mbf, GetRelativePoseTrl()
+//   static bool  H::project_last(const Frame& CF, MapPoint*, float& u, float& v, float& invz)
+//                ref:src/ORBmatcher.cc:1993-2009 (Tcw * x3Dw, invzc, mpCamera->project); false = skip
+//   static float H::tlc_z(const Frame& CF, const Frame& LF)          (Tlw * twc)(2), ref:src/ORBmatcher.cc:1972-1980
+//   static bool  H::kf_query(const Frame& CF, MapPoint*, float& u, float& v, int& level)
+//                ref:src/ORBmatcher.cc:2238-2262 (project, image bounds, distance range, PredictScale)
+#ifndef OSG_ORBSLAM3_H
+#define OSG_ORBSLAM3_H
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <list>
+#include <map>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <tuple>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "osg.h"
+#include "osg_ba.h"
+
+namespace osg_orbslam3 {
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string &what) : std::runtime_error(what), code(c) {}
+};
+
+// One context per host thread: Tracking, LocalMapping and LoopClosing each get their own stream
+// and scratch (ref:src/System.cc:234,254 start them as separate threads).
+inline osg_ctx *thread_ctx(int device = 0)
+{
+    struct Holder {
+        osg_ctx *ctx = nullptr;
+        ~Holder()
+        {
+            if (ctx) osg_ctx_destroy(ctx);
+        }
+    };
+    static thread_local Holder h;
+    if (!h.ctx) {
+        const int rc = osg_ctx_create(device, &h.ctx);
+        if (rc < 0) throw Error(rc, std::string("osg_ctx_create: ") + osg_strerror(rc));
+    }
+    return h.ctx;
+}
+
+inline int check(osg_ctx *ctx, int rc, const char *what)
+{
+    if (rc < 0) throw Error(rc, std::string(what) + ": " + osg_strerror(rc) + " (" + osg_ctx_last_error(ctx) + ")");
+    return rc;
+}
+
+// ---------------------------------------------------------------------------------- gathering
+template <class KeyPointT>
+inline void push_kp(const KeyPointT &kp, std::vector<float> &x, std::vector<float> &y, std::vector<float> &a,
+                    std::vector<int32_t> &o)
+{
+    x.push_back(kp.pt.x);
+    y.push_back(kp.pt.y);
+    a.push_back(kp.angle);
+    o.push_back(kp.octave);
+}
+
+template <class MatT>
+inline void copy_desc_rows(const MatT &m, int n, std::vector<uint8_t> &out)
+{
+    out.resize((size_t)n * 32);
+    for (int i = 0; i < n; i++) std::memcpy(&out[(size_t)32 * i], m.template ptr<unsigned char>(i), 32);
+}
+
+// osg_frame of a Frame (ref:include/Frame.h:218-296): keypoints (mvKeysUn, or mvKeys + mvKeysRight
+// for a two-camera rig), descriptors, mvuRight, the 64 x 48 grid as CSR in GetFeaturesInArea's
+// enumeration order (ix outer, iy inner, cell contents in insertion order).
+template <class FrameT>
+struct FrameView {
+    std::vector<float> kx, ky, ka, ur, scale;
+    std::vector<int32_t> ko, gs, gi;
+    std::vector<uint8_t> desc;
+    osg_frame v{};
+
+    explicit FrameView(const FrameT &F)
+    {
+        const int n = F.N;
+        if (F.Nleft == -1) {
+            for (int i = 0; i < n; i++) push_kp(F.mvKeysUn[i], kx, ky, ka, ko);
+        } else {
+            for (int i = 0; i < F.Nleft; i++) push_kp(F.mvKeys[i], kx, ky, ka, ko);
+            for (int i = F.Nleft; i < n; i++) push_kp(F.mvKeysRight[i - F.Nleft], kx, ky, ka, ko);
+        }
+        copy_desc_rows(F.mDescriptors, n, desc);
+        ur.assign(F.mvuRight.begin(), F.mvuRight.end());
+        ur.resize(n, -1.0f);
+        gs.assign(OSG_GRID_CELLS + 1, 0);
+        for (int ix = 0; ix < OSG_GRID_COLS; ix++)
+            for (int iy = 0; iy < OSG_GRID_ROWS; iy++) {
+                const auto &cell = F.mGrid[ix][iy];
+                gs[ix * OSG_GRID_ROWS + iy + 1] = (int32_t)cell.size();
+                for (auto idx : cell) gi.push_back((int32_t)idx);
+            }
+        for (int c = 0; c < OSG_GRID_CELLS; c++) gs[c + 1] += gs[c];
+        scale.assign(F.mvScaleFactors.begin(), F.mvScaleFactors.end());
+        v.n = n;
+        v.nleft = F.Nleft;
+        v.desc = desc.data();
+        v.kp_x = kx.data();
+        v.kp_y = ky.data();
+        v.kp_angle = ka.data();
+        v.kp_octave = ko.data();
+        v.u_right = ur.data();
+        v.grid_start = gs.data();
+        v.grid_idx = gi.data();
+        v.min_x = F.mnMinX;
+        v.max_x = F.mnMaxX;
+        v.min_y = F.mnMinY;
+        v.max_y = F.mnMaxY;
+        v.grid_inv_w = F.mfGridElementWidthInv;
+        v.grid_inv_h = F.mfGridElementHeightInv;
+        v.scale_factors = scale.data();
+        v.n_levels = F.mnScaleLevels;
+        v.mb = F.mb;
+        v.mbf = F.mbf;
+    }
+};
+
+// Slot state of Frame::mvpMapPoints with stable ids: ids [0, nq) are the caller's query MapPoints,
+// a slot already holding another MapPoint gets id nq + slot.
+template <class MapPointT>
+struct Slots {
+    std::vector<int32_t> mp;
+    std::vector<uint8_t> taken;
+    std::vector<MapPointT *> occupant;
+    Slots(const std::vector<MapPointT *> &slots, int nq, bool need_obs)
+    {
+        const int n = (int)slots.size();
+        mp.assign(n, -1);
+        taken.assign(n, 0);
+        occupant = slots;
+        for (int i = 0; i < n; i++)
+            if (slots[i]) {
+                mp[i] = nq + i;
+                taken[i] = need_obs ? (slots[i]->Observations() > 0) : 1;
+            }
+    }
+    // writes back the slots whose id changed; returns nothing (the count comes from the ABI)
+    template <class QueryPtrVec>
+    void apply(std::vector<MapPointT *> &slots, const QueryPtrVec &queries, int nq) const
+    {
+        for (size_t i = 0; i < slots.size(); i++) {
+            const int id = mp[i];
+            if (id < 0) slots[i] = nullptr;
+            else if (id < nq) slots[i] = queries[id];
+            else slots[i] = occupant[id - nq];
+        }
+    }
+};
+
+// ---------------------------------------------------------------------- a1 DescriptorDistance
+template <class MatT>
+inline int descriptor_distance(const MatT &a, const MatT &b)
+{
+    return osg_descriptor_distance(a.template ptr<unsigned char>(0), b.template ptr<unsigned char>(0));
+}
+
+// ---------------------------------------------- a5 SearchByProjection(Frame&, vector<MapPoint*>)
+// ref:src/ORBmatcher.cc:44-242
+template <class H, class FrameT, class MapPointT>
+int search_by_projection_mps(FrameT &F, const std::vector<MapPointT *> &vpMapPoints, float th, bool bFarPoints,
+                             float thFarPoints, float nnratio)
+{
+    osg_ctx *ctx = thread_ctx();
+    FrameView<FrameT> fv(F);
+    const int nq = (int)vpMapPoints.size();
+    std::vector<int32_t> id(nq), lvl(nq), lvl_r(nq);
+    std::vector<uint8_t> desc((size_t)nq * 32), usable(nq), has_obs(nq), in_view(nq), in_view_r(nq);
+    std::vector<float> px(nq), py(nq), pxr(nq), pyr(nq), vc(nq), vcr(nq), depth(nq);
+    for (int i = 0; i < nq; i++) {
+        MapPointT *p = vpMapPoints[i];
+        id[i] = i;
+        in_view[i] = p->mbTrackInView;
+        in_view_r[i] = p->mbTrackInViewR;
+        if (!in_view[i] && !in_view_r[i]) continue;  // the reference skips before any other read
+        usable[i] = !p->isBad();
+        has_obs[i] = p->Observations() > 0;
+        const auto d = p->GetDescriptor();
+        std::memcpy(&desc[(size_t)32 * i], d.template ptr<unsigned char>(0), 32);
+        px[i] = p->mTrackProjX;
+        py[i] = p->mTrackProjY;
+        pxr[i] = p->mTrackProjXR;
+        pyr[i] = p->mTrackProjYR;
+        vc[i] = p->mTrackViewCos;
+        vcr[i] = p->mTrackViewCosR;
+        lvl[i] = p->mnTrackScaleLevel;
+        lvl_r[i] = p->mnTrackScaleLevelR;
+        depth[i] = p->mTrackDepth;
+    }
+    osg_mp_queries q{};
+    q.n = nq;
+    q.mp_id = id.data();
+    q.desc = desc.data();
+    q.usable = usable.data();
+    q.has_obs = has_obs.data();
+    q.in_view = in_view.data();
+    q.proj_x = px.data();
+    q.proj_y = py.data();
+    q.proj_xr = pxr.data();
+    q.view_cos = vc.data();
+    q.pred_level = lvl.data();
+    q.track_depth = depth.data();
+    q.in_view_r = in_view_r.data();
+    q.proj_yr = pyr.data();
+    q.view_cos_r = vcr.data();
+    q.pred_level_r = lvl_r.data();
+    Slots<MapPointT> slots(F.mvpMapPoints, nq, true);
+    const int nm = check(ctx, osg_search_by_projection_mps(ctx, &fv.v, &q, nnratio, th, bFarPoints, thFarPoints,
+                                                           slots.mp.data(), slots.taken.data()),
+                         "osg_search_by_projection_mps");
+    slots.apply(F.mvpMapPoints, vpMapPoints, nq);
+    return nm;
+}
+
+// ------------------------------------------------- a6 SearchByProjection(Frame&, const Frame&)
+// ref:src/ORBmatcher.cc:1957-2191
+template <class H, class FrameT>
+int search_by_projection_last(FrameT &CF, const FrameT &LF, float th, bool bMono, bool checkOri)
+{
+    using MapPointT = typename std::remove_pointer<typename std::decay<decltype(LF.mvpMapPoints[0])>::type>::type;
+    osg_ctx *ctx = thread_ctx();
+    FrameView<FrameT> fv(CF);
+    const int n = LF.N;
+    std::vector<int32_t> id(n, -1), oct(n, 0);
+    std::vector<uint8_t> desc((size_t)n * 32), valid(n, 0), has_obs(n, 0);
+    std::vector<float> u(n), v(n), invz(n), ang(n);
+    std::vector<MapPointT *> queries(n, nullptr);
+    for (int i = 0; i < n; i++) {
+        MapPointT *p = LF.mvpMapPoints[i];
+        const auto &kp = (LF.Nleft == -1) ? LF.mvKeysUn[i]
+                                          : (i < LF.Nleft ? LF.mvKeys[i] : LF.mvKeysRight[i - LF.Nleft]);
+        oct[i] = (LF.Nleft == -1 || i < LF.Nleft) ? LF.mvKeys[i].octave : LF.mvKeysRight[i - LF.Nleft].octave;
+        ang[i] = kp.angle;
+        if (!p || LF.mvbOutlier[i]) continue;
+        if (!H::project_last(CF, p, u[i], v[i], invz[i])) continue;
+        valid[i] = 1;
+        id[i] = i;
+        queries[i] = p;
+        has_obs[i] = p->Observations() > 0;
+        const auto d = p->GetDescriptor();
+        std::memcpy(&desc[(size_t)32 * i], d.template ptr<unsigned char>(0), 32);
+    }
+    osg_last_queries q{};
+    q.n = n;
+    q.mp_id = id.data();
+    q.desc = desc.data();
+    q.valid = valid.data();
+    q.has_obs = has_obs.data();
+    q.u = u.data();
+    q.v = v.data();
+    q.invz = invz.data();
+    q.octave = oct.data();
+    q.angle = ang.data();
+    q.tlc_z = H::tlc_z(CF, LF);
+    Slots<MapPointT> slots(CF.mvpMapPoints, n, true);
+    const int nm = check(ctx, osg_search_by_projection_last(ctx, &fv.v, &q, th, bMono, checkOri, slots.mp.data(),
+                                                            slots.taken.data()),
+                         "osg_search_by_projection_last");
+    slots.apply(CF.mvpMapPoints, queries, n);
+    return nm;
+}
+
+// ---------------------------------- a7 SearchByProjection(Frame&, KeyFrame*, set<MapPoint*>, ...)
+// ref:src/ORBmatcher.cc:2203-2330
+template <class H, class FrameT, class KeyFrameT, class MapPointT>
+int search_by_projection_kf(FrameT &CF, KeyFrameT *pKF, const std::set<MapPointT *> &sAlreadyFound, float th,
+                            int ORBdist, bool checkOri)
+{
+    osg_ctx *ctx = thread_ctx();
+    FrameView<FrameT> fv(CF);
+    const std::vector<MapPointT *> vpMPs = pKF->GetMapPointMatches();
+    const int n = (int)vpMPs.size();
+    std::vector<int32_t> id(n, -1), lvl(n, 0);
+    std::vector<uint8_t> desc((size_t)n * 32), valid(n, 0);
+    std::vector<float> u(n), v(n), ang(n);
+    for (int i = 0; i < n; i++) {
+        MapPointT *p = vpMPs[i];
+        ang[i] = pKF->mvKeysUn[i].angle;
+        if (!p || p->isBad() || sAlreadyFound.count(p)) continue;
+        if (!H::kf_query(CF, p, u[i], v[i], lvl[i])) continue;
+        valid[i] = 1;
+        id[i] = i;
+        const auto d = p->GetDescriptor();
+        std::memcpy(&desc[(size_t)32 * i], d.template ptr<unsigned char>(0), 32);
+    }
+    osg_kf_queries q{};
+    q.n = n;
+    q.mp_id = id.data();
+    q.desc = desc.data();
+    q.valid = valid.data();
+    q.u = u.data();
+    q.v = v.data();
+    q.pred_level = lvl.data();
+    q.angle = ang.data();
+    Slots<MapPointT> slots(CF.mvpMapPoints, n, false);
+    const int nm = check(ctx, osg_search_by_projection_kf(ctx, &fv.v, &q, th, ORBdist, checkOri, slots.mp.data()),
+                         "osg_search_by_projection_kf");
+    slots.apply(CF.mvpMapPoints, vpMPs, n);
+    return nm;
+}
+
+// ------------------------------------------------------------------------------- a3/a4 BoW
+// DBoW2::FeatureVector (std::map<NodeId, vector<unsigned>>) as CSR in key order.
+template <class FeatVecT>
+struct FeatVecCSR {
+    std::vector<uint32_t> node;
+    std::vector<int32_t> start, feat;
+    explicit FeatVecCSR(const FeatVecT &fvec)
+    {
+        start.push_back(0);
+        for (const auto &kv : fvec) {
+            node.push_back((uint32_t)kv.first);
+            for (auto f : kv.second) feat.push_back((int32_t)f);
+            start.push_back((int32_t)feat.size());
+        }
+    }
+    osg_featvec view() const { return osg_featvec{(int32_t)node.size(), node.data(), start.data(), feat.data()}; }
+};
+
+// ref:src/ORBmatcher.cc:262-496.  vpMapPointMatches = vector<MapPoint*>(F.N, NULL) with the KF's
+// MapPoints matched to Frame keypoints.
+template <class H, class KeyFrameT, class FrameT, class MapPointT>
+int search_by_bow_kf_f(KeyFrameT *pKF, FrameT &F, std::vector<MapPointT *> &vpMapPointMatches, float nnratio,
+                       bool checkOri)
+{
+    osg_ctx *ctx = thread_ctx();
+    const std::vector<MapPointT *> vpMPsKF = pKF->GetMapPointMatches();
+    const int nk = (int)vpMPsKF.size(), nf = F.N;
+    std::vector<uint8_t> dk, df, good(nk);
+    std::vector<float> ak(nk), af(nf);
+    std::vector<int32_t> idk(nk, -1);
+    copy_desc_rows(pKF->mDescriptors, nk, dk);
+    copy_desc_rows(F.mDescriptors, nf, df);
+    for (int i = 0; i < nk; i++) {
+        ak[i] = pKF->mvKeysUn[i].angle;
+        good[i] = vpMPsKF[i] && !vpMPsKF[i]->isBad();
+        if (vpMPsKF[i]) idk[i] = i;
+    }
+    for (int i = 0; i < nf; i++) af[i] = (F.Nleft == -1) ? F.mvKeysUn[i].angle : (i < F.Nleft ? F.mvKeys[i].angle : F.mvKeysRight[i - F.Nleft].angle);
+    FeatVecCSR<decltype(pKF->mFeatVec)> fk(pKF->mFeatVec);
+    FeatVecCSR<decltype(F.mFeatVec)> ff(F.mFeatVec);
+    osg_bow_side sk{nk, pKF->NLeft, dk.data(), ak.data(), idk.data(), good.data(), fk.view()};
+    osg_bow_side sf{nf, F.Nleft, df.data(), af.data(), nullptr, nullptr, ff.view()};
+    std::vector<int32_t> out(nf, -1);
+    const int nm = check(ctx, osg_search_by_bow_kf_f(ctx, &sk, &sf, nnratio, checkOri, out.data()), "osg_search_by_bow_kf_f");
+    vpMapPointMatches.assign(nf, nullptr);
+    for (int i = 0; i < nf; i++)
+        if (out[i] >= 0) vpMapPointMatches[i] = vpMPsKF[out[i]];
+    return nm;
+}
+
+// ref:src/ORBmatcher.cc:890-1043.  vpMatches12[i] = KF2 MapPoint matched to KF1 keypoint i.
+template <class H, class KeyFrameT, class MapPointT>
+int search_by_bow_kf_kf(KeyFrameT *pKF1, KeyFrameT *pKF2, std::vector<MapPointT *> &vpMatches12, float nnratio,
+                        bool checkOri)
+{
+    osg_ctx *ctx = thread_ctx();
+    const std::vector<MapPointT *> v1 = pKF1->GetMapPointMatches(), v2 = pKF2->GetMapPointMatches();
+    const int n1 = (int)v1.size(), n2 = (int)v2.size();
+    std::vector<uint8_t> d1, d2, g1(n1), g2(n2);
+    std::vector<float> a1(n1), a2(n2);
+    std::vector<int32_t> id1(n1, -1), id2(n2, -1);
+    copy_desc_rows(pKF1->mDescriptors, n1, d1);
+    copy_desc_rows(pKF2->mDescriptors, n2, d2);
+    for (int i = 0; i < n1; i++) {
+        a1[i] = pKF1->mvKeysUn[i].angle;
+        g1[i] = v1[i] && !v1[i]->isBad();
+        if (v1[i]) id1[i] = i;
+    }
+    for (int i = 0; i < n2; i++) {
+        a2[i] = pKF2->mvKeysUn[i].angle;
+        g2[i] = v2[i] && !v2[i]->isBad();
+        if (v2[i]) id2[i] = i;
+    }
+    FeatVecCSR<decltype(pKF1->mFeatVec)> f1(pKF1->mFeatVec);
+    FeatVecCSR<decltype(pKF2->mFeatVec)> f2(pKF2->mFeatVec);
+    osg_bow_side s1{n1, pKF1->NLeft, d1.data(), a1.data(), id1.data(), g1.data(), f1.view()};
+    osg_bow_side s2{n2, pKF2->NLeft, d2.data(), a2.data(), id2.data(), g2.data(), f2.view()};
+    std::vector<int32_t> out(n1, -1);
+    const int nm = check(ctx, osg_search_by_bow_kf_kf(ctx, &s1, &s2, nnratio, checkOri, out.data()), "osg_search_by_bow_kf_kf");
+    vpMatches12.assign(n1, nullptr);
+    for (int i = 0; i < n1; i++)
+        if (out[i] >= 0) vpMatches12[i] = v2[out[i]];
+    return nm;
+}
+
+// ------------------------------------------------------------------- a10 PoseOptimization
+// ref:src/Optimizer.cc:71-420: one edge per Frame slot holding a MapPoint, in slot order; the
+// result sets mvbOutlier and the pose and returns nInitialCorrespondences - nBad.
+template <class H, class FrameT>
+int pose_optimization(FrameT *pFrame)
+{
+    osg_ctx *ctx = thread_ctx();
+    const int N = pFrame->N;
+    std::vector<int8_t> kind;
+    std::vector<double> xw, obs;
+    std::vector<float> isig;
+    std::vector<int> slot;
+    const bool two = (bool)pFrame->mpCamera2;
+    for (int i = 0; i < N; i++) {
+        auto *pMP = pFrame->mvpMapPoints[i];
+        if (!pMP) continue;
+        double X[3];
+        H::world_pos(pMP, X);
+        int8_t k;
+        double o[3] = {0, 0, 0};
+        int oct;
+        if (!two) {
+            const auto &kp = pFrame->mvKeysUn[i];
+            k = pFrame->mvuRight[i] < 0 ? OSG_EDGE_MONO : OSG_EDGE_STEREO;
+            o[0] = kp.pt.x;
+            o[1] = kp.pt.y;
+            if (k == OSG_EDGE_STEREO) o[2] = pFrame->mvuRight[i];
+            oct = kp.octave;
+        } else if (i < pFrame->Nleft) {
+            const auto &kp = pFrame->mvKeys[i];
+            k = OSG_EDGE_MONO;
+            o[0] = kp.pt.x;
+            o[1] = kp.pt.y;
+            oct = kp.octave;
+        } else {
+            const auto &kp = pFrame->mvKeysRight[i - pFrame->Nleft];
+            k = OSG_EDGE_BODY;
+            o[0] = kp.pt.x;
+            o[1] = kp.pt.y;
+            oct = kp.octave;
+        }
+        pFrame->mvbOutlier[i] = false;
+        kind.push_back(k);
+        xw.insert(xw.end(), X, X + 3);
+        obs.insert(obs.end(), o, o + 3);
+        isig.push_back(pFrame->mvInvLevelSigma2[oct]);
+        slot.push_back(i);
+    }
+    osg_pose_problem p{};
+    H::pose(*pFrame, p.pose);
+    p.n_edges = (int32_t)kind.size();
+    p.kind = kind.data();
+    p.xw = xw.data();
+    p.obs = obs.data();
+    p.inv_sigma2 = isig.data();
+    H::camera(*pFrame, false, p.cam);
+    if (two) H::camera(*pFrame, true, p.cam2);
+    std::vector<uint8_t> outl(kind.size());
+    osg_pose_result r{};
+    r.outlier = outl.data();
+    check(ctx, osg_pose_optimization(ctx, &p, &r), "osg_pose_optimization");
+    if (p.n_edges < 3) return 0;  // ref:src/Optimizer.cc:289-290 (pose untouched)
+    for (size_t e = 0; e < slot.size(); e++) pFrame->mvbOutlier[slot[e]] = outl[e] != 0;
+    H::set_pose(*pFrame, r.pose);
+    return r.n_inliers;
+}
+
+// ---------------------------------------------------------- a11 LocalBundleAdjustment (g2o part)
+// The local window (ref:src/Optimizer.cc:1762-1873: lLocalKeyFrames, lLocalMapPoints,
+// lFixedCameras) is collected by the reference code unchanged; from the graph build on
+// (ref:src/Optimizer.cc:1877-2203) this replaces g2o.  Vertex order = g2o id order (KeyFrames by
+// mnId, MapPoints by mnId + maxKFid + 1); edges in the reference's insertion order (MapPoint list
+// order x observation map order; left/stereo edge, then the right-camera edge).
+template <class KeyFrameT, class MapPointT>
+struct LbaOutcome {
+    std::vector<std::pair<KeyFrameT *, MapPointT *>> to_erase;  // vToErase
+    std::vector<std::pair<KeyFrameT *, std::vector<double>>> poses;   // optimised local KF poses (7)
+    std::vector<std::pair<MapPointT *, std::vector<double>>> points;  // optimised MapPoints (3)
+    int num_fixedKF = 0, num_OptKF = 0, num_MPs = 0, num_edges = 0;
+    bool aborted = false;
+};
+
+template <class H, class KeyFrameT, class MapPointT, class MapT>
+LbaOutcome<KeyFrameT, MapPointT> local_bundle_adjustment(const std::list<KeyFrameT *> &lLocalKeyFrames,
+                                                         const std::list<KeyFrameT *> &lFixedCameras,
+                                                         const std::list<MapPointT *> &lLocalMapPoints,
+                                                         MapT *pCurrentMap, unsigned long initKFid,
+                                                         bool *pbStopFlag, bool bInertial)
+{
+    osg_ctx *ctx = thread_ctx();
+    LbaOutcome<KeyFrameT, MapPointT> out;
+    // vertices sorted by g2o id
+    std::vector<std::pair<unsigned long, KeyFrameT *>> kfs;
+    std::unordered_map<KeyFrameT *, int> kf_fixed;
+    unsigned long maxKFid = 0;
+    for (auto *k : lLocalKeyFrames) {
+        kfs.push_back({k->mnId, k});
+        kf_fixed[k] = (k->mnId == initKFid);
+        maxKFid = std::max(maxKFid, (unsigned long)k->mnId);
+    }
+    for (auto *k : lFixedCameras) {
+        kfs.push_back({k->mnId, k});
+        kf_fixed[k] = 1;
+        maxKFid = std::max(maxKFid, (unsigned long)k->mnId);
+    }
+    std::sort(kfs.begin(), kfs.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+    std::unordered_map<KeyFrameT *, int> kf_index;
+    std::vector<double> pose(7 * kfs.size());
+    std::vector<uint8_t> fixed(kfs.size());
+    std::vector<osg_camera> cams(2 * kfs.size());
+    for (size_t i = 0; i < kfs.size(); i++) {
+        kf_index[kfs[i].second] = (int)i;
+        H::pose(*kfs[i].second, &pose[7 * i]);
+        fixed[i] = (uint8_t)kf_fixed[kfs[i].second];
+        H::camera(*kfs[i].second, false, cams[2 * i]);
+        if (kfs[i].second->mpCamera2) H::camera(*kfs[i].second, true, cams[2 * i + 1]);
+    }
+    out.num_OptKF = (int)lLocalKeyFrames.size();
+    out.num_fixedKF = (int)lFixedCameras.size();
+    std::vector<std::pair<unsigned long, MapPointT *>> mps;
+    for (auto *p : lLocalMapPoints) mps.push_back({p->mnId, p});
+    std::sort(mps.begin(), mps.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+    std::unordered_map<MapPointT *, int> mp_index;
+    std::vector<double> point(3 * mps.size());
+    for (size_t i = 0; i < mps.size(); i++) {
+        mp_index[mps[i].second] = (int)i;
+        H::world_pos(mps[i].second, &point[3 * i]);
+    }
+    out.num_MPs = (int)mps.size();
+    std::vector<int32_t> e_point, e_pose, e_cam;
+    std::vector<int8_t> e_kind;
+    std::vector<double> e_obs;
+    std::vector<float> e_isig;
+    std::vector<std::pair<KeyFrameT *, MapPointT *>> e_pair;
+    for (auto *pMP : lLocalMapPoints) {
+        const auto observations = pMP->GetObservations();
+        for (const auto &ob : observations) {
+            KeyFrameT *pKFi = ob.first;
+            if (pKFi->isBad() || pKFi->GetMap() != pCurrentMap) continue;
+            const auto itk = kf_index.find(pKFi);
+            if (itk == kf_index.end()) continue;
+            const int leftIndex = std::get<0>(ob.second);
+            auto add = [&](int8_t kind, int cam, const auto &kp, double ur) {
+                e_point.push_back(mp_index[pMP]);
+                e_pose.push_back(itk->second);
+                e_kind.push_back(kind);
+                e_cam.push_back(cam);
+                e_obs.push_back(kp.pt.x);
+                e_obs.push_back(kp.pt.y);
+                e_obs.push_back(ur);
+                e_isig.push_back(pKFi->mvInvLevelSigma2[kp.octave]);
+                e_pair.push_back({pKFi, pMP});
+            };
+            if (leftIndex != -1 && pKFi->mvuRight[leftIndex] < 0)
+                add(OSG_EDGE_MONO, 2 * itk->second, pKFi->mvKeysUn[leftIndex], 0.0);
+            else if (leftIndex != -1 && pKFi->mvuRight[leftIndex] >= 0)
+                add(OSG_EDGE_STEREO, 2 * itk->second, pKFi->mvKeysUn[leftIndex], pKFi->mvuRight[leftIndex]);
+            if (pKFi->mpCamera2) {
+                const int rightIndex = std::get<1>(ob.second);
+                if (rightIndex != -1)
+                    add(OSG_EDGE_BODY, 2 * itk->second + 1, pKFi->mvKeysRight[rightIndex - pKFi->NLeft], 0.0);
+            }
+        }
+    }
+    out.num_edges = (int)e_kind.size();
+    if (pbStopFlag && *pbStopFlag) {
+        out.aborted = true;
+        return out;
+    }
+    osg_ba_graph g{};
+    g.n_poses = (int32_t)kfs.size();
+    g.pose = pose.data();
+    g.pose_fixed = fixed.data();
+    g.n_points = (int32_t)mps.size();
+    g.point = point.data();
+    g.n_edges = (int32_t)e_kind.size();
+    g.e_point = e_point.data();
+    g.e_pose = e_pose.data();
+    g.e_kind = e_kind.data();
+    g.e_cam = e_cam.data();
+    g.e_obs = e_obs.data();
+    g.e_inv_sigma2 = e_isig.data();
+    g.n_cams = (int32_t)cams.size();
+    g.cams = cams.data();
+    g.iterations = 10;
+    g.user_lambda_init = bInertial ? 100.0 : 0.0;
+    std::vector<double> pose_out(pose.size()), point_out(point.size());
+    std::vector<uint8_t> bad(e_kind.size());
+    osg_ba_result r{};
+    r.pose = pose_out.data();
+    r.point = point_out.data();
+    r.edge_bad = bad.data();
+    static_assert(sizeof(bool) == 1, "pbStopFlag is passed as one byte");
+    check(ctx, osg_local_bundle_adjustment(ctx, &g, &r, reinterpret_cast<const volatile uint8_t *>(pbStopFlag)),
+          "osg_local_bundle_adjustment");
+    out.aborted = r.aborted != 0;
+    // ref:src/Optimizer.cc:2125-2168: edges over the chi2 threshold or behind the camera
+    for (size_t e = 0; e < bad.size(); e++)
+        if (bad[e]) out.to_erase.push_back(e_pair[e]);
+    // only the local KeyFrames are written back (fixed cameras are not), ref:src/Optimizer.cc:2187-2203
+    for (auto *k : lLocalKeyFrames) {
+        const int i = kf_index[k];
+        out.poses.push_back({k, std::vector<double>(&pose_out[7 * i], &pose_out[7 * i] + 7)});
+    }
+    for (size_t i = 0; i < mps.size(); i++)
+        out.points.push_back({mps[i].second, std::vector<double>(&point_out[3 * i], &point_out[3 * i] + 3)});
+    return out;
+}
+
+// Applies an LbaOutcome exactly as ref:src/Optimizer.cc:2171-2203 does; the caller holds
+// pMap->mMutexMapUpdate.
+template <class H, class KeyFrameT, class MapPointT>
+void apply_local_bundle_adjustment(const LbaOutcome<KeyFrameT, MapPointT> &o)
+{
+    for (const auto &km : o.to_erase) {
+        km.first->EraseMapPointMatch(km.second);
+        km.second->EraseObservation(km.first);
+    }
+    for (const auto &kp : o.poses) H::set_pose(*kp.first, kp.second.data());
+    for (const auto &mp : o.points) H::set_world_pos(mp.first, mp.second.data());
+}
+
+}  // namespace osg_orbslam3
+#endif

@@ -101,9 +101,10 @@ typedef struct osg_ba_result {
     int32_t aborted;           /* stop flag observed */
 } osg_ba_result;
 
-/* stop_flag: the reference's pbStopFlag, polled between LM iterations and trials (may be NULL). */
+/* stop_flag: the reference's bool *pbStopFlag read as one byte (nonzero = stop), polled between LM
+ * iterations and trials (may be NULL). */
 int osg_local_bundle_adjustment(struct osg_ctx *ctx, const osg_ba_graph *g, osg_ba_result *r,
-                                const volatile int *stop_flag);
+                                const volatile uint8_t *stop_flag);
 
 #ifdef __cplusplus
 }

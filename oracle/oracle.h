@@ -35,7 +35,7 @@ int oracle_search_by_bow_kf_kf(const osg_bow_side *K1, const osg_bow_side *K2, f
 /* bundle adjustment (oracle_ba.c) */
 int oracle_pose_optimization(const osg_pose_problem *P, osg_pose_result *R);
 int oracle_local_bundle_adjustment(const osg_ba_graph *G, osg_ba_result *R,
-                                   const volatile int *stop_flag);
+                                   const volatile uint8_t *stop_flag);
 
 #ifdef __cplusplus
 }

@@ -484,7 +484,7 @@ typedef struct {
     int nBad;
     double user_lambda;
     int trials;
-    const volatile int *stop;
+    const volatile uint8_t *stop;
 } graph_t;
 
 static int cmp_int(const void *a, const void *b)
@@ -1022,7 +1022,7 @@ int oracle_pose_optimization(const osg_pose_problem *P, osg_pose_result *R)
 
 /* ---------------------------------------------------------------- LocalBundleAdjustment */
 /* ref:src/Optimizer.cc:1877-2203 (the part after the graph is gathered) */
-int oracle_local_bundle_adjustment(const osg_ba_graph *G, osg_ba_result *R, const volatile int *stop)
+int oracle_local_bundle_adjustment(const osg_ba_graph *G, osg_ba_result *R, const volatile uint8_t *stop)
 {
     const float thHuberMono = sqrt(5.991);
     const float thHuberStereo = sqrt(7.815);

@@ -886,7 +886,7 @@ T *carve(char *base, size_t &off, size_t count)
 }  // namespace
 
 extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, osg_ba_result *R,
-                                           const volatile int *stop)
+                                           const volatile uint8_t *stop)
 {
     if (!ctx) return OSG_E_INVALID;
     OSG_REQUIRE(ctx, G && R, "null argument");
@@ -938,6 +938,7 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
     const int nhp = (int)hp_pose.size(), nhl = (int)hl_point.size();
     if (nhp + nhl == 0) return 0;
     OSG_REQUIRE(ctx, 6 * nhp <= CMAX, "%d free poses exceed the dense reduced-system limit (%d)", nhp, CMAX / 6);
+    const double t_s0 = ms_since(tp0);
     // edges per landmark (stable in edge order)
     std::vector<int32_t> lm_e_start(nhl + 1, 0), lm_e(ne);
     for (int e = 0; e < ne; e++) lm_e_start[point_h[G->e_point[e]] + 1]++;
@@ -946,6 +947,7 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
         std::vector<int32_t> fill(lm_e_start.begin(), lm_e_start.end() - 1);
         for (int e = 0; e < ne; e++) lm_e[fill[point_h[G->e_point[e]]]++] = e;
     }
+    const double t_s1 = ms_since(tp0);
     // blocks per landmark: unique free poses sorted by hessian index
     std::vector<int32_t> lm_b_start(nhl + 1, 0), blk_pose, edge_blk(ne, -1);
     blk_pose.reserve(ne);
@@ -973,6 +975,7 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
         }
     }
     const int nblk = (int)blk_pose.size();
+    const double t_s2 = ms_since(tp0);
     std::vector<int32_t> blk_lm(nblk), blk_e_start(nblk + 1, 0), blk_e;
     for (int l = 0; l < nhl; l++)
         for (int b = lm_b_start[l]; b < lm_b_start[l + 1]; b++) blk_lm[b] = l;
@@ -1002,6 +1005,7 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
         std::vector<int32_t> fill(hp_b_start.begin(), hp_b_start.end() - 1);
         for (int b = 0; b < nblk; b++) hp_b[fill[blk_pose[b]]++] = b;
     }
+    const double t_s3 = ms_since(tp0);
     // pose pairs (i <= j), dense index; contributions in landmark order
     const int npairs = nhp * (nhp + 1) / 2;
     auto pid = [nhp](int i, int j) { return i * nhp - i * (i - 1) / 2 + (j - i); };
@@ -1308,8 +1312,8 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
         }
     }
     if (prof)
-        fprintf(stderr, "[osg lba] structure %.3f ms, pack+upload %.3f ms, LM %.3f ms (%d it, %d trials), pairs %d contrib %d\n",
-                t_struct, t_upload, ms_since(tp1), iters, trials, npairs, pair_start[npairs]);
+        fprintf(stderr, "[osg lba] structure %.3f ms (index %.3f, lm csr %.3f, blocks %.3f, pose csr %.3f, pairs %.3f), pack+upload %.3f ms, LM %.3f ms (%d it, %d trials), pairs %d contrib %d\n",
+                t_struct, t_s0, t_s1 - t_s0, t_s2 - t_s1, t_s3 - t_s2, t_struct - t_s3, t_upload, ms_since(tp1), iters, trials, npairs, pair_start[npairs]);
     R->iterations = iters;
     R->trials = trials;
     R->aborted = (stop && *stop) ? 1 : 0;

@@ -255,6 +255,8 @@ class Optimizer:
         lib, h = self.ctx.lib, self.ctx.handle
         R, pose, point, bad = make_ba_result(G)
         gs = G.struct()
+        if stop_flag is not None:
+            assert stop_flag.dtype == np.uint8, "stop flag is one byte (bool *pbStopFlag)"
         sf = None if stop_flag is None else _p(stop_flag)
         rc = lib.osg_local_bundle_adjustment(h, C.byref(gs), C.byref(R), sf)
         self.ctx.check(rc, "LocalBundleAdjustment")

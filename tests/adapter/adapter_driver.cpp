@@ -1,0 +1,414 @@
+// adapter_driver.cpp — runs adapters/orbslam3/osg_orbslam3.h on mock ORB-SLAM3 objects built from
+// arrays written by tests/test_adapter.py, and writes the adapter's results back (test-only).
+//
+//   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba
+//
+// Array file: repeated {u32 name_len, name, u8 dtype ('b' u8, 'i' i32, 'f' f32, 'd' f64), u64 count,
+// data}.
+#include <cstdio>
+#include <cstdlib>
+#include <list>
+#include <memory>
+#include <string>
+#include <unordered_map>
+
+#include "../../adapters/orbslam3/osg_orbslam3.h"
+#include "mock_orbslam3.h"
+
+using namespace mock;
+
+struct Arr {
+    char t = 0;
+    std::vector<unsigned char> b;
+    size_t n = 0;
+    template <class T>
+    const T *p() const { return reinterpret_cast<const T *>(b.data()); }
+};
+using Arrays = std::unordered_map<std::string, Arr>;
+
+static Arrays read_arrays(const char *path)
+{
+    Arrays m;
+    FILE *f = fopen(path, "rb");
+    if (!f) throw std::runtime_error(std::string("cannot open ") + path);
+    for (;;) {
+        uint32_t len;
+        if (fread(&len, 4, 1, f) != 1) break;
+        std::string name(len, '\0');
+        fread(&name[0], 1, len, f);
+        Arr a;
+        fread(&a.t, 1, 1, f);
+        uint64_t n;
+        fread(&n, 8, 1, f);
+        a.n = n;
+        const size_t es = a.t == 'b' ? 1 : a.t == 'd' ? 8 : 4;
+        a.b.resize(n * es);
+        if (n) fread(a.b.data(), es, n, f);
+        m[name] = std::move(a);
+    }
+    fclose(f);
+    return m;
+}
+
+static void write_arrays(const char *path, const Arrays &m)
+{
+    FILE *f = fopen(path, "wb");
+    for (const auto &kv : m) {
+        const uint32_t len = (uint32_t)kv.first.size();
+        fwrite(&len, 4, 1, f);
+        fwrite(kv.first.data(), 1, len, f);
+        fwrite(&kv.second.t, 1, 1, f);
+        const uint64_t n = kv.second.n;
+        fwrite(&n, 8, 1, f);
+        fwrite(kv.second.b.data(), 1, kv.second.b.size(), f);
+    }
+    fclose(f);
+}
+
+template <class T>
+static Arr make(char t, const std::vector<T> &v)
+{
+    Arr a;
+    a.t = t;
+    a.n = v.size();
+    a.b.resize(v.size() * sizeof(T));
+    if (!v.empty()) std::memcpy(a.b.data(), v.data(), a.b.size());
+    return a;
+}
+
+static const Arr &get(const Arrays &m, const std::string &k)
+{
+    auto it = m.find(k);
+    if (it == m.end()) throw std::runtime_error("missing array " + k);
+    return it->second;
+}
+
+static bool has(const Arrays &m, const std::string &k) { return m.count(k) != 0; }
+
+// Frame from the FrameSoA arrays "F.*" (keypoints, descriptors, mvuRight, grid CSR, scales)
+static void build_frame(const Arrays &m, Frame &F)
+{
+    const int n = (int)get(m, "F.kp_x").n;
+    F.N = n;
+    F.Nleft = -1;
+    const float *x = get(m, "F.kp_x").p<float>(), *y = get(m, "F.kp_y").p<float>(), *a = get(m, "F.kp_angle").p<float>();
+    const int32_t *o = get(m, "F.kp_octave").p<int32_t>();
+    F.mvKeysUn.resize(n);
+    for (int i = 0; i < n; i++) {
+        F.mvKeysUn[i].pt.x = x[i];
+        F.mvKeysUn[i].pt.y = y[i];
+        F.mvKeysUn[i].angle = a[i];
+        F.mvKeysUn[i].octave = o[i];
+    }
+    F.mvKeys = F.mvKeysUn;
+    F.mDescriptors = cv::Mat(n, 32);
+    std::memcpy(F.mDescriptors.buf.data(), get(m, "F.desc").b.data(), (size_t)n * 32);
+    F.mvuRight.assign(n, -1.0f);
+    if (has(m, "F.u_right")) std::memcpy(F.mvuRight.data(), get(m, "F.u_right").b.data(), (size_t)n * 4);
+    const int32_t *gs = get(m, "F.grid_start").p<int32_t>(), *gi = get(m, "F.grid_idx").p<int32_t>();
+    for (int ix = 0; ix < OSG_GRID_COLS; ix++)
+        for (int iy = 0; iy < OSG_GRID_ROWS; iy++) {
+            const int c = ix * OSG_GRID_ROWS + iy;
+            for (int j = gs[c]; j < gs[c + 1]; j++) F.mGrid[ix][iy].push_back((size_t)gi[j]);
+        }
+    const float *sc = get(m, "F.scalars").p<float>();  // min_x max_x min_y max_y inv_w inv_h mb mbf
+    Frame::mnMinX = sc[0];
+    Frame::mnMaxX = sc[1];
+    Frame::mnMinY = sc[2];
+    Frame::mnMaxY = sc[3];
+    Frame::mfGridElementWidthInv = sc[4];
+    Frame::mfGridElementHeightInv = sc[5];
+    F.mb = sc[6];
+    F.mbf = sc[7];
+    const Arr &s = get(m, "F.scale");
+    F.mvScaleFactors.assign(s.p<float>(), s.p<float>() + s.n);
+    F.mnScaleLevels = (int)s.n;
+    F.mvpMapPoints.assign(n, nullptr);
+    F.mvbOutlier.assign(n, false);
+}
+
+// occupants of Frame::mvpMapPoints from "S.slot_mp" / "S.slot_taken"
+static void build_slots(const Arrays &m, Frame &F, std::vector<std::unique_ptr<MapPoint>> &pool)
+{
+    const int32_t *sm = get(m, "S.slot_mp").p<int32_t>();
+    const uint8_t *st = has(m, "S.slot_taken") ? get(m, "S.slot_taken").p<uint8_t>() : nullptr;
+    for (int i = 0; i < F.N; i++)
+        if (sm[i] >= 0) {
+            pool.emplace_back(new MapPoint());
+            pool.back()->mnId = (unsigned long)sm[i];
+            pool.back()->nobs = st ? st[i] : 1;
+            F.mvpMapPoints[i] = pool.back().get();
+        }
+}
+
+static std::vector<int32_t> slot_ids(const std::vector<MapPoint *> &v)
+{
+    std::vector<int32_t> r(v.size(), -1);
+    for (size_t i = 0; i < v.size(); i++)
+        if (v[i]) r[i] = (int32_t)v[i]->mnId;
+    return r;
+}
+
+static void fill_featvec(const Arrays &m, const std::string &pre, std::map<unsigned int, std::vector<unsigned int>> &fv)
+{
+    const Arr &nid = get(m, pre + "node_id"), &ns = get(m, pre + "node_start"), &ft = get(m, pre + "feat");
+    for (size_t k = 0; k < nid.n; k++) {
+        auto &v = fv[nid.p<uint32_t>()[k]];
+        for (int j = ns.p<int32_t>()[k]; j < ns.p<int32_t>()[k + 1]; j++) v.push_back((unsigned)ft.p<int32_t>()[j]);
+    }
+}
+
+// a BoW side "B1." / "B2." as a KeyFrame with MapPoints (mnId = mp_id, bad = !mp_good)
+static void build_bow_kf(const Arrays &m, const std::string &pre, KeyFrame &K, std::vector<std::unique_ptr<MapPoint>> &pool)
+{
+    const Arr &d = get(m, pre + "desc");
+    const int n = (int)(d.n / 32);
+    K.N = n;
+    K.NLeft = -1;
+    K.mDescriptors = cv::Mat(n, 32);
+    std::memcpy(K.mDescriptors.buf.data(), d.b.data(), d.b.size());
+    K.mvKeysUn.resize(n);
+    const float *ang = get(m, pre + "angle").p<float>();
+    for (int i = 0; i < n; i++) K.mvKeysUn[i].angle = ang[i];
+    K.mvpMapPoints.assign(n, nullptr);
+    const int32_t *id = get(m, pre + "mp_id").p<int32_t>();
+    const uint8_t *good = get(m, pre + "mp_good").p<uint8_t>();
+    for (int i = 0; i < n; i++)
+        if (id[i] >= 0) {
+            pool.emplace_back(new MapPoint());
+            pool.back()->mnId = (unsigned long)id[i];
+            pool.back()->bad = !good[i];
+            K.mvpMapPoints[i] = pool.back().get();
+        }
+    fill_featvec(m, pre, K.mFeatVec);
+}
+
+int main(int argc, char **argv)
+{
+    if (argc != 4) {
+        fprintf(stderr, "usage: %s MODE in out\n", argv[0]);
+        return 2;
+    }
+    const std::string mode = argv[1];
+    try {
+        const Arrays in = read_arrays(argv[2]);
+        Arrays out;
+        std::vector<std::unique_ptr<MapPoint>> pool;
+        const float *prm = has(in, "params") ? get(in, "params").p<float>() : nullptr;
+        if (mode == "mps") {
+            Frame F;
+            build_frame(in, F);
+            build_slots(in, F, pool);
+            const int nq = (int)get(in, "Q.mp_id").n;
+            std::vector<MapPoint *> q(nq);
+            for (int i = 0; i < nq; i++) {
+                pool.emplace_back(new MapPoint());
+                MapPoint *p = pool.back().get();
+                p->mnId = (unsigned long)get(in, "Q.mp_id").p<int32_t>()[i];
+                std::memcpy(p->desc.buf.data(), get(in, "Q.desc").p<uint8_t>() + 32 * i, 32);
+                p->bad = !get(in, "Q.usable").p<uint8_t>()[i];
+                p->nobs = get(in, "Q.has_obs").p<uint8_t>()[i];
+                p->mbTrackInView = get(in, "Q.in_view").p<uint8_t>()[i];
+                p->mTrackProjX = get(in, "Q.proj_x").p<float>()[i];
+                p->mTrackProjY = get(in, "Q.proj_y").p<float>()[i];
+                p->mTrackProjXR = get(in, "Q.proj_xr").p<float>()[i];
+                p->mTrackViewCos = get(in, "Q.view_cos").p<float>()[i];
+                p->mnTrackScaleLevel = get(in, "Q.pred_level").p<int32_t>()[i];
+                p->mTrackDepth = get(in, "Q.track_depth").p<float>()[i];
+                q[i] = p;
+            }
+            // params: nnratio th far thfar
+            const int nm = osg_orbslam3::search_by_projection_mps<MockHooks>(F, q, prm[1], prm[2] != 0, prm[3], prm[0]);
+            out["nmatches"] = make('i', std::vector<int32_t>{nm});
+            out["slot_mp"] = make('i', slot_ids(F.mvpMapPoints));
+        } else if (mode == "last") {
+            Frame CF, LF;
+            build_frame(in, CF);
+            build_slots(in, CF, pool);
+            const int n = (int)get(in, "L.mp_id").n;
+            LF.N = n;
+            LF.Nleft = -1;
+            LF.mvKeysUn.resize(n);
+            LF.mvpMapPoints.assign(n, nullptr);
+            LF.mvbOutlier.assign(n, false);
+            for (int i = 0; i < n; i++) {
+                LF.mvKeysUn[i].octave = get(in, "L.octave").p<int32_t>()[i];
+                LF.mvKeysUn[i].angle = get(in, "L.angle").p<float>()[i];
+                const int id = get(in, "L.mp_id").p<int32_t>()[i];
+                if (id < 0) continue;
+                pool.emplace_back(new MapPoint());
+                MapPoint *p = pool.back().get();
+                p->mnId = (unsigned long)id;
+                std::memcpy(p->desc.buf.data(), get(in, "L.desc").p<uint8_t>() + 32 * i, 32);
+                p->nobs = get(in, "L.has_obs").p<uint8_t>()[i];
+                p->proj_ok = true;
+                p->proj_u = get(in, "L.u").p<float>()[i];
+                p->proj_v = get(in, "L.v").p<float>()[i];
+                p->proj_invz = get(in, "L.invz").p<float>()[i];
+                LF.mvpMapPoints[i] = p;
+                LF.mvbOutlier[i] = !get(in, "L.valid").p<uint8_t>()[i];
+            }
+            LF.mvKeys = LF.mvKeysUn;
+            CF.tlc_z_value = prm[3];
+            // params: th mono ori tlc_z
+            const int nm = osg_orbslam3::search_by_projection_last<MockHooks>(CF, LF, prm[0], prm[1] != 0, prm[2] != 0);
+            out["nmatches"] = make('i', std::vector<int32_t>{nm});
+            out["slot_mp"] = make('i', slot_ids(CF.mvpMapPoints));
+        } else if (mode == "kf") {
+            Frame CF;
+            build_frame(in, CF);
+            build_slots(in, CF, pool);
+            KeyFrame K;
+            const int n = (int)get(in, "K.mp_id").n;
+            K.N = n;
+            K.mvKeysUn.resize(n);
+            K.mvpMapPoints.assign(n, nullptr);
+            for (int i = 0; i < n; i++) {
+                K.mvKeysUn[i].angle = get(in, "K.angle").p<float>()[i];
+                pool.emplace_back(new MapPoint());
+                MapPoint *p = pool.back().get();
+                p->mnId = (unsigned long)get(in, "K.mp_id").p<int32_t>()[i];
+                std::memcpy(p->desc.buf.data(), get(in, "K.desc").p<uint8_t>() + 32 * i, 32);
+                p->proj_ok = get(in, "K.valid").p<uint8_t>()[i];
+                p->proj_u = get(in, "K.u").p<float>()[i];
+                p->proj_v = get(in, "K.v").p<float>()[i];
+                p->proj_level = get(in, "K.pred_level").p<int32_t>()[i];
+                K.mvpMapPoints[i] = p;
+            }
+            std::set<MapPoint *> already;
+            // params: th orbdist ori
+            const int nm = osg_orbslam3::search_by_projection_kf<MockHooks>(CF, &K, already, prm[0], (int)prm[1], prm[2] != 0);
+            out["nmatches"] = make('i', std::vector<int32_t>{nm});
+            out["slot_mp"] = make('i', slot_ids(CF.mvpMapPoints));
+        } else if (mode == "bow_kf_f") {
+            KeyFrame K, KF;
+            build_bow_kf(in, "B1.", K, pool);
+            build_bow_kf(in, "B2.", KF, pool);
+            Frame F;  // the Frame side: descriptors, angles, FeatureVector
+            F.N = KF.N;
+            F.Nleft = -1;
+            F.mDescriptors = KF.mDescriptors;
+            F.mvKeysUn = KF.mvKeysUn;
+            F.mFeatVec = KF.mFeatVec;
+            std::vector<MapPoint *> matches;
+            // params: nnratio ori
+            const int nm = osg_orbslam3::search_by_bow_kf_f<MockHooks>(&K, F, matches, prm[0], prm[1] != 0);
+            out["nmatches"] = make('i', std::vector<int32_t>{nm});
+            out["out_mp"] = make('i', slot_ids(matches));
+        } else if (mode == "bow_kf_kf") {
+            KeyFrame K1, K2;
+            build_bow_kf(in, "B1.", K1, pool);
+            build_bow_kf(in, "B2.", K2, pool);
+            std::vector<MapPoint *> matches;
+            const int nm = osg_orbslam3::search_by_bow_kf_kf<MockHooks>(&K1, &K2, matches, prm[0], prm[1] != 0);
+            out["nmatches"] = make('i', std::vector<int32_t>{nm});
+            out["out_mp"] = make('i', slot_ids(matches));
+        } else if (mode == "pose") {
+            Frame F;
+            const int n = (int)get(in, "P.kind").n;
+            F.N = n;
+            F.Nleft = -1;
+            F.mvKeysUn.resize(n);
+            F.mvuRight.assign(n, -1.0f);
+            F.mvInvLevelSigma2.resize(n);
+            F.mvpMapPoints.assign(n, nullptr);
+            F.mvbOutlier.assign(n, false);
+            const double *obs = get(in, "P.obs").p<double>(), *xw = get(in, "P.xw").p<double>();
+            for (int i = 0; i < n; i++) {
+                pool.emplace_back(new MapPoint());
+                std::memcpy(pool.back()->pos, xw + 3 * i, 24);
+                F.mvpMapPoints[i] = pool.back().get();
+                F.mvKeysUn[i].pt.x = (float)obs[3 * i];
+                F.mvKeysUn[i].pt.y = (float)obs[3 * i + 1];
+                F.mvKeysUn[i].octave = i;  // one information level per keypoint
+                F.mvInvLevelSigma2[i] = get(in, "P.inv_sigma2").p<float>()[i];
+                if (get(in, "P.kind").p<uint8_t>()[i] == OSG_EDGE_STEREO) F.mvuRight[i] = (float)obs[3 * i + 2];
+            }
+            std::memcpy(F.pose, get(in, "P.pose").b.data(), 56);
+            const float *cam = get(in, "P.cam").p<float>();  // type p0..p7 fx fy cx cy bf
+            Camera c;
+            c.type = (int)cam[0];
+            c.params.assign(cam + 1, cam + 9);
+            F.mpCamera = &c;
+            F.fx = cam[9];
+            F.fy = cam[10];
+            F.cx = cam[11];
+            F.cy = cam[12];
+            F.mbf = cam[13];
+            const int inl = osg_orbslam3::pose_optimization<MockHooks>(&F);
+            std::vector<uint8_t> outl(n);
+            for (int i = 0; i < n; i++) outl[i] = F.mvbOutlier[i];
+            out["n_inliers"] = make('i', std::vector<int32_t>{inl});
+            out["pose"] = make('d', std::vector<double>(F.pose, F.pose + 7));
+            out["outlier"] = make('b', outl);
+        } else if (mode == "lba") {
+            const int np = (int)(get(in, "G.pose").n / 7), npt = (int)(get(in, "G.point").n / 3), ne = (int)get(in, "G.e_pose").n;
+            const float *cam = get(in, "G.cam").p<float>();
+            Camera c;
+            c.type = (int)cam[0];
+            c.params.assign(cam + 1, cam + 9);
+            Map map;
+            std::vector<KeyFrame> kf(np);
+            std::vector<MapPoint> mp(npt);
+            for (int i = 0; i < np; i++) {
+                kf[i].mnId = (unsigned long)i;
+                kf[i].map = &map;
+                std::memcpy(kf[i].pose, get(in, "G.pose").p<double>() + 7 * i, 56);
+                kf[i].mpCamera = &c;
+                kf[i].fx = cam[9];
+                kf[i].fy = cam[10];
+                kf[i].cx = cam[11];
+                kf[i].cy = cam[12];
+                kf[i].mbf = cam[13];
+            }
+            for (int j = 0; j < npt; j++) {
+                mp[j].mnId = (unsigned long)j;
+                std::memcpy(mp[j].pos, get(in, "G.point").p<double>() + 3 * j, 24);
+            }
+            for (int e = 0; e < ne; e++) {
+                KeyFrame &k = kf[get(in, "G.e_pose").p<int32_t>()[e]];
+                MapPoint &p = mp[get(in, "G.e_point").p<int32_t>()[e]];
+                const double *o = get(in, "G.e_obs").p<double>() + 3 * e;
+                cv::KeyPoint kp;
+                kp.pt.x = (float)o[0];
+                kp.pt.y = (float)o[1];
+                kp.octave = (int)k.mvKeysUn.size();
+                k.mvKeysUn.push_back(kp);
+                k.mvInvLevelSigma2.push_back(get(in, "G.e_inv_sigma2").p<float>()[e]);
+                k.mvuRight.push_back(get(in, "G.e_kind").p<uint8_t>()[e] == OSG_EDGE_STEREO ? (float)o[2] : -1.0f);
+                k.mvpMapPoints.push_back(&p);
+                p.obs[&k] = std::make_tuple(kp.octave, -1);
+            }
+            std::list<KeyFrame *> local, fixedc;
+            const uint8_t *fx = get(in, "G.pose_fixed").p<uint8_t>();
+            for (int i = 0; i < np; i++) (fx[i] ? fixedc : local).push_back(&kf[i]);
+            std::list<MapPoint *> mps;
+            for (auto &p : mp) mps.push_back(&p);
+            bool stop = false;
+            auto o = osg_orbslam3::local_bundle_adjustment<MockHooks>(local, fixedc, mps, &map, ~0ul, &stop, false);
+            std::vector<uint8_t> bad(ne, 0);
+            {
+                std::map<std::pair<KeyFrame *, MapPoint *>, int> edge_of;
+                for (int e = 0; e < ne; e++)
+                    edge_of[{&kf[get(in, "G.e_pose").p<int32_t>()[e]], &mp[get(in, "G.e_point").p<int32_t>()[e]]}] = e;
+                for (auto &km : o.to_erase) bad[edge_of[km]] = 1;
+            }
+            osg_orbslam3::apply_local_bundle_adjustment<MockHooks>(o);
+            std::vector<double> pose(7 * (size_t)np), point(3 * (size_t)npt);
+            for (int i = 0; i < np; i++) std::memcpy(&pose[7 * i], kf[i].pose, 56);
+            for (int j = 0; j < npt; j++) std::memcpy(&point[3 * j], mp[j].pos, 24);
+            out["pose"] = make('d', pose);
+            out["point"] = make('d', point);
+            out["edge_bad"] = make('b', bad);
+            out["num_edges"] = make('i', std::vector<int32_t>{o.num_edges});
+        } else {
+            fprintf(stderr, "unknown mode %s\n", mode.c_str());
+            return 2;
+        }
+        write_arrays(argv[3], out);
+    } catch (const std::exception &e) {
+        fprintf(stderr, "adapter_driver: %s\n", e.what());
+        return 1;
+    }
+    return 0;
+}

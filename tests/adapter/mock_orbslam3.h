@@ -1,0 +1,156 @@
+// mock_orbslam3.h — POD stand-ins for the ORB-SLAM3 types the adapter reads (test-only).
+// Member names follow ref:include/Frame.h, KeyFrame.h, MapPoint.h so adapters/orbslam3/
+// osg_orbslam3.h compiles unchanged against them; math the reference does with Sophus / Eigen is
+// supplied through MockHooks from values stored on the objects.
+#ifndef MOCK_ORBSLAM3_H
+#define MOCK_ORBSLAM3_H
+
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <set>
+#include <tuple>
+#include <vector>
+
+#include "osg.h"
+#include "osg_ba.h"
+
+namespace cv {
+struct Point2f {
+    float x = 0, y = 0;
+};
+struct KeyPoint {
+    Point2f pt;
+    float size = 0, angle = 0, response = 0;
+    int octave = 0, class_id = -1;
+};
+struct Mat {  // CV_8UC1 rows x cols
+    int rows = 0, cols = 0;
+    std::vector<unsigned char> buf;
+    Mat() = default;
+    Mat(int r, int c) : rows(r), cols(c), buf((size_t)r * c) {}
+    template <class T>
+    T *ptr(int i) { return reinterpret_cast<T *>(buf.data() + (size_t)i * cols); }
+    template <class T>
+    const T *ptr(int i) const { return reinterpret_cast<const T *>(buf.data() + (size_t)i * cols); }
+};
+}  // namespace cv
+
+namespace mock {
+
+struct Map {};
+struct KeyFrame;
+
+struct Camera {
+    int type = OSG_CAM_PINHOLE;
+    std::vector<float> params;
+};
+
+struct MapPoint {
+    unsigned long mnId = 0;
+    bool bad = false;
+    int nobs = 0;
+    cv::Mat desc{1, 32};
+    double pos[3] = {0, 0, 0};
+    // isInFrustum results (SearchByProjection(Frame&, vector<MapPoint*>))
+    float mTrackProjX = 0, mTrackProjY = 0, mTrackDepth = 0, mTrackDepthR = 0, mTrackProjXR = 0, mTrackProjYR = 0;
+    bool mbTrackInView = false, mbTrackInViewR = false;
+    int mnTrackScaleLevel = 0, mnTrackScaleLevelR = 0;
+    float mTrackViewCos = 0, mTrackViewCosR = 0;
+    // test-only: what MockHooks::project_last / kf_query return for this MapPoint
+    bool proj_ok = false;
+    float proj_u = 0, proj_v = 0, proj_invz = 0;
+    int proj_level = 0;
+    std::map<KeyFrame *, std::tuple<int, int>> obs;
+
+    bool isBad() const { return bad; }
+    int Observations() const { return nobs; }
+    cv::Mat GetDescriptor() const { return desc; }
+    std::map<KeyFrame *, std::tuple<int, int>> GetObservations() const { return obs; }
+    void EraseObservation(KeyFrame *k) { obs.erase(k); }
+};
+
+struct Frame {
+    int N = 0, Nleft = -1;
+    std::vector<cv::KeyPoint> mvKeys, mvKeysUn, mvKeysRight;
+    cv::Mat mDescriptors;
+    std::vector<float> mvuRight;
+    std::vector<MapPoint *> mvpMapPoints;
+    std::vector<bool> mvbOutlier;
+    std::vector<std::size_t> mGrid[OSG_GRID_COLS][OSG_GRID_ROWS];
+    static inline float mnMinX = 0, mnMaxX = 0, mnMinY = 0, mnMaxY = 0;
+    static inline float mfGridElementWidthInv = 0, mfGridElementHeightInv = 0;
+    int mnScaleLevels = 8;
+    std::vector<float> mvScaleFactors, mvInvLevelSigma2;
+    float mb = 0, mbf = 0, fx = 0, fy = 0, cx = 0, cy = 0;
+    Camera *mpCamera = nullptr, *mpCamera2 = nullptr;
+    std::map<unsigned int, std::vector<unsigned int>> mFeatVec;
+    double pose[7] = {0, 0, 0, 1, 0, 0, 0};
+    float tlc_z_value = 0;  // test-only: MockHooks::tlc_z
+};
+
+struct KeyFrame {
+    unsigned long mnId = 0;
+    int N = 0, NLeft = -1;
+    bool bad = false;
+    Map *map = nullptr;
+    std::vector<cv::KeyPoint> mvKeys, mvKeysUn, mvKeysRight;
+    cv::Mat mDescriptors;
+    std::vector<float> mvuRight, mvInvLevelSigma2;
+    std::vector<MapPoint *> mvpMapPoints;
+    std::map<unsigned int, std::vector<unsigned int>> mFeatVec;
+    float mbf = 0, fx = 0, fy = 0, cx = 0, cy = 0;
+    Camera *mpCamera = nullptr, *mpCamera2 = nullptr;
+    double pose[7] = {0, 0, 0, 1, 0, 0, 0};
+
+    std::vector<MapPoint *> GetMapPointMatches() const { return mvpMapPoints; }
+    bool isBad() const { return bad; }
+    Map *GetMap() const { return map; }
+    void EraseMapPointMatch(MapPoint *p)
+    {
+        for (auto &q : mvpMapPoints)
+            if (q == p) q = nullptr;
+    }
+};
+
+struct MockHooks {
+    template <class T>
+    static void pose(const T &o, double q[7]) { std::memcpy(q, o.pose, sizeof o.pose); }
+    template <class T>
+    static void set_pose(T &o, const double q[7]) { std::memcpy(o.pose, q, sizeof o.pose); }
+    static void world_pos(MapPoint *p, double x[3]) { std::memcpy(x, p->pos, sizeof p->pos); }
+    static void set_world_pos(MapPoint *p, const double x[3]) { std::memcpy(p->pos, x, sizeof p->pos); }
+    template <class T>
+    static void camera(const T &o, bool right, osg_camera &c)
+    {
+        std::memset(&c, 0, sizeof c);
+        const Camera *cam = right ? o.mpCamera2 : o.mpCamera;
+        c.type = cam ? cam->type : OSG_CAM_PINHOLE;
+        if (cam)
+            for (size_t i = 0; i < cam->params.size() && i < 8; i++) c.p[i] = cam->params[i];
+        c.fx = o.fx;
+        c.fy = o.fy;
+        c.cx = o.cx;
+        c.cy = o.cy;
+        c.bf = o.mbf;
+        c.trl[3] = 1.0;
+    }
+    static bool project_last(const Frame &, MapPoint *p, float &u, float &v, float &invz)
+    {
+        u = p->proj_u;
+        v = p->proj_v;
+        invz = p->proj_invz;
+        return p->proj_ok;
+    }
+    static float tlc_z(const Frame &CF, const Frame &) { return CF.tlc_z_value; }
+    static bool kf_query(const Frame &, MapPoint *p, float &u, float &v, int &level)
+    {
+        u = p->proj_u;
+        v = p->proj_v;
+        level = p->proj_level;
+        return p->proj_ok;
+    }
+};
+
+}  // namespace mock
+#endif

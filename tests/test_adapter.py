@@ -1,0 +1,203 @@
+"""The ORB-SLAM3-side adapter (adapters/orbslam3/osg_orbslam3.h) on mock Frame / KeyFrame /
+MapPoint objects (tests/adapter/mock_orbslam3.h) built from the synthetic SoA generators.
+
+* CPU: the adapter and the driver compile against the mocks (member names of the reference).
+* GPU: every entry point run through the adapter gives the oracle's results (matchers, bit-exact)
+  or exactly the direct C-ABI results on the same graph (PoseOptimization, LBA) — so gathering
+  from objects and writing back into them loses nothing.
+"""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from orb_slam3_comments_ghr_amd import frames as fr
+from orb_slam3_comments_ghr_amd import optimizer as op
+from tests import oracle_calls as oc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DRIVER_SRC = os.path.join(ROOT, "tests", "adapter", "adapter_driver.cpp")
+PKG = os.path.join(ROOT, "orb_slam3_comments_ghr_amd")
+_CODES = {np.dtype(np.uint8): b"b", np.dtype(np.int8): b"b", np.dtype(np.int32): b"i", np.dtype(np.uint32): b"i",
+          np.dtype(np.float32): b"f", np.dtype(np.float64): b"d"}
+_DTYPES = {b"b": np.uint8, b"i": np.int32, b"f": np.float32, b"d": np.float64}
+
+
+def write_arrays(path, arrays):
+    with open(path, "wb") as f:
+        for name, a in arrays.items():
+            a = np.ascontiguousarray(a)
+            code = _CODES[a.dtype]
+            nb = name.encode()
+            f.write(np.uint32(len(nb)).tobytes() + nb + code + np.uint64(a.size).tobytes() + a.tobytes())
+
+
+def read_arrays(path):
+    out = {}
+    with open(path, "rb") as f:
+        data = f.read()
+    o = 0
+    while o < len(data):
+        n = int(np.frombuffer(data, np.uint32, 1, o)[0]); o += 4
+        name = data[o:o + n].decode(); o += n
+        code = data[o:o + 1]; o += 1
+        cnt = int(np.frombuffer(data, np.uint64, 1, o)[0]); o += 8
+        dt = np.dtype(_DTYPES[code])
+        out[name] = np.frombuffer(data, dt, cnt, o).copy(); o += cnt * dt.itemsize
+    return out
+
+
+def frame_arrays(F):
+    return {"F.kp_x": F.kp_x, "F.kp_y": F.kp_y, "F.kp_angle": F.kp_angle, "F.kp_octave": F.kp_octave,
+            "F.desc": F.desc.reshape(-1), "F.u_right": (F.u_right if F.u_right is not None
+                                                       else np.full(F.n, -1, np.float32)),
+            "F.grid_start": F.grid_start, "F.grid_idx": F.grid_idx, "F.scale": F.scale,
+            "F.scalars": np.array([F.min_x, F.max_x, F.min_y, F.max_y, F.inv_w, F.inv_h, F.mb, F.mbf],
+                                  np.float32)}
+
+
+def bow_arrays(pre, S):
+    return {pre + "desc": S.desc.reshape(-1), pre + "angle": S.angle, pre + "mp_id": S.mp_id,
+            pre + "mp_good": S.mp_good, pre + "node_id": S.node_id, pre + "node_start": S.node_start,
+            pre + "feat": S.feat}
+
+
+def cam_array(c):
+    return np.array([c.type, *[c.p[i] for i in range(8)], c.fx, c.fy, c.cx, c.cy, c.bf], np.float32)
+
+
+def test_adapter_compiles_against_mocks():
+    """The header-only adapter + driver compile against the mocks (reference member names)."""
+    gxx = shutil.which("g++")
+    assert gxx, "g++ is part of the image"
+    r = subprocess.run([gxx, "-std=c++17", "-fsyntax-only", "-Wall", "-Werror", "-Wno-unused-result",
+                        "-I" + os.path.join(ROOT, "include"), DRIVER_SRC], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+
+
+@pytest.fixture(scope="module")
+def driver(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("adapter") / "adapter_driver")
+    r = subprocess.run(["g++", "-std=c++17", "-O2", "-I" + os.path.join(ROOT, "include"), DRIVER_SRC, "-o", exe,
+                        "-L" + PKG, "-lorbslam3_amd", "-Wl,-rpath," + PKG], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return exe
+
+
+def run(driver, tmp_path, mode, arrays):
+    fi, fo = str(tmp_path / f"{mode}.in"), str(tmp_path / f"{mode}.out")
+    write_arrays(fi, arrays)
+    r = subprocess.run([driver, mode, fi, fo], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return read_arrays(fo)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,far", [(1, False), (2, True)])
+def test_adapter_search_by_projection_mps(driver, tmp_path, oracle, seed, far):
+    rng = np.random.default_rng(700 + seed)
+    F = fr.synth_frame(rng, n=1200, stereo=(seed % 2 == 0))
+    Q = fr.synth_mp_queries(rng, F, m=3000)
+    slot_mp, taken = fr.synth_slots(rng, F.n)
+    nn, th, thfar = 0.8, 1.0, 20.0
+    arrays = {**frame_arrays(F), "S.slot_mp": slot_mp.astype(np.int32), "S.slot_taken": taken.astype(np.uint8),
+              "params": np.array([nn, th, float(far), thfar], np.float32)}
+    for k in ["mp_id", "desc", "usable", "has_obs", "in_view", "proj_x", "proj_y", "proj_xr", "view_cos",
+              "pred_level", "track_depth"]:
+        arrays["Q." + k] = getattr(Q, k).reshape(-1)
+    out = run(driver, tmp_path, "mps", arrays)
+    n_ref, s_ref = oc.mps(oracle, F, Q, nn, th, far, thfar, slot_mp.astype(np.int32), taken)
+    assert int(out["nmatches"][0]) == n_ref
+    np.testing.assert_array_equal(out["slot_mp"], s_ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mono,tlc", [(True, 0.0), (False, 0.5)])
+def test_adapter_search_by_projection_last(driver, tmp_path, oracle, mono, tlc):
+    rng = np.random.default_rng(710 + int(mono))
+    F = fr.synth_frame(rng, n=1200, stereo=not mono)
+    L = fr.synth_last_queries(rng, F, n_last=1100, tlc_z=tlc)
+    L.valid = (L.valid.astype(bool) & (L.mp_id >= 0)).astype(np.uint8)  # a valid slot holds a MapPoint
+    slot_mp, taken = fr.synth_slots(rng, F.n)
+    th = 7.0
+    arrays = {**frame_arrays(F), "S.slot_mp": slot_mp.astype(np.int32), "S.slot_taken": taken.astype(np.uint8),
+              "params": np.array([th, float(mono), 1.0, tlc], np.float32)}
+    for k in ["mp_id", "desc", "valid", "has_obs", "u", "v", "invz", "octave", "angle"]:
+        arrays["L." + k] = getattr(L, k).reshape(-1)
+    out = run(driver, tmp_path, "last", arrays)
+    n_ref, s_ref = oc.last(oracle, F, L, th, mono, True, slot_mp.astype(np.int32), taken)
+    assert int(out["nmatches"][0]) == n_ref
+    np.testing.assert_array_equal(out["slot_mp"], s_ref)
+
+
+@pytest.mark.gpu
+def test_adapter_search_by_projection_kf(driver, tmp_path, oracle):
+    rng = np.random.default_rng(720)
+    F = fr.synth_frame(rng, n=1200)
+    K = fr.synth_kf_queries(rng, F, n_kf=1000)
+    slot_mp, _ = fr.synth_slots(rng, F.n, frac_assigned=0.2)
+    th, orb = 10.0, 100
+    arrays = {**frame_arrays(F), "S.slot_mp": slot_mp.astype(np.int32),
+              "params": np.array([th, orb, 1.0], np.float32)}
+    for k in ["mp_id", "desc", "valid", "u", "v", "pred_level", "angle"]:
+        arrays["K." + k] = getattr(K, k).reshape(-1)
+    out = run(driver, tmp_path, "kf", arrays)
+    n_ref, s_ref = oc.kf(oracle, F, K, th, orb, True, slot_mp.astype(np.int32))
+    assert int(out["nmatches"][0]) == n_ref
+    np.testing.assert_array_equal(out["slot_mp"], s_ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["bow_kf_f", "bow_kf_kf"])
+def test_adapter_search_by_bow(driver, tmp_path, oracle, mode):
+    rng = np.random.default_rng(730 + len(mode))
+    A, B = fr.synth_bow_pair(rng, n_kf=1200, n_f=1200, n_nodes=100)
+    for S in (A, B):  # a good slot holds a MapPoint
+        S.mp_good = (S.mp_good.astype(bool) & (S.mp_id >= 0)).astype(np.uint8)
+    nn = 0.7
+    arrays = {**bow_arrays("B1.", A), **bow_arrays("B2.", B), "params": np.array([nn, 1.0], np.float32)}
+    out = run(driver, tmp_path, mode, arrays)
+    n_ref, o_ref = getattr(oc, mode)(oracle, A, B, nn, True)
+    assert int(out["nmatches"][0]) == n_ref
+    np.testing.assert_array_equal(out["out_mp"], o_ref)
+
+
+@pytest.mark.gpu
+def test_adapter_pose_optimization(driver, tmp_path, ctx):
+    rng = np.random.default_rng(740)
+    P = op.synth_pose_problem(rng, n_edges=400)
+    P.obs = P.obs.astype(np.float32).astype(np.float64)  # keypoints / mvuRight are float in the reference
+    arrays = {"P.kind": P.kind.astype(np.uint8), "P.xw": P.xw.reshape(-1), "P.obs": P.obs.reshape(-1),
+              "P.inv_sigma2": P.inv_sigma2, "P.pose": P.pose, "P.cam": cam_array(P.cam)}
+    out = run(driver, tmp_path, "pose", arrays)
+    ref = op.Optimizer(ctx).PoseOptimization(P)
+    assert int(out["n_inliers"][0]) == ref.n_inliers
+    np.testing.assert_array_equal(out["outlier"], ref.outlier)
+    np.testing.assert_array_equal(out["pose"], ref.pose)
+
+
+@pytest.mark.gpu
+def test_adapter_local_bundle_adjustment(driver, tmp_path, ctx):
+    rng = np.random.default_rng(750)
+    G = op.synth_lba_graph(rng, n_kf=10, n_points=800, stereo_frac=0.3)
+    assert len(G.cams) == 1 and (G.e_cam == 0).all()
+    # the adapter emits edges in MapPoint order x observation-map order (KeyFrame order here)
+    order = np.lexsort((G.e_pose, G.e_point))
+    for k in ["e_point", "e_pose", "e_kind", "e_cam", "e_obs", "e_inv_sigma2"]:
+        setattr(G, k, np.ascontiguousarray(getattr(G, k)[order]))
+    G.e_obs = G.e_obs.astype(np.float32).astype(np.float64)
+    pairs = set(zip(G.e_point.tolist(), G.e_pose.tolist()))
+    assert len(pairs) == len(G.e_point), "one observation per (MapPoint, KeyFrame)"
+    arrays = {"G.pose": G.pose.reshape(-1), "G.pose_fixed": G.pose_fixed.astype(np.uint8),
+              "G.point": G.point.reshape(-1), "G.e_point": G.e_point.astype(np.int32),
+              "G.e_pose": G.e_pose.astype(np.int32), "G.e_kind": G.e_kind.astype(np.uint8),
+              "G.e_obs": G.e_obs.reshape(-1), "G.e_inv_sigma2": G.e_inv_sigma2.astype(np.float32),
+              "G.cam": cam_array(G.cams[0])}
+    out = run(driver, tmp_path, "lba", arrays)
+    ref = op.Optimizer(ctx).LocalBundleAdjustment(G)
+    assert int(out["num_edges"][0]) == len(G.e_point)
+    np.testing.assert_array_equal(out["edge_bad"], ref.edge_bad)
+    np.testing.assert_array_equal(out["pose"].reshape(-1, 7), ref.pose.reshape(-1, 7))
+    np.testing.assert_array_equal(out["point"].reshape(-1, 3), ref.point.reshape(-1, 3))

@@ -92,7 +92,7 @@ def test_lba_user_lambda_and_stop_flag(ctx, oracle):
     G = op.synth_lba_graph(rng, n_kf=8, n_points=600)
     G.user_lambda_init = 100.0  # inertial maps: setUserLambdaInit(100)
     check_lba(ctx, oracle, G)
-    stop = np.ones(1, np.int32)
+    stop = np.ones(1, np.uint8)  # the reference's bool *pbStopFlag
     r = op.Optimizer(ctx).LocalBundleAdjustment(G, stop_flag=stop)
     assert r.aborted == 1 and r.iterations == 0
     np.testing.assert_array_equal(r.pose, G.pose)
