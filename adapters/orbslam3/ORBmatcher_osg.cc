@@ -1,0 +1,44 @@
+// ORBmatcher_osg.cc — drop-in bodies for the ORBmatcher operators on the MI355X path, for an
+// ORB-SLAM3 tree built with -DORB_SLAM3_OSG.  The reference's
+// src/ORBmatcher.cc keeps every other member; the bodies below replace the six hot-path ones
+// under #ifdef ORB_SLAM3_OSG (signatures: ref:include/ORBmatcher.h:36-66).
+#include "ORBmatcher.h"
+#include "osg_hooks_orbslam3.h"
+
+namespace ORB_SLAM3 {
+
+using H = OsgHooks;
+
+int ORBmatcher::DescriptorDistance(const cv::Mat &a, const cv::Mat &b)
+{  // ref:src/ORBmatcher.cc:2388-2408 (host scalar; batched distances run on the GPU inside the searches)
+    return osg_orbslam3::descriptor_distance(a, b);
+}
+
+int ORBmatcher::SearchByProjection(Frame &F, const std::vector<MapPoint *> &vpMapPoints, const float th,
+                                   const bool bFarPoints, const float thFarPoints)
+{  // ref:src/ORBmatcher.cc:44-242
+    return osg_orbslam3::search_by_projection_mps<H>(F, vpMapPoints, th, bFarPoints, thFarPoints, mfNNratio);
+}
+
+int ORBmatcher::SearchByProjection(Frame &CurrentFrame, const Frame &LastFrame, const float th, const bool bMono)
+{  // ref:src/ORBmatcher.cc:1957-2191
+    return osg_orbslam3::search_by_projection_last<H>(CurrentFrame, LastFrame, th, bMono, mbCheckOrientation);
+}
+
+int ORBmatcher::SearchByProjection(Frame &CurrentFrame, KeyFrame *pKF, const std::set<MapPoint *> &sAlreadyFound,
+                                   const float th, const int ORBdist)
+{  // ref:src/ORBmatcher.cc:2203-2330
+    return osg_orbslam3::search_by_projection_kf<H>(CurrentFrame, pKF, sAlreadyFound, th, ORBdist, mbCheckOrientation);
+}
+
+int ORBmatcher::SearchByBoW(KeyFrame *pKF, Frame &F, std::vector<MapPoint *> &vpMapPointMatches)
+{  // ref:src/ORBmatcher.cc:262-496
+    return osg_orbslam3::search_by_bow_kf_f<H>(pKF, F, vpMapPointMatches, mfNNratio, mbCheckOrientation);
+}
+
+int ORBmatcher::SearchByBoW(KeyFrame *pKF1, KeyFrame *pKF2, std::vector<MapPoint *> &vpMatches12)
+{  // ref:src/ORBmatcher.cc:890-1043
+    return osg_orbslam3::search_by_bow_kf_kf<H>(pKF1, pKF2, vpMatches12, mfNNratio, mbCheckOrientation);
+}
+
+}  // namespace ORB_SLAM3

@@ -1,0 +1,99 @@
+// osg_hooks_orbslam3.h — the hook policy of osg_orbslam3.h written with ORB-SLAM3's own Sophus /
+// Eigen / GeometricCamera calls, so every float the reference computes before its matching and
+// optimisation loops is computed by the same code.  Compiled only inside an ORB-SLAM3 tree.
+#ifndef OSG_HOOKS_ORBSLAM3_H
+#define OSG_HOOKS_ORBSLAM3_H
+
+#include "Frame.h"
+#include "KeyFrame.h"
+#include "MapPoint.h"
+#include "osg_orbslam3.h"
+
+namespace ORB_SLAM3 {
+
+struct OsgHooks {
+    template <class T>
+    static void pose(T &o, double q[7])
+    {
+        const Sophus::SE3<float> Tcw = const_cast<T &>(o).GetPose();
+        const Eigen::Quaterniond qd = Tcw.unit_quaternion().cast<double>();
+        const Eigen::Vector3d t = Tcw.translation().cast<double>();
+        q[0] = qd.x(); q[1] = qd.y(); q[2] = qd.z(); q[3] = qd.w();
+        q[4] = t.x(); q[5] = t.y(); q[6] = t.z();
+    }
+    template <class T>
+    static void set_pose(T &o, const double q[7])
+    {  // ref:src/Optimizer.cc:413-416 / 2187-2195: SE3Quat estimate -> SE3f
+        const Eigen::Quaternionf qf(Eigen::Quaterniond(q[3], q[0], q[1], q[2]).cast<float>());
+        o.SetPose(Sophus::SE3<float>(qf, Eigen::Vector3d(q[4], q[5], q[6]).cast<float>()));
+    }
+    static void world_pos(MapPoint *p, double x[3])
+    {
+        const Eigen::Vector3d X = p->GetWorldPos().cast<double>();
+        x[0] = X.x(); x[1] = X.y(); x[2] = X.z();
+    }
+    static void set_world_pos(MapPoint *p, const double x[3])
+    {  // ref:src/Optimizer.cc:2197-2203
+        p->SetWorldPos(Eigen::Vector3d(x[0], x[1], x[2]).cast<float>());
+        p->UpdateNormalAndDepth();
+    }
+    template <class T>
+    static void camera(const T &o, bool right, osg_camera &c)
+    {
+        std::memset(&c, 0, sizeof c);
+        GeometricCamera *cam = right ? o.mpCamera2 : o.mpCamera;
+        c.type = (cam->GetType() == GeometricCamera::CAM_FISHEYE) ? OSG_CAM_KB8 : OSG_CAM_PINHOLE;
+        for (size_t i = 0; i < cam->size() && i < 8; i++) c.p[i] = cam->getParameter((int)i);
+        c.fx = o.fx; c.fy = o.fy; c.cx = o.cx; c.cy = o.cy; c.bf = o.mbf;
+        c.trl[3] = 1.0;
+        if (right) {
+            const Sophus::SE3f Trl = const_cast<T &>(o).GetRelativePoseTrl();
+            const Eigen::Quaterniond qd = Trl.unit_quaternion().cast<double>();
+            const Eigen::Vector3d t = Trl.translation().cast<double>();
+            c.trl[0] = qd.x(); c.trl[1] = qd.y(); c.trl[2] = qd.z(); c.trl[3] = qd.w();
+            c.trl[4] = t.x(); c.trl[5] = t.y(); c.trl[6] = t.z();
+        }
+    }
+    // ref:src/ORBmatcher.cc:1993-2009; the invz < 0 and image-bounds tests stay in the kernel
+    static bool project_last(const Frame &CF, MapPoint *pMP, float &u, float &v, float &invz)
+    {
+        const Sophus::SE3f Tcw = const_cast<Frame &>(CF).GetPose();
+        const Eigen::Vector3f x3Dw = pMP->GetWorldPos();
+        const Eigen::Vector3f x3Dc = Tcw * x3Dw;
+        invz = 1.0 / x3Dc(2);
+        const Eigen::Vector2f uv = CF.mpCamera->project(x3Dc);
+        u = uv(0);
+        v = uv(1);
+        return true;
+    }
+    // ref:src/ORBmatcher.cc:1972-1980
+    static float tlc_z(const Frame &CF, const Frame &LF)
+    {
+        const Sophus::SE3f Tcw = const_cast<Frame &>(CF).GetPose();
+        const Eigen::Vector3f twc = Tcw.inverse().translation();
+        const Sophus::SE3f Tlw = const_cast<Frame &>(LF).GetPose();
+        const Eigen::Vector3f tlc = Tlw * twc;
+        return tlc(2);
+    }
+    // ref:src/ORBmatcher.cc:2238-2262: projection, image bounds, scale-invariance range, PredictScale
+    static bool kf_query(const Frame &CF, MapPoint *pMP, float &u, float &v, int &level)
+    {
+        Frame &F = const_cast<Frame &>(CF);
+        const Sophus::SE3f Tcw = F.GetPose();
+        const Eigen::Vector3f Ow = Tcw.inverse().translation();
+        const Eigen::Vector3f x3Dw = pMP->GetWorldPos();
+        const Eigen::Vector3f x3Dc = Tcw * x3Dw;
+        const Eigen::Vector2f uv = CF.mpCamera->project(x3Dc);
+        if (uv(0) < CF.mnMinX || uv(0) > CF.mnMaxX) return false;
+        if (uv(1) < CF.mnMinY || uv(1) > CF.mnMaxY) return false;
+        const float dist3D = (x3Dw - Ow).norm();
+        if (dist3D < pMP->GetMinDistanceInvariance() || dist3D > pMP->GetMaxDistanceInvariance()) return false;
+        level = pMP->PredictScale(dist3D, &F);
+        u = uv(0);
+        v = uv(1);
+        return true;
+    }
+};
+
+}  // namespace ORB_SLAM3
+#endif

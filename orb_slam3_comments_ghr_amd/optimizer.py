@@ -285,10 +285,23 @@ def synth_pose_problem(rng, n_edges=400, stereo_frac=0.6, outlier_frac=0.1, n_le
     cam = cam or pinhole_camera()
     Rcw = small_rotation(rng, 20.0)
     tcw = rng.normal(0, 1.0, 3)
-    u = rng.uniform(20, EUROC_W - 20, n_edges)
-    v = rng.uniform(20, EUROC_H - 20, n_edges)
-    z = rng.uniform(1.0, 10.0, n_edges)
-    Xc = np.stack([(u - EUROC_CX) / EUROC_FX * z, (v - EUROC_CY) / EUROC_FY * z, z], 1)
+    if cam.type == _abi.CAM_KB8:
+        # fisheye (TUM-VI-like 512 x 512): directions up to 70 deg off-axis, projected by KB8
+        th = rng.uniform(0.05, 1.2, n_edges)
+        ps = rng.uniform(-np.pi, np.pi, n_edges)
+        d = rng.uniform(1.0, 10.0, n_edges)
+        Xc = np.stack([d * np.sin(th) * np.cos(ps), d * np.sin(th) * np.sin(ps), d * np.cos(th)], 1)
+        k = [float(cam.p[i]) for i in range(8)]
+        r = th + k[4] * th ** 3 + k[5] * th ** 5 + k[6] * th ** 7 + k[7] * th ** 9
+        u = k[0] * r * np.cos(ps) + k[2]
+        v = k[1] * r * np.sin(ps) + k[3]
+        z = Xc[:, 2]
+        stereo_frac = 0.0  # no rectified stereo on a fisheye rig
+    else:
+        u = rng.uniform(20, EUROC_W - 20, n_edges)
+        v = rng.uniform(20, EUROC_H - 20, n_edges)
+        z = rng.uniform(1.0, 10.0, n_edges)
+        Xc = np.stack([(u - EUROC_CX) / EUROC_FX * z, (v - EUROC_CY) / EUROC_FY * z, z], 1)
     Xw = (Xc - tcw) @ Rcw  # Rcw^T (Xc - t)
     Xw = Xw.astype(np.float32).astype(np.float64)
     octv = rng.choice(n_levels, n_edges, p=np.array([1.2 ** -i for i in range(n_levels)]) / sum(1.2 ** -i for i in range(n_levels)))

@@ -21,6 +21,7 @@ pytestmark = pytest.mark.gpu
 POSE_TOL = 1e-6       # quaternion / translation components after 4 x 10 LM iterations
 STATE_TOL = 1e-6      # LBA poses and points (metres / unit quaternion)
 CHI2_RTOL = 1e-9
+KB8_POSE_TOL = 2e-5  # fisheye: libm vs device atan2f (see test_pose_optimization_kb8_fisheye)
 
 
 def trials_close(a, b):
@@ -39,6 +40,25 @@ def test_pose_optimization_batch(ctx, oracle):
         assert trials_close(g.lm_trials, r.lm_trials), (i, g.lm_trials, r.lm_trials)
         np.testing.assert_array_equal(g.outlier, r.outlier)
         np.testing.assert_allclose(g.pose, r.pose, atol=POSE_TOL, rtol=0)
+
+
+def test_pose_optimization_kb8_fisheye(ctx, oracle):
+    """KannalaBrandt8 camera (TUM-VI-like fisheye): project / projectJac with float atan2f.  The
+    device atan2f and glibc 2.35's (faithful, not correctly rounded: 16 % of random arguments
+    differ from the correctly rounded value) disagree by an ulp at times, which makes the cost
+    piecewise constant at ~1e-7 relative: converged poses agree to 2e-5 (classification exactly)
+    and the accept/reject sign near convergence can flip once per round (iteration totals over
+    the 4 rounds within +-4)."""
+    rng = np.random.default_rng(14)
+    probs = [op.synth_pose_problem(rng, n_edges=int(rng.integers(30, 400)), cam=op.kb8_camera()) for _ in range(16)]
+    ref = op.oracle_pose(oracle, probs)
+    got = op.Optimizer(ctx).PoseOptimization(probs)
+    for i, (g, r) in enumerate(zip(got, ref)):
+        assert g.n_inliers == r.n_inliers, i
+        assert r.n_inliers > 0.6 * len(probs[i].kind), "fisheye problems are well posed"
+        assert abs(g.lm_iterations - r.lm_iterations) <= 4, (i, g.lm_iterations, r.lm_iterations)
+        np.testing.assert_array_equal(g.outlier, r.outlier)
+        np.testing.assert_allclose(g.pose, r.pose, atol=KB8_POSE_TOL, rtol=0)
 
 
 def test_pose_optimization_small_and_degenerate(ctx, oracle):
