@@ -32,6 +32,20 @@ PEAK_VALU_TOPS = 256 * 128 * 2.4e9 / 1e12  # 256 CU x 4 SIMD32 x 32 lanes x 2.4 
 VALU_OPS_PER_PAIR = 19         # 8 v_xor + 8 v_bcnt(acc) + 1 v_lshl_or + v_med3 + v_min
 
 
+def job_totals(elapsed, units, world, dist=None, device="cpu"):
+    """Whole-job figures from per-rank (elapsed seconds, units processed): the slowest rank's time
+    (max over ranks) and the units of all ranks (sum).  Weak scaling: every rank processes its own
+    independent frames / windows; the only collectives are these two reductions and barriers."""
+    if world == 1 or dist is None:
+        return float(elapsed), float(units)
+    import torch
+    mx = torch.tensor([float(elapsed)], dtype=torch.float64, device=device)
+    sm = torch.tensor([float(units)], dtype=torch.float64, device=device)
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+    return float(mx.item()), float(sm.item())
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -97,12 +111,9 @@ def main():
     barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
     pairs_per_step = nq * nt
-    value = world * pairs_per_step * args.steps / elapsed / 1e6
+    elapsed, total_pairs = job_totals(elapsed, pairs_per_step * args.steps, world, dist if world > 1 else None, dev)
+    value = total_pairs / elapsed / 1e6
 
     # ---- dominant kernel roofline: HIP events on the launch stream -------------------------
     # The kernel's average duration = (end - start) / n over n back-to-back launches between two
@@ -241,13 +252,8 @@ def bench_lba(ctx, rank, world, dist, dev, args):
         iters += r.iterations
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([el, iters], dtype=torch.float64, device=dev)
-        mx = tt.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = tt.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        el, iters = float(mx[0].item()), int(sm[1].item())
+    el, iters = job_totals(el, iters, world, dist if world > 1 else None, dev)
+    iters = int(iters)
     res = {
         "metric": "LocalBA iters/s", "value": round(iters / el, 1), "unit": "LM iterations/s",
         "workload": f"C4: {len(G.pose)} KF x {len(G.point)} points x {len(G.e_point)} mono edges, optimize(10), {reps} LBAs per rank",
