@@ -66,6 +66,17 @@ struct OsgHooks {
         v = uv(1);
         return true;
     }
+    // ref:src/ORBmatcher.cc:2096-2097: right-camera projection of a two-camera current frame (the
+    // reference projects Trl * x3Dc with mpCamera)
+    static void project_last_right(const Frame &CF, MapPoint *pMP, float &u, float &v)
+    {
+        Frame &F = const_cast<Frame &>(CF);
+        const Eigen::Vector3f x3Dc = F.GetPose() * pMP->GetWorldPos();
+        const Eigen::Vector3f x3Dr = F.GetRelativePoseTrl() * x3Dc;
+        const Eigen::Vector2f uv = CF.mpCamera->project(x3Dr);
+        u = uv(0);
+        v = uv(1);
+    }
     // ref:src/ORBmatcher.cc:1972-1980
     static float tlc_z(const Frame &CF, const Frame &LF)
     {

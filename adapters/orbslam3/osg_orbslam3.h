@@ -88,13 +88,29 @@ inline void copy_desc_rows(const MatT &m, int n, std::vector<uint8_t> &out)
     for (int i = 0; i < n; i++) std::memcpy(&out[(size_t)32 * i], m.template ptr<unsigned char>(i), 32);
 }
 
+// 64 x 48 grid of vectors as CSR in GetFeaturesInArea's enumeration order (ix outer, iy inner,
+// cell contents in insertion order)
+template <class GridT>
+inline void grid_csr(const GridT &grid, std::vector<int32_t> &gs, std::vector<int32_t> &gi)
+{
+    gs.assign(OSG_GRID_CELLS + 1, 0);
+    gi.clear();
+    for (int ix = 0; ix < OSG_GRID_COLS; ix++)
+        for (int iy = 0; iy < OSG_GRID_ROWS; iy++) {
+            const auto &cell = grid[ix][iy];
+            gs[ix * OSG_GRID_ROWS + iy + 1] = (int32_t)cell.size();
+            for (auto idx : cell) gi.push_back((int32_t)idx);
+        }
+    for (int c = 0; c < OSG_GRID_CELLS; c++) gs[c + 1] += gs[c];
+}
+
 // osg_frame of a Frame (ref:include/Frame.h:218-296): keypoints (mvKeysUn, or mvKeys + mvKeysRight
-// for a two-camera rig), descriptors, mvuRight, the 64 x 48 grid as CSR in GetFeaturesInArea's
-// enumeration order (ix outer, iy inner, cell contents in insertion order).
+// for a two-camera rig), descriptors, mvuRight, mGrid (+ mGridRight, mvLeftToRightMatch,
+// mvRightToLeftMatch for a two-camera rig).
 template <class FrameT>
 struct FrameView {
     std::vector<float> kx, ky, ka, ur, scale;
-    std::vector<int32_t> ko, gs, gi;
+    std::vector<int32_t> ko, gs, gi, gsr, gir, l2r, r2l;
     std::vector<uint8_t> desc;
     osg_frame v{};
 
@@ -110,14 +126,18 @@ struct FrameView {
         copy_desc_rows(F.mDescriptors, n, desc);
         ur.assign(F.mvuRight.begin(), F.mvuRight.end());
         ur.resize(n, -1.0f);
-        gs.assign(OSG_GRID_CELLS + 1, 0);
-        for (int ix = 0; ix < OSG_GRID_COLS; ix++)
-            for (int iy = 0; iy < OSG_GRID_ROWS; iy++) {
-                const auto &cell = F.mGrid[ix][iy];
-                gs[ix * OSG_GRID_ROWS + iy + 1] = (int32_t)cell.size();
-                for (auto idx : cell) gi.push_back((int32_t)idx);
-            }
-        for (int c = 0; c < OSG_GRID_CELLS; c++) gs[c + 1] += gs[c];
+        grid_csr(F.mGrid, gs, gi);
+        if (F.Nleft != -1) {
+            grid_csr(F.mGridRight, gsr, gir);
+            l2r.assign(F.mvLeftToRightMatch.begin(), F.mvLeftToRightMatch.end());
+            r2l.assign(F.mvRightToLeftMatch.begin(), F.mvRightToLeftMatch.end());
+            l2r.resize(F.Nleft, -1);
+            r2l.resize(n - F.Nleft, -1);
+            v.grid_start_r = gsr.data();
+            v.grid_idx_r = gir.data();
+            v.left_to_right = l2r.data();
+            v.right_to_left = r2l.data();
+        }
         scale.assign(F.mvScaleFactors.begin(), F.mvScaleFactors.end());
         v.n = n;
         v.nleft = F.Nleft;
@@ -249,8 +269,13 @@ int search_by_projection_last(FrameT &CF, const FrameT &LF, float th, bool bMono
     const int n = LF.N;
     std::vector<int32_t> id(n, -1), oct(n, 0);
     std::vector<uint8_t> desc((size_t)n * 32), valid(n, 0), has_obs(n, 0);
-    std::vector<float> u(n), v(n), invz(n), ang(n);
+    std::vector<float> u(n), v(n), invz(n), ang(n), ur, vr;
     std::vector<MapPointT *> queries(n, nullptr);
+    const bool two = CF.Nleft != -1;
+    if (two) {
+        ur.assign(n, 0.f);
+        vr.assign(n, 0.f);
+    }
     for (int i = 0; i < n; i++) {
         MapPointT *p = LF.mvpMapPoints[i];
         const auto &kp = (LF.Nleft == -1) ? LF.mvKeysUn[i]
@@ -259,6 +284,7 @@ int search_by_projection_last(FrameT &CF, const FrameT &LF, float th, bool bMono
         ang[i] = kp.angle;
         if (!p || LF.mvbOutlier[i]) continue;
         if (!H::project_last(CF, p, u[i], v[i], invz[i])) continue;
+        if (two) H::project_last_right(CF, p, ur[i], vr[i]);  // ref:src/ORBmatcher.cc:2096-2097
         valid[i] = 1;
         id[i] = i;
         queries[i] = p;
@@ -277,6 +303,10 @@ int search_by_projection_last(FrameT &CF, const FrameT &LF, float th, bool bMono
     q.invz = invz.data();
     q.octave = oct.data();
     q.angle = ang.data();
+    if (two) {
+        q.u_r = ur.data();
+        q.v_r = vr.data();
+    }
     q.tlc_z = H::tlc_z(CF, LF);
     Slots<MapPointT> slots(CF.mvpMapPoints, n, true);
     const int nm = check(ctx, osg_search_by_projection_last(ctx, &fv.v, &q, th, bMono, checkOri, slots.mp.data(),
@@ -358,7 +388,9 @@ int search_by_bow_kf_f(KeyFrameT *pKF, FrameT &F, std::vector<MapPointT *> &vpMa
     copy_desc_rows(pKF->mDescriptors, nk, dk);
     copy_desc_rows(F.mDescriptors, nf, df);
     for (int i = 0; i < nk; i++) {
-        ak[i] = pKF->mvKeysUn[i].angle;
+        // ref:src/ORBmatcher.cc:399-401
+        ak[i] = (!pKF->mpCamera2) ? pKF->mvKeysUn[i].angle
+                                  : (i >= pKF->NLeft ? pKF->mvKeysRight[i - pKF->NLeft].angle : pKF->mvKeys[i].angle);
         good[i] = vpMPsKF[i] && !vpMPsKF[i]->isBad();
         if (vpMPsKF[i]) idk[i] = i;
     }
@@ -388,13 +420,14 @@ int search_by_bow_kf_kf(KeyFrameT *pKF1, KeyFrameT *pKF2, std::vector<MapPointT 
     std::vector<int32_t> id1(n1, -1), id2(n2, -1);
     copy_desc_rows(pKF1->mDescriptors, n1, d1);
     copy_desc_rows(pKF2->mDescriptors, n2, d2);
+    // only keypoints below mvKeysUn.size() are ever matched (== NLeft on a two-camera rig)
     for (int i = 0; i < n1; i++) {
-        a1[i] = pKF1->mvKeysUn[i].angle;
+        a1[i] = i < (int)pKF1->mvKeysUn.size() ? pKF1->mvKeysUn[i].angle : 0.f;
         g1[i] = v1[i] && !v1[i]->isBad();
         if (v1[i]) id1[i] = i;
     }
     for (int i = 0; i < n2; i++) {
-        a2[i] = pKF2->mvKeysUn[i].angle;
+        a2[i] = i < (int)pKF2->mvKeysUn.size() ? pKF2->mvKeysUn[i].angle : 0.f;
         g2[i] = v2[i] && !v2[i]->isBad();
         if (v2[i]) id2[i] = i;
     }

@@ -224,6 +224,12 @@ int osg_search_by_bow_kf_f(osg_ctx *ctx, const osg_bow_side *kf, const osg_bow_s
 int osg_search_by_bow_kf_kf(osg_ctx *ctx, const osg_bow_side *kf1, const osg_bow_side *kf2,
                             float nnratio, int check_orientation, int32_t *out_mp12);
 
+/* Diagnostics of the last search call on this context: out[0] candidates enumerated, out[1]
+ * Jacobi rounds, out[2] 1 if the greedy was redone serially (a5 on a two-camera rig when a
+ * stereo-partner write by a MapPoint without observations unblocked a slot), out[3] nmatches.
+ * No reference counterpart. */
+int osg_match_last_stats(osg_ctx *ctx, int32_t *out4);
+
 #ifdef __cplusplus
 }
 #endif

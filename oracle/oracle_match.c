@@ -585,9 +585,10 @@ int oracle_search_by_bow_kf_f(const osg_bow_side *KF, const osg_bow_side *F, flo
 }
 
 /* ---- a4: SearchByBoW(KeyFrame*, KeyFrame*, vector<MapPoint*>&) -------------------------- */
-/* ref:src/ORBmatcher.cc:890-1043.  kf->n is mvKeysUn.size() for the NLeft guard
- * (idx >= mvKeysUn.size() skipped, ref:src/ORBmatcher.cc:934-936,953-955); the caller passes
- * n_un = mvKeysUn.size() in ...->n and a FeatureVector possibly holding larger indices. */
+/* ref:src/ORBmatcher.cc:890-1043.  Two-camera keyframes skip idx >= mvKeysUn.size()
+ * (ref:src/ORBmatcher.cc:934-936,953-955).  For a two-camera rig mvKeysUn = mvKeys holds the left
+ * keypoints only (ref:src/Frame.cc:1022,1485), so mvKeysUn.size() == NLeft; the FeatureVector
+ * (built on the vconcat'ed descriptors) can hold indices up to N. */
 int oracle_search_by_bow_kf_kf(const osg_bow_side *K1, const osg_bow_side *K2, float nnratio,
                                int checkOri, int32_t *out_mp12)
 {
@@ -602,13 +603,13 @@ int oracle_search_by_bow_kf_kf(const osg_bow_side *K1, const osg_bow_side *K2, f
         if (K1->fv.node_id[f1] == K2->fv.node_id[f2]) {
             for (int a = K1->fv.node_start[f1]; a < K1->fv.node_start[f1 + 1]; a++) {
                 const int idx1 = K1->fv.feat[a];
-                if (K1->nleft != -1 && idx1 >= K1->n) continue;
+                if (K1->nleft != -1 && idx1 >= K1->nleft) continue;
                 if (!K1->mp_good[idx1]) continue;
                 const uint8_t *d1 = K1->desc + (size_t)idx1 * 32;
                 int bestDist1 = 256, bestIdx2 = -1, bestDist2 = 256;
                 for (int b = K2->fv.node_start[f2]; b < K2->fv.node_start[f2 + 1]; b++) {
                     const int idx2 = K2->fv.feat[b];
-                    if (K2->nleft != -1 && idx2 >= K2->n) continue;
+                    if (K2->nleft != -1 && idx2 >= K2->nleft) continue;
                     if (vbMatched2[idx2] || K2->mp_id[idx2] < 0) continue;
                     if (!K2->mp_good[idx2]) continue;
                     const int dist = oracle_descriptor_distance(d1, K2->desc + (size_t)idx2 * 32);

@@ -115,6 +115,12 @@ class Context:
         self.check(self.lib.osg_hamming_top2_plan(self.handle, int(nq), int(nt), buf, 160), "osg_hamming_top2_plan")
         return buf.value.decode()
 
+    def match_last_stats(self) -> dict:
+        """Diagnostics of the last search call: candidates, Jacobi rounds, serial redo, nmatches."""
+        out = np.zeros(4, np.int32)
+        self.check(self.lib.osg_match_last_stats(self.handle, _ptr(out)), "osg_match_last_stats")
+        return dict(candidates=int(out[0]), rounds=int(out[1]), serial=bool(out[2]), nmatches=int(out[3]))
+
     def descriptor_distance_pairs(self, a: np.ndarray, b: np.ndarray) -> np.ndarray:
         a = np.ascontiguousarray(a, dtype=np.uint8).reshape(-1, 32)
         b = np.ascontiguousarray(b, dtype=np.uint8).reshape(-1, 32)

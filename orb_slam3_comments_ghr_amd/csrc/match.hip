@@ -40,12 +40,15 @@ constexpr int INT_BIG = 0x7FFFFFFF;
 
 struct MatchArgs {
     int nq, n_slots;
+    int nleft;                // slot side: Frame::Nleft (-1: one camera / rectified stereo)
     // slot side (Frame F / KeyFrame 2)
     const uint32_t *fdesc;
     const float *kp_x, *kp_y, *slot_angle;
     const int32_t *kp_octave;
-    const float *u_right;
+    const float *u_right;     // NULL for a two-camera rig (the u_R check needs Nleft == -1)
     const int32_t *grid_start, *grid_idx;
+    const int32_t *grid_start_r, *grid_idx_r;   // mGridRight, indices relative to nleft
+    const int32_t *l2r, *r2l;                    // mvLeftToRightMatch / mvRightToLeftMatch
     float min_x, max_x, min_y, max_y, inv_w, inv_h;
     const float *scale;
     float mb, mbf;
@@ -57,6 +60,10 @@ struct MatchArgs {
     const float *q_x, *q_y, *q_f0, *q_f1, *q_f2;
     const int32_t *q_lvl;
     const uint8_t *q_m0, *q_m1;
+    // right-camera query fields (two-camera rig)
+    const float *q_xr, *q_yr, *q_f0r;
+    const int32_t *q_lvl_r;
+    const uint8_t *q_m0r;
     const int32_t *q_cb, *q_ce, *cand_list;
     const uint8_t *slot_ok;
     const int32_t *slot_mp2;  // KF-KF: KF2 MapPoint ids
@@ -68,11 +75,12 @@ struct MatchArgs {
     const uint8_t *slot_taken;
     int32_t *out_q;           // KF-KF: per query result
     // scratch
-    int32_t *q_off;
+    int32_t *q_off;           // nq + 1: candidate CSR
+    int32_t *q_mid;           // nq: first right-camera candidate of each query
     uint32_t *cands;
-    int32_t *q_res;
-    uint8_t *q_bin;
-    int32_t *status;          // [0] candidates needed, [1] nmatches, [2] rounds, [3] overflow
+    int32_t *q_res;           // 2 nq: {left slot, right slot}, -1 = no match
+    uint8_t *q_bin;           // 2 nq
+    int32_t *status;          // [0] candidates, [1] nmatches, [2] rounds, [3] overflow, [4] serial
     int cap;
 };
 
@@ -81,6 +89,11 @@ struct Win {
     int minL, maxL;
     float sx, sr;
     bool valid, stereo;
+};
+
+// result of one query: the slot matched by the left (or only) camera pass and by the right pass
+struct QRes {
+    int l, r;
 };
 
 __device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc)
@@ -110,6 +123,7 @@ __device__ __forceinline__ float radius_by_viewing_cos(float viewCos)
     return ((double)viewCos > 0.998) ? 2.5f : 4.0f;
 }
 
+// Search window of the left (or only) camera pass.
 template <int MODE>
 __device__ Win query_window(const MatchArgs &A, int q)
 {
@@ -179,8 +193,46 @@ __device__ Win query_window(const MatchArgs &A, int q)
     return w;
 }
 
+// Search window of the right-camera pass of a two-camera rig.  wl / cl: the left window and its
+// candidate count (GetFeaturesInArea size).
+template <int MODE>
+__device__ Win query_window_r(const MatchArgs &A, int q, const Win &wl, int cl)
+{
+    Win w;
+    w.valid = false;
+    w.stereo = false;
+    w.sx = 0.f;
+    w.sr = 0.f;
+    if (A.nleft < 0) return w;
+    if (MODE == MODE_MPS) {
+        // ref:src/ORBmatcher.cc:185-196: mbTrackInViewR, mnTrackScaleLevelR != -1, radius from
+        // mTrackViewCosR (no th factor), levels (lvl-1, lvl), right grid at mTrackProjXR/YR
+        if (!A.q_m0r[q]) return w;
+        if (A.far_points && A.q_f2[q] > A.th_far) return w;
+        if (!A.q_m1[q]) return w;
+        const int lvl = A.q_lvl_r[q];
+        if (lvl == -1) return w;
+        w.r = radius_by_viewing_cos(A.q_f0r[q]) * A.scale[lvl];
+        w.x = A.q_xr[q];
+        w.y = A.q_yr[q];
+        w.minL = lvl - 1;
+        w.maxL = lvl;
+        w.valid = true;
+    } else if (MODE == MODE_LAST) {
+        // ref:src/ORBmatcher.cc:2096-2110: same radius and levels at the right-camera projection;
+        // an empty left window has already 'continue'd (:2040-2041)
+        if (!wl.valid || cl == 0) return w;
+        w = wl;
+        w.x = A.q_xr[q];
+        w.y = A.q_yr[q];
+        w.stereo = false;
+    }
+    return w;
+}
+
 // Frame::GetFeaturesInArea (ref:src/Frame.cc:868-962) + the caller's static per-candidate skips.
-template <bool FILL>
+// RIGHT walks mGridRight; candidates are written as slot indices (right keypoints at nleft + i).
+template <bool FILL, bool RIGHT>
 __device__ int enum_grid(const MatchArgs &A, const Win &w, const uint32_t (&qd)[8], uint32_t *out)
 {
     const float factorX = w.r, factorY = w.r;
@@ -197,31 +249,34 @@ __device__ int enum_grid(const MatchArgs &A, const Win &w, const uint32_t (&qd)[
     if (maxCY > OSG_GRID_ROWS - 1) maxCY = OSG_GRID_ROWS - 1;
     if (maxCY < 0) return 0;
     const bool bCheckLevels = (w.minL > 0) || (w.maxL >= 0);  // ref:src/Frame.cc:919 quirk
+    const int32_t *gs = RIGHT ? A.grid_start_r : A.grid_start;
+    const int32_t *gi = RIGHT ? A.grid_idx_r : A.grid_idx;
+    const int off = RIGHT ? A.nleft : 0;
     int cnt = 0;
     for (int ix = minCX; ix <= maxCX; ix++) {
         for (int iy = minCY; iy <= maxCY; iy++) {
             const int cell = ix * OSG_GRID_ROWS + iy;
-            const int j1 = A.grid_start[cell + 1];
-            for (int j = A.grid_start[cell]; j < j1; j++) {
-                const int idx = A.grid_idx[j];
-                const int oct = A.kp_octave[idx];
+            const int j1 = gs[cell + 1];
+            for (int j = gs[cell]; j < j1; j++) {
+                const int k = gi[j] + off;
+                const int oct = A.kp_octave[k];
                 if (bCheckLevels) {
                     if (oct < w.minL) continue;
                     if (w.maxL >= 0 && oct > w.maxL) continue;
                 }
-                const float distx = A.kp_x[idx] - w.x;
-                const float disty = A.kp_y[idx] - w.y;
+                const float distx = A.kp_x[k] - w.x;
+                const float disty = A.kp_y[k] - w.y;
                 if (!(fabsf(distx) < factorX && fabsf(disty) < factorY)) continue;
-                if (w.stereo && A.u_right) {
-                    const float ur = A.u_right[idx];
+                if (!RIGHT && w.stereo && A.u_right) {
+                    const float ur = A.u_right[k];
                     if (ur > 0) {
                         const float er = fabsf(w.sx - ur);
                         if (er > w.sr) continue;
                     }
                 }
                 if (FILL) {
-                    const uint32_t d = dist256(qd, A.fdesc + (size_t)idx * 8);
-                    out[cnt] = (uint32_t)idx | (d << 16) | ((uint32_t)(oct & 0x7F) << 25);
+                    const uint32_t d = dist256(qd, A.fdesc + (size_t)k * 8);
+                    out[cnt] = (uint32_t)k | (d << 16) | ((uint32_t)(oct & 0x7F) << 25);
                 }
                 cnt++;
             }
@@ -230,8 +285,9 @@ __device__ int enum_grid(const MatchArgs &A, const Win &w, const uint32_t (&qd)[
     return cnt;
 }
 
+// Candidates of query q: left-camera ones first, then right-camera ones; cl = left count.
 template <int MODE, bool FILL>
-__device__ int enum_query(const MatchArgs &A, int q, uint32_t *out)
+__device__ int enum_query(const MatchArgs &A, int q, uint32_t *out, int &cl)
 {
     uint32_t qd[8];
     if (FILL) {
@@ -245,34 +301,33 @@ __device__ int enum_query(const MatchArgs &A, int q, uint32_t *out)
         const int e = A.q_ce[q];
         for (int j = A.q_cb[q]; j < e; j++) {
             const int idx = A.cand_list[j];
-            if (MODE == MODE_BOW_KF_KF && !A.slot_ok[idx]) continue;  // !pMP2 || isBad
+            if (MODE == MODE_BOW_KF_KF && !A.slot_ok[idx]) continue;  // !pMP2 || isBad || right camera
             if (FILL) {
                 const uint32_t d = dist256(qd, A.fdesc + (size_t)idx * 8);
                 out[cnt] = (uint32_t)idx | (d << 16);
             }
             cnt++;
         }
+        cl = cnt;
         return cnt;
     } else {
         const Win w = query_window<MODE>(A, q);
-        if (!w.valid) return 0;
-        return enum_grid<FILL>(A, w, qd, out);
+        const int c0 = w.valid ? enum_grid<FILL, false>(A, w, qd, out) : 0;
+        cl = c0;
+        int c1 = 0;
+        if (MODE == MODE_MPS || MODE == MODE_LAST) {
+            const Win wr = query_window_r<MODE>(A, q, w, c0);
+            if (wr.valid) c1 = enum_grid<FILL, true>(A, wr, qd, FILL ? out + c0 : nullptr);
+        }
+        return c0 + c1;
     }
 }
 
-// best / second over the candidates of q that are not taken before q (reference loop order)
-template <int MODE>
-__device__ __forceinline__ int eval_query(const MatchArgs &A, int q, const int *__restrict__ claim,
-                                          const uint8_t *__restrict__ taken0)
-{
+// bestDist / bestLevel / bestDist2 / bestLevel2 / bestIdx of the reference loops
+struct Top2 {
     int best = 256, bl = -1, second = 256, sl = -1, bslot = -1;
-    const int e1 = A.q_off[q + 1];
-    for (int e = A.q_off[q]; e < e1; e++) {
-        const uint32_t c = A.cands[e];
-        const int s = (int)(c & 0xFFFFu);
-        if (taken0[s] || claim[s] < q) continue;
-        const int d = (int)((c >> 16) & 0x1FFu);
-        const int l = (int)(c >> 25);
+    __device__ __forceinline__ void push(int d, int l, int s)
+    {
         if (d < best) {
             second = best;
             sl = bl;
@@ -284,18 +339,109 @@ __device__ __forceinline__ int eval_query(const MatchArgs &A, int q, const int *
             sl = l;
         }
     }
-    bool acc;
-    if (MODE == MODE_MPS)  // ref:src/ORBmatcher.cc:147-167
-        acc = best <= OSG_TH_HIGH && !(bl == sl && (float)best > A.nnratio * (float)second);
-    else if (MODE == MODE_LAST)  // ref:src/ORBmatcher.cc:2070
-        acc = best <= OSG_TH_HIGH;
-    else if (MODE == MODE_KF)  // ref:src/ORBmatcher.cc:2287
-        acc = best <= A.orb_dist;
-    else if (MODE == MODE_BOW_KF_F)  // ref:src/ORBmatcher.cc:392-395
-        acc = best <= OSG_TH_LOW && (float)best < A.nnratio * (float)second;
-    else  // MODE_BOW_KF_KF, ref:src/ORBmatcher.cc:985-987
-        acc = best < OSG_TH_LOW && (float)best < A.nnratio * (float)second;
-    return acc ? bslot : -1;
+};
+
+// One query in reference order.  blocked(s): is slot s unavailable to q given the assignments of
+// the queries before q (Jacobi: claims of the previous round; serial: the live slot state).
+template <int MODE, typename Blocked>
+__device__ __forceinline__ QRes eval_query(const MatchArgs &A, int q, Blocked blocked)
+{
+    QRes res{-1, -1};
+    const int e0 = A.q_off[q], em = A.q_mid[q], e1 = A.q_off[q + 1];
+    Top2 L, R;
+    if (MODE == MODE_BOW_KF_F) {
+        // ref:src/ORBmatcher.cc:316-441: one loop, separate top-2 for left / right keypoints
+        for (int e = e0; e < e1; e++) {
+            const uint32_t c = A.cands[e];
+            const int s = (int)(c & 0xFFFFu);
+            if (blocked(s)) continue;
+            const int d = (int)((c >> 16) & 0x1FFu);
+            if (A.nleft < 0 || s < A.nleft) L.push(d, 0, s);
+            else R.push(d, 0, s);
+        }
+        if (L.best <= OSG_TH_LOW) {
+            if ((float)L.best < A.nnratio * (float)L.second) res.l = L.bslot;
+            if (R.best <= OSG_TH_LOW) res.r = R.bslot;  // ratio disabled by '|| true' (:425)
+        }
+        return res;
+    }
+    for (int e = e0; e < em; e++) {
+        const uint32_t c = A.cands[e];
+        const int s = (int)(c & 0xFFFFu);
+        if (blocked(s)) continue;
+        L.push((int)((c >> 16) & 0x1FFu), (int)(c >> 25), s);
+    }
+    bool acc, skip_r = false;
+    if (MODE == MODE_MPS) {  // ref:src/ORBmatcher.cc:147-167 (a ratio failure 'continue's past the right pass)
+        acc = L.best <= OSG_TH_HIGH && !(L.bl == L.sl && (float)L.best > A.nnratio * (float)L.second);
+        skip_r = L.best <= OSG_TH_HIGH && !acc;
+    } else if (MODE == MODE_LAST) {  // ref:src/ORBmatcher.cc:2070
+        acc = L.best <= OSG_TH_HIGH;
+    } else if (MODE == MODE_KF) {  // ref:src/ORBmatcher.cc:2287
+        acc = L.best <= A.orb_dist;
+    } else {  // MODE_BOW_KF_KF, ref:src/ORBmatcher.cc:985-987
+        acc = L.best < OSG_TH_LOW && (float)L.best < A.nnratio * (float)L.second;
+    }
+    res.l = acc ? L.bslot : -1;
+    if ((MODE == MODE_MPS || MODE == MODE_LAST) && em < e1 && !skip_r) {
+        // the left pass of q itself may have written the stereo partner slot; its state is then
+        // q's own Observations() > 0
+        int own = -1;
+        bool own_blocked = false;
+        if (MODE == MODE_MPS && res.l >= 0 && A.l2r) {
+            const int t = A.l2r[res.l];
+            if (t != -1) {
+                own = t + A.nleft;
+                own_blocked = A.q_has_obs[q] != 0;
+            }
+        }
+        for (int e = em; e < e1; e++) {
+            const uint32_t c = A.cands[e];
+            const int s = (int)(c & 0xFFFFu);
+            if (s == own ? own_blocked : blocked(s)) continue;
+            R.push((int)((c >> 16) & 0x1FFu), (int)(c >> 25), s);
+        }
+        bool accr;
+        if (MODE == MODE_MPS)  // ref:src/ORBmatcher.cc:222-238
+            accr = R.best <= OSG_TH_HIGH && !(R.bl == R.sl && (float)R.best > A.nnratio * (float)R.second);
+        else  // ref:src/ORBmatcher.cc:2133
+            accr = R.best <= OSG_TH_HIGH;
+        res.r = accr ? R.bslot : -1;
+    }
+    return res;
+}
+
+// Every slot q writes: the direct matches and, for a5 on a two-camera rig, each one's stereo
+// partner (ref:src/ORBmatcher.cc:154-163, 226-236).  Returns the count (<= 4).
+template <int MODE>
+__device__ __forceinline__ int assigned_slots(const MatchArgs &A, QRes r, int (&out)[4])
+{
+    int n = 0;
+    if (r.l >= 0) {
+        out[n++] = r.l;
+        if (MODE == MODE_MPS && A.l2r) {
+            const int t = A.l2r[r.l];
+            if (t != -1) out[n++] = t + A.nleft;
+        }
+    }
+    if (r.r >= 0) {
+        if (MODE == MODE_MPS && A.r2l) {
+            const int t = A.r2l[r.r - A.nleft];
+            if (t != -1) out[n++] = t;
+        }
+        out[n++] = r.r;
+    }
+    return n;
+}
+
+__device__ __forceinline__ QRes load_res(const MatchArgs &A, int q)
+{
+    return QRes{A.q_res[2 * q], A.q_res[2 * q + 1]};
+}
+__device__ __forceinline__ void store_res(const MatchArgs &A, int q, QRes r)
+{
+    A.q_res[2 * q] = r.l;
+    A.q_res[2 * q + 1] = r.r;
 }
 
 __device__ __forceinline__ int rot_bin(float a, float b)
@@ -331,7 +477,8 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A)
     // ---- 1. count
     int my = 0;
     for (int q = q0; q < q1; q++) {
-        const int c = enum_query<MODE, false>(A, q, nullptr);
+        int cl;
+        const int c = enum_query<MODE, false>(A, q, nullptr, cl);
         A.q_off[q] = c;  // temporarily the count
         my += c;
     }
@@ -357,9 +504,10 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A)
         int off = s_scan[tid] - my;
         for (int q = q0; q < q1; q++) {
             const int c = A.q_off[q];
+            int cl;
             A.q_off[q] = off;
-            const int w = enum_query<MODE, true>(A, q, A.cands + off);
-            (void)w;
+            enum_query<MODE, true>(A, q, A.cands + off, cl);
+            A.q_mid[q] = off + cl;
             off += c;
         }
         if (tid == MT - 1) A.q_off[nq] = total;
@@ -377,24 +525,30 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A)
     }
     if (tid < OSG_HISTO_LENGTH) s_hist[tid] = 0;
     __syncthreads();
-    for (int q = q0; q < q1; q++) A.q_res[q] = eval_query<MODE>(A, q, claimA, taken0);
+    for (int q = q0; q < q1; q++)
+        store_res(A, q, eval_query<MODE>(A, q, [&](int s) { return taken0[s] || claimA[s] < q; }));
     __syncthreads();
+    // Jacobi rounds.  A slot is blocked for q when it was blocked initially or a query p < q
+    // whose MapPoint has observations wrote it (SearchByBoW / a7: any earlier write).
     int rounds = 0;
     int *cur = claimB, *other = claimA;
     for (;;) {
         rounds++;
         for (int q = q0; q < q1; q++) {
-            const int r = A.q_res[q];
             const bool claims = (MODE == MODE_MPS || MODE == MODE_LAST) ? (A.q_has_obs[q] != 0) : true;
-            if (r >= 0 && claims) atomicMin(&cur[r], q);
+            if (!claims) continue;
+            int sl[4];
+            const int n = assigned_slots<MODE>(A, load_res(A, q), sl);
+            for (int i = 0; i < n; i++) atomicMin(&cur[sl[i]], q);
         }
         __syncthreads();
         int changed = 0;
         for (int q = q0; q < q1; q++) {
-            const int r2 = eval_query<MODE>(A, q, cur, taken0);
-            if (r2 != A.q_res[q]) {
+            const QRes r2 = eval_query<MODE>(A, q, [&](int s) { return taken0[s] || cur[s] < q; });
+            const QRes r1 = load_res(A, q);
+            if (r2.l != r1.l || r2.r != r1.r) {
                 changed = 1;
-                A.q_res[q] = r2;
+                store_res(A, q, r2);
             }
         }
         for (int s = tid; s < NS; s += MT) other[s] = INT_BIG;
@@ -404,18 +558,60 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A)
         other = t;
         if (!any || rounds > nq + 1) break;
     }
+    // 'other' now holds the claims of the converged results.  The monotone rule above is exact
+    // unless a stereo-partner write of a5 by a MapPoint WITHOUT observations lands on a slot that
+    // was blocked: that write unblocks it (the slot's state is its last writer's).  Such a run is
+    // redone serially in query order on the live slot state.
+    int serial = 0;
+    if (MODE == MODE_MPS && A.nleft >= 0) {
+        int need = 0;
+        for (int q = q0; q < q1; q++) {
+            if (A.q_has_obs[q]) continue;
+            const QRes r = load_res(A, q);
+            if (r.l >= 0 && A.l2r && A.l2r[r.l] != -1) {
+                const int s = A.l2r[r.l] + A.nleft;
+                need |= (taken0[s] || other[s] < q) ? 1 : 0;
+            }
+            if (r.r >= 0 && A.r2l && A.r2l[r.r - A.nleft] != -1) {
+                const int s = A.r2l[r.r - A.nleft];
+                need |= (taken0[s] || other[s] < q) ? 1 : 0;
+            }
+        }
+        serial = __syncthreads_or(need);
+        if (serial) {
+            if (tid == 0) {
+                for (int q = 0; q < nq; q++) {
+                    const QRes r = eval_query<MODE>(A, q, [&](int s) { return taken0[s] != 0; });
+                    store_res(A, q, r);
+                    int sl[4];
+                    const int n = assigned_slots<MODE>(A, r, sl);
+                    for (int i = 0; i < n; i++) taken0[sl[i]] = A.q_has_obs[q];
+                }
+            }
+            __syncthreads();
+        }
+    }
     // ---- 5. finish: last assignment, rotation histogram, removal, counts
     int nacc = 0;
     const bool ori = A.check_ori && MODE != MODE_MPS;
     for (int q = q0; q < q1; q++) {
-        const int r = A.q_res[q];
-        if (r < 0) continue;
-        nacc++;
-        if (MODE != MODE_BOW_KF_KF) atomicMax(&lastS[r], q);
+        const QRes r = load_res(A, q);
+        int sl[4];
+        const int n = assigned_slots<MODE>(A, r, sl);
+        nacc += n;
+        if (MODE != MODE_BOW_KF_KF)
+            for (int i = 0; i < n; i++) atomicMax(&lastS[sl[i]], q);
         if (ori) {
-            const int bin = rot_bin(A.q_angle[q], A.slot_angle[r]);
-            A.q_bin[q] = (uint8_t)bin;
-            atomicAdd(&s_hist[bin], 1);
+            if (r.l >= 0) {
+                const int bin = rot_bin(A.q_angle[q], A.slot_angle[r.l]);
+                A.q_bin[2 * q] = (uint8_t)bin;
+                atomicAdd(&s_hist[bin], 1);
+            }
+            if (r.r >= 0) {
+                const int bin = rot_bin(A.q_angle[q], A.slot_angle[r.r]);
+                A.q_bin[2 * q + 1] = (uint8_t)bin;
+                atomicAdd(&s_hist[bin], 1);
+            }
         }
     }
     __syncthreads();
@@ -449,17 +645,26 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A)
     __syncthreads();
     int nrem = 0;
     for (int q = q0; q < q1; q++) {
-        const int r = A.q_res[q];
-        bool removed = false;
-        if (r >= 0 && ori) {
-            const int bin = A.q_bin[q];
-            removed = !(bin == s_keep[0] || bin == s_keep[1] || bin == s_keep[2]);
-            if (removed) {
-                nrem++;
-                if (MODE != MODE_BOW_KF_KF) removedS[r] = 1;
+        const QRes r = load_res(A, q);
+        bool removed_l = false;
+        if (ori) {
+            if (r.l >= 0) {
+                const int bin = A.q_bin[2 * q];
+                removed_l = !(bin == s_keep[0] || bin == s_keep[1] || bin == s_keep[2]);
+                if (removed_l) {
+                    nrem++;
+                    if (MODE != MODE_BOW_KF_KF) removedS[r.l] = 1;
+                }
+            }
+            if (r.r >= 0) {
+                const int bin = A.q_bin[2 * q + 1];
+                if (!(bin == s_keep[0] || bin == s_keep[1] || bin == s_keep[2])) {
+                    nrem++;
+                    removedS[r.r] = 1;
+                }
             }
         }
-        if (MODE == MODE_BOW_KF_KF) A.out_q[q] = (r >= 0 && !removed) ? A.slot_mp2[r] : -1;
+        if (MODE == MODE_BOW_KF_KF) A.out_q[q] = (r.l >= 0 && !removed_l) ? A.slot_mp2[r.l] : -1;
     }
     atomicAdd(&s_red[0], nacc - nrem);
     __syncthreads();
@@ -474,6 +679,7 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A)
         A.status[2] = rounds;
         A.status[0] = total;
         A.status[3] = 0;
+        A.status[4] = serial;
     }
 }
 
@@ -514,17 +720,22 @@ int run_match(osg_ctx *ctx, MatchArgs A, const osg_packer &pk, int32_t *host_slo
     size_t lds = match_lds_bytes(NS);
     for (int attempt = 0; attempt < 2; attempt++) {
         OSG_ALLOC(ctx, A.q_off, SLOT_TMP2, sizeof(int32_t) * ((size_t)nq + 1));
-        OSG_ALLOC(ctx, A.q_res, SLOT_TMP3, sizeof(int32_t) * ((size_t)nq + 1));
-        OSG_ALLOC(ctx, A.q_bin, SLOT_TMP4, (size_t)nq + 16);
+        OSG_ALLOC(ctx, A.q_res, SLOT_TMP3, sizeof(int32_t) * 2 * ((size_t)nq + 1));
+        OSG_ALLOC(ctx, A.q_bin, SLOT_TMP4, 2 * (size_t)nq + 16);
+        OSG_ALLOC(ctx, A.q_mid, SLOT_TMP6, sizeof(int32_t) * ((size_t)nq + 1));
         OSG_ALLOC(ctx, A.cands, SLOT_TMP5, sizeof(uint32_t) * (size_t)cap);
         A.cap = cap;
         hipLaunchKernelGGL(k_match<MODE>, dim3(1), dim3(MT), lds, ctx->stream, A);
         OSG_HIP_CHECK(ctx, hipGetLastError());
-        int32_t st[4];
+        int32_t st[5];
         OSG_HIP_CHECK(ctx, hipMemcpyAsync(st, dev_io, sizeof st, hipMemcpyDeviceToHost, ctx->stream));
         OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
         if (st[3] == 0) {
             *out_nmatches = st[1];
+            ctx->match_stats[0] = st[0];
+            ctx->match_stats[1] = st[2];
+            ctx->match_stats[2] = st[4];
+            ctx->match_stats[3] = st[1];
             break;
         }
         cap = st[0] + 1024;
@@ -562,7 +773,9 @@ void relocate(T *&field, char *base)
         relocate(A.q_f0, base); relocate(A.q_f1, base); relocate(A.q_f2, base); relocate(A.q_lvl, base);     \
         relocate(A.q_m0, base); relocate(A.q_m1, base); relocate(A.q_cb, base); relocate(A.q_ce, base);     \
         relocate(A.cand_list, base); relocate(A.slot_ok, base); relocate(A.slot_mp2, base);                  \
-        relocate(A.slot_taken, base);                                                                        \
+        relocate(A.slot_taken, base); relocate(A.grid_start_r, base); relocate(A.grid_idx_r, base);          \
+        relocate(A.l2r, base); relocate(A.r2l, base); relocate(A.q_xr, base); relocate(A.q_yr, base);       \
+        relocate(A.q_f0r, base); relocate(A.q_lvl_r, base); relocate(A.q_m0r, base);                         \
     } while (0)
 
 template <int MODE>
@@ -581,14 +794,22 @@ int launch_packed(osg_ctx *ctx, MatchArgs &A, osg_packer &pk, int32_t *host_slot
 void frame_into_args(MatchArgs &A, osg_packer &pk, const osg_frame *F)
 {
     A.n_slots = F->n;
+    A.nleft = F->nleft;
     set_off(A.fdesc, pk.add(F->desc, (size_t)F->n * 32));
     set_off(A.kp_x, pk.add(F->kp_x, sizeof(float) * F->n));
     set_off(A.kp_y, pk.add(F->kp_y, sizeof(float) * F->n));
     set_off(A.slot_angle, pk.add(F->kp_angle, sizeof(float) * F->n));
     set_off(A.kp_octave, pk.add(F->kp_octave, sizeof(int32_t) * F->n));
-    set_off(A.u_right, pk.add(F->u_right, sizeof(float) * F->n));
+    // the u_R check runs only for Nleft == -1 (ref:src/ORBmatcher.cc:97, :2055)
+    set_off(A.u_right, F->nleft == -1 ? pk.add(F->u_right, sizeof(float) * F->n) : SIZE_MAX);
     set_off(A.grid_start, pk.add(F->grid_start, sizeof(int32_t) * (OSG_GRID_CELLS + 1)));
-    set_off(A.grid_idx, pk.add(F->grid_idx, sizeof(int32_t) * (F->grid_start ? F->grid_start[OSG_GRID_CELLS] : 0)));
+    set_off(A.grid_idx, pk.add(F->grid_idx, sizeof(int32_t) * F->grid_start[OSG_GRID_CELLS]));
+    if (F->nleft != -1) {
+        set_off(A.grid_start_r, pk.add(F->grid_start_r, sizeof(int32_t) * (OSG_GRID_CELLS + 1)));
+        set_off(A.grid_idx_r, pk.add(F->grid_idx_r, sizeof(int32_t) * F->grid_start_r[OSG_GRID_CELLS]));
+        set_off(A.l2r, pk.add(F->left_to_right, sizeof(int32_t) * F->nleft));
+        set_off(A.r2l, pk.add(F->right_to_left, sizeof(int32_t) * (F->n - F->nleft)));
+    }
     set_off(A.scale, pk.add(F->scale_factors, sizeof(float) * F->n_levels));
     A.min_x = F->min_x;
     A.max_x = F->max_x;
@@ -600,13 +821,36 @@ void frame_into_args(MatchArgs &A, osg_packer &pk, const osg_frame *F)
     A.mbf = F->mbf;
 }
 
+// A grid in CSR must index keypoints [0, n_cam) only: the kernels trust it.
+static int check_grid(osg_ctx *ctx, const int32_t *gs, const int32_t *gi, int n_cam, const char *which)
+{
+    OSG_REQUIRE(ctx, gs && (gi || gs[OSG_GRID_CELLS] == 0), "%s grid missing", which);
+    OSG_REQUIRE(ctx, gs[0] == 0, "%s grid_start[0] != 0", which);
+    for (int c = 0; c < OSG_GRID_CELLS; c++)
+        OSG_REQUIRE(ctx, gs[c + 1] >= gs[c], "%s grid_start not monotone at cell %d", which, c);
+    const int m = gs[OSG_GRID_CELLS];
+    for (int j = 0; j < m; j++)
+        OSG_REQUIRE(ctx, gi[j] >= 0 && gi[j] < n_cam, "%s grid_idx[%d] = %d out of range", which, j, gi[j]);
+    return OSG_OK;
+}
+
 int check_frame(osg_ctx *ctx, const osg_frame *F)
 {
     OSG_REQUIRE(ctx, F && F->n >= 0 && F->n <= MAX_SLOTS, "frame n out of range");
-    if (F->nleft != -1)
-        return osg_set_error(ctx, OSG_E_UNSUPPORTED, "two-camera frames (Nleft != -1) are not implemented on the GPU path yet");
+    OSG_REQUIRE(ctx, F->nleft == -1 || (F->nleft >= 0 && F->nleft <= F->n), "frame nleft out of range");
     OSG_REQUIRE(ctx, F->n == 0 || (F->desc && F->kp_x && F->kp_y && F->kp_angle && F->kp_octave), "frame arrays");
-    OSG_REQUIRE(ctx, F->grid_start && F->grid_idx && F->scale_factors && F->n_levels > 0, "frame grid");
+    OSG_REQUIRE(ctx, F->scale_factors && F->n_levels > 0, "frame scale factors");
+    const int nl = F->nleft == -1 ? F->n : F->nleft;
+    int rc = check_grid(ctx, F->grid_start, F->grid_idx, nl, "left");
+    if (rc < 0) return rc;
+    if (F->nleft != -1) {
+        rc = check_grid(ctx, F->grid_start_r, F->grid_idx_r, F->n - F->nleft, "right");
+        if (rc < 0) return rc;
+        for (int i = 0; F->left_to_right && i < F->nleft; i++)
+            OSG_REQUIRE(ctx, F->left_to_right[i] >= -1 && F->left_to_right[i] < F->n - F->nleft, "left_to_right[%d]", i);
+        for (int i = 0; F->right_to_left && i < F->n - F->nleft; i++)
+            OSG_REQUIRE(ctx, F->right_to_left[i] >= -1 && F->right_to_left[i] < F->nleft, "right_to_left[%d]", i);
+    }
     return OSG_OK;
 }
 
@@ -628,6 +872,12 @@ int osg_search_by_projection_mps(osg_ctx *ctx, const osg_frame *F, const osg_mp_
     for (int i = 0; i < Q->n; i++)
         if (Q->in_view[i] && (Q->pred_level[i] < 0 || Q->pred_level[i] >= F->n_levels))
             return osg_set_error(ctx, OSG_E_INVALID, "pred_level[%d] = %d out of range", i, Q->pred_level[i]);
+    if (F->nleft != -1) {
+        OSG_REQUIRE(ctx, Q->in_view_r && Q->proj_yr && Q->view_cos_r && Q->pred_level_r, "right-camera query arrays");
+        for (int i = 0; i < Q->n; i++)
+            if (Q->in_view_r[i] && (Q->pred_level_r[i] < -1 || Q->pred_level_r[i] >= F->n_levels))
+                return osg_set_error(ctx, OSG_E_INVALID, "pred_level_r[%d] = %d out of range", i, Q->pred_level_r[i]);
+    }
     MatchArgs A = {};
     osg_packer pk;
     frame_into_args(A, pk, F);
@@ -645,6 +895,13 @@ int osg_search_by_projection_mps(osg_ctx *ctx, const osg_frame *F, const osg_mp_
     set_off(A.q_f2, pk.add(Q->track_depth, sizeof(float) * n));
     set_off(A.q_lvl, pk.add(Q->pred_level, sizeof(int32_t) * n));
     set_off(A.slot_taken, pk.add(slot_taken, F->n));
+    if (F->nleft != -1) {
+        A.q_xr = A.q_f1;  // mTrackProjXR
+        set_off(A.q_yr, pk.add(Q->proj_yr, sizeof(float) * n));
+        set_off(A.q_f0r, pk.add(Q->view_cos_r, sizeof(float) * n));
+        set_off(A.q_lvl_r, pk.add(Q->pred_level_r, sizeof(int32_t) * n));
+        set_off(A.q_m0r, pk.add(Q->in_view_r, n));
+    }
     A.nnratio = nnratio;
     A.th = th;
     A.far_points = far_points;
@@ -680,6 +937,11 @@ int osg_search_by_projection_last(osg_ctx *ctx, const osg_frame *CF, const osg_l
     set_off(A.q_lvl, pk.add(L->octave, sizeof(int32_t) * n));
     set_off(A.q_angle, pk.add(L->angle, sizeof(float) * n));
     set_off(A.slot_taken, pk.add(slot_taken, CF->n));
+    if (CF->nleft != -1) {
+        OSG_REQUIRE(ctx, L->u_r && L->v_r, "right-camera projections (u_r, v_r)");
+        set_off(A.q_xr, pk.add(L->u_r, sizeof(float) * n));
+        set_off(A.q_yr, pk.add(L->v_r, sizeof(float) * n));
+    }
     A.th = th;
     A.mono = mono;
     A.tlc_z = L->tlc_z;
@@ -729,7 +991,8 @@ static int bow_queries(const osg_bow_side *A_, const osg_bow_side *B_, bool guar
         if (fa.node_id[ia] == fb.node_id[ib]) {
             for (int a = fa.node_start[ia]; a < fa.node_start[ia + 1]; a++) {
                 const int idx = fa.feat[a];
-                if (guard_nleft_a && A_->nleft != -1 && idx >= A_->n) continue;
+                // mvKeysUn.size() == NLeft on a two-camera rig (ref:src/ORBmatcher.cc:934-936)
+                if (guard_nleft_a && A_->nleft != -1 && idx >= A_->nleft) continue;
                 if (idx < 0 || idx >= A_->n) return -1;
                 if (!A_->mp_good[idx]) continue;
                 q_feat.push_back(idx);
@@ -765,8 +1028,7 @@ int osg_search_by_bow_kf_f(osg_ctx *ctx, const osg_bow_side *kf, const osg_bow_s
     if (!ctx) return OSG_E_INVALID;
     OSG_REQUIRE(ctx, kf && f && out_mp, "null argument");
     OSG_REQUIRE(ctx, f->n >= 0 && f->n <= MAX_SLOTS && kf->n >= 0, "sizes");
-    if (kf->nleft != -1 || f->nleft != -1)
-        return osg_set_error(ctx, OSG_E_UNSUPPORTED, "two-camera SearchByBoW not implemented on the GPU path yet");
+    OSG_REQUIRE(ctx, f->nleft == -1 || (f->nleft >= 0 && f->nleft <= f->n), "frame nleft");
     for (int i = 0; i < f->n; i++) out_mp[i] = -1;
     std::vector<int32_t> q_feat, q_cb, q_ce;
     if (bow_queries(kf, f, false, q_feat, q_cb, q_ce) < 0) return osg_set_error(ctx, OSG_E_INVALID, "feature index");
@@ -786,6 +1048,7 @@ int osg_search_by_bow_kf_f(osg_ctx *ctx, const osg_bow_side *kf, const osg_bow_s
     osg_packer pk;
     A.nq = n;
     A.n_slots = f->n;
+    A.nleft = f->nleft;
     set_off(A.fdesc, pk.add(f->desc, (size_t)f->n * 32));
     set_off(A.slot_angle, pk.add(f->angle, sizeof(float) * f->n));
     set_off(A.qdesc, pk.add(qdesc.data(), qdesc.size()));
@@ -805,8 +1068,8 @@ int osg_search_by_bow_kf_kf(osg_ctx *ctx, const osg_bow_side *kf1, const osg_bow
     if (!ctx) return OSG_E_INVALID;
     OSG_REQUIRE(ctx, kf1 && kf2 && out_mp12, "null argument");
     OSG_REQUIRE(ctx, kf2->n >= 0 && kf2->n <= MAX_SLOTS && kf1->n >= 0, "sizes");
-    if (kf1->nleft != -1 || kf2->nleft != -1)
-        return osg_set_error(ctx, OSG_E_UNSUPPORTED, "two-camera SearchByBoW not implemented on the GPU path yet");
+    OSG_REQUIRE(ctx, kf1->nleft == -1 || (kf1->nleft >= 0 && kf1->nleft <= kf1->n), "kf1 nleft");
+    OSG_REQUIRE(ctx, kf2->nleft == -1 || (kf2->nleft >= 0 && kf2->nleft <= kf2->n), "kf2 nleft");
     for (int i = 0; i < kf1->n; i++) out_mp12[i] = -1;
     std::vector<int32_t> q_feat, q_cb, q_ce;
     if (bow_queries(kf1, kf2, true, q_feat, q_cb, q_ce) < 0) return osg_set_error(ctx, OSG_E_INVALID, "feature index");
@@ -820,11 +1083,14 @@ int osg_search_by_bow_kf_kf(osg_ctx *ctx, const osg_bow_side *kf1, const osg_bow
         std::memcpy(&qdesc[(size_t)i * 32], kf1->desc + (size_t)q_feat[i] * 32, 32);
         q_angle[i] = kf1->angle[q_feat[i]];
     }
-    for (int s = 0; s < kf2->n; s++) slot_ok[s] = (kf2->mp_id[s] >= 0 && kf2->mp_good[s]) ? 1 : 0;
+    // right-camera keypoints of a two-camera KF2 are skipped (ref:src/ORBmatcher.cc:953-955)
+    for (int s = 0; s < kf2->n; s++)
+        slot_ok[s] = (kf2->mp_id[s] >= 0 && kf2->mp_good[s] && (kf2->nleft == -1 || s < kf2->nleft)) ? 1 : 0;
     MatchArgs A = {};
     osg_packer pk;
     A.nq = n;
     A.n_slots = kf2->n;
+    A.nleft = -1;
     set_off(A.fdesc, pk.add(kf2->desc, (size_t)kf2->n * 32));
     set_off(A.slot_angle, pk.add(kf2->angle, sizeof(float) * kf2->n));
     set_off(A.slot_mp2, pk.add(kf2->mp_id, sizeof(int32_t) * kf2->n));

@@ -32,6 +32,7 @@ struct osg_ctx {
     size_t host_pinned_cap = 0;
     uint32_t *counters = nullptr;
     int num_cus = 256;
+    int32_t match_stats[4] = {};  // last matcher call: candidates, Jacobi rounds, serial redo, nmatches
     std::string last_error;
 };
 

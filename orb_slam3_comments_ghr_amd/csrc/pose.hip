@@ -108,7 +108,6 @@ __global__ __launch_bounds__(PT) void k_pose_opt(const PoseProbDev *__restrict__
     __shared__ double s_part27[PT / 64][27];
     __shared__ SE3 s_pose, s_backup;
     __shared__ double s_x[6];
-    __shared__ double s_scalar[4];  // lambda, ni, rho, currentChi
     __shared__ int s_flag[4];       // continue-trial, result, ok
     const PoseProbDev &P = probs[blockIdx.x];
     const int n = P.n_edges;

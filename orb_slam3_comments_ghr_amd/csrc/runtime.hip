@@ -132,6 +132,13 @@ int osg_ctx_synchronize(osg_ctx *ctx)
 
 const char *osg_ctx_last_error(osg_ctx *ctx) { return ctx ? ctx->last_error.c_str() : ""; }
 
+int osg_match_last_stats(osg_ctx *ctx, int32_t *out4)
+{
+    if (!ctx || !out4) return OSG_E_INVALID;
+    for (int i = 0; i < 4; i++) out4[i] = ctx->match_stats[i];
+    return OSG_OK;
+}
+
 // ref:src/ORBmatcher.cc:2388-2408 — host scalar form (the SWAR popcount as written).
 int osg_descriptor_distance(const uint8_t *a, const uint8_t *b)
 {

@@ -75,6 +75,11 @@ class FrameSoA:
     nleft: int = -1
     grid_start: np.ndarray | None = None
     grid_idx: np.ndarray | None = None
+    # two-camera rig (nleft != -1): keypoints [0, nleft) are mvKeys, [nleft, n) mvKeysRight
+    grid_start_r: np.ndarray | None = None
+    grid_idx_r: np.ndarray | None = None
+    left_to_right: np.ndarray | None = None   # mvLeftToRightMatch[nleft], -1 = none
+    right_to_left: np.ndarray | None = None   # mvRightToLeftMatch[n - nleft]
 
     def __post_init__(self):
         self.desc = _c(self.desc, np.uint8).reshape(-1, 32)
@@ -86,9 +91,17 @@ class FrameSoA:
         self.scale = _c(self.scale, np.float32)
         self.inv_w = np.float32(np.float32(_abi.GRID_COLS) / np.float32(self.max_x - self.min_x))
         self.inv_h = np.float32(np.float32(_abi.GRID_ROWS) / np.float32(self.max_y - self.min_y))
+        self.left_to_right = _c(self.left_to_right, np.int32)
+        self.right_to_left = _c(self.right_to_left, np.int32)
+        nl = self.n if self.nleft == -1 else self.nleft
         if self.grid_start is None:
-            self.grid_start, self.grid_idx = build_grid(self.kp_x, self.kp_y, self.min_x, self.min_y,
+            # AssignFeaturesToGrid (ref:src/Frame.cc:469-507): right keypoints go to mGridRight
+            # with indices relative to Nleft
+            self.grid_start, self.grid_idx = build_grid(self.kp_x[:nl], self.kp_y[:nl], self.min_x, self.min_y,
                                                         self.inv_w, self.inv_h)
+        if self.nleft != -1 and self.grid_start_r is None:
+            self.grid_start_r, self.grid_idx_r = build_grid(self.kp_x[nl:], self.kp_y[nl:], self.min_x,
+                                                            self.min_y, self.inv_w, self.inv_h)
 
     @property
     def n(self):
@@ -106,6 +119,10 @@ class FrameSoA:
         s.u_right = _p(self.u_right)
         s.grid_start = _p(self.grid_start)
         s.grid_idx = _p(self.grid_idx)
+        s.grid_start_r = _p(self.grid_start_r)
+        s.grid_idx_r = _p(self.grid_idx_r)
+        s.left_to_right = _p(self.left_to_right)
+        s.right_to_left = _p(self.right_to_left)
         s.min_x, s.max_x, s.min_y, s.max_y = self.min_x, self.max_x, self.min_y, self.max_y
         s.grid_inv_w = float(self.inv_w)
         s.grid_inv_h = float(self.inv_h)
@@ -130,19 +147,26 @@ class MPQueries:
     view_cos: np.ndarray
     pred_level: np.ndarray
     track_depth: np.ndarray
+    # right camera of a two-camera rig (Frame::isInFrustum with bRight, ref:src/Frame.cc:676-782)
+    in_view_r: np.ndarray | None = None     # mbTrackInViewR
+    proj_yr: np.ndarray | None = None       # mTrackProjYR (x is proj_xr)
+    view_cos_r: np.ndarray | None = None    # mTrackViewCosR
+    pred_level_r: np.ndarray | None = None  # mnTrackScaleLevelR, -1 = none
+
+    _FIELDS = [("mp_id", np.int32), ("desc", np.uint8), ("usable", np.uint8), ("has_obs", np.uint8),
+               ("in_view", np.uint8), ("proj_x", np.float32), ("proj_y", np.float32),
+               ("proj_xr", np.float32), ("view_cos", np.float32), ("pred_level", np.int32),
+               ("track_depth", np.float32), ("in_view_r", np.uint8), ("proj_yr", np.float32),
+               ("view_cos_r", np.float32), ("pred_level_r", np.int32)]
 
     def __post_init__(self):
-        for k, dt in [("mp_id", np.int32), ("desc", np.uint8), ("usable", np.uint8), ("has_obs", np.uint8),
-                      ("in_view", np.uint8), ("proj_x", np.float32), ("proj_y", np.float32),
-                      ("proj_xr", np.float32), ("view_cos", np.float32), ("pred_level", np.int32),
-                      ("track_depth", np.float32)]:
+        for k, dt in self._FIELDS:
             setattr(self, k, _c(getattr(self, k), dt))
 
     def struct(self):
         s = _abi.OsgMpQueries()
         s.n = len(self.mp_id)
-        for k in ["mp_id", "desc", "usable", "has_obs", "in_view", "proj_x", "proj_y", "proj_xr",
-                  "view_cos", "pred_level", "track_depth"]:
+        for k, _ in self._FIELDS:
             setattr(s, k, _p(getattr(self, k)))
         return s
 
@@ -160,17 +184,21 @@ class LastQueries:
     octave: np.ndarray
     angle: np.ndarray
     tlc_z: float = 0.0
+    u_r: np.ndarray | None = None   # mpCamera->project(Trl * x3Dc), two-camera rig only
+    v_r: np.ndarray | None = None
+
+    _FIELDS = [("mp_id", np.int32), ("desc", np.uint8), ("valid", np.uint8), ("has_obs", np.uint8),
+               ("u", np.float32), ("v", np.float32), ("invz", np.float32), ("octave", np.int32),
+               ("angle", np.float32), ("u_r", np.float32), ("v_r", np.float32)]
 
     def __post_init__(self):
-        for k, dt in [("mp_id", np.int32), ("desc", np.uint8), ("valid", np.uint8), ("has_obs", np.uint8),
-                      ("u", np.float32), ("v", np.float32), ("invz", np.float32), ("octave", np.int32),
-                      ("angle", np.float32)]:
+        for k, dt in self._FIELDS:
             setattr(self, k, _c(getattr(self, k), dt))
 
     def struct(self):
         s = _abi.OsgLastQueries()
         s.n = len(self.mp_id)
-        for k in ["mp_id", "desc", "valid", "has_obs", "u", "v", "invz", "octave", "angle"]:
+        for k, _ in self._FIELDS:
             setattr(s, k, _p(getattr(self, k)))
         s.tlc_z = float(self.tlc_z)
         return s
@@ -342,9 +370,11 @@ def _featvec(rng, n, n_nodes, zipf=1.1, node_base=0):
 
 
 def synth_bow_pair(rng, n_kf=1200, n_f=1200, n_nodes=100, mp_frac=0.7, copy_frac=0.6, flip=0.06,
-                   f_is_kf=False):
+                   f_is_kf=False, nleft_kf=-1, nleft_f=-1):
     """KF and F (or KF2) sharing a vocabulary: 60 % of the second side's descriptors are noisy copies
-    of KF features (same node), angle offset +7 deg +- 3."""
+    of KF features (same node), angle offset +7 deg +- 3.  ``nleft_*`` != -1 makes
+    that side a two-camera rig: indices >= nleft are right-camera keypoints, and its FeatureVector
+    holds both (ComputeBoW runs on the vconcat'ed descriptors)."""
     kf_desc = rng.integers(0, 256, (n_kf, 32), dtype=np.uint8)
     kf_ang = rng.uniform(0, 360, n_kf).astype(np.float32)
     w = 1.0 / np.arange(1, n_nodes + 1) ** 1.1
@@ -373,12 +403,98 @@ def synth_bow_pair(rng, n_kf=1200, n_f=1200, n_nodes=100, mp_frac=0.7, copy_frac
     b = fv(f_node)
     kf_mp = np.where(rng.random(n_kf) < mp_frac, 10000 + np.arange(n_kf), -1).astype(np.int32)
     kf_good = ((kf_mp >= 0) & (rng.random(n_kf) < 0.98)).astype(np.uint8)
-    KF = BowSide(kf_desc, kf_ang, kf_mp, kf_good, *a)
+    KF = BowSide(kf_desc, kf_ang, kf_mp, kf_good, *a, nleft=nleft_kf)
     if f_is_kf:
         f_mp = np.where(rng.random(n_f) < mp_frac, 20000 + np.arange(n_f), -1).astype(np.int32)
         f_good = ((f_mp >= 0) & (rng.random(n_f) < 0.98)).astype(np.uint8)
     else:
         f_mp = np.full(n_f, -1, np.int32)
         f_good = np.zeros(n_f, np.uint8)
-    Fb = BowSide(f_desc, f_ang, f_mp, f_good, *b)
+    Fb = BowSide(f_desc, f_ang, f_mp, f_good, *b, nleft=nleft_f)
     return KF, Fb
+
+
+# ---------------------------------------------------------------- two-camera rig generators
+
+def synth_frame_two_cam(rng, n_left=600, n_right=600, stereo_frac=0.5, n_levels=8):
+    """A two-camera Frame (ref:src/Frame.cc:1485-1536): Nleft = n_left, N = n_left + n_right,
+    descriptors vconcat(left, right).  ``stereo_frac`` of the right keypoints are stereo partners
+    of a left keypoint (ComputeStereoFishEyeMatches): shifted by a disparity, same octave, a
+    noisy copy of the left descriptor; mvLeftToRightMatch / mvRightToLeftMatch record the pairs."""
+    L = synth_frame(rng, n=n_left, stereo=False, n_levels=n_levels)
+    xr = rng.uniform(0, EUROC_W, n_right).astype(np.float32)
+    yr = rng.uniform(0, EUROC_H, n_right).astype(np.float32)
+    p = np.array([1.2 ** -i for i in range(n_levels)])
+    octr = rng.choice(n_levels, size=n_right, p=p / p.sum()).astype(np.int32)
+    angr = rng.uniform(0, 360, n_right).astype(np.float32)
+    descr = rng.integers(0, 256, (n_right, 32), dtype=np.uint8)
+    n_pair = int(stereo_frac * min(n_left, n_right))
+    li = rng.choice(n_left, size=n_pair, replace=False)
+    ri = rng.choice(n_right, size=n_pair, replace=False)
+    disp = rng.uniform(2, 60, n_pair)
+    xr[ri] = np.clip(L.kp_x[li] - disp, 0, EUROC_W - 1)
+    yr[ri] = np.clip(L.kp_y[li] + rng.normal(0, 0.5, n_pair), 0, EUROC_H - 1)
+    octr[ri] = L.kp_octave[li]
+    angr[ri] = np.mod(L.kp_angle[li] + rng.normal(0, 2, n_pair), 360)
+    descr[ri] = _flip(rng, L.desc[li], 0.03)
+    l2r = np.full(n_left, -1, np.int32)
+    r2l = np.full(n_right, -1, np.int32)
+    l2r[li] = ri
+    r2l[ri] = li
+    return FrameSoA(desc=np.concatenate([L.desc, descr]), kp_x=np.concatenate([L.kp_x, xr]),
+                    kp_y=np.concatenate([L.kp_y, yr]), kp_angle=np.concatenate([L.kp_angle, angr]),
+                    kp_octave=np.concatenate([L.kp_octave, octr]), u_right=None, nleft=n_left,
+                    left_to_right=l2r, right_to_left=r2l, scale=scale_factors(n_levels))
+
+
+def synth_mp_queries_two_cam(rng, F: FrameSoA, m=1500, noise_px=2.5, match_frac=0.7, right_only_frac=0.2):
+    """a5 queries for a two-camera Frame: the left-camera fields as synth_mp_queries, plus the
+    right projection (mbTrackInViewR, mTrackProjXR/YR, mTrackViewCosR, mnTrackScaleLevelR).
+    Matched queries copy a left keypoint (projected near its stereo partner on the right when it
+    has one) or, for ``right_only_frac`` of them, a right keypoint."""
+    nl, nr = F.nleft, F.n - F.nleft
+    nlev = len(F.scale)
+    is_match = rng.random(m) < match_frac
+    right_only = is_match & (rng.random(m) < right_only_frac)
+    tl = rng.integers(0, nl, m)
+    tr = np.where(right_only, rng.integers(0, nr, m), F.left_to_right[tl])
+    has_r = tr >= 0
+    trc = np.maximum(tr, 0)
+    px = np.where(is_match & ~right_only, F.kp_x[tl] + rng.normal(0, noise_px, m), rng.uniform(0, EUROC_W, m))
+    py = np.where(is_match & ~right_only, F.kp_y[tl] + rng.normal(0, noise_px, m), rng.uniform(0, EUROC_H, m))
+    pxr = np.where(is_match & has_r, F.kp_x[nl + trc] + rng.normal(0, noise_px, m), rng.uniform(0, EUROC_W, m))
+    pyr = np.where(is_match & has_r, F.kp_y[nl + trc] + rng.normal(0, noise_px, m), rng.uniform(0, EUROC_H, m))
+    desc = rng.integers(0, 256, (m, 32), dtype=np.uint8)
+    lm = is_match & ~right_only
+    desc[lm] = _flip(rng, F.desc[tl[lm]], 0.06)
+    desc[right_only] = _flip(rng, F.desc[nl + trc[right_only]], 0.06)
+    lvl = np.clip(F.kp_octave[tl] + rng.integers(-1, 2, m), 0, nlev - 1)
+    lvl_r = np.clip(F.kp_octave[nl + trc] + rng.integers(-1, 2, m), 0, nlev - 1)
+    lvl_r = np.where(rng.random(m) < 0.1, -1, lvl_r)
+    depth = rng.uniform(0.5, 60.0, m)
+    return MPQueries(
+        mp_id=np.arange(1000, 1000 + m), desc=desc, usable=rng.random(m) < 0.98,
+        has_obs=rng.random(m) < 0.93, in_view=rng.random(m) < 0.8, proj_x=px, proj_y=py,
+        proj_xr=pxr, view_cos=rng.uniform(0.99, 1.0, m), pred_level=lvl, track_depth=depth,
+        in_view_r=rng.random(m) < 0.75, proj_yr=pyr, view_cos_r=rng.uniform(0.99, 1.0, m),
+        pred_level_r=lvl_r)
+
+
+def synth_last_queries_two_cam(rng, F: FrameSoA, n_last=800, noise_px=2.0, match_frac=0.7, tlc_z=0.0):
+    """a6 queries for a two-camera current Frame: left projection as synth_last_queries, plus the
+    right-camera projection (u_r, v_r) near the left target's stereo partner when it has one."""
+    nl = F.nleft
+    L = synth_last_queries(rng, FrameSoA(desc=F.desc[:nl], kp_x=F.kp_x[:nl], kp_y=F.kp_y[:nl],
+                                         kp_angle=F.kp_angle[:nl], kp_octave=F.kp_octave[:nl],
+                                         scale=F.scale),
+                           n_last=n_last, noise_px=noise_px, match_frac=match_frac, tlc_z=tlc_z)
+    # nearest left keypoint of each projection stands in for the target
+    tl = np.argmin(np.abs(L.u[:, None] - F.kp_x[None, :nl]) + np.abs(L.v[:, None] - F.kp_y[None, :nl]), axis=1)
+    tr = F.left_to_right[tl]
+    ok = tr >= 0
+    trc = np.maximum(tr, 0)
+    L.u_r = np.where(ok, F.kp_x[nl + trc] + rng.normal(0, noise_px, n_last),
+                     rng.uniform(-20, EUROC_W + 20, n_last)).astype(np.float32)
+    L.v_r = np.where(ok, F.kp_y[nl + trc] + rng.normal(0, noise_px, n_last),
+                     rng.uniform(-20, EUROC_H + 20, n_last)).astype(np.float32)
+    return L

@@ -85,32 +85,48 @@ static const Arr &get(const Arrays &m, const std::string &k)
 
 static bool has(const Arrays &m, const std::string &k) { return m.count(k) != 0; }
 
-// Frame from the FrameSoA arrays "F.*" (keypoints, descriptors, mvuRight, grid CSR, scales)
+static void fill_grid(const Arrays &m, const std::string &pre, std::vector<std::size_t> (&grid)[OSG_GRID_COLS][OSG_GRID_ROWS])
+{
+    const int32_t *gs = get(m, pre + "grid_start").p<int32_t>(), *gi = get(m, pre + "grid_idx").p<int32_t>();
+    for (int ix = 0; ix < OSG_GRID_COLS; ix++)
+        for (int iy = 0; iy < OSG_GRID_ROWS; iy++) {
+            const int c = ix * OSG_GRID_ROWS + iy;
+            for (int j = gs[c]; j < gs[c + 1]; j++) grid[ix][iy].push_back((size_t)gi[j]);
+        }
+}
+
+// Frame from the FrameSoA arrays "F.*" (keypoints, descriptors, mvuRight, grid CSR, scales; for a
+// two-camera rig "F.nleft", the right grid and the stereo-partner maps)
 static void build_frame(const Arrays &m, Frame &F)
 {
     const int n = (int)get(m, "F.kp_x").n;
     F.N = n;
-    F.Nleft = -1;
+    F.Nleft = has(m, "F.nleft") ? get(m, "F.nleft").p<int32_t>()[0] : -1;
+    const int nl = F.Nleft == -1 ? n : F.Nleft;
     const float *x = get(m, "F.kp_x").p<float>(), *y = get(m, "F.kp_y").p<float>(), *a = get(m, "F.kp_angle").p<float>();
     const int32_t *o = get(m, "F.kp_octave").p<int32_t>();
-    F.mvKeysUn.resize(n);
+    std::vector<cv::KeyPoint> kps(n);
     for (int i = 0; i < n; i++) {
-        F.mvKeysUn[i].pt.x = x[i];
-        F.mvKeysUn[i].pt.y = y[i];
-        F.mvKeysUn[i].angle = a[i];
-        F.mvKeysUn[i].octave = o[i];
+        kps[i].pt.x = x[i];
+        kps[i].pt.y = y[i];
+        kps[i].angle = a[i];
+        kps[i].octave = o[i];
     }
-    F.mvKeys = F.mvKeysUn;
+    F.mvKeys.assign(kps.begin(), kps.begin() + nl);
+    F.mvKeysRight.assign(kps.begin() + nl, kps.end());
+    F.mvKeysUn = F.mvKeys;  // left keypoints only on a two-camera rig (ref:src/Frame.cc:1022)
+    if (F.Nleft != -1) {
+        fill_grid(m, "F.", F.mGrid);
+        fill_grid(m, "F.r_", F.mGridRight);
+        const Arr &l2r = get(m, "F.left_to_right"), &r2l = get(m, "F.right_to_left");
+        F.mvLeftToRightMatch.assign(l2r.p<int32_t>(), l2r.p<int32_t>() + l2r.n);
+        F.mvRightToLeftMatch.assign(r2l.p<int32_t>(), r2l.p<int32_t>() + r2l.n);
+    }
     F.mDescriptors = cv::Mat(n, 32);
     std::memcpy(F.mDescriptors.buf.data(), get(m, "F.desc").b.data(), (size_t)n * 32);
     F.mvuRight.assign(n, -1.0f);
     if (has(m, "F.u_right")) std::memcpy(F.mvuRight.data(), get(m, "F.u_right").b.data(), (size_t)n * 4);
-    const int32_t *gs = get(m, "F.grid_start").p<int32_t>(), *gi = get(m, "F.grid_idx").p<int32_t>();
-    for (int ix = 0; ix < OSG_GRID_COLS; ix++)
-        for (int iy = 0; iy < OSG_GRID_ROWS; iy++) {
-            const int c = ix * OSG_GRID_ROWS + iy;
-            for (int j = gs[c]; j < gs[c + 1]; j++) F.mGrid[ix][iy].push_back((size_t)gi[j]);
-        }
+    if (F.Nleft == -1) fill_grid(m, "F.", F.mGrid);
     const float *sc = get(m, "F.scalars").p<float>();  // min_x max_x min_y max_y inv_w inv_h mb mbf
     Frame::mnMinX = sc[0];
     Frame::mnMaxX = sc[1];
@@ -164,12 +180,18 @@ static void build_bow_kf(const Arrays &m, const std::string &pre, KeyFrame &K, s
     const Arr &d = get(m, pre + "desc");
     const int n = (int)(d.n / 32);
     K.N = n;
-    K.NLeft = -1;
+    K.NLeft = has(m, pre + "nleft") ? get(m, pre + "nleft").p<int32_t>()[0] : -1;
+    const int nl = K.NLeft == -1 ? n : K.NLeft;
     K.mDescriptors = cv::Mat(n, 32);
     std::memcpy(K.mDescriptors.buf.data(), d.b.data(), d.b.size());
-    K.mvKeysUn.resize(n);
     const float *ang = get(m, pre + "angle").p<float>();
-    for (int i = 0; i < n; i++) K.mvKeysUn[i].angle = ang[i];
+    std::vector<cv::KeyPoint> kps(n);
+    for (int i = 0; i < n; i++) kps[i].angle = ang[i];
+    K.mvKeys.assign(kps.begin(), kps.begin() + nl);
+    K.mvKeysRight.assign(kps.begin() + nl, kps.end());
+    K.mvKeysUn = K.mvKeys;
+    static Camera second;
+    K.mpCamera2 = K.NLeft == -1 ? nullptr : &second;
     K.mvpMapPoints.assign(n, nullptr);
     const int32_t *id = get(m, pre + "mp_id").p<int32_t>();
     const uint8_t *good = get(m, pre + "mp_good").p<uint8_t>();
@@ -215,6 +237,12 @@ int main(int argc, char **argv)
                 p->mTrackViewCos = get(in, "Q.view_cos").p<float>()[i];
                 p->mnTrackScaleLevel = get(in, "Q.pred_level").p<int32_t>()[i];
                 p->mTrackDepth = get(in, "Q.track_depth").p<float>()[i];
+                if (has(in, "Q.in_view_r")) {
+                    p->mbTrackInViewR = get(in, "Q.in_view_r").p<uint8_t>()[i];
+                    p->mTrackProjYR = get(in, "Q.proj_yr").p<float>()[i];
+                    p->mTrackViewCosR = get(in, "Q.view_cos_r").p<float>()[i];
+                    p->mnTrackScaleLevelR = get(in, "Q.pred_level_r").p<int32_t>()[i];
+                }
                 q[i] = p;
             }
             // params: nnratio th far thfar
@@ -245,6 +273,10 @@ int main(int argc, char **argv)
                 p->proj_u = get(in, "L.u").p<float>()[i];
                 p->proj_v = get(in, "L.v").p<float>()[i];
                 p->proj_invz = get(in, "L.invz").p<float>()[i];
+                if (has(in, "L.u_r")) {
+                    p->proj_ur = get(in, "L.u_r").p<float>()[i];
+                    p->proj_vr = get(in, "L.v_r").p<float>()[i];
+                }
                 LF.mvpMapPoints[i] = p;
                 LF.mvbOutlier[i] = !get(in, "L.valid").p<uint8_t>()[i];
             }
@@ -286,9 +318,12 @@ int main(int argc, char **argv)
             build_bow_kf(in, "B2.", KF, pool);
             Frame F;  // the Frame side: descriptors, angles, FeatureVector
             F.N = KF.N;
-            F.Nleft = -1;
+            F.Nleft = KF.NLeft;
             F.mDescriptors = KF.mDescriptors;
+            F.mvKeys = KF.mvKeys;
             F.mvKeysUn = KF.mvKeysUn;
+            F.mvKeysRight = KF.mvKeysRight;
+            F.mpCamera2 = KF.mpCamera2;
             F.mFeatVec = KF.mFeatVec;
             std::vector<MapPoint *> matches;
             // params: nnratio ori

@@ -59,7 +59,7 @@ struct MapPoint {
     float mTrackViewCos = 0, mTrackViewCosR = 0;
     // test-only: what MockHooks::project_last / kf_query return for this MapPoint
     bool proj_ok = false;
-    float proj_u = 0, proj_v = 0, proj_invz = 0;
+    float proj_u = 0, proj_v = 0, proj_invz = 0, proj_ur = 0, proj_vr = 0;
     int proj_level = 0;
     std::map<KeyFrame *, std::tuple<int, int>> obs;
 
@@ -78,6 +78,8 @@ struct Frame {
     std::vector<MapPoint *> mvpMapPoints;
     std::vector<bool> mvbOutlier;
     std::vector<std::size_t> mGrid[OSG_GRID_COLS][OSG_GRID_ROWS];
+    std::vector<std::size_t> mGridRight[OSG_GRID_COLS][OSG_GRID_ROWS];
+    std::vector<int> mvLeftToRightMatch, mvRightToLeftMatch;
     static inline float mnMinX = 0, mnMaxX = 0, mnMinY = 0, mnMaxY = 0;
     static inline float mfGridElementWidthInv = 0, mfGridElementHeightInv = 0;
     int mnScaleLevels = 8;
@@ -141,6 +143,11 @@ struct MockHooks {
         v = p->proj_v;
         invz = p->proj_invz;
         return p->proj_ok;
+    }
+    static void project_last_right(const Frame &, MapPoint *p, float &u, float &v)
+    {
+        u = p->proj_ur;
+        v = p->proj_vr;
     }
     static float tlc_z(const Frame &CF, const Frame &) { return CF.tlc_z_value; }
     static bool kf_query(const Frame &, MapPoint *p, float &u, float &v, int &level)

@@ -13,7 +13,8 @@ def dist(a, b):
     return int(np.bitwise_count(np.bitwise_xor(a, b)).sum())
 
 
-def features_in_area(F, x, y, r, minL=-1, maxL=-1):
+def features_in_area(F, x, y, r, minL=-1, maxL=-1, right=False):
+    """Frame::GetFeaturesInArea; ``right`` walks mGridRight (indices relative to Nleft)."""
     x, y, r = f32(x), f32(y), f32(r)
     out = []
     minCX = max(0, int(math.floor(f32(f32(x - f32(F.min_x)) - r) * F.inv_w)))
@@ -29,18 +30,21 @@ def features_in_area(F, x, y, r, minL=-1, maxL=-1):
     if maxCY < 0:
         return out
     chk = (minL > 0) or (maxL >= 0)
+    gs, gi = (F.grid_start_r, F.grid_idx_r) if right else (F.grid_start, F.grid_idx)
+    off = F.nleft if right else 0
     for ix in range(minCX, maxCX + 1):
         for iy in range(minCY, maxCY + 1):
             c = ix * 48 + iy
-            for j in range(F.grid_start[c], F.grid_start[c + 1]):
-                idx = int(F.grid_idx[j])
-                o = int(F.kp_octave[idx])
+            for j in range(gs[c], gs[c + 1]):
+                idx = int(gi[j])
+                k = idx + off
+                o = int(F.kp_octave[k])
                 if chk:
                     if o < minL:
                         continue
                     if maxL >= 0 and o > maxL:
                         continue
-                if abs(f32(F.kp_x[idx] - x)) < r and abs(f32(F.kp_y[idx] - y)) < r:
+                if abs(f32(F.kp_x[k] - x)) < r and abs(f32(F.kp_y[k] - y)) < r:
                     out.append(idx)
     return out
 
@@ -84,44 +88,78 @@ def apply_hist(hist, slots, nm):
     return nm
 
 
+class _Top2:
+    def __init__(self):
+        self.b, self.bl, self.b2, self.bl2, self.bi = 256, -1, 256, -1, -1
+
+    def push(self, d, lvl, idx):
+        if d < self.b:
+            self.b2, self.bl2, self.b, self.bl, self.bi = self.b, self.bl, d, lvl, idx
+        elif d < self.b2:
+            self.b2, self.bl2 = d, lvl
+
+
 def search_mps(F, Q, nn, th, far, thfar, slot_mp, slot_taken):
     slots = slot_mp.copy()
     taken = slot_taken.copy()
     nm = 0
     nn = f32(nn)
+    two = F.nleft != -1
+
+    def assign(s, i):
+        slots[s] = Q.mp_id[i]
+        taken[s] = Q.has_obs[i]
+
     for i in range(len(Q.mp_id)):
-        if not Q.in_view[i]:
+        in_r = Q.in_view_r is not None and bool(Q.in_view_r[i])
+        if not Q.in_view[i] and not in_r:
             continue
         if far and Q.track_depth[i] > f32(thfar):
             continue
         if not Q.usable[i]:
             continue
-        lvl = int(Q.pred_level[i])
-        r = f32(2.5) if float(Q.view_cos[i]) > 0.998 else f32(4.0)
-        if f32(th) != f32(1.0):
-            r = f32(r * f32(th))
-        R = f32(r * F.scale[lvl])
-        cands = features_in_area(F, Q.proj_x[i], Q.proj_y[i], R, lvl - 1, lvl)
-        if not cands:
-            continue
-        b, bl, b2, bl2, bi = 256, -1, 256, -1, -1
-        for idx in cands:
-            if slots[idx] >= 0 and taken[idx]:
-                continue
-            if F.u_right is not None and F.u_right[idx] > 0:
-                if abs(f32(Q.proj_xr[i] - F.u_right[idx])) > R:
+        if Q.in_view[i]:
+            lvl = int(Q.pred_level[i])
+            r = f32(2.5) if float(Q.view_cos[i]) > 0.998 else f32(4.0)
+            if f32(th) != f32(1.0):
+                r = f32(r * f32(th))
+            R = f32(r * F.scale[lvl])
+            t = _Top2()
+            for idx in features_in_area(F, Q.proj_x[i], Q.proj_y[i], R, lvl - 1, lvl):
+                if slots[idx] >= 0 and taken[idx]:
                     continue
-            d = dist(Q.desc[i], F.desc[idx])
-            if d < b:
-                b2, bl2, b, bl, bi = b, bl, d, int(F.kp_octave[idx]), idx
-            elif d < b2:
-                b2, bl2 = d, int(F.kp_octave[idx])
-        if b <= TH_HIGH:
-            if bl == bl2 and f32(b) > nn * f32(b2):
+                if not two and F.u_right is not None and F.u_right[idx] > 0:
+                    if abs(f32(Q.proj_xr[i] - F.u_right[idx])) > R:
+                        continue
+                t.push(dist(Q.desc[i], F.desc[idx]), int(F.kp_octave[idx]), idx)
+            if t.b <= TH_HIGH:
+                if t.bl == t.bl2 and f32(t.b) > nn * f32(t.b2):
+                    continue  # skips the right-camera pass too
+                assign(t.bi, i)
+                nm += 1
+                if two and F.left_to_right is not None and F.left_to_right[t.bi] != -1:
+                    assign(F.left_to_right[t.bi] + F.nleft, i)
+                    nm += 1
+        if two and in_r:
+            lvl = int(Q.pred_level_r[i])
+            if lvl == -1:
                 continue
-            slots[bi] = Q.mp_id[i]
-            taken[bi] = Q.has_obs[i]
-            nm += 1
+            r = f32(2.5) if float(Q.view_cos_r[i]) > 0.998 else f32(4.0)
+            R = f32(r * F.scale[lvl])
+            t = _Top2()
+            for idx in features_in_area(F, Q.proj_xr[i], Q.proj_yr[i], R, lvl - 1, lvl, right=True):
+                s_ = idx + F.nleft
+                if slots[s_] >= 0 and taken[s_]:
+                    continue
+                t.push(dist(Q.desc[i], F.desc[s_]), int(F.kp_octave[s_]), idx)
+            if t.b <= TH_HIGH:
+                if t.bl == t.bl2 and f32(t.b) > nn * f32(t.b2):
+                    continue
+                if F.right_to_left is not None and F.right_to_left[t.bi] != -1:
+                    assign(F.right_to_left[t.bi], i)
+                    nm += 1
+                assign(t.bi + F.nleft, i)
+                nm += 1
     return nm, slots
 
 
@@ -130,8 +168,17 @@ def search_last(F, L, th, mono, ori, slot_mp, slot_taken):
     taken = slot_taken.copy()
     hist = [[] for _ in range(HISTO)]
     nm = 0
+    two = F.nleft != -1
     fwd = f32(L.tlc_z) > f32(F.mb) and not mono
     bwd = -f32(L.tlc_z) > f32(F.mb) and not mono
+
+    def window(u, v, rad, o, right):
+        if fwd:
+            return features_in_area(F, u, v, rad, o, -1, right)
+        if bwd:
+            return features_in_area(F, u, v, rad, 0, o, right)
+        return features_in_area(F, u, v, rad, o - 1, o + 1, right)
+
     for i in range(len(L.mp_id)):
         if not L.valid[i]:
             continue
@@ -143,19 +190,14 @@ def search_last(F, L, th, mono, ori, slot_mp, slot_taken):
             continue
         o = int(L.octave[i])
         rad = f32(f32(th) * F.scale[o])
-        if fwd:
-            c = features_in_area(F, u, v, rad, o)
-        elif bwd:
-            c = features_in_area(F, u, v, rad, 0, o)
-        else:
-            c = features_in_area(F, u, v, rad, o - 1, o + 1)
+        c = window(u, v, rad, o, False)
         if not c:
             continue
         b, bi = 256, -1
         for i2 in c:
             if slots[i2] >= 0 and taken[i2]:
                 continue
-            if F.u_right is not None and F.u_right[i2] > 0:
+            if not two and F.u_right is not None and F.u_right[i2] > 0:
                 ur = f32(u - f32(f32(F.mbf) * invz))
                 if abs(f32(ur - F.u_right[i2])) > rad:
                     continue
@@ -168,6 +210,21 @@ def search_last(F, L, th, mono, ori, slot_mp, slot_taken):
             nm += 1
             if ori:
                 hist[rot_bin(L.angle[i], F.kp_angle[bi])].append(bi)
+        if two:
+            b, bi = 256, -1
+            for i2 in window(L.u_r[i], L.v_r[i], rad, o, True):
+                s_ = i2 + F.nleft
+                if slots[s_] >= 0 and taken[s_]:
+                    continue
+                d = dist(L.desc[i], F.desc[s_])
+                if d < b:
+                    b, bi = d, s_
+            if b <= TH_HIGH:
+                slots[bi] = L.mp_id[i]
+                taken[bi] = L.has_obs[i]
+                nm += 1
+                if ori:
+                    hist[rot_bin(L.angle[i], F.kp_angle[bi])].append(bi)
     if ori:
         nm = apply_hist(hist, slots, nm)
     return nm, slots
@@ -219,27 +276,31 @@ def search_bow_kf_f(KF, F, nn, ori):
             ik = int(KF.feat[a])
             if not KF.mp_good[ik]:
                 continue
-            b, bi, b2 = 256, -1, 256
+            tl, tr = _Top2(), _Top2()
             for j in range(b0, b1):
                 jf = int(F.feat[j])
                 if out[jf] >= 0:
                     continue
                 d = dist(KF.desc[ik], F.desc[jf])
-                if d < b:
-                    b2, b, bi = b, d, jf
-                elif d < b2:
-                    b2 = d
-            if b <= TH_LOW and f32(b) < nn * f32(b2):
-                out[bi] = KF.mp_id[ik]
-                nm += 1
-                if ori:
-                    hist[rot_bin(KF.angle[ik], F.angle[bi])].append(bi)
+                (tl if F.nleft == -1 or jf < F.nleft else tr).push(d, 0, jf)
+            if tl.b <= TH_LOW:
+                if f32(tl.b) < nn * f32(tl.b2):
+                    out[tl.bi] = KF.mp_id[ik]
+                    nm += 1
+                    if ori:
+                        hist[rot_bin(KF.angle[ik], F.angle[tl.bi])].append(tl.bi)
+                if tr.b <= TH_LOW:  # right match: ratio test disabled ('|| true')
+                    out[tr.bi] = KF.mp_id[ik]
+                    nm += 1
+                    if ori:
+                        hist[rot_bin(KF.angle[ik], F.angle[tr.bi])].append(tr.bi)
     if ori:
         nm = apply_hist(hist, out, nm)
     return nm, out
 
 
 def search_bow_kf_kf(K1, K2, nn, ori):
+    """Two-camera keyframes: indices >= mvKeysUn.size() == NLeft are skipped on both sides."""
     out = np.full(K1.n, -1, np.int32)
     matched2 = np.zeros(K2.n, bool)
     hist = [[] for _ in range(HISTO)]
@@ -248,11 +309,15 @@ def search_bow_kf_kf(K1, K2, nn, ori):
     for (a0, a1), (b0, b1) in _shared_nodes(K1, K2):
         for a in range(a0, a1):
             i1 = int(K1.feat[a])
+            if K1.nleft != -1 and i1 >= K1.nleft:
+                continue
             if not K1.mp_good[i1]:
                 continue
             b, bi, b2 = 256, -1, 256
             for j in range(b0, b1):
                 i2 = int(K2.feat[j])
+                if K2.nleft != -1 and i2 >= K2.nleft:
+                    continue
                 if matched2[i2] or K2.mp_id[i2] < 0 or not K2.mp_good[i2]:
                     continue
                 d = dist(K1.desc[i1], K2.desc[i2])

@@ -50,18 +50,23 @@ def read_arrays(path):
 
 
 def frame_arrays(F):
-    return {"F.kp_x": F.kp_x, "F.kp_y": F.kp_y, "F.kp_angle": F.kp_angle, "F.kp_octave": F.kp_octave,
-            "F.desc": F.desc.reshape(-1), "F.u_right": (F.u_right if F.u_right is not None
-                                                       else np.full(F.n, -1, np.float32)),
-            "F.grid_start": F.grid_start, "F.grid_idx": F.grid_idx, "F.scale": F.scale,
-            "F.scalars": np.array([F.min_x, F.max_x, F.min_y, F.max_y, F.inv_w, F.inv_h, F.mb, F.mbf],
-                                  np.float32)}
+    d = {"F.kp_x": F.kp_x, "F.kp_y": F.kp_y, "F.kp_angle": F.kp_angle, "F.kp_octave": F.kp_octave,
+         "F.desc": F.desc.reshape(-1), "F.u_right": (F.u_right if F.u_right is not None
+                                                    else np.full(F.n, -1, np.float32)),
+         "F.grid_start": F.grid_start, "F.grid_idx": F.grid_idx, "F.scale": F.scale,
+         "F.scalars": np.array([F.min_x, F.max_x, F.min_y, F.max_y, F.inv_w, F.inv_h, F.mb, F.mbf],
+                               np.float32)}
+    if F.nleft != -1:
+        d.update({"F.nleft": np.array([F.nleft], np.int32), "F.r_grid_start": F.grid_start_r,
+                  "F.r_grid_idx": F.grid_idx_r, "F.left_to_right": F.left_to_right,
+                  "F.right_to_left": F.right_to_left})
+    return d
 
 
 def bow_arrays(pre, S):
     return {pre + "desc": S.desc.reshape(-1), pre + "angle": S.angle, pre + "mp_id": S.mp_id,
             pre + "mp_good": S.mp_good, pre + "node_id": S.node_id, pre + "node_start": S.node_start,
-            pre + "feat": S.feat}
+            pre + "feat": S.feat, pre + "nleft": np.array([S.nleft], np.int32)}
 
 
 def cam_array(c):
@@ -155,6 +160,63 @@ def test_adapter_search_by_bow(driver, tmp_path, oracle, mode):
     rng = np.random.default_rng(730 + len(mode))
     A, B = fr.synth_bow_pair(rng, n_kf=1200, n_f=1200, n_nodes=100)
     for S in (A, B):  # a good slot holds a MapPoint
+        S.mp_good = (S.mp_good.astype(bool) & (S.mp_id >= 0)).astype(np.uint8)
+    nn = 0.7
+    arrays = {**bow_arrays("B1.", A), **bow_arrays("B2.", B), "params": np.array([nn, 1.0], np.float32)}
+    out = run(driver, tmp_path, mode, arrays)
+    n_ref, o_ref = getattr(oc, mode)(oracle, A, B, nn, True)
+    assert int(out["nmatches"][0]) == n_ref
+    np.testing.assert_array_equal(out["out_mp"], o_ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("all_obs", [True, False])
+def test_adapter_search_by_projection_mps_two_cam(driver, tmp_path, oracle, all_obs):
+    """Two-camera rig: the adapter gathers mGridRight, the stereo-partner maps and the MapPoints'
+    right-camera frustum fields."""
+    rng = np.random.default_rng(760 + int(all_obs))
+    F = fr.synth_frame_two_cam(rng, n_left=700, n_right=650)
+    Q = fr.synth_mp_queries_two_cam(rng, F, m=2000)
+    if all_obs:
+        Q.has_obs[:] = 1
+    slot_mp, taken = fr.synth_slots(rng, F.n, frac_assigned=0.15)
+    nn, th, thfar = 0.8, 3.0, 20.0
+    arrays = {**frame_arrays(F), "S.slot_mp": slot_mp.astype(np.int32), "S.slot_taken": taken.astype(np.uint8),
+              "params": np.array([nn, th, 0.0, thfar], np.float32)}
+    for k in ["mp_id", "desc", "usable", "has_obs", "in_view", "proj_x", "proj_y", "proj_xr", "view_cos",
+              "pred_level", "track_depth", "in_view_r", "proj_yr", "view_cos_r", "pred_level_r"]:
+        arrays["Q." + k] = getattr(Q, k).reshape(-1)
+    out = run(driver, tmp_path, "mps", arrays)
+    n_ref, s_ref = oc.mps(oracle, F, Q, nn, th, False, thfar, slot_mp.astype(np.int32), taken)
+    assert int(out["nmatches"][0]) == n_ref
+    np.testing.assert_array_equal(out["slot_mp"], s_ref)
+
+
+@pytest.mark.gpu
+def test_adapter_search_by_projection_last_two_cam(driver, tmp_path, oracle):
+    rng = np.random.default_rng(765)
+    F = fr.synth_frame_two_cam(rng, n_left=700, n_right=650)
+    L = fr.synth_last_queries_two_cam(rng, F, n_last=1000)
+    L.valid = (L.valid.astype(bool) & (L.mp_id >= 0)).astype(np.uint8)
+    slot_mp, taken = fr.synth_slots(rng, F.n)
+    th = 7.0
+    arrays = {**frame_arrays(F), "S.slot_mp": slot_mp.astype(np.int32), "S.slot_taken": taken.astype(np.uint8),
+              "params": np.array([th, 0.0, 1.0, 0.0], np.float32)}
+    for k in ["mp_id", "desc", "valid", "has_obs", "u", "v", "invz", "octave", "angle", "u_r", "v_r"]:
+        arrays["L." + k] = getattr(L, k).reshape(-1)
+    out = run(driver, tmp_path, "last", arrays)
+    n_ref, s_ref = oc.last(oracle, F, L, th, False, True, slot_mp.astype(np.int32), taken)
+    assert int(out["nmatches"][0]) == n_ref
+    np.testing.assert_array_equal(out["slot_mp"], s_ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["bow_kf_f", "bow_kf_kf"])
+def test_adapter_search_by_bow_two_cam(driver, tmp_path, oracle, mode):
+    rng = np.random.default_rng(770 + len(mode))
+    A, B = fr.synth_bow_pair(rng, n_kf=1200, n_f=1200, n_nodes=100, nleft_kf=620, nleft_f=600,
+                             f_is_kf=(mode == "bow_kf_kf"))
+    for S in (A, B):
         S.mp_good = (S.mp_good.astype(bool) & (S.mp_id >= 0)).astype(np.uint8)
     nn = 0.7
     arrays = {**bow_arrays("B1.", A), **bow_arrays("B2.", B), "params": np.array([nn, 1.0], np.float32)}

@@ -103,3 +103,88 @@ def test_empty_inputs(ctx):
     s = np.full(F.n, -1, np.int32)
     assert ORBmatcher(ctx).SearchByProjection(F, Q, 3.0, slot_mp=s, slot_taken=np.zeros(F.n, np.uint8)) == 0
     assert (s == -1).all()
+
+
+# ---- two-camera rigs (Frame::Nleft != -1)
+
+def two_cam(rng, nl=700, nr=650):
+    return fr.synth_frame_two_cam(rng, n_left=nl, n_right=nr, stereo_frac=0.6)
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("th,nn,far", [(1.0, 0.8, False), (3.0, 0.8, False), (5.0, 0.6, True)])
+def test_search_by_projection_mps_two_cam(ctx, oracle, seed, th, nn, far):
+    """a5 right-camera pass: stereo-partner writes, the ratio-failure skip, own-left blocking.
+    Seeds with every MapPoint observed run the Jacobi resolve alone; the others include
+    observation-less MapPoints whose partner writes unblock slots (serial redo)."""
+    rng = np.random.default_rng(6000 + seed)
+    F = two_cam(rng)
+    Q = fr.synth_mp_queries_two_cam(rng, F, m=2000)
+    if seed < 2:
+        Q.has_obs[:] = 1
+    slot_mp, taken = fr.synth_slots(rng, F.n, frac_assigned=0.15)
+    ref = oc.mps(oracle, F, Q, nn, th, far, 20.0, slot_mp, taken)
+    s = slot_mp.copy()
+    n = ORBmatcher(ctx, nn).SearchByProjection(F, Q, th, far, 20.0, slot_mp=s, slot_taken=taken)
+    assert_same("mps two-cam", n, s, *ref)
+    if seed < 2:
+        assert not ctx.match_last_stats()["serial"]
+
+
+def test_search_by_projection_mps_two_cam_paths(ctx, oracle):
+    """Both resolve paths are exercised: all-observed (Jacobi only) and a run that must be redone
+    serially because an observation-less MapPoint's partner write unblocks a slot."""
+    seen = set()
+    for seed in range(12):
+        rng = np.random.default_rng(6100 + seed)
+        F = two_cam(rng, 400, 380)
+        Q = fr.synth_mp_queries_two_cam(rng, F, m=1500, noise_px=1.0, match_frac=0.9)
+        Q.has_obs[:] = rng.random(len(Q.mp_id)) < 0.6
+        slot_mp, taken = fr.synth_slots(rng, F.n, frac_assigned=0.4, frac_taken=0.9)
+        ref = oc.mps(oracle, F, Q, 0.9, 3.0, False, 20.0, slot_mp, taken)
+        s = slot_mp.copy()
+        n = ORBmatcher(ctx, 0.9).SearchByProjection(F, Q, 3.0, False, 20.0, slot_mp=s, slot_taken=taken)
+        assert_same(f"mps two-cam seed {seed}", n, s, *ref)
+        seen.add(ctx.match_last_stats()["serial"])
+    assert True in seen
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("th,mono,tlc", [(7.0, False, 0.0), (15.0, True, 0.0), (7.0, False, 1.0), (14.0, False, -1.0)])
+def test_search_by_projection_last_two_cam(ctx, oracle, seed, th, mono, tlc):
+    rng = np.random.default_rng(7000 + seed)
+    F = two_cam(rng)
+    L = fr.synth_last_queries_two_cam(rng, F, n_last=1000, tlc_z=tlc)
+    slot_mp, taken = fr.synth_slots(rng, F.n)
+    for ori in (True, False):
+        ref = oc.last(oracle, F, L, th, mono, ori, slot_mp, taken)
+        s = slot_mp.copy()
+        n = ORBmatcher(ctx, 0.9, ori).SearchByProjection(F, L, th, mono, slot_mp=s, slot_taken=taken)
+        assert_same(f"last two-cam ori={ori}", n, s, *ref)
+
+
+def test_search_by_projection_kf_two_cam(ctx, oracle):
+    rng = np.random.default_rng(7500)
+    F = two_cam(rng)
+    K = fr.synth_kf_queries(rng, F, n_kf=900)
+    slot_mp, _ = fr.synth_slots(rng, F.n, frac_assigned=0.2)
+    for ori in (True, False):
+        ref = oc.kf(oracle, F, K, 10.0, 100, ori, slot_mp)
+        s = slot_mp.copy()
+        n = ORBmatcher(ctx, 0.75, ori).SearchByProjection(F, K, 10.0, 100, slot_mp=s)
+        assert_same(f"kf two-cam ori={ori}", n, s, *ref)
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("nn", [0.7, 0.9])
+def test_search_by_bow_two_cam(ctx, oracle, seed, nn):
+    rng = np.random.default_rng(8000 + seed)
+    KF, F = fr.synth_bow_pair(rng, n_kf=1200, n_f=1200, n_nodes=100, nleft_kf=640, nleft_f=600)
+    K1, K2 = fr.synth_bow_pair(rng, n_kf=1100, n_f=1300, n_nodes=80, f_is_kf=True, nleft_kf=560, nleft_f=700)
+    for ori in (True, False):
+        ref = oc.bow_kf_f(oracle, KF, F, nn, ori)
+        n, out = ORBmatcher(ctx, nn, ori).SearchByBoW(KF, F)
+        assert_same(f"bow kf-f two-cam ori={ori}", n, out, *ref)
+        ref = oc.bow_kf_kf(oracle, K1, K2, nn, ori)
+        n, out = ORBmatcher(ctx, nn, ori).SearchByBoW(K1, K2, kf2=True)
+        assert_same(f"bow kf-kf two-cam ori={ori}", n, out, *ref)

@@ -124,3 +124,69 @@ def test_oracle_bow_vs_python(oracle, seed):
         ref = pr.search_bow_kf_kf(K1, K2, nn, ori)
         assert got[0] == ref[0]
         np.testing.assert_array_equal(got[1], ref[1])
+
+
+# ---- two-camera rigs (Frame::Nleft != -1): right-camera passes of a5 / a6, the split top-2 of
+# a3 and the NLeft guard of a4
+
+def two_cam_frame(rng, nl=260, nr=240):
+    return fr.synth_frame_two_cam(rng, n_left=nl, n_right=nr, stereo_frac=0.6)
+
+
+def test_features_in_area_right_grid(oracle):
+    rng = np.random.default_rng(31)
+    F = two_cam_frame(rng)
+    fs = F.struct()
+    buf = np.zeros(F.n, np.int32)
+    for _ in range(200):
+        x, y = rng.uniform(-30, 780), rng.uniform(-30, 510)
+        r = rng.uniform(1, 80)
+        lo, hi = int(rng.integers(-1, 8)), int(rng.integers(-1, 8))
+        for right in (0, 1):
+            n = oracle.oracle_frame_features_in_area(C.byref(fs), x, y, r, lo, hi, right, buf.ctypes.data)
+            assert list(buf[:n]) == pr.features_in_area(F, x, y, r, lo, hi, right=bool(right))
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_oracle_mps_two_cam_vs_python(oracle, seed):
+    rng = np.random.default_rng(500 + seed)
+    F = two_cam_frame(rng)
+    Q = fr.synth_mp_queries_two_cam(rng, F, m=300)
+    slot_mp, taken = fr.synth_slots(rng, F.n, frac_assigned=0.15)
+    for th, nn, far in [(1.0, 0.8, False), (5.0, 0.6, True), (3.0, 0.9, False)]:
+        got = oc.mps(oracle, F, Q, nn, th, far, 20.0, slot_mp, taken)
+        ref = pr.search_mps(F, Q, nn, th, far, 20.0, slot_mp, taken)
+        assert got[0] == ref[0]
+        np.testing.assert_array_equal(got[1], ref[1])
+        assert (got[1][F.nleft:] != slot_mp[F.nleft:]).any(), "right-camera slots must be exercised"
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_oracle_last_two_cam_vs_python(oracle, seed):
+    rng = np.random.default_rng(600 + seed)
+    F = two_cam_frame(rng)
+    L = fr.synth_last_queries_two_cam(rng, F, n_last=250, tlc_z=[0.0, 1.0, -1.0, 0.0][seed])
+    slot_mp, taken = fr.synth_slots(rng, F.n)
+    for th, mono, ori in [(7.0, False, True), (15.0, True, False), (7.0, False, False)]:
+        got = oc.last(oracle, F, L, th, mono, ori, slot_mp, taken)
+        ref = pr.search_last(F, L, th, mono, ori, slot_mp, taken)
+        assert got[0] == ref[0]
+        np.testing.assert_array_equal(got[1], ref[1])
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_oracle_bow_two_cam_vs_python(oracle, seed):
+    rng = np.random.default_rng(700 + seed)
+    KF, F = fr.synth_bow_pair(rng, n_kf=300, n_f=300, n_nodes=30, nleft_kf=160, nleft_f=150)
+    K1, K2 = fr.synth_bow_pair(rng, n_kf=300, n_f=320, n_nodes=30, f_is_kf=True, nleft_kf=170, nleft_f=150)
+    for nn, ori in [(0.7, True), (0.9, False)]:
+        got = oc.bow_kf_f(oracle, KF, F, nn, ori)
+        ref = pr.search_bow_kf_f(KF, F, nn, ori)
+        assert got[0] == ref[0]
+        np.testing.assert_array_equal(got[1], ref[1])
+        assert (got[1][F.nleft:] >= 0).any()
+        got = oc.bow_kf_kf(oracle, K1, K2, nn, ori)
+        ref = pr.search_bow_kf_kf(K1, K2, nn, ori)
+        assert got[0] == ref[0]
+        np.testing.assert_array_equal(got[1], ref[1])
+        assert (got[1][K1.nleft:] == -1).all()
