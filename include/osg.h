@@ -224,11 +224,33 @@ int osg_search_by_bow_kf_f(osg_ctx *ctx, const osg_bow_side *kf, const osg_bow_s
 int osg_search_by_bow_kf_kf(osg_ctx *ctx, const osg_bow_side *kf1, const osg_bow_side *kf2,
                             float nnratio, int check_orientation, int32_t *out_mp12);
 
-/* Diagnostics of the last search call on this context: out[0] candidates enumerated, out[1]
- * Jacobi rounds, out[2] 1 if the greedy was redone serially (a5 on a two-camera rig when a
+/* ---- batched forms ----------------------------------------------------------------------------
+ * B independent problems (frames / keyframe pairs) in one launch, one workgroup each; the
+ * throughput path for frame batches.  F / queries / sides are arrays of B
+ * structs.  The per-problem slot / output arrays are concatenated in problem order: problem b's
+ * starts at the sum of the sizes (frame n / kf1 n) of problems 0..b-1.  nmatches[b] receives what
+ * the single form returns for problem b.  Returns OSG_OK or an error naming the problem. */
+int osg_search_by_projection_mps_batch(osg_ctx *ctx, const osg_frame *F, const osg_mp_queries *mps, int32_t B,
+                                       float nnratio, float th, int far_points, float th_far_points,
+                                       int32_t *slot_mp, const uint8_t *slot_taken, int32_t *nmatches);
+int osg_search_by_projection_last_batch(osg_ctx *ctx, const osg_frame *CF, const osg_last_queries *last, int32_t B,
+                                        float th, int mono, int check_orientation, int32_t *slot_mp,
+                                        const uint8_t *slot_taken, int32_t *nmatches);
+int osg_search_by_projection_kf_batch(osg_ctx *ctx, const osg_frame *CF, const osg_kf_queries *kfq, int32_t B,
+                                      float th, int orb_dist, int check_orientation, int32_t *slot_mp,
+                                      int32_t *nmatches);
+int osg_search_by_bow_kf_f_batch(osg_ctx *ctx, const osg_bow_side *kf, const osg_bow_side *f, int32_t B,
+                                 float nnratio, int check_orientation, int32_t *out_mp, int32_t *nmatches);
+int osg_search_by_bow_kf_kf_batch(osg_ctx *ctx, const osg_bow_side *kf1, const osg_bow_side *kf2, int32_t B,
+                                  float nnratio, int check_orientation, int32_t *out_mp12, int32_t *nmatches);
+
+/* Diagnostics of the last search call on this context (summed / maxed over a batch): out[0]
+ * candidates enumerated, out[1] Jacobi rounds, out[2] problems whose greedy was redone serially (a5 on a two-camera rig when a
  * stereo-partner write by a MapPoint without observations unblocked a slot), out[3] nmatches.
  * No reference counterpart. */
 int osg_match_last_stats(osg_ctx *ctx, int32_t *out4);
+/* Device time of the last search call's matching kernel (HIP events around the launch), ms. */
+int osg_match_last_kernel_ms(osg_ctx *ctx, double *ms);
 
 #ifdef __cplusplus
 }

@@ -128,7 +128,9 @@ EXPORTS = [
     "osg_descriptor_distance", "osg_descriptor_distance_pairs", "osg_hamming_top2",
     "osg_hamming_top2_dev", "osg_hamming_top2_plan", "osg_search_by_projection_mps", "osg_search_by_projection_last",
     "osg_search_by_projection_kf", "osg_search_by_bow_kf_f", "osg_search_by_bow_kf_kf",
-    "osg_match_last_stats", "osg_pose_optimization", "osg_pose_optimization_batch",
+    "osg_search_by_projection_mps_batch", "osg_search_by_projection_last_batch",
+    "osg_search_by_projection_kf_batch", "osg_search_by_bow_kf_f_batch", "osg_search_by_bow_kf_kf_batch",
+    "osg_match_last_stats", "osg_match_last_kernel_ms", "osg_pose_optimization", "osg_pose_optimization_batch",
     "osg_local_bundle_adjustment",
 ]
 
@@ -163,7 +165,13 @@ def declare(lib: C.CDLL) -> C.CDLL:
                                            C.c_int, vp]
     lib.osg_search_by_bow_kf_kf.argtypes = [vp, C.POINTER(OsgBowSide), C.POINTER(OsgBowSide), f32,
                                             C.c_int, vp]
+    lib.osg_search_by_projection_mps_batch.argtypes = [vp, vp, vp, i32, f32, f32, C.c_int, f32, vp, vp, vp]
+    lib.osg_search_by_projection_last_batch.argtypes = [vp, vp, vp, i32, f32, C.c_int, C.c_int, vp, vp, vp]
+    lib.osg_search_by_projection_kf_batch.argtypes = [vp, vp, vp, i32, f32, C.c_int, C.c_int, vp, vp]
+    lib.osg_search_by_bow_kf_f_batch.argtypes = [vp, vp, vp, i32, f32, C.c_int, vp, vp]
+    lib.osg_search_by_bow_kf_kf_batch.argtypes = [vp, vp, vp, i32, f32, C.c_int, vp, vp]
     lib.osg_match_last_stats.argtypes = [vp, vp]
+    lib.osg_match_last_kernel_ms.argtypes = [vp, vp]
     lib.osg_pose_optimization.argtypes = [vp, C.POINTER(OsgPoseProblem), C.POINTER(OsgPoseResult)]
     lib.osg_pose_optimization_batch.argtypes = [vp, C.POINTER(OsgPoseProblem), i32,
                                                 C.POINTER(OsgPoseResult)]

@@ -27,8 +27,19 @@
 //   5. finish  — last assignment per slot, rotation histogram with the reference's 1/30 factor,
 //                ComputeThreeMaxima, removal, nmatches.
 #include <algorithm>
+#include <deque>
+#include <type_traits>
+#include <string>
 
 #include "match_common.h"
+
+// Every MatchArgs array lives in global memory; typing the pointers so (address space 1) makes the
+// compiler emit global_load / global_store instead of flat accesses for pointers read from the
+// per-problem argument array.
+#define GLOBAL __attribute__((address_space(1)))
+// native vector types (the HIP vector classes cannot be copied through such pointers on the host pass)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
@@ -42,45 +53,47 @@ struct MatchArgs {
     int nq, n_slots;
     int nleft;                // slot side: Frame::Nleft (-1: one camera / rectified stereo)
     // slot side (Frame F / KeyFrame 2)
-    const uint32_t *fdesc;
-    const float *kp_x, *kp_y, *slot_angle;
-    const int32_t *kp_octave;
-    const float *u_right;     // NULL for a two-camera rig (the u_R check needs Nleft == -1)
-    const int32_t *grid_start, *grid_idx;
-    const int32_t *grid_start_r, *grid_idx_r;   // mGridRight, indices relative to nleft
-    const int32_t *l2r, *r2l;                    // mvLeftToRightMatch / mvRightToLeftMatch
+    GLOBAL const uint32_t *fdesc;
+    GLOBAL const float *kp_x, *kp_y, *slot_angle;
+    GLOBAL const int32_t *kp_octave;
+    GLOBAL const float *u_right;     // NULL for a two-camera rig (the u_R check needs Nleft == -1)
+    GLOBAL const int32_t *grid_start, *grid_idx;
+    GLOBAL const int32_t *grid_start_r, *grid_idx_r;   // mGridRight, indices relative to nleft
+    GLOBAL const int32_t *l2r, *r2l;                    // mvLeftToRightMatch / mvRightToLeftMatch
     float min_x, max_x, min_y, max_y, inv_w, inv_h;
-    const float *scale;
+    GLOBAL const float *scale;
+    int n_levels;
     float mb, mbf;
     // queries
-    const uint32_t *qdesc;
-    const int32_t *q_mp;
-    const uint8_t *q_has_obs;
-    const float *q_angle;
-    const float *q_x, *q_y, *q_f0, *q_f1, *q_f2;
-    const int32_t *q_lvl;
-    const uint8_t *q_m0, *q_m1;
+    GLOBAL const uint32_t *qdesc;
+    GLOBAL const int32_t *q_mp;
+    GLOBAL const uint8_t *q_has_obs;
+    GLOBAL const float *q_angle;
+    GLOBAL const float *q_x, *q_y, *q_f0, *q_f1, *q_f2;
+    GLOBAL const int32_t *q_lvl;
+    GLOBAL const uint8_t *q_m0, *q_m1;
     // right-camera query fields (two-camera rig)
-    const float *q_xr, *q_yr, *q_f0r;
-    const int32_t *q_lvl_r;
-    const uint8_t *q_m0r;
-    const int32_t *q_cb, *q_ce, *cand_list;
-    const uint8_t *slot_ok;
-    const int32_t *slot_mp2;  // KF-KF: KF2 MapPoint ids
+    GLOBAL const float *q_xr, *q_yr, *q_f0r;
+    GLOBAL const int32_t *q_lvl_r;
+    GLOBAL const uint8_t *q_m0r;
+    GLOBAL const int32_t *q_cb, *q_ce, *cand_list;
+    GLOBAL const uint8_t *slot_ok;
+    GLOBAL const int32_t *slot_mp2;  // KF-KF: KF2 MapPoint ids
     // parameters
     float nnratio, th, th_far, tlc_z;
     int far_points, orb_dist, check_ori, mono;
     // state / outputs
-    int32_t *slot_mp;         // in/out (out_mp for KF-F)
-    const uint8_t *slot_taken;
-    int32_t *out_q;           // KF-KF: per query result
+    GLOBAL int32_t *slot_mp;         // in/out (out_mp for KF-F)
+    GLOBAL const uint8_t *slot_taken;
+    GLOBAL int32_t *out_q;           // KF-KF: per query result
     // scratch
-    int32_t *q_off;           // nq + 1: candidate CSR
-    int32_t *q_mid;           // nq: first right-camera candidate of each query
-    uint32_t *cands;
-    int32_t *q_res;           // 2 nq: {left slot, right slot}, -1 = no match
-    uint8_t *q_bin;           // 2 nq
-    int32_t *status;          // [0] candidates, [1] nmatches, [2] rounds, [3] overflow, [4] serial
+    GLOBAL int32_t *q_off;           // nq + 1: candidate CSR
+    GLOBAL int32_t *q_mid;           // nq: first right-camera candidate of each query
+    GLOBAL f32x4 *q_win;            // 4 nq: left / right search windows (grid modes)
+    GLOBAL uint32_t *cands;
+    GLOBAL int32_t *q_res;           // 2 nq: {left slot, right slot}, -1 = no match
+    GLOBAL uint8_t *q_bin;           // 2 nq
+    GLOBAL int32_t *status;          // [0] candidates, [1] nmatches, [2] rounds, [3] overflow, [4] serial
     int cap;
 };
 
@@ -103,9 +116,17 @@ __device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc)
     return r;
 }
 
-__device__ __forceinline__ uint32_t dist256(const uint32_t (&a)[8], const uint32_t *__restrict__ b)
+__device__ __forceinline__ uint4 ld4(GLOBAL const uint32_t *p)
 {
-    const uint4 b0 = *(const uint4 *)b, b1 = *(const uint4 *)(b + 4);
+    const u32x4 v = *(GLOBAL const u32x4 *)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint4 ld4(const uint32_t *p) { return *(const uint4 *)p; }
+
+template <typename P>
+__device__ __forceinline__ uint32_t dist256(const uint32_t (&a)[8], P b)
+{
+    const uint4 b0 = ld4(b), b1 = ld4(b + 4);
     uint32_t d = __popc(a[0] ^ b0.x);
     d = bcnt_acc(a[1] ^ b0.y, d);
     d = bcnt_acc(a[2] ^ b0.z, d);
@@ -123,54 +144,47 @@ __device__ __forceinline__ float radius_by_viewing_cos(float viewCos)
     return ((double)viewCos > 0.998) ? 2.5f : 4.0f;
 }
 
-// Search window of the left (or only) camera pass.
+// Search window of the left (or only) camera pass.  Every query field is loaded before any test
+// (selects, no branches), so a query costs one round of memory latency, not one per field.
 template <int MODE>
-__device__ Win query_window(const MatchArgs &A, int q)
+__device__ __forceinline__ Win query_window(const MatchArgs &A, int q)
 {
     Win w;
-    w.valid = false;
     w.stereo = false;
     w.sx = 0.f;
     w.sr = 0.f;
+    const int nl1 = A.n_levels - 1;
     if (MODE == MODE_MPS) {
         // ref:src/ORBmatcher.cc:55-80
-        if (!A.q_m0[q]) return w;                                     // mbTrackInView
-        if (A.far_points && A.q_f2[q] > A.th_far) return w;          // mTrackDepth > thFarPoints
-        if (!A.q_m1[q]) return w;                                     // isBad()
+        const bool in_view = A.q_m0[q] != 0, usable = A.q_m1[q] != 0;   // mbTrackInView, !isBad()
+        const float depth = A.q_f2[q], vcos = A.q_f0[q];
+        const float x = A.q_x[q], y = A.q_y[q], xr = A.q_f1[q];
         const int lvl = A.q_lvl[q];
-        float r = radius_by_viewing_cos(A.q_f0[q]);
+        const float sc = A.scale[min(max(lvl, 0), nl1)];
+        w.valid = in_view && !(A.far_points && depth > A.th_far) && usable;
+        float r = radius_by_viewing_cos(vcos);
         if (A.th != 1.0f) r *= A.th;
-        w.r = r * A.scale[lvl];
-        w.x = A.q_x[q];
-        w.y = A.q_y[q];
+        w.r = r * sc;
+        w.x = x;
+        w.y = y;
         w.minL = lvl - 1;
         w.maxL = lvl;
         w.stereo = true;
-        w.sx = A.q_f1[q];   // mTrackProjXR
+        w.sx = xr;          // mTrackProjXR
         w.sr = w.r;         // r * mvScaleFactors[nPredictedLevel]
-        w.valid = true;
     } else if (MODE == MODE_LAST) {
         // ref:src/ORBmatcher.cc:1984-2030
-        if (!A.q_m0[q]) return w;
+        const bool valid = A.q_m0[q] != 0;
         const float invzc = A.q_f0[q];
-        if (invzc < 0) return w;
         const float u = A.q_x[q], v = A.q_y[q];
-        if (u < A.min_x || u > A.max_x) return w;
-        if (v < A.min_y || v > A.max_y) return w;
         const int oct = A.q_lvl[q];
-        const float radius = A.th * A.scale[oct];
+        const float sc = A.scale[min(max(oct, 0), nl1)];
+        w.valid = valid && !(invzc < 0) && !(u < A.min_x || u > A.max_x) && !(v < A.min_y || v > A.max_y);
+        const float radius = A.th * sc;
         const bool bForward = A.tlc_z > A.mb && !A.mono;
         const bool bBackward = -A.tlc_z > A.mb && !A.mono;
-        if (bForward) {
-            w.minL = oct;
-            w.maxL = -1;
-        } else if (bBackward) {
-            w.minL = 0;
-            w.maxL = oct;
-        } else {
-            w.minL = oct - 1;
-            w.maxL = oct + 1;
-        }
+        w.minL = bForward ? oct : bBackward ? 0 : oct - 1;
+        w.maxL = bForward ? -1 : bBackward ? oct : oct + 1;
         w.x = u;
         w.y = v;
         w.r = radius;
@@ -178,63 +192,107 @@ __device__ Win query_window(const MatchArgs &A, int q)
         const float prod = A.mbf * invzc;
         w.sx = u - prod;   // ur = uv(0) - mbf * invzc
         w.sr = radius;
-        w.valid = true;
-    } else if (MODE == MODE_KF) {
-        // ref:src/ORBmatcher.cc:2262-2265
-        if (!A.q_m0[q]) return w;
+    } else {
+        // MODE_KF, ref:src/ORBmatcher.cc:2262-2265
+        const bool valid = A.q_m0[q] != 0;
         const int lvl = A.q_lvl[q];
-        w.r = A.th * A.scale[lvl];
-        w.x = A.q_x[q];
-        w.y = A.q_y[q];
+        const float x = A.q_x[q], y = A.q_y[q];
+        const float sc = A.scale[min(max(lvl, 0), nl1)];
+        w.valid = valid;
+        w.r = A.th * sc;
+        w.x = x;
+        w.y = y;
         w.minL = lvl - 1;
         w.maxL = lvl + 1;
-        w.valid = true;
     }
     return w;
 }
 
-// Search window of the right-camera pass of a two-camera rig.  wl / cl: the left window and its
-// candidate count (GetFeaturesInArea size).
+// Search window of the right-camera pass of a two-camera rig.  For a6 the pass is also skipped when
+// the left window was empty (:2040-2041 'continue'); enumeration applies that rule.
 template <int MODE>
-__device__ Win query_window_r(const MatchArgs &A, int q, const Win &wl, int cl)
+__device__ __forceinline__ Win query_window_r(const MatchArgs &A, int q, const Win &wl)
 {
     Win w;
     w.valid = false;
     w.stereo = false;
     w.sx = 0.f;
     w.sr = 0.f;
+    w.x = w.y = w.r = 0.f;
+    w.minL = w.maxL = 0;
     if (A.nleft < 0) return w;
     if (MODE == MODE_MPS) {
         // ref:src/ORBmatcher.cc:185-196: mbTrackInViewR, mnTrackScaleLevelR != -1, radius from
         // mTrackViewCosR (no th factor), levels (lvl-1, lvl), right grid at mTrackProjXR/YR
-        if (!A.q_m0r[q]) return w;
-        if (A.far_points && A.q_f2[q] > A.th_far) return w;
-        if (!A.q_m1[q]) return w;
+        const bool in_view_r = A.q_m0r[q] != 0, usable = A.q_m1[q] != 0;
+        const float depth = A.q_f2[q], vcos = A.q_f0r[q];
+        const float x = A.q_xr[q], y = A.q_yr[q];
         const int lvl = A.q_lvl_r[q];
-        if (lvl == -1) return w;
-        w.r = radius_by_viewing_cos(A.q_f0r[q]) * A.scale[lvl];
-        w.x = A.q_xr[q];
-        w.y = A.q_yr[q];
+        const float sc = A.scale[min(max(lvl, 0), A.n_levels - 1)];
+        w.valid = in_view_r && !(A.far_points && depth > A.th_far) && usable && lvl != -1;
+        w.r = radius_by_viewing_cos(vcos) * sc;
+        w.x = x;
+        w.y = y;
         w.minL = lvl - 1;
         w.maxL = lvl;
-        w.valid = true;
     } else if (MODE == MODE_LAST) {
-        // ref:src/ORBmatcher.cc:2096-2110: same radius and levels at the right-camera projection;
-        // an empty left window has already 'continue'd (:2040-2041)
-        if (!wl.valid || cl == 0) return w;
+        // ref:src/ORBmatcher.cc:2096-2110: same radius and levels at the right-camera projection
+        const float x = A.q_xr[q], y = A.q_yr[q];
         w = wl;
-        w.x = A.q_xr[q];
-        w.y = A.q_yr[q];
+        w.x = x;
+        w.y = y;
         w.stereo = false;
     }
     return w;
 }
 
-// Frame::GetFeaturesInArea (ref:src/Frame.cc:868-962) + the caller's static per-candidate skips.
-// RIGHT walks mGridRight; candidates are written as slot indices (right keypoints at nleft + i).
-template <bool FILL, bool RIGHT>
-__device__ int enum_grid(const MatchArgs &A, const Win &w, const uint32_t (&qd)[8], uint32_t *out)
+// Windows are computed once per query (phase 0) and kept as two float4 each.
+__device__ __forceinline__ void store_win(GLOBAL f32x4 *dst, const Win &w)
 {
+    dst[0] = f32x4{w.x, w.y, w.r, w.sx};
+    dst[1] = f32x4{w.sr, __int_as_float(w.minL), __int_as_float(w.maxL),
+                   __int_as_float((w.valid ? 1 : 0) | (w.stereo ? 2 : 0))};
+}
+__device__ __forceinline__ Win load_win(GLOBAL const f32x4 *src)
+{
+    const f32x4 a = src[0], b = src[1];
+    Win w;
+    w.x = a.x;
+    w.y = a.y;
+    w.r = a.z;
+    w.sx = a.w;
+    w.sr = b.x;
+    w.minL = __float_as_int(b.y);
+    w.maxL = __float_as_int(b.z);
+    const int f = __float_as_int(b.w);
+    w.valid = (f & 1) != 0;
+    w.stereo = (f & 2) != 0;
+    return w;
+}
+
+// Where a grid walk reads the frame.  STAGE 0: the frame's own arrays in global memory; STAGE 1:
+// per-entry records in grid order staged in LDS; STAGE 2: also the descriptors in LDS.
+template <int STAGE>
+struct GridView {
+    using GsPtr = std::conditional_t<(STAGE >= 1), const int32_t *, GLOBAL const int32_t *>;
+    using FdPtr = std::conditional_t<(STAGE >= 2), const uint32_t *, GLOBAL const uint32_t *>;
+    GsPtr gs;                   // cell offsets, OSG_GRID_CELLS + 1
+    GLOBAL const int32_t *gi;   // STAGE 0: keypoint index relative to the camera
+    int off;                    // STAGE 0: slot offset (nleft for the right grid)
+    const float *rx, *ry, *ru;  // STAGE >= 1: x, y, u_R (or -1) of each grid entry
+    const int32_t *rk;          // STAGE >= 1: slot << 8 | octave of each grid entry
+    FdPtr fd;                   // descriptors by slot
+};
+
+// Frame::GetFeaturesInArea (ref:src/Frame.cc:868-962) + the caller's static per-candidate skips.
+// The cells (ix, minCY..maxCY) of one column are consecutive in the CSR (cell = ix*48 + iy), so
+// each column is ONE contiguous run in the reference's iy-then-insertion order.  Candidates are
+// written as slot indices (right keypoints at nleft + i).
+template <bool FILL, int STAGE, bool RIGHT>
+__device__ __forceinline__ int enum_grid(const MatchArgs &A, const GridView<STAGE> &G, const Win &w,
+                                         const uint32_t (&qd)[8], GLOBAL uint32_t *out)
+{
+    constexpr bool STAGED = STAGE >= 1;
     const float factorX = w.r, factorY = w.r;
     int minCX = (int)floorf((w.x - A.min_x - factorX) * A.inv_w);
     if (minCX < 0) minCX = 0;
@@ -249,77 +307,93 @@ __device__ int enum_grid(const MatchArgs &A, const Win &w, const uint32_t (&qd)[
     if (maxCY > OSG_GRID_ROWS - 1) maxCY = OSG_GRID_ROWS - 1;
     if (maxCY < 0) return 0;
     const bool bCheckLevels = (w.minL > 0) || (w.maxL >= 0);  // ref:src/Frame.cc:919 quirk
-    const int32_t *gs = RIGHT ? A.grid_start_r : A.grid_start;
-    const int32_t *gi = RIGHT ? A.grid_idx_r : A.grid_idx;
-    const int off = RIGHT ? A.nleft : 0;
+    const bool stereo = !RIGHT && w.stereo && A.u_right;      // u_R check (one-camera frames only)
     int cnt = 0;
     for (int ix = minCX; ix <= maxCX; ix++) {
-        for (int iy = minCY; iy <= maxCY; iy++) {
-            const int cell = ix * OSG_GRID_ROWS + iy;
-            const int j1 = gs[cell + 1];
-            for (int j = gs[cell]; j < j1; j++) {
-                const int k = gi[j] + off;
-                const int oct = A.kp_octave[k];
-                if (bCheckLevels) {
-                    if (oct < w.minL) continue;
-                    if (w.maxL >= 0 && oct > w.maxL) continue;
-                }
-                const float distx = A.kp_x[k] - w.x;
-                const float disty = A.kp_y[k] - w.y;
-                if (!(fabsf(distx) < factorX && fabsf(disty) < factorY)) continue;
-                if (!RIGHT && w.stereo && A.u_right) {
-                    const float ur = A.u_right[k];
-                    if (ur > 0) {
-                        const float er = fabsf(w.sx - ur);
-                        if (er > w.sr) continue;
-                    }
-                }
-                if (FILL) {
-                    const uint32_t d = dist256(qd, A.fdesc + (size_t)k * 8);
-                    out[cnt] = (uint32_t)k | (d << 16) | ((uint32_t)(oct & 0x7F) << 25);
-                }
-                cnt++;
+        const int j0 = G.gs[ix * OSG_GRID_ROWS + minCY], j1 = G.gs[ix * OSG_GRID_ROWS + maxCY + 1];
+        for (int j = j0; j < j1; j++) {
+            int k, oct;
+            float x, y;
+            if (STAGED) {
+                const int r = G.rk[j];
+                k = r >> 8;
+                oct = r & 0xFF;
+                x = G.rx[j];
+                y = G.ry[j];
+            } else {
+                k = G.gi[j] + G.off;
+                oct = A.kp_octave[k];
+                x = A.kp_x[k];
+                y = A.kp_y[k];
             }
+            if (bCheckLevels) {
+                if (oct < w.minL) continue;
+                if (w.maxL >= 0 && oct > w.maxL) continue;
+            }
+            const float distx = x - w.x;
+            const float disty = y - w.y;
+            if (!(fabsf(distx) < factorX && fabsf(disty) < factorY)) continue;
+            if (stereo) {
+                const float ur = STAGED ? G.ru[j] : A.u_right[k];
+                if (ur > 0) {
+                    const float er = fabsf(w.sx - ur);
+                    if (er > w.sr) continue;
+                }
+            }
+            if (FILL) {
+                const uint32_t d = dist256(qd, G.fd + (size_t)k * 8);
+                out[cnt] = (uint32_t)k | (d << 16) | ((uint32_t)(oct & 0x7F) << 25);
+            }
+            cnt++;
         }
     }
     return cnt;
 }
 
-// Candidates of query q: left-camera ones first, then right-camera ones; cl = left count.
-template <int MODE, bool FILL>
-__device__ int enum_query(const MatchArgs &A, int q, uint32_t *out, int &cl)
+__device__ __forceinline__ void load_desc(const MatchArgs &A, int q, uint32_t (&qd)[8])
+{
+    const uint4 a = ld4(A.qdesc + (size_t)q * 8);
+    const uint4 b = ld4(A.qdesc + (size_t)q * 8 + 4);
+    qd[0] = a.x; qd[1] = a.y; qd[2] = a.z; qd[3] = a.w;
+    qd[4] = b.x; qd[5] = b.y; qd[6] = b.z; qd[7] = b.w;
+}
+
+// Candidates of grid-mode query q from its precomputed windows: left-camera ones first, then
+// right-camera ones; cl = left count.
+template <int MODE, bool FILL, int STAGE>
+__device__ __forceinline__ int enum_query(const MatchArgs &A, const GridView<STAGE> &GL, const GridView<STAGE> &GR,
+                                          int q, GLOBAL uint32_t *out, int &cl)
 {
     uint32_t qd[8];
-    if (FILL) {
-        const uint4 a = *(const uint4 *)(A.qdesc + (size_t)q * 8);
-        const uint4 b = *(const uint4 *)(A.qdesc + (size_t)q * 8 + 4);
-        qd[0] = a.x; qd[1] = a.y; qd[2] = a.z; qd[3] = a.w;
-        qd[4] = b.x; qd[5] = b.y; qd[6] = b.z; qd[7] = b.w;
+    if (FILL) load_desc(A, q, qd);
+    const Win w = load_win(A.q_win + 4 * (size_t)q);
+    const int c0 = w.valid ? enum_grid<FILL, STAGE, false>(A, GL, w, qd, out) : 0;
+    cl = c0;
+    int c1 = 0;
+    if ((MODE == MODE_MPS || MODE == MODE_LAST) && A.nleft >= 0 && (MODE != MODE_LAST || c0 > 0)) {
+        const Win wr = load_win(A.q_win + 4 * (size_t)q + 2);
+        if (wr.valid) c1 = enum_grid<FILL, STAGE, true>(A, GR, wr, qd, FILL ? out + c0 : nullptr);
     }
-    if (MODE == MODE_BOW_KF_F || MODE == MODE_BOW_KF_KF) {
-        int cnt = 0;
-        const int e = A.q_ce[q];
-        for (int j = A.q_cb[q]; j < e; j++) {
-            const int idx = A.cand_list[j];
-            if (MODE == MODE_BOW_KF_KF && !A.slot_ok[idx]) continue;  // !pMP2 || isBad || right camera
-            if (FILL) {
-                const uint32_t d = dist256(qd, A.fdesc + (size_t)idx * 8);
-                out[cnt] = (uint32_t)idx | (d << 16);
-            }
-            cnt++;
-        }
-        cl = cnt;
-        return cnt;
-    } else {
-        const Win w = query_window<MODE>(A, q);
-        const int c0 = w.valid ? enum_grid<FILL, false>(A, w, qd, out) : 0;
-        cl = c0;
-        int c1 = 0;
-        if (MODE == MODE_MPS || MODE == MODE_LAST) {
-            const Win wr = query_window_r<MODE>(A, q, w, c0);
-            if (wr.valid) c1 = enum_grid<FILL, true>(A, wr, qd, FILL ? out + c0 : nullptr);
-        }
-        return c0 + c1;
+    return c0 + c1;
+}
+
+// SearchByBoW candidates: the other side's feature list of the query's vocabulary node, in list
+// order.  BOW_G lanes share one query.  A KF-KF candidate without a usable MapPoint (or a right-
+// camera keypoint) keeps its position with distance 0x1FF, which evaluation skips.
+constexpr int BOW_G = 16;
+
+template <int MODE>
+__device__ __forceinline__ void fill_bow_group(const MatchArgs &A, int q, int lane)
+{
+    uint32_t qd[8];
+    load_desc(A, q, qd);
+    const int cb = A.q_cb[q], ce = A.q_ce[q];
+    GLOBAL uint32_t *out = A.cands + A.q_off[q] - cb;
+    for (int j = cb + lane; j < ce; j += BOW_G) {
+        const int idx = A.cand_list[j];
+        uint32_t d = dist256(qd, A.fdesc + (size_t)idx * 8);
+        if (MODE == MODE_BOW_KF_KF && !A.slot_ok[idx]) d = 0x1FF;  // !pMP2 || isBad || right camera
+        out[j] = (uint32_t)idx | (d << 16);
     }
 }
 
@@ -341,30 +415,15 @@ struct Top2 {
     }
 };
 
-// One query in reference order.  blocked(s): is slot s unavailable to q given the assignments of
-// the queries before q (Jacobi: claims of the previous round; serial: the live slot state).
+// One grid-mode query in reference order.  blocked(s): is slot s unavailable to q given the
+// assignments of the queries before q (Jacobi: claims of the previous round; serial: the live slot
+// state).
 template <int MODE, typename Blocked>
 __device__ __forceinline__ QRes eval_query(const MatchArgs &A, int q, Blocked blocked)
 {
     QRes res{-1, -1};
     const int e0 = A.q_off[q], em = A.q_mid[q], e1 = A.q_off[q + 1];
     Top2 L, R;
-    if (MODE == MODE_BOW_KF_F) {
-        // ref:src/ORBmatcher.cc:316-441: one loop, separate top-2 for left / right keypoints
-        for (int e = e0; e < e1; e++) {
-            const uint32_t c = A.cands[e];
-            const int s = (int)(c & 0xFFFFu);
-            if (blocked(s)) continue;
-            const int d = (int)((c >> 16) & 0x1FFu);
-            if (A.nleft < 0 || s < A.nleft) L.push(d, 0, s);
-            else R.push(d, 0, s);
-        }
-        if (L.best <= OSG_TH_LOW) {
-            if ((float)L.best < A.nnratio * (float)L.second) res.l = L.bslot;
-            if (R.best <= OSG_TH_LOW) res.r = R.bslot;  // ratio disabled by '|| true' (:425)
-        }
-        return res;
-    }
     for (int e = e0; e < em; e++) {
         const uint32_t c = A.cands[e];
         const int s = (int)(c & 0xFFFFu);
@@ -377,10 +436,8 @@ __device__ __forceinline__ QRes eval_query(const MatchArgs &A, int q, Blocked bl
         skip_r = L.best <= OSG_TH_HIGH && !acc;
     } else if (MODE == MODE_LAST) {  // ref:src/ORBmatcher.cc:2070
         acc = L.best <= OSG_TH_HIGH;
-    } else if (MODE == MODE_KF) {  // ref:src/ORBmatcher.cc:2287
+    } else {  // MODE_KF, ref:src/ORBmatcher.cc:2287
         acc = L.best <= A.orb_dist;
-    } else {  // MODE_BOW_KF_KF, ref:src/ORBmatcher.cc:985-987
-        acc = L.best < OSG_TH_LOW && (float)L.best < A.nnratio * (float)L.second;
     }
     res.l = acc ? L.bslot : -1;
     if ((MODE == MODE_MPS || MODE == MODE_LAST) && em < e1 && !skip_r) {
@@ -407,6 +464,63 @@ __device__ __forceinline__ QRes eval_query(const MatchArgs &A, int q, Blocked bl
         else  // ref:src/ORBmatcher.cc:2133
             accr = R.best <= OSG_TH_HIGH;
         res.r = accr ? R.bslot : -1;
+    }
+    return res;
+}
+
+// top-2 of packed keys (distance << 16 | position in the query's list).  Keys are distinct, and
+// their order is the reference loop's (distance, then enumeration order): the first key is
+// (bestDist, bestIdx), the second is bestDist2 with multiplicity.
+constexpr uint32_t KEY_NONE = (256u << 16) | 0xFFFFu;
+
+__device__ __forceinline__ void push2(uint32_t &a1, uint32_t &a2, uint32_t k)
+{
+    const uint32_t hi = max(a1, k);
+    a1 = min(a1, k);
+    a2 = min(a2, hi);
+}
+
+__device__ __forceinline__ void merge2(uint32_t &a1, uint32_t &a2, int o)
+{
+    const uint32_t b1 = (uint32_t)__shfl_xor((int)a1, o), b2 = (uint32_t)__shfl_xor((int)a2, o);
+    const uint32_t hi = max(a1, b1);
+    a1 = min(a1, b1);
+    a2 = min(min(a2, b2), hi);
+}
+
+// One SearchByBoW query evaluated by the BOW_G lanes of a group (every lane returns the result).
+// ref:src/ORBmatcher.cc:316-441 (KF-F: separate left / right top-2 on a two-camera frame) and
+// :960-987 (KF-KF).
+template <int MODE, typename Blocked>
+__device__ __forceinline__ QRes eval_bow_group(const MatchArgs &A, int q, int lane, Blocked blocked)
+{
+    const int e0 = A.q_off[q], e1 = A.q_off[q + 1];
+    uint32_t l1 = KEY_NONE, l2 = KEY_NONE, r1 = KEY_NONE, r2 = KEY_NONE;
+    for (int e = e0 + lane; e < e1; e += BOW_G) {
+        const uint32_t c = A.cands[e];
+        const int s = (int)(c & 0xFFFFu);
+        const uint32_t d = (c >> 16) & 0x1FFu;
+        if (d > 256 || blocked(s)) continue;
+        const uint32_t key = (d << 16) | (uint32_t)(e - e0);
+        if (MODE == MODE_BOW_KF_KF || A.nleft < 0 || s < A.nleft) push2(l1, l2, key);
+        else push2(r1, r2, key);
+    }
+#pragma unroll
+    for (int o = BOW_G / 2; o > 0; o >>= 1) {
+        merge2(l1, l2, o);
+        if (MODE == MODE_BOW_KF_F) merge2(r1, r2, o);
+    }
+    const int best = (int)(l1 >> 16), second = (int)(l2 >> 16);
+    QRes res{-1, -1};
+    if (MODE == MODE_BOW_KF_F) {
+        if (best <= OSG_TH_LOW) {
+            if ((float)best < A.nnratio * (float)second) res.l = (int)(A.cands[e0 + (l1 & 0xFFFFu)] & 0xFFFFu);
+            if ((int)(r1 >> 16) <= OSG_TH_LOW)  // ratio disabled by '|| true' (:425)
+                res.r = (int)(A.cands[e0 + (r1 & 0xFFFFu)] & 0xFFFFu);
+        }
+    } else {
+        if (best < OSG_TH_LOW && (float)best < A.nnratio * (float)second)
+            res.l = (int)(A.cands[e0 + (l1 & 0xFFFFu)] & 0xFFFFu);
     }
     return res;
 }
@@ -454,9 +568,23 @@ __device__ __forceinline__ int rot_bin(float a, float b)
     return bin;
 }
 
-template <int MODE>
-__global__ __launch_bounds__(MT) void k_match(MatchArgs A)
+// Extra LDS of a staged grid-mode launch: cell offsets (one or two grids) + 4 words per keypoint.
+constexpr int GS_PAD = (OSG_GRID_CELLS + 1 + 3) & ~3;
+// STAGE 1: cell offsets + per-entry records; STAGE 2: also the descriptors (32 B per slot).
+__host__ __device__ inline size_t staged_lds_bytes(int ns, bool two_cam, int stage)
 {
+    if (stage <= 0) return 0;
+    size_t b = sizeof(int) * ((size_t)GS_PAD * (two_cam ? 2 : 1) + 4 * (size_t)ns);
+    if (stage >= 2) b = ((b + 15) & ~size_t(15)) + 32 * (size_t)ns;
+    return b;
+}
+
+template <int MODE, int STAGE>
+__global__ __launch_bounds__(MT) void k_match(const MatchArgs *__restrict__ args)
+{
+    constexpr bool BOW = MODE == MODE_BOW_KF_F || MODE == MODE_BOW_KF_KF;
+    constexpr bool STAGED = STAGE >= 1;
+    const MatchArgs &A = args[blockIdx.x];  // one problem per workgroup
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int NS = A.n_slots;
     int *claimA = (int *)smem;
@@ -471,17 +599,97 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A)
 
     const int tid = threadIdx.x;
     const int nq = A.nq;
+    if (nq == 0) return;  // status was zeroed by the host; the slot arrays stay as they are
     const int per = (nq + MT - 1) / MT;
     const int q0 = min(nq, tid * per), q1 = min(nq, q0 + per);
+    const int lane = tid & (BOW_G - 1), grp = tid / BOW_G;  // BoW: BOW_G lanes per query
+    constexpr int NGRP = MT / BOW_G;
+    // phase clocks (s_memtime) for OSG_MATCH_PROFILE: count, scan, fill, init, rounds, finish
+    uint64_t tclk[9];
+    tclk[0] = __builtin_amdgcn_s_memtime();
 
+    // ---- 0. grid views; a staged launch copies the grids into LDS as records in grid order
+    GridView<STAGE> GL{}, GR{};
+    if (!BOW) {
+        if constexpr (STAGED) {
+            const bool two = A.nleft >= 0;
+            int *gsL = (int *)(removedS + ((NS + 15) & ~15));
+            int *gsR = gsL + GS_PAD;
+            float *rx = (float *)(gsL + GS_PAD * (two ? 2 : 1));
+            float *ry = rx + NS, *ru = ry + NS;
+            int *rk = (int *)(ru + NS);
+            const int mL = A.grid_start[OSG_GRID_CELLS];
+            for (int c = tid; c <= OSG_GRID_CELLS; c += MT) gsL[c] = A.grid_start[c];
+            for (int j = tid; j < mL; j += MT) {
+                const int k = A.grid_idx[j];
+                rx[j] = A.kp_x[k];
+                ry[j] = A.kp_y[k];
+                ru[j] = A.u_right ? A.u_right[k] : -1.f;
+                rk[j] = (k << 8) | A.kp_octave[k];
+            }
+            if (two) {
+                const int mR = A.grid_start_r[OSG_GRID_CELLS];
+                for (int c = tid; c <= OSG_GRID_CELLS; c += MT) gsR[c] = A.grid_start_r[c] + mL;
+                for (int j = tid; j < mR; j += MT) {
+                    const int k = A.grid_idx_r[j] + A.nleft;
+                    rx[mL + j] = A.kp_x[k];
+                    ry[mL + j] = A.kp_y[k];
+                    ru[mL + j] = -1.f;
+                    rk[mL + j] = (k << 8) | A.kp_octave[k];
+                }
+            }
+            typename GridView<STAGE>::FdPtr fd;
+            if constexpr (STAGE >= 2) {
+                u32x4 *fdl = (u32x4 *)(smem + (((uintptr_t)(rk + NS) - (uintptr_t)smem + 15) & ~uintptr_t(15)));
+                GLOBAL const u32x4 *src = (GLOBAL const u32x4 *)A.fdesc;
+                for (int i = tid; i < 2 * NS; i += MT) fdl[i] = src[i];
+                fd = (const uint32_t *)fdl;
+            } else {
+                fd = A.fdesc;
+            }
+            GL = GridView<STAGE>{gsL, nullptr, 0, rx, ry, ru, rk, fd};
+            GR = GridView<STAGE>{gsR, nullptr, 0, rx, ry, ru, rk, fd};
+            __syncthreads();
+        } else {
+            if constexpr (STAGE == 0) {
+                GL = GridView<STAGE>{A.grid_start, A.grid_idx, 0, nullptr, nullptr, nullptr, nullptr, A.fdesc};
+                GR = GridView<STAGE>{A.grid_start_r, A.grid_idx_r, A.nleft, nullptr, nullptr, nullptr, nullptr, A.fdesc};
+            }
+        }
+        tclk[1] = __builtin_amdgcn_s_memtime();
+        // search windows, computed once; four queries per thread per step with all loads first
+        const bool two = (MODE == MODE_MPS || MODE == MODE_LAST) && A.nleft >= 0;
+        for (int qb = tid; qb < nq; qb += 4 * MT) {
+            Win wl[4], wr[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int q = min(qb + u * MT, nq - 1);
+                wl[u] = query_window<MODE>(A, q);
+                if (two) wr[u] = query_window_r<MODE>(A, q, wl[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int q = qb + u * MT;
+                if (q < nq) {
+                    store_win(A.q_win + 4 * (size_t)q, wl[u]);
+                    if (two) store_win(A.q_win + 4 * (size_t)q + 2, wr[u]);
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    tclk[2] = __builtin_amdgcn_s_memtime();
     // ---- 1. count
     int my = 0;
     for (int q = q0; q < q1; q++) {
         int cl;
-        const int c = enum_query<MODE, false>(A, q, nullptr, cl);
+        const int c = BOW ? A.q_ce[q] - A.q_cb[q] : enum_query<MODE, false, STAGE>(A, GL, GR, q, nullptr, cl);
         A.q_off[q] = c;  // temporarily the count
         my += c;
     }
+    __syncthreads();
+    tclk[3] = __builtin_amdgcn_s_memtime();
     // ---- 2. block scan (inclusive, Hillis-Steele)
     s_scan[tid] = my;
     __syncthreads();
@@ -499,19 +707,30 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A)
         }
         return;
     }
+    tclk[4] = __builtin_amdgcn_s_memtime();
     // ---- 3. fill
     {
         int off = s_scan[tid] - my;
         for (int q = q0; q < q1; q++) {
             const int c = A.q_off[q];
-            int cl;
             A.q_off[q] = off;
-            enum_query<MODE, true>(A, q, A.cands + off, cl);
-            A.q_mid[q] = off + cl;
+            if (BOW) {
+                A.q_mid[q] = off + c;
+            } else {
+                int cl;
+                enum_query<MODE, true, STAGE>(A, GL, GR, q, A.cands + off, cl);
+                A.q_mid[q] = off + cl;
+            }
             off += c;
         }
         if (tid == MT - 1) A.q_off[nq] = total;
+        if (BOW) {
+            __syncthreads();
+            for (int q = grp; q < nq; q += NGRP) fill_bow_group<MODE>(A, q, lane);
+        }
     }
+    __syncthreads();
+    tclk[5] = __builtin_amdgcn_s_memtime();
     // ---- 4. resolve: init slot state
     for (int s = tid; s < NS; s += MT) {
         claimA[s] = INT_BIG;
@@ -525,11 +744,19 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A)
     }
     if (tid < OSG_HISTO_LENGTH) s_hist[tid] = 0;
     __syncthreads();
-    for (int q = q0; q < q1; q++)
-        store_res(A, q, eval_query<MODE>(A, q, [&](int s) { return taken0[s] || claimA[s] < q; }));
+    if (BOW) {
+        for (int q = grp; q < nq; q += NGRP) {
+            const QRes r = eval_bow_group<MODE>(A, q, lane, [&](int s) { return taken0[s] != 0; });
+            if (lane == 0) store_res(A, q, r);
+        }
+    } else {
+        for (int q = q0; q < q1; q++)
+            store_res(A, q, eval_query<MODE>(A, q, [&](int s) { return taken0[s] != 0; }));
+    }
     __syncthreads();
     // Jacobi rounds.  A slot is blocked for q when it was blocked initially or a query p < q
     // whose MapPoint has observations wrote it (SearchByBoW / a7: any earlier write).
+    tclk[6] = __builtin_amdgcn_s_memtime();
     int rounds = 0;
     int *cur = claimB, *other = claimA;
     for (;;) {
@@ -543,12 +770,25 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A)
         }
         __syncthreads();
         int changed = 0;
-        for (int q = q0; q < q1; q++) {
-            const QRes r2 = eval_query<MODE>(A, q, [&](int s) { return taken0[s] || cur[s] < q; });
-            const QRes r1 = load_res(A, q);
-            if (r2.l != r1.l || r2.r != r1.r) {
-                changed = 1;
-                store_res(A, q, r2);
+        if (BOW) {
+            for (int q = grp; q < nq; q += NGRP) {
+                const QRes r2 = eval_bow_group<MODE>(A, q, lane, [&](int s) { return taken0[s] || cur[s] < q; });
+                if (lane == 0) {
+                    const QRes r1 = load_res(A, q);
+                    if (r2.l != r1.l || r2.r != r1.r) {
+                        changed = 1;
+                        store_res(A, q, r2);
+                    }
+                }
+            }
+        } else {
+            for (int q = q0; q < q1; q++) {
+                const QRes r2 = eval_query<MODE>(A, q, [&](int s) { return taken0[s] || cur[s] < q; });
+                const QRes r1 = load_res(A, q);
+                if (r2.l != r1.l || r2.r != r1.r) {
+                    changed = 1;
+                    store_res(A, q, r2);
+                }
             }
         }
         for (int s = tid; s < NS; s += MT) other[s] = INT_BIG;
@@ -562,6 +802,7 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A)
     // unless a stereo-partner write of a5 by a MapPoint WITHOUT observations lands on a slot that
     // was blocked: that write unblocks it (the slot's state is its last writer's).  Such a run is
     // redone serially in query order on the live slot state.
+    tclk[7] = __builtin_amdgcn_s_memtime();
     int serial = 0;
     if (MODE == MODE_MPS && A.nleft >= 0) {
         int need = 0;
@@ -680,75 +921,15 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A)
         A.status[0] = total;
         A.status[3] = 0;
         A.status[4] = serial;
+        tclk[8] = __builtin_amdgcn_s_memtime();
+        if (BOW) tclk[1] = tclk[2] = tclk[0];
+        for (int i = 0; i < 8; i++) A.status[5 + i] = (int32_t)(tclk[i + 1] - tclk[i]);
     }
 }
 
 size_t match_lds_bytes(int ns)
 {
     return (size_t)ns * 3 * sizeof(int) + 2 * (((size_t)ns + 15) & ~size_t(15));
-}
-
-// Upload the packed inputs + the in/out slot array, launch (growing the candidate buffer when the
-// count pass reports more than the capacity), download slot array / out_q + status.
-template <int MODE>
-int run_match(osg_ctx *ctx, MatchArgs A, const osg_packer &pk, int32_t *host_slot, int n_slot_io,
-              int32_t *host_out_q, int32_t *out_nmatches, void **dev_base_out)
-{
-    (void)dev_base_out;
-    const int nq = A.nq, NS = A.n_slots;
-    OSG_REQUIRE(ctx, NS <= MAX_SLOTS, "%d slots exceed the %d supported per problem", NS, MAX_SLOTS);
-    // layout of the device io block: [status 16 ints][slot 'n_slot_io' ints][out_q nq ints]
-    const size_t io_bytes = 64 + sizeof(int32_t) * ((size_t)n_slot_io + (size_t)nq) + 64;
-    char *pin = (char *)osg_pinned(ctx, pk.total + io_bytes + 256);
-    if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));  // pinned block may still be in use
-    pk.fill(pin);
-    char *dev_in = nullptr;
-    OSG_ALLOC(ctx, dev_in, SLOT_TMP0, pk.total + 256);
-    char *dev_io = nullptr;
-    OSG_ALLOC(ctx, dev_io, SLOT_TMP1, io_bytes);
-    char *pin_io = pin + ((pk.total + 255) & ~size_t(255));
-    std::memset(pin_io, 0, 64);
-    if (n_slot_io > 0) std::memcpy(pin_io + 64, host_slot, sizeof(int32_t) * n_slot_io);
-    if (pk.total) OSG_HIP_CHECK(ctx, hipMemcpyAsync(dev_in, pin, pk.total, hipMemcpyHostToDevice, ctx->stream));
-    OSG_HIP_CHECK(ctx, hipMemcpyAsync(dev_io, pin_io, 64 + sizeof(int32_t) * n_slot_io, hipMemcpyHostToDevice,
-                                      ctx->stream));
-    A.status = (int32_t *)dev_io;
-    A.slot_mp = (int32_t *)(dev_io + 64);
-    A.out_q = (int32_t *)(dev_io + 64 + sizeof(int32_t) * n_slot_io);
-    int cap = std::max(nq * 64, 1 << 16);
-    size_t lds = match_lds_bytes(NS);
-    for (int attempt = 0; attempt < 2; attempt++) {
-        OSG_ALLOC(ctx, A.q_off, SLOT_TMP2, sizeof(int32_t) * ((size_t)nq + 1));
-        OSG_ALLOC(ctx, A.q_res, SLOT_TMP3, sizeof(int32_t) * 2 * ((size_t)nq + 1));
-        OSG_ALLOC(ctx, A.q_bin, SLOT_TMP4, 2 * (size_t)nq + 16);
-        OSG_ALLOC(ctx, A.q_mid, SLOT_TMP6, sizeof(int32_t) * ((size_t)nq + 1));
-        OSG_ALLOC(ctx, A.cands, SLOT_TMP5, sizeof(uint32_t) * (size_t)cap);
-        A.cap = cap;
-        hipLaunchKernelGGL(k_match<MODE>, dim3(1), dim3(MT), lds, ctx->stream, A);
-        OSG_HIP_CHECK(ctx, hipGetLastError());
-        int32_t st[5];
-        OSG_HIP_CHECK(ctx, hipMemcpyAsync(st, dev_io, sizeof st, hipMemcpyDeviceToHost, ctx->stream));
-        OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
-        if (st[3] == 0) {
-            *out_nmatches = st[1];
-            ctx->match_stats[0] = st[0];
-            ctx->match_stats[1] = st[2];
-            ctx->match_stats[2] = st[4];
-            ctx->match_stats[3] = st[1];
-            break;
-        }
-        cap = st[0] + 1024;
-        if (attempt == 1) return osg_set_error(ctx, OSG_E_HIP, "candidate buffer overflow after resize");
-    }
-    const size_t back = sizeof(int32_t) * ((size_t)n_slot_io + (host_out_q ? (size_t)nq : 0));
-    if (back) {
-        OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_io + 64, dev_io + 64, back, hipMemcpyDeviceToHost, ctx->stream));
-        OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
-        if (n_slot_io > 0) std::memcpy(host_slot, pin_io + 64, sizeof(int32_t) * n_slot_io);
-        if (host_out_q) std::memcpy(host_out_q, pin_io + 64 + sizeof(int32_t) * n_slot_io, sizeof(int32_t) * nq);
-    }
-    return OSG_OK;
 }
 
 // Pointer fields of MatchArgs are first filled with packer offsets (+1 so that offset 0 is not
@@ -778,17 +959,178 @@ void relocate(T *&field, char *base)
         relocate(A.q_f0r, base); relocate(A.q_lvl_r, base); relocate(A.q_m0r, base);                         \
     } while (0)
 
+// One problem of a launch: its packed arguments plus host-side bookkeeping.  The vectors hold
+// host-built inputs (BoW query arrays) that must stay alive until the packer copies them.
+struct Problem {
+    MatchArgs A = {};
+    int32_t *host_slot = nullptr;  // slot array (in/out), n_slot entries
+    int n_slot = 0;
+    std::vector<int32_t> q_feat, q_cb, q_ce, q_mp;
+    std::vector<uint8_t> qdesc, slot_ok;
+    std::vector<float> q_angle;
+    int32_t *out_mp12 = nullptr;   // KF-KF: result indexed by KF1 keypoint
+};
+
+constexpr int STATUS_INTS = 16;
+
+// Upload every problem's packed inputs and slot arrays, launch one workgroup per problem (growing
+// a problem's candidate buffer when its count pass reports more than the capacity), and download
+// the slot arrays / KF-KF results and the per-problem match counts.
 template <int MODE>
-int launch_packed(osg_ctx *ctx, MatchArgs &A, osg_packer &pk, int32_t *host_slot, int n_slot_io,
-                  int32_t *host_out_q)
+int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_t *nmatches)
 {
-    char *dev_in = nullptr;
+    const int B = (int)P.size();
+    if (B == 0) return OSG_OK;
+    std::vector<size_t> slot_off(B + 1, 0), q_base(B + 1, 0);
+    size_t lds = 0;
+    for (int b = 0; b < B; b++) {
+        OSG_REQUIRE(ctx, P[b].A.n_slots <= MAX_SLOTS, "problem %d: %d slots exceed the %d supported", b,
+                    P[b].A.n_slots, MAX_SLOTS);
+        slot_off[b + 1] = slot_off[b] + (size_t)P[b].n_slot;
+        q_base[b + 1] = q_base[b] + (size_t)P[b].A.nq + 1;
+        lds = std::max(lds, match_lds_bytes(P[b].A.n_slots));
+    }
+    // grid modes stage the frames' grids (and descriptors) in LDS when every problem's fits
+    constexpr bool BOW = MODE == MODE_BOW_KF_F || MODE == MODE_BOW_KF_KF;
+    static const int stage_env = getenv("OSG_MATCH_STAGE") ? atoi(getenv("OSG_MATCH_STAGE")) : 2;
+    const size_t lds_budget = (size_t)std::max(0, ctx->lds_per_block - 8 * 1024);  // static LDS ~4.3 KB
+    int stage = 0;
+    if (!BOW)
+        for (int st = std::min(stage_env, 2); st >= 1 && stage == 0; st--) {
+            size_t need = lds;
+            for (int b = 0; b < B; b++)
+                need = std::max(need, match_lds_bytes(P[b].A.n_slots) +
+                                          staged_lds_bytes(P[b].A.n_slots, P[b].A.nleft >= 0, st));
+            if (need <= lds_budget) {
+                stage = st;
+                lds = need;
+            }
+        }
+    // (dynamic LDS up to the 160 KiB of a CU launches without a function attribute on gfx950:
+    // tools/micro/lds_limit.hip)
+    const size_t n_slot_total = slot_off[B], nq_total = q_base[B];
+    // device io block: [status B x 16 ints][slot arrays][out_q]
+    const size_t status_bytes = sizeof(int32_t) * STATUS_INTS * (size_t)B;
+    const size_t io_in_bytes = status_bytes + sizeof(int32_t) * n_slot_total;
+    const size_t io_bytes = io_in_bytes + sizeof(int32_t) * nq_total + 64;
+    const size_t in_bytes = (pk.total + 255) & ~size_t(255);
+    const size_t io_pad = (io_bytes + 255) & ~size_t(255);
+    const size_t args_bytes = sizeof(MatchArgs) * (size_t)B;
+    char *pin = (char *)osg_pinned(ctx, in_bytes + io_pad + args_bytes + 256);
+    if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
+    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));  // pinned block may still be in use
+    pk.fill(pin);
+    char *pin_io = pin + in_bytes;
+    MatchArgs *pin_args = (MatchArgs *)(pin_io + io_pad);
+    std::memset(pin_io, 0, status_bytes);
+    for (int b = 0; b < B; b++)
+        if (P[b].n_slot > 0)
+            std::memcpy(pin_io + status_bytes + sizeof(int32_t) * slot_off[b], P[b].host_slot,
+                        sizeof(int32_t) * P[b].n_slot);
+    char *dev_in = nullptr, *dev_io = nullptr;
+    MatchArgs *dev_args = nullptr;
     OSG_ALLOC(ctx, dev_in, SLOT_TMP0, pk.total + 256);
-    OSG_RELOCATE_ALL(A, dev_in);
-    int nm = 0;
-    const int rc = run_match<MODE>(ctx, A, pk, host_slot, n_slot_io, host_out_q, &nm, nullptr);
-    if (rc < 0) return rc;
-    return nm;
+    OSG_ALLOC(ctx, dev_io, SLOT_TMP1, io_bytes);
+    OSG_ALLOC(ctx, dev_args, SLOT_TMP7, args_bytes);
+    if (pk.total) OSG_HIP_CHECK(ctx, hipMemcpyAsync(dev_in, pin, pk.total, hipMemcpyHostToDevice, ctx->stream));
+    for (int b = 0; b < B; b++) {
+        MatchArgs &A = P[b].A;
+        OSG_RELOCATE_ALL(A, dev_in);
+        A.status = (GLOBAL int32_t *)dev_io + STATUS_INTS * b;
+        A.slot_mp = (GLOBAL int32_t *)(dev_io + status_bytes) + slot_off[b];
+        A.out_q = (GLOBAL int32_t *)(dev_io + io_in_bytes) + q_base[b];
+    }
+    std::vector<size_t> cap(B), cand_off(B + 1);
+    for (int b = 0; b < B; b++) cap[b] = std::max<size_t>((size_t)P[b].A.nq * 32, 1024);
+    std::vector<int32_t> st((size_t)STATUS_INTS * B);
+    for (int attempt = 0; attempt < 2; attempt++) {
+        cand_off[0] = 0;
+        for (int b = 0; b < B; b++) cand_off[b + 1] = cand_off[b] + cap[b];
+        int32_t *q_off, *q_mid, *q_res;
+        uint8_t *q_bin;
+        uint32_t *cands;
+        OSG_ALLOC(ctx, q_off, SLOT_TMP2, sizeof(int32_t) * nq_total);
+        OSG_ALLOC(ctx, q_res, SLOT_TMP3, sizeof(int32_t) * 2 * nq_total);
+        OSG_ALLOC(ctx, q_bin, SLOT_TMP4, 2 * nq_total + 16);
+        OSG_ALLOC(ctx, q_mid, SLOT_TMP6, sizeof(int32_t) * nq_total);
+        float4 *q_win = nullptr;
+        if (!BOW) OSG_ALLOC(ctx, q_win, SLOT_TMP8, sizeof(float4) * 4 * nq_total);
+        OSG_ALLOC(ctx, cands, SLOT_TMP5, sizeof(uint32_t) * cand_off[B]);
+        for (int b = 0; b < B; b++) {
+            MatchArgs &A = P[b].A;
+            A.q_off = (GLOBAL int32_t *)(q_off + q_base[b]);
+            A.q_mid = (GLOBAL int32_t *)(q_mid + q_base[b]);
+            A.q_win = q_win ? (GLOBAL f32x4 *)(q_win + 4 * q_base[b]) : nullptr;
+            A.q_res = (GLOBAL int32_t *)(q_res + 2 * q_base[b]);
+            A.q_bin = (GLOBAL uint8_t *)(q_bin + 2 * q_base[b]);
+            A.cands = (GLOBAL uint32_t *)(cands + cand_off[b]);
+            A.cap = (int)std::min<size_t>(cap[b], INT_BIG);
+            pin_args[b] = A;
+        }
+        // (re)upload the status block and the input slot state: a retry must not see the slot
+        // arrays written by the problems that fitted the first time
+        OSG_HIP_CHECK(ctx, hipMemcpyAsync(dev_io, pin_io, io_in_bytes, hipMemcpyHostToDevice, ctx->stream));
+        OSG_HIP_CHECK(ctx, hipMemcpyAsync(dev_args, pin_args, args_bytes, hipMemcpyHostToDevice, ctx->stream));
+        if (!ctx->ev[0]) {
+            OSG_HIP_CHECK(ctx, hipEventCreate(&ctx->ev[0]));
+            OSG_HIP_CHECK(ctx, hipEventCreate(&ctx->ev[1]));
+        }
+        OSG_HIP_CHECK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
+        if (stage == 2)
+            hipLaunchKernelGGL((k_match<MODE, 2>), dim3(B), dim3(MT), lds, ctx->stream, dev_args);
+        else if (stage == 1)
+            hipLaunchKernelGGL((k_match<MODE, 1>), dim3(B), dim3(MT), lds, ctx->stream, dev_args);
+        else
+            hipLaunchKernelGGL((k_match<MODE, 0>), dim3(B), dim3(MT), lds, ctx->stream, dev_args);
+        OSG_HIP_CHECK(ctx, hipGetLastError());
+        OSG_HIP_CHECK(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
+        OSG_HIP_CHECK(ctx, hipMemcpyAsync(st.data(), dev_io, status_bytes, hipMemcpyDeviceToHost, ctx->stream));
+        OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+        bool overflow = false;
+        for (int b = 0; b < B; b++)
+            if (st[(size_t)STATUS_INTS * b + 3]) {
+                overflow = true;
+                cap[b] = (size_t)st[(size_t)STATUS_INTS * b] + 256;
+            }
+        if (!overflow) break;
+        if (attempt == 1) return osg_set_error(ctx, OSG_E_HIP, "candidate buffer overflow after resize");
+    }
+    const size_t back = sizeof(int32_t) * (n_slot_total + (MODE == MODE_BOW_KF_KF ? nq_total : 0));
+    if (back) {
+        OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_io + status_bytes, dev_io + status_bytes, back, hipMemcpyDeviceToHost,
+                                          ctx->stream));
+        OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    int64_t cand_sum = 0, nm_sum = 0;
+    int rounds_max = 0, serial_n = 0;
+    for (int b = 0; b < B; b++) {
+        const int32_t *sb = &st[(size_t)STATUS_INTS * b];
+        nmatches[b] = sb[1];
+        cand_sum += sb[0];
+        nm_sum += sb[1];
+        rounds_max = std::max(rounds_max, (int)sb[2]);
+        serial_n += sb[4] ? 1 : 0;
+        if (P[b].n_slot > 0)
+            std::memcpy(P[b].host_slot, pin_io + status_bytes + sizeof(int32_t) * slot_off[b],
+                        sizeof(int32_t) * P[b].n_slot);
+        if (MODE == MODE_BOW_KF_KF) {
+            const int32_t *oq = (const int32_t *)(pin_io + io_in_bytes) + q_base[b];
+            for (size_t i = 0; i < P[b].q_feat.size(); i++) P[b].out_mp12[P[b].q_feat[i]] = oq[i];
+        }
+    }
+    float ms = 0.f;
+    OSG_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]));
+    ctx->match_kernel_ms = ms;
+    static const bool prof = getenv("OSG_MATCH_PROFILE") != nullptr;
+    if (prof)
+        fprintf(stderr, "[osg match] mode %d B %d kernel %.3f ms | problem 0: nq %d cands %d rounds %d serial %d | "
+                        "clk stage %d windows %d count %d scan %d fill %d init %d rounds %d finish %d (stage %d)\n",
+                MODE, B, ms, P[0].A.nq, st[0], st[2], st[4], st[5], st[6], st[7], st[8], st[9], st[10], st[11], st[12], stage);
+    ctx->match_stats[0] = (int32_t)std::min<int64_t>(cand_sum, INT_BIG);
+    ctx->match_stats[1] = rounds_max;
+    ctx->match_stats[2] = serial_n;
+    ctx->match_stats[3] = (int32_t)std::min<int64_t>(nm_sum, INT_BIG);
+    return OSG_OK;
 }
 
 void frame_into_args(MatchArgs &A, osg_packer &pk, const osg_frame *F)
@@ -811,6 +1153,7 @@ void frame_into_args(MatchArgs &A, osg_packer &pk, const osg_frame *F)
         set_off(A.r2l, pk.add(F->right_to_left, sizeof(int32_t) * (F->n - F->nleft)));
     }
     set_off(A.scale, pk.add(F->scale_factors, sizeof(float) * F->n_levels));
+    A.n_levels = F->n_levels;
     A.min_x = F->min_x;
     A.max_x = F->max_x;
     A.min_y = F->min_y;
@@ -822,7 +1165,7 @@ void frame_into_args(MatchArgs &A, osg_packer &pk, const osg_frame *F)
 }
 
 // A grid in CSR must index keypoints [0, n_cam) only: the kernels trust it.
-static int check_grid(osg_ctx *ctx, const int32_t *gs, const int32_t *gi, int n_cam, const char *which)
+int check_grid(osg_ctx *ctx, const int32_t *gs, const int32_t *gi, int n_cam, const char *which)
 {
     OSG_REQUIRE(ctx, gs && (gi || gs[OSG_GRID_CELLS] == 0), "%s grid missing", which);
     OSG_REQUIRE(ctx, gs[0] == 0, "%s grid_start[0] != 0", which);
@@ -840,6 +1183,8 @@ int check_frame(osg_ctx *ctx, const osg_frame *F)
     OSG_REQUIRE(ctx, F->nleft == -1 || (F->nleft >= 0 && F->nleft <= F->n), "frame nleft out of range");
     OSG_REQUIRE(ctx, F->n == 0 || (F->desc && F->kp_x && F->kp_y && F->kp_angle && F->kp_octave), "frame arrays");
     OSG_REQUIRE(ctx, F->scale_factors && F->n_levels > 0, "frame scale factors");
+    for (int i = 0; i < F->n; i++)  // octaves are packed in 7 bits
+        OSG_REQUIRE(ctx, F->kp_octave[i] >= 0 && F->kp_octave[i] < 128, "kp_octave[%d] = %d", i, F->kp_octave[i]);
     const int nl = F->nleft == -1 ? F->n : F->nleft;
     int rc = check_grid(ctx, F->grid_start, F->grid_idx, nl, "left");
     if (rc < 0) return rc;
@@ -854,35 +1199,36 @@ int check_frame(osg_ctx *ctx, const osg_frame *F)
     return OSG_OK;
 }
 
-}  // namespace
+// ---- per-operator problem setup (validation + packing); ref lines are the operators' own
 
-extern "C" {
-
-int osg_search_by_projection_mps(osg_ctx *ctx, const osg_frame *F, const osg_mp_queries *Q, float nnratio,
-                                 float th, int far_points, float th_far_points, int32_t *slot_mp,
-                                 const uint8_t *slot_taken)
+int prep_mps(osg_ctx *ctx, Problem &P, osg_packer &pk, const osg_frame *F, const osg_mp_queries *Q, float nnratio,
+             float th, int far_points, float th_far_points, int32_t *slot_mp, const uint8_t *slot_taken)
 {
-    if (!ctx) return OSG_E_INVALID;
     int rc = check_frame(ctx, F);
     if (rc < 0) return rc;
     OSG_REQUIRE(ctx, Q && Q->n >= 0 && slot_mp && slot_taken, "null argument");
-    if (Q->n == 0) return 0;
+    MatchArgs &A = P.A;
+    frame_into_args(A, pk, F);
+    P.host_slot = slot_mp;
+    P.n_slot = F->n;
+    const int n = Q->n;
+    A.nq = n;
+    A.nnratio = nnratio;
+    A.th = th;
+    A.far_points = far_points;
+    A.th_far = th_far_points;
+    if (n == 0) return OSG_OK;
     OSG_REQUIRE(ctx, Q->desc && Q->mp_id && Q->usable && Q->has_obs && Q->in_view && Q->proj_x && Q->proj_y &&
                          Q->proj_xr && Q->view_cos && Q->pred_level && Q->track_depth, "query arrays");
-    for (int i = 0; i < Q->n; i++)
+    for (int i = 0; i < n; i++)
         if (Q->in_view[i] && (Q->pred_level[i] < 0 || Q->pred_level[i] >= F->n_levels))
             return osg_set_error(ctx, OSG_E_INVALID, "pred_level[%d] = %d out of range", i, Q->pred_level[i]);
     if (F->nleft != -1) {
         OSG_REQUIRE(ctx, Q->in_view_r && Q->proj_yr && Q->view_cos_r && Q->pred_level_r, "right-camera query arrays");
-        for (int i = 0; i < Q->n; i++)
+        for (int i = 0; i < n; i++)
             if (Q->in_view_r[i] && (Q->pred_level_r[i] < -1 || Q->pred_level_r[i] >= F->n_levels))
                 return osg_set_error(ctx, OSG_E_INVALID, "pred_level_r[%d] = %d out of range", i, Q->pred_level_r[i]);
     }
-    MatchArgs A = {};
-    osg_packer pk;
-    frame_into_args(A, pk, F);
-    const int n = Q->n;
-    A.nq = n;
     set_off(A.qdesc, pk.add(Q->desc, (size_t)n * 32));
     set_off(A.q_mp, pk.add(Q->mp_id, sizeof(int32_t) * n));
     set_off(A.q_has_obs, pk.add(Q->has_obs, n));
@@ -902,31 +1248,31 @@ int osg_search_by_projection_mps(osg_ctx *ctx, const osg_frame *F, const osg_mp_
         set_off(A.q_lvl_r, pk.add(Q->pred_level_r, sizeof(int32_t) * n));
         set_off(A.q_m0r, pk.add(Q->in_view_r, n));
     }
-    A.nnratio = nnratio;
-    A.th = th;
-    A.far_points = far_points;
-    A.th_far = th_far_points;
-    return launch_packed<MODE_MPS>(ctx, A, pk, slot_mp, F->n, nullptr);
+    return OSG_OK;
 }
 
-int osg_search_by_projection_last(osg_ctx *ctx, const osg_frame *CF, const osg_last_queries *L, float th,
-                                  int mono, int check_orientation, int32_t *slot_mp, const uint8_t *slot_taken)
+int prep_last(osg_ctx *ctx, Problem &P, osg_packer &pk, const osg_frame *CF, const osg_last_queries *L, float th,
+              int mono, int check_orientation, int32_t *slot_mp, const uint8_t *slot_taken)
 {
-    if (!ctx) return OSG_E_INVALID;
     int rc = check_frame(ctx, CF);
     if (rc < 0) return rc;
     OSG_REQUIRE(ctx, L && L->n >= 0 && slot_mp && slot_taken, "null argument");
-    if (L->n == 0) return 0;
-    OSG_REQUIRE(ctx, L->desc && L->mp_id && L->valid && L->has_obs && L->u && L->v && L->invz && L->octave &&
-                         L->angle, "query arrays");
-    for (int i = 0; i < L->n; i++)
-        if (L->valid[i] && (L->octave[i] < 0 || L->octave[i] >= CF->n_levels))
-            return osg_set_error(ctx, OSG_E_INVALID, "octave[%d] out of range", i);
-    MatchArgs A = {};
-    osg_packer pk;
+    MatchArgs &A = P.A;
     frame_into_args(A, pk, CF);
+    P.host_slot = slot_mp;
+    P.n_slot = CF->n;
     const int n = L->n;
     A.nq = n;
+    A.th = th;
+    A.mono = mono;
+    A.tlc_z = L->tlc_z;
+    A.check_ori = check_orientation;
+    if (n == 0) return OSG_OK;
+    OSG_REQUIRE(ctx, L->desc && L->mp_id && L->valid && L->has_obs && L->u && L->v && L->invz && L->octave &&
+                         L->angle, "query arrays");
+    for (int i = 0; i < n; i++)
+        if (L->valid[i] && (L->octave[i] < 0 || L->octave[i] >= CF->n_levels))
+            return osg_set_error(ctx, OSG_E_INVALID, "octave[%d] out of range", i);
     set_off(A.qdesc, pk.add(L->desc, (size_t)n * 32));
     set_off(A.q_mp, pk.add(L->mp_id, sizeof(int32_t) * n));
     set_off(A.q_has_obs, pk.add(L->has_obs, n));
@@ -942,30 +1288,29 @@ int osg_search_by_projection_last(osg_ctx *ctx, const osg_frame *CF, const osg_l
         set_off(A.q_xr, pk.add(L->u_r, sizeof(float) * n));
         set_off(A.q_yr, pk.add(L->v_r, sizeof(float) * n));
     }
-    A.th = th;
-    A.mono = mono;
-    A.tlc_z = L->tlc_z;
-    A.check_ori = check_orientation;
-    return launch_packed<MODE_LAST>(ctx, A, pk, slot_mp, CF->n, nullptr);
+    return OSG_OK;
 }
 
-int osg_search_by_projection_kf(osg_ctx *ctx, const osg_frame *CF, const osg_kf_queries *K, float th, int orb_dist,
-                                int check_orientation, int32_t *slot_mp)
+int prep_kf(osg_ctx *ctx, Problem &P, osg_packer &pk, const osg_frame *CF, const osg_kf_queries *K, float th,
+            int orb_dist, int check_orientation, int32_t *slot_mp)
 {
-    if (!ctx) return OSG_E_INVALID;
     int rc = check_frame(ctx, CF);
     if (rc < 0) return rc;
     OSG_REQUIRE(ctx, K && K->n >= 0 && slot_mp, "null argument");
-    if (K->n == 0) return 0;
-    OSG_REQUIRE(ctx, K->desc && K->mp_id && K->valid && K->u && K->v && K->pred_level && K->angle, "query arrays");
-    for (int i = 0; i < K->n; i++)
-        if (K->valid[i] && (K->pred_level[i] < 0 || K->pred_level[i] >= CF->n_levels))
-            return osg_set_error(ctx, OSG_E_INVALID, "pred_level[%d] out of range", i);
-    MatchArgs A = {};
-    osg_packer pk;
+    MatchArgs &A = P.A;
     frame_into_args(A, pk, CF);
+    P.host_slot = slot_mp;
+    P.n_slot = CF->n;
     const int n = K->n;
     A.nq = n;
+    A.th = th;
+    A.orb_dist = orb_dist;
+    A.check_ori = check_orientation;
+    if (n == 0) return OSG_OK;
+    OSG_REQUIRE(ctx, K->desc && K->mp_id && K->valid && K->u && K->v && K->pred_level && K->angle, "query arrays");
+    for (int i = 0; i < n; i++)
+        if (K->valid[i] && (K->pred_level[i] < 0 || K->pred_level[i] >= CF->n_levels))
+            return osg_set_error(ctx, OSG_E_INVALID, "pred_level[%d] out of range", i);
     set_off(A.qdesc, pk.add(K->desc, (size_t)n * 32));
     set_off(A.q_mp, pk.add(K->mp_id, sizeof(int32_t) * n));
     set_off(A.q_m0, pk.add(K->valid, n));
@@ -973,17 +1318,14 @@ int osg_search_by_projection_kf(osg_ctx *ctx, const osg_frame *CF, const osg_kf_
     set_off(A.q_y, pk.add(K->v, sizeof(float) * n));
     set_off(A.q_lvl, pk.add(K->pred_level, sizeof(int32_t) * n));
     set_off(A.q_angle, pk.add(K->angle, sizeof(float) * n));
-    A.th = th;
-    A.orb_dist = orb_dist;
-    A.check_ori = check_orientation;
-    return launch_packed<MODE_KF>(ctx, A, pk, slot_mp, CF->n, nullptr);
+    return OSG_OK;
 }
 
 // Host half of SearchByBoW: the FeatureVector merge-walk (ref:src/ORBmatcher.cc:292-467) emits the
 // query order (shared nodes ascending, KeyFrame features in node order); each query's candidate
 // list is the other side's feature list of the same node.
-static int bow_queries(const osg_bow_side *A_, const osg_bow_side *B_, bool guard_nleft_a,
-                       std::vector<int32_t> &q_feat, std::vector<int32_t> &q_cb, std::vector<int32_t> &q_ce)
+int bow_queries(const osg_bow_side *A_, const osg_bow_side *B_, bool guard_nleft_a, std::vector<int32_t> &q_feat,
+                std::vector<int32_t> &q_cb, std::vector<int32_t> &q_ce)
 {
     int ia = 0, ib = 0;
     const osg_featvec &fa = A_->fv, &fb = B_->fv;
@@ -1022,91 +1364,245 @@ static int bow_queries(const osg_bow_side *A_, const osg_bow_side *B_, bool guar
     return 0;
 }
 
-int osg_search_by_bow_kf_f(osg_ctx *ctx, const osg_bow_side *kf, const osg_bow_side *f, float nnratio,
-                           int check_orientation, int32_t *out_mp)
+int check_bow_side(osg_ctx *ctx, const osg_bow_side *S, const char *which, bool slot_side)
 {
-    if (!ctx) return OSG_E_INVALID;
-    OSG_REQUIRE(ctx, kf && f && out_mp, "null argument");
-    OSG_REQUIRE(ctx, f->n >= 0 && f->n <= MAX_SLOTS && kf->n >= 0, "sizes");
-    OSG_REQUIRE(ctx, f->nleft == -1 || (f->nleft >= 0 && f->nleft <= f->n), "frame nleft");
-    for (int i = 0; i < f->n; i++) out_mp[i] = -1;
-    std::vector<int32_t> q_feat, q_cb, q_ce;
-    if (bow_queries(kf, f, false, q_feat, q_cb, q_ce) < 0) return osg_set_error(ctx, OSG_E_INVALID, "feature index");
-    const int n = (int)q_feat.size();
-    if (n == 0) return 0;
-    for (int j = 0; j < f->fv.node_start[f->fv.n_nodes]; j++)
-        OSG_REQUIRE(ctx, f->fv.feat[j] >= 0 && f->fv.feat[j] < f->n, "frame feature index");
-    std::vector<uint8_t> qdesc((size_t)n * 32);
-    std::vector<int32_t> q_mp(n);
-    std::vector<float> q_angle(n);
-    for (int i = 0; i < n; i++) {
-        std::memcpy(&qdesc[(size_t)i * 32], kf->desc + (size_t)q_feat[i] * 32, 32);
-        q_mp[i] = kf->mp_id[q_feat[i]];
-        q_angle[i] = kf->angle[q_feat[i]];
+    OSG_REQUIRE(ctx, S->n >= 0 && (!slot_side || S->n <= MAX_SLOTS), "%s: n out of range", which);
+    OSG_REQUIRE(ctx, S->nleft == -1 || (S->nleft >= 0 && S->nleft <= S->n), "%s: nleft out of range", which);
+    OSG_REQUIRE(ctx, S->fv.n_nodes >= 0 && (S->fv.n_nodes == 0 || (S->fv.node_id && S->fv.node_start)),
+                "%s: FeatureVector", which);
+    if (S->fv.n_nodes > 0) {
+        const int m = S->fv.node_start[S->fv.n_nodes];
+        OSG_REQUIRE(ctx, m == 0 || S->fv.feat, "%s: FeatureVector features", which);
+        for (int j = 0; j < m; j++)
+            OSG_REQUIRE(ctx, S->fv.feat[j] >= 0 && S->fv.feat[j] < S->n, "%s: feature index %d", which, S->fv.feat[j]);
     }
-    MatchArgs A = {};
-    osg_packer pk;
+    return OSG_OK;
+}
+
+int prep_bow_kf_f(osg_ctx *ctx, Problem &P, osg_packer &pk, const osg_bow_side *kf, const osg_bow_side *f,
+                  float nnratio, int check_orientation, int32_t *out_mp)
+{
+    OSG_REQUIRE(ctx, kf && f && out_mp, "null argument");
+    int rc = check_bow_side(ctx, kf, "keyframe", false);
+    if (rc < 0) return rc;
+    rc = check_bow_side(ctx, f, "frame", true);
+    if (rc < 0) return rc;
+    OSG_REQUIRE(ctx, kf->n == 0 || (kf->desc && kf->angle && kf->mp_id && kf->mp_good), "keyframe arrays");
+    OSG_REQUIRE(ctx, f->n == 0 || (f->desc && f->angle), "frame arrays");
+    for (int i = 0; i < f->n; i++) out_mp[i] = -1;
+    if (bow_queries(kf, f, false, P.q_feat, P.q_cb, P.q_ce) < 0) return osg_set_error(ctx, OSG_E_INVALID, "feature index");
+    const int n = (int)P.q_feat.size();
+    P.qdesc.resize((size_t)n * 32);
+    P.q_mp.resize(n);
+    P.q_angle.resize(n);
+    for (int i = 0; i < n; i++) {
+        std::memcpy(&P.qdesc[(size_t)i * 32], kf->desc + (size_t)P.q_feat[i] * 32, 32);
+        P.q_mp[i] = kf->mp_id[P.q_feat[i]];
+        P.q_angle[i] = kf->angle[P.q_feat[i]];
+    }
+    MatchArgs &A = P.A;
     A.nq = n;
     A.n_slots = f->n;
     A.nleft = f->nleft;
-    set_off(A.fdesc, pk.add(f->desc, (size_t)f->n * 32));
-    set_off(A.slot_angle, pk.add(f->angle, sizeof(float) * f->n));
-    set_off(A.qdesc, pk.add(qdesc.data(), qdesc.size()));
-    set_off(A.q_mp, pk.add(q_mp.data(), sizeof(int32_t) * n));
-    set_off(A.q_angle, pk.add(q_angle.data(), sizeof(float) * n));
-    set_off(A.q_cb, pk.add(q_cb.data(), sizeof(int32_t) * n));
-    set_off(A.q_ce, pk.add(q_ce.data(), sizeof(int32_t) * n));
-    set_off(A.cand_list, pk.add(f->fv.feat, sizeof(int32_t) * f->fv.node_start[f->fv.n_nodes]));
+    P.host_slot = out_mp;
+    P.n_slot = f->n;
     A.nnratio = nnratio;
     A.check_ori = check_orientation;
-    return launch_packed<MODE_BOW_KF_F>(ctx, A, pk, out_mp, f->n, nullptr);
+    if (n == 0) return OSG_OK;
+    set_off(A.fdesc, pk.add(f->desc, (size_t)f->n * 32));
+    set_off(A.slot_angle, pk.add(f->angle, sizeof(float) * f->n));
+    set_off(A.qdesc, pk.add(P.qdesc.data(), P.qdesc.size()));
+    set_off(A.q_mp, pk.add(P.q_mp.data(), sizeof(int32_t) * n));
+    set_off(A.q_angle, pk.add(P.q_angle.data(), sizeof(float) * n));
+    set_off(A.q_cb, pk.add(P.q_cb.data(), sizeof(int32_t) * n));
+    set_off(A.q_ce, pk.add(P.q_ce.data(), sizeof(int32_t) * n));
+    set_off(A.cand_list, pk.add(f->fv.feat, sizeof(int32_t) * f->fv.node_start[f->fv.n_nodes]));
+    return OSG_OK;
+}
+
+int prep_bow_kf_kf(osg_ctx *ctx, Problem &P, osg_packer &pk, const osg_bow_side *kf1, const osg_bow_side *kf2,
+                   float nnratio, int check_orientation, int32_t *out_mp12)
+{
+    OSG_REQUIRE(ctx, kf1 && kf2 && out_mp12, "null argument");
+    int rc = check_bow_side(ctx, kf1, "keyframe 1", false);
+    if (rc < 0) return rc;
+    rc = check_bow_side(ctx, kf2, "keyframe 2", true);
+    if (rc < 0) return rc;
+    OSG_REQUIRE(ctx, kf1->n == 0 || (kf1->desc && kf1->angle && kf1->mp_good), "keyframe 1 arrays");
+    OSG_REQUIRE(ctx, kf2->n == 0 || (kf2->desc && kf2->angle && kf2->mp_id && kf2->mp_good), "keyframe 2 arrays");
+    for (int i = 0; i < kf1->n; i++) out_mp12[i] = -1;
+    if (bow_queries(kf1, kf2, true, P.q_feat, P.q_cb, P.q_ce) < 0) return osg_set_error(ctx, OSG_E_INVALID, "feature index");
+    const int n = (int)P.q_feat.size();
+    P.qdesc.resize((size_t)n * 32);
+    P.q_angle.resize(n);
+    P.slot_ok.resize(kf2->n);
+    for (int i = 0; i < n; i++) {
+        std::memcpy(&P.qdesc[(size_t)i * 32], kf1->desc + (size_t)P.q_feat[i] * 32, 32);
+        P.q_angle[i] = kf1->angle[P.q_feat[i]];
+    }
+    // right-camera keypoints of a two-camera KF2 are skipped (ref:src/ORBmatcher.cc:953-955)
+    for (int s = 0; s < kf2->n; s++)
+        P.slot_ok[s] = (kf2->mp_id[s] >= 0 && kf2->mp_good[s] && (kf2->nleft == -1 || s < kf2->nleft)) ? 1 : 0;
+    MatchArgs &A = P.A;
+    A.nq = n;
+    A.n_slots = kf2->n;
+    A.nleft = -1;
+    P.out_mp12 = out_mp12;
+    A.nnratio = nnratio;
+    A.check_ori = check_orientation;
+    if (n == 0) return OSG_OK;
+    set_off(A.fdesc, pk.add(kf2->desc, (size_t)kf2->n * 32));
+    set_off(A.slot_angle, pk.add(kf2->angle, sizeof(float) * kf2->n));
+    set_off(A.slot_mp2, pk.add(kf2->mp_id, sizeof(int32_t) * kf2->n));
+    set_off(A.slot_ok, pk.add(P.slot_ok.data(), P.slot_ok.size()));
+    set_off(A.qdesc, pk.add(P.qdesc.data(), P.qdesc.size()));
+    set_off(A.q_angle, pk.add(P.q_angle.data(), sizeof(float) * n));
+    set_off(A.q_cb, pk.add(P.q_cb.data(), sizeof(int32_t) * n));
+    set_off(A.q_ce, pk.add(P.q_ce.data(), sizeof(int32_t) * n));
+    set_off(A.cand_list, pk.add(kf2->fv.feat, sizeof(int32_t) * kf2->fv.node_start[kf2->fv.n_nodes]));
+    return OSG_OK;
+}
+
+// Single and batched entry points share one path: prepare B problems, one launch.
+template <int MODE, typename Prep>
+int run_problems(osg_ctx *ctx, int B, int32_t *nmatches, Prep prep)
+{
+    if (!ctx) return OSG_E_INVALID;
+    OSG_REQUIRE(ctx, B >= 0 && (B == 0 || nmatches), "batch size / nmatches");
+    std::deque<Problem> P;
+    osg_packer pk;
+    for (int b = 0; b < B; b++) {
+        P.emplace_back();
+        const int rc = prep(P.back(), pk, b);
+        if (rc < 0) {
+            if (B > 1) {
+                const std::string msg = ctx->last_error;
+                return osg_set_error(ctx, rc, "problem %d: %s", b, msg.c_str());
+            }
+            return rc;
+        }
+    }
+    return run_batch<MODE>(ctx, P, pk, nmatches);
+}
+
+template <int MODE, typename Prep>
+int run_single(osg_ctx *ctx, Prep prep)
+{
+    int32_t nm = 0;
+    const int rc = run_problems<MODE>(ctx, 1, &nm, [&](Problem &P, osg_packer &pk, int) { return prep(P, pk); });
+    return rc < 0 ? rc : nm;
+}
+
+}  // namespace
+
+extern "C" {
+
+int osg_search_by_projection_mps(osg_ctx *ctx, const osg_frame *F, const osg_mp_queries *Q, float nnratio,
+                                 float th, int far_points, float th_far_points, int32_t *slot_mp,
+                                 const uint8_t *slot_taken)
+{
+    return run_single<MODE_MPS>(ctx, [&](Problem &P, osg_packer &pk) {
+        return prep_mps(ctx, P, pk, F, Q, nnratio, th, far_points, th_far_points, slot_mp, slot_taken);
+    });
+}
+
+int osg_search_by_projection_last(osg_ctx *ctx, const osg_frame *CF, const osg_last_queries *L, float th,
+                                  int mono, int check_orientation, int32_t *slot_mp, const uint8_t *slot_taken)
+{
+    return run_single<MODE_LAST>(ctx, [&](Problem &P, osg_packer &pk) {
+        return prep_last(ctx, P, pk, CF, L, th, mono, check_orientation, slot_mp, slot_taken);
+    });
+}
+
+int osg_search_by_projection_kf(osg_ctx *ctx, const osg_frame *CF, const osg_kf_queries *K, float th, int orb_dist,
+                                int check_orientation, int32_t *slot_mp)
+{
+    return run_single<MODE_KF>(ctx, [&](Problem &P, osg_packer &pk) {
+        return prep_kf(ctx, P, pk, CF, K, th, orb_dist, check_orientation, slot_mp);
+    });
+}
+
+int osg_search_by_bow_kf_f(osg_ctx *ctx, const osg_bow_side *kf, const osg_bow_side *f, float nnratio,
+                           int check_orientation, int32_t *out_mp)
+{
+    return run_single<MODE_BOW_KF_F>(ctx, [&](Problem &P, osg_packer &pk) {
+        return prep_bow_kf_f(ctx, P, pk, kf, f, nnratio, check_orientation, out_mp);
+    });
 }
 
 int osg_search_by_bow_kf_kf(osg_ctx *ctx, const osg_bow_side *kf1, const osg_bow_side *kf2, float nnratio,
                             int check_orientation, int32_t *out_mp12)
 {
-    if (!ctx) return OSG_E_INVALID;
-    OSG_REQUIRE(ctx, kf1 && kf2 && out_mp12, "null argument");
-    OSG_REQUIRE(ctx, kf2->n >= 0 && kf2->n <= MAX_SLOTS && kf1->n >= 0, "sizes");
-    OSG_REQUIRE(ctx, kf1->nleft == -1 || (kf1->nleft >= 0 && kf1->nleft <= kf1->n), "kf1 nleft");
-    OSG_REQUIRE(ctx, kf2->nleft == -1 || (kf2->nleft >= 0 && kf2->nleft <= kf2->n), "kf2 nleft");
-    for (int i = 0; i < kf1->n; i++) out_mp12[i] = -1;
-    std::vector<int32_t> q_feat, q_cb, q_ce;
-    if (bow_queries(kf1, kf2, true, q_feat, q_cb, q_ce) < 0) return osg_set_error(ctx, OSG_E_INVALID, "feature index");
-    const int n = (int)q_feat.size();
-    if (n == 0) return 0;
-    for (int j = 0; j < kf2->fv.node_start[kf2->fv.n_nodes]; j++)
-        OSG_REQUIRE(ctx, kf2->fv.feat[j] >= 0 && kf2->fv.feat[j] < kf2->n, "keyframe feature index");
-    std::vector<uint8_t> qdesc((size_t)n * 32), slot_ok(kf2->n);
-    std::vector<float> q_angle(n);
-    for (int i = 0; i < n; i++) {
-        std::memcpy(&qdesc[(size_t)i * 32], kf1->desc + (size_t)q_feat[i] * 32, 32);
-        q_angle[i] = kf1->angle[q_feat[i]];
-    }
-    // right-camera keypoints of a two-camera KF2 are skipped (ref:src/ORBmatcher.cc:953-955)
-    for (int s = 0; s < kf2->n; s++)
-        slot_ok[s] = (kf2->mp_id[s] >= 0 && kf2->mp_good[s] && (kf2->nleft == -1 || s < kf2->nleft)) ? 1 : 0;
-    MatchArgs A = {};
-    osg_packer pk;
-    A.nq = n;
-    A.n_slots = kf2->n;
-    A.nleft = -1;
-    set_off(A.fdesc, pk.add(kf2->desc, (size_t)kf2->n * 32));
-    set_off(A.slot_angle, pk.add(kf2->angle, sizeof(float) * kf2->n));
-    set_off(A.slot_mp2, pk.add(kf2->mp_id, sizeof(int32_t) * kf2->n));
-    set_off(A.slot_ok, pk.add(slot_ok.data(), slot_ok.size()));
-    set_off(A.qdesc, pk.add(qdesc.data(), qdesc.size()));
-    set_off(A.q_angle, pk.add(q_angle.data(), sizeof(float) * n));
-    set_off(A.q_cb, pk.add(q_cb.data(), sizeof(int32_t) * n));
-    set_off(A.q_ce, pk.add(q_ce.data(), sizeof(int32_t) * n));
-    set_off(A.cand_list, pk.add(kf2->fv.feat, sizeof(int32_t) * kf2->fv.node_start[kf2->fv.n_nodes]));
-    A.nnratio = nnratio;
-    A.check_ori = check_orientation;
-    std::vector<int32_t> out_q(n, -1);
-    const int nm = launch_packed<MODE_BOW_KF_KF>(ctx, A, pk, nullptr, 0, out_q.data());
-    if (nm < 0) return nm;
-    for (int i = 0; i < n; i++) out_mp12[q_feat[i]] = out_q[i];
-    return nm;
+    return run_single<MODE_BOW_KF_KF>(ctx, [&](Problem &P, osg_packer &pk) {
+        return prep_bow_kf_kf(ctx, P, pk, kf1, kf2, nnratio, check_orientation, out_mp12);
+    });
+}
+
+// ---- batched forms: problem b's slot array starts at the sum of the earlier problems' sizes
+
+int osg_search_by_projection_mps_batch(osg_ctx *ctx, const osg_frame *F, const osg_mp_queries *Q, int32_t B,
+                                       float nnratio, float th, int far_points, float th_far_points,
+                                       int32_t *slot_mp, const uint8_t *slot_taken, int32_t *nmatches)
+{
+    size_t off = 0;
+    return run_problems<MODE_MPS>(ctx, B, nmatches, [&](Problem &P, osg_packer &pk, int b) {
+        OSG_REQUIRE(ctx, F && Q && slot_mp && slot_taken, "null argument");
+        const int rc = prep_mps(ctx, P, pk, &F[b], &Q[b], nnratio, th, far_points, th_far_points, slot_mp + off,
+                                slot_taken + off);
+        off += F[b].n;
+        return rc;
+    });
+}
+
+int osg_search_by_projection_last_batch(osg_ctx *ctx, const osg_frame *CF, const osg_last_queries *L, int32_t B,
+                                        float th, int mono, int check_orientation, int32_t *slot_mp,
+                                        const uint8_t *slot_taken, int32_t *nmatches)
+{
+    size_t off = 0;
+    return run_problems<MODE_LAST>(ctx, B, nmatches, [&](Problem &P, osg_packer &pk, int b) {
+        OSG_REQUIRE(ctx, CF && L && slot_mp && slot_taken, "null argument");
+        const int rc = prep_last(ctx, P, pk, &CF[b], &L[b], th, mono, check_orientation, slot_mp + off,
+                                 slot_taken + off);
+        off += CF[b].n;
+        return rc;
+    });
+}
+
+int osg_search_by_projection_kf_batch(osg_ctx *ctx, const osg_frame *CF, const osg_kf_queries *K, int32_t B,
+                                      float th, int orb_dist, int check_orientation, int32_t *slot_mp,
+                                      int32_t *nmatches)
+{
+    size_t off = 0;
+    return run_problems<MODE_KF>(ctx, B, nmatches, [&](Problem &P, osg_packer &pk, int b) {
+        OSG_REQUIRE(ctx, CF && K && slot_mp, "null argument");
+        const int rc = prep_kf(ctx, P, pk, &CF[b], &K[b], th, orb_dist, check_orientation, slot_mp + off);
+        off += CF[b].n;
+        return rc;
+    });
+}
+
+int osg_search_by_bow_kf_f_batch(osg_ctx *ctx, const osg_bow_side *kf, const osg_bow_side *f, int32_t B,
+                                 float nnratio, int check_orientation, int32_t *out_mp, int32_t *nmatches)
+{
+    size_t off = 0;
+    return run_problems<MODE_BOW_KF_F>(ctx, B, nmatches, [&](Problem &P, osg_packer &pk, int b) {
+        OSG_REQUIRE(ctx, kf && f && out_mp, "null argument");
+        const int rc = prep_bow_kf_f(ctx, P, pk, &kf[b], &f[b], nnratio, check_orientation, out_mp + off);
+        off += f[b].n;
+        return rc;
+    });
+}
+
+int osg_search_by_bow_kf_kf_batch(osg_ctx *ctx, const osg_bow_side *kf1, const osg_bow_side *kf2, int32_t B,
+                                  float nnratio, int check_orientation, int32_t *out_mp12, int32_t *nmatches)
+{
+    size_t off = 0;
+    return run_problems<MODE_BOW_KF_KF>(ctx, B, nmatches, [&](Problem &P, osg_packer &pk, int b) {
+        OSG_REQUIRE(ctx, kf1 && kf2 && out_mp12, "null argument");
+        const int rc = prep_bow_kf_kf(ctx, P, pk, &kf1[b], &kf2[b], nnratio, check_orientation, out_mp12 + off);
+        off += kf1[b].n;
+        return rc;
+    });
 }
 
 }  // extern "C"

@@ -32,7 +32,10 @@ struct osg_ctx {
     size_t host_pinned_cap = 0;
     uint32_t *counters = nullptr;
     int num_cus = 256;
+    int lds_per_block = 65536;
     int32_t match_stats[4] = {};  // last matcher call: candidates, Jacobi rounds, serial redo, nmatches
+    double match_kernel_ms = 0;   // last matcher call: k_match launch time (HIP events)
+    hipEvent_t ev[2] = {};        // lazily created timing events
     std::string last_error;
 };
 

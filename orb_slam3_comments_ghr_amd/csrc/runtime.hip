@@ -85,6 +85,7 @@ int osg_ctx_create(int device, osg_ctx **out)
     osg_ctx *ctx = new osg_ctx();
     ctx->device = device;
     ctx->num_cus = prop.multiProcessorCount;
+    ctx->lds_per_block = (int)prop.sharedMemPerBlock;
     if (hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return OSG_E_HIP;
@@ -109,6 +110,8 @@ int osg_ctx_destroy(osg_ctx *ctx)
         if (ctx->buf[i]) (void)hipFree(ctx->buf[i]);
     if (ctx->host_pinned) (void)hipHostFree(ctx->host_pinned);
     if (ctx->counters) (void)hipFree(ctx->counters);
+    for (hipEvent_t e : ctx->ev)
+        if (e) (void)hipEventDestroy(e);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
     return OSG_OK;
@@ -136,6 +139,13 @@ int osg_match_last_stats(osg_ctx *ctx, int32_t *out4)
 {
     if (!ctx || !out4) return OSG_E_INVALID;
     for (int i = 0; i < 4; i++) out4[i] = ctx->match_stats[i];
+    return OSG_OK;
+}
+
+int osg_match_last_kernel_ms(osg_ctx *ctx, double *ms)
+{
+    if (!ctx || !ms) return OSG_E_INVALID;
+    *ms = ctx->match_kernel_ms;
     return OSG_OK;
 }
 

@@ -79,3 +79,77 @@ class ORBmatcher:
         rc = lib.osg_search_by_bow_kf_kf(h, C.byref(a), C.byref(b), self.mfNNratio,
                                          int(self.mbCheckOrientation), out.ctypes.data)
         return self.ctx.check(rc, "SearchByBoW(KeyFrame, KeyFrame)"), out
+
+    # ---- batched forms (no reference counterpart: B independent problems in one launch) -------
+
+    def SearchByProjectionBatch(self, Fs, qs, *args, slot_mps=None, slot_takens=None, **kw):
+        """B independent SearchByProjection calls of one overload in one launch.  ``Fs`` / ``qs`` are
+        sequences of FrameSoA and MPQueries / LastQueries / KFQueries; ``slot_mps`` (updated in place)
+        and ``slot_takens`` per problem.  Returns the per-problem match counts."""
+        lib, h = self.ctx.lib, self.ctx.handle
+        B = len(Fs)
+        assert len(qs) == B
+        kind = type(qs[0])
+        assert all(type(q) is kind for q in qs), "one overload per batch"
+        fa = (_abi.OsgFrame * B)(*[F.struct() for F in Fs])
+        sizes = [F.n for F in Fs]
+        if slot_mps is None:
+            slot_mps = [np.full(n, -1, np.int32) for n in sizes]
+        for s, n in zip(slot_mps, sizes):
+            assert s.dtype == np.int32 and len(s) == n
+        slot = np.concatenate(slot_mps) if B else np.zeros(0, np.int32)
+        nm = np.zeros(B, np.int32)
+        if kind is MPQueries:
+            th = args[0] if len(args) > 0 else kw.get("th", 3.0)
+            far = args[1] if len(args) > 1 else kw.get("bFarPoints", False)
+            thfar = args[2] if len(args) > 2 else kw.get("thFarPoints", 50.0)
+            taken = np.concatenate([np.ascontiguousarray(t, np.uint8) for t in slot_takens]) if slot_takens \
+                else np.zeros(len(slot), np.uint8)
+            qa = (_abi.OsgMpQueries * B)(*[q.struct() for q in qs])
+            rc = lib.osg_search_by_projection_mps_batch(h, C.addressof(fa), C.addressof(qa), B, self.mfNNratio,
+                                                        float(th), int(bool(far)), float(thfar), slot.ctypes.data,
+                                                        taken.ctypes.data, nm.ctypes.data)
+        elif kind is LastQueries:
+            th = args[0] if len(args) > 0 else kw["th"]
+            mono = args[1] if len(args) > 1 else kw["bMono"]
+            taken = np.concatenate([np.ascontiguousarray(t, np.uint8) for t in slot_takens]) if slot_takens \
+                else np.zeros(len(slot), np.uint8)
+            qa = (_abi.OsgLastQueries * B)(*[q.struct() for q in qs])
+            rc = lib.osg_search_by_projection_last_batch(h, C.addressof(fa), C.addressof(qa), B, float(th),
+                                                         int(bool(mono)), int(self.mbCheckOrientation),
+                                                         slot.ctypes.data, taken.ctypes.data, nm.ctypes.data)
+        elif kind is KFQueries:
+            th = args[0] if len(args) > 0 else kw["th"]
+            orb = args[1] if len(args) > 1 else kw["ORBdist"]
+            qa = (_abi.OsgKfQueries * B)(*[q.struct() for q in qs])
+            rc = lib.osg_search_by_projection_kf_batch(h, C.addressof(fa), C.addressof(qa), B, float(th), int(orb),
+                                                       int(self.mbCheckOrientation), slot.ctypes.data,
+                                                       nm.ctypes.data)
+        else:
+            raise TypeError(f"no SearchByProjection overload for {kind.__name__}")
+        self.ctx.check(rc, "SearchByProjection batch")
+        o = 0
+        for s, n in zip(slot_mps, sizes):
+            s[:] = slot[o:o + n]
+            o += n
+        return nm
+
+    def SearchByBoWBatch(self, KFs, others, kf2: bool = False):
+        """B independent SearchByBoW calls in one launch; returns (nmatches[B], list of outputs)."""
+        lib, h = self.ctx.lib, self.ctx.handle
+        B = len(KFs)
+        assert len(others) == B
+        a = (_abi.OsgBowSide * B)(*[k.struct() for k in KFs])
+        b = (_abi.OsgBowSide * B)(*[o.struct() for o in others])
+        sizes = [k.n for k in KFs] if kf2 else [o.n for o in others]
+        out = np.full(sum(sizes), -1, np.int32)
+        nm = np.zeros(B, np.int32)
+        fn = lib.osg_search_by_bow_kf_kf_batch if kf2 else lib.osg_search_by_bow_kf_f_batch
+        rc = fn(h, C.addressof(a), C.addressof(b), B, self.mfNNratio, int(self.mbCheckOrientation),
+                out.ctypes.data, nm.ctypes.data)
+        self.ctx.check(rc, "SearchByBoW batch")
+        outs, o = [], 0
+        for n in sizes:
+            outs.append(out[o:o + n].copy())
+            o += n
+        return nm, outs

@@ -188,3 +188,51 @@ def test_search_by_bow_two_cam(ctx, oracle, seed, nn):
         ref = oc.bow_kf_kf(oracle, K1, K2, nn, ori)
         n, out = ORBmatcher(ctx, nn, ori).SearchByBoW(K1, K2, kf2=True)
         assert_same(f"bow kf-kf two-cam ori={ori}", n, out, *ref)
+
+
+# ---- batched forms: B problems in one launch equal B single calls (and the oracle)
+
+def test_batch_projection_all_overloads(ctx, oracle):
+    rng = np.random.default_rng(9000)
+    B = 24
+    m = ORBmatcher(ctx, 0.8, True)
+    # a5, mixing one-camera and two-camera frames, and an empty query set
+    Fs = [fr.synth_frame(rng, n=900, stereo=(b % 2 == 0)) if b % 3 else two_cam(rng, 500, 450) for b in range(B)]
+    Qs = [fr.synth_mp_queries_two_cam(rng, F, m=1200) if F.nleft != -1 else fr.synth_mp_queries(rng, F, m=1500)
+          for F in Fs]
+    Qs[5] = fr.synth_mp_queries(rng, Fs[5], m=0)
+    slots = [fr.synth_slots(rng, F.n) for F in Fs]
+    s_in = [s.copy() for s, _ in slots]
+    nm = m.SearchByProjectionBatch(Fs, Qs, 3.0, False, 20.0, slot_mps=s_in, slot_takens=[t for _, t in slots])
+    for b in range(B):
+        ref = oc.mps(oracle, Fs[b], Qs[b], 0.8, 3.0, False, 20.0, slots[b][0], slots[b][1])
+        assert_same(f"mps batch [{b}]", int(nm[b]), s_in[b], *ref)
+    # a6
+    Ls = [fr.synth_last_queries_two_cam(rng, F, n_last=600) if F.nleft != -1 else fr.synth_last_queries(rng, F, 700)
+          for F in Fs]
+    s_in = [s.copy() for s, _ in slots]
+    nm = m.SearchByProjectionBatch(Fs, Ls, 7.0, False, slot_mps=s_in, slot_takens=[t for _, t in slots])
+    for b in range(B):
+        ref = oc.last(oracle, Fs[b], Ls[b], 7.0, False, True, slots[b][0], slots[b][1])
+        assert_same(f"last batch [{b}]", int(nm[b]), s_in[b], *ref)
+    # a7
+    Ks = [fr.synth_kf_queries(rng, F, n_kf=500) for F in Fs]
+    s_in = [s.copy() for s, _ in slots]
+    nm = m.SearchByProjectionBatch(Fs, Ks, 10.0, 100, slot_mps=s_in)
+    for b in range(B):
+        ref = oc.kf(oracle, Fs[b], Ks[b], 10.0, 100, True, slots[b][0])
+        assert_same(f"kf batch [{b}]", int(nm[b]), s_in[b], *ref)
+
+
+@pytest.mark.parametrize("kf2", [False, True])
+def test_batch_bow(ctx, oracle, kf2):
+    rng = np.random.default_rng(9100 + kf2)
+    B = 40
+    pairs = [fr.synth_bow_pair(rng, n_kf=800 + 10 * b, n_f=900, n_nodes=60, f_is_kf=kf2,
+                               nleft_kf=(400 if b % 4 == 0 else -1), nleft_f=(450 if b % 4 == 0 else -1))
+             for b in range(B)]
+    m = ORBmatcher(ctx, 0.75, True)
+    nm, outs = m.SearchByBoWBatch([p[0] for p in pairs], [p[1] for p in pairs], kf2=kf2)
+    for b, (A, Bs) in enumerate(pairs):
+        ref = (oc.bow_kf_kf if kf2 else oc.bow_kf_f)(oracle, A, Bs, 0.75, True)
+        assert_same(f"bow batch [{b}]", int(nm[b]), outs[b], *ref)
