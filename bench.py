@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--no-stream", action="store_true")
     ap.add_argument("--no-ba", action="store_true")
     ap.add_argument("--ba-reps", type=int, default=20)
+    ap.add_argument("--no-frames", action="store_true", help="skip the frame-batched C3 / C5 workloads")
+    ap.add_argument("--frames", type=int, default=1024, help="frames per launch (C3 / C5 batches)")
+    ap.add_argument("--frame-reps", type=int, default=5)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-launch HBM traffic from the rocprofv3 PMC passes (tools/gpu_profile.sh)")
     return ap.parse_args()
@@ -204,6 +207,11 @@ def main():
         out["cpu_baseline"] = cpu_baseline(q_np, t_np, args.cpu_seconds)
         out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
 
+    # ---- frame-batched C3 / C5: matching + PoseOptimization, B frames per launch ------------
+    if not args.no_frames:
+        out["frames_c3"] = bench_c3(ctx, rank, world, dist, dev, args)
+        out["frames_c5"] = bench_c5(ctx, rank, world, dist, dev, args)
+
     # ---- LocalBA iters/s on C4 (50 KF x 10k points), the second half of the metric ----------
     if not args.no_ba:
         out["local_ba"] = bench_lba(ctx, rank, world, dist, dev, args)
@@ -277,6 +285,129 @@ def bench_lba(ctx, rank, world, dist, dev, args):
                                "sample": f"{n} x C4 LBA (oracle_local_bundle_adjustment, gcc -O3, 1 thread, dense LDL^T) in {cel:.1f} s"}
         res["speedup_vs_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
     return res
+
+
+_ORACLE = []
+
+
+def _oracle():
+    """The CPU oracle (test infrastructure), loaded only by the cpu_baseline legs."""
+    if not _ORACLE:
+        from orb_slam3_comments_ghr_amd import _abi
+        from tests import oracle_calls
+        _ORACLE.append((_abi.declare_oracle(ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))), oracle_calls))
+    return _ORACLE[0]
+
+
+def _frame_batches(ctx, rank, world, dist, dev, args, steps, cpu_step, label, workload, n_pool):
+    """Time `steps` (a list of callables, each one batched launch over B frames that leaves its
+    kernel time in ctx.last_kernel_ms()) over args.frame_reps repetitions.  value = frames / summed
+    kernel time (inputs resident in HBM: the device time of the launches); the wall rate includes
+    host packing and PCIe.  cpu_step(i) runs frame i of the pool through the oracle."""
+    import torch
+    for f in steps:
+        f()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    k_ms = 0.0
+    per = [0.0] * len(steps)
+    t0 = time.perf_counter()
+    for _ in range(args.frame_reps):
+        for i, f in enumerate(steps):
+            f()
+            ms = ctx.last_kernel_ms()
+            per[i] += ms
+            k_ms += ms
+    wall = time.perf_counter() - t0
+    frames = args.frames * args.frame_reps
+    k_s, tot = job_totals(k_ms / 1e3, frames, world, dist if world > 1 else None, dev)
+    w_s, _ = job_totals(wall, frames, world, dist if world > 1 else None, dev)
+    res = {"metric": "frames/s", "value": round(tot / k_s, 1), "unit": "frames/s",
+           "workload": workload, "frames_per_launch": args.frames, "distinct_frames": n_pool,
+           "kernel_us_per_frame": {lab: round(v * 1e3 / frames, 3) for lab, v in zip(label, per)},
+           "wall_frames_per_s_incl_host_and_pcie": round(tot / w_s, 1), "n_gpus": world,
+           "scaling": "weak", "parallelism": f"replicas x{world} (independent frame batches per GPU)"}
+    if rank == 0 and world == 1 and not args.no_cpu:
+        n = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < args.cpu_seconds / 4 or n == 0:
+            cpu_step(n % n_pool)
+            n += 1
+        cel = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": round(n / cel, 1), "unit": "frames/s", "cores": 1, "kind": "port",
+                               "sample": f"{n} frames through the oracle (gcc -O3, 1 thread) in {cel:.1f} s"}
+        res["speedup_vs_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
+    return res
+
+
+def bench_c3(ctx, rank, world, dist, dev, args):
+    """C3: SearchByBoW(KF, F) + PoseOptimization per frame, B frames per launch.
+    The pose problem of a frame has as many edges as its BoW matches (60 % stereo, 10 % outliers)."""
+    from orb_slam3_comments_ghr_amd import frames as fr, optimizer as op
+    from orb_slam3_comments_ghr_amd.matcher import ORBmatcher
+    n_pool = 32
+    rng = np.random.default_rng(0x0B5EED03 + rank)
+    pairs = [fr.synth_bow_pair(rng, n_kf=1200, n_f=1200, n_nodes=100) for _ in range(n_pool)]
+    m = ORBmatcher(ctx, 0.7, True)
+    nm, _ = m.SearchByBoWBatch([p[0] for p in pairs], [p[1] for p in pairs])
+    probs = [op.synth_pose_problem(rng, n_edges=int(max(nm[i], 10))) for i in range(n_pool)]
+    B = args.frames
+    KB = [pairs[i % n_pool][0] for i in range(B)]
+    FB = [pairs[i % n_pool][1] for i in range(B)]
+    PB = [probs[i % n_pool] for i in range(B)]
+    opt = op.Optimizer(ctx)
+
+    def cpu(i):  # the cpu_baseline leg: the oracle restatement, 1 thread
+        oracle, oc = _oracle()
+        oc.bow_kf_f(oracle, pairs[i][0], pairs[i][1], 0.7, True)
+        op.oracle_pose(oracle, [probs[i]])
+
+    return _frame_batches(ctx, rank, world, dist, dev, args,
+                          [lambda: m.SearchByBoWBatch(KB, FB), lambda: opt.PoseOptimization(PB)], cpu,
+                          ["SearchByBoW", "PoseOptimization"],
+                          f"C3: SearchByBoW(KF,F) 1200x1200 (100 nodes) + PoseOptimization "
+                          f"(mean {int(np.mean(nm))} edges, 60 % stereo), {B} frames per launch", n_pool)
+
+
+def bench_c5(ctx, rank, world, dist, dev, args):
+    """C5: TUM-VI-like two-camera KB8 fisheye rig (512 x 512, 1000 keypoints per
+    camera): SearchByProjection(F, LastF) + SearchByProjection(F, local map) + PoseOptimization
+    (40 % right-camera edges) per frame, B frames per launch."""
+    from orb_slam3_comments_ghr_amd import frames as fr, optimizer as op
+    from orb_slam3_comments_ghr_amd.matcher import ORBmatcher
+    n_pool = 32
+    rng = np.random.default_rng(0x0B5EED10 + rank)
+    F = [fr.synth_frame_two_cam(rng, n_left=1000, n_right=1000, stereo_frac=0.5, width=512, height=512)
+         for _ in range(n_pool)]
+    L = [fr.synth_last_queries_two_cam(rng, f, n_last=2000) for f in F]
+    Q = [fr.synth_mp_queries_two_cam(rng, f, m=1500) for f in F]
+    S = [fr.synth_slots(rng, f.n, frac_assigned=0.05) for f in F]
+    probs = [op.synth_pose_problem(rng, n_edges=600, cam=op.kb8_camera(), body_frac=0.4) for _ in range(n_pool)]
+    B = args.frames
+    idx = [i % n_pool for i in range(B)]
+    FB, LB, QB, PB = [F[i] for i in idx], [L[i] for i in idx], [Q[i] for i in idx], [probs[i] for i in idx]
+    TB = [S[i][1] for i in idx]
+    m = ORBmatcher(ctx, 0.9, True)
+    m_local = ORBmatcher(ctx, 0.9, True)
+    opt = op.Optimizer(ctx)
+
+    def cpu(i):  # the cpu_baseline leg: the oracle restatement, 1 thread
+        oracle, oc = _oracle()
+        oc.last(oracle, F[i], L[i], 7.0, False, True, S[i][0], S[i][1])
+        oc.mps(oracle, F[i], Q[i], 0.9, 3.0, False, 20.0, S[i][0], S[i][1])
+        op.oracle_pose(oracle, [probs[i]])
+
+    return _frame_batches(ctx, rank, world, dist, dev, args,
+                          [lambda: m.SearchByProjectionBatch(FB, LB, 7.0, False, slot_mps=[S[i][0].copy() for i in idx],
+                                                             slot_takens=TB),
+                           lambda: m_local.SearchByProjectionBatch(FB, QB, 3.0, False, 20.0,
+                                                                   slot_mps=[S[i][0].copy() for i in idx],
+                                                                   slot_takens=TB),
+                           lambda: opt.PoseOptimization(PB)], cpu,
+                          ["SearchByProjection(F,LastF)", "SearchByProjection(F,localMPs)", "PoseOptimization"],
+                          f"C5: two-camera KB8 512x512, 2x1000 keypoints; LastF 2000 + local map 1500 queries; "
+                          f"PoseOptimization 600 edges (40 % right camera); {B} frames per launch", n_pool)
 
 
 def cpu_baseline(q_np, t_np, seconds):

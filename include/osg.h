@@ -249,8 +249,9 @@ int osg_search_by_bow_kf_kf_batch(osg_ctx *ctx, const osg_bow_side *kf1, const o
  * stereo-partner write by a MapPoint without observations unblocked a slot), out[3] nmatches.
  * No reference counterpart. */
 int osg_match_last_stats(osg_ctx *ctx, int32_t *out4);
-/* Device time of the last search call's matching kernel (HIP events around the launch), ms. */
-int osg_match_last_kernel_ms(osg_ctx *ctx, double *ms);
+/* Device time (HIP events around the launch, ms) of the last matching or pose-optimization kernel
+ * this context ran: the search calls and osg_pose_optimization[_batch]. */
+int osg_ctx_last_kernel_ms(osg_ctx *ctx, double *ms);
 
 #ifdef __cplusplus
 }

@@ -119,10 +119,14 @@ class Context:
         """Diagnostics of the last search call: candidates, Jacobi rounds, serial redo, nmatches."""
         out = np.zeros(4, np.int32)
         self.check(self.lib.osg_match_last_stats(self.handle, _ptr(out)), "osg_match_last_stats")
-        ms = np.zeros(1, np.float64)
-        self.check(self.lib.osg_match_last_kernel_ms(self.handle, _ptr(ms)), "osg_match_last_kernel_ms")
         return dict(candidates=int(out[0]), rounds=int(out[1]), serial=bool(out[2]), nmatches=int(out[3]),
-                    kernel_ms=float(ms[0]))
+                    kernel_ms=self.last_kernel_ms())
+
+    def last_kernel_ms(self) -> float:
+        """Device time of the last matching / pose-optimization kernel (HIP events), ms."""
+        ms = np.zeros(1, np.float64)
+        self.check(self.lib.osg_ctx_last_kernel_ms(self.handle, _ptr(ms)), "osg_ctx_last_kernel_ms")
+        return float(ms[0])
 
     def descriptor_distance_pairs(self, a: np.ndarray, b: np.ndarray) -> np.ndarray:
         a = np.ascontiguousarray(a, dtype=np.uint8).reshape(-1, 32)

@@ -1071,11 +1071,9 @@ int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_
         // arrays written by the problems that fitted the first time
         OSG_HIP_CHECK(ctx, hipMemcpyAsync(dev_io, pin_io, io_in_bytes, hipMemcpyHostToDevice, ctx->stream));
         OSG_HIP_CHECK(ctx, hipMemcpyAsync(dev_args, pin_args, args_bytes, hipMemcpyHostToDevice, ctx->stream));
-        if (!ctx->ev[0]) {
-            OSG_HIP_CHECK(ctx, hipEventCreate(&ctx->ev[0]));
-            OSG_HIP_CHECK(ctx, hipEventCreate(&ctx->ev[1]));
-        }
-        OSG_HIP_CHECK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
+        hipEvent_t *ev = osg_ctx_events(ctx);
+        if (!ev) return osg_set_error(ctx, OSG_E_HIP, "event create failed");
+        OSG_HIP_CHECK(ctx, hipEventRecord(ev[0], ctx->stream));
         if (stage == 2)
             hipLaunchKernelGGL((k_match<MODE, 2>), dim3(B), dim3(MT), lds, ctx->stream, dev_args);
         else if (stage == 1)
@@ -1083,7 +1081,7 @@ int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_
         else
             hipLaunchKernelGGL((k_match<MODE, 0>), dim3(B), dim3(MT), lds, ctx->stream, dev_args);
         OSG_HIP_CHECK(ctx, hipGetLastError());
-        OSG_HIP_CHECK(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
+        OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
         OSG_HIP_CHECK(ctx, hipMemcpyAsync(st.data(), dev_io, status_bytes, hipMemcpyDeviceToHost, ctx->stream));
         OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
         bool overflow = false;
@@ -1120,7 +1118,7 @@ int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_
     }
     float ms = 0.f;
     OSG_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]));
-    ctx->match_kernel_ms = ms;
+    ctx->last_kernel_ms = ms;
     static const bool prof = getenv("OSG_MATCH_PROFILE") != nullptr;
     if (prof)
         fprintf(stderr, "[osg match] mode %d B %d kernel %.3f ms | problem 0: nq %d cands %d rounds %d serial %d | "

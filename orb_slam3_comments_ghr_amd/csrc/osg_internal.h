@@ -34,12 +34,14 @@ struct osg_ctx {
     int num_cus = 256;
     int lds_per_block = 65536;
     int32_t match_stats[4] = {};  // last matcher call: candidates, Jacobi rounds, serial redo, nmatches
-    double match_kernel_ms = 0;   // last matcher call: k_match launch time (HIP events)
-    hipEvent_t ev[2] = {};        // lazily created timing events
+    double last_kernel_ms = 0;    // last k_match / k_pose_opt launch time (HIP events)
+    hipEvent_t ev[2] = {};        // timing events (osg_ctx_events)
     std::string last_error;
 };
 
 int osg_set_error(osg_ctx *ctx, int code, const char *fmt, ...);
+// the context's two timing events, created on first use (nullptr on failure)
+hipEvent_t *osg_ctx_events(osg_ctx *ctx);
 // device buffer of at least `bytes` for `slot` (grows, never shrinks)
 void *osg_scratch(osg_ctx *ctx, int slot, size_t bytes);
 void *osg_pinned(osg_ctx *ctx, size_t bytes);

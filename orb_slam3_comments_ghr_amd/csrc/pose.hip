@@ -397,15 +397,22 @@ int osg_pose_optimization_batch(osg_ctx *ctx, const osg_pose_problem *p, int32_t
     OSG_ALLOC(ctx, din, SLOT_BA0, in_bytes);
     OSG_ALLOC(ctx, dio, SLOT_BA1, io_bytes);
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(din, pin, in_bytes, hipMemcpyHostToDevice, ctx->stream));
+    hipEvent_t *ev = osg_ctx_events(ctx);
+    if (!ev) return osg_set_error(ctx, OSG_E_HIP, "event create failed");
+    OSG_HIP_CHECK(ctx, hipEventRecord(ev[0], ctx->stream));
     hipLaunchKernelGGL(k_pose_opt, dim3(nb), dim3(PT), 0, ctx->stream, (const PoseProbDev *)(din + o_probs),
                        (const int8_t *)(din + o_kind), (const double *)(din + o_xw), (const double *)(din + o_obs),
                        (const float *)(din + o_isig), (double *)(dio + o_err), (uint8_t *)(dio + o_outl),
                        (PoseOut *)(dio + o_res));
     OSG_HIP_CHECK(ctx, hipGetLastError());
+    OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
     char *pout = pin + in_bytes;
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(pout + o_outl, dio + o_outl, io_bytes - o_outl, hipMemcpyDeviceToHost,
                                       ctx->stream));
     OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    float kms = 0.f;
+    OSG_HIP_CHECK(ctx, hipEventElapsedTime(&kms, ev[0], ev[1]));
+    ctx->last_kernel_ms = kms;
     const PoseOut *res = (const PoseOut *)(pout + o_res);
     int sum = 0;
     for (int b = 0; b < nb; b++) {

@@ -37,6 +37,14 @@ void *osg_scratch(osg_ctx *ctx, int slot, size_t bytes)
     return p;
 }
 
+hipEvent_t *osg_ctx_events(osg_ctx *ctx)
+{
+    if (!ctx->ev[0]) {
+        if (hipEventCreate(&ctx->ev[0]) != hipSuccess || hipEventCreate(&ctx->ev[1]) != hipSuccess) return nullptr;
+    }
+    return ctx->ev;
+}
+
 void *osg_pinned(osg_ctx *ctx, size_t bytes)
 {
     if (ctx->host_pinned_cap >= bytes) return ctx->host_pinned;
@@ -142,10 +150,10 @@ int osg_match_last_stats(osg_ctx *ctx, int32_t *out4)
     return OSG_OK;
 }
 
-int osg_match_last_kernel_ms(osg_ctx *ctx, double *ms)
+int osg_ctx_last_kernel_ms(osg_ctx *ctx, double *ms)
 {
     if (!ctx || !ms) return OSG_E_INVALID;
-    *ms = ctx->match_kernel_ms;
+    *ms = ctx->last_kernel_ms;
     return OSG_OK;
 }
 

@@ -275,11 +275,11 @@ def _flip(rng, rows, p):
     return np.packbits(bits ^ (rng.random(bits.shape) < p).astype(np.uint8), axis=1)
 
 
-def synth_frame(rng, n=1200, stereo=True, n_levels=8):
-    """Keypoints uniform in 752x480, octave ~ geometric(1/1.2) truncated to 8 levels,
-    angle U[0,360), 60 % with a stereo u_R (bf = 47.9)."""
-    x = rng.uniform(0, EUROC_W, n).astype(np.float32)
-    y = rng.uniform(0, EUROC_H, n).astype(np.float32)
+def synth_frame(rng, n=1200, stereo=True, n_levels=8, width=EUROC_W, height=EUROC_H):
+    """Keypoints uniform in the image (EuRoC 752x480 by default), octave ~ geometric(1/1.2)
+    truncated to 8 levels, angle U[0,360), 60 % with a stereo u_R (bf = 47.9)."""
+    x = rng.uniform(0, width, n).astype(np.float32)
+    y = rng.uniform(0, height, n).astype(np.float32)
     p = np.array([1.2 ** -i for i in range(n_levels)])
     oct_ = rng.choice(n_levels, size=n, p=p / p.sum()).astype(np.int32)
     ang = rng.uniform(0, 360, n).astype(np.float32)
@@ -289,7 +289,7 @@ def synth_frame(rng, n=1200, stereo=True, n_levels=8):
         depth = rng.uniform(1, 10, n)
         ur = np.where(rng.random(n) < 0.6, x - EUROC_BF / depth, -1.0).astype(np.float32)
     return FrameSoA(desc=desc, kp_x=x, kp_y=y, kp_angle=ang, kp_octave=oct_, u_right=ur,
-                    scale=scale_factors(n_levels))
+                    scale=scale_factors(n_levels), max_x=float(width), max_y=float(height))
 
 
 def synth_mp_queries(rng, F: FrameSoA, m=3000, noise_px=3.0, match_frac=0.6):
@@ -297,8 +297,8 @@ def synth_mp_queries(rng, F: FrameSoA, m=3000, noise_px=3.0, match_frac=0.6):
     n = F.n
     tgt = rng.integers(0, n, m)
     is_match = rng.random(m) < match_frac
-    px = np.where(is_match, F.kp_x[tgt] + rng.normal(0, noise_px, m), rng.uniform(0, EUROC_W, m))
-    py = np.where(is_match, F.kp_y[tgt] + rng.normal(0, noise_px, m), rng.uniform(0, EUROC_H, m))
+    px = np.where(is_match, F.kp_x[tgt] + rng.normal(0, noise_px, m), rng.uniform(0, F.max_x, m))
+    py = np.where(is_match, F.kp_y[tgt] + rng.normal(0, noise_px, m), rng.uniform(0, F.max_y, m))
     desc = rng.integers(0, 256, (m, 32), dtype=np.uint8)
     desc[is_match] = _flip(rng, F.desc[tgt[is_match]], 0.06)
     lvl = np.clip(F.kp_octave[tgt] + rng.integers(-1, 2, m), 0, len(F.scale) - 1)
@@ -322,8 +322,8 @@ def synth_last_queries(rng, F: FrameSoA, n_last=1000, noise_px=2.0, match_frac=0
     n = F.n
     tgt = rng.integers(0, n, n_last)
     is_match = rng.random(n_last) < match_frac
-    u = np.where(is_match, F.kp_x[tgt] + rng.normal(0, noise_px, n_last), rng.uniform(-20, EUROC_W + 20, n_last))
-    v = np.where(is_match, F.kp_y[tgt] + rng.normal(0, noise_px, n_last), rng.uniform(-20, EUROC_H + 20, n_last))
+    u = np.where(is_match, F.kp_x[tgt] + rng.normal(0, noise_px, n_last), rng.uniform(-20, F.max_x + 20, n_last))
+    v = np.where(is_match, F.kp_y[tgt] + rng.normal(0, noise_px, n_last), rng.uniform(-20, F.max_y + 20, n_last))
     desc = rng.integers(0, 256, (n_last, 32), dtype=np.uint8)
     desc[is_match] = _flip(rng, F.desc[tgt[is_match]], 0.06)
     depth = rng.uniform(1, 20, n_last)
@@ -416,14 +416,14 @@ def synth_bow_pair(rng, n_kf=1200, n_f=1200, n_nodes=100, mp_frac=0.7, copy_frac
 
 # ---------------------------------------------------------------- two-camera rig generators
 
-def synth_frame_two_cam(rng, n_left=600, n_right=600, stereo_frac=0.5, n_levels=8):
+def synth_frame_two_cam(rng, n_left=600, n_right=600, stereo_frac=0.5, n_levels=8, width=EUROC_W, height=EUROC_H):
     """A two-camera Frame (ref:src/Frame.cc:1485-1536): Nleft = n_left, N = n_left + n_right,
     descriptors vconcat(left, right).  ``stereo_frac`` of the right keypoints are stereo partners
     of a left keypoint (ComputeStereoFishEyeMatches): shifted by a disparity, same octave, a
     noisy copy of the left descriptor; mvLeftToRightMatch / mvRightToLeftMatch record the pairs."""
-    L = synth_frame(rng, n=n_left, stereo=False, n_levels=n_levels)
-    xr = rng.uniform(0, EUROC_W, n_right).astype(np.float32)
-    yr = rng.uniform(0, EUROC_H, n_right).astype(np.float32)
+    L = synth_frame(rng, n=n_left, stereo=False, n_levels=n_levels, width=width, height=height)
+    xr = rng.uniform(0, width, n_right).astype(np.float32)
+    yr = rng.uniform(0, height, n_right).astype(np.float32)
     p = np.array([1.2 ** -i for i in range(n_levels)])
     octr = rng.choice(n_levels, size=n_right, p=p / p.sum()).astype(np.int32)
     angr = rng.uniform(0, 360, n_right).astype(np.float32)
@@ -432,8 +432,8 @@ def synth_frame_two_cam(rng, n_left=600, n_right=600, stereo_frac=0.5, n_levels=
     li = rng.choice(n_left, size=n_pair, replace=False)
     ri = rng.choice(n_right, size=n_pair, replace=False)
     disp = rng.uniform(2, 60, n_pair)
-    xr[ri] = np.clip(L.kp_x[li] - disp, 0, EUROC_W - 1)
-    yr[ri] = np.clip(L.kp_y[li] + rng.normal(0, 0.5, n_pair), 0, EUROC_H - 1)
+    xr[ri] = np.clip(L.kp_x[li] - disp, 0, width - 1)
+    yr[ri] = np.clip(L.kp_y[li] + rng.normal(0, 0.5, n_pair), 0, height - 1)
     octr[ri] = L.kp_octave[li]
     angr[ri] = np.mod(L.kp_angle[li] + rng.normal(0, 2, n_pair), 360)
     descr[ri] = _flip(rng, L.desc[li], 0.03)
@@ -444,7 +444,8 @@ def synth_frame_two_cam(rng, n_left=600, n_right=600, stereo_frac=0.5, n_levels=
     return FrameSoA(desc=np.concatenate([L.desc, descr]), kp_x=np.concatenate([L.kp_x, xr]),
                     kp_y=np.concatenate([L.kp_y, yr]), kp_angle=np.concatenate([L.kp_angle, angr]),
                     kp_octave=np.concatenate([L.kp_octave, octr]), u_right=None, nleft=n_left,
-                    left_to_right=l2r, right_to_left=r2l, scale=scale_factors(n_levels))
+                    left_to_right=l2r, right_to_left=r2l, scale=scale_factors(n_levels),
+                    max_x=float(width), max_y=float(height))
 
 
 def synth_mp_queries_two_cam(rng, F: FrameSoA, m=1500, noise_px=2.5, match_frac=0.7, right_only_frac=0.2):
@@ -460,10 +461,10 @@ def synth_mp_queries_two_cam(rng, F: FrameSoA, m=1500, noise_px=2.5, match_frac=
     tr = np.where(right_only, rng.integers(0, nr, m), F.left_to_right[tl])
     has_r = tr >= 0
     trc = np.maximum(tr, 0)
-    px = np.where(is_match & ~right_only, F.kp_x[tl] + rng.normal(0, noise_px, m), rng.uniform(0, EUROC_W, m))
-    py = np.where(is_match & ~right_only, F.kp_y[tl] + rng.normal(0, noise_px, m), rng.uniform(0, EUROC_H, m))
-    pxr = np.where(is_match & has_r, F.kp_x[nl + trc] + rng.normal(0, noise_px, m), rng.uniform(0, EUROC_W, m))
-    pyr = np.where(is_match & has_r, F.kp_y[nl + trc] + rng.normal(0, noise_px, m), rng.uniform(0, EUROC_H, m))
+    px = np.where(is_match & ~right_only, F.kp_x[tl] + rng.normal(0, noise_px, m), rng.uniform(0, F.max_x, m))
+    py = np.where(is_match & ~right_only, F.kp_y[tl] + rng.normal(0, noise_px, m), rng.uniform(0, F.max_y, m))
+    pxr = np.where(is_match & has_r, F.kp_x[nl + trc] + rng.normal(0, noise_px, m), rng.uniform(0, F.max_x, m))
+    pyr = np.where(is_match & has_r, F.kp_y[nl + trc] + rng.normal(0, noise_px, m), rng.uniform(0, F.max_y, m))
     desc = rng.integers(0, 256, (m, 32), dtype=np.uint8)
     lm = is_match & ~right_only
     desc[lm] = _flip(rng, F.desc[tl[lm]], 0.06)
@@ -486,7 +487,7 @@ def synth_last_queries_two_cam(rng, F: FrameSoA, n_last=800, noise_px=2.0, match
     nl = F.nleft
     L = synth_last_queries(rng, FrameSoA(desc=F.desc[:nl], kp_x=F.kp_x[:nl], kp_y=F.kp_y[:nl],
                                          kp_angle=F.kp_angle[:nl], kp_octave=F.kp_octave[:nl],
-                                         scale=F.scale),
+                                         scale=F.scale, max_x=F.max_x, max_y=F.max_y),
                            n_last=n_last, noise_px=noise_px, match_frac=match_frac, tlc_z=tlc_z)
     # nearest left keypoint of each projection stands in for the target
     tl = np.argmin(np.abs(L.u[:, None] - F.kp_x[None, :nl]) + np.abs(L.v[:, None] - F.kp_y[None, :nl]), axis=1)
@@ -494,7 +495,7 @@ def synth_last_queries_two_cam(rng, F: FrameSoA, n_last=800, noise_px=2.0, match
     ok = tr >= 0
     trc = np.maximum(tr, 0)
     L.u_r = np.where(ok, F.kp_x[nl + trc] + rng.normal(0, noise_px, n_last),
-                     rng.uniform(-20, EUROC_W + 20, n_last)).astype(np.float32)
+                     rng.uniform(-20, F.max_x + 20, n_last)).astype(np.float32)
     L.v_r = np.where(ok, F.kp_y[nl + trc] + rng.normal(0, noise_px, n_last),
-                     rng.uniform(-20, EUROC_H + 20, n_last)).astype(np.float32)
+                     rng.uniform(-20, F.max_y + 20, n_last)).astype(np.float32)
     return L

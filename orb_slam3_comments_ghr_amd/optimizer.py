@@ -278,10 +278,25 @@ def oracle_pose(oracle, problems):
 
 
 # ----------------------------------------------------------------------------- generators
-def synth_pose_problem(rng, n_edges=400, stereo_frac=0.6, outlier_frac=0.1, n_levels=8, cam=None):
+def kb8_project(cam, Xc):
+    """KannalaBrandt8::project (ref:src/CameraModels/KannalaBrandt8.cpp:76-99) in float64."""
+    k = [float(cam.p[i]) for i in range(8)]
+    th = np.arctan2(np.hypot(Xc[:, 0], Xc[:, 1]), Xc[:, 2])
+    ps = np.arctan2(Xc[:, 1], Xc[:, 0])
+    r = th + k[4] * th ** 3 + k[5] * th ** 5 + k[6] * th ** 7 + k[7] * th ** 9
+    return k[0] * r * np.cos(ps) + k[2], k[1] * r * np.sin(ps) + k[3]
+
+
+# TUM-VI-like right-from-left extrinsic of the fisheye pair: 10.1 cm baseline, ~0.5 deg rotation
+TUMVI_TRL = [0.0021, -0.0023, 0.0011, 0.99999, -0.101, 0.0005, -0.0004]
+
+
+def synth_pose_problem(rng, n_edges=400, stereo_frac=0.6, outlier_frac=0.1, n_levels=8, cam=None, body_frac=0.0):
     """C3 PoseOptimization: Xw depth U[1,10] m in front of the camera, pose perturbed by
     1 cm / 0.5 deg, pixel noise 1 px * 1.2^octave, 10 % outliers (+20..50 px), stereo u_R for
-    60 % of the edges (bf = 47.9)."""
+    60 % of the edges (bf = 47.9).  With a KB8 camera and ``body_frac`` > 0 (C5, two-camera rig),
+    that fraction of the edges are right-camera observations (EdgeSE3ProjectXYZOnlyPoseToBody, the
+    second camera ``kb8_camera(trl=TUMVI_TRL)``)."""
     cam = cam or pinhole_camera()
     Rcw = small_rotation(rng, 20.0)
     tcw = rng.normal(0, 1.0, 3)
@@ -320,7 +335,24 @@ def synth_pose_problem(rng, n_edges=400, stereo_frac=0.6, outlier_frac=0.1, n_le
     R0 = small_rotation(rng, 0.5) @ Rcw
     t0 = tcw + rng.normal(0, 0.01, 3)
     isig = inv_level_sigma2(n_levels)[octv]
-    return PoseProblem(pose7(R0, t0), kind, Xw, obs, isig, cam=cam, cam2=cam)
+    cam2 = cam
+    if cam.type == _abi.CAM_KB8 and body_frac > 0:
+        cam2 = kb8_camera(trl=TUMVI_TRL)
+        q = np.array(TUMVI_TRL[:4]) / np.linalg.norm(TUMVI_TRL[:4])
+        from scipy.spatial.transform import Rotation
+        Rrl = Rotation.from_quat(q).as_matrix()
+        Xr = Xc @ Rrl.T + np.array(TUMVI_TRL[4:])
+        body = (rng.random(n_edges) < body_frac) & (Xr[:, 2] > 0.1)
+        ur, vr = kb8_project(cam2, Xr[body])
+        sb = sig[body]
+        obs[body, 0] = ur + rng.normal(0, 1, body.sum()) * sb
+        obs[body, 1] = vr + rng.normal(0, 1, body.sum()) * sb
+        obs[body, 2] = 0.0
+        ob = body & out
+        obs[ob, 0] += rng.uniform(20, 50, ob.sum()) * rng.choice([-1, 1], ob.sum())
+        obs = obs.astype(np.float32).astype(np.float64)
+        kind = np.where(body, _abi.EDGE_BODY, kind).astype(np.int8)
+    return PoseProblem(pose7(R0, t0), kind, Xw, obs, isig, cam=cam, cam2=cam2)
 
 
 def synth_lba_graph(rng, n_kf=50, n_points=10000, k_range=(2, 8), n_fixed=2, stereo_frac=0.0,

@@ -61,6 +61,22 @@ def test_pose_optimization_kb8_fisheye(ctx, oracle):
         np.testing.assert_allclose(g.pose, r.pose, atol=KB8_POSE_TOL, rtol=0)
 
 
+def test_pose_optimization_kb8_two_camera(ctx, oracle):
+    """C5 shape: KB8 fisheye pair with right-camera (body) edges through Trl; same tolerance
+    argument as the one-camera KB8 case."""
+    rng = np.random.default_rng(15)
+    probs = [op.synth_pose_problem(rng, n_edges=int(rng.integers(60, 400)), cam=op.kb8_camera(), body_frac=0.4)
+             for _ in range(16)]
+    ref = op.oracle_pose(oracle, probs)
+    got = op.Optimizer(ctx).PoseOptimization(probs)
+    for i, (g, r) in enumerate(zip(got, ref)):
+        assert (probs[i].kind == 2).any()
+        assert g.n_inliers == r.n_inliers, i
+        assert abs(g.lm_iterations - r.lm_iterations) <= 4, (i, g.lm_iterations, r.lm_iterations)
+        np.testing.assert_array_equal(g.outlier, r.outlier)
+        np.testing.assert_allclose(g.pose, r.pose, atol=KB8_POSE_TOL, rtol=0)
+
+
 def test_pose_optimization_small_and_degenerate(ctx, oracle):
     rng = np.random.default_rng(12)
     probs = [op.synth_pose_problem(rng, n_edges=n) for n in (0, 1, 2, 3, 5, 9, 10, 11)]

@@ -85,6 +85,21 @@ def test_pose_optimization_oracle_vs_numpy(oracle, seed, stereo, kb8):
     assert abs(got.lm_iterations - iters) <= 1
 
 
+@pytest.mark.parametrize("seed", [1, 2])
+def test_pose_optimization_two_camera_kb8_oracle_vs_numpy(oracle, seed):
+    """C5 shape: a KB8 fisheye pair, 40 % of the edges observed by the right camera (body edges
+    through Trl)."""
+    rng = np.random.default_rng(1100 + seed)
+    P = op.synth_pose_problem(rng, n_edges=200, cam=op.kb8_camera(), body_frac=0.4)
+    assert (P.kind == 2).sum() > 40
+    got = op.oracle_pose(oracle, [P])[0]
+    pose, outl, ninl, iters = pr.pose_optimization(P)
+    assert got.n_inliers == ninl
+    np.testing.assert_array_equal(got.outlier, outl)
+    np.testing.assert_allclose(got.pose, pose, atol=STATE_TOL, rtol=0)
+    assert abs(got.lm_iterations - iters) <= 1
+
+
 def test_pose_optimization_too_few_edges(oracle):
     rng = np.random.default_rng(7)
     P = op.synth_pose_problem(rng, n_edges=2)
