@@ -106,6 +106,13 @@ typedef struct osg_ba_result {
 int osg_local_bundle_adjustment(struct osg_ctx *ctx, const osg_ba_graph *g, osg_ba_result *r,
                                 const volatile uint8_t *stop_flag);
 
+/* Batched form: n_graphs independent windows (e.g. the LocalMapping windows of several maps or
+ * sequences) optimised in lockstep, every kernel launched once per LM trial for all of them; each
+ * graph follows exactly the single-graph LM (its own lambda, accept / reject, stop rules).
+ * Returns the summed LM iterations or a negative OSG_E_* code.  No reference counterpart. */
+int osg_local_bundle_adjustment_batch(struct osg_ctx *ctx, const osg_ba_graph *graphs, int32_t n_graphs,
+                                      osg_ba_result *results, const volatile uint8_t *stop_flag);
+
 #ifdef __cplusplus
 }
 #endif

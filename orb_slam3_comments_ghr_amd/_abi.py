@@ -131,7 +131,7 @@ EXPORTS = [
     "osg_search_by_projection_mps_batch", "osg_search_by_projection_last_batch",
     "osg_search_by_projection_kf_batch", "osg_search_by_bow_kf_f_batch", "osg_search_by_bow_kf_kf_batch",
     "osg_match_last_stats", "osg_ctx_last_kernel_ms", "osg_pose_optimization", "osg_pose_optimization_batch",
-    "osg_local_bundle_adjustment",
+    "osg_local_bundle_adjustment", "osg_local_bundle_adjustment_batch",
 ]
 
 
@@ -177,6 +177,7 @@ def declare(lib: C.CDLL) -> C.CDLL:
                                                 C.POINTER(OsgPoseResult)]
     lib.osg_local_bundle_adjustment.argtypes = [vp, C.POINTER(OsgBaGraph), C.POINTER(OsgBaResult),
                                                 vp]
+    lib.osg_local_bundle_adjustment_batch.argtypes = [vp, vp, i32, vp, vp]
     return lib
 
 

@@ -29,6 +29,8 @@
 #include <chrono>
 #include <cstdlib>
 #include <cmath>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "ba_common.h"
@@ -40,6 +42,14 @@ namespace {
 
 constexpr int EB = 256;      // edge-parallel kernels
 constexpr int NPART = 1024;  // max chi2 / scale partials
+
+// Per-graph control of one lockstep step (host → device each step; k_lambda_init may set lambda).
+enum : int { M_ERRC = 1, M_LIN = 2, M_INIT = 4, M_ACT = 8, M_FIN = 16 };
+struct LbaCtl {
+    int mode;       // M_* bits: current errors / linearize / lambda init / trial / classify
+    int sel;        // 0: estimate A is current, 1: B
+    double lambda;
+};
 
 struct LbaDev {
     // sizes
@@ -70,21 +80,35 @@ struct LbaDev {
     const int32_t *chunk_start;          // contribution range of each chunk (chunks never span pairs)
     const int32_t *pair_chunk;           // per pair: first chunk (npairs + 1)
     double *chunk_part;                  // 36 per chunk
-    // state
-    const double *pose_cur, *point_cur;
-    double *pose_new, *point_new;
+    // launch extents of this graph (grids are sized for the largest graph of the batch)
+    int ge, gl, gu, nblk_red;
+    double user_lambda;
+    // state: estimate buffers A / B; ctl->sel says which one is current
+    double *poseA, *poseB, *pointA, *pointB;
+    LbaCtl *ctl;                         // per-step control, written by the host each step
+    double *out;                         // per-step results (k_step_reduce)
+    uint8_t *bad;                        // classification
     double *err;                         // 3 per edge
     double *J;                           // EC per edge: quadratic-form contributions
     double *Hll, *bl, *Hpl, *Hpp, *bp;
     double *Dinv, *db, *BDinv, *coef;
     double *Hs, *bs, *x;
     double *Linv;                        // inverses of the 32x32 diagonal blocks of L, row-major per block row
-    double *part;                        // [0..NPART): chi partials, [NPART..2NPART): scale, [2NPART..]: max diag
+    double *part;                        // [0, NPART): chi of the trial, [NPART, 2NPART): scale,
+                                         // [2NPART, 3NPART): max diag, [3NPART, 4NPART): chi of the current estimate
     int *flag;                           // [0] cholesky ok
     unsigned long long *tstamp;          // phase timestamps (OSG_LBA_PROFILE=2), else null
 };
 
 __device__ inline double edge_w(const LbaDev &D, int e) { return (double)D.e_isig2[e]; }
+__device__ inline const double *cur_pose(const LbaDev &D) { return D.ctl->sel ? D.poseB : D.poseA; }
+__device__ inline const double *cur_point(const LbaDev &D) { return D.ctl->sel ? D.pointB : D.pointA; }
+__device__ inline double *new_pose(const LbaDev &D) { return D.ctl->sel ? D.poseA : D.poseB; }
+__device__ inline double *new_point(const LbaDev &D) { return D.ctl->sel ? D.pointA : D.pointB; }
+// one problem per blockIdx.y; a workgroup whose graph skips this kernel leaves at once
+#define LBA_GRAPH(MODEBITS)                                  \
+    const LbaDev &D = Ds[blockIdx.y];                        \
+    if (!(D.ctl->mode & (MODEBITS))) return
 
 __device__ inline void kind_delta(int kind, double &delta, float &dsqr)
 {
@@ -107,9 +131,14 @@ __device__ inline double block_sum_d(double v, double *s)
 }
 
 // per edge error + robust chi2 -> partial sums per workgroup (deterministic order)
-__global__ __launch_bounds__(EB) void k_errors(LbaDev D, const double *__restrict__ poses,
-                                               const double *__restrict__ points, int part_off)
+// which = 0: the trial estimate -> part[0, ge); which = 1: the current estimate -> part[3 NPART, ..)
+__global__ __launch_bounds__(EB) void k_errors(const LbaDev *__restrict__ Ds, int which)
 {
+    LBA_GRAPH(which ? M_ERRC : M_ACT);
+    if ((int)blockIdx.x >= D.ge) return;
+    const double *poses = which ? cur_pose(D) : new_pose(D);
+    const double *points = which ? cur_point(D) : new_point(D);
+    const int part_off = which ? 3 * NPART : 0;
     __shared__ double s[EB / 64];
     const int e = blockIdx.x * EB + threadIdx.x;
     double rho0 = 0.0;
@@ -137,13 +166,14 @@ __global__ __launch_bounds__(EB) void k_errors(LbaDev D, const double *__restric
 // base_binary_edge.hpp:55-120, robust branch): C[e] = {Hpp 21 (upper), b_p 6, Hll 6 (upper),
 // b_l 3, Hpl 18 (6x3)} = 54 doubles; the reductions below only sum them.
 constexpr int EC = 54;
-__global__ __launch_bounds__(EB) void k_linearize(LbaDev D)
+__global__ __launch_bounds__(EB) void k_linearize(const LbaDev *__restrict__ Ds)
 {
+    LBA_GRAPH(M_LIN);
     const int e = blockIdx.x * EB + threadIdx.x;
     if (e >= D.ne) return;
     const int k = D.e_kind[e];
-    const SE3 T = se3_from7(D.pose_cur + 7 * (size_t)D.e_pose[e]);
-    const double *X = D.point_cur + 3 * (size_t)D.e_point[e];
+    const SE3 T = se3_from7(cur_pose(D) + 7 * (size_t)D.e_pose[e]);
+    const double *X = cur_point(D) + 3 * (size_t)D.e_point[e];
     double Jp[3][6], Jx[3][3];
     edge_jacobians(k, true, D.cams[D.e_cam[e]], T, X, Jp, Jx);
     const int dim = (k == OSG_EDGE_STEREO) ? 3 : 2;
@@ -177,8 +207,9 @@ __global__ __launch_bounds__(EB) void k_linearize(LbaDev D)
 
 // per block: Hpl = sum of its edges' contributions (usually one edge; mono + body of one
 // keyframe share a block)
-__global__ __launch_bounds__(EB) void k_block_red(LbaDev D)
+__global__ __launch_bounds__(EB) void k_block_red(const LbaDev *__restrict__ Ds)
 {
+    LBA_GRAPH(M_LIN);
     const int blk = blockIdx.x * EB + threadIdx.x;
     if (blk >= D.nblk) return;
     double h[18];
@@ -191,8 +222,10 @@ __global__ __launch_bounds__(EB) void k_block_red(LbaDev D)
 }
 
 // per landmark: Hll (3x3) and b_l (sums of edge contributions)
-__global__ __launch_bounds__(EB) void k_point_red(LbaDev D)
+__global__ __launch_bounds__(EB) void k_point_red(const LbaDev *__restrict__ Ds)
 {
+    LBA_GRAPH(M_LIN);
+    if ((int)blockIdx.x >= max(D.gl, 1)) return;
     __shared__ double s[EB / 64];
     const int l = blockIdx.x * EB + threadIdx.x;
     double md = 0.0;
@@ -222,10 +255,13 @@ __global__ __launch_bounds__(EB) void k_point_red(LbaDev D)
 }
 
 // per free pose (one workgroup): Hpp (6x6) and b_p from its edges
-__global__ __launch_bounds__(EB) void k_pose_red(LbaDev D, int diag_off)
+__global__ __launch_bounds__(EB) void k_pose_red(const LbaDev *__restrict__ Ds)
 {
-    __shared__ double s[EB / 64][27];
+    LBA_GRAPH(M_LIN);
     const int i = blockIdx.x;
+    if (i >= D.nhp) return;
+    const int diag_off = 2 * NPART + D.gl;
+    __shared__ double s[EB / 64][27];
     double acc[27];
     for (int k = 0; k < 27; k++) acc[k] = 0.0;
     for (int q = D.hp_e_start[i] + threadIdx.x; q < D.hp_e_start[i + 1]; q += EB) {
@@ -276,8 +312,25 @@ __device__ inline void inv3(const double *m, double *o)
 #undef M_
 }
 
-__global__ __launch_bounds__(EB) void k_schur_point(LbaDev D, double lambda)
+// computeLambdaInit (ref:Thirdparty/g2o/g2o/core/optimization_algorithm_levenberg.cpp:178-194): tau
+// times the largest |diagonal| of H, unless the user set an initial lambda
+__global__ void k_lambda_init(const LbaDev *__restrict__ Ds)
 {
+    LBA_GRAPH(M_INIT);
+    if (threadIdx.x != 0) return;
+    if (D.user_lambda > 0) {
+        D.ctl->lambda = D.user_lambda;
+        return;
+    }
+    double md = 0;
+    for (int i = 0; i < D.gl + D.nhp; i++) md = fmax(md, D.part[2 * NPART + i]);
+    D.ctl->lambda = 1e-5 * md;
+}
+
+__global__ __launch_bounds__(EB) void k_schur_point(const LbaDev *__restrict__ Ds)
+{
+    LBA_GRAPH(M_ACT);
+    const double lambda = D.ctl->lambda;
     const int l = blockIdx.x * EB + threadIdx.x;
     if (l >= D.nhl) return;
     double Dm[9];
@@ -293,8 +346,9 @@ __global__ __launch_bounds__(EB) void k_schur_point(LbaDev D, double lambda)
 }
 
 // per block: BDinv = Hpl Dinv, coef = Hpl Dinv b_l
-__global__ __launch_bounds__(EB) void k_schur_block(LbaDev D)
+__global__ __launch_bounds__(EB) void k_schur_block(const LbaDev *__restrict__ Ds)
 {
+    LBA_GRAPH(M_ACT);
     const int blk = blockIdx.x * EB + threadIdx.x;
     if (blk >= D.nblk) return;
     const int l = D.blk_lm[blk];
@@ -319,8 +373,9 @@ __global__ __launch_bounds__(EB) void k_schur_block(LbaDev D)
 //   k_schur_pairs   one wave per pair: sums its chunk partials in chunk order (deterministic),
 //                   writes Hs = Hpp + lambda I - S (both triangles) and b_schur.
 constexpr int SCH = 32;
-__global__ __launch_bounds__(256) void k_schur_chunks(LbaDev D)
+__global__ __launch_bounds__(256) void k_schur_chunks(const LbaDev *__restrict__ Ds)
 {
+    LBA_GRAPH(M_ACT);
     const int ch = (blockIdx.x * 256 + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (ch >= D.nchunks) return;
@@ -357,8 +412,10 @@ __global__ __launch_bounds__(256) void k_schur_chunks(LbaDev D)
     if (lane < 36) D.chunk_part[36 * (size_t)ch + lane] = acc;
 }
 
-__global__ __launch_bounds__(256) void k_schur_pairs(LbaDev D, double lambda)
+__global__ __launch_bounds__(256) void k_schur_pairs(const LbaDev *__restrict__ Ds)
 {
+    LBA_GRAPH(M_ACT);
+    const double lambda = D.ctl->lambda;
     const int wave = (blockIdx.x * 256 + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (wave >= D.npairs) return;
@@ -385,10 +442,12 @@ __global__ __launch_bounds__(256) void k_schur_pairs(LbaDev D, double lambda)
 }
 
 // b_schur_i = b_p,i - sum over pose i's blocks of Hpl Dinv b_l: one workgroup per pose
-__global__ __launch_bounds__(256) void k_bschur(LbaDev D)
+__global__ __launch_bounds__(256) void k_bschur(const LbaDev *__restrict__ Ds)
 {
-    __shared__ double s[4][6];
+    LBA_GRAPH(M_ACT);
     const int i = blockIdx.x;
+    if (i >= D.nhp) return;
+    __shared__ double s[4][6];
     double acc[6] = {0, 0, 0, 0, 0, 0};
     for (int q = D.hp_b_start[i] + threadIdx.x; q < D.hp_b_start[i + 1]; q += 256) {
         const double *cf = D.coef + 6 * (size_t)D.hp_b[q];
@@ -571,8 +630,10 @@ __device__ __forceinline__ double rcp_nr(double d)
 //     applied to the identity give M = Lt^-1, so L_jj^-1 = D^-1/2 M without a triangular solve.
 //  3. workgroup 0: L_jj^-1 -> Linv, y_j = L_jj^-1 rhs -> x;  workgroup t > 0: L_tj = X L_jj^-T
 //     (MFMA) written over A_tj.  A_jj itself is never written (nothing downstream needs L_jj).
-__global__ __launch_bounds__(256) void k_chol_col(LbaDev D, int j)
+__global__ __launch_bounds__(256) void k_chol_col(const LbaDev *__restrict__ Ds, int j)
 {
+    LBA_GRAPH(M_ACT);
+    if (j >= D.nblk_red || (int)blockIdx.x >= D.nblk_red - j) return;
     __shared__ double sP[4][CB][CB + 1];  // per-wave partial tiles
     __shared__ double sG[CB][CB + 1];     // T under elimination
     __shared__ double sM[CB][CB + 1];     // Lt^-1, then L_jj^-1
@@ -724,8 +785,10 @@ __device__ __forceinline__ void lds_barrier()
     asm volatile("" ::: "memory");
 }
 
-__global__ __launch_bounds__(1024) void k_chol_back(LbaDev D)
+__global__ __launch_bounds__(1024) void k_chol_back(const LbaDev *__restrict__ Ds)
 {
+    LBA_GRAPH(M_ACT);
+    if (D.nhp == 0) return;
     __shared__ double s_x[CMAX];
     __shared__ double s_y[CMAX];
     __shared__ double s_li[CMAX * CB];
@@ -811,8 +874,13 @@ __global__ __launch_bounds__(1024) void k_chol_back(LbaDev D)
 }
 
 // landmark back-substitution + new estimates + LM scale partials
-__global__ __launch_bounds__(EB) void k_update(LbaDev D, double lambda)
+__global__ __launch_bounds__(EB) void k_update(const LbaDev *__restrict__ Ds)
 {
+    LBA_GRAPH(M_ACT);
+    if ((int)blockIdx.x >= D.gu) return;
+    const double lambda = D.ctl->lambda;
+    const double *pose_cur = cur_pose(D), *point_cur = cur_point(D);
+    double *pose_new = new_pose(D), *point_new = new_point(D);
     __shared__ double s[EB / 64];
     const int t = blockIdx.x * EB + threadIdx.x;
     const int sp = 6 * D.nhp;
@@ -834,35 +902,37 @@ __global__ __launch_bounds__(EB) void k_update(LbaDev D, double lambda)
         for (int r = 0; r < 3; r++) {
             const double xl = Di[3 * r] * cl[0] + Di[3 * r + 1] * cl[1] + Di[3 * r + 2] * cl[2];
             D.x[sp + 3 * l + r] = xl;
-            D.point_new[3 * (size_t)p + r] = D.point_cur[3 * (size_t)p + r] + xl;
+            point_new[3 * (size_t)p + r] = point_cur[3 * (size_t)p + r] + xl;
             sc += xl * (lambda * xl + D.bl[3 * (size_t)l + r]);
         }
     }
     if (t < D.np) {  // poses: exp(x) * T for free active poses, copy otherwise
         const int hi = D.pose_h[t];
         if (hi >= 0) {
-            SE3 T = se3_from7(D.pose_cur + 7 * (size_t)t);
+            SE3 T = se3_from7(pose_cur + 7 * (size_t)t);
             double upd[6];
             for (int k = 0; k < 6; k++) {
                 upd[k] = D.x[6 * hi + k];
                 sc += upd[k] * (lambda * upd[k] + D.bp[6 * (size_t)hi + k]);
             }
             se3_oplus(T, upd);
-            se3_to7(T, D.pose_new + 7 * (size_t)t);
+            se3_to7(T, pose_new + 7 * (size_t)t);
         } else {
-            for (int k = 0; k < 7; k++) D.pose_new[7 * (size_t)t + k] = D.pose_cur[7 * (size_t)t + k];
+            for (int k = 0; k < 7; k++) pose_new[7 * (size_t)t + k] = pose_cur[7 * (size_t)t + k];
         }
     }
     // points without a landmark index (no edges) keep their estimate
     if (t < D.npt && D.point_h[t] < 0)
-        for (int k = 0; k < 3; k++) D.point_new[3 * (size_t)t + k] = D.point_cur[3 * (size_t)t + k];
+        for (int k = 0; k < 3; k++) point_new[3 * (size_t)t + k] = point_cur[3 * (size_t)t + k];
     const double tot = block_sum_d(sc, s);
     if (threadIdx.x == 0) D.part[NPART + blockIdx.x] = tot;
 }
 
-__global__ __launch_bounds__(EB) void k_classify(LbaDev D, const double *__restrict__ poses,
-                                                 const double *__restrict__ points, uint8_t *__restrict__ bad)
+__global__ __launch_bounds__(EB) void k_classify(const LbaDev *__restrict__ Ds)
 {
+    LBA_GRAPH(M_FIN);
+    const double *poses = cur_pose(D), *points = cur_point(D);
+    uint8_t *bad = D.bad;
     const int e = blockIdx.x * EB + threadIdx.x;
     if (e >= D.ne) return;
     const int k = D.e_kind[e];
@@ -874,6 +944,27 @@ __global__ __launch_bounds__(EB) void k_classify(LbaDev D, const double *__restr
     bad[e] = (chi2_of(ev, dim, edge_w(D, e)) > th || !pos) ? 1 : 0;
 }
 
+// The step's scalars per graph, summed in the host's former order (sequential from index 0):
+// out = {chi of the trial, LM scale, Cholesky ok, lambda used, chi of the current estimate}
+__global__ void k_step_reduce(const LbaDev *__restrict__ Ds)
+{
+    LBA_GRAPH(M_ACT | M_ERRC);
+    if (threadIdx.x != 0) return;
+    const int mode = D.ctl->mode;
+    double chi = 0, sc = 0, chic = 0;
+    if (mode & M_ACT) {
+        for (int i = 0; i < D.ge; i++) chi += D.part[i];
+        for (int i = 0; i < D.gu; i++) sc += D.part[NPART + i];
+    }
+    if (mode & M_ERRC)
+        for (int i = 0; i < D.ge; i++) chic += D.part[3 * NPART + i];
+    D.out[0] = chi;
+    D.out[1] = sc;
+    D.out[2] = (D.nhp > 0 && (mode & M_ACT)) ? (double)D.flag[0] : 1.0;
+    D.out[3] = D.ctl->lambda;
+    D.out[4] = chic;
+}
+
 template <typename T>
 T *carve(char *base, size_t &off, size_t count)
 {
@@ -883,449 +974,623 @@ T *carve(char *base, size_t &off, size_t count)
     return p;
 }
 
-}  // namespace
+// ---------------------------------------------------------------------------------------------
+// Host side.  One graph = one LbaHost: the BlockSolver structure (built once, like
+// BlockSolver::buildStructure) and g2o's LM state.  A batch runs B graphs in lockstep: every step
+// is one LM trial of every graph still running (one launch of each kernel for all of them, grid.y
+// = graph), then ONE download of 5 scalars per graph, and the host applies the reference's
+// accept / reject / lambda rules per graph.  A graph starting an iteration also linearises (and
+// recomputes the current estimate's errors, or initialises lambda) in the same step.
+struct LbaHost {
+    const osg_ba_graph *G = nullptr;
+    osg_ba_result *R = nullptr;
+    int np = 0, npt = 0, ne = 0, nhp = 0, nhl = 0, nblk = 0, npairs = 0, nchunks = 0;
+    int ge = 0, gl = 0, gu = 0, nblk_red = 0;
+    bool trivial = false;  // nothing to optimise: the estimates are returned unchanged
+    std::vector<int32_t> pose_h, hp_pose, point_h, hl_point, lm_e_start, lm_e, lm_b_start, blk_pose, edge_blk, blk_lm,
+        blk_e_start, blk_e, hp_e_start, hp_e, hp_b_start, hp_b, pair_start, pair_ab, chunk_start, pair_chunk;
+    double t_struct = 0;
+    // LM state (ref:Thirdparty/g2o/g2o/core/optimization_algorithm_levenberg.cpp:61-194 and
+    // sparse_optimizer.cpp optimize())
+    double lambda = 0, ni = 2, currentChi = 0, iniChi = 0, rho = 0;
+    int nBad = 0, iters = 0, trials = 0, qmax = 0, it = 0, sel = 0;
+    bool errors_current = true, new_iter = true, done = false;
+    size_t o_in = 0, o_st = 0;  // offsets of this graph's inputs / state
+};
 
-extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, osg_ba_result *R,
-                                           const volatile uint8_t *stop)
+int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
 {
-    if (!ctx) return OSG_E_INVALID;
-    OSG_REQUIRE(ctx, G && R, "null argument");
-    const int np = G->n_poses, npt = G->n_points, ne = G->n_edges;
-    OSG_REQUIRE(ctx, np >= 0 && npt >= 0 && ne >= 0 && G->n_cams >= 0, "sizes");
-    OSG_REQUIRE(ctx, R->pose && R->point && (ne == 0 || R->edge_bad), "result buffers");
-    R->iterations = 0;
-    R->trials = 0;
-    R->aborted = 0;
-    R->chi2_initial = R->chi2_final = 0.0;
-    std::memcpy(R->pose, G->pose, sizeof(double) * 7 * np);
-    std::memcpy(R->point, G->point, sizeof(double) * 3 * npt);
-    if (ne > 0) std::memset(R->edge_bad, 0, ne);
-    if (stop && *stop) {  // ref:src/Optimizer.cc:2112-2114
-        R->aborted = 1;
-        return 0;
-    }
-    if (ne == 0) return 0;
-    for (int e = 0; e < ne; e++) {
-        if (G->e_pose[e] < 0 || G->e_pose[e] >= np || G->e_point[e] < 0 || G->e_point[e] >= npt ||
-            G->e_cam[e] < 0 || G->e_cam[e] >= G->n_cams)
-            return osg_set_error(ctx, OSG_E_INVALID, "edge %d references out of range", e);
-    }
-    // ---------------------------------------------------------------- structure (host)
-    static const int prof_level = getenv("OSG_LBA_PROFILE") ? atoi(getenv("OSG_LBA_PROFILE")) : 0;
-    static const bool prof = prof_level > 0;
-    const bool prof_ts = prof_level >= 2;
-    int ts_printed = 0;
     const auto tp0 = std::chrono::steady_clock::now();
-    auto ms_since = [&](std::chrono::steady_clock::time_point t) {
-        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
-    };
+    const int np = G->n_poses, npt = G->n_points, ne = G->n_edges;
+    H.np = np;
+    H.npt = npt;
+    H.ne = ne;
     std::vector<int32_t> pose_cnt(np, 0), point_cnt(npt, 0);
     for (int e = 0; e < ne; e++) {
         pose_cnt[G->e_pose[e]]++;
         point_cnt[G->e_point[e]]++;
     }
-    std::vector<int32_t> pose_h(np, -1), hp_pose, point_h(npt, -1), hl_point;
+    H.pose_h.assign(np, -1);
+    H.point_h.assign(npt, -1);
     for (int i = 0; i < np; i++)
         if (!G->pose_fixed[i] && pose_cnt[i] > 0) {
-            pose_h[i] = (int)hp_pose.size();
-            hp_pose.push_back(i);
+            H.pose_h[i] = (int)H.hp_pose.size();
+            H.hp_pose.push_back(i);
         }
     for (int i = 0; i < npt; i++)
         if (point_cnt[i] > 0) {
-            point_h[i] = (int)hl_point.size();
-            hl_point.push_back(i);
+            H.point_h[i] = (int)H.hl_point.size();
+            H.hl_point.push_back(i);
         }
-    const int nhp = (int)hp_pose.size(), nhl = (int)hl_point.size();
-    if (nhp + nhl == 0) return 0;
-    OSG_REQUIRE(ctx, 6 * nhp <= CMAX, "%d free poses exceed the dense reduced-system limit (%d)", nhp, CMAX / 6);
-    const double t_s0 = ms_since(tp0);
-    // edges per landmark (stable in edge order)
-    std::vector<int32_t> lm_e_start(nhl + 1, 0), lm_e(ne);
-    for (int e = 0; e < ne; e++) lm_e_start[point_h[G->e_point[e]] + 1]++;
-    for (int l = 0; l < nhl; l++) lm_e_start[l + 1] += lm_e_start[l];
-    {
-        std::vector<int32_t> fill(lm_e_start.begin(), lm_e_start.end() - 1);
-        for (int e = 0; e < ne; e++) lm_e[fill[point_h[G->e_point[e]]]++] = e;
+    const int nhp = (int)H.hp_pose.size(), nhl = (int)H.hl_point.size();
+    H.nhp = nhp;
+    H.nhl = nhl;
+    if (nhp + nhl == 0) {
+        H.trivial = true;
+        return OSG_OK;
     }
-    const double t_s1 = ms_since(tp0);
+    if (6 * nhp > CMAX)
+        return osg_set_error(ctx, OSG_E_INVALID, "%d free poses exceed the dense reduced-system limit (%d)", nhp,
+                             CMAX / 6);
+    const std::vector<int32_t> &pose_h = H.pose_h, &point_h = H.point_h;
+    // edges per landmark (stable in edge order)
+    H.lm_e_start.assign(nhl + 1, 0);
+    H.lm_e.assign(ne, 0);
+    for (int e = 0; e < ne; e++) H.lm_e_start[point_h[G->e_point[e]] + 1]++;
+    for (int l = 0; l < nhl; l++) H.lm_e_start[l + 1] += H.lm_e_start[l];
+    {
+        std::vector<int32_t> fill(H.lm_e_start.begin(), H.lm_e_start.end() - 1);
+        for (int e = 0; e < ne; e++) H.lm_e[fill[point_h[G->e_point[e]]]++] = e;
+    }
     // blocks per landmark: unique free poses sorted by hessian index
-    std::vector<int32_t> lm_b_start(nhl + 1, 0), blk_pose, edge_blk(ne, -1);
-    blk_pose.reserve(ne);
+    H.lm_b_start.assign(nhl + 1, 0);
+    H.edge_blk.assign(ne, -1);
+    H.blk_pose.reserve(ne);
     std::vector<int32_t> tmp;
     for (int l = 0; l < nhl; l++) {
         tmp.clear();
-        for (int q = lm_e_start[l]; q < lm_e_start[l + 1]; q++) {
-            const int ph = pose_h[G->e_pose[lm_e[q]]];
+        for (int q = H.lm_e_start[l]; q < H.lm_e_start[l + 1]; q++) {
+            const int ph = pose_h[G->e_pose[H.lm_e[q]]];
             if (ph >= 0) tmp.push_back(ph);
         }
         std::sort(tmp.begin(), tmp.end());
         tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
-        const int base = (int)blk_pose.size();
-        for (int ph : tmp) blk_pose.push_back(ph);
-        lm_b_start[l + 1] = (int)blk_pose.size();
-        for (int q = lm_e_start[l]; q < lm_e_start[l + 1]; q++) {
-            const int e = lm_e[q];
+        const int base = (int)H.blk_pose.size();
+        for (int ph : tmp) H.blk_pose.push_back(ph);
+        H.lm_b_start[l + 1] = (int)H.blk_pose.size();
+        for (int q = H.lm_e_start[l]; q < H.lm_e_start[l + 1]; q++) {
+            const int e = H.lm_e[q];
             const int ph = pose_h[G->e_pose[e]];
             if (ph < 0) continue;
             for (int k = 0; k < (int)tmp.size(); k++)
                 if (tmp[k] == ph) {
-                    edge_blk[e] = base + k;
+                    H.edge_blk[e] = base + k;
                     break;
                 }
         }
     }
-    const int nblk = (int)blk_pose.size();
-    const double t_s2 = ms_since(tp0);
-    std::vector<int32_t> blk_lm(nblk), blk_e_start(nblk + 1, 0), blk_e;
+    const int nblk = (int)H.blk_pose.size();
+    H.nblk = nblk;
+    H.blk_lm.assign(nblk, 0);
+    H.blk_e_start.assign(nblk + 1, 0);
     for (int l = 0; l < nhl; l++)
-        for (int b = lm_b_start[l]; b < lm_b_start[l + 1]; b++) blk_lm[b] = l;
+        for (int b = H.lm_b_start[l]; b < H.lm_b_start[l + 1]; b++) H.blk_lm[b] = l;
     for (int e = 0; e < ne; e++)
-        if (edge_blk[e] >= 0) blk_e_start[edge_blk[e] + 1]++;
-    for (int b = 0; b < nblk; b++) blk_e_start[b + 1] += blk_e_start[b];
-    blk_e.resize(blk_e_start[nblk]);
+        if (H.edge_blk[e] >= 0) H.blk_e_start[H.edge_blk[e] + 1]++;
+    for (int b = 0; b < nblk; b++) H.blk_e_start[b + 1] += H.blk_e_start[b];
+    H.blk_e.assign(H.blk_e_start[nblk], 0);
     {
-        std::vector<int32_t> fill(blk_e_start.begin(), blk_e_start.end() - 1);
+        std::vector<int32_t> fill(H.blk_e_start.begin(), H.blk_e_start.end() - 1);
         for (int e = 0; e < ne; e++)
-            if (edge_blk[e] >= 0) blk_e[fill[edge_blk[e]]++] = e;
+            if (H.edge_blk[e] >= 0) H.blk_e[fill[H.edge_blk[e]]++] = e;
     }
     // edges / blocks per hessian pose
-    std::vector<int32_t> hp_e_start(nhp + 1, 0), hp_e, hp_b_start(nhp + 1, 0), hp_b(nblk);
+    H.hp_e_start.assign(nhp + 1, 0);
+    H.hp_b_start.assign(nhp + 1, 0);
+    H.hp_b.assign(nblk, 0);
     for (int e = 0; e < ne; e++)
-        if (pose_h[G->e_pose[e]] >= 0) hp_e_start[pose_h[G->e_pose[e]] + 1]++;
-    for (int i = 0; i < nhp; i++) hp_e_start[i + 1] += hp_e_start[i];
-    hp_e.resize(hp_e_start[nhp]);
+        if (pose_h[G->e_pose[e]] >= 0) H.hp_e_start[pose_h[G->e_pose[e]] + 1]++;
+    for (int i = 0; i < nhp; i++) H.hp_e_start[i + 1] += H.hp_e_start[i];
+    H.hp_e.assign(H.hp_e_start[nhp], 0);
     {
-        std::vector<int32_t> fill(hp_e_start.begin(), hp_e_start.end() - 1);
+        std::vector<int32_t> fill(H.hp_e_start.begin(), H.hp_e_start.end() - 1);
         for (int e = 0; e < ne; e++)
-            if (pose_h[G->e_pose[e]] >= 0) hp_e[fill[pose_h[G->e_pose[e]]]++] = e;
+            if (pose_h[G->e_pose[e]] >= 0) H.hp_e[fill[pose_h[G->e_pose[e]]]++] = e;
     }
-    for (int b = 0; b < nblk; b++) hp_b_start[blk_pose[b] + 1]++;
-    for (int i = 0; i < nhp; i++) hp_b_start[i + 1] += hp_b_start[i];
+    for (int b = 0; b < nblk; b++) H.hp_b_start[H.blk_pose[b] + 1]++;
+    for (int i = 0; i < nhp; i++) H.hp_b_start[i + 1] += H.hp_b_start[i];
     {
-        std::vector<int32_t> fill(hp_b_start.begin(), hp_b_start.end() - 1);
-        for (int b = 0; b < nblk; b++) hp_b[fill[blk_pose[b]]++] = b;
+        std::vector<int32_t> fill(H.hp_b_start.begin(), H.hp_b_start.end() - 1);
+        for (int b = 0; b < nblk; b++) H.hp_b[fill[H.blk_pose[b]]++] = b;
     }
-    const double t_s3 = ms_since(tp0);
     // pose pairs (i <= j), dense index; contributions in landmark order
     const int npairs = nhp * (nhp + 1) / 2;
+    H.npairs = npairs;
     auto pid = [nhp](int i, int j) { return i * nhp - i * (i - 1) / 2 + (j - i); };
-    std::vector<int32_t> pair_start(npairs + 1, 0);
+    H.pair_start.assign(npairs + 1, 0);
     for (int l = 0; l < nhl; l++)
-        for (int a = lm_b_start[l]; a < lm_b_start[l + 1]; a++)
-            for (int b = a; b < lm_b_start[l + 1]; b++) pair_start[pid(blk_pose[a], blk_pose[b]) + 1]++;
-    for (int k = 0; k < npairs; k++) pair_start[k + 1] += pair_start[k];
-    std::vector<int32_t> pair_ab(2 * (size_t)std::max(pair_start[npairs], 1));
+        for (int a = H.lm_b_start[l]; a < H.lm_b_start[l + 1]; a++)
+            for (int b = a; b < H.lm_b_start[l + 1]; b++) H.pair_start[pid(H.blk_pose[a], H.blk_pose[b]) + 1]++;
+    for (int k = 0; k < npairs; k++) H.pair_start[k + 1] += H.pair_start[k];
+    H.pair_ab.assign(2 * (size_t)std::max(H.pair_start[npairs], 1), 0);
     {
-        std::vector<int32_t> fill(pair_start.begin(), pair_start.end() - 1);
+        std::vector<int32_t> fill(H.pair_start.begin(), H.pair_start.end() - 1);
         for (int l = 0; l < nhl; l++)
-            for (int a = lm_b_start[l]; a < lm_b_start[l + 1]; a++)
-                for (int b = a; b < lm_b_start[l + 1]; b++) {
-                    const int k = fill[pid(blk_pose[a], blk_pose[b])]++;
-                    pair_ab[2 * k] = a;
-                    pair_ab[2 * k + 1] = b;
+            for (int a = H.lm_b_start[l]; a < H.lm_b_start[l + 1]; a++)
+                for (int b = a; b < H.lm_b_start[l + 1]; b++) {
+                    const int k = fill[pid(H.blk_pose[a], H.blk_pose[b])]++;
+                    H.pair_ab[2 * k] = a;
+                    H.pair_ab[2 * k + 1] = b;
                 }
     }
-    const double t_struct = ms_since(tp0);
     // chunks of <= SCH contributions, never spanning two pairs
-    std::vector<int32_t> chunk_start, pair_chunk(npairs + 1, 0);
+    H.pair_chunk.assign(npairs + 1, 0);
     for (int k = 0; k < npairs; k++) {
-        pair_chunk[k] = (int)chunk_start.size();
-        for (int q = pair_start[k]; q < pair_start[k + 1]; q += SCH) chunk_start.push_back(q);
+        H.pair_chunk[k] = (int)H.chunk_start.size();
+        for (int q = H.pair_start[k]; q < H.pair_start[k + 1]; q += SCH) H.chunk_start.push_back(q);
     }
-    pair_chunk[npairs] = (int)chunk_start.size();
-    const int nchunks = (int)chunk_start.size();
-    chunk_start.push_back(pair_start[npairs]);
-    // ---------------------------------------------------------------- device layout
+    H.pair_chunk[npairs] = (int)H.chunk_start.size();
+    H.nchunks = (int)H.chunk_start.size();
+    H.chunk_start.push_back(H.pair_start[npairs]);
+    H.ge = (ne + EB - 1) / EB;
+    H.gl = (nhl + EB - 1) / EB;
+    H.gu = (std::max(std::max(nhl, np), npt) + EB - 1) / EB;
+    H.nblk_red = (6 * nhp + CB - 1) / CB;
+    if (!(H.ge <= NPART && H.gu <= NPART && H.gl + nhp <= NPART))
+        return osg_set_error(ctx, OSG_E_INVALID, "graph too large for the partial buffers");
+    H.t_struct = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp0).count();
+    return OSG_OK;
+}
+
+int check_graph(osg_ctx *ctx, const osg_ba_graph *G, const osg_ba_result *R)
+{
+    OSG_REQUIRE(ctx, G && R, "null argument");
+    const int np = G->n_poses, npt = G->n_points, ne = G->n_edges;
+    OSG_REQUIRE(ctx, np >= 0 && npt >= 0 && ne >= 0 && G->n_cams >= 0, "sizes");
+    OSG_REQUIRE(ctx, R->pose && R->point && (ne == 0 || R->edge_bad), "result buffers");
+    for (int e = 0; e < ne; e++) {
+        if (G->e_pose[e] < 0 || G->e_pose[e] >= np || G->e_point[e] < 0 || G->e_point[e] >= npt ||
+            G->e_cam[e] < 0 || G->e_cam[e] >= G->n_cams)
+            return osg_set_error(ctx, OSG_E_INVALID, "edge %d references out of range", e);
+    }
+    return OSG_OK;
+}
+
+// device state of one graph (sizes only when base == nullptr)
+void carve_state(char *base, size_t &off, const LbaHost &H, LbaDev *D, bool prof_ts)
+{
+    const int np = H.np, npt = H.npt, ne = H.ne, nhl = H.nhl, nhp = H.nhp, nblk = H.nblk;
+    const int sp = 6 * nhp;
+    double *pA = carve<double>(base, off, 7 * (size_t)np);
+    double *pB = carve<double>(base, off, 7 * (size_t)np);
+    double *qA = carve<double>(base, off, 3 * (size_t)npt);
+    double *qB = carve<double>(base, off, 3 * (size_t)npt);
+    double *err = carve<double>(base, off, 3 * (size_t)ne);
+    double *J = carve<double>(base, off, EC * (size_t)ne);
+    double *Hll = carve<double>(base, off, 9 * (size_t)nhl);
+    double *bl = carve<double>(base, off, 3 * (size_t)nhl);
+    double *Hpl = carve<double>(base, off, 18 * (size_t)nblk);
+    double *Hpp = carve<double>(base, off, 36 * (size_t)nhp);
+    double *bp = carve<double>(base, off, 6 * (size_t)nhp);
+    double *Dinv = carve<double>(base, off, 9 * (size_t)nhl);
+    double *BDinv = carve<double>(base, off, 18 * (size_t)nblk);
+    double *coef = carve<double>(base, off, 6 * (size_t)nblk);
+    double *Hs = carve<double>(base, off, (size_t)sp * sp);
+    double *bs = carve<double>(base, off, (size_t)sp);
+    double *x = carve<double>(base, off, (size_t)sp + 3 * (size_t)nhl);
+    double *part = carve<double>(base, off, 4 * (size_t)NPART + 64);
+    double *chunk_part = carve<double>(base, off, 36 * (size_t)std::max(H.nchunks, 1));
+    double *db = carve<double>(base, off, 3 * (size_t)nhl);
+    double *Linv = carve<double>(base, off, (size_t)sp * CB);
+    int *flag = carve<int>(base, off, 16);
+    unsigned long long *ts = prof_ts ? carve<unsigned long long>(base, off, 8 * 2 * 64 + 64) : nullptr;
+    uint8_t *bad = carve<uint8_t>(base, off, ne);
+    if (!D) return;
+    D->poseA = pA;
+    D->poseB = pB;
+    D->pointA = qA;
+    D->pointB = qB;
+    D->err = err;
+    D->J = J;
+    D->Hll = Hll;
+    D->bl = bl;
+    D->Hpl = Hpl;
+    D->Hpp = Hpp;
+    D->bp = bp;
+    D->Dinv = Dinv;
+    D->BDinv = BDinv;
+    D->coef = coef;
+    D->Hs = Hs;
+    D->bs = bs;
+    D->x = x;
+    D->part = part;
+    D->chunk_part = chunk_part;
+    D->db = db;
+    D->Linv = Linv;
+    D->flag = flag;
+    D->tstamp = ts;
+    D->bad = bad;
+}
+
+int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, int B, const volatile uint8_t *stop)
+{
+    if (!ctx) return OSG_E_INVALID;
+    OSG_REQUIRE(ctx, B >= 0 && (B == 0 || (graphs && results)), "batch arguments");
+    static const int prof_level = getenv("OSG_LBA_PROFILE") ? atoi(getenv("OSG_LBA_PROFILE")) : 0;
+    const bool prof = prof_level > 0, prof_ts = prof_level >= 2 && B == 1;
+    const auto tp0 = std::chrono::steady_clock::now();
+    auto ms_since = [&](std::chrono::steady_clock::time_point t) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+    };
+    for (int b = 0; b < B; b++) {
+        const int rc = check_graph(ctx, &graphs[b], &results[b]);
+        if (rc < 0) return B > 1 ? osg_set_error(ctx, rc, "graph %d: %s", b, std::string(ctx->last_error).c_str()) : rc;
+        osg_ba_result *R = &results[b];
+        const osg_ba_graph *G = &graphs[b];
+        R->iterations = 0;
+        R->trials = 0;
+        R->aborted = 0;
+        R->chi2_initial = R->chi2_final = 0.0;
+        std::memcpy(R->pose, G->pose, sizeof(double) * 7 * G->n_poses);
+        std::memcpy(R->point, G->point, sizeof(double) * 3 * G->n_points);
+        if (G->n_edges > 0) std::memset(R->edge_bad, 0, G->n_edges);
+    }
+    if (stop && *stop) {  // ref:src/Optimizer.cc:2112-2114
+        for (int b = 0; b < B; b++) results[b].aborted = 1;
+        return 0;
+    }
+    // ---- structures (host threads for a batch; each graph is independent)
+    std::vector<LbaHost> H(B);
+    std::vector<int> rcs(B, OSG_OK);
+    {
+        auto work = [&](int b0, int b1) {
+            for (int b = b0; b < b1; b++) {
+                H[b].G = &graphs[b];
+                H[b].R = &results[b];
+                if (graphs[b].n_edges == 0) {
+                    H[b].trivial = true;
+                    continue;
+                }
+                rcs[b] = build_structure(ctx, &graphs[b], H[b]);
+            }
+        };
+        const int nthr = std::min<int>(B, std::max(1, std::min<int>(16, (int)std::thread::hardware_concurrency())));
+        if (nthr <= 1) {
+            work(0, B);
+        } else {
+            std::vector<std::thread> th;
+            const int per = (B + nthr - 1) / nthr;
+            for (int t = 0; t < nthr; t++) th.emplace_back(work, std::min(B, t * per), std::min(B, (t + 1) * per));
+            for (auto &t : th) t.join();
+        }
+        for (int b = 0; b < B; b++)
+            if (rcs[b] < 0)
+                return B > 1 ? osg_set_error(ctx, rcs[b], "graph %d: structure", b) : rcs[b];
+    }
+    std::vector<int> act;  // graphs with something to optimise
+    for (int b = 0; b < B; b++)
+        if (!H[b].trivial) act.push_back(b);
+    const int NA = (int)act.size();
+    if (NA == 0) return 0;
+    const double t_struct = ms_since(tp0);
+    // ---- device layout: one packed input block, one state block, the LbaDev / control arrays
     osg_packer pk;
-    const size_t o_fixed = pk.add(G->pose_fixed, np);
-    const size_t o_epose = pk.add(G->e_pose, 4 * (size_t)ne);
-    const size_t o_epoint = pk.add(G->e_point, 4 * (size_t)ne);
-    const size_t o_ecam = pk.add(G->e_cam, 4 * (size_t)ne);
-    const size_t o_ekind = pk.add(G->e_kind, ne);
-    const size_t o_eobs = pk.add(G->e_obs, 24 * (size_t)ne);
-    const size_t o_eisig = pk.add(G->e_inv_sigma2, 4 * (size_t)ne);
-    const size_t o_cams = pk.add(G->cams, sizeof(osg_camera) * G->n_cams);
-    const size_t o_poseh = pk.add(pose_h.data(), 4 * (size_t)np);
-    const size_t o_hppose = pk.add(hp_pose.data(), 4 * (size_t)nhp);
-    const size_t o_pointh = pk.add(point_h.data(), 4 * (size_t)npt);
-    const size_t o_hlpoint = pk.add(hl_point.data(), 4 * (size_t)nhl);
-    const size_t o_lmes = pk.add(lm_e_start.data(), 4 * (size_t)(nhl + 1));
-    const size_t o_lme = pk.add(lm_e.data(), 4 * (size_t)ne);
-    const size_t o_lmbs = pk.add(lm_b_start.data(), 4 * (size_t)(nhl + 1));
-    const size_t o_blkpose = pk.add(blk_pose.data(), 4 * (size_t)nblk);
-    const size_t o_eblk = pk.add(edge_blk.data(), 4 * (size_t)ne);
-    const size_t o_hpes = pk.add(hp_e_start.data(), 4 * (size_t)(nhp + 1));
-    const size_t o_hpe = pk.add(hp_e.data(), 4 * hp_e.size());
-    const size_t o_hpbs = pk.add(hp_b_start.data(), 4 * (size_t)(nhp + 1));
-    const size_t o_hpb = pk.add(hp_b.data(), 4 * (size_t)nblk);
-    const size_t o_pairs = pk.add(pair_start.data(), 4 * (size_t)(npairs + 1));
-    const size_t o_pairab = pk.add(pair_ab.data(), 4 * pair_ab.size());
-    const size_t o_chs = pk.add(chunk_start.data(), 4 * chunk_start.size());
-    const size_t o_blklm = pk.add(blk_lm.data(), 4 * (size_t)nblk);
-    const size_t o_blkes = pk.add(blk_e_start.data(), 4 * (size_t)(nblk + 1));
-    const size_t o_blke = pk.add(blk_e.data(), 4 * blk_e.size());
-    const size_t o_pch = pk.add(pair_chunk.data(), 4 * pair_chunk.size());
-    const size_t o_pose0 = pk.add(G->pose, 56 * (size_t)np);
-    const size_t o_point0 = pk.add(G->point, 24 * (size_t)npt);
-    char *pin = (char *)osg_pinned(ctx, pk.total + 4096 + sizeof(double) * (3 * NPART + 64));
+    struct InOff {
+        size_t fixed, epose, epoint, ecam, ekind, eobs, eisig, cams, poseh, hppose, pointh, hlpoint, lmes, lme, lmbs,
+            blkpose, eblk, hpes, hpe, hpbs, hpb, pairs, pairab, chs, blklm, blkes, blke, pch, pose0, point0;
+    };
+    std::vector<InOff> io(NA);
+    for (int a = 0; a < NA; a++) {
+        const LbaHost &h = H[act[a]];
+        const osg_ba_graph *G = h.G;
+        const int np = h.np, npt = h.npt, ne = h.ne, nhp = h.nhp, nhl = h.nhl, nblk = h.nblk;
+        InOff &o = io[a];
+        o.fixed = pk.add(G->pose_fixed, np);
+        o.epose = pk.add(G->e_pose, 4 * (size_t)ne);
+        o.epoint = pk.add(G->e_point, 4 * (size_t)ne);
+        o.ecam = pk.add(G->e_cam, 4 * (size_t)ne);
+        o.ekind = pk.add(G->e_kind, ne);
+        o.eobs = pk.add(G->e_obs, 24 * (size_t)ne);
+        o.eisig = pk.add(G->e_inv_sigma2, 4 * (size_t)ne);
+        o.cams = pk.add(G->cams, sizeof(osg_camera) * G->n_cams);
+        o.poseh = pk.add(h.pose_h.data(), 4 * (size_t)np);
+        o.hppose = pk.add(h.hp_pose.data(), 4 * (size_t)nhp);
+        o.pointh = pk.add(h.point_h.data(), 4 * (size_t)npt);
+        o.hlpoint = pk.add(h.hl_point.data(), 4 * (size_t)nhl);
+        o.lmes = pk.add(h.lm_e_start.data(), 4 * (size_t)(nhl + 1));
+        o.lme = pk.add(h.lm_e.data(), 4 * (size_t)ne);
+        o.lmbs = pk.add(h.lm_b_start.data(), 4 * (size_t)(nhl + 1));
+        o.blkpose = pk.add(h.blk_pose.data(), 4 * (size_t)nblk);
+        o.eblk = pk.add(h.edge_blk.data(), 4 * (size_t)ne);
+        o.hpes = pk.add(h.hp_e_start.data(), 4 * (size_t)(nhp + 1));
+        o.hpe = pk.add(h.hp_e.data(), 4 * h.hp_e.size());
+        o.hpbs = pk.add(h.hp_b_start.data(), 4 * (size_t)(nhp + 1));
+        o.hpb = pk.add(h.hp_b.data(), 4 * (size_t)nblk);
+        o.pairs = pk.add(h.pair_start.data(), 4 * (size_t)(h.npairs + 1));
+        o.pairab = pk.add(h.pair_ab.data(), 4 * h.pair_ab.size());
+        o.chs = pk.add(h.chunk_start.data(), 4 * h.chunk_start.size());
+        o.blklm = pk.add(h.blk_lm.data(), 4 * (size_t)nblk);
+        o.blkes = pk.add(h.blk_e_start.data(), 4 * (size_t)(nblk + 1));
+        o.blke = pk.add(h.blk_e.data(), 4 * h.blk_e.size());
+        o.pch = pk.add(h.pair_chunk.data(), 4 * h.pair_chunk.size());
+        o.pose0 = pk.add(G->pose, 56 * (size_t)np);
+        o.point0 = pk.add(G->point, 24 * (size_t)npt);
+    }
+    // state sizes
+    std::vector<size_t> st_off(NA + 1, 0);
+    for (int a = 0; a < NA; a++) {
+        size_t sz = 0;
+        carve_state(nullptr, sz, H[act[a]], nullptr, prof_ts);
+        st_off[a + 1] = st_off[a] + ((sz + 255) & ~size_t(255)) + 256;
+    }
+    const size_t in_pad = (pk.total + 255) & ~size_t(255);
+    const size_t dev_bytes = sizeof(LbaDev) * (size_t)NA;
+    const size_t ctl_bytes = sizeof(LbaCtl) * (size_t)NA;
+    const size_t out_bytes = sizeof(double) * 8 * (size_t)NA;
+    char *pin = (char *)osg_pinned(ctx, in_pad + dev_bytes + ctl_bytes + out_bytes + 1024);
     if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
     OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
     pk.fill(pin);
-    char *din = nullptr;
+    LbaDev *h_dev = (LbaDev *)(pin + in_pad);
+    LbaCtl *h_ctl = (LbaCtl *)((char *)h_dev + dev_bytes);
+    double *h_out = (double *)((char *)h_ctl + ctl_bytes);
+    char *din = nullptr, *dst = nullptr, *dsm = nullptr;
     OSG_ALLOC(ctx, din, SLOT_BA2, pk.total + 256);
+    OSG_ALLOC(ctx, dst, SLOT_BA3, st_off[NA]);
+    OSG_ALLOC(ctx, dsm, SLOT_BA4, dev_bytes + ctl_bytes + out_bytes + 256);
+    LbaDev *d_dev = (LbaDev *)dsm;
+    LbaCtl *d_ctl = (LbaCtl *)(dsm + dev_bytes);
+    double *d_out = (double *)(dsm + dev_bytes + ctl_bytes);
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(din, pin, pk.total, hipMemcpyHostToDevice, ctx->stream));
-    // state buffers
-    const int sp = 6 * nhp;
-    size_t off = 0;
-    size_t st_bytes = 0;
-    {  // size pass
-        char *z = nullptr;
-        carve<double>(z, st_bytes, 7 * (size_t)np);      // pose A
-        carve<double>(z, st_bytes, 7 * (size_t)np);      // pose B
-        carve<double>(z, st_bytes, 3 * (size_t)npt);     // point A
-        carve<double>(z, st_bytes, 3 * (size_t)npt);     // point B
-        carve<double>(z, st_bytes, 3 * (size_t)ne);      // err
-        carve<double>(z, st_bytes, EC * (size_t)ne);     // per-edge contributions
-        carve<double>(z, st_bytes, 9 * (size_t)nhl);     // Hll
-        carve<double>(z, st_bytes, 3 * (size_t)nhl);     // bl
-        carve<double>(z, st_bytes, 18 * (size_t)nblk);   // Hpl
-        carve<double>(z, st_bytes, 36 * (size_t)nhp);    // Hpp
-        carve<double>(z, st_bytes, 6 * (size_t)nhp);     // bp
-        carve<double>(z, st_bytes, 9 * (size_t)nhl);     // Dinv
-        carve<double>(z, st_bytes, 18 * (size_t)nblk);   // BDinv
-        carve<double>(z, st_bytes, 6 * (size_t)nblk);    // coef
-        carve<double>(z, st_bytes, (size_t)sp * sp);     // Hs
-        carve<double>(z, st_bytes, (size_t)sp);          // bs
-        carve<double>(z, st_bytes, (size_t)sp + 3 * (size_t)nhl);  // x
-        carve<double>(z, st_bytes, 3 * (size_t)NPART + 64);        // partials
-        carve<double>(z, st_bytes, 36 * (size_t)std::max(nchunks, 1));  // chunk partials
-        carve<double>(z, st_bytes, 3 * (size_t)nhl);                     // db
-        carve<double>(z, st_bytes, (size_t)sp * CB);                     // Linv
-        carve<int>(z, st_bytes, 16);                                // flags
-        if (prof_ts) carve<unsigned long long>(z, st_bytes, 8 * 2 * 64 + 64);  // phase timestamps
-        carve<uint8_t>(z, st_bytes, ne);                            // edge_bad
-        st_bytes += 256;
+    int mx_ge = 0, mx_gl = 1, mx_gu = 0, mx_nblk = 0, mx_nhp = 0, mx_chunks = 0, mx_pairs = 0, mx_red = 0;
+    for (int a = 0; a < NA; a++) {
+        const LbaHost &h = H[act[a]];
+        const InOff &o = io[a];
+        LbaDev &D = h_dev[a];
+        D = LbaDev{};
+        D.np = h.np;
+        D.npt = h.npt;
+        D.ne = h.ne;
+        D.nhp = h.nhp;
+        D.nhl = h.nhl;
+        D.nblk = h.nblk;
+        D.npairs = h.npairs;
+        D.n_cams = h.G->n_cams;
+        D.pose_fixed = osg_dptr<uint8_t>(din, o.fixed);
+        D.e_pose = osg_dptr<int32_t>(din, o.epose);
+        D.e_point = osg_dptr<int32_t>(din, o.epoint);
+        D.e_cam = osg_dptr<int32_t>(din, o.ecam);
+        D.e_kind = osg_dptr<int8_t>(din, o.ekind);
+        D.e_obs = osg_dptr<double>(din, o.eobs);
+        D.e_isig2 = osg_dptr<float>(din, o.eisig);
+        D.cams = osg_dptr<osg_camera>(din, o.cams);
+        D.pose_h = osg_dptr<int32_t>(din, o.poseh);
+        D.hp_pose = osg_dptr<int32_t>(din, o.hppose);
+        D.point_h = osg_dptr<int32_t>(din, o.pointh);
+        D.hl_point = osg_dptr<int32_t>(din, o.hlpoint);
+        D.lm_e_start = osg_dptr<int32_t>(din, o.lmes);
+        D.lm_e = osg_dptr<int32_t>(din, o.lme);
+        D.lm_b_start = osg_dptr<int32_t>(din, o.lmbs);
+        D.blk_pose = osg_dptr<int32_t>(din, o.blkpose);
+        D.edge_blk = osg_dptr<int32_t>(din, o.eblk);
+        D.hp_e_start = osg_dptr<int32_t>(din, o.hpes);
+        D.hp_e = osg_dptr<int32_t>(din, o.hpe);
+        D.hp_b_start = osg_dptr<int32_t>(din, o.hpbs);
+        D.hp_b = osg_dptr<int32_t>(din, o.hpb);
+        D.pair_start = osg_dptr<int32_t>(din, o.pairs);
+        D.pair_ab = osg_dptr<int32_t>(din, o.pairab);
+        D.nchunks = h.nchunks;
+        D.chunk_start = osg_dptr<int32_t>(din, o.chs);
+        D.blk_lm = osg_dptr<int32_t>(din, o.blklm);
+        D.blk_e_start = osg_dptr<int32_t>(din, o.blkes);
+        D.blk_e = osg_dptr<int32_t>(din, o.blke);
+        D.pair_chunk = osg_dptr<int32_t>(din, o.pch);
+        D.ge = h.ge;
+        D.gl = h.gl;
+        D.gu = h.gu;
+        D.nblk_red = h.nblk_red;
+        D.user_lambda = h.G->user_lambda_init;
+        size_t off = 0;
+        carve_state(dst + st_off[a], off, h, &D, prof_ts);
+        D.ctl = d_ctl + a;
+        D.out = d_out + 8 * a;
+        OSG_HIP_CHECK(ctx, hipMemcpyAsync(D.poseA, din + o.pose0, 56 * (size_t)h.np, hipMemcpyDeviceToDevice, ctx->stream));
+        OSG_HIP_CHECK(ctx, hipMemcpyAsync(D.pointA, din + o.point0, 24 * (size_t)h.npt, hipMemcpyDeviceToDevice, ctx->stream));
+        mx_ge = std::max(mx_ge, h.ge);
+        mx_gl = std::max(mx_gl, h.gl);
+        mx_gu = std::max(mx_gu, h.gu);
+        mx_nblk = std::max(mx_nblk, h.nblk);
+        mx_nhp = std::max(mx_nhp, h.nhp);
+        mx_chunks = std::max(mx_chunks, h.nchunks);
+        mx_pairs = std::max(mx_pairs, h.npairs);
+        mx_red = std::max(mx_red, h.nblk_red);
     }
-    char *dst = nullptr;
-    OSG_ALLOC(ctx, dst, SLOT_BA3, st_bytes);
-    double *poseA = carve<double>(dst, off, 7 * (size_t)np);
-    double *poseB = carve<double>(dst, off, 7 * (size_t)np);
-    double *pointA = carve<double>(dst, off, 3 * (size_t)npt);
-    double *pointB = carve<double>(dst, off, 3 * (size_t)npt);
-    LbaDev D = {};
-    D.np = np;
-    D.npt = npt;
-    D.ne = ne;
-    D.nhp = nhp;
-    D.nhl = nhl;
-    D.nblk = nblk;
-    D.npairs = npairs;
-    D.n_cams = G->n_cams;
-    D.pose_fixed = osg_dptr<uint8_t>(din, o_fixed);
-    D.e_pose = osg_dptr<int32_t>(din, o_epose);
-    D.e_point = osg_dptr<int32_t>(din, o_epoint);
-    D.e_cam = osg_dptr<int32_t>(din, o_ecam);
-    D.e_kind = osg_dptr<int8_t>(din, o_ekind);
-    D.e_obs = osg_dptr<double>(din, o_eobs);
-    D.e_isig2 = osg_dptr<float>(din, o_eisig);
-    D.cams = osg_dptr<osg_camera>(din, o_cams);
-    D.pose_h = osg_dptr<int32_t>(din, o_poseh);
-    D.hp_pose = osg_dptr<int32_t>(din, o_hppose);
-    D.point_h = osg_dptr<int32_t>(din, o_pointh);
-    D.hl_point = osg_dptr<int32_t>(din, o_hlpoint);
-    D.lm_e_start = osg_dptr<int32_t>(din, o_lmes);
-    D.lm_e = osg_dptr<int32_t>(din, o_lme);
-    D.lm_b_start = osg_dptr<int32_t>(din, o_lmbs);
-    D.blk_pose = osg_dptr<int32_t>(din, o_blkpose);
-    D.edge_blk = osg_dptr<int32_t>(din, o_eblk);
-    D.hp_e_start = osg_dptr<int32_t>(din, o_hpes);
-    D.hp_e = osg_dptr<int32_t>(din, o_hpe);
-    D.hp_b_start = osg_dptr<int32_t>(din, o_hpbs);
-    D.hp_b = osg_dptr<int32_t>(din, o_hpb);
-    D.pair_start = osg_dptr<int32_t>(din, o_pairs);
-    D.pair_ab = osg_dptr<int32_t>(din, o_pairab);
-    D.err = carve<double>(dst, off, 3 * (size_t)ne);
-    D.J = carve<double>(dst, off, EC * (size_t)ne);
-    D.Hll = carve<double>(dst, off, 9 * (size_t)nhl);
-    D.bl = carve<double>(dst, off, 3 * (size_t)nhl);
-    D.Hpl = carve<double>(dst, off, 18 * (size_t)nblk);
-    D.Hpp = carve<double>(dst, off, 36 * (size_t)nhp);
-    D.bp = carve<double>(dst, off, 6 * (size_t)nhp);
-    D.Dinv = carve<double>(dst, off, 9 * (size_t)nhl);
-    D.BDinv = carve<double>(dst, off, 18 * (size_t)nblk);
-    D.coef = carve<double>(dst, off, 6 * (size_t)nblk);
-    D.Hs = carve<double>(dst, off, (size_t)sp * sp);
-    D.bs = carve<double>(dst, off, (size_t)sp);
-    D.x = carve<double>(dst, off, (size_t)sp + 3 * (size_t)nhl);
-    D.part = carve<double>(dst, off, 3 * (size_t)NPART + 64);
-    D.chunk_part = carve<double>(dst, off, 36 * (size_t)std::max(nchunks, 1));
-    D.nchunks = nchunks;
-    D.chunk_start = osg_dptr<int32_t>(din, o_chs);
-    D.blk_lm = osg_dptr<int32_t>(din, o_blklm);
-    D.blk_e_start = osg_dptr<int32_t>(din, o_blkes);
-    D.blk_e = osg_dptr<int32_t>(din, o_blke);
-    D.db = carve<double>(dst, off, 3 * (size_t)nhl);
-    D.pair_chunk = osg_dptr<int32_t>(din, o_pch);
-    D.Linv = carve<double>(dst, off, (size_t)sp * CB);
-    D.flag = carve<int>(dst, off, 16);
-    D.tstamp = nullptr;
-    if (prof_ts) D.tstamp = carve<unsigned long long>(dst, off, 8 * 2 * 64 + 64);
-    uint8_t *d_bad = carve<uint8_t>(dst, off, ne);
-    OSG_HIP_CHECK(ctx, hipMemcpyAsync(poseA, din + o_pose0, 56 * (size_t)np, hipMemcpyDeviceToDevice, ctx->stream));
-    OSG_HIP_CHECK(ctx, hipMemcpyAsync(pointA, din + o_point0, 24 * (size_t)npt, hipMemcpyDeviceToDevice, ctx->stream));
-
-    const int ge = (ne + EB - 1) / EB;
-    const int gl = (nhl + EB - 1) / EB;
-    const int gu = (std::max(std::max(nhl, np), npt) + EB - 1) / EB;
-    OSG_REQUIRE(ctx, ge <= NPART && gu <= NPART && gl + nhp <= NPART, "graph too large for the partial buffers");
-    double *h_part = (double *)(pin + ((pk.total + 255) & ~size_t(255)));
-    double *cur_pose = poseA, *cur_point = pointA, *new_pose = poseB, *new_point = pointB;
-
-    auto errors = [&](const double *poses, const double *points) -> int {
-        hipLaunchKernelGGL(k_errors, dim3(ge), dim3(EB), 0, ctx->stream, D, poses, points, 0);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
-    };
-    auto fetch = [&](size_t first, size_t count) -> int {
-        if (hipMemcpyAsync(h_part + first, D.part + first, sizeof(double) * count, hipMemcpyDeviceToHost,
-                           ctx->stream) != hipSuccess)
-            return -1;
-        return hipStreamSynchronize(ctx->stream) == hipSuccess ? 0 : -1;
-    };
-    auto sum_part = [&](size_t first, int count) {
-        double s = 0;
-        for (int i = 0; i < count; i++) s += h_part[first + i];
-        return s;
-    };
-
+    OSG_HIP_CHECK(ctx, hipMemcpyAsync(d_dev, h_dev, dev_bytes, hipMemcpyHostToDevice, ctx->stream));
     const double t_upload = ms_since(tp0) - t_struct;
     const auto tp1 = std::chrono::steady_clock::now();
-    // initial chi2 (activeRobustChi2 before optimising)
-    D.pose_cur = cur_pose;
-    D.point_cur = cur_point;
-    if (errors(cur_pose, cur_point) || fetch(0, ge)) return osg_set_error(ctx, OSG_E_HIP, "k_errors");
-    double currentChi = sum_part(0, ge);
-    R->chi2_initial = currentChi;
-    bool errors_current = true;  // err[] holds the current estimate's errors
-    double lambda = 0, ni = 2;
-    int nBad = 0, iters = 0, trials = 0;
-    const int max_it = G->iterations;
-    bool ok = true;
-    for (int it = 0; it < max_it && !(stop && *stop) && ok; it++) {
-        D.pose_cur = cur_pose;
-        D.point_cur = cur_point;
-        if (!errors_current) {
-            if (errors(cur_pose, cur_point) || fetch(0, ge)) return osg_set_error(ctx, OSG_E_HIP, "k_errors");
-            currentChi = sum_part(0, ge);
+
+    // one lockstep step: every kernel once for all graphs, then 5 scalars per graph back
+    auto run_step = [&]() -> int {
+        OSG_HIP_CHECK(ctx, hipMemcpyAsync(d_ctl, h_ctl, ctl_bytes, hipMemcpyHostToDevice, ctx->stream));
+        const dim3 yb(1, NA);
+        auto gx = [&](int n) { return dim3(std::max(n, 1), NA); };
+        hipLaunchKernelGGL(k_errors, gx(mx_ge), dim3(EB), 0, ctx->stream, d_dev, 1);
+        hipLaunchKernelGGL(k_linearize, gx(mx_ge), dim3(EB), 0, ctx->stream, d_dev);
+        hipLaunchKernelGGL(k_point_red, gx(mx_gl), dim3(EB), 0, ctx->stream, d_dev);
+        if (mx_nblk > 0) hipLaunchKernelGGL(k_block_red, gx((mx_nblk + EB - 1) / EB), dim3(EB), 0, ctx->stream, d_dev);
+        if (mx_nhp > 0) hipLaunchKernelGGL(k_pose_red, gx(mx_nhp), dim3(EB), 0, ctx->stream, d_dev);
+        hipLaunchKernelGGL(k_lambda_init, yb, dim3(64), 0, ctx->stream, d_dev);
+        hipLaunchKernelGGL(k_schur_point, gx(mx_gl), dim3(EB), 0, ctx->stream, d_dev);
+        if (mx_nblk > 0) hipLaunchKernelGGL(k_schur_block, gx((mx_nblk + EB - 1) / EB), dim3(EB), 0, ctx->stream, d_dev);
+        if (mx_nhp > 0) {
+            if (mx_chunks > 0) hipLaunchKernelGGL(k_schur_chunks, gx((mx_chunks * 64 + 255) / 256), dim3(256), 0, ctx->stream, d_dev);
+            hipLaunchKernelGGL(k_schur_pairs, gx((mx_pairs * 64 + 255) / 256), dim3(256), 0, ctx->stream, d_dev);
+            hipLaunchKernelGGL(k_bschur, gx(mx_nhp), dim3(256), 0, ctx->stream, d_dev);
+            for (int jb = 0; jb < mx_red; jb++)  // row blocks at and below the diagonal block
+                hipLaunchKernelGGL(k_chol_col, gx(mx_red - jb), dim3(256), 0, ctx->stream, d_dev, jb);
+            hipLaunchKernelGGL(k_chol_back, yb, dim3(1024), 0, ctx->stream, d_dev);
         }
-        const double iniChi = currentChi;
-        hipLaunchKernelGGL(k_linearize, dim3(ge), dim3(EB), 0, ctx->stream, D);
-        hipLaunchKernelGGL(k_point_red, dim3(std::max(gl, 1)), dim3(EB), 0, ctx->stream, D);
-        if (nblk > 0) hipLaunchKernelGGL(k_block_red, dim3((nblk + EB - 1) / EB), dim3(EB), 0, ctx->stream, D);
-        if (nhp > 0) hipLaunchKernelGGL(k_pose_red, dim3(nhp), dim3(EB), 0, ctx->stream, D, 2 * NPART + gl);
+        hipLaunchKernelGGL(k_update, gx(mx_gu), dim3(EB), 0, ctx->stream, d_dev);
+        hipLaunchKernelGGL(k_errors, gx(mx_ge), dim3(EB), 0, ctx->stream, d_dev, 0);
+        hipLaunchKernelGGL(k_step_reduce, yb, dim3(64), 0, ctx->stream, d_dev);
         OSG_HIP_CHECK(ctx, hipGetLastError());
-        if (it == 0) {
-            if (fetch(2 * NPART, (size_t)gl + nhp)) return osg_set_error(ctx, OSG_E_HIP, "diag fetch");
-            if (G->user_lambda_init > 0) lambda = G->user_lambda_init;
-            else {
-                double md = 0;
-                for (int i = 0; i < gl + nhp; i++) md = std::max(md, h_part[2 * NPART + i]);
-                lambda = 1e-5 * md;
-            }
-            ni = 2;
-            nBad = 0;
-        }
-        double rho = 0;
-        int qmax = 0;
-        do {
-            trials++;
-            hipLaunchKernelGGL(k_schur_point, dim3(std::max(gl, 1)), dim3(EB), 0, ctx->stream, D, lambda);
-            if (nblk > 0) hipLaunchKernelGGL(k_schur_block, dim3((nblk + EB - 1) / EB), dim3(EB), 0, ctx->stream, D);
-            if (nhp > 0) {
-                if (nchunks > 0)
-                    hipLaunchKernelGGL(k_schur_chunks, dim3((nchunks * 64 + 255) / 256), dim3(256), 0, ctx->stream, D);
-                hipLaunchKernelGGL(k_schur_pairs, dim3((npairs * 64 + 255) / 256), dim3(256), 0, ctx->stream, D, lambda);
-                hipLaunchKernelGGL(k_bschur, dim3(nhp), dim3(256), 0, ctx->stream, D);
-                const int nred = 6 * nhp;
-                const int nblk_red = (nred + CB - 1) / CB;
-                for (int jb = 0; jb < nblk_red; jb++)  // row blocks at and below the diagonal block
-                    hipLaunchKernelGGL(k_chol_col, dim3(nblk_red - jb), dim3(256), 0, ctx->stream, D, jb);
-                hipLaunchKernelGGL(k_chol_back, dim3(1), dim3(1024), 0, ctx->stream, D);
-            }
-            D.pose_new = new_pose;
-            D.point_new = new_point;
-            hipLaunchKernelGGL(k_update, dim3(gu), dim3(EB), 0, ctx->stream, D, lambda);
-            OSG_HIP_CHECK(ctx, hipGetLastError());
-            if (errors(new_pose, new_point)) return osg_set_error(ctx, OSG_E_HIP, "k_errors");
-            // one download: chi partials, scale partials, cholesky flag
-            OSG_HIP_CHECK(ctx, hipMemcpyAsync(h_part, D.part, sizeof(double) * 2 * NPART, hipMemcpyDeviceToHost, ctx->stream));
-            int hflag = 1;
-            if (nhp > 0) OSG_HIP_CHECK(ctx, hipMemcpyAsync(&hflag, D.flag, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-            OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
-            if (prof_ts && !ts_printed && nhp > 0) {
-                ts_printed = 1;
-                const int nbr = (6 * nhp + CB - 1) / CB;
-                std::vector<unsigned long long> h(8 * 2 * nbr);
-                OSG_HIP_CHECK(ctx, hipMemcpy(h.data(), D.tstamp, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
-                {
-                    std::vector<unsigned long long> hb(64);
-                    OSG_HIP_CHECK(ctx, hipMemcpy(hb.data(), D.tstamp + 8 * 2 * 32, sizeof(unsigned long long) * 64, hipMemcpyDeviceToHost));
-                    fprintf(stderr, "[osg back] staging %.2f us;", (hb[41] - hb[0]) * 0.01);
-                    for (int bb = nbr - 1; bb >= 0; bb--)
-                        fprintf(stderr, " b%d@%.2f", bb, (hb[1 + bb] - hb[0]) * 0.01);
-                    fprintf(stderr, " end@%.2f\n", (hb[40] - hb[0]) * 0.01);
+        OSG_HIP_CHECK(ctx, hipMemcpyAsync(h_out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
+        OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+        return OSG_OK;
+    };
+
+    // initial chi2 (activeRobustChi2 before optimising): a step with only M_ERRC
+    for (int a = 0; a < NA; a++) h_ctl[a] = LbaCtl{M_ERRC, 0, 0.0};
+    {
+        const int rc = run_step();
+        if (rc < 0) return rc;
+    }
+    for (int a = 0; a < NA; a++) {
+        LbaHost &h = H[act[a]];
+        h.currentChi = h_out[8 * a + 4];
+        h.R->chi2_initial = h.currentChi;
+        h.errors_current = true;
+    }
+    int steps = 0;
+    bool ts_printed = false;
+    for (;;) {
+        const bool stopped = stop && *stop;
+        int n_run = 0;
+        for (int a = 0; a < NA; a++) {
+            LbaHost &h = H[act[a]];
+            LbaCtl &c = h_ctl[a];
+            c = LbaCtl{0, h.sel, h.lambda};
+            if (h.done) continue;
+            if (h.new_iter) {
+                // sparse_optimizer.cpp optimize(): for (i < iterations && !terminate() && ok)
+                if (h.it >= h.G->iterations || stopped) {
+                    h.done = true;
+                    continue;
                 }
-                for (int jb = 0; jb < nbr; jb++)
-                    for (int tt = 0; tt < 2 && tt < nbr - jb; tt++) {
-                        const unsigned long long *q = &h[8 * (2 * jb + tt)];
-                        fprintf(stderr, "[osg chol] j=%d wg=%d gemm %.2f factor+inverse %.2f tail %.2f us\n", jb, tt,
-                                (q[1] - q[0]) * 0.01, (q[2] - q[1]) * 0.01, (q[3] - q[2]) * 0.01);
-                    }
+                c.mode = M_LIN | M_ACT | (h.errors_current ? 0 : M_ERRC) | (h.it == 0 ? M_INIT : 0);
+            } else {
+                c.mode = M_ACT;  // another trial (the loop condition was evaluated after the last one)
             }
-            double tempChi = sum_part(0, ge);
-            if (!hflag) tempChi = DBL_MAX;
-            rho = currentChi - tempChi;
-            double scale = sum_part(NPART, gu) + 1e-3;
+            n_run++;
+        }
+        if (n_run == 0) break;
+        {
+            const int rc = run_step();
+            if (rc < 0) return rc;
+        }
+        steps++;
+        if (prof_ts && !ts_printed && H[act[0]].nhp > 0) {
+            ts_printed = true;
+            const LbaDev &D0 = h_dev[0];
+            const int nbr = H[act[0]].nblk_red;
+            std::vector<unsigned long long> hts(8 * 2 * nbr);
+            OSG_HIP_CHECK(ctx, hipMemcpy(hts.data(), D0.tstamp, sizeof(unsigned long long) * hts.size(), hipMemcpyDeviceToHost));
+            std::vector<unsigned long long> hb(64);
+            OSG_HIP_CHECK(ctx, hipMemcpy(hb.data(), D0.tstamp + 8 * 2 * 32, sizeof(unsigned long long) * 64, hipMemcpyDeviceToHost));
+            fprintf(stderr, "[osg back] staging %.2f us;", (hb[41] - hb[0]) * 0.01);
+            for (int bb = nbr - 1; bb >= 0; bb--) fprintf(stderr, " b%d@%.2f", bb, (hb[1 + bb] - hb[0]) * 0.01);
+            fprintf(stderr, " end@%.2f\n", (hb[40] - hb[0]) * 0.01);
+            for (int jb = 0; jb < nbr; jb++)
+                for (int tt = 0; tt < 2 && tt < nbr - jb; tt++) {
+                    const unsigned long long *q = &hts[8 * (2 * jb + tt)];
+                    fprintf(stderr, "[osg chol] j=%d wg=%d gemm %.2f factor+inverse %.2f tail %.2f us\n", jb, tt,
+                            (q[1] - q[0]) * 0.01, (q[2] - q[1]) * 0.01, (q[3] - q[2]) * 0.01);
+                }
+        }
+        // optimization_algorithm_levenberg.cpp:61-176, per graph
+        for (int a = 0; a < NA; a++) {
+            LbaHost &h = H[act[a]];
+            const int mode = h_ctl[a].mode;
+            if (!(mode & M_ACT)) continue;
+            const double *o = h_out + 8 * a;
+            if (mode & M_ERRC) h.currentChi = o[4];
+            if (h.new_iter) {
+                h.iniChi = h.currentChi;
+                if (mode & M_INIT) {
+                    h.lambda = o[3];
+                    h.ni = 2;
+                    h.nBad = 0;
+                }
+                h.qmax = 0;
+                h.new_iter = false;
+            }
+            h.trials++;
+            double tempChi = o[0];
+            if (o[2] == 0.0) tempChi = DBL_MAX;
+            double rho = h.currentChi - tempChi;
+            const double scale = o[1] + 1e-3;
             rho /= scale;
             if (rho > 0 && std::isfinite(tempChi)) {
                 double alpha = 1. - std::pow((2 * rho - 1), 3);
                 alpha = std::min(alpha, 2. / 3.);
                 const double scaleFactor = std::max(1. / 3., alpha);
-                lambda *= scaleFactor;
-                ni = 2;
-                currentChi = tempChi;
-                std::swap(cur_pose, new_pose);
-                std::swap(cur_point, new_point);
-                errors_current = true;
+                h.lambda *= scaleFactor;
+                h.ni = 2;
+                h.currentChi = tempChi;
+                h.sel ^= 1;  // the trial estimate becomes current
+                h.errors_current = true;
             } else {
-                lambda *= ni;
-                ni *= 2;
-                errors_current = false;  // err[] holds the rejected estimate's errors
+                h.lambda *= h.ni;
+                h.ni *= 2;
+                h.errors_current = false;  // err[] holds the rejected estimate's errors
             }
-            qmax++;
-        } while (rho < 0 && qmax < 10 && !(stop && *stop));
-        iters++;
-        if (qmax == 10 || rho == 0) ok = false;
-        else {
-            if ((iniChi - currentChi) * 1e3 < iniChi) nBad++;
-            else nBad = 0;
-            if (nBad >= 3) ok = false;
+            h.rho = rho;
+            h.qmax++;
+            const bool again = rho < 0 && h.qmax < 10 && !(stop && *stop);
+            if (again) continue;
+            // iteration done
+            h.iters++;
+            h.it++;
+            h.new_iter = true;
+            if (h.qmax == 10 || rho == 0) {
+                h.done = true;
+            } else {
+                if ((h.iniChi - h.currentChi) * 1e3 < h.iniChi) h.nBad++;
+                else h.nBad = 0;
+                if (h.nBad >= 3) h.done = true;
+            }
         }
     }
     if (prof)
-        fprintf(stderr, "[osg lba] structure %.3f ms (index %.3f, lm csr %.3f, blocks %.3f, pose csr %.3f, pairs %.3f), pack+upload %.3f ms, LM %.3f ms (%d it, %d trials), pairs %d contrib %d\n",
-                t_struct, t_s0, t_s1 - t_s0, t_s2 - t_s1, t_s3 - t_s2, t_struct - t_s3, t_upload, ms_since(tp1), iters, trials, npairs, pair_start[npairs]);
-    R->iterations = iters;
-    R->trials = trials;
-    R->aborted = (stop && *stop) ? 1 : 0;
-    R->chi2_final = currentChi;
-    // classification with the last computed errors; estimates out
-    D.pose_cur = cur_pose;
-    D.point_cur = cur_point;
-    hipLaunchKernelGGL(k_classify, dim3(ge), dim3(EB), 0, ctx->stream, D, cur_pose, cur_point, d_bad);
+        fprintf(stderr, "[osg lba] %d graphs: structure %.3f ms (graph 0: %.3f ms), pack+upload %.3f ms, LM %.3f ms "
+                        "(%d lockstep steps)\n",
+                NA, t_struct, H[act[0]].t_struct, t_upload, ms_since(tp1), steps);
+    // classification with the last computed errors (current estimate's, or the rejected trial's,
+    // exactly as the reference's computeActiveErrors order leaves them); estimates out
+    for (int a = 0; a < NA; a++) h_ctl[a] = LbaCtl{M_FIN, H[act[a]].sel, 0.0};
+    OSG_HIP_CHECK(ctx, hipMemcpyAsync(d_ctl, h_ctl, ctl_bytes, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_classify, dim3(std::max(mx_ge, 1), NA), dim3(EB), 0, ctx->stream, d_dev);
     OSG_HIP_CHECK(ctx, hipGetLastError());
-    OSG_HIP_CHECK(ctx, hipMemcpyAsync(R->pose, cur_pose, 56 * (size_t)np, hipMemcpyDeviceToHost, ctx->stream));
-    OSG_HIP_CHECK(ctx, hipMemcpyAsync(R->point, cur_point, 24 * (size_t)npt, hipMemcpyDeviceToHost, ctx->stream));
-    OSG_HIP_CHECK(ctx, hipMemcpyAsync(R->edge_bad, d_bad, ne, hipMemcpyDeviceToHost, ctx->stream));
+    int total_iters = 0;
+    for (int a = 0; a < NA; a++) {
+        LbaHost &h = H[act[a]];
+        const LbaDev &D = h_dev[a];
+        osg_ba_result *R = h.R;
+        R->iterations = h.iters;
+        R->trials = h.trials;
+        R->aborted = (stop && *stop) ? 1 : 0;
+        R->chi2_final = h.currentChi;
+        total_iters += h.iters;
+        OSG_HIP_CHECK(ctx, hipMemcpyAsync(R->pose, h.sel ? D.poseB : D.poseA, 56 * (size_t)h.np, hipMemcpyDeviceToHost,
+                                          ctx->stream));
+        OSG_HIP_CHECK(ctx, hipMemcpyAsync(R->point, h.sel ? D.pointB : D.pointA, 24 * (size_t)h.npt,
+                                          hipMemcpyDeviceToHost, ctx->stream));
+        OSG_HIP_CHECK(ctx, hipMemcpyAsync(R->edge_bad, D.bad, h.ne, hipMemcpyDeviceToHost, ctx->stream));
+    }
     OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
-    return iters;
+    return B == 1 ? results[0].iterations : total_iters;
+}
+
+}  // namespace
+
+extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, osg_ba_result *R,
+                                           const volatile uint8_t *stop)
+{
+    return lba_batch(ctx, G, R, 1, stop);
+}
+
+extern "C" int osg_local_bundle_adjustment_batch(osg_ctx *ctx, const osg_ba_graph *graphs, int32_t n_graphs,
+                                                 osg_ba_result *results, const volatile uint8_t *stop)
+{
+    return lba_batch(ctx, graphs, results, n_graphs, stop);
 }

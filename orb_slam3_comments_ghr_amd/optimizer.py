@@ -262,6 +262,24 @@ class Optimizer:
         self.ctx.check(rc, "LocalBundleAdjustment")
         return BAResult(pose, point, bad, R.iterations, R.trials, R.chi2_initial, R.chi2_final, R.aborted)
 
+    def LocalBundleAdjustmentBatch(self, graphs, stop_flag: np.ndarray | None = None) -> list:
+        """B independent windows in lockstep, one launch per kernel per LM trial for all of them
+        (no reference counterpart; each graph follows the single-graph LM exactly)."""
+        lib, h = self.ctx.lib, self.ctx.handle
+        B = len(graphs)
+        made = [make_ba_result(G) for G in graphs]
+        gs = (_abi.OsgBaGraph * B)(*[G.struct() for G in graphs])
+        rs = (_abi.OsgBaResult * B)(*[m[0] for m in made])
+        if stop_flag is not None:
+            assert stop_flag.dtype == np.uint8, "stop flag is one byte (bool *pbStopFlag)"
+        sf = None if stop_flag is None else _p(stop_flag)
+        rc = lib.osg_local_bundle_adjustment_batch(h, C.addressof(gs), B, C.addressof(rs), sf)
+        self.ctx.check(rc, "LocalBundleAdjustment batch")
+        out = []
+        for (R0, pose, point, bad), R in zip(made, rs):
+            out.append(BAResult(pose, point, bad, R.iterations, R.trials, R.chi2_initial, R.chi2_final, R.aborted))
+        return out
+
 
 def oracle_lba(oracle, G: BAGraph, stop_flag=None) -> BAResult:
     R, pose, point, bad = make_ba_result(G)

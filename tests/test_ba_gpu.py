@@ -147,3 +147,40 @@ def test_lba_c4_full_size(ctx, oracle):
     G = op.synth_lba_graph(rng, n_kf=50, n_points=10000)
     got, ref = check_lba(ctx, oracle, G)
     assert got.iterations >= 1
+
+
+def test_lba_batch_equals_single_calls(ctx, oracle):
+    """Lockstep batch of heterogeneous windows: every graph's result equals its own single call
+    exactly (same kernels, per-graph deterministic reductions) and the oracle within tolerance."""
+    rng = np.random.default_rng(31)
+    graphs = [op.synth_lba_graph(rng, n_kf=int(k), n_points=int(p), stereo_frac=s)
+              for k, p, s in [(5, 300, 0.0), (12, 900, 0.3), (8, 600, 1.0), (20, 2000, 0.0), (6, 400, 0.0)]]
+    graphs[2].user_lambda_init = 100.0
+    graphs[4].pose_fixed[:] = 1
+    opt = op.Optimizer(ctx)
+    batch = opt.LocalBundleAdjustmentBatch(graphs)
+    for i, (G, got) in enumerate(zip(graphs, batch)):
+        single = opt.LocalBundleAdjustment(G)
+        assert (got.iterations, got.trials) == (single.iterations, single.trials), i
+        assert got.chi2_initial == single.chi2_initial and got.chi2_final == single.chi2_final, i
+        np.testing.assert_array_equal(got.pose, single.pose)
+        np.testing.assert_array_equal(got.point, single.point)
+        np.testing.assert_array_equal(got.edge_bad, single.edge_bad)
+        ref = op.oracle_lba(oracle, G)
+        assert abs(got.iterations - ref.iterations) <= 1
+        np.testing.assert_allclose(got.pose, ref.pose, atol=STATE_TOL, rtol=0)
+        np.testing.assert_array_equal(got.edge_bad, ref.edge_bad)
+
+
+def test_lba_batch_c4_windows(ctx, oracle):
+    """8 C4-sized windows (50 KF x 10k points) in one batch against the oracle."""
+    rng = np.random.default_rng(0x0B5EED04 + 7)
+    graphs = [op.synth_lba_graph(rng, n_kf=50, n_points=10000) for _ in range(8)]
+    got = op.Optimizer(ctx).LocalBundleAdjustmentBatch(graphs)
+    for G, g in zip(graphs, got):
+        ref = op.oracle_lba(oracle, G)
+        assert abs(g.iterations - ref.iterations) <= 1
+        assert trials_close(g.trials, ref.trials)
+        np.testing.assert_allclose(g.pose, ref.pose, atol=STATE_TOL, rtol=0)
+        np.testing.assert_allclose(g.point, ref.point, atol=STATE_TOL, rtol=0)
+        np.testing.assert_array_equal(g.edge_bad, ref.edge_bad)
