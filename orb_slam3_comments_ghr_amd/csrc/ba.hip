@@ -9,21 +9,24 @@
 //   (free pose, point) pair; CSR of edges per point and per pose; for every pose pair (i <= j)
 //   the list of (block_i, block_j) contributions in landmark order (the Schur outer loop order).
 //
+// Batches: B independent graphs run in lockstep, one launch of each kernel per LM trial for all of
+// them (grid.y = graph; a graph that skips a kernel this step leaves at once).
 // Per LM iteration (device):
 //   k_errors      per edge: error, Huber rho -> per-workgroup chi2 partials        (HBM/latency)
-//   k_linearize   per edge: Jacobians -> the edge's Hpp/b_p/Hll/b_l/Hpl terms      (FP64 VALU)
-//   k_point_red   per point: sums Hll, b_l and its Hpl blocks                      (segmented, no atomics)
+//   k_linearize   per landmark: its edges' Jacobians -> Hll, b_l, the Hpl blocks, and each edge's
+//                 pose part (Hpp upper + b_p) for k_pose_red                       (FP64 VALU)
 //   k_pose_red    per pose: Hpp, b_p from its edges (workgroup reduction)
-// Per LM trial (lambda known on the host):
-//   k_schur_point per point: Dinv = (Hll + lambda I)^-1, BDinv = Hpl Dinv, coef = Hpl Dinv b_l
-//   k_schur_pairs per pose pair (i <= j), one wave: S_ij = sum_p BDinv_ip Hpl_jp^T ; writes the
-//                 dense reduced camera matrix Hpp + lambda I - S and b_schur
-//   k_chol_*      blocked Cholesky of the reduced system (n = 6 x free poses): panel kernel,
-//                 FP64-MFMA trailing SYRK, blocked triangular solves
+// Per LM trial:
+//   k_schur_point / k_schur_block   Dinv = (Hll + lambda I)^-1, BDinv = Hpl Dinv, coef
+//   k_schur_chunks / k_schur_pairs  S_ij = sum_p BDinv_ip Hpl_jp^T over fixed chunks, then the dense
+//                 reduced camera matrix Hpp + lambda I - S and b_schur (k_bschur)
+//   k_chol_col x ceil(n/32), k_chol_back   left-looking blocked Cholesky (FP64 MFMA tile updates),
+//                 forward solve fused, backward solve
 //   k_update      per point: x_l = Dinv (b_l - Hpl^T x_p), new estimates (poses: exp(x) * T)
-//                 and the LM scale sum;  then k_errors on the new estimates -> tempChi
-// The host reads back 3 scalars per trial and runs the accept / reject / lambda logic exactly as
-// the reference; push/pop is a swap of the current / trial estimate buffers.
+//                 and the LM scale sum;  then k_errors on the new estimates
+//   k_step_reduce the step's scalars per graph (chi2 of trial and current, scale, lambda, pivot flag)
+// The host reads back 5 scalars per graph per trial and runs the accept / reject / lambda logic
+// exactly as the reference; push/pop is a swap of the current / trial estimate buffers.
 #include <algorithm>
 #include <cfloat>
 #include <chrono>
@@ -162,67 +165,15 @@ __global__ __launch_bounds__(EB) void k_errors(const LbaDev *__restrict__ Ds, in
     if (threadIdx.x == 0) D.part[part_off + blockIdx.x] = t;
 }
 
-// per edge: Jacobians and the edge's quadratic-form contributions (ref:Thirdparty/g2o/g2o/core/
-// base_binary_edge.hpp:55-120, robust branch): C[e] = {Hpp 21 (upper), b_p 6, Hll 6 (upper),
-// b_l 3, Hpl 18 (6x3)} = 54 doubles; the reductions below only sum them.
-constexpr int EC = 54;
+// Linearisation, landmark-major: one thread per landmark walks its edges in edge order (ref:
+// Thirdparty/g2o/g2o/core/base_binary_edge.hpp:55-120, robust branch) and
+//   * sums Hll (upper 6) and b_l in registers (the order of a per-landmark reduction over lm_e),
+//   * writes each Hpl block: a block's edges are in edge order inside its landmark, so the first
+//     edge stores and the others add (the order of a per-block reduction over blk_e),
+//   * writes the edge's pose part {Hpp upper 21, b_p 6} = EC doubles to J for k_pose_red,
+// and the workgroup's max |diag Hll| for computeLambdaInit.
+constexpr int EC = 27;
 __global__ __launch_bounds__(EB) void k_linearize(const LbaDev *__restrict__ Ds)
-{
-    LBA_GRAPH(M_LIN);
-    const int e = blockIdx.x * EB + threadIdx.x;
-    if (e >= D.ne) return;
-    const int k = D.e_kind[e];
-    const SE3 T = se3_from7(cur_pose(D) + 7 * (size_t)D.e_pose[e]);
-    const double *X = cur_point(D) + 3 * (size_t)D.e_point[e];
-    double Jp[3][6], Jx[3][3];
-    edge_jacobians(k, true, D.cams[D.e_cam[e]], T, X, Jp, Jx);
-    const int dim = (k == OSG_EDGE_STEREO) ? 3 : 2;
-    const double w = edge_w(D, e);
-    const double ev[3] = {D.err[3 * e], D.err[3 * e + 1], D.err[3 * e + 2]};
-    double delta, r0, rho1;
-    float dsqr;
-    kind_delta(k, delta, dsqr);
-    huber(chi2_of(ev, dim, w), delta, dsqr, r0, rho1);
-    const double ww = rho1 * w;
-    double om[3];
-    for (int d = 0; d < 3; d++) om[d] = (d < dim) ? -(w * ev[d]) * rho1 : 0.0;
-    if (dim == 2) {
-        for (int j = 0; j < 6; j++) Jp[2][j] = 0.0;
-        for (int j = 0; j < 3; j++) Jx[2][j] = 0.0;
-    }
-    double *o = D.J + EC * (size_t)e;
-    int c = 0;
-    for (int a = 0; a < 6; a++)
-        for (int bb = a; bb < 6; bb++)
-            o[c++] = Jp[0][a] * ww * Jp[0][bb] + Jp[1][a] * ww * Jp[1][bb] + Jp[2][a] * ww * Jp[2][bb];
-    for (int a = 0; a < 6; a++) o[c++] = Jp[0][a] * om[0] + Jp[1][a] * om[1] + Jp[2][a] * om[2];
-    for (int a = 0; a < 3; a++)
-        for (int bb = a; bb < 3; bb++)
-            o[c++] = Jx[0][a] * ww * Jx[0][bb] + Jx[1][a] * ww * Jx[1][bb] + Jx[2][a] * ww * Jx[2][bb];
-    for (int a = 0; a < 3; a++) o[c++] = Jx[0][a] * om[0] + Jx[1][a] * om[1] + Jx[2][a] * om[2];
-    for (int a = 0; a < 6; a++)
-        for (int bb = 0; bb < 3; bb++)
-            o[c++] = Jp[0][a] * ww * Jx[0][bb] + Jp[1][a] * ww * Jx[1][bb] + Jp[2][a] * ww * Jx[2][bb];
-}
-
-// per block: Hpl = sum of its edges' contributions (usually one edge; mono + body of one
-// keyframe share a block)
-__global__ __launch_bounds__(EB) void k_block_red(const LbaDev *__restrict__ Ds)
-{
-    LBA_GRAPH(M_LIN);
-    const int blk = blockIdx.x * EB + threadIdx.x;
-    if (blk >= D.nblk) return;
-    double h[18];
-    for (int i = 0; i < 18; i++) h[i] = 0.0;
-    for (int q = D.blk_e_start[blk]; q < D.blk_e_start[blk + 1]; q++) {
-        const double *C = D.J + EC * (size_t)D.blk_e[q];
-        for (int i = 0; i < 18; i++) h[i] += C[36 + i];
-    }
-    for (int i = 0; i < 18; i++) D.Hpl[18 * (size_t)blk + i] = h[i];
-}
-
-// per landmark: Hll (3x3) and b_l (sums of edge contributions)
-__global__ __launch_bounds__(EB) void k_point_red(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_LIN);
     if ((int)blockIdx.x >= max(D.gl, 1)) return;
@@ -230,16 +181,54 @@ __global__ __launch_bounds__(EB) void k_point_red(const LbaDev *__restrict__ Ds)
     const int l = blockIdx.x * EB + threadIdx.x;
     double md = 0.0;
     if (l < D.nhl) {
-        double H6[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
+        const double *X = cur_point(D) + 3 * (size_t)D.hl_point[l];
+        const double *poses = cur_pose(D);
+        double H6[6] = {0, 0, 0, 0, 0, 0}, bl3[3] = {0, 0, 0};
         for (int q = D.lm_e_start[l]; q < D.lm_e_start[l + 1]; q++) {
             const int e = D.lm_e[q];
-            const double *C = D.J + EC * (size_t)e;
-            for (int i = 0; i < 6; i++) H6[i] += C[27 + i];
-            for (int i = 0; i < 3; i++) b[i] += C[33 + i];
+            const int k = D.e_kind[e];
+            const SE3 T = se3_from7(poses + 7 * (size_t)D.e_pose[e]);
+            double Jp[3][6], Jx[3][3];
+            edge_jacobians(k, true, D.cams[D.e_cam[e]], T, X, Jp, Jx);
+            const int dim = (k == OSG_EDGE_STEREO) ? 3 : 2;
+            const double w = edge_w(D, e);
+            const double ev[3] = {D.err[3 * e], D.err[3 * e + 1], D.err[3 * e + 2]};
+            double delta, r0, rho1;
+            float dsqr;
+            kind_delta(k, delta, dsqr);
+            huber(chi2_of(ev, dim, w), delta, dsqr, r0, rho1);
+            const double ww = rho1 * w;
+            double om[3];
+            for (int d = 0; d < 3; d++) om[d] = (d < dim) ? -(w * ev[d]) * rho1 : 0.0;
+            if (dim == 2) {
+                for (int j = 0; j < 6; j++) Jp[2][j] = 0.0;
+                for (int j = 0; j < 3; j++) Jx[2][j] = 0.0;
+            }
+            const int blk = D.edge_blk[e];
+            if (blk >= 0) {  // free pose: pose part and Hpl
+                double *o = D.J + EC * (size_t)e;
+                int c = 0;
+                for (int a = 0; a < 6; a++)
+                    for (int bb = a; bb < 6; bb++)
+                        o[c++] = Jp[0][a] * ww * Jp[0][bb] + Jp[1][a] * ww * Jp[1][bb] + Jp[2][a] * ww * Jp[2][bb];
+                for (int a = 0; a < 6; a++) o[c++] = Jp[0][a] * om[0] + Jp[1][a] * om[1] + Jp[2][a] * om[2];
+                const bool first = D.blk_e[D.blk_e_start[blk]] == e;
+                double *hp = D.Hpl + 18 * (size_t)blk;
+                for (int a = 0; a < 6; a++)
+                    for (int bb = 0; bb < 3; bb++) {
+                        const double v = Jp[0][a] * ww * Jx[0][bb] + Jp[1][a] * ww * Jx[1][bb] + Jp[2][a] * ww * Jx[2][bb];
+                        hp[3 * a + bb] = first ? v : hp[3 * a + bb] + v;
+                    }
+            }
+            int c = 0;
+            for (int a = 0; a < 3; a++)
+                for (int bb = a; bb < 3; bb++)
+                    H6[c++] += Jx[0][a] * ww * Jx[0][bb] + Jx[1][a] * ww * Jx[1][bb] + Jx[2][a] * ww * Jx[2][bb];
+            for (int a = 0; a < 3; a++) bl3[a] += Jx[0][a] * om[0] + Jx[1][a] * om[1] + Jx[2][a] * om[2];
         }
         const double H[9] = {H6[0], H6[1], H6[2], H6[1], H6[3], H6[4], H6[2], H6[4], H6[5]};
         for (int i = 0; i < 9; i++) D.Hll[9 * (size_t)l + i] = H[i];
-        for (int i = 0; i < 3; i++) D.bl[3 * (size_t)l + i] = b[i];
+        for (int i = 0; i < 3; i++) D.bl[3 * (size_t)l + i] = bl3[i];
         md = fmax(fabs(H[0]), fmax(fabs(H[4]), fabs(H[8])));
     }
     // max |diag| per workgroup for computeLambdaInit
@@ -372,44 +361,54 @@ __global__ __launch_bounds__(EB) void k_schur_block(const LbaDev *__restrict__ D
 //                   8 contributions' loads in flight per step -> chunk partial;
 //   k_schur_pairs   one wave per pair: sums its chunk partials in chunk order (deterministic),
 //                   writes Hs = Hpp + lambda I - S (both triangles) and b_schur.
-constexpr int SCH = 32;
+constexpr int SCH = 64;
+// One wave per chunk.  Lane = (group g = lane >> 2, quarter q = lane & 3): group g takes
+// contributions g, g + 16, ... of the chunk; quarter q owns rows 3 (q >> 1) .. + 2 and columns
+// 3 (q & 1) .. + 2 of the 6x6 product, so a lane loads 9 + 9 doubles for 27 FMAs (the former
+// 36-lane layout re-loaded every row six times).  The 16 groups are summed by a fixed xor
+// butterfly at the end of the chunk: deterministic.
 __global__ __launch_bounds__(256) void k_schur_chunks(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT);
     const int ch = (blockIdx.x * 256 + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (ch >= D.nchunks) return;
-    const int r = (lane < 36) ? lane / 6 : 0, c = (lane < 36) ? lane % 6 : 0;
+    const int g = lane >> 2, q = lane & 3;
+    const int r0 = 3 * (q >> 1), c0 = 3 * (q & 1);
     const double *__restrict__ BDv = D.BDinv;
     const double *__restrict__ Hv = D.Hpl;
     const int *__restrict__ ab = D.pair_ab;
     const int q0 = D.chunk_start[ch], q1 = D.chunk_start[ch + 1];
-    double acc = 0.0;
-    int q = q0;
-    for (; q + 7 < q1; q += 8) {
-        int a[8], b[8];
+    double acc[9];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-            a[u] = ab[2 * (q + u)];
-            b[u] = ab[2 * (q + u) + 1];
-        }
-        double t[8];
+    for (int i = 0; i < 9; i++) acc[i] = 0.0;
+    for (int qq = q0 + g; qq < q1; qq += 16) {
+        const int2 p = *(const int2 *)(ab + 2 * qq);
+        const double *BD = BDv + 18 * (size_t)p.x + 3 * r0;  // rows r0..r0+2 of BDinv_i (6x3)
+        const double *Bj = Hv + 18 * (size_t)p.y + 3 * c0;   // rows c0..c0+2 of Hpl_j (6x3)
+        double a[9], b[9];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const double *BD = BDv + 18 * (size_t)a[u] + 3 * r;
-            const double *Bj = Hv + 18 * (size_t)b[u] + 3 * c;
-            t[u] = BD[0] * Bj[0] + BD[1] * Bj[1] + BD[2] * Bj[2];
+        for (int i = 0; i < 9; i++) {
+            a[i] = BD[i];
+            b[i] = Bj[i];
         }
 #pragma unroll
-        for (int u = 0; u < 8; u++) acc += t[u];
+        for (int r = 0; r < 3; r++)
+#pragma unroll
+            for (int c = 0; c < 3; c++)
+                acc[3 * r + c] += a[3 * r] * b[3 * c] + a[3 * r + 1] * b[3 * c + 1] + a[3 * r + 2] * b[3 * c + 2];
     }
-    for (; q < q1; q++) {
-        const int a = ab[2 * q], b = ab[2 * q + 1];
-        const double *BD = BDv + 18 * (size_t)a + 3 * r;
-        const double *Bj = Hv + 18 * (size_t)b + 3 * c;
-        acc += BD[0] * Bj[0] + BD[1] * Bj[1] + BD[2] * Bj[2];
+#pragma unroll
+    for (int off = 4; off < 64; off <<= 1)
+#pragma unroll
+        for (int i = 0; i < 9; i++) acc[i] += __shfl_xor(acc[i], off);
+    if (g == 0) {
+        double *out = D.chunk_part + 36 * (size_t)ch;
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+#pragma unroll
+            for (int c = 0; c < 3; c++) out[6 * (r0 + r) + c0 + c] = acc[3 * r + c];
     }
-    if (lane < 36) D.chunk_part[36 * (size_t)ch + lane] = acc;
 }
 
 __global__ __launch_bounds__(256) void k_schur_pairs(const LbaDev *__restrict__ Ds)
@@ -945,22 +944,28 @@ __global__ __launch_bounds__(EB) void k_classify(const LbaDev *__restrict__ Ds)
 }
 
 // The step's scalars per graph, summed in the host's former order (sequential from index 0):
-// out = {chi of the trial, LM scale, Cholesky ok, lambda used, chi of the current estimate}
-__global__ void k_step_reduce(const LbaDev *__restrict__ Ds)
+// out = {chi of the trial, LM scale, Cholesky ok, lambda used, chi of the current estimate}.
+// The partials are first staged in LDS by all threads (one memory latency), then summed in order.
+__global__ __launch_bounds__(256) void k_step_reduce(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT | M_ERRC);
-    if (threadIdx.x != 0) return;
+    __shared__ double s_chi[NPART], s_sc[NPART], s_cur[NPART];
     const int mode = D.ctl->mode;
-    double chi = 0, sc = 0, chic = 0;
-    if (mode & M_ACT) {
-        for (int i = 0; i < D.ge; i++) chi += D.part[i];
-        for (int i = 0; i < D.gu; i++) sc += D.part[NPART + i];
+    const bool act = (mode & M_ACT) != 0, errc = (mode & M_ERRC) != 0;
+    for (int i = threadIdx.x; i < D.ge; i += 256) {
+        s_chi[i] = act ? D.part[i] : 0.0;
+        s_cur[i] = errc ? D.part[3 * NPART + i] : 0.0;
     }
-    if (mode & M_ERRC)
-        for (int i = 0; i < D.ge; i++) chic += D.part[3 * NPART + i];
+    for (int i = threadIdx.x; i < D.gu; i += 256) s_sc[i] = act ? D.part[NPART + i] : 0.0;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    double chi = 0, sc = 0, chic = 0;
+    for (int i = 0; i < D.ge; i++) chi += s_chi[i];
+    for (int i = 0; i < D.gu; i++) sc += s_sc[i];
+    for (int i = 0; i < D.ge; i++) chic += s_cur[i];
     D.out[0] = chi;
     D.out[1] = sc;
-    D.out[2] = (D.nhp > 0 && (mode & M_ACT)) ? (double)D.flag[0] : 1.0;
+    D.out[2] = (D.nhp > 0 && act) ? (double)D.flag[0] : 1.0;
     D.out[3] = D.ctl->lambda;
     D.out[4] = chic;
 }
@@ -996,6 +1001,33 @@ struct LbaHost {
     int nBad = 0, iters = 0, trials = 0, qmax = 0, it = 0, sel = 0;
     bool errors_current = true, new_iter = true, done = false;
     size_t o_in = 0, o_st = 0;  // offsets of this graph's inputs / state
+
+    // new call: scalars back to their initial values; the vectors keep their capacity (a batch of
+    // windows frees and re-faults hundreds of MB otherwise)
+    void reset()
+    {
+        G = nullptr;
+        R = nullptr;
+        np = npt = ne = nhp = nhl = nblk = npairs = nchunks = 0;
+        ge = gl = gu = nblk_red = 0;
+        trivial = false;
+        hp_pose.clear();
+        hl_point.clear();
+        blk_pose.clear();
+        chunk_start.clear();
+        t_struct = 0;
+        lambda = 0;
+        ni = 2;
+        currentChi = iniChi = rho = 0;
+        nBad = iters = trials = qmax = it = sel = 0;
+        errors_current = true;
+        new_iter = true;
+        done = false;
+    }
+};
+
+struct LbaCache {
+    std::vector<LbaHost> H;
 };
 
 int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
@@ -1240,7 +1272,10 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         return 0;
     }
     // ---- structures (host threads for a batch; each graph is independent)
-    std::vector<LbaHost> H(B);
+    if (!ctx->lba_cache) ctx->lba_cache = std::make_shared<LbaCache>();
+    std::vector<LbaHost> &H = static_cast<LbaCache *>(ctx->lba_cache.get())->H;
+    if ((int)H.size() < B) H.resize(B);
+    for (int b = 0; b < B; b++) H[b].reset();
     std::vector<int> rcs(B, OSG_OK);
     {
         auto work = [&](int b0, int b1) {
@@ -1330,7 +1365,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     char *pin = (char *)osg_pinned(ctx, in_pad + dev_bytes + ctl_bytes + out_bytes + 1024);
     if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
     OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
-    pk.fill(pin);
+    pk.fill_parallel(pin, std::min(16, std::max(1, (int)std::thread::hardware_concurrency())));
     LbaDev *h_dev = (LbaDev *)(pin + in_pad);
     LbaCtl *h_ctl = (LbaCtl *)((char *)h_dev + dev_bytes);
     double *h_out = (double *)((char *)h_ctl + ctl_bytes);
@@ -1415,9 +1450,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         const dim3 yb(1, NA);
         auto gx = [&](int n) { return dim3(std::max(n, 1), NA); };
         hipLaunchKernelGGL(k_errors, gx(mx_ge), dim3(EB), 0, ctx->stream, d_dev, 1);
-        hipLaunchKernelGGL(k_linearize, gx(mx_ge), dim3(EB), 0, ctx->stream, d_dev);
-        hipLaunchKernelGGL(k_point_red, gx(mx_gl), dim3(EB), 0, ctx->stream, d_dev);
-        if (mx_nblk > 0) hipLaunchKernelGGL(k_block_red, gx((mx_nblk + EB - 1) / EB), dim3(EB), 0, ctx->stream, d_dev);
+        hipLaunchKernelGGL(k_linearize, gx(mx_gl), dim3(EB), 0, ctx->stream, d_dev);
         if (mx_nhp > 0) hipLaunchKernelGGL(k_pose_red, gx(mx_nhp), dim3(EB), 0, ctx->stream, d_dev);
         hipLaunchKernelGGL(k_lambda_init, yb, dim3(64), 0, ctx->stream, d_dev);
         hipLaunchKernelGGL(k_schur_point, gx(mx_gl), dim3(EB), 0, ctx->stream, d_dev);
@@ -1432,7 +1465,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         }
         hipLaunchKernelGGL(k_update, gx(mx_gu), dim3(EB), 0, ctx->stream, d_dev);
         hipLaunchKernelGGL(k_errors, gx(mx_ge), dim3(EB), 0, ctx->stream, d_dev, 0);
-        hipLaunchKernelGGL(k_step_reduce, yb, dim3(64), 0, ctx->stream, d_dev);
+        hipLaunchKernelGGL(k_step_reduce, yb, dim3(256), 0, ctx->stream, d_dev);
         OSG_HIP_CHECK(ctx, hipGetLastError());
         OSG_HIP_CHECK(ctx, hipMemcpyAsync(h_out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
         OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
@@ -1551,10 +1584,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
             }
         }
     }
-    if (prof)
-        fprintf(stderr, "[osg lba] %d graphs: structure %.3f ms (graph 0: %.3f ms), pack+upload %.3f ms, LM %.3f ms "
-                        "(%d lockstep steps)\n",
-                NA, t_struct, H[act[0]].t_struct, t_upload, ms_since(tp1), steps);
+    const double t_lm = ms_since(tp1);
+    const auto tp2 = std::chrono::steady_clock::now();
     // classification with the last computed errors (current estimate's, or the rejected trial's,
     // exactly as the reference's computeActiveErrors order leaves them); estimates out
     for (int a = 0; a < NA; a++) h_ctl[a] = LbaCtl{M_FIN, H[act[a]].sel, 0.0};
@@ -1578,6 +1609,10 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         OSG_HIP_CHECK(ctx, hipMemcpyAsync(R->edge_bad, D.bad, h.ne, hipMemcpyDeviceToHost, ctx->stream));
     }
     OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    if (prof)
+        fprintf(stderr, "[osg lba] %d graphs: structure %.3f ms (graph 0: %.3f ms), pack+upload %.3f ms, LM %.3f ms "
+                        "(%d lockstep steps), classify+download %.3f ms, total %.3f ms\n",
+                NA, t_struct, H[act[0]].t_struct, t_upload, t_lm, steps, ms_since(tp2), ms_since(tp0));
     return B == 1 ? results[0].iterations : total_iters;
 }
 

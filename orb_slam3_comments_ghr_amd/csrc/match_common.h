@@ -1,7 +1,9 @@
 // match_common.h — host/device helpers shared by the matcher kernels (match.hip).
 #pragma once
 #include <cstdint>
+#include <algorithm>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "osg_internal.h"
@@ -28,6 +30,27 @@ struct osg_packer {
     void fill(void *dst) const
     {
         for (const item &it : items) std::memcpy((char *)dst + it.off, it.src, it.bytes);
+    }
+    // the same copy split over up to `nthreads` host threads by bytes (large batches)
+    void fill_parallel(void *dst, int nthreads) const
+    {
+        if (nthreads <= 1 || total < (size_t(8) << 20)) {
+            fill(dst);
+            return;
+        }
+        const size_t per = (total + nthreads - 1) / nthreads;
+        std::vector<std::thread> th;
+        for (int t = 0; t < nthreads; t++) {
+            const size_t lo = t * per, hi = std::min(total, lo + per);
+            if (lo >= hi) break;
+            th.emplace_back([this, dst, lo, hi] {
+                for (const item &it : items) {  // the part of each item inside [lo, hi)
+                    const size_t a = std::max(lo, it.off), b = std::min(hi, it.off + it.bytes);
+                    if (a < b) std::memcpy((char *)dst + a, (const char *)it.src + (a - it.off), b - a);
+                }
+            });
+        }
+        for (auto &t : th) t.join();
     }
 };
 

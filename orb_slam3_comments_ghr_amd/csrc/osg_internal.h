@@ -4,6 +4,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <memory>
 #include <string>
 
 #include "../../include/osg.h"
@@ -36,6 +37,7 @@ struct osg_ctx {
     int32_t match_stats[4] = {};  // last matcher call: candidates, Jacobi rounds, serial redo, nmatches
     double last_kernel_ms = 0;    // last k_match / k_pose_opt launch time (HIP events)
     hipEvent_t ev[2] = {};        // timing events (osg_ctx_events)
+    std::shared_ptr<void> lba_cache;  // host structures of the last LBA batch, reused (ba.hip)
     std::string last_error;
 };
 

@@ -22,7 +22,10 @@ def main():
         t = time.perf_counter()
         it = 0
         for _ in range(reps):
+            t1 = time.perf_counter()
             res = opt.LocalBundleAdjustmentBatch(graphs)
+            if os.environ.get("OSG_LBA_PROFILE"):
+                print(f"  python call {1e3 * (time.perf_counter() - t1):.2f} ms", flush=True)
             it += sum(r.iterations for r in res)
         el = time.perf_counter() - t
         print(f"B={B:3d}  {it / el:10.1f} LM iters/s   {el / reps * 1e3:8.2f} ms per batch   "
