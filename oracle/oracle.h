@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include "../include/osg.h"
 #include "../include/osg_ba.h"
+#include "../include/osg_dbow.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -31,6 +32,9 @@ int oracle_search_by_bow_kf_f(const osg_bow_side *KF, const osg_bow_side *F, flo
                               int checkOri, int32_t *out_mp);
 int oracle_search_by_bow_kf_kf(const osg_bow_side *K1, const osg_bow_side *K2, float nnratio,
                                int checkOri, int32_t *out_mp12);
+
+/* DBoW2 vocabulary transform (oracle_dbow.c) */
+void oracle_dbow_transform(const osg_vocabulary_desc *V, const uint8_t *desc, int n, int levelsup, osg_bow_out *out);
 
 /* bundle adjustment (oracle_ba.c) */
 int oracle_pose_optimization(const osg_pose_problem *P, osg_pose_result *R);

@@ -121,7 +121,21 @@ class OsgBaResult(C.Structure):
     ]
 
 
-# Every symbol include/osg.h and include/osg_ba.h declare (checked by tests/test_abi.py).
+class OsgVocabularyDesc(C.Structure):
+    _fields_ = [
+        ("k", i32), ("L", i32), ("scoring", i32), ("weighting", i32), ("n_nodes", i32),
+        ("parent", P), ("is_leaf", P), ("desc", P), ("weight", P),
+    ]
+
+
+class OsgBowOut(C.Structure):
+    _fields_ = [
+        ("n_words", i32), ("word", P), ("value", P), ("n_nodes", i32), ("node_id", P),
+        ("node_start", P), ("feat", P),
+    ]
+
+
+# Every symbol include/osg.h, include/osg_ba.h and include/osg_dbow.h declare (checked by tests/test_abi.py).
 EXPORTS = [
     "osg_ctx_create", "osg_ctx_destroy", "osg_ctx_set_stream", "osg_ctx_stream",
     "osg_ctx_synchronize", "osg_strerror", "osg_ctx_last_error", "osg_version",
@@ -132,6 +146,8 @@ EXPORTS = [
     "osg_search_by_projection_kf_batch", "osg_search_by_bow_kf_f_batch", "osg_search_by_bow_kf_kf_batch",
     "osg_match_last_stats", "osg_ctx_last_kernel_ms", "osg_pose_optimization", "osg_pose_optimization_batch",
     "osg_local_bundle_adjustment", "osg_local_bundle_adjustment_batch",
+    "osg_vocabulary_create", "osg_vocabulary_load_text", "osg_vocabulary_destroy", "osg_vocabulary_info",
+    "osg_vocabulary_transform", "osg_vocabulary_transform_batch",
 ]
 
 
@@ -178,6 +194,12 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.osg_local_bundle_adjustment.argtypes = [vp, C.POINTER(OsgBaGraph), C.POINTER(OsgBaResult),
                                                 vp]
     lib.osg_local_bundle_adjustment_batch.argtypes = [vp, vp, i32, vp, vp]
+    lib.osg_vocabulary_create.argtypes = [vp, C.POINTER(OsgVocabularyDesc), C.POINTER(vp)]
+    lib.osg_vocabulary_load_text.argtypes = [vp, C.c_char_p, C.POINTER(vp)]
+    lib.osg_vocabulary_destroy.argtypes = [vp]
+    lib.osg_vocabulary_info.argtypes = [vp, vp]
+    lib.osg_vocabulary_transform.argtypes = [vp, vp, vp, i32, i32, C.POINTER(OsgBowOut)]
+    lib.osg_vocabulary_transform_batch.argtypes = [vp, vp, vp, vp, i32, i32, vp]
     return lib
 
 
@@ -205,4 +227,6 @@ def declare_oracle(lib: C.CDLL) -> C.CDLL:
     lib.oracle_pose_optimization.argtypes = [C.POINTER(OsgPoseProblem), C.POINTER(OsgPoseResult)]
     lib.oracle_local_bundle_adjustment.argtypes = [C.POINTER(OsgBaGraph), C.POINTER(OsgBaResult),
                                                    vp]
+    lib.oracle_dbow_transform.argtypes = [C.POINTER(OsgVocabularyDesc), vp, C.c_int, C.c_int, C.POINTER(OsgBowOut)]
+    lib.oracle_dbow_transform.restype = None
     return lib

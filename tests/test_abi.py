@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def header_symbols():
     syms = set()
-    for h in ("osg.h", "osg_ba.h"):
+    for h in ("osg.h", "osg_ba.h", "osg_dbow.h"):
         text = open(os.path.join(ROOT, "include", h)).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         for m in re.finditer(r"\b(osg_[a-z0-9_]+)\s*\(", text):
