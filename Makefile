@@ -7,7 +7,7 @@ CSRC = $(PKG)/csrc
 LIB = $(PKG)/liborbslam3_amd.so
 OBJDIR = build/obj
 HIPFLAGS = --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-function
-# bit-exact float geometry in the matcher: no FMA contraction in those translation units
+# bit-exact float geometry in the matcher and BowVector sums: no FMA contraction in those units
 EXACT = -ffp-contract=off
 HDRS = include/osg.h include/osg_ba.h $(CSRC)/osg_internal.h
 
@@ -29,7 +29,7 @@ $(OBJDIR)/pose.o: $(CSRC)/pose.hip $(HDRS) $(CSRC)/ba_common.h | $(OBJDIR)
 $(OBJDIR)/ba.o: $(CSRC)/ba.hip $(HDRS) $(CSRC)/ba_common.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 $(OBJDIR)/dbow.o: $(CSRC)/dbow.hip $(HDRS) include/osg_dbow.h $(CSRC)/match_common.h | $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(EXACT) -c $< -o $@
 
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)

@@ -11,9 +11,10 @@
 //                   the first child in order wins), the node at level L - levelsup, the word and
 //                   its weight                                             (latency / L2-MALL)
 //   k_bow_assemble  one workgroup per descriptor set: bitonic sort of (word, feature) and
-//                   (node, feature) keys in LDS, BowVector sums in feature order (addWeight) or the
-//                   first weight (addIfNotExist), the reference's normalisation summed in ascending
-//                   word order, FeatureVector CSR in feature order
+//                   (node rank, feature) keys in LDS — packed into 32 bits when they fit (ORBvoc:
+//                   20 + 11 bits at 2048 features), 64 otherwise — BowVector sums in feature order
+//                   (addWeight) or the first weight (addIfNotExist), the reference's normalisation
+//                   summed in ascending word order, FeatureVector CSR in feature order
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -34,6 +35,8 @@ struct osg_vocabulary {
     uint4 *desc = nullptr;       // per BFS node: 2 x uint4
     double *weight = nullptr;    // per BFS node
     uint32_t *old_id = nullptr;  // per BFS node: the reference's node id
+    uint32_t *lvl_rank = nullptr;  // per BFS node: rank of its old id among the nodes of its depth
+    int level_count[16] = {};      // nodes per depth
 };
 
 namespace {
@@ -67,15 +70,16 @@ __device__ __forceinline__ uint32_t dist256(const uint4 a0, const uint4 a1, cons
 __global__ __launch_bounds__(DT) void k_voc_descend(const int4 *__restrict__ meta, const uint4 *__restrict__ vdesc,
                                                     const double *__restrict__ vweight,
                                                     const uint32_t *__restrict__ old_id,
+                                                    const uint32_t *__restrict__ lvl_rank,
                                                     const uint4 *__restrict__ feat, int nf, int nid_level,
                                                     int32_t *__restrict__ o_word, double *__restrict__ o_w,
-                                                    uint32_t *__restrict__ o_nid)
+                                                    uint32_t *__restrict__ o_nid, uint32_t *__restrict__ o_nrank)
 {
     const int f = blockIdx.x * DT + threadIdx.x;
     if (f >= nf) return;
     const uint4 a0 = feat[2 * f], a1 = feat[2 * f + 1];
     int node = 0, level = 0;
-    uint32_t nid = 0;  // the root when nid_level <= 0 (and if no descent step reaches it)
+    uint32_t nid = 0, nrank = 0;  // the root when nid_level <= 0 (and if no descent step reaches it)
     int4 m = meta[0];
     while (!m.z) {
         ++level;
@@ -101,11 +105,15 @@ __global__ __launch_bounds__(DT) void k_voc_descend(const int4 *__restrict__ met
         }
         node = best;
         m = meta[node];
-        if (level == nid_level) nid = old_id[node];
+        if (level == nid_level) {
+            nid = old_id[node];
+            nrank = 1 + lvl_rank[node];  // sorts like nid: ranks follow old ids, the root (0) first
+        }
     }
     o_word[f] = m.w;
     o_w[f] = vweight[node];
     o_nid[f] = nid;
+    o_nrank[f] = nrank;
 }
 
 struct SetArgs {
@@ -118,16 +126,29 @@ struct SetArgs {
     int32_t *counts;       // [0] n_words, [1] n_nodes
 };
 
-// bitonic sort of 64-bit keys in LDS (n2 a power of two, padded with ~0)
-__device__ void lds_sort(unsigned long long *k, int n2)
+// bitonic sort of 64-bit keys in LDS (n2 a power of two, padded with ~0).  Compare-exchange pair i
+// (lo, lo + stride) is handled by thread i % AT, so for stride <= 64 every wave touches only its
+// own 128-key segments: those stages are ordered by the wave's in-order LDS queue and need no
+// workgroup barrier (only a compiler fence).  n2 = 2048 has 10 barrier stages instead of 66.
+template <typename K>
+__device__ void lds_sort(K *k, int n2)
 {
+    __syncthreads();
+    int prev = 0;
     for (int size = 2; size <= n2; size <<= 1)
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            __syncthreads();
+            if (stride > 64 || prev > 64) {
+                __syncthreads();
+            } else {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            prev = stride;
             for (int i = threadIdx.x; i < n2 / 2; i += AT) {
-                const int lo = 2 * stride * (i / stride) + (i % stride), hi = lo + stride;
+                const int lo = ((i & ~(stride - 1)) << 1) | (i & (stride - 1)), hi = lo + stride;  // stride: 2^k
                 const bool up = ((lo & size) == 0);
-                const unsigned long long a = k[lo], b = k[hi];
+                const K a = k[lo], b = k[hi];
                 if ((a > b) == up) {
                     k[lo] = b;
                     k[hi] = a;
@@ -137,109 +158,185 @@ __device__ void lds_sort(unsigned long long *k, int n2)
     __syncthreads();
 }
 
-// BowVector + FeatureVector of one descriptor set, ref:TemplatedVocabulary.h:1126-1192,
-// BowVector.cpp:35-85, FeatureVector.cpp:32-46.  The order-dependent parts (sums per word in feature
-// order, the norm in ascending word order) run in one thread over LDS; everything else is parallel.
-__global__ __launch_bounds__(AT) void k_bow_assemble(const SetArgs *__restrict__ sets, const int32_t *__restrict__ i_word,
-                                                     const double *__restrict__ i_w, const uint32_t *__restrict__ i_nid,
-                                                     int weighting, int scoring)
+// Exclusive prefix count of one flag per thread (thread order) over the workgroup; *total gets the
+// count of all flags.  Two barriers; s_wtot holds AT / 64 ints.
+__device__ int block_scan_flag(bool f, int *s_wtot, int *total)
 {
-    const SetArgs S = sets[blockIdx.x];
-    __shared__ unsigned long long key[MAX_SET];
-    __shared__ double val[MAX_SET];
-    __shared__ int s_m, s_nw;
-    __shared__ double s_scale;
+    const unsigned long long mask = __ballot(f);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int before = __popcll(mask & ((1ull << lane) - 1ull));
+    if (lane == 0) s_wtot[w] = __popcll(mask);
+    __syncthreads();
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < AT / 64; i++) {
+        const int c = s_wtot[i];
+        off += (i < w) ? c : 0;
+        tot += c;
+    }
+    __syncthreads();
+    *total = tot;
+    return off + before;
+}
+
+// BowVector + FeatureVector of one descriptor set, ref:TemplatedVocabulary.h:1126-1192,
+// BowVector.cpp:35-85, FeatureVector.cpp:32-46.  Sorting (word, feature) makes every word's
+// features one run in feature order, so each run head sums its run sequentially (addWeight: the
+// reference's += in feature order; addIfNotExist: the first value) and a flag scan gives the run's
+// output slot.  Only the norm — one sum in ascending word order — stays serial, in wave 0.
+// K: key type (uint32_t when word / node-rank bits + fbits fit in 31, else 64-bit with fbits 32).
+template <typename K>
+__device__ void assemble(const SetArgs &S, K *key, double *val, int *s_wtot, int *s_m, double *s_norm,
+                         const int32_t *__restrict__ i_word, const double *__restrict__ i_w,
+                         const uint32_t *__restrict__ i_nid, const uint32_t *__restrict__ i_nrank, int fbits,
+                         bool add, bool must, bool l2, unsigned long long *prof)
+{
+    constexpr int PER = MAX_SET / AT;
+    const K PAD = ~K(0), FMASK = (K(1) << fbits) - 1;
+#define STAMP(k)                                                                    \
+    if (prof && blockIdx.x == 0 && threadIdx.x == 0) prof[k] = __builtin_amdgcn_s_memtime()
     const int n = S.n;
     int n2 = 1;
     while (n2 < n) n2 <<= 1;
-    const bool add = (weighting == OSG_W_TF || weighting == OSG_W_TF_IDF);
-    const bool must = scoring != OSG_S_DOT, l2 = scoring == OSG_S_L2;
     // ---- BowVector: sort (word, feature) of the non-stopped features
-    if (threadIdx.x == 0) s_m = 0;
-    __syncthreads();
     for (int i = threadIdx.x; i < n2; i += AT) {
-        unsigned long long v = ~0ull;
+        K v = PAD;
         if (i < n && i_w[S.first + i] > 0) {
-            v = ((unsigned long long)(uint32_t)i_word[S.first + i] << 32) | (uint32_t)i;
-            atomicAdd(&s_m, 1);
+            v = ((K)(uint32_t)i_word[S.first + i] << fbits) | (K)i;
+            atomicAdd(s_m, 1);
         }
         key[i] = v;
     }
+    STAMP(1);
     lds_sort(key, n2);
-    const int m = s_m;  // valid keys, sorted to the front
-    for (int i = threadIdx.x; i < m; i += AT) val[i] = i_w[S.first + (uint32_t)key[i]];
+    STAMP(2);
+    const int m = *s_m;  // valid keys, sorted to the front
+    for (int i = threadIdx.x; i < m; i += AT) val[i] = i_w[S.first + (uint32_t)(key[i] & FMASK)];
     __syncthreads();
-    if (threadIdx.x == 0) {
-        // addWeight (sum in feature order) / addIfNotExist (first); val[j] <- word j's value
-        int nw = 0;
-        uint32_t cur = 0;
-        double acc = 0.0;
-        for (int i = 0; i < m; i++) {
-            const uint32_t w = (uint32_t)(key[i] >> 32);
-            const double v = val[i];
-            if (nw > 0 && cur == w) {
-                if (add) acc += v;
-            } else {
-                if (nw > 0) val[nw - 1] = acc;
-                cur = w;
-                acc = v;
-                key[nw] = ((unsigned long long)w << 32) | (key[nw] & 0xFFFFFFFFull);  // word of slot nw
-                nw++;
-            }
+    STAMP(3);
+    double rsum[PER];
+    int rslot[PER];
+    uint32_t rword[PER];
+    int nw = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        rslot[k] = -1;
+        if (k * AT >= m) continue;  // uniform
+        const int i = k * AT + threadIdx.x;
+        const uint32_t w = i < m ? (uint32_t)(key[i] >> fbits) : 0u;
+        const bool head = i < m && (i == 0 || (uint32_t)(key[i - 1] >> fbits) != w);
+        int tot;
+        const int pos = nw + block_scan_flag(head, s_wtot, &tot);
+        nw += tot;
+        if (head) {
+            double acc = val[i];
+            for (int j = i + 1; j < m && (uint32_t)(key[j] >> fbits) == w; j++)
+                if (add) acc += val[j];
+            rsum[k] = acc;
+            rslot[k] = pos;
+            rword[k] = w;
         }
-        if (nw > 0) val[nw - 1] = acc;
-        double scale = 1.0;  // applied below as v / nd, then v / norm, exactly the reference's two divisions
-        if (add && nw > 0 && !must) {
-            const double nd = (double)nw;
-            for (int j = 0; j < nw; j++) val[j] /= nd;
-        }
-        if (must) {
-            double norm = 0.0;
-            if (!l2)
-                for (int j = 0; j < nw; j++) norm += fabs(val[j]);
-            else {
-                for (int j = 0; j < nw; j++) norm += val[j] * val[j];
-                norm = sqrt(norm);
-            }
-            scale = norm > 0.0 ? norm : 0.0;
-        }
-        s_nw = nw;
-        s_scale = scale;
-        S.counts[0] = nw;
     }
     __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PER; k++)
+        if (rslot[k] >= 0) {
+            val[rslot[k]] = (add && !must) ? rsum[k] / (double)nw : rsum[k];  // DOT_PRODUCT: v / n_words
+            key[rslot[k]] = (K)rword[k] << fbits;
+        }
+    __syncthreads();
+    STAMP(4);
+    if (must && threadIdx.x < 64) {
+        // ascending word order, one add at a time: the wave loads 64 values, then every lane adds
+        // them in lane order through readlane (the zero padding past nw adds +0.0 to a
+        // non-negative sum: exact)
+        const int lane = threadIdx.x;
+        double norm = 0.0;
+        for (int j0 = 0; j0 < nw; j0 += 64) {
+            const int j = j0 + lane;
+            double x = j < nw ? val[j] : 0.0;
+            x = l2 ? x * x : fabs(x);
+            const unsigned long long bits = (unsigned long long)__double_as_longlong(x);
+            const int lo = (int)(uint32_t)bits, hi = (int)(uint32_t)(bits >> 32);
+#pragma unroll
+            for (int u = 0; u < 64; u++) {
+                const unsigned long long y = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(hi, u) << 32) |
+                                             (uint32_t)__builtin_amdgcn_readlane(lo, u);
+                norm += __longlong_as_double((long long)y);
+            }
+        }
+        if (lane == 0) *s_norm = l2 ? sqrt(norm) : norm;
+    }
+    if (threadIdx.x == 0) S.counts[0] = nw;
+    __syncthreads();
+    STAMP(5);
     {
-        const int nw = s_nw;
-        const double norm = s_scale;
+        const double norm = must ? *s_norm : 0.0;
         for (int j = threadIdx.x; j < nw; j += AT) {
-            S.word[j] = (int32_t)(uint32_t)(key[j] >> 32);
-            S.value[j] = (must && norm > 0.0) ? val[j] / norm : val[j];
+            S.word[j] = (int32_t)(uint32_t)(key[j] >> fbits);
+            S.value[j] = norm > 0.0 ? val[j] / norm : val[j];
         }
     }
     __syncthreads();
-    // ---- FeatureVector: sort (node, feature); push_back in feature order
+    // ---- FeatureVector: sort (node rank, feature); a node's features are one run, pushed in
+    // feature order
     for (int i = threadIdx.x; i < n2; i += AT) {
-        unsigned long long v = ~0ull;
-        if (i < n && i_w[S.first + i] > 0) v = ((unsigned long long)i_nid[S.first + i] << 32) | (uint32_t)i;
+        K v = PAD;
+        if (i < n && i_w[S.first + i] > 0) v = ((K)i_nrank[S.first + i] << fbits) | (K)i;
         key[i] = v;
     }
+    STAMP(6);
     lds_sort(key, n2);
-    for (int i = threadIdx.x; i < m; i += AT) S.feat[i] = (int32_t)(uint32_t)key[i];
-    if (threadIdx.x == 0) {
-        int nn = 0;
-        uint32_t prev = 0;
-        for (int i = 0; i < m; i++) {
-            const uint32_t nd = (uint32_t)(key[i] >> 32);
-            if (!(nn > 0 && prev == nd)) {
-                S.node_id[nn] = nd;
-                S.node_start[nn] = i;
-                prev = nd;
-                nn++;
-            }
+    STAMP(7);
+    int nn = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        if (k * AT >= m) continue;
+        const int i = k * AT + threadIdx.x;
+        const uint32_t r = i < m ? (uint32_t)(key[i] >> fbits) : 0u;
+        const bool head = i < m && (i == 0 || (uint32_t)(key[i - 1] >> fbits) != r);
+        int tot;
+        const int pos = nn + block_scan_flag(head, s_wtot, &tot);
+        nn += tot;
+        const int f = i < m ? (int)(uint32_t)(key[i] & FMASK) : 0;
+        if (i < m) S.feat[i] = f;
+        if (head) {
+            S.node_id[pos] = i_nid[S.first + f];
+            S.node_start[pos] = i;
         }
+    }
+    if (threadIdx.x == 0) {
         S.node_start[nn] = m;
         S.counts[1] = nn;
     }
+    STAMP(8);
+#undef STAMP
+}
+
+__global__ __launch_bounds__(AT) void k_bow_assemble(const SetArgs *__restrict__ sets, const int32_t *__restrict__ i_word,
+                                                     const double *__restrict__ i_w, const uint32_t *__restrict__ i_nid,
+                                                     const uint32_t *__restrict__ i_nrank, int wbits, int rbits,
+                                                     int weighting, int scoring, unsigned long long *prof)
+{
+    // OSG_DBOW_PROFILE: s_memtime per phase of workgroup 0
+    if (prof && blockIdx.x == 0 && threadIdx.x == 0) prof[0] = __builtin_amdgcn_s_memtime();
+    const SetArgs S = sets[blockIdx.x];
+    __shared__ unsigned long long key[MAX_SET];
+    __shared__ double val[MAX_SET];
+    __shared__ int s_m, s_wtot[AT / 64];
+    __shared__ double s_norm;
+    const bool add = (weighting == OSG_W_TF || weighting == OSG_W_TF_IDF);
+    const bool must = scoring != OSG_S_DOT, l2 = scoring == OSG_S_L2;
+    if (threadIdx.x == 0) s_m = 0;
+    __syncthreads();
+    int fbits = 1;
+    while ((1 << fbits) < S.n) fbits++;
+    if (max(wbits, rbits) + fbits <= 31)
+        assemble<uint32_t>(S, (uint32_t *)key, val, s_wtot, &s_m, &s_norm, i_word, i_w, i_nid, i_nrank, fbits, add,
+                           must, l2, prof);
+    else
+        assemble<unsigned long long>(S, key, val, s_wtot, &s_m, &s_norm, i_word, i_w, i_nid, i_nrank, 32, add, must,
+                                     l2, prof);
 }
 
 int voc_upload(osg_ctx *ctx, const osg_vocabulary_desc *V, osg_vocabulary **out)
@@ -285,7 +382,15 @@ int voc_upload(osg_ctx *ctx, const osg_vocabulary_desc *V, osg_vocabulary **out)
     std::vector<int4> meta(n);
     std::vector<uint8_t> desc(32 * (size_t)n, 0);
     std::vector<double> weight(n, 0.0);
-    std::vector<uint32_t> old(n);
+    std::vector<uint32_t> old(n), rank(n);
+    // depth of every node, and its rank by old id among the nodes of that depth
+    std::vector<int> depth(n, 0), per_depth(1, 0);
+    for (int p = 1; p < n; p++) depth[order[p]] = depth[V->parent[order[p]]] + 1;
+    std::vector<uint32_t> rank_old(n);
+    for (int o = 0; o < n; o++) {
+        if (depth[o] >= (int)per_depth.size()) per_depth.resize(depth[o] + 1, 0);
+        rank_old[o] = (uint32_t)per_depth[depth[o]]++;
+    }
     for (int p = 0; p < n; p++) {
         const int o = order[p];
         const int nc = cstart[o + 1] - cstart[o];
@@ -296,6 +401,7 @@ int voc_upload(osg_ctx *ctx, const osg_vocabulary_desc *V, osg_vocabulary **out)
             weight[p] = V->weight[o];
         }
         old[p] = (uint32_t)o;
+        rank[p] = rank_old[o];
     }
     osg_vocabulary *voc = new osg_vocabulary();
     voc->ctx = ctx;
@@ -305,13 +411,16 @@ int voc_upload(osg_ctx *ctx, const osg_vocabulary_desc *V, osg_vocabulary **out)
     voc->weighting = V->weighting;
     voc->n_nodes = n;
     voc->n_words = nw;
+    for (int d = 0; d < (int)per_depth.size() && d < 16; d++) voc->level_count[d] = per_depth[d];
     bool ok = hipMalloc(&voc->meta, sizeof(int4) * n) == hipSuccess && hipMalloc(&voc->desc, 32 * (size_t)n) == hipSuccess &&
-              hipMalloc(&voc->weight, sizeof(double) * n) == hipSuccess && hipMalloc(&voc->old_id, 4 * (size_t)n) == hipSuccess;
+              hipMalloc(&voc->weight, sizeof(double) * n) == hipSuccess && hipMalloc(&voc->old_id, 4 * (size_t)n) == hipSuccess &&
+              hipMalloc(&voc->lvl_rank, 4 * (size_t)n) == hipSuccess;
     if (ok)
         ok = hipMemcpy(voc->meta, meta.data(), sizeof(int4) * n, hipMemcpyHostToDevice) == hipSuccess &&
              hipMemcpy(voc->desc, desc.data(), 32 * (size_t)n, hipMemcpyHostToDevice) == hipSuccess &&
              hipMemcpy(voc->weight, weight.data(), sizeof(double) * n, hipMemcpyHostToDevice) == hipSuccess &&
-             hipMemcpy(voc->old_id, old.data(), 4 * (size_t)n, hipMemcpyHostToDevice) == hipSuccess;
+             hipMemcpy(voc->old_id, old.data(), 4 * (size_t)n, hipMemcpyHostToDevice) == hipSuccess &&
+             hipMemcpy(voc->lvl_rank, rank.data(), 4 * (size_t)n, hipMemcpyHostToDevice) == hipSuccess;
     if (!ok) {
         osg_vocabulary_destroy(voc);
         return osg_set_error(ctx, OSG_E_NOMEM, "vocabulary upload failed");
@@ -386,6 +495,7 @@ int osg_vocabulary_destroy(osg_vocabulary *voc)
     if (voc->desc) (void)hipFree(voc->desc);
     if (voc->weight) (void)hipFree(voc->weight);
     if (voc->old_id) (void)hipFree(voc->old_id);
+    if (voc->lvl_rank) (void)hipFree(voc->lvl_rank);
     delete voc;
     return OSG_OK;
 }
@@ -428,7 +538,7 @@ int osg_vocabulary_transform_batch(osg_ctx *ctx, const osg_vocabulary *voc, cons
     char *din = nullptr, *dmid = nullptr, *dout = nullptr;
     SetArgs *dsets = nullptr;
     OSG_ALLOC(ctx, din, SLOT_TMP0, pk.total + 256);
-    OSG_ALLOC(ctx, dmid, SLOT_TMP1, 16 * (size_t)total + 256);
+    OSG_ALLOC(ctx, dmid, SLOT_TMP1, 20 * (size_t)total + 256);
     // per set: word 4n, value 8n, node_id 4n, node_start 4(n+1), feat 4n, counts 8 -> padded
     std::vector<size_t> so(B + 1, 0);
     for (int b = 0; b < B; b++) so[b + 1] = so[b] + ((24 * (size_t)n[b] + 4 + 8 + 255) & ~size_t(255)) + 256;
@@ -438,6 +548,13 @@ int osg_vocabulary_transform_batch(osg_ctx *ctx, const osg_vocabulary *voc, cons
     int32_t *d_word = (int32_t *)dmid;
     double *d_w = (double *)(dmid + ((4 * (size_t)total + 15) & ~size_t(15)));
     uint32_t *d_nid = (uint32_t *)((char *)d_w + 8 * (size_t)total);
+    uint32_t *d_nrank = d_nid + total;
+    // key widths: word ids < n_words; node ranks 0 (root) .. level_count[nid_level]
+    const int nid_level = voc->L - levelsup;
+    const int lvl_n = (nid_level >= 1 && nid_level < 16) ? voc->level_count[nid_level] : 0;
+    int wbits = 1, rbits = 1;
+    while ((1ll << wbits) < voc->n_words) wbits++;
+    while ((1ll << rbits) <= lvl_n) rbits++;
     std::vector<SetArgs> hs(B);
     int first = 0;
     for (int b = 0; b < B; b++) {
@@ -460,10 +577,13 @@ int osg_vocabulary_transform_batch(osg_ctx *ctx, const osg_vocabulary *voc, cons
     if (!ev) return osg_set_error(ctx, OSG_E_HIP, "event create failed");
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[0], ctx->stream));
     hipLaunchKernelGGL(k_voc_descend, dim3((total + DT - 1) / DT), dim3(DT), 0, ctx->stream, voc->meta, voc->desc,
-                       voc->weight, voc->old_id, (const uint4 *)(din + o_feat), total, voc->L - levelsup, d_word, d_w,
-                       d_nid);
-    hipLaunchKernelGGL(k_bow_assemble, dim3(B), dim3(AT), 0, ctx->stream, dsets, d_word, d_w, d_nid, voc->weighting,
-                       voc->scoring);
+                       voc->weight, voc->old_id, voc->lvl_rank, (const uint4 *)(din + o_feat), total, nid_level,
+                       d_word, d_w, d_nid, d_nrank);
+    static const bool prof_on = getenv("OSG_DBOW_PROFILE") != nullptr;
+    unsigned long long *dprof = nullptr;
+    if (prof_on) OSG_ALLOC(ctx, dprof, SLOT_TMP4, 16 * sizeof(unsigned long long));
+    hipLaunchKernelGGL(k_bow_assemble, dim3(B), dim3(AT), 0, ctx->stream, dsets, d_word, d_w, d_nid, d_nrank, wbits,
+                       rbits, voc->weighting, voc->scoring, dprof);
     OSG_HIP_CHECK(ctx, hipGetLastError());
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
     char *pout = (char *)pin_sets + ((sizeof(SetArgs) * B + 255) & ~size_t(255));
@@ -472,6 +592,13 @@ int osg_vocabulary_transform_batch(osg_ctx *ctx, const osg_vocabulary *voc, cons
     float kms = 0.f;
     OSG_HIP_CHECK(ctx, hipEventElapsedTime(&kms, ev[0], ev[1]));
     ctx->last_kernel_ms = kms;
+    if (prof_on) {
+        unsigned long long st[16];
+        OSG_HIP_CHECK(ctx, hipMemcpy(st, dprof, sizeof(st), hipMemcpyDeviceToHost));
+        fprintf(stderr, "[dbow] B=%d kernels %.1f us; assemble wg0 phases (cycles):", B, kms * 1e3);
+        for (int k = 1; k <= 8; k++) fprintf(stderr, " %llu", st[k] - st[k - 1]);
+        fprintf(stderr, "\n");
+    }
     for (int b = 0; b < B; b++) {
         const char *base = pout + so[b];
         const int nb = n[b];

@@ -78,3 +78,16 @@ def test_featurevector_feeds_search_by_bow(ctx, oracle):
     n, out = ORBmatcher(ctx, 0.75, True).SearchByBoW(KF, F)
     assert n == ref[0] and n > 50
     np.testing.assert_array_equal(out, ref[1])
+
+
+def test_key_width_paths(ctx, oracle):
+    """ORBvoc-sized tree (~4.8e5 words, 20-bit word ids): sets of 2047 / 2048 features sort 32-bit
+    (word << 11 | feature) keys, 4096 / 8192 (the MAX_SET limit) fall back to 64-bit keys."""
+    rng = np.random.default_rng(14)
+    voc = vb.synth_vocabulary(rng, k=10, L=6, min_children=8, min_leaf_depth=6)
+    assert voc.n_words > (1 << 19)
+    gv = vb.ORBVocabulary(ctx, voc)
+    for n, lu in ((2047, 4), (2048, 2), (4096, 4), (8192, 0)):
+        desc = vb.synth_features(rng, voc, n=n)
+        same(gv.transform(desc, lu), vb.oracle_transform(oracle, voc, desc, lu))
+    gv.close()

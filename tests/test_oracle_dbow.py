@@ -13,6 +13,7 @@ CASES = [
     (10, 4, vb.L1_NORM, vb.TF_IDF, 2, 0.0, 0.0),     # ORBvoc's types (L1, TF-IDF)
     (10, 4, vb.L1_NORM, vb.TF_IDF, 2, 0.3, 0.05),    # early leaves, stopped words
     (6, 5, vb.L2_NORM, vb.TF, 3, 0.2, 0.0),
+    (8, 5, vb.L2_NORM, vb.TF_IDF, 2, 0.1, 0.02),   # sum of squares of non-integers: no FMA contraction
     (5, 5, vb.DOT_PRODUCT, vb.TF_IDF, 1, 0.0, 0.02),  # no normalisation: values / n_words
     (8, 4, vb.CHI_SQUARE, vb.IDF, 2, 0.1, 0.05),     # addIfNotExist
     (4, 6, vb.KL, vb.BINARY, 4, 0.2, 0.0),
