@@ -16,7 +16,6 @@ C2' streaming kernel's HBM roofline (Q = 4 x M = 2^24), the CPU restatement time
 from __future__ import annotations
 
 import argparse
-import ctypes
 import json
 import os
 import sys
@@ -213,6 +212,7 @@ def main():
     if not args.no_frames:
         out["frames_c3"] = bench_c3(ctx, rank, world, dist, dev, args)
         out["frames_c5"] = bench_c5(ctx, rank, world, dist, dev, args)
+        out["frames_dbow"] = bench_dbow(ctx, rank, world, dist, dev, args)
 
     # ---- LocalBA iters/s on C4 (50 KF x 10k points), the second half of the metric ----------
     if not args.no_ba:
@@ -299,14 +299,12 @@ def bench_lba(ctx, rank, world, dist, dev, args):
         "single_window": single,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        so = os.path.join(ROOT, "oracle", "liboracle.so")
-        from orb_slam3_comments_ghr_amd import _abi
-        lib = _abi.declare_oracle(ctypes.CDLL(so))
+        lib, oc = _oracle()
         t0 = time.perf_counter()
         n = 0
         ci = 0
         while time.perf_counter() - t0 < args.cpu_seconds / 2 or n == 0:
-            rr = op.oracle_lba(lib, G)
+            rr = oc.lba(lib, G)
             ci += rr.iterations
             n += 1
         cel = time.perf_counter() - t0
@@ -323,17 +321,17 @@ _ORACLE = []
 def _oracle():
     """The CPU oracle (test infrastructure), loaded only by the cpu_baseline legs."""
     if not _ORACLE:
-        from orb_slam3_comments_ghr_amd import _abi
         from tests import oracle_calls
-        _ORACLE.append((_abi.declare_oracle(ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))), oracle_calls))
+        _ORACLE.append((oracle_calls.load(), oracle_calls))
     return _ORACLE[0]
 
 
-def _frame_batches(ctx, rank, world, dist, dev, args, steps, cpu_step, label, workload, n_pool):
+def _frame_batches(ctx, rank, world, dist, dev, args, steps, cpu_step, label, workload, n_pool, cpu_frames=1):
     """Time `steps` (a list of callables, each one batched launch over B frames that leaves its
     kernel time in ctx.last_kernel_ms()) over args.frame_reps repetitions.  value = frames / summed
     kernel time (inputs resident in HBM: the device time of the launches); the wall rate includes
-    host packing and PCIe.  cpu_step(i) runs frame i of the pool through the oracle."""
+    host packing and PCIe.  cpu_step(i) runs frame i of the pool (or cpu_frames frames from i)
+    through the oracle."""
     import torch
     for f in steps:
         f()
@@ -363,7 +361,7 @@ def _frame_batches(ctx, rank, world, dist, dev, args, steps, cpu_step, label, wo
         t0 = time.perf_counter()
         while time.perf_counter() - t0 < args.cpu_seconds / 4 or n == 0:
             cpu_step(n % n_pool)
-            n += 1
+            n += cpu_frames
         cel = time.perf_counter() - t0
         res["cpu_baseline"] = {"value": round(n / cel, 1), "unit": "frames/s", "cores": 1, "kind": "port",
                                "sample": f"{n} frames through the oracle (gcc -O3, 1 thread) in {cel:.1f} s"}
@@ -391,7 +389,7 @@ def bench_c3(ctx, rank, world, dist, dev, args):
     def cpu(i):  # the cpu_baseline leg: the oracle restatement, 1 thread
         oracle, oc = _oracle()
         oc.bow_kf_f(oracle, pairs[i][0], pairs[i][1], 0.7, True)
-        op.oracle_pose(oracle, [probs[i]])
+        oc.pose(oracle, [probs[i]])
 
     return _frame_batches(ctx, rank, world, dist, dev, args,
                           [lambda: m.SearchByBoWBatch(KB, FB), lambda: opt.PoseOptimization(PB)], cpu,
@@ -426,7 +424,7 @@ def bench_c5(ctx, rank, world, dist, dev, args):
         oracle, oc = _oracle()
         oc.last(oracle, F[i], L[i], 7.0, False, True, S[i][0], S[i][1])
         oc.mps(oracle, F[i], Q[i], 0.9, 3.0, False, 20.0, S[i][0], S[i][1])
-        op.oracle_pose(oracle, [probs[i]])
+        oc.pose(oracle, [probs[i]])
 
     return _frame_batches(ctx, rank, world, dist, dev, args,
                           [lambda: m.SearchByProjectionBatch(FB, LB, 7.0, False, slot_mps=[S[i][0].copy() for i in idx],
@@ -440,15 +438,38 @@ def bench_c5(ctx, rank, world, dist, dev, args):
                           f"PoseOptimization 600 edges (40 % right camera); {B} frames per launch", n_pool)
 
 
+def bench_dbow(ctx, rank, world, dist, dev, args):
+    """SURVEY.md §8(f) rank 1: Frame::ComputeBoW = DBoW2 transform(features, BowVector,
+    FeatureVector, levelsup = 4) against an ORBvoc-shaped vocabulary (k = 10, L = 6, seeded
+    synthetic: ORBvoc.txt is not in the container), 1200 descriptors per frame, B frames per
+    launch."""
+    from orb_slam3_comments_ghr_amd import vocabulary as vb
+    n_pool = 16
+    rng = np.random.default_rng(0x0B5EEDB0 + rank)
+    voc = vb.synth_vocabulary(rng, k=10, L=6, min_children=8, min_leaf_depth=6)
+    gv = vb.ORBVocabulary(ctx, voc)
+    pool = [vb.synth_features(rng, voc, n=1200) for _ in range(n_pool)]
+    B = args.frames
+    sets = [pool[i % n_pool] for i in range(B)]
+
+    def cpu(i):  # the cpu_baseline leg: the oracle, children index built once per 16 frames
+        oracle, oc = _oracle()
+        oc.dbow_batch(oracle, voc, pool, 4)
+
+    res = _frame_batches(ctx, rank, world, dist, dev, args, [lambda: gv.transform_batch(sets, 4)], cpu,
+                         ["transform"],
+                         f"DBoW2 transform, levelsup 4: k=10 L=6 vocabulary ({voc.n_nodes} nodes, {voc.n_words} "
+                         f"words), 1200 descriptors per frame; {B} frames per launch", n_pool, cpu_frames=n_pool)
+    gv.transform_batch(sets[:1], 4)
+    res["single_frame_kernel_us"] = round(ctx.last_kernel_ms() * 1e3, 2)
+    gv.close()
+    return res
+
+
 def cpu_baseline(q_np, t_np, seconds):
     """oracle_hamming_top2 (the reference's serial DescriptorDistance + top-2 loop, restated in C,
     -O3) on 1 host thread, repeated on the same 2000 x 2000 workload for ~`seconds`."""
-    so = os.path.join(ROOT, "oracle", "liboracle.so")
-    if not os.path.exists(so):
-        import subprocess
-        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, stdout=subprocess.DEVNULL)
-    from orb_slam3_comments_ghr_amd import _abi
-    lib = _abi.declare_oracle(ctypes.CDLL(so))
+    lib, _ = _oracle()
     nq, nt = q_np.shape[0], t_np.shape[0]
     bi, bd, sd = (np.empty(nq, np.int32) for _ in range(3))
     reps = 0

@@ -35,6 +35,8 @@ int oracle_search_by_bow_kf_kf(const osg_bow_side *K1, const osg_bow_side *K2, f
 
 /* DBoW2 vocabulary transform (oracle_dbow.c) */
 void oracle_dbow_transform(const osg_vocabulary_desc *V, const uint8_t *desc, int n, int levelsup, osg_bow_out *out);
+void oracle_dbow_transform_batch(const osg_vocabulary_desc *V, const uint8_t *desc, const int32_t *n, int B,
+                                 int levelsup, osg_bow_out *out);
 
 /* bundle adjustment (oracle_ba.c) */
 int oracle_pose_optimization(const osg_pose_problem *P, osg_pose_result *R);

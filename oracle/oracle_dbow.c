@@ -104,14 +104,14 @@ static int kv_cmp(const void *a, const void *b)
     return x->idx < y->idx ? -1 : (x->idx > y->idx);
 }
 
-void oracle_dbow_transform(const osg_vocabulary_desc *V, const uint8_t *desc, int n, int levelsup, osg_bow_out *out)
+static void transform_one(const osg_vocabulary_desc *V, const voc_index *Xp, const uint8_t *desc, int n,
+                          int levelsup, osg_bow_out *out)
 {
     out->n_words = 0;
     out->n_nodes = 0;
     out->node_start[0] = 0;
     if (V->n_nodes <= 1 || n <= 0) return; /* empty(): ref:TemplatedVocabulary.h:1133-1136 */
-    voc_index X;
-    voc_build(V, &X);
+    const voc_index X = *Xp;
     kv *bw = (kv *)malloc(sizeof(kv) * (size_t)n), *fv = (kv *)malloc(sizeof(kv) * (size_t)n);
     int m = 0;
     for (int i = 0; i < n; i++) {
@@ -174,5 +174,27 @@ void oracle_dbow_transform(const osg_vocabulary_desc *V, const uint8_t *desc, in
     out->n_nodes = nn;
     free(bw);
     free(fv);
+}
+
+void oracle_dbow_transform(const osg_vocabulary_desc *V, const uint8_t *desc, int n, int levelsup, osg_bow_out *out)
+{
+    voc_index X;
+    voc_build(V, &X);
+    transform_one(V, &X, desc, n, levelsup, out);
+    voc_free(&X);
+}
+
+/* B sets with the children index built once, as the reference builds its tree once at load
+ * (the CPU baseline's per-frame work) */
+void oracle_dbow_transform_batch(const osg_vocabulary_desc *V, const uint8_t *desc, const int32_t *n, int B,
+                                 int levelsup, osg_bow_out *out)
+{
+    voc_index X;
+    voc_build(V, &X);
+    size_t first = 0;
+    for (int b = 0; b < B; b++) {
+        transform_one(V, &X, desc + 32 * first, n[b], levelsup, &out[b]);
+        first += (size_t)n[b];
+    }
     voc_free(&X);
 }

@@ -2,7 +2,7 @@
 
 Only plain pointers and sizes cross the boundary; every pointer field is a ``c_void_p`` filled
 from a numpy array's address by the helpers in this package.  The structures are shared by the
-product bindings (liborbslam3_amd.so) and the tests' oracle bindings (oracle/liboracle.so).
+product bindings (liborbslam3_amd.so); the oracle's (test infrastructure) are in tests/oracle_calls.py.
 """
 from __future__ import annotations
 
@@ -200,33 +200,4 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.osg_vocabulary_info.argtypes = [vp, vp]
     lib.osg_vocabulary_transform.argtypes = [vp, vp, vp, i32, i32, C.POINTER(OsgBowOut)]
     lib.osg_vocabulary_transform_batch.argtypes = [vp, vp, vp, vp, i32, i32, vp]
-    return lib
-
-
-def declare_oracle(lib: C.CDLL) -> C.CDLL:
-    """argtypes for oracle/liboracle.so (test infrastructure)."""
-    vp = C.c_void_p
-    lib.oracle_descriptor_distance.argtypes = [vp, vp]
-    lib.oracle_hamming_top2.argtypes = [vp, C.c_int, vp, C.c_int, vp, vp, vp]
-    lib.oracle_hamming_top2_mt.argtypes = [vp, C.c_int, vp, C.c_int, vp, vp, vp, C.c_int]
-    lib.oracle_frame_features_in_area.argtypes = [C.POINTER(OsgFrame), f32, f32, f32, C.c_int,
-                                                  C.c_int, C.c_int, vp]
-    lib.oracle_compute_three_maxima.argtypes = [vp, C.c_int, vp, vp, vp]
-    lib.oracle_rot_bin.argtypes = [f32, f32]
-    lib.oracle_search_by_projection_mps.argtypes = [C.POINTER(OsgFrame), C.POINTER(OsgMpQueries),
-                                                    f32, f32, C.c_int, f32, vp, vp]
-    lib.oracle_search_by_projection_last.argtypes = [C.POINTER(OsgFrame),
-                                                     C.POINTER(OsgLastQueries), f32, C.c_int,
-                                                     C.c_int, vp, vp]
-    lib.oracle_search_by_projection_kf.argtypes = [C.POINTER(OsgFrame), C.POINTER(OsgKfQueries),
-                                                   f32, C.c_int, C.c_int, vp]
-    lib.oracle_search_by_bow_kf_f.argtypes = [C.POINTER(OsgBowSide), C.POINTER(OsgBowSide), f32,
-                                              C.c_int, vp]
-    lib.oracle_search_by_bow_kf_kf.argtypes = [C.POINTER(OsgBowSide), C.POINTER(OsgBowSide), f32,
-                                               C.c_int, vp]
-    lib.oracle_pose_optimization.argtypes = [C.POINTER(OsgPoseProblem), C.POINTER(OsgPoseResult)]
-    lib.oracle_local_bundle_adjustment.argtypes = [C.POINTER(OsgBaGraph), C.POINTER(OsgBaResult),
-                                                   vp]
-    lib.oracle_dbow_transform.argtypes = [C.POINTER(OsgVocabularyDesc), vp, C.c_int, C.c_int, C.POINTER(OsgBowOut)]
-    lib.oracle_dbow_transform.restype = None
     return lib

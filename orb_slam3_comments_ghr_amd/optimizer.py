@@ -214,7 +214,8 @@ class BAResult:
 
 
 def run_pose(fn, problems, handle=None):
-    """Call a PoseOptimization entry point (product batch API or the oracle) on problems."""
+    """Call a PoseOptimization entry point on problems: the batch API (handle given) or a
+    per-problem function fn(problem_structs, result_structs)."""
     res_structs = (_abi.OsgPoseResult * len(problems))()
     outl = [np.zeros(p.n, np.uint8) for p in problems]
     for r, o in zip(res_structs, outl):
@@ -279,20 +280,6 @@ class Optimizer:
         for (R0, pose, point, bad), R in zip(made, rs):
             out.append(BAResult(pose, point, bad, R.iterations, R.trials, R.chi2_initial, R.chi2_final, R.aborted))
         return out
-
-
-def oracle_lba(oracle, G: BAGraph, stop_flag=None) -> BAResult:
-    R, pose, point, bad = make_ba_result(G)
-    gs = G.struct()
-    oracle.oracle_local_bundle_adjustment(C.byref(gs), C.byref(R), None if stop_flag is None else _p(stop_flag))
-    return BAResult(pose, point, bad, R.iterations, R.trials, R.chi2_initial, R.chi2_final, R.aborted)
-
-
-def oracle_pose(oracle, problems):
-    fn = lambda probs, res: [oracle.oracle_pose_optimization(C.byref(probs[i]), C.byref(res[i]))  # noqa: E731
-                             for i in range(len(probs))]
-    _, out = run_pose(fn, problems)
-    return out
 
 
 # ----------------------------------------------------------------------------- generators

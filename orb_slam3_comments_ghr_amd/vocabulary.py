@@ -206,12 +206,3 @@ class ORBVocabulary:
             self.close()
         except Exception:
             pass
-
-
-def oracle_transform(oracle, voc: Vocabulary, desc, levelsup=4) -> BowResult:
-    """The C oracle (test infrastructure) on the same inputs."""
-    desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
-    o, bufs = make_bow_out(desc.shape[0])
-    s = voc.struct()
-    oracle.oracle_dbow_transform(C.byref(s), _p(desc), desc.shape[0], int(levelsup), C.byref(o))
-    return bow_result(o, bufs)

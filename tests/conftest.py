@@ -9,26 +9,18 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-from orb_slam3_comments_ghr_amd import _abi  # noqa: E402
+from tests import oracle_calls as oc  # noqa: E402
 
-ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
 
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) and the HIP library")
 
 
-def _build_oracle():
-    if not os.path.exists(ORACLE_SO):
-        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True,
-                       stdout=subprocess.DEVNULL)
-
-
 @pytest.fixture(scope="session")
 def oracle():
     """The CPU restatement (test infrastructure only): the checker for every parity test."""
-    _build_oracle()
-    return _abi.declare_oracle(ctypes.CDLL(ORACLE_SO))
+    return oc.load()
 
 
 @pytest.fixture(scope="session")

@@ -1,7 +1,61 @@
-"""Helpers that run the C oracle (test infrastructure) on the SoA containers."""
+"""The C oracle (oracle/liboracle.so, test infrastructure): its ctypes declarations and helpers
+that run it on the package's SoA containers.  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline legs use this module; the product package never imports it."""
 import ctypes as C
+import os
+import subprocess
 
 import numpy as np
+
+from orb_slam3_comments_ghr_amd import optimizer as op
+from orb_slam3_comments_ghr_amd import vocabulary as vb
+from orb_slam3_comments_ghr_amd._abi import (OsgBaGraph, OsgBaResult, OsgBowOut, OsgBowSide, OsgFrame,
+                                             OsgKfQueries, OsgLastQueries, OsgMpQueries, OsgPoseProblem,
+                                             OsgPoseResult, OsgVocabularyDesc)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
+f32 = C.c_float
+
+
+def load():
+    """Build oracle/liboracle.so if needed and return it declared."""
+    if not os.path.exists(ORACLE_SO):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, stdout=subprocess.DEVNULL)
+    return declare(C.CDLL(ORACLE_SO))
+
+
+
+
+def declare(lib: C.CDLL) -> C.CDLL:
+    """argtypes for oracle/liboracle.so (test infrastructure)."""
+    vp = C.c_void_p
+    lib.oracle_descriptor_distance.argtypes = [vp, vp]
+    lib.oracle_hamming_top2.argtypes = [vp, C.c_int, vp, C.c_int, vp, vp, vp]
+    lib.oracle_hamming_top2_mt.argtypes = [vp, C.c_int, vp, C.c_int, vp, vp, vp, C.c_int]
+    lib.oracle_frame_features_in_area.argtypes = [C.POINTER(OsgFrame), f32, f32, f32, C.c_int,
+                                                  C.c_int, C.c_int, vp]
+    lib.oracle_compute_three_maxima.argtypes = [vp, C.c_int, vp, vp, vp]
+    lib.oracle_rot_bin.argtypes = [f32, f32]
+    lib.oracle_search_by_projection_mps.argtypes = [C.POINTER(OsgFrame), C.POINTER(OsgMpQueries),
+                                                    f32, f32, C.c_int, f32, vp, vp]
+    lib.oracle_search_by_projection_last.argtypes = [C.POINTER(OsgFrame),
+                                                     C.POINTER(OsgLastQueries), f32, C.c_int,
+                                                     C.c_int, vp, vp]
+    lib.oracle_search_by_projection_kf.argtypes = [C.POINTER(OsgFrame), C.POINTER(OsgKfQueries),
+                                                   f32, C.c_int, C.c_int, vp]
+    lib.oracle_search_by_bow_kf_f.argtypes = [C.POINTER(OsgBowSide), C.POINTER(OsgBowSide), f32,
+                                              C.c_int, vp]
+    lib.oracle_search_by_bow_kf_kf.argtypes = [C.POINTER(OsgBowSide), C.POINTER(OsgBowSide), f32,
+                                               C.c_int, vp]
+    lib.oracle_pose_optimization.argtypes = [C.POINTER(OsgPoseProblem), C.POINTER(OsgPoseResult)]
+    lib.oracle_local_bundle_adjustment.argtypes = [C.POINTER(OsgBaGraph), C.POINTER(OsgBaResult),
+                                                   vp]
+    lib.oracle_dbow_transform.argtypes = [C.POINTER(OsgVocabularyDesc), vp, C.c_int, C.c_int, C.POINTER(OsgBowOut)]
+    lib.oracle_dbow_transform.restype = None
+    lib.oracle_dbow_transform_batch.argtypes = [C.POINTER(OsgVocabularyDesc), vp, vp, C.c_int, C.c_int, vp]
+    lib.oracle_dbow_transform_batch.restype = None
+    return lib
 
 
 def mps(oracle, F, Q, nn, th, far, thfar, slot_mp, slot_taken):
@@ -41,3 +95,41 @@ def bow_kf_kf(oracle, K1, K2, nn, ori):
     a, b = K1.struct(), K2.struct()
     n = oracle.oracle_search_by_bow_kf_kf(C.byref(a), C.byref(b), nn, int(ori), out.ctypes.data)
     return n, out
+
+
+def pose(oracle, problems):
+    """PoseOptimization through the oracle, one problem at a time."""
+    fn = lambda probs, res: [oracle.oracle_pose_optimization(C.byref(probs[i]), C.byref(res[i]))  # noqa: E731
+                             for i in range(len(probs))]
+    _, out = op.run_pose(fn, problems)
+    return out
+
+
+def lba(oracle, G, stop_flag=None):
+    R, pose_, point, bad = op.make_ba_result(G)
+    gs = G.struct()
+    oracle.oracle_local_bundle_adjustment(C.byref(gs), C.byref(R),
+                                          None if stop_flag is None else stop_flag.ctypes.data)
+    return op.BAResult(pose_, point, bad, R.iterations, R.trials, R.chi2_initial, R.chi2_final, R.aborted)
+
+
+def dbow(oracle, voc, desc, levelsup=4):
+    """DBoW2 transform of one descriptor set through the oracle."""
+    desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    o, bufs = vb.make_bow_out(desc.shape[0])
+    s = voc.struct()
+    oracle.oracle_dbow_transform(C.byref(s), desc.ctypes.data, desc.shape[0], int(levelsup), C.byref(o))
+    return vb.bow_result(o, bufs)
+
+
+def dbow_batch(oracle, voc, sets, levelsup=4):
+    """B descriptor sets with the vocabulary index built once (the CPU baseline's per-frame work)."""
+    sets = [np.ascontiguousarray(d, np.uint8).reshape(-1, 32) for d in sets]
+    outs = [vb.make_bow_out(d.shape[0]) for d in sets]
+    arr = (OsgBowOut * len(sets))(*[o for o, _ in outs])
+    n = np.array([d.shape[0] for d in sets], np.int32)
+    cat = np.concatenate(sets) if sets else np.zeros((0, 32), np.uint8)
+    s = voc.struct()
+    oracle.oracle_dbow_transform_batch(C.byref(s), cat.ctypes.data, n.ctypes.data, len(sets), int(levelsup),
+                                       C.addressof(arr))
+    return [vb.bow_result(arr[i], outs[i][1]) for i in range(len(sets))]

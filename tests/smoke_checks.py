@@ -1,14 +1,16 @@
 """Small end-to-end checks of every hot-path operator against the CPU oracle, used by
-__graft_entry__.smoke() (the oracle is the checker only)."""
+__graft_entry__.smoke() (the oracle is the checker only; this module is test infrastructure)."""
 from __future__ import annotations
 
 import ctypes as C
 
 import numpy as np
 
-from . import frames as fr
-from . import optimizer as op
-from .matcher import ORBmatcher
+from orb_slam3_comments_ghr_amd import frames as fr
+from orb_slam3_comments_ghr_amd import optimizer as op
+from orb_slam3_comments_ghr_amd import vocabulary as vb
+from orb_slam3_comments_ghr_amd.matcher import ORBmatcher
+from tests import oracle_calls as oc
 
 
 def run(ctx, oracle):
@@ -34,7 +36,7 @@ def run(ctx, oracle):
         raise AssertionError("SearchByBoW mismatch vs oracle")
     # PoseOptimization
     probs = [op.synth_pose_problem(rng, n_edges=200) for _ in range(4)]
-    refp = op.oracle_pose(oracle, probs)
+    refp = oc.pose(oracle, probs)
     gotp = op.Optimizer(ctx).PoseOptimization(probs)
     for g, r in zip(gotp, refp):
         if g.n_inliers != r.n_inliers or not np.array_equal(g.outlier, r.outlier) or \
@@ -42,8 +44,17 @@ def run(ctx, oracle):
             raise AssertionError("PoseOptimization mismatch vs oracle")
     # LocalBundleAdjustment
     G = op.synth_lba_graph(rng, n_kf=6, n_points=400)
-    refl = op.oracle_lba(oracle, G)
+    refl = oc.lba(oracle, G)
     gotl = op.Optimizer(ctx).LocalBundleAdjustment(G)
     if not np.array_equal(gotl.edge_bad, refl.edge_bad) or np.max(np.abs(gotl.point - refl.point)) > 1e-6 or \
             np.max(np.abs(gotl.pose - refl.pose)) > 1e-6:
         raise AssertionError("LocalBundleAdjustment mismatch vs oracle")
+    # DBoW2 transform (Frame::ComputeBoW)
+    voc = vb.synth_vocabulary(rng, k=10, L=4, early_leaf=0.1, min_leaf_depth=3)
+    desc = vb.synth_features(rng, voc, n=700)
+    gv = vb.ORBVocabulary(ctx, voc)
+    gb, rb = gv.transform(desc, 2), oc.dbow(oracle, voc, desc, 2)
+    gv.close()
+    for f in ("word", "value", "node_id", "node_start", "feat"):
+        if not np.array_equal(getattr(gb, f), getattr(rb, f)):
+            raise AssertionError(f"DBoW2 transform mismatch vs oracle ({f})")

@@ -30,7 +30,7 @@ def test_transform_parity(ctx, oracle, case):
     gv = vb.ORBVocabulary(ctx, voc)
     for n in (0, 1, 37, 1200, 4000):
         desc = vb.synth_features(rng, voc, n=n)
-        same(gv.transform(desc, lu), vb.oracle_transform(oracle, voc, desc, lu))
+        same(gv.transform(desc, lu), oc.dbow(oracle, voc, desc, lu))
     gv.close()
 
 
@@ -44,7 +44,7 @@ def test_orbvoc_shape_and_text_loader(ctx, oracle, tmp_path):
     info = gv.info()
     assert info["n_nodes"] == voc.n_nodes and info["n_words"] == voc.n_words
     desc = vb.synth_features(rng, voc, n=1500)
-    same(gv.transform(desc, 4), vb.oracle_transform(oracle, voc, desc, 4))
+    same(gv.transform(desc, 4), oc.dbow(oracle, voc, desc, 4))
 
 
 def test_transform_batch(ctx, oracle):
@@ -54,7 +54,7 @@ def test_transform_batch(ctx, oracle):
     sets = [vb.synth_features(rng, voc, n=int(n)) for n in rng.integers(0, 2500, 40)]
     got = gv.transform_batch(sets, 3)
     for d, g in zip(sets, got):
-        same(g, vb.oracle_transform(oracle, voc, d, 3))
+        same(g, oc.dbow(oracle, voc, d, 3))
 
 
 def test_featurevector_feeds_search_by_bow(ctx, oracle):
@@ -67,8 +67,8 @@ def test_featurevector_feeds_search_by_bow(ctx, oracle):
     f_desc = kf_desc.copy()
     f_desc = np.where(rng.random((1000, 1)) < 0.6, vb._flip(rng, kf_desc, 0.04), rng.integers(0, 256, (1000, 32), dtype=np.uint8))
     bk, bf = gv.transform_batch([kf_desc, f_desc], 3)
-    same(bk, vb.oracle_transform(oracle, voc, kf_desc, 3))
-    same(bf, vb.oracle_transform(oracle, voc, f_desc, 3))
+    same(bk, oc.dbow(oracle, voc, kf_desc, 3))
+    same(bf, oc.dbow(oracle, voc, f_desc, 3))
     mp = np.where(rng.random(1000) < 0.7, 10000 + np.arange(1000), -1).astype(np.int32)
     KF = fr.BowSide(kf_desc, rng.uniform(0, 360, 1000), mp, (mp >= 0).astype(np.uint8),
                     bk.node_id, np.append(bk.node_start[:len(bk.node_id)], bk.node_start[len(bk.node_id)]), bk.feat)
@@ -89,5 +89,5 @@ def test_key_width_paths(ctx, oracle):
     gv = vb.ORBVocabulary(ctx, voc)
     for n, lu in ((2047, 4), (2048, 2), (4096, 4), (8192, 0)):
         desc = vb.synth_features(rng, voc, n=n)
-        same(gv.transform(desc, lu), vb.oracle_transform(oracle, voc, desc, lu))
+        same(gv.transform(desc, lu), oc.dbow(oracle, voc, desc, lu))
     gv.close()

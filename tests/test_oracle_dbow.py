@@ -7,6 +7,7 @@ import pytest
 
 from orb_slam3_comments_ghr_amd import vocabulary as vb
 from tests import pyref_bow as pb
+from tests import oracle_calls as oc
 
 CASES = [
     # k, L, scoring, weighting, levelsup, early_leaf, stop_frac
@@ -38,7 +39,7 @@ def test_oracle_transform_vs_python(oracle, case):
     voc = vb.synth_vocabulary(rng, k=k, L=L, scoring=sc, weighting=wt, early_leaf=early,
                               min_leaf_depth=max(2, L - lu + 1), stop_frac=stop)
     desc = vb.synth_features(rng, voc, n=250)
-    got = vb.oracle_transform(oracle, voc, desc, lu)
+    got = oc.dbow(oracle, voc, desc, lu)
     check(got, voc, desc, lu)
     assert len(got.word) > 10
 
@@ -50,7 +51,7 @@ def test_oracle_ties_first_child_wins(oracle):
     # root -> {1, 2} identical descriptors (both leaves)
     voc = vb.Vocabulary(2, 1, vb.L1_NORM, vb.TF_IDF, np.array([0, 0, 0]), np.array([0, 1, 1]),
                         np.concatenate([np.zeros((1, 32), np.uint8), d, d]), np.array([0.0, 1.0, 2.0]))
-    got = vb.oracle_transform(oracle, voc, d, 0)
+    got = oc.dbow(oracle, voc, d, 0)
     assert list(got.word) == [0] and got.value[0] == 1.0  # node 1 = word 0
     assert list(got.node_id) == [1]
 
@@ -58,7 +59,7 @@ def test_oracle_ties_first_child_wins(oracle):
 def test_oracle_empty_inputs(oracle):
     rng = np.random.default_rng(6)
     voc = vb.synth_vocabulary(rng, k=4, L=3)
-    got = vb.oracle_transform(oracle, voc, np.zeros((0, 32), np.uint8), 1)
+    got = oc.dbow(oracle, voc, np.zeros((0, 32), np.uint8), 1)
     assert len(got.word) == 0 and len(got.node_id) == 0
 
 

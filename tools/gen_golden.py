@@ -1,7 +1,6 @@
 """Regenerate tests/golden/*.npz from the CPU oracle (the reference itself cannot be built or
 run here: SURVEY.md §8c).  Each fixture stores inputs and the oracle's outputs; the numpy
 cross-checks in tests/ pin the oracle independently."""
-import ctypes
 import os
 import sys
 
@@ -9,14 +8,15 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from orb_slam3_comments_ghr_amd import _abi, synth  # noqa: E402
+from orb_slam3_comments_ghr_amd import synth  # noqa: E402
+from tests import oracle_calls  # noqa: E402
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
 def main():
     os.makedirs(GOLDEN, exist_ok=True)
-    lib = _abi.declare_oracle(ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so")))
+    lib = oracle_calls.load()
     q, t = synth.descriptors_c2(400, 600, seed=0x60D1)
     n = q.shape[0]
     bi, bd, sd = (np.empty(n, np.int32) for _ in range(3))
