@@ -20,6 +20,8 @@
  *                                ref:src/ORBmatcher.cc:1957-2191
  *   osg_search_by_projection_kf    ← ORBmatcher::SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist)
  *                                ref:src/ORBmatcher.cc:2203-2330
+ *   osg_fuse_search*           ← the search half of ORBmatcher::Fuse (both overloads)
+ *                                ref:src/ORBmatcher.cc:1330-1541, 1553-1694
  *   osg_pose_optimization*     ← Optimizer::PoseOptimization(Frame*)   ref:src/Optimizer.cc:71-420
  *   osg_local_bundle_adjustment← Optimizer::LocalBundleAdjustment(...) ref:src/Optimizer.cc:1758-2206
  *                                (graph already gathered; g2o LM + BlockSolver_6_3 inner loop on device)
@@ -243,6 +245,41 @@ int osg_search_by_bow_kf_f_batch(osg_ctx *ctx, const osg_bow_side *kf, const osg
                                  float nnratio, int check_orientation, int32_t *out_mp, int32_t *nmatches);
 int osg_search_by_bow_kf_kf_batch(osg_ctx *ctx, const osg_bow_side *kf1, const osg_bow_side *kf2, int32_t B,
                                   float nnratio, int check_orientation, int32_t *out_mp12, int32_t *nmatches);
+
+/* ---- b1/b2: Fuse — the search half ------------------------------------------------------------
+ *   gated = 1  Fuse(KeyFrame*, const vector<MapPoint*>&, th, bRight)         ref:src/ORBmatcher.cc:1330-1541
+ *              (LocalMapping::SearchInNeighbors, ref:src/LocalMapping.cc:1021-1063)
+ *   gated = 0  Fuse(KeyFrame*, Sophus::Sim3f&, const vector<MapPoint*>&, th,
+ *              vector<MapPoint*>&)                                            ref:src/ORBmatcher.cc:1553-1694
+ *              (LoopClosing; right = 0)
+ * The caller applies the reference's pre-search filters per MapPoint (isBad, already in the KF,
+ * negative depth, outside the image, dist3D outside [min, max] invariance, viewing angle > 60 deg)
+ * and projects it with the KF camera (ref:src/ORBmatcher.cc:1366-1429).  The device does the rest
+ * of the loop body up to the best candidate: KeyFrame::GetFeaturesInArea(u, v, th *
+ * mvScaleFactors[pred_level], right) (ref:src/KeyFrame.cc:859-907), the level window
+ * [pred_level - 1, pred_level], for gated = 1 the reprojection gate (chi2 7.8 with u_right[idx]
+ * >= 0, else 5.99, times mvInvLevelSigma2[octave]; ref:src/ORBmatcher.cc:1452-1486), and the
+ * minimum DescriptorDistance (strict '<': the first candidate in area order wins).
+ * Outputs per MapPoint: best_idx = the KF keypoint index (right camera: nleft + i) when the best
+ * distance is <= TH_LOW, else -1; best_dist = the best distance (256 when no candidate).  Returns
+ * the number of best_idx >= 0.  The replace / add step that follows mutates the map and stays
+ * with the caller, in MapPoint order (the results stay exact under it). */
+typedef struct osg_fuse_queries {
+    int32_t n;
+    const uint8_t *desc;           /* n x 32: MapPoint::GetDescriptor() */
+    const uint8_t *valid;          /* passed the pre-search filters */
+    const float *u, *v;            /* pCamera->project(Tcw * p3Dw) */
+    const float *ur;               /* u - mbf * invz (gated = 1; may be NULL when no keypoint has u_right >= 0) */
+    const int32_t *pred_level;     /* MapPoint::PredictScale(dist3D, pKF) */
+    const float *inv_level_sigma2; /* pKF->mvInvLevelSigma2[n_levels] (gated = 1) */
+} osg_fuse_queries;
+
+int osg_fuse_search(osg_ctx *ctx, const osg_frame *KF, const osg_fuse_queries *Q, float th, int right, int gated,
+                    int32_t *best_idx, int32_t *best_dist);
+/* B (KeyFrame, MapPoint list) problems in one launch (SearchInNeighbors fuses one list into ~20
+ * neighbours).  Outputs concatenated in problem order by Q[b].n; nfused[b] as the single form. */
+int osg_fuse_search_batch(osg_ctx *ctx, const osg_frame *KF, const osg_fuse_queries *Q, int32_t B, float th,
+                          int right, int gated, int32_t *best_idx, int32_t *best_dist, int32_t *nfused);
 
 /* Diagnostics of the last search call on this context (summed / maxed over a batch): out[0]
  * candidates enumerated, out[1] Jacobi rounds, out[2] problems whose greedy was redone serially (a5 on a two-camera rig when a

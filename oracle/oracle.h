@@ -35,6 +35,9 @@ int oracle_search_by_bow_kf_kf(const osg_bow_side *K1, const osg_bow_side *K2, f
 
 /* DBoW2 vocabulary transform (oracle_dbow.c) */
 void oracle_dbow_transform(const osg_vocabulary_desc *V, const uint8_t *desc, int n, int levelsup, osg_bow_out *out);
+/* Fuse search half (oracle_fuse.c) */
+int oracle_fuse_search(const osg_frame *KF, const osg_fuse_queries *Q, float th, int right, int gated,
+                       int32_t *best_idx, int32_t *best_dist);
 void oracle_dbow_transform_batch(const osg_vocabulary_desc *V, const uint8_t *desc, const int32_t *n, int B,
                                  int levelsup, osg_bow_out *out);
 

@@ -73,6 +73,13 @@ class OsgKfQueries(C.Structure):
     ]
 
 
+class OsgFuseQueries(C.Structure):
+    _fields_ = [
+        ("n", i32), ("desc", P), ("valid", P), ("u", P), ("v", P), ("ur", P), ("pred_level", P),
+        ("inv_level_sigma2", P),
+    ]
+
+
 class OsgFeatVec(C.Structure):
     _fields_ = [("n_nodes", i32), ("node_id", P), ("node_start", P), ("feat", P)]
 
@@ -148,6 +155,7 @@ EXPORTS = [
     "osg_local_bundle_adjustment", "osg_local_bundle_adjustment_batch",
     "osg_vocabulary_create", "osg_vocabulary_load_text", "osg_vocabulary_destroy", "osg_vocabulary_info",
     "osg_vocabulary_transform", "osg_vocabulary_transform_batch",
+    "osg_fuse_search", "osg_fuse_search_batch",
 ]
 
 
@@ -200,4 +208,7 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.osg_vocabulary_info.argtypes = [vp, vp]
     lib.osg_vocabulary_transform.argtypes = [vp, vp, vp, i32, i32, C.POINTER(OsgBowOut)]
     lib.osg_vocabulary_transform_batch.argtypes = [vp, vp, vp, vp, i32, i32, vp]
+    lib.osg_fuse_search.argtypes = [vp, C.POINTER(OsgFrame), C.POINTER(OsgFuseQueries), f32, C.c_int, C.c_int,
+                                    vp, vp]
+    lib.osg_fuse_search_batch.argtypes = [vp, vp, vp, i32, f32, C.c_int, C.c_int, vp, vp, vp]
     return lib

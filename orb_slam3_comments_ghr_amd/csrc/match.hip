@@ -1493,6 +1493,8 @@ int run_single(osg_ctx *ctx, Prep prep)
 
 }  // namespace
 
+int osg_check_frame(osg_ctx *ctx, const osg_frame *F) { return check_frame(ctx, F); }
+
 extern "C" {
 
 int osg_search_by_projection_mps(osg_ctx *ctx, const osg_frame *F, const osg_mp_queries *Q, float nnratio,

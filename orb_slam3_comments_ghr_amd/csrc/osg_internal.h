@@ -68,6 +68,9 @@ void *osg_pinned(osg_ctx *ctx, size_t bytes);
                                          (size_t)(bytes));                                   \
     } while (0)
 
+// frame view validation (match.hip): array presence, grids index [0, n_cam), octaves in [0, 128)
+int osg_check_frame(osg_ctx *ctx, const osg_frame *F);
+
 // internal device-pointer launchers shared between translation units
 int osg_launch_top2(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d_train, int32_t nt,
                     void *d_out);

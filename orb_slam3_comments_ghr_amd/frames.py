@@ -229,6 +229,42 @@ class KFQueries:
 
 
 @dataclass
+class FuseQueries:
+    """MapPoints projected into a KeyFrame for ORBmatcher::Fuse (ref:src/ORBmatcher.cc:1366-1437):
+    the caller's pre-search filters folded into ``valid``, the projection, ur = u - bf * invz,
+    PredictScale, and the KeyFrame's mvInvLevelSigma2."""
+    desc: np.ndarray
+    valid: np.ndarray
+    u: np.ndarray
+    v: np.ndarray
+    ur: np.ndarray | None
+    pred_level: np.ndarray
+    inv_level_sigma2: np.ndarray
+
+    def __post_init__(self):
+        for k, dt in [("desc", np.uint8), ("valid", np.uint8), ("u", np.float32), ("v", np.float32),
+                      ("ur", np.float32), ("pred_level", np.int32), ("inv_level_sigma2", np.float32)]:
+            setattr(self, k, _c(getattr(self, k), dt))
+
+    @property
+    def n(self):
+        return len(self.valid)
+
+    def struct(self):
+        s = _abi.OsgFuseQueries()
+        s.n = self.n
+        for k in ["desc", "valid", "u", "v", "ur", "pred_level", "inv_level_sigma2"]:
+            setattr(s, k, _p(getattr(self, k)))
+        return s
+
+
+def inv_level_sigma2(scale):
+    """ORBextractor: mvLevelSigma2 = s * s, mvInvLevelSigma2 = 1.0f / mvLevelSigma2 (float)."""
+    s = np.asarray(scale, np.float32)
+    return (np.float32(1.0) / (s * s)).astype(np.float32)
+
+
+@dataclass
 class BowSide:
     """One side of SearchByBoW: descriptors, angles, map-point slots and the FeatureVector."""
     desc: np.ndarray
@@ -352,6 +388,29 @@ def synth_kf_queries(rng, F: FrameSoA, n_kf=1000, noise_px=2.0, match_frac=0.6):
     ang = np.where(is_match, F.kp_angle[tgt] + 7.0 + rng.normal(0, 3, n_kf), rng.uniform(0, 360, n_kf))
     return KFQueries(mp_id=3000 + np.arange(n_kf), desc=desc, valid=rng.random(n_kf) < 0.7, u=u, v=v,
                      pred_level=lvl, angle=np.mod(ang, 360))
+
+
+def synth_fuse_queries(rng, F: FrameSoA, m=1000, noise_px=1.0, match_frac=0.6, valid_frac=0.85, right=False):
+    """MapPoints of a neighbouring keyframe projected into keyframe F (LocalMapping::SearchInNeighbors):
+    match_frac of them land near a keypoint of F (pixel noise, the keypoint's octave or one above as
+    the predicted level, a noisy copy of its descriptor, ur near its u_R), the rest anywhere."""
+    lo, hi = (F.nleft, F.n) if right else (0, F.n if F.nleft < 0 else F.nleft)
+    tgt = rng.integers(lo, max(hi, lo + 1), m)
+    is_match = (rng.random(m) < match_frac) & (hi > lo)
+    tgt = np.minimum(tgt, max(F.n - 1, 0))
+    u = np.where(is_match, F.kp_x[tgt] + rng.normal(0, noise_px, m), rng.uniform(F.min_x, F.max_x, m))
+    v = np.where(is_match, F.kp_y[tgt] + rng.normal(0, noise_px, m), rng.uniform(F.min_y, F.max_y, m))
+    nl = len(F.scale)
+    lvl = np.where(is_match, np.clip(F.kp_octave[tgt] + rng.integers(0, 2, m), 0, nl - 1), rng.integers(0, nl, m))
+    desc = rng.integers(0, 256, (m, 32), dtype=np.uint8)
+    desc[is_match] = _flip(rng, F.desc[tgt[is_match]], 0.05)
+    ur = u - EUROC_BF / rng.uniform(1, 10, m)
+    if F.u_right is not None:
+        loc = tgt - (F.nleft if right else 0)
+        kr = F.u_right[np.clip(loc, 0, F.n - 1)]
+        ur = np.where(is_match & (kr >= 0), kr + rng.normal(0, noise_px, m), ur)
+    return FuseQueries(desc=desc, valid=rng.random(m) < valid_frac, u=u, v=v, ur=ur, pred_level=lvl,
+                       inv_level_sigma2=inv_level_sigma2(F.scale))
 
 
 def _featvec(rng, n, n_nodes, zipf=1.1, node_base=0):

@@ -8,6 +8,8 @@ runs on the GPU (there is no CPU fallback).
     n = m.SearchByProjection(CF, kfq, th, ORBdist, slot_mp=slots)               # (Frame&, KeyFrame*, set)
     n, vpMapPointMatches = m.SearchByBoW(KF, F)                                 # (KeyFrame*, Frame&)
     n, vpMatches12 = m.SearchByBoW(KF1, KF2, kf2=True)                          # (KeyFrame*, KeyFrame*)
+    n, best_idx, best_dist = m.Fuse(KF, fq, th=3.0, bRight=False)               # Fuse(KeyFrame*, vector<MapPoint*>)
+    n, best_idx, best_dist = m.Fuse(KF, fq, th, sim3=True)                      # Fuse(KeyFrame*, Sim3f, ...)
 """
 from __future__ import annotations
 
@@ -16,7 +18,7 @@ import ctypes as C
 import numpy as np
 
 from . import Context, _abi, descriptor_distance
-from .frames import BowSide, FrameSoA, KFQueries, LastQueries, MPQueries
+from .frames import BowSide, FrameSoA, FuseQueries, KFQueries, LastQueries, MPQueries
 
 
 class ORBmatcher:
@@ -79,6 +81,37 @@ class ORBmatcher:
         rc = lib.osg_search_by_bow_kf_kf(h, C.byref(a), C.byref(b), self.mfNNratio,
                                          int(self.mbCheckOrientation), out.ctypes.data)
         return self.ctx.check(rc, "SearchByBoW(KeyFrame, KeyFrame)"), out
+
+    def Fuse(self, KF: FrameSoA, fq: FuseQueries, th: float = 3.0, bRight: bool = False, sim3: bool = False):
+        """The search half of ``Fuse`` (ref:src/ORBmatcher.cc:1330-1541; ``sim3=True``: the Sim3
+        overload :1553-1694, no reprojection gate).  Returns (nfused, best_idx, best_dist): per MapPoint
+        the KeyFrame keypoint to fuse with (-1 = none).  The replace / add step is the caller's."""
+        lib, h = self.ctx.lib, self.ctx.handle
+        bi = np.full(fq.n, -1, np.int32)
+        bd = np.full(fq.n, 256, np.int32)
+        fs, qs = KF.struct(), fq.struct()
+        rc = lib.osg_fuse_search(h, C.byref(fs), C.byref(qs), float(th), int(bool(bRight)), int(not sim3),
+                                 bi.ctypes.data, bd.ctypes.data)
+        return self.ctx.check(rc, "Fuse"), bi, bd
+
+    def FuseBatch(self, KFs, fqs, th: float = 3.0, bRight: bool = False, sim3: bool = False):
+        """B (KeyFrame, MapPoint list) Fuse searches in one launch; returns (nfused[B], [best_idx],
+        [best_dist])."""
+        lib, h = self.ctx.lib, self.ctx.handle
+        B = len(KFs)
+        assert len(fqs) == B
+        fa = (_abi.OsgFrame * B)(*[F.struct() for F in KFs])
+        qa = (_abi.OsgFuseQueries * B)(*[q.struct() for q in fqs])
+        tot = sum(q.n for q in fqs)
+        bi = np.full(tot, -1, np.int32)
+        bd = np.full(tot, 256, np.int32)
+        nf = np.zeros(B, np.int32)
+        rc = lib.osg_fuse_search_batch(h, C.addressof(fa), C.addressof(qa), B, float(th), int(bool(bRight)),
+                                       int(not sim3), bi.ctypes.data, bd.ctypes.data, nf.ctypes.data)
+        self.ctx.check(rc, "Fuse batch")
+        cuts = np.cumsum([0] + [q.n for q in fqs])
+        return nf, [bi[a:b].copy() for a, b in zip(cuts[:-1], cuts[1:])], [bd[a:b].copy() for a, b in
+                                                                           zip(cuts[:-1], cuts[1:])]
 
     # ---- batched forms (no reference counterpart: B independent problems in one launch) -------
 

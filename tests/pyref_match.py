@@ -334,3 +334,46 @@ def search_bow_kf_kf(K1, K2, nn, ori):
     if ori:
         nm = apply_hist(hist, out, nm)
     return nm, out
+
+
+def fuse_search(F, Q, th, right=False, gated=True):
+    """Search half of ORBmatcher::Fuse (both overloads): KeyFrame::GetFeaturesInArea (no levels),
+    level window [pred-1, pred], chi2 gate (gated), strict '<' best, accept <= TH_LOW."""
+    n = len(Q.valid)
+    bi = np.full(n, -1, np.int32)
+    bd = np.full(n, 256, np.int32)
+    off = F.nleft if right else 0
+    nf = 0
+    for i in range(n):
+        if not Q.valid[i]:
+            continue
+        lvl = int(Q.pred_level[i])
+        rad = f32(f32(th) * F.scale[lvl])
+        u, v = f32(Q.u[i]), f32(Q.v[i])
+        best, besti = (256 if gated else 2 ** 31 - 1), -1
+        for idx in features_in_area(F, u, v, rad, -1, -1, right=right):
+            k = idx + off
+            o = int(F.kp_octave[k])
+            if o < lvl - 1 or o > lvl:
+                continue
+            if gated:
+                ex, ey = f32(u - F.kp_x[k]), f32(v - F.kp_y[k])
+                inv = f32(Q.inv_level_sigma2[o])
+                kr = F.u_right[idx] if F.u_right is not None else f32(-1)
+                if kr >= 0:
+                    er = f32(f32(Q.ur[i]) - f32(kr))
+                    e2 = f32(f32(f32(ex * ex) + f32(ey * ey)) + f32(er * er))
+                    if float(f32(e2 * inv)) > 7.8:
+                        continue
+                else:
+                    e2 = f32(f32(ex * ex) + f32(ey * ey))
+                    if float(f32(e2 * inv)) > 5.99:
+                        continue
+            d = dist(Q.desc[i], F.desc[k])
+            if d < best:
+                best, besti = d, k
+        bd[i] = min(best, 256)
+        if best <= TH_LOW:
+            bi[i] = besti
+            nf += 1
+    return nf, bi, bd

@@ -190,3 +190,52 @@ def test_oracle_bow_two_cam_vs_python(oracle, seed):
         assert got[0] == ref[0]
         np.testing.assert_array_equal(got[1], ref[1])
         assert (got[1][K1.nleft:] == -1).all()
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_oracle_fuse_vs_python(oracle, seed):
+    """Fuse search half, both overloads (gated: Fuse(KF, vpMapPoints); ungated: the Sim3 Fuse)."""
+    rng = np.random.default_rng(700 + seed)
+    F = small_frame(rng, n=300)
+    Q = fr.synth_fuse_queries(rng, F, m=300, noise_px=1.5)
+    for th, gated in [(3.0, True), (1.0, True), (5.0, False), (3.0, False)]:
+        got = oc.fuse(oracle, F, Q, th, gated=gated)
+        ref = pr.fuse_search(F, Q, th, gated=gated)
+        assert got[0] == ref[0] and got[0] > 20
+        np.testing.assert_array_equal(got[1], ref[1])
+        np.testing.assert_array_equal(got[2], ref[2])
+
+
+def test_oracle_fuse_two_cam_vs_python(oracle):
+    """bRight: the right grid, mvKeysRight, mvuRight[local idx], best index offset by NLeft."""
+    rng = np.random.default_rng(710)
+    F = two_cam_frame(rng)
+    for right in (False, True):
+        Q = fr.synth_fuse_queries(rng, F, m=300, noise_px=1.5, right=right)
+        got = oc.fuse(oracle, F, Q, 3.0, right=right)
+        ref = pr.fuse_search(F, Q, 3.0, right=right)
+        assert got[0] == ref[0] and got[0] > 10
+        np.testing.assert_array_equal(got[1], ref[1])
+        np.testing.assert_array_equal(got[2], ref[2])
+        if right:
+            assert (got[1][got[1] >= 0] >= F.nleft).all()
+
+
+def test_oracle_fuse_gate_hand_case(oracle):
+    """Known answer for the chi2 gate: a keypoint 2 px away at octave 0 (invSigma2 = 1) passes the
+    mono gate (4 <= 5.99); 2.5 px fails it (6.25 > 5.99); a stereo keypoint 1.5 px off in u and
+    2.5 px in u_R fails the stereo gate (2.25 + 6.25 = 8.5 > 7.8)."""
+    n = 3
+    desc = np.zeros((n, 32), np.uint8)
+    F = fr.FrameSoA(desc=desc, kp_x=np.array([100.0, 200.0, 300.0], np.float32),
+                    kp_y=np.array([100.0, 100.0, 100.0], np.float32), kp_angle=np.zeros(n, np.float32),
+                    kp_octave=np.zeros(n, np.int32), u_right=np.array([-1.0, -1.0, 280.0], np.float32))
+    Q = fr.FuseQueries(desc=np.zeros((3, 32), np.uint8), valid=np.ones(3, np.uint8),
+                       u=np.array([102.0, 202.5, 301.5], np.float32), v=np.array([100.0, 100.0, 100.0], np.float32),
+                       ur=np.array([0.0, 0.0, 282.5], np.float32), pred_level=np.zeros(3, np.int32),
+                       inv_level_sigma2=fr.inv_level_sigma2(F.scale))
+    n_f, bi, bd = oc.fuse(oracle, F, Q, 3.0)
+    assert list(bi) == [0, -1, -1] and n_f == 1
+    assert list(pr.fuse_search(F, Q, 3.0)[1]) == [0, -1, -1]
+    n_f, bi, bd = oc.fuse(oracle, F, Q, 3.0, gated=False)  # Sim3 Fuse: no gate
+    assert list(bi) == [0, 1, 2] and list(bd) == [0, 0, 0]
