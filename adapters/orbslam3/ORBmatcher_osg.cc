@@ -1,6 +1,7 @@
 // ORBmatcher_osg.cc — drop-in bodies for the ORBmatcher operators on the MI355X path, for an
 // ORB-SLAM3 tree built with -DORB_SLAM3_OSG.  The reference's
-// src/ORBmatcher.cc keeps every other member; the bodies below replace the six hot-path ones
+// src/ORBmatcher.cc keeps every other member; the bodies below replace the six hot-path ones and
+// the two Fuse overloads
 // under #ifdef ORB_SLAM3_OSG (signatures: ref:include/ORBmatcher.h:36-66).
 #include "ORBmatcher.h"
 #include "osg_hooks_orbslam3.h"
@@ -39,6 +40,17 @@ int ORBmatcher::SearchByBoW(KeyFrame *pKF, Frame &F, std::vector<MapPoint *> &vp
 int ORBmatcher::SearchByBoW(KeyFrame *pKF1, KeyFrame *pKF2, std::vector<MapPoint *> &vpMatches12)
 {  // ref:src/ORBmatcher.cc:890-1043
     return osg_orbslam3::search_by_bow_kf_kf<H>(pKF1, pKF2, vpMatches12, mfNNratio, mbCheckOrientation);
+}
+
+int ORBmatcher::Fuse(KeyFrame *pKF, const std::vector<MapPoint *> &vpMapPoints, const float th, const bool bRight)
+{  // ref:src/ORBmatcher.cc:1330-1541
+    return osg_orbslam3::fuse<H>(pKF, vpMapPoints, th, bRight);
+}
+
+int ORBmatcher::Fuse(KeyFrame *pKF, Sophus::Sim3f &Scw, const std::vector<MapPoint *> &vpPoints, float th,
+                     std::vector<MapPoint *> &vpReplacePoint)
+{  // ref:src/ORBmatcher.cc:1553-1694
+    return osg_orbslam3::fuse_sim3<H>(pKF, Scw, vpPoints, th, vpReplacePoint);
 }
 
 }  // namespace ORB_SLAM3

@@ -104,6 +104,56 @@ struct OsgHooks {
         v = uv(1);
         return true;
     }
+    // ref:src/ORBmatcher.cc:1336-1347, 1385-1433 (Fuse): pose / centre / camera of the chosen side,
+    // depth, projection, IsInImage, ur, scale-invariance range, viewing angle, PredictScale
+    static bool fuse_query(KeyFrame *pKF, MapPoint *pMP, bool bRight, float &u, float &v, float &ur, int &level)
+    {
+        const Sophus::SE3f Tcw = bRight ? pKF->GetRightPose() : pKF->GetPose();
+        const Eigen::Vector3f Ow = bRight ? pKF->GetRightCameraCenter() : pKF->GetCameraCenter();
+        GeometricCamera *pCamera = bRight ? pKF->mpCamera2 : pKF->mpCamera;
+        const float &bf = pKF->mbf;
+        const Eigen::Vector3f p3Dw = pMP->GetWorldPos();
+        const Eigen::Vector3f p3Dc = Tcw * p3Dw;
+        if (p3Dc(2) < 0.0f) return false;
+        const float invz = 1 / p3Dc(2);
+        const Eigen::Vector2f uv = pCamera->project(p3Dc);
+        if (!pKF->IsInImage(uv(0), uv(1))) return false;
+        ur = uv(0) - bf * invz;
+        const float maxDistance = pMP->GetMaxDistanceInvariance();
+        const float minDistance = pMP->GetMinDistanceInvariance();
+        const Eigen::Vector3f PO = p3Dw - Ow;
+        const float dist3D = PO.norm();
+        if (dist3D < minDistance || dist3D > maxDistance) return false;
+        const Eigen::Vector3f Pn = pMP->GetNormal();
+        if (PO.dot(Pn) < 0.5 * dist3D) return false;
+        level = pMP->PredictScale(dist3D, pKF);
+        u = uv(0);
+        v = uv(1);
+        return true;
+    }
+    // ref:src/ORBmatcher.cc:1560-1562, 1587-1622 (Fuse with Sim3): the same tests with Tcw from Scw
+    static bool fuse_sim3_query(KeyFrame *pKF, const Sophus::Sim3f &Scw, MapPoint *pMP, float &u, float &v,
+                                int &level)
+    {
+        const Sophus::SE3f Tcw = Sophus::SE3f(Scw.rotationMatrix(), Scw.translation() / Scw.scale());
+        const Eigen::Vector3f Ow = Tcw.inverse().translation();
+        const Eigen::Vector3f p3Dw = pMP->GetWorldPos();
+        const Eigen::Vector3f p3Dc = Tcw * p3Dw;
+        if (p3Dc(2) < 0.0f) return false;
+        const Eigen::Vector2f uv = pKF->mpCamera->project(p3Dc);
+        if (!pKF->IsInImage(uv(0), uv(1))) return false;
+        const float maxDistance = pMP->GetMaxDistanceInvariance();
+        const float minDistance = pMP->GetMinDistanceInvariance();
+        const Eigen::Vector3f PO = p3Dw - Ow;
+        const float dist3D = PO.norm();
+        if (dist3D < minDistance || dist3D > maxDistance) return false;
+        const Eigen::Vector3f Pn = pMP->GetNormal();
+        if (PO.dot(Pn) < 0.5 * dist3D) return false;
+        level = pMP->PredictScale(dist3D, pKF);
+        u = uv(0);
+        v = uv(1);
+        return true;
+    }
 };
 
 }  // namespace ORB_SLAM3

@@ -19,6 +19,7 @@
 //   static float H::tlc_z(const Frame& CF, const Frame& LF)          (Tlw * twc)(2), ref:src/ORBmatcher.cc:1972-1980
 //   static bool  H::kf_query(const Frame& CF, MapPoint*, float& u, float& v, int& level)
 //                ref:src/ORBmatcher.cc:2238-2262 (project, image bounds, distance range, PredictScale)
+//   static bool  H::fuse_query / H::fuse_sim3_query   see b1/b2 Fuse below
 #ifndef OSG_ORBSLAM3_H
 #define OSG_ORBSLAM3_H
 
@@ -104,9 +105,21 @@ inline void grid_csr(const GridT &grid, std::vector<int32_t> &gs, std::vector<in
     for (int c = 0; c < OSG_GRID_CELLS; c++) gs[c + 1] += gs[c];
 }
 
-// osg_frame of a Frame (ref:include/Frame.h:218-296): keypoints (mvKeysUn, or mvKeys + mvKeysRight
-// for a two-camera rig), descriptors, mvuRight, mGrid (+ mGridRight, mvLeftToRightMatch,
-// mvRightToLeftMatch for a two-camera rig).
+// Frame::Nleft / KeyFrame::NLeft (ref:include/Frame.h, include/KeyFrame.h spell it differently)
+template <class T>
+inline auto nleft_of(const T &F, int) -> decltype(F.Nleft, int())
+{
+    return F.Nleft;
+}
+template <class T>
+inline auto nleft_of(const T &F, long) -> decltype(F.NLeft, int())
+{
+    return F.NLeft;
+}
+
+// osg_frame of a Frame or KeyFrame (ref:include/Frame.h:218-296, include/KeyFrame.h:321-508):
+// keypoints (mvKeysUn, or mvKeys + mvKeysRight for a two-camera rig), descriptors, mvuRight, mGrid
+// (+ mGridRight, mvLeftToRightMatch, mvRightToLeftMatch for a two-camera rig).
 template <class FrameT>
 struct FrameView {
     std::vector<float> kx, ky, ka, ur, scale;
@@ -116,23 +129,23 @@ struct FrameView {
 
     explicit FrameView(const FrameT &F)
     {
-        const int n = F.N;
-        if (F.Nleft == -1) {
+        const int n = F.N, nleft = nleft_of(F, 0);
+        if (nleft == -1) {
             for (int i = 0; i < n; i++) push_kp(F.mvKeysUn[i], kx, ky, ka, ko);
         } else {
-            for (int i = 0; i < F.Nleft; i++) push_kp(F.mvKeys[i], kx, ky, ka, ko);
-            for (int i = F.Nleft; i < n; i++) push_kp(F.mvKeysRight[i - F.Nleft], kx, ky, ka, ko);
+            for (int i = 0; i < nleft; i++) push_kp(F.mvKeys[i], kx, ky, ka, ko);
+            for (int i = nleft; i < n; i++) push_kp(F.mvKeysRight[i - nleft], kx, ky, ka, ko);
         }
         copy_desc_rows(F.mDescriptors, n, desc);
         ur.assign(F.mvuRight.begin(), F.mvuRight.end());
         ur.resize(n, -1.0f);
         grid_csr(F.mGrid, gs, gi);
-        if (F.Nleft != -1) {
+        if (nleft != -1) {
             grid_csr(F.mGridRight, gsr, gir);
             l2r.assign(F.mvLeftToRightMatch.begin(), F.mvLeftToRightMatch.end());
             r2l.assign(F.mvRightToLeftMatch.begin(), F.mvRightToLeftMatch.end());
-            l2r.resize(F.Nleft, -1);
-            r2l.resize(n - F.Nleft, -1);
+            l2r.resize(nleft, -1);
+            r2l.resize(n - nleft, -1);
             v.grid_start_r = gsr.data();
             v.grid_idx_r = gir.data();
             v.left_to_right = l2r.data();
@@ -140,7 +153,7 @@ struct FrameView {
         }
         scale.assign(F.mvScaleFactors.begin(), F.mvScaleFactors.end());
         v.n = n;
-        v.nleft = F.Nleft;
+        v.nleft = nleft;
         v.desc = desc.data();
         v.kp_x = kx.data();
         v.kp_y = ky.data();
@@ -353,6 +366,126 @@ int search_by_projection_kf(FrameT &CF, KeyFrameT *pKF, const std::set<MapPointT
                          "osg_search_by_projection_kf");
     slots.apply(CF.mvpMapPoints, vpMPs, n);
     return nm;
+}
+
+// ---------------------------------------------------------------------------------- b1/b2 Fuse
+// The reference's loop is "for each MapPoint in order: filters, search, then replace / add", and the
+// replace / add mutates the map.  Here the search of every MapPoint runs first (one launch) and
+// the replace / add runs after it, in order, re-checking the filters that can change inside the
+// loop.  That is the same result because nothing a replace / add does changes the search of a
+// MapPoint that still passes those checks:
+//   * the search reads the KeyFrame's keypoints / grid (never mutated here) and the MapPoint's
+//     position, normal, distances (unchanged by Replace / AddObservation) and descriptor;
+//   * a descriptor changes only on the survivor of a Replace (MapPoint::Replace ->
+//     ComputeDistinctiveDescriptors, ref:src/MapPoint.cc:313-395), and the survivor is in pKF
+//     afterwards (it held, or took over, the slot bestIdx), so its own later turn is skipped by
+//     IsInKeyFrame(pKF);
+//   * isBad() / IsInKeyFrame(pKF) can only become true during the loop (Replace marks the
+//     replaced point bad; AddObservation adds pKF), so the gather-time filter keeps a superset and
+//     the apply-time re-check removes exactly the ones the reference skips.
+// Fuse(pKF, vpMapPoints, th, bRight), ref:src/ORBmatcher.cc:1330-1541.  Hook:
+//   static bool H::fuse_query(KeyFrame*, MapPoint*, bool right, float& u, float& v, float& ur, int& level)
+//                ref:src/ORBmatcher.cc:1336-1347, 1385-1433 (Tcw * p3Dw, depth, project, IsInImage, ur, distance
+//                range, viewing angle, PredictScale); false = skipped
+template <class H, class KeyFrameT, class MapPointT>
+int fuse(KeyFrameT *pKF, const std::vector<MapPointT *> &vpMapPoints, float th, bool bRight)
+{
+    osg_ctx *ctx = thread_ctx();
+    FrameView<KeyFrameT> fv(*pKF);
+    const int n = (int)vpMapPoints.size();
+    std::vector<uint8_t> desc((size_t)n * 32), valid(n, 0);
+    std::vector<float> u(n, 0.f), v(n, 0.f), ur(n, 0.f);
+    std::vector<int32_t> lvl(n, 0), best_idx(n, -1), best_dist(n, 256);
+    for (int i = 0; i < n; i++) {
+        MapPointT *p = vpMapPoints[i];
+        if (!p || p->isBad() || p->IsInKeyFrame(pKF)) continue;  // ref:src/ORBmatcher.cc:1367-1382
+        if (!H::fuse_query(pKF, p, bRight, u[i], v[i], ur[i], lvl[i])) continue;
+        valid[i] = 1;
+        const auto d = p->GetDescriptor();
+        std::memcpy(&desc[(size_t)32 * i], d.template ptr<unsigned char>(0), 32);
+    }
+    std::vector<float> inv_s2(pKF->mvInvLevelSigma2.begin(), pKF->mvInvLevelSigma2.end());
+    osg_fuse_queries q{};
+    q.n = n;
+    q.desc = desc.data();
+    q.valid = valid.data();
+    q.u = u.data();
+    q.v = v.data();
+    q.ur = ur.data();
+    q.pred_level = lvl.data();
+    q.inv_level_sigma2 = inv_s2.data();
+    check(ctx, osg_fuse_search(ctx, &fv.v, &q, th, bRight ? 1 : 0, 1, best_idx.data(), best_dist.data()),
+          "osg_fuse_search");
+    int nFused = 0;
+    for (int i = 0; i < n; i++) {  // ref:src/ORBmatcher.cc:1514-1539, in MapPoint order
+        MapPointT *pMP = vpMapPoints[i];
+        if (!valid[i] || best_idx[i] < 0) continue;
+        if (pMP->isBad() || pMP->IsInKeyFrame(pKF)) continue;  // changed earlier in this loop
+        const int bestIdx = best_idx[i];
+        MapPointT *pMPinKF = pKF->GetMapPoint(bestIdx);
+        if (pMPinKF) {
+            if (!pMPinKF->isBad()) {
+                if (pMPinKF->Observations() > pMP->Observations())
+                    pMP->Replace(pMPinKF);
+                else
+                    pMPinKF->Replace(pMP);
+            }
+        } else {
+            pMP->AddObservation(pKF, bestIdx);
+            pKF->AddMapPoint(pMP, bestIdx);
+        }
+        nFused++;
+    }
+    return nFused;
+}
+
+// Fuse(pKF, Scw, vpPoints, th, vpReplacePoint), ref:src/ORBmatcher.cc:1553-1694 (LoopClosing).
+// Nothing in this loop makes a point bad, and spAlreadyFound is a snapshot, so the filters are
+// static; only GetMapPoint(bestIdx) sees earlier iterations' AddMapPoint, and the apply reads it
+// in order.  Hook:
+//   static bool H::fuse_sim3_query(KeyFrame*, const Sim3&, MapPoint*, float& u, float& v, int& level)
+//                ref:src/ORBmatcher.cc:1560-1562, 1587-1622; false = skipped
+template <class H, class KeyFrameT, class Sim3T, class MapPointT>
+int fuse_sim3(KeyFrameT *pKF, const Sim3T &Scw, const std::vector<MapPointT *> &vpPoints, float th,
+              std::vector<MapPointT *> &vpReplacePoint)
+{
+    osg_ctx *ctx = thread_ctx();
+    FrameView<KeyFrameT> fv(*pKF);
+    const auto spAlreadyFound = pKF->GetMapPoints();
+    const int n = (int)vpPoints.size();
+    std::vector<uint8_t> desc((size_t)n * 32), valid(n, 0);
+    std::vector<float> u(n, 0.f), v(n, 0.f);
+    std::vector<int32_t> lvl(n, 0), best_idx(n, -1), best_dist(n, 256);
+    for (int i = 0; i < n; i++) {
+        MapPointT *p = vpPoints[i];
+        if (p->isBad() || spAlreadyFound.count(p)) continue;  // ref:src/ORBmatcher.cc:1582
+        if (!H::fuse_sim3_query(pKF, Scw, p, u[i], v[i], lvl[i])) continue;
+        valid[i] = 1;
+        const auto d = p->GetDescriptor();
+        std::memcpy(&desc[(size_t)32 * i], d.template ptr<unsigned char>(0), 32);
+    }
+    osg_fuse_queries q{};
+    q.n = n;
+    q.desc = desc.data();
+    q.valid = valid.data();
+    q.u = u.data();
+    q.v = v.data();
+    q.pred_level = lvl.data();
+    check(ctx, osg_fuse_search(ctx, &fv.v, &q, th, 0, 0, best_idx.data(), best_dist.data()), "osg_fuse_search");
+    int nFused = 0;
+    for (int i = 0; i < n; i++) {  // ref:src/ORBmatcher.cc:1661-1681
+        if (!valid[i] || best_idx[i] < 0) continue;
+        MapPointT *pMP = vpPoints[i];
+        MapPointT *pMPinKF = pKF->GetMapPoint(best_idx[i]);
+        if (pMPinKF) {
+            if (!pMPinKF->isBad()) vpReplacePoint[i] = pMPinKF;
+        } else {
+            pMP->AddObservation(pKF, best_idx[i]);
+            pKF->AddMapPoint(pMP, best_idx[i]);
+        }
+        nFused++;
+    }
+    return nFused;
 }
 
 // ------------------------------------------------------------------------------- a3/a4 BoW

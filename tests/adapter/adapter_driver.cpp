@@ -1,7 +1,7 @@
 // adapter_driver.cpp — runs adapters/orbslam3/osg_orbslam3.h on mock ORB-SLAM3 objects built from
 // arrays written by tests/test_adapter.py, and writes the adapter's results back (test-only).
 //
-//   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba
+//   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba fuse fuse_sim3
 //
 // Array file: repeated {u32 name_len, name, u8 dtype ('b' u8, 'i' i32, 'f' f32, 'd' f64), u64 count,
 // data}.
@@ -203,6 +203,40 @@ static void build_bow_kf(const Arrays &m, const std::string &pre, KeyFrame &K, s
             K.mvpMapPoints[i] = pool.back().get();
         }
     fill_featvec(m, pre, K.mFeatVec);
+}
+
+// KeyFrame with keypoints / grid / scales from the FrameSoA arrays "F.*" (Fuse target)
+static void build_kf_frame(const Arrays &m, KeyFrame &K)
+{
+    Frame F;
+    build_frame(m, F);
+    K.N = F.N;
+    K.NLeft = F.Nleft;
+    K.mvKeys = F.mvKeys;
+    K.mvKeysUn = F.mvKeysUn;
+    K.mvKeysRight = F.mvKeysRight;
+    K.mDescriptors = F.mDescriptors;
+    K.mvuRight = F.mvuRight;
+    K.mGrid.assign(OSG_GRID_COLS, std::vector<std::vector<std::size_t>>(OSG_GRID_ROWS));
+    K.mGridRight.assign(OSG_GRID_COLS, std::vector<std::vector<std::size_t>>(OSG_GRID_ROWS));
+    for (int ix = 0; ix < OSG_GRID_COLS; ix++)
+        for (int iy = 0; iy < OSG_GRID_ROWS; iy++) {
+            K.mGrid[ix][iy] = F.mGrid[ix][iy];
+            K.mGridRight[ix][iy] = F.mGridRight[ix][iy];
+        }
+    K.mvLeftToRightMatch = F.mvLeftToRightMatch;
+    K.mvRightToLeftMatch = F.mvRightToLeftMatch;
+    K.mnMinX = (int)Frame::mnMinX;
+    K.mnMaxX = (int)Frame::mnMaxX;
+    K.mnMinY = (int)Frame::mnMinY;
+    K.mnMaxY = (int)Frame::mnMaxY;
+    K.mfGridElementWidthInv = Frame::mfGridElementWidthInv;
+    K.mfGridElementHeightInv = Frame::mfGridElementHeightInv;
+    K.mvScaleFactors = F.mvScaleFactors;
+    K.mnScaleLevels = F.mnScaleLevels;
+    K.mb = F.mb;
+    K.mbf = F.mbf;
+    K.mvpMapPoints.assign(K.N, nullptr);
 }
 
 int main(int argc, char **argv)
@@ -436,6 +470,56 @@ int main(int argc, char **argv)
             out["point"] = make('d', point);
             out["edge_bad"] = make('b', bad);
             out["num_edges"] = make('i', std::vector<int32_t>{o.num_edges});
+        } else if (mode == "fuse" || mode == "fuse_sim3") {
+            // pool of MapPoints "P.*" (index = id), the keyframe's slot occupants "K.slot_mp", the
+            // list to fuse "L.list" (pool indices, -1 = NULL); params: th right
+            KeyFrame K;
+            build_kf_frame(in, K);
+            const Arr &is2 = get(in, "K.inv_s2");
+            K.mvInvLevelSigma2.assign(is2.p<float>(), is2.p<float>() + is2.n);
+            const int np = (int)get(in, "P.nobs").n;
+            std::vector<MapPoint> P(np);
+            for (int i = 0; i < np; i++) {
+                MapPoint &p = P[i];
+                p.mnId = (unsigned long)i;
+                std::memcpy(p.desc.buf.data(), get(in, "P.desc").p<uint8_t>() + 32 * i, 32);
+                p.proj_ok = get(in, "P.ok").p<uint8_t>()[i];
+                p.proj_u = get(in, "P.u").p<float>()[i];
+                p.proj_v = get(in, "P.v").p<float>()[i];
+                p.proj_fuse_ur = get(in, "P.ur").p<float>()[i];
+                p.proj_level = get(in, "P.level").p<int32_t>()[i];
+                p.bad = get(in, "P.bad").p<uint8_t>()[i];
+                p.nobs = get(in, "P.nobs").p<int32_t>()[i];
+            }
+            const int32_t *sm = get(in, "K.slot_mp").p<int32_t>();
+            for (int k = 0; k < K.N; k++)
+                if (sm[k] >= 0) {
+                    K.mvpMapPoints[k] = &P[sm[k]];
+                    P[sm[k]].obs[&K] = std::make_tuple(k, -1);
+                }
+            const Arr &L = get(in, "L.list");
+            std::vector<MapPoint *> list(L.n);
+            for (size_t i = 0; i < L.n; i++) list[i] = L.p<int32_t>()[i] < 0 ? nullptr : &P[L.p<int32_t>()[i]];
+            int nf;
+            std::vector<int32_t> repl(L.n, -1);
+            if (mode == "fuse") {
+                nf = osg_orbslam3::fuse<MockHooks>(&K, list, prm[0], prm[1] != 0);
+            } else {
+                std::vector<MapPoint *> vpReplace(L.n, nullptr);
+                nf = osg_orbslam3::fuse_sim3<MockHooks>(&K, Sim3{}, list, prm[0], vpReplace);
+                for (size_t i = 0; i < L.n; i++) repl[i] = vpReplace[i] ? (int32_t)vpReplace[i]->mnId : -1;
+            }
+            std::vector<uint8_t> bad(np);
+            std::vector<int32_t> nobs(np);
+            for (int i = 0; i < np; i++) {
+                bad[i] = P[i].bad;
+                nobs[i] = P[i].nobs;
+            }
+            out["nfused"] = make('i', std::vector<int32_t>{nf});
+            out["slot_mp"] = make('i', slot_ids(K.mvpMapPoints));
+            out["bad"] = make('b', bad);
+            out["nobs"] = make('i', nobs);
+            out["replace"] = make('i', repl);
         } else {
             fprintf(stderr, "unknown mode %s\n", mode.c_str());
             return 2;

@@ -59,7 +59,7 @@ struct MapPoint {
     float mTrackViewCos = 0, mTrackViewCosR = 0;
     // test-only: what MockHooks::project_last / kf_query return for this MapPoint
     bool proj_ok = false;
-    float proj_u = 0, proj_v = 0, proj_invz = 0, proj_ur = 0, proj_vr = 0;
+    float proj_u = 0, proj_v = 0, proj_invz = 0, proj_ur = 0, proj_vr = 0, proj_fuse_ur = 0;
     int proj_level = 0;
     std::map<KeyFrame *, std::tuple<int, int>> obs;
 
@@ -68,6 +68,16 @@ struct MapPoint {
     cv::Mat GetDescriptor() const { return desc; }
     std::map<KeyFrame *, std::tuple<int, int>> GetObservations() const { return obs; }
     void EraseObservation(KeyFrame *k) { obs.erase(k); }
+    bool IsInKeyFrame(KeyFrame *k) const { return obs.count(k) != 0; }
+    void AddObservation(KeyFrame *k, int idx)
+    {
+        obs[k] = std::make_tuple(idx, -1);
+        nobs++;
+    }
+    // MapPoint::Replace (ref:src/MapPoint.cc:313-395) over the keyframes this test models; the
+    // observations in other keyframes (nobs - obs.size()) move along; the survivor's descriptor
+    // changes as ComputeDistinctiveDescriptors would (test-only: byte 0 ^= 0x5A)
+    void Replace(MapPoint *p);
 };
 
 struct Frame {
@@ -101,9 +111,16 @@ struct KeyFrame {
     std::vector<float> mvuRight, mvInvLevelSigma2;
     std::vector<MapPoint *> mvpMapPoints;
     std::map<unsigned int, std::vector<unsigned int>> mFeatVec;
-    float mbf = 0, fx = 0, fy = 0, cx = 0, cy = 0;
+    float mbf = 0, mb = 0, fx = 0, fy = 0, cx = 0, cy = 0;
     Camera *mpCamera = nullptr, *mpCamera2 = nullptr;
     double pose[7] = {0, 0, 0, 1, 0, 0, 0};
+    // grid fields as in ref:include/KeyFrame.h:321-508 (mnMinX.. are int there)
+    std::vector<std::vector<std::vector<std::size_t>>> mGrid, mGridRight;
+    std::vector<int> mvLeftToRightMatch, mvRightToLeftMatch;
+    int mnMinX = 0, mnMaxX = 0, mnMinY = 0, mnMaxY = 0;
+    float mfGridElementWidthInv = 0, mfGridElementHeightInv = 0;
+    int mnScaleLevels = 8;
+    std::vector<float> mvScaleFactors;
 
     std::vector<MapPoint *> GetMapPointMatches() const { return mvpMapPoints; }
     bool isBad() const { return bad; }
@@ -113,7 +130,39 @@ struct KeyFrame {
         for (auto &q : mvpMapPoints)
             if (q == p) q = nullptr;
     }
+    MapPoint *GetMapPoint(std::size_t idx) const { return mvpMapPoints[idx]; }
+    void AddMapPoint(MapPoint *p, std::size_t idx) { mvpMapPoints[idx] = p; }
+    std::set<MapPoint *> GetMapPoints() const
+    {  // ref:src/KeyFrame.cc GetMapPoints: the non-NULL, non-bad slot occupants
+        std::set<MapPoint *> s;
+        for (MapPoint *p : mvpMapPoints)
+            if (p && !p->isBad()) s.insert(p);
+        return s;
+    }
 };
+
+inline void MapPoint::Replace(MapPoint *p)
+{
+    if (p->mnId == mnId) return;
+    const int other = nobs - (int)obs.size();
+    auto o = obs;
+    obs.clear();
+    bad = true;
+    for (auto &kv : o) {
+        KeyFrame *k = kv.first;
+        const int li = std::get<0>(kv.second);
+        if (!p->IsInKeyFrame(k)) {
+            k->mvpMapPoints[li] = p;
+            p->AddObservation(k, li);
+        } else {
+            k->mvpMapPoints[li] = nullptr;
+        }
+    }
+    p->nobs += other;
+    p->desc.buf[0] ^= 0x5A;
+}
+
+struct Sim3 {};  // Fuse(KeyFrame*, Sim3f&, ...): the projection is MockHooks' (test-only)
 
 struct MockHooks {
     template <class T>
@@ -151,6 +200,21 @@ struct MockHooks {
     }
     static float tlc_z(const Frame &CF, const Frame &) { return CF.tlc_z_value; }
     static bool kf_query(const Frame &, MapPoint *p, float &u, float &v, int &level)
+    {
+        u = p->proj_u;
+        v = p->proj_v;
+        level = p->proj_level;
+        return p->proj_ok;
+    }
+    static bool fuse_query(KeyFrame *, MapPoint *p, bool, float &u, float &v, float &ur, int &level)
+    {
+        u = p->proj_u;
+        v = p->proj_v;
+        ur = p->proj_fuse_ur;
+        level = p->proj_level;
+        return p->proj_ok;
+    }
+    static bool fuse_sim3_query(KeyFrame *, const Sim3 &, MapPoint *p, float &u, float &v, int &level)
     {
         u = p->proj_u;
         v = p->proj_v;

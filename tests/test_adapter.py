@@ -263,3 +263,183 @@ def test_adapter_local_bundle_adjustment(driver, tmp_path, ctx):
     np.testing.assert_array_equal(out["edge_bad"], ref.edge_bad)
     np.testing.assert_array_equal(out["pose"].reshape(-1, 7), ref.pose.reshape(-1, 7))
     np.testing.assert_array_equal(out["point"].reshape(-1, 3), ref.point.reshape(-1, 3))
+
+
+def _fuse_world(rng, F, m_new=500, occ_frac=0.3, n_occ_in_list=60, null_frac=0.0):
+    """A keyframe with slot occupants and a MapPoint list to fuse into it (new points, some
+    occupants, some bad, optional NULLs) with many list points landing on the same keypoints."""
+    n = F.n
+    occ = np.nonzero(rng.random(n) < occ_frac)[0]
+    Q = fr.synth_fuse_queries(rng, F, m=m_new, noise_px=1.0, match_frac=0.8)
+    n_occ = len(occ)
+    npool = n_occ + m_new
+    desc = np.concatenate([F.desc[occ], Q.desc]) if n_occ else Q.desc.copy()
+    P = {"desc": desc, "ok": np.concatenate([np.ones(n_occ, np.uint8), Q.valid]),
+         "u": np.concatenate([F.kp_x[occ], Q.u]).astype(np.float32),
+         "v": np.concatenate([F.kp_y[occ], Q.v]).astype(np.float32),
+         "ur": np.concatenate([np.zeros(n_occ, np.float32), Q.ur]).astype(np.float32),
+         "level": np.concatenate([F.kp_octave[occ], Q.pred_level]).astype(np.int32),
+         "bad": (rng.random(npool) < 0.05).astype(np.uint8),
+         "nobs": rng.integers(1, 7, npool).astype(np.int32)}
+    slot_mp = np.full(n, -1, np.int32)
+    slot_mp[occ] = np.arange(n_occ, dtype=np.int32)
+    lst = list(range(n_occ, npool)) + list(rng.choice(n_occ, size=min(n_occ_in_list, n_occ), replace=False))
+    lst = np.array(lst, np.int32)
+    rng.shuffle(lst)
+    if null_frac:
+        lst[rng.random(len(lst)) < null_frac] = -1
+    return P, slot_mp, lst, fr.inv_level_sigma2(F.scale)
+
+
+def _model_fuse(oracle, F, inv_s2, P, slot_mp, lst, th, sim3):
+    """The reference's loop (ref:src/ORBmatcher.cc:1359-1541 / 1566-1694) run literally over the
+    mock world: each MapPoint searched at its own turn with its current descriptor, then replace /
+    add (MapPoint::Replace as the mock models it)."""
+    desc = P["desc"].copy()
+    bad = P["bad"].astype(bool).copy()
+    nobs = P["nobs"].copy()
+    slot = slot_mp.copy()
+    in_k = {int(p): k for k, p in enumerate(slot) if p >= 0}
+    snapshot = {int(p) for p in slot if p >= 0 and not bad[p]}
+    replace = np.full(len(lst), -1, np.int32)
+    nf = 0
+
+    def do_replace(a, b):  # a->Replace(b)
+        if a == b:
+            return
+        other = nobs[a] - (1 if a in in_k else 0)
+        bad[a] = True
+        if a in in_k:
+            li = in_k.pop(a)
+            if b not in in_k:
+                slot[li] = b
+                in_k[b] = li
+                nobs[b] += 1
+            else:
+                slot[li] = -1
+        nobs[b] += other
+        desc[b, 0] ^= 0x5A
+
+    for i, p in enumerate(lst):
+        p = int(p)
+        if p < 0:
+            continue
+        if bad[p] or (p in snapshot if sim3 else p in in_k):
+            continue
+        if not P["ok"][p]:
+            continue
+        q = fr.FuseQueries(desc=desc[p:p + 1], valid=np.ones(1), u=P["u"][p:p + 1], v=P["v"][p:p + 1],
+                           ur=P["ur"][p:p + 1], pred_level=P["level"][p:p + 1], inv_level_sigma2=inv_s2)
+        b = int(oc.fuse(oracle, F, q, th, gated=not sim3)[1][0])
+        if b < 0:
+            continue
+        pin = int(slot[b])
+        if pin >= 0:
+            if not bad[pin]:
+                if sim3:
+                    replace[i] = pin
+                elif nobs[pin] > nobs[p]:
+                    do_replace(p, pin)
+                else:
+                    do_replace(pin, p)
+        else:
+            in_k[p] = b
+            nobs[p] += 1
+            slot[b] = p
+        nf += 1
+    return nf, slot, bad, nobs, replace
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sim3", [False, True])
+def test_adapter_fuse(driver, tmp_path, oracle, sim3):
+    """Fuse through the adapter (GPU search of every MapPoint, then replace / add in order) equals
+    the reference's loop run literally, search by search, on the same mock map — including
+    Replace chains on shared keypoints and survivors whose descriptor changed mid-loop."""
+    rng = np.random.default_rng(760 + int(sim3))
+    F = fr.synth_frame(rng, n=600)
+    P, slot_mp, lst, inv_s2 = _fuse_world(rng, F, null_frac=0.0 if sim3 else 0.03)
+    th = 3.0
+    arrays = {**frame_arrays(F), "K.inv_s2": inv_s2, "K.slot_mp": slot_mp, "L.list": lst,
+              "params": np.array([th, 0.0], np.float32)}
+    for k, a in P.items():
+        arrays["P." + k] = a.reshape(-1)
+    out = run(driver, tmp_path, "fuse_sim3" if sim3 else "fuse", arrays)
+    nf, slot, bad, nobs, replace = _model_fuse(oracle, F, inv_s2, P, slot_mp, lst, th, sim3)
+    assert nf > 100
+    if not sim3:
+        assert bad.sum() > P["bad"].sum() + 10, "the world must exercise Replace"
+    assert int(out["nfused"][0]) == nf
+    np.testing.assert_array_equal(out["slot_mp"], slot)
+    np.testing.assert_array_equal(out["bad"].astype(bool), bad)
+    np.testing.assert_array_equal(out["nobs"], nobs)
+    np.testing.assert_array_equal(out["replace"], replace)
+
+
+@pytest.mark.parametrize("seed", range(3))
+@pytest.mark.parametrize("sim3", [False, True])
+def test_fuse_split_equals_literal_loop(oracle, seed, sim3):
+    """CPU, oracle only: the adapter's strategy — search every MapPoint first (gather-time state),
+    then replace / add in order re-checking isBad / IsInKeyFrame — gives exactly the literal
+    reference loop (osg_orbslam3.h explains why); this is what lets the search run as one launch."""
+    rng = np.random.default_rng(900 + seed + 10 * int(sim3))
+    F = fr.synth_frame(rng, n=500)
+    P, slot_mp, lst, inv_s2 = _fuse_world(rng, F, m_new=400, null_frac=0.0 if sim3 else 0.03)
+    th = 3.0
+    ref = _model_fuse(oracle, F, inv_s2, P, slot_mp, lst, th, sim3)
+    # split: one search over the gather-time state
+    bad0 = P["bad"].astype(bool)
+    in_k0 = {int(p) for p in slot_mp if p >= 0}
+    idx = np.maximum(lst, 0)
+    valid = (lst >= 0) & ~bad0[idx] & np.array([int(p) not in in_k0 for p in idx]) & (P["ok"][idx] != 0)
+    q = fr.FuseQueries(desc=P["desc"][idx], valid=valid, u=P["u"][idx], v=P["v"][idx], ur=P["ur"][idx],
+                       pred_level=P["level"][idx], inv_level_sigma2=inv_s2)
+    _, best, _ = oc.fuse(oracle, F, q, th, gated=not sim3)
+    bad = bad0.copy()
+    nobs = P["nobs"].copy()
+    slot = slot_mp.copy()
+    in_k = {int(p): k for k, p in enumerate(slot) if p >= 0}
+    replace = np.full(len(lst), -1, np.int32)
+    nf = 0
+
+    def do_replace(a, b):
+        if a == b:
+            return
+        other = nobs[a] - (1 if a in in_k else 0)
+        bad[a] = True
+        if a in in_k:
+            li = in_k.pop(a)
+            if b not in in_k:
+                slot[li] = b
+                in_k[b] = li
+                nobs[b] += 1
+            else:
+                slot[li] = -1
+        nobs[b] += other
+
+    for i, p in enumerate(lst):
+        if not valid[i] or best[i] < 0:
+            continue
+        p = int(p)
+        if not sim3 and (bad[p] or p in in_k):
+            continue
+        b = int(best[i])
+        pin = int(slot[b])
+        if pin >= 0:
+            if not bad[pin]:
+                if sim3:
+                    replace[i] = pin
+                elif nobs[pin] > nobs[p]:
+                    do_replace(p, pin)
+                else:
+                    do_replace(pin, p)
+        else:
+            in_k[p] = b
+            nobs[p] += 1
+            slot[b] = p
+        nf += 1
+    assert nf == ref[0]
+    np.testing.assert_array_equal(slot, ref[1])
+    np.testing.assert_array_equal(bad, ref[2])
+    np.testing.assert_array_equal(nobs, ref[3])
+    np.testing.assert_array_equal(replace, ref[4])
