@@ -11,7 +11,7 @@ HIPFLAGS = --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-functio
 EXACT = -ffp-contract=off
 HDRS = include/osg.h include/osg_ba.h $(CSRC)/osg_internal.h
 
-OBJS = $(OBJDIR)/runtime.o $(OBJDIR)/hamming.o $(OBJDIR)/match.o $(OBJDIR)/pose.o $(OBJDIR)/ba.o $(OBJDIR)/dbow.o $(OBJDIR)/fuse.o
+OBJS = $(OBJDIR)/runtime.o $(OBJDIR)/hamming.o $(OBJDIR)/match.o $(OBJDIR)/pose.o $(OBJDIR)/ba.o $(OBJDIR)/dbow.o $(OBJDIR)/fuse.o $(OBJDIR)/triang.o
 
 all: $(LIB) oracle
 
@@ -32,6 +32,9 @@ $(OBJDIR)/dbow.o: $(CSRC)/dbow.hip $(HDRS) include/osg_dbow.h $(CSRC)/match_comm
 	$(HIPCC) $(HIPFLAGS) $(EXACT) -c $< -o $@
 
 $(OBJDIR)/fuse.o: $(CSRC)/fuse.hip $(HDRS) $(CSRC)/match_common.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) $(EXACT) -c $< -o $@
+
+$(OBJDIR)/triang.o: $(CSRC)/triang.hip $(HDRS) $(CSRC)/match_common.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(EXACT) -c $< -o $@
 
 $(LIB): $(OBJS)

@@ -281,6 +281,56 @@ int osg_fuse_search(osg_ctx *ctx, const osg_frame *KF, const osg_fuse_queries *Q
 int osg_fuse_search_batch(osg_ctx *ctx, const osg_frame *KF, const osg_fuse_queries *Q, int32_t B, float th,
                           int right, int gated, int32_t *best_idx, int32_t *best_dist, int32_t *nfused);
 
+/* ---- b3: SearchForTriangulation ---------------------------------------------------------------
+ * ORBmatcher::SearchForTriangulation(KeyFrame *pKF1, KeyFrame *pKF2, vector<pair<size_t,size_t>>&,
+ * bOnlyStereo, bCoarse)  ref:src/ORBmatcher.cc:1045-1328 (LocalMapping::CreateNewMapPoints,
+ * ref:src/LocalMapping.cc:630).  For every KF1 keypoint without a MapPoint in a vocabulary node
+ * shared with KF2: the KF2 keypoint of the same node without a MapPoint that minimises the distance
+ * (<= TH_LOW; '<=' so the LAST of equal distances in node order wins, ref:src/ORBmatcher.cc:1180),
+ * passing the epipole-distance test (both keypoints monocular, no second camera,
+ * ref:src/ORBmatcher.cc:1189-1203) and, unless bCoarse, Pinhole::epipolarConstrain
+ * (ref:src/CameraModels/Pinhole.cpp:189-219).  Then the rotation histogram + ComputeThreeMaxima.
+ * In this fork vbMatched2[bestIdx2] = true is commented out (ref:src/ORBmatcher.cc:1262), so KF1
+ * keypoints never compete for a KF2 keypoint: every query is independent. */
+typedef struct osg_kf_side {
+    int32_t n;                  /* KeyFrame::N */
+    int32_t nleft;              /* NLeft, -1 without a two-camera rig */
+    int32_t two_cam;            /* mpCamera2 != NULL */
+    const uint8_t *desc;        /* n x 32 */
+    const float *kp_x, *kp_y;   /* (NLeft == -1) ? mvKeysUn : idx < NLeft ? mvKeys : mvKeysRight[idx - NLeft] */
+    const float *kp_angle;
+    const int32_t *kp_octave;
+    const float *u_right;       /* mvuRight[n] (NULL: all < 0) */
+    const uint8_t *has_mp;      /* GetMapPoint(i) != NULL */
+    const float *level_sigma2;  /* mvLevelSigma2[n_levels] */
+    const float *scale_factors; /* mvScaleFactors[n_levels] */
+    int32_t n_levels;
+    osg_featvec fv;             /* mFeatVec */
+} osg_kf_side;
+
+/* The two-view geometry the reference computes with Sophus / Eigen before its loop
+ * (ref:src/ORBmatcher.cc:1052-1083), supplied by the caller so the float values are the reference's
+ * own.  F12[k] = K1^-T * [t12]x * R12 * K2^-1 (Pinhole.cpp:194-197), row-major, for the camera pair
+ * k = 2 * bRight1 + bRight2 (ll, lr, rl, rr: T12 = Tll, Tlr, Trl, Trr, ref:src/ORBmatcher.cc:1205-1244);
+ * only F12[0] is read without a rig.  pinhole = 0 (KannalaBrandt8: epipolarConstrain triangulates
+ * through Eigen's JacobiSVD) is accepted only with coarse = 1. */
+typedef struct osg_triang_geom {
+    float ep_x, ep_y;           /* pKF2->mpCamera->project(T2w * pKF1->GetCameraCenter()) */
+    float F12[4][9];
+    int32_t pinhole;
+} osg_triang_geom;
+
+/* match12[kf1.n]: KF2 keypoint index per KF1 keypoint (vMatches12 after the histogram), -1 = none.
+ * vMatchedPairs = the (i, match12[i] >= 0) in ascending i.  Returns nmatches. */
+int osg_search_for_triangulation(osg_ctx *ctx, const osg_kf_side *kf1, const osg_kf_side *kf2,
+                                 const osg_triang_geom *geom, int only_stereo, int coarse,
+                                 int check_orientation, int32_t *match12);
+/* B keyframe pairs in one launch (CreateNewMapPoints: the new keyframe against its ~10-20
+ * neighbours).  match12 concatenated in problem order by kf1[b].n; nmatches[b] as the single form. */
+int osg_search_for_triangulation_batch(osg_ctx *ctx, const osg_kf_side *kf1, const osg_kf_side *kf2,
+                                       const osg_triang_geom *geom, int32_t B, int only_stereo, int coarse,
+                                       int check_orientation, int32_t *match12, int32_t *nmatches);
+
 /* Diagnostics of the last search call on this context (summed / maxed over a batch): out[0]
  * candidates enumerated, out[1] Jacobi rounds, out[2] problems whose greedy was redone serially (a5 on a two-camera rig when a
  * stereo-partner write by a MapPoint without observations unblocked a slot), out[3] nmatches.

@@ -91,6 +91,18 @@ class OsgBowSide(C.Structure):
     ]
 
 
+class OsgKfSide(C.Structure):
+    _fields_ = [
+        ("n", i32), ("nleft", i32), ("two_cam", i32), ("desc", P), ("kp_x", P), ("kp_y", P), ("kp_angle", P),
+        ("kp_octave", P), ("u_right", P), ("has_mp", P), ("level_sigma2", P), ("scale_factors", P),
+        ("n_levels", i32), ("fv", OsgFeatVec),
+    ]
+
+
+class OsgTriangGeom(C.Structure):
+    _fields_ = [("ep_x", f32), ("ep_y", f32), ("F12", f32 * 36), ("pinhole", i32)]
+
+
 class OsgCamera(C.Structure):
     _fields_ = [
         ("type", i32), ("p", f32 * 8), ("fx", f32), ("fy", f32), ("cx", f32), ("cy", f32),
@@ -155,7 +167,7 @@ EXPORTS = [
     "osg_local_bundle_adjustment", "osg_local_bundle_adjustment_batch",
     "osg_vocabulary_create", "osg_vocabulary_load_text", "osg_vocabulary_destroy", "osg_vocabulary_info",
     "osg_vocabulary_transform", "osg_vocabulary_transform_batch",
-    "osg_fuse_search", "osg_fuse_search_batch",
+    "osg_fuse_search", "osg_fuse_search_batch", "osg_search_for_triangulation", "osg_search_for_triangulation_batch",
 ]
 
 
@@ -211,4 +223,7 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.osg_fuse_search.argtypes = [vp, C.POINTER(OsgFrame), C.POINTER(OsgFuseQueries), f32, C.c_int, C.c_int,
                                     vp, vp]
     lib.osg_fuse_search_batch.argtypes = [vp, vp, vp, i32, f32, C.c_int, C.c_int, vp, vp, vp]
+    lib.osg_search_for_triangulation.argtypes = [vp, C.POINTER(OsgKfSide), C.POINTER(OsgKfSide),
+                                                 C.POINTER(OsgTriangGeom), C.c_int, C.c_int, C.c_int, vp]
+    lib.osg_search_for_triangulation_batch.argtypes = [vp, vp, vp, vp, i32, C.c_int, C.c_int, C.c_int, vp, vp]
     return lib

@@ -558,3 +558,202 @@ def synth_last_queries_two_cam(rng, F: FrameSoA, n_last=800, noise_px=2.0, match
     L.v_r = np.where(ok, F.kp_y[nl + trc] + rng.normal(0, noise_px, n_last),
                      rng.uniform(-20, F.max_y + 20, n_last)).astype(np.float32)
     return L
+
+
+# ------------------------------------------------------------- b3 SearchForTriangulation
+
+@dataclass
+class KFSide:
+    """One keyframe of SearchForTriangulation (osg_kf_side): keypoints as the reference indexes them
+    (mvKeysUn, or mvKeys / mvKeysRight on a two-camera rig), mvuRight, MapPoint presence, the level
+    tables and mFeatVec as CSR."""
+    desc: np.ndarray
+    kp_x: np.ndarray
+    kp_y: np.ndarray
+    kp_angle: np.ndarray
+    kp_octave: np.ndarray
+    u_right: np.ndarray | None
+    has_mp: np.ndarray
+    node_id: np.ndarray
+    node_start: np.ndarray
+    feat: np.ndarray
+    nleft: int = -1
+    two_cam: int = 0
+    scale: np.ndarray = field(default_factory=scale_factors)
+
+    def __post_init__(self):
+        self.desc = _c(self.desc, np.uint8).reshape(-1, 32)
+        self.kp_x = _c(self.kp_x, np.float32)
+        self.kp_y = _c(self.kp_y, np.float32)
+        self.kp_angle = _c(self.kp_angle, np.float32)
+        self.kp_octave = _c(self.kp_octave, np.int32)
+        self.u_right = _c(self.u_right, np.float32)
+        self.has_mp = _c(self.has_mp, np.uint8)
+        self.node_id = _c(self.node_id, np.uint32)
+        self.node_start = _c(self.node_start, np.int32)
+        self.feat = _c(self.feat, np.int32)
+        self.scale = _c(self.scale, np.float32)
+        self.level_sigma2 = (self.scale * self.scale).astype(np.float32)  # ORBextractor: s * s in float
+
+    @property
+    def n(self):
+        return self.desc.shape[0]
+
+    def struct(self):
+        s = _abi.OsgKfSide()
+        s.n, s.nleft, s.two_cam = self.n, self.nleft, int(self.two_cam)
+        s.desc = _p(self.desc)
+        s.kp_x, s.kp_y = _p(self.kp_x), _p(self.kp_y)
+        s.kp_angle, s.kp_octave = _p(self.kp_angle), _p(self.kp_octave)
+        s.u_right = _p(self.u_right)
+        s.has_mp = _p(self.has_mp)
+        s.level_sigma2 = _p(self.level_sigma2)
+        s.scale_factors = _p(self.scale)
+        s.n_levels = len(self.scale)
+        s.fv.n_nodes = len(self.node_id)
+        s.fv.node_id = _p(self.node_id)
+        s.fv.node_start = _p(self.node_start)
+        s.fv.feat = _p(self.feat)
+        return s
+
+
+@dataclass
+class TriangGeom:
+    """The epipole and the fundamental matrices the reference builds before its loop
+    (ref:src/ORBmatcher.cc:1052-1083; Pinhole.cpp:194-197): F12[k] for k = 2 * bRight1 + bRight2."""
+    ep: tuple
+    F12: np.ndarray            # (4, 3, 3) float32; [0] only without a rig
+    pinhole: bool = True
+
+    def struct(self):
+        s = _abi.OsgTriangGeom()
+        s.ep_x, s.ep_y = float(self.ep[0]), float(self.ep[1])
+        F = np.zeros((4, 3, 3), np.float32)
+        F[:len(self.F12)] = self.F12
+        for i, v in enumerate(F.reshape(-1)):
+            s.F12[i] = float(v)
+        s.pinhole = int(bool(self.pinhole))
+        return s
+
+
+def _rot(rng, deg):
+    ax = rng.normal(size=3)
+    ax /= np.linalg.norm(ax)
+    th = np.deg2rad(deg)
+    Kx = np.array([[0, -ax[2], ax[1]], [ax[2], 0, -ax[0]], [-ax[1], ax[0], 0]])
+    return np.eye(3) + np.sin(th) * Kx + (1 - np.cos(th)) * Kx @ Kx
+
+
+def fundamental(K1, K2, R12, t12):
+    """Pinhole::epipolarConstrain's F12 = K1^-T [t12]x R12 K2^-1 (float64 here, stored as float)."""
+    tx = np.array([[0, -t12[2], t12[1]], [t12[2], 0, -t12[0]], [-t12[1], t12[0], 0]])
+    return (np.linalg.inv(K1).T @ tx @ R12 @ np.linalg.inv(K2)).astype(np.float32)
+
+
+def synth_triang_pair(rng, n1=1000, n2=1000, n_nodes=100, common=0.6, mp_frac=0.5, stereo=True, forward=False,
+                      two_cam=False, noise=0.7, flip=0.05, n_levels=8, distract=0.15):
+    """Two keyframes seeing one scene (EuRoC pinhole, 752x480): KF2 is KF1 moved 0.25 m sideways
+    (``forward``: 0.4 m along the optical axis, so the epipole lies in the image) and turned 2 deg.
+    ``common`` of the keypoints are projections of shared points (noise ``noise`` px x 1.2^octave,
+    noisy descriptor copies, same vocabulary node, angle offset -7 +- 3 deg); the rest are random.
+    ``mp_frac`` of each side already carry a MapPoint; ``stereo`` gives half of them a mvuRight.
+    ``two_cam``: each keyframe is a two-camera rig (Nleft = n/2; right camera 0.11 m to the right),
+    keypoints [0, Nleft) in the left camera, the rest in the right one.  Returns (KF1, KF2, geom)."""
+    from .synth import EUROC_CX, EUROC_CY, EUROC_FY
+    K = np.array([[EUROC_FX, 0, EUROC_CX], [0, EUROC_FY, EUROC_CY], [0, 0, 1.0]])
+    R2 = _rot(rng, 2.0)
+    C2 = np.array([0.05, 0.01, 0.4]) if forward else np.array([0.25, 0.02, 0.03])
+    Tcw = {(1, 0): (np.eye(3), np.zeros(3)), (2, 0): (R2, -R2 @ C2)}
+    b = np.array([-0.11, 0.0, 0.0])  # right camera: x_r = x_l + b
+    if two_cam:
+        for k in (1, 2):
+            R, t = Tcw[(k, 0)]
+            Tcw[(k, 1)] = (R, t + b)
+    ns = (n1, n2)
+    nleft = [n // 2 if two_cam else -1 for n in ns]
+    cams = [np.where(np.arange(n) < nl, 0, 1) if two_cam else np.zeros(n, int) for n, nl in zip(ns, nleft)]
+    p = np.array([1.2 ** -i for i in range(n_levels)])
+    octs = [rng.choice(n_levels, size=n, p=p / p.sum()).astype(np.int32) for n in ns]
+    xs = [rng.uniform(0, EUROC_W, n) for n in ns]
+    ys = [rng.uniform(0, EUROC_H, n) for n in ns]
+    angs = [rng.uniform(0, 360, n) for n in ns]
+    descs = [rng.integers(0, 256, (n, 32), dtype=np.uint8) for n in ns]
+    w = 1.0 / np.arange(1, n_nodes + 1) ** 1.1
+    nodes = [rng.choice(n_nodes, size=n, p=w / w.sum()) for n in ns]
+    depth = [rng.uniform(1, 10, n) for n in ns]
+    # shared points: pick KF1 keypoints, back-project to a depth, reproject into KF2's camera
+    m = int(common * min(n1, n2))
+    i1 = rng.choice(n1, size=m, replace=False)
+    i2 = rng.choice(n2, size=m, replace=False)
+    Kinv = np.linalg.inv(K)
+    keep = np.zeros(m, bool)
+    for j in range(m):
+        a, c = i1[j], i2[j]
+        R1, t1 = Tcw[(1, cams[0][a])]
+        Xc = Kinv @ np.array([xs[0][a], ys[0][a], 1.0]) * rng.uniform(2, 8)
+        Xw = R1.T @ (Xc - t1)
+        R, t = Tcw[(2, cams[1][c])]
+        X2 = R @ Xw + t
+        if X2[2] <= 0.1:
+            continue
+        u = K @ (X2 / X2[2])
+        if not (0 <= u[0] < EUROC_W and 0 <= u[1] < EUROC_H):
+            continue
+        keep[j] = True
+        s = 1.2 ** octs[0][a]
+        octs[1][c] = octs[0][a]
+        xs[1][c] = u[0] + rng.normal(0, noise * s)
+        ys[1][c] = u[1] + rng.normal(0, noise * s)
+        xs[0][a] += rng.normal(0, noise * s)
+        ys[0][a] += rng.normal(0, noise * s)
+        descs[1][c] = _flip(rng, descs[0][a][None], flip)[0]
+        nodes[1][c] = nodes[0][a]
+        angs[1][c] = np.mod(angs[0][a] - 7.0 - rng.normal(0, 3), 360)
+        depth[1][c] = X2[2]
+    # distractors: KF2 keypoints outside the shared set that copy a shared KF1 descriptor (a third
+    # exactly: ties in node order) in the same node, at a random position (or, ``forward``, beside
+    # the epipole), so the epipolar / epipole tests and the '<=' tie rule decide the best match
+    rest = np.setdiff1d(np.arange(n2), i2[keep])
+    src = i1[keep]
+    n_dis = min(len(rest), int(distract * n2)) if len(src) else 0
+    dis = rng.choice(rest, size=n_dis, replace=False)
+    for j, c in enumerate(dis):
+        a = src[rng.integers(len(src))]
+        descs[1][c] = descs[0][a] if j % 3 == 0 else _flip(rng, descs[0][a][None], 0.04)[0]
+        nodes[1][c] = nodes[0][a]
+        octs[1][c] = octs[0][a]
+    node_ids = np.sort(rng.choice(np.arange(0, 10 * n_nodes), size=n_nodes, replace=False)).astype(np.uint32)
+    sides = []
+    for k in range(2):
+        n = ns[k]
+        used = np.unique(nodes[k])
+        start = np.zeros(len(used) + 1, np.int32)
+        feats = []
+        for q, nd in enumerate(used):
+            f = np.nonzero(nodes[k] == nd)[0]
+            feats.append(f)
+            start[q + 1] = start[q] + len(f)
+        x = np.clip(xs[k], 0, EUROC_W - 1e-3).astype(np.float32)
+        ur = None
+        if stereo and not two_cam:
+            ur = np.where(rng.random(n) < 0.5, x - EUROC_BF / depth[k], -1.0).astype(np.float32)
+        sides.append(KFSide(desc=descs[k], kp_x=x, kp_y=np.clip(ys[k], 0, EUROC_H - 1e-3), kp_angle=angs[k],
+                            kp_octave=octs[k], u_right=ur, has_mp=rng.random(n) < mp_frac,
+                            node_id=node_ids[used], node_start=start, feat=np.concatenate(feats),
+                            nleft=nleft[k], two_cam=int(two_cam), scale=scale_factors(n_levels)))
+    F = []
+    for c1 in (0, 1) if two_cam else (0,):
+        for c2 in (0, 1) if two_cam else (0,):
+            R1, t1 = Tcw[(1, c1)]
+            R2_, t2 = Tcw[(2, c2)]
+            R12 = R1 @ R2_.T                 # T12 = T1w * T2w^-1
+            t12 = t1 - R12 @ t2
+            F.append(fundamental(K, K, R12, t12))
+    Rl2, tl2 = Tcw[(2, 0)]
+    e = Rl2 @ np.zeros(3) + tl2             # T2w * Cw (KF1 centre = world origin)
+    ep = (np.float32(EUROC_FX * e[0] / e[2] + EUROC_CX), np.float32(EUROC_FY * e[1] / e[2] + EUROC_CY))
+    if forward and n_dis:                   # a third of the distractors within ~20 px of the epipole
+        near = dis[: n_dis // 3]
+        sides[1].kp_x[near] = np.float32(ep[0]) + rng.uniform(-20, 20, len(near)).astype(np.float32)
+        sides[1].kp_y[near] = np.float32(ep[1]) + rng.uniform(-20, 20, len(near)).astype(np.float32)
+    return sides[0], sides[1], TriangGeom(ep=ep, F12=np.stack(F))

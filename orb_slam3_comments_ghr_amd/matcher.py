@@ -10,6 +10,7 @@ runs on the GPU (there is no CPU fallback).
     n, vpMatches12 = m.SearchByBoW(KF1, KF2, kf2=True)                          # (KeyFrame*, KeyFrame*)
     n, best_idx, best_dist = m.Fuse(KF, fq, th=3.0, bRight=False)               # Fuse(KeyFrame*, vector<MapPoint*>)
     n, best_idx, best_dist = m.Fuse(KF, fq, th, sim3=True)                      # Fuse(KeyFrame*, Sim3f, ...)
+    n, vMatchedPairs = m.SearchForTriangulation(KF1, KF2, geom, bOnlyStereo, bCoarse)
 """
 from __future__ import annotations
 
@@ -18,7 +19,7 @@ import ctypes as C
 import numpy as np
 
 from . import Context, _abi, descriptor_distance
-from .frames import BowSide, FrameSoA, FuseQueries, KFQueries, LastQueries, MPQueries
+from .frames import BowSide, FrameSoA, FuseQueries, KFQueries, KFSide, LastQueries, MPQueries, TriangGeom
 
 
 class ORBmatcher:
@@ -112,6 +113,41 @@ class ORBmatcher:
         cuts = np.cumsum([0] + [q.n for q in fqs])
         return nf, [bi[a:b].copy() for a, b in zip(cuts[:-1], cuts[1:])], [bd[a:b].copy() for a, b in
                                                                            zip(cuts[:-1], cuts[1:])]
+
+    @staticmethod
+    def _pairs(m12):
+        i = np.nonzero(m12 >= 0)[0]
+        return np.stack([i, m12[i]], axis=1).astype(np.int64)
+
+    def SearchForTriangulation(self, KF1: KFSide, KF2: KFSide, geom: TriangGeom, bOnlyStereo: bool = False,
+                               bCoarse: bool = False):
+        """``SearchForTriangulation(pKF1, pKF2, vMatchedPairs, bOnlyStereo, bCoarse)``
+        (ref:src/ORBmatcher.cc:1045-1328).  Returns (nmatches, vMatchedPairs) with vMatchedPairs an
+        (nmatches, 2) array of (KF1 index, KF2 index) in ascending KF1 index, as the reference fills it."""
+        lib, h = self.ctx.lib, self.ctx.handle
+        m12 = np.full(KF1.n, -1, np.int32)
+        a, b, g = KF1.struct(), KF2.struct(), geom.struct()
+        rc = lib.osg_search_for_triangulation(h, C.byref(a), C.byref(b), C.byref(g), int(bool(bOnlyStereo)),
+                                              int(bool(bCoarse)), int(self.mbCheckOrientation), m12.ctypes.data)
+        return self.ctx.check(rc, "SearchForTriangulation"), self._pairs(m12)
+
+    def SearchForTriangulationBatch(self, KF1s, KF2s, geoms, bOnlyStereo: bool = False, bCoarse: bool = False):
+        """B keyframe pairs in one launch (LocalMapping::CreateNewMapPoints' neighbour loop); returns
+        (nmatches[B], [vMatchedPairs])."""
+        lib, h = self.ctx.lib, self.ctx.handle
+        B = len(KF1s)
+        assert len(KF2s) == B and len(geoms) == B
+        a = (_abi.OsgKfSide * B)(*[k.struct() for k in KF1s])
+        b = (_abi.OsgKfSide * B)(*[k.struct() for k in KF2s])
+        g = (_abi.OsgTriangGeom * B)(*[x.struct() for x in geoms])
+        m12 = np.full(sum(k.n for k in KF1s), -1, np.int32)
+        nm = np.zeros(B, np.int32)
+        rc = lib.osg_search_for_triangulation_batch(h, C.addressof(a), C.addressof(b), C.addressof(g), B,
+                                                    int(bool(bOnlyStereo)), int(bool(bCoarse)),
+                                                    int(self.mbCheckOrientation), m12.ctypes.data, nm.ctypes.data)
+        self.ctx.check(rc, "SearchForTriangulation batch")
+        cuts = np.cumsum([0] + [k.n for k in KF1s])
+        return nm, [self._pairs(m12[x:y]) for x, y in zip(cuts[:-1], cuts[1:])]
 
     # ---- batched forms (no reference counterpart: B independent problems in one launch) -------
 

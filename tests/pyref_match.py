@@ -377,3 +377,69 @@ def fuse_search(F, Q, th, right=False, gated=True):
             bi[i] = besti
             nf += 1
     return nf, bi, bd
+
+
+def search_for_triangulation(K1, K2, geom, only_stereo=False, coarse=False, ori=True):
+    """ORBmatcher::SearchForTriangulation (ref:src/ORBmatcher.cc:1045-1328) with
+    Pinhole::epipolarConstrain (ref:src/CameraModels/Pinhole.cpp:189-219).  Node pairing by set
+    intersection (not the reference's lower_bound walk); returns (nmatches, pairs)."""
+    nodes1 = {int(K1.node_id[k]): K1.feat[K1.node_start[k]:K1.node_start[k + 1]] for k in range(len(K1.node_id))}
+    nodes2 = {int(K2.node_id[k]): K2.feat[K2.node_start[k]:K2.node_start[k + 1]] for k in range(len(K2.node_id))}
+    m12 = [-1] * K1.n
+    hist = [[] for _ in range(HISTO)]
+    nm = 0
+    F = geom.F12
+
+    def stereo(K, i):
+        return (not K.two_cam) and K.u_right is not None and K.u_right[i] >= 0
+
+    def right(K, i):
+        return not (K.nleft == -1 or i < K.nleft)
+
+    for node in sorted(set(nodes1) & set(nodes2)):
+        for idx1 in nodes1[node]:
+            idx1 = int(idx1)
+            if K1.has_mp[idx1]:
+                continue
+            s1 = stereo(K1, idx1)
+            if only_stereo and not s1:
+                continue
+            x1, y1 = f32(K1.kp_x[idx1]), f32(K1.kp_y[idx1])
+            best_d, best = TH_LOW, -1
+            for idx2 in nodes2[node]:
+                idx2 = int(idx2)
+                if K2.has_mp[idx2]:
+                    continue
+                s2 = stereo(K2, idx2)
+                if only_stereo and not s2:
+                    continue
+                d = dist(K1.desc[idx1], K2.desc[idx2])
+                if d > TH_LOW or d > best_d:
+                    continue
+                x2, y2 = f32(K2.kp_x[idx2]), f32(K2.kp_y[idx2])
+                o2 = int(K2.kp_octave[idx2])
+                if not s1 and not s2 and not K1.two_cam:
+                    ex, ey = f32(f32(geom.ep[0]) - x2), f32(f32(geom.ep[1]) - y2)
+                    if f32(f32(ex * ex) + f32(ey * ey)) < f32(f32(100) * K2.scale[o2]):
+                        continue
+                k = (2 * right(K1, idx1) + right(K2, idx2)) if (K1.two_cam and K2.two_cam) else 0
+                ok = coarse
+                if not ok:
+                    Fk = F[k]
+                    a = f32(f32(f32(x1 * Fk[0, 0]) + f32(y1 * Fk[1, 0])) + Fk[2, 0])
+                    b = f32(f32(f32(x1 * Fk[0, 1]) + f32(y1 * Fk[1, 1])) + Fk[2, 1])
+                    c = f32(f32(f32(x1 * Fk[0, 2]) + f32(y1 * Fk[1, 2])) + Fk[2, 2])
+                    num = f32(f32(f32(a * x2) + f32(b * y2)) + c)
+                    den = f32(f32(a * a) + f32(b * b))
+                    ok = den != 0 and float(f32(f32(num * num) / den)) < 3.84 * float(K2.level_sigma2[o2])
+                if ok:
+                    best, best_d = idx2, d
+            if best >= 0:
+                m12[idx1] = best
+                nm += 1
+                if ori:
+                    hist[rot_bin(K1.kp_angle[idx1], K2.kp_angle[best])].append(idx1)
+    if ori:
+        nm = apply_hist(hist, m12, nm)
+    pairs = [(i, j) for i, j in enumerate(m12) if j >= 0]
+    return nm, np.array(pairs, np.int64).reshape(-1, 2)

@@ -1,0 +1,83 @@
+"""GPU parity: SearchForTriangulation through the C ABI against the CPU oracle — vMatchedPairs and
+nmatches bit-exact."""
+import numpy as np
+import pytest
+
+from orb_slam3_comments_ghr_amd import OsgError
+from orb_slam3_comments_ghr_amd import frames as fr
+from orb_slam3_comments_ghr_amd.matcher import ORBmatcher
+from tests import oracle_calls as oc
+from tests.test_oracle_triang import hand_pair
+
+pytestmark = pytest.mark.gpu
+
+
+def check(got, ref, name):
+    assert got[0] == ref[0], f"{name}: nmatches {got[0]} != {ref[0]}"
+    np.testing.assert_array_equal(got[1], ref[1], err_msg=name)
+
+
+@pytest.mark.parametrize("seed", range(3))
+@pytest.mark.parametrize("forward", [False, True])
+@pytest.mark.parametrize("coarse,only_stereo,ori", [(False, False, True), (True, False, True),
+                                                    (False, True, True), (False, False, False)])
+def test_triang(ctx, oracle, seed, forward, coarse, only_stereo, ori):
+    """CreateNewMapPoints shape: two 1200-keypoint keyframes, half the keypoints with MapPoints."""
+    rng = np.random.default_rng(7200 + seed)
+    K1, K2, g = fr.synth_triang_pair(rng, n1=1200, n2=1200, forward=forward)
+    ref = oc.triangulation(oracle, K1, K2, g, only_stereo, coarse, ori)
+    got = ORBmatcher(ctx, checkOri=ori).SearchForTriangulation(K1, K2, g, only_stereo, coarse)
+    check(got, ref, "triangulation")
+    assert ref[0] > (20 if only_stereo else 50)
+
+
+@pytest.mark.parametrize("coarse", [False, True])
+def test_triang_two_cam(ctx, oracle, coarse):
+    rng = np.random.default_rng(7300)
+    K1, K2, g = fr.synth_triang_pair(rng, n1=1000, n2=1000, two_cam=True)
+    check(ORBmatcher(ctx).SearchForTriangulation(K1, K2, g, bCoarse=coarse),
+          oc.triangulation(oracle, K1, K2, g, coarse=coarse), "two-camera")
+
+
+def test_triang_hand_case(ctx, oracle):
+    m = ORBmatcher(ctx)
+    K1, K2, g = hand_pair()
+    assert m.SearchForTriangulation(K1, K2, g)[1].tolist() == [[0, 1]]
+    assert m.SearchForTriangulation(K1, K2, g, bCoarse=True)[1].tolist() == [[0, 2]]
+    K1s, K2s, gs = hand_pair(stereo1=True)
+    assert m.SearchForTriangulation(K1s, K2s, gs)[1].tolist() == [[0, 3]]
+    assert m.SearchForTriangulation(K1s, K2s, gs, bOnlyStereo=True)[0] == 0
+
+
+def test_triang_edges(ctx, oracle):
+    """No shared node, every keypoint with a MapPoint, an empty keyframe, KB8 without bCoarse."""
+    rng = np.random.default_rng(7400)
+    m = ORBmatcher(ctx)
+    K1, K2, g = fr.synth_triang_pair(rng, n1=400, n2=400, n_nodes=40)
+    K2b = fr.KFSide(desc=K2.desc, kp_x=K2.kp_x, kp_y=K2.kp_y, kp_angle=K2.kp_angle, kp_octave=K2.kp_octave,
+                    u_right=K2.u_right, has_mp=K2.has_mp, node_id=K2.node_id + 100000, node_start=K2.node_start,
+                    feat=K2.feat)
+    assert m.SearchForTriangulation(K1, K2b, g)[0] == 0
+    K1.has_mp[:] = 1
+    assert m.SearchForTriangulation(K1, K2, g)[0] == 0
+    E = fr.KFSide(desc=np.zeros((0, 32), np.uint8), kp_x=[], kp_y=[], kp_angle=[], kp_octave=[], u_right=None,
+                  has_mp=[], node_id=[], node_start=[0], feat=[])
+    assert m.SearchForTriangulation(E, K2, g)[0] == 0
+    assert m.SearchForTriangulation(K2, E, g)[0] == 0
+    g.pinhole = False
+    with pytest.raises(OsgError):
+        m.SearchForTriangulation(K2, K1, g)
+    K1.has_mp[:] = 0
+    check(m.SearchForTriangulation(K1, K2, g, bCoarse=True), oc.triangulation(oracle, K1, K2, g, coarse=True),
+          "KB8 coarse")
+
+
+def test_triang_batch(ctx, oracle):
+    """CreateNewMapPoints: the new keyframe against 20 neighbours in one launch."""
+    rng = np.random.default_rng(7500)
+    pairs = [fr.synth_triang_pair(rng, n1=int(rng.integers(200, 1300)), n2=int(rng.integers(200, 1300)),
+                                  forward=bool(i % 2)) for i in range(20)]
+    nm, got = ORBmatcher(ctx).SearchForTriangulationBatch([p[0] for p in pairs], [p[1] for p in pairs],
+                                                          [p[2] for p in pairs])
+    for (K1, K2, g), n, pr_ in zip(pairs, nm, got):
+        check((n, pr_), oc.triangulation(oracle, K1, K2, g), "batch")
