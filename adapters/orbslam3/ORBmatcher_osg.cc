@@ -1,7 +1,7 @@
 // ORBmatcher_osg.cc — drop-in bodies for the ORBmatcher operators on the MI355X path, for an
 // ORB-SLAM3 tree built with -DORB_SLAM3_OSG.  The reference's
-// src/ORBmatcher.cc keeps every other member; the bodies below replace the six hot-path ones and
-// the two Fuse overloads
+// src/ORBmatcher.cc keeps every other member; the bodies below replace the six hot-path ones,
+// the two Fuse overloads and SearchForTriangulation
 // under #ifdef ORB_SLAM3_OSG (signatures: ref:include/ORBmatcher.h:36-66).
 #include "ORBmatcher.h"
 #include "osg_hooks_orbslam3.h"
@@ -51,6 +51,12 @@ int ORBmatcher::Fuse(KeyFrame *pKF, Sophus::Sim3f &Scw, const std::vector<MapPoi
                      std::vector<MapPoint *> &vpReplacePoint)
 {  // ref:src/ORBmatcher.cc:1553-1694
     return osg_orbslam3::fuse_sim3<H>(pKF, Scw, vpPoints, th, vpReplacePoint);
+}
+
+int ORBmatcher::SearchForTriangulation(KeyFrame *pKF1, KeyFrame *pKF2, std::vector<std::pair<size_t, size_t>> &vMatchedPairs,
+                                       const bool bOnlyStereo, const bool bCoarse)
+{  // ref:src/ORBmatcher.cc:1045-1328
+    return osg_orbslam3::search_for_triangulation<H>(pKF1, pKF2, vMatchedPairs, bOnlyStereo, bCoarse, mbCheckOrientation);
 }
 
 }  // namespace ORB_SLAM3

@@ -54,6 +54,45 @@ struct OsgHooks {
             c.trl[4] = t.x(); c.trl[5] = t.y(); c.trl[6] = t.z();
         }
     }
+    // ref:src/ORBmatcher.cc:1052-1083 and Pinhole.cpp:194-197: the epipole and F12 = K1^-T [t12]x R12 K2^-1
+    // for each camera pair (ll, lr, rl, rr), evaluated with the reference's own Sophus / Eigen expressions
+    static void triang_geom(KeyFrame *pKF1, KeyFrame *pKF2, osg_triang_geom &g)
+    {
+        std::memset(&g, 0, sizeof g);
+        const Sophus::SE3f T1w = pKF1->GetPose(), T2w = pKF2->GetPose(), Tw2 = pKF2->GetPoseInverse();
+        const Eigen::Vector3f Cw = pKF1->GetCameraCenter();
+        const Eigen::Vector3f C2 = T2w * Cw;
+        const Eigen::Vector2f ep = pKF2->mpCamera->project(C2);
+        g.ep_x = ep(0);
+        g.ep_y = ep(1);
+        Sophus::SE3f T[4];
+        int nk = 1;
+        T[0] = T1w * Tw2;
+        if (pKF1->mpCamera2 || pKF2->mpCamera2) {
+            const Sophus::SE3f Tr1w = pKF1->GetRightPose(), Twr2 = pKF2->GetRightPoseInverse();
+            T[1] = T1w * Twr2;
+            T[2] = Tr1w * Tw2;
+            T[3] = Tr1w * Twr2;
+            nk = 4;
+        }
+        GeometricCamera *c1[2] = {pKF1->mpCamera, pKF1->mpCamera2}, *c2[2] = {pKF2->mpCamera, pKF2->mpCamera2};
+        g.pinhole = 1;
+        for (int k = 0; k < nk; k++)
+            if (c1[k >> 1]->GetType() != GeometricCamera::CAM_PINHOLE ||
+                c2[k & 1]->GetType() != GeometricCamera::CAM_PINHOLE)
+                g.pinhole = 0;
+        if (!g.pinhole) return;  // KB8: only the bCoarse path runs on the GPU
+        for (int k = 0; k < nk; k++) {
+            const Eigen::Matrix3f R12 = T[k].rotationMatrix();
+            const Eigen::Vector3f t12 = T[k].translation();
+            const Eigen::Matrix3f t12x = Sophus::SO3f::hat(t12);
+            const Eigen::Matrix3f K1 = c1[k >> 1]->toK_();
+            const Eigen::Matrix3f K2 = c2[k & 1]->toK_();
+            const Eigen::Matrix3f F12 = K1.transpose().inverse() * t12x * R12 * K2.inverse();
+            for (int r = 0; r < 3; r++)
+                for (int c = 0; c < 3; c++) g.F12[k][3 * r + c] = F12(r, c);
+        }
+    }
     // ref:src/ORBmatcher.cc:1993-2009; the invz < 0 and image-bounds tests stay in the kernel
     static bool project_last(const Frame &CF, MapPoint *pMP, float &u, float &v, float &invz)
     {

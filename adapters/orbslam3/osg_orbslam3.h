@@ -28,10 +28,12 @@
 #include <cstring>
 #include <list>
 #include <map>
+#include <memory>
 #include <set>
 #include <stdexcept>
 #include <string>
 #include <tuple>
+#include <utility>
 #include <unordered_map>
 #include <utility>
 #include <vector>
@@ -573,6 +575,54 @@ int search_by_bow_kf_kf(KeyFrameT *pKF1, KeyFrameT *pKF2, std::vector<MapPointT 
     vpMatches12.assign(n1, nullptr);
     for (int i = 0; i < n1; i++)
         if (out[i] >= 0) vpMatches12[i] = v2[out[i]];
+    return nm;
+}
+
+// ----------------------------------------------------------------- b3 SearchForTriangulation
+// ref:src/ORBmatcher.cc:1045-1328.  vMatchedPairs = (KF1 index, KF2 index) in ascending KF1 index.
+// The epipole and the F12 matrices come from the hook (the reference's Sophus / Eigen code).
+template <class H, class KeyFrameT>
+int search_for_triangulation(KeyFrameT *pKF1, KeyFrameT *pKF2, std::vector<std::pair<size_t, size_t>> &vMatchedPairs,
+                             bool bOnlyStereo, bool bCoarse, bool checkOri)
+{
+    osg_ctx *ctx = thread_ctx();
+    struct Side {
+        std::vector<uint8_t> desc, has_mp;
+        std::vector<float> x, y, a;
+        std::vector<int32_t> oct;
+    } s[2];
+    KeyFrameT *K[2] = {pKF1, pKF2};
+    osg_kf_side v[2];
+    std::vector<std::unique_ptr<FeatVecCSR<decltype(pKF1->mFeatVec)>>> fv;
+    for (int k = 0; k < 2; k++) {
+        KeyFrameT *p = K[k];
+        const int n = p->N;
+        copy_desc_rows(p->mDescriptors, n, s[k].desc);
+        s[k].has_mp.resize(n);
+        for (int i = 0; i < n; i++) {
+            // ref:src/ORBmatcher.cc:1142-1144 / 1184-1186: mvKeysUn, or mvKeys / mvKeysRight on a rig
+            const auto &kp = (p->NLeft == -1) ? p->mvKeysUn[i] : (i < p->NLeft ? p->mvKeys[i] : p->mvKeysRight[i - p->NLeft]);
+            s[k].x.push_back(kp.pt.x);
+            s[k].y.push_back(kp.pt.y);
+            s[k].a.push_back(kp.angle);
+            s[k].oct.push_back(kp.octave);
+            s[k].has_mp[i] = p->GetMapPoint(i) != nullptr;
+        }
+        fv.emplace_back(new FeatVecCSR<decltype(pKF1->mFeatVec)>(p->mFeatVec));
+        v[k] = osg_kf_side{n, p->NLeft, p->mpCamera2 != nullptr, s[k].desc.data(), s[k].x.data(), s[k].y.data(),
+                           s[k].a.data(), s[k].oct.data(), p->mvuRight.empty() ? nullptr : p->mvuRight.data(),
+                           s[k].has_mp.data(), p->mvLevelSigma2.data(), p->mvScaleFactors.data(),
+                           (int32_t)p->mvScaleFactors.size(), fv[k]->view()};
+    }
+    osg_triang_geom g;
+    H::triang_geom(pKF1, pKF2, g);
+    std::vector<int32_t> m12(pKF1->N, -1);
+    const int nm = check(ctx, osg_search_for_triangulation(ctx, &v[0], &v[1], &g, bOnlyStereo, bCoarse, checkOri,
+                                                           m12.data()), "osg_search_for_triangulation");
+    vMatchedPairs.clear();
+    vMatchedPairs.reserve(nm);
+    for (int i = 0; i < pKF1->N; i++)
+        if (m12[i] >= 0) vMatchedPairs.push_back(std::make_pair((size_t)i, (size_t)m12[i]));
     return nm;
 }
 

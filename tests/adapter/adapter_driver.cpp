@@ -1,7 +1,7 @@
 // adapter_driver.cpp — runs adapters/orbslam3/osg_orbslam3.h on mock ORB-SLAM3 objects built from
 // arrays written by tests/test_adapter.py, and writes the adapter's results back (test-only).
 //
-//   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba fuse fuse_sim3
+//   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba fuse fuse_sim3 triang
 //
 // Array file: repeated {u32 name_len, name, u8 dtype ('b' u8, 'i' i32, 'f' f32, 'd' f64), u64 count,
 // data}.
@@ -237,6 +237,51 @@ static void build_kf_frame(const Arrays &m, KeyFrame &K)
     K.mb = F.mb;
     K.mbf = F.mbf;
     K.mvpMapPoints.assign(K.N, nullptr);
+}
+
+// a SearchForTriangulation keyframe "A." / "B." (KFSide arrays); MapPoints where has_mp
+static void build_triang_kf(const Arrays &m, const std::string &pre, KeyFrame &K, std::vector<std::unique_ptr<MapPoint>> &pool)
+{
+    const Arr &d = get(m, pre + "desc");
+    const int n = (int)(d.n / 32);
+    K.N = n;
+    K.NLeft = get(m, pre + "nleft").p<int32_t>()[0];
+    static Camera second;
+    K.mpCamera2 = get(m, pre + "two_cam").p<int32_t>()[0] ? &second : nullptr;
+    K.mDescriptors = cv::Mat(n, 32);
+    std::memcpy(K.mDescriptors.buf.data(), d.b.data(), d.b.size());
+    std::vector<cv::KeyPoint> kps(n);
+    for (int i = 0; i < n; i++) {
+        kps[i].pt.x = get(m, pre + "kp_x").p<float>()[i];
+        kps[i].pt.y = get(m, pre + "kp_y").p<float>()[i];
+        kps[i].angle = get(m, pre + "kp_angle").p<float>()[i];
+        kps[i].octave = get(m, pre + "kp_octave").p<int32_t>()[i];
+    }
+    const int nl = K.NLeft == -1 ? n : K.NLeft;
+    if (K.NLeft == -1) {
+        K.mvKeysUn = kps;
+        K.mvKeys = kps;
+    } else {  // mvKeysUn is not read on a rig: give it garbage positions to prove it
+        K.mvKeys.assign(kps.begin(), kps.begin() + nl);
+        K.mvKeysRight.assign(kps.begin() + nl, kps.end());
+        K.mvKeysUn = K.mvKeys;
+        for (auto &kp : K.mvKeysUn) kp.pt.x = -1e9f;
+    }
+    if (has(m, pre + "u_right")) {
+        const Arr &u = get(m, pre + "u_right");
+        K.mvuRight.assign(u.p<float>(), u.p<float>() + u.n);
+    }
+    const Arr &sc = get(m, pre + "scale"), &s2 = get(m, pre + "level_sigma2");
+    K.mvScaleFactors.assign(sc.p<float>(), sc.p<float>() + sc.n);
+    K.mvLevelSigma2.assign(s2.p<float>(), s2.p<float>() + s2.n);
+    K.mvpMapPoints.assign(n, nullptr);
+    for (int i = 0; i < n; i++)
+        if (get(m, pre + "has_mp").p<uint8_t>()[i]) {
+            pool.emplace_back(new MapPoint());
+            pool.back()->mnId = (unsigned long)i;
+            K.mvpMapPoints[i] = pool.back().get();
+        }
+    fill_featvec(m, pre, K.mFeatVec);
 }
 
 int main(int argc, char **argv)
@@ -520,6 +565,26 @@ int main(int argc, char **argv)
             out["bad"] = make('b', bad);
             out["nobs"] = make('i', nobs);
             out["replace"] = make('i', repl);
+        } else if (mode == "triang") {
+            // keyframes "A." / "B.", geometry "G.geom" {ep_x, ep_y, F12[36], pinhole}; params: only_stereo coarse ori
+            KeyFrame A, B;
+            build_triang_kf(in, "A.", A, pool);
+            build_triang_kf(in, "B.", B, pool);
+            const float *g = get(in, "G.geom").p<float>();
+            A.triang_geom.ep_x = g[0];
+            A.triang_geom.ep_y = g[1];
+            std::memcpy(A.triang_geom.F12, g + 2, sizeof(float) * 36);
+            A.triang_geom.pinhole = g[38] != 0;
+            std::vector<std::pair<size_t, size_t>> pairs;
+            const int nm = osg_orbslam3::search_for_triangulation<MockHooks>(&A, &B, pairs, prm[0] != 0, prm[1] != 0,
+                                                                              prm[2] != 0);
+            std::vector<int32_t> flat;
+            for (auto &pr : pairs) {
+                flat.push_back((int32_t)pr.first);
+                flat.push_back((int32_t)pr.second);
+            }
+            out["nmatches"] = make('i', std::vector<int32_t>{nm});
+            out["pairs"] = make('i', flat);
         } else {
             fprintf(stderr, "unknown mode %s\n", mode.c_str());
             return 2;

@@ -120,7 +120,8 @@ struct KeyFrame {
     int mnMinX = 0, mnMaxX = 0, mnMinY = 0, mnMaxY = 0;
     float mfGridElementWidthInv = 0, mfGridElementHeightInv = 0;
     int mnScaleLevels = 8;
-    std::vector<float> mvScaleFactors;
+    std::vector<float> mvScaleFactors, mvLevelSigma2;
+    osg_triang_geom triang_geom{};  // test-only: MockHooks::triang_geom
 
     std::vector<MapPoint *> GetMapPointMatches() const { return mvpMapPoints; }
     bool isBad() const { return bad; }
@@ -214,6 +215,7 @@ struct MockHooks {
         level = p->proj_level;
         return p->proj_ok;
     }
+    static void triang_geom(KeyFrame *pKF1, KeyFrame *, osg_triang_geom &g) { g = pKF1->triang_geom; }
     static bool fuse_sim3_query(KeyFrame *, const Sim3 &, MapPoint *p, float &u, float &v, int &level)
     {
         u = p->proj_u;

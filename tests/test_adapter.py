@@ -443,3 +443,32 @@ def test_fuse_split_equals_literal_loop(oracle, seed, sim3):
     np.testing.assert_array_equal(bad, ref[2])
     np.testing.assert_array_equal(nobs, ref[3])
     np.testing.assert_array_equal(replace, ref[4])
+
+
+def triang_arrays(pre, K):
+    d = {pre + "desc": K.desc.reshape(-1), pre + "kp_x": K.kp_x, pre + "kp_y": K.kp_y, pre + "kp_angle": K.kp_angle,
+         pre + "kp_octave": K.kp_octave, pre + "has_mp": K.has_mp, pre + "scale": K.scale,
+         pre + "level_sigma2": K.level_sigma2, pre + "node_id": K.node_id, pre + "node_start": K.node_start,
+         pre + "feat": K.feat, pre + "nleft": np.array([K.nleft], np.int32),
+         pre + "two_cam": np.array([K.two_cam], np.int32)}
+    if K.u_right is not None:
+        d[pre + "u_right"] = K.u_right
+    return d
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("two_cam,coarse,only_stereo", [(False, False, False), (False, True, False),
+                                                        (False, False, True), (True, False, False)])
+def test_adapter_search_for_triangulation(driver, tmp_path, oracle, two_cam, coarse, only_stereo):
+    """SearchForTriangulation through the adapter (KeyFrame fields gathered by member name, geometry from
+    the hook, vMatchedPairs rebuilt) gives the oracle's pairs."""
+    rng = np.random.default_rng(780 + 2 * two_cam + coarse)
+    K1, K2, g = fr.synth_triang_pair(rng, n1=900, n2=900, forward=not two_cam, two_cam=two_cam)
+    geom = np.concatenate([[g.ep[0], g.ep[1]], np.resize(g.F12.reshape(-1), 36) if two_cam else
+                           np.concatenate([g.F12.reshape(-1), np.zeros(27)]), [1.0]]).astype(np.float32)
+    out = run(driver, tmp_path, "triang", {**triang_arrays("A.", K1), **triang_arrays("B.", K2), "G.geom": geom,
+                                           "params": np.array([only_stereo, coarse, 1.0], np.float32)})
+    n, pairs = oc.triangulation(oracle, K1, K2, g, only_stereo, coarse)
+    assert n > 10
+    assert int(out["nmatches"][0]) == n
+    np.testing.assert_array_equal(out["pairs"].reshape(-1, 2), pairs)
