@@ -331,6 +331,19 @@ int osg_search_for_triangulation_batch(osg_ctx *ctx, const osg_kf_side *kf1, con
                                        const osg_triang_geom *geom, int32_t B, int only_stereo, int coarse,
                                        int check_orientation, int32_t *match12, int32_t *nmatches);
 
+/* ---- b4: MapPoint::ComputeDistinctiveDescriptors ------------------------------------------------
+ * ref:src/MapPoint.cc:444-535, for a list of MapPoints at once (LocalMapping runs it for every MapPoint
+ * of a keyframe, ref:src/LocalMapping.cc:421-436, 1066-1082).  MapPoint p's observation descriptors
+ * are rows desc[start[p] .. start[p+1]) in the order the reference gathers them (mObservations
+ * std::map order; per keyframe the left row, then the right row).  best_idx[p] = the row whose
+ * sorted distance row (self-distance 0 included) has the smallest element [(N - 1) / 2], first row
+ * on ties; -1 when N = 0 (the reference returns without touching mDescriptor).  N <= 65535. */
+int osg_compute_distinctive_descriptors(osg_ctx *ctx, const uint8_t *desc, const int32_t *start, int32_t n_points,
+                                        int32_t *best_idx);
+/* Device form: d_desc (rows), d_start (n_points + 1), d_best_idx (n_points) in HBM; asynchronous. */
+int osg_compute_distinctive_descriptors_dev(osg_ctx *ctx, const void *d_desc, const void *d_start, int32_t n_points,
+                                            void *d_best_idx);
+
 /* Diagnostics of the last search call on this context (summed / maxed over a batch): out[0]
  * candidates enumerated, out[1] Jacobi rounds, out[2] problems whose greedy was redone serially (a5 on a two-camera rig when a
  * stereo-partner write by a MapPoint without observations unblocked a slot), out[3] nmatches.

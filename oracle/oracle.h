@@ -38,6 +38,8 @@ void oracle_dbow_transform(const osg_vocabulary_desc *V, const uint8_t *desc, in
 /* Fuse search half (oracle_fuse.c) */
 int oracle_fuse_search(const osg_frame *KF, const osg_fuse_queries *Q, float th, int right, int gated,
                        int32_t *best_idx, int32_t *best_dist);
+/* MapPoint::ComputeDistinctiveDescriptors over a list (oracle_desc.c) */
+void oracle_compute_distinctive_descriptors(const uint8_t *desc, const int32_t *start, int n_points, int32_t *best_idx);
 /* SearchForTriangulation (oracle_triang.c) */
 int oracle_search_for_triangulation(const osg_kf_side *K1, const osg_kf_side *K2, const osg_triang_geom *G,
                                     int bOnlyStereo, int bCoarse, int checkOri, int32_t *vMatches12);

@@ -59,6 +59,8 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.oracle_fuse_search.argtypes = [C.POINTER(OsgFrame), C.POINTER(OsgFuseQueries), f32, C.c_int, C.c_int, vp, vp]
     lib.oracle_search_for_triangulation.argtypes = [C.POINTER(OsgKfSide), C.POINTER(OsgKfSide),
                                                     C.POINTER(OsgTriangGeom), C.c_int, C.c_int, C.c_int, vp]
+    lib.oracle_compute_distinctive_descriptors.argtypes = [vp, vp, C.c_int, vp]
+    lib.oracle_compute_distinctive_descriptors.restype = None
     return lib
 
 
@@ -156,3 +158,13 @@ def triangulation(oracle, K1, K2, geom, only_stereo=False, coarse=False, ori=Tru
                                                int(bool(coarse)), int(bool(ori)), m12.ctypes.data)
     i = np.nonzero(m12 >= 0)[0]
     return n, np.stack([i, m12[i]], axis=1).astype(np.int64)
+
+
+def distinctive(oracle, desc, start):
+    """ComputeDistinctiveDescriptors over a CSR list of observation descriptors: best row per point."""
+    desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    start = np.ascontiguousarray(start, np.int32)
+    out = np.full(len(start) - 1, -1, np.int32)
+    oracle.oracle_compute_distinctive_descriptors(desc.ctypes.data, start.ctypes.data, len(start) - 1,
+                                                  out.ctypes.data)
+    return out

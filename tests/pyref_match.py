@@ -443,3 +443,19 @@ def search_for_triangulation(K1, K2, geom, only_stereo=False, coarse=False, ori=
         nm = apply_hist(hist, m12, nm)
     pairs = [(i, j) for i, j in enumerate(m12) if j >= 0]
     return nm, np.array(pairs, np.int64).reshape(-1, 2)
+
+
+def distinctive(desc_lists):
+    """MapPoint::ComputeDistinctiveDescriptors (ref:src/MapPoint.cc:444-535) with numpy: the distance
+    matrix by bitwise_count, per-row sorted median at int(0.5 * (N - 1)), first minimum."""
+    out = []
+    for d in desc_lists:
+        d = np.asarray(d, np.uint8).reshape(-1, 32)
+        n = len(d)
+        if n == 0:
+            out.append(-1)
+            continue
+        M = np.bitwise_count(d[:, None, :] ^ d[None, :, :]).sum(axis=2)
+        med = np.sort(M, axis=1)[:, int(0.5 * (n - 1))]
+        out.append(int(np.argmin(med)))
+    return np.array(out, np.int32)
