@@ -93,6 +93,13 @@ struct OsgHooks {
                 for (int c = 0; c < 3; c++) g.F12[k][3 * r + c] = F12(r, c);
         }
     }
+    // ref:src/MapPoint.cc:530-534: mDescriptor = vDescriptors[BestIdx].clone() under mMutexFeatures
+    // (OsgHooks is a friend of MapPoint under ORB_SLAM3_OSG)
+    static void set_descriptor(MapPoint *pMP, const uint8_t *row)
+    {
+        std::unique_lock<std::mutex> lock(pMP->mMutexFeatures);
+        pMP->mDescriptor = cv::Mat(1, 32, CV_8UC1, const_cast<uint8_t *>(row)).clone();
+    }
     // ref:src/ORBmatcher.cc:1993-2009; the invz < 0 and image-bounds tests stay in the kernel
     static bool project_last(const Frame &CF, MapPoint *pMP, float &u, float &v, float &invz)
     {

@@ -626,6 +626,44 @@ int search_for_triangulation(KeyFrameT *pKF1, KeyFrameT *pKF2, std::vector<std::
     return nm;
 }
 
+// ------------------------------------------------------ b4 MapPoint::ComputeDistinctiveDescriptors
+// ref:src/MapPoint.cc:444-535 for a list of MapPoints in one launch (the loops of
+// ref:src/LocalMapping.cc:421-436, 1066-1082).  Gathers each point's observation rows in the
+// reference's order (mObservations map order; left row, then right row; bad keyframes skipped) and
+// writes the chosen row back through H::set_descriptor (mDescriptor is protected: the hook is a
+// friend of MapPoint).  Null / bad points and points without rows are left alone.
+template <class H, class MapPointT>
+void compute_distinctive_descriptors(const std::vector<MapPointT *> &vpMPs)
+{
+    osg_ctx *ctx = thread_ctx();
+    const int np = (int)vpMPs.size();
+    std::vector<uint8_t> rows;
+    std::vector<int32_t> start(np + 1, 0);
+    for (int p = 0; p < np; p++) {
+        MapPointT *pMP = vpMPs[p];
+        if (pMP && !pMP->isBad()) {
+            const auto observations = pMP->GetObservations();
+            for (const auto &kv : observations) {
+                const auto *pKF = kv.first;
+                if (pKF->isBad()) continue;
+                const int l = std::get<0>(kv.second), r = std::get<1>(kv.second);
+                for (int idx : {l, r}) {
+                    if (idx == -1) continue;
+                    const size_t o = rows.size();
+                    rows.resize(o + 32);
+                    std::memcpy(&rows[o], pKF->mDescriptors.template ptr<uint8_t>(idx), 32);
+                }
+            }
+        }
+        start[p + 1] = (int32_t)(rows.size() / 32);
+    }
+    std::vector<int32_t> best(np, -1);
+    check(ctx, osg_compute_distinctive_descriptors(ctx, rows.data(), start.data(), np, best.data()),
+          "osg_compute_distinctive_descriptors");
+    for (int p = 0; p < np; p++)
+        if (best[p] >= 0) H::set_descriptor(vpMPs[p], &rows[32 * ((size_t)start[p] + best[p])]);
+}
+
 // ------------------------------------------------------------------- a10 PoseOptimization
 // ref:src/Optimizer.cc:71-420: one edge per Frame slot holding a MapPoint, in slot order; the
 // result sets mvbOutlier and the pose and returns nInitialCorrespondences - nBad.

@@ -1,7 +1,7 @@
 // adapter_driver.cpp — runs adapters/orbslam3/osg_orbslam3.h on mock ORB-SLAM3 objects built from
 // arrays written by tests/test_adapter.py, and writes the adapter's results back (test-only).
 //
-//   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba fuse fuse_sim3 triang
+//   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba fuse fuse_sim3 triang distinct
 //
 // Array file: repeated {u32 name_len, name, u8 dtype ('b' u8, 'i' i32, 'f' f32, 'd' f64), u64 count,
 // data}.
@@ -585,6 +585,35 @@ int main(int argc, char **argv)
             }
             out["nmatches"] = make('i', std::vector<int32_t>{nm});
             out["pairs"] = make('i', flat);
+        } else if (mode == "distinct") {
+            // keyframes: "K.desc" (nk x nkp rows), "K.bad"; MapPoints: "M.bad", "M.desc" (initial);
+            // observations CSR "O.start" / "O.kf" / "O.left" / "O.right"
+            const int nk = (int)get(in, "K.bad").n, nm = (int)get(in, "M.bad").n;
+            const int nkp = (int)(get(in, "K.desc").n / 32 / (nk ? nk : 1));
+            std::vector<KeyFrame> K(nk);
+            for (int k = 0; k < nk; k++) {
+                K[k].N = nkp;
+                K[k].bad = get(in, "K.bad").p<uint8_t>()[k];
+                K[k].mDescriptors = cv::Mat(nkp, 32);
+                std::memcpy(K[k].mDescriptors.buf.data(), get(in, "K.desc").p<uint8_t>() + (size_t)k * nkp * 32,
+                            (size_t)nkp * 32);
+            }
+            std::vector<MapPoint> M(nm);
+            std::vector<MapPoint *> list;
+            const int32_t *os = get(in, "O.start").p<int32_t>();
+            for (int i = 0; i < nm; i++) {
+                M[i].mnId = (unsigned long)i;
+                M[i].bad = get(in, "M.bad").p<uint8_t>()[i];
+                std::memcpy(M[i].desc.buf.data(), get(in, "M.desc").p<uint8_t>() + 32 * (size_t)i, 32);
+                for (int o = os[i]; o < os[i + 1]; o++)
+                    M[i].obs[&K[get(in, "O.kf").p<int32_t>()[o]]] =
+                        std::make_tuple(get(in, "O.left").p<int32_t>()[o], get(in, "O.right").p<int32_t>()[o]);
+                list.push_back(i % 17 == 5 ? nullptr : &M[i]);  // a NULL entry now and then
+            }
+            osg_orbslam3::compute_distinctive_descriptors<MockHooks>(list);
+            std::vector<uint8_t> d(32 * (size_t)nm);
+            for (int i = 0; i < nm; i++) std::memcpy(&d[32 * (size_t)i], M[i].desc.buf.data(), 32);
+            out["desc"] = make('b', d);
         } else {
             fprintf(stderr, "unknown mode %s\n", mode.c_str());
             return 2;
