@@ -281,6 +281,26 @@ int osg_fuse_search(osg_ctx *ctx, const osg_frame *KF, const osg_fuse_queries *Q
 int osg_fuse_search_batch(osg_ctx *ctx, const osg_frame *KF, const osg_fuse_queries *Q, int32_t B, float th,
                           int right, int gated, int32_t *best_idx, int32_t *best_dist, int32_t *nfused);
 
+/* ---- b5: the Sim3 projections of LoopClosing -------------------------------------------------------
+ *   SearchByProjection(KeyFrame*, Sophus::Sim3f& Scw, const vector<MapPoint*>&, vector<MapPoint*>& vpMatched,
+ *                      th, ratioHamming)                                  ref:src/ORBmatcher.cc:498-609
+ *   SearchByProjection(KeyFrame*, Sim3f&, vpPoints, vpPointsKFs, vpMatched, vpMatchedKF, th, ratioHamming)
+ *                                                                         ref:src/ORBmatcher.cc:611-733
+ * (ref:src/LoopClosing.cc:1062, 1091, 1368).  Queries are osg_fuse_queries (ur and inv_level_sigma2
+ * unused): valid = !isBad() && not already in vpMatched && depth >= 0 && in image && dist3D inside
+ * [min, max] invariance && PO.dot(Pn) >= 0.5 dist; u, v = the Sim3 projection; pred_level =
+ * PredictScale (the caller's part, :525-569).  The device walks KeyFrame::GetFeaturesInArea(u, v,
+ * th * mvScaleFactors[pred_level]) skipping taken slots and keypoints outside [pred_level - 1,
+ * pred_level], keeps the first minimum distance and accepts it iff bestDist <= TH_LOW * ratioHamming
+ * (float); the accepted slot is taken for every later MapPoint (sequential greedy, solved exactly).
+ * slot_query[KF.n] in: -2 = vpMatched[i] != NULL, -1 = free; out: the query index that took the
+ * slot (the caller writes vpMatched[i] = vpPoints[q], and vpMatchedKF[i] = vpPointsKFs[q]).
+ * Returns nmatches.  KF.n <= 8192. */
+int osg_search_by_projection_sim3(osg_ctx *ctx, const osg_frame *KF, const osg_fuse_queries *Q, float th,
+                                  float ratio_hamming, int32_t *slot_query);
+int osg_search_by_projection_sim3_batch(osg_ctx *ctx, const osg_frame *KF, const osg_fuse_queries *Q, int32_t B,
+                                        float th, float ratio_hamming, int32_t *slot_query, int32_t *nmatches);
+
 /* ---- b3: SearchForTriangulation ---------------------------------------------------------------
  * ORBmatcher::SearchForTriangulation(KeyFrame *pKF1, KeyFrame *pKF2, vector<pair<size_t,size_t>>&,
  * bOnlyStereo, bCoarse)  ref:src/ORBmatcher.cc:1045-1328 (LocalMapping::CreateNewMapPoints,

@@ -11,6 +11,7 @@ runs on the GPU (there is no CPU fallback).
     n, best_idx, best_dist = m.Fuse(KF, fq, th=3.0, bRight=False)               # Fuse(KeyFrame*, vector<MapPoint*>)
     n, best_idx, best_dist = m.Fuse(KF, fq, th, sim3=True)                      # Fuse(KeyFrame*, Sim3f, ...)
     n, vMatchedPairs = m.SearchForTriangulation(KF1, KF2, geom, bOnlyStereo, bCoarse)
+    n = m.SearchByProjectionSim3(KF, fq, mp_id, vpMatched, th, ratioHamming[, vpPointsKFs, vpMatchedKF])
 """
 from __future__ import annotations
 
@@ -113,6 +114,25 @@ class ORBmatcher:
         cuts = np.cumsum([0] + [q.n for q in fqs])
         return nf, [bi[a:b].copy() for a, b in zip(cuts[:-1], cuts[1:])], [bd[a:b].copy() for a, b in
                                                                            zip(cuts[:-1], cuts[1:])]
+
+    def SearchByProjectionSim3(self, KF: FrameSoA, fq: FuseQueries, mp_id, vpMatched, th: int, ratioHamming: float,
+                               vpPointsKFs=None, vpMatchedKF=None) -> int:
+        """``SearchByProjection(KeyFrame*, Sim3f&, vpPoints, [vpPointsKFs,] vpMatched, [vpMatchedKF,] th,
+        ratioHamming)`` (ref:src/ORBmatcher.cc:498-733).  ``fq`` holds the projected MapPoints (``valid`` =
+        the caller's pre-search filters), ``mp_id[q]`` their ids; ``vpMatched`` (KF.n MapPoint ids, -1 =
+        NULL) and ``vpMatchedKF`` are updated in place like the reference's output vectors."""
+        lib, h = self.ctx.lib, self.ctx.handle
+        vpMatched = np.asarray(vpMatched)
+        sq = np.where(vpMatched >= 0, -2, -1).astype(np.int32)
+        fs, qs = KF.struct(), fq.struct()
+        rc = lib.osg_search_by_projection_sim3(h, C.byref(fs), C.byref(qs), float(th), float(ratioHamming),
+                                               sq.ctypes.data)
+        n = self.ctx.check(rc, "SearchByProjection(KeyFrame, Sim3)")
+        new = np.nonzero(sq >= 0)[0]
+        vpMatched[new] = np.asarray(mp_id)[sq[new]]
+        if vpMatchedKF is not None:
+            vpMatchedKF[new] = np.asarray(vpPointsKFs)[sq[new]]
+        return n
 
     @staticmethod
     def _pairs(m12):

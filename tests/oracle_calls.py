@@ -59,6 +59,7 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.oracle_fuse_search.argtypes = [C.POINTER(OsgFrame), C.POINTER(OsgFuseQueries), f32, C.c_int, C.c_int, vp, vp]
     lib.oracle_search_for_triangulation.argtypes = [C.POINTER(OsgKfSide), C.POINTER(OsgKfSide),
                                                     C.POINTER(OsgTriangGeom), C.c_int, C.c_int, C.c_int, vp]
+    lib.oracle_search_by_projection_sim3.argtypes = [C.POINTER(OsgFrame), C.POINTER(OsgFuseQueries), f32, f32, vp]
     lib.oracle_compute_distinctive_descriptors.argtypes = [vp, vp, C.c_int, vp]
     lib.oracle_compute_distinctive_descriptors.restype = None
     return lib
@@ -168,3 +169,11 @@ def distinctive(oracle, desc, start):
     oracle.oracle_compute_distinctive_descriptors(desc.ctypes.data, start.ctypes.data, len(start) - 1,
                                                   out.ctypes.data)
     return out
+
+
+def sim3(oracle, KF, Q, th, ratio, slot_query):
+    """The Sim3 projection matcher through the oracle; slot_query: -2 taken, -1 free (copied)."""
+    s = np.ascontiguousarray(slot_query, np.int32).copy()
+    fs, qs = KF.struct(), Q.struct()
+    n = oracle.oracle_search_by_projection_sim3(C.byref(fs), C.byref(qs), float(th), float(ratio), s.ctypes.data)
+    return n, s

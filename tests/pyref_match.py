@@ -459,3 +459,29 @@ def distinctive(desc_lists):
         med = np.sort(M, axis=1)[:, int(0.5 * (n - 1))]
         out.append(int(np.argmin(med)))
     return np.array(out, np.int32)
+
+
+def search_sim3(F, Q, th, ratio, slot_query):
+    """SearchByProjection(KeyFrame*, Sim3f&, ...) (ref:src/ORBmatcher.cc:498-609) from the area walk on:
+    vpMatched written as soon as a MapPoint is accepted.  slot_query: -2 taken, -1 free."""
+    s = np.array(slot_query, np.int32).copy()
+    n = 0
+    for q in range(Q.n):
+        if not Q.valid[q]:
+            continue
+        lvl = int(Q.pred_level[q])
+        r = f32(f32(th) * F.scale[lvl])
+        bd, bi = 256, -1
+        for idx in features_in_area(F, Q.u[q], Q.v[q], r):
+            if s[idx] != -1:
+                continue
+            o = int(F.kp_octave[idx])
+            if o < lvl - 1 or o > lvl:
+                continue
+            d = dist(Q.desc[q], F.desc[idx])
+            if d < bd:
+                bd, bi = d, idx
+        if float(bd) <= float(f32(f32(TH_LOW) * f32(ratio))):
+            s[bi] = q
+            n += 1
+    return n, s

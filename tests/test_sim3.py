@@ -1,0 +1,96 @@
+"""The Sim3 projection matchers of LoopClosing (ref:src/ORBmatcher.cc:498-733): the oracle pinned by the
+pure-Python restatement and a hand case (CPU); the GPU fixed-point greedy bit-exact against the oracle."""
+import numpy as np
+import pytest
+
+from orb_slam3_comments_ghr_amd import frames as fr
+from orb_slam3_comments_ghr_amd.matcher import ORBmatcher
+from tests import oracle_calls as oc
+from tests import pyref_match as pr
+
+# LoopClosing's calls: (th, ratioHamming) at ref:src/LoopClosing.cc:1062, 1091, 1368
+CALLS = [(8, 1.5), (5, 1.0), (3, 1.5)]
+
+
+def world(seed, n=1000, m=3000, taken=0.1):
+    rng = np.random.default_rng(seed)
+    F = fr.synth_frame(rng, n=n, stereo=False)
+    Q = fr.synth_fuse_queries(rng, F, m=m, match_frac=0.7)
+    sq = np.where(rng.random(F.n) < taken, -2, -1).astype(np.int32)
+    return F, Q, sq
+
+
+@pytest.mark.parametrize("seed", range(3))
+@pytest.mark.parametrize("th,ratio", CALLS)
+def test_oracle_vs_python(oracle, seed, th, ratio):
+    F, Q, sq = world(9000 + seed, n=250, m=500)
+    ref = oc.sim3(oracle, F, Q, th, ratio, sq)
+    got = pr.search_sim3(F, Q, th, ratio, sq)
+    assert ref[0] == got[0] and ref[0] > 20
+    np.testing.assert_array_equal(ref[1], got[1])
+
+
+def bits(k):
+    b = np.zeros(256, np.uint8)
+    b[:k] = 1
+    return np.packbits(b)
+
+
+def hand_case():
+    """Keypoints 0 (100, 100) and 1 (102, 100) share a window; keypoint 2 (300, 100) is taken before the
+    call.  MapPoint 0 (d 3 to keypoint 0, 38 to 1) takes keypoint 0; MapPoint 1 (d 1 and 40) finds 0 taken
+    and falls back to 1 (40 <= 50 * 1.0); MapPoints 2 and 3 see only the taken keypoint 2."""
+    F = fr.FrameSoA(desc=np.stack([bits(0), bits(41), bits(0)]), kp_x=np.array([100.0, 102.0, 300.0], np.float32),
+                    kp_y=np.array([100.0, 100.0, 100.0], np.float32), kp_angle=np.zeros(3, np.float32),
+                    kp_octave=np.zeros(3, np.int32))
+    Q = fr.FuseQueries(desc=np.stack([bits(3), bits(1), bits(0), bits(60)]), valid=np.ones(4, np.uint8),
+                       u=np.array([101, 101, 300, 300], np.float32), v=np.array([100, 100, 100, 100], np.float32),
+                       ur=None, pred_level=np.zeros(4, np.int32), inv_level_sigma2=fr.inv_level_sigma2(F.scale))
+    return F, Q, np.array([-1, -1, -2], np.int32)
+
+
+def test_oracle_hand_case(oracle):
+    F, Q, sq = hand_case()
+    n, s_ = oc.sim3(oracle, F, Q, 3, 1.0, sq)
+    assert n == 2 and s_.tolist() == [0, 1, -2]
+    assert pr.search_sim3(F, Q, 3, 1.0, sq)[1].tolist() == [0, 1, -2]
+    # ratioHamming 0.7: 40 > 35, MapPoint 1 gets nothing
+    assert oc.sim3(oracle, F, Q, 3, 0.7, sq)[1].tolist() == [0, -1, -2]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(3))
+@pytest.mark.parametrize("th,ratio", CALLS)
+def test_gpu_vs_oracle(ctx, oracle, seed, th, ratio):
+    """LoopClosing shape: a 1200-keypoint keyframe, 3000-6000 projected MapPoints with slot collisions."""
+    F, Q, sq = world(9100 + seed, n=1200, m=3000 * (1 + seed))
+    n_ref, s_ref = oc.sim3(oracle, F, Q, th, ratio, sq)
+    mp_id = 100000 + np.arange(Q.n, dtype=np.int32)
+    vpMatched = np.where(sq == -2, 7, -1).astype(np.int32)
+    kfs = np.arange(Q.n, dtype=np.int32) % 17
+    vpMatchedKF = np.full(F.n, -1, np.int32)
+    n = ORBmatcher(ctx).SearchByProjectionSim3(F, Q, mp_id, vpMatched, th, ratio, kfs, vpMatchedKF)
+    assert n == n_ref and n > 300
+    new = s_ref >= 0
+    np.testing.assert_array_equal(vpMatched[new], mp_id[s_ref[new]])
+    np.testing.assert_array_equal(vpMatched[s_ref == -2], 7)
+    np.testing.assert_array_equal(vpMatched[s_ref == -1], -1)
+    np.testing.assert_array_equal(vpMatchedKF[new], kfs[s_ref[new]])
+    assert ctx.match_last_stats()["rounds"] >= 2  # collisions exercised the resolve
+
+
+@pytest.mark.gpu
+def test_gpu_hand_case_and_edges(ctx, oracle):
+    F, Q, sq = hand_case()
+    vp = np.where(sq == -2, 9, -1).astype(np.int32)
+    assert ORBmatcher(ctx).SearchByProjectionSim3(F, Q, np.arange(4), vp, 3, 1.0) == 2
+    assert vp.tolist() == [0, 1, 9]
+    m = ORBmatcher(ctx)
+    F, Q, sq = world(9200, n=600, m=0)
+    assert m.SearchByProjectionSim3(F, Q, [], np.full(F.n, -1, np.int32), 3, 1.5) == 0
+    F, Q, sq = world(9201, n=600, m=500)
+    Q.valid[:] = 0
+    assert m.SearchByProjectionSim3(F, Q, np.arange(500), np.full(F.n, -1, np.int32), 3, 1.5) == 0
+    F, Q, sq = world(9202, n=600, m=500)
+    vp = np.full(F.n, 5, np.int32)  # every slot taken before the call
+    assert m.SearchByProjectionSim3(F, Q, np.arange(500), vp, 8, 1.5) == 0
