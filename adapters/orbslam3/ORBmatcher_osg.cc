@@ -1,7 +1,8 @@
 // ORBmatcher_osg.cc — drop-in bodies for the ORBmatcher operators on the MI355X path, for an
 // ORB-SLAM3 tree built with -DORB_SLAM3_OSG.  The reference's
 // src/ORBmatcher.cc keeps every other member; the bodies below replace the six hot-path ones,
-// the two Fuse overloads and SearchForTriangulation
+// the two Fuse overloads, SearchForTriangulation and the two Sim3
+// SearchByProjection overloads
 // under #ifdef ORB_SLAM3_OSG (signatures: ref:include/ORBmatcher.h:36-66).
 #include "ORBmatcher.h"
 #include "osg_hooks_orbslam3.h"
@@ -57,6 +58,21 @@ int ORBmatcher::SearchForTriangulation(KeyFrame *pKF1, KeyFrame *pKF2, std::vect
                                        const bool bOnlyStereo, const bool bCoarse)
 {  // ref:src/ORBmatcher.cc:1045-1328
     return osg_orbslam3::search_for_triangulation<H>(pKF1, pKF2, vMatchedPairs, bOnlyStereo, bCoarse, mbCheckOrientation);
+}
+
+int ORBmatcher::SearchByProjection(KeyFrame *pKF, Sophus::Sim3f &Scw, const std::vector<MapPoint *> &vpPoints,
+                                   std::vector<MapPoint *> &vpMatched, int th, float ratioHamming)
+{  // ref:src/ORBmatcher.cc:498-621
+    return osg_orbslam3::search_by_projection_sim3<H, KeyFrame>(pKF, Scw, vpPoints, nullptr, vpMatched, nullptr, th,
+                                                               ratioHamming);
+}
+
+int ORBmatcher::SearchByProjection(KeyFrame *pKF, Sophus::Sim3<float> &Scw, const std::vector<MapPoint *> &vpPoints,
+                                   const std::vector<KeyFrame *> &vpPointsKFs, std::vector<MapPoint *> &vpMatched,
+                                   std::vector<KeyFrame *> &vpMatchedKF, int th, float ratioHamming)
+{  // ref:src/ORBmatcher.cc:623-733
+    return osg_orbslam3::search_by_projection_sim3<H, KeyFrame>(pKF, Scw, vpPoints, &vpPointsKFs, vpMatched,
+                                                               &vpMatchedKF, th, ratioHamming);
 }
 
 }  // namespace ORB_SLAM3

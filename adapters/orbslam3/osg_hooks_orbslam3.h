@@ -178,16 +178,30 @@ struct OsgHooks {
         return true;
     }
     // ref:src/ORBmatcher.cc:1560-1562, 1587-1622 (Fuse with Sim3): the same tests with Tcw from Scw
-    static bool fuse_sim3_query(KeyFrame *pKF, const Sophus::Sim3f &Scw, MapPoint *pMP, float &u, float &v,
-                                int &level)
+    // ref:src/ORBmatcher.cc:1589-1622 (Fuse, Sim3) and :530-572 / :649-688 (SearchByProjection, Sim3):
+    // depth, image, distance and viewing-angle tests, the projection and PredictScale.  The second
+    // SearchByProjection overload projects with its own pinhole formula (invz = 1 / z; u = fx * x * invz
+    // + cx, :661-667) instead of mpCamera->project — different float rounding, so it is kept apart.
+    static bool sim3_query(KeyFrame *pKF, const Sophus::Sim3f &Scw, MapPoint *pMP, bool pinhole_formula, float &u,
+                           float &v, int &level)
     {
         const Sophus::SE3f Tcw = Sophus::SE3f(Scw.rotationMatrix(), Scw.translation() / Scw.scale());
         const Eigen::Vector3f Ow = Tcw.inverse().translation();
         const Eigen::Vector3f p3Dw = pMP->GetWorldPos();
         const Eigen::Vector3f p3Dc = Tcw * p3Dw;
         if (p3Dc(2) < 0.0f) return false;
-        const Eigen::Vector2f uv = pKF->mpCamera->project(p3Dc);
-        if (!pKF->IsInImage(uv(0), uv(1))) return false;
+        if (pinhole_formula) {
+            const float invz = 1 / p3Dc(2);
+            const float x = p3Dc(0) * invz;
+            const float y = p3Dc(1) * invz;
+            u = pKF->fx * x + pKF->cx;
+            v = pKF->fy * y + pKF->cy;
+        } else {
+            const Eigen::Vector2f uv = pKF->mpCamera->project(p3Dc);
+            u = uv(0);
+            v = uv(1);
+        }
+        if (!pKF->IsInImage(u, v)) return false;
         const float maxDistance = pMP->GetMaxDistanceInvariance();
         const float minDistance = pMP->GetMinDistanceInvariance();
         const Eigen::Vector3f PO = p3Dw - Ow;
@@ -196,9 +210,12 @@ struct OsgHooks {
         const Eigen::Vector3f Pn = pMP->GetNormal();
         if (PO.dot(Pn) < 0.5 * dist3D) return false;
         level = pMP->PredictScale(dist3D, pKF);
-        u = uv(0);
-        v = uv(1);
         return true;
+    }
+    static bool fuse_sim3_query(KeyFrame *pKF, const Sophus::Sim3f &Scw, MapPoint *pMP, float &u, float &v,
+                                int &level)
+    {
+        return sim3_query(pKF, Scw, pMP, false, u, v, level);
     }
 };
 

@@ -578,6 +578,49 @@ int search_by_bow_kf_kf(KeyFrameT *pKF1, KeyFrameT *pKF2, std::vector<MapPointT 
     return nm;
 }
 
+// ------------------------------------------------- b5 SearchByProjection(KeyFrame*, Sim3f&, ...)
+// ref:src/ORBmatcher.cc:498-621 (vpPointsKFs == nullptr) and :623-733 (with vpPointsKFs / vpMatchedKF).
+// The pre-search part and the projection come from H::sim3_query; the GPU takes the greedy search.
+template <class H, class KeyFrameT, class Sim3T, class MapPointT>
+int search_by_projection_sim3(KeyFrameT *pKF, const Sim3T &Scw, const std::vector<MapPointT *> &vpPoints,
+                              const std::vector<KeyFrameT *> *vpPointsKFs, std::vector<MapPointT *> &vpMatched,
+                              std::vector<KeyFrameT *> *vpMatchedKF, int th, float ratioHamming)
+{
+    osg_ctx *ctx = thread_ctx();
+    FrameView<KeyFrameT> fv(*pKF);
+    std::set<MapPointT *> spAlreadyFound(vpMatched.begin(), vpMatched.end());  // :515-516
+    spAlreadyFound.erase(static_cast<MapPointT *>(nullptr));
+    const int n = (int)vpPoints.size();
+    std::vector<uint8_t> desc((size_t)n * 32), valid(n, 0);
+    std::vector<float> u(n, 0.f), v(n, 0.f);
+    std::vector<int32_t> lvl(n, 0);
+    for (int i = 0; i < n; i++) {
+        MapPointT *p = vpPoints[i];
+        if (p->isBad() || spAlreadyFound.count(p)) continue;  // :528, :647
+        if (!H::sim3_query(pKF, Scw, p, vpPointsKFs != nullptr, u[i], v[i], lvl[i])) continue;
+        valid[i] = 1;
+        const auto d = p->GetDescriptor();
+        std::memcpy(&desc[(size_t)32 * i], d.template ptr<unsigned char>(0), 32);
+    }
+    std::vector<int32_t> slot_query(pKF->N);
+    for (int i = 0; i < pKF->N; i++) slot_query[i] = vpMatched[i] ? -2 : -1;
+    osg_fuse_queries q{};
+    q.n = n;
+    q.desc = desc.data();
+    q.valid = valid.data();
+    q.u = u.data();
+    q.v = v.data();
+    q.pred_level = lvl.data();
+    const int nm = check(ctx, osg_search_by_projection_sim3(ctx, &fv.v, &q, (float)th, ratioHamming, slot_query.data()),
+                         "osg_search_by_projection_sim3");
+    for (int i = 0; i < pKF->N; i++)
+        if (slot_query[i] >= 0) {  // vpMatched[bestIdx] = pMP (, vpMatchedKF[bestIdx] = pKFi), :614 / :726-727
+            vpMatched[i] = vpPoints[slot_query[i]];
+            if (vpMatchedKF) (*vpMatchedKF)[i] = (*vpPointsKFs)[slot_query[i]];
+        }
+    return nm;
+}
+
 // ----------------------------------------------------------------- b3 SearchForTriangulation
 // ref:src/ORBmatcher.cc:1045-1328.  vMatchedPairs = (KF1 index, KF2 index) in ascending KF1 index.
 // The epipole and the F12 matrices come from the hook (the reference's Sophus / Eigen code).

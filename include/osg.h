@@ -283,13 +283,13 @@ int osg_fuse_search_batch(osg_ctx *ctx, const osg_frame *KF, const osg_fuse_quer
 
 /* ---- b5: the Sim3 projections of LoopClosing -------------------------------------------------------
  *   SearchByProjection(KeyFrame*, Sophus::Sim3f& Scw, const vector<MapPoint*>&, vector<MapPoint*>& vpMatched,
- *                      th, ratioHamming)                                  ref:src/ORBmatcher.cc:498-609
+ *                      th, ratioHamming)                                  ref:src/ORBmatcher.cc:498-621
  *   SearchByProjection(KeyFrame*, Sim3f&, vpPoints, vpPointsKFs, vpMatched, vpMatchedKF, th, ratioHamming)
- *                                                                         ref:src/ORBmatcher.cc:611-733
+ *                                                                         ref:src/ORBmatcher.cc:623-733
  * (ref:src/LoopClosing.cc:1062, 1091, 1368).  Queries are osg_fuse_queries (ur and inv_level_sigma2
  * unused): valid = !isBad() && not already in vpMatched && depth >= 0 && in image && dist3D inside
  * [min, max] invariance && PO.dot(Pn) >= 0.5 dist; u, v = the Sim3 projection; pred_level =
- * PredictScale (the caller's part, :525-569).  The device walks KeyFrame::GetFeaturesInArea(u, v,
+ * PredictScale (the caller's part, :528-572).  The device walks KeyFrame::GetFeaturesInArea(u, v,
  * th * mvScaleFactors[pred_level]) skipping taken slots and keypoints outside [pred_level - 1,
  * pred_level], keeps the first minimum distance and accepts it iff bestDist <= TH_LOW * ratioHamming
  * (float); the accepted slot is taken for every later MapPoint (sequential greedy, solved exactly).

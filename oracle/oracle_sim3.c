@@ -1,8 +1,8 @@
 /* oracle_sim3.c — CPU restatement of the Sim3 projection matchers of LoopClosing.
  * TEST INFRASTRUCTURE ONLY: the checker for tests/, never linked into the product.
  *
- *   SearchByProjection(KeyFrame*, Sim3f&, vpPoints, vpMatched, th, ratioHamming)   ref:src/ORBmatcher.cc:498-609
- *   SearchByProjection(KeyFrame*, Sim3f&, vpPoints, vpPointsKFs, ...)              ref:src/ORBmatcher.cc:611-733
+ *   SearchByProjection(KeyFrame*, Sim3f&, vpPoints, vpMatched, th, ratioHamming)   ref:src/ORBmatcher.cc:498-621
+ *   SearchByProjection(KeyFrame*, Sim3f&, vpPoints, vpPointsKFs, ...)              ref:src/ORBmatcher.cc:623-733
  * The caller's pre-search part (bad / already found / depth / image / distance / angle, the
  * projection and PredictScale) arrives folded into the queries (osg.h).  The loop body from
  * GetFeaturesInArea on is literal: vpMatched is written as soon as a MapPoint is accepted. */
@@ -18,7 +18,7 @@ int oracle_search_by_projection_sim3(const osg_frame *KF, const osg_fuse_queries
     for (int iMP = 0; iMP < Q->n; iMP++) {
         if (!Q->valid[iMP]) continue;
         const int nPredictedLevel = Q->pred_level[iMP];
-        const float radius = th * KF->scale_factors[nPredictedLevel];                            /* :561 */
+        const float radius = th * KF->scale_factors[nPredictedLevel];                            /* :574 */
         const int nc = oracle_frame_features_in_area(KF, Q->u[iMP], Q->v[iMP], radius, -1, -1, 0, vIndices);
         if (nc == 0) continue;
         const uint8_t *dMP = Q->desc + 32 * (size_t)iMP;
@@ -34,7 +34,7 @@ int oracle_search_by_projection_sim3(const osg_frame *KF, const osg_fuse_queries
                 bestIdx = idx;
             }
         }
-        if (bestDist <= OSG_TH_LOW * ratioHamming) {                                             /* :603 */
+        if (bestDist <= OSG_TH_LOW * ratioHamming) {                                             /* :612 */
             slot_query[bestIdx] = iMP;
             nmatches++;
         }

@@ -1,7 +1,7 @@
 // sim3.hip — the Sim3 projection matchers of LoopClosing on gfx950:
 //   SearchByProjection(KeyFrame*, Sim3f& Scw, const vector<MapPoint*>&, vector<MapPoint*>& vpMatched, th, ratioHamming)
-//                                                                     ref:src/ORBmatcher.cc:498-609
-//   and its vpPointsKFs / vpMatchedKF overload                         ref:src/ORBmatcher.cc:611-733
+//                                                                     ref:src/ORBmatcher.cc:498-621
+//   and its vpPointsKFs / vpMatchedKF overload                         ref:src/ORBmatcher.cc:623-733
 // (LoopClosing calls them at ref:src/LoopClosing.cc:1062, 1091, 1368).
 //
 // Per MapPoint (query, list order): KeyFrame::GetFeaturesInArea (ix outer, iy inner, strict window;
@@ -55,7 +55,7 @@ __device__ int choose(const Sim3Args &A, int q, const int *claim, const uint8_t 
 {
     const int lvl = A.lvl[q];
     const float u = A.u[q], v = A.v[q];
-    const float r = A.th * A.scale[lvl];  // ref:src/ORBmatcher.cc:561 / 682
+    const float r = A.th * A.scale[lvl];  // ref:src/ORBmatcher.cc:574 / 690
     int minCX = (int)floorf((u - A.min_x - r) * A.inv_w);
     minCX = minCX < 0 ? 0 : minCX;
     int maxCX = (int)ceilf((u - A.min_x + r) * A.inv_w);
@@ -66,16 +66,16 @@ __device__ int choose(const Sim3Args &A, int q, const int *claim, const uint8_t 
     maxCY = maxCY > OSG_GRID_ROWS - 1 ? OSG_GRID_ROWS - 1 : maxCY;
     const bool empty = minCX >= OSG_GRID_COLS || maxCX < 0 || minCY >= OSG_GRID_ROWS || maxCY < 0;
     const u32x4 qa = *(GLOBAL const u32x4 *)(A.qdesc + 8 * q), qb = *(GLOBAL const u32x4 *)(A.qdesc + 8 * q + 4);
-    int bd = 256, bi = -1;  // :578-579
+    int bd = 256, bi = -1;  // :585-586
     for (int ix = empty ? maxCX + 1 : minCX; ix <= maxCX; ix++) {
         const int j1 = A.gs[ix * OSG_GRID_ROWS + maxCY + 1];
         for (int j = A.gs[ix * OSG_GRID_ROWS + minCY]; j < j1; j++) {
             const int idx = A.gi[j];
             const float kx = A.kp_x[idx], ky = A.kp_y[idx];
             if (!(fabsf(kx - u) < r && fabsf(ky - v) < r)) continue;  // ref:src/KeyFrame.cc:897-900
-            if (taken0[idx] || claim[idx] < q) continue;              // vpMatched[idx], :584-585
+            if (taken0[idx] || claim[idx] < q) continue;              // vpMatched[idx], :595-596
             const int oct = A.kp_octave[idx];
-            if (oct < lvl - 1 || oct > lvl) continue;                  // :589-590
+            if (oct < lvl - 1 || oct > lvl) continue;                  // :597-598
             const u32x4 ka = *(GLOBAL const u32x4 *)(A.kdesc + 8 * idx), kb = *(GLOBAL const u32x4 *)(A.kdesc + 8 * idx + 4);
             uint32_t d = __popc(qa.x ^ ka.x);
             d = bcnt_acc(qa.y ^ ka.y, d);
@@ -85,13 +85,13 @@ __device__ int choose(const Sim3Args &A, int q, const int *claim, const uint8_t 
             d = bcnt_acc(qb.y ^ kb.y, d);
             d = bcnt_acc(qb.z ^ kb.z, d);
             d = bcnt_acc(qb.w ^ kb.w, d);
-            if ((int)d < bd) {  // :596-600
+            if ((int)d < bd) {  // :604-608
                 bd = (int)d;
                 bi = idx;
             }
         }
     }
-    return ((float)bd <= A.thr) ? bi : -1;  // bestDist <= TH_LOW * ratioHamming, :603
+    return ((float)bd <= A.thr) ? bi : -1;  // bestDist <= TH_LOW * ratioHamming, :612 / :724
 }
 
 __global__ __launch_bounds__(ST) void k_sim3(const Sim3Args *__restrict__ args)

@@ -1,7 +1,7 @@
 // adapter_driver.cpp — runs adapters/orbslam3/osg_orbslam3.h on mock ORB-SLAM3 objects built from
 // arrays written by tests/test_adapter.py, and writes the adapter's results back (test-only).
 //
-//   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba fuse fuse_sim3 triang distinct
+//   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba fuse fuse_sim3 triang distinct sim3 sim3_kfs
 //
 // Array file: repeated {u32 name_len, name, u8 dtype ('b' u8, 'i' i32, 'f' f32, 'd' f64), u64 count,
 // data}.
@@ -585,6 +585,52 @@ int main(int argc, char **argv)
             }
             out["nmatches"] = make('i', std::vector<int32_t>{nm});
             out["pairs"] = make('i', flat);
+        } else if (mode == "sim3" || mode == "sim3_kfs") {
+            // keyframe "F.*"; MapPoint pool "P.*" (desc ok u v level bad); "L.list" pool indices;
+            // "V.matched" initial vpMatched (pool index, -1); params: th ratio
+            KeyFrame K;
+            build_kf_frame(in, K);
+            const int np = (int)get(in, "P.bad").n;
+            std::vector<MapPoint> P(np);
+            for (int i = 0; i < np; i++) {
+                MapPoint &p = P[i];
+                p.mnId = (unsigned long)i;
+                std::memcpy(p.desc.buf.data(), get(in, "P.desc").p<uint8_t>() + 32 * i, 32);
+                p.proj_ok = get(in, "P.ok").p<uint8_t>()[i];
+                p.proj_u = get(in, "P.u").p<float>()[i];
+                p.proj_v = get(in, "P.v").p<float>()[i];
+                p.proj_level = get(in, "P.level").p<int32_t>()[i];
+                p.bad = get(in, "P.bad").p<uint8_t>()[i];
+            }
+            const Arr &L = get(in, "L.list");
+            std::vector<MapPoint *> list(L.n);
+            std::vector<KeyFrame> owners(7);
+            std::vector<KeyFrame *> list_kfs(L.n);
+            for (size_t i = 0; i < L.n; i++) {
+                list[i] = &P[L.p<int32_t>()[i]];
+                list_kfs[i] = &owners[i % 7];
+            }
+            std::vector<MapPoint *> matched(K.N, nullptr);
+            std::vector<KeyFrame *> matched_kf(K.N, nullptr);
+            for (int k = 0; k < K.N; k++) {
+                const int32_t m = get(in, "V.matched").p<int32_t>()[k];
+                if (m >= 0) matched[k] = &P[m];
+            }
+            int nm;
+            if (mode == "sim3")
+                nm = osg_orbslam3::search_by_projection_sim3<MockHooks, KeyFrame>(&K, Sim3{}, list, nullptr, matched,
+                                                                                 nullptr, (int)prm[0], prm[1]);
+            else
+                nm = osg_orbslam3::search_by_projection_sim3<MockHooks, KeyFrame>(&K, Sim3{}, list, &list_kfs, matched,
+                                                                                 &matched_kf, (int)prm[0], prm[1]);
+            std::vector<int32_t> mo(K.N, -1), mk(K.N, -1);
+            for (int k = 0; k < K.N; k++) {
+                if (matched[k]) mo[k] = (int32_t)matched[k]->mnId;
+                if (matched_kf[k]) mk[k] = (int32_t)(matched_kf[k] - owners.data());
+            }
+            out["nmatches"] = make('i', std::vector<int32_t>{nm});
+            out["matched"] = make('i', mo);
+            out["matched_kf"] = make('i', mk);
         } else if (mode == "distinct") {
             // keyframes: "K.desc" (nk x nkp rows), "K.bad"; MapPoints: "M.bad", "M.desc" (initial);
             // observations CSR "O.start" / "O.kf" / "O.left" / "O.right"

@@ -216,6 +216,13 @@ struct MockHooks {
         return p->proj_ok;
     }
     static void triang_geom(KeyFrame *pKF1, KeyFrame *, osg_triang_geom &g) { g = pKF1->triang_geom; }
+    static bool sim3_query(KeyFrame *, const Sim3 &, MapPoint *p, bool, float &u, float &v, int &level)
+    {
+        u = p->proj_u;
+        v = p->proj_v;
+        level = p->proj_level;
+        return p->proj_ok;
+    }
     static void set_descriptor(MapPoint *p, const uint8_t *row) { std::memcpy(p->desc.buf.data(), row, 32); }
     static bool fuse_sim3_query(KeyFrame *, const Sim3 &, MapPoint *p, float &u, float &v, int &level)
     {

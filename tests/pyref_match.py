@@ -462,7 +462,7 @@ def distinctive(desc_lists):
 
 
 def search_sim3(F, Q, th, ratio, slot_query):
-    """SearchByProjection(KeyFrame*, Sim3f&, ...) (ref:src/ORBmatcher.cc:498-609) from the area walk on:
+    """SearchByProjection(KeyFrame*, Sim3f&, ...) (ref:src/ORBmatcher.cc:498-621) from the area walk on:
     vpMatched written as soon as a MapPoint is accepted.  slot_query: -2 taken, -1 free."""
     s = np.array(slot_query, np.int32).copy()
     n = 0

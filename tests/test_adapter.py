@@ -520,3 +520,38 @@ def test_adapter_compute_distinctive_descriptors(driver, tmp_path, oracle):
             want[i] = lists[i][best[i]]
     assert (best >= 0).sum() > 500
     np.testing.assert_array_equal(out["desc"].reshape(-1, 32), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("with_kfs", [False, True])
+def test_adapter_search_by_projection_sim3(driver, tmp_path, oracle, with_kfs):
+    """Both Sim3 SearchByProjection overloads through the adapter: MapPoints already in vpMatched and bad
+    ones skipped, slots taken before the call kept, vpMatched / vpMatchedKF written like the reference."""
+    rng = np.random.default_rng(800 + with_kfs)
+    F = fr.synth_frame(rng, n=700, stereo=False)
+    np_ = 2000
+    Q = fr.synth_fuse_queries(rng, F, m=np_, match_frac=0.7)
+    bad = (rng.random(np_) < 0.05).astype(np.uint8)
+    lst = rng.permutation(np_)[:1600].astype(np.int32)
+    matched0 = np.full(F.n, -1, np.int32)
+    pre = rng.choice(F.n, size=60, replace=False)
+    matched0[pre] = rng.choice(np_, size=60, replace=False)
+    out = run(driver, tmp_path, "sim3_kfs" if with_kfs else "sim3", {
+        **frame_arrays(F), "P.desc": Q.desc.reshape(-1), "P.ok": Q.valid, "P.u": Q.u, "P.v": Q.v,
+        "P.level": Q.pred_level, "P.bad": bad, "L.list": lst, "V.matched": matched0,
+        "params": np.array([5, 1.0], np.float32)})
+    found = set(matched0[matched0 >= 0].tolist())
+    sub = fr.FuseQueries(desc=Q.desc[lst], valid=np.array([Q.valid[p] and not bad[p] and p not in found for p in lst],
+                                                          np.uint8),
+                         u=Q.u[lst], v=Q.v[lst], ur=None, pred_level=Q.pred_level[lst],
+                         inv_level_sigma2=Q.inv_level_sigma2)
+    n, sq = oc.sim3(oracle, F, sub, 5, 1.0, np.where(matched0 >= 0, -2, -1))
+    assert n > 200
+    want = matched0.copy()
+    want[sq >= 0] = lst[sq[sq >= 0]]
+    assert int(out["nmatches"][0]) == n
+    np.testing.assert_array_equal(out["matched"], want)
+    if with_kfs:
+        wk = np.full(F.n, -1, np.int32)
+        wk[sq >= 0] = sq[sq >= 0] % 7
+        np.testing.assert_array_equal(out["matched_kf"], wk)
