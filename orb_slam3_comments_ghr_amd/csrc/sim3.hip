@@ -73,7 +73,7 @@ __device__ int choose(const Sim3Args &A, int q, const int *claim, const uint8_t 
             const int idx = A.gi[j];
             const float kx = A.kp_x[idx], ky = A.kp_y[idx];
             if (!(fabsf(kx - u) < r && fabsf(ky - v) < r)) continue;  // ref:src/KeyFrame.cc:897-900
-            if (taken0[idx] || claim[idx] < q) continue;              // vpMatched[idx], :595-596
+            if (taken0[idx] || claim[idx] < q) continue;              // vpMatched[idx], :591-592
             const int oct = A.kp_octave[idx];
             if (oct < lvl - 1 || oct > lvl) continue;                  // :597-598
             const u32x4 ka = *(GLOBAL const u32x4 *)(A.kdesc + 8 * idx), kb = *(GLOBAL const u32x4 *)(A.kdesc + 8 * idx + 4);

@@ -1,0 +1,66 @@
+"""Kernel device time of the §8(f) matchers built this round, at their reference call shapes, beside the
+C oracle on one host thread (bounded samples).  python tools/widen_bench.py
+
+  triang    SearchForTriangulation, 1200 x 1200 keypoints, batches of B keyframe pairs
+  sim3      SearchByProjection(KeyFrame*, Sim3f&, ...), 1200 keypoints, 3000 / 9000 MapPoints (th 8, 1.5)
+  distinct  ComputeDistinctiveDescriptors, 1000 / 100 000 MapPoints, N ~ U{1..30} rows
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from orb_slam3_comments_ghr_amd import Context, frames as fr, mappoint as mp  # noqa: E402
+from orb_slam3_comments_ghr_amd.matcher import ORBmatcher  # noqa: E402
+from tests import oracle_calls as oc  # noqa: E402
+
+
+def best_of(fn, ctx, n=3):
+    fn()
+    ks = []
+    for _ in range(n):
+        fn()
+        ks.append(ctx.last_kernel_ms())
+    return min(ks)
+
+
+def cpu(fn, n):
+    t = time.perf_counter()
+    for i in range(n):
+        fn(i)
+    return (time.perf_counter() - t) / n * 1e3
+
+
+def main():
+    ctx = Context(0)
+    o = oc.load()
+    m = ORBmatcher(ctx)
+    rng = np.random.default_rng(11)
+    pairs = [fr.synth_triang_pair(rng, n1=1200, n2=1200, forward=bool(i % 2)) for i in range(8)]
+    for B in (1, 20, 256):
+        P = [pairs[i % 8] for i in range(B)]
+        k = best_of(lambda: m.SearchForTriangulationBatch([p[0] for p in P], [p[1] for p in P], [p[2] for p in P]), ctx)
+        print(f"triang   B={B:4d}  kernel {k * 1e3 / B:8.2f} us/pair", flush=True)
+    c = cpu(lambda i: oc.triangulation(o, *pairs[i % 8]), 64)
+    print(f"triang   oracle {c * 1e3:8.2f} us/pair (1 thread)", flush=True)
+    for nq in (3000, 9000):
+        F = fr.synth_frame(rng, n=1200, stereo=False)
+        Q = fr.synth_fuse_queries(rng, F, m=nq, match_frac=0.7)
+        ids = np.arange(nq, dtype=np.int32)
+        k = best_of(lambda: m.SearchByProjectionSim3(F, Q, ids, np.full(F.n, -1, np.int32), 8, 1.5), ctx)
+        rounds = ctx.match_last_stats()["rounds"]
+        c = cpu(lambda i: oc.sim3(o, F, Q, 8, 1.5, np.full(F.n, -1, np.int32)), 20)
+        print(f"sim3     nq={nq:5d}  kernel {k * 1e3:8.2f} us  rounds {rounds}  oracle {c * 1e3:8.2f} us", flush=True)
+    for n in (1000, 100000):
+        lists = mp.synth_observations(rng, n_points=n, n_max=30)
+        desc, start = mp.to_csr(lists)
+        k = best_of(lambda: mp.ComputeDistinctiveDescriptors(ctx, desc=desc, start=start), ctx)
+        c = cpu(lambda i: oc.distinctive(o, desc, start), 1 if n > 1000 else 10)
+        print(f"distinct n={n:6d}  kernel {k * 1e3:9.2f} us ({k * 1e6 / n:7.1f} ns/point)  oracle {c * 1e3:10.1f} us",
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
