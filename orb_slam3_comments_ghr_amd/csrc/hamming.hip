@@ -292,6 +292,103 @@ __device__ __forceinline__ void qs_scan(const uint4 *rows, int n, int sl, uint32
     }
 }
 
+// Query-split with QT queries per thread: a row read from LDS once serves QT queries, so the
+// per-workgroup LDS read volume drops QT-fold (the QT = 1 form reads 16 x 32 B per thread at
+// C2).  G = QB / QT query groups, S = 1024 / G row slices; thread t: group t % G, slice t / G.
+// dbg (sweeps only): 1 = no compute, 2 = no global staging loads, 4 = no reduction.
+template <int QB, int QT>
+__global__ __launch_bounds__(1024) void k_top2_qsplit_mq(const uint4 *__restrict__ query, int nq,
+                                                         const uint4 *__restrict__ train, int nt,
+                                                         int32_t *__restrict__ out, int dbg)
+{
+    constexpr int G = QB / QT;
+    constexpr int S = 1024 / G;
+    __shared__ uint4 s_rows[2 * QS_ROWS];
+    __shared__ uint32_t s_k1[16][QB], s_k2[16][QB];
+    const int t = threadIdx.x;
+    const int w = t >> 6, lane = t & 63;
+    const int g = t % G;
+    const int sl = t / G;
+    uint32_t qd[QT][8];
+#pragma unroll
+    for (int j = 0; j < QT; j++) {
+        int qq = blockIdx.x * QB + g * QT + j;
+        qq = qq < nq ? qq : nq - 1;
+        const uint4 a = query[2 * qq], b = query[2 * qq + 1];
+        qd[j][0] = a.x; qd[j][1] = a.y; qd[j][2] = a.z; qd[j][3] = a.w;
+        qd[j][4] = b.x; qd[j][5] = b.y; qd[j][6] = b.z; qd[j][7] = b.w;
+    }
+    uint32_t k1[QT], k2[QT];
+#pragma unroll
+    for (int j = 0; j < QT; j++) k1[j] = k2[j] = KEY_EMPTY;
+    for (int c0 = 0; c0 < nt; c0 += QS_ROWS) {
+        const int n = min(QS_ROWS, nt - c0);
+        const uint4 *src = train + 2 * (size_t)c0;
+        const int last = 2 * n - 1;
+        uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0, v2 = v0, v3 = v0;
+        if (!(dbg & 2)) {
+            v0 = src[min(t, last)];
+            v1 = src[min(1024 + t, last)];
+            v2 = src[min(2048 + t, last)];
+            v3 = src[min(3072 + t, last)];
+        }
+        if (c0 > 0) __syncthreads();
+        s_rows[t] = v0;
+        s_rows[1024 + t] = v1;
+        s_rows[2048 + t] = v2;
+        s_rows[3072 + t] = v3;
+        __syncthreads();
+        if (dbg & 1) continue;
+        int r = sl;
+        for (; r + S < n; r += 2 * S) {
+            uint32_t tr[2][8];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const uint4 a = s_rows[2 * (r + u * S)], b = s_rows[2 * (r + u * S) + 1];
+                tr[u][0] = a.x; tr[u][1] = a.y; tr[u][2] = a.z; tr[u][3] = a.w;
+                tr[u][4] = b.x; tr[u][5] = b.y; tr[u][6] = b.z; tr[u][7] = b.w;
+            }
+#pragma unroll
+            for (int u = 0; u < 2; u++)
+#pragma unroll
+                for (int j = 0; j < QT; j++)
+                    key_push(k1[j], k2[j], (hamming8(qd[j], tr[u]) << KEY_SHIFT) | (uint32_t)(c0 + r + u * S));
+        }
+        for (; r < n; r += S) {
+            const uint4 a = s_rows[2 * r], b = s_rows[2 * r + 1];
+            const uint32_t tr[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+            for (int j = 0; j < QT; j++) key_push(k1[j], k2[j], (hamming8(qd[j], tr) << KEY_SHIFT) | (uint32_t)(c0 + r));
+        }
+    }
+    if (!(dbg & 4)) {
+        // lanes of one query group inside the wave: lane ^ G, ^ 2G, ... < 64
+#pragma unroll
+        for (int off = G; off < 64; off <<= 1)
+#pragma unroll
+            for (int j = 0; j < QT; j++) {
+                const uint32_t a1 = __shfl_xor(k1[j], off), a2 = __shfl_xor(k2[j], off);
+                key_merge(k1[j], k2[j], a1, a2);
+            }
+    }
+    if (lane < G) {
+#pragma unroll
+        for (int j = 0; j < QT; j++) {
+            s_k1[w][lane * QT + j] = k1[j];
+            s_k2[w][lane * QT + j] = k2[j];
+        }
+    }
+    __syncthreads();
+    const int q = blockIdx.x * QB + t;
+    if (t < QB && q < nq) {
+        uint32_t a1 = s_k1[0][t], a2 = s_k2[0][t];
+#pragma unroll
+        for (int o = 1; o < 16; o++) key_merge(a1, a2, s_k1[o][t], s_k2[o][t]);
+        const uint2 p = key_to_part(a1, a2, 0u);
+        write_result(out, q, p.y >> 16, p.x, p.y & 0xFFFFu);
+    }
+}
+
 // (Measured on MI355X at 2000 x 2000, kernel average over back-to-back launches: this register
 // staging 5.75 us; LDS-DMA staging (global_load_lds_dwordx4) with per-quarter counted waits
 // 6.1 us, whether the rows are then read with compiler-scheduled or inline-asm ds_reads.)
@@ -525,14 +622,14 @@ int env_int(const char *name, int dflt)
     return (v && *v) ? atoi(v) : dflt;
 }
 struct top2_knobs {
-    int variant, waves, target_wg, min_rows, dbg, stream_g, qs_wg;
+    int variant, waves, target_wg, min_rows, dbg, stream_g, qs_wg, qt;
 };
 const top2_knobs &knobs(int cus)
 {
     static const top2_knobs k = {env_int("OSG_TOP2_VARIANT", 2), env_int("OSG_TOP2_WAVES", 0),
                                  env_int("OSG_TOP2_WG", cus), env_int("OSG_TOP2_MIN_ROWS", 64),
                                  env_int("OSG_TOP2_DEBUG", 0), env_int("OSG_TOP2_STREAM_G", 2 * cus),
-                                 env_int("OSG_TOP2_QS_WG", cus * 9 / 10)};
+                                 env_int("OSG_TOP2_QS_WG", cus * 9 / 10), env_int("OSG_TOP2_QT", 1)};
     return k;
 }
 
@@ -587,6 +684,20 @@ int osg_launch_top2(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d
         const uint4 *q = (const uint4 *)d_query;
         const uint4 *t = (const uint4 *)d_train;
         int32_t *o = (int32_t *)d_out;
+        const int qt = std::min(kn.qt, qb);
+        if (qt > 1 || kn.dbg) {  // QT queries per thread (sweeps: OSG_TOP2_QT, OSG_TOP2_DEBUG)
+            const int dbg = kn.dbg;
+#define OSG_MQ(QB_, QT_)                                                                                       \
+    if (qb == QB_ && qt == QT_) {                                                                             \
+        hipLaunchKernelGGL((k_top2_qsplit_mq<QB_, QT_>), grid, block, 0, ctx->stream, q, nq, t, nt, o, dbg);   \
+        OSG_HIP_CHECK(ctx, hipGetLastError());                                                                 \
+        return OSG_OK;                                                                                         \
+    }
+            OSG_MQ(8, 1) OSG_MQ(8, 2) OSG_MQ(8, 4) OSG_MQ(8, 8)
+            OSG_MQ(16, 1) OSG_MQ(16, 2) OSG_MQ(16, 4) OSG_MQ(16, 8)
+            OSG_MQ(4, 1) OSG_MQ(4, 2) OSG_MQ(4, 4)
+#undef OSG_MQ
+        }
         switch (qb) {
         case 64: hipLaunchKernelGGL(k_top2_qsplit<64>, grid, block, 0, ctx->stream, q, nq, t, nt, o); break;
         case 32: hipLaunchKernelGGL(k_top2_qsplit<32>, grid, block, 0, ctx->stream, q, nq, t, nt, o); break;

@@ -1,7 +1,7 @@
 """Per-configuration timing of the top-2 tile kernel; one child process per configuration because
 the launch knobs (OSG_TOP2_*) are read once per process.  The parent never touches the GPU.
 
-    python tools/top2_breakdown.py nq nt "VARIANT:WAVES:WG:DEBUG[:STREAM_G]" ...
+    python tools/top2_breakdown.py nq nt "VARIANT:WAVES:WG:DEBUG[:STREAM_G[:QT]]" ...
 
 Each child prints one JSON line: per-launch event bracket, empty bracket, and back-to-back
 average, so the event calibration can be compared with rocprofv3 --kernel-trace."""
@@ -66,8 +66,10 @@ def main():
         variant, waves, wg, dbg = f[:4]
         env = dict(os.environ, OSG_ROOT=root, OSG_TOP2_VARIANT=variant, OSG_TOP2_WAVES=waves,
                    OSG_TOP2_WG=wg, OSG_TOP2_QS_WG=wg, OSG_TOP2_DEBUG=dbg)
-        if len(f) > 4:
+        if len(f) > 4 and f[4]:
             env["OSG_TOP2_STREAM_G"] = f[4]
+        if len(f) > 5 and f[5]:
+            env["OSG_TOP2_QT"] = f[5]
         r = subprocess.run([sys.executable, "-c", CHILD, nq, nt], env=env, capture_output=True, text=True, timeout=300)
         line = r.stdout.strip().splitlines()[-1] if r.returncode == 0 and r.stdout.strip() else json.dumps({"rc": r.returncode, "err": r.stderr[-400:]})
         print(json.dumps({"nq": int(nq), "nt": int(nt), "cfg": cfg, **json.loads(line)}), flush=True)
