@@ -281,6 +281,21 @@ int osg_fuse_search(osg_ctx *ctx, const osg_frame *KF, const osg_fuse_queries *Q
 int osg_fuse_search_batch(osg_ctx *ctx, const osg_frame *KF, const osg_fuse_queries *Q, int32_t B, float th,
                           int right, int gated, int32_t *best_idx, int32_t *best_dist, int32_t *nfused);
 
+/* ---- b6: SearchForInitialization ------------------------------------------------------------------
+ * ORBmatcher::SearchForInitialization(Frame &F1, Frame &F2, vector<cv::Point2f> &vbPrevMatched,
+ * vector<int> &vnMatches12, windowSize)  ref:src/ORBmatcher.cc:735-878 (monocular initialisation,
+ * ref:src/Tracking.cc:2956).  F1 / F2: monocular frames (mvKeysUn; F1's grid is not read).
+ * prev_xy[2 * F1.n] in/out = vbPrevMatched; matches12[F1.n] out = vnMatches12.  The reference's
+ * order-dependent state (vMatchedDistance skip, vnMatches21 steal, every accepted match counted in
+ * the rotation histogram even if stolen later) is reproduced exactly.  Returns nmatches.
+ * F2.n <= 8192. */
+int osg_search_for_initialization(osg_ctx *ctx, const osg_frame *F1, const osg_frame *F2, float *prev_xy,
+                                  int window_size, float nnratio, int check_orientation, int32_t *matches12);
+/* B frame pairs in one launch; prev_xy / matches12 concatenated by F1[b].n. */
+int osg_search_for_initialization_batch(osg_ctx *ctx, const osg_frame *F1, const osg_frame *F2, int32_t B,
+                                        float *prev_xy, int window_size, float nnratio, int check_orientation,
+                                        int32_t *matches12, int32_t *nmatches);
+
 /* ---- b5: the Sim3 projections of LoopClosing -------------------------------------------------------
  *   SearchByProjection(KeyFrame*, Sophus::Sim3f& Scw, const vector<MapPoint*>&, vector<MapPoint*>& vpMatched,
  *                      th, ratioHamming)                                  ref:src/ORBmatcher.cc:498-621

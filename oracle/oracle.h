@@ -38,6 +38,9 @@ void oracle_dbow_transform(const osg_vocabulary_desc *V, const uint8_t *desc, in
 /* Fuse search half (oracle_fuse.c) */
 int oracle_fuse_search(const osg_frame *KF, const osg_fuse_queries *Q, float th, int right, int gated,
                        int32_t *best_idx, int32_t *best_dist);
+/* SearchForInitialization (oracle_init.c); prev_xy in/out */
+int oracle_search_for_initialization(const osg_frame *F1, const osg_frame *F2, float *prev_xy, int windowSize,
+                                     float mfNNratio, int checkOri, int32_t *vnMatches12);
 /* Sim3 projections of LoopClosing (oracle_sim3.c); slot_query as osg_search_by_projection_sim3 */
 int oracle_search_by_projection_sim3(const osg_frame *KF, const osg_fuse_queries *Q, float th, float ratioHamming,
                                      int32_t *slot_query);

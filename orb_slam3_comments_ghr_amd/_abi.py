@@ -170,6 +170,7 @@ EXPORTS = [
     "osg_fuse_search", "osg_fuse_search_batch", "osg_search_for_triangulation", "osg_search_for_triangulation_batch",
     "osg_compute_distinctive_descriptors", "osg_compute_distinctive_descriptors_dev",
     "osg_search_by_projection_sim3", "osg_search_by_projection_sim3_batch",
+    "osg_search_for_initialization", "osg_search_for_initialization_batch",
 ]
 
 
@@ -229,6 +230,9 @@ def declare(lib: C.CDLL) -> C.CDLL:
                                                  C.POINTER(OsgTriangGeom), C.c_int, C.c_int, C.c_int, vp]
     lib.osg_search_by_projection_sim3.argtypes = [vp, C.POINTER(OsgFrame), C.POINTER(OsgFuseQueries), f32, f32, vp]
     lib.osg_search_by_projection_sim3_batch.argtypes = [vp, vp, vp, i32, f32, f32, vp, vp]
+    lib.osg_search_for_initialization.argtypes = [vp, C.POINTER(OsgFrame), C.POINTER(OsgFrame), vp, C.c_int, f32,
+                                                  C.c_int, vp]
+    lib.osg_search_for_initialization_batch.argtypes = [vp, vp, vp, i32, vp, C.c_int, f32, C.c_int, vp, vp]
     lib.osg_compute_distinctive_descriptors.argtypes = [vp, vp, vp, i32, vp]
     lib.osg_compute_distinctive_descriptors_dev.argtypes = [vp, vp, vp, i32, vp]
     lib.osg_search_for_triangulation_batch.argtypes = [vp, vp, vp, vp, i32, C.c_int, C.c_int, C.c_int, vp, vp]

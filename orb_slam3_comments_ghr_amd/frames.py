@@ -757,3 +757,43 @@ def synth_triang_pair(rng, n1=1000, n2=1000, n_nodes=100, common=0.6, mp_frac=0.
         sides[1].kp_x[near] = np.float32(ep[0]) + rng.uniform(-20, 20, len(near)).astype(np.float32)
         sides[1].kp_y[near] = np.float32(ep[1]) + rng.uniform(-20, 20, len(near)).astype(np.float32)
     return sides[0], sides[1], TriangGeom(ep=ep, F12=np.stack(F))
+
+
+# ------------------------------------------------------------- b6 SearchForInitialization
+
+def synth_init_pair(rng, n1=2000, n2=2000, match=0.7, level0=0.5, shift=(12.0, -4.0), noise=1.5, steal=0.15,
+                    n_levels=8):
+    """Monocular initialisation (Tracking::MonocularInitialization, 2x features): F2 sees F1's scene
+    moved by ``shift`` px (+ noise); ``match`` of F1's keypoints have a noisy descriptor copy in F2 (same
+    octave; ``level0`` of all keypoints at octave 0, the only level the matcher reads).  ``steal`` of
+    the matched F2 keypoints get a second, LATER F1 keypoint nearby with a closer descriptor copy, so
+    vnMatches21 steals and vMatchedDistance skips happen.  Returns (F1, F2, vbPrevMatched = F1's
+    keypoint positions)."""
+    def frame(n):
+        x = rng.uniform(0, EUROC_W, n).astype(np.float32)
+        y = rng.uniform(0, EUROC_H, n).astype(np.float32)
+        oct_ = np.where(rng.random(n) < level0, 0, rng.integers(1, n_levels, n)).astype(np.int32)
+        return x, y, oct_, rng.uniform(0, 360, n).astype(np.float32), rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    x1, y1, o1, a1, d1 = frame(n1)
+    x2, y2, o2, a2, d2 = frame(n2)
+    m = int(match * min(n1, n2))
+    i1 = rng.choice(n1 // 2, size=min(m, n1 // 2), replace=False)   # steal partners come from the upper half
+    i2 = rng.choice(n2, size=len(i1), replace=False)
+    x2[i2] = np.clip(x1[i1] + shift[0] + rng.normal(0, noise, len(i1)), 0, EUROC_W - 1e-3)
+    y2[i2] = np.clip(y1[i1] + shift[1] + rng.normal(0, noise, len(i1)), 0, EUROC_H - 1e-3)
+    o2[i2] = o1[i1]
+    a2[i2] = np.mod(a1[i1] - 7 - rng.normal(0, 3, len(i1)), 360)
+    d2[i2] = _flip(rng, d1[i1], 0.08)
+    ns = int(steal * len(i1))
+    later = rng.choice(np.arange(n1 // 2, n1), size=ns, replace=False)
+    src = rng.choice(len(i1), size=ns, replace=False)
+    x1[later] = x1[i1[src]] + rng.normal(0, 2.0, ns)
+    y1[later] = y1[i1[src]] + rng.normal(0, 2.0, ns)
+    o1[later] = o1[i1[src]]
+    a1[later] = a1[i1[src]]
+    d1[later] = _flip(rng, d2[i2[src]], 0.03)
+    F1 = FrameSoA(desc=d1, kp_x=np.clip(x1, 0, EUROC_W - 1e-3), kp_y=np.clip(y1, 0, EUROC_H - 1e-3), kp_angle=a1,
+                  kp_octave=o1, scale=scale_factors(n_levels))
+    F2 = FrameSoA(desc=d2, kp_x=x2, kp_y=y2, kp_angle=a2, kp_octave=o2, scale=scale_factors(n_levels))
+    prev = np.stack([F1.kp_x, F1.kp_y], axis=1).astype(np.float32)
+    return F1, F2, prev

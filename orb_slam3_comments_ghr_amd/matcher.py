@@ -12,6 +12,7 @@ runs on the GPU (there is no CPU fallback).
     n, best_idx, best_dist = m.Fuse(KF, fq, th, sim3=True)                      # Fuse(KeyFrame*, Sim3f, ...)
     n, vMatchedPairs = m.SearchForTriangulation(KF1, KF2, geom, bOnlyStereo, bCoarse)
     n = m.SearchByProjectionSim3(KF, fq, mp_id, vpMatched, th, ratioHamming[, vpPointsKFs, vpMatchedKF])
+    n, vnMatches12 = m.SearchForInitialization(F1, F2, vbPrevMatched, windowSize)   # vbPrevMatched updated
 """
 from __future__ import annotations
 
@@ -133,6 +134,19 @@ class ORBmatcher:
         if vpMatchedKF is not None:
             vpMatchedKF[new] = np.asarray(vpPointsKFs)[sq[new]]
         return n
+
+    def SearchForInitialization(self, F1: FrameSoA, F2: FrameSoA, vbPrevMatched: np.ndarray, windowSize: int = 100):
+        """``SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize)``
+        (ref:src/ORBmatcher.cc:735-878).  ``vbPrevMatched`` (F1.n x 2 float32) is updated in place;
+        returns (nmatches, vnMatches12)."""
+        lib, h = self.ctx.lib, self.ctx.handle
+        assert vbPrevMatched.dtype == np.float32 and vbPrevMatched.flags["C_CONTIGUOUS"]
+        assert vbPrevMatched.shape == (F1.n, 2)
+        m12 = np.full(F1.n, -1, np.int32)
+        a, b = F1.struct(), F2.struct()
+        rc = lib.osg_search_for_initialization(h, C.byref(a), C.byref(b), vbPrevMatched.ctypes.data, int(windowSize),
+                                               self.mfNNratio, int(self.mbCheckOrientation), m12.ctypes.data)
+        return self.ctx.check(rc, "SearchForInitialization"), m12
 
     @staticmethod
     def _pairs(m12):

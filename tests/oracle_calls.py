@@ -60,6 +60,8 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.oracle_search_for_triangulation.argtypes = [C.POINTER(OsgKfSide), C.POINTER(OsgKfSide),
                                                     C.POINTER(OsgTriangGeom), C.c_int, C.c_int, C.c_int, vp]
     lib.oracle_search_by_projection_sim3.argtypes = [C.POINTER(OsgFrame), C.POINTER(OsgFuseQueries), f32, f32, vp]
+    lib.oracle_search_for_initialization.argtypes = [C.POINTER(OsgFrame), C.POINTER(OsgFrame), vp, C.c_int, f32,
+                                                     C.c_int, vp]
     lib.oracle_compute_distinctive_descriptors.argtypes = [vp, vp, C.c_int, vp]
     lib.oracle_compute_distinctive_descriptors.restype = None
     return lib
@@ -177,3 +179,13 @@ def sim3(oracle, KF, Q, th, ratio, slot_query):
     fs, qs = KF.struct(), Q.struct()
     n = oracle.oracle_search_by_projection_sim3(C.byref(fs), C.byref(qs), float(th), float(ratio), s.ctypes.data)
     return n, s
+
+
+def initialization(oracle, F1, F2, prev_xy, window=100, nn=0.9, ori=True):
+    """SearchForInitialization through the oracle: (nmatches, vnMatches12, vbPrevMatched after)."""
+    p = np.ascontiguousarray(prev_xy, np.float32).copy()
+    m12 = np.full(F1.n, -1, np.int32)
+    a, b = F1.struct(), F2.struct()
+    n = oracle.oracle_search_for_initialization(C.byref(a), C.byref(b), p.ctypes.data, int(window), float(nn),
+                                                int(bool(ori)), m12.ctypes.data)
+    return n, m12, p

@@ -485,3 +485,54 @@ def search_sim3(F, Q, th, ratio, slot_query):
             s[bi] = q
             n += 1
     return n, s
+
+
+def search_for_initialization(F1, F2, prev, window=100, nn=0.9, ori=True):
+    """ORBmatcher::SearchForInitialization (ref:src/ORBmatcher.cc:735-878): (nmatches, vnMatches12, prev)."""
+    INT_MAX = 2147483647
+    n1, n2 = F1.n, F2.n
+    m12 = [-1] * n1
+    md = [INT_MAX] * n2
+    m21 = [-1] * n2
+    hist = [[] for _ in range(HISTO)]
+    nm = 0
+    for i1 in range(n1):
+        if F1.kp_octave[i1] > 0:
+            continue
+        cand = features_in_area(F2, prev[i1, 0], prev[i1, 1], float(window), 0, 0)
+        if not cand:
+            continue
+        b1 = b2 = INT_MAX
+        bi = -1
+        for i2 in cand:
+            d = dist(F1.desc[i1], F2.desc[i2])
+            if md[i2] <= d:
+                continue
+            if d < b1:
+                b1, b2, bi = d, b1, i2
+            elif d < b2:
+                b2 = d
+        if b1 <= TH_LOW and float(f32(b1)) < float(f32(f32(b2) * f32(nn))):
+            if m21[bi] >= 0:
+                m12[m21[bi]] = -1
+                nm -= 1
+            m12[i1] = bi
+            m21[bi] = i1
+            md[bi] = b1
+            nm += 1
+            if ori:
+                hist[rot_bin(F1.kp_angle[i1], F2.kp_angle[bi])].append(i1)
+    if ori:
+        keep = three_maxima([len(h) for h in hist])
+        for i in range(HISTO):
+            if i in keep:
+                continue
+            for i1 in hist[i]:
+                if m12[i1] >= 0:
+                    m12[i1] = -1
+                    nm -= 1
+    p = np.array(prev, np.float32).copy()
+    for i1 in range(n1):
+        if m12[i1] >= 0:
+            p[i1] = (F2.kp_x[m12[i1]], F2.kp_y[m12[i1]])
+    return nm, np.array(m12, np.int32), p
