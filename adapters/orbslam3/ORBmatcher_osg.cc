@@ -1,8 +1,8 @@
 // ORBmatcher_osg.cc — drop-in bodies for the ORBmatcher operators on the MI355X path, for an
 // ORB-SLAM3 tree built with -DORB_SLAM3_OSG.  The reference's
 // src/ORBmatcher.cc keeps every other member; the bodies below replace the six hot-path ones,
-// the two Fuse overloads, SearchForTriangulation and the two Sim3
-// SearchByProjection overloads
+// the two Fuse overloads, SearchForTriangulation, the two Sim3
+// SearchByProjection overloads and SearchForInitialization
 // under #ifdef ORB_SLAM3_OSG (signatures: ref:include/ORBmatcher.h:36-66).
 #include "ORBmatcher.h"
 #include "osg_hooks_orbslam3.h"
@@ -73,6 +73,13 @@ int ORBmatcher::SearchByProjection(KeyFrame *pKF, Sophus::Sim3<float> &Scw, cons
 {  // ref:src/ORBmatcher.cc:623-733
     return osg_orbslam3::search_by_projection_sim3<H, KeyFrame>(pKF, Scw, vpPoints, &vpPointsKFs, vpMatched,
                                                                &vpMatchedKF, th, ratioHamming);
+}
+
+int ORBmatcher::SearchForInitialization(Frame &F1, Frame &F2, std::vector<cv::Point2f> &vbPrevMatched,
+                                        std::vector<int> &vnMatches12, int windowSize)
+{  // ref:src/ORBmatcher.cc:735-878
+    return osg_orbslam3::search_for_initialization<H>(F1, F2, vbPrevMatched, vnMatches12, windowSize, mfNNratio,
+                                                      mbCheckOrientation);
 }
 
 }  // namespace ORB_SLAM3

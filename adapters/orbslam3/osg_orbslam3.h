@@ -621,6 +621,33 @@ int search_by_projection_sim3(KeyFrameT *pKF, const Sim3T &Scw, const std::vecto
     return nm;
 }
 
+// ---------------------------------------------------------------- b6 SearchForInitialization
+// ref:src/ORBmatcher.cc:735-878: vnMatches12 sized F1.mvKeysUn.size(), vbPrevMatched updated for the
+// surviving matches.
+template <class H, class FrameT, class PointT>
+int search_for_initialization(FrameT &F1, FrameT &F2, std::vector<PointT> &vbPrevMatched, std::vector<int> &vnMatches12,
+                              int windowSize, float nnratio, bool checkOri)
+{
+    osg_ctx *ctx = thread_ctx();
+    FrameView<FrameT> f1(F1), f2(F2);
+    const int n1 = (int)F1.mvKeysUn.size();
+    std::vector<float> prev(2 * (size_t)n1);
+    for (int i = 0; i < n1; i++) {
+        prev[2 * i] = vbPrevMatched[i].x;
+        prev[2 * i + 1] = vbPrevMatched[i].y;
+    }
+    std::vector<int32_t> m12(n1, -1);
+    const int nm = check(ctx, osg_search_for_initialization(ctx, &f1.v, &f2.v, prev.data(), windowSize, nnratio, checkOri,
+                                                            m12.data()), "osg_search_for_initialization");
+    vnMatches12.assign(m12.begin(), m12.end());
+    for (int i = 0; i < n1; i++)
+        if (m12[i] >= 0) {
+            vbPrevMatched[i].x = prev[2 * i];
+            vbPrevMatched[i].y = prev[2 * i + 1];
+        }
+    return nm;
+}
+
 // ----------------------------------------------------------------- b3 SearchForTriangulation
 // ref:src/ORBmatcher.cc:1045-1328.  vMatchedPairs = (KF1 index, KF2 index) in ascending KF1 index.
 // The epipole and the F12 matrices come from the hook (the reference's Sophus / Eigen code).

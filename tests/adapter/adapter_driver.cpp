@@ -1,7 +1,7 @@
 // adapter_driver.cpp — runs adapters/orbslam3/osg_orbslam3.h on mock ORB-SLAM3 objects built from
 // arrays written by tests/test_adapter.py, and writes the adapter's results back (test-only).
 //
-//   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba fuse fuse_sim3 triang distinct sim3 sim3_kfs
+//   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba fuse fuse_sim3 triang distinct sim3 sim3_kfs init
 //
 // Array file: repeated {u32 name_len, name, u8 dtype ('b' u8, 'i' i32, 'f' f32, 'd' f64), u64 count,
 // data}.
@@ -97,14 +97,14 @@ static void fill_grid(const Arrays &m, const std::string &pre, std::vector<std::
 
 // Frame from the FrameSoA arrays "F.*" (keypoints, descriptors, mvuRight, grid CSR, scales; for a
 // two-camera rig "F.nleft", the right grid and the stereo-partner maps)
-static void build_frame(const Arrays &m, Frame &F)
+static void build_frame(const Arrays &m, Frame &F, const std::string &P = "F.")
 {
-    const int n = (int)get(m, "F.kp_x").n;
+    const int n = (int)get(m, P + "kp_x").n;
     F.N = n;
-    F.Nleft = has(m, "F.nleft") ? get(m, "F.nleft").p<int32_t>()[0] : -1;
+    F.Nleft = has(m, P + "nleft") ? get(m, P + "nleft").p<int32_t>()[0] : -1;
     const int nl = F.Nleft == -1 ? n : F.Nleft;
-    const float *x = get(m, "F.kp_x").p<float>(), *y = get(m, "F.kp_y").p<float>(), *a = get(m, "F.kp_angle").p<float>();
-    const int32_t *o = get(m, "F.kp_octave").p<int32_t>();
+    const float *x = get(m, P + "kp_x").p<float>(), *y = get(m, P + "kp_y").p<float>(), *a = get(m, P + "kp_angle").p<float>();
+    const int32_t *o = get(m, P + "kp_octave").p<int32_t>();
     std::vector<cv::KeyPoint> kps(n);
     for (int i = 0; i < n; i++) {
         kps[i].pt.x = x[i];
@@ -116,18 +116,18 @@ static void build_frame(const Arrays &m, Frame &F)
     F.mvKeysRight.assign(kps.begin() + nl, kps.end());
     F.mvKeysUn = F.mvKeys;  // left keypoints only on a two-camera rig (ref:src/Frame.cc:1022)
     if (F.Nleft != -1) {
-        fill_grid(m, "F.", F.mGrid);
-        fill_grid(m, "F.r_", F.mGridRight);
-        const Arr &l2r = get(m, "F.left_to_right"), &r2l = get(m, "F.right_to_left");
+        fill_grid(m, P, F.mGrid);
+        fill_grid(m, P + "r_", F.mGridRight);
+        const Arr &l2r = get(m, P + "left_to_right"), &r2l = get(m, P + "right_to_left");
         F.mvLeftToRightMatch.assign(l2r.p<int32_t>(), l2r.p<int32_t>() + l2r.n);
         F.mvRightToLeftMatch.assign(r2l.p<int32_t>(), r2l.p<int32_t>() + r2l.n);
     }
     F.mDescriptors = cv::Mat(n, 32);
-    std::memcpy(F.mDescriptors.buf.data(), get(m, "F.desc").b.data(), (size_t)n * 32);
+    std::memcpy(F.mDescriptors.buf.data(), get(m, P + "desc").b.data(), (size_t)n * 32);
     F.mvuRight.assign(n, -1.0f);
-    if (has(m, "F.u_right")) std::memcpy(F.mvuRight.data(), get(m, "F.u_right").b.data(), (size_t)n * 4);
-    if (F.Nleft == -1) fill_grid(m, "F.", F.mGrid);
-    const float *sc = get(m, "F.scalars").p<float>();  // min_x max_x min_y max_y inv_w inv_h mb mbf
+    if (has(m, P + "u_right")) std::memcpy(F.mvuRight.data(), get(m, P + "u_right").b.data(), (size_t)n * 4);
+    if (F.Nleft == -1) fill_grid(m, P, F.mGrid);
+    const float *sc = get(m, P + "scalars").p<float>();  // min_x max_x min_y max_y inv_w inv_h mb mbf
     Frame::mnMinX = sc[0];
     Frame::mnMaxX = sc[1];
     Frame::mnMinY = sc[2];
@@ -136,7 +136,7 @@ static void build_frame(const Arrays &m, Frame &F)
     Frame::mfGridElementHeightInv = sc[5];
     F.mb = sc[6];
     F.mbf = sc[7];
-    const Arr &s = get(m, "F.scale");
+    const Arr &s = get(m, P + "scale");
     F.mvScaleFactors.assign(s.p<float>(), s.p<float>() + s.n);
     F.mnScaleLevels = (int)s.n;
     F.mvpMapPoints.assign(n, nullptr);
@@ -631,6 +631,28 @@ int main(int argc, char **argv)
             out["nmatches"] = make('i', std::vector<int32_t>{nm});
             out["matched"] = make('i', mo);
             out["matched_kf"] = make('i', mk);
+        } else if (mode == "init") {
+            // F1 "F.*", F2 "G.*", vbPrevMatched "V.prev" (n1 x 2); params: windowSize nnratio checkOri
+            Frame F1, F2;
+            build_frame(in, F1, "F.");
+            build_frame(in, F2, "G.");
+            const Arr &pv = get(in, "V.prev");
+            std::vector<cv::Point2f> prev(F1.N);
+            for (int i = 0; i < F1.N; i++) {
+                prev[i].x = pv.p<float>()[2 * i];
+                prev[i].y = pv.p<float>()[2 * i + 1];
+            }
+            std::vector<int> m12;
+            const int nm = osg_orbslam3::search_for_initialization<MockHooks>(F1, F2, prev, m12, (int)prm[0], prm[1],
+                                                                               prm[2] != 0);
+            std::vector<float> po(2 * (size_t)F1.N);
+            for (int i = 0; i < F1.N; i++) {
+                po[2 * i] = prev[i].x;
+                po[2 * i + 1] = prev[i].y;
+            }
+            out["nmatches"] = make('i', std::vector<int32_t>{nm});
+            out["m12"] = make('i', std::vector<int32_t>(m12.begin(), m12.end()));
+            out["prev"] = make('f', po);
         } else if (mode == "distinct") {
             // keyframes: "K.desc" (nk x nkp rows), "K.bad"; MapPoints: "M.bad", "M.desc" (initial);
             // observations CSR "O.start" / "O.kf" / "O.left" / "O.right"

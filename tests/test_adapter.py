@@ -555,3 +555,16 @@ def test_adapter_search_by_projection_sim3(driver, tmp_path, oracle, with_kfs):
         wk = np.full(F.n, -1, np.int32)
         wk[sq >= 0] = sq[sq >= 0] % 7
         np.testing.assert_array_equal(out["matched_kf"], wk)
+
+
+@pytest.mark.gpu
+def test_adapter_search_for_initialization(driver, tmp_path, oracle):
+    """SearchForInitialization through the adapter: Frame gather, vbPrevMatched in / out as cv::Point2f."""
+    F1, F2, prev = fr.synth_init_pair(np.random.default_rng(810), n1=1500, n2=1500)
+    g = {("G." + k[2:]): v for k, v in frame_arrays(F2).items()}
+    out = run(driver, tmp_path, "init", {**frame_arrays(F1), **g, "V.prev": prev.reshape(-1),
+                                         "params": np.array([100, 0.9, 1], np.float32)})
+    n, m12, p = oc.initialization(oracle, F1, F2, prev, 100, 0.9, True)
+    assert n > 100 and int(out["nmatches"][0]) == n
+    np.testing.assert_array_equal(out["m12"], m12)
+    np.testing.assert_array_equal(out["prev"].reshape(-1, 2), p)
