@@ -4,6 +4,7 @@ C oracle on one host thread (bounded samples).  python tools/widen_bench.py
   triang    SearchForTriangulation, 1200 x 1200 keypoints, batches of B keyframe pairs
   sim3      SearchByProjection(KeyFrame*, Sim3f&, ...), 1200 keypoints, 3000 / 9000 MapPoints (th 8, 1.5)
   distinct  ComputeDistinctiveDescriptors, 1000 / 100 000 MapPoints, N ~ U{1..30} rows
+  init      SearchForInitialization, 2 x 2000 keypoints, windowSize 100, nnratio 0.9
 """
 import os
 import sys
@@ -60,6 +61,16 @@ def main():
         c = cpu(lambda i: oc.distinctive(o, desc, start), 1 if n > 1000 else 10)
         print(f"distinct n={n:6d}  kernel {k * 1e3:9.2f} us ({k * 1e6 / n:7.1f} ns/point)  oracle {c * 1e3:10.1f} us",
               flush=True)
+    init_bench(ctx, o)
+
+
+def init_bench(ctx, o):
+    rng = np.random.default_rng(12)
+    F1, F2, prev = fr.synth_init_pair(rng)
+    m = ORBmatcher(ctx, nnratio=0.9)
+    k = best_of(lambda: m.SearchForInitialization(F1, F2, prev.copy(), 100), ctx)
+    c = cpu(lambda i: oc.initialization(o, F1, F2, prev, 100, 0.9, True), 10)
+    print(f"init     2000x2000  kernel {k * 1e3:8.2f} us  oracle {c * 1e3:8.2f} us", flush=True)
 
 
 if __name__ == "__main__":
