@@ -57,13 +57,41 @@ def test_oracle_hand_case(oracle):
 @pytest.mark.parametrize("seed", range(3))
 @pytest.mark.parametrize("window,ori", [(100, True), (50, True), (100, False)])
 def test_gpu_vs_oracle(ctx, oracle, seed, window, ori):
-    """Monocular initialisation shape: 2 x 2000 keypoints (2x features), windowSize 100, nnratio 0.9."""
-    F1, F2, prev = fr.synth_init_pair(np.random.default_rng(9600 + seed))
+    """Monocular initialisation shape: 2 x 5000 keypoints (the 5 x nFeatures initialisation extractor,
+    ref:src/Tracking.cc:667), ~22 % at level 0, windowSize 100, nnratio 0.9 (ref:src/Tracking.cc:2951)."""
+    F1, F2, prev = fr.synth_init_pair(np.random.default_rng(9600 + seed), n1=5000, n2=5000, level0=0.22)
     ref = oc.initialization(oracle, F1, F2, prev, window, 0.9, ori)
     p = prev.copy()
     n, m12 = ORBmatcher(ctx, nnratio=0.9, checkOri=ori).SearchForInitialization(F1, F2, p, window)
     same((n, m12, p), ref)
     assert n > 200
+    st = ctx.match_last_stats()
+    assert st["rounds"] >= 2 and not st["serial"]  # the fixed point ran (and resolved steals)
+
+
+@pytest.mark.gpu
+def test_gpu_serial_paths(ctx, oracle):
+    """The one-wave sequential walk: (a) more level-0 F2 keypoints than the claim tables hold; (b) a
+    pile-up of 12 F1 keypoints stealing one F2 keypoint in turn (claim-list overflow)."""
+    m = ORBmatcher(ctx, nnratio=0.9)
+    F1, F2, prev = fr.synth_init_pair(np.random.default_rng(9800), n1=3000, n2=6000, level0=1.0)
+    ref = oc.initialization(oracle, F1, F2, prev, 100, 0.9, True)
+    p = prev.copy()
+    same((*m.SearchForInitialization(F1, F2, p, 100), p), ref)
+    assert ctx.match_last_stats()["serial"]
+    # (b): F1 keypoint k has a copy of F2 0's descriptor with 12 - k flipped bits
+    d2 = np.stack([bits(0), bits(200)])
+    d1 = np.stack([bits(12 - k) for k in range(12)])
+    F1 = fr.FrameSoA(desc=d1, kp_x=np.full(12, 100, np.float32), kp_y=np.full(12, 100, np.float32),
+                     kp_angle=np.zeros(12, np.float32), kp_octave=np.zeros(12, np.int32))
+    F2 = fr.FrameSoA(desc=d2, kp_x=np.array([100, 110], np.float32), kp_y=np.array([100, 100], np.float32),
+                     kp_angle=np.zeros(2, np.float32), kp_octave=np.zeros(2, np.int32))
+    prev = np.stack([F1.kp_x, F1.kp_y], axis=1).astype(np.float32)
+    ref = oc.initialization(oracle, F1, F2, prev, 100, 0.9, True)
+    p = prev.copy()
+    same((*m.SearchForInitialization(F1, F2, p, 100), p), ref)
+    assert ref[1].tolist() == [-1] * 11 + [0]
+    assert ctx.match_last_stats()["serial"]
 
 
 @pytest.mark.gpu

@@ -4,7 +4,7 @@ C oracle on one host thread (bounded samples).  python tools/widen_bench.py
   triang    SearchForTriangulation, 1200 x 1200 keypoints, batches of B keyframe pairs
   sim3      SearchByProjection(KeyFrame*, Sim3f&, ...), 1200 keypoints, 3000 / 9000 MapPoints (th 8, 1.5)
   distinct  ComputeDistinctiveDescriptors, 1000 / 100 000 MapPoints, N ~ U{1..30} rows
-  init      SearchForInitialization, 2 x 2000 keypoints, windowSize 100, nnratio 0.9
+  init      SearchForInitialization, 2 x 5000 keypoints (22 % level 0), windowSize 100, nnratio 0.9
 """
 import os
 import sys
@@ -66,11 +66,12 @@ def main():
 
 def init_bench(ctx, o):
     rng = np.random.default_rng(12)
-    F1, F2, prev = fr.synth_init_pair(rng)
+    F1, F2, prev = fr.synth_init_pair(rng, n1=5000, n2=5000, level0=0.22)
     m = ORBmatcher(ctx, nnratio=0.9)
     k = best_of(lambda: m.SearchForInitialization(F1, F2, prev.copy(), 100), ctx)
+    st = ctx.match_last_stats()
     c = cpu(lambda i: oc.initialization(o, F1, F2, prev, 100, 0.9, True), 10)
-    print(f"init     2000x2000  kernel {k * 1e3:8.2f} us  oracle {c * 1e3:8.2f} us", flush=True)
+    print(f"init     5000x5000  kernel {k * 1e3:8.2f} us  rounds {st['rounds']}  oracle {c * 1e3:8.2f} us", flush=True)
 
 
 if __name__ == "__main__":
