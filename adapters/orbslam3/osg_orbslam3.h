@@ -648,6 +648,75 @@ int search_for_initialization(FrameT &F1, FrameT &F2, std::vector<PointT> &vbPre
     return nm;
 }
 
+// ------------------------------------------------------------------ b7 ComputeStereoMatches
+// ref:src/Frame.cc:1117-1373, called by the stereo Frame constructor (ref:src/Frame.cc:165).  Reads
+// mvKeys / mvKeysRight, mDescriptors / mDescriptorsRight, mvScaleFactors / mvInvScaleFactors, mb,
+// mbf and both ORBextractors' mvImagePyramid (ROI views: the row step comes from Mat::step[0]);
+// writes mvuRight and mvDepth.  Returns the matches kept.
+template <class MatT>
+struct PyramidView {
+    std::vector<const uint8_t *> data;
+    std::vector<int32_t> rows, cols, step;
+    osg_image_pyramid v{};
+
+    PyramidView(const std::vector<MatT> &pyr, int n_levels)
+    {
+        for (int l = 0; l < n_levels; l++) {
+            data.push_back(pyr[l].template ptr<unsigned char>(0));
+            rows.push_back(pyr[l].rows);
+            cols.push_back(pyr[l].cols);
+            step.push_back((int32_t)pyr[l].step[0]);
+        }
+        v.n_levels = n_levels;
+        v.on_device = 0;
+        v.data = data.data();
+        v.rows = rows.data();
+        v.cols = cols.data();
+        v.step = step.data();
+    }
+};
+
+template <class FrameT>
+int compute_stereo_matches(FrameT &F)
+{
+    osg_ctx *ctx = thread_ctx();
+    const int n = F.N, nr = (int)F.mvKeysRight.size();
+    std::vector<float> x, y, xr, yr, ang;
+    std::vector<int32_t> o, orr;
+    for (int i = 0; i < n; i++) push_kp(F.mvKeys[i], x, y, ang, o);
+    for (int i = 0; i < nr; i++) push_kp(F.mvKeysRight[i], xr, yr, ang, orr);
+    std::vector<uint8_t> dl, dr;
+    copy_desc_rows(F.mDescriptors, n, dl);
+    copy_desc_rows(F.mDescriptorsRight, nr, dr);
+    std::vector<float> sc(F.mvScaleFactors.begin(), F.mvScaleFactors.end());
+    std::vector<float> isc(F.mvInvScaleFactors.begin(), F.mvInvScaleFactors.end());
+    const int levels = (int)sc.size();
+    using MatT = typename std::decay<decltype(F.mpORBextractorLeft->mvImagePyramid[0])>::type;
+    PyramidView<MatT> pl(F.mpORBextractorLeft->mvImagePyramid, levels), pr(F.mpORBextractorRight->mvImagePyramid, levels);
+    osg_stereo_frame s{};
+    s.n = n;
+    s.x = x.data();
+    s.y = y.data();
+    s.octave = o.data();
+    s.desc = dl.data();
+    s.n_right = nr;
+    s.xr = xr.data();
+    s.yr = yr.data();
+    s.octave_r = orr.data();
+    s.desc_r = dr.data();
+    s.scale_factors = sc.data();
+    s.inv_scale_factors = isc.data();
+    s.n_levels = levels;
+    s.mb = F.mb;
+    s.mbf = F.mbf;
+    s.left = pl.v;
+    s.right = pr.v;
+    F.mvuRight.assign(n, -1.0f);  // :1134-1135
+    F.mvDepth.assign(n, -1.0f);
+    return check(ctx, osg_compute_stereo_matches(ctx, &s, F.mvuRight.data(), F.mvDepth.data()),
+                 "osg_compute_stereo_matches");
+}
+
 // ----------------------------------------------------------------- b3 SearchForTriangulation
 // ref:src/ORBmatcher.cc:1045-1328.  vMatchedPairs = (KF1 index, KF2 index) in ascending KF1 index.
 // The epipole and the F12 matrices come from the hook (the reference's Sophus / Eigen code).

@@ -213,6 +213,7 @@ def main():
         out["frames_c3"] = bench_c3(ctx, rank, world, dist, dev, args)
         out["frames_c5"] = bench_c5(ctx, rank, world, dist, dev, args)
         out["frames_dbow"] = bench_dbow(ctx, rank, world, dist, dev, args)
+        out["frames_stereo"] = bench_stereo(ctx, rank, world, dist, dev, args)
 
     # ---- LocalBA iters/s on C4 (50 KF x 10k points), the second half of the metric ----------
     if not args.no_ba:
@@ -463,6 +464,31 @@ def bench_dbow(ctx, rank, world, dist, dev, args):
     gv.transform_batch(sets[:1], 4)
     res["single_frame_kernel_us"] = round(ctx.last_kernel_ms() * 1e3, 2)
     gv.close()
+    return res
+
+
+def bench_stereo(ctx, rank, world, dist, dev, args):
+    """SURVEY.md §8(f) rank 3: Frame::ComputeStereoMatches on EuRoC-shaped stereo pairs (752 x 480,
+    8 levels x 1.2, 1200 keypoints per side; seeded synthetic scene, no EuRoC images in the
+    container), B frames per launch, both image pyramids resident in HBM."""
+    from orb_slam3_comments_ghr_amd import stereo as st
+    n_pool = 16
+    rng = np.random.default_rng(0x0B5EED20 + rank)
+    pool = [st.synth_stereo_frame(rng, n=1200) for _ in range(n_pool)]
+    dpool = [f.to_device(dev) for f in pool]
+    B = args.frames
+    frames = [dpool[i % n_pool] for i in range(B)]
+
+    def cpu(i):  # the cpu_baseline leg: the oracle restatement, 1 thread
+        oracle, oc = _oracle()
+        oc.stereo(oracle, pool[i])
+
+    res = _frame_batches(ctx, rank, world, dist, dev, args, [lambda: st.ComputeStereoMatchesBatch(ctx, frames)], cpu,
+                         ["ComputeStereoMatches"],
+                         f"ComputeStereoMatches: EuRoC-shaped 752x480 stereo pairs, 8 levels, 1200 keypoints per "
+                         f"side, pyramids in HBM; {B} frames per launch", n_pool)
+    st.ComputeStereoMatchesBatch(ctx, frames[:1])
+    res["single_frame_kernel_us"] = round(ctx.last_kernel_ms() * 1e3, 2)
     return res
 
 

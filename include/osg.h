@@ -281,6 +281,48 @@ int osg_fuse_search(osg_ctx *ctx, const osg_frame *KF, const osg_fuse_queries *Q
 int osg_fuse_search_batch(osg_ctx *ctx, const osg_frame *KF, const osg_fuse_queries *Q, int32_t B, float th,
                           int right, int gated, int32_t *best_idx, int32_t *best_dist, int32_t *nfused);
 
+/* ---- b7: Frame::ComputeStereoMatches -------------------------------------------------------------
+ * ref:src/Frame.cc:1117-1373 (rectified stereo: the Frame constructor, ref:src/Frame.cc:165).  For
+ * every left keypoint: the right keypoints listed on its row (vRowIndices: each right keypoint on
+ * rows floor(y - 2 s) .. ceil(y + 2 s), s = mvScaleFactors[octave]), octave within +-1, uR inside
+ * [uL - mbf / mb, uL]; the first minimum DescriptorDistance below TH_HIGH, accepted below
+ * (TH_HIGH + TH_LOW) / 2; then the 11 x 11 SAD (cv::NORM_L1) over incR = -5..5 at the keypoint's
+ * pyramid level, the parabola fit, the disparity range test, and finally the removal of every
+ * match whose SAD is >= 1.5 * 1.4 * the median SAD.  Outputs mvuRight / mvDepth (-1 = none).
+ * Images: the ORBextractor pyramids (mvImagePyramid[level], 8-bit, `step` bytes per row).  The
+ * SAD patches must lie inside the level image: the reference's colRange/rowRange throw otherwise
+ * (ORBextractor keeps keypoints EDGE_THRESHOLD = 19 px from the border, so they do); a keypoint
+ * whose patch would leave the image gets no match here. */
+typedef struct osg_image_pyramid {
+    int32_t n_levels;
+    int32_t on_device;            /* 1: data[l] are device addresses, read in place (rows / cols / step
+                                     stay host arrays); 0: host images, packed and uploaded per call */
+    const uint8_t *const *data;   /* per level: the top-left pixel */
+    const int32_t *rows, *cols, *step;  /* step: bytes per row (>= cols) */
+} osg_image_pyramid;
+
+typedef struct osg_stereo_frame {
+    int32_t n;                    /* left keypoints (mvKeys) */
+    const float *x, *y;
+    const int32_t *octave;
+    const uint8_t *desc;          /* n x 32 (mDescriptors) */
+    int32_t n_right;              /* mvKeysRight */
+    const float *xr, *yr;
+    const int32_t *octave_r;
+    const uint8_t *desc_r;        /* n_right x 32 (mDescriptorsRight) */
+    const float *scale_factors;   /* mvScaleFactors */
+    const float *inv_scale_factors; /* mvInvScaleFactors */
+    int32_t n_levels;
+    float mb, mbf;
+    osg_image_pyramid left, right;
+} osg_stereo_frame;
+
+/* u_right[n], depth[n] out.  Returns the matches kept (accepted, then not removed by the median cut). */
+int osg_compute_stereo_matches(osg_ctx *ctx, const osg_stereo_frame *F, float *u_right, float *depth);
+/* B frames in one launch; outputs concatenated by F[b].n; nmatches[b] per frame. */
+int osg_compute_stereo_matches_batch(osg_ctx *ctx, const osg_stereo_frame *F, int32_t B, float *u_right,
+                                     float *depth, int32_t *nmatches);
+
 /* ---- b6: SearchForInitialization ------------------------------------------------------------------
  * ORBmatcher::SearchForInitialization(Frame &F1, Frame &F2, vector<cv::Point2f> &vbPrevMatched,
  * vector<int> &vnMatches12, windowSize)  ref:src/ORBmatcher.cc:735-878 (monocular initialisation,

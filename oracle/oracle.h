@@ -49,6 +49,8 @@ void oracle_compute_distinctive_descriptors(const uint8_t *desc, const int32_t *
 /* SearchForTriangulation (oracle_triang.c) */
 int oracle_search_for_triangulation(const osg_kf_side *K1, const osg_kf_side *K2, const osg_triang_geom *G,
                                     int bOnlyStereo, int bCoarse, int checkOri, int32_t *vMatches12);
+/* Frame::ComputeStereoMatches (oracle_stereo.c): mvuRight / mvDepth out, returns the kept matches */
+int oracle_compute_stereo_matches(const osg_stereo_frame *F, float *mvuRight, float *mvDepth);
 void oracle_dbow_transform_batch(const osg_vocabulary_desc *V, const uint8_t *desc, const int32_t *n, int B,
                                  int levelsup, osg_bow_out *out);
 

@@ -103,6 +103,18 @@ class OsgTriangGeom(C.Structure):
     _fields_ = [("ep_x", f32), ("ep_y", f32), ("F12", f32 * 36), ("pinhole", i32)]
 
 
+class OsgImagePyramid(C.Structure):
+    _fields_ = [("n_levels", i32), ("on_device", i32), ("data", P), ("rows", P), ("cols", P), ("step", P)]
+
+
+class OsgStereoFrame(C.Structure):
+    _fields_ = [
+        ("n", i32), ("x", P), ("y", P), ("octave", P), ("desc", P), ("n_right", i32), ("xr", P), ("yr", P),
+        ("octave_r", P), ("desc_r", P), ("scale_factors", P), ("inv_scale_factors", P), ("n_levels", i32),
+        ("mb", f32), ("mbf", f32), ("left", OsgImagePyramid), ("right", OsgImagePyramid),
+    ]
+
+
 class OsgCamera(C.Structure):
     _fields_ = [
         ("type", i32), ("p", f32 * 8), ("fx", f32), ("fy", f32), ("cx", f32), ("cy", f32),
@@ -171,6 +183,7 @@ EXPORTS = [
     "osg_compute_distinctive_descriptors", "osg_compute_distinctive_descriptors_dev",
     "osg_search_by_projection_sim3", "osg_search_by_projection_sim3_batch",
     "osg_search_for_initialization", "osg_search_for_initialization_batch",
+    "osg_compute_stereo_matches", "osg_compute_stereo_matches_batch",
 ]
 
 
@@ -233,6 +246,8 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.osg_search_for_initialization.argtypes = [vp, C.POINTER(OsgFrame), C.POINTER(OsgFrame), vp, C.c_int, f32,
                                                   C.c_int, vp]
     lib.osg_search_for_initialization_batch.argtypes = [vp, vp, vp, i32, vp, C.c_int, f32, C.c_int, vp, vp]
+    lib.osg_compute_stereo_matches.argtypes = [vp, C.POINTER(OsgStereoFrame), vp, vp]
+    lib.osg_compute_stereo_matches_batch.argtypes = [vp, vp, i32, vp, vp, vp]
     lib.osg_compute_distinctive_descriptors.argtypes = [vp, vp, vp, i32, vp]
     lib.osg_compute_distinctive_descriptors_dev.argtypes = [vp, vp, vp, i32, vp]
     lib.osg_search_for_triangulation_batch.argtypes = [vp, vp, vp, vp, i32, C.c_int, C.c_int, C.c_int, vp, vp]

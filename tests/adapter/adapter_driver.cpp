@@ -1,7 +1,7 @@
 // adapter_driver.cpp — runs adapters/orbslam3/osg_orbslam3.h on mock ORB-SLAM3 objects built from
 // arrays written by tests/test_adapter.py, and writes the adapter's results back (test-only).
 //
-//   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba fuse fuse_sim3 triang distinct sim3 sim3_kfs init
+//   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba fuse fuse_sim3 triang distinct sim3 sim3_kfs init stereo
 //
 // Array file: repeated {u32 name_len, name, u8 dtype ('b' u8, 'i' i32, 'f' f32, 'd' f64), u64 count,
 // data}.
@@ -653,6 +653,55 @@ int main(int argc, char **argv)
             out["nmatches"] = make('i', std::vector<int32_t>{nm});
             out["m12"] = make('i', std::vector<int32_t>(m12.begin(), m12.end()));
             out["prev"] = make('f', po);
+        } else if (mode == "stereo") {
+            // left "S.x/y/oct/desc", right "S.xr/yr/oct_r/desc_r", "S.scale", "S.inv_scale", "S.mb_mbf";
+            // pyramids "PL.img" / "PR.img" (levels concatenated) with "PL.dims" / "PR.dims" (rows, cols)
+            // held as ROIs of wider rows (step = cols + 7), as ORBextractor's bordered levels are
+            Frame F;
+            const int n = (int)get(in, "S.x").n, nr = (int)get(in, "S.xr").n;
+            F.N = n;
+            auto kps = [&](const char *x, const char *y, const char *o, int cnt) {
+                std::vector<cv::KeyPoint> v(cnt);
+                for (int i = 0; i < cnt; i++) {
+                    v[i].pt.x = get(in, x).p<float>()[i];
+                    v[i].pt.y = get(in, y).p<float>()[i];
+                    v[i].octave = get(in, o).p<int32_t>()[i];
+                }
+                return v;
+            };
+            F.mvKeys = kps("S.x", "S.y", "S.oct", n);
+            F.mvKeysRight = kps("S.xr", "S.yr", "S.oct_r", nr);
+            F.mDescriptors = cv::Mat(n, 32);
+            std::memcpy(F.mDescriptors.buf.data(), get(in, "S.desc").b.data(), (size_t)n * 32);
+            F.mDescriptorsRight = cv::Mat(nr, 32);
+            std::memcpy(F.mDescriptorsRight.buf.data(), get(in, "S.desc_r").b.data(), (size_t)nr * 32);
+            const Arr &sc = get(in, "S.scale"), &isc = get(in, "S.inv_scale");
+            F.mvScaleFactors.assign(sc.p<float>(), sc.p<float>() + sc.n);
+            F.mvInvScaleFactors.assign(isc.p<float>(), isc.p<float>() + isc.n);
+            F.mnScaleLevels = (int)sc.n;
+            F.mb = get(in, "S.mb_mbf").p<float>()[0];
+            F.mbf = get(in, "S.mb_mbf").p<float>()[1];
+            ORBextractor el, er;
+            auto pyr = [&](const char *img, const char *dims, ORBextractor &e) {
+                const uint8_t *src = get(in, img).p<uint8_t>();
+                const int32_t *d = get(in, dims).p<int32_t>();
+                for (size_t l = 0; l < sc.n; l++) {
+                    const int rows = d[2 * l], cols = d[2 * l + 1];
+                    cv::Mat m(rows, cols, (size_t)cols + 7);
+                    for (int r = 0; r < rows; r++) std::memcpy(m.ptr<unsigned char>(r), src + (size_t)r * cols, cols);
+                    src += (size_t)rows * cols;
+                    e.mvImagePyramid.push_back(std::move(m));
+                }
+            };
+            pyr("PL.img", "PL.dims", el);
+            pyr("PR.img", "PR.dims", er);
+            F.mpORBextractorLeft = &el;
+            F.mpORBextractorRight = &er;
+            F.mvuRight.assign(n, 123.0f);  // overwritten, as the reference's are
+            const int nm = osg_orbslam3::compute_stereo_matches(F);
+            out["nmatches"] = make('i', std::vector<int32_t>{nm});
+            out["ur"] = make('f', F.mvuRight);
+            out["depth"] = make('f', F.mvDepth);
         } else if (mode == "distinct") {
             // keyframes: "K.desc" (nk x nkp rows), "K.bad"; MapPoints: "M.bad", "M.desc" (initial);
             // observations CSR "O.start" / "O.kf" / "O.left" / "O.right"

@@ -24,15 +24,17 @@ struct KeyPoint {
     float size = 0, angle = 0, response = 0;
     int octave = 0, class_id = -1;
 };
-struct Mat {  // CV_8UC1 rows x cols
+struct Mat {  // CV_8UC1 rows x cols, step[0] bytes per row (an ROI of a wider buffer when > cols)
     int rows = 0, cols = 0;
     std::vector<unsigned char> buf;
+    size_t step[2] = {0, 1};
     Mat() = default;
-    Mat(int r, int c) : rows(r), cols(c), buf((size_t)r * c) {}
+    Mat(int r, int c) : rows(r), cols(c), buf((size_t)r * c), step{(size_t)c, 1} {}
+    Mat(int r, int c, size_t s) : rows(r), cols(c), buf((size_t)r * s), step{s, 1} {}
     template <class T>
-    T *ptr(int i) { return reinterpret_cast<T *>(buf.data() + (size_t)i * cols); }
+    T *ptr(int i) { return reinterpret_cast<T *>(buf.data() + (size_t)i * step[0]); }
     template <class T>
-    const T *ptr(int i) const { return reinterpret_cast<const T *>(buf.data() + (size_t)i * cols); }
+    const T *ptr(int i) const { return reinterpret_cast<const T *>(buf.data() + (size_t)i * step[0]); }
 };
 }  // namespace cv
 
@@ -80,11 +82,16 @@ struct MapPoint {
     void Replace(MapPoint *p);
 };
 
+struct ORBextractor {
+    std::vector<cv::Mat> mvImagePyramid;
+};
+
 struct Frame {
     int N = 0, Nleft = -1;
     std::vector<cv::KeyPoint> mvKeys, mvKeysUn, mvKeysRight;
-    cv::Mat mDescriptors;
-    std::vector<float> mvuRight;
+    cv::Mat mDescriptors, mDescriptorsRight;
+    std::vector<float> mvuRight, mvDepth, mvInvScaleFactors;
+    ORBextractor *mpORBextractorLeft = nullptr, *mpORBextractorRight = nullptr;
     std::vector<MapPoint *> mvpMapPoints;
     std::vector<bool> mvbOutlier;
     std::vector<std::size_t> mGrid[OSG_GRID_COLS][OSG_GRID_ROWS];

@@ -568,3 +568,29 @@ def test_adapter_search_for_initialization(driver, tmp_path, oracle):
     assert n > 100 and int(out["nmatches"][0]) == n
     np.testing.assert_array_equal(out["m12"], m12)
     np.testing.assert_array_equal(out["prev"].reshape(-1, 2), p)
+
+
+def stereo_arrays(F):
+    def dims(P):
+        return np.array([[lv.shape[0], lv.shape[1]] for lv in P.levels], np.int32).reshape(-1)
+
+    def img(P):
+        return np.concatenate([np.ascontiguousarray(lv).reshape(-1) for lv in P.levels])
+
+    return {"S.x": F.x, "S.y": F.y, "S.oct": F.octave, "S.desc": F.desc.reshape(-1), "S.xr": F.xr, "S.yr": F.yr,
+            "S.oct_r": F.octave_r, "S.desc_r": F.desc_r.reshape(-1), "S.scale": F.scale, "S.inv_scale": F.inv_scale,
+            "S.mb_mbf": np.array([F.mb, F.mbf], np.float32), "PL.img": img(F.left), "PL.dims": dims(F.left),
+            "PR.img": img(F.right), "PR.dims": dims(F.right)}
+
+
+@pytest.mark.gpu
+def test_adapter_compute_stereo_matches(driver, tmp_path, oracle):
+    """Frame::ComputeStereoMatches through the adapter: Frame members gathered (pyramid levels as ROIs
+    with a row step), mvuRight / mvDepth written back; the oracle's values bit for bit."""
+    from orb_slam3_comments_ghr_amd import stereo as st
+    F = st.synth_stereo_frame(np.random.default_rng(820), n=1200)
+    out = run(driver, tmp_path, "stereo", stereo_arrays(F))
+    ur, d, n = oc.stereo(oracle, F)
+    assert n > 500 and int(out["nmatches"][0]) == n
+    np.testing.assert_array_equal(out["ur"].view(np.int32), ur.view(np.int32))
+    np.testing.assert_array_equal(out["depth"].view(np.int32), d.view(np.int32))

@@ -5,6 +5,7 @@ C oracle on one host thread (bounded samples).  python tools/widen_bench.py
   sim3      SearchByProjection(KeyFrame*, Sim3f&, ...), 1200 keypoints, 3000 / 9000 MapPoints (th 8, 1.5)
   distinct  ComputeDistinctiveDescriptors, 1000 / 100 000 MapPoints, N ~ U{1..30} rows
   init      SearchForInitialization, 2 x 5000 keypoints (22 % level 0), windowSize 100, nnratio 0.9
+  stereo    ComputeStereoMatches, EuRoC 752 x 480 x 8 levels, 1200 keypoints per side (`... stereo` alone)
 """
 import os
 import sys
@@ -34,9 +35,35 @@ def cpu(fn, n):
     return (time.perf_counter() - t) / n * 1e3
 
 
+def stereo_bench(ctx, o):
+    """ComputeStereoMatches, EuRoC stereo 752 x 480, 8 levels, 1200 keypoints per side."""
+    from orb_slam3_comments_ghr_amd import stereo as st
+    rng = np.random.default_rng(13)
+    pool = [st.synth_stereo_frame(rng, n=1200) for _ in range(16)]
+    dev = [f.to_device() for f in pool]
+    for B in (1, 16, 256, 1024):
+        frames = [dev[i % 16] for i in range(B)]
+        k = best_of(lambda: st.ComputeStereoMatchesBatch(ctx, frames), ctx)
+        t = time.perf_counter()
+        st.ComputeStereoMatchesBatch(ctx, frames)
+        w = time.perf_counter() - t
+        print(f"stereo   B={B:4d}  kernel {k * 1e3 / B:8.2f} us/frame  wall {w * 1e6 / B:8.1f} us/frame "
+              f"(pyramids in HBM)", flush=True)
+    k = best_of(lambda: st.ComputeStereoMatchesBatch(ctx, pool), ctx)
+    t = time.perf_counter()
+    st.ComputeStereoMatchesBatch(ctx, pool)
+    w = time.perf_counter() - t
+    print(f"stereo   B=  16  kernel {k * 1e3 / 16:8.2f} us/frame  wall {w * 1e6 / 16:8.1f} us/frame "
+          f"(host pyramids packed + uploaded)", flush=True)
+    c = cpu(lambda i: oc.stereo(o, pool[i % 16]), 48)
+    print(f"stereo   oracle {c * 1e3:8.2f} us/frame (1 thread)", flush=True)
+
+
 def main():
     ctx = Context(0)
     o = oc.load()
+    if sys.argv[1:] == ["stereo"]:
+        return stereo_bench(ctx, o)
     m = ORBmatcher(ctx)
     rng = np.random.default_rng(11)
     pairs = [fr.synth_triang_pair(rng, n1=1200, n2=1200, forward=bool(i % 2)) for i in range(8)]
@@ -62,6 +89,7 @@ def main():
         print(f"distinct n={n:6d}  kernel {k * 1e3:9.2f} us ({k * 1e6 / n:7.1f} ns/point)  oracle {c * 1e3:10.1f} us",
               flush=True)
     init_bench(ctx, o)
+    stereo_bench(ctx, o)
 
 
 def init_bench(ctx, o):
