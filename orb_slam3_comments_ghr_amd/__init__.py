@@ -32,6 +32,7 @@ def load_library() -> C.CDLL:
             raise OsgError(
                 f"{LIB_PATH} is missing: build it with `make` (hipcc --offload-arch=gfx950); "
                 "there is no CPU fallback for the hot path")
+        _torch_device_first()
         _lib = _abi.declare(C.CDLL(LIB_PATH))
     return _lib
 
@@ -45,6 +46,20 @@ def _ptr(a) -> int | None:
         return int(a.data_ptr())
     assert isinstance(a, np.ndarray) and a.flags["C_CONTIGUOUS"], "need a C-contiguous ndarray"
     return int(a.ctypes.data)
+
+
+def _torch_device_first():
+    """torch ships its own libamdhip64 (same soname as /opt/rocm's).  Measured on the MI355X box: when
+    the library's HIP runtime is loaded or initialised before torch's, torch reports no GPU for the
+    rest of the process (and the other way round the library does); when torch is imported and
+    initialised first, both share torch's runtime and device tensors pass through the ABI (bench.py's
+    order).  So the library is loaded after torch has opened the device."""
+    try:
+        import torch
+    except ImportError:
+        return
+    if torch.cuda.is_available():
+        torch.cuda.init()
 
 
 class Context:
