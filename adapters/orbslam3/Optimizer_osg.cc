@@ -1,5 +1,5 @@
-// Optimizer_osg.cc — drop-in bodies for Optimizer::PoseOptimization and the g2o part of
-// Optimizer::LocalBundleAdjustment on the MI355X path (ORB-SLAM3 tree built with -DORB_SLAM3_OSG;
+// Optimizer_osg.cc — drop-in bodies for Optimizer::PoseOptimization, the g2o part of
+// Optimizer::LocalBundleAdjustment and Optimizer::BundleAdjustment (global BA) on the MI355X path (ORB-SLAM3 tree built with -DORB_SLAM3_OSG;
 // see INTEGRATION.md).  Signatures: ref:include/Optimizer.h:54-90.
 #include "Optimizer.h"
 #include "osg_hooks_orbslam3.h"
@@ -32,6 +32,15 @@ void OsgLocalBundleAdjustmentTail(KeyFrame *pKF, bool *pbStopFlag, Map *pMap,
     std::unique_lock<std::mutex> lock(pMap->mMutexMapUpdate);  // ref:src/Optimizer.cc:2171
     osg_orbslam3::apply_local_bundle_adjustment<OsgHooks>(out);
     pMap->IncreaseChangeIndex();
+}
+
+void Optimizer::BundleAdjustment(const std::vector<KeyFrame *> &vpKFs, const std::vector<MapPoint *> &vpMP,
+                                 int nIterations, bool *pbStopFlag, const unsigned long nLoopKF, const bool bRobust)
+{  // ref:src/Optimizer.cc:2850-3237 (GlobalBundleAdjustemnt, :2831-2839, passes the whole map)
+    Map *pMap = vpKFs[0]->GetMap();
+    auto out = osg_orbslam3::bundle_adjustment<OsgHooks>(vpKFs, vpMP, pMap->GetInitKFid(), nIterations, pbStopFlag,
+                                                         bRobust);
+    osg_orbslam3::apply_bundle_adjustment<OsgHooks>(out, nLoopKF, nLoopKF == pMap->GetOriginKF()->mnId);
 }
 
 }  // namespace ORB_SLAM3

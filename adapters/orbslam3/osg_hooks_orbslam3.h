@@ -37,6 +37,17 @@ struct OsgHooks {
         p->SetWorldPos(Eigen::Vector3d(x[0], x[1], x[2]).cast<float>());
         p->UpdateNormalAndDepth();
     }
+    static void set_gba_pose(KeyFrame &k, const double q[7], unsigned long nLoopKF)
+    {  // ref:src/Optimizer.cc:3144-3145: SE3d(SE3quat.rotation(), SE3quat.translation()).cast<float>()
+        const Eigen::Quaterniond qd(q[3], q[0], q[1], q[2]);
+        k.mTcwGBA = Sophus::SE3d(qd, Eigen::Vector3d(q[4], q[5], q[6])).cast<float>();
+        k.mnBAGlobalForKF = nLoopKF;
+    }
+    static void set_gba_pos(MapPoint *p, const double x[3], unsigned long nLoopKF)
+    {  // ref:src/Optimizer.cc:3233-3234
+        p->mPosGBA = Eigen::Vector3d(x[0], x[1], x[2]).cast<float>();
+        p->mnBAGlobalForKF = nLoopKF;
+    }
     template <class T>
     static void camera(const T &o, bool right, osg_camera &c)
     {

@@ -20,10 +20,13 @@
 //   static bool  H::kf_query(const Frame& CF, MapPoint*, float& u, float& v, int& level)
 //                ref:src/ORBmatcher.cc:2238-2262 (project, image bounds, distance range, PredictScale)
 //   static bool  H::fuse_query / H::fuse_sim3_query   see b1/b2 Fuse below
+//   static void  H::set_gba_pose(KeyFrame&, const double q[7], nLoopKF)   mTcwGBA, mnBAGlobalForKF
+//   static void  H::set_gba_pos(MapPoint*, const double x[3], nLoopKF)   mPosGBA, mnBAGlobalForKF
 #ifndef OSG_ORBSLAM3_H
 #define OSG_ORBSLAM3_H
 
 #include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <list>
@@ -1023,6 +1026,156 @@ void apply_local_bundle_adjustment(const LbaOutcome<KeyFrameT, MapPointT> &o)
     }
     for (const auto &kp : o.poses) H::set_pose(*kp.first, kp.second.data());
     for (const auto &mp : o.points) H::set_world_pos(mp.first, mp.second.data());
+}
+
+// ------------------------------------------------------- §8(f) rank 4: global BA (the g2o part)
+// Optimizer::BundleAdjustment(vpKFs, vpMP, nIterations, pbStopFlag, nLoopKF, bRobust)
+// (ref:src/Optimizer.cc:2850-3237; GlobalBundleAdjustemnt hands it the whole map, :2831-2839).
+// Vertices: every non-bad KeyFrame (only the map's init KeyFrame fixed, :2912-2930) and every
+// non-bad MapPoint with a valid observation (:2939-3110), in g2o id order as for the local BA.
+// Edges in the reference's insertion order (vpMP order x observation map order; left / stereo edge,
+// then the right-camera edge behind the reference's `rightIndex < mvKeysRight.size()` test, which it
+// applies before rightIndex -= NLeft, :3063-3097).  Mono / stereo edges carry Huber only with
+// bRobust, body edges always; deltas sqrt(5.99) / sqrt(7.815) as floats (:2933-2934).
+template <class KeyFrameT, class MapPointT>
+struct GbaOutcome {
+    std::vector<std::pair<KeyFrameT *, std::vector<double>>> poses;   // every non-bad KeyFrame (7)
+    std::vector<std::pair<MapPointT *, std::vector<double>>> points;  // the graph's MapPoints (3)
+    int iterations = 0;
+};
+
+template <class H, class KeyFrameT, class MapPointT>
+GbaOutcome<KeyFrameT, MapPointT> bundle_adjustment(const std::vector<KeyFrameT *> &vpKFs,
+                                                   const std::vector<MapPointT *> &vpMP, unsigned long initKFid,
+                                                   int nIterations, bool *pbStopFlag, bool bRobust)
+{
+    osg_ctx *ctx = thread_ctx();
+    GbaOutcome<KeyFrameT, MapPointT> out;
+    std::vector<std::pair<unsigned long, KeyFrameT *>> kfs;
+    unsigned long maxKFid = 0;
+    for (auto *k : vpKFs) {
+        if (k->isBad()) continue;
+        kfs.push_back({k->mnId, k});
+        maxKFid = std::max(maxKFid, (unsigned long)k->mnId);
+    }
+    std::sort(kfs.begin(), kfs.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+    std::unordered_map<KeyFrameT *, int> kf_index;
+    std::vector<double> pose(7 * kfs.size());
+    std::vector<uint8_t> fixed(kfs.size());
+    std::vector<osg_camera> cams(2 * kfs.size());
+    for (size_t i = 0; i < kfs.size(); i++) {
+        KeyFrameT *k = kfs[i].second;
+        kf_index[k] = (int)i;
+        H::pose(*k, &pose[7 * i]);
+        fixed[i] = (uint8_t)(k->mnId == initKFid);
+        H::camera(*k, false, cams[2 * i]);
+        if (k->mpCamera2) H::camera(*k, true, cams[2 * i + 1]);
+    }
+    std::vector<MapPointT *> in_graph;  // vpMP order
+    std::vector<int32_t> e_mp, e_pose, e_cam;
+    std::vector<int8_t> e_kind;
+    std::vector<uint8_t> e_rob;
+    std::vector<double> e_obs;
+    std::vector<float> e_isig;
+    for (auto *pMP : vpMP) {
+        if (pMP->isBad()) continue;
+        const auto observations = pMP->GetObservations();
+        int nEdges = 0;
+        for (const auto &ob : observations) {
+            KeyFrameT *pKF = ob.first;
+            if (pKF->isBad() || pKF->mnId > maxKFid) continue;
+            const auto itk = kf_index.find(pKF);
+            if (itk == kf_index.end()) continue;
+            nEdges++;
+            const int leftIndex = std::get<0>(ob.second);
+            auto add = [&](int8_t kind, int cam, const auto &kp, double ur, bool robust) {
+                e_mp.push_back((int32_t)in_graph.size());
+                e_pose.push_back(itk->second);
+                e_kind.push_back(kind);
+                e_cam.push_back(cam);
+                e_rob.push_back((uint8_t)robust);
+                e_obs.push_back(kp.pt.x);
+                e_obs.push_back(kp.pt.y);
+                e_obs.push_back(ur);
+                e_isig.push_back(pKF->mvInvLevelSigma2[kp.octave]);
+            };
+            if (leftIndex != -1 && pKF->mvuRight[leftIndex] < 0)
+                add(OSG_EDGE_MONO, 2 * itk->second, pKF->mvKeysUn[leftIndex], 0.0, bRobust);
+            else if (leftIndex != -1 && pKF->mvuRight[leftIndex] >= 0)
+                add(OSG_EDGE_STEREO, 2 * itk->second, pKF->mvKeysUn[leftIndex], pKF->mvuRight[leftIndex], bRobust);
+            if (pKF->mpCamera2) {
+                int rightIndex = std::get<1>(ob.second);
+                if (rightIndex != -1 && rightIndex < (int)pKF->mvKeysRight.size()) {
+                    rightIndex -= pKF->NLeft;
+                    add(OSG_EDGE_BODY, 2 * itk->second + 1, pKF->mvKeysRight[rightIndex], 0.0, true);
+                }
+            }
+        }
+        if (nEdges > 0) in_graph.push_back(pMP);  // :3100-3110: a point without edges leaves the graph
+    }
+    // MapPoints in g2o id order (mnId + maxKFid + 1)
+    std::vector<std::pair<unsigned long, int>> ord;
+    for (size_t i = 0; i < in_graph.size(); i++) ord.push_back({(unsigned long)in_graph[i]->mnId, (int)i});
+    std::sort(ord.begin(), ord.end());
+    std::vector<int32_t> slot(in_graph.size());
+    std::vector<double> point(3 * in_graph.size());
+    for (size_t j = 0; j < ord.size(); j++) {
+        slot[ord[j].second] = (int32_t)j;
+        H::world_pos(in_graph[ord[j].second], &point[3 * j]);
+    }
+    std::vector<int32_t> e_point(e_mp.size());
+    for (size_t e = 0; e < e_mp.size(); e++) e_point[e] = slot[e_mp[e]];
+    osg_ba_graph g{};
+    g.n_poses = (int32_t)kfs.size();
+    g.pose = pose.data();
+    g.pose_fixed = fixed.data();
+    g.n_points = (int32_t)in_graph.size();
+    g.point = point.data();
+    g.n_edges = (int32_t)e_kind.size();
+    g.e_point = e_point.data();
+    g.e_pose = e_pose.data();
+    g.e_kind = e_kind.data();
+    g.e_cam = e_cam.data();
+    g.e_obs = e_obs.data();
+    g.e_inv_sigma2 = e_isig.data();
+    g.n_cams = (int32_t)cams.size();
+    g.cams = cams.data();
+    g.iterations = nIterations;
+    g.user_lambda_init = 0.0;
+    g.e_robust = e_rob.data();
+    g.huber_mono = (float)std::sqrt(5.99);   // const float thHuber2D = sqrt(5.99)
+    g.huber_stereo = (float)std::sqrt(7.815);
+    std::vector<double> pose_out(pose.size()), point_out(point.size());
+    std::vector<uint8_t> bad(e_kind.size());
+    osg_ba_result r{};
+    r.pose = pose_out.data();
+    r.point = point_out.data();
+    r.edge_bad = bad.data();
+    static_assert(sizeof(bool) == 1, "pbStopFlag is passed as one byte");
+    check(ctx, osg_bundle_adjustment(ctx, &g, &r, reinterpret_cast<const volatile uint8_t *>(pbStopFlag)),
+          "osg_bundle_adjustment");
+    out.iterations = r.iterations;
+    for (size_t i = 0; i < kfs.size(); i++)
+        out.poses.push_back({kfs[i].second, std::vector<double>(&pose_out[7 * i], &pose_out[7 * i] + 7)});
+    for (size_t j = 0; j < ord.size(); j++)
+        out.points.push_back({in_graph[ord[j].second], std::vector<double>(&point_out[3 * j], &point_out[3 * j] + 3)});
+    return out;
+}
+
+// Writes a GbaOutcome as ref:src/Optimizer.cc:3122-3236 does: straight into the map after the
+// monocular initialisation (nLoopKF == the map's origin KeyFrame id), otherwise into mTcwGBA /
+// mPosGBA with mnBAGlobalForKF = nLoopKF for LoopClosing to apply.
+template <class H, class KeyFrameT, class MapPointT>
+void apply_bundle_adjustment(const GbaOutcome<KeyFrameT, MapPointT> &o, unsigned long nLoopKF, bool into_map)
+{
+    for (const auto &kp : o.poses) {
+        if (into_map) H::set_pose(*kp.first, kp.second.data());
+        else H::set_gba_pose(*kp.first, kp.second.data(), nLoopKF);
+    }
+    for (const auto &mp : o.points) {
+        if (into_map) H::set_world_pos(mp.first, mp.second.data());
+        else H::set_gba_pos(mp.first, mp.second.data(), nLoopKF);
+    }
 }
 
 }  // namespace osg_orbslam3

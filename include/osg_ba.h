@@ -5,6 +5,8 @@
  *   osg_local_bundle_adjustment    ← the g2o part of Optimizer::LocalBundleAdjustment
  *                                    (ref:src/Optimizer.cc:1877-2203: graph → optimize(10) →
  *                                    outlier classification → estimates out)
+ *   osg_bundle_adjustment          ← the g2o part of Optimizer::BundleAdjustment (global BA,
+ *                                    ref:src/Optimizer.cc:2850-3237)
  *
  * The caller (the ORB-SLAM3 side adapter) gathers the graph exactly as the
  * reference builds it — the same vertices, the same edges in the same insertion order, the same
@@ -88,6 +90,13 @@ typedef struct osg_ba_graph {
     const osg_camera *cams;
     int32_t iterations;        /* optimize(iterations): 10 in LocalBundleAdjustment */
     double user_lambda_init;   /* 0 → tau·max(diag H); 100 when the map is inertial */
+    /* Huber kernels.  Zero-initialised these are LocalBundleAdjustment's: every edge robust, deltas
+     * thHuberMono = sqrt(5.991) (mono and body) / thHuberStereo = sqrt(7.815) as floats
+     * (ref:src/Optimizer.cc:1951-1952).  BundleAdjustment (ref:src/Optimizer.cc:2933-2934, 3000-3007,
+     * 3041-3047, 3083-3085) uses sqrt(5.99) / sqrt(7.815) and attaches them to mono / stereo edges
+     * only when bRobust (body edges always). */
+    const uint8_t *e_robust;   /* per edge: a Huber kernel attached (NULL: every edge) */
+    float huber_mono, huber_stereo; /* the deltas as stored by the reference (0: the LBA values) */
 } osg_ba_graph;
 
 typedef struct osg_ba_result {
@@ -105,6 +114,14 @@ typedef struct osg_ba_result {
  * iterations and trials (may be NULL). */
 int osg_local_bundle_adjustment(struct osg_ctx *ctx, const osg_ba_graph *g, osg_ba_result *r,
                                 const volatile uint8_t *stop_flag);
+
+/* Optimizer::BundleAdjustment / GlobalBundleAdjustemnt (ref:src/Optimizer.cc:2831-3237): the same
+ * engine on the whole map — every KeyFrame (only the map's init KeyFrame fixed), every MapPoint with
+ * an edge, optimize(nIterations) with the caller's e_robust / Huber deltas, no outlier pass (edge_bad
+ * is filled but the reference does not read it).  The reduced camera system is dense: up to 1024 free
+ * KeyFrames. */
+int osg_bundle_adjustment(struct osg_ctx *ctx, const osg_ba_graph *g, osg_ba_result *r,
+                          const volatile uint8_t *stop_flag);
 
 /* Batched form: n_graphs independent windows (e.g. the LocalMapping windows of several maps or
  * sequences) optimised in lockstep, every kernel launched once per LM trial for all of them; each

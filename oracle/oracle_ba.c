@@ -1024,8 +1024,10 @@ int oracle_pose_optimization(const osg_pose_problem *P, osg_pose_result *R)
 /* ref:src/Optimizer.cc:1877-2203 (the part after the graph is gathered) */
 int oracle_local_bundle_adjustment(const osg_ba_graph *G, osg_ba_result *R, const volatile uint8_t *stop)
 {
-    const float thHuberMono = sqrt(5.991);
-    const float thHuberStereo = sqrt(7.815);
+    /* LocalBundleAdjustment's deltas (ref:src/Optimizer.cc:1951-1952) unless the graph carries
+     * BundleAdjustment's (thHuber2D = sqrt(5.99), thHuber3D, ref:src/Optimizer.cc:2933-2934) */
+    const float thHuberMono = G->huber_mono > 0.f ? G->huber_mono : (float)sqrt(5.991);
+    const float thHuberStereo = G->huber_stereo > 0.f ? G->huber_stereo : (float)sqrt(7.815);
     graph_t g;
     memset(&g, 0, sizeof g);
     g.n_poses = G->n_poses;
@@ -1046,7 +1048,8 @@ int oracle_local_bundle_adjustment(const osg_ba_graph *G, osg_ba_result *R, cons
         e->cam = &G->cams[G->e_cam[i]];
         memcpy(e->obs, G->e_obs + 3 * i, 3 * sizeof(double));
         e->w = (double)G->e_inv_sigma2[i];
-        e->robust = 1;
+        /* no kernel attached (BundleAdjustment, bRobust = false): the plain chi2 / quadratic form */
+        e->robust = G->e_robust ? (G->e_robust[i] != 0) : 1;
         e->delta = (e->kind == OSG_EDGE_STEREO) ? (double)thHuberStereo : (double)thHuberMono;
         e->dsqr = (float)(e->delta * e->delta);
         e->level = 0;

@@ -141,7 +141,7 @@ class OsgBaGraph(C.Structure):
         ("n_poses", i32), ("pose", P), ("pose_fixed", P), ("n_points", i32), ("point", P),
         ("n_edges", i32), ("e_point", P), ("e_pose", P), ("e_kind", P), ("e_cam", P),
         ("e_obs", P), ("e_inv_sigma2", P), ("n_cams", i32), ("cams", P), ("iterations", i32),
-        ("user_lambda_init", f64),
+        ("user_lambda_init", f64), ("e_robust", P), ("huber_mono", f32), ("huber_stereo", f32),
     ]
 
 
@@ -176,7 +176,7 @@ EXPORTS = [
     "osg_search_by_projection_mps_batch", "osg_search_by_projection_last_batch",
     "osg_search_by_projection_kf_batch", "osg_search_by_bow_kf_f_batch", "osg_search_by_bow_kf_kf_batch",
     "osg_match_last_stats", "osg_ctx_last_kernel_ms", "osg_pose_optimization", "osg_pose_optimization_batch",
-    "osg_local_bundle_adjustment", "osg_local_bundle_adjustment_batch",
+    "osg_local_bundle_adjustment", "osg_local_bundle_adjustment_batch", "osg_bundle_adjustment",
     "osg_vocabulary_create", "osg_vocabulary_load_text", "osg_vocabulary_destroy", "osg_vocabulary_info",
     "osg_vocabulary_transform", "osg_vocabulary_transform_batch",
     "osg_fuse_search", "osg_fuse_search_batch", "osg_search_for_triangulation", "osg_search_for_triangulation_batch",
@@ -228,6 +228,8 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.osg_pose_optimization_batch.argtypes = [vp, C.POINTER(OsgPoseProblem), i32,
                                                 C.POINTER(OsgPoseResult)]
     lib.osg_local_bundle_adjustment.argtypes = [vp, C.POINTER(OsgBaGraph), C.POINTER(OsgBaResult),
+                                                vp]
+    lib.osg_bundle_adjustment.argtypes = [vp, C.POINTER(OsgBaGraph), C.POINTER(OsgBaResult),
                                                 vp]
     lib.osg_local_bundle_adjustment_batch.argtypes = [vp, vp, i32, vp, vp]
     lib.osg_vocabulary_create.argtypes = [vp, C.POINTER(OsgVocabularyDesc), C.POINTER(vp)]

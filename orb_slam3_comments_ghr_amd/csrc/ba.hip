@@ -63,6 +63,8 @@ struct LbaDev {
     const int8_t *e_kind;
     const double *e_obs;
     const float *e_isig2;
+    const uint8_t *e_robust;      // per edge Huber attached, or null: every edge (LocalBundleAdjustment)
+    float hub_mono, hub_stereo;   // Huber deltas as the reference's floats (thHuberMono/2D, thHuberStereo/3D)
     const osg_camera *cams;
     // structure
     const int32_t *pose_h;        // per pose: hessian index or -1
@@ -113,10 +115,17 @@ __device__ inline double *new_point(const LbaDev &D) { return D.ctl->sel ? D.poi
     const LbaDev &D = Ds[blockIdx.y];                        \
     if (!(D.ctl->mode & (MODEBITS))) return
 
-__device__ inline void kind_delta(int kind, double &delta, float &dsqr)
+// The edge's Huber kernel; an edge without one (BundleAdjustment with bRobust = false,
+// ref:src/Optimizer.cc:3000-3007) gets an infinite delta, so rho = (e2, 1, 0) as g2o's unrobustified
+// chi2 / quadratic form
+__device__ inline void edge_delta(const LbaDev &D, int e, int kind, double &delta, float &dsqr)
 {
-    const float dm = (float)sqrt(5.991), ds = (float)sqrt(7.815);
-    const float d = (kind == OSG_EDGE_STEREO) ? ds : dm;
+    if (D.e_robust && !D.e_robust[e]) {
+        delta = __builtin_inf();
+        dsqr = __builtin_inff();
+        return;
+    }
+    const float d = (kind == OSG_EDGE_STEREO) ? D.hub_stereo : D.hub_mono;
     delta = (double)d;
     dsqr = (float)((double)d * (double)d);
 }
@@ -158,7 +167,7 @@ __global__ __launch_bounds__(EB) void k_errors(const LbaDev *__restrict__ Ds, in
         const double c = chi2_of(ev, dim, edge_w(D, e));
         double delta, r1;
         float dsqr;
-        kind_delta(k, delta, dsqr);
+        edge_delta(D, e, k, delta, dsqr);
         huber(c, delta, dsqr, rho0, r1);
     }
     const double t = block_sum_d(rho0, s);
@@ -195,7 +204,7 @@ __global__ __launch_bounds__(EB) void k_linearize(const LbaDev *__restrict__ Ds)
             const double ev[3] = {D.err[3 * e], D.err[3 * e + 1], D.err[3 * e + 2]};
             double delta, r0, rho1;
             float dsqr;
-            kind_delta(k, delta, dsqr);
+            edge_delta(D, e, k, delta, dsqr);
             huber(chi2_of(ev, dim, w), delta, dsqr, r0, rho1);
             const double ww = rho1 * w;
             double om[3];
@@ -501,14 +510,24 @@ __device__ __forceinline__ void tile_left_update2(const double *__restrict__ A, 
         aT[q] = (C0 + r < n && C0 + c < n) ? A[(size_t)(C0 + r) * n + C0 + c] : 0.0;
         aX[q] = (two && R0 + r < n && C0 + c < n) ? A[(size_t)(R0 + r) * n + C0 + c] : 0.0;
     }
-    const int kq = ((K + 63) / 64) * 16;  // per-wave slice, multiple of 16
-    const int mb = w * kq, me = min(K, mb + kq);
     const int g4 = 4 * (l >> 4);
     const int rj0 = C0 + (l & 15), rj1 = C0 + 16 + (l & 15);
     const int rt0 = R0 + (l & 15), rt1 = R0 + 16 + (l & 15);
     const bool vj0 = rj0 < n, vj1 = rj1 < n, vt0 = two && rt0 < n, vt1 = two && rt1 < n;
     const double *pj0 = A + (size_t)(vj0 ? rj0 : 0) * n + g4, *pj1 = A + (size_t)(vj1 ? rj1 : 0) * n + g4;
     const double *pt0 = A + (size_t)(vt0 ? rt0 : 0) * n + g4, *pt1 = A + (size_t)(vt1 ? rt1 : 0) * n + g4;
+    d4 accT[2][2], accX[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) accT[a][b] = accX[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+    double rp0 = 0.0, rp1 = 0.0;
+    // K in chunks of CMAX columns (one chunk up to the LocalBA size; BundleAdjustment's larger
+    // systems loop), each chunk split over the 4 waves
+    for (int kb = 0; kb < K; kb += CMAX) {
+    const int Kc = min(CMAX, K - kb);
+    const int kq = ((Kc + 63) / 64) * 16;  // per-wave slice, multiple of 16
+    const int mb = kb + w * kq, me = min(kb + Kc, mb + kq);
     double2 j0[LU_STEPS][2], j1[LU_STEPS][2], t0[LU_STEPS][2], t1[LU_STEPS][2], yy[LU_STEPS][2];
     const int nst = max(0, (me - mb) / 16);  // wave-uniform step count of this slice
 #pragma unroll
@@ -525,12 +544,6 @@ __device__ __forceinline__ void tile_left_update2(const double *__restrict__ A, 
             yy[s][0] = *(const double2 *)(y + g4 + m); yy[s][1] = *(const double2 *)(y + g4 + m + 2);
         }
     }
-    d4 accT[2][2], accX[2][2];
-#pragma unroll
-    for (int a = 0; a < 2; a++)
-#pragma unroll
-        for (int b = 0; b < 2; b++) accT[a][b] = accX[a][b] = d4{0.0, 0.0, 0.0, 0.0};
-    double rp0 = 0.0, rp1 = 0.0;
 #pragma unroll
     for (int s = 0; s < LU_STEPS; s++) {
         if (s < nst) {
@@ -569,6 +582,7 @@ __device__ __forceinline__ void tile_left_update2(const double *__restrict__ A, 
             }
         }
     }
+    }  // K chunks
     if (y) {  // sum the 4 k-groups of a row (lanes l, l ^ 16, l ^ 32, l ^ 48)
         rp0 += __shfl_xor(rp0, 16);
         rp0 += __shfl_xor(rp0, 32);
@@ -648,7 +662,7 @@ __global__ __launch_bounds__(256) void k_chol_col(const LbaDev *__restrict__ Ds,
     const int t = blockIdx.x;
     const int tid = threadIdx.x;
     const int R0 = k0 + t * CB;
-    unsigned long long *ts = (D.tstamp && t < 2 && tid == 0) ? D.tstamp + 8 * (2 * j + t) : nullptr;
+    unsigned long long *ts = (D.tstamp && t < 2 && tid == 0 && j < 32) ? D.tstamp + 8 * (2 * j + t) : nullptr;
     if (ts) ts[0] = wall_clock64();
 
     const double bj = (t == 0 && tid < nb) ? D.bs[k0 + tid] : 0.0;
@@ -787,7 +801,7 @@ __device__ __forceinline__ void lds_barrier()
 __global__ __launch_bounds__(1024) void k_chol_back(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT);
-    if (D.nhp == 0) return;
+    if (D.nhp == 0 || 6 * D.nhp > CMAX) return;
     __shared__ double s_x[CMAX];
     __shared__ double s_y[CMAX];
     __shared__ double s_li[CMAX * CB];
@@ -869,6 +883,56 @@ __global__ __launch_bounds__(1024) void k_chol_back(const LbaDev *__restrict__ D
         if (bi - 1 >= 0) solve_block(bi - 1, alt, cur);
     }
     if (ts) ts[40] = wall_clock64();
+    for (int i = tid; i < n; i += 1024) D.x[i] = s_x[i];
+}
+
+// Backward substitution for reduced systems past CMAX (BundleAdjustment): the same blocks and
+// summation order as k_chol_back, with x held in LDS (n <= CMAX_LARGE) and each block's 32 x 32
+// L_kk^-1 tile read from Linv when the block is reached instead of staged up front.
+constexpr int CMAX_LARGE = 6144;  // 1024 free poses
+
+__global__ __launch_bounds__(1024) void k_chol_back_large(const LbaDev *__restrict__ Ds)
+{
+    LBA_GRAPH(M_ACT);
+    const int n = 6 * D.nhp;
+    if (n <= CMAX) return;
+    __shared__ double s_x[CMAX_LARGE];
+    __shared__ double s_y[CMAX_LARGE];
+    __shared__ double s_li[CB * CB];
+    __shared__ double s_part[32][33];
+    __shared__ double s_rhs[CB];
+    const double *A = D.Hs;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < n; i += 1024) {
+        s_x[i] = 0.0;
+        s_y[i] = D.x[i];
+    }
+    const int nblk = (n + CB - 1) / CB;
+    const int c = tid & 31, g = tid >> 5;
+    for (int bi = nblk - 1; bi >= 0; bi--) {
+        const int k0 = bi * CB, nb = min(CB, n - k0);
+        s_li[tid] = D.Linv[(size_t)min(k0 + (tid >> 5), n - 1) * CB + (tid & 31)];
+        __syncthreads();
+        double acc = 0.0;
+        if (c < nb)
+            for (int row = k0 + nb + g; row < n; row += 32) acc += A[(size_t)row * n + k0 + c] * s_x[row];
+        s_part[c][g] = acc;
+        __syncthreads();
+        if (tid < CB) {
+            double s = 0.0;
+#pragma unroll
+            for (int gg = 0; gg < 32; gg++) s += s_part[tid][gg];
+            s_rhs[tid] = (tid < nb) ? s_y[k0 + tid] - s : 0.0;
+        }
+        __syncthreads();
+        if (tid < nb) {
+            double xv = 0.0;
+#pragma unroll
+            for (int r = 0; r < CB; r++) xv += s_li[r * CB + tid] * s_rhs[r];
+            s_x[k0 + tid] = xv;
+        }
+        __syncthreads();
+    }
     for (int i = tid; i < n; i += 1024) D.x[i] = s_x[i];
 }
 
@@ -1061,9 +1125,9 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
         H.trivial = true;
         return OSG_OK;
     }
-    if (6 * nhp > CMAX)
+    if (6 * nhp > CMAX_LARGE)
         return osg_set_error(ctx, OSG_E_INVALID, "%d free poses exceed the dense reduced-system limit (%d)", nhp,
-                             CMAX / 6);
+                             CMAX_LARGE / 6);
     const std::vector<int32_t> &pose_h = H.pose_h, &point_h = H.point_h;
     // edges per landmark (stable in edge order)
     H.lm_e_start.assign(nhl + 1, 0);
@@ -1312,7 +1376,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     osg_packer pk;
     struct InOff {
         size_t fixed, epose, epoint, ecam, ekind, eobs, eisig, cams, poseh, hppose, pointh, hlpoint, lmes, lme, lmbs,
-            blkpose, eblk, hpes, hpe, hpbs, hpb, pairs, pairab, chs, blklm, blkes, blke, pch, pose0, point0;
+            blkpose, eblk, hpes, hpe, hpbs, hpb, pairs, pairab, chs, blklm, blkes, blke, pch, pose0, point0, erob;
     };
     std::vector<InOff> io(NA);
     for (int a = 0; a < NA; a++) {
@@ -1328,6 +1392,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         o.eobs = pk.add(G->e_obs, 24 * (size_t)ne);
         o.eisig = pk.add(G->e_inv_sigma2, 4 * (size_t)ne);
         o.cams = pk.add(G->cams, sizeof(osg_camera) * G->n_cams);
+        o.erob = G->e_robust ? pk.add(G->e_robust, ne) : SIZE_MAX;
         o.poseh = pk.add(h.pose_h.data(), 4 * (size_t)np);
         o.hppose = pk.add(h.hp_pose.data(), 4 * (size_t)nhp);
         o.pointh = pk.add(h.point_h.data(), 4 * (size_t)npt);
@@ -1378,6 +1443,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     double *d_out = (double *)(dsm + dev_bytes + ctl_bytes);
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(din, pin, pk.total, hipMemcpyHostToDevice, ctx->stream));
     int mx_ge = 0, mx_gl = 1, mx_gu = 0, mx_nblk = 0, mx_nhp = 0, mx_chunks = 0, mx_pairs = 0, mx_red = 0;
+    bool large = false;  // some graph's reduced system is past CMAX
     for (int a = 0; a < NA; a++) {
         const LbaHost &h = H[act[a]];
         const InOff &o = io[a];
@@ -1399,6 +1465,10 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         D.e_obs = osg_dptr<double>(din, o.eobs);
         D.e_isig2 = osg_dptr<float>(din, o.eisig);
         D.cams = osg_dptr<osg_camera>(din, o.cams);
+        D.e_robust = o.erob == SIZE_MAX ? nullptr : osg_dptr<uint8_t>(din, o.erob);
+        D.hub_mono = h.G->huber_mono > 0.f ? h.G->huber_mono : (float)std::sqrt(5.991);   // thHuberMono
+        D.hub_stereo = h.G->huber_stereo > 0.f ? h.G->huber_stereo : (float)std::sqrt(7.815);
+        large |= 6 * h.nhp > CMAX;
         D.pose_h = osg_dptr<int32_t>(din, o.poseh);
         D.hp_pose = osg_dptr<int32_t>(din, o.hppose);
         D.point_h = osg_dptr<int32_t>(din, o.pointh);
@@ -1462,6 +1532,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
             for (int jb = 0; jb < mx_red; jb++)  // row blocks at and below the diagonal block
                 hipLaunchKernelGGL(k_chol_col, gx(mx_red - jb), dim3(256), 0, ctx->stream, d_dev, jb);
             hipLaunchKernelGGL(k_chol_back, yb, dim3(1024), 0, ctx->stream, d_dev);
+            if (large) hipLaunchKernelGGL(k_chol_back_large, yb, dim3(1024), 0, ctx->stream, d_dev);
         }
         hipLaunchKernelGGL(k_update, gx(mx_gu), dim3(EB), 0, ctx->stream, d_dev);
         hipLaunchKernelGGL(k_errors, gx(mx_ge), dim3(EB), 0, ctx->stream, d_dev, 0);
@@ -1621,6 +1692,11 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
 extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, osg_ba_result *R,
                                            const volatile uint8_t *stop)
 {
+    return lba_batch(ctx, G, R, 1, stop);
+}
+
+extern "C" int osg_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, osg_ba_result *R, const volatile uint8_t *stop)
+{  // Optimizer::BundleAdjustment: the same LM over the whole map (the caller's Huber fields)
     return lba_batch(ctx, G, R, 1, stop);
 }
 

@@ -172,6 +172,9 @@ class BAGraph:
     cams: list
     iterations: int = 10
     user_lambda_init: float = 0.0
+    e_robust: np.ndarray | None = None   # BundleAdjustment: per-edge Huber flag (None: every edge)
+    huber_mono: float = 0.0              # deltas as the reference's floats (0: LocalBundleAdjustment's)
+    huber_stereo: float = 0.0
 
     def __post_init__(self):
         self.pose = np.ascontiguousarray(self.pose, np.float64).reshape(-1, 7)
@@ -183,6 +186,8 @@ class BAGraph:
         self.e_cam = np.ascontiguousarray(self.e_cam, np.int32)
         self.e_obs = np.ascontiguousarray(self.e_obs, np.float64).reshape(-1, 3)
         self.e_inv_sigma2 = np.ascontiguousarray(self.e_inv_sigma2, np.float32)
+        if self.e_robust is not None:
+            self.e_robust = np.ascontiguousarray(self.e_robust, np.uint8)
         self._cams = (_abi.OsgCamera * max(1, len(self.cams)))(*self.cams)
 
     def struct(self):
@@ -198,6 +203,8 @@ class BAGraph:
         s.cams = C.addressof(self._cams)
         s.iterations = self.iterations
         s.user_lambda_init = self.user_lambda_init
+        s.e_robust = _p(self.e_robust)
+        s.huber_mono, s.huber_stereo = self.huber_mono, self.huber_stereo
         return s
 
 
@@ -262,6 +269,21 @@ class Optimizer:
         rc = lib.osg_local_bundle_adjustment(h, C.byref(gs), C.byref(R), sf)
         self.ctx.check(rc, "LocalBundleAdjustment")
         return BAResult(pose, point, bad, R.iterations, R.trials, R.chi2_initial, R.chi2_final, R.aborted)
+
+    def BundleAdjustment(self, G: BAGraph, stop_flag: np.ndarray | None = None) -> BAResult:
+        """The g2o part of ``Optimizer::BundleAdjustment`` (global BA, ref:src/Optimizer.cc:2850-3237):
+        ``G`` built as the reference builds it (``synth_gba_graph`` / the adapter), optimize(G.iterations).
+        The reference reads no outlier flags after a global BA; ``edge_bad`` is informational."""
+        lib, h = self.ctx.lib, self.ctx.handle
+        R, pose, point, bad = make_ba_result(G)
+        gs = G.struct()
+        if stop_flag is not None:
+            assert stop_flag.dtype == np.uint8, "stop flag is one byte (bool *pbStopFlag)"
+        sf = None if stop_flag is None else _p(stop_flag)
+        self.ctx.check(lib.osg_bundle_adjustment(h, C.byref(gs), C.byref(R), sf), "BundleAdjustment")
+        return BAResult(pose, point, bad, R.iterations, R.trials, R.chi2_initial, R.chi2_final, R.aborted)
+
+    GlobalBundleAdjustemnt = BundleAdjustment  # the reference's spelling (ref:include/Optimizer.h)
 
     def LocalBundleAdjustmentBatch(self, graphs, stop_flag: np.ndarray | None = None) -> list:
         """B independent windows in lockstep, one launch per kernel per LM trial for all of them
@@ -420,3 +442,24 @@ def synth_lba_graph(rng, n_kf=50, n_points=10000, k_range=(2, 8), n_fixed=2, ste
     obs = np.array(e_obs, np.float32).astype(np.float64)
     return BAGraph(np.array(poses), fixed, Pn, e_point, np.array(e_pose), np.array(e_kind, np.int8),
                    np.zeros(len(e_point), np.int32), obs, np.array(e_isig, np.float32), [cam])
+
+
+def gba_robust_settings(G: BAGraph, bRobust: bool = True) -> BAGraph:
+    """Give an LBA-shaped graph BundleAdjustment's kernels (ref:src/Optimizer.cc:2933-2934,
+    3000-3007, 3041-3047, 3083-3085): deltas float(sqrt(5.99)) / float(sqrt(7.815)); mono and stereo
+    edges carry them only when bRobust, body edges always."""
+    G.huber_mono = float(np.float32(np.sqrt(5.99)))
+    G.huber_stereo = float(np.float32(np.sqrt(7.815)))
+    G.e_robust = np.where(G.e_kind == _abi.EDGE_BODY, 1, int(bool(bRobust))).astype(np.uint8)
+    return G
+
+
+def synth_gba_graph(rng, n_kf=120, n_points=20000, bRobust=False, iterations=10, stereo_frac=0.0, **kw):
+    """A whole-map BA: keyframes on a longer arc, only the map's init KeyFrame fixed, every point with
+    its observations.  Defaults: LoopClosing's GlobalBundleAdjustemnt(map, 10, &mbStopGBA, nLoopKF,
+    false) (ref:src/LoopClosing.cc:3084); the monocular initialisation runs (map, 20) with bRobust
+    true (ref:src/Tracking.cc:3076)."""
+    G = synth_lba_graph(rng, n_kf=n_kf, n_points=n_points, n_fixed=1, stereo_frac=stereo_frac,
+                        arc_deg=kw.pop("arc_deg", 120.0), **kw)
+    G.iterations = iterations
+    return gba_robust_settings(G, bRobust)

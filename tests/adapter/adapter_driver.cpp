@@ -1,7 +1,7 @@
 // adapter_driver.cpp — runs adapters/orbslam3/osg_orbslam3.h on mock ORB-SLAM3 objects built from
 // arrays written by tests/test_adapter.py, and writes the adapter's results back (test-only).
 //
-//   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba fuse fuse_sim3 triang distinct sim3 sim3_kfs init stereo
+//   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba fuse fuse_sim3 triang distinct sim3 sim3_kfs init stereo gba
 //
 // Array file: repeated {u32 name_len, name, u8 dtype ('b' u8, 'i' i32, 'f' f32, 'd' f64), u64 count,
 // data}.
@@ -284,6 +284,48 @@ static void build_triang_kf(const Arrays &m, const std::string &pre, KeyFrame &K
     fill_featvec(m, pre, K.mFeatVec);
 }
 
+// A BA world from the graph arrays "G.*": one KeyFrame per pose (mnId = index, the shared camera
+// "G.cam"), one MapPoint per point, one observation per edge (keypoint octave = its index in the
+// KeyFrame, so mvInvLevelSigma2[octave] is the edge's weight; mvuRight = ur on stereo edges)
+static void build_ba_world(const Arrays &in, Map &map, Camera &c, std::vector<KeyFrame> &kf, std::vector<MapPoint> &mp)
+{
+    const int np = (int)(get(in, "G.pose").n / 7), npt = (int)(get(in, "G.point").n / 3), ne = (int)get(in, "G.e_pose").n;
+    const float *cam = get(in, "G.cam").p<float>();
+    c.type = (int)cam[0];
+    c.params.assign(cam + 1, cam + 9);
+    kf.resize(np);
+    mp.resize(npt);
+    for (int i = 0; i < np; i++) {
+        kf[i].mnId = (unsigned long)i;
+        kf[i].map = &map;
+        std::memcpy(kf[i].pose, get(in, "G.pose").p<double>() + 7 * i, 56);
+        kf[i].mpCamera = &c;
+        kf[i].fx = cam[9];
+        kf[i].fy = cam[10];
+        kf[i].cx = cam[11];
+        kf[i].cy = cam[12];
+        kf[i].mbf = cam[13];
+    }
+    for (int j = 0; j < npt; j++) {
+        mp[j].mnId = (unsigned long)j;
+        std::memcpy(mp[j].pos, get(in, "G.point").p<double>() + 3 * j, 24);
+    }
+    for (int e = 0; e < ne; e++) {
+        KeyFrame &k = kf[get(in, "G.e_pose").p<int32_t>()[e]];
+        MapPoint &p = mp[get(in, "G.e_point").p<int32_t>()[e]];
+        const double *o = get(in, "G.e_obs").p<double>() + 3 * e;
+        cv::KeyPoint kp;
+        kp.pt.x = (float)o[0];
+        kp.pt.y = (float)o[1];
+        kp.octave = (int)k.mvKeysUn.size();
+        k.mvKeysUn.push_back(kp);
+        k.mvInvLevelSigma2.push_back(get(in, "G.e_inv_sigma2").p<float>()[e]);
+        k.mvuRight.push_back(get(in, "G.e_kind").p<uint8_t>()[e] == OSG_EDGE_STEREO ? (float)o[2] : -1.0f);
+        k.mvpMapPoints.push_back(&p);
+        p.obs[&k] = std::make_tuple(kp.octave, -1);
+    }
+}
+
 int main(int argc, char **argv)
 {
     if (argc != 4) {
@@ -457,42 +499,11 @@ int main(int argc, char **argv)
             out["outlier"] = make('b', outl);
         } else if (mode == "lba") {
             const int np = (int)(get(in, "G.pose").n / 7), npt = (int)(get(in, "G.point").n / 3), ne = (int)get(in, "G.e_pose").n;
-            const float *cam = get(in, "G.cam").p<float>();
             Camera c;
-            c.type = (int)cam[0];
-            c.params.assign(cam + 1, cam + 9);
             Map map;
-            std::vector<KeyFrame> kf(np);
-            std::vector<MapPoint> mp(npt);
-            for (int i = 0; i < np; i++) {
-                kf[i].mnId = (unsigned long)i;
-                kf[i].map = &map;
-                std::memcpy(kf[i].pose, get(in, "G.pose").p<double>() + 7 * i, 56);
-                kf[i].mpCamera = &c;
-                kf[i].fx = cam[9];
-                kf[i].fy = cam[10];
-                kf[i].cx = cam[11];
-                kf[i].cy = cam[12];
-                kf[i].mbf = cam[13];
-            }
-            for (int j = 0; j < npt; j++) {
-                mp[j].mnId = (unsigned long)j;
-                std::memcpy(mp[j].pos, get(in, "G.point").p<double>() + 3 * j, 24);
-            }
-            for (int e = 0; e < ne; e++) {
-                KeyFrame &k = kf[get(in, "G.e_pose").p<int32_t>()[e]];
-                MapPoint &p = mp[get(in, "G.e_point").p<int32_t>()[e]];
-                const double *o = get(in, "G.e_obs").p<double>() + 3 * e;
-                cv::KeyPoint kp;
-                kp.pt.x = (float)o[0];
-                kp.pt.y = (float)o[1];
-                kp.octave = (int)k.mvKeysUn.size();
-                k.mvKeysUn.push_back(kp);
-                k.mvInvLevelSigma2.push_back(get(in, "G.e_inv_sigma2").p<float>()[e]);
-                k.mvuRight.push_back(get(in, "G.e_kind").p<uint8_t>()[e] == OSG_EDGE_STEREO ? (float)o[2] : -1.0f);
-                k.mvpMapPoints.push_back(&p);
-                p.obs[&k] = std::make_tuple(kp.octave, -1);
-            }
+            std::vector<KeyFrame> kf;
+            std::vector<MapPoint> mp;
+            build_ba_world(in, map, c, kf, mp);
             std::list<KeyFrame *> local, fixedc;
             const uint8_t *fx = get(in, "G.pose_fixed").p<uint8_t>();
             for (int i = 0; i < np; i++) (fx[i] ? fixedc : local).push_back(&kf[i]);
@@ -515,6 +526,42 @@ int main(int argc, char **argv)
             out["point"] = make('d', point);
             out["edge_bad"] = make('b', bad);
             out["num_edges"] = make('i', std::vector<int32_t>{o.num_edges});
+        } else if (mode == "gba") {
+            // the "lba" arrays; params: nIterations bRobust nLoopKF.  KeyFrame 0 is the map's init and
+            // origin KeyFrame: nLoopKF 0 writes into the map, anything else into mTcwGBA / mPosGBA
+            const int np = (int)(get(in, "G.pose").n / 7), npt = (int)(get(in, "G.point").n / 3);
+            Camera c;
+            Map map;
+            std::vector<KeyFrame> kf;
+            std::vector<MapPoint> mp;
+            build_ba_world(in, map, c, kf, mp);
+            std::vector<KeyFrame *> vk;
+            std::vector<MapPoint *> vm;
+            for (auto &k : kf) vk.push_back(&k);
+            for (auto &p : mp) vm.push_back(&p);
+            bool stop = false;
+            const unsigned long nLoop = (unsigned long)prm[2];
+            auto o = osg_orbslam3::bundle_adjustment<MockHooks>(vk, vm, 0ul, (int)prm[0], &stop, prm[1] != 0);
+            osg_orbslam3::apply_bundle_adjustment<MockHooks>(o, nLoop, nLoop == 0);
+            std::vector<double> pose(7 * (size_t)np), point(3 * (size_t)npt), pose_gba(7 * (size_t)np),
+                point_gba(3 * (size_t)npt);
+            std::vector<int32_t> ba_for;
+            for (int i = 0; i < np; i++) {
+                std::memcpy(&pose[7 * i], kf[i].pose, 56);
+                std::memcpy(&pose_gba[7 * i], kf[i].pose_gba, 56);
+                ba_for.push_back((int32_t)kf[i].mnBAGlobalForKF);
+            }
+            for (int j = 0; j < npt; j++) {
+                std::memcpy(&point[3 * j], mp[j].pos, 24);
+                std::memcpy(&point_gba[3 * j], mp[j].pos_gba, 24);
+                ba_for.push_back((int32_t)mp[j].mnBAGlobalForKF);
+            }
+            out["pose"] = make('d', pose);
+            out["point"] = make('d', point);
+            out["pose_gba"] = make('d', pose_gba);
+            out["point_gba"] = make('d', point_gba);
+            out["ba_for"] = make('i', ba_for);
+            out["iterations"] = make('i', std::vector<int32_t>{o.iterations});
         } else if (mode == "fuse" || mode == "fuse_sim3") {
             // pool of MapPoints "P.*" (index = id), the keyframe's slot occupants "K.slot_mp", the
             // list to fuse "L.list" (pool indices, -1 = NULL); params: th right

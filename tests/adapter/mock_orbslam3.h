@@ -57,6 +57,8 @@ struct MapPoint {
     // isInFrustum results (SearchByProjection(Frame&, vector<MapPoint*>))
     float mTrackProjX = 0, mTrackProjY = 0, mTrackDepth = 0, mTrackDepthR = 0, mTrackProjXR = 0, mTrackProjYR = 0;
     bool mbTrackInView = false, mbTrackInViewR = false;
+    double pos_gba[3] = {0, 0, 0};  // mPosGBA
+    unsigned long mnBAGlobalForKF = 0;
     int mnTrackScaleLevel = 0, mnTrackScaleLevelR = 0;
     float mTrackViewCos = 0, mTrackViewCosR = 0;
     // test-only: what MockHooks::project_last / kf_query return for this MapPoint
@@ -129,6 +131,8 @@ struct KeyFrame {
     int mnScaleLevels = 8;
     std::vector<float> mvScaleFactors, mvLevelSigma2;
     osg_triang_geom triang_geom{};  // test-only: MockHooks::triang_geom
+    double pose_gba[7] = {0, 0, 0, 0, 0, 0, 0};  // mTcwGBA
+    unsigned long mnBAGlobalForKF = 0;
 
     std::vector<MapPoint *> GetMapPointMatches() const { return mvpMapPoints; }
     bool isBad() const { return bad; }
@@ -179,6 +183,16 @@ struct MockHooks {
     static void set_pose(T &o, const double q[7]) { std::memcpy(o.pose, q, sizeof o.pose); }
     static void world_pos(MapPoint *p, double x[3]) { std::memcpy(x, p->pos, sizeof p->pos); }
     static void set_world_pos(MapPoint *p, const double x[3]) { std::memcpy(p->pos, x, sizeof p->pos); }
+    static void set_gba_pose(KeyFrame &k, const double q[7], unsigned long n)
+    {
+        std::memcpy(k.pose_gba, q, sizeof k.pose_gba);
+        k.mnBAGlobalForKF = n;
+    }
+    static void set_gba_pos(MapPoint *p, const double x[3], unsigned long n)
+    {
+        std::memcpy(p->pos_gba, x, sizeof p->pos_gba);
+        p->mnBAGlobalForKF = n;
+    }
     template <class T>
     static void camera(const T &o, bool right, osg_camera &c)
     {

@@ -405,6 +405,13 @@ def local_bundle_adjustment(G):
     ne = len(G.e_pose)
     E = Edges(G.e_kind, G.e_pose, G.e_point, None, np.asarray(G.e_obs, float).reshape(-1, 3), G.e_inv_sigma2,
               G.cams, G.e_cam, unary=False)
+    # BundleAdjustment's kernels (ref:src/Optimizer.cc:2933-2934, 3000-3007): its own deltas, and no
+    # kernel at all on the edges the graph marks
+    if G.huber_mono > 0 or G.huber_stereo > 0:
+        E.delta = np.where(E.kind == STEREO, float(f32(G.huber_stereo)), float(f32(G.huber_mono)))
+        E.dsqr = (E.delta * E.delta).astype(f32).astype(float)
+    if G.e_robust is not None:
+        E.robust = np.asarray(G.e_robust, bool).copy()
     lm = LM(E, poses, points, np.asarray(G.pose_fixed, bool), user_lambda=G.user_lambda_init)
     lm.initialize(np.arange(ne))
     lm.errors()

@@ -594,3 +594,33 @@ def test_adapter_compute_stereo_matches(driver, tmp_path, oracle):
     assert n > 500 and int(out["nmatches"][0]) == n
     np.testing.assert_array_equal(out["ur"].view(np.int32), ur.view(np.int32))
     np.testing.assert_array_equal(out["depth"].view(np.int32), d.view(np.int32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("robust,loop", [(False, 7), (True, 0)])
+def test_adapter_global_bundle_adjustment(driver, tmp_path, ctx, robust, loop):
+    """Optimizer::BundleAdjustment through the adapter on a mock map (KeyFrame 0 = init / origin, the
+    only fixed vertex): equal to the direct C-ABI call on the same graph, written into mTcwGBA /
+    mPosGBA with mnBAGlobalForKF = nLoopKF (loop closing) or straight into the map (nLoopKF = origin,
+    the monocular initialisation)."""
+    rng = np.random.default_rng(760 + loop)
+    G = op.synth_gba_graph(rng, n_kf=12, n_points=900, bRobust=robust, stereo_frac=0.3,
+                           iterations=20 if robust else 10)
+    order = np.lexsort((G.e_pose, G.e_point))
+    for k in ["e_point", "e_pose", "e_kind", "e_cam", "e_obs", "e_inv_sigma2", "e_robust"]:
+        setattr(G, k, np.ascontiguousarray(getattr(G, k)[order]))
+    G.e_obs = G.e_obs.astype(np.float32).astype(np.float64)
+    arrays = {"G.pose": G.pose.reshape(-1), "G.pose_fixed": G.pose_fixed.astype(np.uint8),
+              "G.point": G.point.reshape(-1), "G.e_point": G.e_point.astype(np.int32),
+              "G.e_pose": G.e_pose.astype(np.int32), "G.e_kind": G.e_kind.astype(np.uint8),
+              "G.e_obs": G.e_obs.reshape(-1), "G.e_inv_sigma2": G.e_inv_sigma2.astype(np.float32),
+              "G.cam": cam_array(G.cams[0]), "params": np.array([G.iterations, robust, loop], np.float32)}
+    out = run(driver, tmp_path, "gba", arrays)
+    ref = op.Optimizer(ctx).BundleAdjustment(G)
+    assert int(out["iterations"][0]) == ref.iterations >= 1
+    pose, point = (out["pose"], out["point"]) if loop == 0 else (out["pose_gba"], out["point_gba"])
+    np.testing.assert_array_equal(pose.reshape(-1, 7), ref.pose.reshape(-1, 7))
+    np.testing.assert_array_equal(point.reshape(-1, 3), ref.point.reshape(-1, 3))
+    if loop:  # the map itself is untouched until LoopClosing applies the result
+        np.testing.assert_array_equal(out["pose"].reshape(-1, 7), G.pose)
+        assert (out["ba_for"] == loop).all()

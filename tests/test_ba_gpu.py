@@ -185,3 +185,39 @@ def test_lba_batch_c4_windows(ctx, oracle):
         np.testing.assert_allclose(g.pose, ref.pose, atol=STATE_TOL, rtol=0)
         np.testing.assert_allclose(g.point, ref.point, atol=STATE_TOL, rtol=0)
         np.testing.assert_array_equal(g.edge_bad, ref.edge_bad)
+
+
+def check_gba(ctx, oracle, G):
+    ref = oc.lba(oracle, G)
+    got = op.Optimizer(ctx).BundleAdjustment(G)
+    assert abs(got.iterations - ref.iterations) <= 1
+    assert trials_close(got.trials, ref.trials), (got.trials, ref.trials)
+    assert abs(got.chi2_initial - ref.chi2_initial) <= CHI2_RTOL * ref.chi2_initial
+    assert abs(got.chi2_final - ref.chi2_final) <= CHI2_RTOL * ref.chi2_final
+    np.testing.assert_allclose(got.pose, ref.pose, atol=STATE_TOL, rtol=0)
+    np.testing.assert_allclose(got.point, ref.point, atol=STATE_TOL, rtol=0)
+    return got, ref
+
+
+@pytest.mark.parametrize("n_kf,n_pts,robust,stereo", [(12, 1000, False, 0.0), (30, 3000, True, 0.3),
+                                                      (80, 8000, False, 0.0), (150, 12000, False, 0.2)])
+def test_gba_parity(ctx, oracle, n_kf, n_pts, robust, stereo):
+    """Optimizer::BundleAdjustment: 80 and 150 keyframes put the reduced system (474 / 894) past the
+    LocalBA size, through the chunked column updates and k_chol_back_large."""
+    rng = np.random.default_rng(3000 + n_kf)
+    G = op.synth_gba_graph(rng, n_kf=n_kf, n_points=n_pts, bRobust=robust, stereo_frac=stereo)
+    got, ref = check_gba(ctx, oracle, G)
+    assert got.chi2_final < got.chi2_initial and got.iterations >= 1
+
+
+def test_gba_and_lba_in_one_batch(ctx, oracle):
+    """A LocalBA window and a whole-map BA in one lockstep batch: each equals its own call."""
+    rng = np.random.default_rng(3300)
+    graphs = [op.synth_lba_graph(rng, n_kf=20, n_points=2000), op.synth_gba_graph(rng, n_kf=90, n_points=6000)]
+    opt = op.Optimizer(ctx)
+    batch = opt.LocalBundleAdjustmentBatch(graphs)
+    for G, b in zip(graphs, batch):
+        s = opt.LocalBundleAdjustment(G)
+        assert (b.iterations, b.trials) == (s.iterations, s.trials)
+        np.testing.assert_array_equal(b.pose, s.pose)
+        np.testing.assert_array_equal(b.point, s.point)

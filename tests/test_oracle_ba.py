@@ -123,3 +123,22 @@ def test_local_bundle_adjustment_oracle_vs_numpy(oracle, seed, stereo, lam):
     np.testing.assert_allclose(got.pose.reshape(-1, 7), pose, atol=STATE_TOL, rtol=0)
     np.testing.assert_allclose(got.point.reshape(-1, 3), point, atol=STATE_TOL, rtol=0)
     assert abs(got.chi2_final - chi_fin) <= 1e-6 * chi_fin
+
+
+@pytest.mark.parametrize("seed,robust,stereo", [(1, False, 0.0), (2, True, 0.3), (3, False, 0.5)])
+def test_bundle_adjustment_oracle_vs_numpy(oracle, seed, robust, stereo):
+    """Optimizer::BundleAdjustment (ref:src/Optimizer.cc:2850-3237): only the init KeyFrame fixed, the
+    sqrt(5.99) / sqrt(7.815) deltas, and with bRobust = false no kernel on mono / stereo edges."""
+    G = op.synth_gba_graph(np.random.default_rng(2100 + seed), n_kf=8, n_points=300, bRobust=robust,
+                           stereo_frac=stereo, iterations=20 if robust else 10)
+    got = oc.lba(oracle, G)
+    pose, point, bad, iters, chi_ini, chi_fin = pr.local_bundle_adjustment(G)
+    assert abs(got.chi2_initial - chi_ini) <= 1e-9 * chi_ini
+    assert abs(got.iterations - iters) <= 1
+    np.testing.assert_allclose(got.pose.reshape(-1, 7), pose, atol=STATE_TOL, rtol=0)
+    np.testing.assert_allclose(got.point.reshape(-1, 3), point, atol=STATE_TOL, rtol=0)
+    assert abs(got.chi2_final - chi_fin) <= 1e-6 * chi_fin
+    if not robust:  # the same graph with kernels: Huber's rho is below e2 on the outliers
+        Gr = op.gba_robust_settings(op.synth_gba_graph(np.random.default_rng(2100 + seed), n_kf=8, n_points=300,
+                                                       stereo_frac=stereo), True)
+        assert oc.lba(oracle, Gr).chi2_initial < got.chi2_initial
