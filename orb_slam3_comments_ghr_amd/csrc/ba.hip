@@ -21,7 +21,8 @@
 //   k_schur_chunks / k_schur_pairs  S_ij = sum_p BDinv_ip Hpl_jp^T over fixed chunks, then the dense
 //                 reduced camera matrix Hpp + lambda I - S and b_schur (k_bschur)
 //   k_chol_col x ceil(n/32), k_chol_back   left-looking blocked Cholesky (FP64 MFMA tile updates),
-//                 forward solve fused, backward solve
+//                 forward solve fused, backward solve; past n = 384 (BundleAdjustment) right-looking:
+//                 k_chol_col + k_chol_trail per column block, then k_chol_back_large
 //   k_update      per point: x_l = Dinv (b_l - Hpl^T x_p), new estimates (poses: exp(x) * T)
 //                 and the LM scale sum;  then k_errors on the new estimates
 //   k_step_reduce the step's scalars per graph (chi2 of trial and current, scale, lambda, pivot flag)
@@ -667,7 +668,9 @@ __global__ __launch_bounds__(256) void k_chol_col(const LbaDev *__restrict__ Ds,
 
     const double bj = (t == 0 && tid < nb) ? D.bs[k0 + tid] : 0.0;
     for (int e = tid; e < CB * (CB + 1); e += 256) (&sM[0][0])[e] = 0.0;
-    tile_left_update2(A, n, k0, t > 0 ? R0 : -1, k0, t == 0 ? D.x : nullptr, sG, sX, sP, s_rp);
+    // past CMAX the system is factored right-looking: k_chol_trail has already applied every earlier
+    // column block to these tiles and to b, so nothing is left to subtract (K = 0)
+    tile_left_update2(A, n, k0, t > 0 ? R0 : -1, n > CMAX ? 0 : k0, t == 0 ? D.x : nullptr, sG, sX, sP, s_rp);
     if (tid < CB) sM[tid][tid] = 1.0;
     __syncthreads();
     if (ts) ts[1] = wall_clock64();
@@ -886,6 +889,56 @@ __global__ __launch_bounds__(1024) void k_chol_back(const LbaDev *__restrict__ D
     for (int i = tid; i < n; i += 1024) D.x[i] = s_x[i];
 }
 
+// Right-looking trailing update for reduced systems past CMAX (BundleAdjustment): after column
+// block j is factored, every lower tile (t, u), j < u <= t, takes A_tu -= L_tj L_uj^T (FP64 MFMA, one
+// workgroup per tile, both L tiles staged in LDS), and the diagonal-tile workgroups update the
+// forward-substitution right-hand side b_t -= L_tj y_j.  The column launches then read their tiles as
+// they stand (K = 0): the O(n^3) work is spread over (nblk - j)^2 / 2 workgroups per step instead of
+// one K-long GEMM per row block (which left one CU per row block MFMA-bound at large n).
+__global__ __launch_bounds__(256) void k_chol_trail(const LbaDev *__restrict__ Ds, int j)
+{
+    LBA_GRAPH(M_ACT);
+    const int n = 6 * D.nhp;
+    if (n <= CMAX) return;
+    const int m = D.nblk_red - j - 1;  // row blocks below block j
+    if (m <= 0 || (int)blockIdx.x >= m * (m + 1) / 2) return;
+    int t = 0, rem = blockIdx.x;  // tile (t, u), u <= t, row-major over the lower triangle
+    while (rem > t) {
+        rem -= t + 1;
+        t++;
+    }
+    const int u = rem;
+    const int R0 = (j + 1 + t) * CB, C0 = (j + 1 + u) * CB, K0 = j * CB;
+    __shared__ double sLt[CB][CB + 1], sLu[CB][CB + 1];
+    const int tid = threadIdx.x;
+    for (int e = tid; e < CB * CB; e += 256) {
+        const int r = e >> 5, c = e & 31;
+        sLt[r][c] = (R0 + r < n) ? D.Hs[(size_t)(R0 + r) * n + K0 + c] : 0.0;
+        sLu[r][c] = (C0 + r < n) ? D.Hs[(size_t)(C0 + r) * n + K0 + c] : 0.0;
+    }
+    __syncthreads();
+    const int w = tid >> 6, l = tid & 63;
+    const int qr = (w >> 1) * 16, qc = (w & 1) * 16;
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int ks = 0; ks < CB / 4; ks++) {
+        const int k = 4 * ks + (l >> 4);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sLt[qr + (l & 15)][k], sLu[qc + (l & 15)][k], acc, 0, 0, 0);
+    }
+    const int c = qc + (l & 15);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int r = qr + (l >> 4) + 4 * q;
+        if (R0 + r < n && C0 + c < n) D.Hs[(size_t)(R0 + r) * n + C0 + c] -= acc[q];
+    }
+    if (t == u && tid < CB && R0 + tid < n) {  // block j is full (m > 0): y_j is 32 entries
+        double s = 0.0;
+#pragma unroll 8
+        for (int k = 0; k < CB; k++) s += sLt[tid][k] * D.x[K0 + k];
+        D.bs[R0 + tid] -= s;
+    }
+}
+
 // Backward substitution for reduced systems past CMAX (BundleAdjustment): the same blocks and
 // summation order as k_chol_back, with x held in LDS (n <= CMAX_LARGE) and each block's 32 x 32
 // L_kk^-1 tile read from Linv when the block is reached instead of staged up front.
@@ -914,8 +967,10 @@ __global__ __launch_bounds__(1024) void k_chol_back_large(const LbaDev *__restri
         s_li[tid] = D.Linv[(size_t)min(k0 + (tid >> 5), n - 1) * CB + (tid & 31)];
         __syncthreads();
         double acc = 0.0;
-        if (c < nb)
+        if (c < nb) {
+#pragma unroll 8
             for (int row = k0 + nb + g; row < n; row += 32) acc += A[(size_t)row * n + k0 + c] * s_x[row];
+        }
         s_part[c][g] = acc;
         __syncthreads();
         if (tid < CB) {
@@ -1529,8 +1584,12 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
             if (mx_chunks > 0) hipLaunchKernelGGL(k_schur_chunks, gx((mx_chunks * 64 + 255) / 256), dim3(256), 0, ctx->stream, d_dev);
             hipLaunchKernelGGL(k_schur_pairs, gx((mx_pairs * 64 + 255) / 256), dim3(256), 0, ctx->stream, d_dev);
             hipLaunchKernelGGL(k_bschur, gx(mx_nhp), dim3(256), 0, ctx->stream, d_dev);
-            for (int jb = 0; jb < mx_red; jb++)  // row blocks at and below the diagonal block
+            for (int jb = 0; jb < mx_red; jb++) {  // row blocks at and below the diagonal block
                 hipLaunchKernelGGL(k_chol_col, gx(mx_red - jb), dim3(256), 0, ctx->stream, d_dev, jb);
+                const int m = mx_red - jb - 1;
+                if (large && m > 0)
+                    hipLaunchKernelGGL(k_chol_trail, gx(m * (m + 1) / 2), dim3(256), 0, ctx->stream, d_dev, jb);
+            }
             hipLaunchKernelGGL(k_chol_back, yb, dim3(1024), 0, ctx->stream, d_dev);
             if (large) hipLaunchKernelGGL(k_chol_back_large, yb, dim3(1024), 0, ctx->stream, d_dev);
         }
