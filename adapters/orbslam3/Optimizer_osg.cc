@@ -1,5 +1,6 @@
 // Optimizer_osg.cc — drop-in bodies for Optimizer::PoseOptimization, the g2o part of
-// Optimizer::LocalBundleAdjustment and Optimizer::BundleAdjustment (global BA) on the MI355X path (ORB-SLAM3 tree built with -DORB_SLAM3_OSG;
+// Optimizer::LocalBundleAdjustment (both overloads) and Optimizer::BundleAdjustment (global BA) on the
+// MI355X path (ORB-SLAM3 tree built with -DORB_SLAM3_OSG;
 // see INTEGRATION.md).  Signatures: ref:include/Optimizer.h:54-90.
 #include "Optimizer.h"
 #include "osg_hooks_orbslam3.h"
@@ -41,6 +42,16 @@ void Optimizer::BundleAdjustment(const std::vector<KeyFrame *> &vpKFs, const std
     auto out = osg_orbslam3::bundle_adjustment<OsgHooks>(vpKFs, vpMP, pMap->GetInitKFid(), nIterations, pbStopFlag,
                                                          bRobust);
     osg_orbslam3::apply_bundle_adjustment<OsgHooks>(out, nLoopKF, nLoopKF == pMap->GetOriginKF()->mnId);
+}
+
+void Optimizer::LocalBundleAdjustment(KeyFrame *pMainKF, std::vector<KeyFrame *> vpAdjustKF,
+                                      std::vector<KeyFrame *> vpFixedKF, bool *pbStopFlag)
+{  // ref:src/Optimizer.cc:5211-5672 (LoopClosing's map merge)
+    auto out = osg_orbslam3::merge_local_bundle_adjustment<OsgHooks, KeyFrame, MapPoint>(pMainKF, vpAdjustKF, vpFixedKF,
+                                                                                        pbStopFlag);
+    if (out.aborted) return;  // :5444-5446
+    std::unique_lock<std::mutex> lock(pMainKF->GetMap()->mMutexMapUpdate);  // :5551
+    osg_orbslam3::apply_merge_local_bundle_adjustment<OsgHooks>(out);
 }
 
 }  // namespace ORB_SLAM3

@@ -1178,5 +1178,215 @@ void apply_bundle_adjustment(const GbaOutcome<KeyFrameT, MapPointT> &o, unsigned
     }
 }
 
+// ------------------------------------------ §8(f) rank 4: the map-merge window BA (the g2o part)
+// Optimizer::LocalBundleAdjustment(pMainKF, vpAdjustKF, vpFixedKF, pbStopFlag)
+// (ref:src/Optimizer.cc:5211-5672), LoopClosing's merge.  Vertices: vpFixedKF (fixed) then
+// vpAdjustKF, each non-bad and in pMainKF's map (a KeyFrame listed twice keeps its first, fixed
+// vertex, as g2o's addVertex does), with their MapPoints (GetMapPoints() set order, deduplicated by
+// mnBALocalForMerge, which is set on both as the reference does); edges per MapPoint in observation
+// map order, mono or stereo by mvuRight, Huber sqrt(5.99) / sqrt(7.815).  Two passes through the C
+// ABI: optimize(5) with the kernels; then (unless stopped) level-1 marking by chi2 / depth, every
+// kernel dropped and a fresh optimize(10) over the level-0 edges; the final classification reads
+// the level-1 edges' first-pass chi2 and the final depth.
+template <class KeyFrameT, class MapPointT>
+struct MergeLbaOutcome {
+    std::vector<std::pair<KeyFrameT *, MapPointT *>> to_erase;        // vToErase, mono edges then stereo
+    std::vector<std::pair<KeyFrameT *, std::vector<double>>> poses;   // vpAdjustKF (7)
+    std::vector<std::pair<MapPointT *, std::vector<double>>> points;  // vpMPs (3)
+    bool aborted = false;                                             // stopped before the first pass
+};
+
+inline bool depth_positive_se3(const double *q, const double *X)
+{  // SE3Quat::map(X).z > 0 (Eigen's quaternion-vector product)
+    const double uv[3] = {2 * (q[1] * X[2] - q[2] * X[1]), 2 * (q[2] * X[0] - q[0] * X[2]), 2 * (q[0] * X[1] - q[1] * X[0])};
+    return X[2] + q[3] * uv[2] + (q[0] * uv[1] - q[1] * uv[0]) + q[6] > 0;
+}
+
+template <class H, class KeyFrameT, class MapPointT>
+MergeLbaOutcome<KeyFrameT, MapPointT> merge_local_bundle_adjustment(KeyFrameT *pMainKF,
+                                                                    const std::vector<KeyFrameT *> &vpAdjustKF,
+                                                                    const std::vector<KeyFrameT *> &vpFixedKF,
+                                                                    bool *pbStopFlag)
+{
+    osg_ctx *ctx = thread_ctx();
+    MergeLbaOutcome<KeyFrameT, MapPointT> out;
+    const auto *pCurrentMap = pMainKF->GetMap();
+    const unsigned long mark = pMainKF->mnId;
+    std::vector<std::pair<unsigned long, KeyFrameT *>> kfs;
+    std::unordered_map<KeyFrameT *, int> kf_fixed;
+    std::vector<MapPointT *> vpMPs;
+    unsigned long maxKFid = 0;
+    auto take = [&](KeyFrameT *k, bool fixed) {  // :5242-5315
+        if (k->isBad() || k->GetMap() != pCurrentMap) return;
+        k->mnBALocalForMerge = mark;
+        if (kf_fixed.count(k)) return;
+        kf_fixed[k] = fixed;
+        kfs.push_back({k->mnId, k});
+        maxKFid = std::max(maxKFid, (unsigned long)k->mnId);
+        for (MapPointT *p : k->GetMapPoints())
+            if (p && !p->isBad() && p->GetMap() == pCurrentMap && p->mnBALocalForMerge != mark) {
+                vpMPs.push_back(p);
+                p->mnBALocalForMerge = mark;
+            }
+    };
+    for (auto *k : vpFixedKF) take(k, true);
+    for (auto *k : vpAdjustKF) take(k, false);
+    std::sort(kfs.begin(), kfs.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+    std::unordered_map<KeyFrameT *, int> kf_index;
+    std::vector<double> pose(7 * kfs.size());
+    std::vector<uint8_t> fixed(kfs.size());
+    std::vector<osg_camera> cams(kfs.size());
+    for (size_t i = 0; i < kfs.size(); i++) {
+        kf_index[kfs[i].second] = (int)i;
+        H::pose(*kfs[i].second, &pose[7 * i]);
+        fixed[i] = (uint8_t)kf_fixed[kfs[i].second];
+        H::camera(*kfs[i].second, false, cams[i]);
+    }
+    // MapPoints (every non-bad one is a vertex, :5347-5358) in g2o id order
+    std::vector<std::pair<unsigned long, MapPointT *>> mps;
+    for (auto *p : vpMPs)
+        if (!p->isBad()) mps.push_back({p->mnId, p});
+    std::sort(mps.begin(), mps.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+    std::unordered_map<MapPointT *, int> mp_index;
+    std::vector<double> point(3 * mps.size());
+    for (size_t j = 0; j < mps.size(); j++) {
+        mp_index[mps[j].second] = (int)j;
+        H::world_pos(mps[j].second, &point[3 * j]);
+    }
+    std::vector<int32_t> e_point, e_pose, e_cam;
+    std::vector<int8_t> e_kind;
+    std::vector<double> e_obs;
+    std::vector<float> e_isig;
+    std::vector<std::pair<KeyFrameT *, MapPointT *>> e_pair;
+    for (auto *pMP : vpMPs) {  // :5347-5442
+        if (pMP->isBad()) continue;
+        for (const auto &ob : pMP->GetObservations()) {
+            KeyFrameT *pKF = ob.first;
+            const int li = std::get<0>(ob.second);
+            if (pKF->isBad() || pKF->mnId > maxKFid || pKF->mnBALocalForMerge != mark || li < 0 || !pKF->GetMapPoint(li))
+                continue;
+            const auto itk = kf_index.find(pKF);
+            if (itk == kf_index.end()) continue;
+            const auto &kp = pKF->mvKeysUn[li];
+            const bool mono = pKF->mvuRight[li] < 0;
+            e_point.push_back(mp_index[pMP]);
+            e_pose.push_back(itk->second);
+            e_kind.push_back(mono ? OSG_EDGE_MONO : OSG_EDGE_STEREO);
+            e_cam.push_back(itk->second);
+            e_obs.push_back(kp.pt.x);
+            e_obs.push_back(kp.pt.y);
+            e_obs.push_back(mono ? 0.0 : pKF->mvuRight[li]);
+            e_isig.push_back(pKF->mvInvLevelSigma2[kp.octave]);
+            e_pair.push_back({pKF, pMP});
+        }
+    }
+    if (pbStopFlag && *pbStopFlag) {  // :5444-5446
+        out.aborted = true;
+        return out;
+    }
+    const size_t ne = e_kind.size();
+    auto pass = [&](const std::vector<size_t> &edges, const std::vector<uint8_t> &robust, int iters,
+                    const std::vector<double> &p_in, const std::vector<double> &x_in, std::vector<double> &p_out,
+                    std::vector<double> &x_out, std::vector<uint8_t> &bad, std::vector<double> &chi2) {
+        std::vector<int32_t> ep, eo, ec;
+        std::vector<int8_t> ek;
+        std::vector<double> eobs;
+        std::vector<float> eis;
+        for (size_t e : edges) {
+            ep.push_back(e_point[e]);
+            eo.push_back(e_pose[e]);
+            ec.push_back(e_cam[e]);
+            ek.push_back(e_kind[e]);
+            eobs.insert(eobs.end(), &e_obs[3 * e], &e_obs[3 * e] + 3);
+            eis.push_back(e_isig[e]);
+        }
+        osg_ba_graph g{};
+        g.n_poses = (int32_t)kfs.size();
+        g.pose = p_in.data();
+        g.pose_fixed = fixed.data();
+        g.n_points = (int32_t)mps.size();
+        g.point = x_in.data();
+        g.n_edges = (int32_t)edges.size();
+        g.e_point = ep.data();
+        g.e_pose = eo.data();
+        g.e_kind = ek.data();
+        g.e_cam = ec.data();
+        g.e_obs = eobs.data();
+        g.e_inv_sigma2 = eis.data();
+        g.n_cams = (int32_t)cams.size();
+        g.cams = cams.data();
+        g.iterations = iters;
+        g.e_robust = robust.data();
+        g.huber_mono = (float)std::sqrt(5.99);   // const float thHuber2D = sqrt(5.99), :5338
+        g.huber_stereo = (float)std::sqrt(7.815);
+        p_out.resize(p_in.size());
+        x_out.resize(x_in.size());
+        bad.assign(edges.size(), 0);
+        chi2.assign(edges.size(), 0.0);
+        osg_ba_result r{};
+        r.pose = p_out.data();
+        r.point = x_out.data();
+        r.edge_bad = bad.data();
+        r.edge_chi2 = chi2.data();
+        check(ctx, osg_bundle_adjustment(ctx, &g, &r, reinterpret_cast<const volatile uint8_t *>(pbStopFlag)),
+              "osg_bundle_adjustment");
+    };
+    std::vector<size_t> all(ne);
+    for (size_t e = 0; e < ne; e++) all[e] = e;
+    std::vector<double> p1, x1, p2, x2, chi1, chi2;
+    std::vector<uint8_t> bad1, bad2;
+    pass(all, std::vector<uint8_t>(ne, 1), 5, pose, point, p1, x1, bad1, chi1);  // :5448-5449
+    std::vector<uint8_t> skip(ne), bad(ne, 0);
+    for (size_t e = 0; e < ne; e++) skip[e] = e_pair[e].second->isBad();
+    const double *pf = p1.data(), *xf = x1.data();
+    if (!(pbStopFlag && *pbStopFlag)) {  // bDoMore, :5451-5498
+        std::vector<size_t> keep;
+        std::vector<uint8_t> rob;
+        for (size_t e = 0; e < ne; e++)
+            if (skip[e] || !bad1[e]) {  // level 0; a bad MapPoint's edges keep their kernel
+                keep.push_back(e);
+                rob.push_back(skip[e]);
+            }
+        pass(keep, rob, 10, p1, x1, p2, x2, bad2, chi2);
+        for (size_t i = 0; i < keep.size(); i++) bad[keep[i]] = bad2[i];
+        for (size_t e = 0; e < ne; e++)
+            if (!skip[e] && bad1[e]) {  // level 1: the first pass's chi2, the final depth
+                const double th = e_kind[e] == OSG_EDGE_STEREO ? 7.815 : 5.991;
+                bad[e] = chi1[e] > th || !depth_positive_se3(&p2[7 * e_pose[e]], &x2[3 * e_point[e]]);
+            }
+        pf = p2.data();
+        xf = x2.data();
+    } else {
+        bad = bad1;
+    }
+    for (int kind : {OSG_EDGE_MONO, OSG_EDGE_STEREO})  // :5506-5546, vToErase order
+        for (size_t e = 0; e < ne; e++)
+            if (e_kind[e] == kind && !skip[e] && bad[e]) out.to_erase.push_back(e_pair[e]);
+    for (auto *k : vpAdjustKF) {  // :5592-5660
+        const auto it = kf_index.find(k);
+        if (k->isBad() || it == kf_index.end()) continue;
+        out.poses.push_back({k, std::vector<double>(pf + 7 * it->second, pf + 7 * it->second + 7)});
+    }
+    for (auto *p : vpMPs) {  // :5663-5671
+        if (p->isBad()) continue;
+        const int j = mp_index[p];
+        out.points.push_back({p, std::vector<double>(xf + 3 * j, xf + 3 * j + 3)});
+    }
+    return out;
+}
+
+// Applies a MergeLbaOutcome as ref:src/Optimizer.cc:5550-5671 does; the caller holds the map's
+// mMutexMapUpdate.
+template <class H, class KeyFrameT, class MapPointT>
+void apply_merge_local_bundle_adjustment(const MergeLbaOutcome<KeyFrameT, MapPointT> &o)
+{
+    for (const auto &km : o.to_erase) {
+        km.first->EraseMapPointMatch(km.second);
+        km.second->EraseObservation(km.first);
+    }
+    for (const auto &kp : o.poses) H::set_pose(*kp.first, kp.second.data());
+    for (const auto &mp : o.points) H::set_world_pos(mp.first, mp.second.data());
+}
+
 }  // namespace osg_orbslam3
 #endif

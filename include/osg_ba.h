@@ -108,6 +108,8 @@ typedef struct osg_ba_result {
     double chi2_initial;       /* activeRobustChi2 before the first iteration */
     double chi2_final;         /* activeRobustChi2 of the accepted state */
     int32_t aborted;           /* stop flag observed */
+    double *edge_chi2;         /* optional (NULL: not written): per edge e'Ωe of its last computed error, the
+                                  e->chi2() the classification reads (the merge BA's second pass needs it) */
 } osg_ba_result;
 
 /* stop_flag: the reference's bool *pbStopFlag read as one byte (nonzero = stop), polled between LM

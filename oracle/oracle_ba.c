@@ -1065,6 +1065,8 @@ int oracle_local_bundle_adjustment(const osg_ba_graph *G, osg_ba_result *R, cons
         R->aborted = 1;
         R->trials = 0;
         for (int i = 0; i < G->n_edges; i++) R->edge_bad[i] = 0;
+        if (R->edge_chi2)
+            for (int i = 0; i < G->n_edges; i++) R->edge_chi2[i] = 0.0;
         memcpy(R->pose, G->pose, sizeof(double) * 7 * G->n_poses);
         memcpy(R->point, G->point, sizeof(double) * 3 * G->n_points);
         g_free(&g);
@@ -1093,6 +1095,7 @@ int oracle_local_bundle_adjustment(const osg_ba_graph *G, osg_ba_result *R, cons
         const edge_t *e = &g.edges[i];
         const double th = (e->kind == OSG_EDGE_STEREO) ? 7.815 : 5.991;
         R->edge_bad[i] = (edge_chi2(e) > th || !edge_depth_positive(e, g.poses, g.points)) ? 1 : 0;
+        if (R->edge_chi2) R->edge_chi2[i] = edge_chi2(e);
     }
     for (int i = 0; i < G->n_poses; i++) se3_get(&g.poses[i], R->pose + 7 * i);
     memcpy(R->point, g.points, sizeof(double) * 3 * G->n_points);

@@ -148,7 +148,7 @@ class OsgBaGraph(C.Structure):
 class OsgBaResult(C.Structure):
     _fields_ = [
         ("pose", P), ("point", P), ("edge_bad", P), ("iterations", i32), ("trials", i32),
-        ("chi2_initial", f64), ("chi2_final", f64), ("aborted", i32),
+        ("chi2_initial", f64), ("chi2_final", f64), ("aborted", i32), ("edge_chi2", P),
     ]
 
 

@@ -94,6 +94,7 @@ struct LbaDev {
     LbaCtl *ctl;                         // per-step control, written by the host each step
     double *out;                         // per-step results (k_step_reduce)
     uint8_t *bad;                        // classification
+    double *chi2o;                       // per edge chi2 of the last computed error (classification)
     double *err;                         // 3 per edge
     double *J;                           // EC per edge: quadratic-form contributions
     double *Hll, *bl, *Hpl, *Hpp, *bp;
@@ -1059,7 +1060,9 @@ __global__ __launch_bounds__(EB) void k_classify(const LbaDev *__restrict__ Ds)
     const double th = (k == OSG_EDGE_STEREO) ? 7.815 : 5.991;
     const SE3 T = se3_from7(poses + 7 * (size_t)D.e_pose[e]);
     const bool pos = edge_depth_positive(k, D.cams[D.e_cam[e]], T, points + 3 * (size_t)D.e_point[e]);
-    bad[e] = (chi2_of(ev, dim, edge_w(D, e)) > th || !pos) ? 1 : 0;
+    const double c2 = chi2_of(ev, dim, edge_w(D, e));
+    bad[e] = (c2 > th || !pos) ? 1 : 0;
+    D.chi2o[e] = c2;
 }
 
 // The step's scalars per graph, summed in the host's former order (sequential from index 0):
@@ -1335,6 +1338,7 @@ void carve_state(char *base, size_t &off, const LbaHost &H, LbaDev *D, bool prof
     double *Linv = carve<double>(base, off, (size_t)sp * CB);
     int *flag = carve<int>(base, off, 16);
     unsigned long long *ts = prof_ts ? carve<unsigned long long>(base, off, 8 * 2 * 64 + 64) : nullptr;
+    double *chi2o = carve<double>(base, off, (size_t)std::max(ne, 1));
     uint8_t *bad = carve<uint8_t>(base, off, ne);
     if (!D) return;
     D->poseA = pA;
@@ -1361,6 +1365,7 @@ void carve_state(char *base, size_t &off, const LbaHost &H, LbaDev *D, bool prof
     D->flag = flag;
     D->tstamp = ts;
     D->bad = bad;
+    D->chi2o = chi2o;
 }
 
 int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, int B, const volatile uint8_t *stop)
@@ -1385,6 +1390,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         std::memcpy(R->pose, G->pose, sizeof(double) * 7 * G->n_poses);
         std::memcpy(R->point, G->point, sizeof(double) * 3 * G->n_points);
         if (G->n_edges > 0) std::memset(R->edge_bad, 0, G->n_edges);
+        if (R->edge_chi2)
+            for (int e = 0; e < G->n_edges; e++) R->edge_chi2[e] = 0.0;
     }
     if (stop && *stop) {  // ref:src/Optimizer.cc:2112-2114
         for (int b = 0; b < B; b++) results[b].aborted = 1;
@@ -1737,6 +1744,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         OSG_HIP_CHECK(ctx, hipMemcpyAsync(R->point, h.sel ? D.pointB : D.pointA, 24 * (size_t)h.npt,
                                           hipMemcpyDeviceToHost, ctx->stream));
         OSG_HIP_CHECK(ctx, hipMemcpyAsync(R->edge_bad, D.bad, h.ne, hipMemcpyDeviceToHost, ctx->stream));
+        if (R->edge_chi2 && h.ne > 0)
+            OSG_HIP_CHECK(ctx, hipMemcpyAsync(R->edge_chi2, D.chi2o, 8 * (size_t)h.ne, hipMemcpyDeviceToHost, ctx->stream));
     }
     OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
     if (prof)

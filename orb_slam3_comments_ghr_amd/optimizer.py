@@ -9,7 +9,7 @@ given directly as those arrays.
 from __future__ import annotations
 
 import ctypes as C
-from dataclasses import dataclass, field
+from dataclasses import dataclass, field, replace
 
 import numpy as np
 
@@ -218,6 +218,7 @@ class BAResult:
     chi2_initial: float
     chi2_final: float
     aborted: int
+    edge_chi2: np.ndarray | None = None   # e->chi2() of each edge's last computed error
 
 
 def run_pose(fn, problems, handle=None):
@@ -235,12 +236,17 @@ def run_pose(fn, problems, handle=None):
 
 
 def make_ba_result(G: BAGraph):
+    """(osg_ba_result, its output arrays): pose, point, edge_bad, edge_chi2."""
     R = _abi.OsgBaResult()
-    pose = np.zeros_like(G.pose)
-    point = np.zeros_like(G.point)
-    bad = np.zeros(len(G.e_point), np.uint8)
-    R.pose, R.point, R.edge_bad = _p(pose), _p(point), _p(bad)
-    return R, pose, point, bad
+    out = (np.zeros_like(G.pose), np.zeros_like(G.point), np.zeros(len(G.e_point), np.uint8),
+           np.zeros(len(G.e_point), np.float64))
+    R.pose, R.point, R.edge_bad, R.edge_chi2 = (_p(a) for a in out)
+    return R, out
+
+
+def finish_ba_result(R, out) -> "BAResult":
+    pose, point, bad, chi2 = out
+    return BAResult(pose, point, bad, R.iterations, R.trials, R.chi2_initial, R.chi2_final, R.aborted, chi2)
 
 
 class Optimizer:
@@ -261,29 +267,34 @@ class Optimizer:
 
     def LocalBundleAdjustment(self, G: BAGraph, stop_flag: np.ndarray | None = None) -> BAResult:
         lib, h = self.ctx.lib, self.ctx.handle
-        R, pose, point, bad = make_ba_result(G)
+        R, out = make_ba_result(G)
         gs = G.struct()
         if stop_flag is not None:
             assert stop_flag.dtype == np.uint8, "stop flag is one byte (bool *pbStopFlag)"
         sf = None if stop_flag is None else _p(stop_flag)
         rc = lib.osg_local_bundle_adjustment(h, C.byref(gs), C.byref(R), sf)
         self.ctx.check(rc, "LocalBundleAdjustment")
-        return BAResult(pose, point, bad, R.iterations, R.trials, R.chi2_initial, R.chi2_final, R.aborted)
+        return finish_ba_result(R, out)
 
     def BundleAdjustment(self, G: BAGraph, stop_flag: np.ndarray | None = None) -> BAResult:
         """The g2o part of ``Optimizer::BundleAdjustment`` (global BA, ref:src/Optimizer.cc:2850-3237):
         ``G`` built as the reference builds it (``synth_gba_graph`` / the adapter), optimize(G.iterations).
         The reference reads no outlier flags after a global BA; ``edge_bad`` is informational."""
         lib, h = self.ctx.lib, self.ctx.handle
-        R, pose, point, bad = make_ba_result(G)
+        R, out = make_ba_result(G)
         gs = G.struct()
         if stop_flag is not None:
             assert stop_flag.dtype == np.uint8, "stop flag is one byte (bool *pbStopFlag)"
         sf = None if stop_flag is None else _p(stop_flag)
         self.ctx.check(lib.osg_bundle_adjustment(h, C.byref(gs), C.byref(R), sf), "BundleAdjustment")
-        return BAResult(pose, point, bad, R.iterations, R.trials, R.chi2_initial, R.chi2_final, R.aborted)
+        return finish_ba_result(R, out)
 
     GlobalBundleAdjustemnt = BundleAdjustment  # the reference's spelling (ref:include/Optimizer.h)
+
+    def LocalBundleAdjustmentMerge(self, G: BAGraph, stop_flag: np.ndarray | None = None, mp_bad=None):
+        """``LocalBundleAdjustment(pMainKF, vpAdjustKF, vpFixedKF, pbStopFlag)`` — the map-merge window BA
+        (ref:src/Optimizer.cc:5211-5672): two g2o passes on the GPU, see merge_local_bundle_adjustment."""
+        return merge_local_bundle_adjustment(G, lambda g, s: self.BundleAdjustment(g, stop_flag=s), stop_flag, mp_bad)
 
     def LocalBundleAdjustmentBatch(self, graphs, stop_flag: np.ndarray | None = None) -> list:
         """B independent windows in lockstep, one launch per kernel per LM trial for all of them
@@ -298,10 +309,7 @@ class Optimizer:
         sf = None if stop_flag is None else _p(stop_flag)
         rc = lib.osg_local_bundle_adjustment_batch(h, C.addressof(gs), B, C.addressof(rs), sf)
         self.ctx.check(rc, "LocalBundleAdjustment batch")
-        out = []
-        for (R0, pose, point, bad), R in zip(made, rs):
-            out.append(BAResult(pose, point, bad, R.iterations, R.trials, R.chi2_initial, R.chi2_final, R.aborted))
-        return out
+        return [finish_ba_result(R, m[1]) for m, R in zip(made, rs)]
 
 
 # ----------------------------------------------------------------------------- generators
@@ -463,3 +471,48 @@ def synth_gba_graph(rng, n_kf=120, n_points=20000, bRobust=False, iterations=10,
                         arc_deg=kw.pop("arc_deg", 120.0), **kw)
     G.iterations = iterations
     return gba_robust_settings(G, bRobust)
+
+
+def depth_positive(G: BAGraph, pose, point, edges):
+    """isDepthPositive of the given edges: z of SE3Quat::map(X) = q X q* + t (Eigen's quaternion-vector
+    product), > 0."""
+    q = np.asarray(pose, np.float64).reshape(-1, 7)[G.e_pose[edges]]
+    X = np.asarray(point, np.float64).reshape(-1, 3)[G.e_point[edges]]
+    u, w = q[:, :3], q[:, 3:4]
+    uv = 2.0 * np.cross(u, X)
+    return (X + w * uv + np.cross(u, uv) + q[:, 4:7])[:, 2] > 0
+
+
+def merge_local_bundle_adjustment(G: BAGraph, run, stop_flag=None, mp_bad=None):
+    """The g2o part of Optimizer::LocalBundleAdjustment(pMainKF, vpAdjustKF, vpFixedKF, pbStopFlag)
+    (ref:src/Optimizer.cc:5211-5672) on a graph gathered as it builds it: mono / stereo edges (no
+    right-camera edges), BundleAdjustment's Huber deltas, vpFixedKF fixed.  ``run(graph, stop_flag)`` is
+    one g2o optimize through the C ABI (Optimizer.BundleAdjustment; the oracle in tests):
+      1. optimize(5) with Huber on every edge (:5448-5449);
+      2. unless stopped: edges with chi2 > 5.991 / 7.815 or behind the camera go to level 1, every kernel
+         is dropped (edges of bad MapPoints are skipped by both steps), and a fresh LM optimize(10) runs on
+         the level-0 edges (:5451-5498);
+      3. the final classification (:5506-5546): level-0 edges by their second-pass errors, level-1 edges by
+         their first-pass chi2 (never recomputed) and the final depth.
+    Returns (pose, point, erase flag per edge, stopped before the first pass)."""
+    ne = len(G.e_point)
+    mp_bad = np.zeros(len(G.point), bool) if mp_bad is None else np.asarray(mp_bad, bool)
+    if stop_flag is not None and stop_flag[0]:  # :5444-5446: return before optimising
+        return G.pose.copy(), G.point.copy(), np.zeros(ne, np.uint8), True
+    G1 = gba_robust_settings(replace(G, iterations=5), True)
+    r1 = run(G1, stop_flag)
+    skip = mp_bad[G.e_point]
+    if stop_flag is not None and stop_flag[0]:  # bDoMore = false: the first pass's classification
+        return r1.pose, r1.point, (r1.edge_bad.astype(bool) & ~skip).astype(np.uint8), False
+    level1 = r1.edge_bad.astype(bool) & ~skip
+    keep = np.nonzero(~level1)[0]
+    G2 = BAGraph(r1.pose, G.pose_fixed, r1.point, G.e_point[keep], G.e_pose[keep], G.e_kind[keep], G.e_cam[keep],
+                 G.e_obs[keep], G.e_inv_sigma2[keep], G.cams, iterations=10, e_robust=skip[keep].astype(np.uint8),
+                 huber_mono=G1.huber_mono, huber_stereo=G1.huber_stereo)
+    r2 = run(G2, stop_flag)
+    bad = np.zeros(ne, bool)
+    bad[keep] = r2.edge_bad.astype(bool)
+    l1 = np.nonzero(level1)[0]
+    th = np.where(G.e_kind[l1] == _abi.EDGE_STEREO, 7.815, 5.991)
+    bad[l1] = (r1.edge_chi2[l1] > th) | ~depth_positive(G, r2.pose, r2.point, l1)
+    return r2.pose, r2.point, (bad & ~skip).astype(np.uint8), False

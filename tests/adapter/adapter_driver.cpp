@@ -1,7 +1,7 @@
 // adapter_driver.cpp — runs adapters/orbslam3/osg_orbslam3.h on mock ORB-SLAM3 objects built from
 // arrays written by tests/test_adapter.py, and writes the adapter's results back (test-only).
 //
-//   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba fuse fuse_sim3 triang distinct sim3 sim3_kfs init stereo gba
+//   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba fuse fuse_sim3 triang distinct sim3 sim3_kfs init stereo gba merge_lba
 //
 // Array file: repeated {u32 name_len, name, u8 dtype ('b' u8, 'i' i32, 'f' f32, 'd' f64), u64 count,
 // data}.
@@ -308,6 +308,7 @@ static void build_ba_world(const Arrays &in, Map &map, Camera &c, std::vector<Ke
     }
     for (int j = 0; j < npt; j++) {
         mp[j].mnId = (unsigned long)j;
+        mp[j].map = &map;
         std::memcpy(mp[j].pos, get(in, "G.point").p<double>() + 3 * j, 24);
     }
     for (int e = 0; e < ne; e++) {
@@ -526,6 +527,33 @@ int main(int argc, char **argv)
             out["point"] = make('d', point);
             out["edge_bad"] = make('b', bad);
             out["num_edges"] = make('i', std::vector<int32_t>{o.num_edges});
+        } else if (mode == "merge_lba") {
+            // the "lba" arrays; params: n_fixed stop.  vpFixedKF = KeyFrames [0, n_fixed), vpAdjustKF the
+            // rest, pMainKF the last; out: poses, points, the erased (KeyFrame, MapPoint) pairs in order
+            const int np = (int)(get(in, "G.pose").n / 7), npt = (int)(get(in, "G.point").n / 3);
+            Camera c;
+            Map map;
+            std::vector<KeyFrame> kf;
+            std::vector<MapPoint> mp;
+            build_ba_world(in, map, c, kf, mp);
+            std::vector<KeyFrame *> fixedk, adjust;
+            for (int i = 0; i < np; i++) (i < (int)prm[0] ? fixedk : adjust).push_back(&kf[i]);
+            bool stop = prm[1] != 0;
+            auto o = osg_orbslam3::merge_local_bundle_adjustment<MockHooks, KeyFrame, MapPoint>(&kf[np - 1], adjust,
+                                                                                             fixedk, &stop);
+            std::vector<int32_t> erased;
+            for (auto &km : o.to_erase) {
+                erased.push_back((int32_t)(km.first - kf.data()));
+                erased.push_back((int32_t)(km.second - mp.data()));
+            }
+            if (!o.aborted) osg_orbslam3::apply_merge_local_bundle_adjustment<MockHooks>(o);
+            std::vector<double> pose(7 * (size_t)np), point(3 * (size_t)npt);
+            for (int i = 0; i < np; i++) std::memcpy(&pose[7 * i], kf[i].pose, 56);
+            for (int j = 0; j < npt; j++) std::memcpy(&point[3 * j], mp[j].pos, 24);
+            out["pose"] = make('d', pose);
+            out["point"] = make('d', point);
+            out["erased"] = make('i', erased);
+            out["aborted"] = make('i', std::vector<int32_t>{(int32_t)o.aborted});
         } else if (mode == "gba") {
             // the "lba" arrays; params: nIterations bRobust nLoopKF.  KeyFrame 0 is the map's init and
             // origin KeyFrame: nLoopKF 0 writes into the map, anything else into mTcwGBA / mPosGBA

@@ -58,7 +58,9 @@ struct MapPoint {
     float mTrackProjX = 0, mTrackProjY = 0, mTrackDepth = 0, mTrackDepthR = 0, mTrackProjXR = 0, mTrackProjYR = 0;
     bool mbTrackInView = false, mbTrackInViewR = false;
     double pos_gba[3] = {0, 0, 0};  // mPosGBA
-    unsigned long mnBAGlobalForKF = 0;
+    unsigned long mnBAGlobalForKF = 0, mnBALocalForMerge = 0;
+    Map *map = nullptr;
+    Map *GetMap() const { return map; }
     int mnTrackScaleLevel = 0, mnTrackScaleLevelR = 0;
     float mTrackViewCos = 0, mTrackViewCosR = 0;
     // test-only: what MockHooks::project_last / kf_query return for this MapPoint
@@ -132,7 +134,7 @@ struct KeyFrame {
     std::vector<float> mvScaleFactors, mvLevelSigma2;
     osg_triang_geom triang_geom{};  // test-only: MockHooks::triang_geom
     double pose_gba[7] = {0, 0, 0, 0, 0, 0, 0};  // mTcwGBA
-    unsigned long mnBAGlobalForKF = 0;
+    unsigned long mnBAGlobalForKF = 0, mnBALocalForMerge = 0;
 
     std::vector<MapPoint *> GetMapPointMatches() const { return mvpMapPoints; }
     bool isBad() const { return bad; }

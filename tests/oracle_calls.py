@@ -116,11 +116,11 @@ def pose(oracle, problems):
 
 
 def lba(oracle, G, stop_flag=None):
-    R, pose_, point, bad = op.make_ba_result(G)
+    R, out = op.make_ba_result(G)
     gs = G.struct()
     oracle.oracle_local_bundle_adjustment(C.byref(gs), C.byref(R),
                                           None if stop_flag is None else stop_flag.ctypes.data)
-    return op.BAResult(pose_, point, bad, R.iterations, R.trials, R.chi2_initial, R.chi2_final, R.aborted)
+    return op.finish_ba_result(R, out)
 
 
 def dbow(oracle, voc, desc, levelsup=4):

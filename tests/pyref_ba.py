@@ -400,6 +400,11 @@ def pose_optimization(P):
 def local_bundle_adjustment(G):
     """g2o part of ref:src/Optimizer.cc:1877-2203 on a BAGraph.  Returns (pose (np x 7),
     point (npt x 3), edge_bad, iterations, chi2_initial, chi2_final)."""
+    return local_bundle_adjustment_chi2(G)[:6]
+
+
+def local_bundle_adjustment_chi2(G):
+    """local_bundle_adjustment plus each edge's chi2 of its last computed error (e->chi2())."""
     poses = [Pose(p) for p in np.asarray(G.pose, float).reshape(-1, 7)]
     points = np.asarray(G.point, float).reshape(-1, 3).copy()
     ne = len(G.e_pose)
@@ -427,4 +432,4 @@ def local_bundle_adjustment(G):
     depth_ok = Xc[:, 2] > 0
     th = np.where(E.kind == STEREO, 7.815, 5.991)
     bad = ((E.chi2() > th) | ~depth_ok).astype(np.uint8)
-    return np.stack([p.p7() for p in lm.poses]), lm.points, bad, iters, chi_ini, chi_fin
+    return np.stack([p.p7() for p in lm.poses]), lm.points, bad, iters, chi_ini, chi_fin, E.chi2()

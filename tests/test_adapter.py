@@ -624,3 +624,50 @@ def test_adapter_global_bundle_adjustment(driver, tmp_path, ctx, robust, loop):
     if loop:  # the map itself is untouched until LoopClosing applies the result
         np.testing.assert_array_equal(out["pose"].reshape(-1, 7), G.pose)
         assert (out["ba_for"] == loop).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stereo", [0.0, 0.4])
+def test_adapter_merge_local_bundle_adjustment(driver, tmp_path, ctx, oracle, stereo):
+    """Optimizer::LocalBundleAdjustment(pMainKF, vpAdjustKF, vpFixedKF, pbStopFlag) through the adapter
+    (its own C++ restatement of the two-pass flow) equals the Python flow on the same GPU passes exactly,
+    and the flow with the oracle's passes within the BA tolerances (identical erase sets)."""
+    rng = np.random.default_rng(780 + int(10 * stereo))
+    G = op.gba_robust_settings(op.synth_lba_graph(rng, n_kf=12, n_points=900, n_fixed=4, stereo_frac=stereo,
+                                                  outlier_frac=0.03), True)
+    # the adapter's edge order: vpMPs as collected (fixed KeyFrames, then the adjusted ones; each
+    # KeyFrame's MapPoints ascending, first sighting wins) x each point's observations in KeyFrame order
+    seen, mp_order = set(), []
+    for k in range(len(G.pose)):
+        for p in np.unique(G.e_point[G.e_pose == k]):
+            if p not in seen:
+                seen.add(p)
+                mp_order.append(p)
+    rank = np.empty(len(G.point), np.int64)
+    rank[mp_order] = np.arange(len(mp_order))
+    order = np.lexsort((G.e_pose, rank[G.e_point]))
+    for k in ["e_point", "e_pose", "e_kind", "e_cam", "e_obs", "e_inv_sigma2", "e_robust"]:
+        setattr(G, k, np.ascontiguousarray(getattr(G, k)[order]))
+    G.e_obs = G.e_obs.astype(np.float32).astype(np.float64)
+    arrays = {"G.pose": G.pose.reshape(-1), "G.pose_fixed": G.pose_fixed.astype(np.uint8),
+              "G.point": G.point.reshape(-1), "G.e_point": G.e_point.astype(np.int32),
+              "G.e_pose": G.e_pose.astype(np.int32), "G.e_kind": G.e_kind.astype(np.uint8),
+              "G.e_obs": G.e_obs.reshape(-1), "G.e_inv_sigma2": G.e_inv_sigma2.astype(np.float32),
+              "G.cam": cam_array(G.cams[0]), "params": np.array([4, 0], np.float32)}
+    out = run(driver, tmp_path, "merge_lba", arrays)
+    pose, point, erase, _ = op.Optimizer(ctx).LocalBundleAdjustmentMerge(G)
+    free = G.pose_fixed == 0
+    np.testing.assert_array_equal(out["pose"].reshape(-1, 7)[free], pose[free])
+    np.testing.assert_array_equal(out["point"].reshape(-1, 3), point)
+    mono_first = np.argsort(G.e_kind != 0, kind="stable")  # vToErase: mono edges, then stereo
+    want = np.stack([G.e_pose, G.e_point], 1)[mono_first][erase[mono_first] != 0].reshape(-1)
+    np.testing.assert_array_equal(out["erased"], want)
+    assert erase.sum() >= 5
+    pose_o, point_o, erase_o, _ = op.merge_local_bundle_adjustment(G, lambda g, s: oc.lba(oracle, g))
+    np.testing.assert_array_equal(erase, erase_o)
+    np.testing.assert_allclose(pose, pose_o, atol=1e-6, rtol=0)
+    np.testing.assert_allclose(point, point_o, atol=1e-6, rtol=0)
+    # stopped before the first pass: nothing is written or erased
+    out = run(driver, tmp_path, "merge_lba", {**arrays, "params": np.array([4, 1], np.float32)})
+    assert int(out["aborted"][0]) == 1 and out["erased"].size == 0
+    np.testing.assert_array_equal(out["pose"].reshape(-1, 7), G.pose)

@@ -142,3 +142,27 @@ def test_bundle_adjustment_oracle_vs_numpy(oracle, seed, robust, stereo):
         Gr = op.gba_robust_settings(op.synth_gba_graph(np.random.default_rng(2100 + seed), n_kf=8, n_points=300,
                                                        stereo_frac=stereo), True)
         assert oc.lba(oracle, Gr).chi2_initial < got.chi2_initial
+
+
+def _pyref_run(G, stop):
+    pose, point, bad, iters, chi_ini, chi_fin, chi2 = pr.local_bundle_adjustment_chi2(G)
+    return op.BAResult(pose, point, bad, iters, 0, chi_ini, chi_fin, 0, chi2)
+
+
+@pytest.mark.parametrize("seed,stereo", [(1, 0.0), (2, 0.4)])
+def test_merge_local_bundle_adjustment_oracle_vs_numpy(oracle, seed, stereo):
+    """The map-merge window BA (ref:src/Optimizer.cc:5211-5672): optimize(5) with Huber, level-1 marking,
+    a kernel-free optimize(10) on the level-0 edges, the final classification; the flow run with the
+    oracle's passes equals the flow run with the numpy restatement's (identical erase sets)."""
+    G = op.gba_robust_settings(op.synth_lba_graph(np.random.default_rng(2200 + seed), n_kf=8, n_points=400,
+                                                  n_fixed=3, stereo_frac=stereo, outlier_frac=0.03), True)
+    pose, point, erase, _ = op.merge_local_bundle_adjustment(G, lambda g, s: oc.lba(oracle, g))
+    pose_n, point_n, erase_n, _ = op.merge_local_bundle_adjustment(G, _pyref_run)
+    np.testing.assert_array_equal(erase, erase_n)
+    assert erase.sum() >= 5  # the planted outliers
+    np.testing.assert_allclose(pose, pose_n, atol=STATE_TOL, rtol=0)
+    np.testing.assert_allclose(point, point_n, atol=STATE_TOL, rtol=0)
+    # stopped before the first pass: nothing changes
+    stop = np.ones(1, np.uint8)
+    p0, q0, e0, stopped = op.merge_local_bundle_adjustment(G, lambda g, s: oc.lba(oracle, g), stop_flag=stop)
+    assert stopped and not e0.any() and np.array_equal(p0, G.pose)
