@@ -11,7 +11,7 @@ HIPFLAGS = --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-functio
 EXACT = -ffp-contract=off
 HDRS = include/osg.h include/osg_ba.h $(CSRC)/osg_internal.h
 
-OBJS = $(OBJDIR)/runtime.o $(OBJDIR)/hamming.o $(OBJDIR)/match.o $(OBJDIR)/pose.o $(OBJDIR)/ba.o $(OBJDIR)/dbow.o $(OBJDIR)/fuse.o $(OBJDIR)/triang.o $(OBJDIR)/desc.o $(OBJDIR)/sim3.o $(OBJDIR)/init.o $(OBJDIR)/stereo.o
+OBJS = $(OBJDIR)/runtime.o $(OBJDIR)/hamming.o $(OBJDIR)/match.o $(OBJDIR)/pose.o $(OBJDIR)/ba.o $(OBJDIR)/dbow.o $(OBJDIR)/fuse.o $(OBJDIR)/triang.o $(OBJDIR)/desc.o $(OBJDIR)/sim3.o $(OBJDIR)/init.o $(OBJDIR)/stereo.o $(OBJDIR)/orb.o
 
 all: $(LIB) oracle
 
@@ -47,6 +47,9 @@ $(OBJDIR)/init.o: $(CSRC)/init.hip $(HDRS) $(CSRC)/match_common.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(EXACT) -c $< -o $@
 
 $(OBJDIR)/stereo.o: $(CSRC)/stereo.hip $(HDRS) $(CSRC)/match_common.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) $(EXACT) -c $< -o $@
+
+$(OBJDIR)/orb.o: $(CSRC)/orb.hip $(HDRS) $(CSRC)/match_common.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(EXACT) -c $< -o $@
 
 $(LIB): $(OBJS)

@@ -421,6 +421,30 @@ int osg_compute_distinctive_descriptors(osg_ctx *ctx, const uint8_t *desc, const
 int osg_compute_distinctive_descriptors_dev(osg_ctx *ctx, const void *d_desc, const void *d_start, int32_t n_points,
                                             void *d_best_idx);
 
+/* ---- b8: ORBextractor's per-keypoint stages --------------------------------------------------------
+ * computeOrientation / IC_Angle (ref:src/ORBextractor.cc:89-136, 585-597) on mvImagePyramid[level] and
+ * computeDescriptors / computeOrbDescriptor (ref:src/ORBextractor.cc:148-208, 1534-1545) on the
+ * GaussianBlur'd level (ref:src/ORBextractor.cc:1628-1652), for keypoints in level coordinates (before
+ * :1663-1667 scales them to level 0).  FAST, the octree distribution and the 7x7 Gaussian blur stay
+ * with the caller (OpenCV).  umax: the extractor's umax (HALF_PATCH_SIZE + 1 = 16 entries, each
+ * <= 15); pattern: its 512 points (ORBextractor::pattern) as (x, y) int pairs.  Every pixel a
+ * keypoint reads must lie inside its level image (the reference would read the extractor's border
+ * or past the blurred clone), else OSG_E_INVALID naming the keypoint.  fastAtan2 is OpenCV's (not
+ * in the reference tree: its published polynomial is restated; parity with OpenCV itself
+ * unpinned).  cos / sin of the angle are the host libm's cosf / sinf (the reference's std::cos(float)),
+ * evaluated between the two kernels so that they agree with it bit for bit. */
+typedef struct osg_orb_keypoints {
+    int32_t n;
+    const float *x, *y;           /* level coordinates (KeyPoint::pt before the level scale) */
+    const int32_t *level;         /* KeyPoint::octave */
+} osg_orb_keypoints;
+
+/* angle[n]: written (IC_Angle) when compute_angle, else read (the keypoints' angles in degrees);
+ * desc[n x 32] written. */
+int osg_orb_describe(osg_ctx *ctx, const osg_image_pyramid *raw, const osg_image_pyramid *blurred,
+                     const osg_orb_keypoints *K, const int32_t *pattern, const int32_t *umax, int32_t compute_angle,
+                     float *angle, uint8_t *desc);
+
 /* Diagnostics of the last search call on this context (summed / maxed over a batch): out[0]
  * candidates enumerated, out[1] Jacobi rounds, out[2] problems whose greedy was redone serially (a5 on a two-camera rig when a
  * stereo-partner write by a MapPoint without observations unblocked a slot), out[3] nmatches.

@@ -51,6 +51,12 @@ int oracle_search_for_triangulation(const osg_kf_side *K1, const osg_kf_side *K2
                                     int bOnlyStereo, int bCoarse, int checkOri, int32_t *vMatches12);
 /* Frame::ComputeStereoMatches (oracle_stereo.c): mvuRight / mvDepth out, returns the kept matches */
 int oracle_compute_stereo_matches(const osg_stereo_frame *F, float *mvuRight, float *mvDepth);
+
+/* ORBextractor IC_Angle + computeOrbDescriptor (oracle_orb.c): -1, or the first keypoint whose
+ * reads leave its level */
+float oracle_fast_atan2(float y, float x);
+int oracle_orb_describe(const osg_image_pyramid *raw, const osg_image_pyramid *blurred, const osg_orb_keypoints *K,
+                        const int32_t *pattern, const int32_t *umax, int compute_angle, float *angle, uint8_t *desc);
 void oracle_dbow_transform_batch(const osg_vocabulary_desc *V, const uint8_t *desc, const int32_t *n, int B,
                                  int levelsup, osg_bow_out *out);
 

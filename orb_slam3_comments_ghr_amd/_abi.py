@@ -115,6 +115,10 @@ class OsgStereoFrame(C.Structure):
     ]
 
 
+class OsgOrbKeypoints(C.Structure):
+    _fields_ = [("n", i32), ("x", P), ("y", P), ("level", P)]
+
+
 class OsgCamera(C.Structure):
     _fields_ = [
         ("type", i32), ("p", f32 * 8), ("fx", f32), ("fy", f32), ("cx", f32), ("cy", f32),
@@ -183,7 +187,7 @@ EXPORTS = [
     "osg_compute_distinctive_descriptors", "osg_compute_distinctive_descriptors_dev",
     "osg_search_by_projection_sim3", "osg_search_by_projection_sim3_batch",
     "osg_search_for_initialization", "osg_search_for_initialization_batch",
-    "osg_compute_stereo_matches", "osg_compute_stereo_matches_batch",
+    "osg_compute_stereo_matches", "osg_compute_stereo_matches_batch", "osg_orb_describe",
 ]
 
 
@@ -250,6 +254,8 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.osg_search_for_initialization_batch.argtypes = [vp, vp, vp, i32, vp, C.c_int, f32, C.c_int, vp, vp]
     lib.osg_compute_stereo_matches.argtypes = [vp, C.POINTER(OsgStereoFrame), vp, vp]
     lib.osg_compute_stereo_matches_batch.argtypes = [vp, vp, i32, vp, vp, vp]
+    lib.osg_orb_describe.argtypes = [vp, C.POINTER(OsgImagePyramid), C.POINTER(OsgImagePyramid),
+                                     C.POINTER(OsgOrbKeypoints), vp, vp, i32, vp, vp]
     lib.osg_compute_distinctive_descriptors.argtypes = [vp, vp, vp, i32, vp]
     lib.osg_compute_distinctive_descriptors_dev.argtypes = [vp, vp, vp, i32, vp]
     lib.osg_search_for_triangulation_batch.argtypes = [vp, vp, vp, vp, i32, C.c_int, C.c_int, C.c_int, vp, vp]

@@ -1,0 +1,114 @@
+"""Host mirror of ORBextractor's per-keypoint stages on the C ABI (``osg_orb_describe``, include/osg.h
+b8): computeOrientation / IC_Angle (ref:src/ORBextractor.cc:89-136, 585-597) on mvImagePyramid and
+computeDescriptors / computeOrbDescriptor (ref:src/ORBextractor.cc:148-208, 1534-1545) on the blurred
+levels (ref:src/ORBextractor.cc:1628-1652).  FAST, the octree distribution and the Gaussian blur stay
+with OpenCV; the caller passes the extractor's ``umax`` and ``pattern``.
+
+    angle, desc = ORBDescribe(ctx, raw, blurred, x, y, level, pattern, umax)        # IC_Angle + rBRIEF
+    _, desc = ORBDescribe(ctx, None, blurred, x, y, level, pattern, angle=angle)    # given angles
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import numpy as np
+
+from . import Context, _abi
+from .stereo import ImagePyramid
+
+HALF_PATCH_SIZE = 15
+EDGE_THRESHOLD = 19
+
+
+def ic_umax(half_patch_size: int = HALF_PATCH_SIZE) -> np.ndarray:
+    """The row half-widths of the circular orientation patch, as the ORBextractor constructor builds
+    them (ref:src/ORBextractor.cc:548-575): cvRound(sqrt(hp^2 - v^2)) up to vmax, then mirrored about
+    the diagonal so the patch is symmetric."""
+    hp = half_patch_size
+    r = float(np.float32(hp) * np.float32(math.sqrt(2.0)) / np.float32(2))  # HALF_PATCH_SIZE * sqrt(2.f) / 2
+    vmax, vmin = math.floor(r + 1), math.ceil(r)
+    umax = [0] * (hp + 1)
+    for v in range(vmax + 1):
+        umax[v] = int(np.rint(math.sqrt(hp * hp - v * v)))
+    v0 = 0
+    for v in range(hp, vmin - 1, -1):
+        while umax[v0] == umax[v0 + 1]:
+            v0 += 1
+        umax[v] = v0
+        v0 += 1
+    return np.array(umax, np.int32)
+
+
+def synth_pattern(rng, npoints: int = 512, radius: int = 13) -> np.ndarray:
+    """A BRIEF test pattern of the reference's shape (ORBextractor::pattern: 512 points, 256 pairs,
+    coordinates within +-13).  The real bit_pattern_31_ comes from the caller's extractor."""
+    return rng.integers(-radius, radius + 1, (npoints, 2)).astype(np.int32)
+
+
+def ORBDescribe(ctx: Context, raw, blurred, x, y, level, pattern, umax=None, angle=None):
+    """IC_Angle (when ``angle`` is None) and the 256-bit steered BRIEF descriptor of every keypoint.
+    raw / blurred: ImagePyramid (mvImagePyramid and its GaussianBlur'd levels) or lists of levels;
+    x, y: level coordinates; level: KeyPoint::octave.  Returns (angle float32[n], desc uint8[n, 32])."""
+    x = np.ascontiguousarray(x, np.float32)
+    y = np.ascontiguousarray(y, np.float32)
+    level = np.ascontiguousarray(level, np.int32)
+    n = len(x)
+    assert len(y) == n and len(level) == n
+    pattern = np.ascontiguousarray(pattern, np.int32).reshape(-1)
+    assert pattern.size == 1024, "ORBextractor::pattern: 512 (x, y) points"
+    compute = angle is None
+    if compute:
+        umax = ic_umax() if umax is None else np.ascontiguousarray(umax, np.int32)
+        assert umax.size == HALF_PATCH_SIZE + 1
+        ang = np.zeros(n, np.float32)
+    else:
+        ang = np.array(angle, np.float32).reshape(-1)
+        assert ang.size == n
+    if blurred is not None and not isinstance(blurred, ImagePyramid):
+        blurred = ImagePyramid(blurred)
+    if raw is not None and not isinstance(raw, ImagePyramid):
+        raw = ImagePyramid(raw)
+    assert blurred is not None and (raw is not None or not compute)
+    desc = np.zeros((n, 32), np.uint8)
+    K = _abi.OsgOrbKeypoints(n, x.ctypes.data, y.ctypes.data, level.ctypes.data)
+    rs = raw.struct() if raw is not None else _abi.OsgImagePyramid()
+    bs = blurred.struct()
+    ctx.check(ctx.lib.osg_orb_describe(ctx.handle, C.byref(rs), C.byref(bs), C.byref(K), pattern.ctypes.data,
+                                       umax.ctypes.data if compute else None, int(compute), ang.ctypes.data,
+                                       desc.ctypes.data), "osg_orb_describe")
+    return ang, desc
+
+
+def synth_orb_frame(rng, n=1200, width=752, height=480, n_levels=8, factor=1.2, fractional=False):
+    """A synthetic extractor output of EuRoC shape: per level a smooth random image (raw) and a second
+    one standing in for its blur, and n keypoints spread over the levels in proportion to their area
+    (ref:src/ORBextractor.cc:474-494), EDGE_THRESHOLD px inside each level.  ``fractional`` adds
+    sub-pixel offsets including exact .5 ties (cvRound is round-half-even)."""
+    raw, blur = [], []
+    scale = 1.0
+    areas = []
+    for _ in range(n_levels):
+        w, h = int(round(width / scale)), int(round(height / scale))
+        base = rng.integers(0, 256, (h // 4 + 2, w // 4 + 2)).astype(np.float32)
+        img = np.kron(base, np.ones((4, 4), np.float32))[:h, :w] + rng.normal(0, 12, (h, w))
+        raw.append(np.clip(img, 0, 255).astype(np.uint8))
+        b = img.copy()
+        b[1:-1, 1:-1] = (img[:-2, 1:-1] + img[2:, 1:-1] + img[1:-1, :-2] + img[1:-1, 2:] + 4 * img[1:-1, 1:-1]) / 8
+        blur.append(np.clip(b, 0, 255).astype(np.uint8))
+        areas.append(w * h)
+        scale *= factor
+    share = np.array(areas, np.float64) / sum(areas)
+    level = rng.choice(n_levels, size=n, p=share).astype(np.int32)
+    x = np.empty(n, np.float32)
+    y = np.empty(n, np.float32)
+    for l in range(n_levels):
+        m = level == l
+        h, w = raw[l].shape
+        x[m] = rng.integers(EDGE_THRESHOLD, w - EDGE_THRESHOLD, m.sum())
+        y[m] = rng.integers(EDGE_THRESHOLD, h - EDGE_THRESHOLD, m.sum())
+    if fractional:
+        off = rng.choice(np.array([0.0, 0.25, 0.5, -0.5, 0.75, -0.3], np.float32), size=(2, n))
+        x += off[0]
+        y += off[1]
+    return raw, blur, x, y, level

@@ -1,0 +1,149 @@
+"""ORBextractor's per-keypoint stages: IC_Angle (ref:src/ORBextractor.cc:89-136) and
+computeOrbDescriptor (ref:src/ORBextractor.cc:148-208).  CPU: the C oracle pinned by the pure-Python
+restatement and hand cases (intensity ramps give known angles; at angle 0 a ramp image gives the
+pattern's own x comparison); the umax table of the extractor constructor.  GPU: the HIP path
+bit-exact against the oracle (angle bit patterns and descriptor bytes) on EuRoC-shaped 8-level
+frames, with computed and given angles, fractional / .5-tie coordinates, row-strided host levels,
+device-resident pyramids and the out-of-image error.  fastAtan2 is OpenCV's published polynomial
+(OpenCV is not in the reference tree): parity with OpenCV itself is unpinned, the restatement is
+checked against atan2 to its published accuracy."""
+import math
+
+import numpy as np
+import pytest
+
+from orb_slam3_comments_ghr_amd import orb
+from tests import oracle_calls as oc
+from tests import pyref_orb as po
+
+
+def small_frame(seed, n=40, fractional=True):
+    rng = np.random.default_rng(seed)
+    raw, blur, x, y, level = orb.synth_orb_frame(rng, n=n, width=160, height=120, n_levels=3,
+                                                 fractional=fractional)
+    return rng, raw, blur, x, y, level
+
+
+def test_umax_table():
+    # the constructor's table for HALF_PATCH_SIZE = 15 (symmetric circular patch)
+    assert orb.ic_umax().tolist() == [15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3]
+
+
+def test_fast_atan2_accuracy(oracle):
+    rng = np.random.default_rng(3)
+    for y, x in list(rng.normal(0, 1000, (2000, 2))) + [(0, 0), (0, 5), (5, 0), (-3, 0), (0, -3), (7, 7), (-7, -7)]:
+        a = oracle.oracle_fast_atan2(float(y), float(x))
+        assert a == float(po.fast_atan2(y, x))
+        assert 0.0 <= a < 360.0 or (x == 0 and y == 0)
+        if x or y:
+            ref = math.degrees(math.atan2(y, x)) % 360.0
+            d = abs(a - ref)
+            assert min(d, 360.0 - d) < 0.01
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_oracle_vs_python(oracle, seed):
+    rng, raw, blur, x, y, level = small_frame(seed)
+    pat = orb.synth_pattern(rng)
+    ang, desc, bad = oc.orb_describe(oracle, raw, blur, x, y, level, pat)
+    assert bad == -1
+    um = orb.ic_umax()
+    for k in range(len(x)):
+        a = po.ic_angle(raw[level[k]], x[k], y[k], um)
+        assert np.float32(ang[k]).view(np.int32) == np.float32(a).view(np.int32)
+        np.testing.assert_array_equal(desc[k], po.orb_descriptor(blur[level[k]], x[k], y[k], a, pat))
+    # given angles (computeDescriptors alone)
+    given = rng.uniform(0, 360, len(x)).astype(np.float32)
+    _, d2, bad = oc.orb_describe(oracle, None, blur, x, y, level, pat, angle=given)
+    assert bad == -1
+    for k in range(len(x)):
+        np.testing.assert_array_equal(d2[k], po.orb_descriptor(blur[level[k]], x[k], y[k], given[k], pat))
+
+
+def test_oracle_hand_cases(oracle):
+    h, w = 64, 64
+    ramp_x = np.tile(np.arange(w, dtype=np.uint8) * 3, (h, 1))
+    ramp_y = np.ascontiguousarray(ramp_x.T)
+    pat = orb.synth_pattern(np.random.default_rng(9))
+    x, y, lv = [32.0], [32.0], [0]
+    a, d, bad = oc.orb_describe(oracle, [ramp_x], [ramp_x], x, y, lv, pat)
+    assert bad == -1 and abs(a[0]) < 1e-3        # brighter to the right: angle 0
+    # angle 0: a = 1, b = 0, the tests compare the pattern points' own x coordinates
+    pts = pat.reshape(256, 2, 2)
+    bits = (pts[:, 0, 0] < pts[:, 1, 0]).astype(np.uint8)
+    np.testing.assert_array_equal(np.unpackbits(d[0], bitorder="little"), bits)
+    a, _, _ = oc.orb_describe(oracle, [ramp_y], [ramp_y], x, y, lv, pat)
+    assert abs(a[0] - 90.0) < 1e-3               # brighter downwards (+v): 90 degrees
+    a, _, _ = oc.orb_describe(oracle, [ramp_x[:, ::-1].copy()], [ramp_x], x, y, lv, pat)
+    assert abs(a[0] - 180.0) < 1e-3
+    flat = np.full((h, w), 77, np.uint8)
+    a, d, _ = oc.orb_describe(oracle, [flat], [flat], x, y, lv, pat)
+    assert a[0] == 0.0 and not d.any()           # fastAtan2(0, 0) = 0; equal pixels give 0 bits
+    # a keypoint whose pattern leaves the image: the index of the first such keypoint
+    _, _, bad = oc.orb_describe(oracle, [flat], [flat], [32.0, 3.0], [32.0, 32.0], [0, 0], pat, angle=[0.0, 0.0])
+    assert bad == 1
+
+
+# ---------------------------------------------------------------------------------------------- GPU
+
+def same(a, b):
+    np.testing.assert_array_equal(np.asarray(a[0], np.float32).view(np.int32), np.asarray(b[0], np.float32).view(np.int32))
+    np.testing.assert_array_equal(a[1], b[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,fractional", [(0, False), (1, True), (2, False)])
+def test_gpu_vs_oracle(ctx, oracle, seed, fractional):
+    rng = np.random.default_rng(100 + seed)
+    raw, blur, x, y, level = orb.synth_orb_frame(rng, n=1500, fractional=fractional)
+    pat = orb.synth_pattern(rng)
+    ref = oc.orb_describe(oracle, raw, blur, x, y, level, pat)
+    assert ref[2] == -1
+    same(orb.ORBDescribe(ctx, raw, blur, x, y, level, pat), ref)
+    given = rng.uniform(0, 360, len(x)).astype(np.float32)
+    ref2 = oc.orb_describe(oracle, None, blur, x, y, level, pat, angle=given)
+    got = orb.ORBDescribe(ctx, None, blur, x, y, level, pat, angle=given)
+    same(got, ref2[:2])
+
+
+@pytest.mark.gpu
+def test_gpu_strided_and_device_pyramids(ctx, oracle):
+    rng = np.random.default_rng(7)
+    raw, blur, x, y, level = orb.synth_orb_frame(rng, n=900, fractional=True)
+    pat = orb.synth_pattern(rng)
+    ref = oc.orb_describe(oracle, raw, blur, x, y, level, pat)
+    # ROI views of bordered buffers (the extractor's layout, ref:src/ORBextractor.cc:1692-1700)
+    B = 19
+    def bordered(levels):
+        out = []
+        for lv in levels:
+            big = rng.integers(0, 256, (lv.shape[0] + 2 * B, lv.shape[1] + 2 * B)).astype(np.uint8)
+            big[B:-B, B:-B] = lv
+            out.append(big[B:-B, B:-B])
+        return out
+    same(orb.ORBDescribe(ctx, bordered(raw), bordered(blur), x, y, level, pat), ref[:2])
+    rp, bp = orb.ImagePyramid(raw).to_device(), orb.ImagePyramid(blur).to_device()
+    same(orb.ORBDescribe(ctx, rp, bp, x, y, level, pat), ref[:2])
+
+
+@pytest.mark.gpu
+def test_gpu_edges(ctx, oracle):
+    from orb_slam3_comments_ghr_amd import OsgError
+    rng = np.random.default_rng(11)
+    raw, blur, x, y, level = orb.synth_orb_frame(rng, n=64)
+    pat = orb.synth_pattern(rng)
+    a, d = orb.ORBDescribe(ctx, raw, blur, x[:0], y[:0], level[:0], pat)
+    assert a.shape == (0,) and d.shape == (0, 32)
+    a, d = orb.ORBDescribe(ctx, raw, blur, x[:1], y[:1], level[:1], pat)    # one keypoint
+    same((a, d), oc.orb_describe(oracle, raw, blur, x[:1], y[:1], level[:1], pat)[:2])
+    # hand case on the GPU: a ramp gives angle 0 and the pattern's own x comparisons
+    ramp = np.tile(np.arange(64, dtype=np.uint8) * 3, (64, 1))
+    a, d = orb.ORBDescribe(ctx, [ramp], [ramp], [32.0], [32.0], [0], pat)
+    pts = pat.reshape(256, 2, 2)
+    assert abs(a[0]) < 1e-3
+    np.testing.assert_array_equal(np.unpackbits(d[0], bitorder="little"), (pts[:, 0, 0] < pts[:, 1, 0]))
+    # the orientation patch leaves the level; the rotated pattern leaves it (given angle)
+    with pytest.raises(OsgError, match="orientation patch"):
+        orb.ORBDescribe(ctx, [ramp], [ramp], [32.0, 10.0], [32.0, 32.0], [0, 0], pat)
+    with pytest.raises(OsgError, match="keypoint 1: the descriptor pattern"):
+        orb.ORBDescribe(ctx, None, [ramp], [32.0, 3.0, 2.0], [32.0, 32.0, 32.0], [0, 0, 0], pat, angle=[0, 0, 45])

@@ -59,11 +59,39 @@ def stereo_bench(ctx, o):
     print(f"stereo   oracle {c * 1e3:8.2f} us/frame (1 thread)", flush=True)
 
 
+def orb_bench(ctx, o):
+    """IC_Angle + rBRIEF for one EuRoC frame's keypoints (752 x 480, 8 levels), and a large batch of
+    keypoints in one call (the kernels' throughput)."""
+    from orb_slam3_comments_ghr_amd import orb
+    rng = np.random.default_rng(14)
+    raw, blur, x, y, level = orb.synth_orb_frame(rng, n=1200)
+    pat = orb.synth_pattern(rng)
+    rp, bp = orb.ImagePyramid(raw).to_device(), orb.ImagePyramid(blur).to_device()
+    for n in (1200, 12000, 120000):
+        idx = np.arange(n) % 1200
+        args = (x[idx], y[idx], level[idx], pat)
+        k = best_of(lambda: orb.ORBDescribe(ctx, rp, bp, *args), ctx)
+        t = time.perf_counter()
+        orb.ORBDescribe(ctx, rp, bp, *args)
+        w = time.perf_counter() - t
+        print(f"orb      n={n:6d}  kernels {k * 1e3:8.2f} us ({k * 1e6 / n:6.2f} ns/kp)  wall {w * 1e6:9.1f} us "
+              f"(pyramids in HBM)", flush=True)
+    k = best_of(lambda: orb.ORBDescribe(ctx, raw, blur, x, y, level, pat), ctx)
+    t = time.perf_counter()
+    orb.ORBDescribe(ctx, raw, blur, x, y, level, pat)
+    w = time.perf_counter() - t
+    print(f"orb      n=  1200  kernels {k * 1e3:8.2f} us  wall {w * 1e6:9.1f} us (host pyramids uploaded)", flush=True)
+    c = cpu(lambda i: oc.orb_describe(o, raw, blur, x, y, level, pat), 20)
+    print(f"orb      oracle {c * 1e3:8.2f} us/frame of 1200 keypoints (1 thread)", flush=True)
+
+
 def main():
     ctx = Context(0)
     o = oc.load()
     if sys.argv[1:] == ["stereo"]:
         return stereo_bench(ctx, o)
+    if sys.argv[1:] == ["orb"]:
+        return orb_bench(ctx, o)
     m = ORBmatcher(ctx)
     rng = np.random.default_rng(11)
     pairs = [fr.synth_triang_pair(rng, n1=1200, n2=1200, forward=bool(i % 2)) for i in range(8)]
@@ -90,6 +118,7 @@ def main():
               flush=True)
     init_bench(ctx, o)
     stereo_bench(ctx, o)
+    orb_bench(ctx, o)
 
 
 def init_bench(ctx, o):
