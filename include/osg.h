@@ -427,9 +427,12 @@ int osg_compute_distinctive_descriptors_dev(osg_ctx *ctx, const void *d_desc, co
  * GaussianBlur'd level (ref:src/ORBextractor.cc:1628-1652), for keypoints in level coordinates (before
  * :1663-1667 scales them to level 0).  FAST, the octree distribution and the 7x7 Gaussian blur stay
  * with the caller (OpenCV).  umax: the extractor's umax (HALF_PATCH_SIZE + 1 = 16 entries, each
- * <= 15); pattern: its 512 points (ORBextractor::pattern) as (x, y) int pairs.  Every pixel a
- * keypoint reads must lie inside its level image (the reference would read the extractor's border
- * or past the blurred clone), else OSG_E_INVALID naming the keypoint.  fastAtan2 is OpenCV's (not
+ * <= 15); pattern: its 512 points (ORBextractor::pattern) as (x, y) int pairs.  The orientation box
+ * (+-15 around the rounded centre) must lie inside the raw level, else OSG_E_INVALID.  The blurred
+ * level is read as the reference's continuous clone (workingMat = mvImagePyramid[level].clone(),
+ * :1628): offsets are linear with step = cols, so a point left of column 0 reads the previous row's
+ * end; device-resident blurred levels must therefore have step == cols.  A point outside the whole
+ * level buffer (the reference reads foreign heap there) reads 0.  fastAtan2 is OpenCV's (not
  * in the reference tree: its published polynomial is restated; parity with OpenCV itself
  * unpinned).  cos / sin of the angle are the host libm's cosf / sinf (the reference's std::cos(float)),
  * evaluated between the two kernels so that they agree with it bit for bit. */
@@ -440,7 +443,7 @@ typedef struct osg_orb_keypoints {
 } osg_orb_keypoints;
 
 /* angle[n]: written (IC_Angle) when compute_angle, else read (the keypoints' angles in degrees);
- * desc[n x 32] written. */
+ * desc[n x 32] written.  Returns the number of keypoints that read outside their level's buffer. */
 int osg_orb_describe(osg_ctx *ctx, const osg_image_pyramid *raw, const osg_image_pyramid *blurred,
                      const osg_orb_keypoints *K, const int32_t *pattern, const int32_t *umax, int32_t compute_angle,
                      float *angle, uint8_t *desc);

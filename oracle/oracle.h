@@ -52,8 +52,8 @@ int oracle_search_for_triangulation(const osg_kf_side *K1, const osg_kf_side *K2
 /* Frame::ComputeStereoMatches (oracle_stereo.c): mvuRight / mvDepth out, returns the kept matches */
 int oracle_compute_stereo_matches(const osg_stereo_frame *F, float *mvuRight, float *mvDepth);
 
-/* ORBextractor IC_Angle + computeOrbDescriptor (oracle_orb.c): -1, or the first keypoint whose
- * reads leave its level */
+/* ORBextractor IC_Angle + computeOrbDescriptor (oracle_orb.c): the keypoints whose descriptor reads
+ * leave their level's buffer, or -(k + 1) for the first keypoint k whose orientation box leaves it */
 float oracle_fast_atan2(float y, float x);
 int oracle_orb_describe(const osg_image_pyramid *raw, const osg_image_pyramid *blurred, const osg_orb_keypoints *K,
                         const int32_t *pattern, const int32_t *umax, int compute_angle, float *angle, uint8_t *desc);

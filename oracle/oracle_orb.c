@@ -9,8 +9,12 @@
  *    I(p[16 i + 2 j]) < I(p[16 i + 2 j + 1]).
  * cvRound is round-half-even (rintf).  fastAtan2 is OpenCV's cv::fastAtan2, which the reference
  * tree does not hold: its published polynomial (degrees, 4 odd terms, DBL_EPSILON guard) is
- * restated below; parity with OpenCV itself is unpinned.  Reads are only checked against the level
- * bounds (returns the first offending keypoint, like the GPU path's OSG_E_INVALID). */
+ * restated below; parity with OpenCV itself is unpinned.  The descriptor reads the blurred level as
+ * the reference's continuous clone (workingMat, :1628): center[dy * step + dx] with step = cols, so a
+ * point left of column 0 reads the previous row's end.  A read outside the whole blurred buffer
+ * (the reference reads whatever heap lies there) is defined as 0 and counted per keypoint, as the GPU
+ * path does; an orientation box leaving the level returns -(k + 1) for the first such keypoint k
+ * (the GPU path's OSG_E_INVALID). */
 #include <float.h>
 #include <math.h>
 
@@ -48,13 +52,14 @@ int oracle_orb_describe(const osg_image_pyramid *raw, const osg_image_pyramid *b
                         const int32_t *pattern, const int32_t *umax, int compute_angle, float *angle, uint8_t *desc)
 {
     const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);   /* :139 */
+    int n_outside = 0;
     for (int k = 0; k < K->n; k++) {
         const int l = K->level[k];
         const int cx = (int)rintf(K->x[k]), cy = (int)rintf(K->y[k]);
         if (compute_angle) {                                                      /* :89-136 */
             if (!inside(raw, l, cx - HALF_PATCH_SIZE, cy - HALF_PATCH_SIZE) ||
                 !inside(raw, l, cx + HALF_PATCH_SIZE, cy + HALF_PATCH_SIZE))
-                return k;
+                return -(k + 1);
             const uint8_t *center = raw->data[l] + (size_t)cy * raw->step[l] + cx;
             const int step = raw->step[l];
             int m_01 = 0, m_10 = 0;
@@ -74,7 +79,8 @@ int oracle_orb_describe(const osg_image_pyramid *raw, const osg_image_pyramid *b
         const float ang = angle[k] * factorPI;                                    /* :153-154 */
         const float a = cosf(ang), b = sinf(ang);
         const uint8_t *img = blurred->data[l];
-        const int step = blurred->step[l];
+        const int step = blurred->step[l], rows = blurred->rows[l], cols = blurred->cols[l];
+        int outside = 0;
         for (int i = 0; i < 32; ++i) {                                            /* :166-205 */
             const int32_t *p = pattern + 32 * i;  /* 16 points of (x, y) */
             int val = 0;
@@ -84,13 +90,20 @@ int oracle_orb_describe(const osg_image_pyramid *raw, const osg_image_pyramid *b
                     const float px = (float)p[4 * j + 2 * s], py = (float)p[4 * j + 2 * s + 1];
                     const int dy = (int)rintf(px * b + py * a);
                     const int dx = (int)rintf(px * a - py * b);
-                    if (!inside(blurred, l, cx + dx, cy + dy)) return k;
-                    t[s] = img[(size_t)(cy + dy) * step + (cx + dx)];
+                    /* workingMat is a continuous clone: the linear offset, wrapping across rows */
+                    const long long off = (long long)(cy + dy) * cols + (cx + dx);
+                    if (off < 0 || off >= (long long)rows * cols) {
+                        outside = 1;
+                        t[s] = 0;
+                    } else {
+                        t[s] = img[(size_t)(off / cols) * step + (size_t)(off % cols)];
+                    }
                 }
                 val |= (t[0] < t[1]) << j;
             }
             desc[32 * k + i] = (uint8_t)val;
         }
+        n_outside += outside;
     }
-    return -1;
+    return n_outside;
 }

@@ -9,9 +9,10 @@
 //    std::sin(float) from the same libm, so the rotated pattern rounds identically.
 //  * k_orb_desc — one thread per (keypoint, descriptor byte), 8 keypoints per 256-thread
 //    workgroup; the 512-point pattern staged in LDS; bit j = I(p[2j]) < I(p[2j+1]) at the rotated,
-//    rint-rounded offsets (cvRound) around the rounded centre.  A read outside the level image
-//    (which the reference would make past the level's ROI or its blurred clone) records the lowest
-//    such keypoint, and the call fails with OSG_E_INVALID.
+//    rint-rounded offsets (cvRound) around the rounded centre, addressed as the reference does in its
+//    continuous blurred clone (a point left of column 0 reads the previous row's end).  A read outside
+//    the whole level buffer (the reference reads whatever heap lies there) yields 0, and the call
+//    returns how many keypoints did that.
 // Built with -ffp-contract=off: the rotation is two float products and a sum, as written.
 #include <algorithm>
 #include <cfloat>
@@ -36,12 +37,12 @@ struct OrbArgs {
     GLOBAL const uint8_t *raw[MAX_LEVELS];
     GLOBAL const uint8_t *blur[MAX_LEVELS];
     int raw_rows[MAX_LEVELS], raw_cols[MAX_LEVELS], raw_step[MAX_LEVELS];
-    int blur_rows[MAX_LEVELS], blur_cols[MAX_LEVELS], blur_step[MAX_LEVELS];
+    int blur_rows[MAX_LEVELS], blur_cols[MAX_LEVELS], blur_step[MAX_LEVELS];  // step == cols
     int umax[HALF_PATCH + 1];
     GLOBAL float *angle;                         // n
     GLOBAL const float *cs;                      // 2n: (cos, sin)
     GLOBAL uint32_t *desc;                       // 8n words = 32n bytes
-    GLOBAL int32_t *bad;                         // lowest keypoint reading outside its level, or INT_MAX
+    GLOBAL int32_t *bad;                         // keypoints that read outside their level's buffer
 };
 
 __device__ __forceinline__ float fast_atan2(float y, float x)
@@ -109,7 +110,10 @@ __global__ __launch_bounds__(256) void k_orb_desc(const OrbArgs *__restrict__ A)
     const int l = A->level[k];
     const int cx = (int)rintf(A->x[k]), cy = (int)rintf(A->y[k]);
     const float a = A->cs[2 * k], b = A->cs[2 * k + 1];
-    const int rows = A->blur_rows[l], cols = A->blur_cols[l], step = A->blur_step[l];
+    // the reference reads a continuous clone (step = cols): a point past a row end wraps to the next row
+    const int cols = A->blur_cols[l];
+    const long long size = (long long)A->blur_rows[l] * cols;
+    const long long c0 = (long long)cy * cols + cx;
     GLOBAL const uint8_t *img = A->blur[l];
     uint32_t val = 0;
     bool bad = false;
@@ -120,15 +124,18 @@ __global__ __launch_bounds__(256) void k_orb_desc(const OrbArgs *__restrict__ A)
         for (int s = 0; s < 2; s++) {
             const int2 p = s_pat[16 * byte + 2 * j + s];
             const float px = (float)p.x, py = (float)p.y;
-            const int yy = cy + (int)rintf(px * b + py * a);
-            const int xx = cx + (int)rintf(px * a - py * b);
-            const bool in = xx >= 0 && yy >= 0 && xx < cols && yy < rows;
+            const int dy = (int)rintf(px * b + py * a);
+            const int dx = (int)rintf(px * a - py * b);
+            const long long off = c0 + (long long)dy * cols + dx;
+            const bool in = off >= 0 && off < size;
             bad |= !in;
-            t[s] = in ? (int)img[(size_t)yy * step + xx] : 0;
+            t[s] = in ? (int)img[off] : 0;  // outside the buffer: 0 (the reference reads foreign heap)
         }
         val |= (uint32_t)(t[0] < t[1]) << j;
     }
-    if (bad) atomicMin((int32_t *)A->bad, k);
+    // keypoints that read outside their level's buffer: one count per keypoint (its 32 lanes)
+    const unsigned long long m = __ballot(bad);
+    if (byte == 0 && ((m >> (threadIdx.x & 32)) & 0xffffffffull)) atomicAdd((int32_t *)A->bad, 1);
     // 4 bytes per word: lanes 4w..4w+3 of a keypoint's 32 build word w
     val <<= 8 * (byte & 3);
     val |= __shfl_xor(val, 1);
@@ -202,6 +209,10 @@ int orb_run(osg_ctx *ctx, const osg_image_pyramid *raw, const osg_image_pyramid 
     }
     int rc = check_pyr(ctx, blurred, n_levels, "blurred");
     if (rc < 0) return rc;
+    if (blurred->on_device)
+        for (int l = 0; l < n_levels; l++)
+            OSG_REQUIRE(ctx, blurred->step[l] == blurred->cols[l],
+                        "blurred level %d on the device must be continuous (step == cols), like the reference's clone", l);
     OrbArgs A{};
     A.n = n;
     osg_packer pk;
@@ -259,7 +270,7 @@ int orb_run(osg_ctx *ctx, const osg_image_pyramid *raw, const osg_image_pyramid 
     A.bad = (GLOBAL int32_t *)(dev_out + o_bad);
     A.desc = (GLOBAL uint32_t *)(dev_out + o_desc);
     *pin_args = A;
-    *(int32_t *)(pin_out + o_bad) = INT32_MAX;
+    *(int32_t *)(pin_out + o_bad) = 0;
     hipEvent_t *ev = osg_ctx_events(ctx);
     if (!ev) return osg_set_error(ctx, OSG_E_HIP, "event create failed");
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(dev_in, pin, pk.total, hipMemcpyHostToDevice, ctx->stream));
@@ -296,13 +307,9 @@ int orb_run(osg_ctx *ctx, const osg_image_pyramid *raw, const osg_image_pyramid 
     float ms_desc = 0.f;
     OSG_HIP_CHECK(ctx, hipEventElapsedTime(&ms_desc, ev[0], ev[1]));
     ctx->last_kernel_ms = ms_angle + ms_desc;
-    const int32_t bad = *(int32_t *)(pin_out + o_bad);
-    if (bad != INT32_MAX)
-        return osg_set_error(ctx, OSG_E_INVALID, "keypoint %d: the descriptor pattern leaves level %d", bad,
-                             K->level[bad]);
     if (compute_angle) std::memcpy(angle, ang, sizeof(float) * n);
     std::memcpy(desc, pin_out + o_desc, (size_t)n * 32);
-    return OSG_OK;
+    return *(int32_t *)(pin_out + o_bad);
 }
 
 }  // namespace

@@ -4,8 +4,11 @@ computeDescriptors / computeOrbDescriptor (ref:src/ORBextractor.cc:148-208, 1534
 levels (ref:src/ORBextractor.cc:1628-1652).  FAST, the octree distribution and the Gaussian blur stay
 with OpenCV; the caller passes the extractor's ``umax`` and ``pattern``.
 
-    angle, desc = ORBDescribe(ctx, raw, blurred, x, y, level, pattern, umax)        # IC_Angle + rBRIEF
-    _, desc = ORBDescribe(ctx, None, blurred, x, y, level, pattern, angle=angle)    # given angles
+    angle, desc, n_out = ORBDescribe(ctx, raw, blurred, x, y, level, pattern, umax)     # IC_Angle + rBRIEF
+    _, desc, n_out = ORBDescribe(ctx, None, blurred, x, y, level, pattern, angle=angle) # given angles
+
+n_out counts the keypoints whose rotated pattern left their level's buffer (read as 0 there; the
+reference reads foreign heap).  The blurred levels are addressed as the reference's continuous clone.
 """
 from __future__ import annotations
 
@@ -49,7 +52,8 @@ def synth_pattern(rng, npoints: int = 512, radius: int = 13) -> np.ndarray:
 def ORBDescribe(ctx: Context, raw, blurred, x, y, level, pattern, umax=None, angle=None):
     """IC_Angle (when ``angle`` is None) and the 256-bit steered BRIEF descriptor of every keypoint.
     raw / blurred: ImagePyramid (mvImagePyramid and its GaussianBlur'd levels) or lists of levels;
-    x, y: level coordinates; level: KeyPoint::octave.  Returns (angle float32[n], desc uint8[n, 32])."""
+    x, y: level coordinates; level: KeyPoint::octave.  Returns (angle float32[n], desc uint8[n, 32],
+    keypoints that read outside their level's buffer)."""
     x = np.ascontiguousarray(x, np.float32)
     y = np.ascontiguousarray(y, np.float32)
     level = np.ascontiguousarray(level, np.int32)
@@ -74,17 +78,19 @@ def ORBDescribe(ctx: Context, raw, blurred, x, y, level, pattern, umax=None, ang
     K = _abi.OsgOrbKeypoints(n, x.ctypes.data, y.ctypes.data, level.ctypes.data)
     rs = raw.struct() if raw is not None else _abi.OsgImagePyramid()
     bs = blurred.struct()
-    ctx.check(ctx.lib.osg_orb_describe(ctx.handle, C.byref(rs), C.byref(bs), C.byref(K), pattern.ctypes.data,
+    n_out = ctx.check(ctx.lib.osg_orb_describe(ctx.handle, C.byref(rs), C.byref(bs), C.byref(K), pattern.ctypes.data,
                                        umax.ctypes.data if compute else None, int(compute), ang.ctypes.data,
                                        desc.ctypes.data), "osg_orb_describe")
-    return ang, desc
+    return ang, desc, n_out
 
 
-def synth_orb_frame(rng, n=1200, width=752, height=480, n_levels=8, factor=1.2, fractional=False):
+def synth_orb_frame(rng, n=1200, width=752, height=480, n_levels=8, factor=1.2, fractional=False,
+                    edge=EDGE_THRESHOLD):
     """A synthetic extractor output of EuRoC shape: per level a smooth random image (raw) and a second
     one standing in for its blur, and n keypoints spread over the levels in proportion to their area
-    (ref:src/ORBextractor.cc:474-494), EDGE_THRESHOLD px inside each level.  ``fractional`` adds
-    sub-pixel offsets including exact .5 ties (cvRound is round-half-even)."""
+    (ref:src/ORBextractor.cc:474-494), ``edge`` px inside each level (FAST's own margin is
+    EDGE_THRESHOLD - 3 = 16, where rotated pattern points can fall off the row and wrap).  ``fractional``
+    adds sub-pixel offsets including exact .5 ties (cvRound is round-half-even)."""
     raw, blur = [], []
     scale = 1.0
     areas = []
@@ -105,10 +111,10 @@ def synth_orb_frame(rng, n=1200, width=752, height=480, n_levels=8, factor=1.2, 
     for l in range(n_levels):
         m = level == l
         h, w = raw[l].shape
-        x[m] = rng.integers(EDGE_THRESHOLD, w - EDGE_THRESHOLD, m.sum())
-        y[m] = rng.integers(EDGE_THRESHOLD, h - EDGE_THRESHOLD, m.sum())
+        x[m] = rng.integers(edge, w - edge, m.sum())
+        y[m] = rng.integers(edge, h - edge, m.sum())
     if fractional:
-        off = rng.choice(np.array([0.0, 0.25, 0.5, -0.5, 0.75, -0.3], np.float32), size=(2, n))
+        off = rng.choice(np.array([0.0, 0.25, 0.5, -0.5, 0.45, -0.3], np.float32), size=(2, n))
         x += off[0]
         y += off[1]
     return raw, blur, x, y, level

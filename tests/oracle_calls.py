@@ -208,7 +208,8 @@ def stereo(oracle, F):
 
 
 def orb_describe(oracle, raw, blurred, x, y, level, pattern, umax=None, angle=None):
-    """IC_Angle + computeOrbDescriptor through the oracle: (angle, desc, first bad keypoint or -1)."""
+    """IC_Angle + computeOrbDescriptor through the oracle: (angle, desc, keypoints reading outside their
+    level's buffer; -(k + 1) when keypoint k's orientation box leaves its level)."""
     from orb_slam3_comments_ghr_amd.orb import ic_umax
     from orb_slam3_comments_ghr_amd.stereo import ImagePyramid
     x, y = (np.ascontiguousarray(v, np.float32) for v in (x, y))

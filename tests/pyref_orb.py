@@ -68,7 +68,9 @@ def orb_descriptor(img, x, y, angle, pattern):
                 px, py = f32(pts[16 * i + 2 * j + s, 0]), f32(pts[16 * i + 2 * j + s, 1])
                 dy = int(np.rint(px * b + py * a))
                 dx = int(np.rint(px * a - py * b))
-                t2.append(int(img[cy + dy, cx + dx]))
+                flat = np.ascontiguousarray(img).reshape(-1)   # the continuous clone: rows wrap
+                off = (cy + dy) * img.shape[1] + (cx + dx)
+                t2.append(int(flat[off]) if 0 <= off < flat.size else 0)   # outside the buffer: 0
             val |= int(t2[0] < t2[1]) << j
         out[i] = val
     return out

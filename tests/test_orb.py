@@ -17,10 +17,10 @@ from tests import oracle_calls as oc
 from tests import pyref_orb as po
 
 
-def small_frame(seed, n=40, fractional=True):
+def small_frame(seed, n=40, fractional=True, edge=orb.EDGE_THRESHOLD):
     rng = np.random.default_rng(seed)
     raw, blur, x, y, level = orb.synth_orb_frame(rng, n=n, width=160, height=120, n_levels=3,
-                                                 fractional=fractional)
+                                                 fractional=fractional, edge=edge)
     return rng, raw, blur, x, y, level
 
 
@@ -41,12 +41,12 @@ def test_fast_atan2_accuracy(oracle):
             assert min(d, 360.0 - d) < 0.01
 
 
-@pytest.mark.parametrize("seed", [0, 1, 2])
-def test_oracle_vs_python(oracle, seed):
-    rng, raw, blur, x, y, level = small_frame(seed)
+@pytest.mark.parametrize("seed,edge", [(0, 19), (1, 19), (2, 16)])
+def test_oracle_vs_python(oracle, seed, edge):
+    rng, raw, blur, x, y, level = small_frame(seed, edge=edge)
     pat = orb.synth_pattern(rng)
     ang, desc, bad = oc.orb_describe(oracle, raw, blur, x, y, level, pat)
-    assert bad == -1
+    assert bad == 0
     um = orb.ic_umax()
     for k in range(len(x)):
         a = po.ic_angle(raw[level[k]], x[k], y[k], um)
@@ -55,7 +55,7 @@ def test_oracle_vs_python(oracle, seed):
     # given angles (computeDescriptors alone)
     given = rng.uniform(0, 360, len(x)).astype(np.float32)
     _, d2, bad = oc.orb_describe(oracle, None, blur, x, y, level, pat, angle=given)
-    assert bad == -1
+    assert bad == 0
     for k in range(len(x)):
         np.testing.assert_array_equal(d2[k], po.orb_descriptor(blur[level[k]], x[k], y[k], given[k], pat))
 
@@ -67,7 +67,7 @@ def test_oracle_hand_cases(oracle):
     pat = orb.synth_pattern(np.random.default_rng(9))
     x, y, lv = [32.0], [32.0], [0]
     a, d, bad = oc.orb_describe(oracle, [ramp_x], [ramp_x], x, y, lv, pat)
-    assert bad == -1 and abs(a[0]) < 1e-3        # brighter to the right: angle 0
+    assert bad == 0 and abs(a[0]) < 1e-3        # brighter to the right: angle 0
     # angle 0: a = 1, b = 0, the tests compare the pattern points' own x coordinates
     pts = pat.reshape(256, 2, 2)
     bits = (pts[:, 0, 0] < pts[:, 1, 0]).astype(np.uint8)
@@ -79,9 +79,17 @@ def test_oracle_hand_cases(oracle):
     flat = np.full((h, w), 77, np.uint8)
     a, d, _ = oc.orb_describe(oracle, [flat], [flat], x, y, lv, pat)
     assert a[0] == 0.0 and not d.any()           # fastAtan2(0, 0) = 0; equal pixels give 0 bits
-    # a keypoint whose pattern leaves the image: the index of the first such keypoint
-    _, _, bad = oc.orb_describe(oracle, [flat], [flat], [32.0, 3.0], [32.0, 32.0], [0, 0], pat, angle=[0.0, 0.0])
-    assert bad == 1
+    # left of column 0 the continuous clone wraps to the previous row's end (no error); a read before
+    # the buffer's first byte is reported with the index of the first such keypoint
+    ramp2 = (np.arange(h * w) % 251).astype(np.uint8).reshape(h, w)
+    _, d, bad = oc.orb_describe(oracle, [flat], [ramp2], [32.0, 3.0], [32.0, 32.0], [0, 0], pat, angle=[0.0, 0.0])
+    assert bad == 0
+    np.testing.assert_array_equal(d[1], po.orb_descriptor(ramp2, 3.0, 32.0, 0.0, pat))
+    _, d, bad = oc.orb_describe(oracle, [flat], [ramp2], [32.0, 3.0], [32.0, 3.0], [0, 0], pat, angle=[0.0, 0.0])
+    assert bad == 1                              # outside the buffer: read as 0, counted
+    np.testing.assert_array_equal(d[1], po.orb_descriptor(ramp2, 3.0, 3.0, 0.0, pat))
+    _, _, bad = oc.orb_describe(oracle, [flat], [flat], [32.0, 10.0], [32.0, 32.0], [0, 0], pat)
+    assert bad == -2                             # keypoint 1's orientation box leaves the level
 
 
 # ---------------------------------------------------------------------------------------------- GPU
@@ -92,18 +100,21 @@ def same(a, b):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed,fractional", [(0, False), (1, True), (2, False)])
-def test_gpu_vs_oracle(ctx, oracle, seed, fractional):
+@pytest.mark.parametrize("seed,fractional,edge", [(0, False, 19), (1, True, 19), (2, False, 16), (3, True, 16)])
+def test_gpu_vs_oracle(ctx, oracle, seed, fractional, edge):
     rng = np.random.default_rng(100 + seed)
-    raw, blur, x, y, level = orb.synth_orb_frame(rng, n=1500, fractional=fractional)
+    raw, blur, x, y, level = orb.synth_orb_frame(rng, n=1500, fractional=fractional, edge=edge)
     pat = orb.synth_pattern(rng)
     ref = oc.orb_describe(oracle, raw, blur, x, y, level, pat)
-    assert ref[2] == -1
-    same(orb.ORBDescribe(ctx, raw, blur, x, y, level, pat), ref)
+    assert ref[2] >= 0
+    got = orb.ORBDescribe(ctx, raw, blur, x, y, level, pat)
+    same(got, ref)
+    assert got[2] == ref[2]
     given = rng.uniform(0, 360, len(x)).astype(np.float32)
     ref2 = oc.orb_describe(oracle, None, blur, x, y, level, pat, angle=given)
     got = orb.ORBDescribe(ctx, None, blur, x, y, level, pat, angle=given)
     same(got, ref2[:2])
+    assert got[2] == ref2[2]
 
 
 @pytest.mark.gpu
@@ -132,18 +143,31 @@ def test_gpu_edges(ctx, oracle):
     rng = np.random.default_rng(11)
     raw, blur, x, y, level = orb.synth_orb_frame(rng, n=64)
     pat = orb.synth_pattern(rng)
-    a, d = orb.ORBDescribe(ctx, raw, blur, x[:0], y[:0], level[:0], pat)
+    a, d, _ = orb.ORBDescribe(ctx, raw, blur, x[:0], y[:0], level[:0], pat)
     assert a.shape == (0,) and d.shape == (0, 32)
-    a, d = orb.ORBDescribe(ctx, raw, blur, x[:1], y[:1], level[:1], pat)    # one keypoint
+    a, d, _ = orb.ORBDescribe(ctx, raw, blur, x[:1], y[:1], level[:1], pat)    # one keypoint
     same((a, d), oc.orb_describe(oracle, raw, blur, x[:1], y[:1], level[:1], pat)[:2])
     # hand case on the GPU: a ramp gives angle 0 and the pattern's own x comparisons
     ramp = np.tile(np.arange(64, dtype=np.uint8) * 3, (64, 1))
-    a, d = orb.ORBDescribe(ctx, [ramp], [ramp], [32.0], [32.0], [0], pat)
+    a, d, _ = orb.ORBDescribe(ctx, [ramp], [ramp], [32.0], [32.0], [0], pat)
     pts = pat.reshape(256, 2, 2)
     assert abs(a[0]) < 1e-3
     np.testing.assert_array_equal(np.unpackbits(d[0], bitorder="little"), (pts[:, 0, 0] < pts[:, 1, 0]))
     # the orientation patch leaves the level; the rotated pattern leaves it (given angle)
     with pytest.raises(OsgError, match="orientation patch"):
         orb.ORBDescribe(ctx, [ramp], [ramp], [32.0, 10.0], [32.0, 32.0], [0, 0], pat)
-    with pytest.raises(OsgError, match="keypoint 1: the descriptor pattern"):
-        orb.ORBDescribe(ctx, None, [ramp], [32.0, 3.0, 2.0], [32.0, 32.0, 32.0], [0, 0, 0], pat, angle=[0, 0, 45])
+    ramp2 = (np.arange(64 * 64) % 251).astype(np.uint8).reshape(64, 64)
+    got = orb.ORBDescribe(ctx, None, [ramp2], [32.0, 3.0, 61.0], [32.0, 32.0, 40.0], [0, 0, 0], pat, angle=[0, 0, 45])
+    ref = oc.orb_describe(oracle, None, [ramp2], [32.0, 3.0, 61.0], [32.0, 32.0, 40.0], [0, 0, 0], pat,
+                          angle=[0, 0, 45])
+    assert ref[2] == 0 and got[2] == 0
+    np.testing.assert_array_equal(got[1], ref[1])                     # row wrap-around as the clone reads
+    args = ([32.0, 3.0, 2.0], [32.0, 3.0, 62.0], [0, 0, 0], pat)
+    got = orb.ORBDescribe(ctx, None, [ramp2], *args, angle=[0, 0, 45])   # before / past the buffer
+    ref = oc.orb_describe(oracle, None, [ramp2], *args, angle=[0, 0, 45])
+    assert got[2] == ref[2] == 2
+    np.testing.assert_array_equal(got[1], ref[1])
+    import torch
+    wide = torch.zeros((64, 80), dtype=torch.uint8, device="cuda")[:, :64]
+    with pytest.raises(OsgError, match="continuous"):
+        orb.ORBDescribe(ctx, None, orb.ImagePyramid([wide]), [32.0], [32.0], [0], pat, angle=[0.0])
