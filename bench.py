@@ -215,6 +215,7 @@ def main():
         out["frames_c5"] = bench_c5(ctx, rank, world, dist, dev, args)
         out["frames_dbow"] = bench_dbow(ctx, rank, world, dist, dev, args)
         out["frames_stereo"] = bench_stereo(ctx, rank, world, dist, dev, args)
+        out["frames_orb"] = bench_orb(ctx, rank, world, dist, dev, args)
 
     # ---- LocalBA iters/s on C4 (50 KF x 10k points), the second half of the metric ----------
     if not args.no_ba:
@@ -533,6 +534,55 @@ def bench_stereo(ctx, rank, world, dist, dev, args):
                          f"side, pyramids in HBM; {B} frames per launch", n_pool)
     st.ComputeStereoMatchesBatch(ctx, frames[:1])
     res["single_frame_kernel_us"] = round(ctx.last_kernel_ms() * 1e3, 2)
+    return res
+
+
+def bench_orb(ctx, rank, world, dist, dev, args):
+    """SURVEY.md §8(f) rank 4 (ORBextractor): IC_Angle + steered BRIEF for one EuRoC frame's keypoints
+    (752 x 480, 8 levels x 1.2, 1200 keypoints spread by level area; seeded synthetic images, no EuRoC
+    images in the container) per call, both pyramids resident in HBM.  One frame per call: the
+    angle -> host cosf/sinf -> descriptor round trip is per frame."""
+    import torch
+    from orb_slam3_comments_ghr_amd import orb
+    n_pool = 4
+    rng = np.random.default_rng(0x0B5EED30 + rank)
+    pool = [orb.synth_orb_frame(rng, n=1200, edge=16) for _ in range(n_pool)]
+    pat = orb.synth_pattern(rng)
+    dpool = [(orb.ImagePyramid(f[0]).to_device(dev), orb.ImagePyramid(f[1]).to_device(dev)) + tuple(f[2:])
+             for f in pool]
+    for f in dpool:
+        orb.ORBDescribe(ctx, f[0], f[1], f[2], f[3], f[4], pat)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    reps = max(args.frame_reps, 1) * 50
+    k_ms = 0.0
+    t0 = time.perf_counter()
+    for i in range(reps):
+        f = dpool[i % n_pool]
+        orb.ORBDescribe(ctx, f[0], f[1], f[2], f[3], f[4], pat)
+        k_ms += ctx.last_kernel_ms()
+    wall = time.perf_counter() - t0
+    k_s, tot = job_totals(k_ms / 1e3, reps, world, dist if world > 1 else None, dev)
+    w_s, _ = job_totals(wall, reps, world, dist if world > 1 else None, dev)
+    res = {"metric": "frames/s", "value": round(tot / k_s, 1), "unit": "frames/s",
+           "workload": "ORBextractor IC_Angle + computeOrbDescriptor: EuRoC-shaped 752x480, 8 levels, 1200 "
+                       "keypoints per frame, pyramids in HBM; 1 frame per call (k_orb_angle + k_orb_desc)",
+           "kernel_us_per_frame": round(k_ms * 1e3 / reps, 2),
+           "wall_frames_per_s_incl_host_roundtrip": round(tot / w_s, 1), "n_gpus": world,
+           "scaling": "weak", "parallelism": f"replicas x{world}"}
+    if rank == 0 and world == 1 and not args.no_cpu:
+        oracle, oc = _oracle()
+        n = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < args.cpu_seconds / 4 or n == 0:
+            f = pool[n % n_pool]
+            oc.orb_describe(oracle, f[0], f[1], f[2], f[3], f[4], pat)
+            n += 1
+        cel = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": round(n / cel, 1), "unit": "frames/s", "cores": 1, "kind": "port",
+                               "sample": f"{n} frames through the oracle (gcc -O3, 1 thread) in {cel:.1f} s"}
+        res["speedup_vs_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
     return res
 
 

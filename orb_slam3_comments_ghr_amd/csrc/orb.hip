@@ -3,7 +3,7 @@
 // one frame in one launch each.
 //  * k_orb_angle — one wave per keypoint; lane u + 15 (u = -15..15) owns column u of the circular
 //    patch: u I(u, 0) + sum over v = 1..15 with |u| <= umax[v] of u (I(u, v) + I(u, -v)) for m_10
-//    and v (I(u, v) - I(u, -v)) for m_01.  Integer sums, so the wave reduction equals the
+//    and v (I(u, v) - I(u, -v)) for m_01, its 31 loads issued together (masked, not branched).  Integer sums, so the wave reduction equals the
 //    reference's row-major order exactly; lane 0 evaluates fastAtan2.
 //  * host: a = cosf(angle factorPI), b = sinf(angle factorPI) — the reference's std::cos(float) /
 //    std::sin(float) from the same libm, so the rotated pattern rounds identically.
@@ -13,7 +13,9 @@
 //    continuous blurred clone (a point left of column 0 reads the previous row's end).  A read outside
 //    the whole level buffer (the reference reads whatever heap lies there) yields 0, and the call
 //    returns how many keypoints did that.
-// Built with -ffp-contract=off: the rotation is two float products and a sum, as written.
+// The argument block (level pointers and sizes, ~1.4 KB) travels as the kernel argument, not as a
+// device copy the waves would first have to load.  Built with -ffp-contract=off: the rotation is two
+// float products and a sum, as written.
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
@@ -67,54 +69,53 @@ __device__ __forceinline__ float fast_atan2(float y, float x)
     return a;
 }
 
-__global__ __launch_bounds__(256) void k_orb_angle(const OrbArgs *__restrict__ A)
+__global__ __launch_bounds__(256) void k_orb_angle(const OrbArgs A)
 {
     const int lane = threadIdx.x & 63;
     const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (k >= A->n) return;
-    const int l = A->level[k];
-    const int cx = (int)rintf(A->x[k]), cy = (int)rintf(A->y[k]);
-    const int step = A->raw_step[l];
-    GLOBAL const uint8_t *c = A->raw[l] + (size_t)cy * step + cx;
-    int m10 = 0, m01 = 0;
-    if (lane <= 2 * HALF_PATCH) {
-        const int u = lane - HALF_PATCH;
-        const int au = u < 0 ? -u : u;
-        m10 = u * (int)c[u];
+    if (k >= A.n) return;
+    const int l = A.level[k];
+    const int cx = (int)rintf(A.x[k]), cy = (int)rintf(A.y[k]);
+    const int step = A.raw_step[l];
+    GLOBAL const uint8_t *c = A.raw[l] + (size_t)cy * step + cx;
+    // every read of the +-15 box is in bounds (checked on the host), so all 31 loads of a lane are
+    // issued unconditionally and masked; lanes 31..63 read the centre column with weight 0
+    const bool act = lane <= 2 * HALF_PATCH;
+    const int u = act ? lane - HALF_PATCH : 0;
+    const int au = u < 0 ? -u : u;
+    int m10 = act ? u * (int)c[u] : 0, m01 = 0;
 #pragma unroll
-        for (int v = 1; v <= HALF_PATCH; v++) {
-            if (au <= A->umax[v]) {
-                const int p = c[u + v * step], m = c[u - v * step];
-                m01 += v * (p - m);
-                m10 += u * (p + m);
-            }
-        }
+    for (int v = 1; v <= HALF_PATCH; v++) {
+        const int p = c[u + v * step], m = c[u - v * step];
+        const int w = (act && au <= A.umax[v]) ? 1 : 0;
+        m01 += w * v * (p - m);
+        m10 += w * u * (p + m);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         m10 += __shfl_xor(m10, o);
         m01 += __shfl_xor(m01, o);
     }
-    if (lane == 0) A->angle[k] = fast_atan2((float)m01, (float)m10);
+    if (lane == 0) A.angle[k] = fast_atan2((float)m01, (float)m10);
 }
 
-__global__ __launch_bounds__(256) void k_orb_desc(const OrbArgs *__restrict__ A)
+__global__ __launch_bounds__(256) void k_orb_desc(const OrbArgs A)
 {
     __shared__ int2 s_pat[NPOINTS];
     for (int i = threadIdx.x; i < NPOINTS; i += 256)
-        s_pat[i] = make_int2(A->pattern[2 * i], A->pattern[2 * i + 1]);
+        s_pat[i] = make_int2(A.pattern[2 * i], A.pattern[2 * i + 1]);
     __syncthreads();
     const int k = blockIdx.x * 8 + (threadIdx.x >> 5);
     const int byte = threadIdx.x & 31;
-    if (k >= A->n) return;
-    const int l = A->level[k];
-    const int cx = (int)rintf(A->x[k]), cy = (int)rintf(A->y[k]);
-    const float a = A->cs[2 * k], b = A->cs[2 * k + 1];
+    if (k >= A.n) return;
+    const int l = A.level[k];
+    const int cx = (int)rintf(A.x[k]), cy = (int)rintf(A.y[k]);
+    const float a = A.cs[2 * k], b = A.cs[2 * k + 1];
     // the reference reads a continuous clone (step = cols): a point past a row end wraps to the next row
-    const int cols = A->blur_cols[l];
-    const long long size = (long long)A->blur_rows[l] * cols;
+    const int cols = A.blur_cols[l];
+    const long long size = (long long)A.blur_rows[l] * cols;
     const long long c0 = (long long)cy * cols + cx;
-    GLOBAL const uint8_t *img = A->blur[l];
+    GLOBAL const uint8_t *img = A.blur[l];
     uint32_t val = 0;
     bool bad = false;
 #pragma unroll
@@ -135,12 +136,12 @@ __global__ __launch_bounds__(256) void k_orb_desc(const OrbArgs *__restrict__ A)
     }
     // keypoints that read outside their level's buffer: one count per keypoint (its 32 lanes)
     const unsigned long long m = __ballot(bad);
-    if (byte == 0 && ((m >> (threadIdx.x & 32)) & 0xffffffffull)) atomicAdd((int32_t *)A->bad, 1);
+    if (byte == 0 && ((m >> (threadIdx.x & 32)) & 0xffffffffull)) atomicAdd((int32_t *)A.bad, 1);
     // 4 bytes per word: lanes 4w..4w+3 of a keypoint's 32 build word w
     val <<= 8 * (byte & 3);
     val |= __shfl_xor(val, 1);
     val |= __shfl_xor(val, 2);
-    if ((byte & 3) == 0) A->desc[8 * k + (byte >> 2)] = val;
+    if ((byte & 3) == 0) A.desc[8 * k + (byte >> 2)] = val;
 }
 
 template <typename T>
@@ -240,22 +241,18 @@ int orb_run(osg_ctx *ctx, const osg_image_pyramid *raw, const osg_image_pyramid 
     set_off(A.level, pk.add(K->level, sizeof(int32_t) * n));
     set_off(A.pattern, pk.add(pattern, sizeof(int32_t) * 2 * NPOINTS));
     const size_t in_bytes = (pk.total + 255) & ~size_t(255);
-    const size_t args_bytes = (sizeof(OrbArgs) + 255) & ~size_t(255);
     // outputs / exchange: angle n | cs 2n | bad 1 (256-aligned) | desc 32n
     const size_t o_cs = ((size_t)n * 4 + 255) & ~size_t(255);
     const size_t o_bad = o_cs + (((size_t)n * 8 + 255) & ~size_t(255));
     const size_t o_desc = o_bad + 256;
     const size_t out_bytes = o_desc + (size_t)n * 32;
-    char *pin = (char *)osg_pinned(ctx, in_bytes + args_bytes + out_bytes + 256);
+    char *pin = (char *)osg_pinned(ctx, in_bytes + out_bytes + 256);
     if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
     OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));  // the pinned block may still be in use
     pk.fill_parallel(pin, 8);
-    OrbArgs *pin_args = (OrbArgs *)(pin + in_bytes);
-    char *pin_out = (char *)pin_args + args_bytes;
+    char *pin_out = pin + in_bytes;
     char *dev_in = nullptr, *dev_out = nullptr;
-    OrbArgs *dev_args = nullptr;
     OSG_ALLOC(ctx, dev_in, SLOT_TMP0, pk.total + 256);
-    OSG_ALLOC(ctx, dev_args, SLOT_TMP1, args_bytes);
     OSG_ALLOC(ctx, dev_out, SLOT_TMP2, out_bytes);
     relocate(A.x, dev_in);
     relocate(A.y, dev_in);
@@ -269,17 +266,15 @@ int orb_run(osg_ctx *ctx, const osg_image_pyramid *raw, const osg_image_pyramid 
     A.cs = (GLOBAL const float *)(dev_out + o_cs);
     A.bad = (GLOBAL int32_t *)(dev_out + o_bad);
     A.desc = (GLOBAL uint32_t *)(dev_out + o_desc);
-    *pin_args = A;
     *(int32_t *)(pin_out + o_bad) = 0;
     hipEvent_t *ev = osg_ctx_events(ctx);
     if (!ev) return osg_set_error(ctx, OSG_E_HIP, "event create failed");
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(dev_in, pin, pk.total, hipMemcpyHostToDevice, ctx->stream));
-    OSG_HIP_CHECK(ctx, hipMemcpyAsync(dev_args, pin_args, sizeof(OrbArgs), hipMemcpyHostToDevice, ctx->stream));
     float ms_angle = 0.f;
     float *ang = (float *)pin_out;
     if (compute_angle) {
         OSG_HIP_CHECK(ctx, hipEventRecord(ev[0], ctx->stream));
-        hipLaunchKernelGGL(k_orb_angle, dim3((n + 3) / 4), dim3(256), 0, ctx->stream, dev_args);
+        hipLaunchKernelGGL(k_orb_angle, dim3((n + 3) / 4), dim3(256), 0, ctx->stream, A);
         OSG_HIP_CHECK(ctx, hipGetLastError());
         OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
         OSG_HIP_CHECK(ctx, hipMemcpyAsync(ang, dev_out, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
@@ -298,7 +293,7 @@ int orb_run(osg_ctx *ctx, const osg_image_pyramid *raw, const osg_image_pyramid 
     }
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(dev_out + o_cs, cs, o_bad - o_cs + 256, hipMemcpyHostToDevice, ctx->stream));
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[0], ctx->stream));
-    hipLaunchKernelGGL(k_orb_desc, dim3((n + 7) / 8), dim3(256), 0, ctx->stream, dev_args);
+    hipLaunchKernelGGL(k_orb_desc, dim3((n + 7) / 8), dim3(256), 0, ctx->stream, A);
     OSG_HIP_CHECK(ctx, hipGetLastError());
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_out + o_bad, dev_out + o_bad, out_bytes - o_bad, hipMemcpyDeviceToHost,
