@@ -720,6 +720,49 @@ int compute_stereo_matches(FrameT &F)
                  "osg_compute_stereo_matches");
 }
 
+// ----------------------------------------------------------------- b8 ORBextractor per-keypoint stages
+// computeOrientation + computeDescriptors inside ORBextractor::operator() (ref:src/ORBextractor.cc:
+// 585-597, 1534-1545, 1557-1652), for code that lives in ORBextractor.cc (pattern / umax are its
+// members).  allKeypoints[level] in level coordinates, as ComputeKeyPointsOctTree leaves them;
+// blurred[level] = the GaussianBlur'd clone of mvImagePyramid[level] (:1628-1640).  Writes
+// KeyPoint::angle and the 32-byte rows in allKeypoints order (level by level) into `desc`; returns
+// the keypoints whose rotated pattern left their level's buffer (the reference reads foreign heap).
+template <class MatT, class KeyPointT, class PointT>
+int orb_describe(const std::vector<MatT> &pyramid, const std::vector<MatT> &blurred,
+                 std::vector<std::vector<KeyPointT>> &allKeypoints, const std::vector<PointT> &pattern,
+                 const std::vector<int> &umax, std::vector<uint8_t> &desc)
+{
+    osg_ctx *ctx = thread_ctx();
+    const int levels = (int)allKeypoints.size();
+    std::vector<float> x, y;
+    std::vector<int32_t> lev;
+    for (int l = 0; l < levels; l++)
+        for (const KeyPointT &kp : allKeypoints[l]) {
+            x.push_back(kp.pt.x);
+            y.push_back(kp.pt.y);
+            lev.push_back(l);
+        }
+    const int n = (int)x.size();
+    if (pattern.size() != 512 || umax.size() < 16) throw Error(OSG_E_INVALID, "orb_describe: pattern / umax shape");
+    std::vector<int32_t> pat(2 * pattern.size());
+    for (size_t i = 0; i < pattern.size(); i++) {  // cv::Point -> (x, y) int pairs
+        pat[2 * i] = pattern[i].x;
+        pat[2 * i + 1] = pattern[i].y;
+    }
+    std::vector<int32_t> um(umax.begin(), umax.begin() + 16);
+    PyramidView<MatT> raw(pyramid, levels), blur(blurred, levels);
+    osg_orb_keypoints K{n, x.data(), y.data(), lev.data()};
+    std::vector<float> angle(n);
+    desc.assign((size_t)n * 32, 0);
+    const int outside = check(ctx, osg_orb_describe(ctx, &raw.v, &blur.v, &K, pat.data(), um.data(), 1, angle.data(),
+                                                    desc.data()),
+                              "osg_orb_describe");
+    int i = 0;
+    for (int l = 0; l < levels; l++)
+        for (KeyPointT &kp : allKeypoints[l]) kp.angle = angle[i++];
+    return outside;
+}
+
 // ----------------------------------------------------------------- b3 SearchForTriangulation
 // ref:src/ORBmatcher.cc:1045-1328.  vMatchedPairs = (KF1 index, KF2 index) in ascending KF1 index.
 // The epipole and the F12 matrices come from the hook (the reference's Sophus / Eigen code).

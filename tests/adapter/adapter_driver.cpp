@@ -1,7 +1,7 @@
 // adapter_driver.cpp — runs adapters/orbslam3/osg_orbslam3.h on mock ORB-SLAM3 objects built from
 // arrays written by tests/test_adapter.py, and writes the adapter's results back (test-only).
 //
-//   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba fuse fuse_sim3 triang distinct sim3 sim3_kfs init stereo gba merge_lba
+//   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba fuse fuse_sim3 triang distinct sim3 sim3_kfs init stereo gba merge_lba orb
 //
 // Array file: repeated {u32 name_len, name, u8 dtype ('b' u8, 'i' i32, 'f' f32, 'd' f64), u64 count,
 // data}.
@@ -777,6 +777,45 @@ int main(int argc, char **argv)
             out["nmatches"] = make('i', std::vector<int32_t>{nm});
             out["ur"] = make('f', F.mvuRight);
             out["depth"] = make('f', F.mvDepth);
+        } else if (mode == "orb") {
+            // levels "O.raw" / "O.blur" concatenated with "O.dims" (rows, cols); keypoints "O.x", "O.y",
+            // "O.level" (sorted by level); "O.pattern" (512 x 2), "O.umax" (16).  mvImagePyramid levels are
+            // ROIs of wider rows (step = cols + 7); the blurred levels are continuous clones
+            const Arr &dims = get(in, "O.dims");
+            const int levels = (int)dims.n / 2;
+            ORBextractor ex;
+            std::vector<cv::Mat> blurred;
+            const uint8_t *sr = get(in, "O.raw").p<uint8_t>(), *sb = get(in, "O.blur").p<uint8_t>();
+            for (int l = 0; l < levels; l++) {
+                const int rows = dims.p<int32_t>()[2 * l], cols = dims.p<int32_t>()[2 * l + 1];
+                cv::Mat m(rows, cols, (size_t)cols + 7), b(rows, cols);
+                for (int r = 0; r < rows; r++) std::memcpy(m.ptr<unsigned char>(r), sr + (size_t)r * cols, cols);
+                std::memcpy(b.buf.data(), sb, (size_t)rows * cols);
+                sr += (size_t)rows * cols;
+                sb += (size_t)rows * cols;
+                ex.mvImagePyramid.push_back(std::move(m));
+                blurred.push_back(std::move(b));
+            }
+            const Arr &pa = get(in, "O.pattern"), &um = get(in, "O.umax");
+            for (size_t i = 0; i < pa.n / 2; i++) ex.pattern.push_back(cv::Point{pa.p<int32_t>()[2 * i], pa.p<int32_t>()[2 * i + 1]});
+            ex.umax.assign(um.p<int32_t>(), um.p<int32_t>() + um.n);
+            std::vector<std::vector<cv::KeyPoint>> all(levels);
+            const Arr &kx = get(in, "O.x");
+            for (size_t i = 0; i < kx.n; i++) {
+                cv::KeyPoint kp;
+                kp.pt.x = kx.p<float>()[i];
+                kp.pt.y = get(in, "O.y").p<float>()[i];
+                kp.angle = -7.0f;  // overwritten
+                all[get(in, "O.level").p<int32_t>()[i]].push_back(kp);
+            }
+            std::vector<uint8_t> desc;
+            const int n_out = osg_orbslam3::orb_describe(ex.mvImagePyramid, blurred, all, ex.pattern, ex.umax, desc);
+            std::vector<float> ang;
+            for (auto &lv : all)
+                for (auto &kp : lv) ang.push_back(kp.angle);
+            out["n_out"] = make('i', std::vector<int32_t>{n_out});
+            out["angle"] = make('f', ang);
+            out["desc"] = make('b', desc);
         } else if (mode == "distinct") {
             // keyframes: "K.desc" (nk x nkp rows), "K.bad"; MapPoints: "M.bad", "M.desc" (initial);
             // observations CSR "O.start" / "O.kf" / "O.left" / "O.right"

@@ -16,6 +16,9 @@
 #include "osg_ba.h"
 
 namespace cv {
+struct Point {
+    int x = 0, y = 0;
+};
 struct Point2f {
     float x = 0, y = 0;
 };
@@ -88,6 +91,8 @@ struct MapPoint {
 
 struct ORBextractor {
     std::vector<cv::Mat> mvImagePyramid;
+    std::vector<cv::Point> pattern;  // ref:include/ORBextractor.h (512 points of bit_pattern_31_)
+    std::vector<int> umax;           // HALF_PATCH_SIZE + 1 row half-widths
 };
 
 struct Frame {

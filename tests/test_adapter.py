@@ -597,6 +597,29 @@ def test_adapter_compute_stereo_matches(driver, tmp_path, oracle):
 
 
 @pytest.mark.gpu
+def test_adapter_orb_describe(driver, tmp_path, oracle):
+    """ORBextractor's orientation + descriptor stages through the adapter: allKeypoints per level (level
+    coordinates, 16 px from the edges as FAST leaves them), mvImagePyramid as ROIs with a row step, the
+    blurred clones, the extractor's pattern / umax; KeyPoint::angle and the descriptor rows written
+    back in level order; the oracle's values bit for bit."""
+    from orb_slam3_comments_ghr_amd import orb
+    rng = np.random.default_rng(830)
+    raw, blur, x, y, level = orb.synth_orb_frame(rng, n=1200, edge=16, fractional=True)
+    order = np.argsort(level, kind="stable")
+    x, y, level = x[order], y[order], level[order]
+    pat = orb.synth_pattern(rng)
+    arrays = {"O.raw": np.concatenate([lv.reshape(-1) for lv in raw]),
+              "O.blur": np.concatenate([lv.reshape(-1) for lv in blur]),
+              "O.dims": np.array([lv.shape for lv in raw], np.int32).reshape(-1),
+              "O.x": x, "O.y": y, "O.level": level, "O.pattern": pat.reshape(-1), "O.umax": orb.ic_umax()}
+    out = run(driver, tmp_path, "orb", arrays)
+    ang, desc, n_out = oc.orb_describe(oracle, raw, blur, x, y, level, pat)
+    assert n_out >= 0 and int(out["n_out"][0]) == n_out
+    np.testing.assert_array_equal(out["angle"].view(np.int32), ang.view(np.int32))
+    np.testing.assert_array_equal(out["desc"].reshape(-1, 32), desc)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("robust,loop", [(False, 7), (True, 0)])
 def test_adapter_global_bundle_adjustment(driver, tmp_path, ctx, robust, loop):
     """Optimizer::BundleAdjustment through the adapter on a mock map (KeyFrame 0 = init / origin, the
