@@ -61,6 +61,9 @@ void oracle_dbow_transform_batch(const osg_vocabulary_desc *V, const uint8_t *de
                                  int levelsup, osg_bow_out *out);
 
 /* bundle adjustment (oracle_ba.c) */
+double oracle_ref_pow3(double t);  /* the reference's libm calls, correctly rounded */
+double oracle_ref_sin(double x);
+double oracle_ref_cos(double x);
 int oracle_pose_optimization(const osg_pose_problem *P, osg_pose_result *R);
 int oracle_local_bundle_adjustment(const osg_ba_graph *G, osg_ba_result *R,
                                    const volatile uint8_t *stop_flag);

@@ -33,6 +33,75 @@
 
 #include "oracle.h"
 
+/* ---------------------------------------------------------------- libm calls of the reference
+ * SE3Quat::exp's sin(theta), cos(theta), pow(theta, 3) and the LM rule's pow(2 rho - 1, 3) are
+ * evaluated CORRECTLY ROUNDED here: the mathematical value carried in double-double (~106 bits)
+ * and rounded once.  The reference takes them from whatever libm it links; glibc 2.35 misrounds
+ * 0.06-0.09 % of these arguments, so the reference's last bit is platform-dependent, and the
+ * correctly rounded value is the one canonical reading of the expression.  This restatement sums
+ * the Taylor terms by their recurrence (term_k = -term_{k-1} x^2 / ((2k+o-1)(2k+o))), unlike the
+ * device's Horner over tabulated coefficients (csrc/exact_math.h); tests/test_exact_math.py checks
+ * both against mpmath and against each other.  sin / cos take the series on [0, 0.8] (LM update
+ * magnitudes) and libm beyond, like the device. */
+typedef struct {
+    double hi, lo;
+} ddouble;
+static ddouble dd_norm(double a, double b)
+{ /* fast two-sum, |a| >= |b| */
+    ddouble r;
+    r.hi = a + b;
+    r.lo = b - (r.hi - a);
+    return r;
+}
+static ddouble dd_sum(ddouble a, ddouble b)
+{
+    const double s = a.hi + b.hi, v = s - a.hi;
+    const double e = (a.hi - (s - v)) + (b.hi - v);
+    return dd_norm(s, e + a.lo + b.lo);
+}
+static ddouble dd_prod(ddouble a, ddouble b)
+{
+    const double p = a.hi * b.hi;
+    const double e = fma(a.hi, b.hi, -p);
+    return dd_norm(p, e + (a.hi * b.lo + a.lo * b.hi));
+}
+static ddouble dd_div_int(ddouble a, double d)
+{ /* a / d for an exactly representable integer d */
+    const double q1 = a.hi / d;
+    const double r = fma(-q1, d, a.hi) + a.lo; /* remainder, exact first term */
+    return dd_norm(q1, r / d);
+}
+double oracle_ref_pow3(double t)
+{
+    const double p = t * t, q = p * t;
+    if (!(fabs(q) < 1e300) || !(fabs(p) < 1e300) || q == 0.0) return q;
+    ddouble T = {t, 0.0};
+    ddouble c = dd_prod(dd_prod(T, T), T);
+    return c.hi + c.lo;
+}
+static double ref_series(double x, int odd)
+{
+    ddouble X = {x, 0.0};
+    const ddouble x2 = dd_prod(X, X);
+    ddouble term = odd ? X : (ddouble){1.0, 0.0}, sum = term;
+    for (int k = 1; k < 30; k++) {
+        term = dd_div_int(dd_prod(term, x2), (double)((2 * k - 1 + odd) * (2 * k + odd)));
+        term.hi = -term.hi;
+        term.lo = -term.lo;
+        sum = dd_sum(sum, term);
+        if (fabs(term.hi) < 1e-40 * fabs(sum.hi)) break;
+    }
+    return sum.hi + sum.lo;
+}
+double oracle_ref_sin(double x)
+{
+    return (x >= 0.0 && x <= 0.8) ? ref_series(x, 1) : sin(x);
+}
+double oracle_ref_cos(double x)
+{
+    return (x >= 0.0 && x <= 0.8) ? ref_series(x, 0) : cos(x);
+}
+
 /* ---------------------------------------------------------------- SE3Quat (x y z w | t) */
 typedef struct {
     double q[4]; /* x y z w (Eigen coeffs order) */
@@ -163,9 +232,9 @@ static void se3_exp(const double *upd, se3 *O)
             for (int j = 0; j < 3; j++) R[i][j] = (i == j ? 1.0 : 0.0) + Om[i][j] + Om2[i][j];
         memcpy(V, R, sizeof R);
     } else {
-        const double a = sin(theta) / theta;
-        const double b = (1 - cos(theta)) / (theta * theta);
-        const double c = (theta - sin(theta)) / (pow(theta, 3));
+        const double a = oracle_ref_sin(theta) / theta;
+        const double b = (1 - oracle_ref_cos(theta)) / (theta * theta);
+        const double c = (theta - oracle_ref_sin(theta)) / (oracle_ref_pow3(theta));
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 3; j++) {
                 R[i][j] = (i == j ? 1.0 : 0.0) + a * Om[i][j] + b * Om2[i][j];
@@ -857,7 +926,7 @@ static int g_lm_solve(graph_t *g, int iteration, int require_positive)
         scale += 1e-3;
         rho /= scale;
         if (rho > 0 && isfinite(tempChi)) {
-            double alpha = 1. - pow((2 * rho - 1), 3);
+            double alpha = 1. - oracle_ref_pow3(2 * rho - 1);
             alpha = fmin(alpha, 2. / 3.);
             const double scaleFactor = fmax(1. / 3., alpha);
             g->lambda *= scaleFactor;

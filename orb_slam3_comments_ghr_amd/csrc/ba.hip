@@ -1691,7 +1691,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
             const double scale = o[1] + 1e-3;
             rho /= scale;
             if (rho > 0 && std::isfinite(tempChi)) {
-                double alpha = 1. - std::pow((2 * rho - 1), 3);
+                double alpha = 1. - osgx::cube_rn(2 * rho - 1);  // pow(., 3), correctly rounded
                 alpha = std::min(alpha, 2. / 3.);
                 const double scaleFactor = std::max(1. / 3., alpha);
                 h.lambda *= scaleFactor;

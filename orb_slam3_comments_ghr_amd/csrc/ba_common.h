@@ -11,6 +11,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "exact_math.h"
 #include "osg_internal.h"
 
 namespace osgba {
@@ -60,6 +61,34 @@ __host__ __device__ inline void quat_to_R(const double *q, double R[3][3])
     R[1][0] = txy + twz; R[1][1] = 1 - (txx + tzz); R[1][2] = tyz - twx;
     R[2][0] = txz - twy; R[2][1] = tyz + twx; R[2][2] = 1 - (txx + tyy);
 }
+// Eigen quaternionbase_assign_impl<Matrix3>; the largest-diagonal branch is spelled out per
+// index (constant subscripts keep the matrix in registers)
+__host__ __device__ inline void quat_from_R_branch(const double m[3][3], int i, double *q)
+{
+    const int j = (i + 1) % 3, k = (j + 1) % 3;
+    double mii, mjj, mkk, mkj, mjk, mji, mij, mki, mik;
+    if (i == 0) {
+        mii = m[0][0]; mjj = m[1][1]; mkk = m[2][2]; mkj = m[2][1]; mjk = m[1][2];
+        mji = m[1][0]; mij = m[0][1]; mki = m[2][0]; mik = m[0][2];
+    } else if (i == 1) {
+        mii = m[1][1]; mjj = m[2][2]; mkk = m[0][0]; mkj = m[0][2]; mjk = m[2][0];
+        mji = m[2][1]; mij = m[1][2]; mki = m[0][1]; mik = m[1][0];
+    } else {
+        mii = m[2][2]; mjj = m[0][0]; mkk = m[1][1]; mkj = m[1][0]; mjk = m[0][1];
+        mji = m[0][2]; mij = m[2][0]; mki = m[1][2]; mik = m[2][1];
+    }
+    double s = sqrt(mii - mjj - mkk + 1.0);
+    const double qi = 0.5 * s;
+    s = 0.5 / s;
+    const double qw = (mkj - mjk) * s;
+    const double qj = (mji + mij) * s;
+    const double qk = (mki + mik) * s;
+    q[3] = qw;
+    q[0] = i == 0 ? qi : (j == 0 ? qj : qk);
+    q[1] = i == 1 ? qi : (j == 1 ? qj : qk);
+    q[2] = i == 2 ? qi : (j == 2 ? qj : qk);
+    (void)k;
+}
 __host__ __device__ inline void R_to_quat(const double m[3][3], double *q)
 {
     const double t = m[0][0] + m[1][1] + m[2][2];
@@ -73,14 +102,8 @@ __host__ __device__ inline void R_to_quat(const double m[3][3], double *q)
     } else {
         int i = 0;
         if (m[1][1] > m[0][0]) i = 1;
-        if (m[2][2] > m[i][i]) i = 2;
-        const int j = (i + 1) % 3, k = (j + 1) % 3;
-        double s = sqrt(m[i][i] - m[j][j] - m[k][k] + 1.0);
-        q[i] = 0.5 * s;
-        s = 0.5 / s;
-        q[3] = (m[k][j] - m[j][k]) * s;
-        q[j] = (m[j][i] + m[i][j]) * s;
-        q[k] = (m[k][i] + m[i][k]) * s;
+        if (m[2][2] > (i == 0 ? m[0][0] : m[1][1])) i = 2;
+        quat_from_R_branch(m, i, q);
     }
 }
 __host__ __device__ inline SE3 se3_from7(const double *p)
@@ -130,9 +153,11 @@ __host__ __device__ inline SE3 se3_exp(const double *upd)
                 V[i][j] = R[i][j];
             }
     } else {
-        const double a = sin(theta) / theta;
-        const double b = (1 - cos(theta)) / (theta * theta);
-        const double c = (theta - sin(theta)) / (theta * theta * theta);
+        // sin / cos / pow(theta, 3) of the reference, correctly rounded (exact_math.h)
+        const double st = osgx::sin_ref(theta);
+        const double a = st / theta;
+        const double b = (1 - osgx::cos_ref(theta)) / (theta * theta);
+        const double c = (theta - st) / osgx::cube_rn(theta);
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 3; j++) {
                 R[i][j] = (i == j ? 1.0 : 0.0) + a * Om[i][j] + b * Om2[i][j];
@@ -151,6 +176,53 @@ __host__ __device__ inline void se3_oplus(SE3 &T, const double *upd)
     T = se3_mul(E, T);
 }
 
+// sin / cos of psi = atan2f(...) in [-pi, pi] for the KannalaBrandt8 projection: Cody-Waite
+// reduction by pi/2 (two-term constant) and the classic odd / even minimax kernels (fdlibm's
+// published coefficients, error < 1 ulp).  The device library's sin / cos carry a Payne-Hanek
+// branch for huge arguments whose register footprint would set the whole pose kernel's; psi never
+// needs it.  Like the device libm, this is not bit-identical to glibc, which is why KB8 poses are
+// compared within the fisheye tolerance.
+__host__ __device__ inline double kb_sin_kernel(double x, double y)
+{
+    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    const double z = x * x, v = z * x;
+    const double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+    return x - ((z * (0.5 * y - v * r) - y) - v * S1);
+}
+__host__ __device__ inline double kb_cos_kernel(double x, double y)
+{
+    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    const double z = x * x;
+    const double r = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+    const double hz = 0.5 * z, w = 1.0 - hz;
+    return w + (((1.0 - w) - hz) + (z * r - x * y));
+}
+__host__ __device__ inline void kb_sincos(double x, double &sn, double &cs)
+{
+    if (!(fabs(x) <= 4.0)) {
+        sn = sin(x);
+        cs = cos(x);
+        return;
+    }
+    const double pio2_1 = 1.57079632673412561417e+00, pio2_1t = 6.07710050650619224932e-11;
+    const double n = rint(x * 6.36619772367581382433e-01);
+    const double r = x - n * pio2_1;  // exact: n * pio2_1 has 35 significant bits
+    const double w = n * pio2_1t;
+    const double y0 = r - w;
+    const double y1 = (r - y0) - w;
+    const double s0 = kb_sin_kernel(y0, y1), c0 = kb_cos_kernel(y0, y1);
+    switch (((int)n) & 3) {
+    case 0: sn = s0; cs = c0; break;
+    case 1: sn = c0; cs = -s0; break;
+    case 2: sn = -s0; cs = -c0; break;
+    default: sn = -c0; cs = s0; break;
+    }
+}
+
 // ------------------------------------------------------------------------------ cameras
 __device__ inline void cam_project(const osg_camera &c, const double *v, double *uv)
 {
@@ -164,8 +236,10 @@ __device__ inline void cam_project(const osg_camera &c, const double *v, double 
         const double theta7 = theta5 * theta2;
         const double theta9 = theta7 * theta2;
         const double r = theta + c.p[4] * theta3 + c.p[5] * theta5 + c.p[6] * theta7 + c.p[7] * theta9;
-        uv[0] = c.p[0] * r * cos(psi) + c.p[2];
-        uv[1] = c.p[1] * r * sin(psi) + c.p[3];
+        double sp, cp;
+        kb_sincos(psi, sp, cp);
+        uv[0] = c.p[0] * r * cp + c.p[2];
+        uv[1] = c.p[1] * r * sp + c.p[3];
     } else {
         uv[0] = c.p[0] * v[0] / v[2] + c.p[2];
         uv[1] = c.p[1] * v[1] / v[2] + c.p[3];

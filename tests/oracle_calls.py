@@ -50,6 +50,9 @@ def declare(lib: C.CDLL) -> C.CDLL:
                                               C.c_int, vp]
     lib.oracle_search_by_bow_kf_kf.argtypes = [C.POINTER(OsgBowSide), C.POINTER(OsgBowSide), f32,
                                                C.c_int, vp]
+    for f in ("oracle_ref_pow3", "oracle_ref_sin", "oracle_ref_cos"):
+        getattr(lib, f).argtypes = [C.c_double]
+        getattr(lib, f).restype = C.c_double
     lib.oracle_pose_optimization.argtypes = [C.POINTER(OsgPoseProblem), C.POINTER(OsgPoseResult)]
     lib.oracle_local_bundle_adjustment.argtypes = [C.POINTER(OsgBaGraph), C.POINTER(OsgBaResult),
                                                    vp]

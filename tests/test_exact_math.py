@@ -1,0 +1,55 @@
+"""The reference's libm calls on the LM path — sin / cos / pow(theta, 3) in SE3Quat::exp
+(ref:Thirdparty/g2o/g2o/types/se3quat.h:223-257) and pow(2 rho - 1, 3) in the LM rule
+(ref:Thirdparty/g2o/g2o/core/optimization_algorithm_levenberg.cpp:134-140) — are evaluated
+correctly rounded on both sides: the oracle's double-double term recurrence (oracle/oracle_ba.c)
+and the device's double-double Horner (csrc/exact_math.h, compiled here for the host from the same
+source the kernels include).  Both must equal mpmath's correctly rounded value, and each other."""
+import os
+import random
+import subprocess
+
+import pytest
+
+from tests import oracle_calls as oc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+mpmath = pytest.importorskip("mpmath")
+
+
+def _args(n, seed):
+    rng = random.Random(seed)
+    th = [1e-6 * (0.8 / 1e-6) ** rng.random() for _ in range(n)]  # LM rotation-update magnitudes
+    t = [2 * (4 * rng.random()) - 1 for _ in range(n)]               # 2 rho - 1
+    return th, t
+
+
+def test_oracle_libm_calls_correctly_rounded():
+    lib = oc.load()
+    mpmath.mp.prec = 200
+    th, t = _args(3000, 7)
+    for x in th:
+        X = mpmath.mpf(x)
+        assert lib.oracle_ref_sin(x) == float(mpmath.sin(X)), x
+        assert lib.oracle_ref_cos(x) == float(mpmath.cos(X)), x
+        assert lib.oracle_ref_pow3(x) == float(X ** 3), x
+    for x in t:
+        assert lib.oracle_ref_pow3(x) == float(mpmath.mpf(x) ** 3), x
+    # hard cases for glibc (it misrounds these; both sides must not)
+    for x, want in [(0.13004755302255505, 0.12968129423820343), (0.37051921509751778, 0.36209946163395573)]:
+        assert lib.oracle_ref_sin(x) == want
+    assert lib.oracle_ref_pow3(0.42910327558778544) == 0.079010623555401518
+    # outside the series interval both sides use libm; special values pass through
+    assert lib.oracle_ref_pow3(0.0) == 0.0 and lib.oracle_ref_pow3(-2.0) == -8.0
+    assert lib.oracle_ref_pow3(1e200) == float("inf")
+
+
+def test_device_math_equals_oracle(tmp_path):
+    """Host build of csrc/exact_math.h (the kernels' code) against the oracle on 400k arguments."""
+    oc.load()
+    exe = str(tmp_path / "emc")
+    subprocess.run(["g++", "-O2", os.path.join(ROOT, "tools", "exact_math_check.cc"), "-L" + os.path.join(ROOT, "oracle"),
+                    "-loracle", "-Wl,-rpath," + os.path.join(ROOT, "oracle"), "-o", exe], check=True)
+    out = subprocess.run([exe, "400000"], check=True, capture_output=True, text=True).stdout
+    import json
+    r = json.loads(out)
+    assert r["sin"] == 0 and r["cos"] == 0 and r["cube"] == 0, r

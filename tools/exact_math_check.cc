@@ -1,0 +1,34 @@
+// Host build of csrc/exact_math.h (the device's correctly rounded sin / cos / cube, compiled for
+// the CPU from the same source) against the oracle's independent __float128 versions.  Prints the
+// mismatch counts; tests/test_exact_math.py builds and runs it.
+//   g++ -O2 tools/exact_math_check.cc -Loracle -loracle -Wl,-rpath,$PWD/oracle -o /tmp/emc
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+
+#include "../orb_slam3_comments_ghr_amd/csrc/exact_math.h"
+
+extern "C" {
+double oracle_ref_pow3(double t);
+double oracle_ref_sin(double x);
+double oracle_ref_cos(double x);
+}
+
+int main(int argc, char **argv)
+{
+    const long N = argc > 1 ? atol(argv[1]) : 2000000;
+    std::mt19937_64 g(12345);
+    std::uniform_real_distribution<double> U(0, 1);
+    long bad_sin = 0, bad_cos = 0, bad_cube = 0;
+    for (long i = 0; i < N; i++) {
+        const double th = 1e-6 * std::pow(0.85 / 1e-6, U(g));  // log-uniform, across the 0.8 switch
+        if (osgx::sin_ref(th) != oracle_ref_sin(th)) bad_sin++;
+        if (osgx::cos_ref(th) != oracle_ref_cos(th)) bad_cos++;
+        if (osgx::cube_rn(th) != oracle_ref_pow3(th)) bad_cube++;
+        const double t = 2 * (8 * U(g)) - 1;  // 2 rho - 1
+        if (osgx::cube_rn(t) != oracle_ref_pow3(t)) bad_cube++;
+    }
+    std::printf("{\"n\": %ld, \"sin\": %ld, \"cos\": %ld, \"cube\": %ld}\n", N, bad_sin, bad_cos, bad_cube);
+    return 0;
+}
