@@ -9,6 +9,10 @@ OBJDIR = build/obj
 HIPFLAGS = --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-function
 # bit-exact float geometry in the matcher and BowVector sums: no FMA contraction in those units
 EXACT = -ffp-contract=off
+# make POSE_PROF=1: phase cycle counters in k_pose_opt (tools/pose_prof.py)
+ifdef POSE_PROF
+HIPFLAGS += -DOSG_POSE_PROF
+endif
 HDRS = include/osg.h include/osg_ba.h $(CSRC)/osg_internal.h
 
 OBJS = $(OBJDIR)/runtime.o $(OBJDIR)/hamming.o $(OBJDIR)/match.o $(OBJDIR)/pose.o $(OBJDIR)/ba.o $(OBJDIR)/dbow.o $(OBJDIR)/fuse.o $(OBJDIR)/triang.o $(OBJDIR)/desc.o $(OBJDIR)/sim3.o $(OBJDIR)/init.o $(OBJDIR)/stereo.o $(OBJDIR)/orb.o

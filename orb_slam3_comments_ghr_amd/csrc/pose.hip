@@ -1,28 +1,33 @@
 // pose.hip — Optimizer::PoseOptimization (ref:src/Optimizer.cc:71-420) for a batch of frames.
 //
-// One wave (64 lanes) per frame, persistent over the whole call: 4 rounds x optimize(10) with
-// the g2o Levenberg-Marquardt control flow (ref:Thirdparty/g2o/g2o/core/
-// optimization_algorithm_levenberg.cpp:61-169) executed in-kernel, no workgroup barrier anywhere.
+// NW waves (1, 2, 4 or 8 x 64 lanes) per frame, persistent over the whole call: 4 rounds x
+// optimize(10) with the g2o Levenberg-Marquardt control flow (ref:Thirdparty/g2o/g2o/core/
+// optimization_algorithm_levenberg.cpp:61-169) executed in-kernel.  The host picks NW: several
+// waves when few frames share the chip (the drop-in's one-frame call: latency), one when a batch
+// fills the chip's wave slots (throughput).
 //
-//   * Edge e lives on lane e % 64 of chunk e / 64.  A pass evaluates one chunk per step: every
-//     lane computes its edge's terms, writes them to a padded LDS tile, and the terms are summed
-//     SEQUENTIALLY IN EDGE ORDER — the order of g2o's loops over _activeEdges
-//     (activeRobustChi2, ref:Thirdparty/g2o/g2o/core/sparse_optimizer.cpp:104-120; buildSystem,
-//     ref:Thirdparty/g2o/g2o/core/block_solver.hpp:529-557).  The iteration pass carries 28
-//     streams (the 21 upper entries of H, the 6 of b, and chi2), summed by lanes 0..27 at once;
-//     the trial pass carries chi2 only.  Together with -ffp-contract=off and the correctly
-//     rounded sin / cos / cube of exact_math.h, every double the kernel forms is the one the
-//     oracle forms, so iteration counts, trial counts, outlier flags and the pose are identical
-//     to it (pinhole; KannalaBrandt8 differs only through the device atan2f / atan2).
+//   * Edge e lives on lane e % 64 of chunk e / 64; chunk c is computed by wave c % NW.  A pass
+//     evaluates NW chunks per step: every lane computes its edge's terms into its wave's padded
+//     LDS tile, and wave 0 sums the tiles SEQUENTIALLY IN EDGE ORDER — the order of g2o's loops
+//     over _activeEdges (activeRobustChi2, ref:Thirdparty/g2o/g2o/core/sparse_optimizer.cpp:
+//     104-120; buildSystem, ref:Thirdparty/g2o/g2o/core/block_solver.hpp:529-557).  The iteration
+//     pass carries 28 streams (the 21 upper entries of H, the 6 of b, and chi2), summed by lanes
+//     0..27 at once; the trial pass carries chi2 only.  Together with -ffp-contract=off and the
+//     correctly rounded sin / cos / cube of exact_math.h, every double the kernel forms is the one
+//     the oracle forms, so iteration counts, trial counts, outlier flags and the pose are
+//     identical to it (pinhole; KannalaBrandt8 differs only through the device atan2f / atan2).
 //   * The first chi2 pass of an LM iteration and buildSystem run at the same pose, so they are
-//     one fused pass (errors recomputed from the pose, never stored).  The classification after a
+//     one pass (errors recomputed from the pose, never stored).  The classification after a
 //     round reads each active edge's error at the pose of the LAST chi2 evaluation (a rejected
 //     trial's, when the last trial was rejected), exactly as the reference reads e->chi2() from
 //     the stale _error; inactive edges are re-evaluated at the final pose (computeError()).
-//   * The 6x6 damped solve, exp-map update and lambda control are evaluated by every lane on
-//     wave-uniform values (no broadcast needed).  The edge arrays are read from global memory on
-//     every pass (L1/L2 resident); the only global stores are the outlier flags, once per round.
+//   * The 6x6 damped solve, exp-map update and lambda control are evaluated by every lane of
+//     every wave on identical values (each wave keeps a private copy of the pose state, so none
+//     can overwrite what a slower wave still reads).  Outlier flags are a per-lane register
+//     bitmask, stored once at the end; the edge arrays are re-read every pass (L2 resident).
+#include <algorithm>
 #include <cfloat>
+#include <cstdlib>
 #include <vector>
 
 #include "ba_common.h"
@@ -35,7 +40,7 @@ namespace {
 
 constexpr int PW = 64;        // lanes per frame
 constexpr int NT = 28;        // H upper (21) | -b terms (6) | robust chi2 (1)
-constexpr int LDS_ROW = 65;   // padded row: lane q reads row q column j -> banks 2q + 2j
+constexpr int ROW = 66;       // padded tile row, 16-byte aligned (ds_read_b128 in seq_sum)
 
 struct PoseProbDev {
     double pose[7];
@@ -43,6 +48,16 @@ struct PoseProbDev {
     int edge_off;  // into the batched edge arrays
     osg_camera cam, cam2;
 };
+
+#ifdef OSG_POSE_PROF
+// phase cycle counters of the first frames (profiling builds only: make POSE_PROF=1)
+__device__ unsigned long long g_pose_prof[64][8];
+#define PROF_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define PROF_ADD(slot, t0) if (threadIdx.x == 0 && blockIdx.x < 64) g_pose_prof[blockIdx.x][slot] += __builtin_amdgcn_s_memtime() - (t0)
+#else
+#define PROF_T(v)
+#define PROF_ADD(slot, t0)
+#endif
 
 struct PoseOut {
     double pose[7];
@@ -239,9 +254,31 @@ __device__ inline double edge_chi2_of(const double *ev, bool stereo, double w)
     return s;
 }
 
-// sum of the first `cnt` entries of LDS row `row` in order, onto acc
+// sum of the first `cnt` (<= 64) entries of a 16-byte aligned LDS row, in order, onto acc.  Full
+// rows go 16 entries at a time with the next 16 already loading (ds_read_b128): the add chain, one
+// dependent add per edge, is the floor of every pass.
 __device__ inline double seq_sum(double acc, const double *row, int cnt)
 {
+    if (cnt == PW) {
+        const double2 *r2 = (const double2 *)row;
+        double2 cur[8], nxt[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) cur[u] = r2[u];
+#pragma unroll
+        for (int blk = 0; blk < 4; blk++) {
+            if (blk < 3)
+#pragma unroll
+                for (int u = 0; u < 8; u++) nxt[u] = r2[8 * (blk + 1) + u];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                acc += cur[u].x;
+                acc += cur[u].y;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) cur[u] = nxt[u];
+        }
+        return acc;
+    }
     int j = 0;
     for (; j + 8 <= cnt; j += 8) {
         double v[8];
@@ -254,24 +291,37 @@ __device__ inline double seq_sum(double acc, const double *row, int cnt)
     return acc;
 }
 
-// per-frame state in LDS: read where used, so the long-lived values do not pin registers
-struct PoseWS {
-    SE3 pose, backup, teval, trl;
+// frame constants and the cross-wave results (written by one wave, read by all after a barrier)
+struct PoseShared {
     osg_camera cam, cam2;
+    SE3 trl;
+    double sys[NT];  // the last buildSystem sums: H upper (21) | b (6) | robust chi2
+    double chi;      // the last trial's chi2
+    int n_act[8], n_bad[8];
+};
+// one wave's copy of the wave-uniform LM state: every wave runs the same LM control on the same
+// sums, and a private copy keeps a wave that runs ahead from overwriting what another still reads
+struct PoseWave {
+    SE3 pose, backup, teval;
     double xs[6];  // the solver's x (kept when a factorisation fails)
-    double sys[NT];
 };
 
-__global__ __launch_bounds__(PW) void k_pose_opt(const PoseProbDev *__restrict__ probs,
-                                                 const int8_t *__restrict__ e_kind,
-                                                 const double *__restrict__ e_xw,
-                                                 const double *__restrict__ e_obs,
-                                                 const float *__restrict__ e_isig2,
-                                                 uint8_t *__restrict__ e_out,
-                                                 PoseOut *__restrict__ out)
+// NW waves per frame.  Superchunk s holds chunks s*NW .. s*NW+NW-1 (64 edges each, chunk s*NW+w on
+// wave w); the waves fill their LDS tiles in parallel, then wave 0 adds the tiles in edge order.
+// Outlier flags live in a register bitmask per lane (bit s <-> edge (s*NW+wave)*64+lane) and are
+// stored once at the end.
+template <int NW>
+__global__ __launch_bounds__(NW *PW) void k_pose_opt(const PoseProbDev *__restrict__ probs,
+                                                     const int8_t *__restrict__ e_kind,
+                                                     const double *__restrict__ e_xw,
+                                                     const double *__restrict__ e_obs,
+                                                     const float *__restrict__ e_isig2,
+                                                     uint8_t *__restrict__ e_out,
+                                                     PoseOut *__restrict__ out)
 {
-    __shared__ double s_t[NT * LDS_ROW];
-    __shared__ PoseWS W;
+    __shared__ __attribute__((aligned(16))) double s_t[NW * NT * ROW];
+    __shared__ PoseShared S;
+    __shared__ PoseWave WV[NW];
     const PoseProbDev &P = probs[blockIdx.x];
     const int n = P.n_edges;
     const int8_t *kind = e_kind + P.edge_off;
@@ -279,12 +329,13 @@ __global__ __launch_bounds__(PW) void k_pose_opt(const PoseProbDev *__restrict__
     const double *obs = e_obs + 3 * (size_t)P.edge_off;
     const float *isig2 = e_isig2 + P.edge_off;
     uint8_t *outl = e_out + P.edge_off;
-    const int lane = threadIdx.x;
-    const int nch = (n + PW - 1) / PW;
+    const int wave = threadIdx.x / PW, lane = threadIdx.x % PW;
+    const int nsc = (n + NW * PW - 1) / (NW * PW);
 
-    for (int e = lane; e < n; e += PW) outl[e] = 0;
+    PROF_T(t_start);
     if (n < 3) {  // ref:src/Optimizer.cc:289-290
-        if (lane == 0) {
+        for (int e = threadIdx.x; e < n; e += NW * PW) outl[e] = 0;
+        if (threadIdx.x == 0) {
             for (int i = 0; i < 7; i++) out[blockIdx.x].pose[i] = P.pose[i];
             out[blockIdx.x].n_inliers = 0;
             out[blockIdx.x].lm_iterations = 0;
@@ -292,17 +343,20 @@ __global__ __launch_bounds__(PW) void k_pose_opt(const PoseProbDev *__restrict__
         }
         return;
     }
-    if (lane == 0) {
-        W.cam = P.cam;
-        W.cam2 = P.cam2;
-        W.trl = se3_from7(P.cam2.trl);
-#pragma unroll
-        for (int i = 0; i < 6; i++) W.xs[i] = 0.0;
+    if (threadIdx.x == 0) {
+        S.cam = P.cam;
+        S.cam2 = P.cam2;
+        S.trl = se3_from7(P.cam2.trl);
     }
-    __builtin_amdgcn_wave_barrier();
-    const osg_camera &cam = W.cam, &cam2 = W.cam2;
-    const SE3 &Trl = W.trl;
-    SE3 &pose = W.pose;
+    PoseWave &W = WV[wave];
+#pragma unroll
+    for (int i = 0; i < 6; i++) W.xs[i] = 0.0;
+    __syncthreads();
+    const osg_camera &cam = S.cam, &cam2 = S.cam2;
+    const SE3 &Trl = S.trl;
+    SE3 &pose = W.pose, &T_eval = W.teval;
+    double *xs = W.xs;
+    double *tile = s_t + wave * NT * ROW;
     Huber hb;
     {
         const float deltaMono = (float)sqrt(5.991);  // const float deltaMono = sqrt(5.991)
@@ -315,106 +369,130 @@ __global__ __launch_bounds__(PW) void k_pose_opt(const PoseProbDev *__restrict__
     int robust = 1;
     int nBad = 0;
     int total_iters = 0, total_trials = 0;
-    double *xs = W.xs;
+    uint64_t om = 0;
+    auto edge_of = [&](int s) { return (s * NW + wave) * PW + lane; };
+    auto active = [&](int s) { return edge_of(s) < n && !((om >> s) & 1); };
+    // the edges of chunk w of superchunk s that exist
+    auto chunk_cnt = [&](int s, int w) { return min(PW, n - (s * NW + w) * PW); };
 
-    // robust chi2 of the edge on this lane for chunk c at pose T (0 when inactive / past n)
-    auto chi_term = [&](int e, const SE3 &T) -> double {
-        if (e >= n || outl[e]) return 0.0;
-        const PEdge E = load_edge(e, kind, xw, obs, isig2);
-        double ev[3];
-        pose_edge_error(E, cam, cam2, Trl, T, ev);
-        const bool st = E.k == OSG_EDGE_STEREO;
-        const double c = edge_chi2_of(ev, st, E.w);
-        if (!robust) return c;
-        double r0, r1;
-        if (st) huber(c, hb.delta_stereo, hb.dsqr_stereo, r0, r1);
-        else huber(c, hb.delta_mono, hb.dsqr_mono, r0, r1);
-        return r0;
-    };
-
-    // activeRobustChi2 at T, summed in edge order (lane 0's chain), broadcast
+    // activeRobustChi2 at T, summed in edge order by wave 0 lane 0, broadcast through S.chi
     auto chi_pass = [&](const SE3 &T) -> double {
         double acc = 0.0;
-        for (int c = 0; c < nch; c++) {
+        for (int s = 0; s < nsc; s++) {
             reload_lds();
-            const double v = chi_term(c * PW + lane, T);
-            s_t[lane] = v;
-            __builtin_amdgcn_wave_barrier();
-            if (lane == 0) acc = seq_sum(acc, s_t, min(PW, n - c * PW));
-            __builtin_amdgcn_wave_barrier();
+            double v = 0.0;
+            if (active(s)) {
+                const PEdge E = load_edge(edge_of(s), kind, xw, obs, isig2);
+                double ev[3];
+                pose_edge_error(E, cam, cam2, Trl, T, ev);
+                const bool st = E.k == OSG_EDGE_STEREO;
+                const double c = edge_chi2_of(ev, st, E.w);
+                v = c;
+                if (robust) {
+                    double r1;
+                    if (st) huber(c, hb.delta_stereo, hb.dsqr_stereo, v, r1);
+                    else huber(c, hb.delta_mono, hb.dsqr_mono, v, r1);
+                }
+            }
+            tile[lane] = v;
+            __syncthreads();
+            if (threadIdx.x == 0)
+                for (int w = 0; w < NW && chunk_cnt(s, w) > 0; w++) acc = seq_sum(acc, s_t + w * NT * ROW, chunk_cnt(s, w));
+            __syncthreads();
         }
-        return readlane_d(acc, 0);
+        if (threadIdx.x == 0) S.chi = acc;
+        __syncthreads();
+        return S.chi;
+    };
+    // per-wave counts -> frame total
+    auto frame_count = [&](int v, int *slot) -> int {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) slot[wave] = v;
+        __syncthreads();
+        int t = 0;
+#pragma unroll
+        for (int w = 0; w < NW; w++) t += slot[w];
+        return t;
     };
 
+    // activeRobustChi2 + buildSystem at T: the 28 sums (H upper | b | robust chi2) in edge order,
+    // lane q of wave 0 adding stream q, into dst
+    auto sys_pass = [&](const SE3 &T, double *dst) {
+        double acc = 0.0;
+        for (int s = 0; s < nsc; s++) {
+            reload_lds();
+            double *col = tile + lane;  // term q of this lane's edge -> tile[q * ROW + lane]
+            if (active(s)) {
+                const PEdge E = load_edge(edge_of(s), kind, xw, obs, isig2);
+                double ev[3];
+                pose_edge_error(E, cam, cam2, Trl, T, ev);
+                const bool st = E.k == OSG_EDGE_STEREO;
+                const double chi = edge_chi2_of(ev, st, E.w);
+                double r0 = chi, rho1 = 1.0;
+                if (robust) {
+                    if (st) huber(chi, hb.delta_stereo, hb.dsqr_stereo, r0, rho1);
+                    else huber(chi, hb.delta_mono, hb.dsqr_mono, r0, rho1);
+                }
+                col[27 * ROW] = r0;
+                double Jp[3][6];
+                pose_edge_jac(E, cam, cam2, Trl, T, Jp);
+                const double ww = rho1 * E.w;
+                int q = 0;
+#pragma unroll
+                for (int i = 0; i < 6; i++)
+#pragma unroll
+                    for (int j = i; j < 6; j++) {
+                        double h = 0;
+                        h += Jp[0][i] * ww * Jp[0][j];
+                        h += Jp[1][i] * ww * Jp[1][j];
+                        if (st) h += Jp[2][i] * ww * Jp[2][j];
+                        col[(q++) * ROW] = h;
+                    }
+#pragma unroll
+                for (int i = 0; i < 6; i++) {
+                    double sb = 0;
+                    sb += rho1 * Jp[0][i] * (E.w * ev[0]);
+                    sb += rho1 * Jp[1][i] * (E.w * ev[1]);
+                    if (st) sb += rho1 * Jp[2][i] * (E.w * ev[2]);
+                    col[(21 + i) * ROW] = -sb;  // b -= s  ==  b + (-s), exactly
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < NT; q++) col[q * ROW] = 0.0;
+            }
+            __syncthreads();
+            if (wave == 0) {  // lane q < 28 adds stream q; the others repeat stream 27, unused
+                const int q = lane < NT ? lane : NT - 1;
+                for (int w = 0; w < NW && chunk_cnt(s, w) > 0; w++)
+                    acc = seq_sum(acc, s_t + (w * NT + q) * ROW, chunk_cnt(s, w));
+            }
+            __syncthreads();
+        }
+        if (wave == 0 && lane < NT) dst[lane] = acc;
+        __syncthreads();
+    };
     for (int it = 0; it < 4; it++) {
         // every round restarts from the input pose (ref:src/Optimizer.cc:306-307)
-        if (lane == 0) {
-            W.pose = se3_from7(P.pose);
-            W.teval = W.pose;
-        }
+        pose = se3_from7(P.pose);
+        T_eval = pose;
         __builtin_amdgcn_wave_barrier();
-        SE3 &T_eval = W.teval;
-        int nact = 0;
-        for (int e = lane; e < n; e += PW) nact += outl[e] ? 0 : 1;
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) nact += __shfl_xor(nact, off);
+        int na = 0;
+        for (int s = 0; s < nsc; s++) na += active(s) ? 1 : 0;
+        const int nact = frame_count(na, S.n_act);
         if (nact > 0) {
             double lambda = 0, ni = 2;
             int nBadLM = 0;
             for (int iter = 0; iter < 10; iter++) {
                 total_iters++;
-                // computeActiveErrors + activeRobustChi2 + buildSystem at `pose`, one pass
-                double acc = 0.0;
-                for (int c = 0; c < nch; c++) {
-                    reload_lds();
-                    const int e = c * PW + lane;
-                    double *col = s_t + lane;  // term q of this lane's edge -> s_t[q * LDS_ROW + lane]
-                    if (e < n && !outl[e]) {
-                        const PEdge E = load_edge(e, kind, xw, obs, isig2);
-                        double ev[3];
-                        pose_edge_error(E, cam, cam2, Trl, pose, ev);
-                        const bool st = E.k == OSG_EDGE_STEREO;
-                        const double chi = edge_chi2_of(ev, st, E.w);
-                        double r0 = chi, rho1 = 1.0;
-                        if (robust) {
-                            if (st) huber(chi, hb.delta_stereo, hb.dsqr_stereo, r0, rho1);
-                            else huber(chi, hb.delta_mono, hb.dsqr_mono, r0, rho1);
-                        }
-                        col[27 * LDS_ROW] = r0;
-                        double Jp[3][6];
-                        pose_edge_jac(E, cam, cam2, Trl, pose, Jp);
-                        const double ww = rho1 * E.w;
-                        int q = 0;
-#pragma unroll
-                        for (int i = 0; i < 6; i++)
-#pragma unroll
-                            for (int j = i; j < 6; j++) {
-                                double h = 0;
-                                h += Jp[0][i] * ww * Jp[0][j];
-                                h += Jp[1][i] * ww * Jp[1][j];
-                                if (st) h += Jp[2][i] * ww * Jp[2][j];
-                                col[(q++) * LDS_ROW] = h;
-                            }
-#pragma unroll
-                        for (int i = 0; i < 6; i++) {
-                            double s = 0;
-                            s += rho1 * Jp[0][i] * (E.w * ev[0]);
-                            s += rho1 * Jp[1][i] * (E.w * ev[1]);
-                            if (st) s += rho1 * Jp[2][i] * (E.w * ev[2]);
-                            col[(21 + i) * LDS_ROW] = -s;  // b -= s  ==  b + (-s), exactly
-                        }
-                    } else {
-#pragma unroll
-                        for (int q = 0; q < NT; q++) col[q * LDS_ROW] = 0.0;
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    if (lane < NT) acc = seq_sum(acc, s_t + lane * LDS_ROW, min(PW, n - c * PW));
-                    __builtin_amdgcn_wave_barrier();
-                }
+                // computeActiveErrors + activeRobustChi2 + buildSystem at `pose`, one pass.  (Summing
+                // buildSystem along with every trial chi2, to skip this pass after an accepted step,
+                // measured slower at every frame size: the Jacobian terms cost more than the pass.)
+                PROF_T(t_h);
+                sys_pass(pose, S.sys);
+                PROF_ADD(0, t_h);
                 T_eval = pose;
-                double *sys = W.sys;  // H upper (21) | b (6) | chi2
-                if (lane < NT) sys[lane] = acc;
-                __builtin_amdgcn_wave_barrier();
+                const double *sys = S.sys;  // H upper (21) | b (6) | chi2
                 const double iniChi = sys[27];
                 double currentChi = iniChi;
                 if (iter == 0) {  // computeLambdaInit: tau * max |diag H|
@@ -432,6 +510,7 @@ __global__ __launch_bounds__(PW) void k_pose_opt(const PoseProbDev *__restrict__
                     reload_lds();
                     total_trials++;
                     W.backup = pose;  // push
+                    PROF_T(t_s);
                     double A[6][6], bvec[6];
                     {
                         int q = 0;
@@ -451,8 +530,13 @@ __global__ __launch_bounds__(PW) void k_pose_opt(const PoseProbDev *__restrict__
                     if (ok2)
 #pragma unroll
                         for (int i = 0; i < 6; i++) xs[i] = x[i];
+                    PROF_ADD(1, t_s);
+                    PROF_T(t_x);
                     se3_oplus(pose, xs);  // exp(update) * estimate
+                    PROF_ADD(2, t_x);
+                    PROF_T(t_c);
                     double tempChi = chi_pass(pose);
+                    PROF_ADD(3, t_c);
                     T_eval = pose;
                     if (!ok2) tempChi = DBL_MAX;
                     rho = (currentChi - tempChi);
@@ -487,27 +571,33 @@ __global__ __launch_bounds__(PW) void k_pose_opt(const PoseProbDev *__restrict__
         }
         // classification (ref:src/Optimizer.cc:314-403): active edges read their last computed
         // error (at T_eval), inactive ones computeError() at the final pose
+        PROF_T(t_cl);
         int bad = 0;
-        for (int e = lane; e < n; e += PW) {
+        for (int s = 0; s < nsc; s++) {
             reload_lds();
+            const int e = edge_of(s);
+            if (e >= n) continue;
             const PEdge E = load_edge(e, kind, xw, obs, isig2);
-            const bool was_out = outl[e] != 0;
+            const bool was_out = (om >> s) & 1;
             double ev[3];
             pose_edge_error(E, cam, cam2, Trl, was_out ? pose : T_eval, ev);
             const bool st = E.k == OSG_EDGE_STEREO;
             const float chi2 = (float)edge_chi2_of(ev, st, E.w);
             const float th = st ? 7.815f : 5.991f;
             const bool b = chi2 > th;
-            outl[e] = b ? 1 : 0;
+            om = (om & ~(uint64_t(1) << s)) | (uint64_t(b ? 1 : 0) << s);
             bad += b ? 1 : 0;
         }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) bad += __shfl_xor(bad, off);
-        nBad = bad;
+        nBad = frame_count(bad, S.n_bad);
+        PROF_ADD(4, t_cl);
         if (it == 2) robust = 0;
         if (n < 10) break;
+        __syncthreads();  // S.n_act / S.n_bad are rewritten next round
     }
-    if (lane == 0) {
+    for (int s = 0; s < nsc; s++)
+        if (edge_of(s) < n) outl[edge_of(s)] = (om >> s) & 1;
+    PROF_ADD(5, t_start);
+    if (threadIdx.x == 0) {
         se3_to7(pose, out[blockIdx.x].pose);
         out[blockIdx.x].n_inliers = n - nBad;
         out[blockIdx.x].lm_iterations = total_iters;
@@ -538,6 +628,21 @@ int osg_pose_optimization_batch(osg_ctx *ctx, const osg_pose_problem *p, int32_t
         total += (size_t)p[b].n_edges;
     }
     OSG_REQUIRE(ctx, total < (size_t(1) << 31), "too many edges in one batch");
+    // waves per frame: enough to spread a lone frame's chunks (latency), one when the batch fills
+    // the chip's ~2048 wave slots (throughput); at least enough for the 64-bit outlier masks
+    int nmax = 0;
+    for (int b = 0; b < nb; b++) nmax = std::max(nmax, p[b].n_edges);
+    const int chunks = (nmax + PW - 1) / PW;
+    int nw = 1;
+    if (const char *f = getenv("OSG_POSE_NW")) nw = atoi(f);  // tests pin the variant
+    else {
+        // waves per frame: up to one per 1.5 chunks of a lone frame's edges (latency; 8 waves share
+        // 4 SIMDs and measured no faster than 4), one when the batch fills the chip's wave slots
+        while (nw < 4 && 3 * nw <= 2 * chunks && (size_t)nb * 2 * nw <= 2048) nw *= 2;
+        while (nw < 8 && chunks > 64 * nw) nw *= 2;
+    }
+    OSG_REQUIRE(ctx, nw == 1 || nw == 2 || nw == 4 || nw == 8, "OSG_POSE_NW must be 1, 2, 4 or 8");
+    OSG_REQUIRE(ctx, chunks <= 64 * nw, "more than 32768 edges in one frame");
     // pack: probs | kind | xw | obs | isig2
     osg_packer pk;
     const size_t o_probs = pk.add(hp.data(), sizeof(PoseProbDev) * nb);
@@ -568,9 +673,21 @@ int osg_pose_optimization_batch(osg_ctx *ctx, const osg_pose_problem *p, int32_t
     hipEvent_t *ev = osg_ctx_events(ctx);
     if (!ev) return osg_set_error(ctx, OSG_E_HIP, "event create failed");
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[0], ctx->stream));
-    hipLaunchKernelGGL(k_pose_opt, dim3(nb), dim3(PW), 0, ctx->stream, (const PoseProbDev *)din,
-                       (const int8_t *)(din + o_kind), (const double *)(din + o_xw), (const double *)(din + o_obs),
-                       (const float *)(din + o_isig), (uint8_t *)(dio + o_outl), (PoseOut *)(dio + o_res));
+    const PoseProbDev *a0 = (const PoseProbDev *)din;
+    const int8_t *a1 = (const int8_t *)(din + o_kind);
+    const double *a2 = (const double *)(din + o_xw), *a3 = (const double *)(din + o_obs);
+    const float *a4 = (const float *)(din + o_isig);
+    uint8_t *a5 = (uint8_t *)(dio + o_outl);
+    PoseOut *a6 = (PoseOut *)(dio + o_res);
+#define OSG_POSE_LAUNCH(W_) \
+    hipLaunchKernelGGL(k_pose_opt<W_>, dim3(nb), dim3(W_ * PW), 0, ctx->stream, a0, a1, a2, a3, a4, a5, a6)
+    switch (nw) {
+    case 1: OSG_POSE_LAUNCH(1); break;
+    case 2: OSG_POSE_LAUNCH(2); break;
+    case 4: OSG_POSE_LAUNCH(4); break;
+    default: OSG_POSE_LAUNCH(8); break;
+    }
+#undef OSG_POSE_LAUNCH
     OSG_HIP_CHECK(ctx, hipGetLastError());
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
     char *pout = pin + in_bytes;
@@ -591,6 +708,18 @@ int osg_pose_optimization_batch(osg_ctx *ctx, const osg_pose_problem *p, int32_t
     }
     return sum;
 }
+
+#ifdef OSG_POSE_PROF
+int osg_debug_pose_prof(unsigned long long *dst, int reset)
+{
+    if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_pose_prof), sizeof(g_pose_prof)) != hipSuccess) return -1;
+    if (reset) {
+        static unsigned long long z[64][8];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_pose_prof), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 
 int osg_pose_optimization(osg_ctx *ctx, const osg_pose_problem *p, osg_pose_result *r)
 {
