@@ -8,9 +8,9 @@
 namespace ORB_SLAM3 {
 
 int Optimizer::PoseOptimization(Frame *pFrame)
-{  // ref:src/Optimizer.cc:71-420; the graph is gathered under MapPoint::mGlobalMutex like the reference
-    std::unique_lock<std::mutex> lock(MapPoint::mGlobalMutex);
-    return osg_orbslam3::pose_optimization<OsgHooks>(pFrame);
+{  // ref:src/Optimizer.cc:71-420; MapPoint::mGlobalMutex is held only while the edges are gathered
+   // (:128-286), released before the GPU solve and the write-back
+    return osg_orbslam3::pose_optimization<OsgHooks>(pFrame, &MapPoint::mGlobalMutex);
 }
 
 // The local window (ref:src/Optimizer.cc:1762-1873) is the reference's code unchanged; it ends with

@@ -32,6 +32,7 @@
 #include <list>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <set>
 #include <stdexcept>
 #include <string>
@@ -852,8 +853,17 @@ void compute_distinctive_descriptors(const std::vector<MapPointT *> &vpMPs)
 // ------------------------------------------------------------------- a10 PoseOptimization
 // ref:src/Optimizer.cc:71-420: one edge per Frame slot holding a MapPoint, in slot order; the
 // result sets mvbOutlier and the pose and returns nInitialCorrespondences - nBad.
-template <class H, class FrameT>
-int pose_optimization(FrameT *pFrame)
+// Locking as the reference: `gather_mutex` (MapPoint::mGlobalMutex in the ORB-SLAM3 tree) is held
+// only while the edges are built from the MapPoints (ref:src/Optimizer.cc:128-286); the GPU solve
+// and the write-back into the Frame run without it, so LocalMapping / LoopClosing's SetWorldPos
+// are not blocked for the device round trip.
+struct NoMutex {
+    void lock() {}
+    void unlock() {}
+};
+
+template <class H, class FrameT, class MutexT = NoMutex>
+int pose_optimization(FrameT *pFrame, MutexT *gather_mutex = nullptr)
 {
     osg_ctx *ctx = thread_ctx();
     const int N = pFrame->N;
@@ -862,6 +872,8 @@ int pose_optimization(FrameT *pFrame)
     std::vector<float> isig;
     std::vector<int> slot;
     const bool two = (bool)pFrame->mpCamera2;
+    std::unique_lock<MutexT> gather_lock;
+    if (gather_mutex) gather_lock = std::unique_lock<MutexT>(*gather_mutex);
     for (int i = 0; i < N; i++) {
         auto *pMP = pFrame->mvpMapPoints[i];
         if (!pMP) continue;
@@ -897,6 +909,7 @@ int pose_optimization(FrameT *pFrame)
         isig.push_back(pFrame->mvInvLevelSigma2[oct]);
         slot.push_back(i);
     }
+    if (gather_lock.owns_lock()) gather_lock.unlock();  // ref:src/Optimizer.cc:286, end of Step 3
     osg_pose_problem p{};
     H::pose(*pFrame, p.pose);
     p.n_edges = (int32_t)kind.size();
@@ -967,7 +980,11 @@ LbaOutcome<KeyFrameT, MapPointT> local_bundle_adjustment(const std::list<KeyFram
         if (kfs[i].second->mpCamera2) H::camera(*kfs[i].second, true, cams[2 * i + 1]);
     }
     out.num_OptKF = (int)lLocalKeyFrames.size();
-    out.num_fixedKF = (int)lFixedCameras.size();
+    // ref:src/Optimizer.cc:1781-1790,1828: the fixed cameras plus the map's init KeyFrame when it is
+    // one of the local KeyFrames (its vertex is fixed too, :1909)
+    bool init_local = false;
+    for (auto *k : lLocalKeyFrames) init_local |= (k->mnId == initKFid);
+    out.num_fixedKF = (int)lFixedCameras.size() + (init_local ? 1 : 0);
     std::vector<std::pair<unsigned long, MapPointT *>> mps;
     for (auto *p : lLocalMapPoints) mps.push_back({p->mnId, p});
     std::sort(mps.begin(), mps.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
@@ -1045,9 +1062,12 @@ LbaOutcome<KeyFrameT, MapPointT> local_bundle_adjustment(const std::list<KeyFram
     check(ctx, osg_local_bundle_adjustment(ctx, &g, &r, reinterpret_cast<const volatile uint8_t *>(pbStopFlag)),
           "osg_local_bundle_adjustment");
     out.aborted = r.aborted != 0;
-    // ref:src/Optimizer.cc:2125-2168: edges over the chi2 threshold or behind the camera
-    for (size_t e = 0; e < bad.size(); e++)
-        if (bad[e]) out.to_erase.push_back(e_pair[e]);
+    // ref:src/Optimizer.cc:2123-2168: edges over the chi2 threshold or behind the camera, collected
+    // in the reference's vToErase order (mono edges, then right-camera edges, then stereo edges),
+    // skipping MapPoints another thread marked bad while the solve ran (:2130, :2145, :2160)
+    for (int k : {OSG_EDGE_MONO, OSG_EDGE_BODY, OSG_EDGE_STEREO})
+        for (size_t e = 0; e < bad.size(); e++)
+            if (e_kind[e] == k && bad[e] && !e_pair[e].second->isBad()) out.to_erase.push_back(e_pair[e]);
     // only the local KeyFrames are written back (fixed cameras are not), ref:src/Optimizer.cc:2187-2203
     for (auto *k : lLocalKeyFrames) {
         const int i = kf_index[k];
@@ -1208,14 +1228,18 @@ GbaOutcome<KeyFrameT, MapPointT> bundle_adjustment(const std::vector<KeyFrameT *
 // Writes a GbaOutcome as ref:src/Optimizer.cc:3122-3236 does: straight into the map after the
 // monocular initialisation (nLoopKF == the map's origin KeyFrame id), otherwise into mTcwGBA /
 // mPosGBA with mnBAGlobalForKF = nLoopKF for LoopClosing to apply.
+// KeyFrames and MapPoints another thread marked bad during the solve are skipped, as the reference's
+// write-back loops re-check isBad() (:3127, :3219).
 template <class H, class KeyFrameT, class MapPointT>
 void apply_bundle_adjustment(const GbaOutcome<KeyFrameT, MapPointT> &o, unsigned long nLoopKF, bool into_map)
 {
     for (const auto &kp : o.poses) {
+        if (kp.first->isBad()) continue;
         if (into_map) H::set_pose(*kp.first, kp.second.data());
         else H::set_gba_pose(*kp.first, kp.second.data(), nLoopKF);
     }
     for (const auto &mp : o.points) {
+        if (mp.first->isBad()) continue;
         if (into_map) H::set_world_pos(mp.first, mp.second.data());
         else H::set_gba_pos(mp.first, mp.second.data(), nLoopKF);
     }

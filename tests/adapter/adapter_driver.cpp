@@ -492,7 +492,14 @@ int main(int argc, char **argv)
             F.cx = cam[11];
             F.cy = cam[12];
             F.mbf = cam[13];
-            const int inl = osg_orbslam3::pose_optimization<MockHooks>(&F);
+            ProbeMutex probe;  // params[0] != 0: pass a MapPoint::mGlobalMutex stand-in and report its use
+            const bool use_probe = prm && prm[0] != 0;
+            if (use_probe) g_probe = &probe;
+            const int inl = use_probe ? osg_orbslam3::pose_optimization<MockHooks>(&F, &probe)
+                                      : osg_orbslam3::pose_optimization<MockHooks>(&F);
+            g_probe = nullptr;
+            out["lock_stats"] = make('i', std::vector<int32_t>{probe.locks, g_gather_unlocked, g_apply_locked,
+                                                               g_apply_try_lock_failed, (int32_t)probe.held});
             std::vector<uint8_t> outl(n);
             for (int i = 0; i < n; i++) outl[i] = F.mvbOutlier[i];
             out["n_inliers"] = make('i', std::vector<int32_t>{inl});
@@ -511,14 +518,25 @@ int main(int argc, char **argv)
             std::list<MapPoint *> mps;
             for (auto &p : mp) mps.push_back(&p);
             bool stop = false;
-            auto o = osg_orbslam3::local_bundle_adjustment<MockHooks>(local, fixedc, mps, &map, ~0ul, &stop, false);
+            // optional: params[0] = the map's init KeyFrame id (default none); "G.mp_bad" = MapPoints
+            // another thread marks bad while the solve runs (in the graph, skipped at classification)
+            const unsigned long init_id = prm ? (unsigned long)prm[0] : ~0ul;
+            if (has(in, "G.mp_bad"))
+                for (int j = 0; j < npt; j++) mp[j].bad = get(in, "G.mp_bad").p<uint8_t>()[j] != 0;
+            auto o = osg_orbslam3::local_bundle_adjustment<MockHooks>(local, fixedc, mps, &map, init_id, &stop, false);
             std::vector<uint8_t> bad(ne, 0);
+            std::vector<int32_t> erased;
             {
                 std::map<std::pair<KeyFrame *, MapPoint *>, int> edge_of;
                 for (int e = 0; e < ne; e++)
                     edge_of[{&kf[get(in, "G.e_pose").p<int32_t>()[e]], &mp[get(in, "G.e_point").p<int32_t>()[e]]}] = e;
-                for (auto &km : o.to_erase) bad[edge_of[km]] = 1;
+                for (auto &km : o.to_erase) {
+                    bad[edge_of[km]] = 1;
+                    erased.push_back(edge_of[km]);
+                }
             }
+            out["erased"] = make('i', erased);
+            out["counts"] = make('i', std::vector<int32_t>{o.num_fixedKF, o.num_OptKF, o.num_MPs, o.num_edges});
             osg_orbslam3::apply_local_bundle_adjustment<MockHooks>(o);
             std::vector<double> pose(7 * (size_t)np), point(3 * (size_t)npt);
             for (int i = 0; i < np; i++) std::memcpy(&pose[7 * i], kf[i].pose, 56);

@@ -5,10 +5,13 @@
 #ifndef MOCK_ORBSLAM3_H
 #define MOCK_ORBSLAM3_H
 
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <set>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -181,14 +184,50 @@ inline void MapPoint::Replace(MapPoint *p)
     p->desc.buf[0] ^= 0x5A;
 }
 
+// test-only: a MapPoint::mGlobalMutex stand-in that records when it is held, and what the hooks saw
+// (world_pos runs during the gather, set_pose during the write-back after the GPU solve)
+struct ProbeMutex {
+    std::mutex m;
+    std::atomic<bool> held{false};
+    int locks = 0;
+    void lock()
+    {
+        m.lock();
+        held = true;
+        locks++;
+    }
+    void unlock()
+    {
+        held = false;
+        m.unlock();
+    }
+};
+inline ProbeMutex *g_probe = nullptr;
+inline int g_gather_unlocked = 0, g_apply_locked = 0, g_apply_try_lock_failed = 0;
+
 struct Sim3 {};  // Fuse(KeyFrame*, Sim3f&, ...): the projection is MockHooks' (test-only)
 
 struct MockHooks {
     template <class T>
     static void pose(const T &o, double q[7]) { std::memcpy(q, o.pose, sizeof o.pose); }
     template <class T>
-    static void set_pose(T &o, const double q[7]) { std::memcpy(o.pose, q, sizeof o.pose); }
-    static void world_pos(MapPoint *p, double x[3]) { std::memcpy(x, p->pos, sizeof p->pos); }
+    static void set_pose(T &o, const double q[7])
+    {
+        if (g_probe) {  // another thread must be able to take the mutex while the result is applied
+            g_apply_locked += g_probe->held ? 1 : 0;
+            std::thread t([] {
+                if (g_probe->m.try_lock()) g_probe->m.unlock();
+                else g_apply_try_lock_failed++;
+            });
+            t.join();
+        }
+        std::memcpy(o.pose, q, sizeof o.pose);
+    }
+    static void world_pos(MapPoint *p, double x[3])
+    {
+        if (g_probe && !g_probe->held) g_gather_unlocked++;
+        std::memcpy(x, p->pos, sizeof p->pos);
+    }
     static void set_world_pos(MapPoint *p, const double x[3]) { std::memcpy(p->pos, x, sizeof p->pos); }
     static void set_gba_pose(KeyFrame &k, const double q[7], unsigned long n)
     {
