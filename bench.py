@@ -68,8 +68,29 @@ def parse():
     return ap.parse_args()
 
 
+def _spawn_ranks(n):
+    """`bench.py --gpus N` outside a launcher: start the N ranks (one process per GPU, torchrun on
+    127.0.0.1) as a child before this process touches a GPU, and return its exit code."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(_spawn_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}; launch one rank per GPU "
+              f"(torchrun --nproc-per-node {args.gpus}) or drop the launcher", file=sys.stderr)
+        sys.exit(2)
     import torch
     import torch.distributed as dist
 
@@ -202,12 +223,16 @@ def main():
             "algorithmic_bytes_per_launch": sbytes,
             "Mmatches_per_s": round(Q * M / (s_us * 1e-6) / 1e6, 1),
         }
+        if world > 1:
+            out["stream_train_sharded"] = bench_stream_sharded(ctx, dist, dev, stream, sq, st, world, rank)
         del st
 
     # ---- CPU baseline: the oracle (restatement of the reference serial loop) on host cores --
     if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(q_np, t_np, args.cpu_seconds)
-        out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
+        out["cpu_baseline"] = cb = cpu_baseline(q_np, t_np, args.cpu_seconds)
+        out["speedup_vs_cpu"] = round(value / cb["value"], 1)
+        out["speedup_vs_cpu_1thread"] = round(value / cb["value_1thread"], 1)
+        out["speedup_vs_cpu_node_estimate"] = round(value / cb["node_estimate"]["value"], 2)
 
     # ---- frame-batched C3 / C5: matching + PoseOptimization, B frames per launch ------------
     if not args.no_frames:
@@ -228,6 +253,45 @@ def main():
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_stream_sharded(ctx, dist, dev, stream, sq, st, world, rank, steps=20):
+    """SURVEY.md §8(e) C2' train-sharded: the train set is world x 2^24 rows, rank r holding rows
+    [r*M, (r+1)*M) in its HBM and the Q queries replicated; one step = the local streaming kernel, an
+    all-gather of the (Q, 3) int32 triples over RCCL and the on-device merge into the serial loop's
+    top-2 (shard.merge_top2_torch).  Weak scaling: pairs per step = Q x M x world."""
+    import torch
+    from orb_slam3_comments_ghr_amd import shard
+    Q, M = sq.shape[0], st.shape[0]
+    so = torch.empty((Q, 3), dtype=torch.int32, device=dev)
+    parts = [torch.empty_like(so) for _ in range(world)]
+    row0 = rank * M
+
+    def step():
+        ctx.hamming_top2_dev(sq, Q, st, M, so)
+        so[:, 0] = torch.where(so[:, 0] >= 0, so[:, 0] + row0, so[:, 0])
+        dist.all_gather(parts, so)
+        return shard.merge_top2_torch(torch.stack(parts))
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        merged = step()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    el, pairs = job_totals(el, Q * M * steps, world, dist, dev)
+    # every rank holds the same merged result: check it agrees across ranks (cheap, outside timing)
+    chk = merged.to(torch.int64).sum().reshape(1)
+    lo, hi = chk.clone(), chk.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    return {"workload": f"C2' train-sharded: {world} x 2^24 train rows (rank-local), Q={Q} replicated; "
+                        f"local kernel + RCCL all-gather of (Q,3) int32 + device merge per step",
+            "value": round(pairs / el / 1e6, 1), "unit": "Mmatches/s", "ms_per_step": round(el / steps * 1e3, 4),
+            "n_gpus": world, "scaling": "weak", "merged_equal_on_all_ranks": bool(lo.item() == hi.item())}
 
 
 def pmc_traffic(path, kernel_substr):
@@ -304,20 +368,28 @@ def bench_lba(ctx, rank, world, dist, dev, args):
         "single_window": single,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        lib, oc = _oracle()
-        t0 = time.perf_counter()
-        n = 0
-        ci = 0
-        while time.perf_counter() - t0 < args.cpu_seconds / 2 or n == 0:
-            rr = oc.lba(lib, G)
-            ci += rr.iterations
-            n += 1
-        cel = time.perf_counter() - t0
-        res["cpu_baseline"] = {"value": round(ci / cel, 2), "unit": "LM iterations/s", "cores": 1, "kind": "port",
-                               "sample": f"{n} x C4 LBA (oracle_local_bundle_adjustment, gcc -O3, 1 thread, dense LDL^T) in {cel:.1f} s"}
-        res["speedup_vs_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
-        single["speedup_vs_cpu"] = round(single["value"] / res["cpu_baseline"]["value"], 1)
+        # LM iterations per window on the CPU, averaged over the pool the workers cycle through
+        it_cpu = float(np.mean([_oracle()[1].lba(_oracle()[0], g).iterations for g in pool]))
+        _attach_cpu(res, _lba_worker(pool), it_cpu, "LM iterations/s", args.cpu_seconds * 0.75,
+                    "C4 LBA (oracle_local_bundle_adjustment, dense LDL^T)", wall_key="")
+        single["speedup_vs_cpu_1thread"] = round(single["value"] / res["cpu_baseline"]["value_1thread"], 1)
     return res
+
+
+def _lba_worker(graphs):
+    """cpu_baseline worker for BA: one graph per call, round-robin over `graphs`; outputs per thread."""
+    def worker(tid):
+        import ctypes as C
+        from orb_slam3_comments_ghr_amd import optimizer as op
+        lib, _ = _oracle()
+        items = []
+        for g in graphs:
+            R, out = op.make_ba_result(g)
+            gs = g.struct()
+            items.append(((C.byref(gs), C.byref(R), None), (R, out, gs)))
+        fn = lib.oracle_local_bundle_adjustment
+        return lambda i, items=items: fn(*items[i % len(items)][0])
+    return worker
 
 
 def bench_gba(ctx, rank, world, dist, dev, args):
@@ -350,14 +422,9 @@ def bench_gba(ctx, rank, world, dist, dev, args):
                        f"reduced system {6 * n_free} (dense), optimize({G.iterations}), no Huber",
            "n_gpus": world, "dtype": "f64", "scaling": "weak", "parallelism": f"replicas x{world} (one map per GPU)"}
     if rank == 0 and world == 1 and not args.no_cpu:
-        lib, oc = _oracle()
-        t0 = time.perf_counter()
-        rr = oc.lba(lib, G)
-        cel = time.perf_counter() - t0
-        res["cpu_baseline"] = {"value": round(rr.iterations / cel, 2), "unit": "LM iterations/s", "cores": 1,
-                               "kind": "port", "sample": f"1 global BA (oracle, gcc -O3, 1 thread, dense LDL^T) "
-                                                         f"in {cel:.1f} s"}
-        res["speedup_vs_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
+        it_cpu = _oracle()[1].lba(_oracle()[0], G).iterations
+        _attach_cpu(res, _lba_worker([G]), it_cpu, "LM iterations/s", max(3.0, args.cpu_seconds * 0.5),
+                    "global BA 150 KF x 20k points (oracle, dense LDL^T)", wall_key="")
     return res
 
 
@@ -372,12 +439,46 @@ def _oracle():
     return _ORACLE[0]
 
 
-def _frame_batches(ctx, rank, world, dist, dev, args, steps, cpu_step, label, workload, n_pool, cpu_frames=1):
+def _pose_result(P):
+    """An osg_pose_result with its outlier buffer (kept alive by the returned tuple)."""
+    from orb_slam3_comments_ghr_amd import _abi
+    r = _abi.OsgPoseResult()
+    o = np.zeros(max(P.n, 1), np.uint8)
+    r.outlier = o.ctypes.data
+    return r, o
+
+
+def _latency(gpu_call, cpu_call=None, reps=200):
+    """Single-call latency of one drop-in call, the way Tracking issues them (one frame at a time,
+    ref:src/Tracking.cc:3507): the C-ABI entry with host inputs and outputs (upload, kernels,
+    download, stream sync), arguments packed beforehand as the C++ adapter packs them.  Median and
+    p90 over `reps` calls; beside it the oracle's 1-thread time for the same call."""
+    def timeit(call, n):
+        for _ in range(5):
+            call()
+        ts = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            call()
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        return ts[len(ts) // 2] * 1e6, ts[int(len(ts) * 0.9)] * 1e6
+    g50, g90 = timeit(gpu_call, reps)
+    out = {"gpu_us_median": round(g50, 1), "gpu_us_p90": round(g90, 1)}
+    if cpu_call is not None:
+        c50, _ = timeit(cpu_call, max(10, reps // 10))
+        out["cpu_1thread_us_median"] = round(c50, 1)
+        out["speedup_vs_cpu_1thread"] = round(c50 / g50, 2)
+    return out
+
+
+def _frame_batches(ctx, rank, world, dist, dev, args, steps, cpu_worker, label, workload, n_pool, cpu_frames=1,
+                   latency=None):
     """Time `steps` (a list of callables, each one batched launch over B frames that leaves its
     kernel time in ctx.last_kernel_ms()) over args.frame_reps repetitions.  value = frames / summed
     kernel time (inputs resident in HBM: the device time of the launches); the wall rate includes
-    host packing and PCIe.  cpu_step(i) runs frame i of the pool (or cpu_frames frames from i)
-    through the oracle."""
+    host packing and PCIe.  cpu_worker(tid) -> call(i) runs frame i of the pool (or cpu_frames frames)
+    through the oracle with its arguments packed once per thread (tests/cpu_mt.py)."""
     import torch
     for f in steps:
         f()
@@ -402,17 +503,25 @@ def _frame_batches(ctx, rank, world, dist, dev, args, steps, cpu_step, label, wo
            "kernel_us_per_frame": {lab: round(v * 1e3 / frames, 3) for lab, v in zip(label, per)},
            "wall_frames_per_s_incl_host_and_pcie": round(tot / w_s, 1), "n_gpus": world,
            "scaling": "weak", "parallelism": f"replicas x{world} (independent frame batches per GPU)"}
+    if latency:
+        res["single_call_latency"] = latency
     if rank == 0 and world == 1 and not args.no_cpu:
-        n = 0
-        t0 = time.perf_counter()
-        while time.perf_counter() - t0 < args.cpu_seconds / 4 or n == 0:
-            cpu_step(n % n_pool)
-            n += cpu_frames
-        cel = time.perf_counter() - t0
-        res["cpu_baseline"] = {"value": round(n / cel, 1), "unit": "frames/s", "cores": 1, "kind": "port",
-                               "sample": f"{n} frames through the oracle (gcc -O3, 1 thread) in {cel:.1f} s"}
-        res["speedup_vs_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
+        _attach_cpu(res, cpu_worker, cpu_frames, "frames/s", args.cpu_seconds * 0.4, label[0] if len(label) == 1
+                    else " + ".join(label))
     return res
+
+
+def _attach_cpu(res, worker, units, unit, seconds, label, wall_key="wall_frames_per_s_incl_host_and_pcie"):
+    """res["cpu_baseline"] (N threads, one problem per thread) and the speedups: kernel-time value and,
+    when recorded, the host- and PCIe-inclusive wall rate, each against the N-thread and 1-thread CPU."""
+    from tests import cpu_mt
+    cb = cpu_mt.baseline(worker, units, unit, seconds, label)
+    res["cpu_baseline"] = cb
+    res["speedup_vs_cpu"] = round(res["value"] / cb["value"], 2)
+    res["speedup_vs_cpu_1thread"] = round(res["value"] / cb["value_1thread"], 1)
+    res["speedup_vs_cpu_node_estimate"] = round(res["value"] / cb["node_estimate"]["value"], 2)
+    if wall_key in res:
+        res["wall_speedup_vs_cpu"] = round(res[wall_key] / cb["value"], 2)
 
 
 def bench_c3(ctx, rank, world, dist, dev, args):
@@ -432,16 +541,28 @@ def bench_c3(ctx, rank, world, dist, dev, args):
     PB = [probs[i % n_pool] for i in range(B)]
     opt = op.Optimizer(ctx)
 
-    def cpu(i):  # the cpu_baseline leg: the oracle restatement, 1 thread
-        oracle, oc = _oracle()
-        oc.bow_kf_f(oracle, pairs[i][0], pairs[i][1], 0.7, True)
-        oc.pose(oracle, [probs[i]])
+    cpu = _c3_worker(pairs, probs)
+    lat = None
+    if rank == 0:
+        import ctypes as C
+        lib, h = ctx.lib, ctx.handle
+        a, b = pairs[0][0].struct(), pairs[0][1].struct()
+        o = np.full(pairs[0][1].n, -1, np.int32)
+        ps, (rs, keep) = probs[0].struct(), _pose_result(probs[0])
+        lat = {"SearchByBoW(KF,F)": _latency(
+                   lambda: lib.osg_search_by_bow_kf_f(h, C.byref(a), C.byref(b), 0.7, 1, o.ctypes.data),
+                   None if args.no_cpu else lambda: _oracle()[0].oracle_search_by_bow_kf_f(
+                       C.byref(a), C.byref(b), 0.7, 1, o.ctypes.data)),
+               f"PoseOptimization ({probs[0].n} edges)": _latency(
+                   lambda: lib.osg_pose_optimization(h, C.byref(ps), C.byref(rs)),
+                   None if args.no_cpu else lambda: _oracle()[0].oracle_pose_optimization(C.byref(ps), C.byref(rs)))}
 
     return _frame_batches(ctx, rank, world, dist, dev, args,
                           [lambda: m.SearchByBoWBatch(KB, FB), lambda: opt.PoseOptimization(PB)], cpu,
                           ["SearchByBoW", "PoseOptimization"],
                           f"C3: SearchByBoW(KF,F) 1200x1200 (100 nodes) + PoseOptimization "
-                          f"(mean {int(np.mean(nm))} edges, 60 % stereo), {B} frames per launch", n_pool)
+                          f"(mean {int(np.mean(nm))} edges, 60 % stereo), {B} frames per launch", n_pool,
+                          latency=lat)
 
 
 def bench_c5(ctx, rank, world, dist, dev, args):
@@ -466,11 +587,30 @@ def bench_c5(ctx, rank, world, dist, dev, args):
     m_local = ORBmatcher(ctx, 0.9, True)
     opt = op.Optimizer(ctx)
 
-    def cpu(i):  # the cpu_baseline leg: the oracle restatement, 1 thread
-        oracle, oc = _oracle()
-        oc.last(oracle, F[i], L[i], 7.0, False, True, S[i][0], S[i][1])
-        oc.mps(oracle, F[i], Q[i], 0.9, 3.0, False, 20.0, S[i][0], S[i][1])
-        oc.pose(oracle, [probs[i]])
+    cpu = _c5_worker(F, L, Q, S, probs)
+    lat = None
+    if rank == 0:
+        import ctypes as C
+        lib, h = ctx.lib, ctx.handle
+        fs, ls, qs = F[0].struct(), L[0].struct(), Q[0].struct()
+        sl, tk = S[0][0].copy(), np.ascontiguousarray(S[0][1], np.uint8)
+        ps, (rs, keep) = probs[0].struct(), _pose_result(probs[0])
+        orc = None if args.no_cpu else _oracle()[0]
+
+        def last(fn, *pre):
+            return lambda: (np.copyto(sl, S[0][0]), fn(*pre, C.byref(fs), C.byref(ls), 7.0, 0, 1, sl.ctypes.data,
+                                                         tk.ctypes.data))
+
+        def mps(fn, *pre):
+            return lambda: (np.copyto(sl, S[0][0]), fn(*pre, C.byref(fs), C.byref(qs), 0.9, 3.0, 0, 20.0,
+                                                         sl.ctypes.data, tk.ctypes.data))
+        lat = {"SearchByProjection(F,LastF)": _latency(last(lib.osg_search_by_projection_last, h),
+                                                       orc and last(orc.oracle_search_by_projection_last)),
+               "SearchByProjection(F,localMPs)": _latency(mps(lib.osg_search_by_projection_mps, h),
+                                                          orc and mps(orc.oracle_search_by_projection_mps)),
+               f"PoseOptimization KB8 ({probs[0].n} edges)": _latency(
+                   lambda: lib.osg_pose_optimization(h, C.byref(ps), C.byref(rs)),
+                   orc and (lambda: orc.oracle_pose_optimization(C.byref(ps), C.byref(rs))))}
 
     return _frame_batches(ctx, rank, world, dist, dev, args,
                           [lambda: m.SearchByProjectionBatch(FB, LB, 7.0, False, slot_mps=[S[i][0].copy() for i in idx],
@@ -481,7 +621,8 @@ def bench_c5(ctx, rank, world, dist, dev, args):
                            lambda: opt.PoseOptimization(PB)], cpu,
                           ["SearchByProjection(F,LastF)", "SearchByProjection(F,localMPs)", "PoseOptimization"],
                           f"C5: two-camera KB8 512x512, 2x1000 keypoints; LastF 2000 + local map 1500 queries; "
-                          f"PoseOptimization 600 edges (40 % right camera); {B} frames per launch", n_pool)
+                          f"PoseOptimization 600 edges (40 % right camera); {B} frames per launch", n_pool,
+                          latency=lat)
 
 
 def bench_dbow(ctx, rank, world, dist, dev, args):
@@ -498,9 +639,7 @@ def bench_dbow(ctx, rank, world, dist, dev, args):
     B = args.frames
     sets = [pool[i % n_pool] for i in range(B)]
 
-    def cpu(i):  # the cpu_baseline leg: the oracle, children index built once per 16 frames
-        oracle, oc = _oracle()
-        oc.dbow_batch(oracle, voc, pool, 4)
+    cpu = _dbow_worker(voc, pool)
 
     res = _frame_batches(ctx, rank, world, dist, dev, args, [lambda: gv.transform_batch(sets, 4)], cpu,
                          ["transform"],
@@ -524,9 +663,7 @@ def bench_stereo(ctx, rank, world, dist, dev, args):
     B = args.frames
     frames = [dpool[i % n_pool] for i in range(B)]
 
-    def cpu(i):  # the cpu_baseline leg: the oracle restatement, 1 thread
-        oracle, oc = _oracle()
-        oc.stereo(oracle, pool[i])
+    cpu = _stereo_worker(pool)
 
     res = _frame_batches(ctx, rank, world, dist, dev, args, [lambda: st.ComputeStereoMatchesBatch(ctx, frames)], cpu,
                          ["ComputeStereoMatches"],
@@ -572,39 +709,156 @@ def bench_orb(ctx, rank, world, dist, dev, args):
            "wall_frames_per_s_incl_host_roundtrip": round(tot / w_s, 1), "n_gpus": world,
            "scaling": "weak", "parallelism": f"replicas x{world}"}
     if rank == 0 and world == 1 and not args.no_cpu:
-        oracle, oc = _oracle()
-        n = 0
-        t0 = time.perf_counter()
-        while time.perf_counter() - t0 < args.cpu_seconds / 4 or n == 0:
-            f = pool[n % n_pool]
-            oc.orb_describe(oracle, f[0], f[1], f[2], f[3], f[4], pat)
-            n += 1
-        cel = time.perf_counter() - t0
-        res["cpu_baseline"] = {"value": round(n / cel, 1), "unit": "frames/s", "cores": 1, "kind": "port",
-                               "sample": f"{n} frames through the oracle (gcc -O3, 1 thread) in {cel:.1f} s"}
-        res["speedup_vs_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
+        cpu = _orb_worker(pool, pat)
+        _attach_cpu(res, cpu, 1, "frames/s", args.cpu_seconds * 0.4, "IC_Angle + computeOrbDescriptor",
+                    wall_key="wall_frames_per_s_incl_host_roundtrip")
     return res
 
 
+def _c3_worker(pairs, probs):
+    """cpu_baseline worker for C3: SearchByBoW(KF,F) + PoseOptimization of one pool frame per call."""
+    n_pool = len(pairs)
+
+    def cpu(tid):  # the cpu_baseline leg: the oracle restatement, arguments packed per thread
+        import ctypes as C
+        from orb_slam3_comments_ghr_amd import _abi
+        oracle, _ = _oracle()
+        bow = [(p[0].struct(), p[1].struct()) for p in pairs]
+        outs = [np.full(p[1].n, -1, np.int32) for p in pairs]
+        pst = [p.struct() for p in probs]
+        res = (_abi.OsgPoseResult * n_pool)()
+        outl = [np.zeros(p.n, np.uint8) for p in probs]
+        for r, o in zip(res, outl):
+            r.outlier = o.ctypes.data
+        args_ = [(C.byref(a), C.byref(b), o.ctypes.data, C.byref(ps), C.byref(r))
+                 for (a, b), o, ps, r in zip(bow, outs, pst, res)]
+        keep = (bow, outs, pst, res, outl)
+        fb, fp = oracle.oracle_search_by_bow_kf_f, oracle.oracle_pose_optimization
+
+        def call(i, keep=keep):
+            a, b, o, ps, r = args_[i % n_pool]
+            fb(a, b, 0.7, 1, o)
+            fp(ps, r)
+        return call
+    return cpu
+
+
+def _c5_worker(F, L, Q, S, probs):
+    """cpu_baseline worker for C5: SearchByProjection(F,LastF) + (F,local map) + PoseOptimization."""
+    n_pool = len(F)
+
+    def cpu(tid):  # the cpu_baseline leg: the oracle restatement, arguments packed per thread
+        import ctypes as C
+        from orb_slam3_comments_ghr_amd import _abi
+        oracle, _ = _oracle()
+        fs = [f.struct() for f in F]
+        ls = [x.struct() for x in L]
+        qs = [x.struct() for x in Q]
+        slot = [S[i][0].copy() for i in range(n_pool)]
+        taken = [np.ascontiguousarray(S[i][1], np.uint8) for i in range(n_pool)]
+        pst = [p.struct() for p in probs]
+        res = (_abi.OsgPoseResult * n_pool)()
+        outl = [np.zeros(p.n, np.uint8) for p in probs]
+        for r, o in zip(res, outl):
+            r.outlier = o.ctypes.data
+        args_ = [(C.byref(fs[i]), C.byref(ls[i]), C.byref(qs[i]), slot[i], S[i][0], slot[i].ctypes.data,
+                  taken[i].ctypes.data, C.byref(pst[i]), C.byref(res[i])) for i in range(n_pool)]
+        keep = (fs, ls, qs, slot, taken, pst, res, outl)
+        fl, fm, fp = (oracle.oracle_search_by_projection_last, oracle.oracle_search_by_projection_mps,
+                      oracle.oracle_pose_optimization)
+
+        def call(i, keep=keep):
+            f, lq, mq, sl, s0, sp, tp, ps, r = args_[i % n_pool]
+            np.copyto(sl, s0)  # both searches start from the frame's slot state, as in the GPU batch
+            fl(f, lq, 7.0, 0, 1, sp, tp)
+            np.copyto(sl, s0)
+            fm(f, mq, 0.9, 3.0, 0, 20.0, sp, tp)
+            fp(ps, r)
+        return call
+    return cpu
+
+
+def _dbow_worker(voc, pool):
+    """cpu_baseline worker for DBoW2 transform: the whole pool (16 frames) per call."""
+    from orb_slam3_comments_ghr_amd import vocabulary as vb
+    n_pool = len(pool)
+
+    def cpu(tid):  # the cpu_baseline leg: the oracle, children index built once per 16 frames
+        import ctypes as C
+        from orb_slam3_comments_ghr_amd._abi import OsgBowOut
+        oracle, _ = _oracle()
+        sets_ = [np.ascontiguousarray(d, np.uint8).reshape(-1, 32) for d in pool]
+        outs = [vb.make_bow_out(d.shape[0]) for d in sets_]
+        arr = (OsgBowOut * n_pool)(*[o for o, _ in outs])
+        n = np.array([d.shape[0] for d in sets_], np.int32)
+        cat = np.concatenate(sets_)
+        vs = voc.struct()
+        a = (C.byref(vs), cat.ctypes.data, n.ctypes.data, n_pool, 4, C.addressof(arr))
+        keep = (sets_, outs, arr, n, cat, vs)
+        fn = oracle.oracle_dbow_transform_batch
+        return lambda i, keep=keep: fn(*a)
+    return cpu
+
+
+def _stereo_worker(pool):
+    """cpu_baseline worker for ComputeStereoMatches: one pool frame per call."""
+    n_pool = len(pool)
+
+    def cpu(tid):  # the cpu_baseline leg: the oracle restatement, arguments packed per thread
+        import ctypes as C
+        oracle, _ = _oracle()
+        ss = [f.struct() for f in pool]
+        outs = [(np.empty(f.n, np.float32), np.empty(f.n, np.float32)) for f in pool]
+        args_ = [(C.byref(s_), u.ctypes.data, d.ctypes.data) for s_, (u, d) in zip(ss, outs)]
+        keep = (ss, outs)
+        fn = oracle.oracle_compute_stereo_matches
+        return lambda i, keep=keep: fn(*args_[i % n_pool])
+    return cpu
+
+
+def _orb_worker(pool, pat):
+    """cpu_baseline worker for IC_Angle + computeOrbDescriptor: one pool frame per call."""
+    from orb_slam3_comments_ghr_amd import orb
+    n_pool = len(pool)
+
+    def cpu(tid):  # IC_Angle + computeOrbDescriptor through the oracle, arguments packed per thread
+        import ctypes as C
+        from orb_slam3_comments_ghr_amd._abi import OsgOrbKeypoints
+        from orb_slam3_comments_ghr_amd.stereo import ImagePyramid
+        oracle, _ = _oracle()
+        umax = orb.ic_umax()
+        patf = np.ascontiguousarray(pat, np.int32).reshape(-1)
+        items = []
+        for f in pool:
+            rp, bp = ImagePyramid(f[0]), ImagePyramid(f[1])
+            x, y = (np.ascontiguousarray(v, np.float32) for v in (f[2], f[3]))
+            lv = np.ascontiguousarray(f[4], np.int32)
+            K = OsgOrbKeypoints(len(x), x.ctypes.data, y.ctypes.data, lv.ctypes.data)
+            ang, desc = np.zeros(len(x), np.float32), np.zeros((len(x), 32), np.uint8)
+            rs, bs = rp.struct(), bp.struct()
+            items.append(((C.byref(rs), C.byref(bs), C.byref(K), patf.ctypes.data, umax.ctypes.data, 1,
+                           ang.ctypes.data, desc.ctypes.data), (rp, bp, x, y, lv, K, ang, desc, rs, bs)))
+        keep = (umax, patf, items)
+        fn = oracle.oracle_orb_describe
+        return lambda i, keep=keep: fn(*items[i % n_pool][0])
+    return cpu
+
+
 def cpu_baseline(q_np, t_np, seconds):
-    """oracle_hamming_top2 (the reference's serial DescriptorDistance + top-2 loop, restated in C,
-    -O3) on 1 host thread, repeated on the same 2000 x 2000 workload for ~`seconds`."""
+    """oracle_hamming_top2 (the reference's serial DescriptorDistance + top-2 loop, restated in C, -O3),
+    one whole 2000 x 2000 frame per host thread, on 1 thread and on every CPU this job may use."""
     lib, _ = _oracle()
+    from tests import cpu_mt
     nq, nt = q_np.shape[0], t_np.shape[0]
-    bi, bd, sd = (np.empty(nq, np.int32) for _ in range(3))
-    reps = 0
-    t0 = time.perf_counter()
-    while True:
-        lib.oracle_hamming_top2(q_np.ctypes.data, nq, t_np.ctypes.data, nt, bi.ctypes.data,
-                                bd.ctypes.data, sd.ctypes.data)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    v = reps * nq * nt / el / 1e6
-    return {"value": round(v, 2), "unit": "Mmatches/s", "cores": 1, "kind": "port",
-            "sample": f"{reps} x C2 {nq}x{nt} top-2 (oracle_hamming_top2, gcc -O3, 1 thread) in {el:.1f} s",
-            "host_cpus": os.cpu_count()}
+    qp, tp = q_np.ctypes.data, t_np.ctypes.data
+
+    def worker(tid):
+        out = [np.empty(nq, np.int32) for _ in range(3)]
+        ptrs = [o.ctypes.data for o in out]
+        fn = lib.oracle_hamming_top2
+        return lambda i, out=out: fn(qp, nq, tp, nt, *ptrs)
+
+    return cpu_mt.baseline(worker, nq * nt / 1e6, "Mmatches/s", seconds, f"C2 {nq}x{nt} top-2 (oracle_hamming_top2)")
 
 
 if __name__ == "__main__":
