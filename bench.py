@@ -27,7 +27,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PEAK_VALU_TOPS = 256 * 128 * 2.4e9 / 1e12  # 256 CU x 4 SIMD32 x 32 lanes x 2.4 GHz = 78.6 T lane-op/s
+# Non-packed 32-bit VALU: 256 CU x 4 SIMD x 16 lanes per cycle x 2.4 GHz = 39.3 T lane-op/s.  Measured
+# on the box (tools/micro/valu_rate.hip, profiles/r02_valu_rate.txt): v_xor_b32, v_bcnt_u32_b32,
+# v_med3_u32, v_add_u32 and v_add_f32 all sustain 38.0-38.5 T lane-op/s = one wave64 instruction per
+# 4 cycles per SIMD at full occupancy; the 157.3 TF FP32 "vector" figure needs packed v_pk_fma_f32
+# (2 FMAs per lane-instruction), which has no integer counterpart.
+PEAK_VALU_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12
 VALU_OPS_PER_PAIR = 19         # 8 v_xor + 8 v_bcnt(acc) + 1 v_lshl_or + v_med3 + v_min
 
 
@@ -52,6 +57,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--nq", type=int, default=2000)
     ap.add_argument("--nt", type=int, default=2000)
+    ap.add_argument("--c2-batch", type=int, default=256,
+                    help="C2 frames per launch of the headline step (1: the single-problem launch)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-stream", action="store_true")
@@ -116,14 +123,25 @@ def main():
             dist.barrier()
 
     # ---- C2: 2000 x 2000 brute-force top-2 on resident inputs -------------------------------
-    nq, nt = args.nq, args.nt
+    # Headline step: B independent 2000 x 2000 frames in one launch (osg_hamming_top2_batch_dev,
+    # frame-batched throughput); the single-problem launch (osg_hamming_top2_dev, the latency form)
+    # is measured beside it.  Frame 0 of the batch is the seeded C2 frame.
+    nq, nt, B = args.nq, args.nt, max(1, args.c2_batch)
     q_np, t_np = synth.descriptors_c2(nq, nt, seed=synth.SEED_C2 + rank)
+    frames = [(q_np, t_np)] + [synth.descriptors_c2(nq, nt, seed=synth.SEED_C2 + 7919 * (b + 1) + rank)
+                               for b in range(1, B)]
     dq = torch.from_numpy(q_np).to(dev)
     dt = torch.from_numpy(t_np).to(dev)
     dout = torch.empty((nq, 3), dtype=torch.int32, device=dev)
+    dqb = torch.from_numpy(np.concatenate([f[0] for f in frames])).to(dev)
+    dtb = torch.from_numpy(np.concatenate([f[1] for f in frames])).to(dev)
+    doutb = torch.empty((B * nq, 3), dtype=torch.int32, device=dev)
+
+    def step_single():
+        ctx.hamming_top2_dev(dq, nq, dt, nt, dout)
 
     def step():
-        ctx.hamming_top2_dev(dq, nq, dt, nt, dout)
+        ctx.hamming_top2_batch_dev(dqb, nq, dtb, nt, B, doutb)
 
     for _ in range(args.warmup):
         step()
@@ -137,34 +155,45 @@ def main():
     barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    pairs_per_step = nq * nt
+    pairs_per_step = B * nq * nt
     elapsed, total_pairs = job_totals(elapsed, pairs_per_step * args.steps, world, dist if world > 1 else None, dev)
     value = total_pairs / elapsed / 1e6
+    # frame 0 of the batch equals the single-problem launch (both are the serial loop's result)
+    step_single()
+    torch.cuda.synchronize(dev)
+    batch_frame0_equal = bool(torch.equal(doutb[:nq], dout))
 
     # ---- dominant kernel roofline: HIP events on the launch stream -------------------------
     # The kernel's average duration = (end - start) / n over n back-to-back launches between two
     # events on its stream.  A stream pre-filled with a spin kernel keeps host launch gaps out.
     # (Per-launch brackets carry a fixed ~5 us event cost on this stack even around nothing, and
     # read high against rocprofv3; the back-to-back average agrees with it.)
-    n_ev = max(50, min(args.steps, 500))
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda._sleep(int(2e6 + n_ev * 2e4))
-    e0.record(stream)
-    for _ in range(n_ev):
-        step()
-    e1.record(stream)
-    torch.cuda.synchronize(dev)
-    k_us = e0.elapsed_time(e1) * 1e3 / n_ev
+    def kernel_us(fn, n_ev):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(int(2e6 + n_ev * 2e4))
+        e0.record(stream)
+        for _ in range(n_ev):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        return e0.elapsed_time(e1) * 1e3 / n_ev
+
+    k_us = kernel_us(step, max(20, min(args.steps, 100)))
+    k1_us = kernel_us(step_single, max(50, min(args.steps, 500)))
     achieved_tops = pairs_per_step * VALU_OPS_PER_PAIR / (k_us * 1e-6) / 1e12
-    alg_bytes = (nq + nt) * 32 + nq * 12
-    plan = ctx.hamming_top2_plan(nq, nt)
-    tr = pmc_traffic(args.traffic, plan.split(" ")[0].split("<")[0])
+    alg_bytes = B * ((nq + nt) * 32 + nq * 12)
+    ql = int(os.environ.get("OSG_TOP2_BATCH_QL", "2"))
+    kname = (f"k_top2_batch<{ql},{int(os.environ.get('OSG_TOP2_BATCH_SCALAR', '1'))}> "
+             f"grid={(nq + 64 * ql - 1) // (64 * ql)} x {B} x 1024")
+    tr = pmc_traffic(args.traffic, "k_top2_batch")
     roofline = {
-        "kernel": plan,
+        "kernel": kname,
         "bound": "valu",
         "achieved": round(achieved_tops, 3),
         "peak": round(PEAK_VALU_TOPS, 1),
         "unit": "Tops/s (int32 VALU lane-ops)",
+        "peak_source": "256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz; measured ceiling 38.0-38.5 T "
+                       "(tools/micro/valu_rate.hip, profiles/r02_valu_rate.txt)",
         "frac": round(achieved_tops / PEAK_VALU_TOPS, 4),
         "traffic": None if tr is None else round(tr[0]),
         "traffic_source": None if tr is None else f"{os.path.relpath(args.traffic, ROOT)}: {tr[1]}",
@@ -172,6 +201,15 @@ def main():
         "algorithmic_ops_per_launch": pairs_per_step * VALU_OPS_PER_PAIR,
         "algorithmic_bytes_per_launch": alg_bytes,
         "hbm_frac_if_priced_as_hbm": round(alg_bytes / (k_us * 1e-6) / 1e9 / PEAK_HBM_GBS, 5),
+    }
+    plan = ctx.hamming_top2_plan(nq, nt)
+    tr1 = pmc_traffic(args.traffic, plan.split(" ")[0].split("<")[0])
+    single = {
+        "kernel": plan, "kernel_us": round(k1_us, 3),
+        "Mmatches_per_s_kernel": round(nq * nt / (k1_us * 1e-6) / 1e6, 1),
+        "frac": round(nq * nt * VALU_OPS_PER_PAIR / (k1_us * 1e-6) / 1e12 / PEAK_VALU_TOPS, 4),
+        "traffic": None if tr1 is None else round(tr1[0]),
+        "note": "one 2000 x 2000 problem per launch (osg_hamming_top2_dev): the latency form",
     }
 
     out = {
@@ -187,10 +225,14 @@ def main():
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (SURVEY.md §8d C2 generator, seed 0x0B5EED01+rank; no EuRoC/ORBvoc in container)",
-        "config": {"workload": "C2: brute-force 256-bit Hamming top-2, 2000 x 2000 descriptors per GPU",
-                   "nq": nq, "nt": nt, "global_batch": world,
+        "config": {"workload": f"C2: brute-force 256-bit Hamming top-2, 2000 x 2000 descriptors per frame, "
+                               f"{B} independent frames per launch per GPU (headline; the one-frame launch is "
+                               f"`single_launch`)",
+                   "nq": nq, "nt": nt, "frames_per_step": B, "global_batch": world * B,
                    "parallelism": f"replicas x{world} (independent frames per GPU, no data-path collective)"},
         "roofline": roofline,
+        "single_launch": single,
+        "batch_frame0_equals_single": batch_frame0_equal,
     }
 
     # ---- C2' streaming kernel: HBM roofline (Q = 4 x M = 2^24, 512 MiB > Infinity Cache) -----

@@ -99,6 +99,16 @@ int osg_hamming_top2(osg_ctx *ctx, const uint8_t *query, int32_t nq, const uint8
 int osg_hamming_top2_dev(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d_train,
                          int32_t nt, void *d_out);
 
+/* Frame-batched device form: nb independent problems of equal shape in one launch, problem b's
+ * queries at rows [b*nq, (b+1)*nq) of d_query, its train set at rows [b*nt, (b+1)*nt) of d_train,
+ * its results at rows [b*nq, (b+1)*nq) of d_out (nq x int32[3] each, as osg_hamming_top2_dev).
+ * Every problem's result is exactly the serial loop's (same semantics as osg_hamming_top2); train
+ * indices are problem-local.  nt <= 2^23, nb <= 65535.  Asynchronous on the context stream.
+ * No reference counterpart: the frame-batched throughput form of the loop above (SURVEY.md §8(d)
+ * C2, one 2000 x 2000 problem per frame). */
+int osg_hamming_top2_batch_dev(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d_train,
+                               int32_t nt, int32_t nb, void *d_out);
+
 /* Diagnostics: name and grid of the kernel osg_hamming_top2[_dev] would launch for (nq, nt) in
  * this process (the launch knobs are read once).  No reference counterpart. */
 int osg_hamming_top2_plan(osg_ctx *ctx, int32_t nq, int32_t nt, char *name, int32_t len);

@@ -123,6 +123,12 @@ class Context:
                                                  _ptr(d_train), int(nt), _ptr(d_out)),
                    "osg_hamming_top2_dev")
 
+    def hamming_top2_batch_dev(self, d_query, nq: int, d_train, nt: int, nb: int, d_out):
+        """nb equal-shape problems in one launch (device pointers / tensors; problem b at rows b*nq of
+        d_query and d_out, b*nt of d_train); async on the stream."""
+        self.check(self.lib.osg_hamming_top2_batch_dev(self.handle, _ptr(d_query), int(nq), _ptr(d_train), int(nt),
+                                                       int(nb), _ptr(d_out)), "osg_hamming_top2_batch_dev")
+
     def hamming_top2_plan(self, nq: int, nt: int) -> str:
         """Name and grid of the kernel a (nq, nt) top-2 launch uses in this process."""
         import ctypes

@@ -447,6 +447,104 @@ __global__ __launch_bounds__(1024) void k_top2_qsplit(const uint4 *__restrict__ 
     }
 }
 
+// ------------------------------------------------------------------------------ batch kernel
+// Frame-batched C2: B independent nq x nt problems in one launch (problem b: query rows
+// [b nq, (b+1) nq), train rows [b nt, (b+1) nt), out rows [b nq, (b+1) nq)).  grid (ceil(nq / (64
+// QL)), B) x 1024 threads: a lane holds QL queries in VGPRs (lane + 64 j), the 16 waves split the
+// train rows (row r on wave r % 16), rows staged in LDS in chunks of BATCH_ROWS and read as
+// wave-uniform broadcasts, so a pair costs the 19 VALU of the tile kernel and a row read from LDS
+// serves QL queries.  The 16 waves' keys meet in LDS (the staging buffer, reused) and are merged
+// in a fixed wave order: deterministic, and the same (first index, second with multiplicity) rule.
+// SCALAR = 1: no LDS staging; each wave reads its rows with scalar loads (wave-uniform address,
+// s_load_dwordx8 into SGPRs, v_xor with an SGPR operand), which frees the LDS return path that
+// the broadcast reads share between the CU's four SIMDs.
+constexpr int BATCH_ROWS = 2048;  // 64 KiB of LDS: two workgroups per CU
+template <int QL, int SCALAR>
+__global__ __launch_bounds__(1024) void k_top2_batch(const uint4 *__restrict__ query, int nq,
+                                                     const uint4 *__restrict__ train, int nt,
+                                                     int32_t *__restrict__ out)
+{
+    __shared__ uint4 s_rows[SCALAR ? 16 * 64 * QL / 2 : 2 * BATCH_ROWS];
+    const int t = threadIdx.x, lane = t & 63;
+    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+    const size_t b = blockIdx.y;
+    const uint4 *qf = query + 2 * b * (size_t)nq;
+    const uint4 *tf = train + 2 * b * (size_t)nt;
+    int32_t *of = out + 3 * b * (size_t)nq;
+    const int q0 = blockIdx.x * 64 * QL;
+    uint32_t qd[QL][8], k1[QL], k2[QL];
+#pragma unroll
+    for (int j = 0; j < QL; j++) {
+        const int qq = min(q0 + 64 * j + lane, nq - 1);
+        const uint4 a = qf[2 * qq], c = qf[2 * qq + 1];
+        qd[j][0] = a.x; qd[j][1] = a.y; qd[j][2] = a.z; qd[j][3] = a.w;
+        qd[j][4] = c.x; qd[j][5] = c.y; qd[j][6] = c.z; qd[j][7] = c.w;
+        k1[j] = k2[j] = KEY_EMPTY;
+    }
+    if (SCALAR) {
+        const uint32_t *tw = (const uint32_t *)tf;
+        int r = w;
+        for (; r + 48 < nt; r += 64) {
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+#pragma unroll
+                for (int j = 0; j < QL; j++)
+                    key_push(k1[j], k2[j], (hamming8(qd[j], tw + (size_t)(r + 16 * u) * 8) << KEY_SHIFT) |
+                                               (uint32_t)(r + 16 * u));
+        }
+        for (; r < nt; r += 16)
+#pragma unroll
+            for (int j = 0; j < QL; j++)
+                key_push(k1[j], k2[j], (hamming8(qd[j], tw + (size_t)r * 8) << KEY_SHIFT) | (uint32_t)r);
+    }
+    for (int c0 = 0; !SCALAR && c0 < nt; c0 += BATCH_ROWS) {
+        const int n = min(BATCH_ROWS, nt - c0);
+        if (c0 > 0) __syncthreads();  // previous chunk fully consumed
+        const uint4 *src = tf + 2 * (size_t)c0;
+        for (int i = t; i < 2 * n; i += 1024) s_rows[i] = src[i];
+        __syncthreads();
+        int r = w;
+        for (; r + 48 < n; r += 64) {
+            uint32_t tr[4][8];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint4 a = s_rows[2 * (r + 16 * u)], c = s_rows[2 * (r + 16 * u) + 1];
+                tr[u][0] = a.x; tr[u][1] = a.y; tr[u][2] = a.z; tr[u][3] = a.w;
+                tr[u][4] = c.x; tr[u][5] = c.y; tr[u][6] = c.z; tr[u][7] = c.w;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+#pragma unroll
+                for (int j = 0; j < QL; j++)
+                    key_push(k1[j], k2[j], (hamming8(qd[j], tr[u]) << KEY_SHIFT) | (uint32_t)(c0 + r + 16 * u));
+        }
+        for (; r < n; r += 16) {
+            const uint4 a = s_rows[2 * r], c = s_rows[2 * r + 1];
+            const uint32_t tr[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+#pragma unroll
+            for (int j = 0; j < QL; j++) key_push(k1[j], k2[j], (hamming8(qd[j], tr) << KEY_SHIFT) | (uint32_t)(c0 + r));
+        }
+    }
+    __syncthreads();  // the staging buffer becomes the merge buffer
+    uint32_t *sk1 = (uint32_t *)s_rows, *sk2 = sk1 + 16 * 64 * QL;
+#pragma unroll
+    for (int j = 0; j < QL; j++) {
+        sk1[(w * QL + j) * 64 + lane] = k1[j];
+        sk2[(w * QL + j) * 64 + lane] = k2[j];
+    }
+    __syncthreads();
+    if (t < 64 * QL) {
+        const int j = t >> 6, q = q0 + t;
+        uint32_t a1 = sk1[t], a2 = sk2[t];
+#pragma unroll
+        for (int o = 1; o < 16; o++) key_merge(a1, a2, sk1[(o * QL + j) * 64 + (t & 63)], sk2[(o * QL + j) * 64 + (t & 63)]);
+        if (q < nq) {
+            const uint2 p = key_to_part(a1, a2, 0u);
+            write_result(of, q, p.y >> 16, p.x, p.y & 0xFFFFu);
+        }
+    }
+}
+
 // ----------------------------------------------------------------------------- stream kernel
 // Completion counters of the stream kernels: 8 group counters and one top counter, each on its
 // own 128-B line at the end of ctx->counters (the tile kernel uses the first nqb entries).
@@ -782,6 +880,44 @@ int osg_hamming_top2_dev(osg_ctx *ctx, const void *d_query, int32_t nq, const vo
     if (!ctx) return OSG_E_INVALID;
     OSG_REQUIRE(ctx, nq >= 0 && (nq == 0 || (d_query && d_out)) && (nt == 0 || d_train), "null pointer");
     return osg_launch_top2(ctx, d_query, nq, d_train, nt, d_out);
+}
+
+int osg_hamming_top2_batch_dev(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d_train, int32_t nt,
+                               int32_t nb, void *d_out)
+{
+    if (!ctx) return OSG_E_INVALID;
+    OSG_REQUIRE(ctx, nq >= 0 && nt >= 0 && nb >= 0, "negative size");
+    if (nq == 0 || nb == 0) return OSG_OK;
+    OSG_REQUIRE(ctx, d_query && d_out && (nt == 0 || d_train), "null pointer");
+    OSG_REQUIRE(ctx, nt <= (int)IDX_MASK, "nt=%d exceeds 2^23 rows per problem", nt);
+    OSG_REQUIRE(ctx, nb <= 65535, "nb=%d exceeds 65535 problems per launch", nb);
+    if (nt == 0) {
+        for (int b = 0; b < nb; b++) {
+            const int rc = osg_launch_top2(ctx, (const char *)d_query + (size_t)b * nq * 32, nq, nullptr, 0,
+                                           (char *)d_out + (size_t)b * nq * 12);
+            if (rc < 0) return rc;
+        }
+        return OSG_OK;
+    }
+    static const int ql_env = getenv("OSG_TOP2_BATCH_QL") ? atoi(getenv("OSG_TOP2_BATCH_QL")) : 2;
+    static const int sc = getenv("OSG_TOP2_BATCH_SCALAR") ? atoi(getenv("OSG_TOP2_BATCH_SCALAR")) : 1;
+    const int ql = (ql_env == 1 || ql_env == 4) ? ql_env : 2;
+    const dim3 grid((nq + 64 * ql - 1) / (64 * ql), nb), block(1024);
+    const uint4 *q = (const uint4 *)d_query, *t = (const uint4 *)d_train;
+    int32_t *o = (int32_t *)d_out;
+#define OSG_BATCH(QL_, SC_) hipLaunchKernelGGL((k_top2_batch<QL_, SC_>), grid, block, 0, ctx->stream, q, nq, t, nt, o)
+    if (sc) {
+        if (ql == 1) OSG_BATCH(1, 1);
+        else if (ql == 4) OSG_BATCH(4, 1);
+        else OSG_BATCH(2, 1);
+    } else {
+        if (ql == 1) OSG_BATCH(1, 0);
+        else if (ql == 4) OSG_BATCH(4, 0);
+        else OSG_BATCH(2, 0);
+    }
+#undef OSG_BATCH
+    OSG_HIP_CHECK(ctx, hipGetLastError());
+    return OSG_OK;
 }
 
 int osg_hamming_top2(osg_ctx *ctx, const uint8_t *query, int32_t nq, const uint8_t *train, int32_t nt,

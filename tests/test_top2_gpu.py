@@ -135,3 +135,71 @@ def test_tile_variants(oracle, variant, waves, wg):
         ref = otop2(oracle, q, t)
         for g, rr in zip(got[seed], ref):
             np.testing.assert_array_equal(np.array(g, np.int32), rr)
+
+
+# ---- frame-batched form (osg_hamming_top2_batch_dev): nb independent problems in one launch
+def _batch(ctx, qs, ts, ql=None, monkeypatch=None):
+    import torch
+    nb, nq, nt = len(qs), qs[0].shape[0], ts[0].shape[0]
+    dq = torch.from_numpy(np.ascontiguousarray(np.concatenate(qs))).cuda()
+    dt = torch.from_numpy(np.ascontiguousarray(np.concatenate(ts) if nt else np.zeros((0, 32), np.uint8))).cuda()
+    do = torch.full((nb * nq, 3), -7, dtype=torch.int32, device="cuda")
+    ctx.hamming_top2_batch_dev(dq, nq, dt, nt, nb, do)
+    torch.cuda.synchronize()
+    return do.cpu().numpy().reshape(nb, nq, 3)
+
+
+@pytest.mark.parametrize("nb,nq,nt", [(1, 2000, 2000), (7, 2000, 2000), (3, 1, 1), (5, 129, 3), (4, 300, 2049),
+                                      (2, 257, 5000), (64, 64, 200)])
+def test_batch_equals_serial_loop(ctx, oracle, nb, nq, nt):
+    qs, ts = zip(*[synth.descriptors_c2(nq, nt, seed=synth.SEED_C2 + 1000 * b + nq + nt) for b in range(nb)])
+    got = _batch(ctx, qs, ts)
+    for b in range(nb):
+        for k, r in enumerate(otop2(oracle, qs[b], ts[b])):
+            np.testing.assert_array_equal(got[b, :, k], r, err_msg=f"problem {b} column {k}")
+
+
+def test_batch_ties_and_sentinels(ctx, oracle):
+    """Exact duplicates straddling the 2048-row LDS chunk and the 16 waves' row slices, and a
+    problem whose every distance is 256 (idx -1), next to ordinary problems."""
+    rng = np.random.default_rng(12)
+    q0 = rng.integers(0, 256, (100, 32), dtype=np.uint8)
+    t0 = np.repeat(q0, 30, axis=0)
+    rng.shuffle(t0, axis=0)
+    q1 = rng.integers(0, 256, (100, 32), dtype=np.uint8)
+    t1 = np.repeat(~q1[:1], 3000, axis=0)
+    q2, t2 = synth.descriptors_c2(100, 3000, seed=99)
+    got = _batch(ctx, [q0, q1[:1].repeat(100, 0), q2], [t0, t1, t2])
+    for b, (q, t) in enumerate([(q0, t0), (q1[:1].repeat(100, 0), t1), (q2, t2)]):
+        for k, r in enumerate(otop2(oracle, q, t)):
+            np.testing.assert_array_equal(got[b, :, k], r)
+    assert (got[1, :, 0] == -1).all() and (got[1, :, 1] == 256).all()
+
+
+def test_batch_empty_train(ctx):
+    q, _ = synth.descriptors_c2(50, 1)
+    got = _batch(ctx, [q, q], [np.zeros((0, 32), np.uint8)] * 2)
+    assert (got[..., 0] == -1).all() and (got[..., 1:] == 256).all()
+
+
+@pytest.mark.parametrize("ql,sc", [("1", "0"), ("2", "0"), ("4", "0"), ("1", "1"), ("4", "1")])
+def test_batch_query_per_lane_variants(oracle, ql, sc):
+    """The queries-per-lane (OSG_TOP2_BATCH_QL) and scalar-load (OSG_TOP2_BATCH_SCALAR) instantiations,
+    read once per process."""
+    import subprocess
+    import sys
+    code = ("import numpy as np, torch\n"
+            "from orb_slam3_comments_ghr_amd import Context, synth\n"
+            "from tests.test_top2_gpu import _batch\n"
+            "ctx = Context(0)\n"
+            "qs, ts = zip(*[synth.descriptors_c2(333, 2100, seed=5 + b) for b in range(3)])\n"
+            "np.save('/tmp/_osg_batch_ql.npy', _batch(ctx, qs, ts))\n")
+    env = dict(__import__("os").environ, OSG_TOP2_BATCH_QL=ql, OSG_TOP2_BATCH_SCALAR=sc)
+    root = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = np.load("/tmp/_osg_batch_ql.npy")
+    qs, ts = zip(*[synth.descriptors_c2(333, 2100, seed=5 + b) for b in range(3)])
+    for b in range(3):
+        for k, ref in enumerate(otop2(oracle, qs[b], ts[b])):
+            np.testing.assert_array_equal(got[b, :, k], ref)
