@@ -2,7 +2,7 @@
 // ORB-SLAM3 tree built with -DORB_SLAM3_OSG.  The reference's
 // src/ORBmatcher.cc keeps every other member; the bodies below replace the six hot-path ones,
 // the two Fuse overloads, SearchForTriangulation, the two Sim3
-// SearchByProjection overloads and SearchForInitialization
+// SearchByProjection overloads, SearchBySim3 and SearchForInitialization
 // under #ifdef ORB_SLAM3_OSG (signatures: ref:include/ORBmatcher.h:36-66).
 #include "ORBmatcher.h"
 #include "osg_hooks_orbslam3.h"
@@ -73,6 +73,12 @@ int ORBmatcher::SearchByProjection(KeyFrame *pKF, Sophus::Sim3<float> &Scw, cons
 {  // ref:src/ORBmatcher.cc:623-733
     return osg_orbslam3::search_by_projection_sim3<H, KeyFrame>(pKF, Scw, vpPoints, &vpPointsKFs, vpMatched,
                                                                &vpMatchedKF, th, ratioHamming);
+}
+
+int ORBmatcher::SearchBySim3(KeyFrame *pKF1, KeyFrame *pKF2, std::vector<MapPoint *> &vpMatches12,
+                             const Sophus::Sim3f &S12, const float th)
+{  // ref:src/ORBmatcher.cc:1696-1939
+    return osg_orbslam3::search_by_sim3<H, KeyFrame>(pKF1, pKF2, vpMatches12, S12, th);
 }
 
 int ORBmatcher::SearchForInitialization(Frame &F1, Frame &F2, std::vector<cv::Point2f> &vbPrevMatched,

@@ -193,6 +193,30 @@ struct OsgHooks {
     // depth, image, distance and viewing-angle tests, the projection and PredictScale.  The second
     // SearchByProjection overload projects with its own pinhole formula (invz = 1 / z; u = fx * x * invz
     // + cx, :661-667) instead of mpCamera->project — different float rounding, so it is kept apart.
+    // ref:src/ORBmatcher.cc:1747-1772 (dir12: KF1's MapPoint into KF2 by S21 * T1w) and :1823-1850
+    // (KF2's into KF1 by S12 * T2w); both directions use pKF1's intrinsics, as the reference does
+    static int index_in_keyframe(MapPoint *pMP, KeyFrame *pKF) { return std::get<0>(pMP->GetIndexInKeyFrame(pKF)); }
+    static bool sim3_pair_query(KeyFrame *pKF1, KeyFrame *pKF2, MapPoint *pMP, const Sophus::Sim3f &S12, bool dir12,
+                                float &u, float &v, int &level)
+    {
+        KeyFrame *from = dir12 ? pKF1 : pKF2, *to = dir12 ? pKF2 : pKF1;
+        const Sophus::Sim3f S = dir12 ? S12.inverse() : S12;
+        const Eigen::Vector3f p3Dw = pMP->GetWorldPos();
+        const Eigen::Vector3f pc = S * (from->GetPose() * p3Dw);
+        if (pc(2) < 0.0) return false;
+        const float invz = 1.0 / pc(2);
+        const float x = pc(0) * invz;
+        const float y = pc(1) * invz;
+        u = pKF1->fx * x + pKF1->cx;
+        v = pKF1->fy * y + pKF1->cy;
+        if (!to->IsInImage(u, v)) return false;
+        const float maxDistance = pMP->GetMaxDistanceInvariance();
+        const float minDistance = pMP->GetMinDistanceInvariance();
+        const float dist3D = pc.norm();
+        if (dist3D < minDistance || dist3D > maxDistance) return false;
+        level = pMP->PredictScale(dist3D, to);
+        return true;
+    }
     static bool sim3_query(KeyFrame *pKF, const Sophus::Sim3f &Scw, MapPoint *pMP, bool pinhole_formula, float &u,
                            float &v, int &level)
     {

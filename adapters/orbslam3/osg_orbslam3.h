@@ -625,6 +625,66 @@ int search_by_projection_sim3(KeyFrameT *pKF, const Sim3T &Scw, const std::vecto
     return nm;
 }
 
+// ------------------------------------------------------------------------- b7 SearchBySim3
+// ref:src/ORBmatcher.cc:1696-1939: vbAlreadyMatched1/2 from vpMatches12 (the KF2 index through
+// GetIndexInKeyFrame), each direction's projection and pre-search filters by the hook (S21 * T1w
+// into KF2, S12 * T2w into KF1: depth, IsInImage, distance range, PredictScale), both searches in
+// one GPU call, the mutual pairs written into vpMatches12.
+template <class H, class KeyFrameT, class Sim3T, class MapPointT>
+int search_by_sim3(KeyFrameT *pKF1, KeyFrameT *pKF2, std::vector<MapPointT *> &vpMatches12, const Sim3T &S12,
+                   float th)
+{
+    osg_ctx *ctx = thread_ctx();
+    FrameView<KeyFrameT> f1(*pKF1), f2(*pKF2);
+    const std::vector<MapPointT *> vpMapPoints1 = pKF1->GetMapPointMatches();
+    const std::vector<MapPointT *> vpMapPoints2 = pKF2->GetMapPointMatches();
+    const int N1 = (int)vpMapPoints1.size(), N2 = (int)vpMapPoints2.size();
+    std::vector<uint8_t> already1(N1, 0), already2(N2, 0);
+    for (int i = 0; i < N1; i++) {  // :1715-1731
+        MapPointT *pMP = vpMatches12[i];
+        if (!pMP) continue;
+        already1[i] = 1;
+        const int idx2 = H::index_in_keyframe(pMP, pKF2);
+        if (idx2 >= 0 && idx2 < N2) already2[idx2] = 1;
+    }
+    struct Q {
+        std::vector<uint8_t> desc, valid;
+        std::vector<float> u, v;
+        std::vector<int32_t> lvl;
+        osg_fuse_queries q{};
+    } q12, q21;
+    auto gather = [&](const std::vector<MapPointT *> &mps, const std::vector<uint8_t> &already, bool dir12, Q &Qd) {
+        const int n = (int)mps.size();
+        Qd.desc.assign((size_t)n * 32, 0);
+        Qd.valid.assign(n, 0);
+        Qd.u.assign(n, 0.f);
+        Qd.v.assign(n, 0.f);
+        Qd.lvl.assign(n, 0);
+        for (int i = 0; i < n; i++) {
+            MapPointT *pMP = mps[i];
+            if (!pMP || already[i] || pMP->isBad()) continue;  // :1737-1742 / :1813-1818
+            if (!H::sim3_pair_query(pKF1, pKF2, pMP, S12, dir12, Qd.u[i], Qd.v[i], Qd.lvl[i])) continue;
+            Qd.valid[i] = 1;
+            const auto d = pMP->GetDescriptor();
+            std::memcpy(&Qd.desc[(size_t)32 * i], d.template ptr<unsigned char>(0), 32);
+        }
+        Qd.q.n = n;
+        Qd.q.desc = Qd.desc.data();
+        Qd.q.valid = Qd.valid.data();
+        Qd.q.u = Qd.u.data();
+        Qd.q.v = Qd.v.data();
+        Qd.q.pred_level = Qd.lvl.data();
+    };
+    gather(vpMapPoints1, already1, true, q12);
+    gather(vpMapPoints2, already2, false, q21);
+    std::vector<int32_t> match12(N1, -1);
+    const int nFound = check(ctx, osg_search_by_sim3(ctx, &f1.v, &f2.v, &q12.q, &q21.q, th, match12.data()),
+                             "osg_search_by_sim3");
+    for (int i1 = 0; i1 < N1; i1++)  // :1920-1936
+        if (match12[i1] >= 0) vpMatches12[i1] = vpMapPoints2[match12[i1]];
+    return nFound;
+}
+
 // ---------------------------------------------------------------- b6 SearchForInitialization
 // ref:src/ORBmatcher.cc:735-878: vnMatches12 sized F1.mvKeysUn.size(), vbPrevMatched updated for the
 // surviving matches.

@@ -368,6 +368,20 @@ int osg_search_by_projection_sim3(osg_ctx *ctx, const osg_frame *KF, const osg_f
 int osg_search_by_projection_sim3_batch(osg_ctx *ctx, const osg_frame *KF, const osg_fuse_queries *Q, int32_t B,
                                         float th, float ratio_hamming, int32_t *slot_query, int32_t *nmatches);
 
+/* ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, S12, th)   ref:src/ORBmatcher.cc:1696-1939
+ * (LoopClosing::DetectCommonRegionsFromBoW / DetectAndReffineSim3FromLastKF, ref:include/ORBmatcher.h:78).
+ * q12: one query per KF1 keypoint: KF1's MapPoint in that slot projected into KF2 by S21 * T1w
+ * (u, v, PredictScale(dist3D, pKF2)); valid = a MapPoint that is not already in vpMatches12, not
+ * bad, in front of KF2, inside its image and within its distance-invariance range (:1737-1772).
+ * q21: one query per KF2 keypoint, KF2's MapPoints into KF1 by S12 * T2w (:1813-1850).  Each query
+ * takes the first minimum-distance keypoint of its window (KeyFrame::GetFeaturesInArea, levels
+ * [pred - 1, pred]) when that distance <= TH_HIGH; match12[i1] = idx2 for the mutual pairs
+ * (vnMatch2[vnMatch1[i1]] == i1), else -1: the caller sets vpMatches12[i1] = vpMapPoints2[idx2].
+ * Returns nFound (>= 0) or an OSG_E_* code.  Descriptor, u/v and pred_level are read for valid
+ * queries only; ur / inv_level_sigma2 are not used. */
+int osg_search_by_sim3(osg_ctx *ctx, const osg_frame *kf1, const osg_frame *kf2, const osg_fuse_queries *q12,
+                       const osg_fuse_queries *q21, float th, int32_t *match12);
+
 /* ---- b3: SearchForTriangulation ---------------------------------------------------------------
  * ORBmatcher::SearchForTriangulation(KeyFrame *pKF1, KeyFrame *pKF2, vector<pair<size_t,size_t>>&,
  * bOnlyStereo, bCoarse)  ref:src/ORBmatcher.cc:1045-1328 (LocalMapping::CreateNewMapPoints,

@@ -44,6 +44,9 @@ int oracle_search_for_initialization(const osg_frame *F1, const osg_frame *F2, f
 /* Sim3 projections of LoopClosing (oracle_sim3.c); slot_query as osg_search_by_projection_sim3 */
 int oracle_search_by_projection_sim3(const osg_frame *KF, const osg_fuse_queries *Q, float th, float ratioHamming,
                                      int32_t *slot_query);
+/* ORBmatcher::SearchBySim3 (oracle_sim3.c) */
+int oracle_search_by_sim3(const osg_frame *KF1, const osg_frame *KF2, const osg_fuse_queries *Q12,
+                          const osg_fuse_queries *Q21, float th, int32_t *match12);
 /* MapPoint::ComputeDistinctiveDescriptors over a list (oracle_desc.c) */
 void oracle_compute_distinctive_descriptors(const uint8_t *desc, const int32_t *start, int n_points, int32_t *best_idx);
 /* SearchForTriangulation (oracle_triang.c) */

@@ -185,7 +185,7 @@ EXPORTS = [
     "osg_vocabulary_transform", "osg_vocabulary_transform_batch",
     "osg_fuse_search", "osg_fuse_search_batch", "osg_search_for_triangulation", "osg_search_for_triangulation_batch",
     "osg_compute_distinctive_descriptors", "osg_compute_distinctive_descriptors_dev",
-    "osg_search_by_projection_sim3", "osg_search_by_projection_sim3_batch",
+    "osg_search_by_projection_sim3", "osg_search_by_projection_sim3_batch", "osg_search_by_sim3",
     "osg_search_for_initialization", "osg_search_for_initialization_batch",
     "osg_compute_stereo_matches", "osg_compute_stereo_matches_batch", "osg_orb_describe",
 ]
@@ -248,6 +248,8 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.osg_fuse_search_batch.argtypes = [vp, vp, vp, i32, f32, C.c_int, C.c_int, vp, vp, vp]
     lib.osg_search_for_triangulation.argtypes = [vp, C.POINTER(OsgKfSide), C.POINTER(OsgKfSide),
                                                  C.POINTER(OsgTriangGeom), C.c_int, C.c_int, C.c_int, vp]
+    lib.osg_search_by_sim3.argtypes = [vp, C.POINTER(OsgFrame), C.POINTER(OsgFrame), C.POINTER(OsgFuseQueries),
+                                       C.POINTER(OsgFuseQueries), f32, vp]
     lib.osg_search_by_projection_sim3.argtypes = [vp, C.POINTER(OsgFrame), C.POINTER(OsgFuseQueries), f32, f32, vp]
     lib.osg_search_by_projection_sim3_batch.argtypes = [vp, vp, vp, i32, f32, f32, vp, vp]
     lib.osg_search_for_initialization.argtypes = [vp, C.POINTER(OsgFrame), C.POINTER(OsgFrame), vp, C.c_int, f32,

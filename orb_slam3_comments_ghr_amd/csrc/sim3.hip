@@ -2,7 +2,12 @@
 //   SearchByProjection(KeyFrame*, Sim3f& Scw, const vector<MapPoint*>&, vector<MapPoint*>& vpMatched, th, ratioHamming)
 //                                                                     ref:src/ORBmatcher.cc:498-621
 //   and its vpPointsKFs / vpMatchedKF overload                         ref:src/ORBmatcher.cc:623-733
-// (LoopClosing calls them at ref:src/LoopClosing.cc:1062, 1091, 1368).
+// (LoopClosing calls them at ref:src/LoopClosing.cc:1062, 1091, 1368), and
+//   SearchBySim3(KeyFrame*, KeyFrame*, vector<MapPoint*>& vpMatches12, Sim3f& S12, th)
+//                                                                     ref:src/ORBmatcher.cc:1696-1939
+// whose two projection searches (KF1's MapPoints into KF2, KF2's into KF1) take no slots: each
+// query's strict-'<' minimum over its window is final after one round (`once`), accepted iff
+// bestDist <= TH_HIGH, and the host keeps the mutual pairs.
 //
 // Per MapPoint (query, list order): KeyFrame::GetFeaturesInArea (ix outer, iy inner, strict window;
 // ref:src/KeyFrame.cc:859-907), skip slots already in vpMatched, level window [pred - 1, pred], the
@@ -39,6 +44,7 @@ struct Sim3Args {
     GLOBAL const int32_t *lvl;
     GLOBAL int32_t *best;          // per query: matched slot or -1
     GLOBAL int32_t *stats;         // per problem: rounds
+    int once;                      // SearchBySim3: no slot claims, one round
 };
 
 __device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc)
@@ -123,7 +129,7 @@ __global__ __launch_bounds__(ST) void k_sim3(const Sim3Args *__restrict__ args)
         if (changed) s_changed = 1;
         rounds++;
         __syncthreads();
-        if (!s_changed) break;
+        if (!s_changed || A.once) break;
         for (int s = tid; s < A.n_slots; s += ST) claim[s] = 0x7FFFFFFF;
         __syncthreads();
         for (int q = tid; q < A.nq; q += ST) {
@@ -146,8 +152,10 @@ void relocate(T *&field, char *base)
     if (field) field = (T *)(base + ((uintptr_t)field - 1));
 }
 
+// once = 0: the Sim3 projections (slot claims, thr = TH_LOW * ratio, results into slot_query);
+// once = 1: SearchBySim3's searches (thr = TH_HIGH, per-query results into query_best)
 int sim3_run(osg_ctx *ctx, const osg_frame *KF, const osg_fuse_queries *Q, int B, float th, float ratio,
-             int32_t *slot_query, int32_t *nmatches)
+             int32_t *slot_query, int32_t *nmatches, int once = 0, int32_t *query_best = nullptr)
 {
     if (!ctx) return OSG_E_INVALID;
     OSG_REQUIRE(ctx, B >= 0 && (B == 0 || (KF && Q && nmatches && slot_query)), "null argument");
@@ -173,7 +181,8 @@ int sim3_run(osg_ctx *ctx, const osg_frame *KF, const osg_fuse_queries *Q, int B
         A.inv_w = F->grid_inv_w;
         A.inv_h = F->grid_inv_h;
         A.th = th;
-        A.thr = (float)OSG_TH_LOW * ratio;
+        A.thr = once ? (float)OSG_TH_HIGH : (float)OSG_TH_LOW * ratio;
+        A.once = once;
         const int32_t *sq = slot_query + s_base[b];
         taken[b].resize(F->n);
         for (int i = 0; i < F->n; i++) {
@@ -202,6 +211,8 @@ int sim3_run(osg_ctx *ctx, const osg_frame *KF, const osg_fuse_queries *Q, int B
     }
     for (int b = 0; b < B; b++) nmatches[b] = 0;
     const size_t nq_total = q_base[B];
+    if (query_best)
+        for (size_t i = 0; i < nq_total; i++) query_best[i] = -1;
     if (nq_total == 0) return OSG_OK;
     const size_t in_bytes = (pk.total + 255) & ~size_t(255);
     const size_t args_bytes = (sizeof(Sim3Args) * (size_t)B + 255) & ~size_t(255);
@@ -252,6 +263,12 @@ int sim3_run(osg_ctx *ctx, const osg_frame *KF, const osg_fuse_queries *Q, int B
     OSG_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ev[0], ev[1]));
     ctx->last_kernel_ms = ms;
     int32_t rounds_max = 0;
+    if (query_best) {
+        for (size_t i = 0; i < nq_total; i++) query_best[i] = pin_out[i];
+        for (int b = 0; b < B; b++) rounds_max = std::max(rounds_max, pin_out[nq_total + b]);
+        ctx->match_stats[1] = rounds_max;
+        return OSG_OK;
+    }
     for (int b = 0; b < B; b++) {
         int32_t *sq = slot_query + s_base[b];
         int nm = 0;
@@ -285,6 +302,35 @@ int osg_search_by_projection_sim3_batch(osg_ctx *ctx, const osg_frame *KF, const
                                         float th, float ratio_hamming, int32_t *slot_query, int32_t *nmatches)
 {
     return sim3_run(ctx, KF, Q, B, th, ratio_hamming, slot_query, nmatches);
+}
+
+// SearchBySim3: both directions in one launch (problem 0: q12 against KF2, problem 1: q21 against
+// KF1), then the mutual check of ref:src/ORBmatcher.cc:1920-1936 in KF1 slot order.
+int osg_search_by_sim3(osg_ctx *ctx, const osg_frame *kf1, const osg_frame *kf2, const osg_fuse_queries *q12,
+                       const osg_fuse_queries *q21, float th, int32_t *match12)
+{
+    if (!ctx) return OSG_E_INVALID;
+    OSG_REQUIRE(ctx, kf1 && kf2 && q12 && q21 && match12, "null argument");
+    OSG_REQUIRE(ctx, q12->n == kf1->n && q21->n == kf2->n,
+                "q12 needs one query per KF1 keypoint (%d vs %d), q21 one per KF2 keypoint (%d vs %d)", q12->n,
+                kf1->n, q21->n, kf2->n);
+    const osg_frame F[2] = {*kf2, *kf1};
+    const osg_fuse_queries Q[2] = {*q12, *q21};
+    std::vector<int32_t> slots((size_t)kf1->n + kf2->n, -1), best((size_t)q12->n + q21->n, -1);
+    int32_t nm[2] = {0, 0};
+    const int rc = sim3_run(ctx, F, Q, 2, th, 1.0f, slots.data(), nm, 1, best.data());
+    if (rc < 0) return rc;
+    const int32_t *vnMatch1 = best.data(), *vnMatch2 = best.data() + q12->n;
+    int nFound = 0;
+    for (int i1 = 0; i1 < kf1->n; i1++) {
+        const int idx2 = vnMatch1[i1];
+        match12[i1] = -1;
+        if (idx2 >= 0 && vnMatch2[idx2] == i1) {
+            match12[i1] = idx2;
+            nFound++;
+        }
+    }
+    return nFound;
 }
 
 }  // extern "C"

@@ -413,6 +413,43 @@ def synth_fuse_queries(rng, F: FrameSoA, m=1000, noise_px=1.0, match_frac=0.6, v
                        inv_level_sigma2=inv_level_sigma2(F.scale))
 
 
+def synth_sim3_pair(rng, n1=1000, n2=1000, shared=0.5, noise_px=1.0, valid_frac=0.9, cross_frac=0.1):
+    """SearchBySim3's inputs (ref:src/ORBmatcher.cc:1696-1939): two keyframes and, per keypoint of each,
+    its MapPoint projected into the other (FuseQueries, one per slot).  `shared` of KF1's slots see a
+    point KF2 also sees: q12 lands near that KF2 keypoint with a noisy copy of its descriptor and q21
+    back near the KF1 keypoint (mutual); `cross_frac` of those are redirected so the two directions
+    disagree; the rest project anywhere with random descriptors."""
+    F1 = synth_frame(rng, n=n1, stereo=False)
+    F2 = synth_frame(rng, n=n2, stereo=False)
+    nl = len(F1.scale)
+
+    def q_for(F, m):
+        return dict(u=rng.uniform(F.min_x, F.max_x, m).astype(np.float32),
+                    v=rng.uniform(F.min_y, F.max_y, m).astype(np.float32),
+                    lvl=rng.integers(0, nl, m).astype(np.int32),
+                    desc=rng.integers(0, 256, (m, 32), dtype=np.uint8))
+    a, b = q_for(F2, n1), q_for(F1, n2)
+    k = int(shared * min(n1, n2))
+    i1 = rng.choice(n1, k, replace=False)
+    i2 = rng.choice(n2, k, replace=False)
+
+    def aim(q, F, src, dst):
+        q["u"][src] = F.kp_x[dst] + rng.normal(0, noise_px, len(src))
+        q["v"][src] = F.kp_y[dst] + rng.normal(0, noise_px, len(src))
+        q["lvl"][src] = np.clip(F.kp_octave[dst] + rng.integers(0, 2, len(src)), 0, nl - 1)
+        q["desc"][src] = _flip(rng, F.desc[dst], 0.05)
+    aim(a, F2, i1, i2)
+    back = i1.copy()
+    cross = rng.random(k) < cross_frac
+    back[cross] = rng.integers(0, n1, int(cross.sum()))
+    aim(b, F1, i2, back)
+
+    def fq(q, F, m):
+        return FuseQueries(desc=q["desc"], valid=rng.random(m) < valid_frac, u=q["u"], v=q["v"], ur=None,
+                           pred_level=q["lvl"], inv_level_sigma2=inv_level_sigma2(F.scale))
+    return F1, F2, fq(a, F2, n1), fq(b, F1, n2)
+
+
 def _featvec(rng, n, n_nodes, zipf=1.1, node_base=0):
     w = 1.0 / np.arange(1, n_nodes + 1) ** zipf
     node_of = rng.choice(n_nodes, size=n, p=w / w.sum())

@@ -116,6 +116,17 @@ class ORBmatcher:
         return nf, [bi[a:b].copy() for a, b in zip(cuts[:-1], cuts[1:])], [bd[a:b].copy() for a, b in
                                                                            zip(cuts[:-1], cuts[1:])]
 
+    def SearchBySim3(self, KF1: FrameSoA, KF2: FrameSoA, q12: FuseQueries, q21: FuseQueries, th: float):
+        """``SearchBySim3(pKF1, pKF2, vpMatches12, S12, th)`` (ref:src/ORBmatcher.cc:1696-1939): q12 = KF1's
+        MapPoints projected into KF2 (one per KF1 keypoint), q21 = KF2's into KF1.  Returns (nFound,
+        match12): the KF2 keypoint matched to each KF1 keypoint (mutual best), -1 = none."""
+        lib, h = self.ctx.lib, self.ctx.handle
+        assert q12.n == KF1.n and q21.n == KF2.n, "one query per keypoint of each KeyFrame"
+        a, b, qa, qb = KF1.struct(), KF2.struct(), q12.struct(), q21.struct()
+        out = np.full(KF1.n, -1, np.int32)
+        rc = lib.osg_search_by_sim3(h, C.byref(a), C.byref(b), C.byref(qa), C.byref(qb), float(th), out.ctypes.data)
+        return self.ctx.check(rc, "SearchBySim3"), out
+
     def SearchByProjectionSim3(self, KF: FrameSoA, fq: FuseQueries, mp_id, vpMatched, th: int, ratioHamming: float,
                                vpPointsKFs=None, vpMatchedKF=None) -> int:
         """``SearchByProjection(KeyFrame*, Sim3f&, vpPoints, [vpPointsKFs,] vpMatched, [vpMatchedKF,] th,

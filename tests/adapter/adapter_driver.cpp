@@ -1,7 +1,7 @@
 // adapter_driver.cpp — runs adapters/orbslam3/osg_orbslam3.h on mock ORB-SLAM3 objects built from
 // arrays written by tests/test_adapter.py, and writes the adapter's results back (test-only).
 //
-//   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba fuse fuse_sim3 triang distinct sim3 sim3_kfs init stereo gba merge_lba orb
+//   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba fuse fuse_sim3 triang distinct sim3 sim3_kfs sim3pair init stereo gba merge_lba orb
 //
 // Array file: repeated {u32 name_len, name, u8 dtype ('b' u8, 'i' i32, 'f' f32, 'd' f64), u64 count,
 // data}.
@@ -724,6 +724,51 @@ int main(int argc, char **argv)
             out["nmatches"] = make('i', std::vector<int32_t>{nm});
             out["matched"] = make('i', mo);
             out["matched_kf"] = make('i', mk);
+        } else if (mode == "sim3pair") {
+            // SearchBySim3: keyframes "F.*" (KF1) and "G.*" (KF2); per KF1 slot "A.*" (has desc ok u v level
+            // bad) of its MapPoint projected into KF2, per KF2 slot "B.*" likewise into KF1; "V.matched":
+            // initial vpMatches12 as KF2 slot indices (-1); params: th.  out: matched (KF2 slot or -1)
+            KeyFrame K1, K2;
+            build_kf_frame(in, K1);
+            {
+                Arrays g;
+                for (auto &kv : in)
+                    if (kv.first.rfind("G.", 0) == 0) g["F." + kv.first.substr(2)] = kv.second;
+                build_kf_frame(g, K2);
+            }
+            std::vector<MapPoint> P1(K1.N), P2(K2.N);
+            auto fill = [&](const char *pre, std::vector<MapPoint> &P, KeyFrame &K, KeyFrame &other, int d) {
+                const std::string a(pre);
+                for (int i = 0; i < K.N; i++) {
+                    MapPoint &p = P[i];
+                    if (!get(in, a + "has").p<uint8_t>()[i]) continue;
+                    std::memcpy(p.desc.buf.data(), get(in, a + "desc").p<uint8_t>() + 32 * i, 32);
+                    p.s3_ok[d] = get(in, a + "ok").p<uint8_t>()[i];
+                    p.s3_u[d] = get(in, a + "u").p<float>()[i];
+                    p.s3_v[d] = get(in, a + "v").p<float>()[i];
+                    p.s3_level[d] = get(in, a + "level").p<int32_t>()[i];
+                    p.bad = get(in, a + "bad").p<uint8_t>()[i];
+                    p.obs[&K] = std::make_tuple(i, -1);
+                    K.mvpMapPoints[i] = &p;
+                }
+                (void)other;
+            };
+            fill("A.", P1, K1, K2, 0);
+            fill("B.", P2, K2, K1, 1);
+            std::vector<MapPoint *> m12(K1.N, nullptr);
+            for (int i = 0; i < K1.N; i++) {
+                const int32_t j = get(in, "V.matched").p<int32_t>()[i];
+                if (j >= 0) {
+                    m12[i] = &P2[j];
+                    P2[j].obs[&K2] = std::make_tuple(j, -1);
+                }
+            }
+            const int nm = osg_orbslam3::search_by_sim3<MockHooks, KeyFrame>(&K1, &K2, m12, Sim3{}, prm[0]);
+            std::vector<int32_t> mo(K1.N, -1);
+            for (int i = 0; i < K1.N; i++)
+                if (m12[i]) mo[i] = (int32_t)(m12[i] - P2.data());
+            out["nmatches"] = make('i', std::vector<int32_t>{nm});
+            out["matched"] = make('i', mo);
         } else if (mode == "init") {
             // F1 "F.*", F2 "G.*", vbPrevMatched "V.prev" (n1 x 2); params: windowSize nnratio checkOri
             Frame F1, F2;

@@ -73,6 +73,10 @@ struct MapPoint {
     bool proj_ok = false;
     float proj_u = 0, proj_v = 0, proj_invz = 0, proj_ur = 0, proj_vr = 0, proj_fuse_ur = 0;
     int proj_level = 0;
+    // test-only: what MockHooks::sim3_pair_query returns, [0] KF1 -> KF2, [1] KF2 -> KF1
+    bool s3_ok[2] = {false, false};
+    float s3_u[2] = {0, 0}, s3_v[2] = {0, 0};
+    int s3_level[2] = {0, 0};
     std::map<KeyFrame *, std::tuple<int, int>> obs;
 
     bool isBad() const { return bad; }
@@ -283,6 +287,20 @@ struct MockHooks {
         return p->proj_ok;
     }
     static void triang_geom(KeyFrame *pKF1, KeyFrame *, osg_triang_geom &g) { g = pKF1->triang_geom; }
+    static int index_in_keyframe(MapPoint *p, KeyFrame *k)
+    {
+        const auto it = p->obs.find(k);
+        return it == p->obs.end() ? -1 : std::get<0>(it->second);
+    }
+    static bool sim3_pair_query(KeyFrame *, KeyFrame *, MapPoint *p, const Sim3 &, bool dir12, float &u, float &v,
+                                int &level)
+    {
+        const int d = dir12 ? 0 : 1;
+        u = p->s3_u[d];
+        v = p->s3_v[d];
+        level = p->s3_level[d];
+        return p->s3_ok[d];
+    }
     static bool sim3_query(KeyFrame *, const Sim3 &, MapPoint *p, bool, float &u, float &v, int &level)
     {
         u = p->proj_u;

@@ -66,6 +66,8 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.oracle_search_by_projection_sim3.argtypes = [C.POINTER(OsgFrame), C.POINTER(OsgFuseQueries), f32, f32, vp]
     lib.oracle_search_for_initialization.argtypes = [C.POINTER(OsgFrame), C.POINTER(OsgFrame), vp, C.c_int, f32,
                                                      C.c_int, vp]
+    lib.oracle_search_by_sim3.argtypes = [C.POINTER(OsgFrame), C.POINTER(OsgFrame), C.POINTER(OsgFuseQueries),
+                                          C.POINTER(OsgFuseQueries), f32, vp]
     lib.oracle_compute_distinctive_descriptors.argtypes = [vp, vp, C.c_int, vp]
     lib.oracle_compute_distinctive_descriptors.restype = None
     lib.oracle_compute_stereo_matches.argtypes = [C.POINTER(OsgStereoFrame), vp, vp]
@@ -188,6 +190,14 @@ def sim3(oracle, KF, Q, th, ratio, slot_query):
     fs, qs = KF.struct(), Q.struct()
     n = oracle.oracle_search_by_projection_sim3(C.byref(fs), C.byref(qs), float(th), float(ratio), s.ctypes.data)
     return n, s
+
+
+def search_by_sim3(oracle, K1, K2, Q12, Q21, th):
+    """SearchBySim3 through the oracle: (nFound, match12 = KF2 slot per KF1 slot or -1)."""
+    out = np.full(K1.n, -1, np.int32)
+    a, b, q1, q2 = K1.struct(), K2.struct(), Q12.struct(), Q21.struct()
+    n = oracle.oracle_search_by_sim3(C.byref(a), C.byref(b), C.byref(q1), C.byref(q2), float(th), out.ctypes.data)
+    return n, out
 
 
 def initialization(oracle, F1, F2, prev_xy, window=100, nn=0.9, ori=True):

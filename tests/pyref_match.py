@@ -487,6 +487,32 @@ def search_sim3(F, Q, th, ratio, slot_query):
     return n, s
 
 
+def search_by_sim3(F1, F2, Q12, Q21, th):
+    """ORBmatcher::SearchBySim3 (ref:src/ORBmatcher.cc:1696-1939) from the area walk on: each direction's
+    strict-'<' minimum from INT_MAX, accepted iff <= TH_HIGH; the mutual pairs in KF1 order."""
+    def direction(F, Q):
+        out = [-1] * Q.n
+        for q in range(Q.n):
+            if not Q.valid[q]:
+                continue
+            lvl = int(Q.pred_level[q])
+            r = f32(f32(th) * F.scale[lvl])
+            bd, bi = 2147483647, -1
+            for idx in features_in_area(F, Q.u[q], Q.v[q], r):
+                o = int(F.kp_octave[idx])
+                if o < lvl - 1 or o > lvl:
+                    continue
+                d = dist(Q.desc[q], F.desc[idx])
+                if d < bd:
+                    bd, bi = d, idx
+            if bd <= TH_HIGH:
+                out[q] = bi
+        return out
+    m1, m2 = direction(F2, Q12), direction(F1, Q21)
+    m12 = [(i2 if i2 >= 0 and m2[i2] == i1 else -1) for i1, i2 in enumerate(m1)]
+    return sum(1 for x in m12 if x >= 0), np.array(m12, np.int32)
+
+
 def search_for_initialization(F1, F2, prev, window=100, nn=0.9, ori=True):
     """ORBmatcher::SearchForInitialization (ref:src/ORBmatcher.cc:735-878): (nmatches, vnMatches12, prev)."""
     INT_MAX = 2147483647

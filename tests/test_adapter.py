@@ -725,3 +725,32 @@ def test_adapter_merge_local_bundle_adjustment(driver, tmp_path, ctx, oracle, st
     out = run(driver, tmp_path, "merge_lba", {**arrays, "params": np.array([4, 1], np.float32)})
     assert int(out["aborted"][0]) == 1 and out["erased"].size == 0
     np.testing.assert_array_equal(out["pose"].reshape(-1, 7), G.pose)
+
+
+@pytest.mark.gpu
+def test_adapter_search_by_sim3(driver, tmp_path, oracle):
+    """ORBmatcher::SearchBySim3 through the adapter: MapPoints per slot (some absent, some bad), some
+    KF1 slots already matched (their KF2 slots excluded through GetIndexInKeyFrame), both projections
+    from the hook; equals the oracle on the filtered queries."""
+    rng = np.random.default_rng(930)
+    K1, K2, q12, q21 = fr.synth_sim3_pair(rng, n1=900, n2=1000)
+    has1, has2 = rng.random(K1.n) < 0.85, rng.random(K2.n) < 0.85
+    bad1, bad2 = rng.random(K1.n) < 0.05, rng.random(K2.n) < 0.05
+    matched = np.full(K1.n, -1, np.int32)
+    pre = np.nonzero(rng.random(K1.n) < 0.05)[0]
+    matched[pre] = rng.choice(np.nonzero(has2)[0], len(pre), replace=False)
+    already2 = np.zeros(K2.n, bool)
+    already2[matched[pre]] = True
+    arrays = dict(frame_arrays(K1))
+    arrays.update({"G." + k[2:]: v for k, v in frame_arrays(K2).items()})
+    for pre_, Q, has, bad in [("A.", q12, has1, bad1), ("B.", q21, has2, bad2)]:
+        arrays.update({pre_ + "has": has.astype(np.uint8), pre_ + "desc": Q.desc.reshape(-1), pre_ + "ok": Q.valid,
+                       pre_ + "u": Q.u, pre_ + "v": Q.v, pre_ + "level": Q.pred_level, pre_ + "bad": bad.astype(np.uint8)})
+    arrays["V.matched"] = matched
+    arrays["params"] = np.array([7.5], np.float32)
+    out = run(driver, tmp_path, "sim3pair", arrays)
+    q12.valid = (q12.valid.astype(bool) & has1 & ~bad1 & (matched < 0)).astype(np.uint8)
+    q21.valid = (q21.valid.astype(bool) & has2 & ~bad2 & ~already2).astype(np.uint8)
+    n_ref, m_ref = oc.search_by_sim3(oracle, K1, K2, q12, q21, 7.5)
+    assert int(out["nmatches"][0]) == n_ref and n_ref > 100
+    np.testing.assert_array_equal(out["matched"], np.where(m_ref >= 0, m_ref, matched))

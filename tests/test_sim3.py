@@ -94,3 +94,58 @@ def test_gpu_hand_case_and_edges(ctx, oracle):
     F, Q, sq = world(9202, n=600, m=500)
     vp = np.full(F.n, 5, np.int32)  # every slot taken before the call
     assert m.SearchByProjectionSim3(F, Q, np.arange(500), vp, 8, 1.5) == 0
+
+
+# ---- ORBmatcher::SearchBySim3 (ref:src/ORBmatcher.cc:1696-1939)
+SIM3_TH = [7.5, 10.0]  # no caller in this fork (ref:include/ORBmatcher.h:78); ORB-SLAM2's LoopClosing::ComputeSim3 used 7.5
+
+
+@pytest.mark.parametrize("seed", range(3))
+@pytest.mark.parametrize("th", SIM3_TH)
+def test_search_by_sim3_oracle_vs_python(oracle, seed, th):
+    K1, K2, q12, q21 = fr.synth_sim3_pair(np.random.default_rng(9300 + seed), n1=200, n2=260)
+    ref = oc.search_by_sim3(oracle, K1, K2, q12, q21, th)
+    got = pr.search_by_sim3(K1, K2, q12, q21, th)
+    assert ref[0] == got[0] and ref[0] > 10
+    np.testing.assert_array_equal(ref[1], got[1])
+
+
+def test_search_by_sim3_hand_case(oracle):
+    """KF1 keypoint 0 <-> KF2 keypoint 0 mutual (d 3 / 2); KF1 keypoint 1 -> KF2 keypoint 0 (d 1, a
+    better one-way match, but KF2 keypoint 0 points back at KF1 keypoint 0): not mutual; KF1 keypoint 2
+    -> KF2 keypoint 1 at d 101 > TH_HIGH: rejected."""
+    F1 = fr.FrameSoA(desc=np.stack([bits(0), bits(90), bits(0)]), kp_x=np.array([100.0, 103.0, 300.0], np.float32),
+                     kp_y=np.array([100.0, 100.0, 100.0], np.float32), kp_angle=np.zeros(3, np.float32),
+                     kp_octave=np.zeros(3, np.int32))
+    F2 = fr.FrameSoA(desc=np.stack([bits(2), bits(101)]), kp_x=np.array([200.0, 400.0], np.float32),
+                     kp_y=np.array([200.0, 200.0], np.float32), kp_angle=np.zeros(2, np.float32),
+                     kp_octave=np.zeros(2, np.int32))
+    isg = fr.inv_level_sigma2(F1.scale)
+    q12 = fr.FuseQueries(desc=np.stack([bits(3), bits(1), bits(0)]), valid=np.ones(3, np.uint8),
+                         u=np.array([200, 200, 400], np.float32), v=np.array([200, 200, 200], np.float32), ur=None,
+                         pred_level=np.zeros(3, np.int32), inv_level_sigma2=isg)
+    q21 = fr.FuseQueries(desc=np.stack([bits(2), bits(0)]), valid=np.ones(2, np.uint8),
+                         u=np.array([101, 300], np.float32), v=np.array([100, 100], np.float32), ur=None,
+                         pred_level=np.zeros(2, np.int32), inv_level_sigma2=isg)
+    n, m12 = oc.search_by_sim3(oracle, F1, F2, q12, q21, 7.5)
+    assert n == 1 and m12.tolist() == [0, -1, -1]
+    assert pr.search_by_sim3(F1, F2, q12, q21, 7.5)[1].tolist() == [0, -1, -1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(3))
+@pytest.mark.parametrize("th", SIM3_TH)
+def test_search_by_sim3_gpu_vs_oracle(ctx, oracle, seed, th):
+    K1, K2, q12, q21 = fr.synth_sim3_pair(np.random.default_rng(9400 + seed), n1=1200, n2=1100 + 100 * seed)
+    n_ref, m_ref = oc.search_by_sim3(oracle, K1, K2, q12, q21, th)
+    n, m12 = ORBmatcher(ctx).SearchBySim3(K1, K2, q12, q21, th)
+    assert n == n_ref and n > 200
+    np.testing.assert_array_equal(m12, m_ref)
+
+
+@pytest.mark.gpu
+def test_search_by_sim3_gpu_empty(ctx):
+    K1, K2, q12, q21 = fr.synth_sim3_pair(np.random.default_rng(1), n1=50, n2=60)
+    q12.valid[:] = 0
+    n, m12 = ORBmatcher(ctx).SearchBySim3(K1, K2, q12, q21, 7.5)
+    assert n == 0 and (m12 == -1).all()
