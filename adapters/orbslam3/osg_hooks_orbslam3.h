@@ -92,7 +92,21 @@ struct OsgHooks {
             if (c1[k >> 1]->GetType() != GeometricCamera::CAM_PINHOLE ||
                 c2[k & 1]->GetType() != GeometricCamera::CAM_PINHOLE)
                 g.pinhole = 0;
-        if (!g.pinhole) return;  // KB8: only the bCoarse path runs on the GPU
+        if (!g.pinhole) {  // KannalaBrandt8: R12 / t12 per pair and the four cameras' parameters
+            for (int k = 0; k < nk; k++) {
+                const Eigen::Matrix3f R12 = T[k].rotationMatrix();
+                const Eigen::Vector3f t12 = T[k].translation();
+                for (int r = 0; r < 3; r++) {
+                    for (int c = 0; c < 3; c++) g.R12[k][3 * r + c] = R12(r, c);
+                    g.t12[k][r] = t12(r);
+                }
+            }
+            GeometricCamera *cams[4] = {c1[0], c1[1], c2[0], c2[1]};
+            for (int i = 0; i < 4; i++)
+                if (cams[i])
+                    for (int j = 0; j < 8 && j < (int)cams[i]->size(); j++) g.kb[i][j] = cams[i]->getParameter(j);
+            return;
+        }
         for (int k = 0; k < nk; k++) {
             const Eigen::Matrix3f R12 = T[k].rotationMatrix();
             const Eigen::Vector3f t12 = T[k].translation();

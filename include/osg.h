@@ -413,12 +413,21 @@ typedef struct osg_kf_side {
  * (ref:src/ORBmatcher.cc:1052-1083), supplied by the caller so the float values are the reference's
  * own.  F12[k] = K1^-T * [t12]x * R12 * K2^-1 (Pinhole.cpp:194-197), row-major, for the camera pair
  * k = 2 * bRight1 + bRight2 (ll, lr, rl, rr: T12 = Tll, Tlr, Trl, Trr, ref:src/ORBmatcher.cc:1205-1244);
- * only F12[0] is read without a rig.  pinhole = 0 (KannalaBrandt8: epipolarConstrain triangulates
- * through Eigen's JacobiSVD) is accepted only with coarse = 1. */
+ * only F12[0] is read without a rig.  pinhole = 0: KannalaBrandt8::epipolarConstrain (ref:src/
+ * CameraModels/KannalaBrandt8.cpp:321-326 -> TriangulateMatches :438-489), which reads, for the camera
+ * pair k, R12[k] / t12[k] (the Rll/tll, Rlr/tlr, Rrl/trl, Rrr/trr of :1205-1244; R12 row-major) and
+ * the cameras' parameters kb[c] = {fx, fy, cx, cy, k0, k1, k2, k3}: kb[0] = pKF1->mpCamera,
+ * kb[1] = pKF1->mpCamera2, kb[2] = pKF2->mpCamera, kb[3] = pKF2->mpCamera2 (only [0] and [2] are read
+ * without a rig).  The triangulation's 4x4 JacobiSVD null vector is taken as the smallest-eigenvalue
+ * eigenvector of A^T A (cyclic Jacobi, double) and atan2f / tanf / cosf / sinf by fixed
+ * double-precision kernels rounded to float: parity with Eigen / libm is unpinned at the last ulp. */
 typedef struct osg_triang_geom {
     float ep_x, ep_y;           /* pKF2->mpCamera->project(T2w * pKF1->GetCameraCenter()) */
     float F12[4][9];
     int32_t pinhole;
+    float R12[4][9];            /* KannalaBrandt8 only */
+    float t12[4][3];
+    float kb[4][8];
 } osg_triang_geom;
 
 /* match12[kf1.n]: KF2 keypoint index per KF1 keypoint (vMatches12 after the histogram), -1 = none.

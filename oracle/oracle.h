@@ -44,6 +44,11 @@ int oracle_search_for_initialization(const osg_frame *F1, const osg_frame *F2, f
 /* Sim3 projections of LoopClosing (oracle_sim3.c); slot_query as osg_search_by_projection_sim3 */
 int oracle_search_by_projection_sim3(const osg_frame *KF, const osg_fuse_queries *Q, float th, float ratioHamming,
                                      int32_t *slot_query);
+/* KannalaBrandt8::epipolarConstrain / unproject / project as SearchForTriangulation uses them (oracle_triang.c) */
+int oracle_kb8_epipolar_constrain(const float *cam1, const float *cam2, float x1, float y1, float x2, float y2,
+                                  const float *R12, const float *t12, float sigmaLevel, float unc);
+void oracle_kb8_unproject(const float *cam, float u, float v, float *r);
+void oracle_kb8_project(const float *cam, const float *X, float *uv);
 /* ORBmatcher::SearchBySim3 (oracle_sim3.c) */
 int oracle_search_by_sim3(const osg_frame *KF1, const osg_frame *KF2, const osg_fuse_queries *Q12,
                           const osg_fuse_queries *Q21, float th, int32_t *match12);

@@ -100,7 +100,8 @@ class OsgKfSide(C.Structure):
 
 
 class OsgTriangGeom(C.Structure):
-    _fields_ = [("ep_x", f32), ("ep_y", f32), ("F12", f32 * 36), ("pinhole", i32)]
+    _fields_ = [("ep_x", f32), ("ep_y", f32), ("F12", f32 * 36), ("pinhole", i32), ("R12", f32 * 36),
+                ("t12", f32 * 12), ("kb", f32 * 32)]
 
 
 class OsgImagePyramid(C.Structure):

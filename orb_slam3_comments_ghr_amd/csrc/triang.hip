@@ -13,12 +13,14 @@
 //   dist > TH_LOW || dist > bestDist -> skip ('<=': the last of equal distances wins) :1180
 //   epipole distance^2 < 100 * mvScaleFactors[octave2] -> skip (both monocular)    :1189-1203
 //   bCoarse || Pinhole::epipolarConstrain (F12 of the camera pair)  :1246, Pinhole.cpp:189-219
+//            || KannalaBrandt8::epipolarConstrain (triangulate + reproject, kb8_epipolar.h)
 // then the rotation histogram (bin of kp1.angle - kp2.angle, factor 1/30 kept) and
 // ComputeThreeMaxima in LDS (:1266-1316).  The FeatureVector merge-walk that pairs the nodes
 // (:1113-1287) is host work (node lists are std::map-ordered already).
 #include <algorithm>
 #include <vector>
 
+#include "kb8_epipolar.h"
 #include "match_common.h"
 
 #define GLOBAL __attribute__((address_space(1)))
@@ -28,9 +30,11 @@ namespace {
 constexpr int TT = 256;  // lanes per workgroup (one workgroup per keyframe pair)
 
 struct TriArgs {
-    int nq, check_ori, coarse, two_cam1;
+    int nq, check_ori, coarse, two_cam1, pinhole;
     float ep_x, ep_y;
     float F[4][9];
+    float R12[4][9], t12[4][3], kb[4][8];  // KannalaBrandt8 (pinhole = 0)
+    GLOBAL const float *qsig;       // KF1 mvLevelSigma2[kp1.octave] per query (KannalaBrandt8)
     GLOBAL const uint32_t *qdesc;   // nq x 32 B: KF1 descriptors of the queries
     GLOBAL const float *qx, *qy, *qang;
     GLOBAL const uint8_t *qflag;    // bit0 bStereo1, bit1 bRight1
@@ -118,7 +122,12 @@ __global__ __launch_bounds__(TT) void k_triang(const TriArgs *__restrict__ args)
                 if (distex * distex + distey * distey < 100 * A.scale2[oct2]) continue;
             }
             const int k = A.two_cam1 ? (right1 ? 2 : 0) + (right2 ? 1 : 0) : 0;  // :1205-1244
-            if (A.coarse || epipolar_ok(A.F[k], x1, y1, x2, y2, A.sigma2_2[oct2])) {  // :1246
+            bool ok = A.coarse;  // :1246
+            if (!ok && A.pinhole) ok = epipolar_ok(A.F[k], x1, y1, x2, y2, A.sigma2_2[oct2]);
+            else if (!ok)  // pCamera1 = KF1 mpCamera / mpCamera2 by bRight1, pCamera2 likewise for KF2
+                ok = kb8::epipolar_constrain(A.kb[right1 ? 1 : 0], A.kb[right2 ? 3 : 2], x1, y1, x2, y2, A.R12[k],
+                                             A.t12[k], A.qsig[q], A.sigma2_2[oct2]);
+            if (ok) {
                 best = idx2;
                 best_dist = dist;
             }
@@ -211,7 +220,7 @@ int check_side(osg_ctx *ctx, const osg_kf_side *S, const char *which, int b)
 struct Problem {
     std::vector<int32_t> q_feat, q_cb, q_ce;
     std::vector<uint32_t> qdesc;
-    std::vector<float> qx, qy, qang;
+    std::vector<float> qx, qy, qang, qsig;
     std::vector<uint8_t> qflag, flag2;
 };
 
@@ -261,10 +270,6 @@ int triang_run(osg_ctx *ctx, const osg_kf_side *K1, const osg_kf_side *K2, const
         if (rc < 0) return rc;
         OSG_REQUIRE(ctx, (k1->two_cam != 0) == (k2->two_cam != 0),
                     "problem %d: both keyframes need the same rig (R12 is undefined otherwise)", b);
-        if (!coarse && !G[b].pinhole)
-            return osg_set_error(ctx, OSG_E_UNSUPPORTED,
-                                 "problem %d: KannalaBrandt8::epipolarConstrain (JacobiSVD triangulation) is not "
-                                 "built; call with coarse = 1 or pinhole cameras", b);
         o_base[b + 1] = o_base[b] + (size_t)k1->n;
         Problem &p = P[b];
         walk(k1, k2, only_stereo, p);
@@ -279,17 +284,24 @@ int triang_run(osg_ctx *ctx, const osg_kf_side *K1, const osg_kf_side *K2, const
         A.ep_x = G[b].ep_x;
         A.ep_y = G[b].ep_y;
         std::memcpy(A.F, G[b].F12, sizeof(A.F));
+        A.pinhole = G[b].pinhole != 0;
+        std::memcpy(A.R12, G[b].R12, sizeof(A.R12));
+        std::memcpy(A.t12, G[b].t12, sizeof(A.t12));
+        std::memcpy(A.kb, G[b].kb, sizeof(A.kb));
         if (nq == 0) continue;
         p.qdesc.resize((size_t)nq * 8);
         p.qx.resize(nq);
         p.qy.resize(nq);
         p.qang.resize(nq);
+        p.qsig.resize(nq);
         for (int i = 0; i < nq; i++) {
             const int f = p.q_feat[i];
             std::memcpy(&p.qdesc[(size_t)i * 8], k1->desc + (size_t)f * 32, 32);
             p.qx[i] = k1->kp_x[f];
             p.qy[i] = k1->kp_y[f];
             p.qang[i] = k1->kp_angle[f];
+            const int o1 = k1->kp_octave[f];
+            p.qsig[i] = (o1 >= 0 && o1 < k1->n_levels) ? k1->level_sigma2[o1] : 0.f;
         }
         p.flag2.resize(k2->n);
         for (int j = 0; j < k2->n; j++) {
@@ -302,6 +314,7 @@ int triang_run(osg_ctx *ctx, const osg_kf_side *K1, const osg_kf_side *K2, const
         set_off(A.qx, pk.add(p.qx.data(), sizeof(float) * nq));
         set_off(A.qy, pk.add(p.qy.data(), sizeof(float) * nq));
         set_off(A.qang, pk.add(p.qang.data(), sizeof(float) * nq));
+        set_off(A.qsig, pk.add(p.qsig.data(), sizeof(float) * nq));
         set_off(A.qflag, pk.add(p.qflag.data(), nq));
         set_off(A.q_cb, pk.add(p.q_cb.data(), sizeof(int32_t) * nq));
         set_off(A.q_ce, pk.add(p.q_ce.data(), sizeof(int32_t) * nq));
@@ -341,6 +354,7 @@ int triang_run(osg_ctx *ctx, const osg_kf_side *K1, const osg_kf_side *K2, const
         relocate(A.qx, dev_in);
         relocate(A.qy, dev_in);
         relocate(A.qang, dev_in);
+        relocate(A.qsig, dev_in);
         relocate(A.qflag, dev_in);
         relocate(A.q_cb, dev_in);
         relocate(A.q_ce, dev_in);

@@ -661,6 +661,9 @@ class TriangGeom:
     ep: tuple
     F12: np.ndarray            # (4, 3, 3) float32; [0] only without a rig
     pinhole: bool = True
+    R12: np.ndarray | None = None   # KannalaBrandt8: (4, 3, 3) float32 per camera pair
+    t12: np.ndarray | None = None   # (4, 3)
+    kb: np.ndarray | None = None    # (4, 8): KF1 mpCamera, mpCamera2, KF2 mpCamera, mpCamera2
 
     def struct(self):
         s = _abi.OsgTriangGeom()
@@ -670,7 +673,29 @@ class TriangGeom:
         for i, v in enumerate(F.reshape(-1)):
             s.F12[i] = float(v)
         s.pinhole = int(bool(self.pinhole))
+        for name, shape in (("R12", (4, 3, 3)), ("t12", (4, 3)), ("kb", (4, 8))):
+            a = getattr(self, name)
+            if a is None:
+                continue
+            z = np.zeros(shape, np.float32)
+            z[:len(a)] = a
+            dst = getattr(s, name)
+            for i, v in enumerate(z.reshape(-1)):
+                dst[i] = float(v)
         return s
+
+
+KB8_TRIANG = np.array([458.654, 457.296, 367.215, 248.375, 3.48e-3, 7.15e-4, -2.05e-3, 2.03e-4], np.float32)
+
+
+def kb8_project(p, X):
+    """KannalaBrandt8::project in float64 (test geometry; the operators take float keypoints)."""
+    X = np.asarray(X, np.float64)
+    r2 = np.hypot(X[..., 0], X[..., 1])
+    theta = np.arctan2(r2, X[..., 2])
+    psi = np.arctan2(X[..., 1], X[..., 0])
+    r = theta + p[4] * theta ** 3 + p[5] * theta ** 5 + p[6] * theta ** 7 + p[7] * theta ** 9
+    return np.stack([p[0] * r * np.cos(psi) + p[2], p[1] * r * np.sin(psi) + p[3]], -1)
 
 
 def _rot(rng, deg):
@@ -688,14 +713,17 @@ def fundamental(K1, K2, R12, t12):
 
 
 def synth_triang_pair(rng, n1=1000, n2=1000, n_nodes=100, common=0.6, mp_frac=0.5, stereo=True, forward=False,
-                      two_cam=False, noise=0.7, flip=0.05, n_levels=8, distract=0.15):
+                      two_cam=False, noise=0.7, flip=0.05, n_levels=8, distract=0.15, kb8=False):
     """Two keyframes seeing one scene (EuRoC pinhole, 752x480): KF2 is KF1 moved 0.25 m sideways
     (``forward``: 0.4 m along the optical axis, so the epipole lies in the image) and turned 2 deg.
     ``common`` of the keypoints are projections of shared points (noise ``noise`` px x 1.2^octave,
     noisy descriptor copies, same vocabulary node, angle offset -7 +- 3 deg); the rest are random.
     ``mp_frac`` of each side already carry a MapPoint; ``stereo`` gives half of them a mvuRight.
     ``two_cam``: each keyframe is a two-camera rig (Nleft = n/2; right camera 0.11 m to the right),
-    keypoints [0, Nleft) in the left camera, the rest in the right one.  Returns (KF1, KF2, geom)."""
+    keypoints [0, Nleft) in the left camera, the rest in the right one.  ``kb8``: KannalaBrandt8 cameras
+    (EuRoC focal, TUM-VI-like distortion): shared keypoints are KB8 projections of points 2-8 m in front
+    and the geometry carries R12 / t12 / camera parameters for the triangulating epipolarConstrain.
+    Returns (KF1, KF2, geom)."""
     from .synth import EUROC_CX, EUROC_CY, EUROC_FY
     K = np.array([[EUROC_FX, 0, EUROC_CX], [0, EUROC_FY, EUROC_CY], [0, 0, 1.0]])
     R2 = _rot(rng, 2.0)
@@ -727,13 +755,20 @@ def synth_triang_pair(rng, n1=1000, n2=1000, n_nodes=100, common=0.6, mp_frac=0.
     for j in range(m):
         a, c = i1[j], i2[j]
         R1, t1 = Tcw[(1, cams[0][a])]
-        Xc = Kinv @ np.array([xs[0][a], ys[0][a], 1.0]) * rng.uniform(2, 8)
+        if kb8:
+            Xc = np.array([rng.uniform(-4, 4), rng.uniform(-3, 3), rng.uniform(2, 8)])
+            u1 = kb8_project(KB8_TRIANG, Xc)
+            if not (0 <= u1[0] < EUROC_W and 0 <= u1[1] < EUROC_H):
+                continue
+            xs[0][a], ys[0][a] = u1
+        else:
+            Xc = Kinv @ np.array([xs[0][a], ys[0][a], 1.0]) * rng.uniform(2, 8)
         Xw = R1.T @ (Xc - t1)
         R, t = Tcw[(2, cams[1][c])]
         X2 = R @ Xw + t
         if X2[2] <= 0.1:
             continue
-        u = K @ (X2 / X2[2])
+        u = kb8_project(KB8_TRIANG, X2) if kb8 else K @ (X2 / X2[2])
         if not (0 <= u[0] < EUROC_W and 0 <= u[1] < EUROC_H):
             continue
         keep[j] = True
@@ -778,7 +813,7 @@ def synth_triang_pair(rng, n1=1000, n2=1000, n_nodes=100, common=0.6, mp_frac=0.
                             kp_octave=octs[k], u_right=ur, has_mp=rng.random(n) < mp_frac,
                             node_id=node_ids[used], node_start=start, feat=np.concatenate(feats),
                             nleft=nleft[k], two_cam=int(two_cam), scale=scale_factors(n_levels)))
-    F = []
+    F, R12s, t12s = [], [], []
     for c1 in (0, 1) if two_cam else (0,):
         for c2 in (0, 1) if two_cam else (0,):
             R1, t1 = Tcw[(1, c1)]
@@ -786,13 +821,22 @@ def synth_triang_pair(rng, n1=1000, n2=1000, n_nodes=100, common=0.6, mp_frac=0.
             R12 = R1 @ R2_.T                 # T12 = T1w * T2w^-1
             t12 = t1 - R12 @ t2
             F.append(fundamental(K, K, R12, t12))
+            R12s.append(R12.astype(np.float32))
+            t12s.append(t12.astype(np.float32))
     Rl2, tl2 = Tcw[(2, 0)]
     e = Rl2 @ np.zeros(3) + tl2             # T2w * Cw (KF1 centre = world origin)
-    ep = (np.float32(EUROC_FX * e[0] / e[2] + EUROC_CX), np.float32(EUROC_FY * e[1] / e[2] + EUROC_CY))
+    if kb8:
+        epk = kb8_project(KB8_TRIANG, e)
+        ep = (np.float32(epk[0]), np.float32(epk[1]))
+    else:
+        ep = (np.float32(EUROC_FX * e[0] / e[2] + EUROC_CX), np.float32(EUROC_FY * e[1] / e[2] + EUROC_CY))
     if forward and n_dis:                   # a third of the distractors within ~20 px of the epipole
         near = dis[: n_dis // 3]
         sides[1].kp_x[near] = np.float32(ep[0]) + rng.uniform(-20, 20, len(near)).astype(np.float32)
         sides[1].kp_y[near] = np.float32(ep[1]) + rng.uniform(-20, 20, len(near)).astype(np.float32)
+    if kb8:
+        return sides[0], sides[1], TriangGeom(ep=ep, F12=np.stack(F), pinhole=False, R12=np.stack(R12s),
+                                              t12=np.stack(t12s), kb=np.tile(KB8_TRIANG, (4, 1)))
     return sides[0], sides[1], TriangGeom(ep=ep, F12=np.stack(F))
 
 

@@ -668,6 +668,12 @@ int main(int argc, char **argv)
             A.triang_geom.ep_y = g[1];
             std::memcpy(A.triang_geom.F12, g + 2, sizeof(float) * 36);
             A.triang_geom.pinhole = g[38] != 0;
+            if (has(in, "G.kb8")) {  // KannalaBrandt8: R12[36] t12[12] kb[32]
+                const float *k = get(in, "G.kb8").p<float>();
+                std::memcpy(A.triang_geom.R12, k, sizeof(float) * 36);
+                std::memcpy(A.triang_geom.t12, k + 36, sizeof(float) * 12);
+                std::memcpy(A.triang_geom.kb, k + 48, sizeof(float) * 32);
+            }
             std::vector<std::pair<size_t, size_t>> pairs;
             const int nm = osg_orbslam3::search_for_triangulation<MockHooks>(&A, &B, pairs, prm[0] != 0, prm[1] != 0,
                                                                               prm[2] != 0);

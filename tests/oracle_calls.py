@@ -66,6 +66,11 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.oracle_search_by_projection_sim3.argtypes = [C.POINTER(OsgFrame), C.POINTER(OsgFuseQueries), f32, f32, vp]
     lib.oracle_search_for_initialization.argtypes = [C.POINTER(OsgFrame), C.POINTER(OsgFrame), vp, C.c_int, f32,
                                                      C.c_int, vp]
+    lib.oracle_kb8_epipolar_constrain.argtypes = [vp, vp, f32, f32, f32, f32, vp, vp, f32, f32]
+    lib.oracle_kb8_unproject.argtypes = [vp, f32, f32, vp]
+    lib.oracle_kb8_unproject.restype = None
+    lib.oracle_kb8_project.argtypes = [vp, vp, vp]
+    lib.oracle_kb8_project.restype = None
     lib.oracle_search_by_sim3.argtypes = [C.POINTER(OsgFrame), C.POINTER(OsgFrame), C.POINTER(OsgFuseQueries),
                                           C.POINTER(OsgFuseQueries), f32, vp]
     lib.oracle_compute_distinctive_descriptors.argtypes = [vp, vp, C.c_int, vp]

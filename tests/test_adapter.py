@@ -490,19 +490,32 @@ def triang_arrays(pre, K):
 @pytest.mark.gpu
 @pytest.mark.parametrize("two_cam,coarse,only_stereo", [(False, False, False), (False, True, False),
                                                         (False, False, True), (True, False, False)])
-def test_adapter_search_for_triangulation(driver, tmp_path, oracle, two_cam, coarse, only_stereo):
+def test_adapter_search_for_triangulation(driver, tmp_path, oracle, two_cam, coarse, only_stereo, kb8=False):
     """SearchForTriangulation through the adapter (KeyFrame fields gathered by member name, geometry from
     the hook, vMatchedPairs rebuilt) gives the oracle's pairs."""
     rng = np.random.default_rng(780 + 2 * two_cam + coarse)
-    K1, K2, g = fr.synth_triang_pair(rng, n1=900, n2=900, forward=not two_cam, two_cam=two_cam)
+    K1, K2, g = fr.synth_triang_pair(rng, n1=900, n2=900, forward=not two_cam, two_cam=two_cam, kb8=kb8)
     geom = np.concatenate([[g.ep[0], g.ep[1]], np.resize(g.F12.reshape(-1), 36) if two_cam else
-                           np.concatenate([g.F12.reshape(-1), np.zeros(27)]), [1.0]]).astype(np.float32)
-    out = run(driver, tmp_path, "triang", {**triang_arrays("A.", K1), **triang_arrays("B.", K2), "G.geom": geom,
-                                           "params": np.array([only_stereo, coarse, 1.0], np.float32)})
+                           np.concatenate([g.F12.reshape(-1), np.zeros(27)]), [0.0 if kb8 else 1.0]]).astype(np.float32)
+    arrays = {**triang_arrays("A.", K1), **triang_arrays("B.", K2), "G.geom": geom,
+              "params": np.array([only_stereo, coarse, 1.0], np.float32)}
+    if kb8:
+        R12, t12 = np.zeros((4, 3, 3), np.float32), np.zeros((4, 3), np.float32)
+        R12[:len(g.R12)], t12[:len(g.t12)] = g.R12, g.t12
+        arrays["G.kb8"] = np.concatenate([R12.reshape(-1), t12.reshape(-1), g.kb.reshape(-1)]).astype(np.float32)
+    out = run(driver, tmp_path, "triang", arrays)
     n, pairs = oc.triangulation(oracle, K1, K2, g, only_stereo, coarse)
     assert n > 10
     assert int(out["nmatches"][0]) == n
     np.testing.assert_array_equal(out["pairs"].reshape(-1, 2), pairs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("two_cam", [False, True])
+def test_adapter_search_for_triangulation_kb8(driver, tmp_path, oracle, two_cam):
+    """KannalaBrandt8 keyframes, bCoarse = false: the hook's R12 / t12 / camera parameters reach the
+    triangulating epipolarConstrain through the adapter."""
+    test_adapter_search_for_triangulation(driver, tmp_path, oracle, two_cam, False, False, kb8=True)
 
 
 @pytest.mark.gpu

@@ -74,3 +74,96 @@ def test_oracle_triang_hand_case(oracle):
     for args in [(False, False), (True, False)]:
         K1, K2, g = hand_pair()
         same(oc.triangulation(oracle, K1, K2, g, *args), pr.search_for_triangulation(K1, K2, g, *args))
+
+
+# ---- KannalaBrandt8::epipolarConstrain (ref:src/CameraModels/KannalaBrandt8.cpp:321-326, 438-489)
+def _f(a):
+    return np.ascontiguousarray(a, np.float32)
+
+
+def test_kb8_project_unproject_round_trip(oracle):
+    """unproject(project(X)) is X's ray and project matches the float64 model to ~1e-4 px."""
+    rng = np.random.default_rng(41)
+    cam = _f(fr.KB8_TRIANG)
+    for _ in range(300):
+        X = _f([rng.uniform(-4, 4), rng.uniform(-3, 3), rng.uniform(1, 8)])
+        uv = np.zeros(2, np.float32)
+        oracle.oracle_kb8_project(cam.ctypes.data, X.ctypes.data, uv.ctypes.data)
+        np.testing.assert_allclose(uv, fr.kb8_project(cam.astype(np.float64), X.astype(np.float64)), atol=2e-3)
+        r = np.zeros(3, np.float32)
+        oracle.oracle_kb8_unproject(cam.ctypes.data, float(uv[0]), float(uv[1]), r.ctypes.data)
+        np.testing.assert_allclose(r[:2], X[:2] / X[2], rtol=0, atol=2e-5)
+        assert r[2] == 1.0
+
+
+def _kb8_ref(cam, x1, y1, x2, y2, R12, t12, s1, s2):
+    """float64 statement of TriangulateMatches > 1e-4: (decision, margin to the nearest threshold)."""
+    def unproj(u, v):
+        pw = np.array([(u - cam[2]) / cam[0], (v - cam[3]) / cam[1]])
+        td = np.hypot(*pw)
+        th = td
+        for _ in range(20):
+            f = th + cam[4] * th ** 3 + cam[5] * th ** 5 + cam[6] * th ** 7 + cam[7] * th ** 9 - td
+            df = 1 + 3 * cam[4] * th ** 2 + 5 * cam[5] * th ** 4 + 7 * cam[6] * th ** 6 + 9 * cam[7] * th ** 8
+            th -= f / df
+        s = np.tan(th) / td if td > 1e-8 else 1.0
+        return np.array([pw[0] * s, pw[1] * s, 1.0])
+    r1, r2 = unproj(x1, y1), unproj(x2, y2)
+    r21 = R12 @ r2
+    cosp = r1 @ r21 / (np.linalg.norm(r1) * np.linalg.norm(r21))
+    R21 = R12.T
+    A = np.stack([r1[0] * np.array([0, 0, 1, 0]) - np.array([1, 0, 0, 0]),
+                  r1[1] * np.array([0, 0, 1, 0]) - np.array([0, 1, 0, 0]),
+                  r2[0] * np.r_[R21[2], -(R21 @ t12)[2]] - np.r_[R21[0], -(R21 @ t12)[0]],
+                  r2[1] * np.r_[R21[2], -(R21 @ t12)[2]] - np.r_[R21[1], -(R21 @ t12)[1]]])
+    h = np.linalg.svd(A)[2][-1]
+    X = h[:3] / h[3]
+    X2 = R21 @ X - R21 @ t12
+    e1 = np.sum((fr.kb8_project(cam, X) - [x1, y1]) ** 2)
+    e2 = np.sum((fr.kb8_project(cam, X2) - [x2, y2]) ** 2)
+    ok = cosp <= 0.9998 and X[2] > 0 and X2[2] > 0 and e1 <= 5.991 * s1 and e2 <= 5.991 * s2 and X[2] > 1e-4
+    margin = min(abs(cosp - 0.9998) * 1e4, abs(X[2]), abs(X2[2]), abs(e1 - 5.991 * s1), abs(e2 - 5.991 * s2))
+    return ok, margin
+
+
+def test_kb8_epipolar_constrain_vs_float64(oracle):
+    """The oracle's float restatement decides as a float64 statement of the same test (numpy SVD) on
+    every case not within rounding of a threshold: true correspondences (2-8 m, 1 px noise), points
+    off the epipolar geometry, and parallax-free pairs."""
+    rng = np.random.default_rng(42)
+    cam = fr.KB8_TRIANG.astype(np.float64)
+    R12 = fr._rot(rng, 3.0)
+    t12 = np.array([0.3, 0.02, 0.05])
+    n_ok = n_rej = 0
+    for i in range(600):
+        X1 = np.array([rng.uniform(-3, 3), rng.uniform(-2, 2), rng.uniform(2, 8)])
+        X2 = R12.T @ X1 - R12.T @ t12
+        uv1, uv2 = fr.kb8_project(cam, X1), fr.kb8_project(cam, X2)
+        if i % 3 == 1:
+            uv2 = uv2 + rng.uniform(-40, 40, 2)      # off the epipolar geometry
+        elif i % 3 == 2:
+            uv1 = uv1 + rng.normal(0, 1.0, 2)
+            uv2 = uv2 + rng.normal(0, 1.0, 2)
+        uv1, uv2 = uv1.astype(np.float32), uv2.astype(np.float32)
+        s1, s2 = np.float32(1.44), np.float32(1.0)
+        want, margin = _kb8_ref(cam, *uv1.astype(np.float64), *uv2.astype(np.float64), R12, t12, float(s1), float(s2))
+        got = oracle.oracle_kb8_epipolar_constrain(_f(cam).ctypes.data, _f(cam).ctypes.data, float(uv1[0]),
+                                                   float(uv1[1]), float(uv2[0]), float(uv2[1]),
+                                                   _f(R12).ctypes.data, _f(t12).ctypes.data, float(s1), float(s2))
+        if margin > 1e-2:
+            assert bool(got) == bool(want), (i, got, want, margin)
+        n_ok += bool(got)
+        n_rej += not got
+    assert n_ok > 250 and n_rej > 150
+
+
+@pytest.mark.parametrize("two_cam", [False, True])
+def test_oracle_triang_kb8_accepts_true_matches(oracle, two_cam):
+    """KannalaBrandt8 keyframes with bCoarse = false: the triangulating check keeps the true
+    correspondences and drops the distractors that bCoarse = true lets through."""
+    K1, K2, g = fr.synth_triang_pair(np.random.default_rng(43), n1=1000, n2=1000, kb8=True, two_cam=two_cam,
+                                     mp_frac=0.0)
+    n_fine, m_fine = oc.triangulation(oracle, K1, K2, g, coarse=False, ori=False)
+    n_coarse, m_coarse = oc.triangulation(oracle, K1, K2, g, coarse=True, ori=False)
+    assert n_fine > 100
+    assert n_fine <= n_coarse
