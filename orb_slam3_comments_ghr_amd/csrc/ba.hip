@@ -13,9 +13,9 @@
 // them (grid.y = graph; a graph that skips a kernel this step leaves at once).
 // Per LM iteration (device):
 //   k_errors      per edge: error, Huber rho -> per-workgroup chi2 partials        (HBM/latency)
-//   k_linearize   per landmark: its edges' Jacobians -> Hll, b_l, the Hpl blocks, and each edge's
-//                 pose part (Hpp upper + b_p) for k_pose_red                       (FP64 VALU)
-//   k_pose_red    per pose: Hpp, b_p from its edges (workgroup reduction)
+//   k_linearize   per landmark: its edges' Jacobians -> Hll, b_l, the Hpl blocks   (FP64 VALU)
+//   k_pose_red    per pose: Hpp, b_p from its edges' pose Jacobians, recomputed in place (a
+//                 workgroup reduction; no per-edge contribution round trip through HBM)
 // Per LM trial:
 //   k_schur_point / k_schur_block   Dinv = (Hll + lambda I)^-1, BDinv = Hpl Dinv, coef
 //   k_schur_chunks / k_schur_pairs  S_ij = sum_p BDinv_ip Hpl_jp^T over fixed chunks, then the dense
@@ -96,7 +96,6 @@ struct LbaDev {
     uint8_t *bad;                        // classification
     double *chi2o;                       // per edge chi2 of the last computed error (classification)
     double *err;                         // 3 per edge
-    double *J;                           // EC per edge: quadratic-form contributions
     double *Hll, *bl, *Hpl, *Hpp, *bp;
     double *Dinv, *db, *BDinv, *coef;
     double *Hs, *bs, *x;
@@ -181,9 +180,9 @@ __global__ __launch_bounds__(EB) void k_errors(const LbaDev *__restrict__ Ds, in
 //   * sums Hll (upper 6) and b_l in registers (the order of a per-landmark reduction over lm_e),
 //   * writes each Hpl block: a block's edges are in edge order inside its landmark, so the first
 //     edge stores and the others add (the order of a per-block reduction over blk_e),
-//   * writes the edge's pose part {Hpp upper 21, b_p 6} = EC doubles to J for k_pose_red,
-// and the workgroup's max |diag Hll| for computeLambdaInit.
-constexpr int EC = 27;
+// and the workgroup's max |diag Hll| for computeLambdaInit.  The edges' pose parts {Hpp upper 21,
+// b_p 6} are not stored: k_pose_red recomputes them pose-major (27 doubles per edge written and
+// read back cost more HBM time than the recomputed Jacobian costs VALU time).
 __global__ __launch_bounds__(EB) void k_linearize(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_LIN);
@@ -216,13 +215,7 @@ __global__ __launch_bounds__(EB) void k_linearize(const LbaDev *__restrict__ Ds)
                 for (int j = 0; j < 3; j++) Jx[2][j] = 0.0;
             }
             const int blk = D.edge_blk[e];
-            if (blk >= 0) {  // free pose: pose part and Hpl
-                double *o = D.J + EC * (size_t)e;
-                int c = 0;
-                for (int a = 0; a < 6; a++)
-                    for (int bb = a; bb < 6; bb++)
-                        o[c++] = Jp[0][a] * ww * Jp[0][bb] + Jp[1][a] * ww * Jp[1][bb] + Jp[2][a] * ww * Jp[2][bb];
-                for (int a = 0; a < 6; a++) o[c++] = Jp[0][a] * om[0] + Jp[1][a] * om[1] + Jp[2][a] * om[2];
+            if (blk >= 0) {  // free pose: Hpl (the pose part is recomputed by k_pose_red)
                 const bool first = D.blk_e[D.blk_e_start[blk]] == e;
                 double *hp = D.Hpl + 18 * (size_t)blk;
                 for (int a = 0; a < 6; a++)
@@ -264,10 +257,33 @@ __global__ __launch_bounds__(EB) void k_pose_red(const LbaDev *__restrict__ Ds)
     __shared__ double s[EB / 64][27];
     double acc[27];
     for (int k = 0; k < 27; k++) acc[k] = 0.0;
+    // every edge of the pose: its pose Jacobian and robust weight recomputed from the estimate and
+    // the error k_errors stored (the same expressions k_linearize evaluates per edge, so the sums are
+    // those of a stored-Jacobian reduction, without writing / reading EC doubles per edge)
+    const SE3 T = se3_from7(cur_pose(D) + 7 * (size_t)D.hp_pose[i]);
+    const double *points = cur_point(D);
     for (int q = D.hp_e_start[i] + threadIdx.x; q < D.hp_e_start[i + 1]; q += EB) {
         const int e = D.hp_e[q];
-        const double *C = D.J + EC * (size_t)e;
-        for (int k = 0; k < 27; k++) acc[k] += C[k];
+        const int k = D.e_kind[e];
+        double Jp[3][6], Jx[3][3];
+        edge_jacobians(k, true, D.cams[D.e_cam[e]], T, points + 3 * (size_t)D.e_point[e], Jp, Jx);
+        const int dim = (k == OSG_EDGE_STEREO) ? 3 : 2;
+        const double w = edge_w(D, e);
+        const double ev[3] = {D.err[3 * e], D.err[3 * e + 1], D.err[3 * e + 2]};
+        double delta, r0, rho1;
+        float dsqr;
+        edge_delta(D, e, k, delta, dsqr);
+        huber(chi2_of(ev, dim, w), delta, dsqr, r0, rho1);
+        const double ww = rho1 * w;
+        double om[3];
+        for (int d = 0; d < 3; d++) om[d] = (d < dim) ? -(w * ev[d]) * rho1 : 0.0;
+        if (dim == 2)
+            for (int j = 0; j < 6; j++) Jp[2][j] = 0.0;
+        int c = 0;
+        for (int a = 0; a < 6; a++)
+            for (int bb = a; bb < 6; bb++)
+                acc[c++] += Jp[0][a] * ww * Jp[0][bb] + Jp[1][a] * ww * Jp[1][bb] + Jp[2][a] * ww * Jp[2][bb];
+        for (int a = 0; a < 6; a++) acc[c++] += Jp[0][a] * om[0] + Jp[1][a] * om[1] + Jp[2][a] * om[2];
     }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int k = 0; k < 27; k++) acc[k] = wave_sum(acc[k]);
@@ -1320,7 +1336,6 @@ void carve_state(char *base, size_t &off, const LbaHost &H, LbaDev *D, bool prof
     double *qA = carve<double>(base, off, 3 * (size_t)npt);
     double *qB = carve<double>(base, off, 3 * (size_t)npt);
     double *err = carve<double>(base, off, 3 * (size_t)ne);
-    double *J = carve<double>(base, off, EC * (size_t)ne);
     double *Hll = carve<double>(base, off, 9 * (size_t)nhl);
     double *bl = carve<double>(base, off, 3 * (size_t)nhl);
     double *Hpl = carve<double>(base, off, 18 * (size_t)nblk);
@@ -1346,7 +1361,6 @@ void carve_state(char *base, size_t &off, const LbaHost &H, LbaDev *D, bool prof
     D->pointA = qA;
     D->pointB = qB;
     D->err = err;
-    D->J = J;
     D->Hll = Hll;
     D->bl = bl;
     D->Hpl = Hpl;

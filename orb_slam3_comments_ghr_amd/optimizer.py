@@ -235,11 +235,13 @@ def run_pose(fn, problems, handle=None):
     return rc, out
 
 
-def make_ba_result(G: BAGraph):
-    """(osg_ba_result, its output arrays): pose, point, edge_bad, edge_chi2."""
+def make_ba_result(G: BAGraph, chi2: bool = True):
+    """(osg_ba_result, its output arrays): pose, point, edge_bad, edge_chi2 (None unless `chi2`: the
+    per-edge chi2 is read only by the map-merge BA's level-1 marking; LocalMapping's LBA needs the
+    classification alone, and each requested array is another device-to-host copy)."""
     R = _abi.OsgBaResult()
     out = (np.zeros_like(G.pose), np.zeros_like(G.point), np.zeros(len(G.e_point), np.uint8),
-           np.zeros(len(G.e_point), np.float64))
+           np.zeros(len(G.e_point), np.float64) if chi2 else None)
     R.pose, R.point, R.edge_bad, R.edge_chi2 = (_p(a) for a in out)
     return R, out
 
@@ -267,7 +269,7 @@ class Optimizer:
 
     def LocalBundleAdjustment(self, G: BAGraph, stop_flag: np.ndarray | None = None) -> BAResult:
         lib, h = self.ctx.lib, self.ctx.handle
-        R, out = make_ba_result(G)
+        R, out = make_ba_result(G, chi2=False)
         gs = G.struct()
         if stop_flag is not None:
             assert stop_flag.dtype == np.uint8, "stop flag is one byte (bool *pbStopFlag)"
@@ -301,7 +303,7 @@ class Optimizer:
         (no reference counterpart; each graph follows the single-graph LM exactly)."""
         lib, h = self.ctx.lib, self.ctx.handle
         B = len(graphs)
-        made = [make_ba_result(G) for G in graphs]
+        made = [make_ba_result(G, chi2=False) for G in graphs]
         gs = (_abi.OsgBaGraph * B)(*[G.struct() for G in graphs])
         rs = (_abi.OsgBaResult * B)(*[m[0] for m in made])
         if stop_flag is not None:
