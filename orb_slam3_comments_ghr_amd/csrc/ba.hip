@@ -17,9 +17,11 @@
 //   k_pose_red    per pose: Hpp, b_p from its edges' pose Jacobians, recomputed in place (a
 //                 workgroup reduction; no per-edge contribution round trip through HBM)
 // Per LM trial:
-//   k_schur_point / k_schur_block   Dinv = (Hll + lambda I)^-1, BDinv = Hpl Dinv, coef
-//   k_schur_chunks / k_schur_pairs  S_ij = sum_p BDinv_ip Hpl_jp^T over fixed chunks, then the dense
-//                 reduced camera matrix Hpp + lambda I - S and b_schur (k_bschur)
+//   k_schur_point  per landmark: Dinv = (Hll + lambda I)^-1, Dinv b_l
+//   k_schur_rows   per row segment (pose i, 400 of its blocks): BD = Hpl Dinv staged in LDS, the
+//                 segment's chunks of S_ij = sum_p BD_ip Hpl_jp^T and its share of b_schur
+//   k_schur_pairs  per pose pair: chunk partials summed in chunk order -> the dense reduced camera
+//                 matrix Hpp + lambda I - S, and b_schur
 //   k_chol_col x ceil(n/32), k_chol_back   left-looking blocked Cholesky (FP64 MFMA tile updates),
 //                 forward solve fused, backward solve; past n = 384 (BundleAdjustment) right-looking:
 //                 k_chol_col + k_chol_trail per column block, then k_chol_back_large
@@ -83,9 +85,16 @@ struct LbaDev {
     const int32_t *pair_start;           // dense (i <= j) pairs
     const int32_t *pair_ab;              // 2 ints per contribution
     int nchunks;
-    const int32_t *chunk_start;          // contribution range of each chunk (chunks never span pairs)
+    const int32_t *chunk_start;          // contribution range of each chunk (chunks never span pairs
+                                         // or row segments)
     const int32_t *pair_chunk;           // per pair: first chunk (npairs + 1)
+    const int32_t *pair_rank;            // per contribution: rank of its first block in pose i's list
+    int n_rs;                            // row segments: RS consecutive blocks of one hessian pose
+    const int32_t *rs_pose, *rs_rank0;   // per row segment: pose, first rank
+    const int32_t *rs_chunk_start, *rs_chunk;  // chunks per row segment
+    const int32_t *hp_rs_start;          // row segments per hessian pose
     double *chunk_part;                  // 36 per chunk
+    double *bs_part;                     // 6 per row segment: sum of Hpl Dinv b_l
     // launch extents of this graph (grids are sized for the largest graph of the batch)
     int ge, gl, gu, nblk_red;
     double user_lambda;
@@ -97,7 +106,7 @@ struct LbaDev {
     double *chi2o;                       // per edge chi2 of the last computed error (classification)
     double *err;                         // 3 per edge
     double *Hll, *bl, *Hpl, *Hpp, *bp;
-    double *Dinv, *db, *BDinv, *coef;
+    double *Dinv, *db;
     double *Hs, *bs, *x;
     double *Linv;                        // inverses of the 32x32 diagonal blocks of L, row-major per block row
     double *part;                        // [0, NPART): chi of the trial, [NPART, 2NPART): scale,
@@ -361,80 +370,94 @@ __global__ __launch_bounds__(EB) void k_schur_point(const LbaDev *__restrict__ D
     for (int r = 0; r < 3; r++) D.db[3 * (size_t)l + r] = Di[3 * r] * b[0] + Di[3 * r + 1] * b[1] + Di[3 * r + 2] * b[2];
 }
 
-// per block: BDinv = Hpl Dinv, coef = Hpl Dinv b_l
-__global__ __launch_bounds__(EB) void k_schur_block(const LbaDev *__restrict__ Ds)
-{
-    LBA_GRAPH(M_ACT);
-    const int blk = blockIdx.x * EB + threadIdx.x;
-    if (blk >= D.nblk) return;
-    const int l = D.blk_lm[blk];
-    double Di[9], db[3], B[18];
-    for (int i = 0; i < 9; i++) Di[i] = D.Dinv[9 * (size_t)l + i];
-    for (int i = 0; i < 3; i++) db[i] = D.db[3 * (size_t)l + i];
-    for (int i = 0; i < 18; i++) B[i] = D.Hpl[18 * (size_t)blk + i];
-    double *BD = D.BDinv + 18 * (size_t)blk;
-    double *cf = D.coef + 6 * (size_t)blk;
-    for (int r = 0; r < 6; r++) {
-        for (int c = 0; c < 3; c++) BD[3 * r + c] = B[3 * r] * Di[c] + B[3 * r + 1] * Di[3 + c] + B[3 * r + 2] * Di[6 + c];
-        cf[r] = B[3 * r] * db[0] + B[3 * r + 1] * db[1] + B[3 * r + 2] * db[2];
-    }
-}
-
-// Schur accumulation S_ij = sum_p BDinv_ip Hpl_jp^T over the (block_i, block_j) contributions of
-// every pose pair (i <= j), in landmark order — the order of g2o's Schur loop
-// (ref:Thirdparty/g2o/g2o/core/block_solver.hpp:381-432).  Diagonal pairs carry ~10x the
-// contributions of off-diagonal ones, so the lists are cut into chunks of <= SCH contributions:
-//   k_schur_chunks  one wave per chunk, lane (r, c) < 36 owns S[r][c] (no cross-lane reduction),
-//                   8 contributions' loads in flight per step -> chunk partial;
-//   k_schur_pairs   one wave per pair: sums its chunk partials in chunk order (deterministic),
-//                   writes Hs = Hpp + lambda I - S (both triangles) and b_schur.
-constexpr int SCH = 64;
-// One wave per chunk.  Lane = (group g = lane >> 2, quarter q = lane & 3): group g takes
+// Schur accumulation S_ij = sum_p BD_ip Hpl_jp^T (BD = Hpl Dinv) over the (block_i, block_j)
+// contributions of every pose pair (i <= j), in landmark order — the order of g2o's Schur loop
+// (ref:Thirdparty/g2o/g2o/core/block_solver.hpp:381-432).  Row-staged: one workgroup per row segment
+// (hessian pose i, RS consecutive blocks of pose i in block order).  It forms BD_a = Hpl_a Dinv_l for
+// its blocks into LDS once — with the segment's share of b_schur, sum of Hpl_a (Dinv b_l) — and its
+// waves take the segment's chunks (<= SCH contributions of one pair (i, j >= i) whose first block is
+// in the segment): BD_a from LDS, Hpl_b from HBM.  A block's BD is formed once per trial instead of
+// written to HBM and gathered again per contribution (the contribution count is sum_l k_l(k_l+1)/2
+// against the block count sum_l k_l).
+//   Wave layout per chunk: lane = (group g = lane >> 2, quarter q = lane & 3); group g takes
 // contributions g, g + 16, ... of the chunk; quarter q owns rows 3 (q >> 1) .. + 2 and columns
-// 3 (q & 1) .. + 2 of the 6x6 product, so a lane loads 9 + 9 doubles for 27 FMAs (the former
-// 36-lane layout re-loaded every row six times).  The 16 groups are summed by a fixed xor
-// butterfly at the end of the chunk: deterministic.
-__global__ __launch_bounds__(256) void k_schur_chunks(const LbaDev *__restrict__ Ds)
+// 3 (q & 1) .. + 2 of the 6x6 product (9 + 9 doubles loaded for 27 FMAs).  The 16 groups are summed
+// by a fixed xor butterfly: deterministic.  k_schur_pairs then sums a pair's chunks in chunk order.
+constexpr int SCH = 64;
+constexpr int RS = 400;  // blocks per row segment: 400 x 18 doubles = 56 KiB of LDS
+constexpr int RT = 512;  // threads per row-segment workgroup
+__global__ __launch_bounds__(RT) void k_schur_rows(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT);
-    const int ch = (blockIdx.x * 256 + threadIdx.x) >> 6;
-    const int lane = threadIdx.x & 63;
-    if (ch >= D.nchunks) return;
+    const int rs = blockIdx.x;
+    if (rs >= D.n_rs) return;
+    __shared__ double s_bd[RS * 18];
+    __shared__ double s_cf[RT / 64][6];
+    const int i = D.rs_pose[rs], rb = D.rs_rank0[rs];
+    const int hb0 = D.hp_b_start[i];
+    const int nr = min(RS, D.hp_b_start[i + 1] - hb0 - rb);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    double cf[6] = {0, 0, 0, 0, 0, 0};
+    for (int r = threadIdx.x; r < nr; r += RT) {
+        const int a = D.hp_b[hb0 + rb + r];
+        const int l = D.blk_lm[a];
+        double Di[9], db[3], B[18];
+        for (int k = 0; k < 9; k++) Di[k] = D.Dinv[9 * (size_t)l + k];
+        for (int k = 0; k < 3; k++) db[k] = D.db[3 * (size_t)l + k];
+        for (int k = 0; k < 18; k++) B[k] = D.Hpl[18 * (size_t)a + k];
+        double *BD = s_bd + 18 * r;
+        for (int rr = 0; rr < 6; rr++) {
+            for (int c = 0; c < 3; c++)
+                BD[3 * rr + c] = B[3 * rr] * Di[c] + B[3 * rr + 1] * Di[3 + c] + B[3 * rr + 2] * Di[6 + c];
+            cf[rr] += B[3 * rr] * db[0] + B[3 * rr + 1] * db[1] + B[3 * rr + 2] * db[2];
+        }
+    }
+    for (int k = 0; k < 6; k++) cf[k] = wave_sum(cf[k]);
+    if (lane == 0)
+        for (int k = 0; k < 6; k++) s_cf[wv][k] = cf[k];
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        double t = 0.0;
+        for (int w = 0; w < RT / 64; w++) t += s_cf[w][threadIdx.x];
+        D.bs_part[6 * (size_t)rs + threadIdx.x] = t;
+    }
     const int g = lane >> 2, q = lane & 3;
     const int r0 = 3 * (q >> 1), c0 = 3 * (q & 1);
-    const double *__restrict__ BDv = D.BDinv;
     const double *__restrict__ Hv = D.Hpl;
-    const int *__restrict__ ab = D.pair_ab;
-    const int q0 = D.chunk_start[ch], q1 = D.chunk_start[ch + 1];
-    double acc[9];
+    for (int t = D.rs_chunk_start[rs] + wv; t < D.rs_chunk_start[rs + 1]; t += RT / 64) {
+        const int ch = D.rs_chunk[t];
+        const int q0 = D.chunk_start[ch], q1 = D.chunk_start[ch + 1];
+        double acc[9];
 #pragma unroll
-    for (int i = 0; i < 9; i++) acc[i] = 0.0;
-    for (int qq = q0 + g; qq < q1; qq += 16) {
-        const int2 p = *(const int2 *)(ab + 2 * qq);
-        const double *BD = BDv + 18 * (size_t)p.x + 3 * r0;  // rows r0..r0+2 of BDinv_i (6x3)
-        const double *Bj = Hv + 18 * (size_t)p.y + 3 * c0;   // rows c0..c0+2 of Hpl_j (6x3)
-        double a[9], b[9];
+        for (int k = 0; k < 9; k++) acc[k] = 0.0;
+        for (int qq = q0 + g; qq < q1; qq += 16) {
+            const int rank = D.pair_rank[qq] - rb;
+            const int b = D.pair_ab[2 * qq + 1];
+            const double *BD = s_bd + 18 * rank + 3 * r0;  // rows r0..r0+2 of BD_i (6x3)
+            const double *Bj = Hv + 18 * (size_t)b + 3 * c0;  // rows c0..c0+2 of Hpl_j (6x3)
+            double av[9], bv[9];
 #pragma unroll
-        for (int i = 0; i < 9; i++) {
-            a[i] = BD[i];
-            b[i] = Bj[i];
+            for (int k = 0; k < 9; k++) {
+                av[k] = BD[k];
+                bv[k] = Bj[k];
+            }
+#pragma unroll
+            for (int r = 0; r < 3; r++)
+#pragma unroll
+                for (int c = 0; c < 3; c++)
+                    acc[3 * r + c] += av[3 * r] * bv[3 * c] + av[3 * r + 1] * bv[3 * c + 1] + av[3 * r + 2] * bv[3 * c + 2];
         }
 #pragma unroll
-        for (int r = 0; r < 3; r++)
+        for (int off = 4; off < 64; off <<= 1)
 #pragma unroll
-            for (int c = 0; c < 3; c++)
-                acc[3 * r + c] += a[3 * r] * b[3 * c] + a[3 * r + 1] * b[3 * c + 1] + a[3 * r + 2] * b[3 * c + 2];
-    }
+            for (int k = 0; k < 9; k++) acc[k] += __shfl_xor(acc[k], off);
+        if (g == 0) {
+            double *out = D.chunk_part + 36 * (size_t)ch;
 #pragma unroll
-    for (int off = 4; off < 64; off <<= 1)
+            for (int r = 0; r < 3; r++)
 #pragma unroll
-        for (int i = 0; i < 9; i++) acc[i] += __shfl_xor(acc[i], off);
-    if (g == 0) {
-        double *out = D.chunk_part + 36 * (size_t)ch;
-#pragma unroll
-        for (int r = 0; r < 3; r++)
-#pragma unroll
-            for (int c = 0; c < 3; c++) out[6 * (r0 + r) + c0 + c] = acc[3 * r + c];
+                for (int c = 0; c < 3; c++) out[6 * (r0 + r) + c0 + c] = acc[3 * r + c];
+        }
     }
 }
 
@@ -464,29 +487,11 @@ __global__ __launch_bounds__(256) void k_schur_pairs(const LbaDev *__restrict__ 
         }
         D.Hs[(size_t)(6 * i + r) * n + 6 * j + c] = v;
         if (i != j) D.Hs[(size_t)(6 * j + c) * n + 6 * i + r] = v;
-    }
-}
-
-// b_schur_i = b_p,i - sum over pose i's blocks of Hpl Dinv b_l: one workgroup per pose
-__global__ __launch_bounds__(256) void k_bschur(const LbaDev *__restrict__ Ds)
-{
-    LBA_GRAPH(M_ACT);
-    const int i = blockIdx.x;
-    if (i >= D.nhp) return;
-    __shared__ double s[4][6];
-    double acc[6] = {0, 0, 0, 0, 0, 0};
-    for (int q = D.hp_b_start[i] + threadIdx.x; q < D.hp_b_start[i + 1]; q += 256) {
-        const double *cf = D.coef + 6 * (size_t)D.hp_b[q];
-        for (int k = 0; k < 6; k++) acc[k] += cf[k];
-    }
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int k = 0; k < 6; k++) acc[k] = wave_sum(acc[k]);
-    if (lane == 0)
-        for (int k = 0; k < 6; k++) s[w][k] = acc[k];
-    __syncthreads();
-    if (threadIdx.x < 6) {
-        const int k = threadIdx.x;
-        D.bs[6 * i + k] = D.bp[6 * (size_t)i + k] - (((s[0][k] + s[1][k]) + s[2][k]) + s[3][k]);
+    } else if (i == j && lane < 42) {  // b_schur_i = b_p,i - its row segments' sums, in segment order
+        const int k = lane - 36;
+        double t = 0.0;
+        for (int rs = D.hp_rs_start[i]; rs < D.hp_rs_start[i + 1]; rs++) t += D.bs_part[6 * (size_t)rs + k];
+        D.bs[6 * i + k] = D.bp[6 * (size_t)i + k] - t;
     }
 }
 
@@ -1131,7 +1136,9 @@ struct LbaHost {
     int ge = 0, gl = 0, gu = 0, nblk_red = 0;
     bool trivial = false;  // nothing to optimise: the estimates are returned unchanged
     std::vector<int32_t> pose_h, hp_pose, point_h, hl_point, lm_e_start, lm_e, lm_b_start, blk_pose, edge_blk, blk_lm,
-        blk_e_start, blk_e, hp_e_start, hp_e, hp_b_start, hp_b, pair_start, pair_ab, chunk_start, pair_chunk;
+        blk_e_start, blk_e, hp_e_start, hp_e, hp_b_start, hp_b, pair_start, pair_ab, chunk_start, pair_chunk,
+        pair_rank, rs_pose, rs_rank0, rs_chunk_start, rs_chunk, hp_rs_start;
+    int n_rs = 0;
     double t_struct = 0;
     // LM state (ref:Thirdparty/g2o/g2o/core/optimization_algorithm_levenberg.cpp:61-194 and
     // sparse_optimizer.cpp optimize())
@@ -1146,13 +1153,16 @@ struct LbaHost {
     {
         G = nullptr;
         R = nullptr;
-        np = npt = ne = nhp = nhl = nblk = npairs = nchunks = 0;
+        np = npt = ne = nhp = nhl = nblk = npairs = nchunks = n_rs = 0;
         ge = gl = gu = nblk_red = 0;
         trivial = false;
         hp_pose.clear();
         hl_point.clear();
         blk_pose.clear();
         chunk_start.clear();
+        rs_pose.clear();
+        rs_rank0.clear();
+        rs_chunk.clear();
         t_struct = 0;
         lambda = 0;
         ni = 2;
@@ -1293,15 +1303,51 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
                     H.pair_ab[2 * k + 1] = b;
                 }
     }
-    // chunks of <= SCH contributions, never spanning two pairs
-    H.pair_chunk.assign(npairs + 1, 0);
-    for (int k = 0; k < npairs; k++) {
-        H.pair_chunk[k] = (int)H.chunk_start.size();
-        for (int q = H.pair_start[k]; q < H.pair_start[k + 1]; q += SCH) H.chunk_start.push_back(q);
+    // rank of each block in its pose's block list (hp_b is in block order); row segments of RS ranks
+    std::vector<int32_t> blk_rank(nblk);
+    for (int i = 0; i < nhp; i++)
+        for (int q = H.hp_b_start[i]; q < H.hp_b_start[i + 1]; q++) blk_rank[H.hp_b[q]] = q - H.hp_b_start[i];
+    H.hp_rs_start.assign(nhp + 1, 0);
+    for (int i = 0; i < nhp; i++) {
+        const int nb = H.hp_b_start[i + 1] - H.hp_b_start[i];
+        H.hp_rs_start[i + 1] = H.hp_rs_start[i] + std::max(1, (nb + RS - 1) / RS);
+        for (int r = 0; r < std::max(1, (nb + RS - 1) / RS); r++) {
+            H.rs_pose.push_back(i);
+            H.rs_rank0.push_back(r * RS);
+        }
     }
+    H.n_rs = H.hp_rs_start[nhp];
+    const size_t ncontrib = (size_t)H.pair_start[npairs];
+    H.pair_rank.assign(std::max<size_t>(ncontrib, 1), 0);
+    for (size_t q = 0; q < ncontrib; q++) H.pair_rank[q] = blk_rank[H.pair_ab[2 * q]];
+    // chunks of <= SCH contributions, never spanning two pairs or two row segments; listed per row
+    // segment (pair order, then contribution order)
+    H.pair_chunk.assign(npairs + 1, 0);
+    std::vector<int32_t> chunk_rs;
+    for (int i = 0, k = 0; i < nhp; i++)
+        for (int j = i; j < nhp; j++, k++) {
+            H.pair_chunk[k] = (int)H.chunk_start.size();
+            int q = H.pair_start[k];
+            while (q < H.pair_start[k + 1]) {
+                const int seg = H.pair_rank[q] / RS;
+                int e = q + 1;
+                while (e < H.pair_start[k + 1] && e - q < SCH && H.pair_rank[e] / RS == seg) e++;
+                H.chunk_start.push_back(q);
+                chunk_rs.push_back(H.hp_rs_start[i] + seg);
+                q = e;
+            }
+        }
     H.pair_chunk[npairs] = (int)H.chunk_start.size();
     H.nchunks = (int)H.chunk_start.size();
     H.chunk_start.push_back(H.pair_start[npairs]);
+    H.rs_chunk_start.assign(H.n_rs + 1, 0);
+    for (int c = 0; c < H.nchunks; c++) H.rs_chunk_start[chunk_rs[c] + 1]++;
+    for (int r = 0; r < H.n_rs; r++) H.rs_chunk_start[r + 1] += H.rs_chunk_start[r];
+    H.rs_chunk.assign(std::max(H.nchunks, 1), 0);
+    {
+        std::vector<int32_t> fill(H.rs_chunk_start.begin(), H.rs_chunk_start.end() - 1);
+        for (int c = 0; c < H.nchunks; c++) H.rs_chunk[fill[chunk_rs[c]]++] = c;
+    }
     H.ge = (ne + EB - 1) / EB;
     H.gl = (nhl + EB - 1) / EB;
     H.gu = (std::max(std::max(nhl, np), npt) + EB - 1) / EB;
@@ -1342,8 +1388,7 @@ void carve_state(char *base, size_t &off, const LbaHost &H, LbaDev *D, bool prof
     double *Hpp = carve<double>(base, off, 36 * (size_t)nhp);
     double *bp = carve<double>(base, off, 6 * (size_t)nhp);
     double *Dinv = carve<double>(base, off, 9 * (size_t)nhl);
-    double *BDinv = carve<double>(base, off, 18 * (size_t)nblk);
-    double *coef = carve<double>(base, off, 6 * (size_t)nblk);
+    double *bs_part = carve<double>(base, off, 6 * (size_t)std::max(H.n_rs, 1));
     double *Hs = carve<double>(base, off, (size_t)sp * sp);
     double *bs = carve<double>(base, off, (size_t)sp);
     double *x = carve<double>(base, off, (size_t)sp + 3 * (size_t)nhl);
@@ -1367,8 +1412,7 @@ void carve_state(char *base, size_t &off, const LbaHost &H, LbaDev *D, bool prof
     D->Hpp = Hpp;
     D->bp = bp;
     D->Dinv = Dinv;
-    D->BDinv = BDinv;
-    D->coef = coef;
+    D->bs_part = bs_part;
     D->Hs = Hs;
     D->bs = bs;
     D->x = x;
@@ -1452,7 +1496,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     osg_packer pk;
     struct InOff {
         size_t fixed, epose, epoint, ecam, ekind, eobs, eisig, cams, poseh, hppose, pointh, hlpoint, lmes, lme, lmbs,
-            blkpose, eblk, hpes, hpe, hpbs, hpb, pairs, pairab, chs, blklm, blkes, blke, pch, pose0, point0, erob;
+            blkpose, eblk, hpes, hpe, hpbs, hpb, pairs, pairab, chs, blklm, blkes, blke, pch, pose0, point0, erob,
+            prank, rspose, rsrank0, rscs, rsc, hprs;
     };
     std::vector<InOff> io(NA);
     for (int a = 0; a < NA; a++) {
@@ -1489,6 +1534,12 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         o.blkes = pk.add(h.blk_e_start.data(), 4 * (size_t)(nblk + 1));
         o.blke = pk.add(h.blk_e.data(), 4 * h.blk_e.size());
         o.pch = pk.add(h.pair_chunk.data(), 4 * h.pair_chunk.size());
+        o.prank = pk.add(h.pair_rank.data(), 4 * h.pair_rank.size());
+        o.rspose = pk.add(h.rs_pose.data(), 4 * h.rs_pose.size());
+        o.rsrank0 = pk.add(h.rs_rank0.data(), 4 * h.rs_rank0.size());
+        o.rscs = pk.add(h.rs_chunk_start.data(), 4 * h.rs_chunk_start.size());
+        o.rsc = pk.add(h.rs_chunk.data(), 4 * h.rs_chunk.size());
+        o.hprs = pk.add(h.hp_rs_start.data(), 4 * h.hp_rs_start.size());
         o.pose0 = pk.add(G->pose, 56 * (size_t)np);
         o.point0 = pk.add(G->point, 24 * (size_t)npt);
     }
@@ -1518,7 +1569,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     LbaCtl *d_ctl = (LbaCtl *)(dsm + dev_bytes);
     double *d_out = (double *)(dsm + dev_bytes + ctl_bytes);
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(din, pin, pk.total, hipMemcpyHostToDevice, ctx->stream));
-    int mx_ge = 0, mx_gl = 1, mx_gu = 0, mx_nblk = 0, mx_nhp = 0, mx_chunks = 0, mx_pairs = 0, mx_red = 0;
+    int mx_ge = 0, mx_gl = 1, mx_gu = 0, mx_nblk = 0, mx_nhp = 0, mx_chunks = 0, mx_pairs = 0, mx_red = 0, mx_rs = 0;
     bool large = false;  // some graph's reduced system is past CMAX
     for (int a = 0; a < NA; a++) {
         const LbaHost &h = H[act[a]];
@@ -1566,6 +1617,13 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         D.blk_e_start = osg_dptr<int32_t>(din, o.blkes);
         D.blk_e = osg_dptr<int32_t>(din, o.blke);
         D.pair_chunk = osg_dptr<int32_t>(din, o.pch);
+        D.pair_rank = osg_dptr<int32_t>(din, o.prank);
+        D.n_rs = h.n_rs;
+        D.rs_pose = osg_dptr<int32_t>(din, o.rspose);
+        D.rs_rank0 = osg_dptr<int32_t>(din, o.rsrank0);
+        D.rs_chunk_start = osg_dptr<int32_t>(din, o.rscs);
+        D.rs_chunk = osg_dptr<int32_t>(din, o.rsc);
+        D.hp_rs_start = osg_dptr<int32_t>(din, o.hprs);
         D.ge = h.ge;
         D.gl = h.gl;
         D.gu = h.gu;
@@ -1583,6 +1641,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         mx_nblk = std::max(mx_nblk, h.nblk);
         mx_nhp = std::max(mx_nhp, h.nhp);
         mx_chunks = std::max(mx_chunks, h.nchunks);
+        mx_rs = std::max(mx_rs, h.n_rs);
         mx_pairs = std::max(mx_pairs, h.npairs);
         mx_red = std::max(mx_red, h.nblk_red);
     }
@@ -1600,11 +1659,9 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         if (mx_nhp > 0) hipLaunchKernelGGL(k_pose_red, gx(mx_nhp), dim3(EB), 0, ctx->stream, d_dev);
         hipLaunchKernelGGL(k_lambda_init, yb, dim3(64), 0, ctx->stream, d_dev);
         hipLaunchKernelGGL(k_schur_point, gx(mx_gl), dim3(EB), 0, ctx->stream, d_dev);
-        if (mx_nblk > 0) hipLaunchKernelGGL(k_schur_block, gx((mx_nblk + EB - 1) / EB), dim3(EB), 0, ctx->stream, d_dev);
         if (mx_nhp > 0) {
-            if (mx_chunks > 0) hipLaunchKernelGGL(k_schur_chunks, gx((mx_chunks * 64 + 255) / 256), dim3(256), 0, ctx->stream, d_dev);
+            hipLaunchKernelGGL(k_schur_rows, gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
             hipLaunchKernelGGL(k_schur_pairs, gx((mx_pairs * 64 + 255) / 256), dim3(256), 0, ctx->stream, d_dev);
-            hipLaunchKernelGGL(k_bschur, gx(mx_nhp), dim3(256), 0, ctx->stream, d_dev);
             for (int jb = 0; jb < mx_red; jb++) {  // row blocks at and below the diagonal block
                 hipLaunchKernelGGL(k_chol_col, gx(mx_red - jb), dim3(256), 0, ctx->stream, d_dev, jb);
                 const int m = mx_red - jb - 1;
