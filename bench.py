@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--ba-reps", type=int, default=20)
     ap.add_argument("--ba-batch", type=int, default=64, help="C4 windows per GPU per lockstep batch")
     ap.add_argument("--ba-batch-reps", type=int, default=3)
+    ap.add_argument("--ba-threads", type=int, default=4,
+                    help="host threads per GPU driving LBA batches, each with its own context and HIP stream")
     ap.add_argument("--no-frames", action="store_true", help="skip the frame-batched C3 / C5 workloads")
     ap.add_argument("--frames", type=int, default=1024, help="frames per launch (C3 / C5 batches)")
     ap.add_argument("--frame-reps", type=int, default=5)
@@ -378,35 +380,87 @@ def bench_lba(ctx, rank, world, dist, dev, args):
     single = {"value": round(iters / el, 1), "unit": "LM iterations/s", "ms_per_lba": round(el / reps * 1e3, 3),
               "iterations_per_lba": r.iterations, "trials_per_lba": r.trials,
               "note": "one window per call (the drop-in's latency)"}
-    # batched: B independent C4 windows per GPU in lockstep (roofline on B = 64 graphs/GPU)
+    # batched: B independent C4 windows per GPU in lockstep (roofline on B = 64 graphs/GPU),
+    # driven by T host threads, each with its own context (own HIP stream): one thread's structure
+    # build and packing overlap the others' device steps, and their kernels share the GPU
+    import threading
     B = args.ba_batch
+    T = max(1, args.ba_threads)
     pool = [G] + [op.synth_lba_graph(rng, n_kf=50, n_points=10000) for _ in range(7)]
     graphs = [pool[i % len(pool)] for i in range(B)]
-    opt.LocalBundleAdjustmentBatch(graphs)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    biters = 0
+    ctxs = [ctx] + [type(ctx)(ctx.device) for _ in range(T - 1)]
+    opts = [opt] + [op.Optimizer(c) for c in ctxs[1:]]
     brep = max(1, args.ba_batch_reps)
-    for _ in range(brep):
-        rr = opt.LocalBundleAdjustmentBatch(graphs)
-        biters += sum(x.iterations for x in rr)
-    torch.cuda.synchronize(dev)
-    bel = time.perf_counter() - t0
-    bel, biters = job_totals(bel, biters, world, dist if world > 1 else None, dev)
+
+    def timed(nthr):
+        for o in opts[:nthr]:
+            o.LocalBundleAdjustmentBatch(graphs)
+        for c in ctxs[:nthr]:
+            c.synchronize()
+        its = [0] * nthr
+
+        def run(t):
+            for _ in range(brep):
+                its[t] += sum(x.iterations for x in opts[t].LocalBundleAdjustmentBatch(graphs))
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        th = [threading.Thread(target=run, args=(t,)) for t in range(nthr)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        torch.cuda.synchronize(dev)
+        return job_totals(time.perf_counter() - t0, sum(its), world, dist if world > 1 else None, dev)
+    bel1, biters1 = timed(1)
+    bel, biters = timed(T) if T > 1 else (bel1, biters1)
+    for c in ctxs[1:]:
+        c.close()
     bval = biters / bel
+    # per-kernel device time of one batch (HIP events around every launch group, a separate untimed
+    # pass): the dominant kernel's roofline
+    op.lba_kernel_times(ctx, True)
+    opt.LocalBundleAdjustmentBatch(graphs)
+    kt = op.lba_kernel_times(ctx, False)
+    steps = max(1, kt["schur_rows"][1])
+    counts = [op.lba_structure_counts(g) for g in graphs]
+    contrib = sum(c["contributions"] for c in counts)
+    blocks = sum(c["blocks"] for c in counts)
+    lms = sum(c["landmarks"] for c in counts)
+    # k_schur_rows per launch: S_ij products (36 x 3 FMA per contribution), BD = Hpl Dinv and the
+    # b_schur share per block (18 x 3 + 6 x 3 FMA); bytes: Hpl, Dinv and Dinv b_l read once, 12 B of
+    # (rank, block) per contribution, one 6x6 chunk partial per 64 contributions written
+    sr_flop = 2.0 * (contrib * 108 + blocks * 72)
+    sr_bytes = blocks * 144 + lms * 96 + contrib * 12 + (contrib / 64.0) * 288
+    sr_s = kt["schur_rows"][0] / 1e3 / steps
+    kernels = {k: round(v[0] / max(1, v[1]), 4) for k, v in kt.items() if v[1]}
+    dom = max(kernels, key=kernels.get)
+    pmc = _load_json(os.path.join(ROOT, "profiles", "r02_schur_pmc.json"))
+    pmc_sr = next((v for k, v in pmc.items() if k.startswith("k_schur_rows<false>")), {})
     flop_iter = 72.6e6
     res = {
         "metric": "LocalBA iters/s", "value": round(bval, 1), "unit": "LM iterations/s",
         "workload": f"C4: {len(G.pose)} KF x {len(G.point)} points x {len(G.e_point)} mono edges, optimize(10); "
-                    f"{B} independent windows per GPU in lockstep (8 distinct), {brep} batches per rank",
-        "ms_per_batch": round(bel / brep * 1e3, 3), "windows_per_batch": B, "n_gpus": world, "dtype": "f64",
+                    f"{B} independent windows per lockstep batch (8 distinct), {T} host threads per GPU each "
+                    f"driving {brep} batches on its own context / HIP stream",
+        "ms_per_round": round(bel / brep * 1e3, 3), "windows_per_batch": B, "host_threads": T,
+        "windows_in_flight": B * T, "one_thread": {"value": round(biters1 / bel1, 1),
+                                                   "ms_per_batch": round(bel1 / brep * 1e3, 3)},
+        "n_gpus": world, "dtype": "f64",
         "scaling": "weak", "parallelism": f"replicas x{world} (independent windows per GPU)",
         "flop_per_iter_survey_formula": flop_iter,
-        "roofline": {"bound": "fp64", "achieved": round(bval * flop_iter / 1e12, 4), "peak": 78.6,
-                     "unit": "TFLOP/s", "frac": round(bval * flop_iter / 1e12 / 78.6, 5),
-                     "note": "whole LBA wall time (host structure build + upload + LM), SURVEY F_iter"},
+        "roofline": {"kernel": "k_schur_rows (Schur product S_ij -= sum BD_i Hpl_j^T on v_mfma_f64_4x4x4f64)",
+                     "dominant_kernel": dom, "bound": "mfma", "achieved": round(sr_flop / sr_s / 1e12, 4),
+                     "peak": 78.6, "unit": "TFLOP/s", "frac": round(sr_flop / sr_s / 1e12 / 78.6, 5),
+                     "kernel_us": round(sr_s * 1e6, 2), "windows_per_launch": B,
+                     "algorithmic_flop_per_launch": sr_flop, "algorithmic_bytes_per_launch": round(sr_bytes),
+                     "hbm_GBps_if_priced_as_hbm": round(sr_bytes / sr_s / 1e9, 1),
+                     "mfma_busy_frac_pmc": pmc_sr.get("mfma_busy_frac"),
+                     "traffic": pmc_sr.get("hbm_bytes_per_launch"),
+                     "pmc_source": "profiles/r02_schur_pmc.json" if pmc else None},
+        "kernel_ms_per_step": kernels,
+        "whole_call_fp64_frac": round(bval * flop_iter / 1e12 / 78.6, 5),
         "single_window": single,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -479,6 +533,14 @@ def _oracle():
         from tests import oracle_calls
         _ORACLE.append((oracle_calls.load(), oracle_calls))
     return _ORACLE[0]
+
+
+def _load_json(path):
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
 
 
 def _pose_result(P):

@@ -132,6 +132,15 @@ int osg_bundle_adjustment(struct osg_ctx *ctx, const osg_ba_graph *g, osg_ba_res
 int osg_local_bundle_adjustment_batch(struct osg_ctx *ctx, const osg_ba_graph *graphs, int32_t n_graphs,
                                       osg_ba_result *results, const volatile uint8_t *stop_flag);
 
+/* Diagnostics: per-kernel device time of the LBA / BA engine.  enable = 1 starts timing every
+ * kernel of every lockstep step with HIP events on the context's stream (and clears the sums);
+ * 0 stops.  ms[OSG_LBA_NK] and steps[OSG_LBA_NK] (either may be NULL) receive the summed time and
+ * the number of timed launch groups since the last enable, indexed errors, linearize, pose_red,
+ * lambda_init, schur_point, schur_rows, schur_pairs, chol (every k_chol_col + k_chol_trail of a
+ * step), chol_back, update, step_reduce, classify. */
+#define OSG_LBA_NK 12
+int osg_lba_kernel_times(struct osg_ctx *ctx, int32_t enable, double *ms, int64_t *steps);
+
 #ifdef __cplusplus
 }
 #endif

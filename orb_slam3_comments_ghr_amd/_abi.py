@@ -182,6 +182,7 @@ EXPORTS = [
     "osg_search_by_projection_kf_batch", "osg_search_by_bow_kf_f_batch", "osg_search_by_bow_kf_kf_batch",
     "osg_match_last_stats", "osg_ctx_last_kernel_ms", "osg_pose_optimization", "osg_pose_optimization_batch",
     "osg_local_bundle_adjustment", "osg_local_bundle_adjustment_batch", "osg_bundle_adjustment",
+    "osg_lba_kernel_times",
     "osg_vocabulary_create", "osg_vocabulary_load_text", "osg_vocabulary_destroy", "osg_vocabulary_info",
     "osg_vocabulary_transform", "osg_vocabulary_transform_batch",
     "osg_fuse_search", "osg_fuse_search_batch", "osg_search_for_triangulation", "osg_search_for_triangulation_batch",
@@ -238,6 +239,7 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.osg_bundle_adjustment.argtypes = [vp, C.POINTER(OsgBaGraph), C.POINTER(OsgBaResult),
                                                 vp]
     lib.osg_local_bundle_adjustment_batch.argtypes = [vp, vp, i32, vp, vp]
+    lib.osg_lba_kernel_times.argtypes = [vp, i32, vp, vp]
     lib.osg_vocabulary_create.argtypes = [vp, C.POINTER(OsgVocabularyDesc), C.POINTER(vp)]
     lib.osg_vocabulary_load_text.argtypes = [vp, C.c_char_p, C.POINTER(vp)]
     lib.osg_vocabulary_destroy.argtypes = [vp]

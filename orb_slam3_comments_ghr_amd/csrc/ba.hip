@@ -18,8 +18,10 @@
 //                 workgroup reduction; no per-edge contribution round trip through HBM)
 // Per LM trial:
 //   k_schur_point  per landmark: Dinv = (Hll + lambda I)^-1, Dinv b_l
-//   k_schur_rows   per row segment (pose i, 400 of its blocks): BD = Hpl Dinv staged in LDS, the
-//                 segment's chunks of S_ij = sum_p BD_ip Hpl_jp^T and its share of b_schur
+//   k_schur_rows   per row segment (pose i, 200 of its blocks): BD = Hpl Dinv staged in LDS, the
+//                 segment's chunks of S_ij = sum_p BD_ip Hpl_jp^T on FP64 MFMA (v_mfma_f64_4x4x4f64,
+//                 one contribution per instruction; OSG_SCHUR_VALU=1: the VALU form) and its share
+//                 of b_schur
 //   k_schur_pairs  per pose pair: chunk partials summed in chunk order -> the dense reduced camera
 //                 matrix Hpp + lambda I - S, and b_schur
 //   k_chol_col x ceil(n/32), k_chol_back   left-looking blocked Cholesky (FP64 MFMA tile updates),
@@ -47,6 +49,16 @@ using namespace osgba;
 namespace {
 
 constexpr int EB = 256;      // edge-parallel kernels
+
+// LbaDev's arrays are generic pointers; the hot gathers read them as global (address space 1) so
+// they issue global_load (counted by vmcnt alone) instead of flat loads, whose lgkmcnt share makes
+// every wait on an LDS read also wait for the outstanding HBM loads
+#define GLOBAL __attribute__((address_space(1)))
+template <class T>
+__device__ inline const GLOBAL T *gbl(const T *p)
+{
+    return (const GLOBAL T *)p;
+}
 constexpr int NPART = 1024;  // max chi2 / scale partials
 
 // Per-graph control of one lockstep step (host → device each step; k_lambda_init may set lambda).
@@ -379,14 +391,17 @@ __global__ __launch_bounds__(EB) void k_schur_point(const LbaDev *__restrict__ D
 // in the segment): BD_a from LDS, Hpl_b from HBM.  A block's BD is formed once per trial instead of
 // written to HBM and gathered again per contribution (the contribution count is sum_l k_l(k_l+1)/2
 // against the block count sum_l k_l).
-//   Wave layout per chunk: lane = (group g = lane >> 2, quarter q = lane & 3); group g takes
-// contributions g, g + 16, ... of the chunk; quarter q owns rows 3 (q >> 1) .. + 2 and columns
-// 3 (q & 1) .. + 2 of the 6x6 product (9 + 9 doubles loaded for 27 FMAs).  The 16 groups are summed
-// by a fixed xor butterfly: deterministic.  k_schur_pairs then sums a pair's chunks in chunk order.
+//   The product runs on FP64 MFMA by default (layout below, at the chunk loop).  The VALU form
+// (OSG_SCHUR_VALU=1, kept for A/B measurements: DESIGN.md §3.4) uses lane = (group g = lane >> 2,
+// quarter q = lane & 3); group g takes contributions g, g + 16, ... of the chunk; quarter q owns
+// rows 3 (q >> 1) .. + 2 and columns 3 (q & 1) .. + 2 of the 6x6 product (9 + 9 doubles loaded for
+// 27 FMAs), the 16 groups summed by a fixed xor butterfly.  Both are deterministic; k_schur_pairs
+// then sums a pair's chunks in chunk order.
 constexpr int SCH = 64;
-constexpr int RS = 400;  // blocks per row segment: 400 x 18 doubles = 56 KiB of LDS
+constexpr int RS = 200;  // blocks per row segment: 200 x 18 doubles = 28 KiB of LDS
 constexpr int RT = 512;  // threads per row-segment workgroup
-__global__ __launch_bounds__(RT) void k_schur_rows(const LbaDev *__restrict__ Ds)
+template <bool VALU>
+__global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT);
     const int rs = blockIdx.x;
@@ -399,12 +414,12 @@ __global__ __launch_bounds__(RT) void k_schur_rows(const LbaDev *__restrict__ Ds
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     double cf[6] = {0, 0, 0, 0, 0, 0};
     for (int r = threadIdx.x; r < nr; r += RT) {
-        const int a = D.hp_b[hb0 + rb + r];
-        const int l = D.blk_lm[a];
+        const int a = gbl(D.hp_b)[hb0 + rb + r];
+        const int l = gbl(D.blk_lm)[a];
         double Di[9], db[3], B[18];
-        for (int k = 0; k < 9; k++) Di[k] = D.Dinv[9 * (size_t)l + k];
-        for (int k = 0; k < 3; k++) db[k] = D.db[3 * (size_t)l + k];
-        for (int k = 0; k < 18; k++) B[k] = D.Hpl[18 * (size_t)a + k];
+        for (int k = 0; k < 9; k++) Di[k] = gbl(D.Dinv)[9 * (size_t)l + k];
+        for (int k = 0; k < 3; k++) db[k] = gbl(D.db)[3 * (size_t)l + k];
+        for (int k = 0; k < 18; k++) B[k] = gbl(D.Hpl)[18 * (size_t)a + k];
         double *BD = s_bd + 18 * r;
         for (int rr = 0; rr < 6; rr++) {
             for (int c = 0; c < 3; c++)
@@ -421,43 +436,131 @@ __global__ __launch_bounds__(RT) void k_schur_rows(const LbaDev *__restrict__ Ds
         for (int w = 0; w < RT / 64; w++) t += s_cf[w][threadIdx.x];
         D.bs_part[6 * (size_t)rs + threadIdx.x] = t;
     }
-    const int g = lane >> 2, q = lane & 3;
-    const int r0 = 3 * (q >> 1), c0 = 3 * (q & 1);
-    const double *__restrict__ Hv = D.Hpl;
-    for (int t = D.rs_chunk_start[rs] + wv; t < D.rs_chunk_start[rs + 1]; t += RT / 64) {
-        const int ch = D.rs_chunk[t];
-        const int q0 = D.chunk_start[ch], q1 = D.chunk_start[ch + 1];
-        double acc[9];
+    if (VALU) {
+        const int g = lane >> 2, q = lane & 3;
+        const int r0 = 3 * (q >> 1), c0 = 3 * (q & 1);
+        const double *__restrict__ Hv = D.Hpl;
+        for (int t = D.rs_chunk_start[rs] + wv; t < D.rs_chunk_start[rs + 1]; t += RT / 64) {
+            const int ch = D.rs_chunk[t];
+            const int q0 = D.chunk_start[ch], q1 = D.chunk_start[ch + 1];
+            double acc[9];
 #pragma unroll
-        for (int k = 0; k < 9; k++) acc[k] = 0.0;
-        for (int qq = q0 + g; qq < q1; qq += 16) {
-            const int rank = D.pair_rank[qq] - rb;
-            const int b = D.pair_ab[2 * qq + 1];
-            const double *BD = s_bd + 18 * rank + 3 * r0;  // rows r0..r0+2 of BD_i (6x3)
-            const double *Bj = Hv + 18 * (size_t)b + 3 * c0;  // rows c0..c0+2 of Hpl_j (6x3)
-            double av[9], bv[9];
+            for (int k = 0; k < 9; k++) acc[k] = 0.0;
+            for (int qq = q0 + g; qq < q1; qq += 16) {
+                const int rank = D.pair_rank[qq] - rb;
+                const int b = D.pair_ab[2 * qq + 1];
+                const double *BD = s_bd + 18 * rank + 3 * r0;  // rows r0..r0+2 of BD_i (6x3)
+                const double *Bj = Hv + 18 * (size_t)b + 3 * c0;  // rows c0..c0+2 of Hpl_j (6x3)
+                double av[9], bv[9];
 #pragma unroll
-            for (int k = 0; k < 9; k++) {
-                av[k] = BD[k];
-                bv[k] = Bj[k];
+                for (int k = 0; k < 9; k++) {
+                    av[k] = BD[k];
+                    bv[k] = Bj[k];
+                }
+#pragma unroll
+                for (int r = 0; r < 3; r++)
+#pragma unroll
+                    for (int c = 0; c < 3; c++)
+                        acc[3 * r + c] += av[3 * r] * bv[3 * c] + av[3 * r + 1] * bv[3 * c + 1] + av[3 * r + 2] * bv[3 * c + 2];
             }
 #pragma unroll
-            for (int r = 0; r < 3; r++)
+            for (int off = 4; off < 64; off <<= 1)
 #pragma unroll
-                for (int c = 0; c < 3; c++)
-                    acc[3 * r + c] += av[3 * r] * bv[3 * c] + av[3 * r + 1] * bv[3 * c + 1] + av[3 * r + 2] * bv[3 * c + 2];
+                for (int k = 0; k < 9; k++) acc[k] += __shfl_xor(acc[k], off);
+            if (g == 0) {
+                double *out = D.chunk_part + 36 * (size_t)ch;
+#pragma unroll
+                for (int r = 0; r < 3; r++)
+#pragma unroll
+                    for (int c = 0; c < 3; c++) out[6 * (r0 + r) + c0 + c] = acc[3 * r + c];
+            }
         }
+        return;
+    }
+    // FP64 MFMA (v_mfma_f64_4x4x4f64: four independent 4x4x4 blocks per wave instruction).  A
+    // chunk's S_ij = sum_p BD_p Hpl_p^T is the GEMM (6 x 3P)(3P x 6); one instruction takes one
+    // contribution (K = its 3 landmark dimensions, padded to 4) for the whole 6x6 product: block
+    // beta = (rb, cb) covers rows 4 rb .. 4 rb + 3 and columns 4 cb .. 4 cb + 3 (rows / columns 6, 7
+    // padded).  Operand layout on gfx950 (tools/micro/mfma_f64.hip, profiles/r02_mfma_f64.txt):
+    //   A(beta, row i, k) in lane 16 k + 4 beta + i,  B(beta, k, col j) in lane 16 k + 4 beta + j,
+    //   D(beta, row i, col j) in lane 16 i + 4 beta + j.
+    // Contributions accumulate in chunk order (= landmark order) through two alternating
+    // accumulators, summed once at the end: deterministic.
+    const int kk = lane >> 4, beta = (lane >> 2) & 3, ri = lane & 3;
+    const int arow = 4 * (beta >> 1) + ri, bcol = 4 * (beta & 1) + ri;
+    const bool aok = kk < 3 && arow < 6, bok = kk < 3 && bcol < 6;
+    const int aoff = aok ? 3 * arow + kk : 0, boff = bok ? 3 * bcol + kk : 0;
+    // a padded lane reads element 0 of the same block and multiplies it by 0 (a non-finite block
+    // poisons S through its real lanes anyway), so every load is unconditional
+    const double amask = aok ? 1.0 : 0.0, bmask = bok ? 1.0 : 0.0;
+    const int orow = 4 * (beta >> 1) + kk, ocol = 4 * (beta & 1) + ri;  // D: i = lane >> 4
+    const GLOBAL double *__restrict__ Hv = gbl(D.Hpl);
+    // Hpl_j blocks are staged per wave through LDS, 16 contributions at a time: 144 16-byte granules
+    // read by 64 lanes with 3 dwordx4 loads (one gather instruction per 5 contributions instead of
+    // one per contribution), the next group's loads in flight while this group's MFMAs run
+    constexpr int GC = 16;
+    __shared__ __attribute__((aligned(16))) double s_hb[RT / 64][GC * 18];
+    double *hb = s_hb[wv];
+    const int t1 = D.rs_chunk_start[rs + 1];
+    int t = D.rs_chunk_start[rs] + wv;
+    int ch = 0, q0 = 0, nq = 0, my_rank = 0, my_b = 0;
+    auto fetch = [&](int tt, int &c, int &qs, int &n, int &mr, int &mb) {
+        c = tt < t1 ? gbl(D.rs_chunk)[tt] : 0;
+        qs = tt < t1 ? gbl(D.chunk_start)[c] : 0;
+        n = tt < t1 ? gbl(D.chunk_start)[c + 1] - qs : 0;  // <= SCH = 64
+        mr = lane < n ? gbl(D.pair_rank)[qs + lane] - rb : 0;
+        mb = lane < n ? gbl(D.pair_ab)[2 * (qs + lane) + 1] : 0;
+    };
+    // granules of group u0 (contributions u0 .. u0 + cnt - 1) into registers
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    auto load_group = [&](int u0, int cnt, int mb, u4 (&R)[3]) {
 #pragma unroll
-        for (int off = 4; off < 64; off <<= 1)
-#pragma unroll
-            for (int k = 0; k < 9; k++) acc[k] += __shfl_xor(acc[k], off);
-        if (g == 0) {
-            double *out = D.chunk_part + 36 * (size_t)ch;
-#pragma unroll
-            for (int r = 0; r < 3; r++)
-#pragma unroll
-                for (int c = 0; c < 3; c++) out[6 * (r0 + r) + c0 + c] = acc[3 * r + c];
+        for (int r = 0; r < 3; r++) {
+            const int idx = lane + 64 * r;
+            const int c = idx / 9, gq = idx - 9 * c;
+            const int bj = __shfl(mb, (u0 + c) & 63);
+            if (idx < GC * 9 && c < cnt) R[r] = *(const GLOBAL u4 *)(Hv + 18 * (size_t)bj + 2 * gq);
         }
+    };
+    fetch(t, ch, q0, nq, my_rank, my_b);
+    u4 R[3];
+    load_group(0, nq, my_b, R);
+    for (; t < t1; t += RT / 64) {
+        int nch, nq0, nnq, nrank, nb;
+        fetch(t + RT / 64, nch, nq0, nnq, nrank, nb);
+        double acc0 = 0.0, acc1 = 0.0;
+        for (int u = 0; u < nq; u += GC) {
+            const int cnt = min(GC, nq - u);
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+                const int idx = lane + 64 * r;
+                if (idx < GC * 9 && idx < 9 * cnt) *(u4 *)(hb + 2 * idx) = R[r];
+            }
+            __builtin_amdgcn_wave_barrier();
+            // next group: the rest of this chunk, else the first group of the next chunk
+            if (u + GC < nq) load_group(u + GC, nq - u - GC, my_b, R);
+            else load_group(0, nnq, nb, R);
+#pragma unroll
+            for (int v = 0; v < GC; v += 2) {
+                if (v < cnt) {
+                    const int rank = __builtin_amdgcn_readlane(my_rank, u + v);
+                    acc0 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[18 * rank + aoff] * amask, hb[18 * v + boff] * bmask,
+                                                              acc0, 0, 0, 0);
+                }
+                if (v + 1 < cnt) {
+                    const int rank = __builtin_amdgcn_readlane(my_rank, u + v + 1);
+                    acc1 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[18 * rank + aoff] * amask,
+                                                              hb[18 * (v + 1) + boff] * bmask, acc1, 0, 0, 0);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (orow < 6 && ocol < 6) D.chunk_part[36 * (size_t)ch + 6 * orow + ocol] = acc0 + acc1;
+        ch = nch;
+        q0 = nq0;
+        nq = nnq;
+        my_rank = nrank;
+        my_b = nb;
     }
 }
 
@@ -1176,7 +1279,15 @@ struct LbaHost {
 
 struct LbaCache {
     std::vector<LbaHost> H;
+    std::vector<hipEvent_t> kev;  // osg_lba_kernel_times marks
+    std::vector<int> kcls;
+    ~LbaCache()
+    {
+        for (hipEvent_t e : kev) (void)hipEventDestroy(e);
+    }
 };
+enum { KT_ERR, KT_LIN, KT_POSE, KT_LINIT, KT_SPOINT, KT_SROWS, KT_SPAIRS, KT_CHOL, KT_BACK, KT_UPD, KT_RED, KT_CLASS, KT_END };
+static_assert(KT_END == OSG_LBA_NK, "osg_lba_kernel_times slots");
 
 int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
 {
@@ -1432,6 +1543,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     OSG_REQUIRE(ctx, B >= 0 && (B == 0 || (graphs && results)), "batch arguments");
     static const int prof_level = getenv("OSG_LBA_PROFILE") ? atoi(getenv("OSG_LBA_PROFILE")) : 0;
     const bool prof = prof_level > 0, prof_ts = prof_level >= 2 && B == 1;
+    // OSG_SCHUR_VALU=1: the VALU Schur product (A/B measurements); default FP64 MFMA
+    static const bool schur_valu = getenv("OSG_SCHUR_VALU") && atoi(getenv("OSG_SCHUR_VALU")) != 0;
     const auto tp0 = std::chrono::steady_clock::now();
     auto ms_since = [&](std::chrono::steady_clock::time_point t) {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
@@ -1457,7 +1570,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     }
     // ---- structures (host threads for a batch; each graph is independent)
     if (!ctx->lba_cache) ctx->lba_cache = std::make_shared<LbaCache>();
-    std::vector<LbaHost> &H = static_cast<LbaCache *>(ctx->lba_cache.get())->H;
+    LbaCache &cache = *static_cast<LbaCache *>(ctx->lba_cache.get());
+    std::vector<LbaHost> &H = cache.H;
     if ((int)H.size() < B) H.resize(B);
     for (int b = 0; b < B; b++) H[b].reset();
     std::vector<int> rcs(B, OSG_OK);
@@ -1649,35 +1763,80 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     const double t_upload = ms_since(tp0) - t_struct;
     const auto tp1 = std::chrono::steady_clock::now();
 
+    // osg_lba_kernel_times: an event before each launch group and one after the last; after the
+    // step's sync, the time between two marks goes to the group that starts at the first
+    int nmark = 0;
+    auto mark = [&](int cls) -> int {
+        if (!ctx->lba_ktime) return OSG_OK;
+        if (nmark == (int)cache.kev.size()) {
+            hipEvent_t e;
+            OSG_HIP_CHECK(ctx, hipEventCreate(&e));
+            cache.kev.push_back(e);
+            cache.kcls.push_back(0);
+        }
+        OSG_HIP_CHECK(ctx, hipEventRecord(cache.kev[nmark], ctx->stream));
+        cache.kcls[nmark++] = cls;
+        return OSG_OK;
+    };
+    auto collect = [&]() -> int {  // after a stream sync
+        for (int m = 0; m + 1 < nmark; m++) {
+            float ms = 0.f;
+            OSG_HIP_CHECK(ctx, hipEventElapsedTime(&ms, cache.kev[m], cache.kev[m + 1]));
+            ctx->lba_kms[cache.kcls[m]] += ms;
+            ctx->lba_kn[cache.kcls[m]]++;
+        }
+        nmark = 0;
+        return OSG_OK;
+    };
+#define LBA_MARK(cls)                  \
+    do {                               \
+        const int _rc = mark(cls);     \
+        if (_rc < 0) return _rc;       \
+    } while (0)
+
     // one lockstep step: every kernel once for all graphs, then 5 scalars per graph back
     auto run_step = [&]() -> int {
         OSG_HIP_CHECK(ctx, hipMemcpyAsync(d_ctl, h_ctl, ctl_bytes, hipMemcpyHostToDevice, ctx->stream));
         const dim3 yb(1, NA);
         auto gx = [&](int n) { return dim3(std::max(n, 1), NA); };
+        LBA_MARK(KT_ERR);
         hipLaunchKernelGGL(k_errors, gx(mx_ge), dim3(EB), 0, ctx->stream, d_dev, 1);
+        LBA_MARK(KT_LIN);
         hipLaunchKernelGGL(k_linearize, gx(mx_gl), dim3(EB), 0, ctx->stream, d_dev);
+        LBA_MARK(KT_POSE);
         if (mx_nhp > 0) hipLaunchKernelGGL(k_pose_red, gx(mx_nhp), dim3(EB), 0, ctx->stream, d_dev);
+        LBA_MARK(KT_LINIT);
         hipLaunchKernelGGL(k_lambda_init, yb, dim3(64), 0, ctx->stream, d_dev);
+        LBA_MARK(KT_SPOINT);
         hipLaunchKernelGGL(k_schur_point, gx(mx_gl), dim3(EB), 0, ctx->stream, d_dev);
         if (mx_nhp > 0) {
-            hipLaunchKernelGGL(k_schur_rows, gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
+            LBA_MARK(KT_SROWS);
+            if (schur_valu) hipLaunchKernelGGL(k_schur_rows<true>, gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
+            else hipLaunchKernelGGL(k_schur_rows<false>, gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
+            LBA_MARK(KT_SPAIRS);
             hipLaunchKernelGGL(k_schur_pairs, gx((mx_pairs * 64 + 255) / 256), dim3(256), 0, ctx->stream, d_dev);
+            LBA_MARK(KT_CHOL);
             for (int jb = 0; jb < mx_red; jb++) {  // row blocks at and below the diagonal block
                 hipLaunchKernelGGL(k_chol_col, gx(mx_red - jb), dim3(256), 0, ctx->stream, d_dev, jb);
                 const int m = mx_red - jb - 1;
                 if (large && m > 0)
                     hipLaunchKernelGGL(k_chol_trail, gx(m * (m + 1) / 2), dim3(256), 0, ctx->stream, d_dev, jb);
             }
+            LBA_MARK(KT_BACK);
             hipLaunchKernelGGL(k_chol_back, yb, dim3(1024), 0, ctx->stream, d_dev);
             if (large) hipLaunchKernelGGL(k_chol_back_large, yb, dim3(1024), 0, ctx->stream, d_dev);
         }
+        LBA_MARK(KT_UPD);
         hipLaunchKernelGGL(k_update, gx(mx_gu), dim3(EB), 0, ctx->stream, d_dev);
+        LBA_MARK(KT_ERR);
         hipLaunchKernelGGL(k_errors, gx(mx_ge), dim3(EB), 0, ctx->stream, d_dev, 0);
+        LBA_MARK(KT_RED);
         hipLaunchKernelGGL(k_step_reduce, yb, dim3(256), 0, ctx->stream, d_dev);
+        LBA_MARK(KT_END);
         OSG_HIP_CHECK(ctx, hipGetLastError());
         OSG_HIP_CHECK(ctx, hipMemcpyAsync(h_out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
         OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
-        return OSG_OK;
+        return collect();
     };
 
     // initial chi2 (activeRobustChi2 before optimising): a step with only M_ERRC
@@ -1798,7 +1957,10 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     // exactly as the reference's computeActiveErrors order leaves them); estimates out
     for (int a = 0; a < NA; a++) h_ctl[a] = LbaCtl{M_FIN, H[act[a]].sel, 0.0};
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(d_ctl, h_ctl, ctl_bytes, hipMemcpyHostToDevice, ctx->stream));
+    LBA_MARK(KT_CLASS);
     hipLaunchKernelGGL(k_classify, dim3(std::max(mx_ge, 1), NA), dim3(EB), 0, ctx->stream, d_dev);
+    LBA_MARK(KT_END);
+#undef LBA_MARK
     OSG_HIP_CHECK(ctx, hipGetLastError());
     int total_iters = 0;
     for (int a = 0; a < NA; a++) {
@@ -1819,6 +1981,10 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
             OSG_HIP_CHECK(ctx, hipMemcpyAsync(R->edge_chi2, D.chi2o, 8 * (size_t)h.ne, hipMemcpyDeviceToHost, ctx->stream));
     }
     OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    {
+        const int rc = collect();
+        if (rc < 0) return rc;
+    }
     if (prof)
         fprintf(stderr, "[osg lba] %d graphs: structure %.3f ms (graph 0: %.3f ms), pack+upload %.3f ms, LM %.3f ms "
                         "(%d lockstep steps), classify+download %.3f ms, total %.3f ms\n",
@@ -1837,6 +2003,22 @@ extern "C" int osg_local_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, 
 extern "C" int osg_bundle_adjustment(osg_ctx *ctx, const osg_ba_graph *G, osg_ba_result *R, const volatile uint8_t *stop)
 {  // Optimizer::BundleAdjustment: the same LM over the whole map (the caller's Huber fields)
     return lba_batch(ctx, G, R, 1, stop);
+}
+
+extern "C" int osg_lba_kernel_times(osg_ctx *ctx, int32_t enable, double *ms, int64_t *steps)
+{
+    if (!ctx) return OSG_E_INVALID;
+    for (int k = 0; k < OSG_LBA_NK; k++) {
+        if (ms) ms[k] = ctx->lba_kms[k];
+        if (steps) steps[k] = ctx->lba_kn[k];
+    }
+    if (enable && !ctx->lba_ktime)
+        for (int k = 0; k < OSG_LBA_NK; k++) {
+            ctx->lba_kms[k] = 0;
+            ctx->lba_kn[k] = 0;
+        }
+    ctx->lba_ktime = enable != 0;
+    return OSG_OK;
 }
 
 extern "C" int osg_local_bundle_adjustment_batch(osg_ctx *ctx, const osg_ba_graph *graphs, int32_t n_graphs,

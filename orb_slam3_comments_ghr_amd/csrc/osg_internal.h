@@ -38,6 +38,9 @@ struct osg_ctx {
     double last_kernel_ms = 0;    // last k_match / k_pose_opt launch time (HIP events)
     hipEvent_t ev[2] = {};        // timing events (osg_ctx_events)
     std::shared_ptr<void> lba_cache;  // host structures of the last LBA batch, reused (ba.hip)
+    bool lba_ktime = false;           // osg_lba_kernel_times: per-kernel HIP-event timing of LBA steps
+    double lba_kms[OSG_LBA_NK] = {};
+    int64_t lba_kn[OSG_LBA_NK] = {};
     std::string last_error;
 };
 

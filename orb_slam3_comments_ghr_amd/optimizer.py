@@ -314,6 +314,32 @@ class Optimizer:
         return [finish_ba_result(R, m[1]) for m, R in zip(made, rs)]
 
 
+LBA_KERNELS = ["errors", "linearize", "pose_red", "lambda_init", "schur_point", "schur_rows", "schur_pairs",
+               "chol", "chol_back", "update", "step_reduce", "classify"]
+
+
+def lba_kernel_times(ctx, enable: bool) -> dict:
+    """osg_lba_kernel_times: per-kernel device time (HIP events) of the LBA engine since the last
+    enable, as {kernel: (ms, launch groups)}; enable=True (re)starts the timing, False stops it."""
+    ms = np.zeros(len(LBA_KERNELS), np.float64)
+    n = np.zeros(len(LBA_KERNELS), np.int64)
+    ctx.check(ctx.lib.osg_lba_kernel_times(ctx.handle, int(enable), _p(ms), _p(n)), "lba_kernel_times")
+    return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(LBA_KERNELS)}
+
+
+def lba_structure_counts(G: "BAGraph") -> dict:
+    """Sizes of the BlockSolver structure of a graph (ba.hip build_structure): free poses with an
+    edge, landmarks, (landmark, free pose) blocks, and Schur contributions sum_l k_l (k_l + 1) / 2
+    (k_l = free poses observing landmark l)."""
+    fixed = np.asarray(G.pose_fixed).astype(bool)
+    ep, et = np.asarray(G.e_pose), np.asarray(G.e_point)
+    free = ~fixed[ep]
+    blocks = np.unique(et[free].astype(np.int64) * (len(G.pose) + 1) + ep[free])
+    k = np.bincount((blocks // (len(G.pose) + 1)).astype(np.int64), minlength=len(G.point))
+    return {"free_poses": int(len(np.unique(ep[free]))), "landmarks": int(len(np.unique(et))),
+            "blocks": int(len(blocks)), "contributions": int((k * (k + 1) // 2).sum())}
+
+
 # ----------------------------------------------------------------------------- generators
 def kb8_project(cam, Xc):
     """KannalaBrandt8::project (ref:src/CameraModels/KannalaBrandt8.cpp:76-99) in float64."""

@@ -57,7 +57,22 @@ def main():
     def bow():
         lib.osg_search_by_bow_kf_f(h, C.byref(a), C.byref(b), 0.7, 1, o.ctypes.data)
 
-    for name, fn in [("mps", mps), ("last", last), ("bow", bow)]:
+    # the bench's C5 latency problem (bench_c5: 32 frames, then their LastF and local-map queries)
+    rngb = np.random.default_rng(0x0B5EED10)
+    FP = [fr.synth_frame_two_cam(rngb, n_left=1000, n_right=1000, stereo_frac=0.5, width=512, height=512)
+          for _ in range(32)]
+    [fr.synth_last_queries_two_cam(rngb, f, n_last=2000) for f in FP]
+    QP = [fr.synth_mp_queries_two_cam(rngb, f, m=1500) for f in FP]
+    SP = [fr.synth_slots(rngb, f.n, frac_assigned=0.05) for f in FP]
+    fsb, qsb = FP[0].struct(), QP[0].struct()
+    slb, tkb = SP[0][0].copy(), np.ascontiguousarray(SP[0][1], np.uint8)
+
+    def mps_bench():
+        np.copyto(slb, SP[0][0])
+        lib.osg_search_by_projection_mps(h, C.byref(fsb), C.byref(qsb), 0.9, 3.0, 0, 20.0, slb.ctypes.data,
+                                         tkb.ctypes.data)
+
+    for name, fn in [("mps", mps), ("mps_bench", mps_bench), ("last", last), ("bow", bow)]:
         w = med(fn)
         fn()
         out[name] = {"wall_us": round(w, 1), "kernel_us": round(ctx.last_kernel_ms() * 1e3, 1),
