@@ -481,6 +481,22 @@ int osg_orb_describe(osg_ctx *ctx, const osg_image_pyramid *raw, const osg_image
                      const osg_orb_keypoints *K, const int32_t *pattern, const int32_t *umax, int32_t compute_angle,
                      float *angle, uint8_t *desc);
 
+/* ---- b9: ORBextractor::ComputeKeyPointsOctTree --------------------------------------------------
+ * ref:src/ORBextractor.cc:1065-1198 with DistributeOctTree (:716-1050), ExtractorNode::DivideNode
+ * (:607-654) and compareNodes (:656-676): per level, W = 35 cells over [EDGE_THRESHOLD - 3,
+ * size - EDGE_THRESHOLD + 3), each cell FAST'd as its own image (rowRange / colRange) with
+ * ini_th_fast and, when that finds nothing, min_th_fast (cv::FAST with non-maximum suppression:
+ * OpenCV's FAST_t<16> / cornerScore<16>, restated; not in the reference tree, so parity with OpenCV
+ * itself is unpinned), then the quadtree distribution down to n_features_per_level[level]
+ * (mnFeaturesPerLevel) keypoints.  Out, level by level in the reference's allKeypoints order:
+ * x, y in level coordinates (after the :1190-1196 shift by the border), response (the FAST score),
+ * size = (int)(PATCH_SIZE * scale_factors[level]) (mvScaleFactor); level_start[n_levels + 1].
+ * Orientation and descriptors follow through osg_orb_describe.  Returns the keypoint count, or
+ * OSG_E_INVALID when it exceeds `capacity` or a level is smaller than one cell. */
+int osg_orb_detect(osg_ctx *ctx, const osg_image_pyramid *raw, int32_t ini_th_fast, int32_t min_th_fast,
+                   const int32_t *n_features_per_level, const float *scale_factors, int32_t capacity,
+                   float *x, float *y, float *response, float *size, int32_t *level_start);
+
 /* Diagnostics of the last search call on this context (summed / maxed over a batch): out[0]
  * candidates enumerated, out[1] Jacobi rounds, out[2] problems whose greedy was redone serially (a5 on a two-camera rig when a
  * stereo-partner write by a MapPoint without observations unblocked a slot), out[3] nmatches.

@@ -68,6 +68,16 @@ int oracle_orb_describe(const osg_image_pyramid *raw, const osg_image_pyramid *b
 void oracle_dbow_transform_batch(const osg_vocabulary_desc *V, const uint8_t *desc, const int32_t *n, int B,
                                  int levelsup, osg_bow_out *out);
 
+/* ORBextractor::ComputeKeyPointsOctTree (oracle_orbdetect.cc): cv::FAST(threshold, nonmax) on one
+ * image (keypoints row-major, response = score); the cell loop + DistributeOctTree over a pyramid,
+ * keypoints level by level in the reference's order (level coordinates, size = (int)(31 * scale)).
+ * Both return the keypoint count, or -1 when it exceeds cap. */
+int oracle_fast(const uint8_t *img, int rows, int cols, int step, int threshold, int cap, float *x, float *y,
+                float *response);
+int oracle_orb_detect(const osg_image_pyramid *P, int ini_th, int min_th, const int32_t *n_features,
+                      const float *scale_factors, int cap, float *x, float *y, float *response, float *size,
+                      int32_t *level_start);
+
 /* bundle adjustment (oracle_ba.c) */
 double oracle_ref_pow3(double t);  /* the reference's libm calls, correctly rounded */
 double oracle_ref_sin(double x);

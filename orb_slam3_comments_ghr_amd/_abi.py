@@ -189,7 +189,7 @@ EXPORTS = [
     "osg_compute_distinctive_descriptors", "osg_compute_distinctive_descriptors_dev",
     "osg_search_by_projection_sim3", "osg_search_by_projection_sim3_batch", "osg_search_by_sim3",
     "osg_search_for_initialization", "osg_search_for_initialization_batch",
-    "osg_compute_stereo_matches", "osg_compute_stereo_matches_batch", "osg_orb_describe",
+    "osg_compute_stereo_matches", "osg_compute_stereo_matches_batch", "osg_orb_describe", "osg_orb_detect",
 ]
 
 
@@ -206,6 +206,7 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.osg_strerror.restype = C.c_char_p
     lib.osg_ctx_last_error.argtypes = [vp]
     lib.osg_ctx_last_error.restype = C.c_char_p
+    lib.osg_version.argtypes = []
     lib.osg_version.restype = C.c_char_p
     lib.osg_descriptor_distance.argtypes = [vp, vp]
     lib.osg_descriptor_distance_pairs.argtypes = [vp, vp, vp, i32, vp]
@@ -260,6 +261,7 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.osg_search_for_initialization_batch.argtypes = [vp, vp, vp, i32, vp, C.c_int, f32, C.c_int, vp, vp]
     lib.osg_compute_stereo_matches.argtypes = [vp, C.POINTER(OsgStereoFrame), vp, vp]
     lib.osg_compute_stereo_matches_batch.argtypes = [vp, vp, i32, vp, vp, vp]
+    lib.osg_orb_detect.argtypes = [vp, C.POINTER(OsgImagePyramid), i32, i32, vp, vp, i32, vp, vp, vp, vp, vp]
     lib.osg_orb_describe.argtypes = [vp, C.POINTER(OsgImagePyramid), C.POINTER(OsgImagePyramid),
                                      C.POINTER(OsgOrbKeypoints), vp, vp, i32, vp, vp]
     lib.osg_compute_distinctive_descriptors.argtypes = [vp, vp, vp, i32, vp]

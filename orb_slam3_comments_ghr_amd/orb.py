@@ -4,6 +4,13 @@ computeDescriptors / computeOrbDescriptor (ref:src/ORBextractor.cc:148-208, 1534
 levels (ref:src/ORBextractor.cc:1628-1652).  FAST, the octree distribution and the Gaussian blur stay
 with OpenCV; the caller passes the extractor's ``umax`` and ``pattern``.
 
+ComputeKeyPointsOctTree (``osg_orb_detect``, include/osg.h b9): FAST per W = 35 cell with
+iniThFAST / minThFAST and DistributeOctTree down to mnFeaturesPerLevel (ref:src/ORBextractor.cc:
+716-1198):
+
+    x, y, response, size, level_start = ORBDetect(ctx, raw, features_per_level(1000, 8, 1.2),
+                                                  scale_factors(8, 1.2))
+
     angle, desc, n_out = ORBDescribe(ctx, raw, blurred, x, y, level, pattern, umax)     # IC_Angle + rBRIEF
     _, desc, n_out = ORBDescribe(ctx, None, blurred, x, y, level, pattern, angle=angle) # given angles
 
@@ -82,6 +89,79 @@ def ORBDescribe(ctx: Context, raw, blurred, x, y, level, pattern, umax=None, ang
                                        umax.ctypes.data if compute else None, int(compute), ang.ctypes.data,
                                        desc.ctypes.data), "osg_orb_describe")
     return ang, desc, n_out
+
+
+def scale_factors(n_levels: int = 8, factor: float = 1.2) -> np.ndarray:
+    """mvScaleFactor as the ORBextractor constructor builds it (ref:src/ORBextractor.cc:484-491):
+    float products of scaleFactor."""
+    s = [np.float32(1.0)]
+    for _ in range(1, n_levels):
+        s.append(np.float32(s[-1] * np.float32(factor)))
+    return np.array(s, np.float32)
+
+
+def features_per_level(nfeatures: int = 1000, n_levels: int = 8, factor: float = 1.2) -> np.ndarray:
+    """mnFeaturesPerLevel (ref:src/ORBextractor.cc:505-528): a geometric share per level in float,
+    cvRound'ed, the last level taking the rest."""
+    f = np.float32(1.0) / np.float32(factor)
+    d = np.float32(np.float32(nfeatures * (np.float32(1) - f)) /
+                   (np.float32(1) - np.float32(math.pow(float(f), float(n_levels)))))
+    out, total = [], 0
+    for _ in range(n_levels - 1):
+        n = int(np.rint(d))
+        out.append(n)
+        total += n
+        d = np.float32(d * f)
+    out.append(max(nfeatures - total, 0))
+    return np.array(out, np.int32)
+
+
+def ORBDetect(ctx: Context, raw, n_features, scales, ini_th: int = 20, min_th: int = 7, capacity: int | None = None):
+    """ORBextractor::ComputeKeyPointsOctTree on the GPU (FAST scores and per-cell suppression) and the
+    host (DistributeOctTree).  raw: ImagePyramid or a list of levels (mvImagePyramid); n_features:
+    mnFeaturesPerLevel; scales: mvScaleFactor.  Returns (x, y, response, size, level_start) with the
+    keypoints of level l at [level_start[l], level_start[l + 1]) in the reference's order, in level
+    coordinates."""
+    if not isinstance(raw, ImagePyramid):
+        raw = ImagePyramid(raw)
+    L = len(raw.levels)
+    n_features = np.ascontiguousarray(n_features, np.int32)
+    scales = np.ascontiguousarray(scales, np.float32)
+    assert n_features.size >= L and scales.size >= L
+    cap = int(capacity if capacity is not None else max(int(n_features[:L].sum()) * 2 + 16, 64))
+    x, y, resp, size = (np.zeros(cap, np.float32) for _ in range(4))
+    ls = np.zeros(L + 1, np.int32)
+    rs = raw.struct()
+    n = ctx.check(ctx.lib.osg_orb_detect(ctx.handle, C.byref(rs), int(ini_th), int(min_th), n_features.ctypes.data,
+                                         scales.ctypes.data, cap, x.ctypes.data, y.ctypes.data, resp.ctypes.data,
+                                         size.ctypes.data, ls.ctypes.data), "osg_orb_detect")
+    return x[:n], y[:n], resp[:n], size[:n], ls
+
+
+def synth_fast_pyramid(rng, width=752, height=480, n_levels=8, factor=1.2, n_blobs=400):
+    """A synthetic image pyramid with FAST corners: a smooth random background plus bright and dark
+    rectangles and discs (corners and blobs at every scale), each level a box-filtered 2x2 resample
+    of the base image at size cvRound(size / scale) (ComputePyramid's shape,
+    ref:src/ORBextractor.cc:1692-1745; cv::resize itself is OpenCV's)."""
+    img = rng.normal(128, 6, (height, width)).astype(np.float32)
+    for _ in range(n_blobs):
+        cx, cy = rng.integers(0, width), rng.integers(0, height)
+        r = int(rng.integers(2, 14))
+        val = float(rng.choice([30.0, 70.0, 190.0, 235.0]))
+        if rng.random() < 0.5:
+            img[max(0, cy - r):cy + r, max(0, cx - r):cx + r] = val
+        else:
+            yy, xx = np.ogrid[:height, :width]
+            img[(yy - cy) ** 2 + (xx - cx) ** 2 <= r * r] = val
+    base = np.clip(img + rng.normal(0, 3, img.shape), 0, 255).astype(np.uint8)
+    levels = [base]
+    sc = scale_factors(n_levels, factor)
+    for l in range(1, n_levels):
+        w, h = int(np.rint(np.float32(width) / sc[l])), int(np.rint(np.float32(height) / sc[l]))
+        ys = np.minimum((np.arange(h) * sc[l]).astype(np.int64), height - 1)
+        xs = np.minimum((np.arange(w) * sc[l]).astype(np.int64), width - 1)
+        levels.append(np.ascontiguousarray(base[np.ix_(ys, xs)]))
+    return levels
 
 
 def synth_orb_frame(rng, n=1200, width=752, height=480, n_levels=8, factor=1.2, fractional=False,

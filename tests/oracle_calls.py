@@ -80,6 +80,9 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.oracle_fast_atan2.argtypes = [C.c_float, C.c_float]
     lib.oracle_orb_describe.argtypes = [C.POINTER(OsgImagePyramid), C.POINTER(OsgImagePyramid),
                                         C.POINTER(OsgOrbKeypoints), vp, vp, C.c_int, vp, vp]
+    lib.oracle_fast.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp]
+    lib.oracle_orb_detect.argtypes = [C.POINTER(OsgImagePyramid), C.c_int, C.c_int, vp, vp, C.c_int, vp, vp, vp,
+                                      vp, vp]
     return lib
 
 
@@ -246,3 +249,28 @@ def orb_describe(oracle, raw, blurred, x, y, level, pattern, umax=None, angle=No
     bad = oracle.oracle_orb_describe(C.byref(rs), C.byref(bs), C.byref(K), pattern.ctypes.data, umax.ctypes.data,
                                      int(compute), ang.ctypes.data, desc.ctypes.data)
     return ang, desc, bad
+
+
+def fast(oracle, img, threshold, cap=100000):
+    """cv::FAST(img, threshold, nonmax = true) through the oracle: (x, y, response)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    x, y, r = (np.zeros(cap, np.float32) for _ in range(3))
+    n = oracle.oracle_fast(img.ctypes.data, img.shape[0], img.shape[1], img.strides[0], int(threshold), cap,
+                           x.ctypes.data, y.ctypes.data, r.ctypes.data)
+    assert n >= 0
+    return x[:n], y[:n], r[:n]
+
+
+def orb_detect(oracle, levels, n_features, scales, ini_th=20, min_th=7, cap=200000):
+    """ORBextractor::ComputeKeyPointsOctTree through the oracle: (x, y, response, size, level_start)."""
+    from orb_slam3_comments_ghr_amd.stereo import ImagePyramid
+    P = levels if isinstance(levels, ImagePyramid) else ImagePyramid(levels)
+    ps = P.struct()
+    nf = np.ascontiguousarray(n_features, np.int32)
+    sc = np.ascontiguousarray(scales, np.float32)
+    x, y, r, s = (np.zeros(cap, np.float32) for _ in range(4))
+    ls = np.zeros(len(P.levels) + 1, np.int32)
+    n = oracle.oracle_orb_detect(C.byref(ps), int(ini_th), int(min_th), nf.ctypes.data, sc.ctypes.data, cap,
+                                 x.ctypes.data, y.ctypes.data, r.ctypes.data, s.ctypes.data, ls.ctypes.data)
+    assert n >= 0
+    return x[:n], y[:n], r[:n], s[:n], ls

@@ -30,6 +30,13 @@ def test_library_exports_every_symbol():
         assert hasattr(lib, s), s
 
 
+def test_every_symbol_has_argtypes():
+    # pointers through an undeclared ctypes call would be truncated to C int
+    lib = load_library()
+    missing = [s for s in _abi.EXPORTS if getattr(lib, s).argtypes is None]
+    assert not missing, missing
+
+
 def test_host_only_entry_points():
     lib = load_library()
     assert b"gfx950" in lib.osg_version()
