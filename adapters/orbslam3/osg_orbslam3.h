@@ -824,6 +824,47 @@ int orb_describe(const std::vector<MatT> &pyramid, const std::vector<MatT> &blur
     return outside;
 }
 
+// ------------------------------------------------- b9 ORBextractor::ComputeKeyPointsOctTree
+// ref:src/ORBextractor.cc:1065-1198 over the extractor's members (mvImagePyramid, mnFeaturesPerLevel,
+// mvScaleFactor, iniThFAST, minThFAST): FAST per cell + DistributeOctTree on the GPU path, then the
+// :1190-1196 loop's fields (pt in level coordinates, octave, size).  KeyPoint::angle stays FAST's -1:
+// computeOrientation runs with the descriptors in orb_describe (IC_Angle reads the raw level only,
+// so the angles are the same as the reference's :1200-1204 pass).
+template <class MatT, class KeyPointT>
+int compute_keypoints_oct_tree(const std::vector<MatT> &pyramid, std::vector<std::vector<KeyPointT>> &allKeypoints,
+                               const std::vector<int> &nFeaturesPerLevel, const std::vector<float> &scaleFactors,
+                               int iniThFAST, int minThFAST)
+{
+    osg_ctx *ctx = thread_ctx();
+    const int levels = (int)pyramid.size();
+    if ((int)nFeaturesPerLevel.size() < levels || (int)scaleFactors.size() < levels)
+        throw Error(OSG_E_INVALID, "compute_keypoints_oct_tree: per-level tables");
+    PyramidView<MatT> raw(pyramid, levels);
+    std::vector<int32_t> nf(nFeaturesPerLevel.begin(), nFeaturesPerLevel.begin() + levels);
+    int cap = 64;
+    for (int l = 0; l < levels; l++) cap += 2 * std::max(nf[l], 0) + 8;  // the octree stops within 3 of N
+    std::vector<float> x(cap), y(cap), resp(cap), size(cap);
+    std::vector<int32_t> ls(levels + 1);
+    check(ctx, osg_orb_detect(ctx, &raw.v, iniThFAST, minThFAST, nf.data(), scaleFactors.data(), cap, x.data(),
+                              y.data(), resp.data(), size.data(), ls.data()),
+          "osg_orb_detect");
+    allKeypoints.assign(levels, {});
+    for (int l = 0; l < levels; l++) {
+        allKeypoints[l].reserve(ls[l + 1] - ls[l]);
+        for (int i = ls[l]; i < ls[l + 1]; i++) {
+            KeyPointT kp;
+            kp.pt.x = x[i];
+            kp.pt.y = y[i];
+            kp.size = size[i];
+            kp.angle = -1.f;
+            kp.response = resp[i];
+            kp.octave = l;
+            allKeypoints[l].push_back(kp);
+        }
+    }
+    return ls[levels];
+}
+
 // ----------------------------------------------------------------- b3 SearchForTriangulation
 // ref:src/ORBmatcher.cc:1045-1328.  vMatchedPairs = (KF1 index, KF2 index) in ascending KF1 index.
 // The epipole and the F12 matrices come from the hook (the reference's Sophus / Eigen code).

@@ -285,6 +285,7 @@ def main():
         out["frames_dbow"] = bench_dbow(ctx, rank, world, dist, dev, args)
         out["frames_stereo"] = bench_stereo(ctx, rank, world, dist, dev, args)
         out["frames_orb"] = bench_orb(ctx, rank, world, dist, dev, args)
+        out["frames_orb_detect"] = bench_orb_detect(ctx, rank, world, dist, dev, args)
 
     # ---- LocalBA iters/s on C4 (50 KF x 10k points), the second half of the metric ----------
     if not args.no_ba:
@@ -817,6 +818,67 @@ def bench_orb(ctx, rank, world, dist, dev, args):
         _attach_cpu(res, cpu, 1, "frames/s", args.cpu_seconds * 0.4, "IC_Angle + computeOrbDescriptor",
                     wall_key="wall_frames_per_s_incl_host_roundtrip")
     return res
+
+
+def bench_orb_detect(ctx, rank, world, dist, dev, args):
+    """SURVEY.md §8(f) rank 4 (ORBextractor::ComputeKeyPointsOctTree): FAST per 35-px cell (iniThFAST 20,
+    minThFAST 7) and DistributeOctTree down to mnFeaturesPerLevel (1000 features, 8 levels x 1.2) for one
+    EuRoC-shaped 752 x 480 frame per call, the pyramid resident in HBM (seeded synthetic images with
+    corners at every scale).  value = frames per wall second of the whole call (GPU FAST + per-cell
+    suppression, keypoint download, host octree); the kernels' device time is beside it."""
+    import torch
+    from orb_slam3_comments_ghr_amd import orb
+    n_pool = 4
+    rng = np.random.default_rng(0x0B5EED31 + rank)
+    pool = [orb.synth_fast_pyramid(rng) for _ in range(n_pool)]
+    nf, sc = orb.features_per_level(1000, 8, 1.2), orb.scale_factors(8, 1.2)
+    dpool = [orb.ImagePyramid(f).to_device(dev) for f in pool]
+    for f in dpool:
+        orb.ORBDetect(ctx, f, nf, sc)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    reps = max(args.frame_reps, 1) * 50
+    k_ms, nk = 0.0, 0
+    t0 = time.perf_counter()
+    for i in range(reps):
+        nk += len(orb.ORBDetect(ctx, dpool[i % n_pool], nf, sc)[0])
+        k_ms += ctx.last_kernel_ms()
+    wall = time.perf_counter() - t0
+    w_s, tot = job_totals(wall, reps, world, dist if world > 1 else None, dev)
+    res = {"metric": "frames/s", "value": round(tot / w_s, 1), "unit": "frames/s",
+           "workload": "ORBextractor::ComputeKeyPointsOctTree: EuRoC-shaped 752x480, 8 levels x 1.2, 1000 features, "
+                       "FAST 20 / 7 per 35 px cell + DistributeOctTree; pyramid in HBM, 1 frame per call",
+           "keypoints_per_frame": round(nk / reps, 1),
+           "kernel_us_per_frame": round(k_ms * 1e3 / reps, 2),
+           "note": "value is the whole call (k_fast_score + k_fast_cells + scan, keypoint download, host octree)",
+           "n_gpus": world, "scaling": "weak", "parallelism": f"replicas x{world}"}
+    if rank == 0 and world == 1 and not args.no_cpu:
+        _attach_cpu(res, _orb_detect_worker(pool, nf, sc), 1, "frames/s", args.cpu_seconds * 0.4,
+                    "ComputeKeyPointsOctTree (FAST cells + DistributeOctTree)", wall_key="")
+    return res
+
+
+def _orb_detect_worker(pool, nf, sc):
+    """cpu_baseline worker for ComputeKeyPointsOctTree: one pool pyramid per call through the oracle."""
+    n_pool = len(pool)
+
+    def cpu(tid):
+        import ctypes as C
+        from orb_slam3_comments_ghr_amd.stereo import ImagePyramid
+        oracle, _ = _oracle()
+        cap = 8192
+        items = []
+        for f in pool:
+            P = ImagePyramid(f)
+            ps = P.struct()
+            outs = [np.zeros(cap, np.float32) for _ in range(4)] + [np.zeros(len(f) + 1, np.int32)]
+            items.append(((C.byref(ps), 20, 7, nf.ctypes.data, sc.ctypes.data, cap) +
+                          tuple(o.ctypes.data for o in outs), (P, ps, outs)))
+        keep = (nf, sc, items)
+        fn = oracle.oracle_orb_detect
+        return lambda i, keep=keep: fn(*items[i % n_pool][0])
+    return cpu
 
 
 def _c3_worker(pairs, probs):

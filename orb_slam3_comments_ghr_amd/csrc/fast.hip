@@ -9,19 +9,23 @@
 //   k_fast_score   every pixel of every level, both thresholds: the 9-of-16 arc test on the circle's
 //                  darker / brighter bit masks and cornerScore<16> (OpenCV's FAST_t / cornerScore,
 //                  restated: cv::FAST is not in the reference tree) -> 2 bytes per pixel
-//   k_fast_cells   one workgroup per cell: the strict 3x3 maximum at iniThFAST inside the cell's
-//                  tested range, the minThFAST pass when it keeps nothing; pass 0 counts, pass 1
-//                  writes the keypoints in the cell's row-major order at the cell's offset
-//   k_cell_scan    exclusive scan of the cell counts (cells in the reference's level / row / column
-//                  order, so the keypoints come out in vToDistributeKeys order)
+//   k_fast_cells   one workgroup per cell: the cell's two score planes staged in LDS with a zero
+//                  ring (suppression neighbours outside the tested range), the strict 3x3 maximum at
+//                  iniThFAST, the minThFAST pass when it keeps nothing, and the kept keypoints written
+//                  in row-major order to the cell's own slot range, with their count
+//   k_cell_gather  one workgroup per cell: its offset = the sum of the counts of the cells before it
+//                  (cells in the reference's level / row / column order, so the keypoints come out in
+//                  vToDistributeKeys order), then its keypoints copied there
 // DistributeOctTree is a short sequential tree walk per level (a few thousand keypoints): it runs
 // on the host over the downloaded keypoints, with the reference's node-list order (push_front,
 // erase by the stored position) and its std::sort of (size, UL.x) for the final expansions.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "match_common.h"
@@ -36,6 +40,9 @@ constexpr int PATCH_SIZE = 31;
 constexpr float CELL_W = 35.f;
 
 struct FastArgs {
+    int block0[MAX_LEVELS + 1];         // first 64 x 4 pixel block of each level (flattened grid)
+    int bx[MAX_LEVELS];                 // blocks per row of 64 pixels
+    int n_levels;
     GLOBAL const uint8_t *img[MAX_LEVELS];
     GLOBAL uint8_t *score[MAX_LEVELS];  // per pixel: (score at min_th, score at ini_th)
     int rows[MAX_LEVELS], cols[MAX_LEVELS], step[MAX_LEVELS];
@@ -45,80 +52,56 @@ struct FastArgs {
 struct Cell {
     int level, r0, r1, c0, c1;  // the cell image: rows r0 .. r1 - 1, columns c0 .. c1 - 1 of the level
     int dx, dy;                 // (j wCell, i hCell): the shift :1168-1169 adds
+    int slot;                   // first slot of the cell's keypoint range (one per tested pixel)
 };
+constexpr int MAX_T = 72;       // tested rows / columns of a cell + the zero ring: hCell, wCell <= 70
 
 struct CellArgs {
     const Cell *cells;
     int n_cells;
     GLOBAL uint8_t *score[MAX_LEVELS];
     int cols[MAX_LEVELS];
-    GLOBAL int32_t *count;        // per cell (pass 0), then the exclusive scan (k_cell_scan)
-    float4 *keys;                 // (x, y, response, 0) in cell order (pass 1)
+    GLOBAL int32_t *count;        // per cell
+    float4 *slots;                // (x, y, response, 0) per cell slot range
+    float4 *keys;                 // compacted, in cell order
+    GLOBAL int32_t *total;
 };
 
-// 9 contiguous set bits in a circular 16-bit mask
-__device__ __forceinline__ bool arc9(uint32_t m)
+// cornerScore<16> (OpenCV fast_score.cpp) with d[k] = v - circle[k] (circle index k mod 16) works
+// out to max(threshold, best_dark, best_bright) - 1, where best_dark = the largest min(d) over the 16
+// arcs of 9 and best_bright = the largest min(-d): its early "a <= a0: continue" skips only arcs that
+// cannot raise the maximum.  A pixel is a FAST corner at threshold t exactly when best_dark > t or
+// best_bright > t (a 9-arc strictly darker than v - t / brighter than v + t), so with
+// s0 = max(best_dark, best_bright) - 1:
+//     corner at t  <=>  s0 >= t,   and then  cornerScore(t) = s0.
+// One branch-free s0 per pixel gives both thresholds' scores (the oracle keeps OpenCV's literal
+// test + cornerScore; the GPU tests compare the two on every pixel of their frames).
+__device__ __forceinline__ int fast_s0(const int (&d)[16])
 {
-    uint32_t r = m | (m << 16);  // rotate by doubling
-    uint32_t a = r;
-#pragma unroll
-    for (int k = 1; k < 9; k++) a &= r >> k;
-    return (a & 0xffffu) != 0;
-}
-
-// cornerScore<16> (OpenCV fast_score.cpp), d[k] = v - circle[k], k < 25 (circle index k mod 16)
-__device__ __forceinline__ int corner_score(const int (&d)[16], int threshold)
-{
-#define D(k) d[(k) & 15]
-    int a0 = threshold;
-#pragma unroll
-    for (int k = 0; k < 16; k += 2) {
-        int a = min(D(k + 1), D(k + 2));
-        a = min(a, D(k + 3));
-        if (a <= a0) continue;
-        a = min(a, D(k + 4));
-        a = min(a, D(k + 5));
-        a = min(a, D(k + 6));
-        a = min(a, D(k + 7));
-        a = min(a, D(k + 8));
-        a0 = max(a0, min(a, D(k)));
-        a0 = max(a0, min(a, D(k + 9)));
-    }
-    int b0 = -a0;
-#pragma unroll
-    for (int k = 0; k < 16; k += 2) {
-        int b = max(D(k + 1), D(k + 2));
-        b = max(b, D(k + 3));
-        b = max(b, D(k + 4));
-        b = max(b, D(k + 5));
-        if (b >= b0) continue;
-        b = max(b, D(k + 6));
-        b = max(b, D(k + 7));
-        b = max(b, D(k + 8));
-        b0 = min(b0, max(b, D(k)));
-        b0 = min(b0, max(b, D(k + 9)));
-    }
-#undef D
-    return -b0 - 1;
-}
-
-// FAST_t<16>'s test at one threshold: a 9-of-16 arc strictly darker than v - t or brighter than v + t
-__device__ __forceinline__ int fast_at(const int (&d)[16], int t)
-{
-    uint32_t dark = 0, bright = 0;
+    int bd = -1024, bb = -1024;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        dark |= (uint32_t)(d[k] > t) << k;     // circle < v - t
-        bright |= (uint32_t)(d[k] < -t) << k;  // circle > v + t
+        int mn = d[k], mx = d[k];
+#pragma unroll
+        for (int j = 1; j < 9; j++) {
+            mn = min(mn, d[(k + j) & 15]);
+            mx = max(mx, d[(k + j) & 15]);
+        }
+        bd = max(bd, mn);
+        bb = max(bb, -mx);
     }
-    return (arc9(dark) || arc9(bright)) ? corner_score(d, t) : 0;
+    return max(bd, bb) - 1;
 }
 
-// grid (ceil(max cols / 64), ceil(max rows / 4), levels), 64 x 4 threads: one pixel each
+// one 64 x 4 pixel block per workgroup, the levels' blocks one after the other (no idle blocks of a
+// grid sized for level 0)
 __global__ __launch_bounds__(256) void k_fast_score(const FastArgs A)
 {
-    const int l = blockIdx.z;
-    const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int b = blockIdx.x;
+    int l = 0;
+    while (l + 1 < A.n_levels && b >= A.block0[l + 1]) l++;
+    const int bl = b - A.block0[l];
+    const int x = (bl % A.bx[l]) * 64 + (threadIdx.x & 63), y = (bl / A.bx[l]) * 4 + (threadIdx.x >> 6);
     const int rows = A.rows[l], cols = A.cols[l];
     if (x >= cols || y >= rows) return;
     uint8_t s_lo = 0, s_hi = 0;
@@ -132,16 +115,15 @@ __global__ __launch_bounds__(256) void k_fast_score(const FastArgs A)
         int d[16];
 #pragma unroll
         for (int k = 0; k < 16; k++) d[k] = v - (int)p[ox[k] + oy[k] * step];
-        s_lo = (uint8_t)fast_at(d, A.min_th);
-        s_hi = (uint8_t)fast_at(d, A.ini_th);
+        const int s0 = fast_s0(d);
+        s_lo = (uint8_t)(s0 >= A.min_th ? s0 : 0);
+        s_hi = (uint8_t)(s0 >= A.ini_th ? s0 : 0);
     }
     GLOBAL uint8_t *o = A.score[l] + 2 * ((size_t)y * cols + x);
     *(GLOBAL uint16_t *)o = (uint16_t)(s_lo | (s_hi << 8));
 }
 
-// one 256-thread workgroup per cell; PASS 0: count (the ini_th pass, else the min_th pass), PASS 1:
-// write the keypoints at the scanned offset in row-major order
-template <int PASS>
+// one 256-thread workgroup per cell
 __global__ __launch_bounds__(256) void k_fast_cells(const CellArgs A)
 {
     const int c = blockIdx.x;
@@ -149,32 +131,36 @@ __global__ __launch_bounds__(256) void k_fast_cells(const CellArgs A)
     const Cell C = A.cells[c];
     const int h = C.r1 - C.r0 - 6, w = C.c1 - C.c0 - 6;  // tested rows / columns of the cell image
     const int cols = A.cols[C.level];
-    GLOBAL const uint8_t *S = A.score[C.level];
+    GLOBAL const uint16_t *S = (GLOBAL const uint16_t *)A.score[C.level];
+    __shared__ uint16_t s_sc[MAX_T * MAX_T];  // (score at min_th, score at ini_th), zero ring
     __shared__ int s_cnt[4];
     __shared__ int s_total;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int n = (h > 0 && w > 0) ? h * w : 0;
-    auto keep_at = [&](int idx, int sel, int &s) -> bool {
+    const int tw = w + 2, nt = (h + 2) * tw;
+    for (int i = threadIdx.x; i < nt; i += 256) {
+        const int rr = i / tw - 1, cc = i % tw - 1;
+        const bool in = rr >= 0 && rr < h && cc >= 0 && cc < w;
+        s_sc[i] = in ? S[(size_t)(C.r0 + 3 + rr) * cols + C.c0 + 3 + cc] : (uint16_t)0;
+    }
+    __syncthreads();
+    const int sh = 8;  // the ini_th score is the high byte
+    auto keep_at = [&](int idx, int shift, int &sc) -> bool {
         const int rr = idx / w, cc = idx - rr * w;
-        const int y = C.r0 + 3 + rr, x = C.c0 + 3 + cc;
-        s = S[2 * ((size_t)y * cols + x) + sel];
-        if (!s) return false;
+        const uint16_t *p = s_sc + (rr + 1) * tw + cc + 1;
+        sc = (p[0] >> shift) & 0xff;
+        if (!sc) return false;
+        const int n8[8] = {p[-tw - 1], p[-tw], p[-tw + 1], p[-1], p[1], p[tw - 1], p[tw], p[tw + 1]};
 #pragma unroll
-        for (int dy = -1; dy <= 1; dy++)
-#pragma unroll
-            for (int dx = -1; dx <= 1; dx++) {
-                if (!dy && !dx) continue;
-                const int r2 = rr + dy, c2 = cc + dx;
-                const int t = (r2 >= 0 && r2 < h && c2 >= 0 && c2 < w) ? S[2 * ((size_t)(y + dy) * cols + x + dx) + sel] : 0;
-                if (!(s > t)) return false;
-            }
+        for (int k = 0; k < 8; k++)
+            if (!(sc > ((n8[k] >> shift) & 0xff))) return false;
         return true;
     };
-    auto count_pass = [&](int sel) -> int {
+    auto count_pass = [&](int shift) -> int {
         int k = 0;
         for (int i = threadIdx.x; i < n; i += 256) {
-            int s;
-            k += keep_at(i, sel, s) ? 1 : 0;
+            int sc;
+            k += keep_at(i, shift, sc) ? 1 : 0;
         }
         for (int o = 32; o > 0; o >>= 1) k += __shfl_xor(k, o);
         if (lane == 0) s_cnt[wv] = k;
@@ -183,24 +169,23 @@ __global__ __launch_bounds__(256) void k_fast_cells(const CellArgs A)
         __syncthreads();
         return t;
     };
-    int sel = 1;  // iniThFAST
-    int total = count_pass(1);
+    int shift = sh;  // iniThFAST
+    int total = count_pass(sh);
     if (total == 0) {  // :1146-1155
-        sel = 0;
+        shift = 0;
         total = count_pass(0);
     }
-    if (PASS == 0) {
-        if (threadIdx.x == 0) A.count[c] = total;
-        return;
+    if (threadIdx.x == 0) {
+        A.count[c] = total;
+        s_total = 0;
     }
     if (total == 0) return;
-    // ordered compaction, 256 pixels per round: wave ballots, then the 4 wave counts
-    if (threadIdx.x == 0) s_total = A.count[c];  // this cell's offset (scanned)
     __syncthreads();
+    // ordered compaction into the cell's slots, 256 pixels per round: wave ballots, then 4 wave counts
     for (int base = 0; base < n; base += 256) {
         const int i = base + threadIdx.x;
-        int s = 0;
-        const bool k = i < n && keep_at(i, sel, s);
+        int sc = 0;
+        const bool k = i < n && keep_at(i, shift, sc);
         const unsigned long long m = __ballot(k);
         if (lane == 0) s_cnt[wv] = __popcll(m);
         __syncthreads();
@@ -209,7 +194,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const CellArgs A)
         off += __popcll(m & ((1ull << lane) - 1));
         if (k) {
             const int rr = i / w, cc = i - rr * w;
-            A.keys[off] = make_float4((float)(cc + 3 + C.dx), (float)(rr + 3 + C.dy), (float)s, 0.f);
+            A.slots[C.slot + off] = make_float4((float)(cc + 3 + C.dx), (float)(rr + 3 + C.dy), (float)sc, 0.f);
         }
         __syncthreads();
         if (threadIdx.x == 0) s_total += s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
@@ -217,30 +202,23 @@ __global__ __launch_bounds__(256) void k_fast_cells(const CellArgs A)
     }
 }
 
-// exclusive scan of the cell counts in place (one workgroup); out_total[0] = the sum
-__global__ __launch_bounds__(1024) void k_cell_scan(GLOBAL int32_t *count, int n, GLOBAL int32_t *out_total)
+// one 256-thread workgroup per cell: offset = sum of the earlier cells' counts (a few hundred loads),
+// then the cell's keypoints moved to it; the last cell writes the total
+__global__ __launch_bounds__(256) void k_cell_gather(const CellArgs A)
 {
-    __shared__ int s[1024];
-    __shared__ int carry;
-    if (threadIdx.x == 0) carry = 0;
+    const int c = blockIdx.x;
+    if (c >= A.n_cells) return;
+    __shared__ int s_part[4];
+    int t = 0;
+    for (int i = threadIdx.x; i < c; i += 256) t += A.count[i];
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+    if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = t;
     __syncthreads();
-    for (int base = 0; base < n; base += 1024) {
-        const int i = base + threadIdx.x;
-        const int v = i < n ? count[i] : 0;
-        s[threadIdx.x] = v;
-        __syncthreads();
-        for (int o = 1; o < 1024; o <<= 1) {
-            const int t = threadIdx.x >= o ? s[threadIdx.x - o] : 0;
-            __syncthreads();
-            s[threadIdx.x] += t;
-            __syncthreads();
-        }
-        if (i < n) count[i] = carry + s[threadIdx.x] - v;
-        __syncthreads();
-        if (threadIdx.x == 1023) carry += s[1023];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) out_total[0] = carry;
+    const int off = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+    const int cnt = A.count[c];
+    const int slot = A.cells[c].slot;
+    for (int i = threadIdx.x; i < cnt; i += 256) A.keys[off + i] = A.slots[slot + i];
+    if (c == A.n_cells - 1 && threadIdx.x == 0) A.total[0] = off + cnt;
 }
 
 // ---- DistributeOctTree (ref:src/ORBextractor.cc:716-1050) on the host ------------------------------
@@ -257,6 +235,7 @@ struct OctTree {
     const float4 *keys;
     std::vector<OctNode> nodes;
     std::vector<int> kidx;
+    std::vector<uint8_t> qbuf;  // DivideNode's quadrant per keypoint (scratch)
     int head = -1, size = 0;
 
     int new_node()
@@ -314,7 +293,8 @@ struct OctTree {
         n4.blx = n3.brx, n4.bly = n3.bry, n4.brx = P.brx, n4.bry = P.bry;
         // classify into four runs of the index pool, each in the parent's order
         int cnt[4] = {0, 0, 0, 0};
-        std::vector<uint8_t> q(P.kcnt);
+        std::vector<uint8_t> &q = qbuf;
+        q.resize(P.kcnt);
         for (int k = 0; k < P.kcnt; k++) {
             const float4 kp = keys[kidx[P.kbeg + k]];
             const int qq = (kp.x < n1.urx) ? ((kp.y < n1.bry) ? 0 : 2) : ((kp.y < n1.bry) ? 1 : 3);
@@ -348,10 +328,14 @@ void distribute_oct_tree(const float4 *keys, int nk, int minX, int maxX, int min
                          std::vector<float4> &out)
 {
     out.clear();
-    OctTree T;
+    // per host thread, kept across calls: fresh multi-MB vectors per call cost more in page faults
+    // than the whole tree walk
+    thread_local OctTree T;
     T.keys = keys;
-    T.nodes.reserve(4 * (size_t)nk + 64);
-    T.kidx.reserve(8 * (size_t)nk + 64);
+    T.nodes.clear();
+    T.kidx.clear();
+    T.head = -1;
+    T.size = 0;
     const int nIni = (int)std::round(static_cast<float>(maxX - minX) / (maxY - minY));
     const float hX = static_cast<float>(maxX - minX) / nIni;
     std::vector<int> ini(nIni);
@@ -459,6 +443,11 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
                int32_t *level_start)
 {
     if (!ctx) return OSG_E_INVALID;
+    static const bool prof = getenv("OSG_ORB_PROFILE") != nullptr;  // host phase times to stderr
+    const auto tp0 = std::chrono::steady_clock::now();
+    auto ms_since = [](std::chrono::steady_clock::time_point t) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+    };
     OSG_REQUIRE(ctx, P && P->n_levels >= 1 && P->n_levels <= MAX_LEVELS && P->data && P->rows && P->cols && P->step,
                 "pyramid (1 .. %d levels)", MAX_LEVELS);
     OSG_REQUIRE(ctx, n_features && scale_factors && level_start && (cap == 0 || (x && y && response && size)),
@@ -470,7 +459,6 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
     FastArgs FA{};
     FA.ini_th = std::min(std::max(ini_th, 0), 255);  // FAST_t clamps the threshold
     FA.min_th = std::min(std::max(min_th, 0), 255);
-    int max_rows = 0, max_cols = 0;
     for (int l = 0; l < L; l++) {
         const int rows = P->rows[l], cols = P->cols[l];
         OSG_REQUIRE(ctx, P->data[l] && rows > 0 && cols > 0 && P->step[l] >= cols, "level %d", l);
@@ -495,14 +483,12 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
                 float maxX = iniX + wCell + 6;
                 if (iniX >= g.maxBX - 6) continue;
                 if (maxX > g.maxBX) maxX = g.maxBX;
-                cells.push_back(Cell{l, (int)iniY, (int)maxY, (int)iniX, (int)maxX, j * wCell, i * hCell});
+                cells.push_back(Cell{l, (int)iniY, (int)maxY, (int)iniX, (int)maxX, j * wCell, i * hCell, 0});
             }
         }
         g.cell1 = (int)cells.size();
         FA.rows[l] = rows;
         FA.cols[l] = cols;
-        max_rows = std::max(max_rows, rows);
-        max_cols = std::max(max_cols, cols);
     }
     const int nc = (int)cells.size();
     // device: packed inputs (host levels row-contiguous, cells), score planes, counts, keys
@@ -525,20 +511,25 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
             img_off[l] = pk.add(keep.back().data(), keep.back().size());
         }
     }
-    const size_t cell_off = pk.add(cells.data(), sizeof(Cell) * cells.size());
     size_t score_bytes = 0;
     std::vector<size_t> score_off(L);
     for (int l = 0; l < L; l++) {
         score_off[l] = score_bytes;
         score_bytes += ((size_t)P->rows[l] * P->cols[l] * 2 + 255) & ~size_t(255);
     }
-    size_t max_keys = 0;  // bound: the tested pixels of every cell
-    for (const Cell &c : cells) max_keys += (size_t)std::max(0, c.r1 - c.r0 - 6) * std::max(0, c.c1 - c.c0 - 6);
+    size_t max_keys = 0;  // one slot per tested pixel of every cell
+    for (Cell &c : cells) {
+        const int h = std::max(0, c.r1 - c.r0 - 6), w = std::max(0, c.c1 - c.c0 - 6);
+        OSG_REQUIRE(ctx, h + 2 <= MAX_T && w + 2 <= MAX_T, "cell of %d x %d tested pixels", h, w);
+        c.slot = (int)max_keys;
+        max_keys += (size_t)h * w;
+    }
+    const size_t cell_off = pk.add(cells.data(), sizeof(Cell) * cells.size());
     char *din = nullptr, *dsc = nullptr, *dcnt = nullptr, *dkeys = nullptr;
     OSG_ALLOC(ctx, din, SLOT_TMP0, pk.total + 256);
     OSG_ALLOC(ctx, dsc, SLOT_TMP1, score_bytes + 256);
     OSG_ALLOC(ctx, dcnt, SLOT_TMP2, sizeof(int32_t) * (nc + 64));
-    OSG_ALLOC(ctx, dkeys, SLOT_TMP3, sizeof(float4) * (max_keys + 1));
+    OSG_ALLOC(ctx, dkeys, SLOT_TMP3, sizeof(float4) * (2 * max_keys + 2));
     for (int l = 0; l < L; l++) {
         if (!P->on_device) FA.img[l] = (GLOBAL const uint8_t *)(din + img_off[l]);
         FA.score[l] = (GLOBAL uint8_t *)(dsc + score_off[l]);
@@ -551,8 +542,17 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
         CA.cols[l] = P->cols[l];
     }
     CA.count = (GLOBAL int32_t *)dcnt;
-    CA.keys = (float4 *)dkeys;
+    CA.slots = (float4 *)dkeys;
+    CA.keys = (float4 *)dkeys + max_keys + 1;
     GLOBAL int32_t *d_total = (GLOBAL int32_t *)(dcnt + sizeof(int32_t) * (nc + 32));
+    CA.total = d_total;
+    // flattened score grid: the levels' 64 x 4 pixel blocks one after another
+    FA.n_levels = L;
+    FA.block0[0] = 0;
+    for (int l = 0; l < L; l++) {
+        FA.bx[l] = (P->cols[l] + 63) / 64;
+        FA.block0[l + 1] = FA.block0[l] + FA.bx[l] * ((P->rows[l] + 3) / 4);
+    }
     // pinned: inputs, then the total (and later the keys)
     char *pin = (char *)osg_pinned(ctx, pk.total + 256 + sizeof(float4) * (max_keys + 1) + 256);
     if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
@@ -563,11 +563,10 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
     if (!ev) return osg_set_error(ctx, OSG_E_HIP, "event create failed");
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(din, pin, pk.total, hipMemcpyHostToDevice, ctx->stream));
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[0], ctx->stream));
-    hipLaunchKernelGGL(k_fast_score, dim3((max_cols + 63) / 64, (max_rows + 3) / 4, L), dim3(256), 0, ctx->stream, FA);
+    hipLaunchKernelGGL(k_fast_score, dim3(FA.block0[L]), dim3(256), 0, ctx->stream, FA);
     if (nc > 0) {
-        hipLaunchKernelGGL(k_fast_cells<0>, dim3(nc), dim3(256), 0, ctx->stream, CA);
-        hipLaunchKernelGGL(k_cell_scan, dim3(1), dim3(1024), 0, ctx->stream, CA.count, nc, d_total);
-        hipLaunchKernelGGL(k_fast_cells<1>, dim3(nc), dim3(256), 0, ctx->stream, CA);
+        hipLaunchKernelGGL(k_fast_cells, dim3(nc), dim3(256), 0, ctx->stream, CA);
+        hipLaunchKernelGGL(k_cell_gather, dim3(nc), dim3(256), 0, ctx->stream, CA);
     }
     OSG_HIP_CHECK(ctx, hipGetLastError());
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
@@ -578,28 +577,60 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
                                           ctx->stream));
         OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
         total = *(int32_t *)pin_out;
-        OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_out, dkeys, sizeof(float4) * (size_t)total, hipMemcpyDeviceToHost,
+        OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_out, CA.keys, sizeof(float4) * (size_t)total, hipMemcpyDeviceToHost,
                                           ctx->stream));
-        OSG_HIP_CHECK(ctx, hipMemcpyAsync(offs.data(), dcnt, sizeof(int32_t) * nc, hipMemcpyDeviceToHost, ctx->stream));
+        OSG_HIP_CHECK(ctx, hipMemcpyAsync(offs.data() + 1, dcnt, sizeof(int32_t) * nc, hipMemcpyDeviceToHost,
+                                          ctx->stream));
     }
     OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
-    offs[nc] = total;
+    for (int c = 0; c < nc; c++) offs[c + 1] += offs[c];  // counts -> offsets
+    const double t_gpu = ms_since(tp0);
+    const auto tp1 = std::chrono::steady_clock::now();
     float ms = 0.f;
     OSG_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ev[0], ev[1]));
     ctx->last_kernel_ms = ms;
-    const float4 *keys = (const float4 *)pin_out;
-    // DistributeOctTree per level over that level's cells' keypoints (:1180-1196)
+    // the keypoints leave the pinned staging block once: the tree walk reads each of them several
+    // times, from ordinary cached memory
+    thread_local std::vector<float4> hkeys;
+    hkeys.resize((size_t)total + 1);
+    std::memcpy(hkeys.data(), pin_out, sizeof(float4) * (size_t)total);
+    const float4 *keys = hkeys.data();
+    const double t_copy = ms_since(tp1);
+    // DistributeOctTree per level over that level's cells' keypoints (:1180-1196); the levels are
+    // independent, so very large frames spread them over a few host threads (contiguous level ranges
+    // of about equal keypoint counts; a thread started per call pays its tree buffers' page faults,
+    // so an EuRoC frame's ~12k FAST keypoints stay on the calling thread)
+    std::vector<std::vector<float4>> kept(L);
+    auto run_levels = [&](int l0, int l1) {
+        for (int l = l0; l < l1; l++) {
+            const LevelGeom &g = lg[l];
+            const int k0 = offs[g.cell0], k1 = offs[g.cell1];
+            distribute_oct_tree(keys + k0, k1 - k0, g.minBX, g.maxBX, g.minBY, g.maxBY, n_features[l], kept[l]);
+        }
+    };
+    const int nthr = total > 60000 ? std::min(L, 3) : 1;
+    if (nthr <= 1) {
+        run_levels(0, L);
+    } else {
+        std::vector<int> cut(nthr + 1, L);
+        cut[0] = 0;
+        for (int t = 1, l = 0; t < nthr; t++) {  // level ranges of ~total / nthr keypoints
+            while (l < L && offs[lg[l].cell1] < (int64_t)total * t / nthr) l++;
+            cut[t] = std::max(cut[t - 1] + 1, std::min(l + 1, L - (nthr - t)));
+        }
+        std::vector<std::thread> th;
+        for (int t = 1; t < nthr; t++) th.emplace_back(run_levels, cut[t], cut[t + 1]);
+        run_levels(cut[0], cut[1]);
+        for (auto &x : th) x.join();
+    }
     int n_out = 0;
     level_start[0] = 0;
-    std::vector<float4> kept;
     for (int l = 0; l < L; l++) {
         const LevelGeom &g = lg[l];
-        const int k0 = offs[g.cell0], k1 = offs[g.cell1];
-        distribute_oct_tree(keys + k0, k1 - k0, g.minBX, g.maxBX, g.minBY, g.maxBY, n_features[l], kept);
         const int scaledPatchSize = (int)(PATCH_SIZE * scale_factors[l]);
-        if (n_out + (int)kept.size() > cap)
+        if (n_out + (int)kept[l].size() > cap)
             return osg_set_error(ctx, OSG_E_INVALID, "keypoint capacity %d exceeded at level %d", cap, l);
-        for (const float4 &k : kept) {
+        for (const float4 &k : kept[l]) {
             x[n_out] = k.x + g.minBX;
             y[n_out] = k.y + g.minBY;
             response[n_out] = k.z;
@@ -608,6 +639,10 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
         }
         level_start[l + 1] = n_out;
     }
+    if (prof)
+        fprintf(stderr, "[osg orb detect] %d cells, %d FAST keypoints -> %d: setup + GPU + download %.3f ms "
+                        "(kernels %.3f ms), key copy %.3f ms, octree %.3f ms\n", nc, total, n_out, t_gpu, (double)ms, t_copy,
+                ms_since(tp1) - t_copy);
     return n_out;
 }
 

@@ -885,6 +885,44 @@ int main(int argc, char **argv)
             out["n_out"] = make('i', std::vector<int32_t>{n_out});
             out["angle"] = make('f', ang);
             out["desc"] = make('b', desc);
+        } else if (mode == "detect") {
+            // levels "D.raw" concatenated with "D.dims" (rows, cols), stored as ROIs (step = cols + 5);
+            // "D.nf" mnFeaturesPerLevel, "D.scale" mvScaleFactor, "D.th" (iniThFAST, minThFAST)
+            const Arr &dims = get(in, "D.dims");
+            const int levels = (int)dims.n / 2;
+            ORBextractor ex;
+            const uint8_t *sr = get(in, "D.raw").p<uint8_t>();
+            for (int l = 0; l < levels; l++) {
+                const int rows = dims.p<int32_t>()[2 * l], cols = dims.p<int32_t>()[2 * l + 1];
+                cv::Mat m(rows, cols, (size_t)cols + 5);
+                for (int r = 0; r < rows; r++) std::memcpy(m.ptr<unsigned char>(r), sr + (size_t)r * cols, cols);
+                sr += (size_t)rows * cols;
+                ex.mvImagePyramid.push_back(std::move(m));
+            }
+            const Arr &nf = get(in, "D.nf"), &sc = get(in, "D.scale"), &th = get(in, "D.th");
+            std::vector<int> nfl(nf.p<int32_t>(), nf.p<int32_t>() + nf.n);
+            std::vector<float> scl(sc.p<float>(), sc.p<float>() + sc.n);
+            std::vector<std::vector<cv::KeyPoint>> all;
+            const int n = osg_orbslam3::compute_keypoints_oct_tree(ex.mvImagePyramid, all, nfl, scl, th.p<int32_t>()[0],
+                                                                  th.p<int32_t>()[1]);
+            std::vector<float> x, y, r, sz, a;
+            std::vector<int32_t> oct;
+            for (auto &lv : all)
+                for (auto &kp : lv) {
+                    x.push_back(kp.pt.x);
+                    y.push_back(kp.pt.y);
+                    r.push_back(kp.response);
+                    sz.push_back(kp.size);
+                    a.push_back(kp.angle);
+                    oct.push_back(kp.octave);
+                }
+            out["n"] = make('i', std::vector<int32_t>{n});
+            out["x"] = make('f', x);
+            out["y"] = make('f', y);
+            out["response"] = make('f', r);
+            out["size"] = make('f', sz);
+            out["angle"] = make('f', a);
+            out["octave"] = make('i', oct);
         } else if (mode == "distinct") {
             // keyframes: "K.desc" (nk x nkp rows), "K.bad"; MapPoints: "M.bad", "M.desc" (initial);
             // observations CSR "O.start" / "O.kf" / "O.left" / "O.right"

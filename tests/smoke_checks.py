@@ -71,3 +71,9 @@ def run(ctx, oracle):
     go, ro = orb.ORBDescribe(ctx, raw, blur, x, y, level, pat), oc.orb_describe(oracle, raw, blur, x, y, level, pat)
     if go[2] != ro[2] or not np.array_equal(go[0].view(np.int32), ro[0].view(np.int32)) or not np.array_equal(go[1], ro[1]):
         raise AssertionError("ORB orientation / descriptor mismatch vs oracle")
+    # ORBextractor::ComputeKeyPointsOctTree (FAST cells + DistributeOctTree)
+    levels = orb.synth_fast_pyramid(rng, width=320, height=240, n_levels=3, n_blobs=120)
+    nf, sc = orb.features_per_level(300, 3, 1.2), orb.scale_factors(3, 1.2)
+    gd, rd = orb.ORBDetect(ctx, levels, nf, sc), oc.orb_detect(oracle, levels, nf, sc)
+    if not all(np.array_equal(g, r) for g, r in zip(gd, rd)):
+        raise AssertionError("ORB keypoint detection mismatch vs oracle")
