@@ -458,7 +458,7 @@ int osg_compute_distinctive_descriptors_dev(osg_ctx *ctx, const void *d_desc, co
  * computeOrientation / IC_Angle (ref:src/ORBextractor.cc:89-136, 585-597) on mvImagePyramid[level] and
  * computeDescriptors / computeOrbDescriptor (ref:src/ORBextractor.cc:148-208, 1534-1545) on the
  * GaussianBlur'd level (ref:src/ORBextractor.cc:1628-1652), for keypoints in level coordinates (before
- * :1663-1667 scales them to level 0).  FAST, the octree distribution and the 7x7 Gaussian blur stay
+ * :1663-1667 scales them to level 0), e.g. from osg_orb_detect (b9).  The 7x7 Gaussian blur stays
  * with the caller (OpenCV).  umax: the extractor's umax (HALF_PATCH_SIZE + 1 = 16 entries, each
  * <= 15); pattern: its 512 points (ORBextractor::pattern) as (x, y) int pairs.  The orientation box
  * (+-15 around the rounded centre) must lie inside the raw level, else OSG_E_INVALID.  The blurred

@@ -1,8 +1,8 @@
 """Host mirror of ORBextractor's per-keypoint stages on the C ABI (``osg_orb_describe``, include/osg.h
 b8): computeOrientation / IC_Angle (ref:src/ORBextractor.cc:89-136, 585-597) on mvImagePyramid and
 computeDescriptors / computeOrbDescriptor (ref:src/ORBextractor.cc:148-208, 1534-1545) on the blurred
-levels (ref:src/ORBextractor.cc:1628-1652).  FAST, the octree distribution and the Gaussian blur stay
-with OpenCV; the caller passes the extractor's ``umax`` and ``pattern``.
+levels (ref:src/ORBextractor.cc:1628-1652).  The pyramid and the Gaussian blur stay with OpenCV; the
+caller passes the extractor's ``umax`` and ``pattern``.
 
 ComputeKeyPointsOctTree (``osg_orb_detect``, include/osg.h b9): FAST per W = 35 cell with
 iniThFAST / minThFAST and DistributeOctTree down to mnFeaturesPerLevel (ref:src/ORBextractor.cc:
