@@ -72,6 +72,7 @@ struct LbaCtl {
 struct LbaDev {
     // sizes
     int np, npt, ne, nhp, nhl, nblk, npairs, n_cams;
+    int n_graphs, xcd_map;        // the batch (the same in every graph's entry): LBA_GRAPH's mapping
     // inputs
     const uint8_t *pose_fixed;
     const int32_t *e_pose, *e_point, *e_cam;
@@ -132,9 +133,19 @@ __device__ inline const double *cur_pose(const LbaDev &D) { return D.ctl->sel ? 
 __device__ inline const double *cur_point(const LbaDev &D) { return D.ctl->sel ? D.pointB : D.pointA; }
 __device__ inline double *new_pose(const LbaDev &D) { return D.ctl->sel ? D.poseA : D.poseB; }
 __device__ inline double *new_point(const LbaDev &D) { return D.ctl->sel ? D.pointA : D.pointB; }
-// one problem per blockIdx.y; a workgroup whose graph skips this kernel leaves at once
-#define LBA_GRAPH(MODEBITS)                                  \
-    const LbaDev &D = Ds[blockIdx.y];                        \
+// One problem per workgroup row; a workgroup whose graph skips this kernel leaves at once.
+// With OSG_LBA_XCD=1, batches of >= 8 graphs run XCD-aware: grid (8 gx, ceil(B / 8)); workgroup (x, y) of the launch
+// goes to XCD x % 8 (dispatch is round-robin over the 8 XCDs in linear order and 8 gx is a multiple
+// of 8), so graph (x % 8) + 8 y runs on one XCD and its Hpl / Dinv / edge arrays stay in that XCD's
+// L2, while the chip works on 8 graphs at a time (their working set fits the MALL).  Measured slower
+// than the default grid (gx, B), which spreads each graph over the whole chip.
+#define LBA_GRAPH(MODEBITS)                                                                      \
+    const bool xcd_map_ = Ds[0].xcd_map;                                                         \
+    const int by = xcd_map_ ? (int)(blockIdx.x & 7) + 8 * (int)blockIdx.y : (int)blockIdx.y;     \
+    const int bx = xcd_map_ ? (int)(blockIdx.x >> 3) : (int)blockIdx.x;                          \
+    (void)bx;                                                                                    \
+    if (by >= Ds[0].n_graphs) return;                                                            \
+    const LbaDev &D = Ds[by];                                                                    \
     if (!(D.ctl->mode & (MODEBITS))) return
 
 // The edge's Huber kernel; an edge without one (BundleAdjustment with bRobust = false,
@@ -169,12 +180,12 @@ __device__ inline double block_sum_d(double v, double *s)
 __global__ __launch_bounds__(EB) void k_errors(const LbaDev *__restrict__ Ds, int which)
 {
     LBA_GRAPH(which ? M_ERRC : M_ACT);
-    if ((int)blockIdx.x >= D.ge) return;
+    if (bx >= D.ge) return;
     const double *poses = which ? cur_pose(D) : new_pose(D);
     const double *points = which ? cur_point(D) : new_point(D);
     const int part_off = which ? 3 * NPART : 0;
     __shared__ double s[EB / 64];
-    const int e = blockIdx.x * EB + threadIdx.x;
+    const int e = bx * EB + threadIdx.x;
     double rho0 = 0.0;
     if (e < D.ne) {
         const int k = D.e_kind[e];
@@ -193,7 +204,7 @@ __global__ __launch_bounds__(EB) void k_errors(const LbaDev *__restrict__ Ds, in
         huber(c, delta, dsqr, rho0, r1);
     }
     const double t = block_sum_d(rho0, s);
-    if (threadIdx.x == 0) D.part[part_off + blockIdx.x] = t;
+    if (threadIdx.x == 0) D.part[part_off + bx] = t;
 }
 
 // Linearisation, landmark-major: one thread per landmark walks its edges in edge order (ref:
@@ -207,9 +218,9 @@ __global__ __launch_bounds__(EB) void k_errors(const LbaDev *__restrict__ Ds, in
 __global__ __launch_bounds__(EB) void k_linearize(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_LIN);
-    if ((int)blockIdx.x >= max(D.gl, 1)) return;
+    if (bx >= max(D.gl, 1)) return;
     __shared__ double s[EB / 64];
-    const int l = blockIdx.x * EB + threadIdx.x;
+    const int l = bx * EB + threadIdx.x;
     double md = 0.0;
     if (l < D.nhl) {
         const double *X = cur_point(D) + 3 * (size_t)D.hl_point[l];
@@ -264,7 +275,7 @@ __global__ __launch_bounds__(EB) void k_linearize(const LbaDev *__restrict__ Ds)
     if (threadIdx.x == 0) {
         double m = 0;
         for (int i = 0; i < EB / 64; i++) m = fmax(m, s[i]);
-        D.part[2 * NPART + blockIdx.x] = m;
+        D.part[2 * NPART + bx] = m;
     }
 }
 
@@ -272,7 +283,7 @@ __global__ __launch_bounds__(EB) void k_linearize(const LbaDev *__restrict__ Ds)
 __global__ __launch_bounds__(EB) void k_pose_red(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_LIN);
-    const int i = blockIdx.x;
+    const int i = bx;
     if (i >= D.nhp) return;
     const int diag_off = 2 * NPART + D.gl;
     __shared__ double s[EB / 64][27];
@@ -368,7 +379,7 @@ __global__ __launch_bounds__(EB) void k_schur_point(const LbaDev *__restrict__ D
 {
     LBA_GRAPH(M_ACT);
     const double lambda = D.ctl->lambda;
-    const int l = blockIdx.x * EB + threadIdx.x;
+    const int l = bx * EB + threadIdx.x;
     if (l >= D.nhl) return;
     double Dm[9];
     for (int i = 0; i < 9; i++) Dm[i] = D.Hll[9 * (size_t)l + i];
@@ -404,7 +415,7 @@ template <bool VALU>
 __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT);
-    const int rs = blockIdx.x;
+    const int rs = bx;
     if (rs >= D.n_rs) return;
     __shared__ double s_bd[RS * 18];
     __shared__ double s_cf[RT / 64][6];
@@ -568,7 +579,7 @@ __global__ __launch_bounds__(256) void k_schur_pairs(const LbaDev *__restrict__ 
 {
     LBA_GRAPH(M_ACT);
     const double lambda = D.ctl->lambda;
-    const int wave = (blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int wave = (bx * 256 + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (wave >= D.npairs) return;
     int i = 0, rem = wave;
@@ -772,7 +783,7 @@ __device__ __forceinline__ double rcp_nr(double d)
 __global__ __launch_bounds__(256) void k_chol_col(const LbaDev *__restrict__ Ds, int j)
 {
     LBA_GRAPH(M_ACT);
-    if (j >= D.nblk_red || (int)blockIdx.x >= D.nblk_red - j) return;
+    if (j >= D.nblk_red || bx >= D.nblk_red - j) return;
     __shared__ double sP[4][CB][CB + 1];  // per-wave partial tiles
     __shared__ double sG[CB][CB + 1];     // T under elimination
     __shared__ double sM[CB][CB + 1];     // Lt^-1, then L_jj^-1
@@ -785,7 +796,7 @@ __global__ __launch_bounds__(256) void k_chol_col(const LbaDev *__restrict__ Ds,
     const double *A = D.Hs;
     const int k0 = j * CB;
     const int nb = min(CB, n - k0);
-    const int t = blockIdx.x;
+    const int t = bx;
     const int tid = threadIdx.x;
     const int R0 = k0 + t * CB;
     unsigned long long *ts = (D.tstamp && t < 2 && tid == 0 && j < 32) ? D.tstamp + 8 * (2 * j + t) : nullptr;
@@ -1026,8 +1037,8 @@ __global__ __launch_bounds__(256) void k_chol_trail(const LbaDev *__restrict__ D
     const int n = 6 * D.nhp;
     if (n <= CMAX) return;
     const int m = D.nblk_red - j - 1;  // row blocks below block j
-    if (m <= 0 || (int)blockIdx.x >= m * (m + 1) / 2) return;
-    int t = 0, rem = blockIdx.x;  // tile (t, u), u <= t, row-major over the lower triangle
+    if (m <= 0 || bx >= m * (m + 1) / 2) return;
+    int t = 0, rem = bx;  // tile (t, u), u <= t, row-major over the lower triangle
     while (rem > t) {
         rem -= t + 1;
         t++;
@@ -1120,12 +1131,12 @@ __global__ __launch_bounds__(1024) void k_chol_back_large(const LbaDev *__restri
 __global__ __launch_bounds__(EB) void k_update(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT);
-    if ((int)blockIdx.x >= D.gu) return;
+    if (bx >= D.gu) return;
     const double lambda = D.ctl->lambda;
     const double *pose_cur = cur_pose(D), *point_cur = cur_point(D);
     double *pose_new = new_pose(D), *point_new = new_point(D);
     __shared__ double s[EB / 64];
-    const int t = blockIdx.x * EB + threadIdx.x;
+    const int t = bx * EB + threadIdx.x;
     const int sp = 6 * D.nhp;
     double sc = 0.0;
     if (t < D.nhl) {
@@ -1168,7 +1179,7 @@ __global__ __launch_bounds__(EB) void k_update(const LbaDev *__restrict__ Ds)
     if (t < D.npt && D.point_h[t] < 0)
         for (int k = 0; k < 3; k++) point_new[3 * (size_t)t + k] = point_cur[3 * (size_t)t + k];
     const double tot = block_sum_d(sc, s);
-    if (threadIdx.x == 0) D.part[NPART + blockIdx.x] = tot;
+    if (threadIdx.x == 0) D.part[NPART + bx] = tot;
 }
 
 __global__ __launch_bounds__(EB) void k_classify(const LbaDev *__restrict__ Ds)
@@ -1176,7 +1187,7 @@ __global__ __launch_bounds__(EB) void k_classify(const LbaDev *__restrict__ Ds)
     LBA_GRAPH(M_FIN);
     const double *poses = cur_pose(D), *points = cur_point(D);
     uint8_t *bad = D.bad;
-    const int e = blockIdx.x * EB + threadIdx.x;
+    const int e = bx * EB + threadIdx.x;
     if (e >= D.ne) return;
     const int k = D.e_kind[e];
     const int dim = (k == OSG_EDGE_STEREO) ? 3 : 2;
@@ -1684,6 +1695,11 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     double *d_out = (double *)(dsm + dev_bytes + ctl_bytes);
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(din, pin, pk.total, hipMemcpyHostToDevice, ctx->stream));
     int mx_ge = 0, mx_gl = 1, mx_gu = 0, mx_nblk = 0, mx_nhp = 0, mx_chunks = 0, mx_pairs = 0, mx_red = 0, mx_rs = 0;
+    // XCD-aware graph placement (LBA_GRAPH) for batches of >= 8 graphs: OSG_LBA_XCD=1.  Off by
+    // default: measured slower (64 C4 windows: k_schur_rows 10.4 vs 8.9 ms, k_linearize 5.4 vs 4.4 ms
+    // per 14-step batch; profiles/r02_lba_xcd.txt)
+    static const bool xcd_env = getenv("OSG_LBA_XCD") && atoi(getenv("OSG_LBA_XCD")) == 1;
+    const bool xcd = xcd_env && NA >= 8;
     bool large = false;  // some graph's reduced system is past CMAX
     for (int a = 0; a < NA; a++) {
         const LbaHost &h = H[act[a]];
@@ -1698,6 +1714,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         D.nblk = h.nblk;
         D.npairs = h.npairs;
         D.n_cams = h.G->n_cams;
+        D.n_graphs = NA;
+        D.xcd_map = xcd ? 1 : 0;
         D.pose_fixed = osg_dptr<uint8_t>(din, o.fixed);
         D.e_pose = osg_dptr<int32_t>(din, o.epose);
         D.e_point = osg_dptr<int32_t>(din, o.epoint);
@@ -1797,8 +1815,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     // one lockstep step: every kernel once for all graphs, then 5 scalars per graph back
     auto run_step = [&]() -> int {
         OSG_HIP_CHECK(ctx, hipMemcpyAsync(d_ctl, h_ctl, ctl_bytes, hipMemcpyHostToDevice, ctx->stream));
-        const dim3 yb(1, NA);
-        auto gx = [&](int n) { return dim3(std::max(n, 1), NA); };
+        const dim3 yb = xcd ? dim3(8, (NA + 7) / 8) : dim3(1, NA);
+        auto gx = [&](int n) { return xcd ? dim3(8 * std::max(n, 1), (NA + 7) / 8) : dim3(std::max(n, 1), NA); };
         LBA_MARK(KT_ERR);
         hipLaunchKernelGGL(k_errors, gx(mx_ge), dim3(EB), 0, ctx->stream, d_dev, 1);
         LBA_MARK(KT_LIN);
@@ -1958,7 +1976,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     for (int a = 0; a < NA; a++) h_ctl[a] = LbaCtl{M_FIN, H[act[a]].sel, 0.0};
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(d_ctl, h_ctl, ctl_bytes, hipMemcpyHostToDevice, ctx->stream));
     LBA_MARK(KT_CLASS);
-    hipLaunchKernelGGL(k_classify, dim3(std::max(mx_ge, 1), NA), dim3(EB), 0, ctx->stream, d_dev);
+    hipLaunchKernelGGL(k_classify, xcd ? dim3(8 * std::max(mx_ge, 1), (NA + 7) / 8) : dim3(std::max(mx_ge, 1), NA),
+                       dim3(EB), 0, ctx->stream, d_dev);
     LBA_MARK(KT_END);
 #undef LBA_MARK
     OSG_HIP_CHECK(ctx, hipGetLastError());
