@@ -56,7 +56,7 @@ $(OBJDIR)/stereo.o: $(CSRC)/stereo.hip $(HDRS) $(CSRC)/match_common.h | $(OBJDIR
 $(OBJDIR)/orb.o: $(CSRC)/orb.hip $(HDRS) $(CSRC)/match_common.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(EXACT) -c $< -o $@
 
-$(OBJDIR)/fast.o: $(CSRC)/fast.hip $(HDRS) $(CSRC)/match_common.h | $(OBJDIR)
+$(OBJDIR)/fast.o: $(CSRC)/fast.hip $(HDRS) $(CSRC)/match_common.h $(CSRC)/octree.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(EXACT) -c $< -o $@
 
 $(LIB): $(OBJS)

@@ -496,6 +496,11 @@ int osg_orb_describe(osg_ctx *ctx, const osg_image_pyramid *raw, const osg_image
 int osg_orb_detect(osg_ctx *ctx, const osg_image_pyramid *raw, int32_t ini_th_fast, int32_t min_th_fast,
                    const int32_t *n_features_per_level, const float *scale_factors, int32_t capacity,
                    float *x, float *y, float *response, float *size, int32_t *level_start);
+/* Diagnostics: the host DistributeOctTree of osg_orb_detect alone, on nk keypoints given as (x, y,
+ * response, unused) float quadruples relative to (minX, minY); kept keypoints out the same way.
+ * Returns the count (no context, no GPU). */
+int osg_debug_distribute_oct_tree(const float *keys4, int32_t nk, int32_t minX, int32_t maxX, int32_t minY,
+                                  int32_t maxY, int32_t N, float *out4, int32_t cap);
 
 /* Diagnostics of the last search call on this context (summed / maxed over a batch): out[0]
  * candidates enumerated, out[1] Jacobi rounds, out[2] problems whose greedy was redone serially (a5 on a two-camera rig when a

@@ -190,6 +190,7 @@ EXPORTS = [
     "osg_search_by_projection_sim3", "osg_search_by_projection_sim3_batch", "osg_search_by_sim3",
     "osg_search_for_initialization", "osg_search_for_initialization_batch",
     "osg_compute_stereo_matches", "osg_compute_stereo_matches_batch", "osg_orb_describe", "osg_orb_detect",
+    "osg_debug_distribute_oct_tree",
 ]
 
 
@@ -261,6 +262,7 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.osg_search_for_initialization_batch.argtypes = [vp, vp, vp, i32, vp, C.c_int, f32, C.c_int, vp, vp]
     lib.osg_compute_stereo_matches.argtypes = [vp, C.POINTER(OsgStereoFrame), vp, vp]
     lib.osg_compute_stereo_matches_batch.argtypes = [vp, vp, i32, vp, vp, vp]
+    lib.osg_debug_distribute_oct_tree.argtypes = [vp, i32, i32, i32, i32, i32, i32, vp, i32]
     lib.osg_orb_detect.argtypes = [vp, C.POINTER(OsgImagePyramid), i32, i32, vp, vp, i32, vp, vp, vp, vp, vp]
     lib.osg_orb_describe.argtypes = [vp, C.POINTER(OsgImagePyramid), C.POINTER(OsgImagePyramid),
                                      C.POINTER(OsgOrbKeypoints), vp, vp, i32, vp, vp]
