@@ -84,7 +84,26 @@ OSG_HD inline double cube_rn(double t)
     return q + (qe + pe * t);
 }
 
-// sin(x) / cos(x) for 0 <= x <= 0.8: Horner in double-double over x^2, one final rounding
+// Terms of the x^2 series that matter at x: the first K coefficients when the first dropped term,
+// |c_K| x^(2K) (c_K = 1 / (2K)! or 1 / (2K + 1)!), is below 2^-118 of the leading 1 — far under the
+// double-double rounding error of the sum (2^-104), so the final rounding is that of the full
+// 15-term series.  LM rotation updates are mostly 1e-5 .. 1e-2 rad: 4 to 8 terms instead of 15.
+OSG_HD inline int series_terms(double x)
+{
+    const double lim[14] = {2.4532694666933987e-18, 2.915197201209678e-09, 3.5972075921221558e-06,
+                            0.00013661476184978878, 0.0012700544907879897, 0.0057973980883841278,
+                            0.017547082534525357,   0.040967787164514206,  0.080299195873085955,
+                            0.13906865564818396,    0.21990626161203589,   0.3245626875579769,
+                            0.45402522493007225,    0.6086654061405502};
+    int K = 15;
+#pragma unroll
+    for (int i = 13; i >= 0; i--)
+        if (x < lim[i]) K = i + 1;
+    return K;
+}
+
+// sin(x) / cos(x) for 0 <= x <= 0.8: Horner in double-double over x^2 from the series_terms(x)-th
+// coefficient down (the branches are uniform when every lane holds the same x), one final rounding
 OSG_HD inline double sin_rn_small(double x)
 {
     OSGX_NOCONTRACT
@@ -104,9 +123,13 @@ OSG_HD inline double sin_rn_small(double x)
                       {-9.183689863795546e-29, -1.4303150396787322e-45},
                       {1.1309962886447716e-31, 1.0498015412959506e-47}};
     const dd x2 = two_prod(x, x);
+    const int K = series_terms(x);
     dd s = c[14];
 #pragma unroll
-    for (int k = 13; k >= 0; k--) s = dd_add(dd_mul(s, x2), c[k]);
+    for (int k = 13; k >= 0; k--) {
+        if (k == K - 1) s = c[k];
+        else if (k < K - 1) s = dd_add(dd_mul(s, x2), c[k]);
+    }
     const dd r = dd_mul(s, dd{x, 0.0});
     return r.h + r.l;
 }
@@ -129,9 +152,13 @@ OSG_HD inline double cos_rn_small(double x)
                       {-2.4795962632247976e-27, 1.2953730964765229e-43},
                       {3.279889237069838e-30, 1.5117542744029879e-46}};
     const dd x2 = two_prod(x, x);
+    const int K = series_terms(x);
     dd s = c[14];
 #pragma unroll
-    for (int k = 13; k >= 0; k--) s = dd_add(dd_mul(s, x2), c[k]);
+    for (int k = 13; k >= 0; k--) {
+        if (k == K - 1) s = c[k];
+        else if (k < K - 1) s = dd_add(dd_mul(s, x2), c[k]);
+    }
     return s.h + s.l;
 }
 OSG_HD inline double sin_ref(double x)
