@@ -66,7 +66,7 @@ def parse():
     ap.add_argument("--no-gba", action="store_true", help="skip the global BA workload")
     ap.add_argument("--ba-reps", type=int, default=20)
     ap.add_argument("--ba-batch", type=int, default=64, help="C4 windows per GPU per lockstep batch")
-    ap.add_argument("--ba-batch-reps", type=int, default=3)
+    ap.add_argument("--ba-batch-reps", type=int, default=6)
     ap.add_argument("--ba-threads", type=int, default=4,
                     help="host threads per GPU driving LBA batches, each with its own context and HIP stream")
     ap.add_argument("--no-frames", action="store_true", help="skip the frame-batched C3 / C5 workloads")
