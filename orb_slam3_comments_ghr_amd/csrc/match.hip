@@ -95,6 +95,7 @@ struct MatchArgs {
     GLOBAL uint8_t *q_bin;           // 2 nq
     GLOBAL int32_t *status;          // [0] candidates, [1] nmatches, [2] rounds, [3] overflow, [4] serial
     int cap;
+    int lds_free;                    // dynamic LDS bytes past the resolve arrays (the staged grid region)
 };
 
 struct Win {
@@ -548,6 +549,49 @@ __device__ __forceinline__ int assigned_slots(const MatchArgs &A, QRes r, int (&
     return n;
 }
 
+// The serial redo of a5 on a two-camera rig (see the resolve phase) on LDS copies of its inputs:
+// eval_query<MODE_MPS> with blocked(s) = taken[s], then the assigned slots' state, query by query.
+struct SerialLds {
+    const int *off, *mid, *l2r, *r2l;
+    const uint32_t *cands;
+    const uint8_t *obs;
+};
+__device__ __forceinline__ QRes eval_mps_lds(const MatchArgs &A, const SerialLds &V, int q, const uint8_t *taken)
+{
+    QRes res{-1, -1};
+    const int e0 = V.off[q], em = V.mid[q], e1 = V.off[q + 1];
+    Top2 L, R;
+    for (int e = e0; e < em; e++) {
+        const uint32_t c = V.cands[e];
+        const int s = (int)(c & 0xFFFFu);
+        if (taken[s]) continue;
+        L.push((int)((c >> 16) & 0x1FFu), (int)(c >> 25), s);
+    }
+    const bool acc = L.best <= OSG_TH_HIGH && !(L.bl == L.sl && (float)L.best > A.nnratio * (float)L.second);
+    const bool skip_r = L.best <= OSG_TH_HIGH && !acc;
+    res.l = acc ? L.bslot : -1;
+    if (em < e1 && !skip_r) {
+        int own = -1;
+        bool own_blocked = false;
+        if (res.l >= 0) {
+            const int t = V.l2r[res.l];
+            if (t != -1) {
+                own = t + A.nleft;
+                own_blocked = V.obs[q] != 0;
+            }
+        }
+        for (int e = em; e < e1; e++) {
+            const uint32_t c = V.cands[e];
+            const int s = (int)(c & 0xFFFFu);
+            if (s == own ? own_blocked : taken[s] != 0) continue;
+            R.push((int)((c >> 16) & 0x1FFu), (int)(c >> 25), s);
+        }
+        const bool accr = R.best <= OSG_TH_HIGH && !(R.bl == R.sl && (float)R.best > A.nnratio * (float)R.second);
+        res.r = accr ? R.bslot : -1;
+    }
+    return res;
+}
+
 __device__ __forceinline__ QRes load_res(const MatchArgs &A, int q)
 {
     return QRes{A.q_res[2 * q], A.q_res[2 * q + 1]};
@@ -820,7 +864,44 @@ __global__ __launch_bounds__(MT) void k_match(const MatchArgs *__restrict__ args
         }
         serial = __syncthreads_or(need);
         if (serial) {
-            if (tid == 0) {
+            // The staged grid region is free after the fill phase: when the walk's inputs fit, they
+            // are copied there (all threads), so the one-thread walk reads LDS instead of a chain of
+            // dependent global loads per query.
+            const int nright = NS - A.nleft;
+            const size_t o_mid = 4 * ((size_t)nq + 1), o_l2r = o_mid + 4 * (size_t)nq;
+            const size_t o_r2l = o_l2r + 4 * (size_t)A.nleft, o_c = o_r2l + 4 * (size_t)nright;
+            const size_t o_obs = o_c + 4 * (size_t)total, lds_need = o_obs + (size_t)nq;
+            if (STAGED && A.l2r && A.r2l && lds_need <= (size_t)A.lds_free) {
+                char *fr = (char *)(removedS + ((NS + 15) & ~15));
+                SerialLds V{(const int *)fr, (const int *)(fr + o_mid), (const int *)(fr + o_l2r),
+                            (const int *)(fr + o_r2l), (const uint32_t *)(fr + o_c), (const uint8_t *)(fr + o_obs)};
+                for (int i = tid; i <= nq; i += MT) ((int *)fr)[i] = A.q_off[i];
+                for (int i = tid; i < nq; i += MT) {
+                    ((int *)(fr + o_mid))[i] = A.q_mid[i];
+                    ((uint8_t *)(fr + o_obs))[i] = A.q_has_obs[i];
+                }
+                for (int i = tid; i < A.nleft; i += MT) ((int *)(fr + o_l2r))[i] = A.l2r[i];
+                for (int i = tid; i < nright; i += MT) ((int *)(fr + o_r2l))[i] = A.r2l[i];
+                for (int i = tid; i < total; i += MT) ((uint32_t *)(fr + o_c))[i] = A.cands[i];
+                __syncthreads();
+                if (tid == 0) {
+                    for (int q = 0; q < nq; q++) {
+                        const QRes r = eval_mps_lds(A, V, q, taken0);
+                        store_res(A, q, r);
+                        const uint8_t o = V.obs[q];
+                        if (r.l >= 0) {
+                            taken0[r.l] = o;
+                            const int t = V.l2r[r.l];
+                            if (t != -1) taken0[t + A.nleft] = o;
+                        }
+                        if (r.r >= 0) {
+                            const int t = V.r2l[r.r - A.nleft];
+                            if (t != -1) taken0[t] = o;
+                            taken0[r.r] = o;
+                        }
+                    }
+                }
+            } else if (tid == 0) {
                 for (int q = 0; q < nq; q++) {
                     const QRes r = eval_query<MODE>(A, q, [&](int s) { return taken0[s] != 0; });
                     store_res(A, q, r);
@@ -1040,6 +1121,7 @@ int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_
         A.slot_mp = (GLOBAL int32_t *)(dev_io + status_bytes) + slot_off[b];
         A.out_q = (GLOBAL int32_t *)(dev_io + io_in_bytes) + q_base[b];
     }
+    for (int b = 0; b < B; b++) P[b].A.lds_free = (int)(lds - match_lds_bytes(P[b].A.n_slots));
     std::vector<size_t> cap(B), cand_off(B + 1);
     for (int b = 0; b < B; b++) cap[b] = std::max<size_t>((size_t)P[b].A.nq * 32, 1024);
     std::vector<int32_t> st((size_t)STATUS_INTS * B);
