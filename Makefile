@@ -15,7 +15,7 @@ HIPFLAGS += -DOSG_POSE_PROF
 endif
 HDRS = include/osg.h include/osg_ba.h $(CSRC)/osg_internal.h
 
-OBJS = $(OBJDIR)/runtime.o $(OBJDIR)/hamming.o $(OBJDIR)/match.o $(OBJDIR)/pose.o $(OBJDIR)/ba.o $(OBJDIR)/dbow.o $(OBJDIR)/fuse.o $(OBJDIR)/triang.o $(OBJDIR)/desc.o $(OBJDIR)/sim3.o $(OBJDIR)/init.o $(OBJDIR)/stereo.o $(OBJDIR)/orb.o $(OBJDIR)/fast.o
+OBJS = $(OBJDIR)/runtime.o $(OBJDIR)/hamming.o $(OBJDIR)/match.o $(OBJDIR)/pose.o $(OBJDIR)/ba.o $(OBJDIR)/dbow.o $(OBJDIR)/fuse.o $(OBJDIR)/triang.o $(OBJDIR)/desc.o $(OBJDIR)/sim3.o $(OBJDIR)/init.o $(OBJDIR)/stereo.o $(OBJDIR)/orb.o $(OBJDIR)/fast.o $(OBJDIR)/pyramid.o
 
 all: $(LIB) oracle
 
@@ -57,6 +57,9 @@ $(OBJDIR)/orb.o: $(CSRC)/orb.hip $(HDRS) $(CSRC)/match_common.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(EXACT) -c $< -o $@
 
 $(OBJDIR)/fast.o: $(CSRC)/fast.hip $(HDRS) $(CSRC)/match_common.h $(CSRC)/octree.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) $(EXACT) -c $< -o $@
+
+$(OBJDIR)/pyramid.o: $(CSRC)/pyramid.hip $(HDRS) $(CSRC)/match_common.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(EXACT) -c $< -o $@
 
 $(LIB): $(OBJS)

@@ -458,8 +458,8 @@ int osg_compute_distinctive_descriptors_dev(osg_ctx *ctx, const void *d_desc, co
  * computeOrientation / IC_Angle (ref:src/ORBextractor.cc:89-136, 585-597) on mvImagePyramid[level] and
  * computeDescriptors / computeOrbDescriptor (ref:src/ORBextractor.cc:148-208, 1534-1545) on the
  * GaussianBlur'd level (ref:src/ORBextractor.cc:1628-1652), for keypoints in level coordinates (before
- * :1663-1667 scales them to level 0), e.g. from osg_orb_detect (b9).  The 7x7 Gaussian blur stays
- * with the caller (OpenCV).  umax: the extractor's umax (HALF_PATCH_SIZE + 1 = 16 entries, each
+ * :1663-1667 scales them to level 0), e.g. from osg_orb_detect (b9).  The 7x7 Gaussian blur is
+ * the caller's (OpenCV) or osg_orb_pyramid's (b10).  umax: the extractor's umax (HALF_PATCH_SIZE + 1 = 16 entries, each
  * <= 15); pattern: its 512 points (ORBextractor::pattern) as (x, y) int pairs.  The orientation box
  * (+-15 around the rounded centre) must lie inside the raw level, else OSG_E_INVALID.  The blurred
  * level is read as the reference's continuous clone (workingMat = mvImagePyramid[level].clone(),
@@ -501,6 +501,30 @@ int osg_orb_detect(osg_ctx *ctx, const osg_image_pyramid *raw, int32_t ini_th_fa
  * Returns the count (no context, no GPU). */
 int osg_debug_distribute_oct_tree(const float *keys4, int32_t nk, int32_t minX, int32_t maxX, int32_t minY,
                                   int32_t maxY, int32_t N, float *out4, int32_t cap);
+
+/* ---- b10: ORBextractor::ComputePyramid + the GaussianBlur of operator() -----------------------------
+ * ComputePyramid (ref:src/ORBextractor.cc:1692-1743): level l is cvRound((float)cols *
+ * mvInvScaleFactor[l]) x cvRound((float)rows * ...), level 0 the image, level l >= 1 cv::resize
+ * (INTER_LINEAR) of level l - 1; each level with a copyMakeBorder(EDGE_THRESHOLD = 19,
+ * BORDER_REFLECT_101) border around it.  With blur, also each level's GaussianBlur(Size(7, 7), 2, 2,
+ * BORDER_REFLECT_101) as operator() computes it on the level's clone (:1628-1636).  Both are OpenCV
+ * calls (not in the reference tree): their 8-bit fixed-point algorithms are restated (OpenCV 4.5+,
+ * no IPP; see oracle/oracle_pyramid.c), so parity with OpenCV itself is unpinned.
+ * osg_orb_pyramid_layout (host only, no context): the level sizes and the byte offsets of each
+ * bordered level ((rows + 38) x (cols + 38), row step cols + 38; mvImagePyramid[l] is the ROI at
+ * (19, 19)) and each blurred level (rows x cols, step cols) in one buffer; returns its size in
+ * bytes, or OSG_E_INVALID.  osg_orb_pyramid fills such a device buffer (dev_out, dev_bytes) from a
+ * host image (image_on_device = 0; any row step) or a device one, on the context's stream, and
+ * returns when it is complete.  The levels then feed osg_orb_detect (raw), osg_orb_describe (raw +
+ * blurred) and osg_compute_stereo_matches as on_device pyramids.  n_levels <= 32. */
+int64_t osg_orb_pyramid_layout(int32_t rows, int32_t cols, int32_t n_levels, const float *inv_scale_factors,
+                               int32_t *level_rows, int32_t *level_cols, int64_t *bordered_offset,
+                               int64_t *blurred_offset);
+int osg_orb_pyramid(osg_ctx *ctx, const uint8_t *image, int32_t rows, int32_t cols, int32_t step,
+                    int32_t image_on_device, int32_t n_levels, const float *inv_scale_factors, uint8_t *dev_out,
+                    int64_t dev_bytes, int32_t blur);
+/* Diagnostics: the 7-tap fixed-point kernel (8 fraction bits) osg_orb_pyramid blurs with. */
+void osg_debug_gaussian_kernel7(int32_t *k7);
 
 /* Diagnostics of the last search call on this context (summed / maxed over a batch): out[0]
  * candidates enumerated, out[1] Jacobi rounds, out[2] problems whose greedy was redone serially (a5 on a two-camera rig when a

@@ -78,6 +78,16 @@ int oracle_orb_detect(const osg_image_pyramid *P, int ini_th, int min_th, const 
                       const float *scale_factors, int cap, float *x, float *y, float *response, float *size,
                       int32_t *level_start);
 
+/* ORBextractor::ComputePyramid + the GaussianBlur of operator() (oracle_pyramid.c): the level sizes
+ * and the byte offsets of each bordered level ((rows + 38) x (cols + 38), the ROI at (19, 19)) and
+ * each blurred level (rows x cols) in one buffer; returns its size.  oracle_orb_pyramid fills such a
+ * buffer from a host image (blur = 0: the bordered levels only) and returns the size, or -1. */
+int64_t oracle_pyramid_layout(int32_t rows, int32_t cols, int32_t n_levels, const float *inv_scale, int32_t *lrows,
+                              int32_t *lcols, int64_t *bordered_off, int64_t *blurred_off);
+void oracle_gaussian_kernel7(int32_t k[7]);
+int64_t oracle_orb_pyramid(const uint8_t *image, int32_t rows, int32_t cols, int32_t step, int32_t n_levels,
+                           const float *inv_scale, uint8_t *out, int32_t blur);
+
 /* bundle adjustment (oracle_ba.c) */
 double oracle_ref_pow3(double t);  /* the reference's libm calls, correctly rounded */
 double oracle_ref_sin(double x);

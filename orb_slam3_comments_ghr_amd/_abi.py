@@ -190,7 +190,7 @@ EXPORTS = [
     "osg_search_by_projection_sim3", "osg_search_by_projection_sim3_batch", "osg_search_by_sim3",
     "osg_search_for_initialization", "osg_search_for_initialization_batch",
     "osg_compute_stereo_matches", "osg_compute_stereo_matches_batch", "osg_orb_describe", "osg_orb_detect",
-    "osg_debug_distribute_oct_tree",
+    "osg_debug_distribute_oct_tree", "osg_orb_pyramid_layout", "osg_orb_pyramid", "osg_debug_gaussian_kernel7",
 ]
 
 
@@ -264,6 +264,11 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.osg_compute_stereo_matches_batch.argtypes = [vp, vp, i32, vp, vp, vp]
     lib.osg_debug_distribute_oct_tree.argtypes = [vp, i32, i32, i32, i32, i32, i32, vp, i32]
     lib.osg_orb_detect.argtypes = [vp, C.POINTER(OsgImagePyramid), i32, i32, vp, vp, i32, vp, vp, vp, vp, vp]
+    lib.osg_orb_pyramid_layout.argtypes = [i32, i32, i32, vp, vp, vp, vp, vp]
+    lib.osg_orb_pyramid_layout.restype = C.c_int64
+    lib.osg_orb_pyramid.argtypes = [vp, vp, i32, i32, i32, i32, i32, vp, vp, C.c_int64, i32]
+    lib.osg_debug_gaussian_kernel7.argtypes = [vp]
+    lib.osg_debug_gaussian_kernel7.restype = None
     lib.osg_orb_describe.argtypes = [vp, C.POINTER(OsgImagePyramid), C.POINTER(OsgImagePyramid),
                                      C.POINTER(OsgOrbKeypoints), vp, vp, i32, vp, vp]
     lib.osg_compute_distinctive_descriptors.argtypes = [vp, vp, vp, i32, vp]

@@ -1,8 +1,13 @@
 """Host mirror of ORBextractor's per-keypoint stages on the C ABI (``osg_orb_describe``, include/osg.h
 b8): computeOrientation / IC_Angle (ref:src/ORBextractor.cc:89-136, 585-597) on mvImagePyramid and
 computeDescriptors / computeOrbDescriptor (ref:src/ORBextractor.cc:148-208, 1534-1545) on the blurred
-levels (ref:src/ORBextractor.cc:1628-1652).  The pyramid and the Gaussian blur stay with OpenCV; the
-caller passes the extractor's ``umax`` and ``pattern``.
+levels (ref:src/ORBextractor.cc:1628-1652).  The caller passes the extractor's ``umax`` and
+``pattern``.
+
+ComputePyramid + the per-level GaussianBlur (``osg_orb_pyramid``, include/osg.h b10; OpenCV's
+fixed-point resize / blur restated, parity with OpenCV itself unpinned):
+
+    P = ComputePyramid(ctx, image, inv_scale_factors(8, 1.2))     # P.raw, P.blurred on the GPU
 
 ComputeKeyPointsOctTree (``osg_orb_detect``, include/osg.h b9): FAST per W = 35 cell with
 iniThFAST / minThFAST and DistributeOctTree down to mnFeaturesPerLevel (ref:src/ORBextractor.cc:
@@ -24,7 +29,7 @@ import math
 
 import numpy as np
 
-from . import Context, _abi
+from . import Context, _abi, load_library
 from .stereo import ImagePyramid
 
 HALF_PATCH_SIZE = 15
@@ -136,6 +141,68 @@ def ORBDetect(ctx: Context, raw, n_features, scales, ini_th: int = 20, min_th: i
                                          scales.ctypes.data, cap, x.ctypes.data, y.ctypes.data, resp.ctypes.data,
                                          size.ctypes.data, ls.ctypes.data), "osg_orb_detect")
     return x[:n], y[:n], resp[:n], size[:n], ls
+
+
+def inv_scale_factors(n_levels: int = 8, factor: float = 1.2) -> np.ndarray:
+    """mvInvScaleFactor: 1.0f / mvScaleFactor[i] in float (ref:src/ORBextractor.cc ORBextractor())."""
+    return (np.float32(1) / scale_factors(n_levels, factor)).astype(np.float32)
+
+
+def pyramid_layout(rows: int, cols: int, inv_scale):
+    """Level sizes and byte offsets of ``osg_orb_pyramid``'s buffer (include/osg.h b10): returns
+    (level_rows, level_cols, bordered_offset, blurred_offset, total_bytes)."""
+    inv_scale = np.ascontiguousarray(inv_scale, np.float32)
+    L = inv_scale.size
+    lr, lc = np.zeros(L, np.int32), np.zeros(L, np.int32)
+    bo, bl = np.zeros(L, np.int64), np.zeros(L, np.int64)
+    total = load_library().osg_orb_pyramid_layout(int(rows), int(cols), L, inv_scale.ctypes.data, lr.ctypes.data,
+                                                  lc.ctypes.data, bo.ctypes.data, bl.ctypes.data)
+    if total < 0:
+        raise ValueError(f"osg_orb_pyramid_layout({rows}, {cols}, {L} levels) = {total}")
+    return lr, lc, bo, bl, int(total)
+
+
+class OrbPyramid:
+    """The device buffer ``ComputePyramid`` fills: ``raw`` is mvImagePyramid (ImagePyramid of the ROI
+    views, row step cols + 38), ``bordered`` the whole bordered levels, ``blurred`` the GaussianBlur'd
+    levels (continuous, as the reference's clone) or None."""
+
+    def __init__(self, buffer, lr, lc, bo, bl, blur):
+        E = EDGE_THRESHOLD
+        self.buffer = buffer
+        self.level_rows, self.level_cols = lr, lc
+        self.bordered = [buffer[int(bo[l]):int(bo[l]) + (int(lr[l]) + 2 * E) * (int(lc[l]) + 2 * E)]
+                         .view(int(lr[l]) + 2 * E, int(lc[l]) + 2 * E) for l in range(lr.size)]
+        self.raw = ImagePyramid([b[E:E + int(lr[l]), E:E + int(lc[l])] for l, b in enumerate(self.bordered)])
+        self.blurred = ImagePyramid([buffer[int(bl[l]):int(bl[l]) + int(lr[l]) * int(lc[l])]
+                                     .view(int(lr[l]), int(lc[l])) for l in range(lr.size)]) if blur else None
+
+
+def ComputePyramid(ctx: Context, image, inv_scale, blur: bool = True, out=None) -> OrbPyramid:
+    """ORBextractor::ComputePyramid (ref:src/ORBextractor.cc:1692-1743) and, with blur, the per-level
+    GaussianBlur(7 x 7, 2, 2, BORDER_REFLECT_101) of operator() (:1628-1636), on the GPU
+    (``osg_orb_pyramid``, include/osg.h b10).  image: 8-bit numpy array (any row step) or a uint8
+    torch tensor on the GPU; inv_scale: mvInvScaleFactor.  out: a reusable uint8 device buffer of at
+    least the layout's size."""
+    import torch
+
+    on_device = hasattr(image, "data_ptr")
+    if on_device:
+        assert image.is_cuda and image.dtype == torch.uint8 and image.dim() == 2 and image.stride(1) == 1
+        rows, cols, step, ptr = image.shape[0], image.shape[1], image.stride(0), image.data_ptr()
+        torch.cuda.synchronize(image.device)  # the kernels run on the context's own stream
+    else:
+        assert image.dtype == np.uint8 and image.ndim == 2 and image.strides[1] == 1, "8-bit rows"
+        rows, cols, step, ptr = image.shape[0], image.shape[1], image.strides[0], image.ctypes.data
+    inv_scale = np.ascontiguousarray(inv_scale, np.float32)
+    lr, lc, bo, bl, total = pyramid_layout(rows, cols, inv_scale)
+    if out is None or out.numel() < total:
+        out = torch.empty(total, dtype=torch.uint8, device=image.device if on_device else "cuda")
+        torch.cuda.synchronize(out.device)
+    ctx.check(ctx.lib.osg_orb_pyramid(ctx.handle, ptr, rows, cols, step, int(on_device), inv_scale.size,
+                                      inv_scale.ctypes.data, out.data_ptr(), out.numel(), int(bool(blur))),
+              "osg_orb_pyramid")
+    return OrbPyramid(out, lr, lc, bo, bl, blur)
 
 
 def synth_fast_pyramid(rng, width=752, height=480, n_levels=8, factor=1.2, n_blobs=400):

@@ -83,6 +83,12 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.oracle_fast.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp]
     lib.oracle_orb_detect.argtypes = [C.POINTER(OsgImagePyramid), C.c_int, C.c_int, vp, vp, C.c_int, vp, vp, vp,
                                       vp, vp]
+    lib.oracle_pyramid_layout.argtypes = [C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp]
+    lib.oracle_pyramid_layout.restype = C.c_int64
+    lib.oracle_gaussian_kernel7.argtypes = [vp]
+    lib.oracle_gaussian_kernel7.restype = None
+    lib.oracle_orb_pyramid.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, C.c_int]
+    lib.oracle_orb_pyramid.restype = C.c_int64
     return lib
 
 
@@ -274,3 +280,30 @@ def orb_detect(oracle, levels, n_features, scales, ini_th=20, min_th=7, cap=2000
                                  x.ctypes.data, y.ctypes.data, r.ctypes.data, s.ctypes.data, ls.ctypes.data)
     assert n >= 0
     return x[:n], y[:n], r[:n], s[:n], ls
+
+
+def orb_pyramid(oracle, image, inv_scale, blur=True):
+    """ComputePyramid (+ GaussianBlur) through the oracle: (buffer uint8[total], level_rows, level_cols,
+    bordered_offset, blurred_offset) in osg_orb_pyramid's layout."""
+    image = np.asarray(image)
+    assert image.dtype == np.uint8 and image.strides[1] == 1
+    inv = np.ascontiguousarray(inv_scale, np.float32)
+    L = inv.size
+    lr, lc = np.zeros(L, np.int32), np.zeros(L, np.int32)
+    bo, bl = np.zeros(L, np.int64), np.zeros(L, np.int64)
+    total = oracle.oracle_pyramid_layout(image.shape[0], image.shape[1], L, inv.ctypes.data, lr.ctypes.data,
+                                         lc.ctypes.data, bo.ctypes.data, bl.ctypes.data)
+    buf = np.zeros(total, np.uint8)
+    got = oracle.oracle_orb_pyramid(image.ctypes.data, image.shape[0], image.shape[1], image.strides[0], L,
+                                    inv.ctypes.data, buf.ctypes.data, int(bool(blur)))
+    assert got == total
+    return buf, lr, lc, bo, bl
+
+
+def pyramid_levels(buf, lr, lc, bo, bl, E=19):
+    """(bordered levels, ROI levels, blurred levels) as numpy views of an orb_pyramid buffer."""
+    bordered = [buf[bo[l]:bo[l] + (lr[l] + 2 * E) * (lc[l] + 2 * E)].reshape(lr[l] + 2 * E, lc[l] + 2 * E)
+                for l in range(lr.size)]
+    roi = [b[E:E + lr[l], E:E + lc[l]] for l, b in enumerate(bordered)]
+    blurred = [buf[bl[l]:bl[l] + lr[l] * lc[l]].reshape(lr[l], lc[l]) for l in range(lr.size)]
+    return bordered, roi, blurred

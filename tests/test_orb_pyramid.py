@@ -1,0 +1,167 @@
+"""ORBextractor::ComputePyramid (ref:src/ORBextractor.cc:1692-1743) and the per-level GaussianBlur of
+operator() (:1628-1636).  CPU: the C oracle pinned by the numpy restatement (tests/pyref_pyramid.py)
+and by known answers (the fixed-point kernel [18 34 48 56 48 34 18], constant images, level sizes);
+the product's host-side layout and kernel equal the oracle's.  GPU: osg_orb_pyramid bit-exact with the
+oracle (every bordered level, every blurred level) on EuRoC / TUM sizes, odd and tiny sizes, host and
+device images with a row step, blur on and off; and the whole extractor chain pyramid -> FAST +
+DistributeOctTree -> IC_Angle + rBRIEF on the GPU equal to the oracle's chain.  cv::resize and
+cv::GaussianBlur are OpenCV's (not in the reference tree): parity with OpenCV itself is unpinned."""
+import numpy as np
+import pytest
+
+from orb_slam3_comments_ghr_amd import load_library, orb
+from tests import oracle_calls as oc
+from tests import pyref_pyramid as pp
+
+KERNEL = [18, 34, 48, 56, 48, 34, 18]
+
+
+def _image(seed, h, w, n_blobs=300):
+    rng = np.random.default_rng(seed)
+    return orb.synth_fast_pyramid(rng, width=w, height=h, n_levels=1, n_blobs=n_blobs)[0]
+
+
+def test_gaussian_kernel(oracle):
+    import ctypes as C
+    k = np.zeros(7, np.int32)
+    oracle.oracle_gaussian_kernel7(k.ctypes.data)
+    assert k.tolist() == KERNEL and k.sum() == 256
+    assert pp.gaussian_kernel7() == KERNEL
+    kp = np.zeros(7, np.int32)
+    load_library().osg_debug_gaussian_kernel7(kp.ctypes.data_as(C.c_void_p))
+    assert kp.tolist() == KERNEL
+
+
+@pytest.mark.parametrize("rows,cols,levels,factor", [(480, 752, 8, 1.2), (480, 640, 8, 1.2), (512, 512, 4, 2.0),
+                                                     (61, 97, 8, 1.2), (1, 1, 1, 1.2)])
+def test_layout_matches_oracle(oracle, rows, cols, levels, factor):
+    inv = orb.inv_scale_factors(levels, factor)
+    lr, lc, bo, bl, total = orb.pyramid_layout(rows, cols, inv)
+    img = np.zeros((rows, cols), np.uint8)
+    _, olr, olc, obo, obl = oc.orb_pyramid(oracle, img, inv)
+    assert (lr == olr).all() and (lc == olc).all() and (bo == obo).all() and (bl == obl).all()
+    assert lc.tolist() == [int(np.rint(np.float32(cols) * s)) for s in inv]
+    if (rows, cols) == (480, 752):
+        assert lc.tolist() == [752, 627, 522, 435, 363, 302, 252, 210]
+        assert lr.tolist() == [480, 400, 333, 278, 231, 193, 161, 134]
+
+
+def test_layout_rejects(oracle):
+    with pytest.raises(ValueError):
+        orb.pyramid_layout(480, 752, np.array([1.0, 1.5], np.float32))  # upscaling: not a pyramid
+    with pytest.raises(ValueError):
+        orb.pyramid_layout(0, 752, orb.inv_scale_factors(2))
+
+
+def test_vector_columns():
+    assert [pp.vector_columns(w) for w in (7, 8, 9, 16, 17, 24, 25, 26, 522, 627)] == [0, 0, 8, 16, 16, 16, 24, 24,
+                                                                                      520, 624]
+
+
+@pytest.mark.parametrize("shape,levels,factor,seed", [((480, 752), 8, 1.2, 1), ((480, 640), 8, 1.2, 2),
+                                                      ((200, 330), 4, 2.0, 3), ((77, 101), 3, 1.2, 4)])
+def test_oracle_vs_numpy(oracle, shape, levels, factor, seed):
+    img = _image(seed, *shape)
+    inv = orb.inv_scale_factors(levels, factor)
+    buf, lr, lc, bo, bl = oc.orb_pyramid(oracle, img, inv)
+    ob, orr, obl = oc.pyramid_levels(buf, lr, lc, bo, bl)
+    nb, nr, nbl = pp.pyramid(img, inv)
+    for l in range(levels):
+        assert np.array_equal(ob[l], nb[l]), f"bordered level {l}"
+        assert np.array_equal(obl[l], nbl[l]), f"blurred level {l}"
+    # a resize that rounds differently in the two vertical formulas somewhere (the split matters)
+    if shape == (480, 752):
+        assert any(pp.vector_columns(int(c)) < int(c) for c in lc[1:])
+
+
+def test_constant_and_ramp(oracle):
+    inv = orb.inv_scale_factors(8, 1.2)
+    buf, lr, lc, bo, bl = oc.orb_pyramid(oracle, np.full((480, 752), 173, np.uint8), inv)
+    assert (buf[:bl[0]][buf[:bl[0]] != 0] == 173).all()
+    b, r, z = oc.pyramid_levels(buf, lr, lc, bo, bl)
+    assert all((x == 173).all() for x in b) and all((x == 173).all() for x in z)
+    # border: reflect-101 of the ROI (gfedcb|abcdefgh|gfedcba)
+    ramp = np.tile(np.arange(60, dtype=np.uint8), (40, 1))
+    buf, lr, lc, bo, bl = oc.orb_pyramid(oracle, ramp, np.ones(1, np.float32))
+    b, _, _ = oc.pyramid_levels(buf, lr, lc, bo, bl)
+    assert b[0][19, :19].tolist() == list(range(19, 0, -1))
+    assert b[0][19, 19 + 60:].tolist() == list(range(58, 39, -1))
+
+
+# ------------------------------------------------------------------------------------------------ GPU
+
+def _gpu_vs_oracle(ctx, oracle, img, inv, blur=True, device_image=False):
+    import torch
+    src = img
+    if device_image:
+        t = torch.zeros((img.shape[0], img.shape[1] + 29), dtype=torch.uint8, device="cuda")
+        t[:, 5:5 + img.shape[1]] = torch.from_numpy(np.ascontiguousarray(img)).cuda()
+        src = t[:, 5:5 + img.shape[1]]
+    P = orb.ComputePyramid(ctx, src, inv, blur=blur)
+    got = P.buffer.cpu().numpy()
+    want, lr, lc, bo, bl = oc.orb_pyramid(oracle, np.ascontiguousarray(img), inv, blur=blur)
+    gb, gr, gz = oc.pyramid_levels(got, lr, lc, bo, bl)
+    wb, wr, wz = oc.pyramid_levels(want, lr, lc, bo, bl)
+    for l in range(inv.size):
+        assert np.array_equal(gb[l], wb[l]), f"bordered level {l}: {np.argwhere(gb[l] != wb[l])[:5]}"
+        if blur:
+            assert np.array_equal(gz[l], wz[l]), f"blurred level {l}: {np.argwhere(gz[l] != wz[l])[:5]}"
+    return P, wr, wz
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,levels,factor,seed", [((480, 752), 8, 1.2, 1), ((480, 640), 8, 1.2, 2),
+                                                      ((512, 512), 4, 2.0, 3), ((61, 97), 8, 1.2, 4),
+                                                      ((1024, 1280), 8, 1.2, 5), ((23, 24), 3, 1.2, 6)])
+def test_gpu_pyramid(ctx, oracle, shape, levels, factor, seed):
+    _gpu_vs_oracle(ctx, oracle, _image(seed, *shape, n_blobs=max(4, shape[0] * shape[1] // 1200)),
+                   orb.inv_scale_factors(levels, factor))
+
+
+@pytest.mark.gpu
+def test_gpu_pyramid_noise_device_image_no_blur(ctx, oracle):
+    rng = np.random.default_rng(7)
+    img = rng.integers(0, 256, (480, 752), dtype=np.uint8)
+    inv = orb.inv_scale_factors(8, 1.2)
+    _gpu_vs_oracle(ctx, oracle, img, inv, device_image=True)
+    _gpu_vs_oracle(ctx, oracle, img, inv, blur=False)
+    # host image with a row step
+    wide = rng.integers(0, 256, (300, 480), dtype=np.uint8)
+    _gpu_vs_oracle(ctx, oracle, wide[:, 40:440], inv)
+
+
+@pytest.mark.gpu
+def test_gpu_pyramid_errors(ctx):
+    import torch
+    from orb_slam3_comments_ghr_amd import OsgError
+    img = np.zeros((480, 752), np.uint8)
+    inv = orb.inv_scale_factors(8, 1.2)
+    small = torch.empty(1000, dtype=torch.uint8, device="cuda")
+    with pytest.raises(OsgError):
+        ctx.check(ctx.lib.osg_orb_pyramid(ctx.handle, img.ctypes.data, 480, 752, 752, 0, 8, inv.ctypes.data,
+                                          small.data_ptr(), small.numel(), 1), "osg_orb_pyramid")
+    bad = np.array([1.0, 1.25], np.float32)
+    with pytest.raises(OsgError):
+        ctx.check(ctx.lib.osg_orb_pyramid(ctx.handle, img.ctypes.data, 480, 752, 752, 0, 2, bad.ctypes.data,
+                                          small.data_ptr(), small.numel(), 1), "osg_orb_pyramid")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,seed", [((480, 752), 11), ((480, 640), 12)])
+def test_gpu_extractor_chain(ctx, oracle, shape, seed):
+    """ORBextractor::operator() minus the final level-0 scaling (:1663-1667): the GPU pyramid feeds
+    the GPU detector and descriptor, the oracle's pyramid feeds the oracle's; all outputs equal."""
+    img = _image(seed, *shape, n_blobs=500)
+    inv, sc = orb.inv_scale_factors(8, 1.2), orb.scale_factors(8, 1.2)
+    nf = orb.features_per_level(1000, 8, 1.2)
+    P, roi, blurred = _gpu_vs_oracle(ctx, oracle, img, inv)
+    gx, gy, gr, gs, gls = orb.ORBDetect(ctx, P.raw, nf, sc)
+    wx, wy, wr, ws, wls = oc.orb_detect(oracle, roi, nf, sc)
+    assert (gls == wls).all() and np.array_equal(gx, wx) and np.array_equal(gy, wy)
+    assert np.array_equal(gr, wr) and np.array_equal(gs, ws)
+    assert len(gx) > 500
+    level = np.repeat(np.arange(8, dtype=np.int32), np.diff(gls))
+    pattern = orb.synth_pattern(np.random.default_rng(seed))
+    ga, gd, gbad = orb.ORBDescribe(ctx, P.raw, P.blurred, gx, gy, level, pattern)
+    wa, wd, wbad = oc.orb_describe(oracle, roi, blurred, wx, wy, level, pattern)
+    assert np.array_equal(ga, wa) and np.array_equal(gd, wd) and gbad == wbad
