@@ -24,6 +24,7 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "oracle.h"
@@ -168,17 +169,35 @@ int64_t oracle_orb_pyramid(const uint8_t *image, int32_t rows, int32_t cols, int
         const int w = lc[l], h = lr[l], bstep = w + 2 * EDGE;
         const uint8_t *roi = out + bo[l] + (int64_t)EDGE * bstep + EDGE;
         uint8_t *o = out + bl[l];
-        for (int y = 0; y < h; y++)
+        /* rows first: ufixedpoint16 sums (<= 255 * 256, exact) of the whole level */
+        uint16_t *H = (uint16_t *)malloc(sizeof(uint16_t) * (size_t)w * h);
+        int *xi = (int *)malloc(sizeof(int) * (size_t)(w + 6));
+        if (!H || !xi) {
+            free(H);
+            free(xi);
+            return -1;
+        }
+        for (int j = 0; j < w + 6; j++) xi[j] = reflect101(j - 3, w);
+        for (int y = 0; y < h; y++) {
+            const uint8_t *r = roi + (int64_t)y * bstep;
+            for (int x = 0; x < w; x++) {
+                uint32_t s = 0;
+                for (int t = 0; t < 7; t++) s += (uint32_t)r[xi[x + t]] * (uint32_t)k[t];
+                H[(size_t)y * w + x] = (uint16_t)s;
+            }
+        }
+        /* then columns (ufixedpoint32, exact) and one rounding */
+        for (int y = 0; y < h; y++) {
+            const uint16_t *hr[7];
+            for (int t = 0; t < 7; t++) hr[t] = H + (size_t)reflect101(y + t - 3, h) * w;
             for (int x = 0; x < w; x++) {
                 uint32_t acc = 0;
-                for (int i = 0; i < 7; i++) {
-                    const uint8_t *r = roi + (int64_t)reflect101(y + i - 3, h) * bstep;
-                    uint32_t hsum = 0; /* ufixedpoint16: exact */
-                    for (int j = 0; j < 7; j++) hsum += (uint32_t)r[reflect101(x + j - 3, w)] * (uint32_t)k[j];
-                    acc += hsum * (uint32_t)k[i];
-                }
+                for (int t = 0; t < 7; t++) acc += (uint32_t)hr[t][x] * (uint32_t)k[t];
                 o[(int64_t)y * w + x] = (uint8_t)((acc + (1u << 15)) >> 16);
             }
+        }
+        free(H);
+        free(xi);
     }
     return total;
 }

@@ -178,19 +178,21 @@ class OrbPyramid:
                                      .view(int(lr[l]), int(lc[l])) for l in range(lr.size)]) if blur else None
 
 
-def ComputePyramid(ctx: Context, image, inv_scale, blur: bool = True, out=None) -> OrbPyramid:
+def ComputePyramid(ctx: Context, image, inv_scale, blur: bool = True, out=None, sync: bool = True) -> OrbPyramid:
     """ORBextractor::ComputePyramid (ref:src/ORBextractor.cc:1692-1743) and, with blur, the per-level
     GaussianBlur(7 x 7, 2, 2, BORDER_REFLECT_101) of operator() (:1628-1636), on the GPU
     (``osg_orb_pyramid``, include/osg.h b10).  image: 8-bit numpy array (any row step) or a uint8
     torch tensor on the GPU; inv_scale: mvInvScaleFactor.  out: a reusable uint8 device buffer of at
-    least the layout's size."""
+    least the layout's size.  sync=False skips the device synchronisation before the call (the caller
+    knows a device image is complete)."""
     import torch
 
     on_device = hasattr(image, "data_ptr")
     if on_device:
         assert image.is_cuda and image.dtype == torch.uint8 and image.dim() == 2 and image.stride(1) == 1
         rows, cols, step, ptr = image.shape[0], image.shape[1], image.stride(0), image.data_ptr()
-        torch.cuda.synchronize(image.device)  # the kernels run on the context's own stream
+        if sync:
+            torch.cuda.synchronize(image.device)  # the kernels run on the context's own stream
     else:
         assert image.dtype == np.uint8 and image.ndim == 2 and image.strides[1] == 1, "8-bit rows"
         rows, cols, step, ptr = image.shape[0], image.shape[1], image.strides[0], image.ctypes.data

@@ -77,3 +77,10 @@ def run(ctx, oracle):
     gd, rd = orb.ORBDetect(ctx, levels, nf, sc), oc.orb_detect(oracle, levels, nf, sc)
     if not all(np.array_equal(g, r) for g, r in zip(gd, rd)):
         raise AssertionError("ORB keypoint detection mismatch vs oracle")
+    # ORBextractor::ComputePyramid + GaussianBlur: every bordered and blurred level byte for byte
+    img = levels[0]
+    inv = orb.inv_scale_factors(3, 1.2)
+    P = orb.ComputePyramid(ctx, img, inv)
+    want = oc.orb_pyramid(oracle, img, inv)[0]
+    if not np.array_equal(P.buffer.cpu().numpy()[:want.size], want):
+        raise AssertionError("ORB pyramid / blur mismatch vs oracle")
