@@ -883,22 +883,52 @@ __global__ __launch_bounds__(MT) void k_match(const MatchArgs *__restrict__ args
                 for (int i = tid; i < A.nleft; i += MT) ((int *)(fr + o_l2r))[i] = A.l2r[i];
                 for (int i = tid; i < nright; i += MT) ((int *)(fr + o_r2l))[i] = A.r2l[i];
                 for (int i = tid; i < total; i += MT) ((uint32_t *)(fr + o_c))[i] = A.cands[i];
+                int *mark = cur;  // the Jacobi claim array is free now: earliest writer lane per slot
+                for (int i = tid; i < NS; i += MT) mark[i] = INT_BIG;
                 __syncthreads();
-                if (tid == 0) {
-                    for (int q = 0; q < nq; q++) {
-                        const QRes r = eval_mps_lds(A, V, q, taken0);
-                        store_res(A, q, r);
-                        const uint8_t o = V.obs[q];
+                // Wave 0 walks the queries 64 at a time, speculatively: every lane evaluates its query
+                // on the slot state at the batch start and marks the slots it writes; lane i's result
+                // is the sequential one unless a lane j < i wrote one of i's candidate slots.  Lanes
+                // below the first such conflict commit, their writes applied in lane order (a slot's
+                // state is its last writer's); the next batch starts at the conflict.  Lane 0 always
+                // commits, so the walk advances.
+                if (tid < 64) {
+                    const int ln = tid;
+                    for (int qb = 0; qb < nq;) {
+                        const int q = qb + ln;
+                        const bool valid = q < nq;
+                        QRes r{-1, -1};
+                        if (valid) r = eval_mps_lds(A, V, q, taken0);
+                        int ws[4], n = 0;
                         if (r.l >= 0) {
-                            taken0[r.l] = o;
+                            ws[n++] = r.l;
                             const int t = V.l2r[r.l];
-                            if (t != -1) taken0[t + A.nleft] = o;
+                            if (t != -1) ws[n++] = t + A.nleft;
                         }
                         if (r.r >= 0) {
                             const int t = V.r2l[r.r - A.nleft];
-                            if (t != -1) taken0[t] = o;
-                            taken0[r.r] = o;
+                            if (t != -1) ws[n++] = t;
+                            ws[n++] = r.r;
                         }
+                        for (int i = 0; i < n; i++) atomicMin(&mark[ws[i]], ln);
+                        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                        bool conf = false;
+                        if (valid)
+                            for (int e = V.off[q], e1 = V.off[q + 1]; e < e1; e++)
+                                conf |= mark[V.cands[e] & 0xFFFFu] < ln;
+                        const unsigned long long cm = __ballot(conf);
+                        const int nvalid = min(64, nq - qb);
+                        const int first = cm ? min((int)__builtin_ctzll(cm), nvalid) : nvalid;
+                        const uint8_t o = valid ? V.obs[q] : (uint8_t)0;
+                        for (int j = 0; j < first; j++) {
+                            if (ln == j)
+                                for (int i = 0; i < n; i++) taken0[ws[i]] = o;
+                            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                        }
+                        if (ln < first) store_res(A, q, r);
+                        for (int i = 0; i < n; i++) mark[ws[i]] = INT_BIG;
+                        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                        qb += first;
                     }
                 }
             } else if (tid == 0) {

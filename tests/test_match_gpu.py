@@ -149,6 +149,21 @@ def test_search_by_projection_mps_two_cam_paths(ctx, oracle):
     assert True in seen
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_search_by_projection_mps_two_cam_dense_conflicts(ctx, oracle, seed):
+    """The serial redo's 64-query speculative batches under heavy conflicts: few keypoints, many
+    queries on the same slots, so most batches stop early and commit a prefix."""
+    rng = np.random.default_rng(6200 + seed)
+    F = two_cam(rng, 70, 60)
+    Q = fr.synth_mp_queries_two_cam(rng, F, m=900, noise_px=1.0, match_frac=0.95)
+    Q.has_obs[:] = rng.random(len(Q.mp_id)) < 0.5
+    slot_mp, taken = fr.synth_slots(rng, F.n, frac_assigned=0.3, frac_taken=0.5)
+    ref = oc.mps(oracle, F, Q, 0.95, 5.0, False, 20.0, slot_mp, taken)
+    s = slot_mp.copy()
+    n = ORBmatcher(ctx, 0.95).SearchByProjection(F, Q, 5.0, False, 20.0, slot_mp=s, slot_taken=taken)
+    assert_same(f"mps two-cam dense seed {seed}", n, s, *ref)
+
+
 @pytest.mark.parametrize("seed", range(6))
 @pytest.mark.parametrize("th,mono,tlc", [(7.0, False, 0.0), (15.0, True, 0.0), (7.0, False, 1.0), (14.0, False, -1.0)])
 def test_search_by_projection_last_two_cam(ctx, oracle, seed, th, mono, tlc):
