@@ -154,9 +154,10 @@ __host__ __device__ inline SE3 se3_exp(const double *upd)
             }
     } else {
         // sin / cos / pow(theta, 3) of the reference, correctly rounded (exact_math.h)
-        const double st = osgx::sin_ref(theta);
+        double st, ct;
+        osgx::sincos_ref(theta, st, ct);
         const double a = st / theta;
-        const double b = (1 - osgx::cos_ref(theta)) / (theta * theta);
+        const double b = (1 - ct) / (theta * theta);
         const double c = (theta - st) / osgx::cube_rn(theta);
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 3; j++) {

@@ -161,6 +161,69 @@ OSG_HD inline double cos_rn_small(double x)
     }
     return s.h + s.l;
 }
+// sin and cos of one argument at once: the two Horner chains of sin_rn_small / cos_rn_small
+// interleaved in one loop (the same operations on the same values, so the same two results), which
+// lets a latency-bound caller (SE3 exp in the LM loops) overlap them.
+OSG_HD inline void sincos_rn_small(double x, double &sn, double &cs)
+{
+    OSGX_NOCONTRACT
+    const dd cs_[15] = {{1.0, 0.0},
+                        {-0.16666666666666666, -9.25185853854297e-18},
+                        {0.008333333333333333, 1.1564823173178714e-19},
+                        {-0.0001984126984126984, -1.7209558293420705e-22},
+                        {2.7557319223985893e-06, -1.858393274046472e-22},
+                        {-2.505210838544172e-08, 1.448814070935912e-24},
+                        {1.6059043836821613e-10, 1.2585294588752098e-26},
+                        {-7.647163731819816e-13, -7.03872877733453e-30},
+                        {2.8114572543455206e-15, 1.6508842730861433e-31},
+                        {-8.22063524662433e-18, -2.2141894119604265e-34},
+                        {1.9572941063391263e-20, -1.3643503830087908e-36},
+                        {-3.868170170630684e-23, 8.843177655482344e-40},
+                        {6.446950284384474e-26, -1.9330404233703465e-42},
+                        {-9.183689863795546e-29, -1.4303150396787322e-45},
+                        {1.1309962886447716e-31, 1.0498015412959506e-47}};
+    const dd cc_[15] = {{1.0, 0.0},
+                        {-0.5, 0.0},
+                        {0.041666666666666664, 2.3129646346357427e-18},
+                        {-0.001388888888888889, 5.300543954373577e-20},
+                        {2.48015873015873e-05, 2.1511947866775882e-23},
+                        {-2.755731922398589e-07, -2.3767714622250297e-23},
+                        {2.08767569878681e-09, -1.20734505911326e-25},
+                        {-1.1470745597729725e-11, -2.0655512752830745e-28},
+                        {4.779477332387385e-14, 4.399205485834081e-31},
+                        {-1.5619206968586225e-16, -1.1910679660273754e-32},
+                        {4.110317623312165e-19, 1.4412973378659527e-36},
+                        {-8.896791392450574e-22, 7.911402614872376e-38},
+                        {1.6117375710961184e-24, -3.6846573564509766e-41},
+                        {-2.4795962632247976e-27, 1.2953730964765229e-43},
+                        {3.279889237069838e-30, 1.5117542744029879e-46}};
+    const dd x2 = two_prod(x, x);
+    const int K = series_terms(x);
+    dd a = cs_[14], c = cc_[14];
+#pragma unroll
+    for (int k = 13; k >= 0; k--) {
+        if (k == K - 1) {
+            a = cs_[k];
+            c = cc_[k];
+        } else if (k < K - 1) {
+            a = dd_add(dd_mul(a, x2), cs_[k]);
+            c = dd_add(dd_mul(c, x2), cc_[k]);
+        }
+    }
+    const dd r = dd_mul(a, dd{x, 0.0});
+    sn = r.h + r.l;
+    cs = c.h + c.l;
+}
+OSG_HD inline void sincos_ref(double x, double &sn, double &cs)
+{
+    OSGX_NOCONTRACT
+    if (x >= 0.0 && x <= 0.8) {
+        sincos_rn_small(x, sn, cs);
+    } else {
+        sn = sin(x);
+        cs = cos(x);
+    }
+}
 OSG_HD inline double sin_ref(double x)
 {
     OSGX_NOCONTRACT

@@ -26,6 +26,10 @@ int main(int argc, char **argv)
         if (osgx::sin_ref(th) != oracle_ref_sin(th)) bad_sin++;
         if (osgx::cos_ref(th) != oracle_ref_cos(th)) bad_cos++;
         if (osgx::cube_rn(th) != oracle_ref_pow3(th)) bad_cube++;
+        double sn, cs;
+        osgx::sincos_ref(th, sn, cs);  // the fused form the SE3 exp uses
+        if (sn != osgx::sin_ref(th)) bad_sin++;
+        if (cs != osgx::cos_ref(th)) bad_cos++;
         const double t = 2 * (8 * U(g)) - 1;  // 2 rho - 1
         if (osgx::cube_rn(t) != oracle_ref_pow3(t)) bad_cube++;
     }
