@@ -2,7 +2,10 @@
 // GaussianBlur of ORBextractor::operator() (ref:src/ORBextractor.cc:1628-1636) on gfx950, writing
 // straight into one caller-owned device buffer that osg_orb_detect / osg_orb_describe /
 // osg_compute_stereo_matches then read in place.
-//  * k_pyr_level — one launch per level (level l reads level l - 1: the chain is the reference's),
+//  * k_pyr_group (OSG_PYR_FUSED=1) — GROUP = 4 levels per launch, each pixel of level l evaluated from the
+//    last stored level by applying the resize formula recursively (4^D stored pixels for D levels
+//    up), with the previous group's blur tiles in the same launch: 3 launches for 8 levels.
+//  * k_pyr_level (default) — one launch per level (level l reads level l - 1),
 //    one thread per pixel of the bordered level (cols + 38) x (rows + 38).  A border pixel is the
 //    reflect-101 image of an interior one (copyMakeBorder BORDER_REFLECT_101 [+ ISOLATED], :1717,
 //    :1738), so each thread maps its coordinates back into the ROI and evaluates that pixel: level 0
@@ -10,13 +13,14 @@
 //    formula at it — the per-column (sx, sx + 1, 11-bit weights) and per-row tables are OpenCV's,
 //    built on the host with its float/double expressions, and the vertical rounding follows the
 //    columns its 128-bit vector loop covers (see oracle/oracle_pyramid.c for the restated algorithm).
-//  * k_pyr_blur — all levels in one launch over 64 x 16 output tiles: the (70 x 22)-byte source tile
+//  * k_pyr_blur (with k_pyr_level) and the blur parts of k_pyr_group — 64 x 16 output tiles: the (70 x 22)-byte source tile
 //    (reflect-101 at the level edges, as on the reference's continuous clone) and the 22 x 64
 //    horizontal sums stay in LDS; the 7-tap fixed-point kernel [18 34 48 56 48 34 18] / 256 of OpenCV's
 //    bit-exact 8-bit GaussianBlur, rows then columns, every sum exact, one rounding (+2^15) >> 16.
 // Everything is integer arithmetic on bytes: HBM/latency-bound, no MFMA.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -114,6 +118,101 @@ __global__ __launch_bounds__(256) void k_pyr_blur(const BlurArgs A)
 #pragma unroll
         for (int j = 0; j <= 2 * KR; j++) s += (uint32_t)s_h[r + j][c] * (uint32_t)A.k[j];
         A.out[l][(long long)y * w + x] = (uint8_t)((s + (1u << 15)) >> 16);
+    }
+}
+
+// ---- the fused form (default): GROUP levels per launch, each from the last stored level ----------
+// A level-l pixel needs the 2 x 2 level-(l - 1) pixels of its resize tables, so a pixel D levels
+// above the stored one is the same integer formula applied recursively over 4^D stored pixels
+// (D <= GROUP): no value changes, only where it is computed.  Launch k computes level group k and
+// blurs group k - 1 (stored by launch k - 1); a last launch blurs the last group.
+constexpr int GROUP = 4;
+constexpr bool PYR_FUSED_DEFAULT = false;
+constexpr int GMAX = 16;  // levels a fused call handles (the level-wise path takes up to MAX_LEVELS)
+
+struct PyrLevelDev {
+    const int4 *xt, *yt;        // resize tables of this level from the previous one
+    GLOBAL uint8_t *dst;        // bordered level
+    GLOBAL uint8_t *blur_out;   // blurred level
+    int xv, w, h, bstep;
+};
+
+struct GroupArgs {
+    GLOBAL const uint8_t *src;  // the stored level src_level (the image for level 0, else an ROI)
+    int sstep, src_level, n_parts;
+    int k[2 * KR + 1];
+    PyrLevelDev L[GMAX];
+    int part_level[2 * GROUP], part_kind[2 * GROUP], part_tiles_x[2 * GROUP], part_block0[2 * GROUP + 1];
+};
+
+template <int D>
+__device__ __forceinline__ int level_px(const GroupArgs &A, int l, int x, int y)
+{
+    if constexpr (D == 0) {
+        return A.src[(long long)y * A.sstep + x];
+    } else {
+        const int4 X = A.L[l].xt[x], Y = A.L[l].yt[y];
+        const int s00 = level_px<D - 1>(A, l - 1, X.x, Y.x), s01 = level_px<D - 1>(A, l - 1, X.y, Y.x);
+        const int s10 = level_px<D - 1>(A, l - 1, X.x, Y.y), s11 = level_px<D - 1>(A, l - 1, X.y, Y.y);
+        const int d0 = s00 * X.z + s01 * X.w, d1 = s10 * X.z + s11 * X.w;
+        int v;
+        if (x < A.L[l].xv)
+            v = ((((d0 >> 4) * Y.z) >> 16) + (((d1 >> 4) * Y.w) >> 16) + 2) >> 2;
+        else
+            v = (d0 * Y.z + d1 * Y.w + (1 << 21)) >> 22;
+        return v < 0 ? 0 : v > 255 ? 255 : v;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pyr_group(const GroupArgs A)
+{
+    constexpr int SW = BT_W + 2 * KR, SH = BT_H + 2 * KR;
+    __shared__ uint8_t s_src[SH][SW + 2];
+    __shared__ uint16_t s_h[SH][BT_W];
+    int p = 0;
+    while (p + 1 < A.n_parts && (int)blockIdx.x >= A.part_block0[p + 1]) p++;
+    const int b = blockIdx.x - A.part_block0[p];
+    const int l = A.part_level[p], tx = A.part_tiles_x[p];
+    const int w = A.L[l].w, h = A.L[l].h, bstep = A.L[l].bstep;
+    if (A.part_kind[p] == 0) {  // a 64 x 4 patch of the bordered level
+        const int bx = (b % tx) * 64 + (threadIdx.x & 63), by = (b / tx) * 4 + (threadIdx.x >> 6);
+        if (bx >= w + 2 * EDGE || by >= h + 2 * EDGE) return;
+        const int x = reflect101(bx - EDGE, w), y = reflect101(by - EDGE, h);
+        int v;
+        switch (l - A.src_level) {
+        case 0: v = level_px<0>(A, l, x, y); break;
+        case 1: v = level_px<1>(A, l, x, y); break;
+        case 2: v = level_px<2>(A, l, x, y); break;
+        case 3: v = level_px<3>(A, l, x, y); break;
+        default: v = level_px<4>(A, l, x, y); break;
+        }
+        A.L[l].dst[(long long)by * bstep + bx] = (uint8_t)v;
+        return;
+    }
+    // a 64 x 16 blur tile (block-uniform branch: the barriers below are reached by every thread)
+    const int tx0 = (b % tx) * BT_W, ty0 = (b / tx) * BT_H;
+    GLOBAL const uint8_t *roi = A.L[l].dst + (long long)EDGE * bstep + EDGE;
+    for (int i = threadIdx.x; i < SH * SW; i += 256) {
+        const int r = i / SW, c = i - r * SW;
+        s_src[r][c] = roi[(long long)reflect101(ty0 + r - KR, h) * bstep + reflect101(tx0 + c - KR, w)];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < SH * BT_W; i += 256) {
+        const int r = i / BT_W, c = i - r * BT_W;
+        uint32_t s = 0;
+#pragma unroll
+        for (int j = 0; j <= 2 * KR; j++) s += (uint32_t)s_src[r][c + j] * (uint32_t)A.k[j];
+        s_h[r][c] = (uint16_t)s;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < BT_H * BT_W; i += 256) {
+        const int r = i / BT_W, c = i - r * BT_W;
+        const int y = ty0 + r, x = tx0 + c;
+        if (y >= h || x >= w) continue;
+        uint32_t s = 0;
+#pragma unroll
+        for (int j = 0; j <= 2 * KR; j++) s += (uint32_t)s_h[r + j][c] * (uint32_t)A.k[j];
+        A.L[l].blur_out[(long long)y * w + x] = (uint8_t)((s + (1u << 15)) >> 16);
     }
 }
 
@@ -241,6 +340,70 @@ int pyramid_run(osg_ctx *ctx, const uint8_t *image, int32_t rows, int32_t cols, 
     hipEvent_t *ev = osg_ctx_events(ctx);
     if (!ev) return osg_set_error(ctx, OSG_E_HIP, "event create failed");
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[0], ctx->stream));
+    // OSG_PYR_FUSED=0/1 picks the launch form per call (the tests compare both); default below
+    const char *fz = getenv("OSG_PYR_FUSED");
+    const bool levelwise = fz ? atoi(fz) == 0 : !PYR_FUSED_DEFAULT;
+    if (!levelwise && n_levels <= GMAX) {
+        GroupArgs G{};
+        gaussian_kernel7(G.k);
+        for (int l = 0; l < n_levels; l++) {
+            PyrLevelDev &V = G.L[l];
+            V.w = lc[l];
+            V.h = lr[l];
+            V.bstep = lc[l] + 2 * EDGE;
+            V.dst = (GLOBAL uint8_t *)(dev_out + bo[l]);
+            V.blur_out = (GLOBAL uint8_t *)(dev_out + bl[l]);
+            if (l > 0) {
+                V.xt = (const int4 *)(din + xo[l]);
+                V.yt = (const int4 *)(din + yo[l]);
+                V.xv = vector_columns(lc[l]);
+            }
+        }
+        const int ng = (n_levels + GROUP - 1) / GROUP;
+        for (int k = 0; k <= ng; k++) {
+            G.n_parts = 0;
+            int nb = 0;
+            auto add_part = [&](int l, int kind, int tiles_x, int tiles) {
+                G.part_level[G.n_parts] = l;
+                G.part_kind[G.n_parts] = kind;
+                G.part_tiles_x[G.n_parts] = tiles_x;
+                G.part_block0[G.n_parts] = nb;
+                G.n_parts++;
+                nb += tiles;
+            };
+            if (k < ng) {
+                if (k == 0) {
+                    G.src = on_device ? (GLOBAL const uint8_t *)image : (GLOBAL const uint8_t *)(din + img_off);
+                    G.sstep = on_device ? step : cols;
+                    G.src_level = 0;
+                } else {
+                    const int s0 = GROUP * k - 1;
+                    G.src = (GLOBAL const uint8_t *)(dev_out + bo[s0] + (int64_t)EDGE * G.L[s0].bstep + EDGE);
+                    G.sstep = G.L[s0].bstep;
+                    G.src_level = s0;
+                }
+                for (int l = GROUP * k; l < std::min(n_levels, GROUP * (k + 1)); l++) {
+                    const int tx = (lc[l] + 2 * EDGE + 63) / 64;
+                    add_part(l, 0, tx, tx * ((lr[l] + 2 * EDGE + 3) / 4));
+                }
+            }
+            if (blur && k >= 1)
+                for (int l = GROUP * (k - 1); l < std::min(n_levels, GROUP * k); l++) {
+                    const int tx = (lc[l] + BT_W - 1) / BT_W;
+                    add_part(l, 1, tx, tx * ((lr[l] + BT_H - 1) / BT_H));
+                }
+            if (G.n_parts == 0) continue;
+            G.part_block0[G.n_parts] = nb;
+            hipLaunchKernelGGL(k_pyr_group, dim3(nb), dim3(256), 0, ctx->stream, G);
+            OSG_HIP_CHECK(ctx, hipGetLastError());
+        }
+        OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
+        OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+        float ms = 0.f;
+        OSG_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ev[0], ev[1]));
+        ctx->last_kernel_ms = ms;
+        return OSG_OK;
+    }
     for (int l = 0; l < n_levels; l++) {
         LevelArgs A{};
         A.w = lc[l];
