@@ -126,8 +126,9 @@ __global__ __launch_bounds__(256) void k_pyr_blur(const BlurArgs A)
 // above the stored one is the same integer formula applied recursively over 4^D stored pixels
 // (D <= GROUP): no value changes, only where it is computed.  Launch k computes level group k and
 // blurs group k - 1 (stored by launch k - 1); a last launch blurs the last group.
-constexpr int GROUP = 4;
+constexpr int GROUP = 4;  // the largest group; OSG_PYR_GROUP=1..4 picks it per call
 constexpr bool PYR_FUSED_DEFAULT = false;
+constexpr int PYR_GROUP_DEFAULT = 4;
 constexpr int GMAX = 16;  // levels a fused call handles (the level-wise path takes up to MAX_LEVELS)
 
 struct PyrLevelDev {
@@ -343,6 +344,8 @@ int pyramid_run(osg_ctx *ctx, const uint8_t *image, int32_t rows, int32_t cols, 
     // OSG_PYR_FUSED=0/1 picks the launch form per call (the tests compare both); default below
     const char *fz = getenv("OSG_PYR_FUSED");
     const bool levelwise = fz ? atoi(fz) == 0 : !PYR_FUSED_DEFAULT;
+    const char *gz = getenv("OSG_PYR_GROUP");
+    const int grp = gz ? std::min(GROUP, std::max(1, atoi(gz))) : PYR_GROUP_DEFAULT;
     if (!levelwise && n_levels <= GMAX) {
         GroupArgs G{};
         gaussian_kernel7(G.k);
@@ -359,7 +362,7 @@ int pyramid_run(osg_ctx *ctx, const uint8_t *image, int32_t rows, int32_t cols, 
                 V.xv = vector_columns(lc[l]);
             }
         }
-        const int ng = (n_levels + GROUP - 1) / GROUP;
+        const int ng = (n_levels + grp - 1) / grp;
         for (int k = 0; k <= ng; k++) {
             G.n_parts = 0;
             int nb = 0;
@@ -377,18 +380,18 @@ int pyramid_run(osg_ctx *ctx, const uint8_t *image, int32_t rows, int32_t cols, 
                     G.sstep = on_device ? step : cols;
                     G.src_level = 0;
                 } else {
-                    const int s0 = GROUP * k - 1;
+                    const int s0 = grp * k - 1;
                     G.src = (GLOBAL const uint8_t *)(dev_out + bo[s0] + (int64_t)EDGE * G.L[s0].bstep + EDGE);
                     G.sstep = G.L[s0].bstep;
                     G.src_level = s0;
                 }
-                for (int l = GROUP * k; l < std::min(n_levels, GROUP * (k + 1)); l++) {
+                for (int l = grp * k; l < std::min(n_levels, grp * (k + 1)); l++) {
                     const int tx = (lc[l] + 2 * EDGE + 63) / 64;
                     add_part(l, 0, tx, tx * ((lr[l] + 2 * EDGE + 3) / 4));
                 }
             }
             if (blur && k >= 1)
-                for (int l = GROUP * (k - 1); l < std::min(n_levels, GROUP * k); l++) {
+                for (int l = grp * (k - 1); l < std::min(n_levels, grp * k); l++) {
                     const int tx = (lc[l] + BT_W - 1) / BT_W;
                     add_part(l, 1, tx, tx * ((lr[l] + BT_H - 1) / BT_H));
                 }

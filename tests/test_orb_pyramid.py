@@ -138,12 +138,26 @@ def test_gpu_pyramid_fused_vs_levelwise_and_many_levels(ctx, oracle, monkeypatch
     inv = orb.inv_scale_factors(8, 1.2)
     monkeypatch.setenv("OSG_PYR_FUSED", "1")
     fused = orb.ComputePyramid(ctx, img, inv).buffer.cpu().numpy()
+    _gpu_vs_oracle(ctx, oracle, img, inv)
     _gpu_vs_oracle(ctx, oracle, img, orb.inv_scale_factors(12, 1.2))
     _gpu_vs_oracle(ctx, oracle, img, orb.inv_scale_factors(5, 1.3))
     _gpu_vs_oracle(ctx, oracle, _image(9, 61, 97), orb.inv_scale_factors(8, 1.2))
     monkeypatch.setenv("OSG_PYR_FUSED", "0")
     lw = orb.ComputePyramid(ctx, img, inv).buffer.cpu().numpy()
-    assert np.array_equal(fused, lw)
+    # the buffer is torch.empty and the 256-byte level padding is never written: compare the levels
+    _, lr, lc, bo, bl = oc.orb_pyramid(oracle, np.ascontiguousarray(img), inv, blur=True)
+    for a, b in zip(oc.pyramid_levels(fused, lr, lc, bo, bl), oc.pyramid_levels(lw, lr, lc, bo, bl)):
+        for l in range(inv.size):
+            assert np.array_equal(a[l], b[l]), f"level {l}: {np.argwhere(a[l] != b[l])[:5]}"
+    monkeypatch.setenv("OSG_PYR_FUSED", "1")
+    for g in (1, 2, 3):  # smaller groups: g levels per launch, depth <= g from the stored level
+        monkeypatch.setenv("OSG_PYR_GROUP", str(g))
+        fg = orb.ComputePyramid(ctx, img, inv).buffer.cpu().numpy()
+        for a, b in zip(oc.pyramid_levels(fg, lr, lc, bo, bl), oc.pyramid_levels(lw, lr, lc, bo, bl)):
+            for l in range(inv.size):
+                assert np.array_equal(a[l], b[l]), f"group {g} level {l}: {np.argwhere(a[l] != b[l])[:5]}"
+        _gpu_vs_oracle(ctx, oracle, _image(9, 61, 97), orb.inv_scale_factors(7, 1.2))
+    monkeypatch.setenv("OSG_PYR_FUSED", "0")
     _gpu_vs_oracle(ctx, oracle, img, orb.inv_scale_factors(12, 1.2))
 
 
