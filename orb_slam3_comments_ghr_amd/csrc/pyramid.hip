@@ -165,8 +165,21 @@ __device__ __forceinline__ int level_px(const GroupArgs &A, int l, int x, int y)
     }
 }
 
-__global__ __launch_bounds__(256) void k_pyr_group(const GroupArgs A)
+// depth d of the level above the stored one, dispatched over the instantiations up to DMAX only (the
+// kernel is instantiated per group size: the deep recursion's code stays out of the shallow launches)
+template <int D, int DMAX>
+__device__ __forceinline__ int level_at(const GroupArgs &A, int d, int l, int x, int y)
 {
+    if constexpr (D == DMAX)
+        return level_px<D>(A, l, x, y);
+    else
+        return d == D ? level_px<D>(A, l, x, y) : level_at<D + 1, DMAX>(A, d, l, x, y);
+}
+
+template <int DMAX>
+__global__ __launch_bounds__(256) void k_pyr_group(const GroupArgs *__restrict__ Ad)
+{
+    const GroupArgs &A = *Ad;
     constexpr int SW = BT_W + 2 * KR, SH = BT_H + 2 * KR;
     __shared__ uint8_t s_src[SH][SW + 2];
     __shared__ uint16_t s_h[SH][BT_W];
@@ -179,14 +192,7 @@ __global__ __launch_bounds__(256) void k_pyr_group(const GroupArgs A)
         const int bx = (b % tx) * 64 + (threadIdx.x & 63), by = (b / tx) * 4 + (threadIdx.x >> 6);
         if (bx >= w + 2 * EDGE || by >= h + 2 * EDGE) return;
         const int x = reflect101(bx - EDGE, w), y = reflect101(by - EDGE, h);
-        int v;
-        switch (l - A.src_level) {
-        case 0: v = level_px<0>(A, l, x, y); break;
-        case 1: v = level_px<1>(A, l, x, y); break;
-        case 2: v = level_px<2>(A, l, x, y); break;
-        case 3: v = level_px<3>(A, l, x, y); break;
-        default: v = level_px<4>(A, l, x, y); break;
-        }
+        const int v = level_at<0, DMAX>(A, l - A.src_level, l, x, y);
         A.L[l].dst[(long long)by * bstep + bx] = (uint8_t)v;
         return;
     }
@@ -329,75 +335,91 @@ int pyramid_run(osg_ctx *ctx, const uint8_t *image, int32_t rows, int32_t cols, 
         xo[l] = pk.add(xt[l].data(), sizeof(int4) * xt[l].size());
         yo[l] = pk.add(yt[l].data(), sizeof(int4) * yt[l].size());
     }
-    char *din = nullptr;
-    if (pk.total) {
-        char *pin = (char *)osg_pinned(ctx, pk.total + 256);
-        if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
-        OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));  // the pinned block may still be in use
-        pk.fill(pin);
-        OSG_ALLOC(ctx, din, SLOT_TMP0, pk.total + 256);
-        OSG_HIP_CHECK(ctx, hipMemcpyAsync(din, pin, pk.total, hipMemcpyHostToDevice, ctx->stream));
-    }
-    hipEvent_t *ev = osg_ctx_events(ctx);
-    if (!ev) return osg_set_error(ctx, OSG_E_HIP, "event create failed");
-    OSG_HIP_CHECK(ctx, hipEventRecord(ev[0], ctx->stream));
     // OSG_PYR_FUSED=0/1 picks the launch form per call (the tests compare both); default below
     const char *fz = getenv("OSG_PYR_FUSED");
     const bool levelwise = fz ? atoi(fz) == 0 : !PYR_FUSED_DEFAULT;
     const char *gz = getenv("OSG_PYR_GROUP");
     const int grp = gz ? std::min(GROUP, std::max(1, atoi(gz))) : PYR_GROUP_DEFAULT;
-    if (!levelwise && n_levels <= GMAX) {
-        GroupArgs G{};
-        gaussian_kernel7(G.k);
-        for (int l = 0; l < n_levels; l++) {
-            PyrLevelDev &V = G.L[l];
-            V.w = lc[l];
-            V.h = lr[l];
-            V.bstep = lc[l] + 2 * EDGE;
-            V.dst = (GLOBAL uint8_t *)(dev_out + bo[l]);
-            V.blur_out = (GLOBAL uint8_t *)(dev_out + bl[l]);
-            if (l > 0) {
-                V.xt = (const int4 *)(din + xo[l]);
-                V.yt = (const int4 *)(din + yo[l]);
-                V.xv = vector_columns(lc[l]);
+    const bool fused = !levelwise && n_levels <= GMAX;
+    const int ng = fused ? (n_levels + grp - 1) / grp : 0;
+    // the fused launches' descriptors travel in the staging upload and the kernel reads them from HBM:
+    // as kernel arguments (~1 KB, indexed by the block's part and level) each dependent read was a
+    // round trip to the host-resident kernarg segment
+    std::vector<GroupArgs> groups(fused ? ng + 1 : 0);
+    std::vector<int> group_blocks(groups.size(), 0);
+    const size_t go = fused ? pk.add(groups.data(), sizeof(GroupArgs) * groups.size()) : SIZE_MAX;
+    char *din = nullptr;
+    if (pk.total) {
+        char *pin = (char *)osg_pinned(ctx, pk.total + 256);
+        if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
+        OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));  // the pinned block may still be in use
+        OSG_ALLOC(ctx, din, SLOT_TMP0, pk.total + 256);
+        if (fused) {
+            GroupArgs G{};
+            gaussian_kernel7(G.k);
+            for (int l = 0; l < n_levels; l++) {
+                PyrLevelDev &V = G.L[l];
+                V.w = lc[l];
+                V.h = lr[l];
+                V.bstep = lc[l] + 2 * EDGE;
+                V.dst = (GLOBAL uint8_t *)(dev_out + bo[l]);
+                V.blur_out = (GLOBAL uint8_t *)(dev_out + bl[l]);
+                if (l > 0) {
+                    V.xt = (const int4 *)(din + xo[l]);
+                    V.yt = (const int4 *)(din + yo[l]);
+                    V.xv = vector_columns(lc[l]);
+                }
+            }
+            for (int k = 0; k <= ng; k++) {
+                G.n_parts = 0;
+                int nb = 0;
+                auto add_part = [&](int l, int kind, int tiles_x, int tiles) {
+                    G.part_level[G.n_parts] = l;
+                    G.part_kind[G.n_parts] = kind;
+                    G.part_tiles_x[G.n_parts] = tiles_x;
+                    G.part_block0[G.n_parts] = nb;
+                    G.n_parts++;
+                    nb += tiles;
+                };
+                if (k < ng) {
+                    if (k == 0) {
+                        G.src = on_device ? (GLOBAL const uint8_t *)image : (GLOBAL const uint8_t *)(din + img_off);
+                        G.sstep = on_device ? step : cols;
+                        G.src_level = 0;
+                    } else {
+                        const int s0 = grp * k - 1;
+                        G.src = (GLOBAL const uint8_t *)(dev_out + bo[s0] + (int64_t)EDGE * G.L[s0].bstep + EDGE);
+                        G.sstep = G.L[s0].bstep;
+                        G.src_level = s0;
+                    }
+                    for (int l = grp * k; l < std::min(n_levels, grp * (k + 1)); l++) {
+                        const int tx = (lc[l] + 2 * EDGE + 63) / 64;
+                        add_part(l, 0, tx, tx * ((lr[l] + 2 * EDGE + 3) / 4));
+                    }
+                }
+                if (blur && k >= 1)
+                    for (int l = grp * (k - 1); l < std::min(n_levels, grp * k); l++) {
+                        const int tx = (lc[l] + BT_W - 1) / BT_W;
+                        add_part(l, 1, tx, tx * ((lr[l] + BT_H - 1) / BT_H));
+                    }
+                G.part_block0[G.n_parts] = nb;
+                groups[k] = G;
+                group_blocks[k] = G.n_parts ? nb : 0;
             }
         }
-        const int ng = (n_levels + grp - 1) / grp;
+        pk.fill(pin);
+        OSG_HIP_CHECK(ctx, hipMemcpyAsync(din, pin, pk.total, hipMemcpyHostToDevice, ctx->stream));
+    }
+    hipEvent_t *ev = osg_ctx_events(ctx);
+    if (!ev) return osg_set_error(ctx, OSG_E_HIP, "event create failed");
+    OSG_HIP_CHECK(ctx, hipEventRecord(ev[0], ctx->stream));
+    if (fused) {
+        auto *kern = grp == 1 ? k_pyr_group<1> : grp == 2 ? k_pyr_group<2> : grp == 3 ? k_pyr_group<3>
+                                                                             : k_pyr_group<4>;
         for (int k = 0; k <= ng; k++) {
-            G.n_parts = 0;
-            int nb = 0;
-            auto add_part = [&](int l, int kind, int tiles_x, int tiles) {
-                G.part_level[G.n_parts] = l;
-                G.part_kind[G.n_parts] = kind;
-                G.part_tiles_x[G.n_parts] = tiles_x;
-                G.part_block0[G.n_parts] = nb;
-                G.n_parts++;
-                nb += tiles;
-            };
-            if (k < ng) {
-                if (k == 0) {
-                    G.src = on_device ? (GLOBAL const uint8_t *)image : (GLOBAL const uint8_t *)(din + img_off);
-                    G.sstep = on_device ? step : cols;
-                    G.src_level = 0;
-                } else {
-                    const int s0 = grp * k - 1;
-                    G.src = (GLOBAL const uint8_t *)(dev_out + bo[s0] + (int64_t)EDGE * G.L[s0].bstep + EDGE);
-                    G.sstep = G.L[s0].bstep;
-                    G.src_level = s0;
-                }
-                for (int l = grp * k; l < std::min(n_levels, grp * (k + 1)); l++) {
-                    const int tx = (lc[l] + 2 * EDGE + 63) / 64;
-                    add_part(l, 0, tx, tx * ((lr[l] + 2 * EDGE + 3) / 4));
-                }
-            }
-            if (blur && k >= 1)
-                for (int l = grp * (k - 1); l < std::min(n_levels, grp * k); l++) {
-                    const int tx = (lc[l] + BT_W - 1) / BT_W;
-                    add_part(l, 1, tx, tx * ((lr[l] + BT_H - 1) / BT_H));
-                }
-            if (G.n_parts == 0) continue;
-            G.part_block0[G.n_parts] = nb;
-            hipLaunchKernelGGL(k_pyr_group, dim3(nb), dim3(256), 0, ctx->stream, G);
+            if (!group_blocks[k]) continue;
+            const GroupArgs *gd = (const GroupArgs *)(din + go + sizeof(GroupArgs) * k);
+            hipLaunchKernelGGL(kern, dim3(group_blocks[k]), dim3(256), 0, ctx->stream, gd);
             OSG_HIP_CHECK(ctx, hipGetLastError());
         }
         OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
