@@ -333,6 +333,22 @@ int osg_compute_stereo_matches(osg_ctx *ctx, const osg_stereo_frame *F, float *u
 int osg_compute_stereo_matches_batch(osg_ctx *ctx, const osg_stereo_frame *F, int32_t B, float *u_right,
                                      float *depth, int32_t *nmatches);
 
+/* Frame::ComputeStereoFishEyeMatches (ref:src/Frame.cc:1546-1603; the KannalaBrandt8 two-camera Frame
+ * constructor, :1523): BFMatcher(NORM_HAMMING).knnMatch(k = 2) of the left stereo rows [mono_left, n_left)
+ * against the right stereo rows [mono_right, n_right), Lowe's ratio 0.7, KannalaBrandt8::TriangulateMatches
+ * (ref:src/CameraModels/KannalaBrandt8.cpp:438-520) with mvLevelSigma2 of both octaves, depth > 0.0001f.
+ * desc_*: n x 32 bytes; kp_*: n x (x, y) float; oct_*: n octaves; cam_*: fx fy cx cy k0 k1 k2 k3;
+ * Rlr (row-major 3x3), tlr: mRlr, mtlr.  Outputs mvLeftToRightMatch[n_left], mvRightToLeftMatch[n_right],
+ * mvDepth[n_left] (-1 unmatched), mvStereo3Dpoints[n_left x 3] (0 unmatched; the reference leaves them
+ * uninitialised).  Returns nMatches (the matches kept) or a negative error. */
+int osg_compute_stereo_fisheye_matches(osg_ctx *ctx, int32_t n_left, int32_t mono_left, const uint8_t *desc_left,
+                                       const float *kp_left, const int32_t *oct_left, int32_t n_right,
+                                       int32_t mono_right, const uint8_t *desc_right, const float *kp_right,
+                                       const int32_t *oct_right, const float *level_sigma2, int32_t n_levels,
+                                       const float *cam_left, const float *cam_right, const float *Rlr,
+                                       const float *tlr, int32_t *left_to_right, int32_t *right_to_left,
+                                       float *depth, float *points3d);
+
 /* ---- b6: SearchForInitialization ------------------------------------------------------------------
  * ORBmatcher::SearchForInitialization(Frame &F1, Frame &F2, vector<cv::Point2f> &vbPrevMatched,
  * vector<int> &vnMatches12, windowSize)  ref:src/ORBmatcher.cc:735-878 (monocular initialisation,

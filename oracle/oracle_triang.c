@@ -225,9 +225,10 @@ static void kb_null4(const float A[4][4], double v[4])
     for (int k = 0; k < 4; k++) v[k] = V[k][m];
 }
 
-/* KannalaBrandt8::TriangulateMatches (KannalaBrandt8.cpp:438-489) > 0.0001f: this = cam1 */
-static int kb_epipolar_constrain(const float *cam1, const float *cam2, float x1, float y1, float x2, float y2,
-                                 const float *R12, const float *t12, float sigmaLevel, float unc)
+/* KannalaBrandt8::TriangulateMatches (KannalaBrandt8.cpp:438-520): this = cam1; z1 with p3D = x3D, or the
+ * reference's negative codes (p3D untouched) */
+static float kb_triangulate_matches(const float *cam1, const float *cam2, float x1, float y1, float x2, float y2,
+                                    const float *R12, const float *t12, float sigmaLevel, float unc, float *p3D)
 {
     float r1[3], r2[3], r21[3];
     kb_unproject(cam1, x1, y1, r1);
@@ -237,7 +238,7 @@ static int kb_epipolar_constrain(const float *cam1, const float *cam2, float x1,
     const float n1 = sqrtf(r1[0] * r1[0] + r1[1] * r1[1] + r1[2] * r1[2]);
     const float n21 = sqrtf(r21[0] * r21[0] + r21[1] * r21[1] + r21[2] * r21[2]);
     const float cosParallaxRays = dot / (n1 * n21);
-    if (cosParallaxRays > 0.9998) return 0;                                     /* return -1 */
+    if (cosParallaxRays > 0.9998) return -1;
     /* Tcw1 = [I | 0], Tcw2 = [R21 | -R21 t12], R21 = R12^T */
     float R21[9], t2[3];
     for (int i = 0; i < 3; i++)
@@ -258,19 +259,30 @@ static int kb_epipolar_constrain(const float *cam1, const float *cam2, float x1,
     const float hf[4] = {(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
     const float x3D[3] = {hf[0] / hf[3], hf[1] / hf[3], hf[2] / hf[3]};
     const float z1 = x3D[2];
-    if (z1 <= 0) return 0;                                                      /* -2 */
+    if (z1 <= 0) return -2;
     const float z2 = (R21[6] * x3D[0] + R21[7] * x3D[1] + R21[8] * x3D[2]) + t2[2];
-    if (z2 <= 0) return 0;                                                      /* -3 */
+    if (z2 <= 0) return -3;
     float uv1[2];
     kb_project(cam1, x3D, uv1);
     const float errX1 = uv1[0] - x1, errY1 = uv1[1] - y1;
-    if ((errX1 * errX1 + errY1 * errY1) > 5.991 * sigmaLevel) return 0;        /* -4 */
+    if ((errX1 * errX1 + errY1 * errY1) > 5.991 * sigmaLevel) return -4;
     float x3D2[3], uv2[2];
     for (int i = 0; i < 3; i++) x3D2[i] = (R21[3 * i] * x3D[0] + R21[3 * i + 1] * x3D[1] + R21[3 * i + 2] * x3D[2]) + t2[i];
     kb_project(cam2, x3D2, uv2);
     const float errX2 = uv2[0] - x2, errY2 = uv2[1] - y2;
-    if ((errX2 * errX2 + errY2 * errY2) > 5.991 * unc) return 0;               /* -5 */
-    return z1 > 0.0001f;
+    if ((errX2 * errX2 + errY2 * errY2) > 5.991 * unc) return -5;
+    p3D[0] = x3D[0];
+    p3D[1] = x3D[1];
+    p3D[2] = x3D[2];
+    return z1;
+}
+
+/* epipolarConstrain = TriangulateMatches(...) > 0.0001f (KannalaBrandt8.cpp:321-326) */
+static int kb_epipolar_constrain(const float *cam1, const float *cam2, float x1, float y1, float x2, float y2,
+                                 const float *R12, const float *t12, float sigmaLevel, float unc)
+{
+    float p3D[3];
+    return kb_triangulate_matches(cam1, cam2, x1, y1, x2, y2, R12, t12, sigmaLevel, unc, p3D) > 0.0001f;
 }
 
 /* exported for tests/test_oracle_triang.py: one KannalaBrandt8::epipolarConstrain evaluation */
@@ -278,6 +290,53 @@ int oracle_kb8_epipolar_constrain(const float *cam1, const float *cam2, float x1
                                   const float *R12, const float *t12, float sigmaLevel, float unc)
 {
     return kb_epipolar_constrain(cam1, cam2, x1, y1, x2, y2, R12, t12, sigmaLevel, unc);
+}
+
+/* Frame::ComputeStereoFishEyeMatches (ref:src/Frame.cc:1546-1603), serial: BFMatcher(NORM_HAMMING)
+ * (ref:src/Frame.cc:47).knnMatch(k = 2) per left stereo row in query order (OpenCV's K-nearest insertion:
+ * a distance equal to the first neighbour's becomes the second), Lowe's ratio (float * 0.7 in double),
+ * TriangulateMatches(cam2, kpL, kpR, mRlr, mtlr, sigma2[octL], sigma2[octR]) > 0.0001f; later queries
+ * overwrite mvRightToLeftMatch.  Unmatched mvStereo3Dpoints rows are 0 here (uninitialised in the reference). */
+int oracle_stereo_fisheye_matches(int32_t n_left, int32_t mono_left, const uint8_t *dl, const float *kl,
+                                  const int32_t *ol, int32_t n_right, int32_t mono_right, const uint8_t *dr,
+                                  const float *kr, const int32_t *orr, const float *sig2, const float *caml,
+                                  const float *camr, const float *Rlr, const float *tlr, int32_t *l2r, int32_t *r2l,
+                                  float *depth, float *p3d)
+{
+    for (int i = 0; i < n_left; i++) {
+        l2r[i] = -1;
+        depth[i] = -1.0f;
+        p3d[3 * i] = p3d[3 * i + 1] = p3d[3 * i + 2] = 0.f;
+    }
+    for (int j = 0; j < n_right; j++) r2l[j] = -1;
+    int nMatches = 0;
+    if (n_right - mono_right < 2) return 0; /* knnMatch returns < 2 neighbours: (*it).size() >= 2 fails */
+    for (int i = mono_left; i < n_left; i++) {
+        int b1 = 0x7fffffff, b2 = 0x7fffffff, j1 = -1;
+        for (int j = mono_right; j < n_right; j++) {
+            int d = 0;
+            for (int k = 0; k < 32; k++) d += __builtin_popcount((unsigned)(dl[32 * i + k] ^ dr[32 * j + k]));
+            if (d < b1) {
+                b2 = b1;
+                b1 = d;
+                j1 = j;
+            } else if (d < b2) {
+                b2 = d;
+            }
+        }
+        if (!((double)(float)b1 < (double)(float)b2 * 0.7)) continue;
+        float x3[3];
+        const float z = kb_triangulate_matches(caml, camr, kl[2 * i], kl[2 * i + 1], kr[2 * j1], kr[2 * j1 + 1], Rlr,
+                                               tlr, sig2[ol[i]], sig2[orr[j1]], x3);
+        if (z > 0.0001f) {
+            l2r[i] = j1;
+            r2l[j1] = i;
+            for (int k = 0; k < 3; k++) p3d[3 * i + k] = x3[k];
+            depth[i] = z;
+            nMatches++;
+        }
+    }
+    return nMatches;
 }
 
 void oracle_kb8_unproject(const float *cam, float u, float v, float *r) { kb_unproject(cam, u, v, r); }

@@ -189,7 +189,8 @@ EXPORTS = [
     "osg_compute_distinctive_descriptors", "osg_compute_distinctive_descriptors_dev",
     "osg_search_by_projection_sim3", "osg_search_by_projection_sim3_batch", "osg_search_by_sim3",
     "osg_search_for_initialization", "osg_search_for_initialization_batch",
-    "osg_compute_stereo_matches", "osg_compute_stereo_matches_batch", "osg_orb_describe", "osg_orb_detect",
+    "osg_compute_stereo_matches", "osg_compute_stereo_matches_batch", "osg_compute_stereo_fisheye_matches",
+    "osg_orb_describe", "osg_orb_detect",
     "osg_debug_distribute_oct_tree", "osg_orb_pyramid_layout", "osg_orb_pyramid", "osg_debug_gaussian_kernel7",
 ]
 
@@ -262,6 +263,8 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.osg_search_for_initialization_batch.argtypes = [vp, vp, vp, i32, vp, C.c_int, f32, C.c_int, vp, vp]
     lib.osg_compute_stereo_matches.argtypes = [vp, C.POINTER(OsgStereoFrame), vp, vp]
     lib.osg_compute_stereo_matches_batch.argtypes = [vp, vp, i32, vp, vp, vp]
+    lib.osg_compute_stereo_fisheye_matches.argtypes = [vp, i32, i32, vp, vp, vp, i32, i32, vp, vp, vp, vp, i32,
+                                                       vp, vp, vp, vp, vp, vp, vp, vp]
     lib.osg_debug_distribute_oct_tree.argtypes = [vp, i32, i32, i32, i32, i32, i32, vp, i32]
     lib.osg_orb_detect.argtypes = [vp, C.POINTER(OsgImagePyramid), i32, i32, vp, vp, i32, vp, vp, vp, vp, vp]
     lib.osg_orb_pyramid_layout.argtypes = [i32, i32, i32, vp, vp, vp, vp, vp]

@@ -206,9 +206,11 @@ __device__ inline void null4(const float A[4][4], double v[4])
     for (int k = 0; k < 4; k++) v[k] = V[k][m];
 }
 
-// TriangulateMatches(...) > 0.0001f with this = cam1 (pCamera1), pCamera2 = cam2
-__device__ inline bool epipolar_constrain(const float *cam1, const float *cam2, float x1, float y1, float x2,
-                                          float y2, const float *R12, const float *t12, float sigmaLevel, float unc)
+// TriangulateMatches with this = cam1 (pCamera1), pCamera2 = cam2: z1 with p3D = x3D, or the reference's
+// negative codes -1..-5 (p3D untouched)
+__device__ inline float triangulate_matches(const float *cam1, const float *cam2, float x1, float y1, float x2,
+                                            float y2, const float *R12, const float *t12, float sigmaLevel,
+                                            float unc, float *p3D)
 {
     float r1[3], r2[3], r21[3];
     unproject(cam1, x1, y1, r1);
@@ -219,7 +221,7 @@ __device__ inline bool epipolar_constrain(const float *cam1, const float *cam2, 
     const float n1 = sqrtf(r1[0] * r1[0] + r1[1] * r1[1] + r1[2] * r1[2]);
     const float n21 = sqrtf(r21[0] * r21[0] + r21[1] * r21[1] + r21[2] * r21[2]);
     const float cosParallaxRays = dot / (n1 * n21);
-    if (cosParallaxRays > 0.9998) return false;
+    if (cosParallaxRays > 0.9998) return -1;
     float R21[9], t2[3];
 #pragma unroll
     for (int i = 0; i < 3; i++)
@@ -243,21 +245,32 @@ __device__ inline bool epipolar_constrain(const float *cam1, const float *cam2, 
     const float hf[4] = {(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
     const float x3D[3] = {hf[0] / hf[3], hf[1] / hf[3], hf[2] / hf[3]};
     const float z1 = x3D[2];
-    if (z1 <= 0) return false;
+    if (z1 <= 0) return -2;
     const float z2 = (R21[6] * x3D[0] + R21[7] * x3D[1] + R21[8] * x3D[2]) + t2[2];
-    if (z2 <= 0) return false;
+    if (z2 <= 0) return -3;
     float uv1[2];
     project(cam1, x3D, uv1);
     const float errX1 = uv1[0] - x1, errY1 = uv1[1] - y1;
-    if ((errX1 * errX1 + errY1 * errY1) > 5.991 * sigmaLevel) return false;
+    if ((errX1 * errX1 + errY1 * errY1) > 5.991 * sigmaLevel) return -4;
     float x3D2[3], uv2[2];
 #pragma unroll
     for (int i = 0; i < 3; i++)
         x3D2[i] = (R21[3 * i] * x3D[0] + R21[3 * i + 1] * x3D[1] + R21[3 * i + 2] * x3D[2]) + t2[i];
     project(cam2, x3D2, uv2);
     const float errX2 = uv2[0] - x2, errY2 = uv2[1] - y2;
-    if ((errX2 * errX2 + errY2 * errY2) > 5.991 * unc) return false;
-    return z1 > 0.0001f;
+    if ((errX2 * errX2 + errY2 * errY2) > 5.991 * unc) return -5;
+    p3D[0] = x3D[0];
+    p3D[1] = x3D[1];
+    p3D[2] = x3D[2];
+    return z1;
+}
+
+// epipolarConstrain: TriangulateMatches(...) > 0.0001f (ref:src/CameraModels/KannalaBrandt8.cpp:321-326)
+__device__ inline bool epipolar_constrain(const float *cam1, const float *cam2, float x1, float y1, float x2,
+                                          float y2, const float *R12, const float *t12, float sigmaLevel, float unc)
+{
+    float p3D[3];
+    return triangulate_matches(cam1, cam2, x1, y1, x2, y2, R12, t12, sigmaLevel, unc, p3D) > 0.0001f;
 }
 
 }  // namespace kb8

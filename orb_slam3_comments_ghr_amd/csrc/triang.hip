@@ -394,9 +394,166 @@ int triang_run(osg_ctx *ctx, const osg_kf_side *K1, const osg_kf_side *K2, const
     return OSG_OK;
 }
 
+
+// ---- Frame::ComputeStereoFishEyeMatches (ref:src/Frame.cc:1546-1603) ---------------------------------
+// BFMatcher(NORM_HAMMING).knnMatch(k = 2) of the left stereo rows [monoLeft, Nleft) against the right stereo
+// rows [monoRight, Nright) (ref:src/Frame.cc:47, :1569), Lowe's ratio d0 < d1 * 0.7 (float * double),
+// then KannalaBrandt8::TriangulateMatches with sigma2 of both octaves and depth > 0.0001f.  One lane per
+// left row walks every right row (knn's insertion order: a tie never displaces the first neighbour, it
+// becomes the second).  mvRightToLeftMatch is written in query order by the reference, so the last
+// accepted query wins: atomicMax over the query index.
+struct FishArgs {
+    const uint4 *dl, *dr;
+    const float2 *kl, *kr;
+    const int32_t *ol, *orr;
+    const float *sig2;
+    float caml[8], camr[8], R[9], t[3];
+    int nl, ml, nr, mr;
+    GLOBAL int32_t *l2r, *r2l, *nmatch;
+    GLOBAL float *depth, *p3d;
+};
+
+__global__ __launch_bounds__(256) void k_stereo_fisheye(const FishArgs A)
+{
+    const int i = A.ml + (int)(blockIdx.x * 256 + threadIdx.x);
+    if (i >= A.nl) return;
+    const uint4 q0 = A.dl[2 * i], q1 = A.dl[2 * i + 1];
+    int b1 = 0x7fffffff, b2 = 0x7fffffff, j1 = -1;
+    for (int j = A.mr; j < A.nr; j++) {
+        const uint4 t0 = A.dr[2 * j], t1 = A.dr[2 * j + 1];
+        const int d = __popc(q0.x ^ t0.x) + __popc(q0.y ^ t0.y) + __popc(q0.z ^ t0.z) + __popc(q0.w ^ t0.w) +
+                      __popc(q1.x ^ t1.x) + __popc(q1.y ^ t1.y) + __popc(q1.z ^ t1.z) + __popc(q1.w ^ t1.w);
+        if (d < b1) {
+            b2 = b1;
+            b1 = d;
+            j1 = j;
+        } else if (d < b2) {
+            b2 = d;
+        }
+    }
+    if (A.nr - A.mr < 2 || !((double)(float)b1 < (double)(float)b2 * 0.7)) return;
+    const float2 a = A.kl[i], b = A.kr[j1];
+    float p[3];
+    const float z = kb8::triangulate_matches(A.caml, A.camr, a.x, a.y, b.x, b.y, A.R, A.t, A.sig2[A.ol[i]],
+                                             A.sig2[A.orr[j1]], p);
+    if (!(z > 0.0001f)) return;
+    A.l2r[i] = j1;
+    A.depth[i] = z;
+    A.p3d[3 * i] = p[0];
+    A.p3d[3 * i + 1] = p[1];
+    A.p3d[3 * i + 2] = p[2];
+    atomicMax((int32_t *)&A.r2l[j1], i);
+    atomicAdd((int32_t *)A.nmatch, 1);
+}
+
+int stereo_fisheye_run(osg_ctx *ctx, int32_t n_left, int32_t mono_left, const uint8_t *desc_left,
+                       const float *kp_left, const int32_t *oct_left, int32_t n_right, int32_t mono_right,
+                       const uint8_t *desc_right, const float *kp_right, const int32_t *oct_right,
+                       const float *level_sigma2, int32_t n_levels, const float *cam_left, const float *cam_right,
+                       const float *Rlr, const float *tlr, int32_t *left_to_right, int32_t *right_to_left,
+                       float *depth, float *points3d)
+{
+    if (!ctx) return OSG_E_INVALID;
+    OSG_REQUIRE(ctx, n_left >= 0 && n_right >= 0 && mono_left >= 0 && mono_left <= n_left && mono_right >= 0 &&
+                         mono_right <= n_right && n_levels >= 1,
+                "sizes (Nleft %d, monoLeft %d, Nright %d, monoRight %d, %d levels)", n_left, mono_left, n_right,
+                mono_right, n_levels);
+    OSG_REQUIRE(ctx, level_sigma2 && cam_left && cam_right && Rlr && tlr, "null camera / rig / level argument");
+    OSG_REQUIRE(ctx, (n_left == 0 || (left_to_right && depth && points3d)) && (n_right == 0 || right_to_left),
+                "null output");
+    for (int i = 0; i < n_left; i++) {
+        left_to_right[i] = -1;
+        depth[i] = -1.0f;
+        points3d[3 * i] = points3d[3 * i + 1] = points3d[3 * i + 2] = 0.f;
+    }
+    for (int j = 0; j < n_right; j++) right_to_left[j] = -1;
+    const int nq = n_left - mono_left, nt = n_right - mono_right;
+    if (nq == 0 || nt < 2) return 0;
+    OSG_REQUIRE(ctx, desc_left && kp_left && oct_left && desc_right && kp_right && oct_right, "null keypoint input");
+    for (int i = mono_left; i < n_left; i++)
+        OSG_REQUIRE(ctx, oct_left[i] >= 0 && oct_left[i] < n_levels, "left octave %d of row %d", oct_left[i], i);
+    for (int j = mono_right; j < n_right; j++)
+        OSG_REQUIRE(ctx, oct_right[j] >= 0 && oct_right[j] < n_levels, "right octave %d of row %d", oct_right[j],
+                    j);
+    osg_packer pk;
+    const size_t o_dl = pk.add(desc_left, 32 * (size_t)n_left), o_dr = pk.add(desc_right, 32 * (size_t)n_right);
+    const size_t o_kl = pk.add(kp_left, 8 * (size_t)n_left), o_kr = pk.add(kp_right, 8 * (size_t)n_right);
+    const size_t o_ol = pk.add(oct_left, 4 * (size_t)n_left), o_or = pk.add(oct_right, 4 * (size_t)n_right);
+    const size_t o_sg = pk.add(level_sigma2, 4 * (size_t)n_levels);
+    const size_t int_bytes = 4 * ((size_t)n_left + n_right + 1);
+    const size_t out_bytes = int_bytes + 16 * (size_t)n_left;
+    const size_t in_bytes = (pk.total + 255) & ~size_t(255);
+    char *pin = (char *)osg_pinned(ctx, in_bytes + out_bytes + 256);
+    if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
+    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));  // the pinned block may still be in use
+    pk.fill(pin);
+    char *pin_out = pin + in_bytes;
+    char *dev_in = nullptr, *dev_out = nullptr;
+    OSG_ALLOC(ctx, dev_in, SLOT_TMP0, pk.total + 256);
+    OSG_ALLOC(ctx, dev_out, SLOT_TMP2, out_bytes);
+    FishArgs A{};
+    A.dl = (const uint4 *)(dev_in + o_dl);
+    A.dr = (const uint4 *)(dev_in + o_dr);
+    A.kl = (const float2 *)(dev_in + o_kl);
+    A.kr = (const float2 *)(dev_in + o_kr);
+    A.ol = (const int32_t *)(dev_in + o_ol);
+    A.orr = (const int32_t *)(dev_in + o_or);
+    A.sig2 = (const float *)(dev_in + o_sg);
+    std::copy(cam_left, cam_left + 8, A.caml);
+    std::copy(cam_right, cam_right + 8, A.camr);
+    std::copy(Rlr, Rlr + 9, A.R);
+    std::copy(tlr, tlr + 3, A.t);
+    A.nl = n_left;
+    A.ml = mono_left;
+    A.nr = n_right;
+    A.mr = mono_right;
+    A.l2r = (GLOBAL int32_t *)dev_out;
+    A.r2l = A.l2r + n_left;
+    A.nmatch = A.r2l + n_right;
+    A.depth = (GLOBAL float *)(dev_out + int_bytes);
+    A.p3d = A.depth + n_left;
+    OSG_HIP_CHECK(ctx, hipMemcpyAsync(dev_in, pin, pk.total, hipMemcpyHostToDevice, ctx->stream));
+    OSG_HIP_CHECK(ctx, hipMemsetAsync(dev_out, 0xff, 4 * ((size_t)n_left + n_right), ctx->stream));
+    OSG_HIP_CHECK(ctx, hipMemsetAsync(dev_out + 4 * ((size_t)n_left + n_right), 0, 4, ctx->stream));
+    hipEvent_t *ev = osg_ctx_events(ctx);
+    if (!ev) return osg_set_error(ctx, OSG_E_HIP, "event create failed");
+    OSG_HIP_CHECK(ctx, hipEventRecord(ev[0], ctx->stream));
+    hipLaunchKernelGGL(k_stereo_fisheye, dim3((nq + 255) / 256), dim3(256), 0, ctx->stream, A);
+    OSG_HIP_CHECK(ctx, hipGetLastError());
+    OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
+    OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_out, dev_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
+    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    float ms = 0.f;
+    OSG_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ev[0], ev[1]));
+    ctx->last_kernel_ms = ms;
+    const int32_t *o_l2r = (const int32_t *)pin_out, *o_r2l = o_l2r + n_left;
+    const float *o_depth = (const float *)(pin_out + int_bytes), *o_p3d = o_depth + n_left;
+    for (int i = mono_left; i < n_left; i++) {
+        if (o_l2r[i] < 0) continue;
+        left_to_right[i] = o_l2r[i];
+        depth[i] = o_depth[i];
+        for (int k = 0; k < 3; k++) points3d[3 * i + k] = o_p3d[3 * i + k];
+    }
+    for (int j = mono_right; j < n_right; j++) right_to_left[j] = o_r2l[j];
+    return o_r2l[n_right];
+}
+
 }  // namespace
 
 extern "C" {
+
+int osg_compute_stereo_fisheye_matches(osg_ctx *ctx, int32_t n_left, int32_t mono_left, const uint8_t *desc_left,
+                                       const float *kp_left, const int32_t *oct_left, int32_t n_right,
+                                       int32_t mono_right, const uint8_t *desc_right, const float *kp_right,
+                                       const int32_t *oct_right, const float *level_sigma2, int32_t n_levels,
+                                       const float *cam_left, const float *cam_right, const float *Rlr,
+                                       const float *tlr, int32_t *left_to_right, int32_t *right_to_left,
+                                       float *depth, float *points3d)
+{
+    return stereo_fisheye_run(ctx, n_left, mono_left, desc_left, kp_left, oct_left, n_right, mono_right, desc_right,
+                              kp_right, oct_right, level_sigma2, n_levels, cam_left, cam_right, Rlr, tlr,
+                              left_to_right, right_to_left, depth, points3d);
+}
 
 int osg_search_for_triangulation(osg_ctx *ctx, const osg_kf_side *kf1, const osg_kf_side *kf2,
                                  const osg_triang_geom *geom, int only_stereo, int coarse, int check_orientation,

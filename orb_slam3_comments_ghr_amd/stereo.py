@@ -216,3 +216,89 @@ def synth_stereo_frame(rng, n=1200, n_right=None, width=EUROC_W, height=EUROC_H,
     return StereoFrame(desc=desc, x=x, y=y, octave=oct_, desc_r=desc_r, xr=np.array(rx, np.float32)[perm],
                        yr=np.array(ry, np.float32)[perm], octave_r=np.array(ro, np.int32)[perm], left=pyramid(False),
                        right=pyramid(True), scale=scale, mb=mb, mbf=mbf)
+
+
+# ------------------------------------------------------------------ the KannalaBrandt8 rig's stereo step
+
+@dataclass
+class FishEyeStereoFrame:
+    """The inputs of ``Frame::ComputeStereoFishEyeMatches()`` (ref:src/Frame.cc:1546-1603): both cameras'
+    keypoints (x, y, octave) and descriptors with the stereo rows from monoLeft / monoRight on, mvLevelSigma2,
+    the two KannalaBrandt8 parameter vectors and the rig's mRlr / mtlr."""
+    kp_left: np.ndarray    # (Nleft, 2) float32
+    oct_left: np.ndarray   # (Nleft,) int32
+    desc_left: np.ndarray  # (Nleft, 32) uint8
+    mono_left: int
+    kp_right: np.ndarray
+    oct_right: np.ndarray
+    desc_right: np.ndarray
+    mono_right: int
+    level_sigma2: np.ndarray  # float32
+    cam_left: np.ndarray      # fx fy cx cy k0 k1 k2 k3, float32
+    cam_right: np.ndarray
+    Rlr: np.ndarray           # (3, 3) float32
+    tlr: np.ndarray           # (3,) float32
+
+    def args(self):
+        f = lambda a, t: np.ascontiguousarray(a, t)  # noqa: E731
+        return (f(self.kp_left, np.float32), f(self.oct_left, np.int32), f(self.desc_left, np.uint8),
+                f(self.kp_right, np.float32), f(self.oct_right, np.int32), f(self.desc_right, np.uint8),
+                f(self.level_sigma2, np.float32), f(self.cam_left, np.float32), f(self.cam_right, np.float32),
+                f(self.Rlr, np.float32), f(self.tlr, np.float32))
+
+
+def ComputeStereoFishEyeMatches(ctx: Context, F: FishEyeStereoFrame):
+    """``Frame::ComputeStereoFishEyeMatches()`` through ``osg_compute_stereo_fisheye_matches``:
+    (mvLeftToRightMatch, mvRightToLeftMatch, mvDepth, mvStereo3Dpoints, nMatches)."""
+    kl, ol, dl, kr, orr, dr, s2, cl, cr, R, t = F.args()
+    nl, nr = kl.shape[0], kr.shape[0]
+    l2r, r2l = np.empty(nl, np.int32), np.empty(nr, np.int32)
+    depth, p3d = np.empty(nl, np.float32), np.empty((nl, 3), np.float32)
+    n = ctx.check(ctx.lib.osg_compute_stereo_fisheye_matches(
+        ctx.handle, nl, F.mono_left, dl.ctypes.data, kl.ctypes.data, ol.ctypes.data, nr, F.mono_right,
+        dr.ctypes.data, kr.ctypes.data, orr.ctypes.data, s2.ctypes.data, s2.size, cl.ctypes.data, cr.ctypes.data,
+        R.ctypes.data, t.ctypes.data, l2r.ctypes.data, r2l.ctypes.data, depth.ctypes.data, p3d.ctypes.data),
+        "ComputeStereoFishEyeMatches")
+    return l2r, r2l, depth, p3d, n
+
+
+def synth_fisheye_stereo(rng, n_points=600, n_mono_left=150, n_mono_right=140, n_distract=120, flip=0.04,
+                         n_levels=8, factor=1.2):
+    """A TUM-VI-like KannalaBrandt8 rig (EuRoC-sized intrinsics, 10 cm baseline, 1-2 degree relative
+    rotation): n_points 3-D points seen by both cameras (right descriptor = left with `flip` of the bits
+    flipped, pixel noise 0.3 px), mono rows first on each side, unrelated right distractors, right stereo rows
+    shuffled.  Some pairs duplicate a descriptor so the knn ties and the ratio test both occur."""
+    from .frames import KB8_TRIANG, kb8_project
+    cam = KB8_TRIANG.astype(np.float32)
+    a = np.deg2rad(rng.uniform(1, 2))
+    Rlr = np.array([[np.cos(a), 0, np.sin(a)], [0, 1, 0], [-np.sin(a), 0, np.cos(a)]], np.float64)
+    tlr = np.array([0.10, 0.002, -0.001])
+    X = np.stack([rng.uniform(-3, 3, n_points), rng.uniform(-2, 2, n_points), rng.uniform(1.0, 8.0, n_points)], 1)
+    Xr = (X - tlr) @ Rlr  # Rlr^T (X - tlr): left-camera point in the right camera
+    uvl = kb8_project(cam.astype(np.float64), X) + rng.normal(0, 0.3, (n_points, 2))
+    uvr = kb8_project(cam.astype(np.float64), Xr) + rng.normal(0, 0.3, (n_points, 2))
+    dl = rng.integers(0, 256, (n_points, 32), dtype=np.uint8)
+    dup = rng.choice(n_points, n_points // 20, replace=False)
+    dl[dup[1::2]] = dl[dup[0::2][:len(dup[1::2])]]  # equal descriptors: knn ties / failed ratio
+    dr = np.stack([_flip1(rng, d, flip) for d in dl])
+    nd = n_distract
+    dr = np.concatenate([dr, rng.integers(0, 256, (nd, 32), dtype=np.uint8)])
+    uvr = np.concatenate([uvr, rng.uniform([0, 0], [752, 480], (nd, 2))])
+    perm = rng.permutation(len(dr))
+    dr, uvr = dr[perm], uvr[perm]
+    octl = rng.integers(0, n_levels, n_points).astype(np.int32)
+    octr = rng.integers(0, n_levels, len(dr)).astype(np.int32)
+    ml = rng.uniform([0, 0], [752, 480], (n_mono_left, 2))
+    mr = rng.uniform([0, 0], [752, 480], (n_mono_right, 2))
+    sf = scale_factors(n_levels, factor)
+    return FishEyeStereoFrame(
+        kp_left=np.concatenate([ml, uvl]).astype(np.float32),
+        oct_left=np.concatenate([rng.integers(0, n_levels, n_mono_left), octl]).astype(np.int32),
+        desc_left=np.concatenate([rng.integers(0, 256, (n_mono_left, 32), dtype=np.uint8), dl]),
+        mono_left=n_mono_left,
+        kp_right=np.concatenate([mr, uvr]).astype(np.float32),
+        oct_right=np.concatenate([rng.integers(0, n_levels, n_mono_right), octr]).astype(np.int32),
+        desc_right=np.concatenate([rng.integers(0, 256, (n_mono_right, 32), dtype=np.uint8), dr]),
+        mono_right=n_mono_right,
+        level_sigma2=(np.asarray(sf, np.float32) ** 2).astype(np.float32),
+        cam_left=cam, cam_right=cam.copy(), Rlr=Rlr.astype(np.float32), tlr=tlr.astype(np.float32))

@@ -71,6 +71,8 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.oracle_kb8_unproject.restype = None
     lib.oracle_kb8_project.argtypes = [vp, vp, vp]
     lib.oracle_kb8_project.restype = None
+    lib.oracle_stereo_fisheye_matches.argtypes = [C.c_int32, C.c_int32, vp, vp, vp, C.c_int32, C.c_int32, vp, vp, vp,
+                                                  vp, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.oracle_search_by_sim3.argtypes = [C.POINTER(OsgFrame), C.POINTER(OsgFrame), C.POINTER(OsgFuseQueries),
                                           C.POINTER(OsgFuseQueries), f32, vp]
     lib.oracle_compute_distinctive_descriptors.argtypes = [vp, vp, C.c_int, vp]
