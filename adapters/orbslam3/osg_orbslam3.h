@@ -781,6 +781,60 @@ int compute_stereo_matches(FrameT &F)
                  "osg_compute_stereo_matches");
 }
 
+// ------------------------------------------------------- b7' ComputeStereoFishEyeMatches (KB8 rigs)
+// ref:src/Frame.cc:1546-1603, called by the two-camera Frame constructor (:1523).  Reads mvKeys /
+// mvKeysRight, mDescriptors / mDescriptorsRight, monoLeft / monoRight, mvLevelSigma2, both cameras'
+// KannalaBrandt8 parameters (GeometricCamera::getParameter 0..7) and mRlr / mtlr; writes
+// mvLeftToRightMatch, mvRightToLeftMatch, mvDepth, mvuRight (-1), mvStereo3Dpoints and mnCloseMPs = 0.
+template <class FrameT>
+int compute_stereo_fisheye_matches(FrameT &F)
+{
+    osg_ctx *ctx = thread_ctx();
+    const int nl = F.Nleft, nr = F.Nright;
+    std::vector<float> kl(2 * (size_t)nl), kr(2 * (size_t)nr);
+    std::vector<int32_t> ol(nl), orr(nr);
+    for (int i = 0; i < nl; i++) {
+        kl[2 * i] = F.mvKeys[i].pt.x;
+        kl[2 * i + 1] = F.mvKeys[i].pt.y;
+        ol[i] = F.mvKeys[i].octave;
+    }
+    for (int j = 0; j < nr; j++) {
+        kr[2 * j] = F.mvKeysRight[j].pt.x;
+        kr[2 * j + 1] = F.mvKeysRight[j].pt.y;
+        orr[j] = F.mvKeysRight[j].octave;
+    }
+    std::vector<uint8_t> dl, dr;
+    copy_desc_rows(F.mDescriptors, nl, dl);
+    copy_desc_rows(F.mDescriptorsRight, nr, dr);
+    std::vector<float> s2(F.mvLevelSigma2.begin(), F.mvLevelSigma2.end());
+    float c1[8], c2[8], R[9], t[3];
+    for (int k = 0; k < 8; k++) {
+        c1[k] = F.mpCamera->getParameter(k);
+        c2[k] = F.mpCamera2->getParameter(k);
+    }
+    for (int r = 0; r < 3; r++) {
+        for (int c = 0; c < 3; c++) R[3 * r + c] = F.mRlr(r, c);
+        t[r] = F.mtlr(r);
+    }
+    std::vector<float> depth(nl), p3d(3 * (size_t)nl);
+    F.mvLeftToRightMatch.assign(nl, -1);  // :1558-1563
+    F.mvRightToLeftMatch.assign(nr, -1);
+    F.mvuRight.assign(nl, -1.0f);
+    F.mnCloseMPs = 0;
+    const int n = check(ctx,
+                        osg_compute_stereo_fisheye_matches(
+                            ctx, nl, F.monoLeft, dl.data(), kl.data(), ol.data(), nr, F.monoRight, dr.data(),
+                            kr.data(), orr.data(), s2.data(), (int32_t)s2.size(), c1, c2, R, t,
+                            F.mvLeftToRightMatch.data(), F.mvRightToLeftMatch.data(), depth.data(), p3d.data()),
+                        "osg_compute_stereo_fisheye_matches");
+    F.mvDepth.assign(depth.begin(), depth.end());
+    F.mvStereo3Dpoints.resize(nl);
+    for (int i = 0; i < nl; i++)
+        if (F.mvLeftToRightMatch[i] >= 0)
+            for (int k = 0; k < 3; k++) F.mvStereo3Dpoints[i](k) = p3d[3 * (size_t)i + k];
+    return n;
+}
+
 // ----------------------------------------------------------------- b8 ORBextractor per-keypoint stages
 // computeOrientation + computeDescriptors inside ORBextractor::operator() (ref:src/ORBextractor.cc:
 // 585-597, 1534-1545, 1557-1652), for code that lives in ORBextractor.cc (pattern / umax are its

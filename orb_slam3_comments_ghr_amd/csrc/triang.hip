@@ -398,9 +398,9 @@ int triang_run(osg_ctx *ctx, const osg_kf_side *K1, const osg_kf_side *K2, const
 // ---- Frame::ComputeStereoFishEyeMatches (ref:src/Frame.cc:1546-1603) ---------------------------------
 // BFMatcher(NORM_HAMMING).knnMatch(k = 2) of the left stereo rows [monoLeft, Nleft) against the right stereo
 // rows [monoRight, Nright) (ref:src/Frame.cc:47, :1569), Lowe's ratio d0 < d1 * 0.7 (float * double),
-// then KannalaBrandt8::TriangulateMatches with sigma2 of both octaves and depth > 0.0001f.  One lane per
-// left row walks every right row (knn's insertion order: a tie never displaces the first neighbour, it
-// becomes the second).  mvRightToLeftMatch is written in query order by the reference, so the last
+// then KannalaBrandt8::TriangulateMatches with sigma2 of both octaves and depth > 0.0001f.  One
+// left row's wave walks every right row (knn's insertion order: a tie never displaces the first neighbour,
+// it becomes the second).  mvRightToLeftMatch is written in query order by the reference, so the last
 // accepted query wins: atomicMax over the query index.
 struct FishArgs {
     const uint4 *dl, *dr;
@@ -415,23 +415,40 @@ struct FishArgs {
 
 __global__ __launch_bounds__(256) void k_stereo_fisheye(const FishArgs A)
 {
-    const int i = A.ml + (int)(blockIdx.x * 256 + threadIdx.x);
-    if (i >= A.nl) return;
+    // one wave per left row: lanes stride over the right rows, each keeps its own (first, second) in row
+    // order, then a butterfly merges them: first = the least (distance, row), second = the least of the
+    // other summary's first and the winner's second (the multiset's second smallest, as knn's insertion)
+    const int lane = threadIdx.x & 63;
+    const int i = A.ml + (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (i >= A.nl) return;  // wave-uniform
     const uint4 q0 = A.dl[2 * i], q1 = A.dl[2 * i + 1];
-    int b1 = 0x7fffffff, b2 = 0x7fffffff, j1 = -1;
-    for (int j = A.mr; j < A.nr; j++) {
+    unsigned long long k1 = ~0ull;  // (distance << 32) | row
+    unsigned int b2 = 0x7fffffffu;
+    for (int j = A.mr + lane; j < A.nr; j += 64) {
         const uint4 t0 = A.dr[2 * j], t1 = A.dr[2 * j + 1];
-        const int d = __popc(q0.x ^ t0.x) + __popc(q0.y ^ t0.y) + __popc(q0.z ^ t0.z) + __popc(q0.w ^ t0.w) +
-                      __popc(q1.x ^ t1.x) + __popc(q1.y ^ t1.y) + __popc(q1.z ^ t1.z) + __popc(q1.w ^ t1.w);
-        if (d < b1) {
-            b2 = b1;
-            b1 = d;
-            j1 = j;
+        const unsigned int d = __popc(q0.x ^ t0.x) + __popc(q0.y ^ t0.y) + __popc(q0.z ^ t0.z) +
+                               __popc(q0.w ^ t0.w) + __popc(q1.x ^ t1.x) + __popc(q1.y ^ t1.y) +
+                               __popc(q1.z ^ t1.z) + __popc(q1.w ^ t1.w);
+        const unsigned long long k = ((unsigned long long)d << 32) | (unsigned int)j;
+        if (k < k1) {
+            b2 = (unsigned int)(k1 >> 32) < b2 ? (unsigned int)(k1 >> 32) : b2;
+            k1 = k;
         } else if (d < b2) {
             b2 = d;
         }
     }
-    if (A.nr - A.mr < 2 || !((double)(float)b1 < (double)(float)b2 * 0.7)) return;
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+        const unsigned long long ok1 = __shfl_xor(k1, m);
+        const unsigned int ob2 = __shfl_xor(b2, m);
+        const unsigned int w1 = (unsigned int)((k1 < ok1 ? ok1 : k1) >> 32);  // the loser's first
+        const unsigned int wb2 = k1 < ok1 ? b2 : ob2;                          // the winner's second
+        k1 = k1 < ok1 ? k1 : ok1;
+        b2 = w1 < wb2 ? w1 : wb2;
+    }
+    if (lane != 0) return;
+    const int b1 = (int)(k1 >> 32), j1 = (int)(k1 & 0xffffffffu);
+    if (A.nr - A.mr < 2 || !((double)(float)b1 < (double)(float)(int)b2 * 0.7)) return;
     const float2 a = A.kl[i], b = A.kr[j1];
     float p[3];
     const float z = kb8::triangulate_matches(A.caml, A.camr, a.x, a.y, b.x, b.y, A.R, A.t, A.sig2[A.ol[i]],
@@ -518,7 +535,7 @@ int stereo_fisheye_run(osg_ctx *ctx, int32_t n_left, int32_t mono_left, const ui
     hipEvent_t *ev = osg_ctx_events(ctx);
     if (!ev) return osg_set_error(ctx, OSG_E_HIP, "event create failed");
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[0], ctx->stream));
-    hipLaunchKernelGGL(k_stereo_fisheye, dim3((nq + 255) / 256), dim3(256), 0, ctx->stream, A);
+    hipLaunchKernelGGL(k_stereo_fisheye, dim3((nq + 3) / 4), dim3(256), 0, ctx->stream, A);
     OSG_HIP_CHECK(ctx, hipGetLastError());
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_out, dev_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
