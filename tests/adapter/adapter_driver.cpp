@@ -1,7 +1,7 @@
 // adapter_driver.cpp — runs adapters/orbslam3/osg_orbslam3.h on mock ORB-SLAM3 objects built from
 // arrays written by tests/test_adapter.py, and writes the adapter's results back (test-only).
 //
-//   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba fuse fuse_sim3 triang distinct sim3 sim3_kfs sim3pair init stereo gba merge_lba orb
+//   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba fuse fuse_sim3 triang distinct sim3 sim3_kfs sim3pair init stereo fisheye gba merge_lba orb
 //
 // Array file: repeated {u32 name_len, name, u8 dtype ('b' u8, 'i' i32, 'f' f32, 'd' f64), u64 count,
 // data}.
@@ -846,6 +846,52 @@ int main(int argc, char **argv)
             out["nmatches"] = make('i', std::vector<int32_t>{nm});
             out["ur"] = make('f', F.mvuRight);
             out["depth"] = make('f', F.mvDepth);
+        } else if (mode == "fisheye") {
+            // "FE.kl" / "FE.kr" (x, y), "FE.ol" / "FE.or", "FE.dl" / "FE.dr", "FE.mono" (monoLeft, monoRight),
+            // "FE.sig2", "FE.cam" (2 x 8 KannalaBrandt8), "FE.R" (3x3), "FE.t"
+            Frame F;
+            const int nl = (int)get(in, "FE.ol").n, nr = (int)get(in, "FE.or").n;
+            auto kps = [&](const char *k, const char *o, int cnt) {
+                std::vector<cv::KeyPoint> v(cnt);
+                for (int i = 0; i < cnt; i++) {
+                    v[i].pt.x = get(in, k).p<float>()[2 * i];
+                    v[i].pt.y = get(in, k).p<float>()[2 * i + 1];
+                    v[i].octave = get(in, o).p<int32_t>()[i];
+                }
+                return v;
+            };
+            F.N = nl + nr;
+            F.Nleft = nl;
+            F.Nright = nr;
+            F.mvKeys = kps("FE.kl", "FE.ol", nl);
+            F.mvKeysRight = kps("FE.kr", "FE.or", nr);
+            F.mDescriptors = cv::Mat(nl, 32);
+            std::memcpy(F.mDescriptors.buf.data(), get(in, "FE.dl").b.data(), (size_t)nl * 32);
+            F.mDescriptorsRight = cv::Mat(nr, 32);
+            std::memcpy(F.mDescriptorsRight.buf.data(), get(in, "FE.dr").b.data(), (size_t)nr * 32);
+            F.monoLeft = get(in, "FE.mono").p<int32_t>()[0];
+            F.monoRight = get(in, "FE.mono").p<int32_t>()[1];
+            const Arr &s2 = get(in, "FE.sig2");
+            F.mvLevelSigma2.assign(s2.p<float>(), s2.p<float>() + s2.n);
+            Camera c1, c2;
+            c1.type = c2.type = OSG_CAM_KB8;
+            c1.params.assign(get(in, "FE.cam").p<float>(), get(in, "FE.cam").p<float>() + 8);
+            c2.params.assign(get(in, "FE.cam").p<float>() + 8, get(in, "FE.cam").p<float>() + 16);
+            F.mpCamera = &c1;
+            F.mpCamera2 = &c2;
+            for (int k = 0; k < 9; k++) F.mRlr.a[k] = get(in, "FE.R").p<float>()[k];
+            for (int k = 0; k < 3; k++) F.mtlr.a[k] = get(in, "FE.t").p<float>()[k];
+            const int nm = osg_orbslam3::compute_stereo_fisheye_matches(F);
+            std::vector<float> p3d(3 * (size_t)nl, 0.f);
+            for (int i = 0; i < nl; i++)
+                if (F.mvLeftToRightMatch[i] >= 0)
+                    for (int k = 0; k < 3; k++) p3d[3 * (size_t)i + k] = F.mvStereo3Dpoints[i](k);
+            out["nmatches"] = make('i', std::vector<int32_t>{nm, F.mnCloseMPs});
+            out["l2r"] = make('i', std::vector<int32_t>(F.mvLeftToRightMatch.begin(), F.mvLeftToRightMatch.end()));
+            out["r2l"] = make('i', std::vector<int32_t>(F.mvRightToLeftMatch.begin(), F.mvRightToLeftMatch.end()));
+            out["depth"] = make('f', F.mvDepth);
+            out["ur"] = make('f', F.mvuRight);
+            out["p3d"] = make('f', p3d);
         } else if (mode == "orb") {
             // levels "O.raw" / "O.blur" concatenated with "O.dims" (rows, cols); keypoints "O.x", "O.y",
             // "O.level" (sorted by level); "O.pattern" (512 x 2), "O.umax" (16).  mvImagePyramid levels are

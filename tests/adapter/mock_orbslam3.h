@@ -52,6 +52,19 @@ struct KeyFrame;
 struct Camera {
     int type = OSG_CAM_PINHOLE;
     std::vector<float> params;
+    float getParameter(const int i) const { return params[i]; }  // GeometricCamera::getParameter
+};
+
+// Eigen::Matrix3f / Vector3f as far as the adapters use them: m(r, c), v(k)
+struct Mat3f {
+    float a[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    float &operator()(int r, int c) { return a[3 * r + c]; }
+    float operator()(int r, int c) const { return a[3 * r + c]; }
+};
+struct Vec3f {
+    float a[3] = {0, 0, 0};
+    float &operator()(int k) { return a[k]; }
+    float operator()(int k) const { return a[k]; }
 };
 
 struct MapPoint {
@@ -122,6 +135,12 @@ struct Frame {
     std::map<unsigned int, std::vector<unsigned int>> mFeatVec;
     double pose[7] = {0, 0, 0, 1, 0, 0, 0};
     float tlc_z_value = 0;  // test-only: MockHooks::tlc_z
+    // two-camera (KannalaBrandt8) Frame members of ComputeStereoFishEyeMatches (ref:include/Frame.h)
+    int Nright = -1, monoLeft = -1, monoRight = -1, mnCloseMPs = -1;
+    std::vector<float> mvLevelSigma2;
+    Mat3f mRlr;
+    Vec3f mtlr;
+    std::vector<Vec3f> mvStereo3Dpoints;
 };
 
 struct KeyFrame {
