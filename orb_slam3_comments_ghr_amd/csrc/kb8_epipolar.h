@@ -198,23 +198,28 @@ __device__ inline void null4(const float A[4][4], double v[4])
                     V[k][q] = sn * vkp + c * vkq;
                 }
             }
+    // the first least diagonal entry, and its column of V, with static indices only (a dynamic index
+    // would put M and V in scratch memory)
     int m = 0;
+    double best = M[0][0];
 #pragma unroll
     for (int i = 1; i < 4; i++)
-        if (M[i][i] < M[m][m]) m = i;
+        if (M[i][i] < best) {
+            best = M[i][i];
+            m = i;
+        }
 #pragma unroll
-    for (int k = 0; k < 4; k++) v[k] = V[k][m];
+    for (int k = 0; k < 4; k++) v[k] = m == 0 ? V[k][0] : m == 1 ? V[k][1] : m == 2 ? V[k][2] : V[k][3];
 }
 
 // TriangulateMatches with this = cam1 (pCamera1), pCamera2 = cam2: z1 with p3D = x3D, or the reference's
 // negative codes -1..-5 (p3D untouched)
-__device__ inline float triangulate_matches(const float *cam1, const float *cam2, float x1, float y1, float x2,
-                                            float y2, const float *R12, const float *t12, float sigmaLevel,
-                                            float unc, float *p3D)
+// the part after the two unprojections (r1 = cam1.unproject(kp1), r2 = cam2.unproject(kp2))
+__device__ inline float triangulate_rays(const float *cam1, const float *cam2, const float *r1, const float *r2,
+                                         float x1, float y1, float x2, float y2, const float *R12, const float *t12,
+                                         float sigmaLevel, float unc, float *p3D)
 {
-    float r1[3], r2[3], r21[3];
-    unproject(cam1, x1, y1, r1);
-    unproject(cam2, x2, y2, r2);
+    float r21[3];
 #pragma unroll
     for (int i = 0; i < 3; i++) r21[i] = R12[3 * i] * r2[0] + R12[3 * i + 1] * r2[1] + R12[3 * i + 2] * r2[2];
     const float dot = r1[0] * r21[0] + r1[1] * r21[1] + r1[2] * r21[2];
@@ -263,6 +268,16 @@ __device__ inline float triangulate_matches(const float *cam1, const float *cam2
     p3D[1] = x3D[1];
     p3D[2] = x3D[2];
     return z1;
+}
+
+__device__ inline float triangulate_matches(const float *cam1, const float *cam2, float x1, float y1, float x2,
+                                            float y2, const float *R12, const float *t12, float sigmaLevel,
+                                            float unc, float *p3D)
+{
+    float r1[3], r2[3];
+    unproject(cam1, x1, y1, r1);
+    unproject(cam2, x2, y2, r2);
+    return triangulate_rays(cam1, cam2, r1, r2, x1, y1, x2, y2, R12, t12, sigmaLevel, unc, p3D);
 }
 
 // epipolarConstrain: TriangulateMatches(...) > 0.0001f (ref:src/CameraModels/KannalaBrandt8.cpp:321-326)

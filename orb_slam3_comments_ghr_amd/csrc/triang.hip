@@ -446,13 +446,18 @@ __global__ __launch_bounds__(256) void k_stereo_fisheye(const FishArgs A)
         k1 = k1 < ok1 ? k1 : ok1;
         b2 = w1 < wb2 ? w1 : wb2;
     }
-    if (lane != 0) return;
-    const int b1 = (int)(k1 >> 32), j1 = (int)(k1 & 0xffffffffu);
-    if (A.nr - A.mr < 2 || !((double)(float)b1 < (double)(float)(int)b2 * 0.7)) return;
+    const int b1 = (int)(k1 >> 32), j1 = (int)(k1 & 0xffffffffu);  // every lane holds the merged result
+    if (A.nr - A.mr < 2 || !((double)(float)b1 < (double)(float)(int)b2 * 0.7)) return;  // wave-uniform
+    // lanes 0 and 1 unproject the left and the right keypoint side by side, lane 0 triangulates
     const float2 a = A.kl[i], b = A.kr[j1];
+    float r[3] = {0.f, 0.f, 0.f};
+    if (lane < 2) kb8::unproject(lane ? A.camr : A.caml, lane ? b.x : a.x, lane ? b.y : a.y, r);
+    const float r1[3] = {r[0], r[1], r[2]};
+    const float r2[3] = {__shfl(r[0], 1), __shfl(r[1], 1), __shfl(r[2], 1)};
+    if (lane != 0) return;
     float p[3];
-    const float z = kb8::triangulate_matches(A.caml, A.camr, a.x, a.y, b.x, b.y, A.R, A.t, A.sig2[A.ol[i]],
-                                             A.sig2[A.orr[j1]], p);
+    const float z = kb8::triangulate_rays(A.caml, A.camr, r1, r2, a.x, a.y, b.x, b.y, A.R, A.t, A.sig2[A.ol[i]],
+                                          A.sig2[A.orr[j1]], p);
     if (!(z > 0.0001f)) return;
     A.l2r[i] = j1;
     A.depth[i] = z;
