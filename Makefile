@@ -38,7 +38,7 @@ $(OBJDIR)/dbow.o: $(CSRC)/dbow.hip $(HDRS) include/osg_dbow.h $(CSRC)/match_comm
 $(OBJDIR)/fuse.o: $(CSRC)/fuse.hip $(HDRS) $(CSRC)/match_common.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(EXACT) -c $< -o $@
 
-$(OBJDIR)/triang.o: $(CSRC)/triang.hip $(HDRS) $(CSRC)/match_common.h | $(OBJDIR)
+$(OBJDIR)/triang.o: $(CSRC)/triang.hip $(HDRS) $(CSRC)/match_common.h $(CSRC)/kb8_epipolar.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(EXACT) -c $< -o $@
 
 $(OBJDIR)/desc.o: $(CSRC)/desc.hip $(HDRS) $(CSRC)/match_common.h | $(OBJDIR)

@@ -28,13 +28,13 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <list>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <set>
-#include <stdexcept>
 #include <string>
 #include <tuple>
 #include <utility>
@@ -47,33 +47,105 @@
 
 namespace osg_orbslam3 {
 
-struct Error : std::runtime_error {
-    int code;
-    Error(int c, const std::string &what) : std::runtime_error(what), code(c) {}
-};
+// ------------------------------------------------------------------------------------ errors
+// Nothing in this adapter throws: ORB-SLAM3's Tracking, LocalMapping and LoopClosing
+// threads have no try / catch.  A failing ABI call (a negative OSG_E_* code) is logged once per
+// thread and code, and the entry point then returns what the reference returns when it finds
+// nothing:
+//   * matchers: 0 matches, the caller's slots untouched (the output vectors the reference
+//     re-initialises at its start -- SearchByBoW's, SearchForInitialization's vnMatches12,
+//     SearchForTriangulation's vMatchedPairs, the stereo Frame members -- re-initialised the same way);
+//   * PoseOptimization: 0, pose untouched (ref:src/Optimizer.cc:289-290);
+//   * LocalBundleAdjustment / the merge BA: the early return of an abort, nothing written back
+//     (ref:src/Optimizer.cc:1869-1873, 2112-2114, 5444-5446);
+//   * global BA: the map's state written back unchanged, i.e. an optimize() that stopped before its
+//     first iteration (LoopClosing then applies mTcwGBA / mPosGBA as after any GBA);
+//   * ORBextractor stages: no keypoints (as for an empty image, ref:src/ORBextractor.cc:1586-1587).
+//
+// Built with -DOSG_ADAPTER_FAULT_INJECTION (tests/adapter/adapter_fault.cpp only), fault::ctx_rc makes
+// the context creation fail and fault::call_rc replaces every ABI call's return code.
+#ifdef OSG_ADAPTER_FAULT_INJECTION
+namespace fault {
+inline thread_local int ctx_rc = 0;
+inline thread_local int call_rc = 0;
+inline thread_local int reports = 0;  // log lines written by this thread
+}  // namespace fault
+#endif
+
+inline void report(osg_ctx *ctx, int rc, const char *what)
+{
+    static thread_local std::set<int> seen;
+    if (!seen.insert(rc).second) return;
+#ifdef OSG_ADAPTER_FAULT_INJECTION
+    fault::reports++;
+    if (fault::call_rc) ctx = nullptr;  // the injected call never reached the context
+#endif
+    std::fprintf(stderr, "osg_orbslam3: %s: %s%s%s (later %s errors on this thread are not logged)\n", what,
+                 osg_strerror(rc), ctx ? ": " : "", ctx ? osg_ctx_last_error(ctx) : "", osg_strerror(rc));
+}
 
 // One context per host thread: Tracking, LocalMapping and LoopClosing each get their own stream
-// and scratch (ref:src/System.cc:234,254 start them as separate threads).
+// and scratch (ref:src/System.cc:234,254 start them as separate threads).  nullptr when no context
+// can be created (no gfx950 device, ...); ctx_error() then holds the code, and every call() on this
+// thread returns it.
+struct ThreadCtx {
+    osg_ctx *ctx = nullptr;
+    int rc = 0;
+    bool tried = false;
+    ~ThreadCtx()
+    {
+        if (ctx) osg_ctx_destroy(ctx);
+    }
+};
+inline ThreadCtx &thread_ctx_slot()
+{
+    static thread_local ThreadCtx h;
+    return h;
+}
+
 inline osg_ctx *thread_ctx(int device = 0)
 {
-    struct Holder {
-        osg_ctx *ctx = nullptr;
-        ~Holder()
-        {
-            if (ctx) osg_ctx_destroy(ctx);
+    ThreadCtx &h = thread_ctx_slot();
+#ifdef OSG_ADAPTER_FAULT_INJECTION
+    if (fault::ctx_rc) {
+        report(nullptr, fault::ctx_rc, "osg_ctx_create");
+        return nullptr;
+    }
+    if (fault::call_rc) return nullptr;  // call() returns the injected code before it needs a context
+#endif
+    if (!h.ctx && !h.tried) {
+        h.tried = true;
+        h.rc = osg_ctx_create(device, &h.ctx);
+        if (h.rc < 0) {
+            h.ctx = nullptr;
+            report(nullptr, h.rc, "osg_ctx_create");
         }
-    };
-    static thread_local Holder h;
-    if (!h.ctx) {
-        const int rc = osg_ctx_create(device, &h.ctx);
-        if (rc < 0) throw Error(rc, std::string("osg_ctx_create: ") + osg_strerror(rc));
     }
     return h.ctx;
 }
 
-inline int check(osg_ctx *ctx, int rc, const char *what)
+inline int ctx_error()
 {
-    if (rc < 0) throw Error(rc, std::string(what) + ": " + osg_strerror(rc) + " (" + osg_ctx_last_error(ctx) + ")");
+#ifdef OSG_ADAPTER_FAULT_INJECTION
+    if (fault::ctx_rc) return fault::ctx_rc;
+#endif
+    const int rc = thread_ctx_slot().rc;
+    return rc < 0 ? rc : OSG_E_NODEVICE;
+}
+
+// Runs one ABI call f() on the thread's context; returns its code (>= 0) or a logged OSG_E_* code.
+template <class F>
+inline int call(osg_ctx *ctx, const char *what, F &&f)
+{
+#ifdef OSG_ADAPTER_FAULT_INJECTION
+    if (fault::call_rc) {
+        report(ctx, fault::call_rc, what);
+        return fault::call_rc;
+    }
+#endif
+    if (!ctx) return ctx_error();  // already logged by thread_ctx()
+    const int rc = f();
+    if (rc < 0) report(ctx, rc, what);
     return rc;
 }
 
@@ -270,9 +342,11 @@ int search_by_projection_mps(FrameT &F, const std::vector<MapPointT *> &vpMapPoi
     q.view_cos_r = vcr.data();
     q.pred_level_r = lvl_r.data();
     Slots<MapPointT> slots(F.mvpMapPoints, nq, true);
-    const int nm = check(ctx, osg_search_by_projection_mps(ctx, &fv.v, &q, nnratio, th, bFarPoints, thFarPoints,
-                                                           slots.mp.data(), slots.taken.data()),
-                         "osg_search_by_projection_mps");
+    const int nm = call(ctx, "osg_search_by_projection_mps", [&] {
+        return osg_search_by_projection_mps(ctx, &fv.v, &q, nnratio, th, bFarPoints, thFarPoints, slots.mp.data(),
+                                            slots.taken.data());
+    });
+    if (nm < 0) return 0;
     slots.apply(F.mvpMapPoints, vpMapPoints, nq);
     return nm;
 }
@@ -328,9 +402,10 @@ int search_by_projection_last(FrameT &CF, const FrameT &LF, float th, bool bMono
     }
     q.tlc_z = H::tlc_z(CF, LF);
     Slots<MapPointT> slots(CF.mvpMapPoints, n, true);
-    const int nm = check(ctx, osg_search_by_projection_last(ctx, &fv.v, &q, th, bMono, checkOri, slots.mp.data(),
-                                                            slots.taken.data()),
-                         "osg_search_by_projection_last");
+    const int nm = call(ctx, "osg_search_by_projection_last", [&] {
+        return osg_search_by_projection_last(ctx, &fv.v, &q, th, bMono, checkOri, slots.mp.data(), slots.taken.data());
+    });
+    if (nm < 0) return 0;
     slots.apply(CF.mvpMapPoints, queries, n);
     return nm;
 }
@@ -368,8 +443,10 @@ int search_by_projection_kf(FrameT &CF, KeyFrameT *pKF, const std::set<MapPointT
     q.pred_level = lvl.data();
     q.angle = ang.data();
     Slots<MapPointT> slots(CF.mvpMapPoints, n, false);
-    const int nm = check(ctx, osg_search_by_projection_kf(ctx, &fv.v, &q, th, ORBdist, checkOri, slots.mp.data()),
-                         "osg_search_by_projection_kf");
+    const int nm = call(ctx, "osg_search_by_projection_kf", [&] {
+        return osg_search_by_projection_kf(ctx, &fv.v, &q, th, ORBdist, checkOri, slots.mp.data());
+    });
+    if (nm < 0) return 0;
     slots.apply(CF.mvpMapPoints, vpMPs, n);
     return nm;
 }
@@ -420,8 +497,10 @@ int fuse(KeyFrameT *pKF, const std::vector<MapPointT *> &vpMapPoints, float th, 
     q.ur = ur.data();
     q.pred_level = lvl.data();
     q.inv_level_sigma2 = inv_s2.data();
-    check(ctx, osg_fuse_search(ctx, &fv.v, &q, th, bRight ? 1 : 0, 1, best_idx.data(), best_dist.data()),
-          "osg_fuse_search");
+    if (call(ctx, "osg_fuse_search", [&] {
+            return osg_fuse_search(ctx, &fv.v, &q, th, bRight ? 1 : 0, 1, best_idx.data(), best_dist.data());
+        }) < 0)
+        return 0;
     int nFused = 0;
     for (int i = 0; i < n; i++) {  // ref:src/ORBmatcher.cc:1514-1539, in MapPoint order
         MapPointT *pMP = vpMapPoints[i];
@@ -477,7 +556,9 @@ int fuse_sim3(KeyFrameT *pKF, const Sim3T &Scw, const std::vector<MapPointT *> &
     q.u = u.data();
     q.v = v.data();
     q.pred_level = lvl.data();
-    check(ctx, osg_fuse_search(ctx, &fv.v, &q, th, 0, 0, best_idx.data(), best_dist.data()), "osg_fuse_search");
+    if (call(ctx, "osg_fuse_search",
+             [&] { return osg_fuse_search(ctx, &fv.v, &q, th, 0, 0, best_idx.data(), best_dist.data()); }) < 0)
+        return 0;
     int nFused = 0;
     for (int i = 0; i < n; i++) {  // ref:src/ORBmatcher.cc:1661-1681
         if (!valid[i] || best_idx[i] < 0) continue;
@@ -539,8 +620,10 @@ int search_by_bow_kf_f(KeyFrameT *pKF, FrameT &F, std::vector<MapPointT *> &vpMa
     osg_bow_side sk{nk, pKF->NLeft, dk.data(), ak.data(), idk.data(), good.data(), fk.view()};
     osg_bow_side sf{nf, F.Nleft, df.data(), af.data(), nullptr, nullptr, ff.view()};
     std::vector<int32_t> out(nf, -1);
-    const int nm = check(ctx, osg_search_by_bow_kf_f(ctx, &sk, &sf, nnratio, checkOri, out.data()), "osg_search_by_bow_kf_f");
-    vpMapPointMatches.assign(nf, nullptr);
+    const int nm = call(ctx, "osg_search_by_bow_kf_f",
+                        [&] { return osg_search_by_bow_kf_f(ctx, &sk, &sf, nnratio, checkOri, out.data()); });
+    vpMapPointMatches.assign(nf, nullptr);  // ref:src/ORBmatcher.cc:268
+    if (nm < 0) return 0;
     for (int i = 0; i < nf; i++)
         if (out[i] >= 0) vpMapPointMatches[i] = vpMPsKF[out[i]];
     return nm;
@@ -575,8 +658,10 @@ int search_by_bow_kf_kf(KeyFrameT *pKF1, KeyFrameT *pKF2, std::vector<MapPointT 
     osg_bow_side s1{n1, pKF1->NLeft, d1.data(), a1.data(), id1.data(), g1.data(), f1.view()};
     osg_bow_side s2{n2, pKF2->NLeft, d2.data(), a2.data(), id2.data(), g2.data(), f2.view()};
     std::vector<int32_t> out(n1, -1);
-    const int nm = check(ctx, osg_search_by_bow_kf_kf(ctx, &s1, &s2, nnratio, checkOri, out.data()), "osg_search_by_bow_kf_kf");
-    vpMatches12.assign(n1, nullptr);
+    const int nm = call(ctx, "osg_search_by_bow_kf_kf",
+                        [&] { return osg_search_by_bow_kf_kf(ctx, &s1, &s2, nnratio, checkOri, out.data()); });
+    vpMatches12.assign(n1, nullptr);  // ref:src/ORBmatcher.cc:904
+    if (nm < 0) return 0;
     for (int i = 0; i < n1; i++)
         if (out[i] >= 0) vpMatches12[i] = v2[out[i]];
     return nm;
@@ -615,8 +700,10 @@ int search_by_projection_sim3(KeyFrameT *pKF, const Sim3T &Scw, const std::vecto
     q.u = u.data();
     q.v = v.data();
     q.pred_level = lvl.data();
-    const int nm = check(ctx, osg_search_by_projection_sim3(ctx, &fv.v, &q, (float)th, ratioHamming, slot_query.data()),
-                         "osg_search_by_projection_sim3");
+    const int nm = call(ctx, "osg_search_by_projection_sim3", [&] {
+        return osg_search_by_projection_sim3(ctx, &fv.v, &q, (float)th, ratioHamming, slot_query.data());
+    });
+    if (nm < 0) return 0;
     for (int i = 0; i < pKF->N; i++)
         if (slot_query[i] >= 0) {  // vpMatched[bestIdx] = pMP (, vpMatchedKF[bestIdx] = pKFi), :614 / :726-727
             vpMatched[i] = vpPoints[slot_query[i]];
@@ -678,8 +765,9 @@ int search_by_sim3(KeyFrameT *pKF1, KeyFrameT *pKF2, std::vector<MapPointT *> &v
     gather(vpMapPoints1, already1, true, q12);
     gather(vpMapPoints2, already2, false, q21);
     std::vector<int32_t> match12(N1, -1);
-    const int nFound = check(ctx, osg_search_by_sim3(ctx, &f1.v, &f2.v, &q12.q, &q21.q, th, match12.data()),
-                             "osg_search_by_sim3");
+    const int nFound = call(ctx, "osg_search_by_sim3",
+                            [&] { return osg_search_by_sim3(ctx, &f1.v, &f2.v, &q12.q, &q21.q, th, match12.data()); });
+    if (nFound < 0) return 0;
     for (int i1 = 0; i1 < N1; i1++)  // :1920-1936
         if (match12[i1] >= 0) vpMatches12[i1] = vpMapPoints2[match12[i1]];
     return nFound;
@@ -701,8 +789,13 @@ int search_for_initialization(FrameT &F1, FrameT &F2, std::vector<PointT> &vbPre
         prev[2 * i + 1] = vbPrevMatched[i].y;
     }
     std::vector<int32_t> m12(n1, -1);
-    const int nm = check(ctx, osg_search_for_initialization(ctx, &f1.v, &f2.v, prev.data(), windowSize, nnratio, checkOri,
-                                                            m12.data()), "osg_search_for_initialization");
+    const int nm = call(ctx, "osg_search_for_initialization", [&] {
+        return osg_search_for_initialization(ctx, &f1.v, &f2.v, prev.data(), windowSize, nnratio, checkOri, m12.data());
+    });
+    if (nm < 0) {
+        vnMatches12.assign(n1, -1);  // ref:src/ORBmatcher.cc:739
+        return 0;
+    }
     vnMatches12.assign(m12.begin(), m12.end());
     for (int i = 0; i < n1; i++)
         if (m12[i] >= 0) {
@@ -777,8 +870,14 @@ int compute_stereo_matches(FrameT &F)
     s.right = pr.v;
     F.mvuRight.assign(n, -1.0f);  // :1134-1135
     F.mvDepth.assign(n, -1.0f);
-    return check(ctx, osg_compute_stereo_matches(ctx, &s, F.mvuRight.data(), F.mvDepth.data()),
-                 "osg_compute_stereo_matches");
+    const int nm = call(ctx, "osg_compute_stereo_matches",
+                        [&] { return osg_compute_stereo_matches(ctx, &s, F.mvuRight.data(), F.mvDepth.data()); });
+    if (nm < 0) {  // no stereo match for any keypoint
+        F.mvuRight.assign(n, -1.0f);
+        F.mvDepth.assign(n, -1.0f);
+        return 0;
+    }
+    return nm;
 }
 
 // ------------------------------------------------------- b7' ComputeStereoFishEyeMatches (KB8 rigs)
@@ -821,14 +920,20 @@ int compute_stereo_fisheye_matches(FrameT &F)
     F.mvRightToLeftMatch.assign(nr, -1);
     F.mvuRight.assign(nl, -1.0f);
     F.mnCloseMPs = 0;
-    const int n = check(ctx,
-                        osg_compute_stereo_fisheye_matches(
-                            ctx, nl, F.monoLeft, dl.data(), kl.data(), ol.data(), nr, F.monoRight, dr.data(),
-                            kr.data(), orr.data(), s2.data(), (int32_t)s2.size(), c1, c2, R, t,
-                            F.mvLeftToRightMatch.data(), F.mvRightToLeftMatch.data(), depth.data(), p3d.data()),
-                        "osg_compute_stereo_fisheye_matches");
-    F.mvDepth.assign(depth.begin(), depth.end());
+    const int n = call(ctx, "osg_compute_stereo_fisheye_matches", [&] {
+        return osg_compute_stereo_fisheye_matches(ctx, nl, F.monoLeft, dl.data(), kl.data(), ol.data(), nr, F.monoRight,
+                                                  dr.data(), kr.data(), orr.data(), s2.data(), (int32_t)s2.size(), c1,
+                                                  c2, R, t, F.mvLeftToRightMatch.data(), F.mvRightToLeftMatch.data(),
+                                                  depth.data(), p3d.data());
+    });
     F.mvStereo3Dpoints.resize(nl);
+    if (n < 0) {  // the :1558-1563 initial state: no stereo match
+        F.mvLeftToRightMatch.assign(nl, -1);
+        F.mvRightToLeftMatch.assign(nr, -1);
+        F.mvDepth.assign(nl, -1.0f);
+        return 0;
+    }
+    F.mvDepth.assign(depth.begin(), depth.end());
     for (int i = 0; i < nl; i++)
         if (F.mvLeftToRightMatch[i] >= 0)
             for (int k = 0; k < 3; k++) F.mvStereo3Dpoints[i](k) = p3d[3 * (size_t)i + k];
@@ -858,7 +963,11 @@ int orb_describe(const std::vector<MatT> &pyramid, const std::vector<MatT> &blur
             lev.push_back(l);
         }
     const int n = (int)x.size();
-    if (pattern.size() != 512 || umax.size() < 16) throw Error(OSG_E_INVALID, "orb_describe: pattern / umax shape");
+    desc.assign((size_t)n * 32, 0);
+    if (pattern.size() != 512 || umax.size() < 16) {
+        report(ctx, OSG_E_INVALID, "orb_describe: pattern / umax shape");
+        return 0;
+    }
     std::vector<int32_t> pat(2 * pattern.size());
     for (size_t i = 0; i < pattern.size(); i++) {  // cv::Point -> (x, y) int pairs
         pat[2 * i] = pattern[i].x;
@@ -868,10 +977,13 @@ int orb_describe(const std::vector<MatT> &pyramid, const std::vector<MatT> &blur
     PyramidView<MatT> raw(pyramid, levels), blur(blurred, levels);
     osg_orb_keypoints K{n, x.data(), y.data(), lev.data()};
     std::vector<float> angle(n);
-    desc.assign((size_t)n * 32, 0);
-    const int outside = check(ctx, osg_orb_describe(ctx, &raw.v, &blur.v, &K, pat.data(), um.data(), 1, angle.data(),
-                                                    desc.data()),
-                              "osg_orb_describe");
+    const int outside = call(ctx, "osg_orb_describe", [&] {
+        return osg_orb_describe(ctx, &raw.v, &blur.v, &K, pat.data(), um.data(), 1, angle.data(), desc.data());
+    });
+    if (outside < 0) {
+        desc.assign((size_t)n * 32, 0);
+        return 0;
+    }
     int i = 0;
     for (int l = 0; l < levels; l++)
         for (KeyPointT &kp : allKeypoints[l]) kp.angle = angle[i++];
@@ -891,18 +1003,22 @@ int compute_keypoints_oct_tree(const std::vector<MatT> &pyramid, std::vector<std
 {
     osg_ctx *ctx = thread_ctx();
     const int levels = (int)pyramid.size();
-    if ((int)nFeaturesPerLevel.size() < levels || (int)scaleFactors.size() < levels)
-        throw Error(OSG_E_INVALID, "compute_keypoints_oct_tree: per-level tables");
+    allKeypoints.assign(levels, {});
+    if ((int)nFeaturesPerLevel.size() < levels || (int)scaleFactors.size() < levels) {
+        report(ctx, OSG_E_INVALID, "compute_keypoints_oct_tree: per-level tables");
+        return 0;
+    }
     PyramidView<MatT> raw(pyramid, levels);
     std::vector<int32_t> nf(nFeaturesPerLevel.begin(), nFeaturesPerLevel.begin() + levels);
     int cap = 64;
     for (int l = 0; l < levels; l++) cap += 2 * std::max(nf[l], 0) + 8;  // the octree stops within 3 of N
     std::vector<float> x(cap), y(cap), resp(cap), size(cap);
     std::vector<int32_t> ls(levels + 1);
-    check(ctx, osg_orb_detect(ctx, &raw.v, iniThFAST, minThFAST, nf.data(), scaleFactors.data(), cap, x.data(),
-                              y.data(), resp.data(), size.data(), ls.data()),
-          "osg_orb_detect");
-    allKeypoints.assign(levels, {});
+    if (call(ctx, "osg_orb_detect", [&] {
+            return osg_orb_detect(ctx, &raw.v, iniThFAST, minThFAST, nf.data(), scaleFactors.data(), cap, x.data(),
+                                  y.data(), resp.data(), size.data(), ls.data());
+        }) < 0)
+        return 0;
     for (int l = 0; l < levels; l++) {
         allKeypoints[l].reserve(ls[l + 1] - ls[l]);
         for (int i = ls[l]; i < ls[l + 1]; i++) {
@@ -958,9 +1074,11 @@ int search_for_triangulation(KeyFrameT *pKF1, KeyFrameT *pKF2, std::vector<std::
     osg_triang_geom g;
     H::triang_geom(pKF1, pKF2, g);
     std::vector<int32_t> m12(pKF1->N, -1);
-    const int nm = check(ctx, osg_search_for_triangulation(ctx, &v[0], &v[1], &g, bOnlyStereo, bCoarse, checkOri,
-                                                           m12.data()), "osg_search_for_triangulation");
-    vMatchedPairs.clear();
+    const int nm = call(ctx, "osg_search_for_triangulation", [&] {
+        return osg_search_for_triangulation(ctx, &v[0], &v[1], &g, bOnlyStereo, bCoarse, checkOri, m12.data());
+    });
+    vMatchedPairs.clear();  // ref:src/ORBmatcher.cc:1317
+    if (nm < 0) return 0;
     vMatchedPairs.reserve(nm);
     for (int i = 0; i < pKF1->N; i++)
         if (m12[i] >= 0) vMatchedPairs.push_back(std::make_pair((size_t)i, (size_t)m12[i]));
@@ -999,8 +1117,9 @@ void compute_distinctive_descriptors(const std::vector<MapPointT *> &vpMPs)
         start[p + 1] = (int32_t)(rows.size() / 32);
     }
     std::vector<int32_t> best(np, -1);
-    check(ctx, osg_compute_distinctive_descriptors(ctx, rows.data(), start.data(), np, best.data()),
-          "osg_compute_distinctive_descriptors");
+    if (call(ctx, "osg_compute_distinctive_descriptors",
+             [&] { return osg_compute_distinctive_descriptors(ctx, rows.data(), start.data(), np, best.data()); }) < 0)
+        return;  // descriptors unchanged
     for (int p = 0; p < np; p++)
         if (best[p] >= 0) H::set_descriptor(vpMPs[p], &rows[32 * ((size_t)start[p] + best[p])]);
 }
@@ -1077,7 +1196,7 @@ int pose_optimization(FrameT *pFrame, MutexT *gather_mutex = nullptr)
     std::vector<uint8_t> outl(kind.size());
     osg_pose_result r{};
     r.outlier = outl.data();
-    check(ctx, osg_pose_optimization(ctx, &p, &r), "osg_pose_optimization");
+    if (call(ctx, "osg_pose_optimization", [&] { return osg_pose_optimization(ctx, &p, &r); }) < 0) return 0;
     if (p.n_edges < 3) return 0;  // ref:src/Optimizer.cc:289-290 (pose untouched)
     for (size_t e = 0; e < slot.size(); e++) pFrame->mvbOutlier[slot[e]] = outl[e] != 0;
     H::set_pose(*pFrame, r.pose);
@@ -1214,8 +1333,12 @@ LbaOutcome<KeyFrameT, MapPointT> local_bundle_adjustment(const std::list<KeyFram
     r.point = point_out.data();
     r.edge_bad = bad.data();
     static_assert(sizeof(bool) == 1, "pbStopFlag is passed as one byte");
-    check(ctx, osg_local_bundle_adjustment(ctx, &g, &r, reinterpret_cast<const volatile uint8_t *>(pbStopFlag)),
-          "osg_local_bundle_adjustment");
+    if (call(ctx, "osg_local_bundle_adjustment", [&] {
+            return osg_local_bundle_adjustment(ctx, &g, &r, reinterpret_cast<const volatile uint8_t *>(pbStopFlag));
+        }) < 0) {
+        out.aborted = true;  // no poses: the caller returns as on an abort, nothing written back
+        return out;
+    }
     out.aborted = r.aborted != 0;
     // ref:src/Optimizer.cc:2123-2168: edges over the chi2 threshold or behind the camera, collected
     // in the reference's vToErase order (mono edges, then right-camera edges, then stereo edges),
@@ -1370,8 +1493,13 @@ GbaOutcome<KeyFrameT, MapPointT> bundle_adjustment(const std::vector<KeyFrameT *
     r.point = point_out.data();
     r.edge_bad = bad.data();
     static_assert(sizeof(bool) == 1, "pbStopFlag is passed as one byte");
-    check(ctx, osg_bundle_adjustment(ctx, &g, &r, reinterpret_cast<const volatile uint8_t *>(pbStopFlag)),
-          "osg_bundle_adjustment");
+    if (call(ctx, "osg_bundle_adjustment", [&] {
+            return osg_bundle_adjustment(ctx, &g, &r, reinterpret_cast<const volatile uint8_t *>(pbStopFlag));
+        }) < 0) {  // an optimize() that stopped before its first iteration: the input state
+        pose_out = pose;
+        point_out = point;
+        r.iterations = 0;
+    }
     out.iterations = r.iterations;
     for (size_t i = 0; i < kfs.size(); i++)
         out.poses.push_back({kfs[i].second, std::vector<double>(&pose_out[7 * i], &pose_out[7 * i] + 7)});
@@ -1550,14 +1678,18 @@ MergeLbaOutcome<KeyFrameT, MapPointT> merge_local_bundle_adjustment(KeyFrameT *p
         r.point = x_out.data();
         r.edge_bad = bad.data();
         r.edge_chi2 = chi2.data();
-        check(ctx, osg_bundle_adjustment(ctx, &g, &r, reinterpret_cast<const volatile uint8_t *>(pbStopFlag)),
-              "osg_bundle_adjustment");
+        return call(ctx, "osg_bundle_adjustment", [&] {
+            return osg_bundle_adjustment(ctx, &g, &r, reinterpret_cast<const volatile uint8_t *>(pbStopFlag));
+        });
     };
     std::vector<size_t> all(ne);
     for (size_t e = 0; e < ne; e++) all[e] = e;
     std::vector<double> p1, x1, p2, x2, chi1, chi2;
     std::vector<uint8_t> bad1, bad2;
-    pass(all, std::vector<uint8_t>(ne, 1), 5, pose, point, p1, x1, bad1, chi1);  // :5448-5449
+    if (pass(all, std::vector<uint8_t>(ne, 1), 5, pose, point, p1, x1, bad1, chi1) < 0) {  // :5448-5449
+        out.aborted = true;  // nothing written back
+        return out;
+    }
     std::vector<uint8_t> skip(ne), bad(ne, 0);
     for (size_t e = 0; e < ne; e++) skip[e] = e_pair[e].second->isBad();
     const double *pf = p1.data(), *xf = x1.data();
@@ -1569,7 +1701,10 @@ MergeLbaOutcome<KeyFrameT, MapPointT> merge_local_bundle_adjustment(KeyFrameT *p
                 keep.push_back(e);
                 rob.push_back(skip[e]);
             }
-        pass(keep, rob, 10, p1, x1, p2, x2, bad2, chi2);
+        if (pass(keep, rob, 10, p1, x1, p2, x2, bad2, chi2) < 0) {
+            out.aborted = true;
+            return out;
+        }
         for (size_t i = 0; i < keep.size(); i++) bad[keep[i]] = bad2[i];
         for (size_t e = 0; e < ne; e++)
             if (!skip[e] && bad1[e]) {  // level 1: the first pass's chi2, the final depth

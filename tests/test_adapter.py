@@ -83,6 +83,35 @@ def test_adapter_compiles_against_mocks():
     assert r.returncode == 0, r.stderr[-3000:]
 
 
+FAULT_SRC = os.path.join(ROOT, "tests", "adapter", "adapter_fault.cpp")
+
+
+@pytest.fixture(scope="module")
+def fault_driver(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("adapter_fault") / "adapter_fault")
+    r = subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-I" + os.path.join(ROOT, "include"), FAULT_SRC,
+                        "-o", exe, "-L" + PKG, "-lorbslam3_amd", "-Wl,-rpath," + PKG, "-pthread"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return exe
+
+
+@pytest.mark.parametrize("mode", ["invalid", "nodevice", "real"])
+def test_adapter_error_contract(fault_driver, mode):
+    """no exception reaches ORB-SLAM3's threads.  With OSG_E_INVALID injected into every
+    ABI call, with the context creation failing (OSG_E_NODEVICE injected), and with the real failure
+    of a host without a gfx950 device, every adapter entry returns the reference's nothing-found
+    outcome (tests/adapter/adapter_fault.cpp lists them) and logs each code once per thread."""
+    r = subprocess.run([fault_driver, mode], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    if r.stdout.startswith("skip"):
+        return
+    assert f"PASS {mode}" in r.stdout, r.stdout[-3000:]
+    assert r.stdout.count("\nok ") + r.stdout.startswith("ok ") >= 24, r.stdout
+    logged = [l for l in r.stderr.splitlines() if l.startswith("osg_orbslam3:")]
+    assert len(logged) == (1 if mode == "invalid" else 2), r.stderr
+
+
 @pytest.fixture(scope="module")
 def driver(tmp_path_factory):
     exe = str(tmp_path_factory.mktemp("adapter") / "adapter_driver")
