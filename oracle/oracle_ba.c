@@ -27,6 +27,7 @@
  */
 #include <float.h>
 #include <math.h>
+#include <quadmath.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -265,8 +266,9 @@ static void cam_project(const osg_camera *c, const double *v, double *uv)
         const double theta7 = theta5 * theta2;
         const double theta9 = theta7 * theta2;
         const double r = theta + c->p[4] * theta3 + c->p[5] * theta5 + c->p[6] * theta7 + c->p[7] * theta9;
-        uv[0] = c->p[0] * r * cos(psi) + c->p[2];
-        uv[1] = c->p[1] * r * sin(psi) + c->p[3];
+        /* cos / sin correctly rounded (libm's last bit is host-dependent; csrc/exact_math.h sincos_psi) */
+        uv[0] = c->p[0] * r * (double)cosq((__float128)psi) + c->p[2];
+        uv[1] = c->p[1] * r * (double)sinq((__float128)psi) + c->p[3];
     } else {
         uv[0] = c->p[0] * v[0] / v[2] + c->p[2];
         uv[1] = c->p[1] * v[1] / v[2] + c->p[3];
@@ -279,7 +281,7 @@ static void cam_project_jac(const osg_camera *c, const double *v, double J[2][3]
         const double r2 = x2 + y2;
         const double r = sqrt(r2);
         const double r3 = r2 * r;
-        const double theta = atan2(r, v[2]);
+        const double theta = (double)atan2q((__float128)r, (__float128)v[2]); /* correctly rounded (atan2_rn) */
         const double theta2 = theta * theta, theta3 = theta2 * theta;
         const double theta4 = theta2 * theta2, theta5 = theta4 * theta;
         const double theta6 = theta2 * theta4, theta7 = theta6 * theta;

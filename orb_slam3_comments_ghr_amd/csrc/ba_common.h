@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include "exact_math.h"
+#include "glibc_math.h"
 #include "osg_internal.h"
 
 namespace osgba {
@@ -177,60 +178,14 @@ __host__ __device__ inline void se3_oplus(SE3 &T, const double *upd)
     T = se3_mul(E, T);
 }
 
-// sin / cos of psi = atan2f(...) in [-pi, pi] for the KannalaBrandt8 projection: Cody-Waite
-// reduction by pi/2 (two-term constant) and the classic odd / even minimax kernels (fdlibm's
-// published coefficients, error < 1 ulp).  The device library's sin / cos carry a Payne-Hanek
-// branch for huge arguments whose register footprint would set the whole pose kernel's; psi never
-// needs it.  Like the device libm, this is not bit-identical to glibc, which is why KB8 poses are
-// compared within the fisheye tolerance.
-__host__ __device__ inline double kb_sin_kernel(double x, double y)
-{
-    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
-                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
-                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
-    const double z = x * x, v = z * x;
-    const double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
-    return x - ((z * (0.5 * y - v * r) - y) - v * S1);
-}
-__host__ __device__ inline double kb_cos_kernel(double x, double y)
-{
-    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
-                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
-                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
-    const double z = x * x;
-    const double r = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
-    const double hz = 0.5 * z, w = 1.0 - hz;
-    return w + (((1.0 - w) - hz) + (z * r - x * y));
-}
-__host__ __device__ inline void kb_sincos(double x, double &sn, double &cs)
-{
-    if (!(fabs(x) <= 4.0)) {
-        sn = sin(x);
-        cs = cos(x);
-        return;
-    }
-    const double pio2_1 = 1.57079632673412561417e+00, pio2_1t = 6.07710050650619224932e-11;
-    const double n = rint(x * 6.36619772367581382433e-01);
-    const double r = x - n * pio2_1;  // exact: n * pio2_1 has 35 significant bits
-    const double w = n * pio2_1t;
-    const double y0 = r - w;
-    const double y1 = (r - y0) - w;
-    const double s0 = kb_sin_kernel(y0, y1), c0 = kb_cos_kernel(y0, y1);
-    switch (((int)n) & 3) {
-    case 0: sn = s0; cs = c0; break;
-    case 1: sn = c0; cs = -s0; break;
-    case 2: sn = -s0; cs = -c0; break;
-    default: sn = -c0; cs = s0; break;
-    }
-}
-
 // ------------------------------------------------------------------------------ cameras
 __device__ inline void cam_project(const osg_camera &c, const double *v, double *uv)
 {
     if (c.type == OSG_CAM_KB8) {
         const double x2_plus_y2 = v[0] * v[0] + v[1] * v[1];
-        const double theta = atan2f(sqrtf((float)x2_plus_y2), (float)v[2]);
-        const double psi = atan2f((float)v[1], (float)v[0]);
+        // the host libm's atan2f, restated bit for bit (glibc_math.h)
+        const double theta = osgm::atan2f_fd(sqrtf((float)x2_plus_y2), (float)v[2]);
+        const double psi = osgm::atan2f_fd((float)v[1], (float)v[0]);
         const double theta2 = theta * theta;
         const double theta3 = theta * theta2;
         const double theta5 = theta3 * theta2;
@@ -238,7 +193,7 @@ __device__ inline void cam_project(const osg_camera &c, const double *v, double 
         const double theta9 = theta7 * theta2;
         const double r = theta + c.p[4] * theta3 + c.p[5] * theta5 + c.p[6] * theta7 + c.p[7] * theta9;
         double sp, cp;
-        kb_sincos(psi, sp, cp);
+        osgx::sincos_psi(psi, sp, cp);  // correctly rounded, as the oracle (exact_math.h)
         uv[0] = c.p[0] * r * cp + c.p[2];
         uv[1] = c.p[1] * r * sp + c.p[3];
     } else {
@@ -253,7 +208,7 @@ __device__ inline void cam_project_jac(const osg_camera &c, const double *v, dou
         const double r2 = x2 + y2;
         const double r = sqrt(r2);
         const double r3 = r2 * r;
-        const double theta = atan2(r, v[2]);
+        const double theta = osgx::atan2_rn(r, v[2]);  // correctly rounded, as the oracle
         const double theta2 = theta * theta, theta3 = theta2 * theta;
         const double theta4 = theta2 * theta2, theta5 = theta4 * theta;
         const double theta6 = theta2 * theta4, theta7 = theta6 * theta;

@@ -53,3 +53,44 @@ def test_device_math_equals_oracle(tmp_path):
     import json
     r = json.loads(out)
     assert r["sin"] == 0 and r["cos"] == 0 and r["cube"] == 0, r
+
+
+@pytest.fixture(scope="module")
+def glibc_math_check(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("gmc") / "glibc_math_check")
+    subprocess.run(["g++", "-O2", "-fopenmp", "-ffp-contract=off", "-std=c++17",
+                    "-I" + os.path.join(ROOT, "orb_slam3_comments_ghr_amd", "csrc"),
+                    os.path.join(ROOT, "tools", "glibc_math_check.cc"), "-o", exe, "-lquadmath"], check=True)
+    return exe
+
+
+def _run_json(exe, *args):
+    import json
+    p = subprocess.run([exe, *map(str, args)], capture_output=True, text=True, timeout=600)
+    r = json.loads(p.stdout)
+    assert p.returncode == 0, r
+    return r
+
+
+def test_atan2f_restatement_equals_host_libm(glibc_math_check):
+    """The KB8 projection's float atan2f (ref:src/CameraModels/KannalaBrandt8.cpp:64-65): csrc/glibc_math.h
+    restates glibc's algorithm; bit-equal to the host atan2f on 4 x 10^7 pairs (uniform bit patterns,
+    KB8 theta / psi arguments, ratios across the reduction intervals) and every special pair.  The
+    committed full run (profiles/r03_glibc_math_atan2.jsonl) covers 10^9 pairs."""
+    r = _run_json(glibc_math_check, "atan2f", 10_000_000)
+    assert r["pairs"] == 40_000_000 and r["special_mismatch"] == 0
+    assert all(r[k] == 0 for k in r if k.startswith("mismatch_")), r
+
+
+def test_kb8_sincos_and_atan2_correctly_rounded(glibc_math_check):
+    """cos / sin(psi) and atan2(r, z) of the KB8 projection / Jacobian: exact_math.h's double-double
+    versions equal the __float128 value rounded once (the oracle's) -- here on a slice of float psi
+    around 0.5..0.75 rad, 1/4 pi..pi and 5e6 KB8-range (r, z); the committed exhaustive run over all
+    2.16e9 floats in [-pi, pi] is profiles/r03_glibc_math_sincos_psi_exhaustive.json.  glibc itself is
+    one ulp off on some of these arguments, which is why both sides leave it."""
+    r = _run_json(glibc_math_check, "sincos_psi", 0x3F000000, 0x3F0C0000)
+    assert r["floats"] > 1_000_000 and r["ours_sin_not_rn"] == 0 and r["ours_cos_not_rn"] == 0, r
+    r = _run_json(glibc_math_check, "sincos_psi", 0x40000000, 0x40000000 + 400_000)
+    assert r["ours_sin_not_rn"] == 0 and r["ours_cos_not_rn"] == 0, r
+    r = _run_json(glibc_math_check, "atan2", 5_000_000)
+    assert r["pairs"] == 5_000_000 and r["ours_not_rn"] == 0 and r["glibc_not_rn"] > 0, r
