@@ -218,3 +218,69 @@ def test_train_sharded_top2_gpu_two_ranks(oracle):
     want = [w.tolist() for w in _oracle_top2(oracle)(qd, td)]
     for rank, merged in res:
         assert merged == want
+
+
+# ------------------------------------------- config 5 on the HIP path: sequences sharded over ranks
+def _c5_gpu_sequence(ctx, frames):
+    """_c5_oracle_sequence through the C-ABI kernels: per frame, two-camera KB8
+    SearchByProjection(F, LastF) and SearchByProjection(F, local map) (k_match) and
+    PoseOptimization (k_pose_opt), with the same arguments as the oracle run."""
+    from orb_slam3_comments_ghr_amd import optimizer as op
+    from orb_slam3_comments_ghr_amd.matcher import ORBmatcher
+    out = []
+    for F, L, Q, S, P in frames:
+        s1 = S[0].copy()
+        n1 = ORBmatcher(ctx, 0.6, True).SearchByProjection(F, L, 7.0, False, slot_mp=s1, slot_taken=S[1])
+        s2 = S[0].copy()
+        n2 = ORBmatcher(ctx, 0.9, True).SearchByProjection(F, Q, 3.0, False, 20.0, slot_mp=s2, slot_taken=S[1])
+        r = op.Optimizer(ctx).PoseOptimization(P)
+        out.append((int(n1), s1.tolist(), int(n2), s2.tolist(), r.pose.tolist(), r.outlier.tolist(), int(r.n_inliers)))
+    return out
+
+
+N_SEQ_GPU = 5
+
+
+def _gpu_c5_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from orb_slam3_comments_ghr_amd import Context
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ctx = Context(0)
+    seqs = _c5_units(N_SEQ_GPU, frames_per_seq=3)
+    local = shard.run_sharded(lambda fr_: _c5_gpu_sequence(ctx, fr_), seqs, dist)
+    everything = shard.gather_results(local, dist)
+    ctx.close()
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((rank, sorted(local), everything))
+
+
+@pytest.mark.gpu
+def test_c5_sequences_sharded_gpu_two_ranks(oracle):
+    """BASELINE config 5 in its sharded form on the HIP path: C5 sequences (two-camera KB8,
+    SearchByProjection x2 + PoseOptimization per frame) round-robin over two processes sharing
+    cuda:0, each through the C-ABI kernels, gathered once at the end; every rank's gathered results
+    equal the single-process oracle run, sequence by sequence, bit for bit."""
+    world = 2
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    port = _free_port()
+    procs = [mpc.Process(target=_gpu_c5_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=110) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    seqs = _c5_units(N_SEQ_GPU, frames_per_seq=3)
+    want = {i: _c5_oracle_sequence(oracle, s) for i, s in enumerate(seqs)}
+    owned = set()
+    for rank, mine, everything in res:
+        assert mine == shard.shard_units(N_SEQ_GPU, rank, world)
+        owned |= set(mine)
+        assert sorted(everything) == list(range(N_SEQ_GPU))
+        for i in range(N_SEQ_GPU):
+            assert everything[i] == want[i], f"rank {rank}: sequence {i} != the single-process oracle run"
+    assert owned == set(range(N_SEQ_GPU))
