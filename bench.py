@@ -530,10 +530,14 @@ _ORACLE = []
 
 
 def _oracle():
-    """The CPU oracle (test infrastructure), loaded only by the cpu_baseline legs."""
+    """The CPU oracle (test infrastructure), loaded only by the cpu_baseline legs.  It times the
+    reference's own arithmetic: the host libm's sin / cos / pow / atan2 (oracle_set_libm), not the
+    correctly rounded evaluations the parity tests hold both sides to."""
     if not _ORACLE:
         from tests import oracle_calls
-        _ORACLE.append((oracle_calls.load(), oracle_calls))
+        lib = oracle_calls.load()
+        lib.oracle_set_libm(1)
+        _ORACLE.append((lib, oracle_calls))
     return _ORACLE[0]
 
 

@@ -92,6 +92,7 @@ int64_t oracle_orb_pyramid(const uint8_t *image, int32_t rows, int32_t cols, int
 double oracle_ref_pow3(double t);  /* the reference's libm calls, correctly rounded */
 double oracle_ref_sin(double x);
 double oracle_ref_cos(double x);
+void oracle_set_libm(int on);  /* 1: the host libm's sin / cos / pow / atan2 (cpu_baseline timing only) */
 int oracle_pose_optimization(const osg_pose_problem *P, osg_pose_result *R);
 int oracle_local_bundle_adjustment(const osg_ba_graph *G, osg_ba_result *R,
                                    const volatile uint8_t *stop_flag);

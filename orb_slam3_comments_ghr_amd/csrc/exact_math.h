@@ -249,6 +249,23 @@ OSG_HD inline double cos_ref(double x)
 // atan2q rounded on 2e8 KB8-range pairs.
 
 OSG_HD inline dd dd_neg(dd a) { return {-a.h, -a.l}; }
+// a + b without the second two_sum of dd_add ("sloppy" addition): ~2^-104 relative error unless
+// a and b nearly cancel, which none of the uses below does
+OSG_HD inline dd dd_add_s(dd a, dd b)
+{
+    OSGX_NOCONTRACT
+    dd s = two_sum(a.h, b.h);
+    s.l += a.l + b.l;
+    return quick_two_sum(s.h, s.l);
+}
+// a + b for a double b
+OSG_HD inline dd dd_add_d(dd a, double b)
+{
+    OSGX_NOCONTRACT
+    dd s = two_sum(a.h, b);
+    s.l += a.l;
+    return quick_two_sum(s.h, s.l);
+}
 OSG_HD inline dd dd_div(dd a, dd b)
 {
     OSGX_NOCONTRACT
@@ -261,71 +278,120 @@ OSG_HD inline dd dd_div(dd a, dd b)
     return dd_add(q, dd{q3, 0.0});
 }
 
-// sin(r), cos(r) of a double-double |r| <= pi/4 + 1e-9: the 15-term series of sin_rn_small /
-// cos_rn_small over r^2 in double-double (terms beyond series_terms(|r|) dropped, as there)
-OSG_HD inline void sincos_dd_kernel(dd r, dd &s, dd &c)
-{
-    OSGX_NOCONTRACT
-    const dd cs_[15] = {{1.0, 0.0},
-                        {-0.16666666666666666, -9.25185853854297e-18},
-                        {0.008333333333333333, 1.1564823173178714e-19},
-                        {-0.0001984126984126984, -1.7209558293420705e-22},
-                        {2.7557319223985893e-06, -1.858393274046472e-22},
-                        {-2.505210838544172e-08, 1.448814070935912e-24},
-                        {1.6059043836821613e-10, 1.2585294588752098e-26},
-                        {-7.647163731819816e-13, -7.03872877733453e-30},
-                        {2.8114572543455206e-15, 1.6508842730861433e-31},
-                        {-8.22063524662433e-18, -2.2141894119604265e-34},
-                        {1.9572941063391263e-20, -1.3643503830087908e-36},
-                        {-3.868170170630684e-23, 8.843177655482344e-40},
-                        {6.446950284384474e-26, -1.9330404233703465e-42},
-                        {-9.183689863795546e-29, -1.4303150396787322e-45},
-                        {1.1309962886447716e-31, 1.0498015412959506e-47}};
-    const dd cc_[15] = {{1.0, 0.0},
-                        {-0.5, 0.0},
-                        {0.041666666666666664, 2.3129646346357427e-18},
-                        {-0.001388888888888889, 5.300543954373577e-20},
-                        {2.48015873015873e-05, 2.1511947866775882e-23},
-                        {-2.755731922398589e-07, -2.3767714622250297e-23},
-                        {2.08767569878681e-09, -1.20734505911326e-25},
-                        {-1.1470745597729725e-11, -2.0655512752830745e-28},
-                        {4.779477332387385e-14, 4.399205485834081e-31},
-                        {-1.5619206968586225e-16, -1.1910679660273754e-32},
-                        {4.110317623312165e-19, 1.4412973378659527e-36},
-                        {-8.896791392450574e-22, 7.911402614872376e-38},
-                        {1.6117375710961184e-24, -3.6846573564509766e-41},
-                        {-2.4795962632247976e-27, 1.2953730964765229e-43},
-                        {3.279889237069838e-30, 1.5117542744029879e-46}};
-    const dd x2 = dd_mul(r, r);
-    const int K = series_terms(fabs(r.h));
-    dd a = cs_[14], b = cc_[14];
-#pragma unroll
-    for (int k = 13; k >= 0; k--) {
-        if (k == K - 1) {
-            a = cs_[k];
-            b = cc_[k];
-        } else if (k < K - 1) {
-            a = dd_add(dd_mul(a, x2), cs_[k]);
-            b = dd_add(dd_mul(b, x2), cc_[k]);
-        }
-    }
-    s = dd_mul(a, r);
-    c = b;
-}
+// sin / cos (k / 32), k = 0..25, as double-double pairs {sin.h, sin.l, cos.h, cos.l}
+#define OSGX_SINCOS32_TABLE \
+        {0.0, 0.0, 1.0, 0.0}, \
+        {0.03124491398532608, -1.562781562225433e-18, 0.9995117584851364, -3.418806487972947e-17}, \
+        {0.0624593178423802, -2.040259504585711e-18, 0.9980475107000991, 3.3232291674141346e-17}, \
+        {0.09361273123551289, 1.4628632005878733e-18, 0.9956086864580017, 3.312922430932991e-17}, \
+        {0.12467473338522769, -2.925947496057858e-18, 0.992197667229329, 4.754870575189364e-17}, \
+        {0.15561499277355603, 8.886053372342288e-18, 0.9878177838164719, 4.91917302237681e-17}, \
+        {0.18640329676226988, 2.3493796901281573e-18, 0.9824733131012553, -3.919920375420088e-17}, \
+        {0.21700958109501015, 1.1170071073364376e-17, 0.9761694738686353, -7.850690609285027e-18}, \
+        {0.24740395925452294, -7.53102495590706e-18, 0.9689124217106447, 5.071436662403936e-17}, \
+        {0.2775567516463363, 1.7674070262791822e-17, 0.9607092430155619, -2.807827063516729e-17}, \
+        {0.30743851458038085, 1.1004366442765296e-19, 0.9515679480481722, -3.8614834675674123e-17}, \
+        {0.33702006902225307, 1.0312279860787216e-17, 0.9414974631278811, -4.8523830236797095e-18}, \
+        {0.36627252908604757, -9.938814562106524e-18, 0.9305076219123143, 4.488760003328074e-18}, \
+        {0.39516733024093426, -1.9613487871414228e-17, 0.9186091557949183, -4.0564150104514996e-17}, \
+        {0.42367625720393803, -2.331800700068871e-17, 0.9058136834259364, 4.2864666490805214e-17}, \
+        {0.4517714714916838, -8.234073942098903e-18, 0.8921336993669944, 2.3160655211380166e-17}, \
+        {0.479425538604203, -5.103969860556013e-18, 0.8775825618903728, -4.2623149864279997e-17}, \
+        {0.5066114548142574, -3.269413423618168e-17, 0.8621744799348805, 4.4132427578105805e-18}, \
+        {0.5333026735360201, 5.129318115032044e-17, 0.8459244992310679, 1.549506647350329e-17}, \
+        {0.5594731312473669, 1.575565514488728e-17, 0.8288484876093257, 1.1163935406617444e-17}, \
+        {0.5850972729404622, -5.4883972461161805e-17, 0.8109631195052179, -3.091333486122179e-17}, \
+        {0.6101500770757914, -1.479826990758988e-17, 0.7922858596771786, -2.9049779312834576e-17}, \
+        {0.6346070800152693, -3.4568582392624965e-17, 0.7728349461524715, 4.231014921891023e-17}, \
+        {0.6584443999105676, -3.7736386700306717e-17, 0.7526293724180665, -1.2970993013150526e-17}, \
+        {0.6816387600233341, 4.410467313197903e-17, 0.7316888688738209, -1.0475824306512768e-17}, \
+        {0.7041675114545337, -3.94095700584825e-17, 0.7100338835660797, 1.505272211891291e-17}
+// atan(k / 64), k = 0..64, double-double
+#define OSGX_ATAN64_TABLE \
+        {0.0, 0.0}, \
+        {0.015623728620476831, -4.913600136566304e-19}, \
+        {0.031239833430268277, -1.188442711587748e-18}, \
+        {0.046840712915969654, -1.655677442254952e-19}, \
+        {0.06241880999595735, -1.5490756308295046e-18}, \
+        {0.0779666338315423, 5.804551873143357e-18}, \
+        {0.09347678115858947, -6.2844725995420954e-18}, \
+        {0.10894195698986579, 6.8267122072409585e-18}, \
+        {0.12435499454676144, -3.1253241424539383e-18}, \
+        {0.13970887428916365, -2.9579864247315813e-18}, \
+        {0.15499674192394097, 9.585415594114324e-18}, \
+        {0.1702119252854744, -3.541164079802125e-18}, \
+        {0.18534794999569476, 4.180692268843079e-18}, \
+        {0.2003985538258785, 3.1399542871844493e-18}, \
+        {0.21535769969773805, 4.738160130078733e-19}, \
+        {0.23021958727684372, 1.2313404529142703e-17}, \
+        {0.24497866312686414, 1.0698755618734451e-17}, \
+        {0.2596296294082575, 1.9238754924615304e-17}, \
+        {0.2741674511196588, 8.261353575163773e-18}, \
+        {0.2885873618940774, -1.428369957377257e-17}, \
+        {0.3028848683749714, -1.1010827903001369e-17}, \
+        {0.31705575320914703, -1.893928924292642e-17}, \
+        {0.3310960767041321, -7.952610375793799e-18}, \
+        {0.34500217720710513, -2.2938804755578304e-17}, \
+        {0.35877067027057225, -2.4623815582638635e-17}, \
+        {0.3723984466767542, 1.9612311504845653e-17}, \
+        {0.38588266939807375, 2.378822732491941e-17}, \
+        {0.39922076957525254, 2.246598105617042e-17}, \
+        {0.4124104415973873, -1.587652227770689e-17}, \
+        {0.42544963737004227, 2.3315530741892885e-17}, \
+        {0.43833655985795783, -2.494277030626541e-17}, \
+        {0.4510696559885235, -2.2703795229420475e-17}, \
+        {0.4636476090008061, 2.2698777452961687e-17}, \
+        {0.4760693303227612, 1.4654487332256713e-17}, \
+        {0.48833395105640554, -1.1373236189329585e-17}, \
+        {0.5004408131472942, -4.7181675085518756e-17}, \
+        {0.5123894603107377, -2.5462781472855804e-17}, \
+        {0.5241796287829132, 5.520094119641666e-18}, \
+        {0.5358112379604637, -4.0637956834825575e-18}, \
+        {0.5472843809874369, 4.923709671396255e-17}, \
+        {0.5585993153435624, -5.4556305485916264e-18}, \
+        {0.5697564534829784, 1.2255062085054184e-17}, \
+        {0.5807563535676704, -1.441464378193067e-17}, \
+        {0.5915997103351114, 4.920495453686772e-17}, \
+        {0.6022873461349642, 2.950430737228402e-17}, \
+        {0.6128202021652414, -3.1552061848586226e-17}, \
+        {0.6231993299340659, 2.672403885140095e-17}, \
+        {0.6334258829691446, -2.7290767436015276e-17}, \
+        {0.6435011087932844, 1.5834785051444286e-17}, \
+        {0.6534263411807619, 3.5800634857340095e-17}, \
+        {0.6632029927060933, -3.076054864429649e-17}, \
+        {0.6728325475937632, -1.899315009714705e-17}, \
+        {0.6823165548747481, 6.943223671560008e-18}, \
+        {0.6916566218531999, -8.117151192285796e-18}, \
+        {0.7008544078844502, -1.987626234335816e-17}, \
+        {0.7099116184635249, -4.597166450584887e-17}, \
+        {0.7188299996216245, -2.1478388444456983e-17}, \
+        {0.7276113326265107, 2.569325697391839e-18}, \
+        {0.7362574289814281, 3.473937648299457e-17}, \
+        {0.7447701257160751, 3.708315849135547e-17}, \
+        {0.7531512809621944, -2.4256934659182068e-17}, \
+        {0.7614027698055784, 9.850030332752822e-18}, \
+        {0.7695264804056583, -3.704991905602721e-17}, \
+        {0.7775243103733478, -2.6676490951944502e-17}, \
+        {0.7853981633974483, 3.061616997868383e-17}
 
-// sin(x), cos(x) correctly rounded for |x| <= 3.2 (psi of the KB8 projection).  x - n pi/2 with
-// n = rint(x 2/pi) in {-2..2}: x - n P1 is exact (n P1 is exact and within a factor of two of x),
-// P2 and P3 (pi/2 = P1 + P2 + P3 to 2^-160) are subtracted in double-double.
-// Out of line: the callers' other paths (pinhole edges) keep their register budget.
+// sin(x), cos(x) correctly rounded for |x| <= 3.2 (psi of the KB8 projection).
+//   * x - n pi/2 with n = rint(x 2/pi) in {-2..2}: x - n P1 is exact (n P1 is exact and within a
+//     factor of two of x), P2 and P3 (pi/2 = P1 + P2 + P3 to 2^-160) are subtracted in double-double;
+//   * r = a + t with a = k / 32 (table) and |t| <= 1/64 (t = r - a exact by Sterbenz for k != 0);
+//   * sin t = t + t^3 (-1/6 + t^2 q_s), cos t = 1 + t^2 (-1/2 + t^2 q_c): the leading coefficients
+//     in double-double, the short tails q_s, q_c (|t^2 q| < 2^-20) in double, so the whole value
+//     carries ~2^-100 relative error; sin r = S cos t + C sin t, cos r = C cos t - S sin t.
+// One final rounding.  Out of line: the callers' other paths (pinhole edges) keep their register
+// budget.
 OSG_HD inline __attribute__((noinline)) void sincos_psi(double x, double &sn, double &cs)
 {
     OSGX_NOCONTRACT
-    const double P1 = 0x1.921fb54442d18p+0, P2 = 0x1.1a62633145c07p-54, P3 = -0x1.f1976b7ed8fbcp-110;
     if (x == 0.0) {  // sin(-0) = -0
         sn = x;
         cs = 1.0;
         return;
     }
+    const double P1 = 0x1.921fb54442d18p+0, P2 = 0x1.1a62633145c07p-54, P3 = -0x1.f1976b7ed8fbcp-110;
     const double n = rint(x * 0x1.45f306dc9c883p-1);
     dd r{x, 0.0};
     if (n != 0.0) {
@@ -333,9 +399,21 @@ OSG_HD inline __attribute__((noinline)) void sincos_psi(double x, double &sn, do
         r.l -= n * P3;
         r = quick_two_sum(r.h, r.l);
     }
-    dd s, c;
-    sincos_dd_kernel(r, s, c);
-    const double s1 = s.h + s.l, c1 = c.h + c.l;
+    static const double tab[26][4] = {OSGX_SINCOS32_TABLE};
+    const double kf = rint(r.h * 32.0);
+    const int ak = (int)fabs(kf);
+    const dd t = two_sum(r.h - kf * 0.03125, r.l);
+    const dd t2 = dd_mul(t, t);
+    const double z = t2.h;
+    const double qs = z * (1.0 / 120.0 + z * (-1.0 / 5040.0 + z * (1.0 / 362880.0)));
+    const double qc = z * (1.0 / 24.0 + z * (-1.0 / 720.0 + z * (1.0 / 40320.0)));
+    const dd sin_t = dd_add_s(t, dd_mul(dd_mul(t, t2), dd_add_d(dd{-0.16666666666666666, -9.25185853854297e-18}, qs)));
+    const dd cos_t = dd_add_d(dd_mul(t2, dd_add_d(dd{-0.5, 0.0}, qc)), 1.0);
+    const double sg = kf < 0.0 ? -1.0 : 1.0;
+    const dd S{sg * tab[ak][0], sg * tab[ak][1]}, C{tab[ak][2], tab[ak][3]};
+    const dd sr = dd_add_s(dd_mul(S, cos_t), dd_mul(C, sin_t));
+    const dd cr = dd_add_s(dd_mul(C, cos_t), dd_neg(dd_mul(S, sin_t)));
+    const double s1 = sr.h + sr.l, c1 = cr.h + cr.l;
     switch (((int)n) & 3) {
     case 0: sn = s1; cs = c1; break;
     case 1: sn = c1; cs = -s1; break;
@@ -345,57 +423,31 @@ OSG_HD inline __attribute__((noinline)) void sincos_psi(double x, double &sn, do
 }
 
 // atan2(y, x) correctly rounded (finite, nonzero x and y; the rest is the library's, whose results
-// there are exact constants): t = min / max of |x|, |y| in double-double, atan(t) = atan(k / 16) +
-// atan(u) with u = (t - k / 16) / (1 + t k / 16), |u| <= 1/32, a 12-term series; then the octant.
+// there are exact constants): t = min / max of |x|, |y| in double-double, atan(t) = atan(k / 64) +
+// atan(u) with u = (t - k / 64) / (1 + t k / 64), |u| <= 1/128, atan u = u + u^3 (-1/3 + u^2 q)
+// (the tail q in double, |u^2 q| < 2^-14); then the octant.  ~2^-100 relative error, one rounding.
 OSG_HD inline __attribute__((noinline)) double atan2_rn(double y, double x)
 {
     OSGX_NOCONTRACT
     const double ay = fabs(y), ax = fabs(x);
     if (!(ay > 0.0 && ay < INFINITY && ax > 0.0 && ax < INFINITY)) return atan2(y, x);
-    const dd tab[17] = {{0.0, 0.0},
-                        {0.06241880999595735, -1.5490756308295046e-18},
-                        {0.12435499454676144, -3.1253241424539383e-18},
-                        {0.18534794999569476, 4.180692268843079e-18},
-                        {0.24497866312686414, 1.0698755618734451e-17},
-                        {0.3028848683749714, -1.1010827903001369e-17},
-                        {0.35877067027057225, -2.4623815582638635e-17},
-                        {0.4124104415973873, -1.587652227770689e-17},
-                        {0.4636476090008061, 2.2698777452961687e-17},
-                        {0.5123894603107377, -2.5462781472855804e-17},
-                        {0.5585993153435624, -5.4556305485916264e-18},
-                        {0.6022873461349642, 2.950430737228402e-17},
-                        {0.6435011087932844, 1.5834785051444286e-17},
-                        {0.6823165548747481, 6.943223671560008e-18},
-                        {0.7188299996216245, -2.1478388444456983e-17},
-                        {0.7531512809621944, -2.4256934659182068e-17},
-                        {0.7853981633974483, 3.061616997868383e-17}};
-    const dd ser[12] = {{1.0, 0.0},
-                        {-0.3333333333333333, -1.850371707708594e-17},
-                        {0.2, -1.1102230246251566e-17},
-                        {-0.14285714285714285, -7.93016446160826e-18},
-                        {0.1111111111111111, 6.1679056923619804e-18},
-                        {-0.09090909090909091, 2.523234146875356e-18},
-                        {0.07692307692307693, -4.270088556250602e-18},
-                        {-0.06666666666666667, -9.251858538542971e-19},
-                        {0.058823529411764705, 8.163404592832033e-19},
-                        {-0.05263157894736842, -2.921639538487254e-18},
-                        {0.047619047619047616, 2.64338815386942e-18},
-                        {-0.043478260869565216, -1.206764157201257e-18}};
+    static const double tab[65][2] = {OSGX_ATAN64_TABLE};
     const bool swap = ay > ax;
     const double num = swap ? ax : ay, den = swap ? ay : ax;
     const double q1 = num / den;
     const double q2 = fma(-q1, den, num) / den;  // the remainder num - q1 den is exact
     const dd t = quick_two_sum(q1, q2);
-    const double k = rint(t.h * 16.0);
-    const double ck = k * 0.0625;
-    const dd u = dd_div(dd_add(t, dd{-ck, 0.0}), dd_add(dd{1.0, 0.0}, dd_mul(t, dd{ck, 0.0})));
+    const double k = rint(t.h * 64.0);
+    const double ck = k * 0.015625;
+    const dd u = dd_div(dd_add_d(t, -ck), dd_add_d(dd_mul(t, dd{ck, 0.0}), 1.0));
     const dd u2 = dd_mul(u, u);
-    dd a = ser[11];
-#pragma unroll
-    for (int j = 10; j >= 0; j--) a = dd_add(dd_mul(a, u2), ser[j]);
-    dd at = dd_add(tab[(int)k], dd_mul(a, u));
-    if (swap) at = dd_add(dd{1.5707963267948966, 6.123233995736766e-17}, dd_neg(at));
-    if (x < 0.0) at = dd_add(dd{3.141592653589793, 1.2246467991473532e-16}, dd_neg(at));
+    const double z = u2.h;
+    const double q = z * (0.2 + z * (-1.0 / 7.0 + z * (1.0 / 9.0 + z * (-1.0 / 11.0))));
+    const dd au = dd_add_s(u, dd_mul(dd_mul(u, u2), dd_add_d(dd{-0.3333333333333333, -1.850371707708594e-17}, q)));
+    const int ik = (int)k;
+    dd at = dd_add_s(dd{tab[ik][0], tab[ik][1]}, au);
+    if (swap) at = dd_add_s(dd{1.5707963267948966, 6.123233995736766e-17}, dd_neg(at));
+    if (x < 0.0) at = dd_add_s(dd{3.141592653589793, 1.2246467991473532e-16}, dd_neg(at));
     const double res = at.h + at.l;
     return y < 0.0 ? -res : res;
 }

@@ -50,6 +50,8 @@ def declare(lib: C.CDLL) -> C.CDLL:
                                               C.c_int, vp]
     lib.oracle_search_by_bow_kf_kf.argtypes = [C.POINTER(OsgBowSide), C.POINTER(OsgBowSide), f32,
                                                C.c_int, vp]
+    lib.oracle_set_libm.argtypes = [C.c_int]
+    lib.oracle_set_libm.restype = None
     for f in ("oracle_ref_pow3", "oracle_ref_sin", "oracle_ref_cos"):
         getattr(lib, f).argtypes = [C.c_double]
         getattr(lib, f).restype = C.c_double
