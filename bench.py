@@ -73,7 +73,11 @@ def parse():
     ap.add_argument("--frames", type=int, default=1024, help="frames per launch (C3 / C5 batches)")
     ap.add_argument("--frame-reps", type=int, default=5)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
-                    help="per-launch HBM traffic from the rocprofv3 PMC passes (tools/gpu_profile.sh)")
+                    help="per-launch HBM traffic from the rocprofv3 PMC passes (tools/gpu_profile_r03.sh)")
+    ap.add_argument("--valu-pmc", default=os.path.join(ROOT, "profiles", "r03_top2_valu_pmc.json"),
+                    help="the headline kernel's VALU counters (tools/pmc_valu.py)")
+    ap.add_argument("--schur-pmc", default=os.path.join(ROOT, "profiles", "r03_schur_pmc.json"),
+                    help="the LBA engine's SQ / MFMA / HBM counters (tools/pmc_kernel_summary.py)")
     return ap.parse_args()
 
 
@@ -188,6 +192,8 @@ def main():
     kname = (f"k_top2_batch<{ql},{int(os.environ.get('OSG_TOP2_BATCH_SCALAR', '1'))}> "
              f"grid={(nq + 64 * ql - 1) // (64 * ql)} x {B} x 1024")
     tr = pmc_traffic(args.traffic, "k_top2_batch")
+    vp = _load_json(args.valu_pmc)
+    vk = next((v for k, v in vp.items() if "k_top2_batch" in k), None)
     roofline = {
         "kernel": kname,
         "bound": "valu",
@@ -203,6 +209,15 @@ def main():
         "algorithmic_ops_per_launch": pairs_per_step * VALU_OPS_PER_PAIR,
         "algorithmic_bytes_per_launch": alg_bytes,
         "hbm_frac_if_priced_as_hbm": round(alg_bytes / (k_us * 1e-6) / 1e9 / PEAK_HBM_GBS, 5),
+        # the guide's 32 lanes / clk (MI355X_MICROARCH.md: a wave64 VALU instruction over 2 cycles)
+        "frac_guide_peak": round(achieved_tops / (2 * PEAK_VALU_TOPS), 4),
+        "peak_guide": round(2 * PEAK_VALU_TOPS, 1),
+        # counters on the kernel itself (one --pmc pass): SIMD-cycles per wave64 VALU instruction and
+        # the issue utilisation at 4 cycles (16 lanes / clk) and at 2 (32 lanes / clk)
+        "valu_issue_util_pmc": None if vk is None else round(vk["valu_issue_util_16"], 4),
+        "valu_issue_util_pmc_at_32_lanes": None if vk is None else round(vk["valu_issue_util_32"], 4),
+        "cycles_per_valu_inst_pmc": None if vk is None else round(vk["cycles_per_valu_inst"], 3),
+        "valu_pmc_source": None if vk is None else os.path.relpath(args.valu_pmc, ROOT),
     }
     plan = ctx.hamming_top2_plan(nq, nt)
     tr1 = pmc_traffic(args.traffic, plan.split(" ")[0].split("<")[0])
@@ -438,7 +453,7 @@ def bench_lba(ctx, rank, world, dist, dev, args):
     sr_s = kt["schur_rows"][0] / 1e3 / steps
     kernels = {k: round(v[0] / max(1, v[1]), 4) for k, v in kt.items() if v[1]}
     dom = max(kernels, key=kernels.get)
-    pmc = _load_json(os.path.join(ROOT, "profiles", "r02_schur_pmc.json"))
+    pmc = _load_json(args.schur_pmc)
     pmc_sr = next((v for k, v in pmc.items() if k.startswith("k_schur_rows<false>")), {})
     flop_iter = 72.6e6
     res = {
@@ -460,7 +475,7 @@ def bench_lba(ctx, rank, world, dist, dev, args):
                      "hbm_GBps_if_priced_as_hbm": round(sr_bytes / sr_s / 1e9, 1),
                      "mfma_busy_frac_pmc": pmc_sr.get("mfma_busy_frac"),
                      "traffic": pmc_sr.get("hbm_bytes_per_launch"),
-                     "pmc_source": "profiles/r02_schur_pmc.json" if pmc else None},
+                     "pmc_source": os.path.relpath(args.schur_pmc, ROOT) if pmc else None},
         "kernel_ms_per_step": kernels,
         "whole_call_fp64_frac": round(bval * flop_iter / 1e12 / 78.6, 5),
         "single_window": single,

@@ -1,0 +1,33 @@
+#!/bin/bash
+# Round-3 profiles (one gpurun call): kernel trace + stats of the default bench, separate FETCH_SIZE /
+# WRITE_SIZE passes (-> pmc_traffic.json), the headline kernel's VALU pass (SQ_INSTS_VALU,
+# SQ_ACTIVE_INST_VALU, GRBM_GUI_ACTIVE -> r03_top2_valu_pmc.json), the LBA engine's SQ / MFMA / HBM
+# passes (-> r03_schur_pmc.json), then the bench line with those files.  Counters are never combined
+# with traces; every GPU step has its own time limit and the chain stops at the first failure.
+set -o pipefail
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+OUT=$R/gpurun_out/${1:-r03prof}
+mkdir -p $OUT
+SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES"
+VALU="SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT"
+HEAD="--no-cpu --no-ba --no-gba --no-frames --no-stream --steps 20 --warmup 5"
+cd /tmp &&
+echo trace > $OUT/progress &&
+timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- python3 $R/bench.py > $OUT/bench_under_trace.json 2> $OUT/trace.err &&
+echo valu > $OUT/progress &&
+timeout -s KILL 120 rocprofv3 --pmc $VALU --output-format csv -d $OUT/valu -o valu -- python3 $R/bench.py $HEAD > $OUT/valu.log 2>&1 &&
+python3 $R/tools/pmc_valu.py $(find $OUT/valu -name '*counter_collection.csv' | head -1) k_top2_batch $OUT/r03_top2_valu_pmc.json > $OUT/valu_summary.txt &&
+echo fetch > $OUT/progress &&
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o fetch -- python3 $R/bench.py --no-cpu --no-ba --no-gba --steps 20 --warmup 5 > $OUT/fetch.log 2>&1 &&
+echo write > $OUT/progress &&
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o write -- python3 $R/bench.py --no-cpu --no-ba --no-gba --steps 20 --warmup 5 > $OUT/write.log 2>&1 &&
+python3 $R/tools/pmc_traffic.py $(find $OUT/fetch -name '*counter_collection.csv' | head -1) $(find $OUT/write -name '*counter_collection.csv' | head -1) $OUT/pmc_traffic.json &&
+echo lba > $OUT/progress &&
+TS=1 BS=64 timeout -s KILL 120 rocprofv3 --pmc $SQ --output-format csv -d $OUT/lba_sq -o sq -- python3 $R/tools/lba_batch_bench.py > $OUT/lba_sq.log 2>&1 &&
+TS=1 BS=64 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/lba_fetch -o f -- python3 $R/tools/lba_batch_bench.py > $OUT/lba_fetch.log 2>&1 &&
+TS=1 BS=64 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/lba_write -o w -- python3 $R/tools/lba_batch_bench.py > $OUT/lba_write.log 2>&1 &&
+python3 $R/tools/pmc_kernel_summary.py $OUT/r03_schur_pmc.json $(find $OUT/lba_sq -name '*counter_collection.csv' | head -1) $(find $OUT/lba_fetch -name '*counter_collection.csv' | head -1) $(find $OUT/lba_write -name '*counter_collection.csv' | head -1) &&
+echo bench > $OUT/progress &&
+timeout -k 10 400 python3 $R/bench.py --traffic $OUT/pmc_traffic.json --valu-pmc $OUT/r03_top2_valu_pmc.json --schur-pmc $OUT/r03_schur_pmc.json > $OUT/bench.json 2> $OUT/bench.err
+echo "exit=$?"
