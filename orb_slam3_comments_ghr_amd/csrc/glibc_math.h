@@ -42,52 +42,42 @@ OSG_GM_HD inline float i2f(int32_t i)
     return x;
 }
 
-// fdlibm float atanf (s_atanf.c)
+// fdlibm float atanf (s_atanf.c).  The interval branches are evaluated branch-free: every lane forms
+// the numerator / denominator of its interval's reduction with the same float operations and
+// divides once (x / 1 = x exactly on the |x| < 0.4375 path), so a wave whose lanes fall into
+// different intervals runs one division, not one per interval.
 OSG_GM_HD inline float atanf_fd(float x)
 {
     OSG_GM_NOCONTRACT
-    const float atanhi[4] = {4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f};
-    const float atanlo[4] = {5.0121582440e-09f, 3.7748947079e-08f, 3.4473217170e-08f, 7.5497894159e-08f};
     const float aT0 = 3.3333334327e-01f, aT1 = -2.0000000298e-01f, aT2 = 1.4285714924e-01f,
                 aT3 = -1.1111110449e-01f, aT4 = 9.0908870101e-02f, aT5 = -7.6918758452e-02f,
                 aT6 = 6.6610731184e-02f, aT7 = -5.8335702866e-02f, aT8 = 4.9768779427e-02f,
                 aT9 = -3.6531571299e-02f, aT10 = 1.6285819933e-02f;
     const int32_t hx = f2i(x);
     const int32_t ix = hx & 0x7fffffff;
-    int id;
     if (ix >= 0x4c000000) {  // |x| >= 2^25
         if (ix > 0x7f800000) return x + x;  // NaN
-        return hx > 0 ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];
+        return hx > 0 ? 1.5707962513e+00f + 7.5497894159e-08f : -1.5707962513e+00f - 7.5497894159e-08f;
     }
-    if (ix < 0x3ee00000) {                  // |x| < 0.4375
-        if (ix < 0x31000000) return x;      // |x| < 2^-29
-        id = -1;
-    } else {
-        x = fabsf(x);
-        if (ix < 0x3f980000) {              // |x| < 1.1875
-            if (ix < 0x3f300000) {          // 7/16 <= |x| < 11/16
-                id = 0;
-                x = (2.0f * x - 1.0f) / (2.0f + x);
-            } else {                        // 11/16 <= |x| < 19/16
-                id = 1;
-                x = (x - 1.0f) / (x + 1.0f);
-            }
-        } else {
-            if (ix < 0x401c0000) {          // |x| < 2.4375
-                id = 2;
-                x = (x - 1.5f) / (1.0f + 1.5f * x);
-            } else {                        // 2.4375 <= |x| < 2^25
-                id = 3;
-                x = -1.0f / x;
-            }
-        }
-    }
+    if (ix < 0x31000000) return x;  // |x| < 2^-29
+    // id: -1 |x| < 0.4375; 0 7/16 <= |x| < 11/16; 1 11/16 <= |x| < 19/16; 2 |x| < 2.4375; 3 otherwise
+    const int id = ix < 0x3ee00000 ? -1 : ix < 0x3f300000 ? 0 : ix < 0x3f980000 ? 1 : ix < 0x401c0000 ? 2 : 3;
+    const float ax = fabsf(x);
+    float num, den;
+    if (id < 0) { num = x; den = 1.0f; }
+    else if (id == 0) { num = 2.0f * ax - 1.0f; den = 2.0f + ax; }
+    else if (id == 1) { num = ax - 1.0f; den = ax + 1.0f; }
+    else if (id == 2) { num = ax - 1.5f; den = 1.0f + 1.5f * ax; }
+    else { num = -1.0f; den = ax; }
+    x = num / den;
     const float z = x * x;
     const float w = z * z;
     const float s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
     const float s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
     if (id < 0) return x - x * (s1 + s2);
-    const float r = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+    const float hi = id == 0 ? 4.6364760399e-01f : id == 1 ? 7.8539812565e-01f : id == 2 ? 9.8279368877e-01f : 1.5707962513e+00f;
+    const float lo = id == 0 ? 5.0121582440e-09f : id == 1 ? 3.7748947079e-08f : id == 2 ? 3.4473217170e-08f : 7.5497894159e-08f;
+    const float r = hi - ((x * (s1 + s2) - lo) - x);
     return hx < 0 ? -r : r;
 }
 
