@@ -96,6 +96,9 @@ struct MatchArgs {
     GLOBAL int32_t *status;          // [0] candidates, [1] nmatches, [2] rounds, [3] overflow, [4] serial
     int cap;
     int lds_free;                    // dynamic LDS bytes past the resolve arrays (the staged grid region)
+    int prefilled;                   // SearchByBoW: k_bow_fill wrote q_off (host CSR), cands and the first q_res;
+                                     // k_bow_claims / k_bow_round ran the first Jacobi round (status[13]: changed)
+    GLOBAL int32_t *claim_g;         // SearchByBoW: n_slots claims of the first round (global scratch)
 };
 
 struct Win {
@@ -497,14 +500,27 @@ __device__ __forceinline__ QRes eval_bow_group(const MatchArgs &A, int q, int la
 {
     const int e0 = A.q_off[q], e1 = A.q_off[q + 1];
     uint32_t l1 = KEY_NONE, l2 = KEY_NONE, r1 = KEY_NONE, r2 = KEY_NONE;
-    for (int e = e0 + lane; e < e1; e += BOW_G) {
-        const uint32_t c = A.cands[e];
-        const int s = (int)(c & 0xFFFFu);
-        const uint32_t d = (c >> 16) & 0x1FFu;
-        if (d > 256 || blocked(s)) continue;
-        const uint32_t key = (d << 16) | (uint32_t)(e - e0);
-        if (MODE == MODE_BOW_KF_KF || A.nleft < 0 || s < A.nleft) push2(l1, l2, key);
-        else push2(r1, r2, key);
+    // BK candidates per lane at a time, all loads issued before the first use: one memory latency
+    // per BK x BOW_G candidates instead of one per candidate
+    constexpr int BK = 8;
+    for (int base = e0 + lane; base < e1; base += BK * BOW_G) {
+        uint32_t cv[BK];
+#pragma unroll
+        for (int k = 0; k < BK; k++) {
+            const int e = base + k * BOW_G;
+            cv[k] = e < e1 ? A.cands[e] : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int k = 0; k < BK; k++) {
+            const int e = base + k * BOW_G;
+            const uint32_t c = cv[k];
+            const int s = (int)(c & 0xFFFFu);
+            const uint32_t d = (c >> 16) & 0x1FFu;
+            if (e >= e1 || d > 256 || blocked(s)) continue;
+            const uint32_t key = (d << 16) | (uint32_t)(e - e0);
+            if (MODE == MODE_BOW_KF_KF || A.nleft < 0 || s < A.nleft) push2(l1, l2, key);
+            else push2(r1, r2, key);
+        }
     }
 #pragma unroll
     for (int o = BOW_G / 2; o > 0; o >>= 1) {
@@ -524,6 +540,69 @@ __device__ __forceinline__ QRes eval_bow_group(const MatchArgs &A, int q, int la
             res.l = (int)(A.cands[e0 + (l1 & 0xFFFFu)] & 0xFFFFu);
     }
     return res;
+}
+
+// SearchByBoW's distances and first evaluation spread over the chip: one BOW_G-lane group per
+// query, BFG queries per workgroup, grid (ceil(max nq / BFG), problems).  The candidate CSR (q_off)
+// comes from the host's merge-walk, so no count / scan pass is needed; each group writes its
+// query's {slot | dist << 16} list and its unclaimed top-2 result, which k_match's resolve starts
+// from (no slot is taken before a SearchByBoW call: every first evaluation sees blocked(s) = false).
+constexpr int BFG = 16;
+template <int MODE>
+__global__ __launch_bounds__(BFG *BOW_G) void k_bow_fill(const MatchArgs *__restrict__ args)
+{
+    const MatchArgs &A = args[blockIdx.y];
+    for (int sl = blockIdx.x * blockDim.x + threadIdx.x; sl < A.n_slots; sl += gridDim.x * blockDim.x)
+        A.claim_g[sl] = INT_BIG;
+    const int lane = threadIdx.x & (BOW_G - 1);
+    const int q = blockIdx.x * BFG + threadIdx.x / BOW_G;
+    if (q >= A.nq) return;
+    uint32_t qd[8];
+    load_desc(A, q, qd);
+    const int cb = A.q_cb[q], ce = A.q_ce[q];
+    GLOBAL uint32_t *out = A.cands + A.q_off[q] - cb;
+    for (int j = cb + lane; j < ce; j += BOW_G) {
+        const int idx = A.cand_list[j];
+        uint32_t d = dist256(qd, A.fdesc + (size_t)idx * 8);
+        if (MODE == MODE_BOW_KF_KF && !A.slot_ok[idx]) d = 0x1FF;
+        out[j] = (uint32_t)idx | (d << 16);
+    }
+    // each lane reads back the entries it wrote (the same strides), so no barrier is needed
+    const QRes r = eval_bow_group<MODE>(A, q, lane, [](int) { return false; });
+    if (lane == 0) {
+        A.q_res[2 * q] = r.l;
+        A.q_res[2 * q + 1] = r.r;
+    }
+}
+
+// The first Jacobi round of SearchByBoW's resolve (see k_match) over the chip: every query's
+// assigned slots claimed (device-scope atomicMin, order-independent), then every query re-evaluated
+// with blocked(s) = claimed by an earlier query.  k_match continues from these results and skips
+// its rounds when nothing changed.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_bow_claims(const MatchArgs *__restrict__ args)
+{
+    const MatchArgs &A = args[blockIdx.y];
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    if (q >= A.nq) return;
+    const QRes r = QRes{A.q_res[2 * q], A.q_res[2 * q + 1]};
+    if (r.l >= 0) atomicMin((int32_t *)&A.claim_g[r.l], q);
+    if (r.r >= 0) atomicMin((int32_t *)&A.claim_g[r.r], q);
+}
+template <int MODE>
+__global__ __launch_bounds__(BFG *BOW_G) void k_bow_round(const MatchArgs *__restrict__ args)
+{
+    const MatchArgs &A = args[blockIdx.y];
+    const int lane = threadIdx.x & (BOW_G - 1);
+    const int q = blockIdx.x * BFG + threadIdx.x / BOW_G;
+    if (q >= A.nq) return;
+    const QRes r1 = QRes{A.q_res[2 * q], A.q_res[2 * q + 1]};
+    const QRes r2 = eval_bow_group<MODE>(A, q, lane, [&](int s) { return A.claim_g[s] < q; });
+    if (lane == 0 && (r2.l != r1.l || r2.r != r1.r)) {
+        A.q_res[2 * q] = r2.l;
+        A.q_res[2 * q + 1] = r2.r;
+        atomicOr((int32_t *)&A.status[13], 1);
+    }
 }
 
 // Every slot q writes: the direct matches and, for a5 on a two-camera rig, each one's stereo
@@ -724,6 +803,9 @@ __global__ __launch_bounds__(MT) void k_match(const MatchArgs *__restrict__ args
     }
 
     tclk[2] = __builtin_amdgcn_s_memtime();
+    const bool pre = BOW && A.prefilled;
+    int total = pre ? A.q_off[nq] : 0;
+    if (!pre) {
     // ---- 1. count
     int my = 0;
     for (int q = q0; q < q1; q++) {
@@ -743,7 +825,7 @@ __global__ __launch_bounds__(MT) void k_match(const MatchArgs *__restrict__ args
         s_scan[tid] += v;
         __syncthreads();
     }
-    const int total = s_scan[MT - 1];
+    total = s_scan[MT - 1];
     if (total > A.cap) {
         if (tid == 0) {
             A.status[0] = total;
@@ -773,6 +855,10 @@ __global__ __launch_bounds__(MT) void k_match(const MatchArgs *__restrict__ args
             for (int q = grp; q < nq; q += NGRP) fill_bow_group<MODE>(A, q, lane);
         }
     }
+    }  // !pre
+    else {
+        tclk[3] = tclk[4] = tclk[2];
+    }
     __syncthreads();
     tclk[5] = __builtin_amdgcn_s_memtime();
     // ---- 4. resolve: init slot state
@@ -789,10 +875,11 @@ __global__ __launch_bounds__(MT) void k_match(const MatchArgs *__restrict__ args
     if (tid < OSG_HISTO_LENGTH) s_hist[tid] = 0;
     __syncthreads();
     if (BOW) {
-        for (int q = grp; q < nq; q += NGRP) {
-            const QRes r = eval_bow_group<MODE>(A, q, lane, [&](int s) { return taken0[s] != 0; });
-            if (lane == 0) store_res(A, q, r);
-        }
+        if (!pre)
+            for (int q = grp; q < nq; q += NGRP) {
+                const QRes r = eval_bow_group<MODE>(A, q, lane, [&](int s) { return taken0[s] != 0; });
+                if (lane == 0) store_res(A, q, r);
+            }
     } else {
         for (int q = q0; q < q1; q++)
             store_res(A, q, eval_query<MODE>(A, q, [&](int s) { return taken0[s] != 0; }));
@@ -801,8 +888,10 @@ __global__ __launch_bounds__(MT) void k_match(const MatchArgs *__restrict__ args
     // Jacobi rounds.  A slot is blocked for q when it was blocked initially or a query p < q
     // whose MapPoint has observations wrote it (SearchByBoW / a7: any earlier write).
     tclk[6] = __builtin_amdgcn_s_memtime();
-    int rounds = 0;
+    int rounds = pre ? 1 : 0;
     int *cur = claimB, *other = claimA;
+    // (the first round ran over the chip; its results are final when it changed nothing)
+    if (!(pre && A.status[13] == 0))
     for (;;) {
         rounds++;
         for (int q = q0; q < q1; q++) {
@@ -1076,7 +1165,7 @@ struct Problem {
     MatchArgs A = {};
     int32_t *host_slot = nullptr;  // slot array (in/out), n_slot entries
     int n_slot = 0;
-    std::vector<int32_t> q_feat, q_cb, q_ce, q_mp;
+    std::vector<int32_t> q_feat, q_cb, q_ce, q_mp, q_off;  // q_off: SearchByBoW's candidate CSR
     std::vector<uint8_t> qdesc, slot_ok;
     std::vector<float> q_angle;
     int32_t *out_mp12 = nullptr;   // KF-KF: result indexed by KF1 keypoint
@@ -1138,22 +1227,25 @@ int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_
         if (P[b].n_slot > 0)
             std::memcpy(pin_io + status_bytes + sizeof(int32_t) * slot_off[b], P[b].host_slot,
                         sizeof(int32_t) * P[b].n_slot);
-    char *dev_in = nullptr, *dev_io = nullptr;
-    MatchArgs *dev_args = nullptr;
-    OSG_ALLOC(ctx, dev_in, SLOT_TMP0, pk.total + 256);
-    OSG_ALLOC(ctx, dev_io, SLOT_TMP1, io_bytes);
-    OSG_ALLOC(ctx, dev_args, SLOT_TMP7, args_bytes);
-    if (pk.total) OSG_HIP_CHECK(ctx, hipMemcpyAsync(dev_in, pin, pk.total, hipMemcpyHostToDevice, ctx->stream));
+    // one device block with the pinned block's layout [inputs | io | args]: the first attempt uploads
+    // it with one copy, and one copy brings status, slots and KF-KF results back (a single call's
+    // host cost is mostly HIP API calls and synchronisations, not bytes)
+    char *dev_in = nullptr;
+    OSG_ALLOC(ctx, dev_in, SLOT_TMP0, in_bytes + io_pad + args_bytes + 256);
+    char *dev_io = dev_in + in_bytes;
+    MatchArgs *dev_args = (MatchArgs *)(dev_io + io_pad);
     for (int b = 0; b < B; b++) {
         MatchArgs &A = P[b].A;
         OSG_RELOCATE_ALL(A, dev_in);
+        if (A.prefilled) relocate(A.q_off, dev_in);
         A.status = (GLOBAL int32_t *)dev_io + STATUS_INTS * b;
         A.slot_mp = (GLOBAL int32_t *)(dev_io + status_bytes) + slot_off[b];
         A.out_q = (GLOBAL int32_t *)(dev_io + io_in_bytes) + q_base[b];
     }
     for (int b = 0; b < B; b++) P[b].A.lds_free = (int)(lds - match_lds_bytes(P[b].A.n_slots));
     std::vector<size_t> cap(B), cand_off(B + 1);
-    for (int b = 0; b < B; b++) cap[b] = std::max<size_t>((size_t)P[b].A.nq * 32, 1024);
+    for (int b = 0; b < B; b++)
+        cap[b] = P[b].A.prefilled ? (size_t)std::max(P[b].q_off.back(), 1) : std::max<size_t>((size_t)P[b].A.nq * 32, 1024);
     std::vector<int32_t> st((size_t)STATUS_INTS * B);
     for (int attempt = 0; attempt < 2; attempt++) {
         cand_off[0] = 0;
@@ -1168,24 +1260,43 @@ int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_
         float4 *q_win = nullptr;
         if (!BOW) OSG_ALLOC(ctx, q_win, SLOT_TMP8, sizeof(float4) * 4 * nq_total);
         OSG_ALLOC(ctx, cands, SLOT_TMP5, sizeof(uint32_t) * cand_off[B]);
+        int32_t *claim_g = nullptr;
+        if (BOW) OSG_ALLOC(ctx, claim_g, SLOT_TMP9, sizeof(int32_t) * (n_slot_total + 1));
         for (int b = 0; b < B; b++) {
             MatchArgs &A = P[b].A;
-            A.q_off = (GLOBAL int32_t *)(q_off + q_base[b]);
+            if (!A.prefilled) A.q_off = (GLOBAL int32_t *)(q_off + q_base[b]);
             A.q_mid = (GLOBAL int32_t *)(q_mid + q_base[b]);
             A.q_win = q_win ? (GLOBAL f32x4 *)(q_win + 4 * q_base[b]) : nullptr;
             A.q_res = (GLOBAL int32_t *)(q_res + 2 * q_base[b]);
             A.q_bin = (GLOBAL uint8_t *)(q_bin + 2 * q_base[b]);
             A.cands = (GLOBAL uint32_t *)(cands + cand_off[b]);
+            A.claim_g = claim_g ? (GLOBAL int32_t *)(claim_g + slot_off[b]) : nullptr;
             A.cap = (int)std::min<size_t>(cap[b], INT_BIG);
             pin_args[b] = A;
         }
-        // (re)upload the status block and the input slot state: a retry must not see the slot
-        // arrays written by the problems that fitted the first time
-        OSG_HIP_CHECK(ctx, hipMemcpyAsync(dev_io, pin_io, io_in_bytes, hipMemcpyHostToDevice, ctx->stream));
-        OSG_HIP_CHECK(ctx, hipMemcpyAsync(dev_args, pin_args, args_bytes, hipMemcpyHostToDevice, ctx->stream));
+        // the inputs, the status block, the input slot state and the arguments in one copy; a retry
+        // re-uploads [io | args] (it must not see the slot arrays written by the problems that fitted
+        // the first time)
+        if (attempt == 0)
+            OSG_HIP_CHECK(ctx, hipMemcpyAsync(dev_in, pin, in_bytes + io_pad + args_bytes, hipMemcpyHostToDevice,
+                                              ctx->stream));
+        else
+            OSG_HIP_CHECK(ctx, hipMemcpyAsync(dev_io, pin_io, io_pad + args_bytes, hipMemcpyHostToDevice, ctx->stream));
         hipEvent_t *ev = osg_ctx_events(ctx);
         if (!ev) return osg_set_error(ctx, OSG_E_HIP, "event create failed");
         OSG_HIP_CHECK(ctx, hipEventRecord(ev[0], ctx->stream));
+        if (BOW) {
+            int max_nq = 0;
+            for (int b = 0; b < B; b++) max_nq = std::max(max_nq, P[b].A.prefilled ? P[b].A.nq : 0);
+            if (max_nq > 0) {
+                hipLaunchKernelGGL((k_bow_fill<MODE>), dim3((max_nq + BFG - 1) / BFG, B), dim3(BFG * BOW_G), 0, ctx->stream,
+                                   dev_args);
+                hipLaunchKernelGGL((k_bow_claims<MODE>), dim3((max_nq + 255) / 256, B), dim3(256), 0, ctx->stream,
+                                   dev_args);
+                hipLaunchKernelGGL((k_bow_round<MODE>), dim3((max_nq + BFG - 1) / BFG, B), dim3(BFG * BOW_G), 0, ctx->stream,
+                                   dev_args);
+            }
+        }
         if (stage == 2)
             hipLaunchKernelGGL((k_match<MODE, 2>), dim3(B), dim3(MT), lds, ctx->stream, dev_args);
         else if (stage == 1)
@@ -1194,8 +1305,11 @@ int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_
             hipLaunchKernelGGL((k_match<MODE, 0>), dim3(B), dim3(MT), lds, ctx->stream, dev_args);
         OSG_HIP_CHECK(ctx, hipGetLastError());
         OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
-        OSG_HIP_CHECK(ctx, hipMemcpyAsync(st.data(), dev_io, status_bytes, hipMemcpyDeviceToHost, ctx->stream));
+        // status, slot arrays and KF-KF results in one copy (the pinned io block is re-filled from the
+        // callers' slots before a retry)
+        OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_io, dev_io, io_bytes, hipMemcpyDeviceToHost, ctx->stream));
         OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+        std::memcpy(st.data(), pin_io, status_bytes);
         bool overflow = false;
         for (int b = 0; b < B; b++)
             if (st[(size_t)STATUS_INTS * b + 3]) {
@@ -1204,12 +1318,11 @@ int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_
             }
         if (!overflow) break;
         if (attempt == 1) return osg_set_error(ctx, OSG_E_HIP, "candidate buffer overflow after resize");
-    }
-    const size_t back = sizeof(int32_t) * (n_slot_total + (MODE == MODE_BOW_KF_KF ? nq_total : 0));
-    if (back) {
-        OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_io + status_bytes, dev_io + status_bytes, back, hipMemcpyDeviceToHost,
-                                          ctx->stream));
-        OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+        std::memset(pin_io, 0, status_bytes);
+        for (int b = 0; b < B; b++)
+            if (P[b].n_slot > 0)
+                std::memcpy(pin_io + status_bytes + sizeof(int32_t) * slot_off[b], P[b].host_slot,
+                            sizeof(int32_t) * P[b].n_slot);
     }
     int64_t cand_sum = 0, nm_sum = 0;
     int rounds_max = 0, serial_n = 0;
@@ -1527,6 +1640,10 @@ int prep_bow_kf_f(osg_ctx *ctx, Problem &P, osg_packer &pk, const osg_bow_side *
     set_off(A.q_cb, pk.add(P.q_cb.data(), sizeof(int32_t) * n));
     set_off(A.q_ce, pk.add(P.q_ce.data(), sizeof(int32_t) * n));
     set_off(A.cand_list, pk.add(f->fv.feat, sizeof(int32_t) * f->fv.node_start[f->fv.n_nodes]));
+    P.q_off.assign(n + 1, 0);
+    for (int i = 0; i < n; i++) P.q_off[i + 1] = P.q_off[i] + (P.q_ce[i] - P.q_cb[i]);
+    set_off(A.q_off, pk.add(P.q_off.data(), sizeof(int32_t) * (n + 1)));
+    A.prefilled = 1;
     return OSG_OK;
 }
 
@@ -1570,6 +1687,10 @@ int prep_bow_kf_kf(osg_ctx *ctx, Problem &P, osg_packer &pk, const osg_bow_side 
     set_off(A.q_cb, pk.add(P.q_cb.data(), sizeof(int32_t) * n));
     set_off(A.q_ce, pk.add(P.q_ce.data(), sizeof(int32_t) * n));
     set_off(A.cand_list, pk.add(kf2->fv.feat, sizeof(int32_t) * kf2->fv.node_start[kf2->fv.n_nodes]));
+    P.q_off.assign(n + 1, 0);
+    for (int i = 0; i < n; i++) P.q_off[i + 1] = P.q_off[i] + (P.q_ce[i] - P.q_cb[i]);
+    set_off(A.q_off, pk.add(P.q_off.data(), sizeof(int32_t) * (n + 1)));
+    A.prefilled = 1;
     return OSG_OK;
 }
 
