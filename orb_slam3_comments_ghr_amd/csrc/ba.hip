@@ -88,6 +88,7 @@ struct LbaDev {
     const int32_t *point_h;       // per point: landmark index or -1
     const int32_t *hl_point;      // per landmark: point index
     const int32_t *lm_e_start, *lm_e;    // edges per landmark
+    const int32_t *lm_perm;              // landmarks ordered by edge count (k_linearize's thread order)
     const int32_t *lm_b_start;           // blocks per landmark (blocks are numbered landmark-major)
     const int32_t *blk_pose;             // per block: hessian pose index
     const int32_t *edge_blk;             // per edge: block or -1
@@ -220,9 +221,12 @@ __global__ __launch_bounds__(EB) void k_linearize(const LbaDev *__restrict__ Ds)
     LBA_GRAPH(M_LIN);
     if (bx >= max(D.gl, 1)) return;
     __shared__ double s[EB / 64];
-    const int l = bx * EB + threadIdx.x;
+    // thread -> landmark through lm_perm (landmarks by edge count): the lanes of a wave walk edge lists
+    // of equal length.  Every landmark's sums are its own, so the order changes no result.
+    const int tl = bx * EB + threadIdx.x;
     double md = 0.0;
-    if (l < D.nhl) {
+    if (tl < D.nhl) {
+        const int l = D.lm_perm[tl];
         const double *X = cur_point(D) + 3 * (size_t)D.hl_point[l];
         const double *poses = cur_pose(D);
         double H6[6] = {0, 0, 0, 0, 0, 0}, bl3[3] = {0, 0, 0};
@@ -1249,7 +1253,7 @@ struct LbaHost {
     int np = 0, npt = 0, ne = 0, nhp = 0, nhl = 0, nblk = 0, npairs = 0, nchunks = 0;
     int ge = 0, gl = 0, gu = 0, nblk_red = 0;
     bool trivial = false;  // nothing to optimise: the estimates are returned unchanged
-    std::vector<int32_t> pose_h, hp_pose, point_h, hl_point, lm_e_start, lm_e, lm_b_start, blk_pose, edge_blk, blk_lm,
+    std::vector<int32_t> pose_h, hp_pose, point_h, hl_point, lm_e_start, lm_e, lm_perm, lm_b_start, blk_pose, edge_blk, blk_lm,
         blk_e_start, blk_e, hp_e_start, hp_e, hp_b_start, hp_b, pair_start, pair_ab, chunk_start, pair_chunk,
         pair_rank, rs_pose, rs_rank0, rs_chunk_start, rs_chunk, hp_rs_start;
     int n_rs = 0;
@@ -1343,6 +1347,14 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
     {
         std::vector<int32_t> fill(H.lm_e_start.begin(), H.lm_e_start.end() - 1);
         for (int e = 0; e < ne; e++) H.lm_e[fill[point_h[G->e_point[e]]]++] = e;
+        // landmarks by edge count (counting sort, stable)
+        int kmax = 0;
+        for (int l = 0; l < nhl; l++) kmax = std::max(kmax, H.lm_e_start[l + 1] - H.lm_e_start[l]);
+        std::vector<int32_t> kc(kmax + 2, 0);
+        for (int l = 0; l < nhl; l++) kc[H.lm_e_start[l + 1] - H.lm_e_start[l] + 1]++;
+        for (int k = 0; k <= kmax; k++) kc[k + 1] += kc[k];
+        H.lm_perm.assign(std::max(nhl, 1), 0);
+        for (int l = 0; l < nhl; l++) H.lm_perm[kc[H.lm_e_start[l + 1] - H.lm_e_start[l]]++] = l;
     }
     // blocks per landmark: unique free poses sorted by hessian index
     H.lm_b_start.assign(nhl + 1, 0);
@@ -1620,7 +1632,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     // ---- device layout: one packed input block, one state block, the LbaDev / control arrays
     osg_packer pk;
     struct InOff {
-        size_t fixed, epose, epoint, ecam, ekind, eobs, eisig, cams, poseh, hppose, pointh, hlpoint, lmes, lme, lmbs,
+        size_t fixed, epose, epoint, ecam, ekind, eobs, eisig, cams, poseh, hppose, pointh, hlpoint, lmes, lme, lmperm, lmbs,
             blkpose, eblk, hpes, hpe, hpbs, hpb, pairs, pairab, chs, blklm, blkes, blke, pch, pose0, point0, erob,
             prank, rspose, rsrank0, rscs, rsc, hprs;
     };
@@ -1645,6 +1657,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         o.hlpoint = pk.add(h.hl_point.data(), 4 * (size_t)nhl);
         o.lmes = pk.add(h.lm_e_start.data(), 4 * (size_t)(nhl + 1));
         o.lme = pk.add(h.lm_e.data(), 4 * (size_t)ne);
+        o.lmperm = pk.add(h.lm_perm.data(), 4 * (size_t)std::max(nhl, 1));
         o.lmbs = pk.add(h.lm_b_start.data(), 4 * (size_t)(nhl + 1));
         o.blkpose = pk.add(h.blk_pose.data(), 4 * (size_t)nblk);
         o.eblk = pk.add(h.edge_blk.data(), 4 * (size_t)ne);
@@ -1734,6 +1747,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         D.hl_point = osg_dptr<int32_t>(din, o.hlpoint);
         D.lm_e_start = osg_dptr<int32_t>(din, o.lmes);
         D.lm_e = osg_dptr<int32_t>(din, o.lme);
+        D.lm_perm = osg_dptr<int32_t>(din, o.lmperm);
         D.lm_b_start = osg_dptr<int32_t>(din, o.lmbs);
         D.blk_pose = osg_dptr<int32_t>(din, o.blkpose);
         D.edge_blk = osg_dptr<int32_t>(din, o.eblk);
