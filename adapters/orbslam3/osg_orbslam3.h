@@ -30,6 +30,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <list>
 #include <map>
 #include <memory>
@@ -46,6 +47,12 @@
 #include "osg_ba.h"
 
 namespace osg_orbslam3 {
+
+// The gather structs below hold ABI views that point into their own vectors: never copied or moved
+// (batches keep them in a std::deque, which constructs in place).
+#define OSG_PINNED_STRUCT(T) \
+    T(const T &) = delete;  \
+    T &operator=(const T &) = delete
 
 // ------------------------------------------------------------------------------------ errors
 // Nothing in this adapter throws: ORB-SLAM3's Tracking, LocalMapping and LoopClosing
@@ -200,6 +207,7 @@ inline auto nleft_of(const T &F, long) -> decltype(F.NLeft, int())
 // (+ mGridRight, mvLeftToRightMatch, mvRightToLeftMatch for a two-camera rig).
 template <class FrameT>
 struct FrameView {
+    OSG_PINNED_STRUCT(FrameView);
     std::vector<float> kx, ky, ka, ur, scale;
     std::vector<int32_t> ko, gs, gi, gsr, gir, l2r, r2l;
     std::vector<uint8_t> desc;
@@ -293,120 +301,157 @@ inline int descriptor_distance(const MatT &a, const MatT &b)
 }
 
 // ---------------------------------------------- a5 SearchByProjection(Frame&, vector<MapPoint*>)
-// ref:src/ORBmatcher.cc:44-242
+// ref:src/ORBmatcher.cc:44-242.  MpsGather: one problem (the Frame, the local MapPoints' isInFrustum
+// results, the slot state), shared by the single and the batched entry points.
+template <class FrameT, class MapPointT>
+struct MpsGather {
+    OSG_PINNED_STRUCT(MpsGather);
+    FrameView<FrameT> fv;
+    std::vector<int32_t> id, lvl, lvl_r;
+    std::vector<uint8_t> desc, usable, has_obs, in_view, in_view_r;
+    std::vector<float> px, py, pxr, pyr, vc, vcr, depth;
+    osg_mp_queries q{};
+    Slots<MapPointT> slots;
+    MpsGather(FrameT &F, const std::vector<MapPointT *> &vpMapPoints)
+        : fv(F), slots(F.mvpMapPoints, (int)vpMapPoints.size(), true)
+    {
+        const int nq = (int)vpMapPoints.size();
+        id.resize(nq);
+        lvl.resize(nq);
+        lvl_r.resize(nq);
+        desc.resize((size_t)nq * 32);
+        usable.resize(nq);
+        has_obs.resize(nq);
+        in_view.resize(nq);
+        in_view_r.resize(nq);
+        for (auto *v : {&px, &py, &pxr, &pyr, &vc, &vcr, &depth}) v->resize(nq);
+        for (int i = 0; i < nq; i++) {
+            MapPointT *p = vpMapPoints[i];
+            id[i] = i;
+            in_view[i] = p->mbTrackInView;
+            in_view_r[i] = p->mbTrackInViewR;
+            if (!in_view[i] && !in_view_r[i]) continue;  // the reference skips before any other read
+            usable[i] = !p->isBad();
+            has_obs[i] = p->Observations() > 0;
+            const auto d = p->GetDescriptor();
+            std::memcpy(&desc[(size_t)32 * i], d.template ptr<unsigned char>(0), 32);
+            px[i] = p->mTrackProjX;
+            py[i] = p->mTrackProjY;
+            pxr[i] = p->mTrackProjXR;
+            pyr[i] = p->mTrackProjYR;
+            vc[i] = p->mTrackViewCos;
+            vcr[i] = p->mTrackViewCosR;
+            lvl[i] = p->mnTrackScaleLevel;
+            lvl_r[i] = p->mnTrackScaleLevelR;
+            depth[i] = p->mTrackDepth;
+        }
+        q.n = nq;
+        q.mp_id = id.data();
+        q.desc = desc.data();
+        q.usable = usable.data();
+        q.has_obs = has_obs.data();
+        q.in_view = in_view.data();
+        q.proj_x = px.data();
+        q.proj_y = py.data();
+        q.proj_xr = pxr.data();
+        q.view_cos = vc.data();
+        q.pred_level = lvl.data();
+        q.track_depth = depth.data();
+        q.in_view_r = in_view_r.data();
+        q.proj_yr = pyr.data();
+        q.view_cos_r = vcr.data();
+        q.pred_level_r = lvl_r.data();
+    }
+};
+
 template <class H, class FrameT, class MapPointT>
 int search_by_projection_mps(FrameT &F, const std::vector<MapPointT *> &vpMapPoints, float th, bool bFarPoints,
                              float thFarPoints, float nnratio)
 {
     osg_ctx *ctx = thread_ctx();
-    FrameView<FrameT> fv(F);
-    const int nq = (int)vpMapPoints.size();
-    std::vector<int32_t> id(nq), lvl(nq), lvl_r(nq);
-    std::vector<uint8_t> desc((size_t)nq * 32), usable(nq), has_obs(nq), in_view(nq), in_view_r(nq);
-    std::vector<float> px(nq), py(nq), pxr(nq), pyr(nq), vc(nq), vcr(nq), depth(nq);
-    for (int i = 0; i < nq; i++) {
-        MapPointT *p = vpMapPoints[i];
-        id[i] = i;
-        in_view[i] = p->mbTrackInView;
-        in_view_r[i] = p->mbTrackInViewR;
-        if (!in_view[i] && !in_view_r[i]) continue;  // the reference skips before any other read
-        usable[i] = !p->isBad();
-        has_obs[i] = p->Observations() > 0;
-        const auto d = p->GetDescriptor();
-        std::memcpy(&desc[(size_t)32 * i], d.template ptr<unsigned char>(0), 32);
-        px[i] = p->mTrackProjX;
-        py[i] = p->mTrackProjY;
-        pxr[i] = p->mTrackProjXR;
-        pyr[i] = p->mTrackProjYR;
-        vc[i] = p->mTrackViewCos;
-        vcr[i] = p->mTrackViewCosR;
-        lvl[i] = p->mnTrackScaleLevel;
-        lvl_r[i] = p->mnTrackScaleLevelR;
-        depth[i] = p->mTrackDepth;
-    }
-    osg_mp_queries q{};
-    q.n = nq;
-    q.mp_id = id.data();
-    q.desc = desc.data();
-    q.usable = usable.data();
-    q.has_obs = has_obs.data();
-    q.in_view = in_view.data();
-    q.proj_x = px.data();
-    q.proj_y = py.data();
-    q.proj_xr = pxr.data();
-    q.view_cos = vc.data();
-    q.pred_level = lvl.data();
-    q.track_depth = depth.data();
-    q.in_view_r = in_view_r.data();
-    q.proj_yr = pyr.data();
-    q.view_cos_r = vcr.data();
-    q.pred_level_r = lvl_r.data();
-    Slots<MapPointT> slots(F.mvpMapPoints, nq, true);
+    MpsGather<FrameT, MapPointT> g(F, vpMapPoints);
     const int nm = call(ctx, "osg_search_by_projection_mps", [&] {
-        return osg_search_by_projection_mps(ctx, &fv.v, &q, nnratio, th, bFarPoints, thFarPoints, slots.mp.data(),
-                                            slots.taken.data());
+        return osg_search_by_projection_mps(ctx, &g.fv.v, &g.q, nnratio, th, bFarPoints, thFarPoints, g.slots.mp.data(),
+                                            g.slots.taken.data());
     });
     if (nm < 0) return 0;
-    slots.apply(F.mvpMapPoints, vpMapPoints, nq);
+    g.slots.apply(F.mvpMapPoints, vpMapPoints, (int)vpMapPoints.size());
     return nm;
 }
 
 // ------------------------------------------------- a6 SearchByProjection(Frame&, const Frame&)
-// ref:src/ORBmatcher.cc:1957-2191
+// ref:src/ORBmatcher.cc:1957-2191.  LastGather: one (CurrentFrame, LastFrame) problem.
+template <class H, class FrameT>
+struct LastGather {
+    OSG_PINNED_STRUCT(LastGather);
+    using MapPointT = typename std::remove_pointer<typename std::decay<decltype(std::declval<FrameT &>().mvpMapPoints[0])>::type>::type;
+    FrameView<FrameT> fv;
+    std::vector<int32_t> id, oct;
+    std::vector<uint8_t> desc, valid, has_obs;
+    std::vector<float> u, v, invz, ang, ur, vr;
+    std::vector<MapPointT *> queries;
+    osg_last_queries q{};
+    Slots<MapPointT> slots;
+    LastGather(FrameT &CF, const FrameT &LF) : fv(CF), slots(CF.mvpMapPoints, LF.N, true)
+    {
+        const int n = LF.N;
+        id.assign(n, -1);
+        oct.assign(n, 0);
+        desc.resize((size_t)n * 32);
+        valid.assign(n, 0);
+        has_obs.assign(n, 0);
+        for (auto *w : {&u, &v, &invz, &ang}) w->resize(n);
+        queries.assign(n, nullptr);
+        const bool two = CF.Nleft != -1;
+        if (two) {
+            ur.assign(n, 0.f);
+            vr.assign(n, 0.f);
+        }
+        for (int i = 0; i < n; i++) {
+            MapPointT *p = LF.mvpMapPoints[i];
+            const auto &kp = (LF.Nleft == -1) ? LF.mvKeysUn[i]
+                                              : (i < LF.Nleft ? LF.mvKeys[i] : LF.mvKeysRight[i - LF.Nleft]);
+            oct[i] = (LF.Nleft == -1 || i < LF.Nleft) ? LF.mvKeys[i].octave : LF.mvKeysRight[i - LF.Nleft].octave;
+            ang[i] = kp.angle;
+            if (!p || LF.mvbOutlier[i]) continue;
+            if (!H::project_last(CF, p, u[i], v[i], invz[i])) continue;
+            if (two) H::project_last_right(CF, p, ur[i], vr[i]);  // ref:src/ORBmatcher.cc:2096-2097
+            valid[i] = 1;
+            id[i] = i;
+            queries[i] = p;
+            has_obs[i] = p->Observations() > 0;
+            const auto d = p->GetDescriptor();
+            std::memcpy(&desc[(size_t)32 * i], d.template ptr<unsigned char>(0), 32);
+        }
+        q.n = n;
+        q.mp_id = id.data();
+        q.desc = desc.data();
+        q.valid = valid.data();
+        q.has_obs = has_obs.data();
+        q.u = u.data();
+        q.v = v.data();
+        q.invz = invz.data();
+        q.octave = oct.data();
+        q.angle = ang.data();
+        if (two) {
+            q.u_r = ur.data();
+            q.v_r = vr.data();
+        }
+        q.tlc_z = H::tlc_z(CF, LF);
+    }
+};
+
 template <class H, class FrameT>
 int search_by_projection_last(FrameT &CF, const FrameT &LF, float th, bool bMono, bool checkOri)
 {
-    using MapPointT = typename std::remove_pointer<typename std::decay<decltype(LF.mvpMapPoints[0])>::type>::type;
     osg_ctx *ctx = thread_ctx();
-    FrameView<FrameT> fv(CF);
-    const int n = LF.N;
-    std::vector<int32_t> id(n, -1), oct(n, 0);
-    std::vector<uint8_t> desc((size_t)n * 32), valid(n, 0), has_obs(n, 0);
-    std::vector<float> u(n), v(n), invz(n), ang(n), ur, vr;
-    std::vector<MapPointT *> queries(n, nullptr);
-    const bool two = CF.Nleft != -1;
-    if (two) {
-        ur.assign(n, 0.f);
-        vr.assign(n, 0.f);
-    }
-    for (int i = 0; i < n; i++) {
-        MapPointT *p = LF.mvpMapPoints[i];
-        const auto &kp = (LF.Nleft == -1) ? LF.mvKeysUn[i]
-                                          : (i < LF.Nleft ? LF.mvKeys[i] : LF.mvKeysRight[i - LF.Nleft]);
-        oct[i] = (LF.Nleft == -1 || i < LF.Nleft) ? LF.mvKeys[i].octave : LF.mvKeysRight[i - LF.Nleft].octave;
-        ang[i] = kp.angle;
-        if (!p || LF.mvbOutlier[i]) continue;
-        if (!H::project_last(CF, p, u[i], v[i], invz[i])) continue;
-        if (two) H::project_last_right(CF, p, ur[i], vr[i]);  // ref:src/ORBmatcher.cc:2096-2097
-        valid[i] = 1;
-        id[i] = i;
-        queries[i] = p;
-        has_obs[i] = p->Observations() > 0;
-        const auto d = p->GetDescriptor();
-        std::memcpy(&desc[(size_t)32 * i], d.template ptr<unsigned char>(0), 32);
-    }
-    osg_last_queries q{};
-    q.n = n;
-    q.mp_id = id.data();
-    q.desc = desc.data();
-    q.valid = valid.data();
-    q.has_obs = has_obs.data();
-    q.u = u.data();
-    q.v = v.data();
-    q.invz = invz.data();
-    q.octave = oct.data();
-    q.angle = ang.data();
-    if (two) {
-        q.u_r = ur.data();
-        q.v_r = vr.data();
-    }
-    q.tlc_z = H::tlc_z(CF, LF);
-    Slots<MapPointT> slots(CF.mvpMapPoints, n, true);
+    LastGather<H, FrameT> g(CF, LF);
     const int nm = call(ctx, "osg_search_by_projection_last", [&] {
-        return osg_search_by_projection_last(ctx, &fv.v, &q, th, bMono, checkOri, slots.mp.data(), slots.taken.data());
+        return osg_search_by_projection_last(ctx, &g.fv.v, &g.q, th, bMono, checkOri, g.slots.mp.data(),
+                                             g.slots.taken.data());
     });
     if (nm < 0) return 0;
-    slots.apply(CF.mvpMapPoints, queries, n);
+    g.slots.apply(CF.mvpMapPoints, g.queries, LF.N);
     return nm;
 }
 
@@ -594,39 +639,60 @@ struct FeatVecCSR {
 };
 
 // ref:src/ORBmatcher.cc:262-496.  vpMapPointMatches = vector<MapPoint*>(F.N, NULL) with the KF's
-// MapPoints matched to Frame keypoints.
+// MapPoints matched to Frame keypoints.  BowKfF gathers one (KeyFrame, Frame) problem; the single
+// and the batched entry points share it.
+template <class KeyFrameT, class FrameT, class MapPointT>
+struct BowKfF {
+    OSG_PINNED_STRUCT(BowKfF);
+    std::vector<MapPointT *> vpMPsKF;
+    std::vector<uint8_t> dk, df, good;
+    std::vector<float> ak, af;
+    std::vector<int32_t> idk;
+    FeatVecCSR<decltype(std::declval<KeyFrameT &>().mFeatVec)> fk;
+    FeatVecCSR<decltype(std::declval<FrameT &>().mFeatVec)> ff;
+    osg_bow_side sk{}, sf{};
+    BowKfF(KeyFrameT *pKF, const FrameT &F) : vpMPsKF(pKF->GetMapPointMatches()), fk(pKF->mFeatVec), ff(F.mFeatVec)
+    {
+        const int nk = (int)vpMPsKF.size(), nf = F.N;
+        good.resize(nk);
+        ak.resize(nk);
+        af.resize(nf);
+        idk.assign(nk, -1);
+        copy_desc_rows(pKF->mDescriptors, nk, dk);
+        copy_desc_rows(F.mDescriptors, nf, df);
+        for (int i = 0; i < nk; i++) {
+            // ref:src/ORBmatcher.cc:399-401
+            ak[i] = (!pKF->mpCamera2) ? pKF->mvKeysUn[i].angle
+                                      : (i >= pKF->NLeft ? pKF->mvKeysRight[i - pKF->NLeft].angle : pKF->mvKeys[i].angle);
+            good[i] = vpMPsKF[i] && !vpMPsKF[i]->isBad();
+            if (vpMPsKF[i]) idk[i] = i;
+        }
+        for (int i = 0; i < nf; i++)
+            af[i] = (F.Nleft == -1) ? F.mvKeysUn[i].angle : (i < F.Nleft ? F.mvKeys[i].angle : F.mvKeysRight[i - F.Nleft].angle);
+        sk = osg_bow_side{nk, pKF->NLeft, dk.data(), ak.data(), idk.data(), good.data(), fk.view()};
+        sf = osg_bow_side{nf, F.Nleft, df.data(), af.data(), nullptr, nullptr, ff.view()};
+    }
+    // ref:src/ORBmatcher.cc:268 (the vector is re-initialised whatever happens) + the matches
+    void apply(const int32_t *out, int nf, std::vector<MapPointT *> &vpMapPointMatches, bool ok) const
+    {
+        vpMapPointMatches.assign(nf, nullptr);
+        if (!ok) return;
+        for (int i = 0; i < nf; i++)
+            if (out[i] >= 0) vpMapPointMatches[i] = vpMPsKF[out[i]];
+    }
+};
+
 template <class H, class KeyFrameT, class FrameT, class MapPointT>
 int search_by_bow_kf_f(KeyFrameT *pKF, FrameT &F, std::vector<MapPointT *> &vpMapPointMatches, float nnratio,
                        bool checkOri)
 {
     osg_ctx *ctx = thread_ctx();
-    const std::vector<MapPointT *> vpMPsKF = pKF->GetMapPointMatches();
-    const int nk = (int)vpMPsKF.size(), nf = F.N;
-    std::vector<uint8_t> dk, df, good(nk);
-    std::vector<float> ak(nk), af(nf);
-    std::vector<int32_t> idk(nk, -1);
-    copy_desc_rows(pKF->mDescriptors, nk, dk);
-    copy_desc_rows(F.mDescriptors, nf, df);
-    for (int i = 0; i < nk; i++) {
-        // ref:src/ORBmatcher.cc:399-401
-        ak[i] = (!pKF->mpCamera2) ? pKF->mvKeysUn[i].angle
-                                  : (i >= pKF->NLeft ? pKF->mvKeysRight[i - pKF->NLeft].angle : pKF->mvKeys[i].angle);
-        good[i] = vpMPsKF[i] && !vpMPsKF[i]->isBad();
-        if (vpMPsKF[i]) idk[i] = i;
-    }
-    for (int i = 0; i < nf; i++) af[i] = (F.Nleft == -1) ? F.mvKeysUn[i].angle : (i < F.Nleft ? F.mvKeys[i].angle : F.mvKeysRight[i - F.Nleft].angle);
-    FeatVecCSR<decltype(pKF->mFeatVec)> fk(pKF->mFeatVec);
-    FeatVecCSR<decltype(F.mFeatVec)> ff(F.mFeatVec);
-    osg_bow_side sk{nk, pKF->NLeft, dk.data(), ak.data(), idk.data(), good.data(), fk.view()};
-    osg_bow_side sf{nf, F.Nleft, df.data(), af.data(), nullptr, nullptr, ff.view()};
-    std::vector<int32_t> out(nf, -1);
+    BowKfF<KeyFrameT, FrameT, MapPointT> g(pKF, F);
+    std::vector<int32_t> out(F.N, -1);
     const int nm = call(ctx, "osg_search_by_bow_kf_f",
-                        [&] { return osg_search_by_bow_kf_f(ctx, &sk, &sf, nnratio, checkOri, out.data()); });
-    vpMapPointMatches.assign(nf, nullptr);  // ref:src/ORBmatcher.cc:268
-    if (nm < 0) return 0;
-    for (int i = 0; i < nf; i++)
-        if (out[i] >= 0) vpMapPointMatches[i] = vpMPsKF[out[i]];
-    return nm;
+                        [&] { return osg_search_by_bow_kf_f(ctx, &g.sk, &g.sf, nnratio, checkOri, out.data()); });
+    g.apply(out.data(), F.N, vpMapPointMatches, nm >= 0);
+    return nm < 0 ? 0 : nm;
 }
 
 // ref:src/ORBmatcher.cc:890-1043.  vpMatches12[i] = KF2 MapPoint matched to KF1 keypoint i.
@@ -812,6 +878,7 @@ int search_for_initialization(FrameT &F1, FrameT &F2, std::vector<PointT> &vbPre
 // writes mvuRight and mvDepth.  Returns the matches kept.
 template <class MatT>
 struct PyramidView {
+    OSG_PINNED_STRUCT(PyramidView);
     std::vector<const uint8_t *> data;
     std::vector<int32_t> rows, cols, step;
     osg_image_pyramid v{};
@@ -834,44 +901,54 @@ struct PyramidView {
 };
 
 template <class FrameT>
+struct StereoGather {
+    OSG_PINNED_STRUCT(StereoGather);
+    using MatT = typename std::decay<decltype(std::declval<FrameT &>().mpORBextractorLeft->mvImagePyramid[0])>::type;
+    std::vector<float> x, y, xr, yr, ang, sc, isc;
+    std::vector<int32_t> o, orr;
+    std::vector<uint8_t> dl, dr;
+    PyramidView<MatT> pl, pr;
+    osg_stereo_frame s{};
+    explicit StereoGather(const FrameT &F)
+        : sc(F.mvScaleFactors.begin(), F.mvScaleFactors.end()), isc(F.mvInvScaleFactors.begin(), F.mvInvScaleFactors.end()),
+          pl(F.mpORBextractorLeft->mvImagePyramid, (int)F.mvScaleFactors.size()),
+          pr(F.mpORBextractorRight->mvImagePyramid, (int)F.mvScaleFactors.size())
+    {
+        const int n = F.N, nr = (int)F.mvKeysRight.size();
+        for (int i = 0; i < n; i++) push_kp(F.mvKeys[i], x, y, ang, o);
+        for (int i = 0; i < nr; i++) push_kp(F.mvKeysRight[i], xr, yr, ang, orr);
+        copy_desc_rows(F.mDescriptors, n, dl);
+        copy_desc_rows(F.mDescriptorsRight, nr, dr);
+        s.n = n;
+        s.x = x.data();
+        s.y = y.data();
+        s.octave = o.data();
+        s.desc = dl.data();
+        s.n_right = nr;
+        s.xr = xr.data();
+        s.yr = yr.data();
+        s.octave_r = orr.data();
+        s.desc_r = dr.data();
+        s.scale_factors = sc.data();
+        s.inv_scale_factors = isc.data();
+        s.n_levels = (int)sc.size();
+        s.mb = F.mb;
+        s.mbf = F.mbf;
+        s.left = pl.v;
+        s.right = pr.v;
+    }
+};
+
+template <class FrameT>
 int compute_stereo_matches(FrameT &F)
 {
     osg_ctx *ctx = thread_ctx();
-    const int n = F.N, nr = (int)F.mvKeysRight.size();
-    std::vector<float> x, y, xr, yr, ang;
-    std::vector<int32_t> o, orr;
-    for (int i = 0; i < n; i++) push_kp(F.mvKeys[i], x, y, ang, o);
-    for (int i = 0; i < nr; i++) push_kp(F.mvKeysRight[i], xr, yr, ang, orr);
-    std::vector<uint8_t> dl, dr;
-    copy_desc_rows(F.mDescriptors, n, dl);
-    copy_desc_rows(F.mDescriptorsRight, nr, dr);
-    std::vector<float> sc(F.mvScaleFactors.begin(), F.mvScaleFactors.end());
-    std::vector<float> isc(F.mvInvScaleFactors.begin(), F.mvInvScaleFactors.end());
-    const int levels = (int)sc.size();
-    using MatT = typename std::decay<decltype(F.mpORBextractorLeft->mvImagePyramid[0])>::type;
-    PyramidView<MatT> pl(F.mpORBextractorLeft->mvImagePyramid, levels), pr(F.mpORBextractorRight->mvImagePyramid, levels);
-    osg_stereo_frame s{};
-    s.n = n;
-    s.x = x.data();
-    s.y = y.data();
-    s.octave = o.data();
-    s.desc = dl.data();
-    s.n_right = nr;
-    s.xr = xr.data();
-    s.yr = yr.data();
-    s.octave_r = orr.data();
-    s.desc_r = dr.data();
-    s.scale_factors = sc.data();
-    s.inv_scale_factors = isc.data();
-    s.n_levels = levels;
-    s.mb = F.mb;
-    s.mbf = F.mbf;
-    s.left = pl.v;
-    s.right = pr.v;
+    StereoGather<FrameT> g(F);
+    const int n = F.N;
     F.mvuRight.assign(n, -1.0f);  // :1134-1135
     F.mvDepth.assign(n, -1.0f);
     const int nm = call(ctx, "osg_compute_stereo_matches",
-                        [&] { return osg_compute_stereo_matches(ctx, &s, F.mvuRight.data(), F.mvDepth.data()); });
+                        [&] { return osg_compute_stereo_matches(ctx, &g.s, F.mvuRight.data(), F.mvDepth.data()); });
     if (nm < 0) {  // no stereo match for any keypoint
         F.mvuRight.assign(n, -1.0f);
         F.mvDepth.assign(n, -1.0f);
@@ -1136,71 +1213,89 @@ struct NoMutex {
     void unlock() {}
 };
 
-template <class H, class FrameT, class MutexT = NoMutex>
-int pose_optimization(FrameT *pFrame, MutexT *gather_mutex = nullptr)
-{
-    osg_ctx *ctx = thread_ctx();
-    const int N = pFrame->N;
+// PoseGather: one Frame's edges (the gather of ref:src/Optimizer.cc:128-286), shared by the single and
+// the batched entry points.
+template <class H, class FrameT>
+struct PoseGather {
+    OSG_PINNED_STRUCT(PoseGather);
     std::vector<int8_t> kind;
     std::vector<double> xw, obs;
     std::vector<float> isig;
     std::vector<int> slot;
-    const bool two = (bool)pFrame->mpCamera2;
-    std::unique_lock<MutexT> gather_lock;
-    if (gather_mutex) gather_lock = std::unique_lock<MutexT>(*gather_mutex);
-    for (int i = 0; i < N; i++) {
-        auto *pMP = pFrame->mvpMapPoints[i];
-        if (!pMP) continue;
-        double X[3];
-        H::world_pos(pMP, X);
-        int8_t k;
-        double o[3] = {0, 0, 0};
-        int oct;
-        if (!two) {
-            const auto &kp = pFrame->mvKeysUn[i];
-            k = pFrame->mvuRight[i] < 0 ? OSG_EDGE_MONO : OSG_EDGE_STEREO;
-            o[0] = kp.pt.x;
-            o[1] = kp.pt.y;
-            if (k == OSG_EDGE_STEREO) o[2] = pFrame->mvuRight[i];
-            oct = kp.octave;
-        } else if (i < pFrame->Nleft) {
-            const auto &kp = pFrame->mvKeys[i];
-            k = OSG_EDGE_MONO;
-            o[0] = kp.pt.x;
-            o[1] = kp.pt.y;
-            oct = kp.octave;
-        } else {
-            const auto &kp = pFrame->mvKeysRight[i - pFrame->Nleft];
-            k = OSG_EDGE_BODY;
-            o[0] = kp.pt.x;
-            o[1] = kp.pt.y;
-            oct = kp.octave;
-        }
-        pFrame->mvbOutlier[i] = false;
-        kind.push_back(k);
-        xw.insert(xw.end(), X, X + 3);
-        obs.insert(obs.end(), o, o + 3);
-        isig.push_back(pFrame->mvInvLevelSigma2[oct]);
-        slot.push_back(i);
-    }
-    if (gather_lock.owns_lock()) gather_lock.unlock();  // ref:src/Optimizer.cc:286, end of Step 3
+    std::vector<uint8_t> outl;
     osg_pose_problem p{};
-    H::pose(*pFrame, p.pose);
-    p.n_edges = (int32_t)kind.size();
-    p.kind = kind.data();
-    p.xw = xw.data();
-    p.obs = obs.data();
-    p.inv_sigma2 = isig.data();
-    H::camera(*pFrame, false, p.cam);
-    if (two) H::camera(*pFrame, true, p.cam2);
-    std::vector<uint8_t> outl(kind.size());
+    template <class MutexT>
+    PoseGather(FrameT *pFrame, MutexT *gather_mutex)
+    {
+        const int N = pFrame->N;
+        const bool two = (bool)pFrame->mpCamera2;
+        std::unique_lock<MutexT> gather_lock;
+        if (gather_mutex) gather_lock = std::unique_lock<MutexT>(*gather_mutex);
+        for (int i = 0; i < N; i++) {
+            auto *pMP = pFrame->mvpMapPoints[i];
+            if (!pMP) continue;
+            double X[3];
+            H::world_pos(pMP, X);
+            int8_t k;
+            double o[3] = {0, 0, 0};
+            int oct;
+            if (!two) {
+                const auto &kp = pFrame->mvKeysUn[i];
+                k = pFrame->mvuRight[i] < 0 ? OSG_EDGE_MONO : OSG_EDGE_STEREO;
+                o[0] = kp.pt.x;
+                o[1] = kp.pt.y;
+                if (k == OSG_EDGE_STEREO) o[2] = pFrame->mvuRight[i];
+                oct = kp.octave;
+            } else if (i < pFrame->Nleft) {
+                const auto &kp = pFrame->mvKeys[i];
+                k = OSG_EDGE_MONO;
+                o[0] = kp.pt.x;
+                o[1] = kp.pt.y;
+                oct = kp.octave;
+            } else {
+                const auto &kp = pFrame->mvKeysRight[i - pFrame->Nleft];
+                k = OSG_EDGE_BODY;
+                o[0] = kp.pt.x;
+                o[1] = kp.pt.y;
+                oct = kp.octave;
+            }
+            pFrame->mvbOutlier[i] = false;
+            kind.push_back(k);
+            xw.insert(xw.end(), X, X + 3);
+            obs.insert(obs.end(), o, o + 3);
+            isig.push_back(pFrame->mvInvLevelSigma2[oct]);
+            slot.push_back(i);
+        }
+        if (gather_lock.owns_lock()) gather_lock.unlock();  // ref:src/Optimizer.cc:286, end of Step 3
+        H::pose(*pFrame, p.pose);
+        p.n_edges = (int32_t)kind.size();
+        p.kind = kind.data();
+        p.xw = xw.data();
+        p.obs = obs.data();
+        p.inv_sigma2 = isig.data();
+        H::camera(*pFrame, false, p.cam);
+        if (two) H::camera(*pFrame, true, p.cam2);
+        outl.resize(kind.size());
+    }
+    // mvbOutlier and the pose, as ref:src/Optimizer.cc:405-419; a frame with < 3 edges keeps its pose
+    int apply(FrameT *pFrame, const osg_pose_result &r) const
+    {
+        if (p.n_edges < 3) return 0;  // ref:src/Optimizer.cc:289-290 (pose untouched)
+        for (size_t e = 0; e < slot.size(); e++) pFrame->mvbOutlier[slot[e]] = outl[e] != 0;
+        H::set_pose(*pFrame, r.pose);
+        return r.n_inliers;
+    }
+};
+
+template <class H, class FrameT, class MutexT = NoMutex>
+int pose_optimization(FrameT *pFrame, MutexT *gather_mutex = nullptr)
+{
+    osg_ctx *ctx = thread_ctx();
+    PoseGather<H, FrameT> g(pFrame, gather_mutex);
     osg_pose_result r{};
-    r.outlier = outl.data();
-    if (call(ctx, "osg_pose_optimization", [&] { return osg_pose_optimization(ctx, &p, &r); }) < 0) return 0;
-    if (p.n_edges < 3) return 0;  // ref:src/Optimizer.cc:289-290 (pose untouched)
-    for (size_t e = 0; e < slot.size(); e++) pFrame->mvbOutlier[slot[e]] = outl[e] != 0;
-    H::set_pose(*pFrame, r.pose);
-    return r.n_inliers;
+    r.outlier = g.outl.data();
+    if (call(ctx, "osg_pose_optimization", [&] { return osg_pose_optimization(ctx, &g.p, &r); }) < 0) return 0;
+    return g.apply(pFrame, r);
 }
 
 // ---------------------------------------------------------- a11 LocalBundleAdjustment (g2o part)
@@ -1743,6 +1838,166 @@ void apply_merge_local_bundle_adjustment(const MergeLbaOutcome<KeyFrameT, MapPoi
     }
     for (const auto &kp : o.poses) H::set_pose(*kp.first, kp.second.data());
     for (const auto &mp : o.points) H::set_world_pos(mp.first, mp.second.data());
+}
+
+// ------------------------------------------------------------------------------ batched forms
+// B independent problems gathered from the reference's objects, solved in one launch (the
+// osg_*_batch entry points: one workgroup or frame slice per problem), and written back exactly as
+// B single calls would.  For hosts that hold several frames at once: the frames of several
+// sequences' Tracking threads (config C5 runs one sequence per thread, ref:src/System.cc:234-273),
+// a replayed sequence, or the neighbours of a new keyframe.  Gathering runs on the calling thread;
+// nmatches[b] / n_inliers[b] receive what the single call returns for problem b.  On an ABI error
+// every problem gets the single call's nothing-found outcome (logged once per thread).
+template <class H, class KeyFrameT, class FrameT, class MapPointT>
+int search_by_bow_kf_f_batch(const std::vector<KeyFrameT *> &kfs, const std::vector<FrameT *> &frames,
+                             std::vector<std::vector<MapPointT *>> &matches, float nnratio, bool checkOri,
+                             int32_t *nmatches)
+{
+    osg_ctx *ctx = thread_ctx();
+    const int B = (int)frames.size();
+    std::deque<BowKfF<KeyFrameT, FrameT, MapPointT>> g;
+    std::vector<osg_bow_side> sk(B), sf(B);
+    std::vector<size_t> off(B + 1, 0);
+    for (int b = 0; b < B; b++) {
+        g.emplace_back(kfs[b], *frames[b]);
+        sk[b] = g.back().sk;
+        sf[b] = g.back().sf;
+        off[b + 1] = off[b] + (size_t)frames[b]->N;
+    }
+    std::vector<int32_t> out(off[B], -1);
+    const int rc = B == 0 ? OSG_OK : call(ctx, "osg_search_by_bow_kf_f_batch", [&] {
+        return osg_search_by_bow_kf_f_batch(ctx, sk.data(), sf.data(), B, nnratio, checkOri, out.data(), nmatches);
+    });
+    matches.resize(B);
+    for (int b = 0; b < B; b++) {
+        g[b].apply(out.data() + off[b], frames[b]->N, matches[b], rc >= 0);
+        if (rc < 0) nmatches[b] = 0;
+    }
+    return rc < 0 ? 0 : B;
+}
+
+template <class H, class FrameT, class MutexT = NoMutex>
+int pose_optimization_batch(const std::vector<FrameT *> &frames, int32_t *n_inliers, MutexT *gather_mutex = nullptr)
+{
+    osg_ctx *ctx = thread_ctx();
+    const int B = (int)frames.size();
+    std::deque<PoseGather<H, FrameT>> g;
+    std::vector<osg_pose_problem> p(B);
+    std::vector<osg_pose_result> r(B);
+    for (int b = 0; b < B; b++) {
+        g.emplace_back(frames[b], gather_mutex);
+        p[b] = g.back().p;
+        r[b] = osg_pose_result{};
+        r[b].outlier = g.back().outl.data();
+    }
+    const int rc = B == 0 ? OSG_OK : call(ctx, "osg_pose_optimization_batch",
+                                          [&] { return osg_pose_optimization_batch(ctx, p.data(), B, r.data()); });
+    for (int b = 0; b < B; b++) n_inliers[b] = rc < 0 ? 0 : g[b].apply(frames[b], r[b]);
+    return rc < 0 ? 0 : B;
+}
+
+template <class H, class FrameT>
+int search_by_projection_last_batch(const std::vector<FrameT *> &CFs, const std::vector<const FrameT *> &LFs, float th,
+                                    bool bMono, bool checkOri, int32_t *nmatches)
+{
+    osg_ctx *ctx = thread_ctx();
+    const int B = (int)CFs.size();
+    std::deque<LastGather<H, FrameT>> g;
+    std::vector<osg_frame> f(B);
+    std::vector<osg_last_queries> q(B);
+    std::vector<size_t> off(B + 1, 0);
+    for (int b = 0; b < B; b++) {
+        g.emplace_back(*CFs[b], *LFs[b]);
+        f[b] = g.back().fv.v;
+        q[b] = g.back().q;
+        off[b + 1] = off[b] + (size_t)CFs[b]->N;
+    }
+    std::vector<int32_t> mp(off[B]);
+    std::vector<uint8_t> taken(off[B]);
+    for (int b = 0; b < B; b++) {
+        std::copy(g[b].slots.mp.begin(), g[b].slots.mp.end(), mp.begin() + off[b]);
+        std::copy(g[b].slots.taken.begin(), g[b].slots.taken.end(), taken.begin() + off[b]);
+    }
+    const int rc = B == 0 ? OSG_OK : call(ctx, "osg_search_by_projection_last_batch", [&] {
+        return osg_search_by_projection_last_batch(ctx, f.data(), q.data(), B, th, bMono, checkOri, mp.data(),
+                                                   taken.data(), nmatches);
+    });
+    for (int b = 0; b < B; b++) {
+        if (rc < 0) {
+            nmatches[b] = 0;
+            continue;
+        }
+        std::copy(mp.begin() + off[b], mp.begin() + off[b + 1], g[b].slots.mp.begin());
+        g[b].slots.apply(CFs[b]->mvpMapPoints, g[b].queries, LFs[b]->N);
+    }
+    return rc < 0 ? 0 : B;
+}
+
+template <class H, class FrameT, class MapPointT>
+int search_by_projection_mps_batch(const std::vector<FrameT *> &Fs, const std::vector<const std::vector<MapPointT *> *> &mps,
+                                   float th, bool bFarPoints, float thFarPoints, float nnratio, int32_t *nmatches)
+{
+    osg_ctx *ctx = thread_ctx();
+    const int B = (int)Fs.size();
+    std::deque<MpsGather<FrameT, MapPointT>> g;
+    std::vector<osg_frame> f(B);
+    std::vector<osg_mp_queries> q(B);
+    std::vector<size_t> off(B + 1, 0);
+    for (int b = 0; b < B; b++) {
+        g.emplace_back(*Fs[b], *mps[b]);
+        f[b] = g.back().fv.v;
+        q[b] = g.back().q;
+        off[b + 1] = off[b] + (size_t)Fs[b]->N;
+    }
+    std::vector<int32_t> mp(off[B]);
+    std::vector<uint8_t> taken(off[B]);
+    for (int b = 0; b < B; b++) {
+        std::copy(g[b].slots.mp.begin(), g[b].slots.mp.end(), mp.begin() + off[b]);
+        std::copy(g[b].slots.taken.begin(), g[b].slots.taken.end(), taken.begin() + off[b]);
+    }
+    const int rc = B == 0 ? OSG_OK : call(ctx, "osg_search_by_projection_mps_batch", [&] {
+        return osg_search_by_projection_mps_batch(ctx, f.data(), q.data(), B, nnratio, th, bFarPoints, thFarPoints,
+                                                  mp.data(), taken.data(), nmatches);
+    });
+    for (int b = 0; b < B; b++) {
+        if (rc < 0) {
+            nmatches[b] = 0;
+            continue;
+        }
+        std::copy(mp.begin() + off[b], mp.begin() + off[b + 1], g[b].slots.mp.begin());
+        g[b].slots.apply(Fs[b]->mvpMapPoints, *mps[b], (int)mps[b]->size());
+    }
+    return rc < 0 ? 0 : B;
+}
+
+template <class FrameT>
+int compute_stereo_matches_batch(const std::vector<FrameT *> &frames, int32_t *nmatches)
+{
+    osg_ctx *ctx = thread_ctx();
+    const int B = (int)frames.size();
+    std::deque<StereoGather<FrameT>> g;
+    std::vector<osg_stereo_frame> s(B);
+    std::vector<size_t> off(B + 1, 0);
+    for (int b = 0; b < B; b++) {
+        g.emplace_back(*frames[b]);
+        s[b] = g.back().s;
+        off[b + 1] = off[b] + (size_t)frames[b]->N;
+    }
+    std::vector<float> ur(off[B], -1.0f), depth(off[B], -1.0f);
+    const int rc = B == 0 ? OSG_OK : call(ctx, "osg_compute_stereo_matches_batch", [&] {
+        return osg_compute_stereo_matches_batch(ctx, s.data(), B, ur.data(), depth.data(), nmatches);
+    });
+    for (int b = 0; b < B; b++) {
+        FrameT &F = *frames[b];
+        F.mvuRight.assign(ur.begin() + off[b], ur.begin() + off[b + 1]);  // :1134-1135 when rc < 0 (all -1)
+        F.mvDepth.assign(depth.begin() + off[b], depth.begin() + off[b + 1]);
+        if (rc < 0) {
+            F.mvuRight.assign(F.N, -1.0f);
+            F.mvDepth.assign(F.N, -1.0f);
+            nmatches[b] = 0;
+        }
+    }
+    return rc < 0 ? 0 : B;
 }
 
 }  // namespace osg_orbslam3

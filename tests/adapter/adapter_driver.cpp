@@ -2,329 +2,100 @@
 // arrays written by tests/test_adapter.py, and writes the adapter's results back (test-only).
 //
 //   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba fuse fuse_sim3 triang distinct sim3 sim3_kfs sim3pair init stereo fisheye gba merge_lba orb
-//
-// Array file: repeated {u32 name_len, name, u8 dtype ('b' u8, 'i' i32, 'f' f32, 'd' f64), u64 count,
-// data}.
-#include <cstdio>
-#include <cstdlib>
-#include <list>
-#include <memory>
-#include <string>
-#include <unordered_map>
+//                                                       and the batched forms bow_kf_f_batch pose_batch last_batch mps_batch stereo_batch
+#include <deque>
 
-#include "../../adapters/orbslam3/osg_orbslam3.h"
-#include "mock_orbslam3.h"
+#include "driver_common.h"
 
-using namespace mock;
-
-struct Arr {
-    char t = 0;
-    std::vector<unsigned char> b;
-    size_t n = 0;
-    template <class T>
-    const T *p() const { return reinterpret_cast<const T *>(b.data()); }
-};
-using Arrays = std::unordered_map<std::string, Arr>;
-
-static Arrays read_arrays(const char *path)
+// Batched forms ("<mode>_batch"): "batch.n" problems under the prefixes "b0.", "b1.", ... with the
+// single mode's arrays and the same "params"; outputs concatenated in problem order.
+static void run_batch_mode(const std::string &mode, const Arrays &in, const float *prm, Arrays &out)
 {
-    Arrays m;
-    FILE *f = fopen(path, "rb");
-    if (!f) throw std::runtime_error(std::string("cannot open ") + path);
-    for (;;) {
-        uint32_t len;
-        if (fread(&len, 4, 1, f) != 1) break;
-        std::string name(len, '\0');
-        fread(&name[0], 1, len, f);
-        Arr a;
-        fread(&a.t, 1, 1, f);
-        uint64_t n;
-        fread(&n, 8, 1, f);
-        a.n = n;
-        const size_t es = a.t == 'b' ? 1 : a.t == 'd' ? 8 : 4;
-        a.b.resize(n * es);
-        if (n) fread(a.b.data(), es, n, f);
-        m[name] = std::move(a);
-    }
-    fclose(f);
-    return m;
-}
-
-static void write_arrays(const char *path, const Arrays &m)
-{
-    FILE *f = fopen(path, "wb");
-    for (const auto &kv : m) {
-        const uint32_t len = (uint32_t)kv.first.size();
-        fwrite(&len, 4, 1, f);
-        fwrite(kv.first.data(), 1, len, f);
-        fwrite(&kv.second.t, 1, 1, f);
-        const uint64_t n = kv.second.n;
-        fwrite(&n, 8, 1, f);
-        fwrite(kv.second.b.data(), 1, kv.second.b.size(), f);
-    }
-    fclose(f);
-}
-
-template <class T>
-static Arr make(char t, const std::vector<T> &v)
-{
-    Arr a;
-    a.t = t;
-    a.n = v.size();
-    a.b.resize(v.size() * sizeof(T));
-    if (!v.empty()) std::memcpy(a.b.data(), v.data(), a.b.size());
-    return a;
-}
-
-static const Arr &get(const Arrays &m, const std::string &k)
-{
-    auto it = m.find(k);
-    if (it == m.end()) throw std::runtime_error("missing array " + k);
-    return it->second;
-}
-
-static bool has(const Arrays &m, const std::string &k) { return m.count(k) != 0; }
-
-static void fill_grid(const Arrays &m, const std::string &pre, std::vector<std::size_t> (&grid)[OSG_GRID_COLS][OSG_GRID_ROWS])
-{
-    const int32_t *gs = get(m, pre + "grid_start").p<int32_t>(), *gi = get(m, pre + "grid_idx").p<int32_t>();
-    for (int ix = 0; ix < OSG_GRID_COLS; ix++)
-        for (int iy = 0; iy < OSG_GRID_ROWS; iy++) {
-            const int c = ix * OSG_GRID_ROWS + iy;
-            for (int j = gs[c]; j < gs[c + 1]; j++) grid[ix][iy].push_back((size_t)gi[j]);
+    namespace oa = osg_orbslam3;
+    const int B = get(in, "batch.n").p<int32_t>()[0];
+    std::vector<std::unique_ptr<MapPoint>> pool;
+    std::vector<int32_t> nm(B, -7);
+    auto pre = [](int b) { return "b" + std::to_string(b) + "."; };
+    if (mode == "bow_kf_f_batch") {
+        std::deque<KeyFrame> K(B);
+        std::deque<Frame> F(B);
+        std::vector<KeyFrame *> kp;
+        std::vector<Frame *> fp;
+        for (int b = 0; b < B; b++) {
+            build_bow_kf_f_problem(in, pre(b), K[b], F[b], pool);
+            kp.push_back(&K[b]);
+            fp.push_back(&F[b]);
         }
-}
-
-// Frame from the FrameSoA arrays "F.*" (keypoints, descriptors, mvuRight, grid CSR, scales; for a
-// two-camera rig "F.nleft", the right grid and the stereo-partner maps)
-static void build_frame(const Arrays &m, Frame &F, const std::string &P = "F.")
-{
-    const int n = (int)get(m, P + "kp_x").n;
-    F.N = n;
-    F.Nleft = has(m, P + "nleft") ? get(m, P + "nleft").p<int32_t>()[0] : -1;
-    const int nl = F.Nleft == -1 ? n : F.Nleft;
-    const float *x = get(m, P + "kp_x").p<float>(), *y = get(m, P + "kp_y").p<float>(), *a = get(m, P + "kp_angle").p<float>();
-    const int32_t *o = get(m, P + "kp_octave").p<int32_t>();
-    std::vector<cv::KeyPoint> kps(n);
-    for (int i = 0; i < n; i++) {
-        kps[i].pt.x = x[i];
-        kps[i].pt.y = y[i];
-        kps[i].angle = a[i];
-        kps[i].octave = o[i];
-    }
-    F.mvKeys.assign(kps.begin(), kps.begin() + nl);
-    F.mvKeysRight.assign(kps.begin() + nl, kps.end());
-    F.mvKeysUn = F.mvKeys;  // left keypoints only on a two-camera rig (ref:src/Frame.cc:1022)
-    if (F.Nleft != -1) {
-        fill_grid(m, P, F.mGrid);
-        fill_grid(m, P + "r_", F.mGridRight);
-        const Arr &l2r = get(m, P + "left_to_right"), &r2l = get(m, P + "right_to_left");
-        F.mvLeftToRightMatch.assign(l2r.p<int32_t>(), l2r.p<int32_t>() + l2r.n);
-        F.mvRightToLeftMatch.assign(r2l.p<int32_t>(), r2l.p<int32_t>() + r2l.n);
-    }
-    F.mDescriptors = cv::Mat(n, 32);
-    std::memcpy(F.mDescriptors.buf.data(), get(m, P + "desc").b.data(), (size_t)n * 32);
-    F.mvuRight.assign(n, -1.0f);
-    if (has(m, P + "u_right")) std::memcpy(F.mvuRight.data(), get(m, P + "u_right").b.data(), (size_t)n * 4);
-    if (F.Nleft == -1) fill_grid(m, P, F.mGrid);
-    const float *sc = get(m, P + "scalars").p<float>();  // min_x max_x min_y max_y inv_w inv_h mb mbf
-    Frame::mnMinX = sc[0];
-    Frame::mnMaxX = sc[1];
-    Frame::mnMinY = sc[2];
-    Frame::mnMaxY = sc[3];
-    Frame::mfGridElementWidthInv = sc[4];
-    Frame::mfGridElementHeightInv = sc[5];
-    F.mb = sc[6];
-    F.mbf = sc[7];
-    const Arr &s = get(m, P + "scale");
-    F.mvScaleFactors.assign(s.p<float>(), s.p<float>() + s.n);
-    F.mnScaleLevels = (int)s.n;
-    F.mvpMapPoints.assign(n, nullptr);
-    F.mvbOutlier.assign(n, false);
-}
-
-// occupants of Frame::mvpMapPoints from "S.slot_mp" / "S.slot_taken"
-static void build_slots(const Arrays &m, Frame &F, std::vector<std::unique_ptr<MapPoint>> &pool)
-{
-    const int32_t *sm = get(m, "S.slot_mp").p<int32_t>();
-    const uint8_t *st = has(m, "S.slot_taken") ? get(m, "S.slot_taken").p<uint8_t>() : nullptr;
-    for (int i = 0; i < F.N; i++)
-        if (sm[i] >= 0) {
-            pool.emplace_back(new MapPoint());
-            pool.back()->mnId = (unsigned long)sm[i];
-            pool.back()->nobs = st ? st[i] : 1;
-            F.mvpMapPoints[i] = pool.back().get();
+        std::vector<std::vector<MapPoint *>> matches;
+        oa::search_by_bow_kf_f_batch<MockHooks>(kp, fp, matches, prm[0], prm[1] != 0, nm.data());
+        std::vector<int32_t> all;
+        for (auto &m : matches) for (int32_t v : slot_ids(m)) all.push_back(v);
+        out["out_mp"] = make('i', all);
+    } else if (mode == "pose_batch") {
+        std::deque<Frame> F(B);
+        std::deque<Camera> c(B), c2(B);
+        std::vector<Frame *> fp;
+        for (int b = 0; b < B; b++) {
+            build_pose_problem(in, pre(b), F[b], c[b], c2[b], pool);
+            fp.push_back(&F[b]);
         }
-}
-
-static std::vector<int32_t> slot_ids(const std::vector<MapPoint *> &v)
-{
-    std::vector<int32_t> r(v.size(), -1);
-    for (size_t i = 0; i < v.size(); i++)
-        if (v[i]) r[i] = (int32_t)v[i]->mnId;
-    return r;
-}
-
-static void fill_featvec(const Arrays &m, const std::string &pre, std::map<unsigned int, std::vector<unsigned int>> &fv)
-{
-    const Arr &nid = get(m, pre + "node_id"), &ns = get(m, pre + "node_start"), &ft = get(m, pre + "feat");
-    for (size_t k = 0; k < nid.n; k++) {
-        auto &v = fv[nid.p<uint32_t>()[k]];
-        for (int j = ns.p<int32_t>()[k]; j < ns.p<int32_t>()[k + 1]; j++) v.push_back((unsigned)ft.p<int32_t>()[j]);
-    }
-}
-
-// a BoW side "B1." / "B2." as a KeyFrame with MapPoints (mnId = mp_id, bad = !mp_good)
-static void build_bow_kf(const Arrays &m, const std::string &pre, KeyFrame &K, std::vector<std::unique_ptr<MapPoint>> &pool)
-{
-    const Arr &d = get(m, pre + "desc");
-    const int n = (int)(d.n / 32);
-    K.N = n;
-    K.NLeft = has(m, pre + "nleft") ? get(m, pre + "nleft").p<int32_t>()[0] : -1;
-    const int nl = K.NLeft == -1 ? n : K.NLeft;
-    K.mDescriptors = cv::Mat(n, 32);
-    std::memcpy(K.mDescriptors.buf.data(), d.b.data(), d.b.size());
-    const float *ang = get(m, pre + "angle").p<float>();
-    std::vector<cv::KeyPoint> kps(n);
-    for (int i = 0; i < n; i++) kps[i].angle = ang[i];
-    K.mvKeys.assign(kps.begin(), kps.begin() + nl);
-    K.mvKeysRight.assign(kps.begin() + nl, kps.end());
-    K.mvKeysUn = K.mvKeys;
-    static Camera second;
-    K.mpCamera2 = K.NLeft == -1 ? nullptr : &second;
-    K.mvpMapPoints.assign(n, nullptr);
-    const int32_t *id = get(m, pre + "mp_id").p<int32_t>();
-    const uint8_t *good = get(m, pre + "mp_good").p<uint8_t>();
-    for (int i = 0; i < n; i++)
-        if (id[i] >= 0) {
-            pool.emplace_back(new MapPoint());
-            pool.back()->mnId = (unsigned long)id[i];
-            pool.back()->bad = !good[i];
-            K.mvpMapPoints[i] = pool.back().get();
+        oa::pose_optimization_batch<MockHooks>(fp, nm.data());
+        std::vector<double> poses;
+        std::vector<uint8_t> outl;
+        for (int b = 0; b < B; b++) {
+            poses.insert(poses.end(), F[b].pose, F[b].pose + 7);
+            for (int i = 0; i < F[b].N; i++) outl.push_back(F[b].mvbOutlier[i]);
         }
-    fill_featvec(m, pre, K.mFeatVec);
-}
-
-// KeyFrame with keypoints / grid / scales from the FrameSoA arrays "F.*" (Fuse target)
-static void build_kf_frame(const Arrays &m, KeyFrame &K)
-{
-    Frame F;
-    build_frame(m, F);
-    K.N = F.N;
-    K.NLeft = F.Nleft;
-    K.mvKeys = F.mvKeys;
-    K.mvKeysUn = F.mvKeysUn;
-    K.mvKeysRight = F.mvKeysRight;
-    K.mDescriptors = F.mDescriptors;
-    K.mvuRight = F.mvuRight;
-    K.mGrid.assign(OSG_GRID_COLS, std::vector<std::vector<std::size_t>>(OSG_GRID_ROWS));
-    K.mGridRight.assign(OSG_GRID_COLS, std::vector<std::vector<std::size_t>>(OSG_GRID_ROWS));
-    for (int ix = 0; ix < OSG_GRID_COLS; ix++)
-        for (int iy = 0; iy < OSG_GRID_ROWS; iy++) {
-            K.mGrid[ix][iy] = F.mGrid[ix][iy];
-            K.mGridRight[ix][iy] = F.mGridRight[ix][iy];
+        out["pose"] = make('d', poses);
+        out["outlier"] = make('b', outl);
+    } else if (mode == "last_batch") {
+        std::deque<Frame> CF(B), LF(B);
+        std::vector<Frame *> cp;
+        std::vector<const Frame *> lp;
+        for (int b = 0; b < B; b++) {
+            build_last_problem(in, pre(b), CF[b], LF[b], pool);
+            CF[b].tlc_z_value = prm[3];
+            cp.push_back(&CF[b]);
+            lp.push_back(&LF[b]);
         }
-    K.mvLeftToRightMatch = F.mvLeftToRightMatch;
-    K.mvRightToLeftMatch = F.mvRightToLeftMatch;
-    K.mnMinX = (int)Frame::mnMinX;
-    K.mnMaxX = (int)Frame::mnMaxX;
-    K.mnMinY = (int)Frame::mnMinY;
-    K.mnMaxY = (int)Frame::mnMaxY;
-    K.mfGridElementWidthInv = Frame::mfGridElementWidthInv;
-    K.mfGridElementHeightInv = Frame::mfGridElementHeightInv;
-    K.mvScaleFactors = F.mvScaleFactors;
-    K.mnScaleLevels = F.mnScaleLevels;
-    K.mb = F.mb;
-    K.mbf = F.mbf;
-    K.mvpMapPoints.assign(K.N, nullptr);
-}
-
-// a SearchForTriangulation keyframe "A." / "B." (KFSide arrays); MapPoints where has_mp
-static void build_triang_kf(const Arrays &m, const std::string &pre, KeyFrame &K, std::vector<std::unique_ptr<MapPoint>> &pool)
-{
-    const Arr &d = get(m, pre + "desc");
-    const int n = (int)(d.n / 32);
-    K.N = n;
-    K.NLeft = get(m, pre + "nleft").p<int32_t>()[0];
-    static Camera second;
-    K.mpCamera2 = get(m, pre + "two_cam").p<int32_t>()[0] ? &second : nullptr;
-    K.mDescriptors = cv::Mat(n, 32);
-    std::memcpy(K.mDescriptors.buf.data(), d.b.data(), d.b.size());
-    std::vector<cv::KeyPoint> kps(n);
-    for (int i = 0; i < n; i++) {
-        kps[i].pt.x = get(m, pre + "kp_x").p<float>()[i];
-        kps[i].pt.y = get(m, pre + "kp_y").p<float>()[i];
-        kps[i].angle = get(m, pre + "kp_angle").p<float>()[i];
-        kps[i].octave = get(m, pre + "kp_octave").p<int32_t>()[i];
-    }
-    const int nl = K.NLeft == -1 ? n : K.NLeft;
-    if (K.NLeft == -1) {
-        K.mvKeysUn = kps;
-        K.mvKeys = kps;
-    } else {  // mvKeysUn is not read on a rig: give it garbage positions to prove it
-        K.mvKeys.assign(kps.begin(), kps.begin() + nl);
-        K.mvKeysRight.assign(kps.begin() + nl, kps.end());
-        K.mvKeysUn = K.mvKeys;
-        for (auto &kp : K.mvKeysUn) kp.pt.x = -1e9f;
-    }
-    if (has(m, pre + "u_right")) {
-        const Arr &u = get(m, pre + "u_right");
-        K.mvuRight.assign(u.p<float>(), u.p<float>() + u.n);
-    }
-    const Arr &sc = get(m, pre + "scale"), &s2 = get(m, pre + "level_sigma2");
-    K.mvScaleFactors.assign(sc.p<float>(), sc.p<float>() + sc.n);
-    K.mvLevelSigma2.assign(s2.p<float>(), s2.p<float>() + s2.n);
-    K.mvpMapPoints.assign(n, nullptr);
-    for (int i = 0; i < n; i++)
-        if (get(m, pre + "has_mp").p<uint8_t>()[i]) {
-            pool.emplace_back(new MapPoint());
-            pool.back()->mnId = (unsigned long)i;
-            K.mvpMapPoints[i] = pool.back().get();
+        oa::search_by_projection_last_batch<MockHooks>(cp, lp, prm[0], prm[1] != 0, prm[2] != 0, nm.data());
+        std::vector<int32_t> all;
+        for (int b = 0; b < B; b++) for (int32_t v : slot_ids(CF[b].mvpMapPoints)) all.push_back(v);
+        out["slot_mp"] = make('i', all);
+    } else if (mode == "mps_batch") {
+        std::deque<Frame> F(B);
+        std::deque<std::vector<MapPoint *>> Q(B);
+        std::vector<Frame *> fp;
+        std::vector<const std::vector<MapPoint *> *> qp;
+        for (int b = 0; b < B; b++) {
+            build_mps_problem(in, pre(b), F[b], Q[b], pool);
+            fp.push_back(&F[b]);
+            qp.push_back(&Q[b]);
         }
-    fill_featvec(m, pre, K.mFeatVec);
-}
-
-// A BA world from the graph arrays "G.*": one KeyFrame per pose (mnId = index, the shared camera
-// "G.cam"), one MapPoint per point, one observation per edge (keypoint octave = its index in the
-// KeyFrame, so mvInvLevelSigma2[octave] is the edge's weight; mvuRight = ur on stereo edges)
-static void build_ba_world(const Arrays &in, Map &map, Camera &c, std::vector<KeyFrame> &kf, std::vector<MapPoint> &mp)
-{
-    const int np = (int)(get(in, "G.pose").n / 7), npt = (int)(get(in, "G.point").n / 3), ne = (int)get(in, "G.e_pose").n;
-    const float *cam = get(in, "G.cam").p<float>();
-    c.type = (int)cam[0];
-    c.params.assign(cam + 1, cam + 9);
-    kf.resize(np);
-    mp.resize(npt);
-    for (int i = 0; i < np; i++) {
-        kf[i].mnId = (unsigned long)i;
-        kf[i].map = &map;
-        std::memcpy(kf[i].pose, get(in, "G.pose").p<double>() + 7 * i, 56);
-        kf[i].mpCamera = &c;
-        kf[i].fx = cam[9];
-        kf[i].fy = cam[10];
-        kf[i].cx = cam[11];
-        kf[i].cy = cam[12];
-        kf[i].mbf = cam[13];
+        oa::search_by_projection_mps_batch<MockHooks>(fp, qp, prm[1], prm[2] != 0, prm[3], prm[0], nm.data());
+        std::vector<int32_t> all;
+        for (int b = 0; b < B; b++) for (int32_t v : slot_ids(F[b].mvpMapPoints)) all.push_back(v);
+        out["slot_mp"] = make('i', all);
+    } else if (mode == "stereo_batch") {
+        std::deque<Frame> F(B);
+        std::deque<ORBextractor> el(B), er(B);
+        std::vector<Frame *> fp;
+        for (int b = 0; b < B; b++) {
+            build_stereo_problem(in, pre(b), F[b], el[b], er[b]);
+            fp.push_back(&F[b]);
+        }
+        oa::compute_stereo_matches_batch(fp, nm.data());
+        std::vector<float> ur, depth;
+        for (int b = 0; b < B; b++) {
+            ur.insert(ur.end(), F[b].mvuRight.begin(), F[b].mvuRight.end());
+            depth.insert(depth.end(), F[b].mvDepth.begin(), F[b].mvDepth.end());
+        }
+        out["ur"] = make('f', ur);
+        out["depth"] = make('f', depth);
+    } else {
+        throw std::runtime_error("unknown batch mode " + mode);
     }
-    for (int j = 0; j < npt; j++) {
-        mp[j].mnId = (unsigned long)j;
-        mp[j].map = &map;
-        std::memcpy(mp[j].pos, get(in, "G.point").p<double>() + 3 * j, 24);
-    }
-    for (int e = 0; e < ne; e++) {
-        KeyFrame &k = kf[get(in, "G.e_pose").p<int32_t>()[e]];
-        MapPoint &p = mp[get(in, "G.e_point").p<int32_t>()[e]];
-        const double *o = get(in, "G.e_obs").p<double>() + 3 * e;
-        cv::KeyPoint kp;
-        kp.pt.x = (float)o[0];
-        kp.pt.y = (float)o[1];
-        kp.octave = (int)k.mvKeysUn.size();
-        k.mvKeysUn.push_back(kp);
-        k.mvInvLevelSigma2.push_back(get(in, "G.e_inv_sigma2").p<float>()[e]);
-        k.mvuRight.push_back(get(in, "G.e_kind").p<uint8_t>()[e] == OSG_EDGE_STEREO ? (float)o[2] : -1.0f);
-        k.mvpMapPoints.push_back(&p);
-        p.obs[&k] = std::make_tuple(kp.octave, -1);
-    }
+    out["nmatches"] = make('i', nm);
 }
 
 int main(int argc, char **argv)
@@ -341,68 +112,15 @@ int main(int argc, char **argv)
         const float *prm = has(in, "params") ? get(in, "params").p<float>() : nullptr;
         if (mode == "mps") {
             Frame F;
-            build_frame(in, F);
-            build_slots(in, F, pool);
-            const int nq = (int)get(in, "Q.mp_id").n;
-            std::vector<MapPoint *> q(nq);
-            for (int i = 0; i < nq; i++) {
-                pool.emplace_back(new MapPoint());
-                MapPoint *p = pool.back().get();
-                p->mnId = (unsigned long)get(in, "Q.mp_id").p<int32_t>()[i];
-                std::memcpy(p->desc.buf.data(), get(in, "Q.desc").p<uint8_t>() + 32 * i, 32);
-                p->bad = !get(in, "Q.usable").p<uint8_t>()[i];
-                p->nobs = get(in, "Q.has_obs").p<uint8_t>()[i];
-                p->mbTrackInView = get(in, "Q.in_view").p<uint8_t>()[i];
-                p->mTrackProjX = get(in, "Q.proj_x").p<float>()[i];
-                p->mTrackProjY = get(in, "Q.proj_y").p<float>()[i];
-                p->mTrackProjXR = get(in, "Q.proj_xr").p<float>()[i];
-                p->mTrackViewCos = get(in, "Q.view_cos").p<float>()[i];
-                p->mnTrackScaleLevel = get(in, "Q.pred_level").p<int32_t>()[i];
-                p->mTrackDepth = get(in, "Q.track_depth").p<float>()[i];
-                if (has(in, "Q.in_view_r")) {
-                    p->mbTrackInViewR = get(in, "Q.in_view_r").p<uint8_t>()[i];
-                    p->mTrackProjYR = get(in, "Q.proj_yr").p<float>()[i];
-                    p->mTrackViewCosR = get(in, "Q.view_cos_r").p<float>()[i];
-                    p->mnTrackScaleLevelR = get(in, "Q.pred_level_r").p<int32_t>()[i];
-                }
-                q[i] = p;
-            }
+            std::vector<MapPoint *> q;
+            build_mps_problem(in, "", F, q, pool);
             // params: nnratio th far thfar
             const int nm = osg_orbslam3::search_by_projection_mps<MockHooks>(F, q, prm[1], prm[2] != 0, prm[3], prm[0]);
             out["nmatches"] = make('i', std::vector<int32_t>{nm});
             out["slot_mp"] = make('i', slot_ids(F.mvpMapPoints));
         } else if (mode == "last") {
             Frame CF, LF;
-            build_frame(in, CF);
-            build_slots(in, CF, pool);
-            const int n = (int)get(in, "L.mp_id").n;
-            LF.N = n;
-            LF.Nleft = -1;
-            LF.mvKeysUn.resize(n);
-            LF.mvpMapPoints.assign(n, nullptr);
-            LF.mvbOutlier.assign(n, false);
-            for (int i = 0; i < n; i++) {
-                LF.mvKeysUn[i].octave = get(in, "L.octave").p<int32_t>()[i];
-                LF.mvKeysUn[i].angle = get(in, "L.angle").p<float>()[i];
-                const int id = get(in, "L.mp_id").p<int32_t>()[i];
-                if (id < 0) continue;
-                pool.emplace_back(new MapPoint());
-                MapPoint *p = pool.back().get();
-                p->mnId = (unsigned long)id;
-                std::memcpy(p->desc.buf.data(), get(in, "L.desc").p<uint8_t>() + 32 * i, 32);
-                p->nobs = get(in, "L.has_obs").p<uint8_t>()[i];
-                p->proj_ok = true;
-                p->proj_u = get(in, "L.u").p<float>()[i];
-                p->proj_v = get(in, "L.v").p<float>()[i];
-                p->proj_invz = get(in, "L.invz").p<float>()[i];
-                if (has(in, "L.u_r")) {
-                    p->proj_ur = get(in, "L.u_r").p<float>()[i];
-                    p->proj_vr = get(in, "L.v_r").p<float>()[i];
-                }
-                LF.mvpMapPoints[i] = p;
-                LF.mvbOutlier[i] = !get(in, "L.valid").p<uint8_t>()[i];
-            }
-            LF.mvKeys = LF.mvKeysUn;
+            build_last_problem(in, "", CF, LF, pool);
             CF.tlc_z_value = prm[3];
             // params: th mono ori tlc_z
             const int nm = osg_orbslam3::search_by_projection_last<MockHooks>(CF, LF, prm[0], prm[1] != 0, prm[2] != 0);
@@ -411,7 +129,7 @@ int main(int argc, char **argv)
         } else if (mode == "kf") {
             Frame CF;
             build_frame(in, CF);
-            build_slots(in, CF, pool);
+            build_slots(in, "", CF, pool);
             KeyFrame K;
             const int n = (int)get(in, "K.mp_id").n;
             K.N = n;
@@ -435,18 +153,9 @@ int main(int argc, char **argv)
             out["nmatches"] = make('i', std::vector<int32_t>{nm});
             out["slot_mp"] = make('i', slot_ids(CF.mvpMapPoints));
         } else if (mode == "bow_kf_f") {
-            KeyFrame K, KF;
-            build_bow_kf(in, "B1.", K, pool);
-            build_bow_kf(in, "B2.", KF, pool);
-            Frame F;  // the Frame side: descriptors, angles, FeatureVector
-            F.N = KF.N;
-            F.Nleft = KF.NLeft;
-            F.mDescriptors = KF.mDescriptors;
-            F.mvKeys = KF.mvKeys;
-            F.mvKeysUn = KF.mvKeysUn;
-            F.mvKeysRight = KF.mvKeysRight;
-            F.mpCamera2 = KF.mpCamera2;
-            F.mFeatVec = KF.mFeatVec;
+            KeyFrame K;
+            Frame F;
+            build_bow_kf_f_problem(in, "", K, F, pool);
             std::vector<MapPoint *> matches;
             // params: nnratio ori
             const int nm = osg_orbslam3::search_by_bow_kf_f<MockHooks>(&K, F, matches, prm[0], prm[1] != 0);
@@ -462,36 +171,9 @@ int main(int argc, char **argv)
             out["out_mp"] = make('i', slot_ids(matches));
         } else if (mode == "pose") {
             Frame F;
-            const int n = (int)get(in, "P.kind").n;
-            F.N = n;
-            F.Nleft = -1;
-            F.mvKeysUn.resize(n);
-            F.mvuRight.assign(n, -1.0f);
-            F.mvInvLevelSigma2.resize(n);
-            F.mvpMapPoints.assign(n, nullptr);
-            F.mvbOutlier.assign(n, false);
-            const double *obs = get(in, "P.obs").p<double>(), *xw = get(in, "P.xw").p<double>();
-            for (int i = 0; i < n; i++) {
-                pool.emplace_back(new MapPoint());
-                std::memcpy(pool.back()->pos, xw + 3 * i, 24);
-                F.mvpMapPoints[i] = pool.back().get();
-                F.mvKeysUn[i].pt.x = (float)obs[3 * i];
-                F.mvKeysUn[i].pt.y = (float)obs[3 * i + 1];
-                F.mvKeysUn[i].octave = i;  // one information level per keypoint
-                F.mvInvLevelSigma2[i] = get(in, "P.inv_sigma2").p<float>()[i];
-                if (get(in, "P.kind").p<uint8_t>()[i] == OSG_EDGE_STEREO) F.mvuRight[i] = (float)obs[3 * i + 2];
-            }
-            std::memcpy(F.pose, get(in, "P.pose").b.data(), 56);
-            const float *cam = get(in, "P.cam").p<float>();  // type p0..p7 fx fy cx cy bf
-            Camera c;
-            c.type = (int)cam[0];
-            c.params.assign(cam + 1, cam + 9);
-            F.mpCamera = &c;
-            F.fx = cam[9];
-            F.fy = cam[10];
-            F.cx = cam[11];
-            F.cy = cam[12];
-            F.mbf = cam[13];
+            Camera c, c2;
+            build_pose_problem(in, "", F, c, c2, pool);
+            const int n = F.N;
             ProbeMutex probe;  // params[0] != 0: pass a MapPoint::mGlobalMutex stand-in and report its use
             const bool use_probe = prm && prm[0] != 0;
             if (use_probe) g_probe = &probe;
@@ -798,54 +480,16 @@ int main(int argc, char **argv)
             out["m12"] = make('i', std::vector<int32_t>(m12.begin(), m12.end()));
             out["prev"] = make('f', po);
         } else if (mode == "stereo") {
-            // left "S.x/y/oct/desc", right "S.xr/yr/oct_r/desc_r", "S.scale", "S.inv_scale", "S.mb_mbf";
-            // pyramids "PL.img" / "PR.img" (levels concatenated) with "PL.dims" / "PR.dims" (rows, cols)
-            // held as ROIs of wider rows (step = cols + 7), as ORBextractor's bordered levels are
             Frame F;
-            const int n = (int)get(in, "S.x").n, nr = (int)get(in, "S.xr").n;
-            F.N = n;
-            auto kps = [&](const char *x, const char *y, const char *o, int cnt) {
-                std::vector<cv::KeyPoint> v(cnt);
-                for (int i = 0; i < cnt; i++) {
-                    v[i].pt.x = get(in, x).p<float>()[i];
-                    v[i].pt.y = get(in, y).p<float>()[i];
-                    v[i].octave = get(in, o).p<int32_t>()[i];
-                }
-                return v;
-            };
-            F.mvKeys = kps("S.x", "S.y", "S.oct", n);
-            F.mvKeysRight = kps("S.xr", "S.yr", "S.oct_r", nr);
-            F.mDescriptors = cv::Mat(n, 32);
-            std::memcpy(F.mDescriptors.buf.data(), get(in, "S.desc").b.data(), (size_t)n * 32);
-            F.mDescriptorsRight = cv::Mat(nr, 32);
-            std::memcpy(F.mDescriptorsRight.buf.data(), get(in, "S.desc_r").b.data(), (size_t)nr * 32);
-            const Arr &sc = get(in, "S.scale"), &isc = get(in, "S.inv_scale");
-            F.mvScaleFactors.assign(sc.p<float>(), sc.p<float>() + sc.n);
-            F.mvInvScaleFactors.assign(isc.p<float>(), isc.p<float>() + isc.n);
-            F.mnScaleLevels = (int)sc.n;
-            F.mb = get(in, "S.mb_mbf").p<float>()[0];
-            F.mbf = get(in, "S.mb_mbf").p<float>()[1];
             ORBextractor el, er;
-            auto pyr = [&](const char *img, const char *dims, ORBextractor &e) {
-                const uint8_t *src = get(in, img).p<uint8_t>();
-                const int32_t *d = get(in, dims).p<int32_t>();
-                for (size_t l = 0; l < sc.n; l++) {
-                    const int rows = d[2 * l], cols = d[2 * l + 1];
-                    cv::Mat m(rows, cols, (size_t)cols + 7);
-                    for (int r = 0; r < rows; r++) std::memcpy(m.ptr<unsigned char>(r), src + (size_t)r * cols, cols);
-                    src += (size_t)rows * cols;
-                    e.mvImagePyramid.push_back(std::move(m));
-                }
-            };
-            pyr("PL.img", "PL.dims", el);
-            pyr("PR.img", "PR.dims", er);
-            F.mpORBextractorLeft = &el;
-            F.mpORBextractorRight = &er;
-            F.mvuRight.assign(n, 123.0f);  // overwritten, as the reference's are
+            build_stereo_problem(in, "", F, el, er);
+            F.mvuRight.assign(F.N, 123.0f);  // overwritten, as the reference's are
             const int nm = osg_orbslam3::compute_stereo_matches(F);
             out["nmatches"] = make('i', std::vector<int32_t>{nm});
             out["ur"] = make('f', F.mvuRight);
             out["depth"] = make('f', F.mvDepth);
+        } else if (mode.size() > 6 && mode.compare(mode.size() - 6, 6, "_batch") == 0) {
+            run_batch_mode(mode, in, prm, out);
         } else if (mode == "fisheye") {
             // "FE.kl" / "FE.kr" (x, y), "FE.ol" / "FE.or", "FE.dl" / "FE.dr", "FE.mono" (monoLeft, monoRight),
             // "FE.sig2", "FE.cam" (2 x 8 KannalaBrandt8), "FE.R" (3x3), "FE.t"
