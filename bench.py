@@ -5,9 +5,11 @@
 
 Headline (BASELINE.json metric "Mmatches/s (256-bit Hamming) + LocalBA iters/s"), workload
 configs[1]: brute-force 256-bit Hamming top-2 of 2000 x 2000 descriptors (C2).  One step = one
-2000 x 2000 match through the C-ABI entry osg_hamming_top2_dev with inputs resident in HBM.  For
-N > 1 every rank matches its own independent frame (frame-batched replicas; no collective in the
-data path); value = pairs of all ranks / max-over-ranks time.
+launch of 256 independent 2000 x 2000 problems (frames) through the C-ABI entry
+osg_hamming_top2_batch_dev (k_top2_batch) with inputs resident in HBM; the one-problem launch
+(osg_hamming_top2_dev) is reported beside it as single_launch.  For N > 1 every rank matches its own
+independent frames (weak scaling; no collective in the data path); value = pairs of all ranks /
+max-over-ranks time.
 
 Also reported (same run): the dominant kernel's roofline (HIP events on its stream), the
 C2' streaming kernel's HBM roofline (Q = 4 x M = 2^24), the CPU restatement timed on this host
