@@ -17,7 +17,9 @@ HDRS = include/osg.h include/osg_ba.h $(CSRC)/osg_internal.h
 
 OBJS = $(OBJDIR)/runtime.o $(OBJDIR)/hamming.o $(OBJDIR)/match.o $(OBJDIR)/pose.o $(OBJDIR)/ba.o $(OBJDIR)/dbow.o $(OBJDIR)/fuse.o $(OBJDIR)/triang.o $(OBJDIR)/desc.o $(OBJDIR)/sim3.o $(OBJDIR)/init.o $(OBJDIR)/stereo.o $(OBJDIR)/orb.o $(OBJDIR)/fast.o $(OBJDIR)/pyramid.o
 
-all: $(LIB) oracle
+WALL_BENCH = tools/adapter_wall_bench
+
+all: $(LIB) oracle $(WALL_BENCH)
 
 $(OBJDIR):
 	mkdir -p $(OBJDIR)
@@ -73,3 +75,8 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean
+
+# the C++ adapter wall-rate bench (bench.py's wall_cpp_adapter_frames_per_s): host code over the
+# library and the HIP runtime (device-resident pyramid levels for the stereo workload)
+$(WALL_BENCH): tools/adapter_wall_bench.cpp adapters/orbslam3/osg_orbslam3.h tests/adapter/driver_common.h tests/adapter/mock_orbslam3.h include/osg.h include/osg_ba.h include/osg_dbow.h $(LIB)
+	g++ -std=c++17 -O2 -Wall -Werror -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude $< -o $@ -L$(PKG) -lorbslam3_amd -L/opt/rocm/lib -lamdhip64 '-Wl,-rpath,$$ORIGIN/../$(PKG)' -Wl,-rpath,/opt/rocm/lib -pthread

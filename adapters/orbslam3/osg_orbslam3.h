@@ -45,6 +45,7 @@
 
 #include "osg.h"
 #include "osg_ba.h"
+#include "osg_dbow.h"
 
 namespace osg_orbslam3 {
 
@@ -883,8 +884,12 @@ struct PyramidView {
     std::vector<int32_t> rows, cols, step;
     osg_image_pyramid v{};
 
-    PyramidView(const std::vector<MatT> &pyr, int n_levels)
+    PyramidView(const std::vector<MatT> &pyr, int n_levels, const osg_image_pyramid *on_device = nullptr)
     {
+        if (on_device) {  // levels already in HBM: read in place, no pixels cross PCIe
+            v = *on_device;
+            return;
+        }
         for (int l = 0; l < n_levels; l++) {
             data.push_back(pyr[l].template ptr<unsigned char>(0));
             rows.push_back(pyr[l].rows);
@@ -900,6 +905,20 @@ struct PyramidView {
     }
 };
 
+// An ORBextractor whose levels were built on the device by osg_orb_pyramid (the
+// pyramid section) keeps their view, on_device = 1, as `mpOsgDeviceLevels`; the stereo matcher then
+// reads those levels in place.  Extractors without the member are gathered from mvImagePyramid.
+template <class E>
+inline auto device_levels(const E &e, int) -> decltype(e.mpOsgDeviceLevels, (const osg_image_pyramid *)nullptr)
+{
+    return e.mpOsgDeviceLevels;
+}
+template <class E>
+inline const osg_image_pyramid *device_levels(const E &, long)
+{
+    return nullptr;
+}
+
 template <class FrameT>
 struct StereoGather {
     OSG_PINNED_STRUCT(StereoGather);
@@ -911,8 +930,8 @@ struct StereoGather {
     osg_stereo_frame s{};
     explicit StereoGather(const FrameT &F)
         : sc(F.mvScaleFactors.begin(), F.mvScaleFactors.end()), isc(F.mvInvScaleFactors.begin(), F.mvInvScaleFactors.end()),
-          pl(F.mpORBextractorLeft->mvImagePyramid, (int)F.mvScaleFactors.size()),
-          pr(F.mpORBextractorRight->mvImagePyramid, (int)F.mvScaleFactors.size())
+          pl(F.mpORBextractorLeft->mvImagePyramid, (int)F.mvScaleFactors.size(), device_levels(*F.mpORBextractorLeft, 0)),
+          pr(F.mpORBextractorRight->mvImagePyramid, (int)F.mvScaleFactors.size(), device_levels(*F.mpORBextractorRight, 0))
     {
         const int n = F.N, nr = (int)F.mvKeysRight.size();
         for (int i = 0; i < n; i++) push_kp(F.mvKeys[i], x, y, ang, o);
@@ -1998,6 +2017,95 @@ int compute_stereo_matches_batch(const std::vector<FrameT *> &frames, int32_t *n
         }
     }
     return rc < 0 ? 0 : B;
+}
+
+// ------------------------------------------------------ §8(f) rank 1: ComputeBoW (DBoW2 transform)
+// Frame::ComputeBoW (ref:src/Frame.cc:995-1010) and KeyFrame::ComputeBoW (ref:src/KeyFrame.cc:102-116):
+// when mBowVec is empty, transform(rows of mDescriptors, mBowVec, mFeatVec, levelsup = 4)
+// (ref:Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1126-1192) runs on the device.  `voc` is the
+// vocabulary uploaded once with osg_vocabulary_load_text (next to System's ORBVocabulary load).
+// KeyFrame's extra `|| mFeatVec.empty()` changes nothing: transform leaves both maps filled or both
+// empty.  Both maps come back in key order, so every insert is an end-hint insert.  On an ABI error
+// both maps stay empty, as for a frame without descriptors.
+struct BowSet {
+    OSG_PINNED_STRUCT(BowSet);
+    std::vector<int32_t> word, node_start, feat;
+    std::vector<double> value;
+    std::vector<uint32_t> node_id;
+    osg_bow_out o{};
+    // (capacities of at least 1: a frame without descriptors still passes non-null arrays)
+    explicit BowSet(int n)
+        : word(std::max(n, 1)), node_start(n + 1), feat(std::max(n, 1)), value(std::max(n, 1)), node_id(std::max(n, 1))
+    {
+        o.word = word.data();
+        o.value = value.data();
+        o.node_id = node_id.data();
+        o.node_start = node_start.data();
+        o.feat = feat.data();
+    }
+    template <class T>
+    void apply(T &F, bool ok) const
+    {
+        F.mBowVec.clear();
+        F.mFeatVec.clear();
+        if (!ok) return;
+        for (int j = 0; j < o.n_words; j++) F.mBowVec.emplace_hint(F.mBowVec.end(), (unsigned)word[j], value[j]);
+        for (int j = 0; j < o.n_nodes; j++)
+            F.mFeatVec.emplace_hint(F.mFeatVec.end(), node_id[j],
+                                    std::vector<unsigned int>(feat.begin() + node_start[j], feat.begin() + node_start[j + 1]));
+    }
+};
+
+template <class T>
+void compute_bow(T &F, const osg_vocabulary *voc)
+{
+    if (!F.mBowVec.empty()) return;
+    osg_ctx *ctx = thread_ctx();
+    const int n = F.mDescriptors.rows;
+    std::vector<uint8_t> desc;
+    copy_desc_rows(F.mDescriptors, n, desc);
+    BowSet s(n);
+    const int rc = call(ctx, "osg_vocabulary_transform",
+                        [&] { return osg_vocabulary_transform(ctx, voc, desc.data(), n, 4, &s.o); });
+    s.apply(F, rc >= 0);
+}
+
+// B frames or keyframes in one launch; those whose mBowVec is already filled are skipped, as the
+// single call skips them.
+template <class T>
+void compute_bow_batch(const std::vector<T *> &frames, const osg_vocabulary *voc)
+{
+    osg_ctx *ctx = thread_ctx();
+    std::vector<T *> todo;
+    std::vector<int32_t> n;
+    size_t rows = 0;
+    for (T *F : frames)
+        if (F->mBowVec.empty()) {
+            todo.push_back(F);
+            n.push_back(F->mDescriptors.rows);
+            rows += (size_t)n.back();
+        }
+    const int B = (int)todo.size();
+    if (B == 0) return;
+    std::vector<uint8_t> desc(32 * rows);
+    std::deque<BowSet> sets;
+    std::vector<osg_bow_out> out(B);
+    size_t r0 = 0;
+    for (int b = 0; b < B; b++) {
+        const auto &M = todo[b]->mDescriptors;
+        for (int i = 0; i < n[b]; i++) std::memcpy(&desc[32 * (r0 + i)], M.template ptr<unsigned char>(i), 32);
+        r0 += (size_t)n[b];
+        sets.emplace_back(n[b]);
+        out[b] = sets.back().o;
+    }
+    const int rc = call(ctx, "osg_vocabulary_transform_batch", [&] {
+        return osg_vocabulary_transform_batch(ctx, voc, desc.data(), n.data(), B, 4, out.data());
+    });
+    for (int b = 0; b < B; b++) {
+        sets[b].o.n_words = out[b].n_words;
+        sets[b].o.n_nodes = out[b].n_nodes;
+        sets[b].apply(*todo[b], rc >= 0);
+    }
 }
 
 }  // namespace osg_orbslam3

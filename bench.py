@@ -28,6 +28,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from tools.adapter_arrays import (bow_arrays, frame_arrays, last_arrays, mps_arrays, pose_arrays,  # noqa: E402
+                                  pose_for_mock, prefixed, slot_arrays, stereo_arrays, vocabulary_arrays)
+
 PEAK_HBM_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # Non-packed 32-bit VALU: 256 CU x 4 SIMD x 16 lanes per cycle x 2.4 GHz = 39.3 T lane-op/s.  Measured
 # on the box (tools/micro/valu_rate.hip, profiles/r02_valu_rate.txt): v_xor_b32, v_bcnt_u32_b32,
@@ -74,6 +77,11 @@ def parse():
     ap.add_argument("--no-frames", action="store_true", help="skip the frame-batched C3 / C5 workloads")
     ap.add_argument("--frames", type=int, default=1024, help="frames per launch (C3 / C5 batches)")
     ap.add_argument("--frame-reps", type=int, default=5)
+    ap.add_argument("--no-wall", action="store_true", help="skip the C++ adapter wall-rate runs")
+    ap.add_argument("--wall-frames", type=int, default=256, help="frames per batched adapter call (C++ wall bench)")
+    ap.add_argument("--wall-reps", type=int, default=8, help="timed repetitions per host thread (C++ wall bench)")
+    ap.add_argument("--wall-threads", type=int, default=8,
+                    help="host threads of the C++ wall bench, each with its own context (Tracking threads)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-launch HBM traffic from the rocprofv3 PMC passes (tools/gpu_profile_r03.sh)")
     ap.add_argument("--valu-pmc", default=os.path.join(ROOT, "profiles", "r03_top2_valu_pmc.json"),
@@ -99,6 +107,7 @@ def _spawn_ranks(n):
 
 def main():
     args = parse()
+    t_start = time.perf_counter()
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
         sys.exit(_spawn_ranks(args.gpus))
@@ -296,20 +305,25 @@ def main():
         out["speedup_vs_cpu_node_estimate"] = round(value / cb["node_estimate"]["value"], 2)
 
     # ---- frame-batched C3 / C5: matching + PoseOptimization, B frames per launch ------------
+    def stage(key, fn):
+        if rank == 0:  # progress on stderr: a long run shows it is alive
+            print(f"[bench] {key} ({time.perf_counter() - t_start:.0f} s)", file=sys.stderr, flush=True)
+        out[key] = fn(ctx, rank, world, dist, dev, args)
+
     if not args.no_frames:
-        out["frames_c3"] = bench_c3(ctx, rank, world, dist, dev, args)
-        out["frames_c5"] = bench_c5(ctx, rank, world, dist, dev, args)
-        out["frames_dbow"] = bench_dbow(ctx, rank, world, dist, dev, args)
-        out["frames_stereo"] = bench_stereo(ctx, rank, world, dist, dev, args)
-        out["frames_orb"] = bench_orb(ctx, rank, world, dist, dev, args)
-        out["frames_orb_detect"] = bench_orb_detect(ctx, rank, world, dist, dev, args)
-        out["frames_orb_extract"] = bench_orb_extract(ctx, rank, world, dist, dev, args)
+        stage("frames_c3", bench_c3)
+        stage("frames_c5", bench_c5)
+        stage("frames_dbow", bench_dbow)
+        stage("frames_stereo", bench_stereo)
+        stage("frames_orb", bench_orb)
+        stage("frames_orb_detect", bench_orb_detect)
+        stage("frames_orb_extract", bench_orb_extract)
 
     # ---- LocalBA iters/s on C4 (50 KF x 10k points), the second half of the metric ----------
     if not args.no_ba:
-        out["local_ba"] = bench_lba(ctx, rank, world, dist, dev, args)
+        stage("local_ba", bench_lba)
     if not args.no_gba:
-        out["global_ba"] = bench_gba(ctx, rank, world, dist, dev, args)
+        stage("global_ba", bench_gba)
 
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -664,6 +678,50 @@ def _frame_batches(ctx, rank, world, dist, dev, args, steps, cpu_worker, label, 
     return res
 
 
+def _cpp_wall(res, workload, arrays, expect, args, rank, world):
+    """The drop-in's wall rate as ORB-SLAM3 would see it: tools/adapter_wall_bench (C++) gathers mock
+    Frames / KeyFrames / MapPoints through adapters/orbslam3/osg_orbslam3.h's batched entries, calls the
+    C-ABI with host inputs and writes the results back into the objects, on --wall-threads host
+    threads with one context each.  `arrays` is the problem pool (tools/adapter_arrays.py);
+    `expect` maps each recorded per-frame result to the kernel-only path's values on the same pool,
+    and `equals_kernel_path` says whether the adapter run reproduced them.  Rank 0 at N = 1 only."""
+    if args.no_wall or rank != 0 or world != 1:
+        return
+    import subprocess
+    import tempfile
+    from tools.adapter_arrays import write_arrays
+    exe = os.path.join(ROOT, "tools", "adapter_wall_bench")
+    if not os.path.exists(exe):
+        res["wall_cpp_adapter"] = {"error": "tools/adapter_wall_bench is not built (make)"}
+        return
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "pool.arrays")
+        write_arrays(path, arrays)
+        r = subprocess.run([exe, workload, path, str(args.wall_frames), str(args.wall_reps), str(args.wall_threads)],
+                           capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        res["wall_cpp_adapter"] = {"error": (r.stdout + r.stderr)[-600:]}
+        return
+    w = json.loads(r.stdout.strip().splitlines()[-1])
+    n = min(args.wall_frames, w["distinct_problems"])
+    first = w.pop("first_rep")
+    bad = {}
+    for k, v in expect.items():
+        got, want = [int(x) for x in first[k]], [int(x) for x in v[:n]]
+        if got != want:
+            i = next((j for j in range(min(len(got), len(want))) if got[j] != want[j]), min(len(got), len(want)))
+            bad[k] = {"first_index": i, "adapter": got[i:i + 4], "kernel_path": want[i:i + 4]}
+    w["equals_kernel_path"] = not bad
+    if bad:
+        w["mismatch"] = bad
+    w["note"] = ("tools/adapter_wall_bench.cpp: gather from mock ORB-SLAM3 objects, C-ABI call with host inputs "
+                 "(pack, PCIe, kernels, download), write-back; frames / wall second over all host threads")
+    res["wall_cpp_adapter_frames_per_s"] = w["frames_per_s"]
+    res["wall_cpp_adapter"] = w
+    if "cpu_baseline" in res:
+        res["wall_cpp_adapter_speedup_vs_cpu"] = round(w["frames_per_s"] / res["cpu_baseline"]["value"], 2)
+
+
 def _attach_cpu(res, worker, units, unit, seconds, label, wall_key="wall_frames_per_s_incl_host_and_pcie"):
     """res["cpu_baseline"] (N threads, one problem per thread) and the speedups: kernel-time value and,
     when recorded, the host- and PCIe-inclusive wall rate, each against the N-thread and 1-thread CPU."""
@@ -685,9 +743,13 @@ def bench_c3(ctx, rank, world, dist, dev, args):
     n_pool = 32
     rng = np.random.default_rng(0x0B5EED03 + rank)
     pairs = [fr.synth_bow_pair(rng, n_kf=1200, n_f=1200, n_nodes=100) for _ in range(n_pool)]
+    for pair in pairs:  # a MapPoint-less keypoint has no goodness flag (the mock KeyFrame holds NULL there)
+        for S in pair:
+            S.mp_good = (S.mp_good.astype(bool) & (S.mp_id >= 0)).astype(np.uint8)
     m = ORBmatcher(ctx, 0.7, True)
     nm, _ = m.SearchByBoWBatch([p[0] for p in pairs], [p[1] for p in pairs])
-    probs = [op.synth_pose_problem(rng, n_edges=int(max(nm[i], 10))) for i in range(n_pool)]
+    # keypoints are float (cv::KeyPoint): the problems the adapter can gather from a Frame
+    probs = [pose_for_mock(op.synth_pose_problem(rng, n_edges=int(max(nm[i], 10)))) for i in range(n_pool)]
     B = args.frames
     KB = [pairs[i % n_pool][0] for i in range(B)]
     FB = [pairs[i % n_pool][1] for i in range(B)]
@@ -710,12 +772,20 @@ def bench_c3(ctx, rank, world, dist, dev, args):
                    lambda: lib.osg_pose_optimization(h, C.byref(ps), C.byref(rs)),
                    None if args.no_cpu else lambda: _oracle()[0].oracle_pose_optimization(C.byref(ps), C.byref(rs)))}
 
-    return _frame_batches(ctx, rank, world, dist, dev, args,
-                          [lambda: m.SearchByBoWBatch(KB, FB), lambda: opt.PoseOptimization(PB)], cpu,
-                          ["SearchByBoW", "PoseOptimization"],
-                          f"C3: SearchByBoW(KF,F) 1200x1200 (100 nodes) + PoseOptimization "
-                          f"(mean {int(np.mean(nm))} edges, 60 % stereo), {B} frames per launch", n_pool,
-                          latency=lat)
+    res = _frame_batches(ctx, rank, world, dist, dev, args,
+                         [lambda: m.SearchByBoWBatch(KB, FB), lambda: opt.PoseOptimization(PB)], cpu,
+                         ["SearchByBoW", "PoseOptimization"],
+                         f"C3: SearchByBoW(KF,F) 1200x1200 (100 nodes) + PoseOptimization "
+                         f"(mean {int(np.mean(nm))} edges, 60 % stereo), {B} frames per launch", n_pool,
+                         latency=lat)
+    arrays = {"pool.n": np.array([n_pool], np.int32)}
+    for i in range(n_pool):
+        arrays.update(prefixed(f"p{i}.", {**bow_arrays("B1.", pairs[i][0]), **bow_arrays("B2.", pairs[i][1]),
+                                          **pose_arrays(probs[i])}))
+    _cpp_wall(res, "c3", arrays, {"SearchByBoW": nm, "PoseOptimization": [r.n_inliers for r in
+                                                                          opt.PoseOptimization(probs)]},
+              args, rank, world)
+    return res
 
 
 def bench_c5(ctx, rank, world, dist, dev, args):
@@ -729,9 +799,15 @@ def bench_c5(ctx, rank, world, dist, dev, args):
     F = [fr.synth_frame_two_cam(rng, n_left=1000, n_right=1000, stereo_frac=0.5, width=512, height=512)
          for _ in range(n_pool)]
     L = [fr.synth_last_queries_two_cam(rng, f, n_last=2000) for f in F]
+    for x in L:  # only a LastFrame slot with a MapPoint can be valid (the mock Frame holds NULL elsewhere)
+        x.valid = (x.valid.astype(bool) & (x.mp_id >= 0)).astype(np.uint8)
     Q = [fr.synth_mp_queries_two_cam(rng, f, m=1500) for f in F]
+    for x in Q:  # the local map's MapPoints all have observations (Tracking::UpdateLocalPoints)
+        x.has_obs[:] = 1
     S = [fr.synth_slots(rng, f.n, frac_assigned=0.05) for f in F]
-    probs = [op.synth_pose_problem(rng, n_edges=600, cam=op.kb8_camera(), body_frac=0.4) for _ in range(n_pool)]
+    # left-camera edges first, then the right camera's, as a two-camera Frame's slots are ordered
+    probs = [pose_for_mock(op.synth_pose_problem(rng, n_edges=600, cam=op.kb8_camera(), body_frac=0.4))
+             for _ in range(n_pool)]
     B = args.frames
     idx = [i % n_pool for i in range(B)]
     FB, LB, QB, PB = [F[i] for i in idx], [L[i] for i in idx], [Q[i] for i in idx], [probs[i] for i in idx]
@@ -765,17 +841,28 @@ def bench_c5(ctx, rank, world, dist, dev, args):
                    lambda: lib.osg_pose_optimization(h, C.byref(ps), C.byref(rs)),
                    orc and (lambda: orc.oracle_pose_optimization(C.byref(ps), C.byref(rs))))}
 
-    return _frame_batches(ctx, rank, world, dist, dev, args,
-                          [lambda: m.SearchByProjectionBatch(FB, LB, 7.0, False, slot_mps=[S[i][0].copy() for i in idx],
-                                                             slot_takens=TB),
-                           lambda: m_local.SearchByProjectionBatch(FB, QB, 3.0, False, 20.0,
-                                                                   slot_mps=[S[i][0].copy() for i in idx],
-                                                                   slot_takens=TB),
-                           lambda: opt.PoseOptimization(PB)], cpu,
-                          ["SearchByProjection(F,LastF)", "SearchByProjection(F,localMPs)", "PoseOptimization"],
-                          f"C5: two-camera KB8 512x512, 2x1000 keypoints; LastF 2000 + local map 1500 queries; "
-                          f"PoseOptimization 600 edges (40 % right camera); {B} frames per launch", n_pool,
-                          latency=lat)
+    res = _frame_batches(ctx, rank, world, dist, dev, args,
+                         [lambda: m.SearchByProjectionBatch(FB, LB, 7.0, False, slot_mps=[S[i][0].copy() for i in idx],
+                                                            slot_takens=TB),
+                          lambda: m_local.SearchByProjectionBatch(FB, QB, 3.0, False, 20.0,
+                                                                  slot_mps=[S[i][0].copy() for i in idx],
+                                                                  slot_takens=TB),
+                          lambda: opt.PoseOptimization(PB)], cpu,
+                         ["SearchByProjection(F,LastF)", "SearchByProjection(F,localMPs)", "PoseOptimization"],
+                         f"C5: two-camera KB8 512x512, 2x1000 keypoints; LastF 2000 + local map 1500 queries; "
+                         f"PoseOptimization 600 edges (40 % right camera); {B} frames per launch", n_pool,
+                         latency=lat)
+    arrays = {"pool.n": np.array([n_pool], np.int32)}
+    for i in range(n_pool):
+        arrays.update(prefixed(f"p{i}.", {**frame_arrays(F[i]), **slot_arrays(*S[i]), **last_arrays(L[i]),
+                                          **mps_arrays(Q[i]), **pose_arrays(probs[i])}))
+    expect = {"SearchByProjection(F,LastF)": m.SearchByProjectionBatch(
+                  F, L, 7.0, False, slot_mps=[x[0].copy() for x in S], slot_takens=[x[1] for x in S]),
+              "SearchByProjection(F,localMPs)": m_local.SearchByProjectionBatch(
+                  F, Q, 3.0, False, 20.0, slot_mps=[x[0].copy() for x in S], slot_takens=[x[1] for x in S]),
+              "PoseOptimization": [r.n_inliers for r in opt.PoseOptimization(probs)]}
+    _cpp_wall(res, "c5", arrays, expect, args, rank, world)
+    return res
 
 
 def bench_dbow(ctx, rank, world, dist, dev, args):
@@ -800,7 +887,13 @@ def bench_dbow(ctx, rank, world, dist, dev, args):
                          f"words), 1200 descriptors per frame; {B} frames per launch", n_pool, cpu_frames=n_pool)
     gv.transform_batch(sets[:1], 4)
     res["single_frame_kernel_us"] = round(ctx.last_kernel_ms() * 1e3, 2)
+    ref = gv.transform_batch(pool, 4)
     gv.close()
+    arrays = {"pool.n": np.array([n_pool], np.int32), **vocabulary_arrays(voc)}
+    for i, d in enumerate(pool):
+        arrays[f"p{i}.D.desc"] = np.ascontiguousarray(d, np.uint8).reshape(-1)
+    _cpp_wall(res, "dbow", arrays, {"n_words": [len(r.word) for r in ref], "n_nodes": [len(r.node_id) for r in ref]},
+              args, rank, world)
     return res
 
 
@@ -824,6 +917,11 @@ def bench_stereo(ctx, rank, world, dist, dev, args):
                          f"side, pyramids in HBM; {B} frames per launch", n_pool)
     st.ComputeStereoMatchesBatch(ctx, frames[:1])
     res["single_frame_kernel_us"] = round(ctx.last_kernel_ms() * 1e3, 2)
+    _, nm = st.ComputeStereoMatchesBatch(ctx, dpool)
+    arrays = {"pool.n": np.array([n_pool], np.int32)}
+    for i, f in enumerate(pool):
+        arrays.update(prefixed(f"p{i}.", stereo_arrays(f)))
+    _cpp_wall(res, "stereo", arrays, {"ComputeStereoMatches": list(nm)}, args, rank, world)
     return res
 
 

@@ -2,7 +2,8 @@
 // arrays written by tests/test_adapter.py, and writes the adapter's results back (test-only).
 //
 //   adapter_driver MODE in.arrays out.arrays      MODE: mps last kf bow_kf_f bow_kf_kf pose lba fuse fuse_sim3 triang distinct sim3 sim3_kfs sim3pair init stereo fisheye gba merge_lba orb
-//                                                       and the batched forms bow_kf_f_batch pose_batch last_batch mps_batch stereo_batch
+//                                                       bow, and the batched forms bow_kf_f_batch pose_batch last_batch mps_batch
+//                                                       stereo_batch bow_batch
 #include <deque>
 
 #include "driver_common.h"
@@ -92,6 +93,25 @@ static void run_batch_mode(const std::string &mode, const Arrays &in, const floa
         }
         out["ur"] = make('f', ur);
         out["depth"] = make('f', depth);
+    } else if (mode == "bow_batch") {  // ComputeBoW, B frames in one launch
+        osg_vocabulary *voc = build_vocabulary(in);
+        std::deque<Frame> F(B);
+        std::vector<Frame *> fp;
+        for (int b = 0; b < B; b++) {
+            build_bow_frame(in, pre(b), F[b]);
+            fp.push_back(&F[b]);
+        }
+        oa::compute_bow_batch(fp, voc);
+        osg_vocabulary_destroy(voc);
+        std::vector<int32_t> word, nid, ns, feat, counts;
+        std::vector<double> value;
+        for (int b = 0; b < B; b++) append_bow(F[b], word, value, nid, ns, feat, counts);
+        out["word"] = make('i', word);
+        out["value"] = make('d', value);
+        out["node_id"] = make('i', nid);
+        out["node_start"] = make('i', ns);
+        out["feat"] = make('i', feat);
+        out["counts"] = make('i', counts);
     } else {
         throw std::runtime_error("unknown batch mode " + mode);
     }
@@ -479,6 +499,25 @@ int main(int argc, char **argv)
             out["nmatches"] = make('i', std::vector<int32_t>{nm});
             out["m12"] = make('i', std::vector<int32_t>(m12.begin(), m12.end()));
             out["prev"] = make('f', po);
+        } else if (mode == "bow") {  // Frame::ComputeBoW, twice: the second call keeps mBowVec (not empty)
+            osg_vocabulary *voc = build_vocabulary(in);
+            Frame F;
+            build_bow_frame(in, "", F);
+            osg_orbslam3::compute_bow(F, voc);
+            std::vector<int32_t> word, nid, ns, feat, counts;
+            std::vector<double> value;
+            append_bow(F, word, value, nid, ns, feat, counts);
+            const auto bow = F.mBowVec;
+            F.mFeatVec.clear();
+            osg_orbslam3::compute_bow(F, voc);
+            osg_vocabulary_destroy(voc);
+            out["word"] = make('i', word);
+            out["value"] = make('d', value);
+            out["node_id"] = make('i', nid);
+            out["node_start"] = make('i', ns);
+            out["feat"] = make('i', feat);
+            out["counts"] = make('i', counts);
+            out["second_call_kept"] = make('i', std::vector<int32_t>{F.mBowVec == bow && F.mFeatVec.empty() ? 1 : 0});
         } else if (mode == "stereo") {
             Frame F;
             ORBextractor el, er;

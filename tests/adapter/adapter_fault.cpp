@@ -409,6 +409,49 @@ static void run_all()
         EXPECT(out.aborted && out.poses.empty() && out.points.empty() && out.to_erase.empty(),
                "merge_local_bundle_adjustment: aborted, nothing written back");
     }
+    {  // ComputeBoW: mBowVec / mFeatVec empty (no vocabulary reachable), single and batched
+        Frame f = w.F;
+        f.mDescriptors = descriptors(NKP, 3);
+        f.mFeatVec[7] = {1, 2};
+        oa::compute_bow(f, nullptr);
+        EXPECT(f.mBowVec.empty() && f.mFeatVec.empty(), "compute_bow: mBowVec / mFeatVec empty");
+        Frame g = f;
+        g.mFeatVec[7] = {1};
+        oa::compute_bow_batch(std::vector<Frame *>{&f, &g}, nullptr);
+        EXPECT(f.mBowVec.empty() && g.mBowVec.empty() && g.mFeatVec.empty(), "compute_bow_batch: maps empty");
+    }
+    {  // the batched forms: each problem gets its single call's outcome
+        Frame f1 = w.F, f2 = w.F;
+        std::vector<std::vector<MapPoint *>> m;
+        int32_t nm[2] = {5, 5};
+        oa::search_by_bow_kf_f_batch<H>(std::vector<KeyFrame *>{&w.K1, &w.K1}, std::vector<Frame *>{&f1, &f2}, m, 0.7f,
+                                        true, nm);
+        EXPECT(nm[0] == 0 && nm[1] == 0 && m.size() == 2 && m[1] == std::vector<MapPoint *>(w.F.N, nullptr),
+               "search_by_bow_kf_f_batch: 0 each, F.N NULLs");
+        const auto before = f1.mvpMapPoints;
+        nm[0] = nm[1] = 5;
+        oa::search_by_projection_last_batch<H>(std::vector<Frame *>{&f1, &f2}, std::vector<const Frame *>{&w.F2, &w.F2},
+                                               7.f, true, true, nm);
+        EXPECT(nm[0] == 0 && nm[1] == 0 && f1.mvpMapPoints == before, "search_by_projection_last_batch: 0, slots untouched");
+        nm[0] = nm[1] = 5;
+        oa::search_by_projection_mps_batch<H>(std::vector<Frame *>{&f1, &f2},
+                                              std::vector<const std::vector<MapPoint *> *>{&w.mps, &w.mps}, 1.f, false,
+                                              20.f, 0.8f, nm);
+        EXPECT(nm[0] == 0 && nm[1] == 0 && f2.mvpMapPoints == before, "search_by_projection_mps_batch: 0, slots untouched");
+        for (int i = 0; i < 4; i++) f1.mvpMapPoints[i] = w.mps[i];
+        double pose_before[7];
+        std::memcpy(pose_before, f1.pose, sizeof pose_before);
+        nm[0] = 5;
+        oa::pose_optimization_batch<H>(std::vector<Frame *>{&f1}, nm);
+        EXPECT(nm[0] == 0 && std::memcmp(pose_before, f1.pose, sizeof pose_before) == 0,
+               "pose_optimization_batch: 0, pose untouched");
+        f2.mvuRight.assign(NKP, 3.f);
+        f2.mvDepth.assign(NKP, 3.f);
+        nm[0] = 5;
+        oa::compute_stereo_matches_batch(std::vector<Frame *>{&f2}, nm);
+        EXPECT(nm[0] == 0 && f2.mvuRight == std::vector<float>(NKP, -1.f) && f2.mvDepth == std::vector<float>(NKP, -1.f),
+               "compute_stereo_matches_batch: 0, mvuRight / mvDepth all -1");
+    }
 }
 
 int main(int argc, char **argv)

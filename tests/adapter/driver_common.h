@@ -36,15 +36,17 @@ inline Arrays read_arrays(const char *path)
         uint32_t len;
         if (fread(&len, 4, 1, f) != 1) break;
         std::string name(len, '\0');
-        fread(&name[0], 1, len, f);
         Arr a;
-        fread(&a.t, 1, 1, f);
-        uint64_t n;
-        fread(&n, 8, 1, f);
+        uint64_t n = 0;
+        bool ok = fread(&name[0], 1, len, f) == len && fread(&a.t, 1, 1, f) == 1 && fread(&n, 8, 1, f) == 1;
         a.n = n;
         const size_t es = a.t == 'b' ? 1 : a.t == 'd' ? 8 : 4;
         a.b.resize(n * es);
-        if (n) fread(a.b.data(), es, n, f);
+        if (ok && n) ok = fread(a.b.data(), es, n, f) == n;
+        if (!ok) {
+            fclose(f);
+            throw std::runtime_error(std::string("truncated array file ") + path);
+        }
         m[name] = std::move(a);
     }
     fclose(f);
@@ -420,7 +422,7 @@ inline void build_bow_kf_f_problem(const Arrays &in, const std::string &pre, Key
     F.mFeatVec = KF.mFeatVec;
 }
 
-// PoseOptimization: "P.kind/xw/obs/inv_sigma2/pose/cam" (+ "P.cam2" with right-camera edges).  One
+// PoseOptimization: "P.kind/xw/obs/inv_sigma2/pose/cam" (+ "P.cam2", "P.cam2_trl" with right-camera edges).  One
 // slot per edge, octave = slot (one information level per keypoint).  A problem with right-camera
 // (BODY) edges becomes a two-camera Frame: its other edges are the left slots, in edge order, then
 // the BODY edges are the right slots.
@@ -476,6 +478,7 @@ inline void build_pose_problem(const Arrays &in, const std::string &pre, Frame &
         const float *k2 = get(in, P + "cam2").p<float>();
         c2.type = (int)k2[0];
         c2.params.assign(k2 + 1, k2 + 9);
+        if (has(in, P + "cam2_trl")) c2.trl.assign(get(in, P + "cam2_trl").p<double>(), get(in, P + "cam2_trl").p<double>() + 7);
         F.mpCamera2 = &c2;
     }
 }
@@ -526,6 +529,57 @@ inline void build_stereo_problem(const Arrays &in, const std::string &pre, Frame
     pyr(pre + "PR.img", pre + "PR.dims", er);
     F.mpORBextractorLeft = &el;
     F.mpORBextractorRight = &er;
+}
+
+// ComputeBoW: a Frame whose mDescriptors are "D.desc" (n x 32)
+inline void build_bow_frame(const Arrays &in, const std::string &pre, Frame &F)
+{
+    const Arr &d = get(in, pre + "D.desc");
+    F.N = (int)(d.n / 32);
+    F.mDescriptors = cv::Mat(F.N, 32);
+    std::memcpy(F.mDescriptors.buf.data(), d.b.data(), d.b.size());
+}
+
+// the vocabulary "V.*" uploaded on this thread's context (the integration loads it once)
+inline osg_vocabulary *build_vocabulary(const Arrays &in)
+{
+    const int32_t *kl = get(in, "V.kl").p<int32_t>();
+    osg_vocabulary_desc v{};
+    v.k = kl[0];
+    v.L = kl[1];
+    v.scoring = kl[2];
+    v.weighting = kl[3];
+    v.n_nodes = (int32_t)get(in, "V.parent").n;
+    v.parent = get(in, "V.parent").p<int32_t>();
+    v.is_leaf = get(in, "V.is_leaf").p<uint8_t>();
+    v.desc = get(in, "V.desc").p<uint8_t>();
+    v.weight = get(in, "V.weight").p<double>();
+    osg_vocabulary *voc = nullptr;
+    osg_ctx *ctx = osg_orbslam3::thread_ctx();
+    if (!ctx || osg_vocabulary_create(ctx, &v, &voc) != OSG_OK) throw std::runtime_error("osg_vocabulary_create failed");
+    return voc;
+}
+
+// mBowVec / mFeatVec of frames appended as flat arrays (word, value, node_id, node_start per frame
+// with its own leading 0, feat) with per-frame counts
+inline void append_bow(const Frame &F, std::vector<int32_t> &word, std::vector<double> &value,
+                       std::vector<int32_t> &node_id, std::vector<int32_t> &node_start, std::vector<int32_t> &feat,
+                       std::vector<int32_t> &counts)
+{
+    for (const auto &kv : F.mBowVec) {
+        word.push_back((int32_t)kv.first);
+        value.push_back(kv.second);
+    }
+    int s = 0;
+    for (const auto &kv : F.mFeatVec) {
+        node_id.push_back((int32_t)kv.first);
+        node_start.push_back(s);
+        for (unsigned f : kv.second) feat.push_back((int32_t)f);
+        s += (int)kv.second.size();
+    }
+    node_start.push_back(s);
+    counts.push_back((int32_t)F.mBowVec.size());
+    counts.push_back((int32_t)F.mFeatVec.size());
 }
 
 #endif

@@ -52,6 +52,7 @@ struct KeyFrame;
 struct Camera {
     int type = OSG_CAM_PINHOLE;
     std::vector<float> params;
+    std::vector<double> trl;  // test-only: GetRelativePoseTrl of a right camera {qx qy qz qw tx ty tz}; empty = identity
     float getParameter(const int i) const { return params[i]; }  // GeometricCamera::getParameter
 };
 
@@ -111,6 +112,7 @@ struct MapPoint {
 
 struct ORBextractor {
     std::vector<cv::Mat> mvImagePyramid;
+    const osg_image_pyramid *mpOsgDeviceLevels = nullptr;  // the integration's device levels (osg_orb_pyramid)
     std::vector<cv::Point> pattern;  // ref:include/ORBextractor.h (512 points of bit_pattern_31_)
     std::vector<int> umax;           // HALF_PATCH_SIZE + 1 row half-widths
 };
@@ -133,6 +135,7 @@ struct Frame {
     float mb = 0, mbf = 0, fx = 0, fy = 0, cx = 0, cy = 0;
     Camera *mpCamera = nullptr, *mpCamera2 = nullptr;
     std::map<unsigned int, std::vector<unsigned int>> mFeatVec;
+    std::map<unsigned int, double> mBowVec;  // DBoW2::BowVector
     double pose[7] = {0, 0, 0, 1, 0, 0, 0};
     float tlc_z_value = 0;  // test-only: MockHooks::tlc_z
     // two-camera (KannalaBrandt8) Frame members of ComputeStereoFishEyeMatches (ref:include/Frame.h)
@@ -153,6 +156,7 @@ struct KeyFrame {
     std::vector<float> mvuRight, mvInvLevelSigma2;
     std::vector<MapPoint *> mvpMapPoints;
     std::map<unsigned int, std::vector<unsigned int>> mFeatVec;
+    std::map<unsigned int, double> mBowVec;  // DBoW2::BowVector
     float mbf = 0, mb = 0, fx = 0, fy = 0, cx = 0, cy = 0;
     Camera *mpCamera = nullptr, *mpCamera2 = nullptr;
     double pose[7] = {0, 0, 0, 1, 0, 0, 0};
@@ -276,6 +280,8 @@ struct MockHooks {
         c.cy = o.cy;
         c.bf = o.mbf;
         c.trl[3] = 1.0;
+        if (right && cam && cam->trl.size() == 7)
+            for (int i = 0; i < 7; i++) c.trl[i] = cam->trl[i];
     }
     static bool project_last(const Frame &, MapPoint *p, float &u, float &v, float &invz)
     {

@@ -17,61 +17,12 @@ from orb_slam3_comments_ghr_amd import _abi
 from orb_slam3_comments_ghr_amd import frames as fr
 from orb_slam3_comments_ghr_amd import optimizer as op
 from tests import oracle_calls as oc
+from tools.adapter_arrays import (bow_arrays, cam_array, frame_arrays, pose_arrays, pose_for_mock, prefixed as _prefixed,
+                                  read_arrays, stereo_arrays, write_arrays)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DRIVER_SRC = os.path.join(ROOT, "tests", "adapter", "adapter_driver.cpp")
 PKG = os.path.join(ROOT, "orb_slam3_comments_ghr_amd")
-_CODES = {np.dtype(np.uint8): b"b", np.dtype(np.int8): b"b", np.dtype(np.int32): b"i", np.dtype(np.uint32): b"i",
-          np.dtype(np.float32): b"f", np.dtype(np.float64): b"d"}
-_DTYPES = {b"b": np.uint8, b"i": np.int32, b"f": np.float32, b"d": np.float64}
-
-
-def write_arrays(path, arrays):
-    with open(path, "wb") as f:
-        for name, a in arrays.items():
-            a = np.ascontiguousarray(a)
-            code = _CODES[a.dtype]
-            nb = name.encode()
-            f.write(np.uint32(len(nb)).tobytes() + nb + code + np.uint64(a.size).tobytes() + a.tobytes())
-
-
-def read_arrays(path):
-    out = {}
-    with open(path, "rb") as f:
-        data = f.read()
-    o = 0
-    while o < len(data):
-        n = int(np.frombuffer(data, np.uint32, 1, o)[0]); o += 4
-        name = data[o:o + n].decode(); o += n
-        code = data[o:o + 1]; o += 1
-        cnt = int(np.frombuffer(data, np.uint64, 1, o)[0]); o += 8
-        dt = np.dtype(_DTYPES[code])
-        out[name] = np.frombuffer(data, dt, cnt, o).copy(); o += cnt * dt.itemsize
-    return out
-
-
-def frame_arrays(F):
-    d = {"F.kp_x": F.kp_x, "F.kp_y": F.kp_y, "F.kp_angle": F.kp_angle, "F.kp_octave": F.kp_octave,
-         "F.desc": F.desc.reshape(-1), "F.u_right": (F.u_right if F.u_right is not None
-                                                    else np.full(F.n, -1, np.float32)),
-         "F.grid_start": F.grid_start, "F.grid_idx": F.grid_idx, "F.scale": F.scale,
-         "F.scalars": np.array([F.min_x, F.max_x, F.min_y, F.max_y, F.inv_w, F.inv_h, F.mb, F.mbf],
-                               np.float32)}
-    if F.nleft != -1:
-        d.update({"F.nleft": np.array([F.nleft], np.int32), "F.r_grid_start": F.grid_start_r,
-                  "F.r_grid_idx": F.grid_idx_r, "F.left_to_right": F.left_to_right,
-                  "F.right_to_left": F.right_to_left})
-    return d
-
-
-def bow_arrays(pre, S):
-    return {pre + "desc": S.desc.reshape(-1), pre + "angle": S.angle, pre + "mp_id": S.mp_id,
-            pre + "mp_good": S.mp_good, pre + "node_id": S.node_id, pre + "node_start": S.node_start,
-            pre + "feat": S.feat, pre + "nleft": np.array([S.nleft], np.int32)}
-
-
-def cam_array(c):
-    return np.array([c.type, *[c.p[i] for i in range(8)], c.fx, c.fy, c.cx, c.cy, c.bf], np.float32)
 
 
 def test_adapter_compiles_against_mocks():
@@ -643,19 +594,6 @@ def test_adapter_search_for_initialization(driver, tmp_path, oracle):
     np.testing.assert_array_equal(out["prev"].reshape(-1, 2), p)
 
 
-def stereo_arrays(F):
-    def dims(P):
-        return np.array([[lv.shape[0], lv.shape[1]] for lv in P.levels], np.int32).reshape(-1)
-
-    def img(P):
-        return np.concatenate([np.ascontiguousarray(lv).reshape(-1) for lv in P.levels])
-
-    return {"S.x": F.x, "S.y": F.y, "S.oct": F.octave, "S.desc": F.desc.reshape(-1), "S.xr": F.xr, "S.yr": F.yr,
-            "S.oct_r": F.octave_r, "S.desc_r": F.desc_r.reshape(-1), "S.scale": F.scale, "S.inv_scale": F.inv_scale,
-            "S.mb_mbf": np.array([F.mb, F.mbf], np.float32), "PL.img": img(F.left), "PL.dims": dims(F.left),
-            "PR.img": img(F.right), "PR.dims": dims(F.right)}
-
-
 @pytest.mark.gpu
 def test_adapter_compute_stereo_fisheye_matches(driver, tmp_path, oracle):
     """Frame::ComputeStereoFishEyeMatches through the adapter: keypoints, descriptors, monoLeft / monoRight,
@@ -842,10 +780,6 @@ def test_adapter_search_by_sim3(driver, tmp_path, oracle):
 
 
 # ---------------------------------------------------------------- batched adapter forms
-def _prefixed(pre, arrays):
-    return {pre + k: v for k, v in arrays.items()}
-
-
 @pytest.mark.gpu
 def test_adapter_batch_search_by_bow_kf_f(driver, tmp_path, oracle):
     """search_by_bow_kf_f_batch: B (KeyFrame, Frame) problems gathered from mock objects, one launch;
@@ -870,21 +804,10 @@ def test_adapter_batch_pose_optimization(driver, tmp_path, ctx):
     edges become the Frame's right slots); each equals the C-ABI's single call bit for bit."""
     rng = np.random.default_rng(791)
     probs = [op.synth_pose_problem(rng, n_edges=int(rng.integers(50, 400)), stereo_frac=0.4) for _ in range(4)]
-    P5 = op.synth_pose_problem(rng, n_edges=300, cam=op.kb8_camera(), body_frac=0.4)
-    order = np.concatenate([np.nonzero(P5.kind != 2)[0], np.nonzero(P5.kind == 2)[0]])  # left slots, then right
-    for k in ("kind", "xw", "obs", "inv_sigma2"):
-        setattr(P5, k, np.ascontiguousarray(getattr(P5, k)[order]))
-    for i in range(7):  # the mock's camera hook reports mTrl as the identity (GetRelativePoseTrl)
-        P5.cam2.trl[i] = 1.0 if i == 3 else 0.0
-    probs.append(P5)
+    probs.append(op.synth_pose_problem(rng, n_edges=300, cam=op.kb8_camera(), body_frac=0.4))
     arrays = {"batch.n": np.array([len(probs)], np.int32)}
     for b, P in enumerate(probs):
-        P.obs = P.obs.astype(np.float32).astype(np.float64)
-        a = {"P.kind": P.kind.astype(np.uint8), "P.xw": P.xw.reshape(-1), "P.obs": P.obs.reshape(-1),
-             "P.inv_sigma2": P.inv_sigma2, "P.pose": P.pose, "P.cam": cam_array(P.cam)}
-        if (P.kind == 2).any():
-            a["P.cam2"] = cam_array(P.cam2)
-        arrays.update(_prefixed(f"b{b}.", a))
+        arrays.update(_prefixed(f"b{b}.", pose_arrays(pose_for_mock(P))))
     out = run(driver, tmp_path, "pose_batch", arrays)
     refs = [op.Optimizer(ctx).PoseOptimization(P) for P in probs]
     assert out["nmatches"].tolist() == [r.n_inliers for r in refs]
@@ -936,3 +859,50 @@ def test_adapter_batch_compute_stereo_matches(driver, tmp_path, oracle):
     assert out["nmatches"].tolist() == [int(r[2]) for r in refs]
     np.testing.assert_array_equal(out["ur"].view(np.int32), np.concatenate([r[0] for r in refs]).view(np.int32))
     np.testing.assert_array_equal(out["depth"].view(np.int32), np.concatenate([r[1] for r in refs]).view(np.int32))
+
+
+def _bow_ref_arrays(refs):
+    """The oracle's BowResults in the driver's flat layout (append_bow)."""
+    ns, counts = [], []
+    for r in refs:
+        ns.append(r.node_start - r.node_start[0] if len(r.node_start) else np.zeros(1, np.int32))
+        counts += [len(r.word), len(r.node_id)]
+    cat = np.concatenate
+    return {"word": cat([r.word for r in refs]), "value": cat([r.value for r in refs]),
+            "node_id": cat([r.node_id.astype(np.int32) for r in refs]), "node_start": cat(ns),
+            "feat": cat([r.feat for r in refs]), "counts": np.array(counts, np.int32)}
+
+
+@pytest.mark.gpu
+def test_adapter_compute_bow(driver, tmp_path, oracle):
+    """Frame::ComputeBoW through the adapter: mDescriptors' rows transformed on the device into
+    mBowVec / mFeatVec (levelsup 4), equal to the oracle's transform bit for bit; a second call on a
+    frame whose mBowVec is filled leaves it alone, as the reference's `if (mBowVec.empty())` does."""
+    from orb_slam3_comments_ghr_amd import vocabulary as vb
+    from tools.adapter_arrays import vocabulary_arrays
+    rng = np.random.default_rng(840)
+    voc = vb.synth_vocabulary(rng, k=10, L=5, min_children=4)
+    desc = vb.synth_features(rng, voc, n=1100)
+    out = run(driver, tmp_path, "bow", {**vocabulary_arrays(voc), "D.desc": desc.reshape(-1)})
+    ref = _bow_ref_arrays([oc.dbow(oracle, voc, desc, 4)])
+    assert len(ref["word"]) > 100 and int(out["second_call_kept"][0]) == 1
+    for k, v in ref.items():
+        np.testing.assert_array_equal(out[k], v, err_msg=k)
+
+
+@pytest.mark.gpu
+def test_adapter_batch_compute_bow(driver, tmp_path, oracle):
+    """compute_bow_batch: frames of different sizes (one empty) in one launch, each equal to the
+    oracle's transform."""
+    from orb_slam3_comments_ghr_amd import vocabulary as vb
+    from tools.adapter_arrays import vocabulary_arrays
+    rng = np.random.default_rng(841)
+    voc = vb.synth_vocabulary(rng, k=10, L=6, min_children=8, min_leaf_depth=6)
+    sets = [vb.synth_features(rng, voc, n=n) for n in (1200, 700, 0, 950)]
+    arrays = {**vocabulary_arrays(voc), "batch.n": np.array([len(sets)], np.int32)}
+    for b, d in enumerate(sets):
+        arrays[f"b{b}.D.desc"] = np.ascontiguousarray(d, np.uint8).reshape(-1)
+    out = run(driver, tmp_path, "bow_batch", arrays)
+    ref = _bow_ref_arrays(oc.dbow_batch(oracle, voc, sets, 4))
+    for k, v in ref.items():
+        np.testing.assert_array_equal(out[k], v, err_msg=k)
