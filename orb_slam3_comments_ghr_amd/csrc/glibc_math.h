@@ -32,13 +32,13 @@ namespace osgm {
 OSG_GM_HD inline int32_t f2i(float x)
 {
     int32_t i;
-    std::memcpy(&i, &x, 4);
+    __builtin_memcpy(&i, &x, 4);
     return i;
 }
 OSG_GM_HD inline float i2f(int32_t i)
 {
     float x;
-    std::memcpy(&x, &i, 4);
+    __builtin_memcpy(&x, &i, 4);
     return x;
 }
 

@@ -1277,11 +1277,8 @@ int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_
         // the inputs, the status block, the input slot state and the arguments in one copy; a retry
         // re-uploads [io | args] (it must not see the slot arrays written by the problems that fitted
         // the first time)
-        if (attempt == 0)
-            OSG_HIP_CHECK(ctx, hipMemcpyAsync(dev_in, pin, in_bytes + io_pad + args_bytes, hipMemcpyHostToDevice,
-                                              ctx->stream));
-        else
-            OSG_HIP_CHECK(ctx, hipMemcpyAsync(dev_io, pin_io, io_pad + args_bytes, hipMemcpyHostToDevice, ctx->stream));
+        if (attempt == 0) OSG_RC(osg_upload(ctx, dev_in, pin, in_bytes + io_pad + args_bytes));
+        else OSG_RC(osg_upload(ctx, dev_io, pin_io, io_pad + args_bytes));
         hipEvent_t *ev = osg_ctx_events(ctx);
         if (!ev) return osg_set_error(ctx, OSG_E_HIP, "event create failed");
         OSG_HIP_CHECK(ctx, hipEventRecord(ev[0], ctx->stream));
@@ -1307,7 +1304,7 @@ int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_
         OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
         // status, slot arrays and KF-KF results in one copy (the pinned io block is re-filled from the
         // callers' slots before a retry)
-        OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_io, dev_io, io_bytes, hipMemcpyDeviceToHost, ctx->stream));
+        OSG_RC(osg_download(ctx, pin_io, dev_io, io_bytes));
         OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
         std::memcpy(st.data(), pin_io, status_bytes);
         bool overflow = false;

@@ -50,6 +50,13 @@ hipEvent_t *osg_ctx_events(osg_ctx *ctx);
 // device buffer of at least `bytes` for `slot` (grows, never shrinks)
 void *osg_scratch(osg_ctx *ctx, int slot, size_t bytes);
 void *osg_pinned(osg_ctx *ctx, size_t bytes);
+// Host <-> device copies between a device buffer and the context's pinned staging buffer
+// (osg_pinned), enqueued on ctx->stream.  Up to OSG_KCOPY_MAX bytes they run as a copy kernel in the
+// stream's own compute queue, the GPU reading / writing the pinned pages over PCIe; larger ones, and
+// host pointers outside the staging buffer, go to hipMemcpyAsync (the copy engines).
+#define OSG_KCOPY_MAX (size_t(4) << 20)
+int osg_upload(osg_ctx *ctx, void *dst_dev, const void *src_pinned, size_t bytes);
+int osg_download(osg_ctx *ctx, void *dst_pinned, const void *src_dev, size_t bytes);
 
 #define OSG_HIP_CHECK(ctx, expr)                                                             \
     do {                                                                                     \
@@ -57,6 +64,13 @@ void *osg_pinned(osg_ctx *ctx, size_t bytes);
         if (_e != hipSuccess)                                                                \
             return osg_set_error((ctx), OSG_E_HIP, "%s failed: %s (%s:%d)", #expr,          \
                                  hipGetErrorString(_e), __FILE__, __LINE__);                 \
+    } while (0)
+
+// propagate a negative OSG_E_* code
+#define OSG_RC(expr)                                                                         \
+    do {                                                                                     \
+        const int _rc = (expr);                                                              \
+        if (_rc < 0) return _rc;                                                             \
     } while (0)
 
 #define OSG_REQUIRE(ctx, cond, ...)                                                          \

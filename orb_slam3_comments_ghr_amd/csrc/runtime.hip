@@ -1,4 +1,5 @@
 // runtime.hip — context lifecycle, scratch pool, errors (C ABI: include/osg.h "context").
+#include <algorithm>
 #include <cstdarg>
 #include <cstring>
 
@@ -60,6 +61,63 @@ void *osg_pinned(osg_ctx *ctx, size_t bytes)
     ctx->host_pinned = p;
     ctx->host_pinned_cap = cap;
     return p;
+}
+
+// Why a kernel for small transfers: an SDMA copy on the stream makes the next kernel wait for the
+// copy engine's completion signal; rocprofv3 --hip-trace of a one-frame SearchByBoW showed the first
+// kernel starting 12 us after its upload had finished, and the download, a blit kernel the runtime
+// inserts for pinned destinations, starting 6 us after the last kernel.  A copy kernel is ordered like
+// any other launch in the queue.  16 bytes per thread per step; the pinned and scratch buffers are
+// 256-byte aligned and callers pass aligned offsets, so only the byte tail is moved singly.
+namespace {
+__global__ __launch_bounds__(256) void k_copy(uint4 *__restrict__ dst, const uint4 *__restrict__ src, size_t n16,
+                                              unsigned char *__restrict__ dtail,
+                                              const unsigned char *__restrict__ stail, int ntail)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) dst[i] = src[i];
+    if (blockIdx.x == 0 && (int)threadIdx.x < ntail) dtail[threadIdx.x] = stail[threadIdx.x];
+}
+
+bool in_pinned(const osg_ctx *ctx, const void *p, size_t bytes)
+{
+    const char *b = (const char *)ctx->host_pinned, *q = (const char *)p;
+    return b && q >= b && q + bytes <= b + ctx->host_pinned_cap;
+}
+
+int kcopy(osg_ctx *ctx, void *dst, const void *src, size_t bytes)
+{
+    const size_t n16 = ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0) ? bytes / 16 : 0;
+    const int ntail = (int)(bytes - 16 * n16);
+    if (ntail > 256) return -1;  // misaligned: the caller falls back to the copy engine
+    const int blocks = (int)std::min<size_t>(std::max<size_t>((n16 + 255) / 256, 1), 1024);
+    hipLaunchKernelGGL(k_copy, dim3(blocks), dim3(256), 0, ctx->stream, (uint4 *)dst, (const uint4 *)src, n16,
+                       (unsigned char *)dst + 16 * n16, (const unsigned char *)src + 16 * n16, ntail);
+    OSG_HIP_CHECK(ctx, hipGetLastError());
+    return OSG_OK;
+}
+}  // namespace
+
+int osg_upload(osg_ctx *ctx, void *dst_dev, const void *src_pinned, size_t bytes)
+{
+    if (bytes == 0) return OSG_OK;
+    if (bytes <= OSG_KCOPY_MAX && in_pinned(ctx, src_pinned, bytes)) {
+        const int rc = kcopy(ctx, dst_dev, src_pinned, bytes);
+        if (rc != -1) return rc;
+    }
+    OSG_HIP_CHECK(ctx, hipMemcpyAsync(dst_dev, src_pinned, bytes, hipMemcpyHostToDevice, ctx->stream));
+    return OSG_OK;
+}
+
+int osg_download(osg_ctx *ctx, void *dst_pinned, const void *src_dev, size_t bytes)
+{
+    if (bytes == 0) return OSG_OK;
+    if (bytes <= OSG_KCOPY_MAX && in_pinned(ctx, dst_pinned, bytes)) {
+        const int rc = kcopy(ctx, dst_pinned, src_dev, bytes);
+        if (rc != -1) return rc;
+    }
+    OSG_HIP_CHECK(ctx, hipMemcpyAsync(dst_pinned, src_dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    return OSG_OK;
 }
 
 extern "C" {

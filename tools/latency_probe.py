@@ -29,6 +29,9 @@ def med(f, n=50):
 def main():
     import torch
     torch.cuda.init()
+    import orb_slam3_comments_ghr_amd as pkg
+    if os.environ.get("OSG_PROBE_LIB"):  # a profiling build (make POSE_PROF=1 into another directory)
+        pkg.LIB_PATH = os.environ["OSG_PROBE_LIB"]
     from orb_slam3_comments_ghr_amd import Context, frames as fr, optimizer as op, _abi
     ctx = Context(0)
     lib, h = ctx.lib, ctx.handle
@@ -84,18 +87,26 @@ def main():
         r = _abi.OsgPoseResult()
         ob = np.zeros(P.n, np.uint8)
         r.outlier = ob.ctypes.data
-        w = med(lambda: lib.osg_pose_optimization(h, C.byref(ps), C.byref(r)))
-        d = {"wall_us": round(w, 1), "kernel_us": round(ctx.last_kernel_ms() * 1e3, 1),
-             "iters": r.lm_iterations, "trials": r.lm_trials}
-        if hasattr(lib, "osg_debug_pose_prof"):
-            f_ = lib.osg_debug_pose_prof
-            f_.argtypes = [C.c_void_p, C.c_int]
-            buf = np.zeros((64, 8), np.uint64)
-            f_(buf.ctypes.data, 1)
-            lib.osg_pose_optimization(h, C.byref(ps), C.byref(r))
-            f_(buf.ctypes.data, 1)
-            d["cycles"] = {k: int(buf[0, i]) for i, k in enumerate(["hpass", "solve", "oplus", "chipass", "class",
-                                                                   "total", "s6", "s7"])}
+        d = {}
+        for var in ["4", None]:  # k_pose_opt with 4 waves, then the default (k_pose_lat for one frame)
+            if var is None:
+                os.environ.pop("OSG_POSE_NW", None)
+            else:
+                os.environ["OSG_POSE_NW"] = var
+            w = med(lambda: lib.osg_pose_optimization(h, C.byref(ps), C.byref(r)))
+            d[f"nw_{var or 'auto'}"] = {"wall_us": round(w, 1), "kernel_us": round(ctx.last_kernel_ms() * 1e3, 1),
+                                         "iters": r.lm_iterations, "trials": r.lm_trials,
+                                         "pose": [float(x) for x in r.pose], "n_inliers": r.n_inliers}
+            if hasattr(lib, "osg_debug_pose_prof"):
+                f_ = lib.osg_debug_pose_prof
+                f_.argtypes = [C.c_void_p, C.c_int]
+                buf = np.zeros((64, 8), np.uint64)
+                f_(buf.ctypes.data, 1)
+                lib.osg_pose_optimization(h, C.byref(ps), C.byref(r))
+                f_(buf.ctypes.data, 1)
+                d[f"nw_{var or 'auto'}"]["cycles"] = {k: int(buf[0, i]) for i, k in enumerate(
+                    ["hpass", "solve", "oplus", "chipass", "class", "total", "pass_compute", "pass_sum"])}
+        os.environ.pop("OSG_POSE_NW", None)
         print(json.dumps({f"pose_{n_edges}": d}), flush=True)
     ctx.close()
 
