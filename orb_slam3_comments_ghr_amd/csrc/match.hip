@@ -605,6 +605,95 @@ __global__ __launch_bounds__(BFG *BOW_G) void k_bow_round(const MatchArgs *__res
     }
 }
 
+__device__ __forceinline__ QRes load_res(const MatchArgs &A, int q)
+{
+    return QRes{A.q_res[2 * q], A.q_res[2 * q + 1]};
+}
+__device__ __forceinline__ void store_res(const MatchArgs &A, int q, QRes r)
+{
+    A.q_res[2 * q] = r.l;
+    A.q_res[2 * q + 1] = r.r;
+}
+
+// SearchByProjection's (a5 / a6 / a7) search windows, candidate counts, candidate fill and first
+// evaluation spread over the chip, for launches of a few problems (the drop-in's one-frame call):
+// one thread per query, grid (ceil(max nq / GQ), problems), and one workgroup per problem for the
+// exclusive scan between them.  k_match then starts its Jacobi rounds from these results
+// (prefilled), so a lone frame no longer walks its queries' grids on one CU.  The enumeration and
+// the evaluation are k_match's own functions on the frame's global arrays (GridView<0>), so the
+// candidate lists and the first results are the ones k_match forms itself.
+constexpr int GQ = 128;
+constexpr int GRID_PREPASS_MAX_B = 64;  // launches of up to this many problems take the prepass
+template <int MODE>
+__device__ __forceinline__ bool taken_init(const MatchArgs &A, int s)
+{
+    if (MODE == MODE_MPS || MODE == MODE_LAST) return A.slot_mp[s] >= 0 && A.slot_taken[s];
+    return A.slot_mp[s] >= 0;  // MODE_KF
+}
+template <int MODE>
+__global__ __launch_bounds__(GQ) void k_grid_count(const MatchArgs *__restrict__ args)
+{
+    const MatchArgs &A = args[blockIdx.y];
+    const int q = blockIdx.x * GQ + threadIdx.x;
+    if (q >= A.nq) return;
+    const Win wl = query_window<MODE>(A, q);
+    store_win(A.q_win + 4 * (size_t)q, wl);
+    if ((MODE == MODE_MPS || MODE == MODE_LAST) && A.nleft >= 0)
+        store_win(A.q_win + 4 * (size_t)q + 2, query_window_r<MODE>(A, q, wl));
+    const GridView<0> GL{A.grid_start, A.grid_idx, 0, nullptr, nullptr, nullptr, nullptr, A.fdesc};
+    const GridView<0> GR{A.grid_start_r, A.grid_idx_r, A.nleft, nullptr, nullptr, nullptr, nullptr, A.fdesc};
+    int cl;
+    A.q_off[q] = enum_query<MODE, false, 0>(A, GL, GR, q, nullptr, cl);  // the count, for k_grid_scan
+}
+template <int MODE>
+__global__ __launch_bounds__(MT) void k_grid_scan(const MatchArgs *__restrict__ args)
+{
+    const MatchArgs &A = args[blockIdx.x];
+    __shared__ int s_scan[MT];
+    const int nq = A.nq, tid = threadIdx.x;
+    const int per = (nq + MT - 1) / MT;
+    const int q0 = min(nq, tid * per), q1 = min(nq, q0 + per);
+    int my = 0;
+    for (int q = q0; q < q1; q++) my += A.q_off[q];
+    s_scan[tid] = my;
+    __syncthreads();
+    for (int o = 1; o < MT; o <<= 1) {
+        const int v = tid >= o ? s_scan[tid - o] : 0;
+        __syncthreads();
+        s_scan[tid] += v;
+        __syncthreads();
+    }
+    int off = s_scan[tid] - my;
+    for (int q = q0; q < q1; q++) {
+        const int c = A.q_off[q];
+        A.q_off[q] = off;
+        off += c;
+    }
+    if (tid == 0) {
+        const int total = s_scan[MT - 1];
+        A.q_off[nq] = total;
+        if (total > A.cap) {  // the host resizes and retries; k_grid_fill and k_match skip the problem
+            A.status[0] = total;
+            A.status[3] = 1;
+        }
+    }
+}
+template <int MODE>
+__global__ __launch_bounds__(GQ) void k_grid_fill(const MatchArgs *__restrict__ args)
+{
+    const MatchArgs &A = args[blockIdx.y];
+    const int q = blockIdx.x * GQ + threadIdx.x;
+    if (q >= A.nq || A.q_off[A.nq] > A.cap) return;
+    const GridView<0> GL{A.grid_start, A.grid_idx, 0, nullptr, nullptr, nullptr, nullptr, A.fdesc};
+    const GridView<0> GR{A.grid_start_r, A.grid_idx_r, A.nleft, nullptr, nullptr, nullptr, nullptr, A.fdesc};
+    const int off = A.q_off[q];
+    int cl;
+    enum_query<MODE, true, 0>(A, GL, GR, q, A.cands + off, cl);
+    A.q_mid[q] = off + cl;
+    // the first evaluation: blocked(s) = the slot's state before the call (k_match's taken0)
+    store_res(A, q, eval_query<MODE>(A, q, [&](int s) { return taken_init<MODE>(A, s); }));
+}
+
 // Every slot q writes: the direct matches and, for a5 on a two-camera rig, each one's stereo
 // partner (ref:src/ORBmatcher.cc:154-163, 226-236).  Returns the count (<= 4).
 template <int MODE>
@@ -671,16 +760,6 @@ __device__ __forceinline__ QRes eval_mps_lds(const MatchArgs &A, const SerialLds
     return res;
 }
 
-__device__ __forceinline__ QRes load_res(const MatchArgs &A, int q)
-{
-    return QRes{A.q_res[2 * q], A.q_res[2 * q + 1]};
-}
-__device__ __forceinline__ void store_res(const MatchArgs &A, int q, QRes r)
-{
-    A.q_res[2 * q] = r.l;
-    A.q_res[2 * q + 1] = r.r;
-}
-
 __device__ __forceinline__ int rot_bin(float a, float b)
 {  // ref:src/ORBmatcher.cc:411-418, factor = 1.0f/HISTO_LENGTH (kept upstream bug)
     const float factor = 1.0f / OSG_HISTO_LENGTH;
@@ -731,9 +810,12 @@ __global__ __launch_bounds__(MT) void k_match(const MatchArgs *__restrict__ args
     uint64_t tclk[9];
     tclk[0] = __builtin_amdgcn_s_memtime();
 
+    // prefilled: SearchByBoW's k_bow_* or a grid mode's k_grid_* kernels formed the candidate CSR,
+    // the candidate lists and the first results (BoW: also the first Jacobi round)
+    const bool pre = A.prefilled != 0;
     // ---- 0. grid views; a staged launch copies the grids into LDS as records in grid order
     GridView<STAGE> GL{}, GR{};
-    if (!BOW) {
+    if (!BOW && !pre) {
         if constexpr (STAGED) {
             const bool two = A.nleft >= 0;
             int *gsL = (int *)(removedS + ((NS + 15) & ~15));
@@ -802,9 +884,12 @@ __global__ __launch_bounds__(MT) void k_match(const MatchArgs *__restrict__ args
         __syncthreads();
     }
 
+    else {
+        tclk[1] = tclk[0];
+    }
     tclk[2] = __builtin_amdgcn_s_memtime();
-    const bool pre = BOW && A.prefilled;
     int total = pre ? A.q_off[nq] : 0;
+    if (pre && total > A.cap) return;  // k_grid_scan flagged the overflow; the host retries
     if (!pre) {
     // ---- 1. count
     int my = 0;
@@ -880,7 +965,7 @@ __global__ __launch_bounds__(MT) void k_match(const MatchArgs *__restrict__ args
                 const QRes r = eval_bow_group<MODE>(A, q, lane, [&](int s) { return taken0[s] != 0; });
                 if (lane == 0) store_res(A, q, r);
             }
-    } else {
+    } else if (!pre) {
         for (int q = q0; q < q1; q++)
             store_res(A, q, eval_query<MODE>(A, q, [&](int s) { return taken0[s] != 0; }));
     }
@@ -888,10 +973,10 @@ __global__ __launch_bounds__(MT) void k_match(const MatchArgs *__restrict__ args
     // Jacobi rounds.  A slot is blocked for q when it was blocked initially or a query p < q
     // whose MapPoint has observations wrote it (SearchByBoW / a7: any earlier write).
     tclk[6] = __builtin_amdgcn_s_memtime();
-    int rounds = pre ? 1 : 0;
+    int rounds = (BOW && pre) ? 1 : 0;
     int *cur = claimB, *other = claimA;
-    // (the first round ran over the chip; its results are final when it changed nothing)
-    if (!(pre && A.status[13] == 0))
+    // (SearchByBoW's first round ran over the chip; its results are final when it changed nothing)
+    if (!(BOW && pre && A.status[13] == 0))
     for (;;) {
         rounds++;
         for (int q = q0; q < q1; q++) {
@@ -1234,10 +1319,15 @@ int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_
     OSG_ALLOC(ctx, dev_in, SLOT_TMP0, in_bytes + io_pad + args_bytes + 256);
     char *dev_io = dev_in + in_bytes;
     MatchArgs *dev_args = (MatchArgs *)(dev_io + io_pad);
+    // grid modes: the k_grid_* prepass for launches of a few problems (OSG_MATCH_PREPASS=0 / 1 pins it)
+    const char *pe = getenv("OSG_MATCH_PREPASS");  // read per call: tests switch it
+    const int prepass_env = pe ? atoi(pe) : -1;
+    const bool grid_pre = !BOW && (prepass_env >= 0 ? prepass_env != 0 : B <= GRID_PREPASS_MAX_B);
     for (int b = 0; b < B; b++) {
         MatchArgs &A = P[b].A;
         OSG_RELOCATE_ALL(A, dev_in);
-        if (A.prefilled) relocate(A.q_off, dev_in);
+        if (BOW && A.prefilled) relocate(A.q_off, dev_in);  // the host CSR (packed input)
+        if (grid_pre) A.prefilled = 1;
         A.status = (GLOBAL int32_t *)dev_io + STATUS_INTS * b;
         A.slot_mp = (GLOBAL int32_t *)(dev_io + status_bytes) + slot_off[b];
         A.out_q = (GLOBAL int32_t *)(dev_io + io_in_bytes) + q_base[b];
@@ -1245,7 +1335,8 @@ int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_
     for (int b = 0; b < B; b++) P[b].A.lds_free = (int)(lds - match_lds_bytes(P[b].A.n_slots));
     std::vector<size_t> cap(B), cand_off(B + 1);
     for (int b = 0; b < B; b++)
-        cap[b] = P[b].A.prefilled ? (size_t)std::max(P[b].q_off.back(), 1) : std::max<size_t>((size_t)P[b].A.nq * 32, 1024);
+        cap[b] = (BOW && P[b].A.prefilled) ? (size_t)std::max(P[b].q_off.back(), 1)
+                                            : std::max<size_t>((size_t)P[b].A.nq * 32, 1024);
     std::vector<int32_t> st((size_t)STATUS_INTS * B);
     for (int attempt = 0; attempt < 2; attempt++) {
         cand_off[0] = 0;
@@ -1264,7 +1355,7 @@ int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_
         if (BOW) OSG_ALLOC(ctx, claim_g, SLOT_TMP9, sizeof(int32_t) * (n_slot_total + 1));
         for (int b = 0; b < B; b++) {
             MatchArgs &A = P[b].A;
-            if (!A.prefilled) A.q_off = (GLOBAL int32_t *)(q_off + q_base[b]);
+            if (!(BOW && A.prefilled)) A.q_off = (GLOBAL int32_t *)(q_off + q_base[b]);
             A.q_mid = (GLOBAL int32_t *)(q_mid + q_base[b]);
             A.q_win = q_win ? (GLOBAL f32x4 *)(q_win + 4 * q_base[b]) : nullptr;
             A.q_res = (GLOBAL int32_t *)(q_res + 2 * q_base[b]);
@@ -1291,6 +1382,17 @@ int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_
                 hipLaunchKernelGGL((k_bow_claims<MODE>), dim3((max_nq + 255) / 256, B), dim3(256), 0, ctx->stream,
                                    dev_args);
                 hipLaunchKernelGGL((k_bow_round<MODE>), dim3((max_nq + BFG - 1) / BFG, B), dim3(BFG * BOW_G), 0, ctx->stream,
+                                   dev_args);
+            }
+        }
+        if (grid_pre) {
+            int max_nq = 0;
+            for (int b = 0; b < B; b++) max_nq = std::max(max_nq, P[b].A.nq);
+            if (max_nq > 0) {
+                hipLaunchKernelGGL((k_grid_count<MODE>), dim3((max_nq + GQ - 1) / GQ, B), dim3(GQ), 0, ctx->stream,
+                                   dev_args);
+                hipLaunchKernelGGL((k_grid_scan<MODE>), dim3(B), dim3(MT), 0, ctx->stream, dev_args);
+                hipLaunchKernelGGL((k_grid_fill<MODE>), dim3((max_nq + GQ - 1) / GQ, B), dim3(GQ), 0, ctx->stream,
                                    dev_args);
             }
         }

@@ -43,6 +43,24 @@ def test_search_by_projection_last(ctx, oracle, seed, th, mono, tlc):
         assert_same(f"last ori={ori}", n, s, *ref)
 
 
+@pytest.mark.parametrize("prepass", ["0", "1"])
+def test_candidate_overflow_retry(ctx, oracle, monkeypatch, prepass):
+    """More than 32 candidates per query (the first candidate-buffer guess): the launch reports the
+    overflow and the host retries with the exact size, with and without the prepass."""
+    monkeypatch.setenv("OSG_MATCH_PREPASS", prepass)
+    rng = np.random.default_rng(79)
+    F = fr.synth_frame(rng, n=3000, stereo=False)
+    Q = fr.synth_mp_queries(rng, F, m=300)
+    Q.in_view[:] = 1
+    Q.usable[:] = 1
+    slot_mp, taken = fr.synth_slots(rng, F.n)
+    ref = oc.mps(oracle, F, Q, 0.9, 40.0, False, 50.0, slot_mp, taken)
+    s = slot_mp.copy()
+    n = ORBmatcher(ctx, 0.9).SearchByProjection(F, Q, 40.0, slot_mp=s, slot_taken=taken)
+    assert ctx.match_last_stats()["candidates"] > 32 * 300
+    assert_same("overflow", n, s, *ref)
+
+
 @pytest.mark.parametrize("seed", range(6))
 @pytest.mark.parametrize("th,orb", [(10.0, 100), (3.0, 64)])
 def test_search_by_projection_kf(ctx, oracle, seed, th, orb):
@@ -79,9 +97,12 @@ def test_search_by_bow_kf_kf(ctx, oracle, seed, nn):
         assert_same(f"bow kf-kf ori={ori}", n, out, *ref)
 
 
-def test_dense_conflicts_many_rounds(ctx, oracle):
+@pytest.mark.parametrize("prepass", ["0", "1"])
+def test_dense_conflicts_many_rounds(ctx, oracle, monkeypatch, prepass):
     """Adversarial greedy: many map points project onto the same few keypoints with nearly equal
-    descriptors, forcing long claim chains in the fixed-point resolve."""
+    descriptors, forcing long claim chains in the fixed-point resolve.  With and without the
+    multi-workgroup prepass (k_grid_*)."""
+    monkeypatch.setenv("OSG_MATCH_PREPASS", prepass)
     rng = np.random.default_rng(77)
     F = fr.synth_frame(rng, n=400, stereo=False)
     Q = fr.synth_mp_queries(rng, F, m=4000, noise_px=0.5, match_frac=1.0)
@@ -131,9 +152,12 @@ def test_search_by_projection_mps_two_cam(ctx, oracle, seed, th, nn, far):
         assert not ctx.match_last_stats()["serial"]
 
 
-def test_search_by_projection_mps_two_cam_paths(ctx, oracle):
+@pytest.mark.parametrize("prepass", ["0", "1"])
+def test_search_by_projection_mps_two_cam_paths(ctx, oracle, monkeypatch, prepass):
     """Both resolve paths are exercised: all-observed (Jacobi only) and a run that must be redone
-    serially because an observation-less MapPoint's partner write unblocks a slot."""
+    serially because an observation-less MapPoint's partner write unblocks a slot; with the candidate
+    lists from k_match itself and from the k_grid_* prepass."""
+    monkeypatch.setenv("OSG_MATCH_PREPASS", prepass)
     seen = set()
     for seed in range(12):
         rng = np.random.default_rng(6100 + seed)
@@ -207,7 +231,12 @@ def test_search_by_bow_two_cam(ctx, oracle, seed, nn):
 
 # ---- batched forms: B problems in one launch equal B single calls (and the oracle)
 
-def test_batch_projection_all_overloads(ctx, oracle):
+@pytest.mark.parametrize("prepass", [None, "0", "1"])
+def test_batch_projection_all_overloads(ctx, oracle, monkeypatch, prepass):
+    """Batches of a5 / a6 / a7 problems (one- and two-camera, an empty query set): every problem
+    equals the oracle, with the k_grid_* prepass pinned on or off, and by default (on for <= 64)."""
+    if prepass is not None:
+        monkeypatch.setenv("OSG_MATCH_PREPASS", prepass)
     rng = np.random.default_rng(9000)
     B = 24
     m = ORBmatcher(ctx, 0.8, True)

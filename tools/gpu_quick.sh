@@ -10,3 +10,5 @@ timeout -k 10 400 python -u -m pytest tests/test_match_gpu.py tests/test_ba_gpu.
 rc=$?
 timeout -k 10 120 python3 tools/latency_probe.py > $OUT/probe.jsonl 2> $OUT/probe.err
 echo "pytest=$rc probe=$?"
+timeout -k 10 60 $R/tools/micro/pose_edge_cost > $OUT/pose_edge_cost.txt 2>&1
+echo "micro=$?"
