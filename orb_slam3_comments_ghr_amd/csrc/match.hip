@@ -622,28 +622,163 @@ __device__ __forceinline__ void store_res(const MatchArgs &A, int q, QRes r)
 // (prefilled), so a lone frame no longer walks its queries' grids on one CU.  The enumeration and
 // the evaluation are k_match's own functions on the frame's global arrays (GridView<0>), so the
 // candidate lists and the first results are the ones k_match forms itself.
-constexpr int GQ = 128;
 constexpr int GRID_PREPASS_MAX_B = 64;  // launches of up to this many problems take the prepass
+constexpr int GQG = 16;                   // queries per prepass workgroup (BOW_G lanes each)
 template <int MODE>
 __device__ __forceinline__ bool taken_init(const MatchArgs &A, int s)
 {
     if (MODE == MODE_MPS || MODE == MODE_LAST) return A.slot_mp[s] >= 0 && A.slot_taken[s];
     return A.slot_mp[s] >= 0;  // MODE_KF
 }
+// enum_grid<STAGE 0> with the BOW_G lanes of a group sharing one query: each column run of the
+// window is read BOW_G entries at a time, one per lane, and the passing entries keep the run's
+// order through a ballot prefix (every lane returns the count; FILL writes the candidates).
+template <bool FILL, bool RIGHT>
+__device__ __forceinline__ int enum_grid_group(const MatchArgs &A, const Win &w, const uint32_t (&qd)[8],
+                                               GLOBAL uint32_t *out, int lane)
+{
+    GLOBAL const int32_t *gs = RIGHT ? A.grid_start_r : A.grid_start;
+    GLOBAL const int32_t *gi = RIGHT ? A.grid_idx_r : A.grid_idx;
+    const int koff = RIGHT ? A.nleft : 0;
+    const float factorX = w.r, factorY = w.r;
+    int minCX = (int)floorf((w.x - A.min_x - factorX) * A.inv_w);
+    if (minCX < 0) minCX = 0;
+    if (minCX >= OSG_GRID_COLS) return 0;
+    int maxCX = (int)ceilf((w.x - A.min_x + factorX) * A.inv_w);
+    if (maxCX > OSG_GRID_COLS - 1) maxCX = OSG_GRID_COLS - 1;
+    if (maxCX < 0) return 0;
+    int minCY = (int)floorf((w.y - A.min_y - factorY) * A.inv_h);
+    if (minCY < 0) minCY = 0;
+    if (minCY >= OSG_GRID_ROWS) return 0;
+    int maxCY = (int)ceilf((w.y - A.min_y + factorY) * A.inv_h);
+    if (maxCY > OSG_GRID_ROWS - 1) maxCY = OSG_GRID_ROWS - 1;
+    if (maxCY < 0) return 0;
+    const bool bCheckLevels = (w.minL > 0) || (w.maxL >= 0);  // ref:src/Frame.cc:919 quirk
+    const bool stereo = !RIGHT && w.stereo && A.u_right;
+    const int gshift = (threadIdx.x & 63) & ~(BOW_G - 1);     // the group's first lane in the wave
+    int cnt = 0;
+    for (int ix = minCX; ix <= maxCX; ix++) {
+        const int j0 = gs[ix * OSG_GRID_ROWS + minCY], j1 = gs[ix * OSG_GRID_ROWS + maxCY + 1];
+        for (int jb = j0; jb < j1; jb += BOW_G) {
+            const int j = jb + lane;
+            bool pass = false;
+            int k = 0, oct = 0;
+            if (j < j1) {
+                k = gi[j] + koff;
+                oct = A.kp_octave[k];
+                const float x = A.kp_x[k], y = A.kp_y[k];
+                pass = !(bCheckLevels && (oct < w.minL || (w.maxL >= 0 && oct > w.maxL)));
+                const float distx = x - w.x, disty = y - w.y;
+                pass = pass && fabsf(distx) < factorX && fabsf(disty) < factorY;
+                if (stereo && pass) {
+                    const float ur = A.u_right[k];
+                    if (ur > 0 && fabsf(w.sx - ur) > w.sr) pass = false;
+                }
+            }
+            const uint32_t m = (uint32_t)(__ballot(pass) >> gshift) & ((1u << BOW_G) - 1);
+            if (FILL && pass) {
+                const uint32_t d = dist256(qd, A.fdesc + (size_t)k * 8);
+                out[cnt + __builtin_popcount(m & ((1u << lane) - 1))] =
+                    (uint32_t)k | (d << 16) | ((uint32_t)(oct & 0x7F) << 25);
+            }
+            cnt += __builtin_popcount(m);
+        }
+    }
+    return cnt;
+}
+// enum_query for a group, from the query's windows: left-camera candidates, then right-camera ones;
+// cl = left count
+template <int MODE, bool FILL>
+__device__ __forceinline__ int enum_query_group(const MatchArgs &A, int q, const Win &w, const Win &wr,
+                                                GLOBAL uint32_t *out, int &cl, int lane)
+{
+    uint32_t qd[8];
+    if (FILL) load_desc(A, q, qd);
+    const int c0 = w.valid ? enum_grid_group<FILL, false>(A, w, qd, out, lane) : 0;
+    cl = c0;
+    int c1 = 0;
+    if ((MODE == MODE_MPS || MODE == MODE_LAST) && A.nleft >= 0 && (MODE != MODE_LAST || c0 > 0))
+        if (wr.valid) c1 = enum_grid_group<FILL, true>(A, wr, qd, FILL ? out + c0 : nullptr, lane);
+    return c0 + c1;
+}
+// eval_query for a group: each pass's top-2 over the candidates as packed keys (distance << 16 |
+// position), merged across the group — the sequential loop's bestDist / bestDist2 with its tie order
+// (see push2) — and the levels read back from the best and second candidates
+template <int MODE, typename Blocked>
+__device__ __forceinline__ QRes eval_query_group(const MatchArgs &A, int q, int e0, int em, int e1, int lane,
+                                                 Blocked blocked)
+{
+    QRes res{-1, -1};
+    auto top2 = [&](int b0, int b1, auto skip, int &best, int &bl, int &second, int &sl, int &bslot) {
+        uint32_t k1 = KEY_NONE, k2 = KEY_NONE;
+        for (int e = b0 + lane; e < b1; e += BOW_G) {
+            const uint32_t c = A.cands[e];
+            const int s = (int)(c & 0xFFFFu);
+            if (skip(s)) continue;
+            push2(k1, k2, (((c >> 16) & 0x1FFu) << 16) | (uint32_t)(e - b0));
+        }
+#pragma unroll
+        for (int o = BOW_G / 2; o > 0; o >>= 1) merge2(k1, k2, o);
+        best = (int)(k1 >> 16);
+        second = (int)(k2 >> 16);
+        // Top2::push takes a candidate only below 256: one at 256 leaves the defaults (-1)
+        const uint32_t c1 = best < 256 ? A.cands[b0 + (k1 & 0xFFFFu)] : 0u;
+        const uint32_t c2 = second < 256 ? A.cands[b0 + (k2 & 0xFFFFu)] : 0u;
+        bl = best < 256 ? (int)(c1 >> 25) : -1;
+        bslot = best < 256 ? (int)(c1 & 0xFFFFu) : -1;
+        sl = second < 256 ? (int)(c2 >> 25) : -1;
+        if (best >= 256) best = 256;
+        if (second >= 256) second = 256;
+    };
+    int best, bl, second, sl, bslot;
+    top2(e0, em, [&](int s) { return blocked(s); }, best, bl, second, sl, bslot);
+    bool acc, skip_r = false;
+    if (MODE == MODE_MPS) {  // ref:src/ORBmatcher.cc:147-167
+        acc = best <= OSG_TH_HIGH && !(bl == sl && (float)best > A.nnratio * (float)second);
+        skip_r = best <= OSG_TH_HIGH && !acc;
+    } else if (MODE == MODE_LAST) {  // ref:src/ORBmatcher.cc:2070
+        acc = best <= OSG_TH_HIGH;
+    } else {  // MODE_KF, ref:src/ORBmatcher.cc:2287
+        acc = best <= A.orb_dist;
+    }
+    res.l = acc ? bslot : -1;
+    if ((MODE == MODE_MPS || MODE == MODE_LAST) && em < e1 && !skip_r) {
+        int own = -1;
+        bool own_blocked = false;
+        if (MODE == MODE_MPS && res.l >= 0 && A.l2r) {
+            const int t = A.l2r[res.l];
+            if (t != -1) {
+                own = t + A.nleft;
+                own_blocked = A.q_has_obs[q] != 0;
+            }
+        }
+        top2(em, e1, [&](int s) { return s == own ? own_blocked : blocked(s); }, best, bl, second, sl, bslot);
+        bool accr;
+        if (MODE == MODE_MPS)  // ref:src/ORBmatcher.cc:222-238
+            accr = best <= OSG_TH_HIGH && !(bl == sl && (float)best > A.nnratio * (float)second);
+        else  // ref:src/ORBmatcher.cc:2133
+            accr = best <= OSG_TH_HIGH;
+        res.r = accr ? bslot : -1;
+    }
+    return res;
+}
 template <int MODE>
-__global__ __launch_bounds__(GQ) void k_grid_count(const MatchArgs *__restrict__ args)
+__global__ __launch_bounds__(GQG *BOW_G) void k_grid_count(const MatchArgs *__restrict__ args)
 {
     const MatchArgs &A = args[blockIdx.y];
-    const int q = blockIdx.x * GQ + threadIdx.x;
+    const int lane = threadIdx.x & (BOW_G - 1);
+    const int q = blockIdx.x * GQG + threadIdx.x / BOW_G;
     if (q >= A.nq) return;
     const Win wl = query_window<MODE>(A, q);
-    store_win(A.q_win + 4 * (size_t)q, wl);
-    if ((MODE == MODE_MPS || MODE == MODE_LAST) && A.nleft >= 0)
-        store_win(A.q_win + 4 * (size_t)q + 2, query_window_r<MODE>(A, q, wl));
-    const GridView<0> GL{A.grid_start, A.grid_idx, 0, nullptr, nullptr, nullptr, nullptr, A.fdesc};
-    const GridView<0> GR{A.grid_start_r, A.grid_idx_r, A.nleft, nullptr, nullptr, nullptr, nullptr, A.fdesc};
+    const bool two = (MODE == MODE_MPS || MODE == MODE_LAST) && A.nleft >= 0;
+    const Win wr = two ? query_window_r<MODE>(A, q, wl) : wl;
+    if (lane == 0) {  // for k_grid_fill and k_match's serial redo
+        store_win(A.q_win + 4 * (size_t)q, wl);
+        if (two) store_win(A.q_win + 4 * (size_t)q + 2, wr);
+    }
     int cl;
-    A.q_off[q] = enum_query<MODE, false, 0>(A, GL, GR, q, nullptr, cl);  // the count, for k_grid_scan
+    const int c = enum_query_group<MODE, false>(A, q, wl, wr, nullptr, cl, lane);
+    if (lane == 0) A.q_off[q] = c;  // the count, for k_grid_scan
 }
 template <int MODE>
 __global__ __launch_bounds__(MT) void k_grid_scan(const MatchArgs *__restrict__ args)
@@ -679,19 +814,28 @@ __global__ __launch_bounds__(MT) void k_grid_scan(const MatchArgs *__restrict__ 
     }
 }
 template <int MODE>
-__global__ __launch_bounds__(GQ) void k_grid_fill(const MatchArgs *__restrict__ args)
+__global__ __launch_bounds__(GQG *BOW_G) void k_grid_fill(const MatchArgs *__restrict__ args)
 {
     const MatchArgs &A = args[blockIdx.y];
-    const int q = blockIdx.x * GQ + threadIdx.x;
+    const int lane = threadIdx.x & (BOW_G - 1);
+    const int q = blockIdx.x * GQG + threadIdx.x / BOW_G;
     if (q >= A.nq || A.q_off[A.nq] > A.cap) return;
-    const GridView<0> GL{A.grid_start, A.grid_idx, 0, nullptr, nullptr, nullptr, nullptr, A.fdesc};
-    const GridView<0> GR{A.grid_start_r, A.grid_idx_r, A.nleft, nullptr, nullptr, nullptr, nullptr, A.fdesc};
     const int off = A.q_off[q];
+    const Win wl = load_win(A.q_win + 4 * (size_t)q);
+    const bool two = (MODE == MODE_MPS || MODE == MODE_LAST) && A.nleft >= 0;
+    const Win wr = two ? load_win(A.q_win + 4 * (size_t)q + 2) : wl;
     int cl;
-    enum_query<MODE, true, 0>(A, GL, GR, q, A.cands + off, cl);
-    A.q_mid[q] = off + cl;
+    const int c = enum_query_group<MODE, true>(A, q, wl, wr, A.cands + off, cl, lane);
+    if (lane == 0) A.q_mid[q] = off + cl;
+    // the group reads back the candidates its lanes wrote: their stores complete first (the lanes
+    // share the CU's write-through L1)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     // the first evaluation: blocked(s) = the slot's state before the call (k_match's taken0)
-    store_res(A, q, eval_query<MODE>(A, q, [&](int s) { return taken_init<MODE>(A, s); }));
+    const QRes r = eval_query_group<MODE>(A, q, off, off + cl, off + c, lane,
+                                          [&](int s) { return taken_init<MODE>(A, s); });
+    if (lane == 0) store_res(A, q, r);
 }
 
 // Every slot q writes: the direct matches and, for a5 on a two-camera rig, each one's stereo
@@ -1389,11 +1533,10 @@ int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_
             int max_nq = 0;
             for (int b = 0; b < B; b++) max_nq = std::max(max_nq, P[b].A.nq);
             if (max_nq > 0) {
-                hipLaunchKernelGGL((k_grid_count<MODE>), dim3((max_nq + GQ - 1) / GQ, B), dim3(GQ), 0, ctx->stream,
-                                   dev_args);
+                const dim3 gq((max_nq + GQG - 1) / GQG, B);
+                hipLaunchKernelGGL((k_grid_count<MODE>), gq, dim3(GQG * BOW_G), 0, ctx->stream, dev_args);
                 hipLaunchKernelGGL((k_grid_scan<MODE>), dim3(B), dim3(MT), 0, ctx->stream, dev_args);
-                hipLaunchKernelGGL((k_grid_fill<MODE>), dim3((max_nq + GQ - 1) / GQ, B), dim3(GQ), 0, ctx->stream,
-                                   dev_args);
+                hipLaunchKernelGGL((k_grid_fill<MODE>), gq, dim3(GQG * BOW_G), 0, ctx->stream, dev_args);
             }
         }
         if (stage == 2)
@@ -1407,7 +1550,7 @@ int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_
         // status, slot arrays and KF-KF results in one copy (the pinned io block is re-filled from the
         // callers' slots before a retry)
         OSG_RC(osg_download(ctx, pin_io, dev_io, io_bytes));
-        OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+        OSG_RC(osg_wait(ctx));
         std::memcpy(st.data(), pin_io, status_bytes);
         bool overflow = false;
         for (int b = 0; b < B; b++)

@@ -37,6 +37,7 @@ struct osg_ctx {
     int32_t match_stats[4] = {};  // last matcher call: candidates, Jacobi rounds, serial redo, nmatches
     double last_kernel_ms = 0;    // last k_match / k_pose_opt launch time (HIP events)
     hipEvent_t ev[2] = {};        // timing events (osg_ctx_events)
+    hipEvent_t ev_done = nullptr; // completion marker of osg_wait (no timing)
     std::shared_ptr<void> lba_cache;  // host structures of the last LBA batch, reused (ba.hip)
     bool lba_ktime = false;           // osg_lba_kernel_times: per-kernel HIP-event timing of LBA steps
     double lba_kms[OSG_LBA_NK] = {};
@@ -57,6 +58,10 @@ void *osg_pinned(osg_ctx *ctx, size_t bytes);
 #define OSG_KCOPY_MAX (size_t(4) << 20)
 int osg_upload(osg_ctx *ctx, void *dst_dev, const void *src_pinned, size_t bytes);
 int osg_download(osg_ctx *ctx, void *dst_pinned, const void *src_dev, size_t bytes);
+// Wait for everything enqueued on ctx->stream: an event recorded behind it, polled with
+// hipEventQuery (a one-frame call returns within ~1 us of its last kernel instead of a blocking
+// synchronisation's wake-up)
+int osg_wait(osg_ctx *ctx);
 
 #define OSG_HIP_CHECK(ctx, expr)                                                             \
     do {                                                                                     \

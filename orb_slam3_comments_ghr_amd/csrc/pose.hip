@@ -28,7 +28,6 @@
 #include <algorithm>
 #include <cfloat>
 #include <cstdlib>
-#include <cstring>
 #include <vector>
 
 #include "ba_common.h"
@@ -607,381 +606,6 @@ __global__ __launch_bounds__(NW *PW) void k_pose_opt(const PoseProbDev *__restri
 }
 
 
-// ------------------------------------------------------------------------------ latency form
-// k_pose_lat: one frame of at most LMAX edges per 8-wave workgroup, for launches of a few frames (the
-// drop-in's one-frame call, where k_pose_opt's cost was the number of serial phases, not the work).
-// The arithmetic and the summation orders are k_pose_opt's, so every result is the oracle's bit for
-// bit; what changes is how the LM steps are scheduled:
-//   * Each lane keeps its edges (X, obs, weight, kind) in registers for the whole call, and the
-//     frame state (pose, lambda, the LM control) in registers, replicated on every lane.
-//   * Speculative trials.  Within one LM iteration H, b and the pose are fixed, and a rejected trial
-//     changes only lambda, along a fixed sequence (lambda *= ni; ni *= 2, starting from ni = 2).  So
-//     trial k's damped solve, its exp-map update and its chi2 do not depend on the trials before it
-//     except through that sequence (and, after a failed factorisation, through the x of the last
-//     successful solve, which a prefix over the batch recovers).  A batch of K trials is solved on
-//     lanes 0..K-1 at once, all K chi2 sums are formed in one pass over the edges (stream k summed in
-//     edge order by lane k of wave 0), and the reference's accept / reject sequence is then replayed
-//     on the K sums: the first accepted trial wins, the trials after it are discarded unread.
-//   * The first batch of an iteration holds KA trials and also forms buildSystem at trial 0's pose;
-//     when trial 0 is accepted (the common case) that is the next iteration's system, so the next
-//     iteration starts without a pass of its own.  Later batches take up to the remaining trials.
-constexpr int LW = 8;                   // waves per frame
-constexpr int LSC = LW * PW;            // edges per superchunk
-constexpr int LNSC = 2;                 // superchunks held in registers
-constexpr int LMAX = LNSC * LSC;        // edges per frame (larger frames take k_pose_opt)
-constexpr int KA = 2;                   // trials of an iteration's first batch
-constexpr int KMAXT = 10;               // trials per iteration (g2o's levenberg: qmax < 10)
-constexpr int LNS = NT + 1;             // streams of the fused pass: H | b | chi2 at trial 0 | chi2 at trial 1
-constexpr int LAT_MAX_FRAMES = 64;      // launches of up to this many frames take k_pose_lat
-
-struct LatShared {
-    osg_camera cam, cam2;
-    SE3 trl;
-    double sys[2][NT];        // buildSystem sums: the current pose's, and trial 0's from the fused pass
-    double tchi[KMAXT];       // the batch's trial chi2 sums
-    int n_act[LW], n_bad[LW];
-};
-struct LatWave {              // one wave's copy of the LM state and the batch's trials (all waves compute the same)
-    SE3 pose, teval;
-    double xs[6];             // the solver's x, kept when a factorisation fails
-    SE3 tp[KMAXT];
-    double x[KMAXT][6];
-    int ok[KMAXT];
-};
-
-__global__ __launch_bounds__(LW *PW) void k_pose_lat(const PoseProbDev *__restrict__ probs,
-                                                     const int8_t *__restrict__ e_kind,
-                                                     const double *__restrict__ e_xw,
-                                                     const double *__restrict__ e_obs,
-                                                     const float *__restrict__ e_isig2,
-                                                     uint8_t *__restrict__ e_out,
-                                                     PoseOut *__restrict__ out)
-{
-    __shared__ __attribute__((aligned(16))) double s_t[LW * LNS * ROW];
-    __shared__ LatShared S;
-    __shared__ LatWave WV[LW];
-    const PoseProbDev &P = probs[blockIdx.x];
-    const int n = P.n_edges;
-    uint8_t *outl = e_out + P.edge_off;
-    const int wave = threadIdx.x / PW, lane = threadIdx.x % PW;
-    const int nsc = (n + LSC - 1) / LSC;  // <= LNSC (the host checks n <= LMAX)
-
-    PROF_T(t_start);
-    if (n < 3) {  // ref:src/Optimizer.cc:289-290
-        for (int e = threadIdx.x; e < n; e += LW * PW) outl[e] = 0;
-        if (threadIdx.x == 0) {
-            for (int i = 0; i < 7; i++) out[blockIdx.x].pose[i] = P.pose[i];
-            out[blockIdx.x].n_inliers = 0;
-            out[blockIdx.x].lm_iterations = 0;
-            out[blockIdx.x].lm_trials = 0;
-        }
-        return;
-    }
-    if (threadIdx.x == 0) {
-        S.cam = P.cam;
-        S.cam2 = P.cam2;
-        S.trl = se3_from7(P.cam2.trl);
-    }
-    // this lane's edges, superchunk s <-> edge s * LSC + threadIdx.x
-    PEdge E[LNSC];
-    bool has[LNSC];
-#pragma unroll
-    for (int s = 0; s < LNSC; s++) {
-        const int e = s * LSC + threadIdx.x;
-        has[s] = e < n;
-        if (has[s]) E[s] = load_edge(P.edge_off + e, e_kind, e_xw, e_obs, e_isig2);
-        else E[s] = PEdge{};
-    }
-    __syncthreads();
-    const osg_camera &cam = S.cam, &cam2 = S.cam2;
-    const SE3 &Trl = S.trl;
-    LatWave &W = WV[wave];
-    double *tile = s_t + wave * LNS * ROW;
-    Huber hb;
-    {
-        const float deltaMono = (float)sqrt(5.991);
-        const float deltaStereo = (float)sqrt(7.815);
-        hb.delta_mono = deltaMono;
-        hb.delta_stereo = deltaStereo;
-        hb.dsqr_mono = (float)((double)deltaMono * (double)deltaMono);
-        hb.dsqr_stereo = (float)((double)deltaStereo * (double)deltaStereo);
-    }
-    int robust = 1;
-    int nBad = 0;
-    int total_iters = 0, total_trials = 0;
-    uint32_t om = 0;  // bit s: this lane's edge of superchunk s is an outlier (level 1)
-    auto active = [&](int s) { return has[s] && !((om >> s) & 1); };
-    auto chunk_cnt = [&](int s, int w) { return min(PW, n - s * LSC - w * PW); };
-    auto robust_chi = [&](const PEdge &Ed, const SE3 &T) -> double {
-        double ev[3];
-        pose_edge_error(Ed, cam, cam2, Trl, T, ev);
-        const bool st = Ed.k == OSG_EDGE_STEREO;
-        const double c = edge_chi2_of(ev, st, Ed.w);
-        double v = c, r1;
-        if (robust) {
-            if (st) huber(c, hb.delta_stereo, hb.dsqr_stereo, v, r1);
-            else huber(c, hb.delta_mono, hb.dsqr_mono, v, r1);
-        }
-        return v;
-    };
-    // buildSystem terms of one edge at T into the tile column (streams 0..27)
-    auto sys_terms = [&](const PEdge &Ed, const SE3 &T, double *col) {
-        double ev[3];
-        pose_edge_error(Ed, cam, cam2, Trl, T, ev);
-        const bool st = Ed.k == OSG_EDGE_STEREO;
-        const double chi = edge_chi2_of(ev, st, Ed.w);
-        double r0 = chi, rho1 = 1.0;
-        if (robust) {
-            if (st) huber(chi, hb.delta_stereo, hb.dsqr_stereo, r0, rho1);
-            else huber(chi, hb.delta_mono, hb.dsqr_mono, r0, rho1);
-        }
-        col[27 * ROW] = r0;
-        double Jp[3][6];
-        pose_edge_jac(Ed, cam, cam2, Trl, T, Jp);
-        const double ww = rho1 * Ed.w;
-        int q = 0;
-#pragma unroll
-        for (int i = 0; i < 6; i++)
-#pragma unroll
-            for (int j = i; j < 6; j++) {
-                double h = 0;
-                h += Jp[0][i] * ww * Jp[0][j];
-                h += Jp[1][i] * ww * Jp[1][j];
-                if (st) h += Jp[2][i] * ww * Jp[2][j];
-                col[(q++) * ROW] = h;
-            }
-#pragma unroll
-        for (int i = 0; i < 6; i++) {
-            double sb = 0;
-            sb += rho1 * Jp[0][i] * (Ed.w * ev[0]);
-            sb += rho1 * Jp[1][i] * (Ed.w * ev[1]);
-            if (st) sb += rho1 * Jp[2][i] * (Ed.w * ev[2]);
-            col[(21 + i) * ROW] = -sb;
-        }
-    };
-    // One pass over the edges.  mode 0: buildSystem at T0 (streams 0..27 -> dst).  mode 1: the fused
-    // first batch: buildSystem at trial 0's pose (streams 0..27 -> dst, stream 27 = trial 0's chi2)
-    // and trial 1's chi2 (stream 28).  mode 2: the chi2 of trials 0..K-1 (streams 0..K-1).  Stream q
-    // is summed in edge order by lane q of wave 0; inactive edges add 0.
-    auto pass = [&](int mode, const SE3 &T0, int K, double *dst) {
-        const int ns = mode == 0 ? NT : mode == 1 ? NT + 1 : K;
-        double acc = 0.0;
-#pragma unroll
-        for (int s = 0; s < LNSC; s++) {
-            if (s >= nsc) break;
-            PROF_T(t_p0);
-            double *col = tile + lane;
-            if (active(s)) {
-                if (mode == 0) sys_terms(E[s], T0, col);
-                else if (mode == 1) {
-                    sys_terms(E[s], W.tp[0], col);
-                    col[NT * ROW] = robust_chi(E[s], W.tp[1]);
-                } else
-                    for (int k = 0; k < K; k++) col[k * ROW] = robust_chi(E[s], W.tp[k]);
-            } else {
-                for (int q = 0; q < ns; q++) col[q * ROW] = 0.0;
-            }
-            __syncthreads();
-            PROF_ADD(6, t_p0);
-            PROF_T(t_p1);
-            if (wave == 0) {
-                const int q = lane < ns ? lane : ns - 1;
-                for (int w = 0; w < LW && chunk_cnt(s, w) > 0; w++)
-                    acc = seq_sum(acc, s_t + (w * LNS + q) * ROW, chunk_cnt(s, w));
-            }
-            __syncthreads();
-            PROF_ADD(7, t_p1);
-        }
-        if (wave == 0 && lane < ns) {
-            if (mode == 2) S.tchi[lane] = acc;
-            else if (lane < NT) dst[lane] = acc;
-            else S.tchi[1] = acc;
-        }
-        __syncthreads();
-        if (mode == 1) S.tchi[0] = dst[27];
-    };
-    auto frame_count = [&](int v, int *slot) -> int {
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-        if (lane == 0) slot[wave] = v;
-        __syncthreads();
-        int t = 0;
-#pragma unroll
-        for (int w = 0; w < LW; w++) t += slot[w];
-        return t;
-    };
-
-    SE3 &pose = W.pose, &T_eval = W.teval;  // wave-uniform: read from LDS where used
-    double *xs = W.xs;
-#pragma unroll
-    for (int i = 0; i < 6; i++) xs[i] = 0.0;
-    for (int it = 0; it < 4; it++) {
-        pose = se3_from7(P.pose);  // every round restarts from the input pose (ref:src/Optimizer.cc:306-307)
-        T_eval = pose;
-        int na = 0;
-#pragma unroll
-        for (int s = 0; s < LNSC; s++) na += active(s) ? 1 : 0;
-        const int nact = frame_count(na, S.n_act);
-        if (nact > 0) {
-            double lambda = 0, ni = 2;
-            int nBadLM = 0;
-            int cur = 0;          // S.sys[cur] holds buildSystem at `pose`
-            bool have_sys = false;
-            for (int iter = 0; iter < 10; iter++) {
-                total_iters++;
-                PROF_T(t_h);
-                if (!have_sys) pass(0, pose, 0, S.sys[cur]);
-                PROF_ADD(0, t_h);
-                T_eval = pose;
-                const double *sys = S.sys[cur];
-                const double iniChi = sys[27];
-                double currentChi = iniChi;
-                if (iter == 0) {  // computeLambdaInit: tau * max |diag H|
-                    const int dpos[6] = {0, 6, 11, 15, 18, 20};
-                    double md = 0;
-#pragma unroll
-                    for (int i = 0; i < 6; i++) md = fmax(fabs(sys[dpos[i]]), md);
-                    lambda = 1e-5 * md;
-                    ni = 2;
-                    nBadLM = 0;
-                }
-                double rho = 0;
-                int qmax = 0;
-                int acc_k = -1;   // the accepted trial of this iteration
-                bool more = true;
-                for (int batch = 0; more; batch++) {
-                    const int K = batch == 0 ? KA : min(KMAXT - qmax, KMAXT);
-                    PROF_T(t_s);
-                    {   // lanes 0..K-1: trial lane's lambda (the rejection sequence), damped solve
-                        double lam = lambda, nk = ni;
-                        for (int j = 0; j < lane && j < K; j++) {
-                            lam *= nk;
-                            nk *= 2;
-                        }
-                        double A[6][6], bvec[6];
-                        int q = 0;
-#pragma unroll
-                        for (int i = 0; i < 6; i++)
-#pragma unroll
-                            for (int j = i; j < 6; j++) {
-                                A[i][j] = sys[q] + (i == j ? lam : 0.0);
-                                A[j][i] = A[i][j];
-                                q++;
-                            }
-#pragma unroll
-                        for (int i = 0; i < 6; i++) bvec[i] = sys[21 + i];
-                        double x[6] = {0, 0, 0, 0, 0, 0};
-                        const bool ok = lane < K && ldlt6(A, bvec, x);
-                        // x used by trial `lane`: its own, else the last successful solve before it
-                        const uint64_t okm = __ballot(ok);
-                        const uint64_t upto = okm & ((lane >= 63) ? ~0ull : ((2ull << lane) - 1));
-                        const int src = upto ? 63 - __clzll(upto) : -1;
-                        double xu[6];
-#pragma unroll
-                        for (int i = 0; i < 6; i++) {
-                            const double v = __shfl(x[i], src < 0 ? 0 : src);
-                            xu[i] = src < 0 ? xs[i] : v;
-                        }
-                        PROF_ADD(1, t_s);
-                        PROF_T(t_x);
-                        SE3 tp = pose;
-                        se3_oplus(tp, xu);  // exp(update) * estimate
-                        if (lane < K) {
-                            W.tp[lane] = tp;
-#pragma unroll
-                            for (int i = 0; i < 6; i++) W.x[lane][i] = xu[i];
-                            W.ok[lane] = ok ? 1 : 0;
-                        }
-                        PROF_ADD(2, t_x);
-                    }
-                    __syncthreads();
-                    PROF_T(t_c);
-                    if (batch == 0) pass(1, pose, K, S.sys[cur ^ 1]);
-                    else pass(2, pose, K, nullptr);
-                    PROF_ADD(3, t_c);
-                    // the reference's accept / reject sequence over the batch's trials
-                    for (int kk = 0; kk < K; kk++) {
-                        total_trials++;
-                        const double *xk = W.x[kk];
-                        double tempChi = W.ok[kk] ? S.tchi[kk] : DBL_MAX;
-                        T_eval = W.tp[kk];
-#pragma unroll
-                        for (int i = 0; i < 6; i++) xs[i] = xk[i];
-                        rho = (currentChi - tempChi);
-                        double scale = 0.;
-#pragma unroll
-                        for (int j = 0; j < 6; j++) scale += xs[j] * (lambda * xs[j] + sys[21 + j]);
-                        scale += 1e-3;
-                        rho /= scale;
-                        if (rho > 0 && isfinite(tempChi)) {
-                            double alpha = 1. - osgx::cube_rn(2 * rho - 1);
-                            alpha = fmin(alpha, 2. / 3.);
-                            const double scaleFactor = fmax(1. / 3., alpha);
-                            lambda *= scaleFactor;
-                            ni = 2;
-                            currentChi = tempChi;
-                            pose = W.tp[kk];
-                            acc_k = batch == 0 ? kk : KA + kk;
-                        } else {
-                            lambda *= ni;
-                            ni *= 2;
-                        }
-                        qmax++;
-                        if (!(rho < 0 && qmax < 10)) {
-                            more = false;
-                            break;
-                        }
-                    }
-                    __syncthreads();  // W / S.tchi are rewritten by the next batch
-                }
-                // buildSystem at the accepted trial 0's pose came with the first batch
-                have_sys = acc_k == 0;
-                if (have_sys) cur ^= 1;
-                bool terminate = false;
-                if (qmax == 10 || rho == 0) terminate = true;
-                else {
-                    if ((iniChi - currentChi) * 1e3 < iniChi) nBadLM++;
-                    else nBadLM = 0;
-                    if (nBadLM >= 3) terminate = true;
-                }
-                if (terminate) break;
-            }
-        }
-        // classification (ref:src/Optimizer.cc:314-403): active edges read their last computed
-        // error (at T_eval), inactive ones computeError() at the final pose
-        PROF_T(t_cl);
-        int bad = 0;
-#pragma unroll
-        for (int s = 0; s < LNSC; s++) {
-            if (!has[s]) continue;
-            const bool was_out = (om >> s) & 1;
-            double ev[3];
-            pose_edge_error(E[s], cam, cam2, Trl, was_out ? pose : T_eval, ev);
-            const bool st = E[s].k == OSG_EDGE_STEREO;
-            const float chi2 = (float)edge_chi2_of(ev, st, E[s].w);
-            const float th = st ? 7.815f : 5.991f;
-            const bool b = chi2 > th;
-            om = (om & ~(1u << s)) | ((b ? 1u : 0u) << s);
-            bad += b ? 1 : 0;
-        }
-        nBad = frame_count(bad, S.n_bad);
-        PROF_ADD(4, t_cl);
-        if (it == 2) robust = 0;
-        if (n < 10) break;
-        __syncthreads();  // S.n_act / S.n_bad are rewritten next round
-    }
-#pragma unroll
-    for (int s = 0; s < LNSC; s++)
-        if (has[s]) outl[s * LSC + threadIdx.x] = (om >> s) & 1;
-    PROF_ADD(5, t_start);
-    if (threadIdx.x == 0) {
-        se3_to7(pose, out[blockIdx.x].pose);
-        out[blockIdx.x].n_inliers = n - nBad;
-        out[blockIdx.x].lm_iterations = total_iters;
-        out[blockIdx.x].lm_trials = total_trials;
-    }
-}
-
 }  // namespace
 
 extern "C" {
@@ -1010,13 +634,8 @@ int osg_pose_optimization_batch(osg_ctx *ctx, const osg_pose_problem *p, int32_t
     int nmax = 0;
     for (int b = 0; b < nb; b++) nmax = std::max(nmax, p[b].n_edges);
     const int chunks = (nmax + PW - 1) / PW;
-    // k_pose_lat for launches of a few frames of at most LMAX edges (latency), k_pose_opt otherwise;
-    // OSG_POSE_NW=lat / 1 / 2 / 4 / 8 pins the variant (tests; "lat" on a larger frame takes k_pose_opt)
-    const char *fv = getenv("OSG_POSE_NW");
-    const bool lat = nmax <= LMAX && (fv ? std::strcmp(fv, "lat") == 0 : nb <= LAT_MAX_FRAMES);
     int nw = 1;
-    if (fv && std::strcmp(fv, "lat") != 0) nw = atoi(fv);
-    else if (fv) nw = 8;
+    if (const char *f = getenv("OSG_POSE_NW")) nw = atoi(f);  // tests pin the variant
     else {
         // waves per frame: up to one per 1.5 chunks of a lone frame's edges (latency; 8 waves share
         // 4 SIMDs and measured no faster than 4), one when the batch fills the chip's wave slots
@@ -1063,8 +682,7 @@ int osg_pose_optimization_batch(osg_ctx *ctx, const osg_pose_problem *p, int32_t
     PoseOut *a6 = (PoseOut *)(dio + o_res);
 #define OSG_POSE_LAUNCH(W_) \
     hipLaunchKernelGGL(k_pose_opt<W_>, dim3(nb), dim3(W_ * PW), 0, ctx->stream, a0, a1, a2, a3, a4, a5, a6)
-    if (lat) hipLaunchKernelGGL(k_pose_lat, dim3(nb), dim3(LW * PW), 0, ctx->stream, a0, a1, a2, a3, a4, a5, a6);
-    else switch (nw) {
+    switch (nw) {
     case 1: OSG_POSE_LAUNCH(1); break;
     case 2: OSG_POSE_LAUNCH(2); break;
     case 4: OSG_POSE_LAUNCH(4); break;
@@ -1075,7 +693,7 @@ int osg_pose_optimization_batch(osg_ctx *ctx, const osg_pose_problem *p, int32_t
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
     char *pout = pin + in_bytes;
     OSG_RC(osg_download(ctx, pout, dio, io_bytes));
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    OSG_RC(osg_wait(ctx));
     float kms = 0.f;
     OSG_HIP_CHECK(ctx, hipEventElapsedTime(&kms, ev[0], ev[1]));
     ctx->last_kernel_ms = kms;

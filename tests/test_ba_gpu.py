@@ -4,8 +4,7 @@ CPU oracle.
 PoseOptimization (pinhole mono + stereo) is bit-exact: the kernel sums every chi2 /
 H / b stream in edge order and both sides evaluate sin / cos / pow(., 3) correctly rounded
 (csrc/exact_math.h), so LM iteration and trial counts, outlier flags and the pose are asserted
-EQUAL, for every variant of the kernel (OSG_POSE_NW pins it: k_pose_opt's waves per frame, or
-"lat" for k_pose_lat's speculative trials).  KannalaBrandt8
+EQUAL, for every waves-per-frame variant of the kernel (OSG_POSE_NW pins it).  KannalaBrandt8
 fisheye frames too: the projection's float atan2f is glibc's algorithm restated bit for bit
 (csrc/glibc_math.h, pinned against the host libm by tests/test_exact_math.py), and its double
 cos / sin / atan2 are correctly rounded on both sides.
@@ -43,7 +42,7 @@ def assert_pose_equal(got, ref):
         np.testing.assert_array_equal(g.pose, r.pose)
 
 
-@pytest.mark.parametrize("nw", [None, "1", "2", "4", "8", "lat"])
+@pytest.mark.parametrize("nw", [None, "1", "2", "4", "8"])
 def test_pose_optimization_batch(ctx, oracle, monkeypatch, nw):
     if nw is not None:
         monkeypatch.setenv("OSG_POSE_NW", nw)
@@ -63,7 +62,7 @@ def test_pose_optimization_single_frame_sizes(ctx, oracle, n_edges):
     assert_pose_equal([op.Optimizer(ctx).PoseOptimization(p)], oc.pose(oracle, [p]))
 
 
-@pytest.mark.parametrize("nw", [None, "1", "8", "lat"])
+@pytest.mark.parametrize("nw", [None, "1", "8"])
 def test_pose_optimization_kb8_fisheye(ctx, oracle, monkeypatch, nw):
     """KannalaBrandt8 camera (TUM-VI-like fisheye): project / projectJac with the host libm's float
     atan2f (restated, glibc_math.h) and correctly rounded cos / sin / atan2: bit-exact, like pinhole."""
@@ -78,7 +77,7 @@ def test_pose_optimization_kb8_fisheye(ctx, oracle, monkeypatch, nw):
     assert_pose_equal(got, ref)
 
 
-@pytest.mark.parametrize("nw", [None, "2", "lat"])
+@pytest.mark.parametrize("nw", [None, "2"])
 def test_pose_optimization_kb8_two_camera(ctx, oracle, monkeypatch, nw):
     """C5 shape: KB8 fisheye pair with right-camera (body) edges through Trl; bit-exact."""
     if nw is not None:

@@ -88,7 +88,7 @@ def main():
         ob = np.zeros(P.n, np.uint8)
         r.outlier = ob.ctypes.data
         d = {}
-        for var in ["4", None]:  # k_pose_opt with 4 waves, then the default (k_pose_lat for one frame)
+        for var in ["4", None]:  # 4 waves per frame, then the host's choice
             if var is None:
                 os.environ.pop("OSG_POSE_NW", None)
             else:
