@@ -792,21 +792,40 @@ static void inv3(const double *m, double *o)
 #undef M
 }
 
-/* dense LDL^T without pivoting on the upper triangle (returns 0 on a zero / non-positive pivot) */
+/* LDL^T without pivoting (returns 0 on a zero / non-positive pivot).  The dense algorithm restricted
+ * to the matrix's envelope: row i's entries left of its first nonzero f[i] are zero in A and stay
+ * zero in L (fill-in never leaves a row's profile), so every sum runs from max(f[i], f[j]) instead of
+ * 0 — the same nonzero terms in the same order.  A map-scale BundleAdjustment's reduced camera
+ * system is banded (keyframes share points with their neighbours only), which keeps the map-scale
+ * parity test in seconds (ref: Eigen's SimplicialLDLT, which g2o's LinearSolverEigen uses, likewise
+ * works on the sparsity only). */
 static int ldlt_solve(double *A, int n, const double *bvec, double *x, int require_positive)
 {
     /* A is row-major n x n symmetric; factor in place: A = L D L^T */
+    int *f = (int *)malloc(sizeof(int) * (size_t)(n > 0 ? n : 1));
+    for (int i = 0; i < n; i++) {
+        int k = 0;
+        while (k < i && A[(size_t)i * n + k] == 0.0) k++;
+        f[i] = k;
+    }
     for (int j = 0; j < n; j++) {
-        double d = A[j * n + j];
-        for (int k = 0; k < j; k++) d -= A[j * n + k] * A[j * n + k] * A[k * n + k];
-        if (d == 0.0 || (require_positive && !(d > 0.0))) return 0;
-        A[j * n + j] = d;
+        const double *Aj = A + (size_t)j * n;
+        double d = Aj[j];
+        for (int k = f[j]; k < j; k++) d -= Aj[k] * Aj[k] * A[(size_t)k * n + k];
+        if (d == 0.0 || (require_positive && !(d > 0.0))) {
+            free(f);
+            return 0;
+        }
+        A[(size_t)j * n + j] = d;
         for (int i = j + 1; i < n; i++) {
-            double s = A[i * n + j];
-            for (int k = 0; k < j; k++) s -= A[i * n + k] * A[j * n + k] * A[k * n + k];
-            A[i * n + j] = s / d;
+            if (f[i] > j) continue;  /* outside row i's profile: stays 0 */
+            double *Ai = A + (size_t)i * n;
+            double s = Ai[j];
+            for (int k = f[i] > f[j] ? f[i] : f[j]; k < j; k++) s -= Ai[k] * Aj[k] * A[(size_t)k * n + k];
+            Ai[j] = s / d;
         }
     }
+    free(f);
     for (int i = 0; i < n; i++) {
         double s = bvec[i];
         for (int k = 0; k < i; k++) s -= A[i * n + k] * x[k];

@@ -59,7 +59,7 @@ __device__ inline const GLOBAL T *gbl(const T *p)
 {
     return (const GLOBAL T *)p;
 }
-constexpr int NPART = 1024;  // max chi2 / scale partials
+constexpr int RED_CHUNK = 1024;  // k_step_reduce stages the partials in LDS this many at a time
 
 // Per-graph control of one lockstep step (host → device each step; k_lambda_init may set lambda).
 enum : int { M_ERRC = 1, M_LIN = 2, M_INIT = 4, M_ACT = 8, M_FIN = 16 };
@@ -123,8 +123,13 @@ struct LbaDev {
     double *Dinv, *db;
     double *Hs, *bs, *x;
     double *Linv;                        // inverses of the 32x32 diagonal blocks of L, row-major per block row
-    double *part;                        // [0, NPART): chi of the trial, [NPART, 2NPART): scale,
-                                         // [2NPART, 3NPART): max diag, [3NPART, 4NPART): chi of the current estimate
+    int npart;                           // partial slots per kind (>= ge, gu, gl + nhp)
+    double *part;                        // [0, P): chi of the trial, [P, 2P): scale, [2P, 3P): max diag,
+                                         // [3P, 4P): chi of the current estimate (P = npart)
+    // envelope of the reduced camera system by 32-row blocks (BundleAdjustment past CMAX): row block t
+    // has nothing left of column block blk_first[t], in A and in its Cholesky factor (fill-in stays
+    // inside the profile); blk_last[j] = the last row block t with blk_first[t] <= j
+    const int32_t *blk_first, *blk_last;
     int *flag;                           // [0] cholesky ok
     unsigned long long *tstamp;          // phase timestamps (OSG_LBA_PROFILE=2), else null
 };
@@ -177,14 +182,14 @@ __device__ inline double block_sum_d(double v, double *s)
 }
 
 // per edge error + robust chi2 -> partial sums per workgroup (deterministic order)
-// which = 0: the trial estimate -> part[0, ge); which = 1: the current estimate -> part[3 NPART, ..)
+// which = 0: the trial estimate -> part[0, ge); which = 1: the current estimate -> part[3 npart, ..)
 __global__ __launch_bounds__(EB) void k_errors(const LbaDev *__restrict__ Ds, int which)
 {
     LBA_GRAPH(which ? M_ERRC : M_ACT);
     if (bx >= D.ge) return;
     const double *poses = which ? cur_pose(D) : new_pose(D);
     const double *points = which ? cur_point(D) : new_point(D);
-    const int part_off = which ? 3 * NPART : 0;
+    const int part_off = which ? 3 * D.npart : 0;
     __shared__ double s[EB / 64];
     const int e = bx * EB + threadIdx.x;
     double rho0 = 0.0;
@@ -279,7 +284,7 @@ __global__ __launch_bounds__(EB) void k_linearize(const LbaDev *__restrict__ Ds)
     if (threadIdx.x == 0) {
         double m = 0;
         for (int i = 0; i < EB / 64; i++) m = fmax(m, s[i]);
-        D.part[2 * NPART + bx] = m;
+        D.part[2 * D.npart + bx] = m;
     }
 }
 
@@ -289,7 +294,7 @@ __global__ __launch_bounds__(EB) void k_pose_red(const LbaDev *__restrict__ Ds)
     LBA_GRAPH(M_LIN);
     const int i = bx;
     if (i >= D.nhp) return;
-    const int diag_off = 2 * NPART + D.gl;
+    const int diag_off = 2 * D.npart + D.gl;
     __shared__ double s[EB / 64][27];
     double acc[27];
     for (int k = 0; k < 27; k++) acc[k] = 0.0;
@@ -375,7 +380,7 @@ __global__ void k_lambda_init(const LbaDev *__restrict__ Ds)
         return;
     }
     double md = 0;
-    for (int i = 0; i < D.gl + D.nhp; i++) md = fmax(md, D.part[2 * NPART + i]);
+    for (int i = 0; i < D.gl + D.nhp; i++) md = fmax(md, D.part[2 * D.npart + i]);
     D.ctl->lambda = 1e-5 * md;
 }
 
@@ -788,6 +793,8 @@ __global__ __launch_bounds__(256) void k_chol_col(const LbaDev *__restrict__ Ds,
 {
     LBA_GRAPH(M_ACT);
     if (j >= D.nblk_red || bx >= D.nblk_red - j) return;
+    // past CMAX a row block outside the envelope has an all-zero tile here, and its L_tj stays zero
+    if (6 * D.nhp > CMAX && bx > 0 && (j + bx > D.blk_last[j] || D.blk_first[j + bx] > j)) return;
     __shared__ double sP[4][CB][CB + 1];  // per-wave partial tiles
     __shared__ double sG[CB][CB + 1];     // T under elimination
     __shared__ double sM[CB][CB + 1];     // Lt^-1, then L_jj^-1
@@ -1040,7 +1047,8 @@ __global__ __launch_bounds__(256) void k_chol_trail(const LbaDev *__restrict__ D
     LBA_GRAPH(M_ACT);
     const int n = 6 * D.nhp;
     if (n <= CMAX) return;
-    const int m = D.nblk_red - j - 1;  // row blocks below block j
+    if (j >= D.nblk_red) return;
+    const int m = D.blk_last[j] - j;  // row blocks below block j inside the envelope's reach
     if (m <= 0 || bx >= m * (m + 1) / 2) return;
     int t = 0, rem = bx;  // tile (t, u), u <= t, row-major over the lower triangle
     while (rem > t) {
@@ -1048,6 +1056,8 @@ __global__ __launch_bounds__(256) void k_chol_trail(const LbaDev *__restrict__ D
         t++;
     }
     const int u = rem;
+    // L_tj or L_uj outside the envelope is zero: the tile's update is zero
+    if (D.blk_first[j + 1 + t] > j || D.blk_first[j + 1 + u] > j) return;
     const int R0 = (j + 1 + t) * CB, C0 = (j + 1 + u) * CB, K0 = j * CB;
     __shared__ double sLt[CB][CB + 1], sLu[CB][CB + 1];
     const int tid = threadIdx.x;
@@ -1088,7 +1098,7 @@ __global__ __launch_bounds__(1024) void k_chol_back_large(const LbaDev *__restri
 {
     LBA_GRAPH(M_ACT);
     const int n = 6 * D.nhp;
-    if (n <= CMAX) return;
+    if (n <= CMAX || n > CMAX_LARGE) return;
     __shared__ double s_x[CMAX_LARGE];
     __shared__ double s_y[CMAX_LARGE];
     __shared__ double s_li[CB * CB];
@@ -1129,6 +1139,54 @@ __global__ __launch_bounds__(1024) void k_chol_back_large(const LbaDev *__restri
         __syncthreads();
     }
     for (int i = tid; i < n; i += 1024) D.x[i] = s_x[i];
+}
+
+// Backward substitution past CMAX_LARGE (maps of more than 1024 free KeyFrames), right-looking by
+// block, one launch per block from the last: every workgroup forms x_bi = L_bi,bi^-T y'_bi (y' =
+// y less the contributions of the blocks already solved; 32 x 32 from Linv, redundantly per
+// workgroup) and subtracts L_bi,u^T x_bi from y'_u for its share of the columns u left of the block,
+// inside the envelope.  y' lives in x, the solution goes to bs (free after the forward
+// substitution) and k_back_copy moves it to x.  The work is the envelope's O(n bw), spread over the
+// chip, instead of one workgroup streaming the whole triangle through LDS.
+constexpr int BSC = 256;  // columns per workgroup of k_back_step
+__global__ __launch_bounds__(BSC) void k_back_step(const LbaDev *__restrict__ Ds, int step)
+{
+    LBA_GRAPH(M_ACT);
+    const int n = 6 * D.nhp;
+    if (n <= CMAX_LARGE) return;
+    const int bi = D.nblk_red - 1 - step;
+    if (bi < 0) return;
+    const int k0 = bi * CB, nb = min(CB, n - k0);
+    const int c0 = D.blk_first[bi] * CB;  // first column of the row panel inside the envelope
+    if (bx > 0 && c0 + (bx - 1) * BSC >= k0) return;
+    __shared__ double s_rhs[CB], s_x[CB];
+    const int tid = threadIdx.x;
+    if (tid < CB) s_rhs[tid] = tid < nb ? D.x[k0 + tid] : 0.0;
+    __syncthreads();
+    if (tid < CB) {
+        double xv = 0.0;
+#pragma unroll
+        for (int r = 0; r < CB; r++) xv += D.Linv[(size_t)min(k0 + r, n - 1) * CB + tid] * s_rhs[r];
+        s_x[tid] = tid < nb ? xv : 0.0;
+        if (bx == 0 && tid < nb) D.bs[k0 + tid] = xv;
+    }
+    __syncthreads();
+    if (bx == 0) return;  // workgroup 0 solved the block; 1.. update the columns
+    const int u = c0 + (bx - 1) * BSC + tid;
+    if (u >= k0) return;
+    const double *A = D.Hs;
+    double acc = 0.0;
+#pragma unroll 8
+    for (int r = 0; r < nb; r++) acc += A[(size_t)(k0 + r) * n + u] * s_x[r];
+    D.x[u] -= acc;
+}
+__global__ __launch_bounds__(EB) void k_back_copy(const LbaDev *__restrict__ Ds)
+{
+    LBA_GRAPH(M_ACT);
+    const int n = 6 * D.nhp;
+    if (n <= CMAX_LARGE) return;
+    const int i = bx * EB + threadIdx.x;
+    if (i < n) D.x[i] = D.bs[i];
 }
 
 // landmark back-substitution + new estimates + LM scale partials
@@ -1183,7 +1241,7 @@ __global__ __launch_bounds__(EB) void k_update(const LbaDev *__restrict__ Ds)
     if (t < D.npt && D.point_h[t] < 0)
         for (int k = 0; k < 3; k++) point_new[3 * (size_t)t + k] = point_cur[3 * (size_t)t + k];
     const double tot = block_sum_d(sc, s);
-    if (threadIdx.x == 0) D.part[NPART + bx] = tot;
+    if (threadIdx.x == 0) D.part[D.npart + bx] = tot;
 }
 
 __global__ __launch_bounds__(EB) void k_classify(const LbaDev *__restrict__ Ds)
@@ -1210,20 +1268,27 @@ __global__ __launch_bounds__(EB) void k_classify(const LbaDev *__restrict__ Ds)
 __global__ __launch_bounds__(256) void k_step_reduce(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT | M_ERRC);
-    __shared__ double s_chi[NPART], s_sc[NPART], s_cur[NPART];
+    __shared__ double s_chi[RED_CHUNK], s_sc[RED_CHUNK], s_cur[RED_CHUNK];
     const int mode = D.ctl->mode;
     const bool act = (mode & M_ACT) != 0, errc = (mode & M_ERRC) != 0;
-    for (int i = threadIdx.x; i < D.ge; i += 256) {
-        s_chi[i] = act ? D.part[i] : 0.0;
-        s_cur[i] = errc ? D.part[3 * NPART + i] : 0.0;
-    }
-    for (int i = threadIdx.x; i < D.gu; i += 256) s_sc[i] = act ? D.part[NPART + i] : 0.0;
-    __syncthreads();
-    if (threadIdx.x != 0) return;
+    const int P = D.npart;
     double chi = 0, sc = 0, chic = 0;
-    for (int i = 0; i < D.ge; i++) chi += s_chi[i];
-    for (int i = 0; i < D.gu; i++) sc += s_sc[i];
-    for (int i = 0; i < D.ge; i++) chic += s_cur[i];
+    for (int base = 0; base < max(D.ge, D.gu); base += RED_CHUNK) {
+        const int ne = min(RED_CHUNK, max(D.ge - base, 0)), nu = min(RED_CHUNK, max(D.gu - base, 0));
+        for (int i = threadIdx.x; i < ne; i += 256) {
+            s_chi[i] = act ? D.part[base + i] : 0.0;
+            s_cur[i] = errc ? D.part[3 * P + base + i] : 0.0;
+        }
+        for (int i = threadIdx.x; i < nu; i += 256) s_sc[i] = act ? D.part[P + base + i] : 0.0;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int i = 0; i < ne; i++) chi += s_chi[i];
+            for (int i = 0; i < nu; i++) sc += s_sc[i];
+            for (int i = 0; i < ne; i++) chic += s_cur[i];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
     D.out[0] = chi;
     D.out[1] = sc;
     D.out[2] = (D.nhp > 0 && act) ? (double)D.flag[0] : 1.0;
@@ -1251,7 +1316,8 @@ struct LbaHost {
     const osg_ba_graph *G = nullptr;
     osg_ba_result *R = nullptr;
     int np = 0, npt = 0, ne = 0, nhp = 0, nhl = 0, nblk = 0, npairs = 0, nchunks = 0;
-    int ge = 0, gl = 0, gu = 0, nblk_red = 0;
+    int ge = 0, gl = 0, gu = 0, nblk_red = 0, npart = 64;
+    std::vector<int32_t> blk_first, blk_last;  // envelope of the reduced system by row block (see LbaDev)
     bool trivial = false;  // nothing to optimise: the estimates are returned unchanged
     std::vector<int32_t> pose_h, hp_pose, point_h, hl_point, lm_e_start, lm_e, lm_perm, lm_b_start, blk_pose, edge_blk, blk_lm,
         blk_e_start, blk_e, hp_e_start, hp_e, hp_b_start, hp_b, pair_start, pair_ab, chunk_start, pair_chunk,
@@ -1273,6 +1339,9 @@ struct LbaHost {
         R = nullptr;
         np = npt = ne = nhp = nhl = nblk = npairs = nchunks = n_rs = 0;
         ge = gl = gu = nblk_red = 0;
+        npart = 64;
+        blk_first.clear();
+        blk_last.clear();
         trivial = false;
         hp_pose.clear();
         hl_point.clear();
@@ -1335,9 +1404,8 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
         H.trivial = true;
         return OSG_OK;
     }
-    if (6 * nhp > CMAX_LARGE)
-        return osg_set_error(ctx, OSG_E_INVALID, "%d free poses exceed the dense reduced-system limit (%d)", nhp,
-                             CMAX_LARGE / 6);
+    if (6 * (size_t)nhp * 6 * (size_t)nhp > (size_t(1) << 31))
+        return osg_set_error(ctx, OSG_E_INVALID, "%d free poses: the dense reduced system would exceed 2^31 entries", nhp);
     const std::vector<int32_t> &pose_h = H.pose_h, &point_h = H.point_h;
     // edges per landmark (stable in edge order)
     H.lm_e_start.assign(nhl + 1, 0);
@@ -1437,6 +1505,29 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
                     H.pair_ab[2 * k + 1] = b;
                 }
     }
+    // envelope of the reduced system (used past CMAX): a pose row's first nonzero pose column is the
+    // smallest pose it shares a landmark with; row block t starts at the smallest over its rows
+    {
+        std::vector<int32_t> minJ(nhp);
+        for (int i = 0; i < nhp; i++) minJ[i] = i;
+        for (int l = 0; l < nhl; l++) {
+            int pm = INT32_MAX;
+            for (int a = H.lm_b_start[l]; a < H.lm_b_start[l + 1]; a++) pm = std::min(pm, (int)H.blk_pose[a]);
+            for (int a = H.lm_b_start[l]; a < H.lm_b_start[l + 1]; a++)
+                minJ[H.blk_pose[a]] = std::min(minJ[H.blk_pose[a]], pm);
+        }
+        const int n = 6 * nhp, nb = (n + CB - 1) / CB;
+        H.blk_first.assign(nb, 0);
+        H.blk_last.assign(nb, 0);
+        for (int t = 0; t < nb; t++) {
+            int f = t;
+            for (int r = CB * t; r < std::min(n, CB * t + CB); r++) f = std::min(f, 6 * minJ[r / 6] / CB);
+            H.blk_first[t] = f;
+        }
+        for (int j = 0; j < nb; j++) H.blk_last[j] = j;
+        for (int t = 0; t < nb; t++)
+            for (int j = H.blk_first[t]; j <= t; j++) H.blk_last[j] = std::max(H.blk_last[j], t);
+    }
     // rank of each block in its pose's block list (hp_b is in block order); row segments of RS ranks
     std::vector<int32_t> blk_rank(nblk);
     for (int i = 0; i < nhp; i++)
@@ -1486,8 +1577,7 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
     H.gl = (nhl + EB - 1) / EB;
     H.gu = (std::max(std::max(nhl, np), npt) + EB - 1) / EB;
     H.nblk_red = (6 * nhp + CB - 1) / CB;
-    if (!(H.ge <= NPART && H.gu <= NPART && H.gl + nhp <= NPART))
-        return osg_set_error(ctx, OSG_E_INVALID, "graph too large for the partial buffers");
+    H.npart = (std::max(std::max(H.ge, H.gu), std::max(H.gl + nhp, 1)) + 63) & ~63;
     H.t_struct = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp0).count();
     return OSG_OK;
 }
@@ -1526,7 +1616,7 @@ void carve_state(char *base, size_t &off, const LbaHost &H, LbaDev *D, bool prof
     double *Hs = carve<double>(base, off, (size_t)sp * sp);
     double *bs = carve<double>(base, off, (size_t)sp);
     double *x = carve<double>(base, off, (size_t)sp + 3 * (size_t)nhl);
-    double *part = carve<double>(base, off, 4 * (size_t)NPART + 64);
+    double *part = carve<double>(base, off, 4 * (size_t)H.npart + 64);
     double *chunk_part = carve<double>(base, off, 36 * (size_t)std::max(H.nchunks, 1));
     double *db = carve<double>(base, off, 3 * (size_t)nhl);
     double *Linv = carve<double>(base, off, (size_t)sp * CB);
@@ -1634,7 +1724,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     struct InOff {
         size_t fixed, epose, epoint, ecam, ekind, eobs, eisig, cams, poseh, hppose, pointh, hlpoint, lmes, lme, lmperm, lmbs,
             blkpose, eblk, hpes, hpe, hpbs, hpb, pairs, pairab, chs, blklm, blkes, blke, pch, pose0, point0, erob,
-            prank, rspose, rsrank0, rscs, rsc, hprs;
+            prank, rspose, rsrank0, rscs, rsc, hprs, bfirst, blast;
     };
     std::vector<InOff> io(NA);
     for (int a = 0; a < NA; a++) {
@@ -1673,6 +1763,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         o.blke = pk.add(h.blk_e.data(), 4 * h.blk_e.size());
         o.pch = pk.add(h.pair_chunk.data(), 4 * h.pair_chunk.size());
         o.prank = pk.add(h.pair_rank.data(), 4 * h.pair_rank.size());
+        o.bfirst = pk.add(h.blk_first.data(), 4 * std::max<size_t>(h.blk_first.size(), 1));
+        o.blast = pk.add(h.blk_last.data(), 4 * std::max<size_t>(h.blk_last.size(), 1));
         o.rspose = pk.add(h.rs_pose.data(), 4 * h.rs_pose.size());
         o.rsrank0 = pk.add(h.rs_rank0.data(), 4 * h.rs_rank0.size());
         o.rscs = pk.add(h.rs_chunk_start.data(), 4 * h.rs_chunk_start.size());
@@ -1714,6 +1806,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     static const bool xcd_env = getenv("OSG_LBA_XCD") && atoi(getenv("OSG_LBA_XCD")) == 1;
     const bool xcd = xcd_env && NA >= 8;
     bool large = false;  // some graph's reduced system is past CMAX
+    bool huge = false;   // ... past CMAX_LARGE (k_back_step instead of k_chol_back_large)
     for (int a = 0; a < NA; a++) {
         const LbaHost &h = H[act[a]];
         const InOff &o = io[a];
@@ -1741,6 +1834,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         D.hub_mono = h.G->huber_mono > 0.f ? h.G->huber_mono : (float)std::sqrt(5.991);   // thHuberMono
         D.hub_stereo = h.G->huber_stereo > 0.f ? h.G->huber_stereo : (float)std::sqrt(7.815);
         large |= 6 * h.nhp > CMAX;
+        huge |= 6 * h.nhp > CMAX_LARGE;
         D.pose_h = osg_dptr<int32_t>(din, o.poseh);
         D.hp_pose = osg_dptr<int32_t>(din, o.hppose);
         D.point_h = osg_dptr<int32_t>(din, o.pointh);
@@ -1764,6 +1858,9 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         D.blk_e = osg_dptr<int32_t>(din, o.blke);
         D.pair_chunk = osg_dptr<int32_t>(din, o.pch);
         D.pair_rank = osg_dptr<int32_t>(din, o.prank);
+        D.blk_first = osg_dptr<int32_t>(din, o.bfirst);
+        D.blk_last = osg_dptr<int32_t>(din, o.blast);
+        D.npart = h.npart;
         D.n_rs = h.n_rs;
         D.rs_pose = osg_dptr<int32_t>(din, o.rspose);
         D.rs_rank0 = osg_dptr<int32_t>(din, o.rsrank0);
@@ -1849,14 +1946,35 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
             hipLaunchKernelGGL(k_schur_pairs, gx((mx_pairs * 64 + 255) / 256), dim3(256), 0, ctx->stream, d_dev);
             LBA_MARK(KT_CHOL);
             for (int jb = 0; jb < mx_red; jb++) {  // row blocks at and below the diagonal block
-                hipLaunchKernelGGL(k_chol_col, gx(mx_red - jb), dim3(256), 0, ctx->stream, d_dev, jb);
-                const int m = mx_red - jb - 1;
+                // past CMAX only the envelope's rows: grids sized by the largest reach of any graph
+                int rows = 0, m = 0;
+                for (int a = 0; a < NA; a++) {
+                    const LbaHost &h = H[act[a]];
+                    if (jb >= h.nblk_red) continue;
+                    const bool big = 6 * h.nhp > CMAX;
+                    rows = std::max(rows, big ? h.blk_last[jb] - jb + 1 : h.nblk_red - jb);
+                    if (big) m = std::max(m, h.blk_last[jb] - jb);
+                }
+                if (rows == 0) continue;
+                hipLaunchKernelGGL(k_chol_col, gx(rows), dim3(256), 0, ctx->stream, d_dev, jb);
                 if (large && m > 0)
                     hipLaunchKernelGGL(k_chol_trail, gx(m * (m + 1) / 2), dim3(256), 0, ctx->stream, d_dev, jb);
             }
             LBA_MARK(KT_BACK);
             hipLaunchKernelGGL(k_chol_back, yb, dim3(1024), 0, ctx->stream, d_dev);
             if (large) hipLaunchKernelGGL(k_chol_back_large, yb, dim3(1024), 0, ctx->stream, d_dev);
+            if (huge) {
+                for (int step = 0; step < mx_red; step++) {
+                    int cols = 0;
+                    for (int a = 0; a < NA; a++) {
+                        const LbaHost &h = H[act[a]];
+                        const int bi = h.nblk_red - 1 - step;
+                        if (6 * h.nhp > CMAX_LARGE && bi >= 0) cols = std::max(cols, CB * (bi - h.blk_first[bi]));
+                    }
+                    hipLaunchKernelGGL(k_back_step, gx(1 + (cols + BSC - 1) / BSC), dim3(BSC), 0, ctx->stream, d_dev, step);
+                }
+                hipLaunchKernelGGL(k_back_copy, gx((6 * mx_nhp + EB - 1) / EB), dim3(EB), 0, ctx->stream, d_dev);
+            }
         }
         LBA_MARK(KT_UPD);
         hipLaunchKernelGGL(k_update, gx(mx_gu), dim3(EB), 0, ctx->stream, d_dev);

@@ -501,6 +501,82 @@ def synth_gba_graph(rng, n_kf=120, n_points=20000, bRobust=False, iterations=10,
     return gba_robust_settings(G, bRobust)
 
 
+def synth_map_graph(rng, n_kf=1500, n_points=150000, spacing=0.3, k_range=(2, 6), bRobust=False, iterations=10,
+                    stereo_frac=0.0, n_levels=8):
+    """A map-scale whole-map BA (GlobalBundleAdjustemnt on a long sequence): n_kf keyframes 'spacing'
+    m apart along a 0.45 km path, looking sideways at points 4 .. 6 m away spread along it, so a
+    keyframe shares points only with its neighbours (~27 on each side) and the reduced camera
+    system is a band, as in an open trajectory without loop closures.  Each point is observed by
+    k ~ U{k_range} of the keyframes that see it; pixel noise 1 px * 1.2^octave, pose noise 1 cm /
+    0.3 deg, point noise 2 cm; the first keyframe is fixed (the map's init KeyFrame)."""
+    cam = pinhole_camera()
+    L = spacing * (n_kf - 1)
+    cx = np.arange(n_kf) * spacing
+    cy = 0.1 * np.sin(np.arange(n_kf) * 0.05)
+    yaw = np.deg2rad(rng.normal(0, 2.0, n_kf))
+    Rs = np.stack([np.array([[np.cos(a), 0, -np.sin(a)], [0, 1, 0], [np.sin(a), 0, np.cos(a)]]) for a in yaw])
+    C = np.stack([cx, cy, np.zeros(n_kf)], 1)
+    ts = -np.einsum("kij,kj->ki", Rs, C)
+    P = np.stack([rng.uniform(-1.0, L + 1.0, n_points), rng.uniform(-1.5, 1.5, n_points),
+                  rng.uniform(4.0, 6.0, n_points)], 1)
+    isig_tab = inv_level_sigma2(n_levels)
+    lev_p = np.array([1.2 ** -i for i in range(n_levels)])
+    lev_p /= lev_p.sum()
+    W = int(np.ceil(6.0 * 0.85 / spacing)) + 2  # keyframes within reach of a point
+    e_point, e_pose, e_obs, e_kind, e_lev = [], [], [], [], []
+    for p0 in range(0, n_points, 20000):
+        Pc = P[p0:p0 + 20000]
+        base = np.clip(np.round(Pc[:, 0] / spacing).astype(int) - W, 0, None)
+        cand = np.clip(base[:, None] + np.arange(2 * W + 1)[None, :], 0, n_kf - 1)  # (m, 2W+1)
+        Xc = np.einsum("mkij,mj->mki", Rs[cand], Pc) + ts[cand]
+        u = EUROC_FX * Xc[..., 0] / Xc[..., 2] + EUROC_CX
+        v = EUROC_FY * Xc[..., 1] / Xc[..., 2] + EUROC_CY
+        vis = (Xc[..., 2] > 0.5) & (u > 0) & (u < EUROC_W) & (v > 0) & (v < EUROC_H)
+        vis[:, 1:] &= cand[:, 1:] != cand[:, :-1]  # clipped duplicates
+        for m in range(len(Pc)):
+            idx = np.nonzero(vis[m])[0]
+            if len(idx) < 2:
+                continue
+            k = min(len(idx), int(rng.integers(k_range[0], k_range[1] + 1)))
+            sel = np.sort(rng.choice(idx, k, replace=False))
+            for j in sel:
+                e_point.append(p0 + m)
+                e_pose.append(cand[m, j])
+                e_obs.append((u[m, j], v[m, j], Xc[m, j, 2]))
+                e_lev.append(int(rng.choice(n_levels, p=lev_p)))
+    e_point = np.array(e_point)
+    e_pose = np.array(e_pose)
+    e_obs = np.array(e_obs)
+    e_lev = np.array(e_lev)
+    ne = len(e_point)
+    s = 1.2 ** e_lev
+    obs = np.zeros((ne, 3))
+    obs[:, 0] = e_obs[:, 0] + rng.normal(0, 1, ne) * s
+    obs[:, 1] = e_obs[:, 1] + rng.normal(0, 1, ne) * s
+    st = rng.random(ne) < stereo_frac
+    obs[:, 2] = np.where(st, obs[:, 0] - EUROC_BF / e_obs[:, 2] + rng.normal(0, 0.5, ne), 0.0)
+    used = np.unique(e_point)
+    remap = -np.ones(n_points, int)
+    remap[used] = np.arange(len(used))
+    e_point = remap[e_point]
+    P = P[used]
+    poses = []
+    for i in range(n_kf):
+        R, t = Rs[i], ts[i]
+        if i >= 1:  # about the keyframe's own centre: 0.3 deg and 1 cm
+            R = small_rotation(rng, 0.3) @ R
+            t = -R @ (C[i] + rng.normal(0, 0.01, 3))
+        poses.append(pose7(R, t))
+    Pn = (P + rng.normal(0, 0.02, P.shape)).astype(np.float32).astype(np.float64)
+    fixed = np.zeros(n_kf, np.uint8)
+    fixed[0] = 1
+    G = BAGraph(np.array(poses), fixed, Pn, e_point, e_pose, np.where(st, _abi.EDGE_STEREO, _abi.EDGE_MONO).astype(np.int8),
+                np.zeros(ne, np.int32), obs.astype(np.float32).astype(np.float64),
+                isig_tab[e_lev].astype(np.float32), [cam])
+    G.iterations = iterations
+    return gba_robust_settings(G, bRobust)
+
+
 def depth_positive(G: BAGraph, pose, point, edges):
     """isDepthPositive of the given edges: z of SE3Quat::map(X) = q X q* + t (Eigen's quaternion-vector
     product), > 0."""

@@ -222,6 +222,19 @@ def test_gba_parity(ctx, oracle, n_kf, n_pts, robust, stereo):
     assert got.chi2_final < got.chi2_initial and got.iterations >= 1
 
 
+@pytest.mark.parametrize("n_kf,n_pts", [(400, 40000), (1500, 150000)])
+def test_gba_map_scale(ctx, oracle, n_kf, n_pts):
+    """BundleAdjustment at map scale (ref:src/Optimizer.cc:2850-3237, LinearSolverEigen): keyframes
+    along a 0.45 km open path sharing points with their neighbours, so the reduced camera system is a
+    band.  400 keyframes (n = 2394) run the envelope-aware right-looking factorisation and the LDS
+    back-substitution; 1500 keyframes x 150 k points (n = 8994, 600 k edges) are past the 1024 free
+    KeyFrames the LDS back-substitution holds and take k_back_step.  Against the oracle (its LDL^T on
+    the envelope) within §5's tolerances."""
+    G = op.synth_map_graph(np.random.default_rng(4100 + n_kf), n_kf=n_kf, n_points=n_pts)
+    got, ref = check_gba(ctx, oracle, G)
+    assert got.chi2_final < 0.2 * got.chi2_initial and got.iterations >= 5
+
+
 def test_gba_and_lba_in_one_batch(ctx, oracle):
     """A LocalBA window and a whole-map BA in one lockstep batch: each equals its own call."""
     rng = np.random.default_rng(3300)
