@@ -68,7 +68,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-stream", action="store_true")
     ap.add_argument("--no-ba", action="store_true")
-    ap.add_argument("--no-gba", action="store_true", help="skip the global BA workload")
+    ap.add_argument("--no-gba", action="store_true", help="skip the global BA workloads")
+    ap.add_argument("--no-gba-map", action="store_true", help="skip the map-scale (1500 KF) global BA")
     ap.add_argument("--ba-reps", type=int, default=20)
     ap.add_argument("--ba-batch", type=int, default=64, help="C4 windows per GPU per lockstep batch")
     ap.add_argument("--ba-batch-reps", type=int, default=6)
@@ -324,6 +325,8 @@ def main():
         stage("local_ba", bench_lba)
     if not args.no_gba:
         stage("global_ba", bench_gba)
+        if not args.no_gba_map:
+            stage("global_ba_map", bench_gba_map)
 
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -554,6 +557,48 @@ def bench_gba(ctx, rank, world, dist, dev, args):
         it_cpu = _oracle()[1].lba(_oracle()[0], G).iterations
         _attach_cpu(res, _lba_worker([G]), it_cpu, "LM iterations/s", max(3.0, args.cpu_seconds * 0.5),
                     "global BA 150 KF x 20k points (oracle, dense LDL^T)", wall_key="")
+    return res
+
+
+def bench_gba_map(ctx, rank, world, dist, dev, args):
+    """SURVEY.md §8(f) rank 4 at map scale: BundleAdjustment over a 1500-KeyFrame x 150 k-point map
+    (optimizer.synth_map_graph: an open 0.45 km path, 600 k edges, reduced system n = 8994, banded).
+    Wall time of the whole call per map.  The CPU baseline is the oracle on one thread: g2o's LM is
+    single-threaded, so more cores do not speed up one map (they only run more maps)."""
+    import torch
+    from orb_slam3_comments_ghr_amd import optimizer as op
+    G = op.synth_map_graph(np.random.default_rng(0x0B5EED31 + rank), n_kf=1500, n_points=150000)
+    opt = op.Optimizer(ctx)
+    r = opt.BundleAdjustment(G)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    reps = 2
+    t0 = time.perf_counter()
+    iters = 0
+    for _ in range(reps):
+        r = opt.BundleAdjustment(G)
+        iters += r.iterations
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    el, iters = job_totals(el, iters, world, dist if world > 1 else None, dev)
+    n_free = int(len(G.pose) - G.pose_fixed.sum())
+    res = {"metric": "GlobalBA iters/s", "value": round(iters / el, 1), "unit": "LM iterations/s",
+           "s_per_gba": round(el / reps, 3), "iterations_per_gba": r.iterations, "trials_per_gba": r.trials,
+           "workload": f"global BA at map scale: {len(G.pose)} KF x {len(G.point)} points x {len(G.e_point)} edges, "
+                       f"reduced system {6 * n_free} (banded: an open trajectory), optimize({G.iterations}), no Huber",
+           "n_gpus": world, "dtype": "f64", "scaling": "weak", "parallelism": f"replicas x{world} (one map per GPU)"}
+    if rank == 0 and world == 1 and not args.no_cpu:
+        orc, oc = _oracle()
+        t1 = time.perf_counter()
+        rc = oc.lba(orc, G)
+        tc = time.perf_counter() - t1
+        res["cpu_baseline"] = {"value": round(rc.iterations / tc, 2), "unit": "LM iterations/s", "cores": 1,
+                               "kind": "port", "seconds_per_gba": round(tc, 2),
+                               "sample": "one call of the oracle on the same map (envelope LDL^T; g2o's LM is "
+                                         "single-threaded, so one map does not use more cores)"}
+        res["speedup_vs_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
+        res["speedup_per_map_seconds"] = round(tc / (el / reps), 1)
     return res
 
 
