@@ -641,10 +641,11 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // read as zero; tile entries past n become the identity (keeps the padded factorisation finite).
 constexpr int LU_STEPS = CMAX / 64;  // 16-wide steps per wave at most
 
+// do_t = false: the diagonal tile is not needed (k_chol_lba has it already); sX is unchanged by it.
 __device__ __forceinline__ void tile_left_update2(const double *__restrict__ A, int n, int C0, int R0, int K,
                                                   const double *__restrict__ y,
                                                   double (*sT)[CB + 1], double (*sX)[CB + 1],
-                                                  double (*sP)[CB][CB + 1], double (*s_rp)[CB])
+                                                  double (*sP)[CB][CB + 1], double (*s_rp)[CB], bool do_t = true)
 {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     const bool two = R0 >= 0;
@@ -699,12 +700,13 @@ __device__ __forceinline__ void tile_left_update2(const double *__restrict__ A, 
             ja[0][2] = z0 ? 0.0 : j0[s][1].x; ja[0][3] = z0 ? 0.0 : j0[s][1].y;
             ja[1][0] = z1 ? 0.0 : j1[s][0].x; ja[1][1] = z1 ? 0.0 : j1[s][0].y;
             ja[1][2] = z1 ? 0.0 : j1[s][1].x; ja[1][3] = z1 ? 0.0 : j1[s][1].y;
+            if (do_t)
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                accT[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(ja[0][i], ja[0][i], accT[0][0], 0, 0, 0);
-                accT[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(ja[1][i], ja[0][i], accT[1][0], 0, 0, 0);
-                accT[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(ja[1][i], ja[1][i], accT[1][1], 0, 0, 0);
-            }
+                for (int i = 0; i < 4; i++) {
+                    accT[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(ja[0][i], ja[0][i], accT[0][0], 0, 0, 0);
+                    accT[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(ja[1][i], ja[0][i], accT[1][0], 0, 0, 0);
+                    accT[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(ja[1][i], ja[1][i], accT[1][1], 0, 0, 0);
+                }
             if (y) {
                 const double yv[4] = {yy[s][0].x, yy[s][0].y, yy[s][1].x, yy[s][1].y};
 #pragma unroll
@@ -739,21 +741,23 @@ __device__ __forceinline__ void tile_left_update2(const double *__restrict__ A, 
             s_rp[w][16 + l] = rp1;
         }
     }
-    // diagonal tile: lower quadrants only (the upper one mirrors (1,0))
+    if (do_t) {
+        // diagonal tile: lower quadrants only (the upper one mirrors (1,0))
 #pragma unroll
-    for (int a = 0; a < 2; a++)
+        for (int a = 0; a < 2; a++)
 #pragma unroll
-        for (int b = 0; b < 2; b++) {
-            if (b > a) continue;
+            for (int b = 0; b < 2; b++) {
+                if (b > a) continue;
 #pragma unroll
-            for (int q = 0; q < 4; q++) sP[w][16 * a + (l >> 4) + 4 * q][16 * b + (l & 15)] = accT[a][b][q];
+                for (int q = 0; q < 4; q++) sP[w][16 * a + (l >> 4) + 4 * q][16 * b + (l & 15)] = accT[a][b][q];
+            }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int e = threadIdx.x + 256 * q, r = e >> 5, c = e & 31;
+            const double sum = (c <= r) ? ((sP[0][r][c] + sP[1][r][c]) + sP[2][r][c]) + sP[3][r][c] : 0.0;
+            sT[r][c] = (C0 + r < n && C0 + c < n) ? aT[q] - sum : (r == c ? 1.0 : 0.0);
         }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int e = threadIdx.x + 256 * q, r = e >> 5, c = e & 31;
-        const double sum = (c <= r) ? ((sP[0][r][c] + sP[1][r][c]) + sP[2][r][c]) + sP[3][r][c] : 0.0;
-        sT[r][c] = (C0 + r < n && C0 + c < n) ? aT[q] - sum : (r == c ? 1.0 : 0.0);
     }
     if (!two) return;
     __syncthreads();
@@ -789,63 +793,48 @@ __device__ __forceinline__ double rcp_nr(double d)
 //     applied to the identity give M = Lt^-1, so L_jj^-1 = D^-1/2 M without a triangular solve.
 //  3. workgroup 0: L_jj^-1 -> Linv, y_j = L_jj^-1 rhs -> x;  workgroup t > 0: L_tj = X L_jj^-T
 //     (MFMA) written over A_tj.  A_jj itself is never written (nothing downstream needs L_jj).
-__global__ __launch_bounds__(256) void k_chol_col(const LbaDev *__restrict__ Ds, int j)
+// The LDS of one column step (k_chol_col, k_chol_lba)
+struct CholLds {
+    double sP[4][CB][CB + 1];  // per-wave partial tiles
+    double sG[CB][CB + 1];     // T under elimination
+    double sM[CB][CB + 1];     // Lt^-1, then L_jj^-1
+    double sX[CB][CB + 1];     // X (row blocks below)
+    double s_rsq[CB];          // D^-1/2
+    double s_d[CB];            // pivots
+    double s_rp[4][CB];
+    double s_rhs[CB];
+};
+
+// Step 2: T (in sG) = Lt D Lt^T by elimination in LDS, one barrier per two columns; the same row
+// operations applied to the identity in sM give M = Lt^-1, then L_jj^-1 = D^-1/2 M.  Returns the
+// pivots' positivity.
+//   Elimination two columns per barrier (2x2 pivot block c, c + 1, redundantly in every thread):
+//   d0 = g_cc, l10 = g_c+1,c / d0, d1 = g_c+1,c+1 - g_c+1,c l10, g'_i,c+1 = g_i,c+1 - g_ic l10
+//   G: g_i,jj -= g_ic g_jj,c / d0 + g'_i,c+1 g'_jj,c+1 / d1        (c + 1 < jj <= i)
+//   M: m_i,m  -= g_ic / d0 m_c,m + g'_i,c+1 / d1 (m_c+1,m - l10 m_c,m)  (i > c + 1, m <= c + 1)
+//      m_c+1,m -= l10 m_c,m (m <= c): written one step later (other threads read row c + 1 now;
+//      nothing reads it in the next step).  Pivots go to s_d (the diagonal of G is read now).
+// An odd nb pairs its last column with padding column nb (identity: l10 = 0, d1 = 1).
+__device__ __forceinline__ int chol_factor_diag(CholLds &L, int nb)
 {
-    LBA_GRAPH(M_ACT);
-    if (j >= D.nblk_red || bx >= D.nblk_red - j) return;
-    // past CMAX a row block outside the envelope has an all-zero tile here, and its L_tj stays zero
-    if (6 * D.nhp > CMAX && bx > 0 && (j + bx > D.blk_last[j] || D.blk_first[j + bx] > j)) return;
-    __shared__ double sP[4][CB][CB + 1];  // per-wave partial tiles
-    __shared__ double sG[CB][CB + 1];     // T under elimination
-    __shared__ double sM[CB][CB + 1];     // Lt^-1, then L_jj^-1
-    __shared__ double sX[CB][CB + 1];     // X (t > 0)
-    __shared__ double s_rsq[CB];          // D^-1/2
-    __shared__ double s_d[CB];            // pivots
-    __shared__ double s_rp[4][CB];
-    __shared__ double s_rhs[CB];
-    const int n = 6 * D.nhp;
-    const double *A = D.Hs;
-    const int k0 = j * CB;
-    const int nb = min(CB, n - k0);
-    const int t = bx;
     const int tid = threadIdx.x;
-    const int R0 = k0 + t * CB;
-    unsigned long long *ts = (D.tstamp && t < 2 && tid == 0 && j < 32) ? D.tstamp + 8 * (2 * j + t) : nullptr;
-    if (ts) ts[0] = wall_clock64();
-
-    const double bj = (t == 0 && tid < nb) ? D.bs[k0 + tid] : 0.0;
-    for (int e = tid; e < CB * (CB + 1); e += 256) (&sM[0][0])[e] = 0.0;
-    // past CMAX the system is factored right-looking: k_chol_trail has already applied every earlier
-    // column block to these tiles and to b, so nothing is left to subtract (K = 0)
-    tile_left_update2(A, n, k0, t > 0 ? R0 : -1, n > CMAX ? 0 : k0, t == 0 ? D.x : nullptr, sG, sX, sP, s_rp);
-    if (tid < CB) sM[tid][tid] = 1.0;
-    __syncthreads();
-    if (ts) ts[1] = wall_clock64();
-
-    // Elimination two columns per barrier (2x2 pivot block c, c + 1, redundantly in every thread):
-    //   d0 = g_cc, l10 = g_c+1,c / d0, d1 = g_c+1,c+1 - g_c+1,c l10, g'_i,c+1 = g_i,c+1 - g_ic l10
-    //   G: g_i,jj -= g_ic g_jj,c / d0 + g'_i,c+1 g'_jj,c+1 / d1        (c + 1 < jj <= i)
-    //   M: m_i,m  -= g_ic / d0 m_c,m + g'_i,c+1 / d1 (m_c+1,m - l10 m_c,m)  (i > c + 1, m <= c + 1)
-    //      m_c+1,m -= l10 m_c,m (m <= c): written one step later (other threads read row c + 1 now;
-    //      nothing reads it in the next step).  Pivots go to s_d (the diagonal of G is read now).
-    // An odd nb pairs its last column with padding column nb (identity: l10 = 0, d1 = 1).
     const int jj = tid & 31, ib = tid >> 5;
     int ok = 1;
     double defer_val = 0.0;
     int defer_at = -1;  // index into sM of the deferred row-(c+1) value
     for (int c = 0; c < nb; c += 2) {
-        if (defer_at >= 0) (&sM[0][0])[defer_at] = defer_val;
+        if (defer_at >= 0) (&L.sM[0][0])[defer_at] = defer_val;
         defer_at = -1;
-        const double d0 = sG[c][c], e = sG[c + 1][c], d1r = sG[c + 1][c + 1];
-        const double gj0 = sG[jj][c], gj1 = sG[jj][c + 1];
-        const double mc = sM[c][jj], mc1 = sM[c + 1][jj];
-        double *const base = (jj > c + 1) ? &sG[0][0] : &sM[0][0];
+        const double d0 = L.sG[c][c], e = L.sG[c + 1][c], d1r = L.sG[c + 1][c + 1];
+        const double gj0 = L.sG[jj][c], gj1 = L.sG[jj][c + 1];
+        const double mc = L.sM[c][jj], mc1 = L.sM[c + 1][jj];
+        double *const base = (jj > c + 1) ? &L.sG[0][0] : &L.sM[0][0];
         double gi0[4], gi1[4], cur[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const int i = ib + 8 * q;
-            gi0[q] = sG[i][c];
-            gi1[q] = sG[i][c + 1];
+            gi0[q] = L.sG[i][c];
+            gi1[q] = L.sG[i][c + 1];
             cur[q] = base[i * (CB + 1) + jj];
         }
         const double r0 = rcp_nr(d0 > 0.0 ? d0 : 1.0);
@@ -854,8 +843,8 @@ __global__ __launch_bounds__(256) void k_chol_col(const LbaDev *__restrict__ Ds,
         ok &= (d0 > 0.0) & (d1 > 0.0);
         const double r1 = rcp_nr(d1 > 0.0 ? d1 : 1.0);
         if (tid == 0) {
-            s_d[c] = d0;
-            s_d[c + 1] = d1;
+            L.s_d[c] = d0;
+            L.s_d[c + 1] = d1;
         }
         const double gj1p = gj1 - gj0 * l10;
         const double mc1p = mc1 - l10 * mc;
@@ -875,62 +864,141 @@ __global__ __launch_bounds__(256) void k_chol_col(const LbaDev *__restrict__ Ds,
         }
         __syncthreads();
     }
-    if (defer_at >= 0) (&sM[0][0])[defer_at] = defer_val;
+    if (defer_at >= 0) (&L.sM[0][0])[defer_at] = defer_val;
     __syncthreads();
     if (tid < CB) {
-        const double d = s_d[tid];
-        s_rsq[tid] = (tid < nb && d > 0.0) ? 1.0 / sqrt(d) : 1.0;
+        const double d = L.s_d[tid];
+        L.s_rsq[tid] = (tid < nb && d > 0.0) ? 1.0 / sqrt(d) : 1.0;
     }
     __syncthreads();
     // L_jj^-1 = D^-1/2 M (lower)
     for (int e = tid; e < CB * CB; e += 256) {
         const int i = e >> 5, m = e & 31;
-        sM[i][m] = (m <= i) ? sM[i][m] * s_rsq[i] : 0.0;
+        L.sM[i][m] = (m <= i) ? L.sM[i][m] * L.s_rsq[i] : 0.0;
     }
     __syncthreads();
-    if (ts) ts[2] = wall_clock64();
+    return ok;
+}
 
-    if (t == 0) {
-        if (tid == 0 && !ok) D.flag[0] = 0;
-        for (int e = tid; e < CB * CB; e += 256) {
-            const int r = e >> 5, c = e & 31;
-            if (k0 + r < n) D.Linv[(size_t)(k0 + r) * CB + c] = sM[r][c];
-        }
-        if (tid < CB) s_rhs[tid] = (tid < nb) ? bj - (((s_rp[0][tid] + s_rp[1][tid]) + s_rp[2][tid]) + s_rp[3][tid]) : 0.0;
-        __syncthreads();
-        // y_i = sum_{m <= i} Linv[i][m] rhs_m, 8 threads per row
-        {
-            const int i = tid >> 3, p = tid & 7;
-            double acc = 0.0;
-#pragma unroll
-            for (int q = 0; q < 4; q++) acc += sM[i][p + 8 * q] * s_rhs[p + 8 * q];
-            acc += __shfl_xor(acc, 1);
-            acc += __shfl_xor(acc, 2);
-            acc += __shfl_xor(acc, 4);
-            if (p == 0 && i < nb) D.x[k0 + i] = acc;
-        }
-        if (ts) ts[3] = ts[4] = wall_clock64();
-        return;
+// Step 3 of the diagonal role: L_jj^-1 -> Linv, y_j = L_jj^-1 (b_j - sum_m L_jm y_m) -> x
+__device__ __forceinline__ void chol_diag_out(const LbaDev &D, CholLds &L, int k0, int nb, int n, double bj, int ok)
+{
+    const int tid = threadIdx.x;
+    if (tid == 0 && !ok) D.flag[0] = 0;
+    for (int e = tid; e < CB * CB; e += 256) {
+        const int r = e >> 5, c = e & 31;
+        if (k0 + r < n) D.Linv[(size_t)(k0 + r) * CB + c] = L.sM[r][c];
     }
-    // L_tj = X L_jj^-T on MFMA: quadrant (qr, qc) per wave, A = X rows, B[k][c] = Linv[c][k]
-    {
-        const int w = tid >> 6, l = tid & 63;
-        const int qr = (w >> 1) * 16, qc = (w & 1) * 16;
-        d4 acc = {0.0, 0.0, 0.0, 0.0};
+    if (tid < CB)
+        L.s_rhs[tid] = (tid < nb) ? bj - (((L.s_rp[0][tid] + L.s_rp[1][tid]) + L.s_rp[2][tid]) + L.s_rp[3][tid]) : 0.0;
+    __syncthreads();
+    // y_i = sum_{m <= i} Linv[i][m] rhs_m, 8 threads per row
+    const int i = tid >> 3, p = tid & 7;
+    double acc = 0.0;
 #pragma unroll
-        for (int ks = 0; ks < CB / 4; ks++) {
-            const int k = 4 * ks + (l >> 4);
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sX[qr + (l & 15)][k], sM[qc + (l & 15)][k], acc, 0, 0, 0);
-        }
-        const int c = qc + (l & 15);
-        double *Aw = D.Hs;
+    for (int q = 0; q < 4; q++) acc += L.sM[i][p + 8 * q] * L.s_rhs[p + 8 * q];
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    acc += __shfl_xor(acc, 4);
+    if (p == 0 && i < nb) D.x[k0 + i] = acc;
+}
+
+// Step 3 of a row-block role: L_tj = X L_jj^-T on MFMA, quadrant (qr, qc) per wave, A = X rows,
+// B[k][c] = Linv[c][k], written over A_tj
+__device__ __forceinline__ void chol_offdiag_out(const LbaDev &D, CholLds &L, int k0, int R0, int nb, int n)
+{
+    const int tid = threadIdx.x;
+    const int w = tid >> 6, l = tid & 63;
+    const int qr = (w >> 1) * 16, qc = (w & 1) * 16;
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int r = qr + (l >> 4) + 4 * q;
-            if (R0 + r < n && c < nb) Aw[(size_t)(R0 + r) * n + k0 + c] = acc[q];
-        }
+    for (int ks = 0; ks < CB / 4; ks++) {
+        const int k = 4 * ks + (l >> 4);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(L.sX[qr + (l & 15)][k], L.sM[qc + (l & 15)][k], acc, 0, 0, 0);
     }
+    const int c = qc + (l & 15);
+    double *Aw = D.Hs;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int r = qr + (l >> 4) + 4 * q;
+        if (R0 + r < n && c < nb) Aw[(size_t)(R0 + r) * n + k0 + c] = acc[q];
+    }
+}
+
+// Column block j (rows/cols k0 = 32 j ..), left-looking: every previous column block is final.
+//  1. T = A_jj - sum_{m < k0} L_jm L_jm^T (every workgroup) and, in workgroup t > 0,
+//     X = A_tj - sum_{m < k0} L_tm L_jm^T (tile_left_update2, FP64 MFMA); workgroup 0 also
+//     reduces b_j - sum_{m < k0} L_jm y_m from the same operand registers.
+//  2. chol_factor_diag: T = Lt D Lt^T, L_jj^-1 = D^-1/2 Lt^-1 without a triangular solve.
+//  3. workgroup 0: chol_diag_out;  workgroup t > 0: chol_offdiag_out.  A_jj itself is never
+//     written (nothing downstream needs L_jj).
+// skip_small: graphs of n <= CMAX are factored by k_chol_lba instead.
+__global__ __launch_bounds__(256) void k_chol_col(const LbaDev *__restrict__ Ds, int j, int skip_small)
+{
+    LBA_GRAPH(M_ACT);
+    if (j >= D.nblk_red || bx >= D.nblk_red - j) return;
+    if (skip_small && 6 * D.nhp <= CMAX) return;
+    // past CMAX a row block outside the envelope has an all-zero tile here, and its L_tj stays zero
+    if (6 * D.nhp > CMAX && bx > 0 && (j + bx > D.blk_last[j] || D.blk_first[j + bx] > j)) return;
+    __shared__ CholLds L;
+    const int n = 6 * D.nhp;
+    const double *A = D.Hs;
+    const int k0 = j * CB;
+    const int nb = min(CB, n - k0);
+    const int t = bx;
+    const int tid = threadIdx.x;
+    const int R0 = k0 + t * CB;
+    unsigned long long *ts = (D.tstamp && t < 2 && tid == 0 && j < 32) ? D.tstamp + 8 * (2 * j + t) : nullptr;
+    if (ts) ts[0] = wall_clock64();
+
+    const double bj = (t == 0 && tid < nb) ? D.bs[k0 + tid] : 0.0;
+    for (int e = tid; e < CB * (CB + 1); e += 256) (&L.sM[0][0])[e] = 0.0;
+    // past CMAX the system is factored right-looking: k_chol_trail has already applied every earlier
+    // column block to these tiles and to b, so nothing is left to subtract (K = 0)
+    tile_left_update2(A, n, k0, t > 0 ? R0 : -1, n > CMAX ? 0 : k0, t == 0 ? D.x : nullptr, L.sG, L.sX, L.sP, L.s_rp);
+    if (tid < CB) L.sM[tid][tid] = 1.0;
+    __syncthreads();
+    if (ts) ts[1] = wall_clock64();
+    const int ok = chol_factor_diag(L, nb);
+    if (ts) ts[2] = wall_clock64();
+    if (t == 0) chol_diag_out(D, L, k0, nb, n, bj, ok);
+    else chol_offdiag_out(D, L, k0, R0, nb, n);
     if (ts) ts[3] = ts[4] = wall_clock64();
+}
+
+// The LocalBundleAdjustment-sized factorisation (n <= CMAX) in one launch: one workgroup per graph
+// walks the column blocks itself, factoring each diagonal tile once and then its row blocks one by
+// one, with the same tile updates, elimination and products as the k_chol_col launches (so the
+// same L, Linv and y), instead of one launch per column block with the diagonal refactored in every
+// row-block workgroup.
+__global__ __launch_bounds__(256) void k_chol_lba(const LbaDev *__restrict__ Ds)
+{
+    LBA_GRAPH(M_ACT);
+    const int n = 6 * D.nhp;
+    if (n == 0 || n > CMAX) return;
+    __shared__ CholLds L;
+    const double *A = D.Hs;
+    const int tid = threadIdx.x;
+    const int nblk = D.nblk_red;
+    for (int j = 0; j < nblk; j++) {
+        const int k0 = j * CB;
+        const int nb = min(CB, n - k0);
+        const double bj = tid < nb ? D.bs[k0 + tid] : 0.0;
+        for (int e = tid; e < CB * (CB + 1); e += 256) (&L.sM[0][0])[e] = 0.0;
+        tile_left_update2(A, n, k0, -1, k0, D.x, L.sG, L.sX, L.sP, L.s_rp);
+        if (tid < CB) L.sM[tid][tid] = 1.0;
+        __syncthreads();
+        const int ok = chol_factor_diag(L, nb);
+        chol_diag_out(D, L, k0, nb, n, bj, ok);
+        for (int t = 1; j + t < nblk; t++) {
+            const int R0 = k0 + t * CB;
+            __syncthreads();  // sX / sP are rewritten
+            tile_left_update2(A, n, k0, R0, k0, nullptr, L.sG, L.sX, L.sP, L.s_rp, false);
+            __syncthreads();
+            chol_offdiag_out(D, L, k0, R0, nb, n);
+        }
+        __syncthreads();  // this column's L tiles and y_j are read by the next column's updates
+    }
 }
 
 // Backward substitution L^T x = y (y in x after the column launches), one 1024-thread
@@ -1807,6 +1875,10 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     const bool xcd = xcd_env && NA >= 8;
     bool large = false;  // some graph's reduced system is past CMAX
     bool huge = false;   // ... past CMAX_LARGE (k_back_step instead of k_chol_back_large)
+    // LocalBA-sized systems: one k_chol_lba launch instead of a k_chol_col launch per column block
+    // (OSG_LBA_CHOL=0: the per-column launches, for A/B measurements)
+    const char *lce = getenv("OSG_LBA_CHOL");  // read per call: tests compare the two
+    const bool lba_chol = !(lce && atoi(lce) == 0);
     for (int a = 0; a < NA; a++) {
         const LbaHost &h = H[act[a]];
         const InOff &o = io[a];
@@ -1945,6 +2017,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
             LBA_MARK(KT_SPAIRS);
             hipLaunchKernelGGL(k_schur_pairs, gx((mx_pairs * 64 + 255) / 256), dim3(256), 0, ctx->stream, d_dev);
             LBA_MARK(KT_CHOL);
+            if (lba_chol) hipLaunchKernelGGL(k_chol_lba, yb, dim3(256), 0, ctx->stream, d_dev);
             for (int jb = 0; jb < mx_red; jb++) {  // row blocks at and below the diagonal block
                 // past CMAX only the envelope's rows: grids sized by the largest reach of any graph
                 int rows = 0, m = 0;
@@ -1955,8 +2028,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
                     rows = std::max(rows, big ? h.blk_last[jb] - jb + 1 : h.nblk_red - jb);
                     if (big) m = std::max(m, h.blk_last[jb] - jb);
                 }
-                if (rows == 0) continue;
-                hipLaunchKernelGGL(k_chol_col, gx(rows), dim3(256), 0, ctx->stream, d_dev, jb);
+                if (rows == 0 || (lba_chol && !large)) continue;
+                hipLaunchKernelGGL(k_chol_col, gx(rows), dim3(256), 0, ctx->stream, d_dev, jb, lba_chol ? 1 : 0);
                 if (large && m > 0)
                     hipLaunchKernelGGL(k_chol_trail, gx(m * (m + 1) / 2), dim3(256), 0, ctx->stream, d_dev, jb);
             }
