@@ -641,11 +641,10 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // read as zero; tile entries past n become the identity (keeps the padded factorisation finite).
 constexpr int LU_STEPS = CMAX / 64;  // 16-wide steps per wave at most
 
-// do_t = false: the diagonal tile is not needed (k_chol_lba has it already); sX is unchanged by it.
 __device__ __forceinline__ void tile_left_update2(const double *__restrict__ A, int n, int C0, int R0, int K,
                                                   const double *__restrict__ y,
                                                   double (*sT)[CB + 1], double (*sX)[CB + 1],
-                                                  double (*sP)[CB][CB + 1], double (*s_rp)[CB], bool do_t = true)
+                                                  double (*sP)[CB][CB + 1], double (*s_rp)[CB])
 {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     const bool two = R0 >= 0;
@@ -700,13 +699,12 @@ __device__ __forceinline__ void tile_left_update2(const double *__restrict__ A, 
             ja[0][2] = z0 ? 0.0 : j0[s][1].x; ja[0][3] = z0 ? 0.0 : j0[s][1].y;
             ja[1][0] = z1 ? 0.0 : j1[s][0].x; ja[1][1] = z1 ? 0.0 : j1[s][0].y;
             ja[1][2] = z1 ? 0.0 : j1[s][1].x; ja[1][3] = z1 ? 0.0 : j1[s][1].y;
-            if (do_t)
 #pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    accT[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(ja[0][i], ja[0][i], accT[0][0], 0, 0, 0);
-                    accT[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(ja[1][i], ja[0][i], accT[1][0], 0, 0, 0);
-                    accT[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(ja[1][i], ja[1][i], accT[1][1], 0, 0, 0);
-                }
+            for (int i = 0; i < 4; i++) {
+                accT[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(ja[0][i], ja[0][i], accT[0][0], 0, 0, 0);
+                accT[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(ja[1][i], ja[0][i], accT[1][0], 0, 0, 0);
+                accT[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(ja[1][i], ja[1][i], accT[1][1], 0, 0, 0);
+            }
             if (y) {
                 const double yv[4] = {yy[s][0].x, yy[s][0].y, yy[s][1].x, yy[s][1].y};
 #pragma unroll
@@ -741,23 +739,21 @@ __device__ __forceinline__ void tile_left_update2(const double *__restrict__ A, 
             s_rp[w][16 + l] = rp1;
         }
     }
-    if (do_t) {
-        // diagonal tile: lower quadrants only (the upper one mirrors (1,0))
+    // diagonal tile: lower quadrants only (the upper one mirrors (1,0))
 #pragma unroll
-        for (int a = 0; a < 2; a++)
+    for (int a = 0; a < 2; a++)
 #pragma unroll
-            for (int b = 0; b < 2; b++) {
-                if (b > a) continue;
+        for (int b = 0; b < 2; b++) {
+            if (b > a) continue;
 #pragma unroll
-                for (int q = 0; q < 4; q++) sP[w][16 * a + (l >> 4) + 4 * q][16 * b + (l & 15)] = accT[a][b][q];
-            }
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int e = threadIdx.x + 256 * q, r = e >> 5, c = e & 31;
-            const double sum = (c <= r) ? ((sP[0][r][c] + sP[1][r][c]) + sP[2][r][c]) + sP[3][r][c] : 0.0;
-            sT[r][c] = (C0 + r < n && C0 + c < n) ? aT[q] - sum : (r == c ? 1.0 : 0.0);
+            for (int q = 0; q < 4; q++) sP[w][16 * a + (l >> 4) + 4 * q][16 * b + (l & 15)] = accT[a][b][q];
         }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int e = threadIdx.x + 256 * q, r = e >> 5, c = e & 31;
+        const double sum = (c <= r) ? ((sP[0][r][c] + sP[1][r][c]) + sP[2][r][c]) + sP[3][r][c] : 0.0;
+        sT[r][c] = (C0 + r < n && C0 + c < n) ? aT[q] - sum : (r == c ? 1.0 : 0.0);
     }
     if (!two) return;
     __syncthreads();
@@ -932,12 +928,10 @@ __device__ __forceinline__ void chol_offdiag_out(const LbaDev &D, CholLds &L, in
 //  2. chol_factor_diag: T = Lt D Lt^T, L_jj^-1 = D^-1/2 Lt^-1 without a triangular solve.
 //  3. workgroup 0: chol_diag_out;  workgroup t > 0: chol_offdiag_out.  A_jj itself is never
 //     written (nothing downstream needs L_jj).
-// skip_small: graphs of n <= CMAX are factored by k_chol_lba instead.
-__global__ __launch_bounds__(256) void k_chol_col(const LbaDev *__restrict__ Ds, int j, int skip_small)
+__global__ __launch_bounds__(256) void k_chol_col(const LbaDev *__restrict__ Ds, int j)
 {
     LBA_GRAPH(M_ACT);
     if (j >= D.nblk_red || bx >= D.nblk_red - j) return;
-    if (skip_small && 6 * D.nhp <= CMAX) return;
     // past CMAX a row block outside the envelope has an all-zero tile here, and its L_tj stays zero
     if (6 * D.nhp > CMAX && bx > 0 && (j + bx > D.blk_last[j] || D.blk_first[j + bx] > j)) return;
     __shared__ CholLds L;
@@ -964,41 +958,6 @@ __global__ __launch_bounds__(256) void k_chol_col(const LbaDev *__restrict__ Ds,
     if (t == 0) chol_diag_out(D, L, k0, nb, n, bj, ok);
     else chol_offdiag_out(D, L, k0, R0, nb, n);
     if (ts) ts[3] = ts[4] = wall_clock64();
-}
-
-// The LocalBundleAdjustment-sized factorisation (n <= CMAX) in one launch: one workgroup per graph
-// walks the column blocks itself, factoring each diagonal tile once and then its row blocks one by
-// one, with the same tile updates, elimination and products as the k_chol_col launches (so the
-// same L, Linv and y), instead of one launch per column block with the diagonal refactored in every
-// row-block workgroup.
-__global__ __launch_bounds__(256) void k_chol_lba(const LbaDev *__restrict__ Ds)
-{
-    LBA_GRAPH(M_ACT);
-    const int n = 6 * D.nhp;
-    if (n == 0 || n > CMAX) return;
-    __shared__ CholLds L;
-    const double *A = D.Hs;
-    const int tid = threadIdx.x;
-    const int nblk = D.nblk_red;
-    for (int j = 0; j < nblk; j++) {
-        const int k0 = j * CB;
-        const int nb = min(CB, n - k0);
-        const double bj = tid < nb ? D.bs[k0 + tid] : 0.0;
-        for (int e = tid; e < CB * (CB + 1); e += 256) (&L.sM[0][0])[e] = 0.0;
-        tile_left_update2(A, n, k0, -1, k0, D.x, L.sG, L.sX, L.sP, L.s_rp);
-        if (tid < CB) L.sM[tid][tid] = 1.0;
-        __syncthreads();
-        const int ok = chol_factor_diag(L, nb);
-        chol_diag_out(D, L, k0, nb, n, bj, ok);
-        for (int t = 1; j + t < nblk; t++) {
-            const int R0 = k0 + t * CB;
-            __syncthreads();  // sX / sP are rewritten
-            tile_left_update2(A, n, k0, R0, k0, nullptr, L.sG, L.sX, L.sP, L.s_rp, false);
-            __syncthreads();
-            chol_offdiag_out(D, L, k0, R0, nb, n);
-        }
-        __syncthreads();  // this column's L tiles and y_j are read by the next column's updates
-    }
 }
 
 // Backward substitution L^T x = y (y in x after the column launches), one 1024-thread
@@ -1875,10 +1834,6 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     const bool xcd = xcd_env && NA >= 8;
     bool large = false;  // some graph's reduced system is past CMAX
     bool huge = false;   // ... past CMAX_LARGE (k_back_step instead of k_chol_back_large)
-    // LocalBA-sized systems: one k_chol_lba launch instead of a k_chol_col launch per column block
-    // (OSG_LBA_CHOL=0: the per-column launches, for A/B measurements)
-    const char *lce = getenv("OSG_LBA_CHOL");  // read per call: tests compare the two
-    const bool lba_chol = !(lce && atoi(lce) == 0);
     for (int a = 0; a < NA; a++) {
         const LbaHost &h = H[act[a]];
         const InOff &o = io[a];
@@ -2017,7 +1972,6 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
             LBA_MARK(KT_SPAIRS);
             hipLaunchKernelGGL(k_schur_pairs, gx((mx_pairs * 64 + 255) / 256), dim3(256), 0, ctx->stream, d_dev);
             LBA_MARK(KT_CHOL);
-            if (lba_chol) hipLaunchKernelGGL(k_chol_lba, yb, dim3(256), 0, ctx->stream, d_dev);
             for (int jb = 0; jb < mx_red; jb++) {  // row blocks at and below the diagonal block
                 // past CMAX only the envelope's rows: grids sized by the largest reach of any graph
                 int rows = 0, m = 0;
@@ -2028,8 +1982,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
                     rows = std::max(rows, big ? h.blk_last[jb] - jb + 1 : h.nblk_red - jb);
                     if (big) m = std::max(m, h.blk_last[jb] - jb);
                 }
-                if (rows == 0 || (lba_chol && !large)) continue;
-                hipLaunchKernelGGL(k_chol_col, gx(rows), dim3(256), 0, ctx->stream, d_dev, jb, lba_chol ? 1 : 0);
+                if (rows == 0) continue;
+                hipLaunchKernelGGL(k_chol_col, gx(rows), dim3(256), 0, ctx->stream, d_dev, jb);
                 if (large && m > 0)
                     hipLaunchKernelGGL(k_chol_trail, gx(m * (m + 1) / 2), dim3(256), 0, ctx->stream, d_dev, jb);
             }

@@ -235,23 +235,6 @@ def test_gba_map_scale(ctx, oracle, n_kf, n_pts):
     assert got.chi2_final < 0.2 * got.chi2_initial and got.iterations >= 5
 
 
-def test_lba_one_launch_factorisation_equals_column_launches(ctx, monkeypatch):
-    """k_chol_lba (one launch per step, the diagonal tile factored once per column) forms the same
-    L, Linv and y as the per-column k_chol_col launches: identical LBA results, bit for bit."""
-    rng = np.random.default_rng(3400)
-    graphs = [op.synth_lba_graph(rng, n_kf=n, n_points=3000) for n in (12, 30, 60)]
-    opt = op.Optimizer(ctx)
-    monkeypatch.setenv("OSG_LBA_CHOL", "0")
-    ref = opt.LocalBundleAdjustmentBatch(graphs)
-    monkeypatch.delenv("OSG_LBA_CHOL")
-    got = opt.LocalBundleAdjustmentBatch(graphs)
-    for g, r in zip(got, ref):
-        assert (g.iterations, g.trials) == (r.iterations, r.trials)
-        np.testing.assert_array_equal(g.pose, r.pose)
-        np.testing.assert_array_equal(g.point, r.point)
-        np.testing.assert_array_equal(g.edge_bad, r.edge_bad)
-
-
 def test_gba_and_lba_in_one_batch(ctx, oracle):
     """A LocalBA window and a whole-map BA in one lockstep batch: each equals its own call."""
     rng = np.random.default_rng(3300)
