@@ -789,7 +789,7 @@ __device__ __forceinline__ double rcp_nr(double d)
 //     applied to the identity give M = Lt^-1, so L_jj^-1 = D^-1/2 M without a triangular solve.
 //  3. workgroup 0: L_jj^-1 -> Linv, y_j = L_jj^-1 rhs -> x;  workgroup t > 0: L_tj = X L_jj^-T
 //     (MFMA) written over A_tj.  A_jj itself is never written (nothing downstream needs L_jj).
-// The LDS of one column step (k_chol_col, k_chol_lba)
+// The LDS of one column step (k_chol_col)
 struct CholLds {
     double sP[4][CB][CB + 1];  // per-wave partial tiles
     double sG[CB][CB + 1];     // T under elimination
