@@ -765,6 +765,15 @@ def _cpp_wall(res, workload, arrays, expect, args, rank, world):
     res["wall_cpp_adapter"] = w
     if "cpu_baseline" in res:
         res["wall_cpp_adapter_speedup_vs_cpu"] = round(w["frames_per_s"] / res["cpu_baseline"]["value"], 2)
+    # the drop-in as ORB-SLAM3 calls it: one frame per call, one thread, from C++ (no Python in the loop)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "pool.arrays")
+        write_arrays(path, arrays)
+        r1 = subprocess.run([exe, workload, path, "1", "200", "1"], capture_output=True, text=True, timeout=300)
+    if r1.returncode == 0:
+        w1 = json.loads(r1.stdout.strip().splitlines()[-1])
+        res["single_call_latency_cpp_adapter_us"] = {k: round(v / w1["reps"] * 1e6, 1)
+                                                     for k, v in w1["thread0_stage_s"].items()}
 
 
 def _attach_cpu(res, worker, units, unit, seconds, label, wall_key="wall_frames_per_s_incl_host_and_pcie"):

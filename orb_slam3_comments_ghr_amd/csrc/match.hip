@@ -762,77 +762,93 @@ __device__ __forceinline__ QRes eval_query_group(const MatchArgs &A, int q, int 
     }
     return res;
 }
+// The prepass in one launch.  Each workgroup counts its queries' candidates and publishes the sum in flags[workgroup] (the call's epoch in the high word, so the
+// buffer needs no clearing), then takes its offset as the sum of its predecessors' published counts
+// (wave 0 reads 64 flags at a time) and fills and evaluates its queries.  A wait that
+// never ends (it cannot, short of a hardware fault) is bounded and reported in status[3] bit 2.
 template <int MODE>
-__global__ __launch_bounds__(GQG *BOW_G) void k_grid_count(const MatchArgs *__restrict__ args)
+__global__ __launch_bounds__(GQG *BOW_G) void k_grid_prepass(const MatchArgs *__restrict__ args,
+                                                             unsigned long long *__restrict__ flags, int flag_stride,
+                                                             unsigned epoch)
 {
     const MatchArgs &A = args[blockIdx.y];
-    const int lane = threadIdx.x & (BOW_G - 1);
-    const int q = blockIdx.x * GQG + threadIdx.x / BOW_G;
-    if (q >= A.nq) return;
-    const Win wl = query_window<MODE>(A, q);
-    const bool two = (MODE == MODE_MPS || MODE == MODE_LAST) && A.nleft >= 0;
-    const Win wr = two ? query_window_r<MODE>(A, q, wl) : wl;
-    if (lane == 0) {  // for k_grid_fill and k_match's serial redo
-        store_win(A.q_win + 4 * (size_t)q, wl);
-        if (two) store_win(A.q_win + 4 * (size_t)q + 2, wr);
-    }
-    int cl;
-    const int c = enum_query_group<MODE, false>(A, q, wl, wr, nullptr, cl, lane);
-    if (lane == 0) A.q_off[q] = c;  // the count, for k_grid_scan
-}
-template <int MODE>
-__global__ __launch_bounds__(MT) void k_grid_scan(const MatchArgs *__restrict__ args)
-{
-    const MatchArgs &A = args[blockIdx.x];
-    __shared__ int s_scan[MT];
-    const int nq = A.nq, tid = threadIdx.x;
-    const int per = (nq + MT - 1) / MT;
-    const int q0 = min(nq, tid * per), q1 = min(nq, q0 + per);
-    int my = 0;
-    for (int q = q0; q < q1; q++) my += A.q_off[q];
-    s_scan[tid] = my;
+    unsigned long long *F = flags + (size_t)blockIdx.y * flag_stride;
+    __shared__ int s_cnt[GQG];
+    __shared__ int s_base;
+    const int lane = threadIdx.x & (BOW_G - 1), g = threadIdx.x / BOW_G;
+    __shared__ int s_wg;
+    const int nwg = (A.nq + GQG - 1) / GQG;
+    if ((int)blockIdx.x >= nwg) return;  // the whole workgroup
+    // the workgroup's place in the order comes from a ticket (status[14], zeroed with the call's
+    // status), not blockIdx: a workgroup then only waits for ones that have started
+    if (threadIdx.x == 0) s_wg = atomicAdd((int *)&A.status[14], 1);
     __syncthreads();
-    for (int o = 1; o < MT; o <<= 1) {
-        const int v = tid >= o ? s_scan[tid - o] : 0;
-        __syncthreads();
-        s_scan[tid] += v;
-        __syncthreads();
+    const int wg = s_wg;
+    const int q = wg * GQG + g;
+    const bool valid = q < A.nq;
+    const bool two = (MODE == MODE_MPS || MODE == MODE_LAST) && A.nleft >= 0;
+    Win wl{}, wr{};
+    int c = 0, cl = 0;
+    if (valid) {
+        wl = query_window<MODE>(A, q);
+        wr = two ? query_window_r<MODE>(A, q, wl) : wl;
+        if (lane == 0) {  // for k_match's serial redo
+            store_win(A.q_win + 4 * (size_t)q, wl);
+            if (two) store_win(A.q_win + 4 * (size_t)q + 2, wr);
+        }
+        c = enum_query_group<MODE, false>(A, q, wl, wr, nullptr, cl, lane);
     }
-    int off = s_scan[tid] - my;
-    for (int q = q0; q < q1; q++) {
-        const int c = A.q_off[q];
-        A.q_off[q] = off;
-        off += c;
+    if (lane == 0) s_cnt[g] = c;
+    __syncthreads();
+    int agg = 0;
+#pragma unroll
+    for (int i = 0; i < GQG; i++) agg += s_cnt[i];
+    if (threadIdx.x == 0)
+        __hip_atomic_store(&F[wg], ((unsigned long long)epoch << 32) | (unsigned)agg, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < 64) {
+        int sum = 0;
+        bool stuck = false;
+        for (int base = 0; base < wg; base += 64) {
+            const int i = base + (int)threadIdx.x;
+            int v = 0;
+            if (i < wg) {
+                unsigned long long f;
+                int spins = 0;
+                do {
+                    f = __hip_atomic_load(&F[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                } while ((unsigned)(f >> 32) != epoch && ++spins < (1 << 22));
+                stuck |= (unsigned)(f >> 32) != epoch;
+                v = (int)(unsigned)f;
+            }
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+            sum += v;
+        }
+        if (__ballot(stuck) && threadIdx.x == 0) atomicOr((int *)&A.status[3], 2);
+        if (threadIdx.x == 0) s_base = sum;
     }
-    if (tid == 0) {
-        const int total = s_scan[MT - 1];
-        A.q_off[nq] = total;
-        if (total > A.cap) {  // the host resizes and retries; k_grid_fill and k_match skip the problem
+    __syncthreads();
+    int off = s_base;
+    for (int i = 0; i < g; i++) off += s_cnt[i];
+    if (valid && lane == 0) A.q_off[q] = off;
+    if (wg == nwg - 1 && threadIdx.x == 0) {
+        const int total = s_base + agg;
+        A.q_off[A.nq] = total;
+        if (total > A.cap) {  // the host resizes and retries; k_match skips the problem
             A.status[0] = total;
-            A.status[3] = 1;
+            atomicOr((int *)&A.status[3], 1);
         }
     }
-}
-template <int MODE>
-__global__ __launch_bounds__(GQG *BOW_G) void k_grid_fill(const MatchArgs *__restrict__ args)
-{
-    const MatchArgs &A = args[blockIdx.y];
-    const int lane = threadIdx.x & (BOW_G - 1);
-    const int q = blockIdx.x * GQG + threadIdx.x / BOW_G;
-    if (q >= A.nq || A.q_off[A.nq] > A.cap) return;
-    const int off = A.q_off[q];
-    const Win wl = load_win(A.q_win + 4 * (size_t)q);
-    const bool two = (MODE == MODE_MPS || MODE == MODE_LAST) && A.nleft >= 0;
-    const Win wr = two ? load_win(A.q_win + 4 * (size_t)q + 2) : wl;
-    int cl;
-    const int c = enum_query_group<MODE, true>(A, q, wl, wr, A.cands + off, cl, lane);
+    if (!valid || off + c > A.cap) return;
+    int cl2;
+    enum_query_group<MODE, true>(A, q, wl, wr, A.cands + off, cl2, lane);
     if (lane == 0) A.q_mid[q] = off + cl;
     // the group reads back the candidates its lanes wrote: their stores complete first (the lanes
     // share the CU's write-through L1)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    // the first evaluation: blocked(s) = the slot's state before the call (k_match's taken0)
     const QRes r = eval_query_group<MODE>(A, q, off, off + cl, off + c, lane,
                                           [&](int s) { return taken_init<MODE>(A, s); });
     if (lane == 0) store_res(A, q, r);
@@ -1033,7 +1049,7 @@ __global__ __launch_bounds__(MT) void k_match(const MatchArgs *__restrict__ args
     }
     tclk[2] = __builtin_amdgcn_s_memtime();
     int total = pre ? A.q_off[nq] : 0;
-    if (pre && total > A.cap) return;  // k_grid_scan flagged the overflow; the host retries
+    if (pre && total > A.cap) return;  // k_grid_prepass flagged the overflow; the host retries
     if (!pre) {
     // ---- 1. count
     int my = 0;
@@ -1348,7 +1364,7 @@ __global__ __launch_bounds__(MT) void k_match(const MatchArgs *__restrict__ args
         A.status[1] = s_red[0];
         A.status[2] = rounds;
         A.status[0] = total;
-        A.status[3] = 0;
+        A.status[3] &= 2;  // keep k_grid_prepass's wait-bound flag
         A.status[4] = serial;
         tclk[8] = __builtin_amdgcn_s_memtime();
         if (BOW) tclk[1] = tclk[2] = tclk[0];
@@ -1533,10 +1549,19 @@ int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_
             int max_nq = 0;
             for (int b = 0; b < B; b++) max_nq = std::max(max_nq, P[b].A.nq);
             if (max_nq > 0) {
-                const dim3 gq((max_nq + GQG - 1) / GQG, B);
-                hipLaunchKernelGGL((k_grid_count<MODE>), gq, dim3(GQG * BOW_G), 0, ctx->stream, dev_args);
-                hipLaunchKernelGGL((k_grid_scan<MODE>), dim3(B), dim3(MT), 0, ctx->stream, dev_args);
-                hipLaunchKernelGGL((k_grid_fill<MODE>), gq, dim3(GQG * BOW_G), 0, ctx->stream, dev_args);
+                const int nwg = (max_nq + GQG - 1) / GQG;
+                const size_t need = (size_t)nwg * B;
+                if (ctx->lb_cap < need) {  // zeroed once: epoch 0 is never a call's
+                    if (ctx->lb_flags) OSG_HIP_CHECK(ctx, hipFree(ctx->lb_flags));
+                    ctx->lb_flags = nullptr;
+                    ctx->lb_cap = 0;
+                    OSG_HIP_CHECK(ctx, hipMalloc(&ctx->lb_flags, sizeof(unsigned long long) * need));
+                    OSG_HIP_CHECK(ctx, hipMemsetAsync(ctx->lb_flags, 0, sizeof(unsigned long long) * need, ctx->stream));
+                    ctx->lb_cap = need;
+                }
+                if (++ctx->lb_epoch == 0) ++ctx->lb_epoch;
+                hipLaunchKernelGGL((k_grid_prepass<MODE>), dim3(nwg, B), dim3(GQG * BOW_G), 0, ctx->stream, dev_args,
+                                   ctx->lb_flags, nwg, ctx->lb_epoch);
             }
         }
         if (stage == 2)
@@ -1553,6 +1578,9 @@ int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_
         OSG_RC(osg_wait(ctx));
         std::memcpy(st.data(), pin_io, status_bytes);
         bool overflow = false;
+        for (int b = 0; b < B; b++)
+            if (st[(size_t)STATUS_INTS * b + 3] & 2)
+                return osg_set_error(ctx, OSG_E_HIP, "problem %d: k_grid_prepass wait bound exceeded", b);
         for (int b = 0; b < B; b++)
             if (st[(size_t)STATUS_INTS * b + 3]) {
                 overflow = true;

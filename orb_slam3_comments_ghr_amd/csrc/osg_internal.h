@@ -38,6 +38,9 @@ struct osg_ctx {
     double last_kernel_ms = 0;    // last k_match / k_pose_opt launch time (HIP events)
     hipEvent_t ev[2] = {};        // timing events (osg_ctx_events)
     hipEvent_t ev_done = nullptr; // completion marker of osg_wait (no timing)
+    unsigned long long *lb_flags = nullptr;  // k_grid_prepass's per-workgroup counts (epoch-tagged)
+    size_t lb_cap = 0;
+    uint32_t lb_epoch = 0;
     std::shared_ptr<void> lba_cache;  // host structures of the last LBA batch, reused (ba.hip)
     bool lba_ktime = false;           // osg_lba_kernel_times: per-kernel HIP-event timing of LBA steps
     double lba_kms[OSG_LBA_NK] = {};

@@ -196,6 +196,7 @@ int osg_ctx_destroy(osg_ctx *ctx)
     for (hipEvent_t e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->ev_done) (void)hipEventDestroy(ctx->ev_done);
+    if (ctx->lb_flags) (void)hipFree(ctx->lb_flags);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
     return OSG_OK;

@@ -11,6 +11,16 @@ from orb_slam3_comments_ghr_amd import orb, stereo as st, vocabulary as vb
 from tests import cpu_mt
 
 
+@pytest.fixture(autouse=True)
+def _libm_off_after():
+    """bench._oracle() switches the shared oracle library to the host libm (the cpu_baseline legs time
+    the reference's own arithmetic); later tests in the session hold it to the correctly rounded path."""
+    yield
+    for lib, _ in bench._ORACLE:
+        lib.oracle_set_libm(0)
+    bench._ORACLE.clear()
+
+
 def _runs(worker):
     for n in (1, 2):
         calls, el = cpu_mt.run(worker, n, 0.05)
