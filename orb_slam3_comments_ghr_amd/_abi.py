@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liborbslam3_amd.so")
+# OSG_LIB_PATH points the package at another build of the same library (a profiling build)
+LIB_PATH = os.environ.get("OSG_LIB_PATH") or os.path.join(_HERE, "liborbslam3_amd.so")
 
 OSG_OK = 0
 OSG_E_INVALID = -1

@@ -66,6 +66,8 @@ def main():
           for _ in range(32)]
     [fr.synth_last_queries_two_cam(rngb, f, n_last=2000) for f in FP]
     QP = [fr.synth_mp_queries_two_cam(rngb, f, m=1500) for f in FP]
+    for x in QP:  # as bench_c5: the local map's MapPoints all have observations
+        x.has_obs[:] = 1
     SP = [fr.synth_slots(rngb, f.n, frac_assigned=0.05) for f in FP]
     fsb, qsb = FP[0].struct(), QP[0].struct()
     slb, tkb = SP[0][0].copy(), np.ascontiguousarray(SP[0][1], np.uint8)
