@@ -91,9 +91,8 @@ struct LbaDev {
     const int32_t *lm_perm;              // landmarks ordered by edge count (k_linearize's thread order)
     const int32_t *lm_b_start;           // blocks per landmark (blocks are numbered landmark-major)
     const int32_t *blk_pose;             // per block: hessian pose index
-    const int32_t *edge_blk;             // per edge: block or -1
+    const int32_t *edge_blk;             // per edge: 2 block + (1 past the block's first edge), or -1
     const int32_t *blk_lm;               // per block: landmark
-    const int32_t *blk_e_start, *blk_e;  // edges per block (edge order)
     const int32_t *hp_e_start, *hp_e;    // edges per hessian pose
     const int32_t *hp_b_start, *hp_b;    // blocks per hessian pose
     const int32_t *pair_start;           // dense (i <= j) pairs
@@ -217,11 +216,11 @@ __global__ __launch_bounds__(EB) void k_errors(const LbaDev *__restrict__ Ds, in
 // Thirdparty/g2o/g2o/core/base_binary_edge.hpp:55-120, robust branch) and
 //   * sums Hll (upper 6) and b_l in registers (the order of a per-landmark reduction over lm_e),
 //   * writes each Hpl block: a block's edges are in edge order inside its landmark, so the first
-//     edge stores and the others add (the order of a per-block reduction over blk_e),
+//     edge stores and the others add (the order of a per-block reduction over its edges),
 // and the workgroup's max |diag Hll| for computeLambdaInit.  The edges' pose parts {Hpp upper 21,
 // b_p 6} are not stored: k_pose_red recomputes them pose-major (27 doubles per edge written and
 // read back cost more HBM time than the recomputed Jacobian costs VALU time).
-__global__ __launch_bounds__(EB) void k_linearize(const LbaDev *__restrict__ Ds)
+__global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_linearize(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_LIN);
     if (bx >= max(D.gl, 1)) return;
@@ -255,9 +254,10 @@ __global__ __launch_bounds__(EB) void k_linearize(const LbaDev *__restrict__ Ds)
                 for (int j = 0; j < 6; j++) Jp[2][j] = 0.0;
                 for (int j = 0; j < 3; j++) Jx[2][j] = 0.0;
             }
-            const int blk = D.edge_blk[e];
-            if (blk >= 0) {  // free pose: Hpl (the pose part is recomputed by k_pose_red)
-                const bool first = D.blk_e[D.blk_e_start[blk]] == e;
+            const int code = D.edge_blk[e];
+            if (code >= 0) {  // free pose: Hpl (the pose part is recomputed by k_pose_red)
+                const int blk = code >> 1;
+                const bool first = !(code & 1);
                 double *hp = D.Hpl + 18 * (size_t)blk;
                 for (int a = 0; a < 6; a++)
                     for (int bb = 0; bb < 3; bb++) {
@@ -289,7 +289,7 @@ __global__ __launch_bounds__(EB) void k_linearize(const LbaDev *__restrict__ Ds)
 }
 
 // per free pose (one workgroup): Hpp (6x6) and b_p from its edges
-__global__ __launch_bounds__(EB) void k_pose_red(const LbaDev *__restrict__ Ds)
+__global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_pose_red(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_LIN);
     const int i = bx;
@@ -1347,7 +1347,7 @@ struct LbaHost {
     std::vector<int32_t> blk_first, blk_last;  // envelope of the reduced system by row block (see LbaDev)
     bool trivial = false;  // nothing to optimise: the estimates are returned unchanged
     std::vector<int32_t> pose_h, hp_pose, point_h, hl_point, lm_e_start, lm_e, lm_perm, lm_b_start, blk_pose, edge_blk, blk_lm,
-        blk_e_start, blk_e, hp_e_start, hp_e, hp_b_start, hp_b, pair_start, pair_ab, chunk_start, pair_chunk,
+        hp_e_start, hp_e, hp_b_start, hp_b, pair_start, pair_ab, chunk_start, pair_chunk,
         pair_rank, rs_pose, rs_rank0, rs_chunk_start, rs_chunk, hp_rs_start;
     int n_rs = 0;
     double t_struct = 0;
@@ -1481,17 +1481,18 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
     const int nblk = (int)H.blk_pose.size();
     H.nblk = nblk;
     H.blk_lm.assign(nblk, 0);
-    H.blk_e_start.assign(nblk + 1, 0);
     for (int l = 0; l < nhl; l++)
         for (int b = H.lm_b_start[l]; b < H.lm_b_start[l + 1]; b++) H.blk_lm[b] = l;
-    for (int e = 0; e < ne; e++)
-        if (H.edge_blk[e] >= 0) H.blk_e_start[H.edge_blk[e] + 1]++;
-    for (int b = 0; b < nblk; b++) H.blk_e_start[b + 1] += H.blk_e_start[b];
-    H.blk_e.assign(H.blk_e_start[nblk], 0);
+    // per edge 2 block + (0 for the block's first edge in edge order, else 1): k_linearize stores the
+    // first edge's Hpl terms and adds the others' (a per-block reduction in edge order)
     {
-        std::vector<int32_t> fill(H.blk_e_start.begin(), H.blk_e_start.end() - 1);
+        std::vector<uint8_t> seen(nblk, 0);
         for (int e = 0; e < ne; e++)
-            if (H.edge_blk[e] >= 0) H.blk_e[fill[H.edge_blk[e]]++] = e;
+            if (H.edge_blk[e] >= 0) {
+                const int b = H.edge_blk[e];
+                H.edge_blk[e] = 2 * b + (seen[b] ? 1 : 0);
+                seen[b] = 1;
+            }
     }
     // edges / blocks per hessian pose
     H.hp_e_start.assign(nhp + 1, 0);
@@ -1750,7 +1751,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     osg_packer pk;
     struct InOff {
         size_t fixed, epose, epoint, ecam, ekind, eobs, eisig, cams, poseh, hppose, pointh, hlpoint, lmes, lme, lmperm, lmbs,
-            blkpose, eblk, hpes, hpe, hpbs, hpb, pairs, pairab, chs, blklm, blkes, blke, pch, pose0, point0, erob,
+            blkpose, eblk, hpes, hpe, hpbs, hpb, pairs, pairab, chs, blklm, pch, pose0, point0, erob,
             prank, rspose, rsrank0, rscs, rsc, hprs, bfirst, blast;
     };
     std::vector<InOff> io(NA);
@@ -1786,8 +1787,6 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         o.pairab = pk.add(h.pair_ab.data(), 4 * h.pair_ab.size());
         o.chs = pk.add(h.chunk_start.data(), 4 * h.chunk_start.size());
         o.blklm = pk.add(h.blk_lm.data(), 4 * (size_t)nblk);
-        o.blkes = pk.add(h.blk_e_start.data(), 4 * (size_t)(nblk + 1));
-        o.blke = pk.add(h.blk_e.data(), 4 * h.blk_e.size());
         o.pch = pk.add(h.pair_chunk.data(), 4 * h.pair_chunk.size());
         o.prank = pk.add(h.pair_rank.data(), 4 * h.pair_rank.size());
         o.bfirst = pk.add(h.blk_first.data(), 4 * std::max<size_t>(h.blk_first.size(), 1));
@@ -1881,8 +1880,6 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         D.nchunks = h.nchunks;
         D.chunk_start = osg_dptr<int32_t>(din, o.chs);
         D.blk_lm = osg_dptr<int32_t>(din, o.blklm);
-        D.blk_e_start = osg_dptr<int32_t>(din, o.blkes);
-        D.blk_e = osg_dptr<int32_t>(din, o.blke);
         D.pair_chunk = osg_dptr<int32_t>(din, o.pch);
         D.pair_rank = osg_dptr<int32_t>(din, o.prank);
         D.blk_first = osg_dptr<int32_t>(din, o.bfirst);

@@ -393,8 +393,11 @@ __device__ inline void edge_jacobians(int kind, bool binary, const osg_camera &c
 
 __device__ inline double chi2_of(const double *err, int dim, double w)
 {
+    // dim is 2 or 3; spelled out so err stays in registers (a dynamic index sends it to scratch)
     double s = 0;
-    for (int i = 0; i < dim; i++) s += err[i] * (w * err[i]);
+    s += err[0] * (w * err[0]);
+    s += err[1] * (w * err[1]);
+    if (dim > 2) s += err[2] * (w * err[2]);
     return s;
 }
 
