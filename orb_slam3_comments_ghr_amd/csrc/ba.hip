@@ -88,10 +88,11 @@ struct LbaDev {
     const int32_t *point_h;       // per point: landmark index or -1
     const int32_t *hl_point;      // per landmark: point index
     const int32_t *lm_e_start, *lm_e;    // edges per landmark
-    const int32_t *lm_perm;              // landmarks ordered by edge count (k_linearize's thread order)
+    const int32_t *lg_start;             // k_linearize's landmark groups: <= EB edges, or one landmark
     const int32_t *lm_b_start;           // blocks per landmark (blocks are numbered landmark-major)
     const int32_t *blk_pose;             // per block: hessian pose index
-    const int32_t *edge_blk;             // per edge: 2 block + (1 past the block's first edge), or -1
+    const int32_t *edge_blk;             // per edge: 4 block + 2 (block has several edges) + 1 (not its
+                                         // first edge), or -1
     const int32_t *blk_lm;               // per block: landmark
     const int32_t *hp_e_start, *hp_e;    // edges per hessian pose
     const int32_t *hp_b_start, *hp_b;    // blocks per hessian pose
@@ -109,7 +110,7 @@ struct LbaDev {
     double *chunk_part;                  // 36 per chunk
     double *bs_part;                     // 6 per row segment: sum of Hpl Dinv b_l
     // launch extents of this graph (grids are sized for the largest graph of the batch)
-    int ge, gl, gu, nblk_red;
+    int ge, gl, gll, gu, nblk_red;       // gll: k_linearize's landmark groups
     double user_lambda;
     // state: estimate buffers A / B; ctl->sel says which one is current
     double *poseA, *poseB, *pointA, *pointB;
@@ -122,7 +123,7 @@ struct LbaDev {
     double *Dinv, *db;
     double *Hs, *bs, *x;
     double *Linv;                        // inverses of the 32x32 diagonal blocks of L, row-major per block row
-    int npart;                           // partial slots per kind (>= ge, gu, gl + nhp)
+    int npart;                           // partial slots per kind (>= ge, gu, gll + nhp)
     double *part;                        // [0, P): chi of the trial, [P, 2P): scale, [2P, 3P): max diag,
                                          // [3P, 4P): chi of the current estimate (P = npart)
     // envelope of the reduced camera system by 32-row blocks (BundleAdjustment past CMAX): row block t
@@ -212,78 +213,109 @@ __global__ __launch_bounds__(EB) void k_errors(const LbaDev *__restrict__ Ds, in
     if (threadIdx.x == 0) D.part[part_off + bx] = t;
 }
 
-// Linearisation, landmark-major: one thread per landmark walks its edges in edge order (ref:
-// Thirdparty/g2o/g2o/core/base_binary_edge.hpp:55-120, robust branch) and
-//   * sums Hll (upper 6) and b_l in registers (the order of a per-landmark reduction over lm_e),
-//   * writes each Hpl block: a block's edges are in edge order inside its landmark, so the first
-//     edge stores and the others add (the order of a per-block reduction over its edges),
-// and the workgroup's max |diag Hll| for computeLambdaInit.  The edges' pose parts {Hpp upper 21,
-// b_p 6} are not stored: k_pose_red recomputes them pose-major (27 doubles per edge written and
-// read back cost more HBM time than the recomputed Jacobian costs VALU time).
-__global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_linearize(const LbaDev *__restrict__ Ds)
+// Linearisation (ref:Thirdparty/g2o/g2o/core/base_binary_edge.hpp:55-120, robust branch), edge-parallel
+// with the landmark-major sums of a per-landmark loop.  Workgroup g takes the landmarks
+// [lg_start[g], lg_start[g + 1]) — at most EB edges, or one landmark with more — and their edges in
+// lm_e order (landmark-major, edge order inside a landmark), EB at a time:
+//   * thread t computes one edge's Jacobians and robust weight, stages its Hll (upper 6) and b_l
+//     terms in LDS, and writes its Hpl block when the block has no other edge;
+//   * then thread t owns landmark lg_start[g] + t and adds its edges' terms in edge order — the sums
+//     of a per-landmark reduction over lm_e — and the Hpl terms of a block with several edges (a
+//     two-camera rig's left and right observations), first edge stored, the others added.
+// The workgroup's max |diag Hll| goes to the computeLambdaInit partials.  The edges' pose parts
+// {Hpp upper 21, b_p 6} are not stored: k_pose_red recomputes them pose-major (27 doubles per edge
+// written and read back cost more HBM time than the recomputed Jacobian costs VALU time).
+template <bool MULTI>
+__global__ __launch_bounds__(EB) void k_linearize(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_LIN);
-    if (bx >= max(D.gl, 1)) return;
-    __shared__ double s[EB / 64];
-    // thread -> landmark through lm_perm (landmarks by edge count): the lanes of a wave walk edge lists
-    // of equal length.  Every landmark's sums are its own, so the order changes no result.
-    const int tl = bx * EB + threadIdx.x;
+    if (bx >= max(D.gll, 1)) return;
+    __shared__ double s_t[9][EB];                 // per edge: Hll upper 6 | b_l 3
+    __shared__ double s_h[MULTI ? 18 : 1][EB];    // per edge of a several-edge block: its Hpl terms
+    __shared__ double s_m[EB / 64];
     double md = 0.0;
-    if (tl < D.nhl) {
-        const int l = D.lm_perm[tl];
-        const double *X = cur_point(D) + 3 * (size_t)D.hl_point[l];
-        const double *poses = cur_pose(D);
+    if (D.nhl > 0) {
+        const int l0 = D.lg_start[bx], l1 = D.lg_start[bx + 1];
+        const int q0 = D.lm_e_start[l0], q1 = D.lm_e_start[l1];
+        const int ol = l0 + (int)threadIdx.x;  // the landmark this thread sums
+        const bool owner = ol < l1;
+        const int oq0 = owner ? D.lm_e_start[ol] : 0, oq1 = owner ? D.lm_e_start[ol + 1] : 0;
+        const double *poses = cur_pose(D), *points = cur_point(D);
         double H6[6] = {0, 0, 0, 0, 0, 0}, bl3[3] = {0, 0, 0};
-        for (int q = D.lm_e_start[l]; q < D.lm_e_start[l + 1]; q++) {
-            const int e = D.lm_e[q];
-            const int k = D.e_kind[e];
-            const SE3 T = se3_from7(poses + 7 * (size_t)D.e_pose[e]);
-            double Jp[3][6], Jx[3][3];
-            edge_jacobians(k, true, D.cams[D.e_cam[e]], T, X, Jp, Jx);
-            const int dim = (k == OSG_EDGE_STEREO) ? 3 : 2;
-            const double w = edge_w(D, e);
-            const double ev[3] = {D.err[3 * e], D.err[3 * e + 1], D.err[3 * e + 2]};
-            double delta, r0, rho1;
-            float dsqr;
-            edge_delta(D, e, k, delta, dsqr);
-            huber(chi2_of(ev, dim, w), delta, dsqr, r0, rho1);
-            const double ww = rho1 * w;
-            double om[3];
-            for (int d = 0; d < 3; d++) om[d] = (d < dim) ? -(w * ev[d]) * rho1 : 0.0;
-            if (dim == 2) {
-                for (int j = 0; j < 6; j++) Jp[2][j] = 0.0;
-                for (int j = 0; j < 3; j++) Jx[2][j] = 0.0;
+        for (int c0 = q0; c0 < q1; c0 += EB) {
+            const int q = c0 + (int)threadIdx.x;
+            if (q < q1) {
+                const int e = D.lm_e[q];
+                const int k = D.e_kind[e];
+                const SE3 T = se3_from7(poses + 7 * (size_t)D.e_pose[e]);
+                double Jp[3][6], Jx[3][3];
+                edge_jacobians(k, true, D.cams[D.e_cam[e]], T, points + 3 * (size_t)D.e_point[e], Jp, Jx);
+                const int dim = (k == OSG_EDGE_STEREO) ? 3 : 2;
+                const double w = edge_w(D, e);
+                const double ev[3] = {D.err[3 * e], D.err[3 * e + 1], D.err[3 * e + 2]};
+                double delta, r0, rho1;
+                float dsqr;
+                edge_delta(D, e, k, delta, dsqr);
+                huber(chi2_of(ev, dim, w), delta, dsqr, r0, rho1);
+                const double ww = rho1 * w;
+                double om[3];
+                for (int d = 0; d < 3; d++) om[d] = (d < dim) ? -(w * ev[d]) * rho1 : 0.0;
+                if (dim == 2) {
+                    for (int j = 0; j < 6; j++) Jp[2][j] = 0.0;
+                    for (int j = 0; j < 3; j++) Jx[2][j] = 0.0;
+                }
+                const int code = D.edge_blk[e];
+                if (code >= 0) {  // free pose: Hpl (the pose part is recomputed by k_pose_red)
+                    const bool multi = MULTI && (code & 2);
+                    double *hp = D.Hpl + 18 * (size_t)(code >> 2);
+                    for (int a = 0; a < 6; a++)
+                        for (int bb = 0; bb < 3; bb++) {
+                            const double v = Jp[0][a] * ww * Jx[0][bb] + Jp[1][a] * ww * Jx[1][bb] + Jp[2][a] * ww * Jx[2][bb];
+                            if (multi) s_h[MULTI ? 3 * a + bb : 0][threadIdx.x] = v;
+                            else hp[3 * a + bb] = v;
+                        }
+                }
+                int c = 0;
+                for (int a = 0; a < 3; a++)
+                    for (int bb = a; bb < 3; bb++)
+                        s_t[c++][threadIdx.x] = Jx[0][a] * ww * Jx[0][bb] + Jx[1][a] * ww * Jx[1][bb] + Jx[2][a] * ww * Jx[2][bb];
+                for (int a = 0; a < 3; a++)
+                    s_t[6 + a][threadIdx.x] = Jx[0][a] * om[0] + Jx[1][a] * om[1] + Jx[2][a] * om[2];
             }
-            const int code = D.edge_blk[e];
-            if (code >= 0) {  // free pose: Hpl (the pose part is recomputed by k_pose_red)
-                const int blk = code >> 1;
-                const bool first = !(code & 1);
-                double *hp = D.Hpl + 18 * (size_t)blk;
-                for (int a = 0; a < 6; a++)
-                    for (int bb = 0; bb < 3; bb++) {
-                        const double v = Jp[0][a] * ww * Jx[0][bb] + Jp[1][a] * ww * Jx[1][bb] + Jp[2][a] * ww * Jx[2][bb];
-                        hp[3 * a + bb] = first ? v : hp[3 * a + bb] + v;
+            __syncthreads();
+            if (owner) {
+                const int a0 = max(oq0, c0), a1 = min(oq1, c0 + EB);
+                for (int qq = a0; qq < a1; qq++) {
+                    const int t = qq - c0;
+                    for (int c = 0; c < 6; c++) H6[c] += s_t[c][t];
+                    for (int a = 0; a < 3; a++) bl3[a] += s_t[6 + a][t];
+                    if (MULTI) {
+                        const int code = D.edge_blk[D.lm_e[qq]];
+                        if (code >= 0 && (code & 2)) {
+                            double *hp = D.Hpl + 18 * (size_t)(code >> 2);
+                            const bool first = !(code & 1);
+                            for (int i = 0; i < 18; i++) hp[i] = first ? s_h[MULTI ? i : 0][t] : hp[i] + s_h[MULTI ? i : 0][t];
+                        }
                     }
+                }
             }
-            int c = 0;
-            for (int a = 0; a < 3; a++)
-                for (int bb = a; bb < 3; bb++)
-                    H6[c++] += Jx[0][a] * ww * Jx[0][bb] + Jx[1][a] * ww * Jx[1][bb] + Jx[2][a] * ww * Jx[2][bb];
-            for (int a = 0; a < 3; a++) bl3[a] += Jx[0][a] * om[0] + Jx[1][a] * om[1] + Jx[2][a] * om[2];
+            __syncthreads();
         }
-        const double H[9] = {H6[0], H6[1], H6[2], H6[1], H6[3], H6[4], H6[2], H6[4], H6[5]};
-        for (int i = 0; i < 9; i++) D.Hll[9 * (size_t)l + i] = H[i];
-        for (int i = 0; i < 3; i++) D.bl[3 * (size_t)l + i] = bl3[i];
-        md = fmax(fabs(H[0]), fmax(fabs(H[4]), fabs(H[8])));
+        if (owner) {
+            const double H[9] = {H6[0], H6[1], H6[2], H6[1], H6[3], H6[4], H6[2], H6[4], H6[5]};
+            for (int i = 0; i < 9; i++) D.Hll[9 * (size_t)ol + i] = H[i];
+            for (int i = 0; i < 3; i++) D.bl[3 * (size_t)ol + i] = bl3[i];
+            md = fmax(fabs(H[0]), fmax(fabs(H[4]), fabs(H[8])));
+        }
     }
     // max |diag| per workgroup for computeLambdaInit
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int off = 32; off >= 1; off >>= 1) md = fmax(md, __shfl_xor(md, off));
-    if (lane == 0) s[w] = md;
+    if (lane == 0) s_m[w] = md;
     __syncthreads();
     if (threadIdx.x == 0) {
         double m = 0;
-        for (int i = 0; i < EB / 64; i++) m = fmax(m, s[i]);
+        for (int i = 0; i < EB / 64; i++) m = fmax(m, s_m[i]);
         D.part[2 * D.npart + bx] = m;
     }
 }
@@ -294,7 +326,7 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(3, 8))) void
     LBA_GRAPH(M_LIN);
     const int i = bx;
     if (i >= D.nhp) return;
-    const int diag_off = 2 * D.npart + D.gl;
+    const int diag_off = 2 * D.npart + D.gll;
     __shared__ double s[EB / 64][27];
     double acc[27];
     for (int k = 0; k < 27; k++) acc[k] = 0.0;
@@ -380,7 +412,7 @@ __global__ void k_lambda_init(const LbaDev *__restrict__ Ds)
         return;
     }
     double md = 0;
-    for (int i = 0; i < D.gl + D.nhp; i++) md = fmax(md, D.part[2 * D.npart + i]);
+    for (int i = 0; i < D.gll + D.nhp; i++) md = fmax(md, D.part[2 * D.npart + i]);
     D.ctl->lambda = 1e-5 * md;
 }
 
@@ -1343,10 +1375,11 @@ struct LbaHost {
     const osg_ba_graph *G = nullptr;
     osg_ba_result *R = nullptr;
     int np = 0, npt = 0, ne = 0, nhp = 0, nhl = 0, nblk = 0, npairs = 0, nchunks = 0;
-    int ge = 0, gl = 0, gu = 0, nblk_red = 0, npart = 64;
+    int ge = 0, gl = 0, gll = 0, gu = 0, nblk_red = 0, npart = 64;
+    bool multi = false;  // a block with several edges (k_linearize<true>)
     std::vector<int32_t> blk_first, blk_last;  // envelope of the reduced system by row block (see LbaDev)
     bool trivial = false;  // nothing to optimise: the estimates are returned unchanged
-    std::vector<int32_t> pose_h, hp_pose, point_h, hl_point, lm_e_start, lm_e, lm_perm, lm_b_start, blk_pose, edge_blk, blk_lm,
+    std::vector<int32_t> pose_h, hp_pose, point_h, hl_point, lm_e_start, lm_e, lg_start, lm_b_start, blk_pose, edge_blk, blk_lm,
         hp_e_start, hp_e, hp_b_start, hp_b, pair_start, pair_ab, chunk_start, pair_chunk,
         pair_rank, rs_pose, rs_rank0, rs_chunk_start, rs_chunk, hp_rs_start;
     int n_rs = 0;
@@ -1365,7 +1398,8 @@ struct LbaHost {
         G = nullptr;
         R = nullptr;
         np = npt = ne = nhp = nhl = nblk = npairs = nchunks = n_rs = 0;
-        ge = gl = gu = nblk_red = 0;
+        ge = gl = gll = gu = nblk_red = 0;
+        multi = false;
         npart = 64;
         blk_first.clear();
         blk_last.clear();
@@ -1442,14 +1476,16 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
     {
         std::vector<int32_t> fill(H.lm_e_start.begin(), H.lm_e_start.end() - 1);
         for (int e = 0; e < ne; e++) H.lm_e[fill[point_h[G->e_point[e]]]++] = e;
-        // landmarks by edge count (counting sort, stable)
-        int kmax = 0;
-        for (int l = 0; l < nhl; l++) kmax = std::max(kmax, H.lm_e_start[l + 1] - H.lm_e_start[l]);
-        std::vector<int32_t> kc(kmax + 2, 0);
-        for (int l = 0; l < nhl; l++) kc[H.lm_e_start[l + 1] - H.lm_e_start[l] + 1]++;
-        for (int k = 0; k <= kmax; k++) kc[k + 1] += kc[k];
-        H.lm_perm.assign(std::max(nhl, 1), 0);
-        for (int l = 0; l < nhl; l++) H.lm_perm[kc[H.lm_e_start[l + 1] - H.lm_e_start[l]]++] = l;
+        // k_linearize's landmark groups: consecutive landmarks with at most EB edges together, a
+        // landmark with more alone
+        H.lg_start.assign(1, 0);
+        for (int l = 0; l < nhl;) {
+            int l1 = l + 1;
+            while (l1 < nhl && H.lm_e_start[l1 + 1] - H.lm_e_start[l] <= EB) l1++;
+            H.lg_start.push_back(l1);
+            l = l1;
+        }
+        if (nhl == 0) H.lg_start.push_back(0);
     }
     // blocks per landmark: unique free poses sorted by hessian index
     H.lm_b_start.assign(nhl + 1, 0);
@@ -1483,15 +1519,20 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
     H.blk_lm.assign(nblk, 0);
     for (int l = 0; l < nhl; l++)
         for (int b = H.lm_b_start[l]; b < H.lm_b_start[l + 1]; b++) H.blk_lm[b] = l;
-    // per edge 2 block + (0 for the block's first edge in edge order, else 1): k_linearize stores the
-    // first edge's Hpl terms and adds the others' (a per-block reduction in edge order)
+    // per edge 4 block + 2 (the block has several edges) + 1 (not the block's first edge in edge
+    // order): k_linearize writes a lone edge's Hpl block directly, and stores the first edge's terms
+    // of a shared block and adds the others' (a per-block reduction in edge order)
     {
+        std::vector<int32_t> cnt(nblk, 0);
+        for (int e = 0; e < ne; e++)
+            if (H.edge_blk[e] >= 0) cnt[H.edge_blk[e]]++;
         std::vector<uint8_t> seen(nblk, 0);
         for (int e = 0; e < ne; e++)
             if (H.edge_blk[e] >= 0) {
                 const int b = H.edge_blk[e];
-                H.edge_blk[e] = 2 * b + (seen[b] ? 1 : 0);
+                H.edge_blk[e] = 4 * b + (cnt[b] > 1 ? 2 : 0) + (seen[b] ? 1 : 0);
                 seen[b] = 1;
+                H.multi |= cnt[b] > 1;
             }
     }
     // edges / blocks per hessian pose
@@ -1603,9 +1644,10 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
     }
     H.ge = (ne + EB - 1) / EB;
     H.gl = (nhl + EB - 1) / EB;
+    H.gll = (int)H.lg_start.size() - 1;
     H.gu = (std::max(std::max(nhl, np), npt) + EB - 1) / EB;
     H.nblk_red = (6 * nhp + CB - 1) / CB;
-    H.npart = (std::max(std::max(H.ge, H.gu), std::max(H.gl + nhp, 1)) + 63) & ~63;
+    H.npart = (std::max(std::max(H.ge, H.gu), std::max(H.gll + nhp, 1)) + 63) & ~63;
     H.t_struct = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp0).count();
     return OSG_OK;
 }
@@ -1750,7 +1792,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     // ---- device layout: one packed input block, one state block, the LbaDev / control arrays
     osg_packer pk;
     struct InOff {
-        size_t fixed, epose, epoint, ecam, ekind, eobs, eisig, cams, poseh, hppose, pointh, hlpoint, lmes, lme, lmperm, lmbs,
+        size_t fixed, epose, epoint, ecam, ekind, eobs, eisig, cams, poseh, hppose, pointh, hlpoint, lmes, lme, lgs, lmbs,
             blkpose, eblk, hpes, hpe, hpbs, hpb, pairs, pairab, chs, blklm, pch, pose0, point0, erob,
             prank, rspose, rsrank0, rscs, rsc, hprs, bfirst, blast;
     };
@@ -1775,7 +1817,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         o.hlpoint = pk.add(h.hl_point.data(), 4 * (size_t)nhl);
         o.lmes = pk.add(h.lm_e_start.data(), 4 * (size_t)(nhl + 1));
         o.lme = pk.add(h.lm_e.data(), 4 * (size_t)ne);
-        o.lmperm = pk.add(h.lm_perm.data(), 4 * (size_t)std::max(nhl, 1));
+        o.lgs = pk.add(h.lg_start.data(), 4 * h.lg_start.size());
         o.lmbs = pk.add(h.lm_b_start.data(), 4 * (size_t)(nhl + 1));
         o.blkpose = pk.add(h.blk_pose.data(), 4 * (size_t)nblk);
         o.eblk = pk.add(h.edge_blk.data(), 4 * (size_t)ne);
@@ -1825,6 +1867,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     LbaCtl *d_ctl = (LbaCtl *)(dsm + dev_bytes);
     double *d_out = (double *)(dsm + dev_bytes + ctl_bytes);
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(din, pin, pk.total, hipMemcpyHostToDevice, ctx->stream));
+    int mx_gll = 1;
+    bool any_multi = false;
     int mx_ge = 0, mx_gl = 1, mx_gu = 0, mx_nblk = 0, mx_nhp = 0, mx_chunks = 0, mx_pairs = 0, mx_red = 0, mx_rs = 0;
     // XCD-aware graph placement (LBA_GRAPH) for batches of >= 8 graphs: OSG_LBA_XCD=1.  Off by
     // default: measured slower (64 C4 windows: k_schur_rows 10.4 vs 8.9 ms, k_linearize 5.4 vs 4.4 ms
@@ -1867,7 +1911,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         D.hl_point = osg_dptr<int32_t>(din, o.hlpoint);
         D.lm_e_start = osg_dptr<int32_t>(din, o.lmes);
         D.lm_e = osg_dptr<int32_t>(din, o.lme);
-        D.lm_perm = osg_dptr<int32_t>(din, o.lmperm);
+        D.lg_start = osg_dptr<int32_t>(din, o.lgs);
         D.lm_b_start = osg_dptr<int32_t>(din, o.lmbs);
         D.blk_pose = osg_dptr<int32_t>(din, o.blkpose);
         D.edge_blk = osg_dptr<int32_t>(din, o.eblk);
@@ -1893,6 +1937,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         D.hp_rs_start = osg_dptr<int32_t>(din, o.hprs);
         D.ge = h.ge;
         D.gl = h.gl;
+        D.gll = h.gll;
         D.gu = h.gu;
         D.nblk_red = h.nblk_red;
         D.user_lambda = h.G->user_lambda_init;
@@ -1904,6 +1949,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         OSG_HIP_CHECK(ctx, hipMemcpyAsync(D.pointA, din + o.point0, 24 * (size_t)h.npt, hipMemcpyDeviceToDevice, ctx->stream));
         mx_ge = std::max(mx_ge, h.ge);
         mx_gl = std::max(mx_gl, h.gl);
+        mx_gll = std::max(mx_gll, h.gll);
+        any_multi |= h.multi;
         mx_gu = std::max(mx_gu, h.gu);
         mx_nblk = std::max(mx_nblk, h.nblk);
         mx_nhp = std::max(mx_nhp, h.nhp);
@@ -1955,7 +2002,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         LBA_MARK(KT_ERR);
         hipLaunchKernelGGL(k_errors, gx(mx_ge), dim3(EB), 0, ctx->stream, d_dev, 1);
         LBA_MARK(KT_LIN);
-        hipLaunchKernelGGL(k_linearize, gx(mx_gl), dim3(EB), 0, ctx->stream, d_dev);
+        if (any_multi) hipLaunchKernelGGL(k_linearize<true>, gx(mx_gll), dim3(EB), 0, ctx->stream, d_dev);
+        else hipLaunchKernelGGL(k_linearize<false>, gx(mx_gll), dim3(EB), 0, ctx->stream, d_dev);
         LBA_MARK(KT_POSE);
         if (mx_nhp > 0) hipLaunchKernelGGL(k_pose_red, gx(mx_nhp), dim3(EB), 0, ctx->stream, d_dev);
         LBA_MARK(KT_LINIT);
