@@ -458,8 +458,9 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__
     LBA_GRAPH(M_ACT);
     const int rs = bx;
     if (rs >= D.n_rs) return;
-    __shared__ double s_bd[RS * 18];
+    __shared__ double s_bd[RS * 18 + 2];  // + a zero: the MFMA's K-padding lanes read it
     __shared__ double s_cf[RT / 64][6];
+    if (threadIdx.x == 0) s_bd[RS * 18] = 0.0;
     const int i = D.rs_pose[rs], rb = D.rs_rank0[rs];
     const int hb0 = D.hp_b_start[i];
     const int nr = min(RS, D.hp_b_start[i + 1] - hb0 - rb);
@@ -540,11 +541,13 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__
     // accumulators, summed once at the end: deterministic.
     const int kk = lane >> 4, beta = (lane >> 2) & 3, ri = lane & 3;
     const int arow = 4 * (beta >> 1) + ri, bcol = 4 * (beta & 1) + ri;
-    const bool aok = kk < 3 && arow < 6, bok = kk < 3 && bcol < 6;
-    const int aoff = aok ? 3 * arow + kk : 0, boff = bok ? 3 * bcol + kk : 0;
-    // a padded lane reads element 0 of the same block and multiplies it by 0 (a non-finite block
-    // poisons S through its real lanes anyway), so every load is unconditional
-    const double amask = aok ? 1.0 : 0.0, bmask = bok ? 1.0 : 0.0;
+    // Padding without arithmetic: the K-padding lanes (k = 3) of A read the zero after s_bd, so the
+    // fourth product of every output is exactly 0; the padded rows (A) and columns (B) 6, 7 read
+    // row / column 5 again and only reach the padded outputs, which are never stored.  B's k = 3
+    // lanes read a real (finite) element, multiplied by that zero.
+    const int a_m = kk < 3 ? 18 : 0;  // A's address: a_m * rank + aoff
+    const int aoff = kk < 3 ? 3 * min(arow, 5) + kk : RS * 18;
+    const int boff = 3 * min(bcol, 5) + min(kk, 2);
     const int orow = 4 * (beta >> 1) + kk, ocol = 4 * (beta & 1) + ri;  // D: i = lane >> 4
     const GLOBAL double *__restrict__ Hv = gbl(D.Hpl);
     // Hpl_j blocks are staged per wave through LDS, 16 contributions at a time: 144 16-byte granules
@@ -596,13 +599,12 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__
             for (int v = 0; v < GC; v += 2) {
                 if (v < cnt) {
                     const int rank = __builtin_amdgcn_readlane(my_rank, u + v);
-                    acc0 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[18 * rank + aoff] * amask, hb[18 * v + boff] * bmask,
-                                                              acc0, 0, 0, 0);
+                    acc0 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[a_m * rank + aoff], hb[18 * v + boff], acc0, 0, 0, 0);
                 }
                 if (v + 1 < cnt) {
                     const int rank = __builtin_amdgcn_readlane(my_rank, u + v + 1);
-                    acc1 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[18 * rank + aoff] * amask,
-                                                              hb[18 * (v + 1) + boff] * bmask, acc1, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[a_m * rank + aoff], hb[18 * (v + 1) + boff], acc1, 0,
+                                                              0, 0);
                 }
             }
             __builtin_amdgcn_wave_barrier();
