@@ -138,6 +138,8 @@ __host__ __device__ inline SE3 se3_mul(const SE3 &A, const SE3 &B)
     quat_normalize_rot(r.q);
     return r;
 }
+// UNI: every lane holds the same update (PoseOptimization), see osgx::sincos_rn_small
+template <bool UNI = false>
 __host__ __device__ inline SE3 se3_exp(const double *upd)
 {
     const double w0 = upd[0], w1 = upd[1], w2 = upd[2];
@@ -156,7 +158,7 @@ __host__ __device__ inline SE3 se3_exp(const double *upd)
     } else {
         // sin / cos / pow(theta, 3) of the reference, correctly rounded (exact_math.h)
         double st, ct;
-        osgx::sincos_ref(theta, st, ct);
+        osgx::sincos_ref<UNI>(theta, st, ct);
         const double a = st / theta;
         const double b = (1 - ct) / (theta * theta);
         const double c = (theta - st) / osgx::cube_rn(theta);
@@ -172,9 +174,10 @@ __host__ __device__ inline SE3 se3_exp(const double *upd)
     quat_normalize_rot(O.q);
     return O;
 }
+template <bool UNI = false>
 __host__ __device__ inline void se3_oplus(SE3 &T, const double *upd)
 {
-    const SE3 E = se3_exp(upd);
+    const SE3 E = se3_exp<UNI>(upd);
     T = se3_mul(E, T);
 }
 

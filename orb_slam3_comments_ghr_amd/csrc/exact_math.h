@@ -162,63 +162,82 @@ OSG_HD inline double cos_rn_small(double x)
     return s.h + s.l;
 }
 // sin and cos of one argument at once: the two Horner chains of sin_rn_small / cos_rn_small
-// interleaved in one loop (the same operations on the same values, so the same two results), which
-// lets a latency-bound caller (SE3 exp in the LM loops) overlap them.
+// interleaved (the same operations on the same values, so the same two results), which lets a
+// latency-bound caller (SE3 exp in the LM loops) overlap them.  The chains enter at term K - 1
+// through one switch and run straight on (one branch per call instead of two per unrolled term).
+// UNI: every lane holds the same x (PoseOptimization's redundant update), so K is read from the
+// first lane and the switch is a scalar branch.
+template <bool UNI = false>
 OSG_HD inline void sincos_rn_small(double x, double &sn, double &cs)
 {
     OSGX_NOCONTRACT
-    const dd cs_[15] = {{1.0, 0.0},
-                        {-0.16666666666666666, -9.25185853854297e-18},
-                        {0.008333333333333333, 1.1564823173178714e-19},
-                        {-0.0001984126984126984, -1.7209558293420705e-22},
-                        {2.7557319223985893e-06, -1.858393274046472e-22},
-                        {-2.505210838544172e-08, 1.448814070935912e-24},
-                        {1.6059043836821613e-10, 1.2585294588752098e-26},
-                        {-7.647163731819816e-13, -7.03872877733453e-30},
-                        {2.8114572543455206e-15, 1.6508842730861433e-31},
-                        {-8.22063524662433e-18, -2.2141894119604265e-34},
-                        {1.9572941063391263e-20, -1.3643503830087908e-36},
-                        {-3.868170170630684e-23, 8.843177655482344e-40},
-                        {6.446950284384474e-26, -1.9330404233703465e-42},
-                        {-9.183689863795546e-29, -1.4303150396787322e-45},
-                        {1.1309962886447716e-31, 1.0498015412959506e-47}};
-    const dd cc_[15] = {{1.0, 0.0},
-                        {-0.5, 0.0},
-                        {0.041666666666666664, 2.3129646346357427e-18},
-                        {-0.001388888888888889, 5.300543954373577e-20},
-                        {2.48015873015873e-05, 2.1511947866775882e-23},
-                        {-2.755731922398589e-07, -2.3767714622250297e-23},
-                        {2.08767569878681e-09, -1.20734505911326e-25},
-                        {-1.1470745597729725e-11, -2.0655512752830745e-28},
-                        {4.779477332387385e-14, 4.399205485834081e-31},
-                        {-1.5619206968586225e-16, -1.1910679660273754e-32},
-                        {4.110317623312165e-19, 1.4412973378659527e-36},
-                        {-8.896791392450574e-22, 7.911402614872376e-38},
-                        {1.6117375710961184e-24, -3.6846573564509766e-41},
-                        {-2.4795962632247976e-27, 1.2953730964765229e-43},
-                        {3.279889237069838e-30, 1.5117542744029879e-46}};
+    constexpr dd S0 = {1.0, 0.0}, S1 = {-0.16666666666666666, -9.25185853854297e-18},
+                 S2 = {0.008333333333333333, 1.1564823173178714e-19}, S3 = {-0.0001984126984126984, -1.7209558293420705e-22},
+                 S4 = {2.7557319223985893e-06, -1.858393274046472e-22}, S5 = {-2.505210838544172e-08, 1.448814070935912e-24},
+                 S6 = {1.6059043836821613e-10, 1.2585294588752098e-26}, S7 = {-7.647163731819816e-13, -7.03872877733453e-30},
+                 S8 = {2.8114572543455206e-15, 1.6508842730861433e-31}, S9 = {-8.22063524662433e-18, -2.2141894119604265e-34},
+                 S10 = {1.9572941063391263e-20, -1.3643503830087908e-36}, S11 = {-3.868170170630684e-23, 8.843177655482344e-40},
+                 S12 = {6.446950284384474e-26, -1.9330404233703465e-42}, S13 = {-9.183689863795546e-29, -1.4303150396787322e-45},
+                 S14 = {1.1309962886447716e-31, 1.0498015412959506e-47};
+    constexpr dd C0 = {1.0, 0.0}, C1 = {-0.5, 0.0}, C2 = {0.041666666666666664, 2.3129646346357427e-18},
+                 C3 = {-0.001388888888888889, 5.300543954373577e-20}, C4 = {2.48015873015873e-05, 2.1511947866775882e-23},
+                 C5 = {-2.755731922398589e-07, -2.3767714622250297e-23}, C6 = {2.08767569878681e-09, -1.20734505911326e-25},
+                 C7 = {-1.1470745597729725e-11, -2.0655512752830745e-28}, C8 = {4.779477332387385e-14, 4.399205485834081e-31},
+                 C9 = {-1.5619206968586225e-16, -1.1910679660273754e-32}, C10 = {4.110317623312165e-19, 1.4412973378659527e-36},
+                 C11 = {-8.896791392450574e-22, 7.911402614872376e-38}, C12 = {1.6117375710961184e-24, -3.6846573564509766e-41},
+                 C13 = {-2.4795962632247976e-27, 1.2953730964765229e-43}, C14 = {3.279889237069838e-30, 1.5117542744029879e-46};
     const dd x2 = two_prod(x, x);
-    const int K = series_terms(x);
-    dd a = cs_[14], c = cc_[14];
-#pragma unroll
-    for (int k = 13; k >= 0; k--) {
-        if (k == K - 1) {
-            a = cs_[k];
-            c = cc_[k];
-        } else if (k < K - 1) {
-            a = dd_add(dd_mul(a, x2), cs_[k]);
-            c = dd_add(dd_mul(c, x2), cc_[k]);
-        }
+    int K = series_terms(x);
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (UNI) K = __builtin_amdgcn_readfirstlane(K);
+#endif
+    dd a, c;
+#define OSGX_STEP(k) \
+    a = dd_add(dd_mul(a, x2), S##k); \
+    c = dd_add(dd_mul(c, x2), C##k)
+    switch (K) {
+    case 15: a = S14; c = C14; goto t13;
+    case 14: a = S13; c = C13; goto t12;
+    case 13: a = S12; c = C12; goto t11;
+    case 12: a = S11; c = C11; goto t10;
+    case 11: a = S10; c = C10; goto t9;
+    case 10: a = S9; c = C9; goto t8;
+    case 9: a = S8; c = C8; goto t7;
+    case 8: a = S7; c = C7; goto t6;
+    case 7: a = S6; c = C6; goto t5;
+    case 6: a = S5; c = C5; goto t4;
+    case 5: a = S4; c = C4; goto t3;
+    case 4: a = S3; c = C3; goto t2;
+    case 3: a = S2; c = C2; goto t1;
+    case 2: a = S1; c = C1; goto t0;
+    default: a = S0; c = C0; goto done;
     }
+t13: OSGX_STEP(13);
+t12: OSGX_STEP(12);
+t11: OSGX_STEP(11);
+t10: OSGX_STEP(10);
+t9: OSGX_STEP(9);
+t8: OSGX_STEP(8);
+t7: OSGX_STEP(7);
+t6: OSGX_STEP(6);
+t5: OSGX_STEP(5);
+t4: OSGX_STEP(4);
+t3: OSGX_STEP(3);
+t2: OSGX_STEP(2);
+t1: OSGX_STEP(1);
+t0: OSGX_STEP(0);
+done:
+#undef OSGX_STEP
     const dd r = dd_mul(a, dd{x, 0.0});
     sn = r.h + r.l;
     cs = c.h + c.l;
 }
+template <bool UNI = false>
 OSG_HD inline void sincos_ref(double x, double &sn, double &cs)
 {
     OSGX_NOCONTRACT
     if (x >= 0.0 && x <= 0.8) {
-        sincos_rn_small(x, sn, cs);
+        sincos_rn_small<UNI>(x, sn, cs);
     } else {
         sn = sin(x);
         cs = cos(x);

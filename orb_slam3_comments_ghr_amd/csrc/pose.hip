@@ -532,7 +532,7 @@ __global__ __launch_bounds__(NW *PW) void k_pose_opt(const PoseProbDev *__restri
                         for (int i = 0; i < 6; i++) xs[i] = x[i];
                     PROF_ADD(1, t_s);
                     PROF_T(t_x);
-                    se3_oplus(pose, xs);  // exp(update) * estimate
+                    se3_oplus<true>(pose, xs);  // exp(update) * estimate (every lane holds the same update)
                     PROF_ADD(2, t_x);
                     PROF_T(t_c);
                     double tempChi = chi_pass(pose);

@@ -53,6 +53,14 @@ __global__ __launch_bounds__(64) void k_cost(const double *in, unsigned long lon
             x += T.q[0];
         } else if (VAR == 8) {  // cube_rn
             x = osgx::cube_rn(x * 0.5 + 0.5);
+        } else if (VAR == 9) {  // sincos_ref with the argument uniform across the wave (PoseOptimization)
+            double s, c;
+            osgx::sincos_ref<true>(1e-3 * (1.0 + 1e-3 * __shfl(x, 0)), s, c);
+            x += s + c;
+        } else if (VAR == 10) {  // se3_oplus<true>
+            upd[0] += 1e-12 * __shfl(x, 0);
+            se3_oplus<true>(T, upd);
+            x += T.q[0];
         }
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -85,9 +93,10 @@ int main()
     (void)hipMalloc(&dsink, 8 * 64);
     (void)hipMemcpy(din, in, sizeof(in), hipMemcpyHostToDevice);
     std::printf("{\"fp64_add\": %.1f, \"fp64_fma\": %.1f, \"sqrt\": %.1f, \"div\": %.1f, \"sincos_ref\": %.1f, "
-                "\"se3_exp\": %.1f, \"se3_mul\": %.1f, \"se3_oplus\": %.1f, \"cube_rn\": %.1f}\n",
+                "\"se3_exp\": %.1f, \"se3_mul\": %.1f, \"se3_oplus\": %.1f, \"cube_rn\": %.1f, \"sincos_ref_uniform\": %.1f, "
+                "\"se3_oplus_uniform\": %.1f}\n",
                 run<0>(din, dc, dsink) / 16, run<1>(din, dc, dsink) / 16, run<2>(din, dc, dsink) / 4,
                 run<3>(din, dc, dsink) / 4, run<4>(din, dc, dsink), run<5>(din, dc, dsink), run<6>(din, dc, dsink),
-                run<7>(din, dc, dsink), run<8>(din, dc, dsink));
+                run<7>(din, dc, dsink), run<8>(din, dc, dsink), run<9>(din, dc, dsink), run<10>(din, dc, dsink));
     return 0;
 }
