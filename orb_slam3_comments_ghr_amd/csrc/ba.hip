@@ -1856,7 +1856,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     const size_t out_bytes = sizeof(double) * 8 * (size_t)NA;
     char *pin = (char *)osg_pinned(ctx, in_pad + dev_bytes + ctl_bytes + out_bytes + 1024);
     if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    OSG_RC(osg_idle(ctx));  // the pinned block may still be in use
     pk.fill_parallel(pin, std::min(16, std::max(1, (int)std::thread::hardware_concurrency())));
     LbaDev *h_dev = (LbaDev *)(pin + in_pad);
     LbaCtl *h_ctl = (LbaCtl *)((char *)h_dev + dev_bytes);
@@ -2058,8 +2058,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         hipLaunchKernelGGL(k_step_reduce, yb, dim3(256), 0, ctx->stream, d_dev);
         LBA_MARK(KT_END);
         OSG_HIP_CHECK(ctx, hipGetLastError());
-        OSG_HIP_CHECK(ctx, hipMemcpyAsync(h_out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
-        OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+        OSG_RC(osg_download(ctx, h_out, d_out, out_bytes));
+        OSG_RC(osg_wait(ctx));
         return collect();
     };
 
@@ -2205,7 +2205,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         if (R->edge_chi2 && h.ne > 0)
             OSG_HIP_CHECK(ctx, hipMemcpyAsync(R->edge_chi2, D.chi2o, 8 * (size_t)h.ne, hipMemcpyDeviceToHost, ctx->stream));
     }
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    OSG_RC(osg_wait(ctx));
     {
         const int rc = collect();
         if (rc < 0) return rc;

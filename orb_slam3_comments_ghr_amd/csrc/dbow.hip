@@ -533,7 +533,7 @@ int osg_vocabulary_transform_batch(osg_ctx *ctx, const osg_vocabulary *voc, cons
     const size_t o_feat = pk.add(desc, 32 * (size_t)total);
     char *pin = (char *)osg_pinned(ctx, pk.total + 64 * (size_t)total + 256 * (size_t)B + 4096);
     if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    OSG_RC(osg_idle(ctx));  // the pinned block may still be in use
     pk.fill(pin);
     char *din = nullptr, *dmid = nullptr, *dout = nullptr;
     SetArgs *dsets = nullptr;
@@ -587,8 +587,8 @@ int osg_vocabulary_transform_batch(osg_ctx *ctx, const osg_vocabulary *voc, cons
     OSG_HIP_CHECK(ctx, hipGetLastError());
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
     char *pout = (char *)pin_sets + ((sizeof(SetArgs) * B + 255) & ~size_t(255));
-    OSG_HIP_CHECK(ctx, hipMemcpyAsync(pout, dout, so[B], hipMemcpyDeviceToHost, ctx->stream));
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    OSG_RC(osg_download(ctx, pout, dout, so[B]));
+    OSG_RC(osg_wait(ctx));
     float kms = 0.f;
     OSG_HIP_CHECK(ctx, hipEventElapsedTime(&kms, ev[0], ev[1]));
     ctx->last_kernel_ms = kms;

@@ -117,7 +117,7 @@ int osg_compute_distinctive_descriptors(osg_ctx *ctx, const uint8_t *desc, const
     const size_t o_bytes = sizeof(int32_t) * (size_t)n_points;
     char *pin = (char *)osg_pinned(ctx, d_bytes + s_bytes + o_bytes + 256);
     if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));  // the pinned block may still be in use
+    OSG_RC(osg_idle(ctx));  // the pinned block may still be in use
     if (total) std::memcpy(pin, desc, total * 32);
     std::memcpy(pin + d_bytes, start, sizeof(int32_t) * (n_points + 1));
     int32_t *pin_out = (int32_t *)(pin + d_bytes + s_bytes);
@@ -130,8 +130,8 @@ int osg_compute_distinctive_descriptors(osg_ctx *ctx, const uint8_t *desc, const
     int rc = launch(ctx, dev, dev + d_bytes, n_points, dev + d_bytes + s_bytes);
     if (rc < 0) return rc;
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
-    OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_out, dev + d_bytes + s_bytes, o_bytes, hipMemcpyDeviceToHost, ctx->stream));
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    OSG_RC(osg_download(ctx, pin_out, dev + d_bytes + s_bytes, o_bytes));
+    OSG_RC(osg_wait(ctx));
     float ms = 0.f;
     OSG_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ev[0], ev[1]));
     ctx->last_kernel_ms = ms;

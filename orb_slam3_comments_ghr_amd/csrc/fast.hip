@@ -347,7 +347,7 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
     // pinned: inputs, then the total (and later the keys)
     char *pin = (char *)osg_pinned(ctx, pk.total + 256 + sizeof(float4) * (max_keys + 1) + 256);
     if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));  // the pinned block may still be in use
+    OSG_RC(osg_idle(ctx));  // the pinned block may still be in use
     pk.fill_parallel(pin, 8);
     char *pin_out = pin + ((pk.total + 255) & ~size_t(255));
     hipEvent_t *ev = osg_ctx_events(ctx);
@@ -364,16 +364,15 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
     int32_t total = 0;
     std::vector<int32_t> offs(nc + 1, 0);
     if (nc > 0) {
-        OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_out, (const void *)d_total, sizeof(int32_t), hipMemcpyDeviceToHost,
-                                          ctx->stream));
-        OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+        OSG_RC(osg_download(ctx, pin_out, (const void *)d_total, sizeof(int32_t)));
+        OSG_RC(osg_wait(ctx));
         total = *(int32_t *)pin_out;
         OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_out, CA.keys, sizeof(float4) * (size_t)total, hipMemcpyDeviceToHost,
                                           ctx->stream));
         OSG_HIP_CHECK(ctx, hipMemcpyAsync(offs.data() + 1, dcnt, sizeof(int32_t) * nc, hipMemcpyDeviceToHost,
                                           ctx->stream));
     }
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    OSG_RC(osg_wait(ctx));
     for (int c = 0; c < nc; c++) offs[c + 1] += offs[c];  // counts -> offsets
     const double t_gpu = ms_since(tp0);
     const auto tp1 = std::chrono::steady_clock::now();

@@ -744,7 +744,7 @@ int osg_launch_top2(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d
         static const int32_t sentinel[3] = {-1, 256, 256};
         int32_t *h = (int32_t *)osg_pinned(ctx, sizeof(int32_t) * 3 * (size_t)nq);
         if (!h) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
-        OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+        OSG_RC(osg_idle(ctx));  // the pinned block may still be in use
         for (int i = 0; i < nq; i++) memcpy(h + 3 * i, sentinel, sizeof sentinel);
         OSG_HIP_CHECK(ctx, hipMemcpyAsync(d_out, h, sizeof(int32_t) * 3 * (size_t)nq, hipMemcpyHostToDevice, ctx->stream));
         return OSG_OK;
@@ -937,8 +937,8 @@ int osg_hamming_top2(osg_ctx *ctx, const uint8_t *query, int32_t nq, const uint8
     if (rc < 0) return rc;
     int32_t *h = (int32_t *)osg_pinned(ctx, (size_t)nq * 12);
     if (!h) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
-    OSG_HIP_CHECK(ctx, hipMemcpyAsync(h, dout, (size_t)nq * 12, hipMemcpyDeviceToHost, ctx->stream));
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    OSG_RC(osg_download(ctx, h, dout, (size_t)nq * 12));
+    OSG_RC(osg_wait(ctx));
     for (int i = 0; i < nq; i++) {
         best_idx[i] = h[3 * i];
         best_dist[i] = h[3 * i + 1];
@@ -962,8 +962,8 @@ int osg_descriptor_distance_pairs(osg_ctx *ctx, const uint8_t *a, const uint8_t 
     hipLaunchKernelGGL(k_pair_dist, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, (const uint4 *)da,
                        (const uint4 *)db, n, (int32_t *)dout);
     OSG_HIP_CHECK(ctx, hipGetLastError());
-    OSG_HIP_CHECK(ctx, hipMemcpyAsync(out, dout, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    OSG_RC(osg_download(ctx, out, dout, (size_t)n * 4));
+    OSG_RC(osg_wait(ctx));
     return OSG_OK;
 }
 

@@ -447,7 +447,7 @@ int init_run(osg_ctx *ctx, const osg_frame *F1, const osg_frame *F2, float *prev
     const size_t out_bytes = sizeof(int32_t) * (o_base[B] + 2 * (size_t)B);
     char *pin = (char *)osg_pinned(ctx, in_bytes + args_bytes + out_bytes + 256);
     if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));  // the pinned block may still be in use
+    OSG_RC(osg_idle(ctx));  // the pinned block may still be in use
     pk.fill_parallel(pin, 8);
     InitArgs *pin_args = (InitArgs *)(pin + in_bytes);
     int32_t *pin_out = (int32_t *)((char *)pin_args + args_bytes);
@@ -489,8 +489,8 @@ int init_run(osg_ctx *ctx, const osg_frame *F1, const osg_frame *F2, float *prev
     hipLaunchKernelGGL(k_init, dim3(B), dim3(IT), 0, ctx->stream, dev_args);
     OSG_HIP_CHECK(ctx, hipGetLastError());
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
-    OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_out, dev_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    OSG_RC(osg_download(ctx, pin_out, dev_out, out_bytes));
+    OSG_RC(osg_wait(ctx));
     float ms = 0.f;
     OSG_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ev[0], ev[1]));
     ctx->last_kernel_ms = ms;

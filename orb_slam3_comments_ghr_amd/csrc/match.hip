@@ -27,6 +27,7 @@
 //   5. finish  — last assignment per slot, rotation histogram with the reference's 1/30 factor,
 //                ComputeThreeMaxima, removal, nmatches.
 #include <algorithm>
+#include <chrono>
 #include <deque>
 #include <type_traits>
 #include <string>
@@ -1426,6 +1427,10 @@ int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_
 {
     const int B = (int)P.size();
     if (B == 0) return OSG_OK;
+    // host phase stamps for OSG_MATCH_PROFILE=2: setup, sync + pack, launches, wait, results
+    using hclock = std::chrono::steady_clock;
+    hclock::time_point hs[6], hx[4];
+    hs[0] = hclock::now();
     std::vector<size_t> slot_off(B + 1, 0), q_base(B + 1, 0);
     size_t lds = 0;
     for (int b = 0; b < B; b++) {
@@ -1463,7 +1468,9 @@ int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_
     const size_t args_bytes = sizeof(MatchArgs) * (size_t)B;
     char *pin = (char *)osg_pinned(ctx, in_bytes + io_pad + args_bytes + 256);
     if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));  // pinned block may still be in use
+    hs[1] = hclock::now();
+    OSG_RC(osg_idle(ctx));  // the pinned block may still be in use
+    hx[0] = hclock::now();
     pk.fill(pin);
     char *pin_io = pin + in_bytes;
     MatchArgs *pin_args = (MatchArgs *)(pin_io + io_pad);
@@ -1528,11 +1535,14 @@ int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_
         // the inputs, the status block, the input slot state and the arguments in one copy; a retry
         // re-uploads [io | args] (it must not see the slot arrays written by the problems that fitted
         // the first time)
+        if (attempt == 0) hs[2] = hclock::now();
         if (attempt == 0) OSG_RC(osg_upload(ctx, dev_in, pin, in_bytes + io_pad + args_bytes));
+        if (attempt == 0) hx[1] = hclock::now();
         else OSG_RC(osg_upload(ctx, dev_io, pin_io, io_pad + args_bytes));
         hipEvent_t *ev = osg_ctx_events(ctx);
         if (!ev) return osg_set_error(ctx, OSG_E_HIP, "event create failed");
         OSG_HIP_CHECK(ctx, hipEventRecord(ev[0], ctx->stream));
+        if (attempt == 0) hx[2] = hclock::now();
         if (BOW) {
             int max_nq = 0;
             for (int b = 0; b < B; b++) max_nq = std::max(max_nq, P[b].A.prefilled ? P[b].A.nq : 0);
@@ -1571,11 +1581,14 @@ int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_
         else
             hipLaunchKernelGGL((k_match<MODE, 0>), dim3(B), dim3(MT), lds, ctx->stream, dev_args);
         OSG_HIP_CHECK(ctx, hipGetLastError());
+        if (attempt == 0) hx[3] = hclock::now();
         OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
         // status, slot arrays and KF-KF results in one copy (the pinned io block is re-filled from the
         // callers' slots before a retry)
         OSG_RC(osg_download(ctx, pin_io, dev_io, io_bytes));
+        hs[3] = hclock::now();
         OSG_RC(osg_wait(ctx));
+        hs[4] = hclock::now();
         std::memcpy(st.data(), pin_io, status_bytes);
         bool overflow = false;
         for (int b = 0; b < B; b++)
@@ -1614,7 +1627,17 @@ int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_
     float ms = 0.f;
     OSG_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]));
     ctx->last_kernel_ms = ms;
-    static const bool prof = getenv("OSG_MATCH_PROFILE") != nullptr;
+    static const int prof_level = getenv("OSG_MATCH_PROFILE") ? atoi(getenv("OSG_MATCH_PROFILE")) : 0;
+    const bool prof = prof_level > 0;
+    hs[5] = hclock::now();
+    if (prof_level >= 2) {
+        auto us = [&](int a, int b) { return std::chrono::duration<double, std::micro>(hs[b] - hs[a]).count(); };
+        auto ux = [&](hclock::time_point a, hclock::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+        fprintf(stderr, "[osg match host] mode %d B %d: setup %.1f | sync+pack %.1f | launches %.1f | wait %.1f | results %.1f us"
+                        " || sync %.1f fill %.1f | upload %.1f event %.1f kernels %.1f event+download %.1f (pack %zu B)\n",
+                MODE, B, us(0, 1), us(1, 2), us(2, 3), us(3, 4), us(4, 5), ux(hs[1], hx[0]), ux(hx[0], hs[2]),
+                ux(hs[2], hx[1]), ux(hx[1], hx[2]), ux(hx[2], hx[3]), ux(hx[3], hs[3]), (size_t)pk.total);
+    }
     if (prof)
         fprintf(stderr, "[osg match] mode %d B %d kernel %.3f ms | problem 0: nq %d cands %d rounds %d serial %d | "
                         "clk stage %d windows %d count %d scan %d fill %d init %d rounds %d finish %d (stage %d)\n",

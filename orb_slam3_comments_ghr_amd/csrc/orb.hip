@@ -248,7 +248,7 @@ int orb_run(osg_ctx *ctx, const osg_image_pyramid *raw, const osg_image_pyramid 
     const size_t out_bytes = o_desc + (size_t)n * 32;
     char *pin = (char *)osg_pinned(ctx, in_bytes + out_bytes + 256);
     if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));  // the pinned block may still be in use
+    OSG_RC(osg_idle(ctx));  // the pinned block may still be in use
     pk.fill_parallel(pin, 8);
     char *pin_out = pin + in_bytes;
     char *dev_in = nullptr, *dev_out = nullptr;
@@ -277,8 +277,8 @@ int orb_run(osg_ctx *ctx, const osg_image_pyramid *raw, const osg_image_pyramid 
         hipLaunchKernelGGL(k_orb_angle, dim3((n + 3) / 4), dim3(256), 0, ctx->stream, A);
         OSG_HIP_CHECK(ctx, hipGetLastError());
         OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
-        OSG_HIP_CHECK(ctx, hipMemcpyAsync(ang, dev_out, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
-        OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+        OSG_RC(osg_download(ctx, ang, dev_out, sizeof(float) * n));
+        OSG_RC(osg_wait(ctx));
         OSG_HIP_CHECK(ctx, hipEventElapsedTime(&ms_angle, ev[0], ev[1]));
     } else {
         std::memcpy(ang, angle, sizeof(float) * n);
@@ -296,9 +296,8 @@ int orb_run(osg_ctx *ctx, const osg_image_pyramid *raw, const osg_image_pyramid 
     hipLaunchKernelGGL(k_orb_desc, dim3((n + 7) / 8), dim3(256), 0, ctx->stream, A);
     OSG_HIP_CHECK(ctx, hipGetLastError());
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
-    OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_out + o_bad, dev_out + o_bad, out_bytes - o_bad, hipMemcpyDeviceToHost,
-                                      ctx->stream));
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    OSG_RC(osg_download(ctx, pin_out + o_bad, dev_out + o_bad, out_bytes - o_bad));
+    OSG_RC(osg_wait(ctx));
     float ms_desc = 0.f;
     OSG_HIP_CHECK(ctx, hipEventElapsedTime(&ms_desc, ev[0], ev[1]));
     ctx->last_kernel_ms = ms_angle + ms_desc;

@@ -65,6 +65,9 @@ int osg_download(osg_ctx *ctx, void *dst_pinned, const void *src_dev, size_t byt
 // hipEventQuery (a one-frame call returns within ~1 us of its last kernel instead of a blocking
 // synchronisation's wake-up)
 int osg_wait(osg_ctx *ctx);
+// Before reusing the pinned block: nothing left on the stream.  A query first — a call that ended in
+// osg_wait left the stream idle, and a synchronisation of an idle stream measured up to 14 us.
+int osg_idle(osg_ctx *ctx);
 
 #define OSG_HIP_CHECK(ctx, expr)                                                             \
     do {                                                                                     \

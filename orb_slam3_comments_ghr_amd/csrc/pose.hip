@@ -656,7 +656,7 @@ int osg_pose_optimization_batch(osg_ctx *ctx, const osg_pose_problem *p, int32_t
     const size_t io_bytes = o_res + sizeof(PoseOut) * nb + 256;
     char *pin = (char *)osg_pinned(ctx, in_bytes + io_bytes);
     if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    OSG_RC(osg_idle(ctx));  // the pinned block may still be in use
     pk.fill(pin);
     (void)o_probs;
     for (int b = 0; b < nb; b++) {

@@ -352,7 +352,7 @@ int pyramid_run(osg_ctx *ctx, const uint8_t *image, int32_t rows, int32_t cols, 
     if (pk.total) {
         char *pin = (char *)osg_pinned(ctx, pk.total + 256);
         if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
-        OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));  // the pinned block may still be in use
+        OSG_RC(osg_idle(ctx));  // the pinned block may still be in use
         OSG_ALLOC(ctx, din, SLOT_TMP0, pk.total + 256);
         if (fused) {
             GroupArgs G{};
@@ -423,7 +423,7 @@ int pyramid_run(osg_ctx *ctx, const uint8_t *image, int32_t rows, int32_t cols, 
             OSG_HIP_CHECK(ctx, hipGetLastError());
         }
         OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
-        OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+        OSG_RC(osg_wait(ctx));
         float ms = 0.f;
         OSG_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ev[0], ev[1]));
         ctx->last_kernel_ms = ms;
@@ -471,7 +471,7 @@ int pyramid_run(osg_ctx *ctx, const uint8_t *image, int32_t rows, int32_t cols, 
         OSG_HIP_CHECK(ctx, hipGetLastError());
     }
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    OSG_RC(osg_wait(ctx));
     float ms = 0.f;
     OSG_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ev[0], ev[1]));
     ctx->last_kernel_ms = ms;

@@ -120,6 +120,13 @@ int osg_download(osg_ctx *ctx, void *dst_pinned, const void *src_dev, size_t byt
     return OSG_OK;
 }
 
+int osg_idle(osg_ctx *ctx)
+{
+    if (hipStreamQuery(ctx->stream) == hipSuccess) return OSG_OK;
+    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    return OSG_OK;
+}
+
 int osg_wait(osg_ctx *ctx)
 {
     if (!ctx->ev_done && hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming) != hipSuccess) {

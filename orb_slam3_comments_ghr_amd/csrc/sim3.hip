@@ -219,7 +219,7 @@ int sim3_run(osg_ctx *ctx, const osg_frame *KF, const osg_fuse_queries *Q, int B
     const size_t out_bytes = sizeof(int32_t) * (nq_total + B);
     char *pin = (char *)osg_pinned(ctx, in_bytes + args_bytes + out_bytes + 256);
     if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));  // the pinned block may still be in use
+    OSG_RC(osg_idle(ctx));  // the pinned block may still be in use
     pk.fill_parallel(pin, 8);
     Sim3Args *pin_args = (Sim3Args *)(pin + in_bytes);
     int32_t *pin_out = (int32_t *)((char *)pin_args + args_bytes);
@@ -257,8 +257,8 @@ int sim3_run(osg_ctx *ctx, const osg_frame *KF, const osg_fuse_queries *Q, int B
     hipLaunchKernelGGL(k_sim3, dim3(B), dim3(ST), 0, ctx->stream, dev_args);
     OSG_HIP_CHECK(ctx, hipGetLastError());
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
-    OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_out, dev_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    OSG_RC(osg_download(ctx, pin_out, dev_out, out_bytes));
+    OSG_RC(osg_wait(ctx));
     float ms = 0.f;
     OSG_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ev[0], ev[1]));
     ctx->last_kernel_ms = ms;

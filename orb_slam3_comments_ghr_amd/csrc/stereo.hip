@@ -394,7 +394,7 @@ int stereo_run(osg_ctx *ctx, const osg_stereo_frame *F, int B, float *u_right, f
     const size_t out_bytes = sizeof(int32_t) * (3 * o_base[B] + B);
     char *pin = (char *)osg_pinned(ctx, in_bytes + args_bytes + out_bytes + 256);
     if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));  // the pinned block may still be in use
+    OSG_RC(osg_idle(ctx));  // the pinned block may still be in use
     pk.fill_parallel(pin, 8);
     StereoArgs *pin_args = (StereoArgs *)(pin + in_bytes);
     int32_t *pin_out = (int32_t *)((char *)pin_args + args_bytes);
@@ -439,8 +439,8 @@ int stereo_run(osg_ctx *ctx, const osg_stereo_frame *F, int B, float *u_right, f
     hipLaunchKernelGGL(k_stereo_filter, dim3(B), dim3(1024), 0, ctx->stream, dev_args);
     OSG_HIP_CHECK(ctx, hipGetLastError());
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
-    OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_out, dev_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    OSG_RC(osg_download(ctx, pin_out, dev_out, out_bytes));
+    OSG_RC(osg_wait(ctx));
     float ms = 0.f;
     OSG_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ev[0], ev[1]));
     ctx->last_kernel_ms = ms;

@@ -338,7 +338,7 @@ int triang_run(osg_ctx *ctx, const osg_kf_side *K1, const osg_kf_side *K2, const
     const size_t out_bytes = sizeof(int32_t) * (nq_total + B);
     char *pin = (char *)osg_pinned(ctx, in_bytes + args_bytes + out_bytes + 256);
     if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));  // the pinned block may still be in use
+    OSG_RC(osg_idle(ctx));  // the pinned block may still be in use
     pk.fill_parallel(pin, 8);
     TriArgs *pin_args = (TriArgs *)(pin + in_bytes);
     int32_t *pin_out = (int32_t *)((char *)pin_args + args_bytes);
@@ -380,8 +380,8 @@ int triang_run(osg_ctx *ctx, const osg_kf_side *K1, const osg_kf_side *K2, const
     hipLaunchKernelGGL(k_triang, dim3(B), dim3(TT), 0, ctx->stream, dev_args);
     OSG_HIP_CHECK(ctx, hipGetLastError());
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
-    OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_out, dev_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    OSG_RC(osg_download(ctx, pin_out, dev_out, out_bytes));
+    OSG_RC(osg_wait(ctx));
     float ms = 0.f;
     OSG_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ev[0], ev[1]));
     ctx->last_kernel_ms = ms;
@@ -507,7 +507,7 @@ int stereo_fisheye_run(osg_ctx *ctx, int32_t n_left, int32_t mono_left, const ui
     const size_t in_bytes = (pk.total + 255) & ~size_t(255);
     char *pin = (char *)osg_pinned(ctx, in_bytes + out_bytes + 256);
     if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));  // the pinned block may still be in use
+    OSG_RC(osg_idle(ctx));  // the pinned block may still be in use
     pk.fill(pin);
     char *pin_out = pin + in_bytes;
     char *dev_in = nullptr, *dev_out = nullptr;
@@ -543,8 +543,8 @@ int stereo_fisheye_run(osg_ctx *ctx, int32_t n_left, int32_t mono_left, const ui
     hipLaunchKernelGGL(k_stereo_fisheye, dim3((nq + 3) / 4), dim3(256), 0, ctx->stream, A);
     OSG_HIP_CHECK(ctx, hipGetLastError());
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
-    OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_out, dev_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
-    OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    OSG_RC(osg_download(ctx, pin_out, dev_out, out_bytes));
+    OSG_RC(osg_wait(ctx));
     float ms = 0.f;
     OSG_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ev[0], ev[1]));
     ctx->last_kernel_ms = ms;
