@@ -79,6 +79,7 @@ def parse():
     ap.add_argument("--frames", type=int, default=1024, help="frames per launch (C3 / C5 batches)")
     ap.add_argument("--frame-reps", type=int, default=5)
     ap.add_argument("--no-wall", action="store_true", help="skip the C++ adapter wall-rate runs")
+    ap.add_argument("--only", default="", help="comma-separated stage keys to run (A/B runs); default: all")
     ap.add_argument("--wall-frames", type=int, default=256, help="frames per batched adapter call (C++ wall bench)")
     ap.add_argument("--wall-reps", type=int, default=8, help="timed repetitions per host thread (C++ wall bench)")
     ap.add_argument("--wall-threads", type=int, default=8,
@@ -306,7 +307,11 @@ def main():
         out["speedup_vs_cpu_node_estimate"] = round(value / cb["node_estimate"]["value"], 2)
 
     # ---- frame-batched C3 / C5: matching + PoseOptimization, B frames per launch ------------
+    only = set(args.only.split(",")) if args.only else None
+
     def stage(key, fn):
+        if only is not None and key not in only:
+            return
         if rank == 0:  # progress on stderr: a long run shows it is alive
             print(f"[bench] {key} ({time.perf_counter() - t_start:.0f} s)", file=sys.stderr, flush=True)
         out[key] = fn(ctx, rank, world, dist, dev, args)

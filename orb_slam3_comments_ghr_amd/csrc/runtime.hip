@@ -1,3 +1,4 @@
+#include <string>
 // runtime.hip — context lifecycle, scratch pool, errors (C ABI: include/osg.h "context").
 #include <algorithm>
 #include <cstdarg>
@@ -129,6 +130,12 @@ int osg_idle(osg_ctx *ctx)
 
 int osg_wait(osg_ctx *ctx)
 {
+    // OSG_WAIT=sync: a stream synchronisation instead of the polled event (A/B runs)
+    static const bool sync_wait = getenv("OSG_WAIT") && std::string(getenv("OSG_WAIT")) == "sync";
+    if (sync_wait) {
+        OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+        return OSG_OK;
+    }
     if (!ctx->ev_done && hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming) != hipSuccess) {
         ctx->ev_done = nullptr;
         OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
