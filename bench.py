@@ -74,7 +74,11 @@ def parse():
     ap.add_argument("--ba-batch", type=int, default=64, help="C4 windows per GPU per lockstep batch")
     ap.add_argument("--ba-batch-reps", type=int, default=6)
     ap.add_argument("--ba-threads", type=int, default=4,
-                    help="host threads per GPU driving LBA batches, each with its own context and HIP stream")
+                    help="host threads per GPU for the one-frame-per-call ORB stages' wall rate, each with its own "
+                         "context and HIP stream")
+    ap.add_argument("--lba-threads", type=int, default=8,
+                    help="host threads per GPU driving LocalBA batches, each with its own context and HIP stream "
+                         "(8 measured 9-18 %% above 4: more batches in flight cover each thread's host phases)")
     ap.add_argument("--no-frames", action="store_true", help="skip the frame-batched C3 / C5 workloads")
     ap.add_argument("--frames", type=int, default=1024, help="frames per launch (C3 / C5 batches)")
     ap.add_argument("--frame-reps", type=int, default=5)
@@ -426,7 +430,7 @@ def bench_lba(ctx, rank, world, dist, dev, args):
     # build and packing overlap the others' device steps, and their kernels share the GPU
     import threading
     B = args.ba_batch
-    T = max(1, args.ba_threads)
+    T = max(1, args.lba_threads)
     pool = [G] + [op.synth_lba_graph(rng, n_kf=50, n_points=10000) for _ in range(7)]
     graphs = [pool[i % len(pool)] for i in range(B)]
     ctxs = [ctx] + [type(ctx)(ctx.device) for _ in range(T - 1)]
