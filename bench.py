@@ -11,9 +11,15 @@ osg_hamming_top2_batch_dev (k_top2_batch) with inputs resident in HBM; the one-p
 independent frames (weak scaling; no collective in the data path); value = pairs of all ranks /
 max-over-ranks time.
 
-Also reported (same run): the dominant kernel's roofline (HIP events on its stream), the
-C2' streaming kernel's HBM roofline (Q = 4 x M = 2^24), the CPU restatement timed on this host
-(cpu_baseline), and — when the BA kernels are built — LocalBA iterations/s on C4.
+Also reported (same run):
+  * the dominant kernel's roofline (HIP events on its stream) and the C2' streaming kernel's HBM roofline
+    (Q = 4 x M = 2^24);
+  * the CPU restatement timed on this host (cpu_baseline);
+  * the frame-batched workloads: C3, C5, DBoW2, ComputeStereoMatches and the ORB extractor stages, with their
+    single-call latencies and the C++ adapter's wall rate (tools/adapter_wall_bench.cpp);
+  * LocalBA iterations/s on C4 (64-window batches, --lba-threads host threads);
+  * global BA on 150 KeyFrames and on the 1500-KeyFrame map.
+--only STAGE[,STAGE] runs a subset of those stages (A/B runs).
 """
 from __future__ import annotations
 
