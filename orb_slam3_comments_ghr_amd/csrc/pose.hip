@@ -640,6 +640,9 @@ int osg_pose_optimization_batch(osg_ctx *ctx, const osg_pose_problem *p, int32_t
         // waves per frame: up to one per 1.5 chunks of a lone frame's edges (latency; 8 waves share
         // 4 SIMDs and measured no faster than 4), one when the batch fills the chip's wave slots
         while (nw < 4 && 3 * nw <= 2 * chunks && (size_t)nb * 2 * nw <= 2048) nw *= 2;
+        // a lone frame of >= 9 chunks (576 edges): 8 waves measured faster (the 600-edge KB8 frame 811 -> 758
+        // us; the 318-edge frame is slower with 8: 468 against 432 us)
+        if (nw == 4 && chunks >= 9 && (size_t)nb * 2 * 8 <= 2048) nw = 8;
         while (nw < 8 && chunks > 64 * nw) nw *= 2;
     }
     OSG_REQUIRE(ctx, nw == 1 || nw == 2 || nw == 4 || nw == 8, "OSG_POSE_NW must be 1, 2, 4 or 8");

@@ -90,7 +90,7 @@ def main():
         ob = np.zeros(P.n, np.uint8)
         r.outlier = ob.ctypes.data
         d = {}
-        for var in ["4", None]:  # 4 waves per frame, then the host's choice
+        for var in ["4", "8", None]:  # 4 and 8 waves per frame, then the host's choice
             if var is None:
                 os.environ.pop("OSG_POSE_NW", None)
             else:
