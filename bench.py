@@ -91,7 +91,7 @@ def parse():
     ap.add_argument("--no-wall", action="store_true", help="skip the C++ adapter wall-rate runs")
     ap.add_argument("--only", default="", help="comma-separated stage keys to run (A/B runs); default: all")
     ap.add_argument("--wall-frames", type=int, default=256, help="frames per batched adapter call (C++ wall bench)")
-    ap.add_argument("--wall-reps", type=int, default=8, help="timed repetitions per host thread (C++ wall bench)")
+    ap.add_argument("--wall-reps", type=int, default=24, help="timed repetitions per host thread (C++ wall bench)")
     ap.add_argument("--wall-threads", type=int, default=8,
                     help="host threads of the C++ wall bench, each with its own context (Tracking threads)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
