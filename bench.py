@@ -85,6 +85,9 @@ def parse():
     ap.add_argument("--lba-threads", type=int, default=8,
                     help="host threads per GPU driving LocalBA batches, each with its own context and HIP stream "
                          "(8 measured 9-18 %% above 4: more batches in flight cover each thread's host phases)")
+    ap.add_argument("--gba-batch", type=int, default=8, help="150-KF maps per GPU per lockstep global-BA batch")
+    ap.add_argument("--gba-threads", type=int, default=8, help="host threads per GPU driving global-BA batches")
+    ap.add_argument("--gba-batch-reps", type=int, default=3)
     ap.add_argument("--no-frames", action="store_true", help="skip the frame-batched C3 / C5 workloads")
     ap.add_argument("--frames", type=int, default=1024, help="frames per launch (C3 / C5 batches)")
     ap.add_argument("--frame-reps", type=int, default=5)
@@ -434,7 +437,6 @@ def bench_lba(ctx, rank, world, dist, dev, args):
     # batched: B independent C4 windows per GPU in lockstep (roofline on B = 64 graphs/GPU),
     # driven by T host threads, each with its own context (own HIP stream): one thread's structure
     # build and packing overlap the others' device steps, and their kernels share the GPU
-    import threading
     B = args.ba_batch
     T = max(1, args.lba_threads)
     pool = [G] + [op.synth_lba_graph(rng, n_kf=50, n_points=10000) for _ in range(7)]
@@ -444,26 +446,7 @@ def bench_lba(ctx, rank, world, dist, dev, args):
     brep = max(1, args.ba_batch_reps)
 
     def timed(nthr):
-        for o in opts[:nthr]:
-            o.LocalBundleAdjustmentBatch(graphs)
-        for c in ctxs[:nthr]:
-            c.synchronize()
-        its = [0] * nthr
-
-        def run(t):
-            for _ in range(brep):
-                its[t] += sum(x.iterations for x in opts[t].LocalBundleAdjustmentBatch(graphs))
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        th = [threading.Thread(target=run, args=(t,)) for t in range(nthr)]
-        for x in th:
-            x.start()
-        for x in th:
-            x.join()
-        torch.cuda.synchronize(dev)
-        return job_totals(time.perf_counter() - t0, sum(its), world, dist if world > 1 else None, dev)
+        return _threaded_batches(ctxs[:nthr], opts[:nthr], graphs, brep, world, dist, dev)
     bel1, biters1 = timed(1)
     bel, biters = timed(T) if T > 1 else (bel1, biters1)
     for c in ctxs[1:]:
@@ -523,6 +506,35 @@ def bench_lba(ctx, rank, world, dist, dev, args):
     return res
 
 
+def _threaded_batches(ctxs, opts, graphs, brep, world, dist, dev):
+    """Each of len(opts) host threads runs `brep` lockstep batches of `graphs`
+    (osg_local_bundle_adjustment_batch) on its own context / HIP stream after one untimed batch;
+    returns (max-over-ranks seconds, LM iterations of all ranks)."""
+    import threading
+    import torch
+    nthr = len(opts)
+    for o in opts:
+        o.LocalBundleAdjustmentBatch(graphs)
+    for c in ctxs:
+        c.synchronize()
+    its = [0] * nthr
+
+    def run(t):
+        for _ in range(brep):
+            its[t] += sum(x.iterations for x in opts[t].LocalBundleAdjustmentBatch(graphs))
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    th = [threading.Thread(target=run, args=(t,)) for t in range(nthr)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    torch.cuda.synchronize(dev)
+    return job_totals(time.perf_counter() - t0, sum(its), world, dist if world > 1 else None, dev)
+
+
 def _lba_worker(graphs):
     """cpu_baseline worker for BA: one graph per call, round-robin over `graphs`; outputs per thread."""
     def worker(tid):
@@ -543,7 +555,11 @@ def bench_gba(ctx, rank, world, dist, dev, args):
     """SURVEY.md §8(f) rank 4: Optimizer::BundleAdjustment (global BA) on a synthetic whole map of 150
     KeyFrames x 20k points (only the init KeyFrame fixed, no Huber kernel: LoopClosing's
     GlobalBundleAdjustemnt(map, 10, &mbStopGBA, nLoopKF, false)); LM iterations per wall second of
-    the whole call (structure build, upload, LM, download).  Replicas: one map per rank."""
+    the whole call (structure build, upload, LM, download).
+    `value`: independent maps per GPU as the CPU baseline runs them (one map per host thread there):
+    B maps per lockstep batch (osg_local_bundle_adjustment_batch, the engine osg_bundle_adjustment
+    runs with B = 1), T host threads with their own contexts.  `single_map`: one map per call, the
+    drop-in's latency.  Replicas: the maps of each rank are its own."""
     import torch
     from orb_slam3_comments_ghr_amd import optimizer as op
     rng = np.random.default_rng(0x0B5EED30 + rank)
@@ -563,15 +579,30 @@ def bench_gba(ctx, rank, world, dist, dev, args):
     el = time.perf_counter() - t0
     el, iters = job_totals(el, iters, world, dist if world > 1 else None, dev)
     n_free = int(len(G.pose) - G.pose_fixed.sum())
-    res = {"metric": "GlobalBA iters/s", "value": round(iters / el, 1), "unit": "LM iterations/s",
-           "ms_per_gba": round(el / reps * 1e3, 3), "iterations_per_gba": r.iterations, "trials_per_gba": r.trials,
+    single = {"value": round(iters / el, 1), "unit": "LM iterations/s", "ms_per_gba": round(el / reps * 1e3, 3),
+              "iterations_per_gba": r.iterations, "trials_per_gba": r.trials,
+              "note": "one map per call (osg_bundle_adjustment: the drop-in's latency)"}
+    B, T, brep = max(1, args.gba_batch), max(1, args.gba_threads), max(1, args.gba_batch_reps)
+    pool = [G] + [op.synth_gba_graph(rng, n_kf=150, n_points=20000) for _ in range(3)]
+    graphs = [pool[i % len(pool)] for i in range(B)]
+    ctxs = [ctx] + [type(ctx)(ctx.device) for _ in range(T - 1)]
+    opts = [opt] + [op.Optimizer(c) for c in ctxs[1:]]
+    bel, biters = _threaded_batches(ctxs, opts, graphs, brep, world, dist, dev)
+    for c in ctxs[1:]:
+        c.close()
+    res = {"metric": "GlobalBA iters/s", "value": round(biters / bel, 1), "unit": "LM iterations/s",
            "workload": f"global BA: {len(G.pose)} KF x {len(G.point)} points x {len(G.e_point)} edges, "
-                       f"reduced system {6 * n_free} (dense), optimize({G.iterations}), no Huber",
-           "n_gpus": world, "dtype": "f64", "scaling": "weak", "parallelism": f"replicas x{world} (one map per GPU)"}
+                       f"reduced system {6 * n_free} (dense), optimize({G.iterations}), no Huber; {B} independent "
+                       f"maps per lockstep batch ({len(pool)} distinct), {T} host threads per GPU each driving "
+                       f"{brep} batches on its own context / HIP stream",
+           "maps_per_batch": B, "host_threads": T, "maps_per_s": round(B * T * brep * world / bel, 1),
+           "single_map": single,
+           "n_gpus": world, "dtype": "f64", "scaling": "weak", "parallelism": f"replicas x{world} (independent maps per GPU)"}
     if rank == 0 and world == 1 and not args.no_cpu:
-        it_cpu = _oracle()[1].lba(_oracle()[0], G).iterations
-        _attach_cpu(res, _lba_worker([G]), it_cpu, "LM iterations/s", max(3.0, args.cpu_seconds * 0.5),
-                    "global BA 150 KF x 20k points (oracle, dense LDL^T)", wall_key="")
+        it_cpu = float(np.mean([_oracle()[1].lba(_oracle()[0], g).iterations for g in pool]))
+        _attach_cpu(res, _lba_worker(pool), it_cpu, "LM iterations/s", max(3.0, args.cpu_seconds * 0.5),
+                    "global BA 150 KF x 20k points (oracle, dense LDL^T), one map per thread", wall_key="")
+        single["speedup_vs_cpu_1thread"] = round(single["value"] / res["cpu_baseline"]["value_1thread"], 1)
     return res
 
 
