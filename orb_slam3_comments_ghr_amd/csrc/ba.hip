@@ -105,7 +105,11 @@ struct LbaDev {
     const int32_t *pair_rank;            // per contribution: rank of its first block in pose i's list
     int n_rs;                            // row segments: RS consecutive blocks of one hessian pose
     const int32_t *rs_pose, *rs_rank0;   // per row segment: pose, first rank
+    const int32_t *rs_info;              // k_schur_rows, 8 per workgroup (launch order): row segment,
+                                         // pose, first rank, hp_b_start[pose], blocks, chunk range
+    const int32_t *hp_b_lm;              // per hp_b entry: the block's landmark
     const int32_t *rs_chunk_start, *rs_chunk;  // chunks per row segment
+    const int32_t *rs_cdesc;             // per rs_chunk entry: {chunk, first contribution, count, 0}
     const int32_t *hp_rs_start;          // row segments per hessian pose
     double *chunk_part;                  // 36 per chunk
     double *bs_part;                     // 6 per row segment: sum of Hpl Dinv b_l
@@ -456,29 +460,100 @@ template <bool VALU>
 __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT);
-    const int rs = bx;
-    if (rs >= D.n_rs) return;
+    if (bx >= D.n_rs) return;
+    typedef int i4 __attribute__((ext_vector_type(4)));
+    // the segment's indices in one 32-byte load (one dependent level instead of four)
+    const i4 inf0 = ((const GLOBAL i4 *)gbl(D.rs_info))[2 * bx];
+    const i4 inf1 = ((const GLOBAL i4 *)gbl(D.rs_info))[2 * bx + 1];
+    const int rs = __builtin_amdgcn_readfirstlane(inf0.x);
+    const int rb = __builtin_amdgcn_readfirstlane(inf0.z), hb0 = __builtin_amdgcn_readfirstlane(inf0.w);
+    const int nr = __builtin_amdgcn_readfirstlane(inf1.x);
     __shared__ double s_bd[RS * 18 + 2];  // + a zero: the MFMA's K-padding lanes read it
     __shared__ double s_cf[RT / 64][6];
     if (threadIdx.x == 0) s_bd[RS * 18] = 0.0;
-    const int i = D.rs_pose[rs], rb = D.rs_rank0[rs];
-    const int hb0 = D.hp_b_start[i];
-    const int nr = min(RS, D.hp_b_start[i + 1] - hb0 - rb);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    double cf[6] = {0, 0, 0, 0, 0, 0};
-    for (int r = threadIdx.x; r < nr; r += RT) {
-        const int a = gbl(D.hp_b)[hb0 + rb + r];
-        const int l = gbl(D.blk_lm)[a];
-        double Di[9], db[3], B[18];
-        for (int k = 0; k < 9; k++) Di[k] = gbl(D.Dinv)[9 * (size_t)l + k];
-        for (int k = 0; k < 3; k++) db[k] = gbl(D.db)[3 * (size_t)l + k];
-        for (int k = 0; k < 18; k++) B[k] = gbl(D.Hpl)[18 * (size_t)a + k];
-        double *BD = s_bd + 18 * r;
-        for (int rr = 0; rr < 6; rr++) {
-            for (int c = 0; c < 3; c++)
-                BD[3 * rr + c] = B[3 * rr] * Di[c] + B[3 * rr + 1] * Di[3 + c] + B[3 * rr + 2] * Di[6 + c];
-            cf[rr] += B[3 * rr] * db[0] + B[3 * rr + 1] * db[1] + B[3 * rr + 2] * db[2];
+    // FP64 MFMA (v_mfma_f64_4x4x4f64: four independent 4x4x4 blocks per wave instruction).  A
+    // chunk's S_ij = sum_p BD_p Hpl_p^T is the GEMM (6 x 3P)(3P x 6); one instruction takes one
+    // contribution (K = its 3 landmark dimensions, padded to 4) for the whole 6x6 product: block
+    // beta = (rb, cb) covers rows 4 rb .. 4 rb + 3 and columns 4 cb .. 4 cb + 3 (rows / columns 6, 7
+    // padded).  Operand layout on gfx950 (tools/micro/mfma_f64.hip, profiles/r02_mfma_f64.txt):
+    //   A(beta, row i, k) in lane 16 k + 4 beta + i,  B(beta, k, col j) in lane 16 k + 4 beta + j,
+    //   D(beta, row i, col j) in lane 16 i + 4 beta + j.
+    // Contributions accumulate in chunk order (= landmark order) through two alternating
+    // accumulators, summed once at the end: deterministic.
+    const int kk = lane >> 4, beta = (lane >> 2) & 3, ri = lane & 3;
+    const int arow = 4 * (beta >> 1) + ri, bcol = 4 * (beta & 1) + ri;
+    // Padding without arithmetic: the K-padding lanes (k = 3) of A read the zero after s_bd, so the
+    // fourth product of every output is exactly 0; the padded rows (A) and columns (B) 6, 7 read
+    // row / column 5 again and only reach the padded outputs, which are never stored.  B's k = 3
+    // lanes read a real (finite) element, multiplied by that zero.
+    const int a_m = kk < 3 ? 18 : 0;  // A's address: a_m * rank + aoff
+    const int aoff = kk < 3 ? 3 * min(arow, 5) + kk : RS * 18;
+    const int boff = 3 * min(bcol, 5) + min(kk, 2);
+    const int orow = 4 * (beta >> 1) + kk, ocol = 4 * (beta & 1) + ri;  // D: i = lane >> 4
+    const GLOBAL double *__restrict__ Hv = gbl(D.Hpl);
+    // Hpl_j blocks are staged per wave through LDS, 16 contributions at a time: 144 16-byte granules
+    // read by 64 lanes with 3 dwordx4 loads (one gather instruction per 5 contributions instead of
+    // one per contribution), the next group's loads in flight while this group's MFMAs run
+    constexpr int GC = 16;
+    __shared__ __attribute__((aligned(16))) double s_hb[RT / 64][GC * 18];
+    double *hb = s_hb[wv];
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    const int t1 = __builtin_amdgcn_readfirstlane(inf1.z);
+    int t = __builtin_amdgcn_readfirstlane(inf1.y) + wv;
+    const GLOBAL i4 *__restrict__ cd = (const GLOBAL i4 *)gbl(D.rs_cdesc);
+    // chunk descriptor {chunk, first contribution, count (<= SCH = 64)} of rs_chunk entry tt
+    auto desc = [&](int tt) -> i4 {
+        i4 d = tt < t1 ? cd[tt] : i4{0, 0, 0, 0};
+        // wave-uniform: scalar registers
+        return i4{__builtin_amdgcn_readfirstlane(d.x), __builtin_amdgcn_readfirstlane(d.y),
+                  __builtin_amdgcn_readfirstlane(d.z), 0};
+    };
+    // lane q: rank (in the segment) of contribution q's first block, and its second block
+    auto contrib = [&](const i4 &d, int &mr, int &mb) {
+        mr = lane < d.z ? gbl(D.pair_rank)[d.y + lane] - rb : 0;
+        mb = lane < d.z ? gbl(D.pair_ab)[2 * (d.y + lane) + 1] : 0;
+    };
+    // granules of group u0 (contributions u0 .. u0 + cnt - 1) into registers
+    auto load_group = [&](int u0, int cnt, int mb, u4 (&R)[3]) {
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            const int idx = lane + 64 * r;
+            const int c = idx / 9, gq = idx - 9 * c;
+            const int bj = __shfl(mb, (u0 + c) & 63);
+            if (idx < GC * 9 && c < cnt) R[r] = *(const GLOBAL u4 *)(Hv + 18 * (size_t)bj + 2 * gq);
         }
+    };
+    i4 dc = {0, 0, 0, 0}, dn = {0, 0, 0, 0};
+    int my_rank = 0, my_b = 0, n_rank = 0, n_b = 0;
+    u4 R[3];
+    if (!VALU) {
+        dc = desc(t);
+        dn = desc(t + RT / 64);
+        contrib(dc, my_rank, my_b);
+        contrib(dn, n_rank, n_b);
+    }
+    double cf[6] = {0, 0, 0, 0, 0, 0};
+    // two threads per block (rows 3h .. 3h + 2 each): half the staging registers per thread
+    {
+        const int h = threadIdx.x & 1;  // RT is even: a thread keeps its half
+        double c3[3] = {0, 0, 0};
+        for (int r2 = threadIdx.x; r2 < 2 * nr; r2 += RT) {
+            const int r = r2 >> 1;
+            const int a = gbl(D.hp_b)[hb0 + rb + r];
+            const int l = gbl(D.hp_b_lm)[hb0 + rb + r];
+            double Di[9], db[3], B[9];
+            for (int k = 0; k < 9; k++) Di[k] = gbl(D.Dinv)[9 * (size_t)l + k];
+            for (int k = 0; k < 3; k++) db[k] = gbl(D.db)[3 * (size_t)l + k];
+            for (int k = 0; k < 9; k++) B[k] = gbl(D.Hpl)[18 * (size_t)a + 9 * h + k];
+            double *BD = s_bd + 18 * r + 9 * h;
+            for (int rr = 0; rr < 3; rr++) {
+                for (int c = 0; c < 3; c++)
+                    BD[3 * rr + c] = B[3 * rr] * Di[c] + B[3 * rr + 1] * Di[3 + c] + B[3 * rr + 2] * Di[6 + c];
+                c3[rr] += B[3 * rr] * db[0] + B[3 * rr + 1] * db[1] + B[3 * rr + 2] * db[2];
+            }
+        }
+        for (int k = 0; k < 6; k++) cf[k] = (k / 3 == h) ? c3[k % 3] : 0.0;
     }
     for (int k = 0; k < 6; k++) cf[k] = wave_sum(cf[k]);
     if (lane == 0)
@@ -530,59 +605,14 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__
         }
         return;
     }
-    // FP64 MFMA (v_mfma_f64_4x4x4f64: four independent 4x4x4 blocks per wave instruction).  A
-    // chunk's S_ij = sum_p BD_p Hpl_p^T is the GEMM (6 x 3P)(3P x 6); one instruction takes one
-    // contribution (K = its 3 landmark dimensions, padded to 4) for the whole 6x6 product: block
-    // beta = (rb, cb) covers rows 4 rb .. 4 rb + 3 and columns 4 cb .. 4 cb + 3 (rows / columns 6, 7
-    // padded).  Operand layout on gfx950 (tools/micro/mfma_f64.hip, profiles/r02_mfma_f64.txt):
-    //   A(beta, row i, k) in lane 16 k + 4 beta + i,  B(beta, k, col j) in lane 16 k + 4 beta + j,
-    //   D(beta, row i, col j) in lane 16 i + 4 beta + j.
-    // Contributions accumulate in chunk order (= landmark order) through two alternating
-    // accumulators, summed once at the end: deterministic.
-    const int kk = lane >> 4, beta = (lane >> 2) & 3, ri = lane & 3;
-    const int arow = 4 * (beta >> 1) + ri, bcol = 4 * (beta & 1) + ri;
-    // Padding without arithmetic: the K-padding lanes (k = 3) of A read the zero after s_bd, so the
-    // fourth product of every output is exactly 0; the padded rows (A) and columns (B) 6, 7 read
-    // row / column 5 again and only reach the padded outputs, which are never stored.  B's k = 3
-    // lanes read a real (finite) element, multiplied by that zero.
-    const int a_m = kk < 3 ? 18 : 0;  // A's address: a_m * rank + aoff
-    const int aoff = kk < 3 ? 3 * min(arow, 5) + kk : RS * 18;
-    const int boff = 3 * min(bcol, 5) + min(kk, 2);
-    const int orow = 4 * (beta >> 1) + kk, ocol = 4 * (beta & 1) + ri;  // D: i = lane >> 4
-    const GLOBAL double *__restrict__ Hv = gbl(D.Hpl);
-    // Hpl_j blocks are staged per wave through LDS, 16 contributions at a time: 144 16-byte granules
-    // read by 64 lanes with 3 dwordx4 loads (one gather instruction per 5 contributions instead of
-    // one per contribution), the next group's loads in flight while this group's MFMAs run
-    constexpr int GC = 16;
-    __shared__ __attribute__((aligned(16))) double s_hb[RT / 64][GC * 18];
-    double *hb = s_hb[wv];
-    const int t1 = D.rs_chunk_start[rs + 1];
-    int t = D.rs_chunk_start[rs] + wv;
-    int ch = 0, q0 = 0, nq = 0, my_rank = 0, my_b = 0;
-    auto fetch = [&](int tt, int &c, int &qs, int &n, int &mr, int &mb) {
-        c = tt < t1 ? gbl(D.rs_chunk)[tt] : 0;
-        qs = tt < t1 ? gbl(D.chunk_start)[c] : 0;
-        n = tt < t1 ? gbl(D.chunk_start)[c + 1] - qs : 0;  // <= SCH = 64
-        mr = lane < n ? gbl(D.pair_rank)[qs + lane] - rb : 0;
-        mb = lane < n ? gbl(D.pair_ab)[2 * (qs + lane) + 1] : 0;
-    };
-    // granules of group u0 (contributions u0 .. u0 + cnt - 1) into registers
-    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-    auto load_group = [&](int u0, int cnt, int mb, u4 (&R)[3]) {
-#pragma unroll
-        for (int r = 0; r < 3; r++) {
-            const int idx = lane + 64 * r;
-            const int c = idx / 9, gq = idx - 9 * c;
-            const int bj = __shfl(mb, (u0 + c) & 63);
-            if (idx < GC * 9 && c < cnt) R[r] = *(const GLOBAL u4 *)(Hv + 18 * (size_t)bj + 2 * gq);
-        }
-    };
-    fetch(t, ch, q0, nq, my_rank, my_b);
-    u4 R[3];
-    load_group(0, nq, my_b, R);
+    // The descriptors and contributions (rank, block) of the wave's first two chunks were issued
+    // before the BD staging above, so their latency overlaps it.  In the loop the descriptor two
+    // chunks ahead is issued at the top and its contributions at the bottom: no dependent load chain
+    // is waited on between chunks.
+    load_group(0, dc.z, my_b, R);
     for (; t < t1; t += RT / 64) {
-        int nch, nq0, nnq, nrank, nb;
-        fetch(t + RT / 64, nch, nq0, nnq, nrank, nb);
+        const i4 d2 = desc(t + 2 * (RT / 64));
+        const int nq = dc.z;
         double acc0 = 0.0, acc1 = 0.0;
         for (int u = 0; u < nq; u += GC) {
             const int cnt = min(GC, nq - u);
@@ -594,7 +624,7 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__
             __builtin_amdgcn_wave_barrier();
             // next group: the rest of this chunk, else the first group of the next chunk
             if (u + GC < nq) load_group(u + GC, nq - u - GC, my_b, R);
-            else load_group(0, nnq, nb, R);
+            else load_group(0, dn.z, n_b, R);
 #pragma unroll
             for (int v = 0; v < GC; v += 2) {
                 if (v < cnt) {
@@ -609,12 +639,12 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__
             }
             __builtin_amdgcn_wave_barrier();
         }
-        if (orow < 6 && ocol < 6) D.chunk_part[36 * (size_t)ch + 6 * orow + ocol] = acc0 + acc1;
-        ch = nch;
-        q0 = nq0;
-        nq = nnq;
-        my_rank = nrank;
-        my_b = nb;
+        if (orow < 6 && ocol < 6) D.chunk_part[36 * (size_t)dc.x + 6 * orow + ocol] = acc0 + acc1;
+        dc = dn;
+        my_rank = n_rank;
+        my_b = n_b;
+        dn = d2;
+        contrib(dn, n_rank, n_b);
     }
 }
 
@@ -1383,7 +1413,7 @@ struct LbaHost {
     bool trivial = false;  // nothing to optimise: the estimates are returned unchanged
     std::vector<int32_t> pose_h, hp_pose, point_h, hl_point, lm_e_start, lm_e, lg_start, lm_b_start, blk_pose, edge_blk, blk_lm,
         hp_e_start, hp_e, hp_b_start, hp_b, pair_start, pair_ab, chunk_start, pair_chunk,
-        pair_rank, rs_pose, rs_rank0, rs_chunk_start, rs_chunk, hp_rs_start;
+        pair_rank, rs_pose, rs_rank0, rs_chunk_start, rs_chunk, hp_rs_start, rs_order, rs_cdesc, rs_info, hp_b_lm;
     int n_rs = 0;
     double t_struct = 0;
     // LM state (ref:Thirdparty/g2o/g2o/core/optimization_algorithm_levenberg.cpp:61-194 and
@@ -1411,6 +1441,10 @@ struct LbaHost {
         blk_pose.clear();
         chunk_start.clear();
         rs_pose.clear();
+        rs_order.clear();
+        rs_cdesc.clear();
+        rs_info.clear();
+        hp_b_lm.clear();
         rs_rank0.clear();
         rs_chunk.clear();
         t_struct = 0;
@@ -1613,6 +1647,22 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
         }
     }
     H.n_rs = H.hp_rs_start[nhp];
+    // launch order of the row segments: by the landmark at the middle of the segment (pose order on
+    // ties) when OSG_SCHUR_ORDER=1, so the segments in flight together read the Hpl blocks of one
+    // landmark range; identity otherwise.  Only which workgroup takes a segment changes: every sum
+    // keeps its order, the results are bit-identical.
+    H.rs_order.resize(H.n_rs);
+    for (int r = 0; r < H.n_rs; r++) H.rs_order[r] = r;
+    static const bool schur_order = getenv("OSG_SCHUR_ORDER") && atoi(getenv("OSG_SCHUR_ORDER")) == 1;
+    if (schur_order) {
+        std::vector<int32_t> key(H.n_rs);
+        for (int r = 0; r < H.n_rs; r++) {
+            const int i = H.rs_pose[r], hb0 = H.hp_b_start[i], nb = H.hp_b_start[i + 1] - hb0;
+            const int mid = std::min(nb - 1, H.rs_rank0[r] + std::min(RS, nb - H.rs_rank0[r]) / 2);
+            key[r] = nb > 0 ? H.blk_lm[H.hp_b[hb0 + mid]] : 0;
+        }
+        std::stable_sort(H.rs_order.begin(), H.rs_order.end(), [&](int a, int b) { return key[a] < key[b]; });
+    }
     const size_t ncontrib = (size_t)H.pair_start[npairs];
     H.pair_rank.assign(std::max<size_t>(ncontrib, 1), 0);
     for (size_t q = 0; q < ncontrib; q++) H.pair_rank[q] = blk_rank[H.pair_ab[2 * q]];
@@ -1643,6 +1693,27 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
     {
         std::vector<int32_t> fill(H.rs_chunk_start.begin(), H.rs_chunk_start.end() - 1);
         for (int c = 0; c < H.nchunks; c++) H.rs_chunk[fill[chunk_rs[c]]++] = c;
+    }
+    H.rs_info.assign(8 * (size_t)std::max(H.n_rs, 1), 0);
+    for (int w = 0; w < H.n_rs; w++) {
+        const int r = H.rs_order[w], i = H.rs_pose[r], hb0 = H.hp_b_start[i];
+        int32_t *f = &H.rs_info[8 * (size_t)w];
+        f[0] = r;
+        f[1] = i;
+        f[2] = H.rs_rank0[r];
+        f[3] = hb0;
+        f[4] = std::min(RS, H.hp_b_start[i + 1] - hb0 - H.rs_rank0[r]);
+        f[5] = H.rs_chunk_start[r];
+        f[6] = H.rs_chunk_start[r + 1];
+    }
+    H.hp_b_lm.assign(std::max<size_t>(H.hp_b.size(), 1), 0);
+    for (size_t q = 0; q < H.hp_b.size(); q++) H.hp_b_lm[q] = H.blk_lm[H.hp_b[q]];
+    H.rs_cdesc.assign(4 * (size_t)std::max(H.nchunks, 1), 0);
+    for (int t = 0; t < H.nchunks; t++) {
+        const int c = H.rs_chunk[t];
+        H.rs_cdesc[4 * (size_t)t] = c;
+        H.rs_cdesc[4 * (size_t)t + 1] = H.chunk_start[c];
+        H.rs_cdesc[4 * (size_t)t + 2] = H.chunk_start[c + 1] - H.chunk_start[c];
     }
     H.ge = (ne + EB - 1) / EB;
     H.gl = (nhl + EB - 1) / EB;
@@ -1796,7 +1867,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     struct InOff {
         size_t fixed, epose, epoint, ecam, ekind, eobs, eisig, cams, poseh, hppose, pointh, hlpoint, lmes, lme, lgs, lmbs,
             blkpose, eblk, hpes, hpe, hpbs, hpb, pairs, pairab, chs, blklm, pch, pose0, point0, erob,
-            prank, rspose, rsrank0, rscs, rsc, hprs, bfirst, blast;
+            prank, rspose, rsrank0, rscs, rsc, hprs, bfirst, blast, rsinfo, hpblm, rscd;
     };
     std::vector<InOff> io(NA);
     for (int a = 0; a < NA; a++) {
@@ -1837,8 +1908,11 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         o.blast = pk.add(h.blk_last.data(), 4 * std::max<size_t>(h.blk_last.size(), 1));
         o.rspose = pk.add(h.rs_pose.data(), 4 * h.rs_pose.size());
         o.rsrank0 = pk.add(h.rs_rank0.data(), 4 * h.rs_rank0.size());
+        o.rsinfo = pk.add(h.rs_info.data(), 4 * h.rs_info.size());
+        o.hpblm = pk.add(h.hp_b_lm.data(), 4 * h.hp_b_lm.size());
         o.rscs = pk.add(h.rs_chunk_start.data(), 4 * h.rs_chunk_start.size());
         o.rsc = pk.add(h.rs_chunk.data(), 4 * h.rs_chunk.size());
+        o.rscd = pk.add(h.rs_cdesc.data(), 4 * h.rs_cdesc.size());
         o.hprs = pk.add(h.hp_rs_start.data(), 4 * h.hp_rs_start.size());
         o.pose0 = pk.add(G->pose, 56 * (size_t)np);
         o.point0 = pk.add(G->point, 24 * (size_t)npt);
@@ -1933,8 +2007,11 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         D.npart = h.npart;
         D.n_rs = h.n_rs;
         D.rs_pose = osg_dptr<int32_t>(din, o.rspose);
+        D.rs_info = osg_dptr<int32_t>(din, o.rsinfo);
+        D.hp_b_lm = osg_dptr<int32_t>(din, o.hpblm);
         D.rs_rank0 = osg_dptr<int32_t>(din, o.rsrank0);
         D.rs_chunk_start = osg_dptr<int32_t>(din, o.rscs);
+        D.rs_cdesc = osg_dptr<int32_t>(din, o.rscd);
         D.rs_chunk = osg_dptr<int32_t>(din, o.rsc);
         D.hp_rs_start = osg_dptr<int32_t>(din, o.hprs);
         D.ge = h.ge;

@@ -1,12 +1,14 @@
 #!/bin/bash
-# k_schur_rows A/B: the FP64 MFMA form against OSG_SCHUR_VALU=1 on the 64-window C4 batch (one gpurun call).
+# k_schur_rows A/B (one gpurun call): 64 C4 windows, per-kernel device times of one batch and the
+# 1- / 8-thread LM iteration rates, MFMA form then the VALU form (OSG_SCHUR_VALU=1); then the LBA
+# GPU parity tests.
 set -o pipefail
-export TMPDIR=/tmp
-R=$GRAFT_REPO_ROOT
-OUT=$R/gpurun_out/${1:-r03schurab}
-mkdir -p $OUT
-cd $R
-for v in 0 1 0 1; do
-  OSG_SCHUR_VALU=$v TS=1 BS=64 KT=1 timeout -k 10 200 python3 tools/lba_batch_bench.py 2>&1 | grep -v amdgpu.ids | sed "s/^/VALU=$v: /" >> $OUT/ab.txt || exit 1
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/${1:-schur_ab}
+mkdir -p $O
+for v in 0 1; do
+  echo "# OSG_SCHUR_VALU=$v" >> $O/ab.txt
+  OSG_SCHUR_VALU=$v KT=1 TS=1,8 BS=64 timeout -k 10 200 python -u tools/lba_batch_bench.py >> $O/ab.txt 2>&1 || exit 1
 done
+timeout -k 10 600 python -u -m pytest tests/test_ba_gpu.py tests/test_golden_ba.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_ba.log 2>&1
 echo "exit=$?"
