@@ -85,7 +85,7 @@ def parse():
     ap.add_argument("--lba-threads", type=int, default=8,
                     help="host threads per GPU driving LocalBA batches, each with its own context and HIP stream "
                          "(8 measured 9-18 %% above 4: more batches in flight cover each thread's host phases)")
-    ap.add_argument("--gba-batch", type=int, default=8, help="150-KF maps per GPU per lockstep global-BA batch")
+    ap.add_argument("--gba-batch", type=int, default=16, help="150-KF maps per GPU per lockstep global-BA batch")
     ap.add_argument("--gba-threads", type=int, default=8, help="host threads per GPU driving global-BA batches")
     ap.add_argument("--gba-batch-reps", type=int, default=3)
     ap.add_argument("--no-frames", action="store_true", help="skip the frame-batched C3 / C5 workloads")
