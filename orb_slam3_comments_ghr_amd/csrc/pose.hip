@@ -297,6 +297,7 @@ struct PoseShared {
     SE3 trl;
     double sys[NT];  // the last buildSystem sums: H upper (21) | b (6) | robust chi2
     double chi;      // the last trial's chi2
+    int ok;          // the last trial's factorisation succeeded (wave 0's solve, broadcast)
     int n_act[8], n_bad[8];
 };
 // one wave's copy of the wave-uniform LM state: every wave runs the same LM control on the same
@@ -511,29 +512,46 @@ __global__ __launch_bounds__(NW *PW) void k_pose_opt(const PoseProbDev *__restri
                     total_trials++;
                     W.backup = pose;  // push
                     PROF_T(t_s);
-                    double A[6][6], bvec[6];
-                    {
-                        int q = 0;
+                    // the 6x6 solve and the exp-map update run on wave 0 alone and are broadcast
+                    // through LDS: with 8 waves two share each SIMD, and the redundant copies of these
+                    // issue-bound chains would halve its rate.  Waves 1.. take wave 0's x and pose
+                    // (their copies are read-only to wave 0 until the next chi_pass barrier).
+                    bool okw = true;
+                    if (wave == 0) {
+                        double A[6][6], bvec[6];
+                        {
+                            int q = 0;
 #pragma unroll
-                        for (int i = 0; i < 6; i++)
+                            for (int i = 0; i < 6; i++)
 #pragma unroll
-                            for (int j = i; j < 6; j++) {
-                                A[i][j] = sys[q] + (i == j ? lambda : 0.0);
-                                A[j][i] = A[i][j];
-                                q++;
-                            }
+                                for (int j = i; j < 6; j++) {
+                                    A[i][j] = sys[q] + (i == j ? lambda : 0.0);
+                                    A[j][i] = A[i][j];
+                                    q++;
+                                }
 #pragma unroll
-                        for (int i = 0; i < 6; i++) bvec[i] = sys[21 + i];
+                            for (int i = 0; i < 6; i++) bvec[i] = sys[21 + i];
+                        }
+                        double x[6];
+                        okw = ldlt6(A, bvec, x);
+                        if (okw)
+#pragma unroll
+                            for (int i = 0; i < 6; i++) xs[i] = x[i];
+                        PROF_ADD(1, t_s);
+                        PROF_T(t_x);
+                        se3_oplus<true>(pose, xs);  // exp(update) * estimate (every lane holds the same update)
+                        PROF_ADD(2, t_x);
+                        if (lane == 0) S.ok = okw ? 1 : 0;
                     }
-                    double x[6];
-                    const bool ok2 = ldlt6(A, bvec, x);
-                    if (ok2)
+                    if (NW > 1) {
+                        __syncthreads();
+                        if (wave != 0) {
 #pragma unroll
-                        for (int i = 0; i < 6; i++) xs[i] = x[i];
-                    PROF_ADD(1, t_s);
-                    PROF_T(t_x);
-                    se3_oplus<true>(pose, xs);  // exp(update) * estimate (every lane holds the same update)
-                    PROF_ADD(2, t_x);
+                            for (int i = 0; i < 6; i++) xs[i] = WV[0].xs[i];
+                            pose = WV[0].pose;
+                        }
+                    }
+                    const bool ok2 = wave == 0 ? okw : S.ok != 0;
                     PROF_T(t_c);
                     double tempChi = chi_pass(pose);
                     PROF_ADD(3, t_c);
@@ -640,9 +658,10 @@ int osg_pose_optimization_batch(osg_ctx *ctx, const osg_pose_problem *p, int32_t
         // waves per frame: up to one per 1.5 chunks of a lone frame's edges (latency; 8 waves share
         // 4 SIMDs and measured no faster than 4), one when the batch fills the chip's wave slots
         while (nw < 4 && 3 * nw <= 2 * chunks && (size_t)nb * 2 * nw <= 2048) nw *= 2;
-        // a lone frame of >= 9 chunks (576 edges): 8 waves measured faster (the 600-edge KB8 frame 811 -> 758
-        // us; the 318-edge frame is slower with 8: 468 against 432 us)
-        if (nw == 4 && chunks >= 9 && (size_t)nb * 2 * 8 <= 2048) nw = 8;
+        // a lone frame of >= 5 chunks (257+ edges): 8 waves, since the solve and the exp-map update run on
+        // wave 0 alone (before, 8 waves ran them twice per SIMD and were slower below 9 chunks).  Measured
+        // (tools/latency_probe.py): the 318-edge frame 439 -> 418 us, the 600-edge KB8 frame 816 -> 721 us
+        if (nw == 4 && chunks >= 5 && (size_t)nb * 2 * 8 <= 2048) nw = 8;
         while (nw < 8 && chunks > 64 * nw) nw *= 2;
     }
     OSG_REQUIRE(ctx, nw == 1 || nw == 2 || nw == 4 || nw == 8, "OSG_POSE_NW must be 1, 2, 4 or 8");
