@@ -381,6 +381,7 @@ __global__ __launch_bounds__(NW *PW) void k_pose_opt(const PoseProbDev *__restri
         double acc = 0.0;
         for (int s = 0; s < nsc; s++) {
             reload_lds();
+            PROF_T(t_pc);
             double v = 0.0;
             if (active(s)) {
                 const PEdge E = load_edge(edge_of(s), kind, xw, obs, isig2);
@@ -396,9 +397,12 @@ __global__ __launch_bounds__(NW *PW) void k_pose_opt(const PoseProbDev *__restri
                 }
             }
             tile[lane] = v;
+            PROF_ADD(6, t_pc);
             __syncthreads();
+            PROF_T(t_ps);
             if (threadIdx.x == 0)
                 for (int w = 0; w < NW && chunk_cnt(s, w) > 0; w++) acc = seq_sum(acc, s_t + w * NT * ROW, chunk_cnt(s, w));
+            PROF_ADD(7, t_ps);
             __syncthreads();
         }
         if (threadIdx.x == 0) S.chi = acc;
