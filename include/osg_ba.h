@@ -120,15 +120,18 @@ int osg_local_bundle_adjustment(struct osg_ctx *ctx, const osg_ba_graph *g, osg_
 /* Optimizer::BundleAdjustment / GlobalBundleAdjustemnt (ref:src/Optimizer.cc:2831-3237): the same
  * engine on the whole map — every KeyFrame (only the map's init KeyFrame fixed), every MapPoint with
  * an edge, optimize(nIterations) with the caller's e_robust / Huber deltas, no outlier pass (edge_bad
- * is filled but the reference does not read it).  The reduced camera system is dense: up to 1024 free
- * KeyFrames. */
+ * is filled but the reference does not read it).  The reduced camera system is dense up to 1024 free
+ * KeyFrames; past that it is factored on its envelope (banded maps), up to 7 723 free KeyFrames
+ * (DESIGN.md §3.11). */
 int osg_bundle_adjustment(struct osg_ctx *ctx, const osg_ba_graph *g, osg_ba_result *r,
                           const volatile uint8_t *stop_flag);
 
 /* Batched form: n_graphs independent windows (e.g. the LocalMapping windows of several maps or
  * sequences) optimised in lockstep, every kernel launched once per LM trial for all of them; each
  * graph follows exactly the single-graph LM (its own lambda, accept / reject, stop rules).
- * Returns the summed LM iterations or a negative OSG_E_* code.  No reference counterpart. */
+ * Whole-map graphs (osg_bundle_adjustment's) are accepted too: bench.py's global_ba line runs 16
+ * independent maps per batch.  Returns the summed LM iterations or a negative OSG_E_* code.  No
+ * reference counterpart. */
 int osg_local_bundle_adjustment_batch(struct osg_ctx *ctx, const osg_ba_graph *graphs, int32_t n_graphs,
                                       osg_ba_result *results, const volatile uint8_t *stop_flag);
 
