@@ -15,7 +15,7 @@ HIPFLAGS += -DOSG_POSE_PROF
 endif
 HDRS = include/osg.h include/osg_ba.h $(CSRC)/osg_internal.h
 
-OBJS = $(OBJDIR)/runtime.o $(OBJDIR)/hamming.o $(OBJDIR)/match.o $(OBJDIR)/pose.o $(OBJDIR)/ba.o $(OBJDIR)/dbow.o $(OBJDIR)/fuse.o $(OBJDIR)/triang.o $(OBJDIR)/desc.o $(OBJDIR)/sim3.o $(OBJDIR)/init.o $(OBJDIR)/stereo.o $(OBJDIR)/orb.o $(OBJDIR)/fast.o $(OBJDIR)/pyramid.o
+OBJS = $(OBJDIR)/runtime.o $(OBJDIR)/hamming.o $(OBJDIR)/hamming_mfma.o $(OBJDIR)/match.o $(OBJDIR)/pose.o $(OBJDIR)/ba.o $(OBJDIR)/dbow.o $(OBJDIR)/fuse.o $(OBJDIR)/triang.o $(OBJDIR)/desc.o $(OBJDIR)/sim3.o $(OBJDIR)/init.o $(OBJDIR)/stereo.o $(OBJDIR)/orb.o $(OBJDIR)/fast.o $(OBJDIR)/pyramid.o
 
 WALL_BENCH = tools/adapter_wall_bench
 
@@ -28,6 +28,8 @@ $(OBJDIR)/runtime.o: $(CSRC)/runtime.hip $(HDRS) | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 $(OBJDIR)/hamming.o: $(CSRC)/hamming.hip $(HDRS) | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(EXACT) -c $< -o $@
+$(OBJDIR)/hamming_mfma.o: $(CSRC)/hamming_mfma.hip $(HDRS) | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 $(OBJDIR)/match.o: $(CSRC)/match.hip $(HDRS) $(CSRC)/match_common.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(EXACT) -c $< -o $@
 $(OBJDIR)/pose.o: $(CSRC)/pose.hip $(HDRS) $(CSRC)/ba_common.h $(CSRC)/exact_math.h $(CSRC)/glibc_math.h $(CSRC)/match_common.h | $(OBJDIR)

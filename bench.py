@@ -44,7 +44,14 @@ PEAK_HBM_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # 4 cycles per SIMD at full occupancy; the 157.3 TF FP32 "vector" figure needs packed v_pk_fma_f32
 # (2 FMAs per lane-instruction), which has no integer counterpart.
 PEAK_VALU_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12
+PEAK_VALU_GUIDE_TOPS = 2 * PEAK_VALU_TOPS   # the guide's 32 lanes / clk (MI355X_MICROARCH.md)
 VALU_OPS_PER_PAIR = 19         # 8 v_xor + 8 v_bcnt(acc) + 1 v_lshl_or + v_med3 + v_min
+# I8 matrix cores: v_mfma_i32_32x32x32_i8 = 32 x 32 x 32 MACs per 32 cycles per SIMD (the cycles of the BF16
+# 32x32x16 form at twice the K, MI355X_MICROARCH.md "Matrix cores"): 256 CU x 4 SIMD x 1024 MAC x 2 ops x 2.4 GHz
+PEAK_I8_TOPS = 256 * 4 * 1024 * 2 * 2.4e9 / 1e12
+I8_OPS_PER_PAIR = 512          # 256 MACs per (query, train row) pair
+MFMA_EPILOGUE_VALU_PER_PAIR = 2  # v_med3_i32 + v_min_i32 on the accumulator's packed key
+MFMA_MAX_ROWS = 8192           # the I8 kernel's 13-bit row field (osg_top2_mfma_max_rows)
 
 
 def job_totals(elapsed, units, world, dist=None, device="cpu"):
@@ -180,13 +187,19 @@ def main():
     torch.cuda.synchronize(dev)
     barrier()
     torch.cuda.synchronize(dev)
+    # HIP events on the launch stream inside the timed region: the kernels' own time over the same K
+    # steps, so the roofline's kernel_us cannot exceed ms_per_step
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for _ in range(args.steps):
         step()
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    k_us_loop = ev0.elapsed_time(ev1) * 1e3 / args.steps
     pairs_per_step = B * nq * nt
     elapsed, total_pairs = job_totals(elapsed, pairs_per_step * args.steps, world, dist if world > 1 else None, dev)
     value = total_pairs / elapsed / 1e6
@@ -210,47 +223,77 @@ def main():
         torch.cuda.synchronize(dev)
         return e0.elapsed_time(e1) * 1e3 / n_ev
 
-    k_us = kernel_us(step, max(20, min(args.steps, 100)))
+    k_us_spin = kernel_us(step, max(20, min(args.steps, 100)))
     k1_us = kernel_us(step_single, max(50, min(args.steps, 500)))
-    achieved_tops = pairs_per_step * VALU_OPS_PER_PAIR / (k_us * 1e-6) / 1e12
+    k_us = k_us_loop
     alg_bytes = B * ((nq + nt) * 32 + nq * 12)
-    ql = int(os.environ.get("OSG_TOP2_BATCH_QL", "2"))
-    kname = (f"k_top2_batch<{ql},{int(os.environ.get('OSG_TOP2_BATCH_SCALAR', '1'))}> "
-             f"grid={(nq + 64 * ql - 1) // (64 * ql)} x {B} x 1024")
-    tr = pmc_traffic(args.traffic, "k_top2_batch")
-    vp = _load_json(args.valu_pmc)
-    vk = next((v for k, v in vp.items() if "k_top2_batch" in k), None)
-    roofline = {
-        "kernel": kname,
-        "bound": "valu",
-        "achieved": round(achieved_tops, 3),
-        "peak": round(PEAK_VALU_TOPS, 1),
-        "unit": "Tops/s (int32 VALU lane-ops)",
-        "peak_source": "256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz; measured ceiling 38.0-38.5 T "
-                       "(tools/micro/valu_rate.hip, profiles/r02_valu_rate.txt)",
-        "frac": round(achieved_tops / PEAK_VALU_TOPS, 4),
+    mfma = os.environ.get("OSG_TOP2_BATCH_MFMA", "1") != "0" and 1 <= nt <= MFMA_MAX_ROWS
+    if mfma:
+        shape = {"0": (16, 1, 256), "1": (8, 2, 256), "2": (8, 1, 128), "3": (8, 2, 128)}[
+            os.environ.get("OSG_TOP2_MFMA_SHAPE", "0")]
+        per_wg = shape[0] * shape[1] * 32
+        kname = f"k_top2_mfma<{shape[0]},{shape[1]},{shape[2]}> grid={(nq + per_wg - 1) // per_wg * B} x {shape[0] * 64}"
+        ksub = "k_top2_mfma"
+        achieved = pairs_per_step * I8_OPS_PER_PAIR / (k_us * 1e-6) / 1e12
+        epi = pairs_per_step * MFMA_EPILOGUE_VALU_PER_PAIR / (k_us * 1e-6) / 1e12
+        roofline = {
+            "kernel": kname, "bound": "mfma", "achieved": round(achieved, 1), "peak": round(PEAK_I8_TOPS, 1),
+            "unit": "TOPS (i8 MFMA, 2 ops per MAC)",
+            "peak_source": "v_mfma_i32_32x32x32_i8: 32x32x32 MACs / 32 cycles / SIMD (MI355X_MICROARCH.md Matrix cores: "
+                           "I8 = the BF16 form's cycles at 2x K) x 1024 SIMDs x 2.4 GHz",
+            "frac": round(achieved / PEAK_I8_TOPS, 4),
+            "algorithmic_ops_per_launch": pairs_per_step * I8_OPS_PER_PAIR,
+            # the VALU side of the same kernel: the 2-op top-2 epilogue per pair against the measured 16-lane
+            # ceiling and the guide's 32-lane figure
+            "valu_epilogue": {"ops_per_pair": MFMA_EPILOGUE_VALU_PER_PAIR, "achieved": round(epi, 2),
+                              "frac_16_lanes": round(epi / PEAK_VALU_TOPS, 4),
+                              "frac_guide_32_lanes": round(epi / PEAK_VALU_GUIDE_TOPS, 4),
+                              "unit": "T lane-ops/s"},
+            # the popcount form's accounting, for comparison with r01-r03 (19 lane-ops per pair)
+            "popcount_equivalent_frac_guide_valu": round(
+                pairs_per_step * VALU_OPS_PER_PAIR / (k_us * 1e-6) / 1e12 / PEAK_VALU_GUIDE_TOPS, 4),
+        }
+    else:
+        ql = int(os.environ.get("OSG_TOP2_BATCH_QL", "2"))
+        kname = (f"k_top2_batch<{ql},{int(os.environ.get('OSG_TOP2_BATCH_SCALAR', '1'))}> "
+                 f"grid={(nq + 64 * ql - 1) // (64 * ql)} x {B} x 1024")
+        ksub = "k_top2_batch"
+        achieved = pairs_per_step * VALU_OPS_PER_PAIR / (k_us * 1e-6) / 1e12
+        vp = _load_json(args.valu_pmc)
+        vk = next((v for k, v in vp.items() if "k_top2_batch" in k), None)
+        roofline = {
+            "kernel": kname, "bound": "valu", "achieved": round(achieved, 3),
+            "peak": round(PEAK_VALU_GUIDE_TOPS, 1), "unit": "Tops/s (int32 VALU lane-ops)",
+            "peak_source": "the guide's 32 lanes/clk (MI355X_MICROARCH.md) x 1024 SIMDs x 2.4 GHz",
+            "frac": round(achieved / PEAK_VALU_GUIDE_TOPS, 4),
+            "algorithmic_ops_per_launch": pairs_per_step * VALU_OPS_PER_PAIR,
+            # the measured ceiling of this instruction mix: one wave64 instruction per 4 cycles per SIMD
+            # (tools/micro/valu_rate.hip, profiles/r02_valu_rate.txt)
+            "peak_measured_16_lanes": round(PEAK_VALU_TOPS, 1),
+            "frac_measured_16_lanes": round(achieved / PEAK_VALU_TOPS, 4),
+            "valu_issue_util_pmc": None if vk is None else round(vk["valu_issue_util_16"], 4),
+            "cycles_per_valu_inst_pmc": None if vk is None else round(vk["cycles_per_valu_inst"], 3),
+            "valu_pmc_source": None if vk is None else os.path.relpath(args.valu_pmc, ROOT),
+        }
+    tr = pmc_traffic(args.traffic, ksub)
+    roofline.update({
         "traffic": None if tr is None else round(tr[0]),
         "traffic_source": None if tr is None else f"{os.path.relpath(args.traffic, ROOT)}: {tr[1]}",
+        # kernel time = HIP events around the K timed steps on the launch stream (inside the wall-clock
+        # region, so <= ms_per_step); the back-to-back launches behind a spin kernel are reported beside it
         "kernel_us": round(k_us, 3),
-        "algorithmic_ops_per_launch": pairs_per_step * VALU_OPS_PER_PAIR,
+        "kernel_us_backtoback_after_spin": round(k_us_spin, 3),
+        "kernel_us_le_ms_per_step": bool(k_us <= elapsed / args.steps * 1e6 + 1e-6),
         "algorithmic_bytes_per_launch": alg_bytes,
         "hbm_frac_if_priced_as_hbm": round(alg_bytes / (k_us * 1e-6) / 1e9 / PEAK_HBM_GBS, 5),
-        # the guide's 32 lanes / clk (MI355X_MICROARCH.md: a wave64 VALU instruction over 2 cycles)
-        "frac_guide_peak": round(achieved_tops / (2 * PEAK_VALU_TOPS), 4),
-        "peak_guide": round(2 * PEAK_VALU_TOPS, 1),
-        # counters on the kernel itself (one --pmc pass): SIMD-cycles per wave64 VALU instruction and
-        # the issue utilisation at 4 cycles (16 lanes / clk) and at 2 (32 lanes / clk)
-        "valu_issue_util_pmc": None if vk is None else round(vk["valu_issue_util_16"], 4),
-        "valu_issue_util_pmc_at_32_lanes": None if vk is None else round(vk["valu_issue_util_32"], 4),
-        "cycles_per_valu_inst_pmc": None if vk is None else round(vk["cycles_per_valu_inst"], 3),
-        "valu_pmc_source": None if vk is None else os.path.relpath(args.valu_pmc, ROOT),
-    }
+    })
     plan = ctx.hamming_top2_plan(nq, nt)
     tr1 = pmc_traffic(args.traffic, plan.split(" ")[0].split("<")[0])
     single = {
         "kernel": plan, "kernel_us": round(k1_us, 3),
         "Mmatches_per_s_kernel": round(nq * nt / (k1_us * 1e-6) / 1e6, 1),
-        "frac": round(nq * nt * VALU_OPS_PER_PAIR / (k1_us * 1e-6) / 1e12 / PEAK_VALU_TOPS, 4),
+        "frac": round(nq * nt * VALU_OPS_PER_PAIR / (k1_us * 1e-6) / 1e12 / PEAK_VALU_GUIDE_TOPS, 4),
+        "frac_measured_16_lanes": round(nq * nt * VALU_OPS_PER_PAIR / (k1_us * 1e-6) / 1e12 / PEAK_VALU_TOPS, 4),
         "traffic": None if tr1 is None else round(tr1[0]),
         "note": "one 2000 x 2000 problem per launch (osg_hamming_top2_dev): the latency form",
     }
@@ -266,7 +309,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u32",
+        "dtype": "i8->i32" if mfma else "u32",
         "data": "synthetic (SURVEY.md §8d C2 generator, seed 0x0B5EED01+rank; no EuRoC/ORBvoc in container)",
         "config": {"workload": f"C2: brute-force 256-bit Hamming top-2, 2000 x 2000 descriptors per frame, "
                                f"{B} independent frames per launch per GPU (headline; the one-frame launch is "

@@ -899,6 +899,10 @@ int osg_hamming_top2_batch_dev(osg_ctx *ctx, const void *d_query, int32_t nq, co
         }
         return OSG_OK;
     }
+    // The I8-MFMA form (hamming_mfma.hip) whenever the key's 13-bit row field holds nt;
+    // OSG_TOP2_BATCH_MFMA=0 pins the popcount form below (A/B runs, the QL / SCALAR variants).
+    static const int mf = getenv("OSG_TOP2_BATCH_MFMA") ? atoi(getenv("OSG_TOP2_BATCH_MFMA")) : 1;
+    if (mf && nt <= osg_top2_mfma_max_rows()) return osg_launch_top2_batch_mfma(ctx, d_query, nq, d_train, nt, nb, d_out);
     static const int ql_env = getenv("OSG_TOP2_BATCH_QL") ? atoi(getenv("OSG_TOP2_BATCH_QL")) : 2;
     static const int sc = getenv("OSG_TOP2_BATCH_SCALAR") ? atoi(getenv("OSG_TOP2_BATCH_SCALAR")) : 1;
     const int ql = (ql_env == 1 || ql_env == 4) ? ql_env : 2;

@@ -1,0 +1,267 @@
+// hamming_mfma.hip — frame-batched brute-force top-2 on the I8 matrix cores (gfx950).
+//
+// Same semantics as k_top2_batch (hamming.hip) and the reference's candidate loop
+// (ref:src/ORBmatcher.cc:327-355 over DescriptorDistance, :2388-2408): per query the smallest
+// distance with the first index among ties, the second smallest distance counted with
+// multiplicity, and a distance of 256 never entering (index -1).
+//
+// Distance as a dot product.  Every descriptor bit becomes one signed byte: a query bit is +64
+// when set and -64 when clear, a train bit -128 when set and 0 when clear.  Summed over the 256 bits
+// (|q| = popcount of the query, |t| of the train row, a = |q & t|):
+//     sum_k q_k t_k = -128 * 64 * (a - (|t| - a)) = 8192 * (|q| + |t| - 2 a - |q|) = 8192 * (H - |q|),
+// exact in the i32 accumulator of v_mfma_i32_32x32x32_i8.  |q| is the same for every train row of a
+// query, so with the train row's offset inside its 32-row tile as the MFMA's C input, the
+// accumulator comes out as a ready packed key
+//     key = (H - |q|) << 13 | row          (row < 8192; smaller key = smaller H, then lower row)
+// and the top-2 update per (query, row) is two VALU ops: k2 = med3(k1, key, k2), k1 = min(k1, key).
+// The 19 VALU ops per pair of the popcount form (8 xor, 8 bcnt, shift-or, min, med3) become the
+// MFMA plus those two.  Keys stay relative to the current tile: after each 32-row tile the kept
+// keys drop by 32 (the same shift for every key, so the order is kept), and the base is added
+// back once at the end.
+//
+// Layout (C/D map of the 32x32 MFMAs on gfx950, dtype-independent): lane l holds column
+// n = l & 31 and rows (i & 3) + 8 (i >> 2) + 4 (l >> 5) in accumulator element i.  Queries are the
+// columns (B operand), train rows the rows (A operand), so a lane owns one query and 16 of the
+// tile's rows; the two lane halves merge once at the end.  K-step s (32 bits) of lane half h
+// carries descriptor bits 32 s + 16 h .. + 15 on both operands (tools/micro/mfma_i8.hip probes the
+// operand maps: A and B place the same k in the same lane half and byte).
+//
+// Data movement: one workgroup = NW waves x QT query tiles of 32 queries of one problem.  Train
+// rows are expanded (32 B -> 256 B of signed bytes) once per workgroup into LDS chunks of CR rows
+// through a 256-entry byte -> 8-byte table in LDS, double-buffered: while the waves multiply chunk
+// c, the packed rows of chunk c + 1 are already in registers, and are expanded into the other
+// buffer after the chunk's MFMAs.  LDS rows are 256 B with the 16-B granules XOR-swizzled by
+// (row & 15): the 16 rows that one ds_read_b128 of a lane half reads at one granule column land
+// on 16 distinct 16-B bank groups.
+#include <algorithm>
+#include <cstdlib>
+
+#include "osg_internal.h"
+
+namespace {
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int MF_SHIFT = 13;                       // key = (H - |q|) << 13 | row
+constexpr int MF_MAX_ROWS = 1 << MF_SHIFT;         // rows per problem on this path
+constexpr int MF_PAD = 1 << 30;                    // rows past nt: above every real key
+
+// The median written as max(min(a, b), min(max(a, b), c)), which the backend selects as one
+// v_med3_i32.  Not inline asm: its operands are MFMA results, and the compiler's MFMA -> VALU
+// read hazard handling does not see inside an asm statement (an asm med3 read stale accumulators
+// in ~1 % of the second distances on the GPU).
+__device__ __forceinline__ int med3_i32(int a, int b, int c)
+{
+    return max(min(a, b), min(max(a, b), c));
+}
+
+// 4 query bits -> 4 signed bytes: bit y -> byte y = +64 (0x40) set, -64 (0xC0) clear.
+// n * 0x204081 & 0x01010101 moves bit y to bit 8 y (the four shifted copies do not overlap);
+// 0x80 - that bit per byte keeps bit 7 iff the bit is clear.
+__device__ __forceinline__ uint32_t spread_query(uint32_t nib)
+{
+    const uint32_t s = __umul24(nib, 0x204081u) & 0x01010101u;
+    return ((0x80808080u - s) & 0x80808080u) | 0x40404040u;
+}
+
+__device__ __forceinline__ void key_push(int &k1, int &k2, int key)
+{
+    k2 = med3_i32(k1, key, k2);
+    k1 = min(k1, key);
+}
+
+__device__ __forceinline__ void key_merge(int &k1, int &k2, int a1, int a2)
+{
+    const int hi = max(k1, a1);
+    k1 = min(k1, a1);
+    k2 = min(min(k2, a2), hi);
+}
+
+template <int NW, int QT, int CR>
+__global__ __launch_bounds__(NW * 64) void k_top2_mfma(const uint32_t *__restrict__ query, int nq,
+                                                        const uint32_t *__restrict__ train, int nt,
+                                                        int nqb, int32_t *__restrict__ out)
+{
+    constexpr int NT = NW * 64;
+    constexpr int BPT = CR * 32 / NT;        // packed bytes per thread per chunk
+    constexpr int WPT = BPT / 4;             // packed words per thread
+    constexpr int TPR = 32 / BPT;            // threads per row
+    static_assert(CR * 32 % NT == 0 && BPT % 4 == 0 && TPR >= 1, "chunk / workgroup shape");
+    __shared__ i32x4 s_buf[2 * CR * 16];     // [2][CR rows][16 granules of 16 B]
+    __shared__ uint2 s_lut[256];             // train byte -> 8 signed bytes (bit y -> byte y: -128 / 0)
+    const unsigned char *s_raw = (const unsigned char *)s_buf;
+
+    const int t = threadIdx.x, lane = t & 63;
+    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+    // XCD-aware numbering: consecutive logical blocks (the nqb blocks of one problem, which share
+    // its train rows) land on one XCD when the grid is a multiple of 8.
+    const int G = gridDim.x, L = blockIdx.x;
+    const int logical = (G % 8 == 0) ? (L % 8) * (G / 8) + L / 8 : L;
+    const int b = logical / nqb, qb = logical % nqb;
+    const uint32_t *qf = query + (size_t)b * nq * 8;
+    const uint32_t *tf = train + (size_t)b * nt * 8;
+    int32_t *of = out + (size_t)b * nq * 3;
+
+    for (int e = t; e < 256; e += NT) {
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int y = 0; y < 4; y++) {
+            lo |= ((e >> y) & 1u) << (8 * y + 7);
+            hi |= ((e >> (y + 4)) & 1u) << (8 * y + 7);
+        }
+        s_lut[e] = make_uint2(lo, hi);
+    }
+
+    const int r = lane & 31, h = lane >> 5;
+    const int qw0 = qb * (NW * QT * 32) + w * (QT * 32);   // first query of this wave
+    const bool active = qw0 < nq;                            // wave-uniform
+
+    // B fragments: the wave's queries, expanded once; the sentinel key (H = 256, row 0) per query
+    i32x4 bq[QT][8];
+    int k1[QT], k2[QT], pq[QT];
+#pragma unroll
+    for (int j = 0; j < QT; j++) {
+        const int q = min(qw0 + 32 * j + r, nq - 1);
+        const uint4 lo = *(const uint4 *)(qf + (size_t)q * 8), hi = *(const uint4 *)(qf + (size_t)q * 8 + 4);
+        const uint32_t wd[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        int pc = 0;
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            pc += __popc(wd[s]);
+            const uint32_t hw = h ? (wd[s] >> 16) : (wd[s] & 0xFFFFu);
+#pragma unroll
+            for (int d = 0; d < 4; d++) bq[j][s][d] = (int)spread_query((hw >> (4 * d)) & 0xFu);
+        }
+        pq[j] = pc;
+        k1[j] = k2[j] = (256 - pc) << MF_SHIFT;
+    }
+    // C input: the accumulator element's row inside the tile
+    i32x16 crow;
+#pragma unroll
+    for (int i = 0; i < 16; i++) crow[i] = (i & 3) + 8 * (i >> 2) + 4 * h;
+    // LDS byte offsets of this lane's A granules inside a tile (row r, granule (2 s + h) ^ (r & 15))
+    int aoff[8];
+#pragma unroll
+    for (int s = 0; s < 8; s++) aoff[s] = r * 256 + ((((2 * s + h) ^ (r & 15))) << 4);
+
+    // expansion of one chunk's packed rows: this thread's WPT words of row erow
+    const int erow = t / TPR, epart = t % TPR;
+    auto load_chunk = [&](int c0, uint32_t (&pw)[WPT]) {
+        const int row = c0 + erow;
+        if (row < nt) {
+            const uint32_t *src = tf + (size_t)row * 8 + epart * WPT;
+#pragma unroll
+            for (int i = 0; i < WPT; i += 2) {
+                const uint2 v = *(const uint2 *)(src + i);
+                pw[i] = v.x;
+                pw[i + 1] = v.y;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < WPT; i++) pw[i] = 0u;   // expands to zero bytes: D = C exactly
+        }
+    };
+    auto store_chunk = [&](int buf, const uint32_t (&pw)[WPT]) {
+        i32x4 *dst = s_buf + ((size_t)buf * CR + erow) * 16;
+#pragma unroll
+        for (int i = 0; i < WPT; i++) {
+#pragma unroll
+            for (int hh = 0; hh < 2; hh++) {    // granule = halfword hh of word (epart WPT + i)
+                const int g = 2 * (epart * WPT + i) + hh;
+                const uint2 v0 = s_lut[(pw[i] >> (16 * hh)) & 0xFFu];
+                const uint2 v1 = s_lut[(pw[i] >> (16 * hh + 8)) & 0xFFu];
+                dst[g ^ (erow & 15)] = i32x4{(int)v0.x, (int)v0.y, (int)v1.x, (int)v1.y};
+            }
+        }
+    };
+
+    const int nch = (nt + CR - 1) / CR;
+    {
+        uint32_t pw[WPT];
+        load_chunk(0, pw);
+        __syncthreads();   // the table
+        store_chunk(0, pw);
+    }
+    __syncthreads();
+    for (int c = 0; c < nch; c++) {
+        const int c0 = c * CR;
+        uint32_t pw[WPT];
+        const bool more = c + 1 < nch;
+        if (more) load_chunk(c0 + CR, pw);
+        if (active) {
+            const unsigned char *sb = s_raw + (size_t)(c & 1) * CR * 256;
+            const int ntile = min(CR / 32, (nt - c0 + 31) / 32);
+#pragma unroll
+            for (int tt = 0; tt < CR / 32; tt++) {
+                if (tt >= ntile) break;
+                i32x4 a[8];
+#pragma unroll
+                for (int s = 0; s < 8; s++) a[s] = *(const i32x4 *)(sb + tt * 32 * 256 + aoff[s]);
+                i32x16 cin = crow;
+                const int lim = nt - (c0 + tt * 32);   // valid rows in this tile
+                if (lim < 32) {
+#pragma unroll
+                    for (int i = 0; i < 16; i++) cin[i] = crow[i] + (crow[i] >= lim ? MF_PAD : 0);
+                }
+#pragma unroll
+                for (int j = 0; j < QT; j++) {
+                    i32x16 acc = cin;
+#pragma unroll
+                    for (int s = 0; s < 8; s++) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[s], bq[j][s], acc, 0, 0, 0);
+#pragma unroll
+                    for (int i = 0; i < 16; i++) key_push(k1[j], k2[j], acc[i]);
+                    k1[j] -= 32;
+                    k2[j] -= 32;
+                }
+            }
+        }
+        if (more) store_chunk((c + 1) & 1, pw);
+        __syncthreads();
+    }
+    if (!active) return;
+    const int base = 32 * ((nt + 31) / 32);   // the keys are relative to one tile past the last
+#pragma unroll
+    for (int j = 0; j < QT; j++) {
+        const int a1 = __shfl_xor(k1[j], 32), a2 = __shfl_xor(k2[j], 32);
+        key_merge(k1[j], k2[j], a1, a2);
+        const int q = qw0 + 32 * j + r;
+        if (h == 0 && q < nq) {
+            const int t1 = k1[j] + base, t2 = k2[j] + base;
+            const int d1 = (t1 >> MF_SHIFT) + pq[j], d2 = (t2 >> MF_SHIFT) + pq[j];
+            of[3 * q + 0] = d1 < 256 ? (t1 & (MF_MAX_ROWS - 1)) : -1;
+            of[3 * q + 1] = min(d1, 256);
+            of[3 * q + 2] = min(d2, 256);
+        }
+    }
+}
+
+template <int NW, int QT, int CR>
+int launch(osg_ctx *ctx, const void *d_query, int nq, const void *d_train, int nt, int nb, void *d_out)
+{
+    const int nqb = (nq + NW * QT * 32 - 1) / (NW * QT * 32);
+    const long long g = (long long)nqb * nb;
+    OSG_REQUIRE(ctx, g <= 0x7FFFFFFF, "grid too large");
+    hipLaunchKernelGGL((k_top2_mfma<NW, QT, CR>), dim3((unsigned)g), dim3(NW * 64), 0, ctx->stream,
+                       (const uint32_t *)d_query, nq, (const uint32_t *)d_train, nt, nqb, (int32_t *)d_out);
+    OSG_HIP_CHECK(ctx, hipGetLastError());
+    return OSG_OK;
+}
+
+}  // namespace
+
+int osg_top2_mfma_max_rows() { return MF_MAX_ROWS; }
+
+// B problems of nq x nt on the I8 MFMA path; requires 1 <= nt <= 8192 (the key's row field)
+int osg_launch_top2_batch_mfma(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d_train, int32_t nt,
+                               int32_t nb, void *d_out)
+{
+    OSG_REQUIRE(ctx, nt >= 1 && nt <= MF_MAX_ROWS, "nt=%d outside the MFMA path's 1..%d rows", nt, MF_MAX_ROWS);
+    static const int shape = getenv("OSG_TOP2_MFMA_SHAPE") ? atoi(getenv("OSG_TOP2_MFMA_SHAPE")) : 0;
+    switch (shape) {
+    case 1: return launch<8, 2, 256>(ctx, d_query, nq, d_train, nt, nb, d_out);
+    case 2: return launch<8, 1, 128>(ctx, d_query, nq, d_train, nt, nb, d_out);
+    case 3: return launch<8, 2, 128>(ctx, d_query, nq, d_train, nt, nb, d_out);
+    default: return launch<16, 1, 256>(ctx, d_query, nq, d_train, nt, nb, d_out);
+    }
+}

@@ -102,3 +102,7 @@ int osg_check_frame(osg_ctx *ctx, const osg_frame *F);
 // internal device-pointer launchers shared between translation units
 int osg_launch_top2(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d_train, int32_t nt,
                     void *d_out);
+// frame-batched top-2 on the I8 matrix cores (hamming_mfma.hip); 1 <= nt <= osg_top2_mfma_max_rows()
+int osg_top2_mfma_max_rows();
+int osg_launch_top2_batch_mfma(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d_train, int32_t nt,
+                               int32_t nb, void *d_out);

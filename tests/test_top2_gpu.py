@@ -182,10 +182,16 @@ def test_batch_empty_train(ctx):
     assert (got[..., 0] == -1).all() and (got[..., 1:] == 256).all()
 
 
-@pytest.mark.parametrize("ql,sc", [("1", "0"), ("2", "0"), ("4", "0"), ("1", "1"), ("4", "1")])
-def test_batch_query_per_lane_variants(oracle, ql, sc):
-    """The queries-per-lane (OSG_TOP2_BATCH_QL) and scalar-load (OSG_TOP2_BATCH_SCALAR) instantiations,
-    read once per process."""
+_VARIANTS = [{"OSG_TOP2_BATCH_MFMA": "0", "OSG_TOP2_BATCH_QL": ql, "OSG_TOP2_BATCH_SCALAR": sc}
+             for ql, sc in [("1", "0"), ("2", "0"), ("4", "0"), ("1", "1"), ("4", "1")]]
+_VARIANTS += [{"OSG_TOP2_MFMA_SHAPE": sh} for sh in ("0", "1", "2", "3")]
+
+
+@pytest.mark.parametrize("env", _VARIANTS, ids=lambda e: "-".join(f"{k[9:]}={v}" for k, v in e.items()))
+def test_batch_query_per_lane_variants(oracle, env):
+    """The popcount kernel's queries-per-lane (OSG_TOP2_BATCH_QL) and scalar-load (OSG_TOP2_BATCH_SCALAR)
+    instantiations, and the I8-MFMA kernel's workgroup shapes (OSG_TOP2_MFMA_SHAPE), read once per process.
+    nt = 2100: a partial LDS chunk and a partial 32-row tile."""
     import subprocess
     import sys
     code = ("import numpy as np, torch\n"
@@ -194,7 +200,7 @@ def test_batch_query_per_lane_variants(oracle, ql, sc):
             "ctx = Context(0)\n"
             "qs, ts = zip(*[synth.descriptors_c2(333, 2100, seed=5 + b) for b in range(3)])\n"
             "np.save('/tmp/_osg_batch_ql.npy', _batch(ctx, qs, ts))\n")
-    env = dict(__import__("os").environ, OSG_TOP2_BATCH_QL=ql, OSG_TOP2_BATCH_SCALAR=sc)
+    env = dict(__import__("os").environ, **env)
     root = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -203,3 +209,37 @@ def test_batch_query_per_lane_variants(oracle, ql, sc):
     for b in range(3):
         for k, ref in enumerate(otop2(oracle, qs[b], ts[b])):
             np.testing.assert_array_equal(got[b, :, k], ref)
+
+
+def test_batch_mfma_edges(ctx, oracle):
+    """The I8-MFMA form's edge cases, each problem against the serial loop:
+    * exact duplicates of the best row straddling the 32-row tiles and the 256-row LDS chunks (first index wins);
+    * the query itself in the train set (H = 0), its complement (H = 256, never enters), all-zero and all-one
+      descriptors (|q| = 0 and 256 shift the key by the most);
+    * nt = 8192, the largest train set the 13-bit row field holds, and nt = 1."""
+    rng = np.random.default_rng(2024)
+    probs = []
+    q = rng.integers(0, 256, (96, 32), dtype=np.uint8)
+    t = rng.integers(0, 256, (600, 32), dtype=np.uint8)
+    for j, rows in enumerate([(31, 32), (255, 256, 257), (0, 511), (63, 64, 512)]):
+        for rr in rows:
+            t[rr] = q[j]
+    t[100] = ~q[10]
+    probs.append((q, t))
+    z = np.zeros((1, 32), np.uint8)
+    o = np.full((1, 32), 255, np.uint8)
+    q2 = np.concatenate([z, o, q[:94]])
+    t2 = np.concatenate([o, z, t[:598]])
+    probs.append((q2, t2))
+    for qq, tt in probs:
+        got = _batch(ctx, [qq], [tt])
+        for k, r in enumerate(otop2(oracle, qq, tt)):
+            np.testing.assert_array_equal(got[0, :, k], r)
+    assert got[0, 0, 1] == 0 and got[0, 1, 1] == 0   # the zero / one rows found at H = 0
+    q3, t3 = synth.descriptors_c2(200, 8192, seed=77)
+    q4, t4 = synth.descriptors_c2(200, 1, seed=78)
+    for qq, tt in [(q3, t3), (q4, t4)]:
+        got = _batch(ctx, [qq, qq], [tt, tt])
+        for b in range(2):
+            for k, r in enumerate(otop2(oracle, qq, tt)):
+                np.testing.assert_array_equal(got[b, :, k], r)
