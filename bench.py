@@ -105,7 +105,7 @@ def parse():
     ap.add_argument("--wall-threads", type=int, default=8,
                     help="host threads of the C++ wall bench, each with its own context (Tracking threads)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
-                    help="per-launch HBM traffic from the rocprofv3 PMC passes (tools/gpu_profile_r03.sh)")
+                    help="per-launch HBM traffic from the rocprofv3 PMC passes (tools/gpu/gpu_profile_r03.sh)")
     ap.add_argument("--valu-pmc", default=os.path.join(ROOT, "profiles", "r03_top2_valu_pmc.json"),
                     help="the headline kernel's VALU counters (tools/pmc_valu.py)")
     ap.add_argument("--schur-pmc", default=os.path.join(ROOT, "profiles", "r03_schur_pmc.json"),

@@ -134,6 +134,14 @@ struct LbaDev {
     // has nothing left of column block blk_first[t], in A and in its Cholesky factor (fill-in stays
     // inside the profile); blk_last[j] = the last row block t with blk_first[t] <= j
     const int32_t *blk_first, *blk_last;
+    // per column block j (past CMAX): the row blocks t > j inside the envelope (blk_first[t] <= j),
+    // ascending, as CSR: the rows k_chol_col / k_chol_trail touch.  A loop closure makes the last rows
+    // reach column 0, so these lists are the band rows plus those few, not every row below j.
+    const int32_t *col_rows_start, *col_rows;
+    // pose pairs (i <= j) k_schur_pairs writes past CMAX: those whose 6 x 6 block reaches a lower tile
+    // inside the envelope (the factorisation reads nothing else); null: every pair (n <= CMAX)
+    const int32_t *live_pairs;
+    int n_live;
     int *flag;                           // [0] cholesky ok
     unsigned long long *tstamp;          // phase timestamps (OSG_LBA_PROFILE=2), else null
 };
@@ -652,16 +660,20 @@ __global__ __launch_bounds__(256) void k_schur_pairs(const LbaDev *__restrict__ 
 {
     LBA_GRAPH(M_ACT);
     const double lambda = D.ctl->lambda;
-    const int wave = (bx * 256 + threadIdx.x) >> 6;
+    const int slot = (bx * 256 + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
-    if (wave >= D.npairs) return;
-    int i = 0, rem = wave;
-    while (rem >= D.nhp - i) {
-        rem -= D.nhp - i;
-        i++;
-    }
-    const int j = i + rem;
-    if (wave == 0 && lane == 0) D.flag[0] = 1;  // the Cholesky of this trial clears it on failure
+    if (slot >= (D.live_pairs ? D.n_live : D.npairs)) return;
+    if (slot == 0 && lane == 0) D.flag[0] = 1;  // the Cholesky of this trial clears it on failure
+    const int wave = D.live_pairs ? D.live_pairs[slot] : slot;  // the pair's index (i-major, j >= i)
+    // pair index -> (i, j): start(i) = i nhp - i (i - 1) / 2 <= wave < start(i + 1), from the root of
+    // the quadratic, then corrected by one either way for rounding
+    const long long m = D.nhp;
+    int i = (int)(((2.0 * m + 1.0) - sqrt((2.0 * m + 1.0) * (2.0 * m + 1.0) - 8.0 * (double)wave)) * 0.5);
+    auto start = [&](long long a) { return a * m - a * (a - 1) / 2; };
+    i = max(0, min(i, (int)m - 1));
+    while (i > 0 && start(i) > wave) i--;
+    while (i + 1 < m && start(i + 1) <= wave) i++;
+    const int j = i + (int)(wave - start(i));
     const int n = 6 * D.nhp;
     if (lane < 36) {
         const int r = lane / 6, c = lane % 6;
@@ -996,14 +1008,17 @@ __global__ __launch_bounds__(256) void k_chol_col(const LbaDev *__restrict__ Ds,
 {
     LBA_GRAPH(M_ACT);
     if (j >= D.nblk_red || bx >= D.nblk_red - j) return;
-    // past CMAX a row block outside the envelope has an all-zero tile here, and its L_tj stays zero
-    if (6 * D.nhp > CMAX && bx > 0 && (j + bx > D.blk_last[j] || D.blk_first[j + bx] > j)) return;
+    // past CMAX workgroup 0 is the diagonal block and workgroup b >= 1 the b-th envelope row of the
+    // column (col_rows): a row block outside the envelope has an all-zero tile here, and its L_tj
+    // stays zero
+    const bool big = 6 * D.nhp > CMAX;
+    if (big && bx > 0 && bx > D.col_rows_start[j + 1] - D.col_rows_start[j]) return;
     __shared__ CholLds L;
     const int n = 6 * D.nhp;
     const double *A = D.Hs;
     const int k0 = j * CB;
     const int nb = min(CB, n - k0);
-    const int t = bx;
+    const int t = (big && bx > 0) ? D.col_rows[D.col_rows_start[j] + bx - 1] - j : bx;  // row block j + t
     const int tid = threadIdx.x;
     const int R0 = k0 + t * CB;
     unsigned long long *ts = (D.tstamp && t < 2 && tid == 0 && j < 32) ? D.tstamp + 8 * (2 * j + t) : nullptr;
@@ -1139,17 +1154,16 @@ __global__ __launch_bounds__(256) void k_chol_trail(const LbaDev *__restrict__ D
     const int n = 6 * D.nhp;
     if (n <= CMAX) return;
     if (j >= D.nblk_red) return;
-    const int m = D.blk_last[j] - j;  // row blocks below block j inside the envelope's reach
+    // the envelope rows of column j (L_tj nonzero): tile (t, u) for every pair of them, u <= t
+    const int r0 = D.col_rows_start[j], m = D.col_rows_start[j + 1] - r0;
     if (m <= 0 || bx >= m * (m + 1) / 2) return;
-    int t = 0, rem = bx;  // tile (t, u), u <= t, row-major over the lower triangle
-    while (rem > t) {
-        rem -= t + 1;
-        t++;
-    }
-    const int u = rem;
-    // L_tj or L_uj outside the envelope is zero: the tile's update is zero
-    if (D.blk_first[j + 1 + t] > j || D.blk_first[j + 1 + u] > j) return;
-    const int R0 = (j + 1 + t) * CB, C0 = (j + 1 + u) * CB, K0 = j * CB;
+    int a = (int)((sqrt(8.0 * bx + 1.0) - 1.0) * 0.5);  // bx = a (a + 1) / 2 + b, b <= a
+    while (a * (a + 1) / 2 > bx) a--;
+    while ((a + 1) * (a + 2) / 2 <= bx) a++;
+    const int b = bx - a * (a + 1) / 2;
+    const int tb = D.col_rows[r0 + a], ub = D.col_rows[r0 + b];
+    const int t = tb - j - 1, u = ub - j - 1;  // as offsets below block j
+    const int R0 = tb * CB, C0 = ub * CB, K0 = j * CB;
     __shared__ double sLt[CB][CB + 1], sLu[CB][CB + 1];
     const int tid = threadIdx.x;
     for (int e = tid; e < CB * CB; e += 256) {
@@ -1207,10 +1221,15 @@ __global__ __launch_bounds__(1024) void k_chol_back_large(const LbaDev *__restri
         const int k0 = bi * CB, nb = min(CB, n - k0);
         s_li[tid] = D.Linv[(size_t)min(k0 + (tid >> 5), n - 1) * CB + (tid & 31)];
         __syncthreads();
+        // the rows below the block inside the envelope only (column block bi's envelope rows, ascending):
+        // every other L entry of this column is zero, and is not stored (k_schur_pairs writes only the
+        // pairs the factorisation reads).  Group g takes row g of each of those row blocks.
         double acc = 0.0;
         if (c < nb) {
-#pragma unroll 8
-            for (int row = k0 + nb + g; row < n; row += 32) acc += A[(size_t)row * n + k0 + c] * s_x[row];
+            for (int q = D.col_rows_start[bi]; q < D.col_rows_start[bi + 1]; q++) {
+                const int row = D.col_rows[q] * CB + g;
+                if (row < n) acc += A[(size_t)row * n + k0 + c] * s_x[row];
+            }
         }
         s_part[c][g] = acc;
         __syncthreads();
@@ -1410,6 +1429,8 @@ struct LbaHost {
     int ge = 0, gl = 0, gll = 0, gu = 0, nblk_red = 0, npart = 64;
     bool multi = false;  // a block with several edges (k_linearize<true>)
     std::vector<int32_t> blk_first, blk_last;  // envelope of the reduced system by row block (see LbaDev)
+    std::vector<int32_t> col_rows_start, col_rows, live_pairs;  // envelope rows per column block, live pairs
+    int max_col_rows = 0;
     bool trivial = false;  // nothing to optimise: the estimates are returned unchanged
     std::vector<int32_t> pose_h, hp_pose, point_h, hl_point, lm_e_start, lm_e, lg_start, lm_b_start, blk_pose, edge_blk, blk_lm,
         hp_e_start, hp_e, hp_b_start, hp_b, pair_start, pair_ab, chunk_start, pair_chunk,
@@ -1435,6 +1456,10 @@ struct LbaHost {
         npart = 64;
         blk_first.clear();
         blk_last.clear();
+        col_rows_start.clear();
+        col_rows.clear();
+        live_pairs.clear();
+        max_col_rows = 0;
         trivial = false;
         hp_pose.clear();
         hl_point.clear();
@@ -1632,6 +1657,26 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
         for (int j = 0; j < nb; j++) H.blk_last[j] = j;
         for (int t = 0; t < nb; t++)
             for (int j = H.blk_first[t]; j <= t; j++) H.blk_last[j] = std::max(H.blk_last[j], t);
+        if (n > CMAX) {
+            H.col_rows_start.assign(nb + 1, 0);
+            for (int t = 0; t < nb; t++)
+                for (int j = H.blk_first[t]; j < t; j++) H.col_rows_start[j + 1]++;
+            for (int j = 0; j < nb; j++) H.col_rows_start[j + 1] += H.col_rows_start[j];
+            H.col_rows.assign(std::max(H.col_rows_start[nb], 1), 0);
+            std::vector<int32_t> fill(H.col_rows_start.begin(), H.col_rows_start.end() - 1);
+            for (int t = 0; t < nb; t++)  // t ascending: each list comes out sorted
+                for (int j = H.blk_first[t]; j < t; j++) H.col_rows[fill[j]++] = t;
+            for (int j = 0; j < nb; j++)
+                H.max_col_rows = std::max(H.max_col_rows, H.col_rows_start[j + 1] - H.col_rows_start[j]);
+            // live pairs: (i <= j) with some entry (row in pose j, column in pose i) in a lower
+            // envelope tile: row block of 6 j + r, column block of 6 i + c, blk_first[row blk] <= col blk
+            for (int i = 0, k = 0; i < nhp; i++)
+                for (int j = i; j < nhp; j++, k++) {
+                    const int cb1 = (6 * i + 5) / CB;  // the block's last column block
+                    if (H.blk_first[(6 * j) / CB] <= cb1 || H.blk_first[(6 * j + 5) / CB] <= cb1)
+                        H.live_pairs.push_back(k);
+                }
+        }
     }
     // rank of each block in its pose's block list (hp_b is in block order); row segments of RS ranks
     std::vector<int32_t> blk_rank(nblk);
@@ -1867,7 +1912,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     struct InOff {
         size_t fixed, epose, epoint, ecam, ekind, eobs, eisig, cams, poseh, hppose, pointh, hlpoint, lmes, lme, lgs, lmbs,
             blkpose, eblk, hpes, hpe, hpbs, hpb, pairs, pairab, chs, blklm, pch, pose0, point0, erob,
-            prank, rspose, rsrank0, rscs, rsc, hprs, bfirst, blast, rsinfo, hpblm, rscd;
+            prank, rspose, rsrank0, rscs, rsc, hprs, bfirst, blast, rsinfo, hpblm, rscd, crs, cr, live;
     };
     std::vector<InOff> io(NA);
     for (int a = 0; a < NA; a++) {
@@ -1906,6 +1951,9 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         o.prank = pk.add(h.pair_rank.data(), 4 * h.pair_rank.size());
         o.bfirst = pk.add(h.blk_first.data(), 4 * std::max<size_t>(h.blk_first.size(), 1));
         o.blast = pk.add(h.blk_last.data(), 4 * std::max<size_t>(h.blk_last.size(), 1));
+        o.crs = h.col_rows_start.empty() ? SIZE_MAX : pk.add(h.col_rows_start.data(), 4 * h.col_rows_start.size());
+        o.cr = h.col_rows_start.empty() ? SIZE_MAX : pk.add(h.col_rows.data(), 4 * h.col_rows.size());
+        o.live = h.col_rows_start.empty() ? SIZE_MAX : pk.add(h.live_pairs.data(), 4 * std::max<size_t>(h.live_pairs.size(), 1));
         o.rspose = pk.add(h.rs_pose.data(), 4 * h.rs_pose.size());
         o.rsrank0 = pk.add(h.rs_rank0.data(), 4 * h.rs_rank0.size());
         o.rsinfo = pk.add(h.rs_info.data(), 4 * h.rs_info.size());
@@ -2004,6 +2052,10 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         D.pair_rank = osg_dptr<int32_t>(din, o.prank);
         D.blk_first = osg_dptr<int32_t>(din, o.bfirst);
         D.blk_last = osg_dptr<int32_t>(din, o.blast);
+        D.col_rows_start = o.crs == SIZE_MAX ? nullptr : osg_dptr<int32_t>(din, o.crs);
+        D.col_rows = o.cr == SIZE_MAX ? nullptr : osg_dptr<int32_t>(din, o.cr);
+        D.live_pairs = o.live == SIZE_MAX ? nullptr : osg_dptr<int32_t>(din, o.live);
+        D.n_live = (int)h.live_pairs.size();
         D.npart = h.npart;
         D.n_rs = h.n_rs;
         D.rs_pose = osg_dptr<int32_t>(din, o.rspose);
@@ -2035,7 +2087,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         mx_nhp = std::max(mx_nhp, h.nhp);
         mx_chunks = std::max(mx_chunks, h.nchunks);
         mx_rs = std::max(mx_rs, h.n_rs);
-        mx_pairs = std::max(mx_pairs, h.npairs);
+        mx_pairs = std::max(mx_pairs, h.col_rows_start.empty() ? h.npairs : (int)h.live_pairs.size());
         mx_red = std::max(mx_red, h.nblk_red);
     }
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(d_dev, h_dev, dev_bytes, hipMemcpyHostToDevice, ctx->stream));
@@ -2094,7 +2146,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
             if (schur_valu) hipLaunchKernelGGL(k_schur_rows<true>, gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
             else hipLaunchKernelGGL(k_schur_rows<false>, gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
             LBA_MARK(KT_SPAIRS);
-            hipLaunchKernelGGL(k_schur_pairs, gx((mx_pairs * 64 + 255) / 256), dim3(256), 0, ctx->stream, d_dev);
+            hipLaunchKernelGGL(k_schur_pairs, gx((int)(((size_t)mx_pairs * 64 + 255) / 256)), dim3(256), 0, ctx->stream, d_dev);
             LBA_MARK(KT_CHOL);
             for (int jb = 0; jb < mx_red; jb++) {  // row blocks at and below the diagonal block
                 // past CMAX only the envelope's rows: grids sized by the largest reach of any graph
@@ -2103,8 +2155,9 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
                     const LbaHost &h = H[act[a]];
                     if (jb >= h.nblk_red) continue;
                     const bool big = 6 * h.nhp > CMAX;
-                    rows = std::max(rows, big ? h.blk_last[jb] - jb + 1 : h.nblk_red - jb);
-                    if (big) m = std::max(m, h.blk_last[jb] - jb);
+                    const int nr = big ? h.col_rows_start[jb + 1] - h.col_rows_start[jb] : 0;
+                    rows = std::max(rows, big ? 1 + nr : h.nblk_red - jb);
+                    if (big) m = std::max(m, nr);
                 }
                 if (rows == 0) continue;
                 hipLaunchKernelGGL(k_chol_col, gx(rows), dim3(256), 0, ctx->stream, d_dev, jb);

@@ -13,9 +13,10 @@
 // query, so with the train row's offset inside its 32-row tile as the MFMA's C input, the
 // accumulator comes out as a ready packed key
 //     key = (H - |q|) << 13 | row          (row < 8192; smaller key = smaller H, then lower row)
-// and the top-2 update per (query, row) is two VALU ops: k2 = med3(k1, key, k2), k1 = min(k1, key).
+// and the top-2 update is 1.5 VALU ops per (query, row): two keys at a time, k1 = min3(k1, x, y),
+// k2 = min(med3(k1, x, y), k2).
 // The 19 VALU ops per pair of the popcount form (8 xor, 8 bcnt, shift-or, min, med3) become the
-// MFMA plus those two.  Keys stay relative to the current tile: after each 32-row tile the kept
+// MFMA plus those.  Keys stay relative to the current tile: after each 32-row tile the kept
 // keys drop by 32 (the same shift for every key, so the order is kept), and the base is added
 // back once at the end.
 //
@@ -46,6 +47,7 @@ typedef int i32x16 __attribute__((ext_vector_type(16)));
 constexpr int MF_SHIFT = 13;                       // key = (H - |q|) << 13 | row
 constexpr int MF_MAX_ROWS = 1 << MF_SHIFT;         // rows per problem on this path
 constexpr int MF_PAD = 1 << 30;                    // rows past nt: above every real key
+constexpr int MF_RS = 272;                         // LDS row stride: 256 B of signed bytes + 16 B pad
 
 // The median written as max(min(a, b), min(max(a, b), c)), which the backend selects as one
 // v_med3_i32.  Not inline asm: its operands are MFMA results, and the compiler's MFMA -> VALU
@@ -71,6 +73,16 @@ __device__ __forceinline__ void key_push(int &k1, int &k2, int key)
     k1 = min(k1, key);
 }
 
+// Two keys at once: with k1 <= k2 and S = {k1, x, y}, the smallest of S u {k2} is min3(k1, x, y) and
+// the second is min(med3(k1, x, y), k2) (k2 >= k1 cannot be the strict smallest): 3 VALU for two
+// keys (v_min3_i32, v_med3_i32, v_min_i32) instead of 4.
+__device__ __forceinline__ void key_push2(int &k1, int &k2, int x, int y)
+{
+    const int m = med3_i32(k1, x, y);
+    k1 = min(min(k1, x), y);
+    k2 = min(m, k2);
+}
+
 __device__ __forceinline__ void key_merge(int &k1, int &k2, int a1, int a2)
 {
     const int hi = max(k1, a1);
@@ -78,7 +90,7 @@ __device__ __forceinline__ void key_merge(int &k1, int &k2, int a1, int a2)
     k2 = min(min(k2, a2), hi);
 }
 
-template <int NW, int QT, int CR>
+template <int NW, int QT, int CR, int PIPE>
 __global__ __launch_bounds__(NW * 64) void k_top2_mfma(const uint32_t *__restrict__ query, int nq,
                                                         const uint32_t *__restrict__ train, int nt,
                                                         int nqb, int32_t *__restrict__ out)
@@ -87,10 +99,10 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(const uint32_t *__restric
     constexpr int BPT = CR * 32 / NT;        // packed bytes per thread per chunk
     constexpr int WPT = BPT / 4;             // packed words per thread
     constexpr int TPR = 32 / BPT;            // threads per row
+    constexpr int NTILE = CR / 32;           // 32-row tiles per chunk
     static_assert(CR * 32 % NT == 0 && BPT % 4 == 0 && TPR >= 1, "chunk / workgroup shape");
-    __shared__ i32x4 s_buf[2 * CR * 16];     // [2][CR rows][16 granules of 16 B]
+    __shared__ __attribute__((aligned(16))) unsigned char s_buf[2 * CR * MF_RS];   // [2][CR rows][272 B]
     __shared__ uint2 s_lut[256];             // train byte -> 8 signed bytes (bit y -> byte y: -128 / 0)
-    const unsigned char *s_raw = (const unsigned char *)s_buf;
 
     const int t = threadIdx.x, lane = t & 63;
     const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -117,9 +129,11 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(const uint32_t *__restric
     const int qw0 = qb * (NW * QT * 32) + w * (QT * 32);   // first query of this wave
     const bool active = qw0 < nq;                            // wave-uniform
 
-    // B fragments: the wave's queries, expanded once; the sentinel key (H = 256, row 0) per query
+    // B fragments: the wave's queries, expanded once.  Each query keeps two running top-2 pairs
+    // (accumulator elements 0-7 and 8-15: two independent dependency chains), merged at the end;
+    // both start at the sentinel key (H = 256, row 0).
     i32x4 bq[QT][8];
-    int k1[QT], k2[QT], pq[QT];
+    int ka1[QT], ka2[QT], kb1[QT], kb2[QT], pq[QT];
 #pragma unroll
     for (int j = 0; j < QT; j++) {
         const int q = min(qw0 + 32 * j + r, nq - 1);
@@ -134,16 +148,14 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(const uint32_t *__restric
             for (int d = 0; d < 4; d++) bq[j][s][d] = (int)spread_query((hw >> (4 * d)) & 0xFu);
         }
         pq[j] = pc;
-        k1[j] = k2[j] = (256 - pc) << MF_SHIFT;
+        ka1[j] = ka2[j] = kb1[j] = kb2[j] = (256 - pc) << MF_SHIFT;
     }
     // C input: the accumulator element's row inside the tile
     i32x16 crow;
 #pragma unroll
     for (int i = 0; i < 16; i++) crow[i] = (i & 3) + 8 * (i >> 2) + 4 * h;
-    // LDS byte offsets of this lane's A granules inside a tile (row r, granule (2 s + h) ^ (r & 15))
-    int aoff[8];
-#pragma unroll
-    for (int s = 0; s < 8; s++) aoff[s] = r * 256 + ((((2 * s + h) ^ (r & 15))) << 4);
+    // this lane's A granule of K-step s in a tile: row r, granule 2 s + h, at lbase + 32 s
+    const int lbase = r * MF_RS + h * 16;
 
     // expansion of one chunk's packed rows: this thread's WPT words of row erow
     const int erow = t / TPR, epart = t % TPR;
@@ -163,7 +175,7 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(const uint32_t *__restric
         }
     };
     auto store_chunk = [&](int buf, const uint32_t (&pw)[WPT]) {
-        i32x4 *dst = s_buf + ((size_t)buf * CR + erow) * 16;
+        unsigned char *dst = s_buf + ((size_t)buf * CR + erow) * MF_RS;
 #pragma unroll
         for (int i = 0; i < WPT; i++) {
 #pragma unroll
@@ -171,9 +183,43 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(const uint32_t *__restric
                 const int g = 2 * (epart * WPT + i) + hh;
                 const uint2 v0 = s_lut[(pw[i] >> (16 * hh)) & 0xFFu];
                 const uint2 v1 = s_lut[(pw[i] >> (16 * hh + 8)) & 0xFFu];
-                dst[g ^ (erow & 15)] = i32x4{(int)v0.x, (int)v0.y, (int)v1.x, (int)v1.y};
+                *(i32x4 *)(dst + 16 * g) = i32x4{(int)v0.x, (int)v0.y, (int)v1.x, (int)v1.y};
             }
         }
+    };
+
+    auto frag = [&](const unsigned char *tb, int s) -> i32x4 { return *(const i32x4 *)(tb + lbase + 32 * s); };
+    auto mfma = [&](const i32x4 &a, const i32x4 &bb, const i32x16 &c) {
+        return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bb, c, 0, 0, 0);
+    };
+    // top-2 update of the wave's queries with one tile's accumulators, then the tile-base shift
+    auto epi = [&](const i32x16 (&acc)[QT]) {
+#pragma unroll
+        for (int j = 0; j < QT; j++) {
+#pragma unroll
+            for (int i = 0; i < 8; i += 2) {
+                key_push2(ka1[j], ka2[j], acc[j][i], acc[j][i + 1]);
+                key_push2(kb1[j], kb2[j], acc[j][i + 8], acc[j][i + 9]);
+            }
+            ka1[j] -= 32;
+            ka2[j] -= 32;
+            kb1[j] -= 32;
+            kb2[j] -= 32;
+        }
+    };
+    // one tile, unpipelined: 8 K-steps of MFMA, then the update (partial chunks, the last tile)
+    auto tile = [&](const unsigned char *tb, const i32x16 &cin) {
+        i32x4 a[8];
+#pragma unroll
+        for (int s = 0; s < 8; s++) a[s] = frag(tb, s);
+        i32x16 acc[QT];
+#pragma unroll
+        for (int j = 0; j < QT; j++) acc[j] = mfma(a[0], bq[j][0], cin);
+#pragma unroll
+        for (int s = 1; s < 8; s++)
+#pragma unroll
+            for (int j = 0; j < QT; j++) acc[j] = mfma(a[s], bq[j][s], acc[j]);
+        epi(acc);
     };
 
     const int nch = (nt + CR - 1) / CR;
@@ -190,44 +236,87 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(const uint32_t *__restric
         const bool more = c + 1 < nch;
         if (more) load_chunk(c0 + CR, pw);
         if (active) {
-            const unsigned char *sb = s_raw + (size_t)(c & 1) * CR * 256;
-            const int ntile = min(CR / 32, (nt - c0 + 31) / 32);
-#pragma unroll
-            for (int tt = 0; tt < CR / 32; tt++) {
-                if (tt >= ntile) break;
+            const unsigned char *sb = s_buf + (size_t)(c & 1) * CR * MF_RS;
+            // full tiles with the plain row offsets; the one partial tile of the problem (its last)
+            // separately, with rows past nt lifted above every real key
+            const int nfull = min(NTILE, (nt - c0) / 32);
+            if (PIPE && nfull == NTILE) {
+                // A whole chunk as one branch-free block, software-pipelined by hand: K-step s of
+                // tile t issues its QT MFMAs, refills the A register it just consumed with tile
+                // t + 1's granule (8 MFMAs of latency cover that LDS read), and performs element s of
+                // each of the two running top-2 chains for tile t - 1's accumulators (4 QT VALU in
+                // the MFMAs' shadow).  sched_barrier keeps each step's instructions in this order.
                 i32x4 a[8];
+                i32x16 accp[QT], acc[QT];
 #pragma unroll
-                for (int s = 0; s < 8; s++) a[s] = *(const i32x4 *)(sb + tt * 32 * 256 + aoff[s]);
-                i32x16 cin = crow;
-                const int lim = nt - (c0 + tt * 32);   // valid rows in this tile
-                if (lim < 32) {
+                for (int s = 0; s < 8; s++) a[s] = frag(sb, s);
 #pragma unroll
-                    for (int i = 0; i < 16; i++) cin[i] = crow[i] + (crow[i] >= lim ? MF_PAD : 0);
+                for (int s = 0; s < 8; s++) {
+#pragma unroll
+                    for (int j = 0; j < QT; j++) accp[j] = mfma(a[s], bq[j][s], s ? accp[j] : crow);
+                    a[s] = frag(sb + 32 * MF_RS, s);
+                    __builtin_amdgcn_sched_barrier(0);
                 }
 #pragma unroll
-                for (int j = 0; j < QT; j++) {
-                    i32x16 acc = cin;
+                for (int tt = 1; tt < NTILE; tt++) {
 #pragma unroll
-                    for (int s = 0; s < 8; s++) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[s], bq[j][s], acc, 0, 0, 0);
+                    for (int s = 0; s < 8; s++) {
 #pragma unroll
-                    for (int i = 0; i < 16; i++) key_push(k1[j], k2[j], acc[i]);
-                    k1[j] -= 32;
-                    k2[j] -= 32;
+                        for (int j = 0; j < QT; j++) acc[j] = mfma(a[s], bq[j][s], s ? acc[j] : crow);
+                        if (tt + 1 < NTILE && !(PIPE & 4)) a[s] = frag(sb + (tt + 1) * 32 * MF_RS, s);
+#pragma unroll
+                        for (int j = 0; j < QT; j++) {
+                            if (PIPE & 2) {   // timing experiment: minimal update (results invalid)
+                                if (s == 0) ka1[j] = min(ka1[j], accp[j][0]);
+                                continue;
+                            }
+                            // pair s of the tile's 8 key pairs: chain A elements 0-7, chain B 8-15
+                            if (s & 1)
+                                key_push2(kb1[j], kb2[j], accp[j][8 + (s & 6)], accp[j][9 + (s & 6)]);
+                            else
+                                key_push2(ka1[j], ka2[j], accp[j][s & 6], accp[j][1 + (s & 6)]);
+                            if (s == 7) {
+                                ka1[j] -= 32;
+                                ka2[j] -= 32;
+                                kb1[j] -= 32;
+                                kb2[j] -= 32;
+                            }
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+#pragma unroll
+                    for (int j = 0; j < QT; j++) accp[j] = acc[j];
+                }
+                epi(accp);
+            } else {
+#pragma unroll
+                for (int tt = 0; tt < NTILE; tt++) {
+                    if (tt >= nfull) break;
+                    tile(sb + tt * 32 * MF_RS, crow);
                 }
             }
+            const int lim = nt - (c0 + nfull * 32);   // rows of a partial tile (< 32 when there is one)
+            if (nfull < NTILE && lim > 0) {
+                i32x16 cin;
+#pragma unroll
+                for (int i = 0; i < 16; i++) cin[i] = crow[i] + (crow[i] >= lim ? MF_PAD : 0);
+                tile(sb + nfull * 32 * MF_RS, cin);
+            }
         }
-        if (more) store_chunk((c + 1) & 1, pw);
+        if (more && !(PIPE & 8)) store_chunk((c + 1) & 1, pw);
         __syncthreads();
     }
     if (!active) return;
     const int base = 32 * ((nt + 31) / 32);   // the keys are relative to one tile past the last
 #pragma unroll
     for (int j = 0; j < QT; j++) {
-        const int a1 = __shfl_xor(k1[j], 32), a2 = __shfl_xor(k2[j], 32);
-        key_merge(k1[j], k2[j], a1, a2);
+        int k1 = ka1[j], k2 = ka2[j];
+        key_merge(k1, k2, kb1[j], kb2[j]);
+        const int a1 = __shfl_xor(k1, 32), a2 = __shfl_xor(k2, 32);
+        key_merge(k1, k2, a1, a2);
         const int q = qw0 + 32 * j + r;
         if (h == 0 && q < nq) {
-            const int t1 = k1[j] + base, t2 = k2[j] + base;
+            const int t1 = k1 + base, t2 = k2 + base;
             const int d1 = (t1 >> MF_SHIFT) + pq[j], d2 = (t2 >> MF_SHIFT) + pq[j];
             of[3 * q + 0] = d1 < 256 ? (t1 & (MF_MAX_ROWS - 1)) : -1;
             of[3 * q + 1] = min(d1, 256);
@@ -236,13 +325,13 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(const uint32_t *__restric
     }
 }
 
-template <int NW, int QT, int CR>
+template <int NW, int QT, int CR, int PIPE>
 int launch(osg_ctx *ctx, const void *d_query, int nq, const void *d_train, int nt, int nb, void *d_out)
 {
     const int nqb = (nq + NW * QT * 32 - 1) / (NW * QT * 32);
     const long long g = (long long)nqb * nb;
     OSG_REQUIRE(ctx, g <= 0x7FFFFFFF, "grid too large");
-    hipLaunchKernelGGL((k_top2_mfma<NW, QT, CR>), dim3((unsigned)g), dim3(NW * 64), 0, ctx->stream,
+    hipLaunchKernelGGL((k_top2_mfma<NW, QT, CR, PIPE>), dim3((unsigned)g), dim3(NW * 64), 0, ctx->stream,
                        (const uint32_t *)d_query, nq, (const uint32_t *)d_train, nt, nqb, (int32_t *)d_out);
     OSG_HIP_CHECK(ctx, hipGetLastError());
     return OSG_OK;
@@ -259,9 +348,16 @@ int osg_launch_top2_batch_mfma(osg_ctx *ctx, const void *d_query, int32_t nq, co
     OSG_REQUIRE(ctx, nt >= 1 && nt <= MF_MAX_ROWS, "nt=%d outside the MFMA path's 1..%d rows", nt, MF_MAX_ROWS);
     static const int shape = getenv("OSG_TOP2_MFMA_SHAPE") ? atoi(getenv("OSG_TOP2_MFMA_SHAPE")) : 0;
     switch (shape) {
-    case 1: return launch<8, 2, 256>(ctx, d_query, nq, d_train, nt, nb, d_out);
-    case 2: return launch<8, 1, 128>(ctx, d_query, nq, d_train, nt, nb, d_out);
-    case 3: return launch<8, 2, 128>(ctx, d_query, nq, d_train, nt, nb, d_out);
-    default: return launch<16, 1, 256>(ctx, d_query, nq, d_train, nt, nb, d_out);
+    case 1: return launch<8, 2, 256, 1>(ctx, d_query, nq, d_train, nt, nb, d_out);
+    case 2: return launch<16, 1, 256, 0>(ctx, d_query, nq, d_train, nt, nb, d_out);
+    case 3: return launch<8, 2, 256, 0>(ctx, d_query, nq, d_train, nt, nb, d_out);
+    case 4: return launch<8, 1, 256, 1>(ctx, d_query, nq, d_train, nt, nb, d_out);
+    // timing experiments (results invalid): 10 no expansion + minimal update, 14 also no A refills,
+    // 12 no A refills, 8 no expansion
+    case 10: return launch<16, 1, 256, 1 | 2 | 8>(ctx, d_query, nq, d_train, nt, nb, d_out);
+    case 14: return launch<16, 1, 256, 1 | 2 | 4 | 8>(ctx, d_query, nq, d_train, nt, nb, d_out);
+    case 12: return launch<16, 1, 256, 1 | 4>(ctx, d_query, nq, d_train, nt, nb, d_out);
+    case 8: return launch<16, 1, 256, 1 | 8>(ctx, d_query, nq, d_train, nt, nb, d_out);
+    default: return launch<16, 1, 256, 1>(ctx, d_query, nq, d_train, nt, nb, d_out);
     }
 }

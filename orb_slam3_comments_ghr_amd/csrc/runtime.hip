@@ -1,7 +1,9 @@
 #include <string>
 // runtime.hip — context lifecycle, scratch pool, errors (C ABI: include/osg.h "context").
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstring>
 
 #include "osg_internal.h"
@@ -58,7 +60,10 @@ void *osg_pinned(osg_ctx *ctx, size_t bytes)
     }
     size_t cap = bytes + bytes / 4 + 4096;
     void *p = nullptr;
-    if (hipHostMalloc(&p, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+    // coherent (fine-grained) pages: k_copy loads and stores them directly, and each call's upload /
+    // download must see the host's latest bytes at the same offsets with no stale GPU L2 line, whatever
+    // fence scope the runtime gives the dispatch (HIP_HOST_COHERENT is not relied on)
+    if (hipHostMalloc(&p, cap, hipHostMallocCoherent) != hipSuccess) return nullptr;
     ctx->host_pinned = p;
     ctx->host_pinned_cap = cap;
     return p;
@@ -128,27 +133,39 @@ int osg_idle(osg_ctx *ctx)
     return OSG_OK;
 }
 
+// Wait for the stream: poll its completion event for up to OSG_WAIT_SPIN_US microseconds (default
+// 100: a one-frame matcher call ends within that, and returns ~1 us after its last kernel), then
+// block on the event (created with hipEventBlockingSync, so the thread sleeps instead of burning a
+// host core that Tracking / LocalMapping / LoopClosing threads need while a long BA call runs).
 int osg_wait(osg_ctx *ctx)
 {
     // OSG_WAIT=sync: a stream synchronisation instead of the polled event (A/B runs)
     static const bool sync_wait = getenv("OSG_WAIT") && std::string(getenv("OSG_WAIT")) == "sync";
+    static const double spin_us = getenv("OSG_WAIT_SPIN_US") ? atof(getenv("OSG_WAIT_SPIN_US")) : 100.0;
     if (sync_wait) {
         OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
         return OSG_OK;
     }
-    if (!ctx->ev_done && hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming) != hipSuccess) {
+    if (!ctx->ev_done &&
+        hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming | hipEventBlockingSync) != hipSuccess) {
         ctx->ev_done = nullptr;
         OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
         return OSG_OK;
     }
     OSG_HIP_CHECK(ctx, hipEventRecord(ctx->ev_done, ctx->stream));
-    for (;;) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int it = 0;; it++) {
         const hipError_t e = hipEventQuery(ctx->ev_done);
         if (e == hipSuccess) return OSG_OK;
         if (e != hipErrorNotReady)
             return osg_set_error(ctx, OSG_E_HIP, "hipEventQuery failed: %s", hipGetErrorString(e));
+        if ((it & 15) == 15 &&
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > spin_us)
+            break;
         __builtin_ia32_pause();
     }
+    OSG_HIP_CHECK(ctx, hipEventSynchronize(ctx->ev_done));
+    return OSG_OK;
 }
 
 extern "C" {

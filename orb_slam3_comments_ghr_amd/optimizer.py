@@ -502,23 +502,43 @@ def synth_gba_graph(rng, n_kf=120, n_points=20000, bRobust=False, iterations=10,
 
 
 def synth_map_graph(rng, n_kf=1500, n_points=150000, spacing=0.3, k_range=(2, 6), bRobust=False, iterations=10,
-                    stereo_frac=0.0, n_levels=8):
+                    stereo_frac=0.0, n_levels=8, loop=False):
     """A map-scale whole-map BA (GlobalBundleAdjustemnt on a long sequence): n_kf keyframes 'spacing'
     m apart along a 0.45 km path, looking sideways at points 4 .. 6 m away spread along it, so a
     keyframe shares points only with its neighbours (~27 on each side) and the reduced camera
     system is a band, as in an open trajectory without loop closures.  Each point is observed by
     k ~ U{k_range} of the keyframes that see it; pixel noise 1 px * 1.2^octave, pose noise 1 cm /
-    0.3 deg, point noise 2 cm; the first keyframe is fixed (the map's init KeyFrame)."""
+    0.3 deg, point noise 2 cm; the first keyframe is fixed (the map's init KeyFrame).
+
+    loop=True: the same path closed into a circle (radius n_kf spacing / 2 pi, cameras looking
+    outwards at a ring of points), so the last keyframes share points with the first ones — the map
+    LoopClosing hands to GlobalBundleAdjustemnt after closing a loop (ref:src/LoopClosing.cc:2436):
+    the reduced camera system is the band plus the two corner blocks that join its ends."""
     cam = pinhole_camera()
     L = spacing * (n_kf - 1)
     cx = np.arange(n_kf) * spacing
     cy = 0.1 * np.sin(np.arange(n_kf) * 0.05)
     yaw = np.deg2rad(rng.normal(0, 2.0, n_kf))
     Rs = np.stack([np.array([[np.cos(a), 0, -np.sin(a)], [0, 1, 0], [np.sin(a), 0, np.cos(a)]]) for a in yaw])
-    C = np.stack([cx, cy, np.zeros(n_kf)], 1)
+    if loop:
+        Rc = spacing * n_kf / (2 * np.pi)
+        th = 2 * np.pi * np.arange(n_kf) / n_kf
+        # camera axes in world coordinates: x along the tangent, y down (world y), z outwards
+        R0 = np.stack([np.array([[np.sin(a), 0, -np.cos(a)], [0, 1, 0], [np.cos(a), 0, np.sin(a)]]) for a in th])
+        Rs = np.einsum("kij,kjl->kil", Rs, R0)
+        C = np.stack([Rc * np.cos(th), cy, Rc * np.sin(th)], 1)
+    else:
+        C = np.stack([cx, cy, np.zeros(n_kf)], 1)
     ts = -np.einsum("kij,kj->ki", Rs, C)
     P = np.stack([rng.uniform(-1.0, L + 1.0, n_points), rng.uniform(-1.5, 1.5, n_points),
                   rng.uniform(4.0, 6.0, n_points)], 1)
+    if loop:  # the same draws as angle (path position) and distance off the path, on the ring
+        phi = 2 * np.pi * P[:, 0] / (spacing * n_kf)
+        rho = Rc + P[:, 2]
+        P = np.stack([rho * np.cos(phi), P[:, 1], rho * np.sin(phi)], 1)
+        pos = phi / (2 * np.pi) * n_kf   # path position in keyframes
+    else:
+        pos = P[:, 0] / spacing
     isig_tab = inv_level_sigma2(n_levels)
     lev_p = np.array([1.2 ** -i for i in range(n_levels)])
     lev_p /= lev_p.sum()
@@ -526,8 +546,12 @@ def synth_map_graph(rng, n_kf=1500, n_points=150000, spacing=0.3, k_range=(2, 6)
     e_point, e_pose, e_obs, e_kind, e_lev = [], [], [], [], []
     for p0 in range(0, n_points, 20000):
         Pc = P[p0:p0 + 20000]
-        base = np.clip(np.round(Pc[:, 0] / spacing).astype(int) - W, 0, None)
-        cand = np.clip(base[:, None] + np.arange(2 * W + 1)[None, :], 0, n_kf - 1)  # (m, 2W+1)
+        if loop:
+            base = np.round(pos[p0:p0 + 20000]).astype(int) - W
+            cand = (base[:, None] + np.arange(2 * W + 1)[None, :]) % n_kf  # (m, 2W+1)
+        else:
+            base = np.clip(np.round(pos[p0:p0 + 20000]).astype(int) - W, 0, None)
+            cand = np.clip(base[:, None] + np.arange(2 * W + 1)[None, :], 0, n_kf - 1)  # (m, 2W+1)
         Xc = np.einsum("mkij,mj->mki", Rs[cand], Pc) + ts[cand]
         u = EUROC_FX * Xc[..., 0] / Xc[..., 2] + EUROC_CX
         v = EUROC_FY * Xc[..., 1] / Xc[..., 2] + EUROC_CY

@@ -280,3 +280,22 @@ def test_batch_bow(ctx, oracle, kf2):
     for b, (A, Bs) in enumerate(pairs):
         ref = (oc.bow_kf_kf if kf2 else oc.bow_kf_f)(oracle, A, Bs, 0.75, True)
         assert_same(f"bow batch [{b}]", int(nm[b]), outs[b], *ref)
+
+
+def test_pinned_staging_reused_back_to_back(ctx, oracle):
+    """The pinned staging block is rewritten at the same offsets by consecutive calls (uploads and
+    downloads by copy kernels over PCIe): alternating different frames through one context, every
+    call must see its own inputs and return its own results (no stale line from the previous call)."""
+    rng = np.random.default_rng(4242)
+    cases = []
+    for k in range(4):
+        F = fr.synth_frame(rng, n=600, stereo=(k % 2 == 0))
+        Q = fr.synth_mp_queries(rng, F, m=900)
+        slot_mp, taken = fr.synth_slots(rng, F.n)
+        cases.append((F, Q, slot_mp, taken, oc.mps(oracle, F, Q, 0.8, 3.0, False, 20.0, slot_mp, taken)))
+    m = ORBmatcher(ctx, 0.8)
+    for rep in range(3):
+        for i, (F, Q, slot_mp, taken, ref) in enumerate(cases):
+            s = slot_mp.copy()
+            n = m.SearchByProjection(F, Q, 3.0, False, 20.0, slot_mp=s, slot_taken=taken)
+            assert_same(f"rep {rep} case {i}", n, s, *ref)
