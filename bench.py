@@ -388,6 +388,7 @@ def main():
         stage("global_ba", bench_gba)
         if not args.no_gba_map:
             stage("global_ba_map", bench_gba_map)
+            stage("global_ba_loop", lambda *a: bench_gba_map(*a, loop=True))
 
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -649,16 +650,23 @@ def bench_gba(ctx, rank, world, dist, dev, args):
     return res
 
 
-def bench_gba_map(ctx, rank, world, dist, dev, args):
+def bench_gba_map(ctx, rank, world, dist, dev, args, loop=False):
     """SURVEY.md §8(f) rank 4 at map scale: BundleAdjustment over a 1500-KeyFrame x 150 k-point map
     (optimizer.synth_map_graph: an open 0.45 km path, 600 k edges, reduced system n = 8994, banded).
     Wall time of the whole call per map.  The CPU baseline is the oracle on one thread: g2o's LM is
-    single-threaded, so more cores do not speed up one map (they only run more maps)."""
+    single-threaded, so more cores do not speed up one map (they only run more maps).
+    loop=True (global_ba_loop): the same map closed into a loop (synth_map_graph(loop=True)), the global
+    BA LoopClosing starts after a loop closure (ref:src/LoopClosing.cc:2436); device memory the call
+    holds (the context's arena after the call, hipMemGetInfo) is reported as peak_device_bytes."""
     import torch
     from orb_slam3_comments_ghr_amd import optimizer as op
-    G = op.synth_map_graph(np.random.default_rng(0x0B5EED31 + rank), n_kf=1500, n_points=150000)
+    G = op.synth_map_graph(np.random.default_rng(0x0B5EED31 + rank), n_kf=1500, n_points=150000, loop=loop)
     opt = op.Optimizer(ctx)
+    torch.cuda.synchronize(dev)
+    free0 = torch.cuda.mem_get_info(dev)[0]
     r = opt.BundleAdjustment(G)
+    torch.cuda.synchronize(dev)
+    held = free0 - torch.cuda.mem_get_info(dev)[0]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -675,7 +683,12 @@ def bench_gba_map(ctx, rank, world, dist, dev, args):
     res = {"metric": "GlobalBA iters/s", "value": round(iters / el, 1), "unit": "LM iterations/s",
            "s_per_gba": round(el / reps, 3), "iterations_per_gba": r.iterations, "trials_per_gba": r.trials,
            "workload": f"global BA at map scale: {len(G.pose)} KF x {len(G.point)} points x {len(G.e_point)} edges, "
-                       f"reduced system {6 * n_free} (banded: an open trajectory), optimize({G.iterations}), no Huber",
+                       f"reduced system {6 * n_free} ("
+                       + ("a loop-closed map: the band plus its corner blocks" if loop else "banded: an open trajectory")
+                       + f"), optimize({G.iterations}), no Huber",
+           "peak_device_bytes": int(held),
+           "peak_device_note": "device memory the context holds after the first call (hipMemGetInfo delta): the "
+                               "arena grows to the call's peak and stays; includes the dense n x n reduced matrix",
            "n_gpus": world, "dtype": "f64", "scaling": "weak", "parallelism": f"replicas x{world} (one map per GPU)"}
     if rank == 0 and world == 1 and not args.no_cpu:
         orc, oc = _oracle()
