@@ -539,6 +539,30 @@ int64_t osg_orb_pyramid_layout(int32_t rows, int32_t cols, int32_t n_levels, con
 int osg_orb_pyramid(osg_ctx *ctx, const uint8_t *image, int32_t rows, int32_t cols, int32_t step,
                     int32_t image_on_device, int32_t n_levels, const float *inv_scale_factors, uint8_t *dev_out,
                     int64_t dev_bytes, int32_t blur);
+/* ---- b11: ORBextractor::operator() for a batch of images -------------------------------------------
+ * ref:src/ORBextractor.cc:1553-1690 (operator(): ComputePyramid, ComputeKeyPointsOctTree, the per-level
+ * GaussianBlur, computeOrientation and computeDescriptors) for n_images device images of one size
+ * (d_images, image_stride bytes apart, row step `step`), each image exactly as osg_orb_pyramid ->
+ * osg_orb_detect -> osg_orb_describe(compute_angle = 1) produce it, with a handful of launches for the
+ * whole batch (the pyramid levels, one FAST pass, one cell pass, one angle and one descriptor pass)
+ * and the octrees of all (image, level) pairs on host threads.  Outputs per image b at offset
+ * b * capacity: x, y in level coordinates (KeyPoint::pt before the :1663-1667 level-0 scaling),
+ * angle (degrees), response, size, octave, desc (32 bytes each); counts[b] = image b's keypoints.
+ * Returns the keypoints of all images, or a negative OSG_E_* code. */
+typedef struct osg_orb_extract_params {
+    int32_t n_levels;                      /* nlevels (<= 32) */
+    const float *scale_factors;            /* mvScaleFactor */
+    const float *inv_scale_factors;        /* mvInvScaleFactor */
+    const int32_t *n_features_per_level;   /* mnFeaturesPerLevel */
+    int32_t ini_th_fast, min_th_fast;      /* iniThFAST, minThFAST */
+    const int32_t *pattern;                /* the 512 (x, y) BRIEF points */
+    const int32_t *umax;                   /* 16 entries */
+} osg_orb_extract_params;
+int osg_orb_extract_batch(osg_ctx *ctx, const uint8_t *d_images, int64_t image_stride, int32_t rows, int32_t cols,
+                          int32_t step, int32_t n_images, const osg_orb_extract_params *params, int32_t capacity,
+                          float *x, float *y, float *angle, float *response, float *size, int32_t *octave,
+                          uint8_t *desc, int32_t *counts);
+
 /* Diagnostics: the 7-tap fixed-point kernel (8 fraction bits) osg_orb_pyramid blurs with. */
 void osg_debug_gaussian_kernel7(int32_t *k7);
 

@@ -117,6 +117,13 @@ class OsgStereoFrame(C.Structure):
     ]
 
 
+class OsgOrbExtractParams(C.Structure):
+    _fields_ = [
+        ("n_levels", i32), ("scale_factors", P), ("inv_scale_factors", P), ("n_features_per_level", P),
+        ("ini_th_fast", i32), ("min_th_fast", i32), ("pattern", P), ("umax", P),
+    ]
+
+
 class OsgOrbKeypoints(C.Structure):
     _fields_ = [("n", i32), ("x", P), ("y", P), ("level", P)]
 
@@ -191,7 +198,7 @@ EXPORTS = [
     "osg_search_by_projection_sim3", "osg_search_by_projection_sim3_batch", "osg_search_by_sim3",
     "osg_search_for_initialization", "osg_search_for_initialization_batch",
     "osg_compute_stereo_matches", "osg_compute_stereo_matches_batch", "osg_compute_stereo_fisheye_matches",
-    "osg_orb_describe", "osg_orb_detect",
+    "osg_orb_describe", "osg_orb_detect", "osg_orb_extract_batch",
     "osg_debug_distribute_oct_tree", "osg_orb_pyramid_layout", "osg_orb_pyramid", "osg_debug_gaussian_kernel7",
 ]
 
@@ -275,6 +282,8 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.osg_debug_gaussian_kernel7.restype = None
     lib.osg_orb_describe.argtypes = [vp, C.POINTER(OsgImagePyramid), C.POINTER(OsgImagePyramid),
                                      C.POINTER(OsgOrbKeypoints), vp, vp, i32, vp, vp]
+    lib.osg_orb_extract_batch.argtypes = [vp, vp, C.c_int64, i32, i32, i32, i32, C.POINTER(OsgOrbExtractParams), i32,
+                                          vp, vp, vp, vp, vp, vp, vp, vp]
     lib.osg_compute_distinctive_descriptors.argtypes = [vp, vp, vp, i32, vp]
     lib.osg_compute_distinctive_descriptors_dev.argtypes = [vp, vp, vp, i32, vp]
     lib.osg_search_for_triangulation_batch.argtypes = [vp, vp, vp, vp, i32, C.c_int, C.c_int, C.c_int, vp, vp]

@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -47,6 +48,7 @@ struct FastArgs {
     GLOBAL uint8_t *score[MAX_LEVELS];  // per pixel: (score at min_th, score at ini_th)
     int rows[MAX_LEVELS], cols[MAX_LEVELS], step[MAX_LEVELS];
     int ini_th, min_th;
+    long long img_bstride, score_bstride;  // batch (blockIdx.y = image): bytes between images
 };
 
 struct Cell {
@@ -65,6 +67,8 @@ struct CellArgs {
     float4 *slots;                // (x, y, response, 0) per cell slot range
     float4 *keys;                 // compacted, in cell order
     GLOBAL int32_t *total;
+    long long score_bstride;      // batch (blockIdx.y = image): score planes, count[n_cells], slots /
+    int max_keys;                 // keys [max_keys], total[1] per image
 };
 
 // cornerScore<16> (OpenCV fast_score.cpp) with d[k] = v - circle[k] (circle index k mod 16) works
@@ -104,10 +108,11 @@ __global__ __launch_bounds__(256) void k_fast_score(const FastArgs A)
     const int x = (bl % A.bx[l]) * 64 + (threadIdx.x & 63), y = (bl / A.bx[l]) * 4 + (threadIdx.x >> 6);
     const int rows = A.rows[l], cols = A.cols[l];
     if (x >= cols || y >= rows) return;
+    const long long bi = blockIdx.y;
     uint8_t s_lo = 0, s_hi = 0;
     if (x >= 3 && y >= 3 && x < cols - 3 && y < rows - 3) {
         const int step = A.step[l];
-        GLOBAL const uint8_t *p = A.img[l] + (size_t)y * step + x;
+        GLOBAL const uint8_t *p = A.img[l] + bi * A.img_bstride + (size_t)y * step + x;
         // the circle (x, y) offsets of OpenCV's offsets16, in order
         const int ox[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
         const int oy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
@@ -119,7 +124,7 @@ __global__ __launch_bounds__(256) void k_fast_score(const FastArgs A)
         s_lo = (uint8_t)(s0 >= A.min_th ? s0 : 0);
         s_hi = (uint8_t)(s0 >= A.ini_th ? s0 : 0);
     }
-    GLOBAL uint8_t *o = A.score[l] + 2 * ((size_t)y * cols + x);
+    GLOBAL uint8_t *o = A.score[l] + bi * A.score_bstride + 2 * ((size_t)y * cols + x);
     *(GLOBAL uint16_t *)o = (uint16_t)(s_lo | (s_hi << 8));
 }
 
@@ -128,10 +133,13 @@ __global__ __launch_bounds__(256) void k_fast_cells(const CellArgs A)
 {
     const int c = blockIdx.x;
     if (c >= A.n_cells) return;
+    const long long bi = blockIdx.y;
     const Cell C = A.cells[c];
     const int h = C.r1 - C.r0 - 6, w = C.c1 - C.c0 - 6;  // tested rows / columns of the cell image
     const int cols = A.cols[C.level];
-    GLOBAL const uint16_t *S = (GLOBAL const uint16_t *)A.score[C.level];
+    GLOBAL const uint16_t *S = (GLOBAL const uint16_t *)(A.score[C.level] + bi * A.score_bstride);
+    GLOBAL int32_t *count = A.count + bi * A.n_cells;
+    float4 *slots = A.slots + bi * A.max_keys;
     __shared__ uint16_t s_sc[MAX_T * MAX_T];  // (score at min_th, score at ini_th), zero ring
     __shared__ int s_cnt[4];
     __shared__ int s_total;
@@ -176,7 +184,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const CellArgs A)
         total = count_pass(0);
     }
     if (threadIdx.x == 0) {
-        A.count[c] = total;
+        count[c] = total;
         s_total = 0;
     }
     if (total == 0) return;
@@ -194,7 +202,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const CellArgs A)
         off += __popcll(m & ((1ull << lane) - 1));
         if (k) {
             const int rr = i / w, cc = i - rr * w;
-            A.slots[C.slot + off] = make_float4((float)(cc + 3 + C.dx), (float)(rr + 3 + C.dy), (float)sc, 0.f);
+            slots[C.slot + off] = make_float4((float)(cc + 3 + C.dx), (float)(rr + 3 + C.dy), (float)sc, 0.f);
         }
         __syncthreads();
         if (threadIdx.x == 0) s_total += s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
@@ -208,17 +216,21 @@ __global__ __launch_bounds__(256) void k_cell_gather(const CellArgs A)
 {
     const int c = blockIdx.x;
     if (c >= A.n_cells) return;
+    const long long bi = blockIdx.y;
+    GLOBAL const int32_t *count = A.count + bi * A.n_cells;
     __shared__ int s_part[4];
     int t = 0;
-    for (int i = threadIdx.x; i < c; i += 256) t += A.count[i];
+    for (int i = threadIdx.x; i < c; i += 256) t += count[i];
     for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
     if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = t;
     __syncthreads();
     const int off = s_part[0] + s_part[1] + s_part[2] + s_part[3];
-    const int cnt = A.count[c];
+    const int cnt = count[c];
     const int slot = A.cells[c].slot;
-    for (int i = threadIdx.x; i < cnt; i += 256) A.keys[off + i] = A.slots[slot + i];
-    if (c == A.n_cells - 1 && threadIdx.x == 0) A.total[0] = off + cnt;
+    float4 *keys = A.keys + bi * A.max_keys;
+    const float4 *slots = A.slots + bi * A.max_keys;
+    for (int i = threadIdx.x; i < cnt; i += 256) keys[off + i] = slots[slot + i];
+    if (c == A.n_cells - 1 && threadIdx.x == 0) A.total[bi] = off + cnt;
 }
 
 #include "octree.h"
@@ -229,9 +241,12 @@ struct LevelGeom {
     int minBX, minBY, maxBX, maxBY, cell0, cell1;
 };
 
+// B images (B > 1: device pyramids pyr_bstride bytes apart, image b's levels at P's pointers + b
+// pyr_bstride); image b's keypoints go to x / y / response / size + b cap and level_start + b (L + 1).
+// Returns the keypoints of all images.
 int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th, const int32_t *n_features,
                const float *scale_factors, int cap, float *x, float *y, float *response, float *size,
-               int32_t *level_start)
+               int32_t *level_start, int B = 1, int64_t pyr_bstride = 0)
 {
     if (!ctx) return OSG_E_INVALID;
     static const bool prof = getenv("OSG_ORB_PROFILE") != nullptr;  // host phase times to stderr
@@ -243,6 +258,7 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
                 "pyramid (1 .. %d levels)", MAX_LEVELS);
     OSG_REQUIRE(ctx, n_features && scale_factors && level_start && (cap == 0 || (x && y && response && size)),
                 "null argument");
+    OSG_REQUIRE(ctx, B >= 1 && B <= 65535 && (B == 1 || P->on_device), "batch of %d images (device pyramids only)", B);
     const int L = P->n_levels;
     // cells in the reference's order (:1071-1175); geometry per level
     std::vector<Cell> cells;
@@ -302,7 +318,7 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
             img_off[l] = pk.add(keep.back().data(), keep.back().size());
         }
     }
-    size_t score_bytes = 0;
+    size_t score_bytes = 0;  // one image's score planes
     std::vector<size_t> score_off(L);
     for (int l = 0; l < L; l++) {
         score_off[l] = score_bytes;
@@ -315,16 +331,20 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
         c.slot = (int)max_keys;
         max_keys += (size_t)h * w;
     }
+    max_keys = (max_keys + 15) & ~size_t(15);
+    OSG_REQUIRE(ctx, (size_t)B * max_keys < (size_t(1) << 31), "batch too large");
     const size_t cell_off = pk.add(cells.data(), sizeof(Cell) * cells.size());
     char *din = nullptr, *dsc = nullptr, *dcnt = nullptr, *dkeys = nullptr;
     OSG_ALLOC(ctx, din, SLOT_TMP0, pk.total + 256);
-    OSG_ALLOC(ctx, dsc, SLOT_TMP1, score_bytes + 256);
-    OSG_ALLOC(ctx, dcnt, SLOT_TMP2, sizeof(int32_t) * (nc + 64));
-    OSG_ALLOC(ctx, dkeys, SLOT_TMP3, sizeof(float4) * (2 * max_keys + 2));
+    OSG_ALLOC(ctx, dsc, SLOT_TMP1, score_bytes * B + 256);
+    OSG_ALLOC(ctx, dcnt, SLOT_TMP2, sizeof(int32_t) * ((size_t)nc * B + B + 64));
+    OSG_ALLOC(ctx, dkeys, SLOT_TMP3, sizeof(float4) * (2 * max_keys * B + 2));
     for (int l = 0; l < L; l++) {
         if (!P->on_device) FA.img[l] = (GLOBAL const uint8_t *)(din + img_off[l]);
         FA.score[l] = (GLOBAL uint8_t *)(dsc + score_off[l]);
     }
+    FA.img_bstride = pyr_bstride;
+    FA.score_bstride = (long long)score_bytes;
     CellArgs CA{};
     CA.cells = (const Cell *)(din + cell_off);
     CA.n_cells = nc;
@@ -332,10 +352,12 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
         CA.score[l] = FA.score[l];
         CA.cols[l] = P->cols[l];
     }
+    CA.score_bstride = (long long)score_bytes;
+    CA.max_keys = (int)max_keys;
     CA.count = (GLOBAL int32_t *)dcnt;
     CA.slots = (float4 *)dkeys;
-    CA.keys = (float4 *)dkeys + max_keys + 1;
-    GLOBAL int32_t *d_total = (GLOBAL int32_t *)(dcnt + sizeof(int32_t) * (nc + 32));
+    CA.keys = (float4 *)dkeys + max_keys * B;
+    GLOBAL int32_t *d_total = (GLOBAL int32_t *)(dcnt + sizeof(int32_t) * ((size_t)nc * B + 32));
     CA.total = d_total;
     // flattened score grid: the levels' 64 x 4 pixel blocks one after another
     FA.n_levels = L;
@@ -344,36 +366,40 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
         FA.bx[l] = (P->cols[l] + 63) / 64;
         FA.block0[l + 1] = FA.block0[l] + FA.bx[l] * ((P->rows[l] + 3) / 4);
     }
-    // pinned: inputs, then the total (and later the keys)
-    char *pin = (char *)osg_pinned(ctx, pk.total + 256 + sizeof(float4) * (max_keys + 1) + 256);
+    // pinned: inputs, then the totals and counts, then the keys
+    const size_t in_pad = (pk.total + 255) & ~size_t(255);
+    const size_t cnt_pad = (sizeof(int32_t) * ((size_t)nc * B + B) + 255) & ~size_t(255);
+    char *pin = (char *)osg_pinned(ctx, in_pad + cnt_pad + sizeof(float4) * (max_keys * B + 1) + 256);
     if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
     OSG_RC(osg_idle(ctx));  // the pinned block may still be in use
     pk.fill_parallel(pin, 8);
-    char *pin_out = pin + ((pk.total + 255) & ~size_t(255));
+    int32_t *pin_tot = (int32_t *)(pin + in_pad);                 // B totals
+    int32_t *pin_cnt = pin_tot + B;                                // B x nc counts
+    char *pin_keys = pin + in_pad + cnt_pad;                       // image b's keys at b max_keys
     hipEvent_t *ev = osg_ctx_events(ctx);
     if (!ev) return osg_set_error(ctx, OSG_E_HIP, "event create failed");
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(din, pin, pk.total, hipMemcpyHostToDevice, ctx->stream));
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[0], ctx->stream));
-    hipLaunchKernelGGL(k_fast_score, dim3(FA.block0[L]), dim3(256), 0, ctx->stream, FA);
+    hipLaunchKernelGGL(k_fast_score, dim3(FA.block0[L], B), dim3(256), 0, ctx->stream, FA);
     if (nc > 0) {
-        hipLaunchKernelGGL(k_fast_cells, dim3(nc), dim3(256), 0, ctx->stream, CA);
-        hipLaunchKernelGGL(k_cell_gather, dim3(nc), dim3(256), 0, ctx->stream, CA);
+        hipLaunchKernelGGL(k_fast_cells, dim3(nc, B), dim3(256), 0, ctx->stream, CA);
+        hipLaunchKernelGGL(k_cell_gather, dim3(nc, B), dim3(256), 0, ctx->stream, CA);
     }
     OSG_HIP_CHECK(ctx, hipGetLastError());
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
-    int32_t total = 0;
-    std::vector<int32_t> offs(nc + 1, 0);
+    std::vector<int32_t> tot(B, 0);
     if (nc > 0) {
-        OSG_RC(osg_download(ctx, pin_out, (const void *)d_total, sizeof(int32_t)));
+        OSG_RC(osg_download(ctx, pin_tot, (const void *)d_total, sizeof(int32_t) * B));
+        OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_cnt, dcnt, sizeof(int32_t) * (size_t)nc * B, hipMemcpyDeviceToHost,
+                                          ctx->stream));
         OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));  // (a polled wait measured slower here)
-        total = *(int32_t *)pin_out;
-        OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_out, CA.keys, sizeof(float4) * (size_t)total, hipMemcpyDeviceToHost,
-                                          ctx->stream));
-        OSG_HIP_CHECK(ctx, hipMemcpyAsync(offs.data() + 1, dcnt, sizeof(int32_t) * nc, hipMemcpyDeviceToHost,
-                                          ctx->stream));
+        for (int b = 0; b < B; b++) tot[b] = pin_tot[b];
+        for (int b = 0; b < B; b++)
+            if (tot[b] > 0)
+                OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_keys + sizeof(float4) * max_keys * b, CA.keys + max_keys * b,
+                                                  sizeof(float4) * (size_t)tot[b], hipMemcpyDeviceToHost, ctx->stream));
     }
     OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));  // (a polled wait measured slower here)
-    for (int c = 0; c < nc; c++) offs[c + 1] += offs[c];  // counts -> offsets
     const double t_gpu = ms_since(tp0);
     const auto tp1 = std::chrono::steady_clock::now();
     float ms = 0.f;
@@ -382,58 +408,97 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
     // the keypoints leave the pinned staging block once: the tree walk reads each of them several
     // times, from ordinary cached memory
     thread_local std::vector<Key4> hkeys;
-    hkeys.resize((size_t)total + 1);
-    std::memcpy(hkeys.data(), pin_out, sizeof(Key4) * (size_t)total);
-    const Key4 *keys = hkeys.data();
-    const double t_copy = ms_since(tp1);
-    // DistributeOctTree per level over that level's cells' keypoints (:1180-1196); the levels are
-    // independent, so very large frames spread them over a few host threads (contiguous level ranges
-    // of about equal keypoint counts; a thread started per call pays its tree buffers' page faults,
-    // so an EuRoC frame's ~12k FAST keypoints stay on the calling thread)
-    std::vector<std::vector<Key4>> kept(L);
-    auto run_levels = [&](int l0, int l1) {
-        for (int l = l0; l < l1; l++) {
-            const LevelGeom &g = lg[l];
-            const int k0 = offs[g.cell0], k1 = offs[g.cell1];
-            distribute_oct_tree(keys + k0, k1 - k0, g.minBX, g.maxBX, g.minBY, g.maxBY, n_features[l], kept[l]);
-        }
-    };
-    const int nthr = total > 60000 ? std::min(L, 3) : 1;
-    if (nthr <= 1) {
-        run_levels(0, L);
-    } else {
-        std::vector<int> cut(nthr + 1, L);
-        cut[0] = 0;
-        for (int t = 1, l = 0; t < nthr; t++) {  // level ranges of ~total / nthr keypoints
-            while (l < L && offs[lg[l].cell1] < (int64_t)total * t / nthr) l++;
-            cut[t] = std::max(cut[t - 1] + 1, std::min(l + 1, L - (nthr - t)));
-        }
-        std::vector<std::thread> th;
-        for (int t = 1; t < nthr; t++) th.emplace_back(run_levels, cut[t], cut[t + 1]);
-        run_levels(cut[0], cut[1]);
-        for (auto &x : th) x.join();
+    thread_local std::vector<int32_t> hoffs;
+    size_t ntot = 0;
+    for (int b = 0; b < B; b++) ntot += (size_t)tot[b];
+    hkeys.resize(ntot + 1);
+    hoffs.assign((size_t)B * (nc + 1), 0);
+    std::vector<size_t> kbase(B + 1, 0);
+    for (int b = 0; b < B; b++) {
+        kbase[b + 1] = kbase[b] + (size_t)tot[b];
+        if (tot[b] > 0) std::memcpy(hkeys.data() + kbase[b], pin_keys + sizeof(float4) * max_keys * b, sizeof(Key4) * tot[b]);
+        int32_t *o = hoffs.data() + (size_t)b * (nc + 1);
+        for (int c = 0; c < nc; c++) o[c + 1] = o[c] + (nc > 0 ? pin_cnt[(size_t)b * nc + c] : 0);  // counts -> offsets
     }
-    int n_out = 0;
-    level_start[0] = 0;
-    for (int l = 0; l < L; l++) {
+    const double t_copy = ms_since(tp1);
+    // DistributeOctTree per (image, level) over that level's cells' keypoints (:1180-1196).  The tasks
+    // are independent: a batch spreads them over host threads; one image keeps its ~12k FAST keypoints
+    // on the calling thread unless the frame is very large (contiguous level ranges of about equal
+    // keypoint counts; a thread started per call pays its tree buffers' page faults)
+    std::vector<std::vector<Key4>> kept((size_t)B * L);
+    // the calling thread's buffers by pointer: inside a lambda run on a worker thread the names
+    // hkeys / hoffs would denote that worker's own (empty) thread_local instances
+    const Key4 *keys_all = hkeys.data();
+    const int32_t *offs_all = hoffs.data();
+    auto run_task = [&](int task) {
+        const int b = task / L, l = task % L;
         const LevelGeom &g = lg[l];
-        const int scaledPatchSize = (int)(PATCH_SIZE * scale_factors[l]);
-        if (n_out + (int)kept[l].size() > cap)
-            return osg_set_error(ctx, OSG_E_INVALID, "keypoint capacity %d exceeded at level %d", cap, l);
-        for (const Key4 &k : kept[l]) {
-            x[n_out] = k.x + g.minBX;
-            y[n_out] = k.y + g.minBY;
-            response[n_out] = k.z;
-            size[n_out] = (float)scaledPatchSize;
-            n_out++;
+        const int32_t *o = offs_all + (size_t)b * (nc + 1);
+        const int k0 = o[g.cell0], k1 = o[g.cell1];
+        distribute_oct_tree(keys_all + kbase[b] + k0, k1 - k0, g.minBX, g.maxBX, g.minBY, g.maxBY, n_features[l],
+                            kept[task]);
+    };
+    const int hw = std::max(1, (int)std::thread::hardware_concurrency());
+    if (B > 1) {
+        const int nthr = std::min(std::min(16, hw), B * L);
+        std::atomic<int> next(0);
+        auto worker = [&]() {
+            for (int t = next++; t < B * L; t = next++) run_task(t);
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < nthr; t++) th.emplace_back(worker);
+        worker();
+        for (auto &t : th) t.join();
+    } else {
+        const int total = tot[0];
+        const int32_t *offs = hoffs.data();
+        auto run_levels = [&](int l0, int l1) {
+            for (int l = l0; l < l1; l++) run_task(l);
+        };
+        const int nthr = total > 60000 ? std::min(L, 3) : 1;
+        if (nthr <= 1) {
+            run_levels(0, L);
+        } else {
+            std::vector<int> cut(nthr + 1, L);
+            cut[0] = 0;
+            for (int t = 1, l = 0; t < nthr; t++) {  // level ranges of ~total / nthr keypoints
+                while (l < L && offs[lg[l].cell1] < (int64_t)total * t / nthr) l++;
+                cut[t] = std::max(cut[t - 1] + 1, std::min(l + 1, L - (nthr - t)));
+            }
+            std::vector<std::thread> th;
+            for (int t = 1; t < nthr; t++) th.emplace_back(run_levels, cut[t], cut[t + 1]);
+            run_levels(cut[0], cut[1]);
+            for (auto &x : th) x.join();
         }
-        level_start[l + 1] = n_out;
+    }
+    int n_all = 0;
+    for (int b = 0; b < B; b++) {
+        int n_out = 0;
+        int32_t *ls = level_start + (size_t)b * (L + 1);
+        const size_t o = (size_t)b * cap;
+        ls[0] = 0;
+        for (int l = 0; l < L; l++) {
+            const LevelGeom &g = lg[l];
+            const std::vector<Key4> &kl = kept[(size_t)b * L + l];
+            const int scaledPatchSize = (int)(PATCH_SIZE * scale_factors[l]);
+            if (n_out + (int)kl.size() > cap)
+                return osg_set_error(ctx, OSG_E_INVALID, "keypoint capacity %d exceeded at level %d (image %d)", cap, l, b);
+            for (const Key4 &k : kl) {
+                x[o + n_out] = k.x + g.minBX;
+                y[o + n_out] = k.y + g.minBY;
+                response[o + n_out] = k.z;
+                size[o + n_out] = (float)scaledPatchSize;
+                n_out++;
+            }
+            ls[l + 1] = n_out;
+        }
+        n_all += n_out;
     }
     if (prof)
-        fprintf(stderr, "[osg orb detect] %d cells, %d FAST keypoints -> %d: setup + GPU + download %.3f ms "
-                        "(kernels %.3f ms), key copy %.3f ms, octree %.3f ms\n", nc, total, n_out, t_gpu, (double)ms, t_copy,
+        fprintf(stderr, "[osg orb detect] %d images x %d cells, %zu FAST keypoints -> %d: setup + GPU + download %.3f ms "
+                        "(kernels %.3f ms), key copy %.3f ms, octree %.3f ms\n", B, nc, ntot, n_all, t_gpu, (double)ms, t_copy,
                 ms_since(tp1) - t_copy);
-    return n_out;
+    return n_all;
 }
 
 }  // namespace
@@ -447,6 +512,15 @@ extern "C" int osg_debug_distribute_oct_tree(const float *keys4, int32_t nk, int
     if ((int)kept.size() > cap) return OSG_E_INVALID;
     std::memcpy(out4, kept.data(), sizeof(Key4) * kept.size());
     return (int)kept.size();
+}
+
+// internal (orb.hip's batched extractor): B device pyramids pyr_bstride bytes apart
+int osg_detect_batch(osg_ctx *ctx, const osg_image_pyramid *raw0, int32_t B, int64_t pyr_bstride, int32_t ini_th_fast,
+                     int32_t min_th_fast, const int32_t *n_features_per_level, const float *scale_factors,
+                     int32_t capacity, float *x, float *y, float *response, float *size, int32_t *level_start)
+{
+    return detect_run(ctx, raw0, ini_th_fast, min_th_fast, n_features_per_level, scale_factors, capacity, x, y,
+                      response, size, level_start, B, pyr_bstride);
 }
 
 extern "C" int osg_orb_detect(osg_ctx *ctx, const osg_image_pyramid *raw, int32_t ini_th_fast, int32_t min_th_fast,

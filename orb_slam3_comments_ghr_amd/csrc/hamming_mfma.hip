@@ -31,9 +31,15 @@
 // rows are expanded (32 B -> 256 B of signed bytes) once per workgroup into LDS chunks of CR rows
 // through a 256-entry byte -> 8-byte table in LDS, double-buffered: while the waves multiply chunk
 // c, the packed rows of chunk c + 1 are already in registers, and are expanded into the other
-// buffer after the chunk's MFMAs.  LDS rows are 256 B with the 16-B granules XOR-swizzled by
-// (row & 15): the 16 rows that one ds_read_b128 of a lane half reads at one granule column land
-// on 16 distinct 16-B bank groups.
+// buffer after the chunk's MFMAs.  LDS rows are 256 B of signed bytes padded to 272 B (MF_RS): the
+// 16 rows that one ds_read_b128 of a lane half reads at one granule column then start 16 B apart
+// modulo the 256-B bank window and land on 16 distinct 16-B bank groups.
+//
+// Full chunks run as one branch-free block pipelined by hand (PIPE = 1): K-step s of tile t issues
+// its MFMAs, refills the A register it consumed with tile t + 1's granule, and performs pair s of
+// tile t - 1's top-2 update, with sched_barrier keeping that order.  Measured: 182.6 us per 256 x
+// 2000^2 launch, 0.57 of the I8 dense peak; the same MFMA chains alone run at 0.72 of it
+// (tools/micro/mfma_i8_rate.hip: the chip holds 18.6 ns per 32x32x32 MFMA per SIMD, not 13.3).
 #include <algorithm>
 #include <cstdlib>
 
@@ -263,13 +269,9 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(const uint32_t *__restric
                     for (int s = 0; s < 8; s++) {
 #pragma unroll
                         for (int j = 0; j < QT; j++) acc[j] = mfma(a[s], bq[j][s], s ? acc[j] : crow);
-                        if (tt + 1 < NTILE && !(PIPE & 4)) a[s] = frag(sb + (tt + 1) * 32 * MF_RS, s);
+                        if (tt + 1 < NTILE) a[s] = frag(sb + (tt + 1) * 32 * MF_RS, s);
 #pragma unroll
                         for (int j = 0; j < QT; j++) {
-                            if (PIPE & 2) {   // timing experiment: minimal update (results invalid)
-                                if (s == 0) ka1[j] = min(ka1[j], accp[j][0]);
-                                continue;
-                            }
                             // pair s of the tile's 8 key pairs: chain A elements 0-7, chain B 8-15
                             if (s & 1)
                                 key_push2(kb1[j], kb2[j], accp[j][8 + (s & 6)], accp[j][9 + (s & 6)]);
@@ -303,7 +305,7 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(const uint32_t *__restric
                 tile(sb + nfull * 32 * MF_RS, cin);
             }
         }
-        if (more && !(PIPE & 8)) store_chunk((c + 1) & 1, pw);
+        if (more) store_chunk((c + 1) & 1, pw);
         __syncthreads();
     }
     if (!active) return;
@@ -352,12 +354,6 @@ int osg_launch_top2_batch_mfma(osg_ctx *ctx, const void *d_query, int32_t nq, co
     case 2: return launch<16, 1, 256, 0>(ctx, d_query, nq, d_train, nt, nb, d_out);
     case 3: return launch<8, 2, 256, 0>(ctx, d_query, nq, d_train, nt, nb, d_out);
     case 4: return launch<8, 1, 256, 1>(ctx, d_query, nq, d_train, nt, nb, d_out);
-    // timing experiments (results invalid): 10 no expansion + minimal update, 14 also no A refills,
-    // 12 no A refills, 8 no expansion
-    case 10: return launch<16, 1, 256, 1 | 2 | 8>(ctx, d_query, nq, d_train, nt, nb, d_out);
-    case 14: return launch<16, 1, 256, 1 | 2 | 4 | 8>(ctx, d_query, nq, d_train, nt, nb, d_out);
-    case 12: return launch<16, 1, 256, 1 | 4>(ctx, d_query, nq, d_train, nt, nb, d_out);
-    case 8: return launch<16, 1, 256, 1 | 8>(ctx, d_query, nq, d_train, nt, nb, d_out);
     default: return launch<16, 1, 256, 1>(ctx, d_query, nq, d_train, nt, nb, d_out);
     }
 }

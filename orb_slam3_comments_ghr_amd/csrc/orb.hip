@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstring>
 #include <vector>
 
 #include "match_common.h"
@@ -45,6 +46,8 @@ struct OrbArgs {
     GLOBAL const float *cs;                      // 2n: (cos, sin)
     GLOBAL uint32_t *desc;                       // 8n words = 32n bytes
     GLOBAL int32_t *bad;                         // keypoints that read outside their level's buffer
+    GLOBAL const int32_t *img;                   // batch: per keypoint its image (null: image 0)
+    long long raw_bstride, blur_bstride;         // batch: bytes between the images' levels
 };
 
 __device__ __forceinline__ float fast_atan2(float y, float x)
@@ -77,7 +80,8 @@ __global__ __launch_bounds__(256) void k_orb_angle(const OrbArgs A)
     const int l = A.level[k];
     const int cx = (int)rintf(A.x[k]), cy = (int)rintf(A.y[k]);
     const int step = A.raw_step[l];
-    GLOBAL const uint8_t *c = A.raw[l] + (size_t)cy * step + cx;
+    const long long bi = A.img ? A.img[k] : 0;
+    GLOBAL const uint8_t *c = A.raw[l] + bi * A.raw_bstride + (size_t)cy * step + cx;
     // every read of the +-15 box is in bounds (checked on the host), so all 31 loads of a lane are
     // issued unconditionally and masked; lanes 31..63 read the centre column with weight 0
     const bool act = lane <= 2 * HALF_PATCH;
@@ -115,7 +119,7 @@ __global__ __launch_bounds__(256) void k_orb_desc(const OrbArgs A)
     const int cols = A.blur_cols[l];
     const long long size = (long long)A.blur_rows[l] * cols;
     const long long c0 = (long long)cy * cols + cx;
-    GLOBAL const uint8_t *img = A.blur[l];
+    GLOBAL const uint8_t *img = A.blur[l] + (A.img ? A.img[k] : 0) * A.blur_bstride;
     uint32_t val = 0;
     bool bad = false;
 #pragma unroll
@@ -191,8 +195,11 @@ void add_levels(osg_packer &pk, const osg_image_pyramid *P, int n_levels, std::v
     }
 }
 
+// kimg (batch): per keypoint its image, whose device levels lie at raw / blurred's pointers + image x
+// raw_bstride / blur_bstride
 int orb_run(osg_ctx *ctx, const osg_image_pyramid *raw, const osg_image_pyramid *blurred, const osg_orb_keypoints *K,
-            const int32_t *pattern, const int32_t *umax, int compute_angle, float *angle, uint8_t *desc)
+            const int32_t *pattern, const int32_t *umax, int compute_angle, float *angle, uint8_t *desc,
+            const int32_t *kimg = nullptr, int64_t raw_bstride = 0, int64_t blur_bstride = 0)
 {
     if (!ctx) return OSG_E_INVALID;
     OSG_REQUIRE(ctx, K && K->n >= 0, "keypoints");
@@ -239,6 +246,12 @@ int orb_run(osg_ctx *ctx, const osg_image_pyramid *raw, const osg_image_pyramid 
     set_off(A.x, pk.add(K->x, sizeof(float) * n));
     set_off(A.y, pk.add(K->y, sizeof(float) * n));
     set_off(A.level, pk.add(K->level, sizeof(int32_t) * n));
+    if (kimg) {
+        OSG_REQUIRE(ctx, raw->on_device && blurred->on_device, "batched keypoints need device pyramids");
+        set_off(A.img, pk.add(kimg, sizeof(int32_t) * n));
+        A.raw_bstride = raw_bstride;
+        A.blur_bstride = blur_bstride;
+    }
     set_off(A.pattern, pk.add(pattern, sizeof(int32_t) * 2 * NPOINTS));
     const size_t in_bytes = (pk.total + 255) & ~size_t(255);
     // outputs / exchange: angle n | cs 2n | bad 1 (256-aligned) | desc 32n
@@ -257,6 +270,7 @@ int orb_run(osg_ctx *ctx, const osg_image_pyramid *raw, const osg_image_pyramid 
     relocate(A.x, dev_in);
     relocate(A.y, dev_in);
     relocate(A.level, dev_in);
+    relocate(A.img, dev_in);
     relocate(A.pattern, dev_in);
     for (int l = 0; l < n_levels; l++) {
         if (compute_angle && !raw->on_device) relocate(A.raw[l], dev_in);
@@ -309,6 +323,74 @@ int orb_run(osg_ctx *ctx, const osg_image_pyramid *raw, const osg_image_pyramid 
 }  // namespace
 
 extern "C" {
+
+// ORBextractor::operator() for B images: osg_pyramid_batch -> osg_detect_batch -> the batched
+// describe (orb_run with per-keypoint images).  Same results as the three per-image calls.
+int osg_orb_extract_batch(osg_ctx *ctx, const uint8_t *d_images, int64_t image_stride, int32_t rows, int32_t cols,
+                          int32_t step, int32_t n_images, const osg_orb_extract_params *P, int32_t capacity, float *x,
+                          float *y, float *angle, float *response, float *size, int32_t *octave, uint8_t *desc,
+                          int32_t *counts)
+{
+    if (!ctx) return OSG_E_INVALID;
+    OSG_REQUIRE(ctx, n_images >= 0 && n_images <= 65535, "n_images = %d", n_images);
+    if (n_images == 0) return 0;
+    OSG_REQUIRE(ctx, d_images && P && P->scale_factors && P->inv_scale_factors && P->n_features_per_level &&
+                         P->pattern && P->umax && counts && capacity >= 0,
+                "null argument");
+    OSG_REQUIRE(ctx, capacity == 0 || (x && y && angle && response && size && octave && desc), "null output");
+    OSG_REQUIRE(ctx, step >= cols && image_stride >= (int64_t)step * rows, "image step / stride");
+    const int L = P->n_levels;
+    OSG_REQUIRE(ctx, L >= 1 && L <= MAX_LEVELS, "n_levels = %d", L);
+    int32_t lr[MAX_LEVELS], lc[MAX_LEVELS];
+    int64_t bo[MAX_LEVELS], bl[MAX_LEVELS];
+    const int64_t total = osg_orb_pyramid_layout(rows, cols, L, P->inv_scale_factors, lr, lc, bo, bl);
+    OSG_REQUIRE(ctx, total > 0, "pyramid layout");
+    const int64_t pstride = (total + 4095) & ~(int64_t)4095;
+    uint8_t *pyr = nullptr;
+    OSG_ALLOC(ctx, pyr, SLOT_TMP8, (size_t)pstride * n_images);
+    OSG_RC(osg_pyramid_batch(ctx, d_images, image_stride, rows, cols, step, n_images, L, P->inv_scale_factors, pyr,
+                             pstride, pstride * n_images));
+    const uint8_t *rawp[MAX_LEVELS], *blp[MAX_LEVELS];
+    int32_t rstep[MAX_LEVELS], bstep[MAX_LEVELS];
+    for (int l = 0; l < L; l++) {
+        rstep[l] = lc[l] + 38;
+        rawp[l] = pyr + bo[l] + (int64_t)19 * rstep[l] + 19;
+        bstep[l] = lc[l];
+        blp[l] = pyr + bl[l];
+    }
+    const osg_image_pyramid raw0 = {L, 1, rawp, lr, lc, rstep};
+    const osg_image_pyramid blur0 = {L, 1, blp, lr, lc, bstep};
+    std::vector<int32_t> ls((size_t)n_images * (L + 1));
+    const int n = osg_detect_batch(ctx, &raw0, n_images, pstride, P->ini_th_fast, P->min_th_fast,
+                                   P->n_features_per_level, P->scale_factors, capacity, x, y, response, size, ls.data());
+    if (n < 0) return n;
+    // all images' keypoints in one list for the describe kernels, with their image and level
+    std::vector<float> kx(n), ky(n), ka(n);
+    std::vector<int32_t> kl(n), ki(n);
+    std::vector<uint8_t> kd((size_t)n * 32);
+    for (int b = 0, q = 0; b < n_images; b++) {
+        const int32_t *lsb = ls.data() + (size_t)b * (L + 1);
+        counts[b] = lsb[L];
+        for (int l = 0; l < L; l++)
+            for (int i = lsb[l]; i < lsb[l + 1]; i++, q++) {
+                kx[q] = x[(size_t)b * capacity + i];
+                ky[q] = y[(size_t)b * capacity + i];
+                kl[q] = l;
+                ki[q] = b;
+                octave[(size_t)b * capacity + i] = l;
+            }
+    }
+    const osg_orb_keypoints K = {n, kx.data(), ky.data(), kl.data()};
+    const int rc = orb_run(ctx, &raw0, &blur0, &K, P->pattern, P->umax, 1, ka.data(), kd.data(), ki.data(), pstride,
+                           pstride);
+    if (rc < 0) return rc;
+    for (int b = 0, q = 0; b < n_images; b++)
+        for (int i = 0; i < counts[b]; i++, q++) {
+            angle[(size_t)b * capacity + i] = ka[q];
+            std::memcpy(desc + ((size_t)b * capacity + i) * 32, kd.data() + (size_t)q * 32, 32);
+        }
+    return n;
+}
 
 int osg_orb_describe(osg_ctx *ctx, const osg_image_pyramid *raw, const osg_image_pyramid *blurred,
                      const osg_orb_keypoints *K, const int32_t *pattern, const int32_t *umax, int32_t compute_angle,

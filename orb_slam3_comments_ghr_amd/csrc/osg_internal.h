@@ -106,3 +106,10 @@ int osg_launch_top2(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d
 int osg_top2_mfma_max_rows();
 int osg_launch_top2_batch_mfma(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d_train, int32_t nt,
                                int32_t nb, void *d_out);
+// the batched ORB extractor's stages (pyramid.hip, fast.hip), called by osg_orb_extract_batch (orb.hip)
+int osg_pyramid_batch(osg_ctx *ctx, const uint8_t *d_images, int64_t img_bstride, int32_t rows, int32_t cols,
+                      int32_t step, int32_t B, int32_t n_levels, const float *inv_scale, uint8_t *dev_out,
+                      int64_t out_bstride, int64_t dev_bytes);
+int osg_detect_batch(osg_ctx *ctx, const osg_image_pyramid *raw0, int32_t B, int64_t pyr_bstride, int32_t ini_th_fast,
+                     int32_t min_th_fast, const int32_t *n_features_per_level, const float *scale_factors,
+                     int32_t capacity, float *x, float *y, float *response, float *size, int32_t *level_start);

@@ -50,6 +50,7 @@ struct LevelArgs {
     const int4 *yt;             // per output row: r0, r1, beta0, beta1
     int xv;                     // columns of the vector loop (rounding of the vertical pass)
     int copy;                   // level 0
+    long long src_bstride, dst_bstride;  // batch (blockIdx.z = image): bytes between images' src / dst
 };
 
 __global__ __launch_bounds__(256) void k_pyr_level(const LevelArgs A)
@@ -58,13 +59,14 @@ __global__ __launch_bounds__(256) void k_pyr_level(const LevelArgs A)
     const int by = blockIdx.y * 4 + (threadIdx.x >> 6);
     if (bx >= A.w + 2 * EDGE || by >= A.h + 2 * EDGE) return;
     const int x = reflect101(bx - EDGE, A.w), y = reflect101(by - EDGE, A.h);
+    GLOBAL const uint8_t *src = A.src + (long long)blockIdx.z * A.src_bstride;
     int v;
     if (A.copy) {
-        v = A.src[(long long)y * A.sstep + x];
+        v = src[(long long)y * A.sstep + x];
     } else {
         const int4 X = A.xt[x], Y = A.yt[y];
-        GLOBAL const uint8_t *S0 = A.src + (long long)Y.x * A.sstep;
-        GLOBAL const uint8_t *S1 = A.src + (long long)Y.y * A.sstep;
+        GLOBAL const uint8_t *S0 = src + (long long)Y.x * A.sstep;
+        GLOBAL const uint8_t *S1 = src + (long long)Y.y * A.sstep;
         const int d0 = S0[X.x] * X.z + S0[X.y] * X.w;  // HResizeLinear: exact int
         const int d1 = S1[X.x] * X.z + S1[X.y] * X.w;
         if (x < A.xv)  // VResizeLinearVec_32s8u: mulhi of (d >> 4) by the weight, (+2) >> 2
@@ -73,7 +75,7 @@ __global__ __launch_bounds__(256) void k_pyr_level(const LevelArgs A)
             v = (d0 * Y.z + d1 * Y.w + (1 << 21)) >> 22;
         v = v < 0 ? 0 : v > 255 ? 255 : v;
     }
-    A.dst[(long long)by * A.bstep + bx] = (uint8_t)v;
+    A.dst[(long long)blockIdx.z * A.dst_bstride + (long long)by * A.bstep + bx] = (uint8_t)v;
 }
 
 struct BlurArgs {
@@ -83,6 +85,7 @@ struct BlurArgs {
     GLOBAL uint8_t *out[MAX_LEVELS];
     int w[MAX_LEVELS], h[MAX_LEVELS], bstep[MAX_LEVELS];
     int tiles_x[MAX_LEVELS], block0[MAX_LEVELS + 1];
+    long long bstride;  // batch (blockIdx.y = image): bytes between the images' pyramid buffers
 };
 
 __global__ __launch_bounds__(256) void k_pyr_blur(const BlurArgs A)
@@ -95,7 +98,7 @@ __global__ __launch_bounds__(256) void k_pyr_blur(const BlurArgs A)
     const int b = blockIdx.x - A.block0[l];
     const int w = A.w[l], h = A.h[l], bstep = A.bstep[l];
     const int tx0 = (b % A.tiles_x[l]) * BT_W, ty0 = (b / A.tiles_x[l]) * BT_H;
-    GLOBAL const uint8_t *roi = A.roi[l];
+    GLOBAL const uint8_t *roi = A.roi[l] + (long long)blockIdx.y * A.bstride;
     for (int i = threadIdx.x; i < SH * SW; i += 256) {
         const int r = i / SW, c = i - r * SW;
         const int y = reflect101(ty0 + r - KR, h), x = reflect101(tx0 + c - KR, w);
@@ -117,7 +120,7 @@ __global__ __launch_bounds__(256) void k_pyr_blur(const BlurArgs A)
         uint32_t s = 0;
 #pragma unroll
         for (int j = 0; j <= 2 * KR; j++) s += (uint32_t)s_h[r + j][c] * (uint32_t)A.k[j];
-        A.out[l][(long long)y * w + x] = (uint8_t)((s + (1u << 15)) >> 16);
+        A.out[l][(long long)blockIdx.y * A.bstride + (long long)y * w + x] = (uint8_t)((s + (1u << 15)) >> 16);
     }
 }
 
@@ -303,18 +306,25 @@ int64_t layout(int32_t rows, int32_t cols, int32_t n_levels, const float *inv_sc
     return at;
 }
 
+// B images (B > 1: device images img_bstride bytes apart, pyramids out_bstride bytes apart in dev_out,
+// the level-wise launches with the image in the grid's last dimension)
 int pyramid_run(osg_ctx *ctx, const uint8_t *image, int32_t rows, int32_t cols, int32_t step, int32_t on_device,
-                int32_t n_levels, const float *inv_scale, uint8_t *dev_out, int64_t dev_bytes, int32_t blur)
+                int32_t n_levels, const float *inv_scale, uint8_t *dev_out, int64_t dev_bytes, int32_t blur,
+                int32_t B = 1, int64_t img_bstride = 0, int64_t out_bstride = 0)
 {
     if (!ctx) return OSG_E_INVALID;
+    OSG_REQUIRE(ctx, B >= 1 && B <= 65535 && (B == 1 || on_device), "batch of %d images (device images only)", B);
     OSG_REQUIRE(ctx, image && dev_out && step >= cols, "null argument or step < cols");
     int32_t lr[MAX_LEVELS], lc[MAX_LEVELS];
     int64_t bo[MAX_LEVELS], bl[MAX_LEVELS];
     const int64_t total = layout(rows, cols, n_levels, inv_scale, lr, lc, bo, bl);
     OSG_REQUIRE(ctx, total > 0, "pyramid layout (%d x %d, %d levels; 0 < mvInvScaleFactor <= 1)", cols, rows,
                 n_levels);
-    OSG_REQUIRE(ctx, dev_bytes >= (blur ? total : bl[0]), "output buffer of %lld bytes, %lld needed",
-                (long long)dev_bytes, (long long)(blur ? total : bl[0]));
+    OSG_REQUIRE(ctx, B == 1 || out_bstride >= total, "pyramid stride %lld < %lld bytes", (long long)out_bstride,
+                (long long)total);
+    const int64_t need = (int64_t)(B - 1) * out_bstride + (blur ? total : bl[0]);
+    OSG_REQUIRE(ctx, dev_bytes >= need, "output buffer of %lld bytes, %lld needed", (long long)dev_bytes,
+                (long long)need);
     osg_packer pk;
     std::vector<uint8_t> packed;
     size_t img_off = SIZE_MAX;
@@ -340,7 +350,7 @@ int pyramid_run(osg_ctx *ctx, const uint8_t *image, int32_t rows, int32_t cols, 
     const bool levelwise = fz ? atoi(fz) == 0 : !PYR_FUSED_DEFAULT;
     const char *gz = getenv("OSG_PYR_GROUP");
     const int grp = gz ? std::min(GROUP, std::max(1, atoi(gz))) : PYR_GROUP_DEFAULT;
-    const bool fused = !levelwise && n_levels <= GMAX;
+    const bool fused = !levelwise && n_levels <= GMAX && B == 1;
     const int ng = fused ? (n_levels + grp - 1) / grp : 0;
     // the fused launches' descriptors travel in the staging upload and the kernel reads them from HBM:
     // as kernel arguments (~1 KB, indexed by the block's part and level) each dependent read was a
@@ -447,11 +457,14 @@ int pyramid_run(osg_ctx *ctx, const uint8_t *image, int32_t rows, int32_t cols, 
             A.yt = (const int4 *)(din + yo[l]);
             A.xv = vector_columns(lc[l]);
         }
-        const dim3 grid((A.w + 2 * EDGE + 63) / 64, (A.h + 2 * EDGE + 3) / 4);
+        A.src_bstride = l == 0 ? img_bstride : out_bstride;
+        A.dst_bstride = out_bstride;
+        const dim3 grid((A.w + 2 * EDGE + 63) / 64, (A.h + 2 * EDGE + 3) / 4, B);
         hipLaunchKernelGGL(k_pyr_level, grid, dim3(256), 0, ctx->stream, A);
         OSG_HIP_CHECK(ctx, hipGetLastError());
     }
     if (blur) {
+        const int nimg = B;
         BlurArgs B{};
         B.n_levels = n_levels;
         gaussian_kernel7(B.k);
@@ -467,7 +480,8 @@ int pyramid_run(osg_ctx *ctx, const uint8_t *image, int32_t rows, int32_t cols, 
             nb += B.tiles_x[l] * ((lr[l] + BT_H - 1) / BT_H);
         }
         B.block0[n_levels] = nb;
-        hipLaunchKernelGGL(k_pyr_blur, dim3(nb), dim3(256), 0, ctx->stream, B);
+        B.bstride = out_bstride;
+        hipLaunchKernelGGL(k_pyr_blur, dim3(nb, nimg), dim3(256), 0, ctx->stream, B);
         OSG_HIP_CHECK(ctx, hipGetLastError());
     }
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
@@ -479,6 +493,15 @@ int pyramid_run(osg_ctx *ctx, const uint8_t *image, int32_t rows, int32_t cols, 
 }
 
 }  // namespace
+
+// internal (orb.hip's batched extractor): B device images -> B pyramids out_bstride bytes apart
+int osg_pyramid_batch(osg_ctx *ctx, const uint8_t *d_images, int64_t img_bstride, int32_t rows, int32_t cols,
+                      int32_t step, int32_t B, int32_t n_levels, const float *inv_scale, uint8_t *dev_out,
+                      int64_t out_bstride, int64_t dev_bytes)
+{
+    return pyramid_run(ctx, d_images, rows, cols, step, 1, n_levels, inv_scale, dev_out, dev_bytes, 1, B, img_bstride,
+                       out_bstride);
+}
 
 extern "C" {
 

@@ -207,6 +207,64 @@ def ComputePyramid(ctx: Context, image, inv_scale, blur: bool = True, out=None, 
     return OrbPyramid(out, lr, lc, bo, bl, blur)
 
 
+class OrbBatchKeypoints:
+    """What ``ORBExtractBatch`` returns: per-image arrays [B, capacity] (x, y in level coordinates,
+    angle in degrees, response, size, octave) and desc [B, capacity, 32]; image b's keypoints are the
+    first counts[b] of its row, level by level in the reference's order."""
+
+    def __init__(self, counts, x, y, angle, response, size, octave, desc):
+        self.counts, self.x, self.y, self.angle = counts, x, y, angle
+        self.response, self.size, self.octave, self.desc = response, size, octave, desc
+
+    def image(self, b: int):
+        """(x, y, angle, response, size, octave, desc) of image b."""
+        n = int(self.counts[b])
+        return (self.x[b, :n], self.y[b, :n], self.angle[b, :n], self.response[b, :n], self.size[b, :n],
+                self.octave[b, :n], self.desc[b, :n])
+
+    def level_coordinates_to_image(self, scales):
+        """KeyPoint::pt *= mvScaleFactor[octave] for octave > 0 (ref:src/ORBextractor.cc:1663-1667)."""
+        s = np.asarray(scales, np.float32)[self.octave]
+        return self.x * s, self.y * s
+
+
+def ORBExtractBatch(ctx: Context, images, n_features: int = 1000, n_levels: int = 8, factor: float = 1.2,
+                    ini_th: int = 20, min_th: int = 7, pattern=None, umax=None, capacity: int | None = None,
+                    sync: bool = True) -> OrbBatchKeypoints:
+    """ORBextractor::operator() (ref:src/ORBextractor.cc:1553-1690) for a batch of same-size images
+    on the GPU (``osg_orb_extract_batch``, include/osg.h b11): each image's keypoints, angles and
+    descriptors equal ComputePyramid -> ORBDetect -> ORBDescribe on that image alone.
+    images: uint8 torch tensor [B, rows, cols] on the GPU (row stride 1 element apart, any image
+    stride); pattern: ORBextractor::pattern (512 (x, y) points)."""
+    import torch
+
+    assert hasattr(images, "data_ptr") and images.is_cuda and images.dtype == torch.uint8, "device uint8 images"
+    assert images.dim() == 3 and images.stride(2) == 1
+    B, rows, cols = images.shape
+    if sync:
+        torch.cuda.synchronize(images.device)  # the kernels run on the context's own stream
+    scales = scale_factors(n_levels, factor)
+    inv = inv_scale_factors(n_levels, factor)
+    nfl = features_per_level(n_features, n_levels, factor)
+    assert pattern is not None, "ORBextractor::pattern"
+    pattern = np.ascontiguousarray(pattern, np.int32).reshape(-1)
+    assert pattern.size == 1024, "ORBextractor::pattern: 512 (x, y) points"
+    umax = ic_umax() if umax is None else np.ascontiguousarray(umax, np.int32)
+    assert umax.size == HALF_PATCH_SIZE + 1
+    cap = int(capacity if capacity is not None else max(int(nfl.sum()) * 2 + 16, 64))
+    prm = _abi.OsgOrbExtractParams(n_levels, scales.ctypes.data, inv.ctypes.data, nfl.ctypes.data, int(ini_th),
+                                   int(min_th), pattern.ctypes.data, umax.ctypes.data)
+    x, y, ang, resp, size = (np.zeros((B, cap), np.float32) for _ in range(5))
+    octave = np.zeros((B, cap), np.int32)
+    desc = np.zeros((B, cap, 32), np.uint8)
+    counts = np.zeros(B, np.int32)
+    ctx.check(ctx.lib.osg_orb_extract_batch(ctx.handle, images.data_ptr(), images.stride(0), rows, cols,
+                                            images.stride(1), B, C.byref(prm), cap, x.ctypes.data, y.ctypes.data,
+                                            ang.ctypes.data, resp.ctypes.data, size.ctypes.data, octave.ctypes.data,
+                                            desc.ctypes.data, counts.ctypes.data), "osg_orb_extract_batch")
+    return OrbBatchKeypoints(counts, x, y, ang, resp, size, octave, desc)
+
+
 def synth_fast_pyramid(rng, width=752, height=480, n_levels=8, factor=1.2, n_blobs=400):
     """A synthetic image pyramid with FAST corners: a smooth random background plus bright and dark
     rectangles and discs (corners and blobs at every scale), each level a box-filtered 2x2 resample

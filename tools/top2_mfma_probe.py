@@ -48,7 +48,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=256)
     ap.add_argument("--reps", type=int, default=50)
-    ap.add_argument("--shapes", default="0,1,2,3,4,5")
+    ap.add_argument("--shapes", default="0,1,2,3,4")
     a = ap.parse_args()
     ref = "/tmp/_top2_mfma_probe_ref.npy"
     if os.path.exists(ref):
