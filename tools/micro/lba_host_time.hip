@@ -1,0 +1,44 @@
+// Host-only timing of the LBA structure build (ba.hip's build_structure) on graphs handed over
+// from Python: no GPU is touched, so it runs in the build container.
+// Build: hipcc --offload-arch=gfx950 -O3 -shared -fPIC tools/micro/lba_host_time.hip \
+//            -Iinclude -Lorb_slam3_comments_ghr_amd -lorbslam3_amd -o tools/micro/liblba_host_time.so
+#include "../../orb_slam3_comments_ghr_amd/csrc/ba.hip"
+
+extern "C" double lba_host_time_ms(const osg_ba_graph *G, int reps, int *ncontrib)
+{
+    osg_ctx ctx;
+    LbaHost H;
+    double best = 1e30;
+    for (int r = 0; r < reps; r++) {
+        H.reset();
+        const auto t0 = std::chrono::steady_clock::now();
+        if (build_structure(&ctx, G, H) != OSG_OK) return -1;
+        best = std::min(best, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+    *ncontrib = H.pair_start.empty() ? 0 : H.pair_start.back();
+    return best;
+}
+
+// FNV-1a over every structure array of the last build (identity check across rewrites)
+extern "C" unsigned long long lba_host_struct_hash(const osg_ba_graph *G)
+{
+    osg_ctx ctx;
+    LbaHost H;
+    if (build_structure(&ctx, G, H) != OSG_OK) return 0;
+    unsigned long long h = 1469598103934665603ull;
+    auto mix = [&](const std::vector<int32_t> &v) {
+        const unsigned char *p = (const unsigned char *)v.data();
+        for (size_t i = 0; i < v.size() * 4; i++) h = (h ^ p[i]) * 1099511628211ull;
+        h = (h ^ v.size()) * 1099511628211ull;
+    };
+    for (auto *v : {&H.blk_first, &H.blk_last, &H.col_rows_start, &H.col_rows, &H.live_pairs, &H.pose_h, &H.hp_pose,
+                    &H.point_h, &H.hl_point, &H.lm_e_start, &H.lm_e, &H.lg_start, &H.lm_b_start, &H.blk_pose,
+                    &H.edge_blk, &H.blk_lm, &H.hp_e_start, &H.hp_e, &H.hp_b_start, &H.hp_b, &H.pair_start,
+                    &H.pair_ab, &H.chunk_start, &H.pair_chunk, &H.pair_rank, &H.rs_pose, &H.rs_rank0,
+                    &H.rs_chunk_start, &H.rs_chunk, &H.hp_rs_start, &H.rs_order, &H.rs_cdesc, &H.rs_info, &H.hp_b_lm})
+        mix(*v);
+    const int sc[] = {H.np, H.npt, H.ne, H.nhp, H.nhl, H.nblk, H.npairs, H.nchunks, H.ge, H.gl, H.gll, H.gu,
+                      H.nblk_red, H.npart, H.n_rs, H.max_col_rows, (int)H.multi};
+    for (int v : sc) h = (h ^ (unsigned)v) * 1099511628211ull;
+    return h;
+}
