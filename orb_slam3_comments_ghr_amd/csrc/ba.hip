@@ -93,18 +93,15 @@ struct LbaDev {
     const int32_t *blk_pose;             // per block: hessian pose index
     const int32_t *edge_blk;             // per edge: 4 block + 2 (block has several edges) + 1 (not its
                                          // first edge), or -1
-    const int32_t *blk_lm;               // per block: landmark
     const int32_t *hp_e_start, *hp_e;    // edges per hessian pose
-    const int32_t *hp_b_start, *hp_b;    // blocks per hessian pose
-    const int32_t *pair_start;           // dense (i <= j) pairs
-    const int32_t *pair_ab;              // 2 ints per contribution
+    const int32_t *hp_b;                 // blocks per hessian pose (hp_b_start on the host)
+    const int32_t *pair_b;               // per contribution (a, b): its second block b
     int nchunks;
     const int32_t *chunk_start;          // contribution range of each chunk (chunks never span pairs
                                          // or row segments)
     const int32_t *pair_chunk;           // per pair: first chunk (npairs + 1)
     const int32_t *pair_rank;            // per contribution: rank of its first block in pose i's list
     int n_rs;                            // row segments: RS consecutive blocks of one hessian pose
-    const int32_t *rs_pose, *rs_rank0;   // per row segment: pose, first rank
     const int32_t *rs_info;              // k_schur_rows, 8 per workgroup (launch order): row segment,
                                          // pose, first rank, hp_b_start[pose], blocks, chunk range
     const int32_t *hp_b_lm;              // per hp_b entry: the block's landmark
@@ -520,7 +517,7 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__
     // lane q: rank (in the segment) of contribution q's first block, and its second block
     auto contrib = [&](const i4 &d, int &mr, int &mb) {
         mr = lane < d.z ? gbl(D.pair_rank)[d.y + lane] - rb : 0;
-        mb = lane < d.z ? gbl(D.pair_ab)[2 * (d.y + lane) + 1] : 0;
+        mb = lane < d.z ? gbl(D.pair_b)[d.y + lane] : 0;
     };
     // granules of group u0 (contributions u0 .. u0 + cnt - 1) into registers
     auto load_group = [&](int u0, int cnt, int mb, u4 (&R)[3]) {
@@ -584,7 +581,7 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__
             for (int k = 0; k < 9; k++) acc[k] = 0.0;
             for (int qq = q0 + g; qq < q1; qq += 16) {
                 const int rank = D.pair_rank[qq] - rb;
-                const int b = D.pair_ab[2 * qq + 1];
+                const int b = D.pair_b[qq];
                 const double *BD = s_bd + 18 * rank + 3 * r0;  // rows r0..r0+2 of BD_i (6x3)
                 const double *Bj = Hv + 18 * (size_t)b + 3 * c0;  // rows c0..c0+2 of Hpl_j (6x3)
                 double av[9], bv[9];
@@ -1433,7 +1430,7 @@ struct LbaHost {
     int max_col_rows = 0;
     bool trivial = false;  // nothing to optimise: the estimates are returned unchanged
     std::vector<int32_t> pose_h, hp_pose, point_h, hl_point, lm_e_start, lm_e, lg_start, lm_b_start, blk_pose, edge_blk, blk_lm,
-        hp_e_start, hp_e, hp_b_start, hp_b, pair_start, pair_ab, chunk_start, pair_chunk,
+        hp_e_start, hp_e, hp_b_start, hp_b, pair_start, pair_b, chunk_start, pair_chunk,
         pair_rank, rs_pose, rs_rank0, rs_chunk_start, rs_chunk, hp_rs_start, rs_order, rs_cdesc, rs_info, hp_b_lm;
     int n_rs = 0;
     double t_struct = 0;
@@ -1615,7 +1612,12 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
         std::vector<int32_t> fill(H.hp_b_start.begin(), H.hp_b_start.end() - 1);
         for (int b = 0; b < nblk; b++) H.hp_b[fill[H.blk_pose[b]]++] = b;
     }
-    // pose pairs (i <= j), dense index; contributions in landmark order
+    // rank of each block in its pose's block list (hp_b is in block order)
+    std::vector<int32_t> blk_rank(nblk);
+    for (int i = 0; i < nhp; i++)
+        for (int q = H.hp_b_start[i]; q < H.hp_b_start[i + 1]; q++) blk_rank[H.hp_b[q]] = q - H.hp_b_start[i];
+    // pose pairs (i <= j), dense index; contributions (a, b) in landmark order: the device reads b
+    // and the rank of a
     const int npairs = nhp * (nhp + 1) / 2;
     H.npairs = npairs;
     auto pid = [nhp](int i, int j) { return i * nhp - i * (i - 1) / 2 + (j - i); };
@@ -1624,15 +1626,17 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
         for (int a = H.lm_b_start[l]; a < H.lm_b_start[l + 1]; a++)
             for (int b = a; b < H.lm_b_start[l + 1]; b++) H.pair_start[pid(H.blk_pose[a], H.blk_pose[b]) + 1]++;
     for (int k = 0; k < npairs; k++) H.pair_start[k + 1] += H.pair_start[k];
-    H.pair_ab.assign(2 * (size_t)std::max(H.pair_start[npairs], 1), 0);
+    const size_t ncontrib = (size_t)H.pair_start[npairs];
+    H.pair_b.assign(std::max<size_t>(ncontrib, 1), 0);
+    H.pair_rank.assign(std::max<size_t>(ncontrib, 1), 0);
     {
         std::vector<int32_t> fill(H.pair_start.begin(), H.pair_start.end() - 1);
         for (int l = 0; l < nhl; l++)
             for (int a = H.lm_b_start[l]; a < H.lm_b_start[l + 1]; a++)
                 for (int b = a; b < H.lm_b_start[l + 1]; b++) {
                     const int k = fill[pid(H.blk_pose[a], H.blk_pose[b])]++;
-                    H.pair_ab[2 * k] = a;
-                    H.pair_ab[2 * k + 1] = b;
+                    H.pair_b[k] = b;
+                    H.pair_rank[k] = blk_rank[a];
                 }
     }
     // envelope of the reduced system (used past CMAX): a pose row's first nonzero pose column is the
@@ -1678,10 +1682,7 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
                 }
         }
     }
-    // rank of each block in its pose's block list (hp_b is in block order); row segments of RS ranks
-    std::vector<int32_t> blk_rank(nblk);
-    for (int i = 0; i < nhp; i++)
-        for (int q = H.hp_b_start[i]; q < H.hp_b_start[i + 1]; q++) blk_rank[H.hp_b[q]] = q - H.hp_b_start[i];
+    // row segments of RS ranks
     H.hp_rs_start.assign(nhp + 1, 0);
     for (int i = 0; i < nhp; i++) {
         const int nb = H.hp_b_start[i + 1] - H.hp_b_start[i];
@@ -1708,9 +1709,6 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
         }
         std::stable_sort(H.rs_order.begin(), H.rs_order.end(), [&](int a, int b) { return key[a] < key[b]; });
     }
-    const size_t ncontrib = (size_t)H.pair_start[npairs];
-    H.pair_rank.assign(std::max<size_t>(ncontrib, 1), 0);
-    for (size_t q = 0; q < ncontrib; q++) H.pair_rank[q] = blk_rank[H.pair_ab[2 * q]];
     // chunks of <= SCH contributions, never spanning two pairs or two row segments; listed per row
     // segment (pair order, then contribution order)
     H.pair_chunk.assign(npairs + 1, 0);
@@ -1876,27 +1874,16 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     if ((int)H.size() < B) H.resize(B);
     for (int b = 0; b < B; b++) H[b].reset();
     std::vector<int> rcs(B, OSG_OK);
-    {
-        auto work = [&](int b0, int b1) {
-            for (int b = b0; b < b1; b++) {
-                H[b].G = &graphs[b];
-                H[b].R = &results[b];
-                if (graphs[b].n_edges == 0) {
-                    H[b].trivial = true;
-                    continue;
-                }
-                rcs[b] = build_structure(ctx, &graphs[b], H[b]);
-            }
-        };
-        const int nthr = std::min<int>(B, std::max(1, std::min<int>(16, (int)std::thread::hardware_concurrency())));
-        if (nthr <= 1) {
-            work(0, B);
-        } else {
-            std::vector<std::thread> th;
-            const int per = (B + nthr - 1) / nthr;
-            for (int t = 0; t < nthr; t++) th.emplace_back(work, std::min(B, t * per), std::min(B, (t + 1) * per));
-            for (auto &t : th) t.join();
+    osg_parallel_for(B, 16, [&](int b) {
+        H[b].G = &graphs[b];
+        H[b].R = &results[b];
+        if (graphs[b].n_edges == 0) {
+            H[b].trivial = true;
+            return;
         }
+        rcs[b] = build_structure(ctx, &graphs[b], H[b]);
+    });
+    {
         for (int b = 0; b < B; b++)
             if (rcs[b] < 0)
                 return B > 1 ? osg_set_error(ctx, rcs[b], "graph %d: structure", b) : rcs[b];
@@ -1911,8 +1898,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     osg_packer pk;
     struct InOff {
         size_t fixed, epose, epoint, ecam, ekind, eobs, eisig, cams, poseh, hppose, pointh, hlpoint, lmes, lme, lgs, lmbs,
-            blkpose, eblk, hpes, hpe, hpbs, hpb, pairs, pairab, chs, blklm, pch, pose0, point0, erob,
-            prank, rspose, rsrank0, rscs, rsc, hprs, bfirst, blast, rsinfo, hpblm, rscd, crs, cr, live;
+            blkpose, eblk, hpes, hpe, hpb, pairb, chs, pch, pose0, point0, erob,
+            prank, rscs, rsc, hprs, bfirst, blast, rsinfo, hpblm, rscd, crs, cr, live;
     };
     std::vector<InOff> io(NA);
     for (int a = 0; a < NA; a++) {
@@ -1941,12 +1928,9 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         o.eblk = pk.add(h.edge_blk.data(), 4 * (size_t)ne);
         o.hpes = pk.add(h.hp_e_start.data(), 4 * (size_t)(nhp + 1));
         o.hpe = pk.add(h.hp_e.data(), 4 * h.hp_e.size());
-        o.hpbs = pk.add(h.hp_b_start.data(), 4 * (size_t)(nhp + 1));
         o.hpb = pk.add(h.hp_b.data(), 4 * (size_t)nblk);
-        o.pairs = pk.add(h.pair_start.data(), 4 * (size_t)(h.npairs + 1));
-        o.pairab = pk.add(h.pair_ab.data(), 4 * h.pair_ab.size());
+        o.pairb = pk.add(h.pair_b.data(), 4 * h.pair_b.size());
         o.chs = pk.add(h.chunk_start.data(), 4 * h.chunk_start.size());
-        o.blklm = pk.add(h.blk_lm.data(), 4 * (size_t)nblk);
         o.pch = pk.add(h.pair_chunk.data(), 4 * h.pair_chunk.size());
         o.prank = pk.add(h.pair_rank.data(), 4 * h.pair_rank.size());
         o.bfirst = pk.add(h.blk_first.data(), 4 * std::max<size_t>(h.blk_first.size(), 1));
@@ -1954,8 +1938,6 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         o.crs = h.col_rows_start.empty() ? SIZE_MAX : pk.add(h.col_rows_start.data(), 4 * h.col_rows_start.size());
         o.cr = h.col_rows_start.empty() ? SIZE_MAX : pk.add(h.col_rows.data(), 4 * h.col_rows.size());
         o.live = h.col_rows_start.empty() ? SIZE_MAX : pk.add(h.live_pairs.data(), 4 * std::max<size_t>(h.live_pairs.size(), 1));
-        o.rspose = pk.add(h.rs_pose.data(), 4 * h.rs_pose.size());
-        o.rsrank0 = pk.add(h.rs_rank0.data(), 4 * h.rs_rank0.size());
         o.rsinfo = pk.add(h.rs_info.data(), 4 * h.rs_info.size());
         o.hpblm = pk.add(h.hp_b_lm.data(), 4 * h.hp_b_lm.size());
         o.rscs = pk.add(h.rs_chunk_start.data(), 4 * h.rs_chunk_start.size());
@@ -1979,7 +1961,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     char *pin = (char *)osg_pinned(ctx, in_pad + dev_bytes + ctl_bytes + out_bytes + 1024);
     if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
     OSG_RC(osg_idle(ctx));  // the pinned block may still be in use
-    pk.fill_parallel(pin, std::min(16, std::max(1, (int)std::thread::hardware_concurrency())));
+    pk.fill_parallel(pin, 16);
     LbaDev *h_dev = (LbaDev *)(pin + in_pad);
     LbaCtl *h_ctl = (LbaCtl *)((char *)h_dev + dev_bytes);
     double *h_out = (double *)((char *)h_ctl + ctl_bytes);
@@ -2041,13 +2023,10 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         D.edge_blk = osg_dptr<int32_t>(din, o.eblk);
         D.hp_e_start = osg_dptr<int32_t>(din, o.hpes);
         D.hp_e = osg_dptr<int32_t>(din, o.hpe);
-        D.hp_b_start = osg_dptr<int32_t>(din, o.hpbs);
         D.hp_b = osg_dptr<int32_t>(din, o.hpb);
-        D.pair_start = osg_dptr<int32_t>(din, o.pairs);
-        D.pair_ab = osg_dptr<int32_t>(din, o.pairab);
+        D.pair_b = osg_dptr<int32_t>(din, o.pairb);
         D.nchunks = h.nchunks;
         D.chunk_start = osg_dptr<int32_t>(din, o.chs);
-        D.blk_lm = osg_dptr<int32_t>(din, o.blklm);
         D.pair_chunk = osg_dptr<int32_t>(din, o.pch);
         D.pair_rank = osg_dptr<int32_t>(din, o.prank);
         D.blk_first = osg_dptr<int32_t>(din, o.bfirst);
@@ -2058,10 +2037,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         D.n_live = (int)h.live_pairs.size();
         D.npart = h.npart;
         D.n_rs = h.n_rs;
-        D.rs_pose = osg_dptr<int32_t>(din, o.rspose);
         D.rs_info = osg_dptr<int32_t>(din, o.rsinfo);
         D.hp_b_lm = osg_dptr<int32_t>(din, o.hpblm);
-        D.rs_rank0 = osg_dptr<int32_t>(din, o.rsrank0);
         D.rs_chunk_start = osg_dptr<int32_t>(din, o.rscs);
         D.rs_cdesc = osg_dptr<int32_t>(din, o.rscd);
         D.rs_chunk = osg_dptr<int32_t>(din, o.rsc);

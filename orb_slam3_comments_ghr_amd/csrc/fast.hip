@@ -438,17 +438,8 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
         distribute_oct_tree(keys_all + kbase[b] + k0, k1 - k0, g.minBX, g.maxBX, g.minBY, g.maxBY, n_features[l],
                             kept[task]);
     };
-    const int hw = std::max(1, (int)std::thread::hardware_concurrency());
     if (B > 1) {
-        const int nthr = std::min(std::min(16, hw), B * L);
-        std::atomic<int> next(0);
-        auto worker = [&]() {
-            for (int t = next++; t < B * L; t = next++) run_task(t);
-        };
-        std::vector<std::thread> th;
-        for (int t = 1; t < nthr; t++) th.emplace_back(worker);
-        worker();
-        for (auto &t : th) t.join();
+        osg_parallel_for(B * L, 16, run_task);
     } else {
         const int total = tot[0];
         const int32_t *offs = hoffs.data();

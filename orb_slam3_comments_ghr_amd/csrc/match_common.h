@@ -31,26 +31,28 @@ struct osg_packer {
     {
         for (const item &it : items) std::memcpy((char *)dst + it.off, it.src, it.bytes);
     }
-    // the same copy split over up to `nthreads` host threads by bytes (large batches)
+    // the same copy split into 4 MiB pieces over up to `nthreads` host threads (the calling one and
+    // budgeted workers, osg_parallel_for) for large batches
     void fill_parallel(void *dst, int nthreads) const
     {
         if (nthreads <= 1 || total < (size_t(8) << 20)) {
             fill(dst);
             return;
         }
-        const size_t per = (total + nthreads - 1) / nthreads;
-        std::vector<std::thread> th;
-        for (int t = 0; t < nthreads; t++) {
-            const size_t lo = t * per, hi = std::min(total, lo + per);
-            if (lo >= hi) break;
-            th.emplace_back([this, dst, lo, hi] {
-                for (const item &it : items) {  // the part of each item inside [lo, hi)
-                    const size_t a = std::max(lo, it.off), b = std::min(hi, it.off + it.bytes);
-                    if (a < b) std::memcpy((char *)dst + a, (const char *)it.src + (a - it.off), b - a);
-                }
-            });
-        }
-        for (auto &t : th) t.join();
+        constexpr size_t PIECE = size_t(4) << 20;
+        const int np = (int)((total + PIECE - 1) / PIECE);
+        osg_parallel_for(np, nthreads, [&](int p) {
+            const size_t lo = (size_t)p * PIECE, hi = std::min(total, lo + PIECE);
+            // the items overlapping [lo, hi): items are in offset order
+            size_t k = std::upper_bound(items.begin(), items.end(), lo,
+                                        [](size_t v, const item &it) { return v < it.off; }) - items.begin();
+            if (k > 0) k--;
+            for (; k < items.size() && items[k].off < hi; k++) {
+                const item &it = items[k];
+                const size_t a = std::max(lo, it.off), b = std::min(hi, it.off + it.bytes);
+                if (a < b) std::memcpy((char *)dst + a, (const char *)it.src + (a - it.off), b - a);
+            }
+        });
     }
 };
 

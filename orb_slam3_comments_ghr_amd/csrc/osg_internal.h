@@ -2,10 +2,14 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <memory>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "../../include/osg.h"
 #include "../../include/osg_ba.h"
@@ -113,3 +117,32 @@ int osg_pyramid_batch(osg_ctx *ctx, const uint8_t *d_images, int64_t img_bstride
 int osg_detect_batch(osg_ctx *ctx, const osg_image_pyramid *raw0, int32_t B, int64_t pyr_bstride, int32_t ini_th_fast,
                      int32_t min_th_fast, const int32_t *n_features_per_level, const float *scale_factors,
                      int32_t capacity, float *x, float *y, float *response, float *size, int32_t *level_start);
+
+// ---- host worker threads -------------------------------------------------------------------------
+// CPUs this process may run on at once: the smallest of the hardware threads, the affinity mask and
+// the cgroup CPU quota (a GPU box's container sees every core of the host but is granted a share);
+// OSG_HOST_THREADS overrides.  Cached after the first call.
+int osg_host_cpus();
+// A process-wide budget of extra worker threads (osg_host_cpus() - 1), shared by every context's
+// host phases, so that concurrent callers (one per host thread driving its own context) do not
+// oversubscribe the CPUs: a call takes what is free (possibly nothing) and runs the rest itself.
+int osg_workers_acquire(int want);
+void osg_workers_release(int n);
+// f(i) for i in [0, n) on the calling thread plus up to max_threads - 1 budgeted workers, indices
+// handed out one at a time (the per-index work is independent; the order of completion is not)
+template <class F>
+void osg_parallel_for(int n, int max_threads, F &&f)
+{
+    if (n <= 0) return;
+    const int extra = n > 1 ? osg_workers_acquire(std::min(n, max_threads) - 1) : 0;
+    std::atomic<int> next(0);
+    auto worker = [&]() {
+        for (int i = next++; i < n; i = next++) f(i);
+    };
+    std::vector<std::thread> th;
+    th.reserve(extra);
+    for (int t = 0; t < extra; t++) th.emplace_back(worker);
+    worker();
+    for (auto &t : th) t.join();
+    osg_workers_release(extra);
+}

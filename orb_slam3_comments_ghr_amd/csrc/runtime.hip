@@ -8,6 +8,66 @@
 
 #include "osg_internal.h"
 
+#include <sched.h>
+
+namespace {
+// the cgroup (v2 cpu.max, else v1 cfs) CPU quota in whole CPUs, rounded up; 0 when unlimited
+int cgroup_cpus()
+{
+    long long quota = -1, period = 0;
+    if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {};
+        if (fscanf(f, "%31s %lld", q, &period) == 2 && strcmp(q, "max") != 0) quota = atoll(q);
+        fclose(f);
+    } else if (FILE *f1 = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
+        if (fscanf(f1, "%lld", &quota) != 1) quota = -1;
+        fclose(f1);
+        if (FILE *f2 = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+            if (fscanf(f2, "%lld", &period) != 1) period = 0;
+            fclose(f2);
+        }
+    }
+    return quota > 0 && period > 0 ? (int)((quota + period - 1) / period) : 0;
+}
+std::atomic<int> g_workers{-1};  // free budget; -1 until first use
+}  // namespace
+
+int osg_host_cpus()
+{
+    static const int n = [] {
+        if (const char *e = getenv("OSG_HOST_THREADS"))
+            if (atoi(e) > 0) return atoi(e);
+        int c = std::max(1, (int)std::thread::hardware_concurrency());
+        cpu_set_t set;
+        if (sched_getaffinity(0, sizeof(set), &set) == 0) c = std::min(c, std::max(1, CPU_COUNT(&set)));
+        const int q = cgroup_cpus();
+        if (q > 0) c = std::min(c, q);
+        return c;
+    }();
+    return n;
+}
+
+int osg_workers_acquire(int want)
+{
+    if (want <= 0) return 0;
+    int cur = g_workers.load();
+    if (cur < 0) {
+        int init = -1;
+        g_workers.compare_exchange_strong(init, osg_host_cpus() - 1);
+        cur = g_workers.load();
+    }
+    while (cur > 0) {
+        const int take = std::min(cur, want);
+        if (g_workers.compare_exchange_weak(cur, cur - take)) return take;
+    }
+    return 0;
+}
+
+void osg_workers_release(int n)
+{
+    if (n > 0) g_workers += n;
+}
+
 int osg_set_error(osg_ctx *ctx, int code, const char *fmt, ...)
 {
     if (ctx) {

@@ -2,7 +2,11 @@
 // from Python: no GPU is touched, so it runs in the build container.
 // Build: hipcc --offload-arch=gfx950 -O3 -shared -fPIC tools/micro/lba_host_time.hip \
 //            -Iinclude -Lorb_slam3_comments_ghr_amd -lorbslam3_amd -o tools/micro/liblba_host_time.so
+#ifdef LBA_HOST_BA_SRC
+#include LBA_HOST_BA_SRC
+#else
 #include "../../orb_slam3_comments_ghr_amd/csrc/ba.hip"
+#endif
 
 extern "C" double lba_host_time_ms(const osg_ba_graph *G, int reps, int *ncontrib)
 {
@@ -31,10 +35,17 @@ extern "C" unsigned long long lba_host_struct_hash(const osg_ba_graph *G)
         for (size_t i = 0; i < v.size() * 4; i++) h = (h ^ p[i]) * 1099511628211ull;
         h = (h ^ v.size()) * 1099511628211ull;
     };
+    // the contributions' second blocks (pair_b; pair_ab's odd entries in older builds)
+#ifdef LBA_HOST_PAIR_AB
+    std::vector<int32_t> pb(std::max<size_t>(H.pair_ab.size() / 2, 1));
+    for (size_t k = 0; k < H.pair_ab.size() / 2; k++) pb[k] = H.pair_ab[2 * k + 1];
+#else
+    std::vector<int32_t> &pb = H.pair_b;
+#endif
     for (auto *v : {&H.blk_first, &H.blk_last, &H.col_rows_start, &H.col_rows, &H.live_pairs, &H.pose_h, &H.hp_pose,
                     &H.point_h, &H.hl_point, &H.lm_e_start, &H.lm_e, &H.lg_start, &H.lm_b_start, &H.blk_pose,
                     &H.edge_blk, &H.blk_lm, &H.hp_e_start, &H.hp_e, &H.hp_b_start, &H.hp_b, &H.pair_start,
-                    &H.pair_ab, &H.chunk_start, &H.pair_chunk, &H.pair_rank, &H.rs_pose, &H.rs_rank0,
+                    &pb, &H.chunk_start, &H.pair_chunk, &H.pair_rank, &H.rs_pose, &H.rs_rank0,
                     &H.rs_chunk_start, &H.rs_chunk, &H.hp_rs_start, &H.rs_order, &H.rs_cdesc, &H.rs_info, &H.hp_b_lm})
         mix(*v);
     const int sc[] = {H.np, H.npt, H.ne, H.nhp, H.nhl, H.nblk, H.npairs, H.nchunks, H.ge, H.gl, H.gll, H.gu,
