@@ -653,6 +653,147 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__
     }
 }
 
+// The same product with the partner blocks staged (OSG_SCHUR_STAGE=1).  A row segment's contributions
+// (a, b) pair each of its blocks a (landmark l) with the blocks b >= a of l, and a landmark's blocks
+// are consecutive (numbered landmark-major, sorted by pose): the partners of rank r are the span
+// [a_r, end of l).  The workgroup copies every span of the segment into LDS once (contiguous global
+// reads, issued together), forms BD from the staged Hpl_a, and its 16 waves then run the chunk loop
+// on LDS operands only.  Slots past the LDS capacity (a segment whose landmarks are observed by
+// unusually many poses) read Hpl_b from global memory.  Same products, same accumulation order as
+// k_schur_rows<false>: the results are bit-identical.
+constexpr int RT2 = 1024;               // 16 waves: one workgroup per CU (its LDS)
+constexpr int SPAN_CAP = 880;           // staged blocks: 880 x 144 B = 124 KiB
+__global__ __launch_bounds__(RT2, 1) void k_schur_rows_st(const LbaDev *__restrict__ Ds)
+{
+    LBA_GRAPH(M_ACT);
+    if (bx >= D.n_rs) return;
+    typedef int i4 __attribute__((ext_vector_type(4)));
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    const i4 inf0 = ((const GLOBAL i4 *)gbl(D.rs_info))[2 * bx];
+    const i4 inf1 = ((const GLOBAL i4 *)gbl(D.rs_info))[2 * bx + 1];
+    const int rs = __builtin_amdgcn_readfirstlane(inf0.x);
+    const int rb = __builtin_amdgcn_readfirstlane(inf0.z), hb0 = __builtin_amdgcn_readfirstlane(inf0.w);
+    const int nr = __builtin_amdgcn_readfirstlane(inf1.x);
+    __shared__ __attribute__((aligned(16))) double s_span[SPAN_CAP * 18];
+    __shared__ double s_bd[RS * 18 + 2];
+    __shared__ int s_pre[RS + 1], s_a[RS];
+    __shared__ double s_cf[RT2 / 64][6];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const GLOBAL double *__restrict__ Hv = gbl(D.Hpl);
+    // 1. spans: first block and length per rank, exclusive prefix (wave 0: 4 ranks per lane)
+    if (wv == 0) {
+        int len[4], a4[4], tot = 0;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int r = 4 * lane + u;
+            len[u] = 0;
+            a4[u] = 0;
+            if (r < nr) {
+                a4[u] = gbl(D.hp_b)[hb0 + rb + r];
+                const int l = gbl(D.hp_b_lm)[hb0 + rb + r];
+                len[u] = gbl(D.lm_b_start)[l + 1] - a4[u];
+            }
+            tot += len[u];
+        }
+        int inc = tot;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int v = __shfl_up(inc, off);
+            if (lane >= off) inc += v;
+        }
+        int run = inc - tot;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int r = 4 * lane + u;
+            if (r < nr) {
+                s_pre[r] = run;
+                s_a[r] = a4[u];
+            }
+            run += len[u];
+        }
+        if (lane == 63) s_pre[nr] = inc;
+        if (threadIdx.x == 0) s_bd[RS * 18] = 0.0;
+    }
+    __syncthreads();
+    // 2. stage the spans: wave w copies ranks w, w + 16, ...; a span is len x 9 16-byte granules,
+    // contiguous in global memory
+    for (int r = wv; r < nr; r += RT2 / 64) {
+        const int p0 = s_pre[r], n9 = 9 * (s_pre[r + 1] - p0), a = s_a[r];
+        for (int g = lane; g < n9; g += 64) {
+            const int slot = p0 + g / 9;
+            if (slot < SPAN_CAP)
+                *(u4 *)(s_span + 18 * (size_t)slot + 2 * (g % 9)) = *(const GLOBAL u4 *)(Hv + 18 * (size_t)a + 2 * g);
+        }
+    }
+    __syncthreads();
+    // 3. BD = Hpl_a Dinv_l into LDS with the segment's share of b_schur (as k_schur_rows)
+    double cf[6] = {0, 0, 0, 0, 0, 0};
+    {
+        const int h = threadIdx.x & 1;
+        double c3[3] = {0, 0, 0};
+        for (int r2 = threadIdx.x; r2 < 2 * nr; r2 += RT2) {
+            const int r = r2 >> 1;
+            const int l = gbl(D.hp_b_lm)[hb0 + rb + r];
+            const int p0 = s_pre[r];
+            double Di[9], db[3], B[9];
+            for (int k = 0; k < 9; k++) Di[k] = gbl(D.Dinv)[9 * (size_t)l + k];
+            for (int k = 0; k < 3; k++) db[k] = gbl(D.db)[3 * (size_t)l + k];
+            if (p0 < SPAN_CAP)
+                for (int k = 0; k < 9; k++) B[k] = s_span[18 * (size_t)p0 + 9 * h + k];
+            else
+                for (int k = 0; k < 9; k++) B[k] = Hv[18 * (size_t)s_a[r] + 9 * h + k];
+            double *BD = s_bd + 18 * r + 9 * h;
+            for (int rr = 0; rr < 3; rr++) {
+                for (int c = 0; c < 3; c++)
+                    BD[3 * rr + c] = B[3 * rr] * Di[c] + B[3 * rr + 1] * Di[3 + c] + B[3 * rr + 2] * Di[6 + c];
+                c3[rr] += B[3 * rr] * db[0] + B[3 * rr + 1] * db[1] + B[3 * rr + 2] * db[2];
+            }
+        }
+        for (int k = 0; k < 6; k++) cf[k] = (k / 3 == h) ? c3[k % 3] : 0.0;
+    }
+    // the butterfly in the same lane order as k_schur_rows (RT = 512: waves 0..7 summed), then the
+    // 16 waves in order
+    for (int k = 0; k < 6; k++) cf[k] = wave_sum(cf[k]);
+    if (lane == 0)
+        for (int k = 0; k < 6; k++) s_cf[wv][k] = cf[k];
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        double t = 0.0;
+        for (int w = 0; w < RT2 / 64; w++) t += s_cf[w][threadIdx.x];
+        D.bs_part[6 * (size_t)rs + threadIdx.x] = t;
+    }
+    // 4. the chunks: per lane q (< count) the contribution's rank and its partner's slot
+    const int kk = lane >> 4, beta = (lane >> 2) & 3, ri = lane & 3;
+    const int arow = 4 * (beta >> 1) + ri, bcol = 4 * (beta & 1) + ri;
+    const int a_m = kk < 3 ? 18 : 0;
+    const int aoff = kk < 3 ? 3 * min(arow, 5) + kk : RS * 18;
+    const int boff = 3 * min(bcol, 5) + min(kk, 2);
+    const int orow = 4 * (beta >> 1) + kk, ocol = 4 * (beta & 1) + ri;
+    const int t1 = __builtin_amdgcn_readfirstlane(inf1.z);
+    const GLOBAL i4 *__restrict__ cd = (const GLOBAL i4 *)gbl(D.rs_cdesc);
+    for (int t = __builtin_amdgcn_readfirstlane(inf1.y) + wv; t < t1; t += RT2 / 64) {
+        const i4 d = cd[t];
+        const int ch = __builtin_amdgcn_readfirstlane(d.x), q0 = __builtin_amdgcn_readfirstlane(d.y);
+        const int nq = __builtin_amdgcn_readfirstlane(d.z);
+        int rank = 0, slot = 0, bblk = 0;
+        if (lane < nq) {
+            rank = gbl(D.pair_rank)[q0 + lane] - rb;
+            bblk = gbl(D.pair_b)[q0 + lane];
+            slot = s_pre[rank] + bblk - s_a[rank];
+        }
+        double acc0 = 0.0, acc1 = 0.0;
+        for (int v = 0; v < nq; v++) {
+            const int rk = __builtin_amdgcn_readlane(rank, v), sl = __builtin_amdgcn_readlane(slot, v);
+            const double av = s_bd[a_m * rk + aoff];
+            const double bv = sl < SPAN_CAP ? s_span[18 * sl + boff]
+                                            : Hv[18 * (size_t)__builtin_amdgcn_readlane(bblk, v) + boff];
+            if (v & 1) acc1 = __builtin_amdgcn_mfma_f64_4x4x4f64(av, bv, acc1, 0, 0, 0);
+            else acc0 = __builtin_amdgcn_mfma_f64_4x4x4f64(av, bv, acc0, 0, 0, 0);
+        }
+        if (orow < 6 && ocol < 6) D.chunk_part[36 * (size_t)ch + 6 * orow + ocol] = acc0 + acc1;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_schur_pairs(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT);
@@ -1844,6 +1985,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     const bool prof = prof_level > 0, prof_ts = prof_level >= 2 && B == 1;
     // OSG_SCHUR_VALU=1: the VALU Schur product (A/B measurements); default FP64 MFMA
     static const bool schur_valu = getenv("OSG_SCHUR_VALU") && atoi(getenv("OSG_SCHUR_VALU")) != 0;
+    // OSG_SCHUR_STAGE=1: partner spans staged in LDS (k_schur_rows_st), bit-identical
+    static const bool schur_stage = getenv("OSG_SCHUR_STAGE") && atoi(getenv("OSG_SCHUR_STAGE")) != 0;
     const auto tp0 = std::chrono::steady_clock::now();
     auto ms_since = [&](std::chrono::steady_clock::time_point t) {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
@@ -2121,6 +2264,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         if (mx_nhp > 0) {
             LBA_MARK(KT_SROWS);
             if (schur_valu) hipLaunchKernelGGL(k_schur_rows<true>, gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
+            else if (schur_stage) hipLaunchKernelGGL(k_schur_rows_st, gx(mx_rs), dim3(RT2), 0, ctx->stream, d_dev);
             else hipLaunchKernelGGL(k_schur_rows<false>, gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
             LBA_MARK(KT_SPAIRS);
             hipLaunchKernelGGL(k_schur_pairs, gx((int)(((size_t)mx_pairs * 64 + 255) / 256)), dim3(256), 0, ctx->stream, d_dev);

@@ -213,6 +213,45 @@ def test_lba_batch_equals_single_calls(ctx, oracle):
         np.testing.assert_array_equal(got.edge_bad, ref.edge_bad)
 
 
+def _lba_batch_graphs():
+    rng = np.random.default_rng(0x0B5EED04 + 11)
+    graphs = [op.synth_lba_graph(rng, n_kf=50, n_points=10000) for _ in range(3)]
+    graphs += [op.synth_lba_graph(rng, n_kf=int(k), n_points=int(p), stereo_frac=s)
+               for k, p, s in [(5, 300, 0.0), (12, 900, 0.3), (20, 2000, 1.0)]]
+    return graphs
+
+
+@pytest.mark.parametrize("env", [{"OSG_SCHUR_STAGE": "1"}, {"OSG_SCHUR_STAGE": "0"}],
+                         ids=lambda e: "-".join(f"{k[4:]}={v}" for k, v in e.items()))
+def test_lba_schur_variants_bit_identical(ctx, env):
+    """The Schur product's two MFMA forms (read once per process, so run in a child): the LDS-staged
+    partner spans (k_schur_rows_st) and the per-group gathers (k_schur_rows) give the same results bit
+    for bit (the same products in the same order)."""
+    import subprocess
+    import sys
+    out = f"/tmp/_osg_lba_variant_{os.getpid()}.npz"
+    code = ("import numpy as np\n"
+            "from orb_slam3_comments_ghr_amd import Context, optimizer as op\n"
+            "from tests.test_ba_gpu import _lba_batch_graphs\n"
+            "res = op.Optimizer(Context(0)).LocalBundleAdjustmentBatch(_lba_batch_graphs())\n"
+            f"np.savez('{out}', **{{f'p{{i}}': r.pose for i, r in enumerate(res)}},\n"
+            "         **{f'q{i}': r.point for i, r in enumerate(res)},\n"
+            "         it=np.array([[r.iterations, r.trials] for r in res]),\n"
+            "         chi=np.array([[r.chi2_initial, r.chi2_final] for r in res]))\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=dict(os.environ, **env), capture_output=True,
+                       text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = np.load(out)
+    os.remove(out)
+    res = op.Optimizer(ctx).LocalBundleAdjustmentBatch(_lba_batch_graphs())
+    np.testing.assert_array_equal(got["it"], [[r.iterations, r.trials] for r in res])
+    np.testing.assert_array_equal(got["chi"], [[r.chi2_initial, r.chi2_final] for r in res])
+    for i, r in enumerate(res):
+        np.testing.assert_array_equal(got[f"p{i}"], r.pose)
+        np.testing.assert_array_equal(got[f"q{i}"], r.point)
+
+
 def test_lba_batch_c4_windows(ctx, oracle):
     """8 C4-sized windows (50 KF x 10k points) in one batch against the oracle."""
     rng = np.random.default_rng(0x0B5EED04 + 7)
