@@ -369,13 +369,16 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
     // pinned: inputs, then the totals and counts, then the keys
     const size_t in_pad = (pk.total + 255) & ~size_t(255);
     const size_t cnt_pad = (sizeof(int32_t) * ((size_t)nc * B + B) + 255) & ~size_t(255);
-    char *pin = (char *)osg_pinned(ctx, in_pad + cnt_pad + sizeof(float4) * (max_keys * B + 1) + 256);
+    // (a batch's keys get their own staging request once the totals are known: max_keys is every
+    // tested pixel of an image, ~100x the keypoints)
+    const size_t keys_pin = B == 1 ? sizeof(float4) * (max_keys + 1) : 0;
+    char *pin = (char *)osg_pinned(ctx, in_pad + cnt_pad + keys_pin + 256);
     if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
     OSG_RC(osg_idle(ctx));  // the pinned block may still be in use
     pk.fill_parallel(pin, 8);
     int32_t *pin_tot = (int32_t *)(pin + in_pad);                 // B totals
     int32_t *pin_cnt = pin_tot + B;                                // B x nc counts
-    char *pin_keys = pin + in_pad + cnt_pad;                       // image b's keys at b max_keys
+    char *pin_keys = pin + in_pad + cnt_pad;                       // image b's keys at kbase[b]
     hipEvent_t *ev = osg_ctx_events(ctx);
     if (!ev) return osg_set_error(ctx, OSG_E_HIP, "event create failed");
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(din, pin, pk.total, hipMemcpyHostToDevice, ctx->stream));
@@ -387,16 +390,27 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
     }
     OSG_HIP_CHECK(ctx, hipGetLastError());
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
-    std::vector<int32_t> tot(B, 0);
+    std::vector<int32_t> tot(B, 0), cnt_copy;
+    std::vector<size_t> kbase(B + 1, 0);
+    const int32_t *cnt_src = pin_cnt;
     if (nc > 0) {
         OSG_RC(osg_download(ctx, pin_tot, (const void *)d_total, sizeof(int32_t) * B));
         OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_cnt, dcnt, sizeof(int32_t) * (size_t)nc * B, hipMemcpyDeviceToHost,
                                           ctx->stream));
         OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));  // (a polled wait measured slower here)
-        for (int b = 0; b < B; b++) tot[b] = pin_tot[b];
+        for (int b = 0; b < B; b++) {
+            tot[b] = pin_tot[b];
+            kbase[b + 1] = kbase[b] + (size_t)tot[b];
+        }
+        if (B > 1) {  // the counts leave the staging block, which the keys may now reuse (stream idle)
+            cnt_copy.assign(pin_cnt, pin_cnt + (size_t)nc * B);
+            cnt_src = cnt_copy.data();
+            pin_keys = (char *)osg_pinned(ctx, sizeof(float4) * (kbase[B] + 1) + 256);
+            if (!pin_keys) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
+        }
         for (int b = 0; b < B; b++)
             if (tot[b] > 0)
-                OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_keys + sizeof(float4) * max_keys * b, CA.keys + max_keys * b,
+                OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_keys + sizeof(float4) * kbase[b], CA.keys + max_keys * b,
                                                   sizeof(float4) * (size_t)tot[b], hipMemcpyDeviceToHost, ctx->stream));
     }
     OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));  // (a polled wait measured slower here)
@@ -413,12 +427,10 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
     for (int b = 0; b < B; b++) ntot += (size_t)tot[b];
     hkeys.resize(ntot + 1);
     hoffs.assign((size_t)B * (nc + 1), 0);
-    std::vector<size_t> kbase(B + 1, 0);
+    if (ntot > 0) std::memcpy(hkeys.data(), pin_keys, sizeof(Key4) * ntot);
     for (int b = 0; b < B; b++) {
-        kbase[b + 1] = kbase[b] + (size_t)tot[b];
-        if (tot[b] > 0) std::memcpy(hkeys.data() + kbase[b], pin_keys + sizeof(float4) * max_keys * b, sizeof(Key4) * tot[b]);
         int32_t *o = hoffs.data() + (size_t)b * (nc + 1);
-        for (int c = 0; c < nc; c++) o[c + 1] = o[c] + (nc > 0 ? pin_cnt[(size_t)b * nc + c] : 0);  // counts -> offsets
+        for (int c = 0; c < nc; c++) o[c + 1] = o[c] + cnt_src[(size_t)b * nc + c];  // counts -> offsets
     }
     const double t_copy = ms_since(tp1);
     // DistributeOctTree per (image, level) over that level's cells' keypoints (:1180-1196).  The tasks
