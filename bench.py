@@ -370,7 +370,12 @@ def main():
             return
         if rank == 0:  # progress on stderr: a long run shows it is alive
             print(f"[bench] {key} ({time.perf_counter() - t_start:.0f} s)", file=sys.stderr, flush=True)
-        out[key] = fn(ctx, rank, world, dist, dev, args)
+        try:
+            out[key] = fn(ctx, rank, world, dist, dev, args)
+        except Exception as e:  # a failing secondary stage must not cost the headline line
+            import traceback
+            traceback.print_exc(file=sys.stderr)
+            out[key] = {"error": f"{type(e).__name__}: {e}"[:500]}
 
     if not args.no_frames:
         stage("frames_c3", bench_c3)
