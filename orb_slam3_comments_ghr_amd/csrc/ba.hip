@@ -1633,6 +1633,12 @@ struct LbaCache {
 enum { KT_ERR, KT_LIN, KT_POSE, KT_LINIT, KT_SPOINT, KT_SROWS, KT_SPAIRS, KT_CHOL, KT_BACK, KT_UPD, KT_RED, KT_CLASS, KT_END };
 static_assert(KT_END == OSG_LBA_NK, "osg_lba_kernel_times slots");
 
+#ifdef OSG_LBA_STRUCT_PROF
+thread_local double g_struct_cp[16];
+#define STRUCT_CP(k) g_struct_cp[k] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp0).count()
+#else
+#define STRUCT_CP(k)
+#endif
 int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
 {
     const auto tp0 = std::chrono::steady_clock::now();
@@ -1666,6 +1672,7 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
     }
     if (6 * (size_t)nhp * 6 * (size_t)nhp > (size_t(1) << 31))
         return osg_set_error(ctx, OSG_E_INVALID, "%d free poses: the dense reduced system would exceed 2^31 entries", nhp);
+    STRUCT_CP(1);
     const std::vector<int32_t> &pose_h = H.pose_h, &point_h = H.point_h;
     // edges per landmark (stable in edge order)
     H.lm_e_start.assign(nhl + 1, 0);
@@ -1686,6 +1693,7 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
         }
         if (nhl == 0) H.lg_start.push_back(0);
     }
+    STRUCT_CP(2);
     // blocks per landmark: unique free poses sorted by hessian index
     H.lm_b_start.assign(nhl + 1, 0);
     H.edge_blk.assign(ne, -1);
@@ -1713,6 +1721,7 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
                 }
         }
     }
+    STRUCT_CP(3);
     const int nblk = (int)H.blk_pose.size();
     H.nblk = nblk;
     H.blk_lm.assign(nblk, 0);
@@ -1734,6 +1743,7 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
                 H.multi |= cnt[b] > 1;
             }
     }
+    STRUCT_CP(4);
     // edges / blocks per hessian pose
     H.hp_e_start.assign(nhp + 1, 0);
     H.hp_b_start.assign(nhp + 1, 0);
@@ -1753,33 +1763,71 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
         std::vector<int32_t> fill(H.hp_b_start.begin(), H.hp_b_start.end() - 1);
         for (int b = 0; b < nblk; b++) H.hp_b[fill[H.blk_pose[b]]++] = b;
     }
-    // rank of each block in its pose's block list (hp_b is in block order)
-    std::vector<int32_t> blk_rank(nblk);
-    for (int i = 0; i < nhp; i++)
-        for (int q = H.hp_b_start[i]; q < H.hp_b_start[i + 1]; q++) blk_rank[H.hp_b[q]] = q - H.hp_b_start[i];
-    // pose pairs (i <= j), dense index; contributions (a, b) in landmark order: the device reads b
-    // and the rank of a
+    STRUCT_CP(5);
+    // pose pairs (i <= j), dense index pid(i, j) = i nhp - i (i - 1) / 2 + j - i; the contributions
+    // (a, b) of a pair in landmark order, of which the device reads b and the rank of a in pose i's
+    // block list.  A window (tens of poses, many per batch on host threads) walks the landmarks in
+    // order.  A map (one large graph per call) goes row by row on host workers: pose i's block list
+    // is in landmark order and each of its blocks a pairs with the blocks b >= a of its landmark
+    // (poses j >= i), so row i counts and then fills its own pairs (consecutive in pid) in landmark
+    // order.  Both give the same arrays.
     const int npairs = nhp * (nhp + 1) / 2;
     H.npairs = npairs;
-    auto pid = [nhp](int i, int j) { return i * nhp - i * (i - 1) / 2 + (j - i); };
+    auto rowbase = [nhp](int i) { return (size_t)i * nhp - (size_t)i * (i - 1) / 2 - i; };  // pid(i, j) - j
+    const int row_threads = nhp >= 512 ? 16 : 1;
     H.pair_start.assign(npairs + 1, 0);
-    for (int l = 0; l < nhl; l++)
-        for (int a = H.lm_b_start[l]; a < H.lm_b_start[l + 1]; a++)
-            for (int b = a; b < H.lm_b_start[l + 1]; b++) H.pair_start[pid(H.blk_pose[a], H.blk_pose[b]) + 1]++;
+    std::vector<int32_t> hpb_end, blk_rank;  // per hp_b entry: one past its landmark's last block
+    if (row_threads > 1) {
+        hpb_end.resize(std::max(nblk, 1));
+        for (size_t q = 0; q < H.hp_b.size(); q++) hpb_end[q] = H.lm_b_start[H.blk_lm[H.hp_b[q]] + 1];
+        osg_parallel_for(nhp, row_threads, [&](int i) {
+            int32_t *ps = H.pair_start.data() + 1 + rowbase(i);  // [j]
+            for (int q = H.hp_b_start[i]; q < H.hp_b_start[i + 1]; q++)
+                for (int b = H.hp_b[q], e = hpb_end[q]; b < e; b++) ps[H.blk_pose[b]]++;
+        });
+    } else {
+        blk_rank.resize(std::max(nblk, 1));
+        for (int i = 0; i < nhp; i++)
+            for (int q = H.hp_b_start[i]; q < H.hp_b_start[i + 1]; q++) blk_rank[H.hp_b[q]] = q - H.hp_b_start[i];
+        for (int l = 0; l < nhl; l++)
+            for (int a = H.lm_b_start[l]; a < H.lm_b_start[l + 1]; a++) {
+                int32_t *ps = H.pair_start.data() + 1 + rowbase(H.blk_pose[a]);
+                for (int b = a; b < H.lm_b_start[l + 1]; b++) ps[H.blk_pose[b]]++;
+            }
+    }
     for (int k = 0; k < npairs; k++) H.pair_start[k + 1] += H.pair_start[k];
     const size_t ncontrib = (size_t)H.pair_start[npairs];
     H.pair_b.assign(std::max<size_t>(ncontrib, 1), 0);
     H.pair_rank.assign(std::max<size_t>(ncontrib, 1), 0);
-    {
+    if (row_threads > 1) {
+        osg_parallel_for(nhp, row_threads, [&](int i) {
+            thread_local std::vector<int32_t> fill;
+            fill.resize(nhp);
+            const size_t rb = rowbase(i);
+            const int hb0 = H.hp_b_start[i], hb1 = H.hp_b_start[i + 1];
+            int jmax = i;  // the row's pairs reach no further than its blocks' poses
+            for (int q = hb0; q < hb1; q++) jmax = std::max(jmax, (int)H.blk_pose[hpb_end[q] - 1]);
+            for (int j = i; j <= jmax; j++) fill[j] = H.pair_start[rb + j];
+            for (int q = hb0; q < hb1; q++)
+                for (int b = H.hp_b[q], e = hpb_end[q]; b < e; b++) {
+                    const int k = fill[H.blk_pose[b]]++;
+                    H.pair_b[k] = b;
+                    H.pair_rank[k] = q - hb0;
+                }
+        });
+    } else {
         std::vector<int32_t> fill(H.pair_start.begin(), H.pair_start.end() - 1);
         for (int l = 0; l < nhl; l++)
-            for (int a = H.lm_b_start[l]; a < H.lm_b_start[l + 1]; a++)
+            for (int a = H.lm_b_start[l]; a < H.lm_b_start[l + 1]; a++) {
+                int32_t *fa = fill.data() + rowbase(H.blk_pose[a]);
                 for (int b = a; b < H.lm_b_start[l + 1]; b++) {
-                    const int k = fill[pid(H.blk_pose[a], H.blk_pose[b])]++;
+                    const int k = fa[H.blk_pose[b]]++;
                     H.pair_b[k] = b;
                     H.pair_rank[k] = blk_rank[a];
                 }
+            }
     }
+    STRUCT_CP(6);
     // envelope of the reduced system (used past CMAX): a pose row's first nonzero pose column is the
     // smallest pose it shares a landmark with; row block t starts at the smallest over its rows
     {
@@ -1823,6 +1871,7 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
                 }
         }
     }
+    STRUCT_CP(7);
     // row segments of RS ranks
     H.hp_rs_start.assign(nhp + 1, 0);
     for (int i = 0; i < nhp; i++) {
@@ -1850,34 +1899,87 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
         }
         std::stable_sort(H.rs_order.begin(), H.rs_order.end(), [&](int a, int b) { return key[a] < key[b]; });
     }
+    STRUCT_CP(8);
     // chunks of <= SCH contributions, never spanning two pairs or two row segments; listed per row
-    // segment (pair order, then contribution order)
-    H.pair_chunk.assign(npairs + 1, 0);
-    std::vector<int32_t> chunk_rs;
-    for (int i = 0, k = 0; i < nhp; i++)
-        for (int j = i; j < nhp; j++, k++) {
-            H.pair_chunk[k] = (int)H.chunk_start.size();
-            int q = H.pair_start[k];
-            while (q < H.pair_start[k + 1]) {
-                const int seg = H.pair_rank[q] / RS;
+    // segment (pair order, then contribution order).  A row's chunks belong to its own segments, so
+    // the rows are numbered from per-row counts and filled independently (host workers for a map).
+    // A pair's ranks ascend (landmark order): a chunk ends at SCH contributions or at the first rank
+    // of the next segment.
+    auto row_chunks = [&](int i, auto &&emit) {
+        const size_t rb = rowbase(i);
+        for (int j = i; j < nhp; j++) {
+            const int k = (int)(rb + j), q1 = H.pair_start[k + 1];
+            emit(k, -1, 0);  // the pair's first chunk
+            for (int q = H.pair_start[k]; q < q1;) {
+                const int seg = H.pair_rank[q] / RS, seg_end = (seg + 1) * RS;
+                const int e1 = std::min(q1, q + SCH);
                 int e = q + 1;
-                while (e < H.pair_start[k + 1] && e - q < SCH && H.pair_rank[e] / RS == seg) e++;
-                H.chunk_start.push_back(q);
-                chunk_rs.push_back(H.hp_rs_start[i] + seg);
+                while (e < e1 && H.pair_rank[e] < seg_end) e++;
+                emit(k, q, seg);
                 q = e;
             }
         }
-    H.pair_chunk[npairs] = (int)H.chunk_start.size();
-    H.nchunks = (int)H.chunk_start.size();
-    H.chunk_start.push_back(H.pair_start[npairs]);
-    H.rs_chunk_start.assign(H.n_rs + 1, 0);
-    for (int c = 0; c < H.nchunks; c++) H.rs_chunk_start[chunk_rs[c] + 1]++;
-    for (int r = 0; r < H.n_rs; r++) H.rs_chunk_start[r + 1] += H.rs_chunk_start[r];
-    H.rs_chunk.assign(std::max(H.nchunks, 1), 0);
-    {
+    };
+    std::vector<int32_t> chunk_rs;
+    if (row_threads == 1) {  // a window: one pass in pair order
+        H.pair_chunk.assign(npairs + 1, 0);
+        H.chunk_start.clear();
+        for (int i = 0; i < nhp; i++)
+            row_chunks(i, [&](int k, int q, int seg) {
+                if (q < 0) {
+                    H.pair_chunk[k] = (int)H.chunk_start.size();
+                    return;
+                }
+                H.chunk_start.push_back(q);
+                chunk_rs.push_back(H.hp_rs_start[i] + seg);
+            });
+        H.nchunks = (int)H.chunk_start.size();
+        H.pair_chunk[npairs] = H.nchunks;
+        H.chunk_start.push_back(H.pair_start[npairs]);
+        H.rs_chunk_start.assign(H.n_rs + 1, 0);
+        for (int c = 0; c < H.nchunks; c++) H.rs_chunk_start[chunk_rs[c] + 1]++;
+        for (int r = 0; r < H.n_rs; r++) H.rs_chunk_start[r + 1] += H.rs_chunk_start[r];
+        H.rs_chunk.assign(std::max(H.nchunks, 1), 0);
         std::vector<int32_t> fill(H.rs_chunk_start.begin(), H.rs_chunk_start.end() - 1);
         for (int c = 0; c < H.nchunks; c++) H.rs_chunk[fill[chunk_rs[c]]++] = c;
+    } else {  // a map: rows numbered from per-row counts, filled on host workers
+    std::vector<int32_t> row_c0(nhp + 1, 0);
+    osg_parallel_for(nhp, row_threads, [&](int i) {
+        int n = 0;
+        row_chunks(i, [&](int, int q, int) { n += q >= 0; });
+        row_c0[i + 1] = n;
+    });
+    for (int i = 0; i < nhp; i++) row_c0[i + 1] += row_c0[i];
+    H.nchunks = row_c0[nhp];
+    H.pair_chunk.assign(npairs + 1, 0);
+    H.chunk_start.assign(H.nchunks + 1, 0);
+    chunk_rs.resize(std::max(H.nchunks, 1));
+    H.rs_chunk_start.assign(H.n_rs + 1, 0);
+    osg_parallel_for(nhp, row_threads, [&](int i) {
+        int c = row_c0[i];
+        row_chunks(i, [&](int k, int q, int seg) {
+            if (q < 0) {
+                H.pair_chunk[k] = c;
+                return;
+            }
+            H.chunk_start[c] = q;
+            chunk_rs[c] = H.hp_rs_start[i] + seg;
+            H.rs_chunk_start[chunk_rs[c] + 1]++;  // the row's own segments
+            c++;
+        });
+    });
+    H.pair_chunk[npairs] = H.nchunks;
+    H.chunk_start[H.nchunks] = H.pair_start[npairs];
+    for (int r = 0; r < H.n_rs; r++) H.rs_chunk_start[r + 1] += H.rs_chunk_start[r];
+    H.rs_chunk.assign(std::max(H.nchunks, 1), 0);
+    osg_parallel_for(nhp, row_threads, [&](int i) {
+        thread_local std::vector<int32_t> fill;
+        const int r0 = H.hp_rs_start[i], r1 = H.hp_rs_start[i + 1];
+        fill.assign(H.rs_chunk_start.begin() + r0, H.rs_chunk_start.begin() + r1);
+        for (int c = row_c0[i]; c < row_c0[i + 1]; c++) H.rs_chunk[fill[chunk_rs[c] - r0]++] = c;
+    });
     }
+    STRUCT_CP(9);
     H.rs_info.assign(8 * (size_t)std::max(H.n_rs, 1), 0);
     for (int w = 0; w < H.n_rs; w++) {
         const int r = H.rs_order[w], i = H.rs_pose[r], hb0 = H.hp_b_start[i];
@@ -1899,6 +2001,7 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
         H.rs_cdesc[4 * (size_t)t + 1] = H.chunk_start[c];
         H.rs_cdesc[4 * (size_t)t + 2] = H.chunk_start[c + 1] - H.chunk_start[c];
     }
+    STRUCT_CP(10);
     H.ge = (ne + EB - 1) / EB;
     H.gl = (nhl + EB - 1) / EB;
     H.gll = (int)H.lg_start.size() - 1;

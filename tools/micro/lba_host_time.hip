@@ -2,6 +2,7 @@
 // from Python: no GPU is touched, so it runs in the build container.
 // Build: hipcc --offload-arch=gfx950 -O3 -shared -fPIC tools/micro/lba_host_time.hip \
 //            -Iinclude -Lorb_slam3_comments_ghr_amd -lorbslam3_amd -o tools/micro/liblba_host_time.so
+#define OSG_LBA_STRUCT_PROF
 #ifdef LBA_HOST_BA_SRC
 #include LBA_HOST_BA_SRC
 #else
@@ -52,4 +53,12 @@ extern "C" unsigned long long lba_host_struct_hash(const osg_ba_graph *G)
                       H.nblk_red, H.npart, H.n_rs, H.max_col_rows, (int)H.multi};
     for (int v : sc) h = (h ^ (unsigned)v) * 1099511628211ull;
     return h;
+}
+
+extern "C" void lba_host_time_phases(double *out16)
+{
+    for (int k = 0; k < 16; k++) {
+        out16[k] = g_struct_cp[k];
+        g_struct_cp[k] = 0;
+    }
 }
