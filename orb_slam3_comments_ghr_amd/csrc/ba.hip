@@ -1633,6 +1633,51 @@ struct LbaCache {
 enum { KT_ERR, KT_LIN, KT_POSE, KT_LINIT, KT_SPOINT, KT_SROWS, KT_SPAIRS, KT_CHOL, KT_BACK, KT_UPD, KT_RED, KT_CLASS, KT_END };
 static_assert(KT_END == OSG_LBA_NK, "osg_lba_kernel_times slots");
 
+// Stable counting sort of the indices [0, n) by key(i) in [0, K) (negative: left out) on up to
+// `threads` host workers: contiguous index ranges, per-range histograms, offsets in (key, range)
+// order, so every key's indices keep their order.  start gets K + 1 offsets, out the indices.
+template <class KeyF>
+void counting_sort_par(int n, int K, KeyF key, std::vector<int32_t> &start, std::vector<int32_t> &out, int threads)
+{
+    const int T = std::max(1, std::min(threads, (n + 4095) / 4096));
+    std::vector<int32_t> hist((size_t)T * K, 0);
+    auto range = [&](int t, int &i0, int &i1) {
+        i0 = (int)((int64_t)n * t / T);
+        i1 = (int)((int64_t)n * (t + 1) / T);
+    };
+    osg_parallel_for(T, T, [&](int t) {
+        int i0, i1;
+        range(t, i0, i1);
+        int32_t *h = hist.data() + (size_t)t * K;
+        for (int i = i0; i < i1; i++) {
+            const int k = key(i);
+            if (k >= 0) h[k]++;
+        }
+    });
+    start.assign(K + 1, 0);
+    int32_t run = 0;
+    for (int k = 0; k < K; k++) {
+        start[k] = run;
+        for (int t = 0; t < T; t++) {
+            const int32_t c = hist[(size_t)t * K + k];
+            hist[(size_t)t * K + k] = run;
+            run += c;
+        }
+    }
+    start[K] = run;
+    out.assign(std::max(run, 1), 0);
+    osg_parallel_for(T, T, [&](int t) {
+        int i0, i1;
+        range(t, i0, i1);
+        int32_t *h = hist.data() + (size_t)t * K;
+        for (int i = i0; i < i1; i++) {
+            const int k = key(i);
+            if (k >= 0) out[h[k]++] = i;
+        }
+    });
+}
+
+// phase clocks of the structure build (tools/micro/lba_host_time.hip defines OSG_LBA_STRUCT_PROF)
 #ifdef OSG_LBA_STRUCT_PROF
 thread_local double g_struct_cp[16];
 #define STRUCT_CP(k) g_struct_cp[k] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp0).count()
@@ -1694,47 +1739,119 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
         if (nhl == 0) H.lg_start.push_back(0);
     }
     STRUCT_CP(2);
-    // blocks per landmark: unique free poses sorted by hessian index
-    H.lm_b_start.assign(nhl + 1, 0);
-    H.edge_blk.assign(ne, -1);
-    H.blk_pose.reserve(ne);
-    std::vector<int32_t> tmp;
-    for (int l = 0; l < nhl; l++) {
-        tmp.clear();
-        for (int q = H.lm_e_start[l]; q < H.lm_e_start[l + 1]; q++) {
-            const int ph = pose_h[G->e_pose[H.lm_e[q]]];
-            if (ph >= 0) tmp.push_back(ph);
-        }
-        std::sort(tmp.begin(), tmp.end());
-        tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
-        const int base = (int)H.blk_pose.size();
-        for (int ph : tmp) H.blk_pose.push_back(ph);
-        H.lm_b_start[l + 1] = (int)H.blk_pose.size();
-        for (int q = H.lm_e_start[l]; q < H.lm_e_start[l + 1]; q++) {
-            const int e = H.lm_e[q];
-            const int ph = pose_h[G->e_pose[e]];
-            if (ph < 0) continue;
-            for (int k = 0; k < (int)tmp.size(); k++)
-                if (tmp[k] == ph) {
-                    H.edge_blk[e] = base + k;
-                    break;
+    // a map (one large graph per call) builds its structure on host workers; a window (many per batch,
+    // each on its own worker) keeps the sequential passes.  Both give the same arrays.
+    const bool map_mode = nhp >= 512;
+    if (map_mode) {
+        // blocks per landmark: unique free poses sorted by hessian index, counted then filled per
+        // landmark range; the per-edge block code as below, settled landmark by landmark (a block's
+        // edges all belong to its landmark and lm_e lists them in edge order)
+        const int NR = std::max(1, std::min(256, nhl / 256));
+        auto lrange = [&](int r, int &l0, int &l1) {
+            l0 = (int)((int64_t)nhl * r / NR);
+            l1 = (int)((int64_t)nhl * (r + 1) / NR);
+        };
+        auto distinct = [&](int l, std::vector<int32_t> &stamp, std::vector<int32_t> &tmp) {
+            tmp.clear();
+            for (int q = H.lm_e_start[l]; q < H.lm_e_start[l + 1]; q++) {
+                const int ph = pose_h[G->e_pose[H.lm_e[q]]];
+                if (ph >= 0 && stamp[ph] != l) {
+                    stamp[ph] = l;
+                    tmp.push_back(ph);
                 }
+            }
+        };
+        H.lm_b_start.assign(nhl + 1, 0);
+        osg_parallel_for(NR, 16, [&](int r) {
+            thread_local std::vector<int32_t> stamp, tmp;
+            stamp.assign(nhp, -1);
+            int l0, l1;
+            lrange(r, l0, l1);
+            for (int l = l0; l < l1; l++) {
+                distinct(l, stamp, tmp);
+                H.lm_b_start[l + 1] = (int)tmp.size();
+            }
+        });
+        for (int l = 0; l < nhl; l++) H.lm_b_start[l + 1] += H.lm_b_start[l];
+        const int nb = H.lm_b_start[nhl];
+        H.blk_pose.assign(nb, 0);
+        H.blk_lm.assign(nb, 0);
+        H.edge_blk.assign(ne, -1);
+        std::atomic<bool> multi(false);
+        osg_parallel_for(NR, 16, [&](int r) {
+            thread_local std::vector<int32_t> stamp, tmp, cnt;
+            thread_local std::vector<uint8_t> seen;
+            stamp.assign(nhp, -1);
+            bool m = false;
+            int l0, l1;
+            lrange(r, l0, l1);
+            for (int l = l0; l < l1; l++) {
+                distinct(l, stamp, tmp);
+                std::sort(tmp.begin(), tmp.end());
+                const int base = H.lm_b_start[l], k = (int)tmp.size();
+                cnt.assign(k, 0);
+                seen.assign(k, 0);
+                for (int u = 0; u < k; u++) {
+                    H.blk_pose[base + u] = tmp[u];
+                    H.blk_lm[base + u] = l;
+                }
+                auto slot = [&](int ph) { return (int)(std::lower_bound(tmp.begin(), tmp.end(), ph) - tmp.begin()); };
+                for (int q = H.lm_e_start[l]; q < H.lm_e_start[l + 1]; q++) {
+                    const int ph = pose_h[G->e_pose[H.lm_e[q]]];
+                    if (ph >= 0) cnt[slot(ph)]++;
+                }
+                for (int q = H.lm_e_start[l]; q < H.lm_e_start[l + 1]; q++) {
+                    const int e = H.lm_e[q];
+                    const int ph = pose_h[G->e_pose[e]];
+                    if (ph < 0) continue;
+                    const int u = slot(ph);
+                    H.edge_blk[e] = 4 * (base + u) + (cnt[u] > 1 ? 2 : 0) + (seen[u] ? 1 : 0);
+                    seen[u] = 1;
+                    m |= cnt[u] > 1;
+                }
+            }
+            if (m) multi = true;
+        });
+        H.multi = multi.load();
+    } else {
+        // blocks per landmark: unique free poses sorted by hessian index
+        H.lm_b_start.assign(nhl + 1, 0);
+        H.edge_blk.assign(ne, -1);
+        H.blk_pose.reserve(ne);
+        std::vector<int32_t> tmp;
+        for (int l = 0; l < nhl; l++) {
+            tmp.clear();
+            for (int q = H.lm_e_start[l]; q < H.lm_e_start[l + 1]; q++) {
+                const int ph = pose_h[G->e_pose[H.lm_e[q]]];
+                if (ph >= 0) tmp.push_back(ph);
+            }
+            std::sort(tmp.begin(), tmp.end());
+            tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
+            const int base = (int)H.blk_pose.size();
+            for (int ph : tmp) H.blk_pose.push_back(ph);
+            H.lm_b_start[l + 1] = (int)H.blk_pose.size();
+            for (int q = H.lm_e_start[l]; q < H.lm_e_start[l + 1]; q++) {
+                const int e = H.lm_e[q];
+                const int ph = pose_h[G->e_pose[e]];
+                if (ph < 0) continue;
+                for (int k = 0; k < (int)tmp.size(); k++)
+                    if (tmp[k] == ph) {
+                        H.edge_blk[e] = base + k;
+                        break;
+                    }
+            }
         }
-    }
-    STRUCT_CP(3);
-    const int nblk = (int)H.blk_pose.size();
-    H.nblk = nblk;
-    H.blk_lm.assign(nblk, 0);
-    for (int l = 0; l < nhl; l++)
-        for (int b = H.lm_b_start[l]; b < H.lm_b_start[l + 1]; b++) H.blk_lm[b] = l;
-    // per edge 4 block + 2 (the block has several edges) + 1 (not the block's first edge in edge
-    // order): k_linearize writes a lone edge's Hpl block directly, and stores the first edge's terms
-    // of a shared block and adds the others' (a per-block reduction in edge order)
-    {
-        std::vector<int32_t> cnt(nblk, 0);
+        const int nb = (int)H.blk_pose.size();
+        H.blk_lm.assign(nb, 0);
+        for (int l = 0; l < nhl; l++)
+            for (int b = H.lm_b_start[l]; b < H.lm_b_start[l + 1]; b++) H.blk_lm[b] = l;
+        // per edge 4 block + 2 (the block has several edges) + 1 (not the block's first edge in edge
+        // order): k_linearize writes a lone edge's Hpl block directly, and stores the first edge's terms
+        // of a shared block and adds the others' (a per-block reduction in edge order)
+        std::vector<int32_t> cnt(nb, 0);
         for (int e = 0; e < ne; e++)
             if (H.edge_blk[e] >= 0) cnt[H.edge_blk[e]]++;
-        std::vector<uint8_t> seen(nblk, 0);
+        std::vector<uint8_t> seen(nb, 0);
         for (int e = 0; e < ne; e++)
             if (H.edge_blk[e] >= 0) {
                 const int b = H.edge_blk[e];
@@ -1743,8 +1860,17 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
                 H.multi |= cnt[b] > 1;
             }
     }
+    STRUCT_CP(3);
+    const int nblk = (int)H.blk_pose.size();
+    H.nblk = nblk;
     STRUCT_CP(4);
     // edges / blocks per hessian pose
+    if (map_mode) {
+        counting_sort_par(ne, nhp, [&](int e) { return pose_h[G->e_pose[e]]; }, H.hp_e_start, H.hp_e, 16);
+        H.hp_e.resize(H.hp_e_start[nhp]);
+        counting_sort_par(nblk, nhp, [&](int b) { return H.blk_pose[b]; }, H.hp_b_start, H.hp_b, 16);
+        H.hp_b.resize(nblk);
+    } else {
     H.hp_e_start.assign(nhp + 1, 0);
     H.hp_b_start.assign(nhp + 1, 0);
     H.hp_b.assign(nblk, 0);
@@ -1763,6 +1889,7 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
         std::vector<int32_t> fill(H.hp_b_start.begin(), H.hp_b_start.end() - 1);
         for (int b = 0; b < nblk; b++) H.hp_b[fill[H.blk_pose[b]]++] = b;
     }
+    }
     STRUCT_CP(5);
     // pose pairs (i <= j), dense index pid(i, j) = i nhp - i (i - 1) / 2 + j - i; the contributions
     // (a, b) of a pair in landmark order, of which the device reads b and the rank of a in pose i's
@@ -1774,12 +1901,15 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
     const int npairs = nhp * (nhp + 1) / 2;
     H.npairs = npairs;
     auto rowbase = [nhp](int i) { return (size_t)i * nhp - (size_t)i * (i - 1) / 2 - i; };  // pid(i, j) - j
-    const int row_threads = nhp >= 512 ? 16 : 1;
+    const int row_threads = map_mode ? 16 : 1;
     H.pair_start.assign(npairs + 1, 0);
     std::vector<int32_t> hpb_end, blk_rank;  // per hp_b entry: one past its landmark's last block
     if (row_threads > 1) {
         hpb_end.resize(std::max(nblk, 1));
-        for (size_t q = 0; q < H.hp_b.size(); q++) hpb_end[q] = H.lm_b_start[H.blk_lm[H.hp_b[q]] + 1];
+        osg_parallel_for(64, row_threads, [&](int t) {
+            const size_t q0 = H.hp_b.size() * t / 64, q1 = H.hp_b.size() * (t + 1) / 64;
+            for (size_t q = q0; q < q1; q++) hpb_end[q] = H.lm_b_start[H.blk_lm[H.hp_b[q]] + 1];
+        });
         osg_parallel_for(nhp, row_threads, [&](int i) {
             int32_t *ps = H.pair_start.data() + 1 + rowbase(i);  // [j]
             for (int q = H.hp_b_start[i]; q < H.hp_b_start[i + 1]; q++)
@@ -1863,12 +1993,13 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
                 H.max_col_rows = std::max(H.max_col_rows, H.col_rows_start[j + 1] - H.col_rows_start[j]);
             // live pairs: (i <= j) with some entry (row in pose j, column in pose i) in a lower
             // envelope tile: row block of 6 j + r, column block of 6 i + c, blk_first[row blk] <= col blk
-            for (int i = 0, k = 0; i < nhp; i++)
-                for (int j = i; j < nhp; j++, k++) {
-                    const int cb1 = (6 * i + 5) / CB;  // the block's last column block
-                    if (H.blk_first[(6 * j) / CB] <= cb1 || H.blk_first[(6 * j + 5) / CB] <= cb1)
-                        H.live_pairs.push_back(k);
-                }
+            std::vector<int32_t> fj(nhp);  // the smallest envelope start over pose j's two row blocks
+            for (int j = 0; j < nhp; j++) fj[j] = std::min(H.blk_first[(6 * j) / CB], H.blk_first[(6 * j + 5) / CB]);
+            for (int i = 0, k = 0; i < nhp; i++) {
+                const int cb1 = (6 * i + 5) / CB;  // the block's last column block
+                for (int j = i; j < nhp; j++, k++)
+                    if (fj[j] <= cb1) H.live_pairs.push_back(k);
+            }
         }
     }
     STRUCT_CP(7);
