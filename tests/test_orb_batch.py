@@ -2,8 +2,8 @@
 ref:src/ORBextractor.cc:1553-1690).  GPU: every image's keypoints, responses, sizes, octaves, angles
 and descriptors equal the single-image chain osg_orb_pyramid -> osg_orb_detect -> osg_orb_describe on
 that image (itself bit-exact with the oracle's chain in test_orb_pyramid.py), and the first image's
-equal the oracle's chain directly; blank images, padded image strides, tiny images and a capacity
-overflow.  CPU: the parameter struct mirrors the header field by field."""
+equal the oracle's chain directly; blank images, padded image strides, small images with another
+level count and scale factor, and a capacity overflow.  CPU: the parameter struct mirrors the header field by field."""
 import ctypes as C
 
 import numpy as np
@@ -80,10 +80,11 @@ def test_batch_padded_stride_and_other_shapes(ctx):
     dev = big.cuda()[:, :480, :640]
     assert dev.stride(0) == 500 * 704 and dev.stride(1) == 704
     _check_batch(ctx, imgs, pattern, dev)
-    # a 4-level, factor-2 extractor with 300 features on small images
-    small = [_image(300 + i, 96, 128, 40) for i in range(4)]
-    _check_batch(ctx, small, pattern, torch.from_numpy(np.stack(small)).cuda(), n_features=300, n_levels=4,
-                 factor=2.0)
+    # a 3-level, factor-1.5 extractor with 300 features on small images (the top level, 107 x 142, still
+    # holds one 35-px cell inside its borders, as the reference's cell grid needs)
+    small = [_image(300 + i, 240, 320, 120) for i in range(4)]
+    _check_batch(ctx, small, pattern, torch.from_numpy(np.stack(small)).cuda(), n_features=300, n_levels=3,
+                 factor=1.5)
 
 
 @pytest.mark.gpu
