@@ -338,7 +338,7 @@ int osg_orb_extract_batch(osg_ctx *ctx, const uint8_t *d_images, int64_t image_s
                          P->pattern && P->umax && counts && capacity >= 0,
                 "null argument");
     OSG_REQUIRE(ctx, capacity == 0 || (x && y && angle && response && size && octave && desc), "null output");
-    OSG_REQUIRE(ctx, step >= cols && image_stride >= (int64_t)step * rows, "image step / stride");
+    OSG_REQUIRE(ctx, step >= cols && (n_images == 1 || image_stride >= (int64_t)step * rows), "image step / stride");
     const int L = P->n_levels;
     OSG_REQUIRE(ctx, L >= 1 && L <= MAX_LEVELS, "n_levels = %d", L);
     int32_t lr[MAX_LEVELS], lc[MAX_LEVELS];

@@ -258,7 +258,9 @@ def ORBExtractBatch(ctx: Context, images, n_features: int = 1000, n_levels: int 
     octave = np.zeros((B, cap), np.int32)
     desc = np.zeros((B, cap, 32), np.uint8)
     counts = np.zeros(B, np.int32)
-    ctx.check(ctx.lib.osg_orb_extract_batch(ctx.handle, images.data_ptr(), images.stride(0), rows, cols,
+    # a size-1 batch dimension may carry any stride (numpy's new axes have 0)
+    istride = images.stride(0) if B > 1 else rows * images.stride(1)
+    ctx.check(ctx.lib.osg_orb_extract_batch(ctx.handle, images.data_ptr(), istride, rows, cols,
                                             images.stride(1), B, C.byref(prm), cap, x.ctypes.data, y.ctypes.data,
                                             ang.ctypes.data, resp.ctypes.data, size.ctypes.data, octave.ctypes.data,
                                             desc.ctypes.data, counts.ctypes.data), "osg_orb_extract_batch")
