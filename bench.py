@@ -662,16 +662,17 @@ def bench_gba_map(ctx, rank, world, dist, dev, args, loop=False):
     single-threaded, so more cores do not speed up one map (they only run more maps).
     loop=True (global_ba_loop): the same map closed into a loop (synth_map_graph(loop=True)), the global
     BA LoopClosing starts after a loop closure (ref:src/LoopClosing.cc:2436); device memory the call
-    holds (the context's arena after the call, hipMemGetInfo) is reported as peak_device_bytes."""
+    holds (a fresh context's arena after one call, osg_ctx_device_bytes) is reported as peak_device_bytes."""
     import torch
     from orb_slam3_comments_ghr_amd import optimizer as op
     G = op.synth_map_graph(np.random.default_rng(0x0B5EED31 + rank), n_kf=1500, n_points=150000, loop=loop)
-    opt = op.Optimizer(ctx)
-    torch.cuda.synchronize(dev)
-    free0 = torch.cuda.mem_get_info(dev)[0]
+    # a context of its own, so its arena is this map's peak alone (slots grow to a call's needs and stay)
+    from orb_slam3_comments_ghr_amd import Context
+    mctx = Context(dev.index if dev.index is not None else 0)
+    opt = op.Optimizer(mctx)
     r = opt.BundleAdjustment(G)
     torch.cuda.synchronize(dev)
-    held = free0 - torch.cuda.mem_get_info(dev)[0]
+    held = mctx.device_bytes()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -692,7 +693,7 @@ def bench_gba_map(ctx, rank, world, dist, dev, args, loop=False):
                        + ("a loop-closed map: the band plus its corner blocks" if loop else "banded: an open trajectory")
                        + f"), optimize({G.iterations}), no Huber",
            "peak_device_bytes": int(held),
-           "peak_device_note": "device memory the context holds after the first call (hipMemGetInfo delta): the "
+           "peak_device_note": "device memory a fresh context holds after one call (osg_ctx_device_bytes): the "
                                "arena grows to the call's peak and stays; includes the dense n x n reduced matrix",
            "n_gpus": world, "dtype": "f64", "scaling": "weak", "parallelism": f"replicas x{world} (one map per GPU)"}
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -574,6 +574,9 @@ int osg_match_last_stats(osg_ctx *ctx, int32_t *out4);
 /* Device time (HIP events around the launch, ms) of the last matching or pose-optimization kernel
  * this context ran: the search calls and osg_pose_optimization[_batch]. */
 int osg_ctx_last_kernel_ms(osg_ctx *ctx, double *ms);
+/* Device memory this context holds (its scratch arena: every slot grows to the largest call so far and
+ * stays), bytes.  No reference counterpart. */
+int osg_ctx_device_bytes(osg_ctx *ctx, int64_t *bytes);
 
 #ifdef __cplusplus
 }

@@ -149,6 +149,12 @@ class Context:
         self.check(self.lib.osg_ctx_last_kernel_ms(self.handle, _ptr(ms)), "osg_ctx_last_kernel_ms")
         return float(ms[0])
 
+    def device_bytes(self) -> int:
+        """Device memory this context's scratch arena holds (slots grow to the largest call and stay)."""
+        b = np.zeros(1, np.int64)
+        self.check(self.lib.osg_ctx_device_bytes(self.handle, _ptr(b)), "osg_ctx_device_bytes")
+        return int(b[0])
+
     def descriptor_distance_pairs(self, a: np.ndarray, b: np.ndarray) -> np.ndarray:
         a = np.ascontiguousarray(a, dtype=np.uint8).reshape(-1, 32)
         b = np.ascontiguousarray(b, dtype=np.uint8).reshape(-1, 32)

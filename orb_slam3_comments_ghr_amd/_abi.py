@@ -188,7 +188,7 @@ EXPORTS = [
     "osg_search_by_projection_kf", "osg_search_by_bow_kf_f", "osg_search_by_bow_kf_kf",
     "osg_search_by_projection_mps_batch", "osg_search_by_projection_last_batch",
     "osg_search_by_projection_kf_batch", "osg_search_by_bow_kf_f_batch", "osg_search_by_bow_kf_kf_batch",
-    "osg_match_last_stats", "osg_ctx_last_kernel_ms", "osg_pose_optimization", "osg_pose_optimization_batch",
+    "osg_match_last_stats", "osg_ctx_last_kernel_ms", "osg_ctx_device_bytes", "osg_pose_optimization", "osg_pose_optimization_batch",
     "osg_local_bundle_adjustment", "osg_local_bundle_adjustment_batch", "osg_bundle_adjustment",
     "osg_lba_kernel_times",
     "osg_vocabulary_create", "osg_vocabulary_load_text", "osg_vocabulary_destroy", "osg_vocabulary_info",
@@ -242,6 +242,7 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.osg_search_by_bow_kf_kf_batch.argtypes = [vp, vp, vp, i32, f32, C.c_int, vp, vp]
     lib.osg_match_last_stats.argtypes = [vp, vp]
     lib.osg_ctx_last_kernel_ms.argtypes = [vp, vp]
+    lib.osg_ctx_device_bytes.argtypes = [vp, vp]
     lib.osg_pose_optimization.argtypes = [vp, C.POINTER(OsgPoseProblem), C.POINTER(OsgPoseResult)]
     lib.osg_pose_optimization_batch.argtypes = [vp, C.POINTER(OsgPoseProblem), i32,
                                                 C.POINTER(OsgPoseResult)]

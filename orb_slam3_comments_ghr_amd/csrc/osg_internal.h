@@ -9,6 +9,7 @@
 #include <memory>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/osg.h"
@@ -123,26 +124,19 @@ int osg_detect_batch(osg_ctx *ctx, const osg_image_pyramid *raw0, int32_t B, int
 // the cgroup CPU quota (a GPU box's container sees every core of the host but is granted a share);
 // OSG_HOST_THREADS overrides.  Cached after the first call.
 int osg_host_cpus();
-// A process-wide budget of extra worker threads (osg_host_cpus() - 1), shared by every context's
-// host phases, so that concurrent callers (one per host thread driving its own context) do not
-// oversubscribe the CPUs: a call takes what is free (possibly nothing) and runs the rest itself.
-int osg_workers_acquire(int want);
-void osg_workers_release(int n);
-// f(i) for i in [0, n) on the calling thread plus up to max_threads - 1 budgeted workers, indices
-// handed out one at a time (the per-index work is independent; the order of completion is not)
+// One process-wide pool of osg_host_cpus() - 1 persistent worker threads, shared by every context's
+// host phases: concurrent callers (one per host thread driving its own context) queue their loops on
+// the same workers instead of starting threads of their own, so the CPUs are not oversubscribed and a
+// worker's thread_local buffers (the octree's nodes) survive from call to call.  The caller runs
+// indices of its own loop too, so a loop finishes even when every worker is busy elsewhere.
+// fn(arg, i) for i in [0, n) on the caller plus up to max_threads - 1 workers, indices handed out one
+// at a time (the per-index work is independent; the order of completion is not).
+void osg_parallel_run(int n, int max_threads, void (*fn)(void *, int), void *arg);
 template <class F>
 void osg_parallel_for(int n, int max_threads, F &&f)
 {
     if (n <= 0) return;
-    const int extra = n > 1 ? osg_workers_acquire(std::min(n, max_threads) - 1) : 0;
-    std::atomic<int> next(0);
-    auto worker = [&]() {
-        for (int i = next++; i < n; i = next++) f(i);
-    };
-    std::vector<std::thread> th;
-    th.reserve(extra);
-    for (int t = 0; t < extra; t++) th.emplace_back(worker);
-    worker();
-    for (auto &t : th) t.join();
-    osg_workers_release(extra);
+    using Fn = typename std::remove_reference<F>::type;
+    osg_parallel_run(n, max_threads, [](void *a, int i) { (*static_cast<Fn *>(a))(i); },
+                     const_cast<void *>(static_cast<const void *>(&f)));
 }

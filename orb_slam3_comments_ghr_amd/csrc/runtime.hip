@@ -10,6 +10,10 @@
 
 #include <sched.h>
 
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+
 namespace {
 // the cgroup (v2 cpu.max, else v1 cfs) CPU quota in whole CPUs, rounded up; 0 when unlimited
 int cgroup_cpus()
@@ -29,7 +33,61 @@ int cgroup_cpus()
     }
     return quota > 0 && period > 0 ? (int)((quota + period - 1) / period) : 0;
 }
-std::atomic<int> g_workers{-1};  // free budget; -1 until first use
+// the worker pool behind osg_parallel_run
+struct PoolJob {
+    void (*fn)(void *, int);
+    void *arg;
+    int n;
+    std::atomic<int> next{0}, done{0}, active{0};
+    int seats;  // workers that may still join (under the pool's mutex)
+};
+struct WorkerPool {
+    std::mutex m;
+    std::condition_variable cv;
+    std::deque<PoolJob *> q;
+    std::vector<std::thread> th;
+    explicit WorkerPool(int nw)
+    {
+        for (int i = 0; i < nw; i++) th.emplace_back([this] { loop(); });
+        for (auto &t : th) t.detach();  // live for the process (never torn down at exit)
+    }
+    static void run(PoolJob *j)
+    {
+        for (int i = j->next++; i < j->n; i = j->next++) {
+            j->fn(j->arg, i);
+            j->done++;
+        }
+    }
+    void loop()
+    {
+        for (;;) {
+            PoolJob *j = nullptr;
+            {
+                std::unique_lock<std::mutex> lk(m);
+                cv.wait(lk, [&] {
+                    for (PoolJob *c : q)
+                        if (c->seats > 0 && c->next.load() < c->n) return true;
+                    return false;
+                });
+                for (PoolJob *c : q)
+                    if (c->seats > 0 && c->next.load() < c->n) {
+                        c->seats--;
+                        c->active++;  // under the mutex: the owner removes the job under it too
+                        j = c;
+                        break;
+                    }
+            }
+            if (!j) continue;
+            run(j);
+            j->active--;  // the worker's last access to the job
+        }
+    }
+};
+WorkerPool *pool()
+{
+    static WorkerPool *p = new WorkerPool(std::max(0, osg_host_cpus() - 1));
+    return p;
+}
 }  // namespace
 
 int osg_host_cpus()
@@ -47,25 +105,36 @@ int osg_host_cpus()
     return n;
 }
 
-int osg_workers_acquire(int want)
+void osg_parallel_run(int n, int max_threads, void (*fn)(void *, int), void *arg)
 {
-    if (want <= 0) return 0;
-    int cur = g_workers.load();
-    if (cur < 0) {
-        int init = -1;
-        g_workers.compare_exchange_strong(init, osg_host_cpus() - 1);
-        cur = g_workers.load();
+    if (n <= 0) return;
+    PoolJob j;
+    j.fn = fn;
+    j.arg = arg;
+    j.n = n;
+    WorkerPool *p = n > 1 && max_threads > 1 ? pool() : nullptr;
+    j.seats = p ? std::min(std::min(n, max_threads) - 1, (int)p->th.size()) : 0;
+    const bool queued = j.seats > 0;
+    if (queued) {
+        {
+            std::lock_guard<std::mutex> lk(p->m);
+            p->q.push_back(&j);
+        }
+        p->cv.notify_all();
     }
-    while (cur > 0) {
-        const int take = std::min(cur, want);
-        if (g_workers.compare_exchange_weak(cur, cur - take)) return take;
+    WorkerPool::run(&j);
+    if (queued) {  // the job lives on this stack: out of the queue and no worker inside before returning
+        while (j.done.load() < n) std::this_thread::yield();
+        {
+            std::lock_guard<std::mutex> lk(p->m);
+            for (auto it = p->q.begin(); it != p->q.end(); ++it)
+                if (*it == &j) {
+                    p->q.erase(it);
+                    break;
+                }
+        }
+        while (j.active.load() > 0) std::this_thread::yield();
     }
-    return 0;
-}
-
-void osg_workers_release(int n)
-{
-    if (n > 0) g_workers += n;
 }
 
 int osg_set_error(osg_ctx *ctx, int code, const char *fmt, ...)
@@ -322,6 +391,15 @@ int osg_ctx_last_kernel_ms(osg_ctx *ctx, double *ms)
 {
     if (!ctx || !ms) return OSG_E_INVALID;
     *ms = ctx->last_kernel_ms;
+    return OSG_OK;
+}
+
+int osg_ctx_device_bytes(osg_ctx *ctx, int64_t *bytes)
+{
+    if (!ctx || !bytes) return OSG_E_INVALID;
+    int64_t t = 0;
+    for (int s = 0; s < SLOT_COUNT; s++) t += (int64_t)ctx->cap[s];
+    *bytes = t;
     return OSG_OK;
 }
 

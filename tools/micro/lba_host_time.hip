@@ -62,3 +62,24 @@ extern "C" void lba_host_time_phases(double *out16)
         g_struct_cp[k] = 0;
     }
 }
+
+// osg_parallel_for under concurrent callers: T threads, each running `loops` loops of n indices that
+// sum i * i; returns the number of wrong sums (0 expected)
+extern "C" int pool_stress(int T, int loops, int n)
+{
+    std::atomic<int> bad{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++)
+        th.emplace_back([&, t] {
+            for (int k = 0; k < loops; k++) {
+                std::vector<long long> v(n, 0);
+                osg_parallel_for(n, 1 + (t + k) % 16, [&](int i) { v[i] = (long long)i * i; });
+                long long s = 0;
+                for (int i = 0; i < n; i++) s += v[i];
+                const long long want = (long long)(n - 1) * n * (2LL * n - 1) / 6;
+                if (s != want) bad++;
+            }
+        });
+    for (auto &x : th) x.join();
+    return bad.load();
+}
