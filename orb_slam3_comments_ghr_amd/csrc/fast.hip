@@ -233,6 +233,19 @@ __global__ __launch_bounds__(256) void k_cell_gather(const CellArgs A)
     if (c == A.n_cells - 1 && threadIdx.x == 0) A.total[bi] = off + cnt;
 }
 
+// A batch's keys made contiguous for one download: image b's total keys move to the sum of the totals
+// before it (the slot area is free once k_cell_gather has run)
+__global__ __launch_bounds__(256) void k_keys_compact(const float4 *keys, int max_keys, const GLOBAL int32_t *total,
+                                                      float4 *out)
+{
+    const int b = blockIdx.y;
+    int base = 0;
+    for (int i = 0; i < b; i++) base += total[i];
+    const int n = total[b];
+    const float4 *src = keys + (size_t)b * max_keys;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) out[base + i] = src[i];
+}
+
 #include "octree.h"
 using osg_oct::Key4;
 using osg_oct::distribute_oct_tree;
@@ -387,6 +400,8 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
     if (nc > 0) {
         hipLaunchKernelGGL(k_fast_cells, dim3(nc, B), dim3(256), 0, ctx->stream, CA);
         hipLaunchKernelGGL(k_cell_gather, dim3(nc, B), dim3(256), 0, ctx->stream, CA);
+        if (B > 1) hipLaunchKernelGGL(k_keys_compact, dim3(32, B), dim3(256), 0, ctx->stream, CA.keys, CA.max_keys, CA.total,
+                                      CA.slots);
     }
     OSG_HIP_CHECK(ctx, hipGetLastError());
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
@@ -408,10 +423,14 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
             pin_keys = (char *)osg_pinned(ctx, sizeof(float4) * (kbase[B] + 1) + 256);
             if (!pin_keys) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
         }
-        for (int b = 0; b < B; b++)
-            if (tot[b] > 0)
-                OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_keys + sizeof(float4) * kbase[b], CA.keys + max_keys * b,
-                                                  sizeof(float4) * (size_t)tot[b], hipMemcpyDeviceToHost, ctx->stream));
+        if (B > 1) {  // compacted on the device (k_keys_compact): one copy
+            if (kbase[B] > 0)
+                OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_keys, CA.slots, sizeof(float4) * kbase[B], hipMemcpyDeviceToHost,
+                                                  ctx->stream));
+        } else if (tot[0] > 0) {
+            OSG_HIP_CHECK(ctx, hipMemcpyAsync(pin_keys, CA.keys, sizeof(float4) * (size_t)tot[0], hipMemcpyDeviceToHost,
+                                              ctx->stream));
+        }
     }
     OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));  // (a polled wait measured slower here)
     const double t_gpu = ms_since(tp0);
@@ -427,7 +446,14 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
     for (int b = 0; b < B; b++) ntot += (size_t)tot[b];
     hkeys.resize(ntot + 1);
     hoffs.assign((size_t)B * (nc + 1), 0);
-    if (ntot > 0) std::memcpy(hkeys.data(), pin_keys, sizeof(Key4) * ntot);
+    if (ntot > 0) {  // a batch's keys (~10 MB) in 1 MiB pieces on the worker pool
+        const size_t bytes = sizeof(Key4) * ntot, piece = size_t(1) << 20;
+        char *dst = (char *)hkeys.data();
+        osg_parallel_for((int)((bytes + piece - 1) / piece), B > 1 ? 16 : 1, [&](int p) {
+            const size_t lo = (size_t)p * piece;
+            std::memcpy(dst + lo, pin_keys + lo, std::min(piece, bytes - lo));
+        });
+    }
     for (int b = 0; b < B; b++) {
         int32_t *o = hoffs.data() + (size_t)b * (nc + 1);
         for (int c = 0; c < nc; c++) o[c + 1] = o[c] + cnt_src[(size_t)b * nc + c];  // counts -> offsets

@@ -18,6 +18,7 @@
 // float products and a sum, as written.
 #include <algorithm>
 #include <cfloat>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -332,6 +333,9 @@ int osg_orb_extract_batch(osg_ctx *ctx, const uint8_t *d_images, int64_t image_s
                           int32_t *counts)
 {
     if (!ctx) return OSG_E_INVALID;
+    static const bool prof = getenv("OSG_ORB_PROFILE") != nullptr;  // host phase times to stderr
+    const auto tp0 = std::chrono::steady_clock::now();
+    auto ms_since = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp0).count(); };
     OSG_REQUIRE(ctx, n_images >= 0 && n_images <= 65535, "n_images = %d", n_images);
     if (n_images == 0) return 0;
     OSG_REQUIRE(ctx, d_images && P && P->scale_factors && P->inv_scale_factors && P->n_features_per_level &&
@@ -364,6 +368,7 @@ int osg_orb_extract_batch(osg_ctx *ctx, const uint8_t *d_images, int64_t image_s
     const int n = osg_detect_batch(ctx, &raw0, n_images, pstride, P->ini_th_fast, P->min_th_fast,
                                    P->n_features_per_level, P->scale_factors, capacity, x, y, response, size, ls.data());
     if (n < 0) return n;
+    const double t_detect = ms_since();
     // all images' keypoints in one list for the describe kernels, with their image and level
     std::vector<float> kx(n), ky(n), ka(n);
     std::vector<int32_t> kl(n), ki(n);
@@ -380,15 +385,20 @@ int osg_orb_extract_batch(osg_ctx *ctx, const uint8_t *d_images, int64_t image_s
                 octave[(size_t)b * capacity + i] = l;
             }
     }
+    const double t_list = ms_since();
     const osg_orb_keypoints K = {n, kx.data(), ky.data(), kl.data()};
     const int rc = orb_run(ctx, &raw0, &blur0, &K, P->pattern, P->umax, 1, ka.data(), kd.data(), ki.data(), pstride,
                            pstride);
     if (rc < 0) return rc;
+    const double t_desc = ms_since();
     for (int b = 0, q = 0; b < n_images; b++)
         for (int i = 0; i < counts[b]; i++, q++) {
             angle[(size_t)b * capacity + i] = ka[q];
             std::memcpy(desc + ((size_t)b * capacity + i) * 32, kd.data() + (size_t)q * 32, 32);
         }
+    if (prof)
+        fprintf(stderr, "[osg orb extract] %d images, %d keypoints: pyramid + detect %.3f ms, list %.3f ms, describe %.3f ms, "
+                        "scatter %.3f ms\n", n_images, n, t_detect, t_list - t_detect, t_desc - t_list, ms_since() - t_desc);
     return n;
 }
 

@@ -485,6 +485,7 @@ int pyramid_run(osg_ctx *ctx, const uint8_t *image, int32_t rows, int32_t cols, 
         OSG_HIP_CHECK(ctx, hipGetLastError());
     }
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
+    if (B > 1) return OSG_OK;  // the batched extractor goes on in the same stream (detection waits for it)
     OSG_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));  // (a polled wait measured slower here)
     float ms = 0.f;
     OSG_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ev[0], ev[1]));
