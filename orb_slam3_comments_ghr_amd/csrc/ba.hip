@@ -630,16 +630,30 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__
             // next group: the rest of this chunk, else the first group of the next chunk
             if (u + GC < nq) load_group(u + GC, nq - u - GC, my_b, R);
             else load_group(0, dn.z, n_b, R);
+            if (cnt == GC) {
+                // a full group: straight-line, so the LDS reads of later contributions issue while
+                // earlier MFMAs run (the guarded form below waits on each pair's reads)
 #pragma unroll
-            for (int v = 0; v < GC; v += 2) {
-                if (v < cnt) {
-                    const int rank = __builtin_amdgcn_readlane(my_rank, u + v);
-                    acc0 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[a_m * rank + aoff], hb[18 * v + boff], acc0, 0, 0, 0);
+                for (int v = 0; v < GC; v += 2) {
+                    const int r0 = __builtin_amdgcn_readlane(my_rank, u + v);
+                    const int r1 = __builtin_amdgcn_readlane(my_rank, u + v + 1);
+                    acc0 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[a_m * r0 + aoff], hb[18 * v + boff], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[a_m * r1 + aoff], hb[18 * (v + 1) + boff], acc1, 0, 0,
+                                                              0);
                 }
-                if (v + 1 < cnt) {
-                    const int rank = __builtin_amdgcn_readlane(my_rank, u + v + 1);
-                    acc1 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[a_m * rank + aoff], hb[18 * (v + 1) + boff], acc1, 0,
-                                                              0, 0);
+            } else {
+#pragma unroll
+                for (int v = 0; v < GC; v += 2) {
+                    if (v < cnt) {
+                        const int rank = __builtin_amdgcn_readlane(my_rank, u + v);
+                        acc0 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[a_m * rank + aoff], hb[18 * v + boff], acc0, 0, 0,
+                                                                  0);
+                    }
+                    if (v + 1 < cnt) {
+                        const int rank = __builtin_amdgcn_readlane(my_rank, u + v + 1);
+                        acc1 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[a_m * rank + aoff], hb[18 * (v + 1) + boff], acc1,
+                                                                  0, 0, 0);
+                    }
                 }
             }
             __builtin_amdgcn_wave_barrier();
