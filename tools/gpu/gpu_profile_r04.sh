@@ -15,5 +15,5 @@ TS=1 BS=64 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d
 TS=1 BS=64 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/lba_write -o w -- python3 $R/tools/lba_batch_bench.py > $OUT/lba_write.log 2>&1 &&
 python3 $R/tools/pmc_kernel_summary.py $OUT/r04_schur_pmc.json $(find $OUT/lba_sq -name '*counter_collection.csv' | head -1) $(find $OUT/lba_fetch -name '*counter_collection.csv' | head -1) $(find $OUT/lba_write -name '*counter_collection.csv' | head -1) > $OUT/schur_pmc_summary.txt &&
 echo trace > $OUT/progress &&
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- python3 $R/bench.py --schur-pmc $OUT/r04_schur_pmc.json > $OUT/bench_under_trace.json 2> $OUT/trace.err
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- python3 $R/bench.py --no-wall --schur-pmc $OUT/r04_schur_pmc.json > $OUT/bench_under_trace.json 2> $OUT/trace.err
 echo "exit=$?"
