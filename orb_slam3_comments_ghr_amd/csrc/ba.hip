@@ -461,7 +461,7 @@ __global__ __launch_bounds__(EB) void k_schur_point(const LbaDev *__restrict__ D
 constexpr int SCH = 64;
 constexpr int RS = 200;  // blocks per row segment: 200 x 18 doubles = 28 KiB of LDS
 constexpr int RT = 512;  // threads per row-segment workgroup
-template <bool VALU>
+template <bool VALU, bool DIRECT = false>
 __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT);
@@ -607,6 +607,45 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__
 #pragma unroll
                     for (int c = 0; c < 3; c++) out[6 * (r0 + r) + c0 + c] = acc[3 * r + c];
             }
+        }
+        return;
+    }
+    if (DIRECT) {
+        // OSG_SCHUR_DIRECT=1: every lane loads its own element of Hpl_j straight from global memory
+        // (no LDS staging, no wave barrier), 16 contributions' loads issued before their MFMAs; the
+        // same operands in the same order as below, so the same sums
+        for (; t < t1; t += RT / 64) {
+            const i4 d2 = desc(t + 2 * (RT / 64));
+            const int nq = dc.z;
+            double acc0 = 0.0, acc1 = 0.0;
+            int v = 0;
+            for (; v + GC <= nq; v += GC) {
+                double bv[GC];
+#pragma unroll
+                for (int w = 0; w < GC; w++) {
+                    const int bj = __builtin_amdgcn_readlane(my_b, v + w);
+                    bv[w] = Hv[18 * (size_t)bj + boff];
+                }
+#pragma unroll
+                for (int w = 0; w < GC; w += 2) {
+                    const int r0 = __builtin_amdgcn_readlane(my_rank, v + w);
+                    const int r1 = __builtin_amdgcn_readlane(my_rank, v + w + 1);
+                    acc0 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[a_m * r0 + aoff], bv[w], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[a_m * r1 + aoff], bv[w + 1], acc1, 0, 0, 0);
+                }
+            }
+            for (; v < nq; v++) {  // the tail one at a time, even / odd contributions as above
+                const int bj = __builtin_amdgcn_readlane(my_b, v), rk = __builtin_amdgcn_readlane(my_rank, v);
+                const double b1 = Hv[18 * (size_t)bj + boff];
+                if (v & 1) acc1 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[a_m * rk + aoff], b1, acc1, 0, 0, 0);
+                else acc0 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[a_m * rk + aoff], b1, acc0, 0, 0, 0);
+            }
+            if (orow < 6 && ocol < 6) D.chunk_part[36 * (size_t)dc.x + 6 * orow + ocol] = acc0 + acc1;
+            dc = dn;
+            my_rank = n_rank;
+            my_b = n_b;
+            dn = d2;
+            contrib(dn, n_rank, n_b);
         }
         return;
     }
@@ -2235,6 +2274,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     static const bool schur_valu = getenv("OSG_SCHUR_VALU") && atoi(getenv("OSG_SCHUR_VALU")) != 0;
     // OSG_SCHUR_STAGE=1: partner spans staged in LDS (k_schur_rows_st), bit-identical
     static const bool schur_stage = getenv("OSG_SCHUR_STAGE") && atoi(getenv("OSG_SCHUR_STAGE")) != 0;
+    // OSG_SCHUR_DIRECT=1: Hpl_j operands loaded per lane from global memory (k_schur_rows<false, true>)
+    static const bool schur_direct = getenv("OSG_SCHUR_DIRECT") && atoi(getenv("OSG_SCHUR_DIRECT")) != 0;
     const auto tp0 = std::chrono::steady_clock::now();
     auto ms_since = [&](std::chrono::steady_clock::time_point t) {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
@@ -2513,6 +2554,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
             LBA_MARK(KT_SROWS);
             if (schur_valu) hipLaunchKernelGGL(k_schur_rows<true>, gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
             else if (schur_stage) hipLaunchKernelGGL(k_schur_rows_st, gx(mx_rs), dim3(RT2), 0, ctx->stream, d_dev);
+            else if (schur_direct)
+                hipLaunchKernelGGL((k_schur_rows<false, true>), gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
             else hipLaunchKernelGGL(k_schur_rows<false>, gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
             LBA_MARK(KT_SPAIRS);
             hipLaunchKernelGGL(k_schur_pairs, gx((int)(((size_t)mx_pairs * 64 + 255) / 256)), dim3(256), 0, ctx->stream, d_dev);

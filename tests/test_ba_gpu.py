@@ -221,7 +221,7 @@ def _lba_batch_graphs():
     return graphs
 
 
-@pytest.mark.parametrize("env", [{"OSG_SCHUR_STAGE": "1"}, {"OSG_SCHUR_STAGE": "0"}],
+@pytest.mark.parametrize("env", [{"OSG_SCHUR_STAGE": "1"}, {"OSG_SCHUR_DIRECT": "1"}],
                          ids=lambda e: "-".join(f"{k[4:]}={v}" for k, v in e.items()))
 def test_lba_schur_variants_bit_identical(ctx, env):
     """The Schur product's two MFMA forms (read once per process, so run in a child): the LDS-staged
