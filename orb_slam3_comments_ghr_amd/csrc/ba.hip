@@ -1794,7 +1794,8 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
     STRUCT_CP(2);
     // a map (one large graph per call) builds its structure on host workers; a window (many per batch,
     // each on its own worker) keeps the sequential passes.  Both give the same arrays.
-    const bool map_mode = nhp >= 512;
+    // (OSG_LBA_MAP_MODE=1 takes the map path for any graph: the host-runtime tests compare the two)
+    const bool map_mode = nhp >= 512 || (getenv("OSG_LBA_MAP_MODE") && atoi(getenv("OSG_LBA_MAP_MODE")) == 1);
     if (map_mode) {
         // blocks per landmark: unique free poses sorted by hessian index, counted then filled per
         // landmark range; the per-edge block code as below, settled landmark by landmark (a block's
