@@ -121,8 +121,9 @@ int osg_detect_batch(osg_ctx *ctx, const osg_image_pyramid *raw0, int32_t B, int
 
 // ---- host worker threads -------------------------------------------------------------------------
 // CPUs this process may run on at once: the smallest of the hardware threads, the affinity mask and
-// the cgroup CPU quota (a GPU box's container sees every core of the host but is granted a share);
-// OSG_HOST_THREADS overrides.  Cached after the first call.
+// the cgroup CPU quota (a GPU box's container sees every core of the host but is granted a share),
+// divided between torchrun's local ranks (LOCAL_WORLD_SIZE); OSG_HOST_THREADS overrides.  Cached
+// after the first call.
 int osg_host_cpus();
 // One process-wide pool of osg_host_cpus() - 1 persistent worker threads, shared by every context's
 // host phases: concurrent callers (one per host thread driving its own context) queue their loops on

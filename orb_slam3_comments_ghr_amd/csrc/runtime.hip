@@ -85,7 +85,8 @@ struct WorkerPool {
 };
 WorkerPool *pool()
 {
-    static WorkerPool *p = new WorkerPool(std::max(0, osg_host_cpus() - 1));
+    // no loop asks for more than 16 threads
+    static WorkerPool *p = new WorkerPool(std::max(0, std::min(osg_host_cpus(), 16) - 1));
     return p;
 }
 }  // namespace
@@ -100,6 +101,9 @@ int osg_host_cpus()
         if (sched_getaffinity(0, sizeof(set), &set) == 0) c = std::min(c, std::max(1, CPU_COUNT(&set)));
         const int q = cgroup_cpus();
         if (q > 0) c = std::min(c, q);
+        // one process per GPU (torchrun): the node's share is split between the local ranks
+        if (const char *lw = getenv("LOCAL_WORLD_SIZE"))
+            if (atoi(lw) > 1) c = std::max(1, c / atoi(lw));
         return c;
     }();
     return n;
