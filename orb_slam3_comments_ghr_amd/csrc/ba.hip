@@ -94,6 +94,9 @@ struct LbaDev {
     const int32_t *edge_blk;             // per edge: 4 block + 2 (block has several edges) + 1 (not its
                                          // first edge), or -1
     const int32_t *hp_e_start, *hp_e;    // edges per hessian pose
+    int nhe;                             // hp_e entries
+    int32_t *hp_rec;                     // per hp_e entry, 4 ints (k_hp_rec, once per call): edge, point,
+                                         // camera | kind << 16 | robust << 24, inverse sigma^2 bits
     const int32_t *hp_b;                 // blocks per hessian pose (hp_b_start on the host)
     const int32_t *pair_b;               // per contribution (a, b): its second block b
     int nchunks;
@@ -121,7 +124,8 @@ struct LbaDev {
     double *chi2o;                       // per edge chi2 of the last computed error (classification)
     double *err;                         // 3 per edge
     double *Hll, *bl, *Hpl, *Hpp, *bp;
-    double *Dinv, *db;
+    double *Dinv, *db;                   // k_schur_point's outputs (OSG_SCHUR_POINT=1 only)
+    int dinv_inline;                     // 1: k_schur_rows / k_update form Dinv from Hll themselves
     double *Hs, *bs, *x;
     double *Linv;                        // inverses of the 32x32 diagonal blocks of L, row-major per block row
     int npart;                           // partial slots per kind (>= ge, gu, gll + nhp)
@@ -166,6 +170,17 @@ __device__ inline double *new_point(const LbaDev &D) { return D.ctl->sel ? D.poi
 // The edge's Huber kernel; an edge without one (BundleAdjustment with bRobust = false,
 // ref:src/Optimizer.cc:3000-3007) gets an infinite delta, so rho = (e2, 1, 0) as g2o's unrobustified
 // chi2 / quadratic form
+__device__ inline void edge_delta_f(const LbaDev &D, bool robust, int kind, double &delta, float &dsqr)
+{
+    if (!robust) {
+        delta = __builtin_inf();
+        dsqr = __builtin_inff();
+        return;
+    }
+    const float d = (kind == OSG_EDGE_STEREO) ? D.hub_stereo : D.hub_mono;
+    delta = (double)d;
+    dsqr = (float)((double)d * (double)d);
+}
 __device__ inline void edge_delta(const LbaDev &D, int e, int kind, double &delta, float &dsqr)
 {
     if (D.e_robust && !D.e_robust[e]) {
@@ -329,7 +344,28 @@ __global__ __launch_bounds__(EB) void k_linearize(const LbaDev *__restrict__ Ds)
     }
 }
 
-// per free pose (one workgroup): Hpp (6x6) and b_p from its edges
+// The static inputs k_pose_red reads per edge, gathered once per call into pose-major records: one
+// 16-byte load per edge instead of five scattered loads (the edge arrays are in landmark order)
+__global__ __launch_bounds__(EB) void k_hp_rec(const LbaDev *__restrict__ Ds)
+{
+    // launched before the first step's control upload: no mode check
+    const bool xcd_map_ = Ds[0].xcd_map;
+    const int by = xcd_map_ ? (int)(blockIdx.x & 7) + 8 * (int)blockIdx.y : (int)blockIdx.y;
+    const int bx = xcd_map_ ? (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+    if (by >= Ds[0].n_graphs) return;
+    const LbaDev &D = Ds[by];
+    const int q = bx * EB + threadIdx.x;
+    if (q >= D.nhe) return;
+    const int e = D.hp_e[q];
+    const int robust = D.e_robust ? (D.e_robust[e] != 0) : 1;
+    const int meta = (D.e_cam[e] & 0xffff) | ((D.e_kind[e] & 0xff) << 16) | (robust << 24);
+    typedef int i4 __attribute__((ext_vector_type(4)));
+    *(i4 *)(D.hp_rec + 4 * (size_t)q) = i4{e, D.e_point[e], meta, __float_as_int(D.e_isig2[e])};
+}
+
+// per free pose (one workgroup): Hpp (6x6) and b_p from its edges.  REC: the edge inputs from the
+// pose-major records (default); false: gathered through hp_e (OSG_POSE_RED_GATHER=1, A/B runs)
+template <bool REC>
 __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_pose_red(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_LIN);
@@ -345,16 +381,33 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(3, 8))) void
     const SE3 T = se3_from7(cur_pose(D) + 7 * (size_t)D.hp_pose[i]);
     const double *points = cur_point(D);
     for (int q = D.hp_e_start[i] + threadIdx.x; q < D.hp_e_start[i + 1]; q += EB) {
-        const int e = D.hp_e[q];
-        const int k = D.e_kind[e];
+        int e, k, cam, pt;
+        bool robust;
+        double w;
+        if (REC) {
+            typedef int i4 __attribute__((ext_vector_type(4)));
+            const i4 r = *(const i4 *)(D.hp_rec + 4 * (size_t)q);
+            e = r.x;
+            pt = r.y;
+            cam = r.z & 0xffff;
+            k = (int)(int8_t)((r.z >> 16) & 0xff);
+            robust = (r.z >> 24) & 1;
+            w = (double)__int_as_float(r.w);
+        } else {
+            e = D.hp_e[q];
+            k = D.e_kind[e];
+            cam = D.e_cam[e];
+            pt = D.e_point[e];
+            robust = !(D.e_robust && !D.e_robust[e]);
+            w = edge_w(D, e);
+        }
         double Jp[3][6], Jx[3][3];
-        edge_jacobians(k, true, D.cams[D.e_cam[e]], T, points + 3 * (size_t)D.e_point[e], Jp, Jx);
+        edge_jacobians(k, true, D.cams[cam], T, points + 3 * (size_t)pt, Jp, Jx);
         const int dim = (k == OSG_EDGE_STEREO) ? 3 : 2;
-        const double w = edge_w(D, e);
         const double ev[3] = {D.err[3 * e], D.err[3 * e + 1], D.err[3 * e + 2]};
         double delta, r0, rho1;
         float dsqr;
-        edge_delta(D, e, k, delta, dsqr);
+        edge_delta_f(D, robust, k, delta, dsqr);
         huber(chi2_of(ev, dim, w), delta, dsqr, r0, rho1);
         const double ww = rho1 * w;
         double om[3];
@@ -425,22 +478,35 @@ __global__ void k_lambda_init(const LbaDev *__restrict__ Ds)
     D.ctl->lambda = 1e-5 * md;
 }
 
+// Dinv_l = (Hll_l + lambda I)^-1 and, with db, Dinv_l b_l (ref:Thirdparty/g2o/g2o/core/block_solver.hpp:
+// 381-395).  Formed where it is used (the BD staging of k_schur_rows, and k_update) instead of
+// written by a kernel of its own and read back: Hll is as many bytes as Dinv, so each reader's
+// traffic is unchanged, and k_schur_point's launch and its 107 MB per 64 C4 windows are gone.
+__device__ inline void landmark_dinv(const LbaDev &D, int l, double lambda, double *Di, double *db)
+{
+    double Dm[9];
+    for (int i = 0; i < 9; i++) Dm[i] = D.Hll[9 * (size_t)l + i];
+    Dm[0] += lambda;
+    Dm[4] += lambda;
+    Dm[8] += lambda;
+    inv3(Dm, Di);
+    if (db) {
+        const double *b = D.bl + 3 * (size_t)l;
+        for (int r = 0; r < 3; r++) db[r] = Di[3 * r] * b[0] + Di[3 * r + 1] * b[1] + Di[3 * r + 2] * b[2];
+    }
+}
+
+// the separate per-landmark pass (OSG_SCHUR_POINT=1, A/B runs): bit-identical
 __global__ __launch_bounds__(EB) void k_schur_point(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT);
     const double lambda = D.ctl->lambda;
     const int l = bx * EB + threadIdx.x;
     if (l >= D.nhl) return;
-    double Dm[9];
-    for (int i = 0; i < 9; i++) Dm[i] = D.Hll[9 * (size_t)l + i];
-    Dm[0] += lambda;
-    Dm[4] += lambda;
-    Dm[8] += lambda;
-    double Di[9];
-    inv3(Dm, Di);
+    double Di[9], db[3];
+    landmark_dinv(D, l, lambda, Di, db);
     for (int i = 0; i < 9; i++) D.Dinv[9 * (size_t)l + i] = Di[i];
-    const double *b = D.bl + 3 * (size_t)l;
-    for (int r = 0; r < 3; r++) D.db[3 * (size_t)l + r] = Di[3 * r] * b[0] + Di[3 * r + 1] * b[1] + Di[3 * r + 2] * b[2];
+    for (int r = 0; r < 3; r++) D.db[3 * (size_t)l + r] = db[r];
 }
 
 // Schur accumulation S_ij = sum_p BD_ip Hpl_jp^T (BD = Hpl Dinv) over the (block_i, block_j)
@@ -473,6 +539,7 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__
     const int rs = __builtin_amdgcn_readfirstlane(inf0.x);
     const int rb = __builtin_amdgcn_readfirstlane(inf0.z), hb0 = __builtin_amdgcn_readfirstlane(inf0.w);
     const int nr = __builtin_amdgcn_readfirstlane(inf1.x);
+    const double lam = D.ctl->lambda;
     __shared__ double s_bd[RS * 18 + 2];  // + a zero: the MFMA's K-padding lanes read it
     __shared__ double s_cf[RT / 64][6];
     if (threadIdx.x == 0) s_bd[RS * 18] = 0.0;
@@ -548,8 +615,12 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__
             const int a = gbl(D.hp_b)[hb0 + rb + r];
             const int l = gbl(D.hp_b_lm)[hb0 + rb + r];
             double Di[9], db[3], B[9];
-            for (int k = 0; k < 9; k++) Di[k] = gbl(D.Dinv)[9 * (size_t)l + k];
-            for (int k = 0; k < 3; k++) db[k] = gbl(D.db)[3 * (size_t)l + k];
+            if (D.dinv_inline) {
+                landmark_dinv(D, l, lam, Di, db);
+            } else {
+                for (int k = 0; k < 9; k++) Di[k] = gbl(D.Dinv)[9 * (size_t)l + k];
+                for (int k = 0; k < 3; k++) db[k] = gbl(D.db)[3 * (size_t)l + k];
+            }
             for (int k = 0; k < 9; k++) B[k] = gbl(D.Hpl)[18 * (size_t)a + 9 * h + k];
             double *BD = s_bd + 18 * r + 9 * h;
             for (int rr = 0; rr < 3; rr++) {
@@ -789,8 +860,12 @@ __global__ __launch_bounds__(RT2, 1) void k_schur_rows_st(const LbaDev *__restri
             const int l = gbl(D.hp_b_lm)[hb0 + rb + r];
             const int p0 = s_pre[r];
             double Di[9], db[3], B[9];
-            for (int k = 0; k < 9; k++) Di[k] = gbl(D.Dinv)[9 * (size_t)l + k];
-            for (int k = 0; k < 3; k++) db[k] = gbl(D.db)[3 * (size_t)l + k];
+            if (D.dinv_inline) {
+                landmark_dinv(D, l, D.ctl->lambda, Di, db);
+            } else {
+                for (int k = 0; k < 9; k++) Di[k] = gbl(D.Dinv)[9 * (size_t)l + k];
+                for (int k = 0; k < 3; k++) db[k] = gbl(D.db)[3 * (size_t)l + k];
+            }
             if (p0 < SPAN_CAP)
                 for (int k = 0; k < 9; k++) B[k] = s_span[18 * (size_t)p0 + 9 * h + k];
             else
@@ -1490,7 +1565,13 @@ __global__ __launch_bounds__(EB) void k_back_copy(const LbaDev *__restrict__ Ds)
     if (i < n) D.x[i] = D.bs[i];
 }
 
-// landmark back-substitution + new estimates + LM scale partials
+// landmark back-substitution + new estimates + LM scale partials.  STAGE (default): the workgroup's
+// Hpl blocks (its EB landmarks' blocks are consecutive) come through LDS in UB-block pieces read with
+// coalesced 16-byte loads, instead of each thread walking its own blocks' 18 doubles (64 cache lines
+// per load instruction); the per-landmark sums are the same expressions in the same order.
+// OSG_UPDATE_DIRECT=1: the per-thread reads (A/B runs), bit-identical.
+constexpr int UB = 256;  // blocks per staged piece: 36 KiB of LDS
+template <bool STAGE>
 __global__ __launch_bounds__(EB) void k_update(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT);
@@ -1502,19 +1583,55 @@ __global__ __launch_bounds__(EB) void k_update(const LbaDev *__restrict__ Ds)
     const int t = bx * EB + threadIdx.x;
     const int sp = 6 * D.nhp;
     double sc = 0.0;
+    double cl[3] = {0, 0, 0};
+    if (t < D.nhl) {
+        cl[0] = D.bl[3 * (size_t)t];
+        cl[1] = D.bl[3 * (size_t)t + 1];
+        cl[2] = D.bl[3 * (size_t)t + 2];
+    }
+    if (STAGE) {
+        __shared__ double s_b[UB * 18];
+        typedef int i4 __attribute__((ext_vector_type(4)));
+        const int l0 = bx * EB;
+        const int g0 = l0 < D.nhl ? D.lm_b_start[l0] : 0;
+        const int g1 = l0 < D.nhl ? D.lm_b_start[min(l0 + EB, D.nhl)] : 0;
+        const int mb0 = t < D.nhl ? D.lm_b_start[t] : 0, mb1 = t < D.nhl ? D.lm_b_start[t + 1] : 0;
+        for (int p0 = g0; p0 < g1; p0 += UB) {  // workgroup-uniform
+            const int nb = min(UB, g1 - p0);
+            const i4 *src = (const i4 *)(D.Hpl + 18 * (size_t)p0);
+            for (int k = threadIdx.x; k < 9 * nb; k += EB) ((i4 *)s_b)[k] = src[k];
+            __syncthreads();
+            const int a1 = min(mb1, p0 + nb);
+            for (int blk = max(mb0, p0); blk < a1; blk++) {
+                const int i1 = D.blk_pose[blk];
+                const double *B = s_b + 18 * (blk - p0);
+                for (int c = 0; c < 3; c++) {
+                    double s_ = 0;
+                    for (int r = 0; r < 6; r++) s_ += B[3 * r + c] * (-D.x[6 * i1 + r]);
+                    cl[c] += s_;
+                }
+            }
+            __syncthreads();
+        }
+    }
     if (t < D.nhl) {
         const int l = t;
-        double cl[3] = {D.bl[3 * (size_t)l], D.bl[3 * (size_t)l + 1], D.bl[3 * (size_t)l + 2]};
-        for (int blk = D.lm_b_start[l]; blk < D.lm_b_start[l + 1]; blk++) {
-            const int i1 = D.blk_pose[blk];
-            const double *B = D.Hpl + 18 * (size_t)blk;
-            for (int c = 0; c < 3; c++) {
-                double s_ = 0;
-                for (int r = 0; r < 6; r++) s_ += B[3 * r + c] * (-D.x[6 * i1 + r]);
-                cl[c] += s_;
+        if (!STAGE)
+            for (int blk = D.lm_b_start[l]; blk < D.lm_b_start[l + 1]; blk++) {
+                const int i1 = D.blk_pose[blk];
+                const double *B = D.Hpl + 18 * (size_t)blk;
+                for (int c = 0; c < 3; c++) {
+                    double s_ = 0;
+                    for (int r = 0; r < 6; r++) s_ += B[3 * r + c] * (-D.x[6 * i1 + r]);
+                    cl[c] += s_;
+                }
             }
-        }
+        double Dv[9];
         const double *Di = D.Dinv + 9 * (size_t)l;
+        if (D.dinv_inline) {
+            landmark_dinv(D, l, lambda, Dv, nullptr);
+            Di = Dv;
+        }
         const int p = D.hl_point[l];
         for (int r = 0; r < 3; r++) {
             const double xl = Di[3 * r] * cl[0] + Di[3 * r + 1] * cl[1] + Di[3 * r + 2] * cl[2];
@@ -2239,7 +2356,9 @@ void carve_state(char *base, size_t &off, const LbaHost &H, LbaDev *D, bool prof
     unsigned long long *ts = prof_ts ? carve<unsigned long long>(base, off, 8 * 2 * 64 + 64) : nullptr;
     double *chi2o = carve<double>(base, off, (size_t)std::max(ne, 1));
     uint8_t *bad = carve<uint8_t>(base, off, ne);
+    int32_t *hp_rec = carve<int32_t>(base, off, 4 * std::max<size_t>(H.hp_e.size(), 1));
     if (!D) return;
+    D->hp_rec = hp_rec;
     D->poseA = pA;
     D->poseB = pB;
     D->pointA = qA;
@@ -2277,6 +2396,12 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     static const bool schur_stage = getenv("OSG_SCHUR_STAGE") && atoi(getenv("OSG_SCHUR_STAGE")) != 0;
     // OSG_SCHUR_DIRECT=1: Hpl_j operands loaded per lane from global memory (k_schur_rows<false, true>)
     static const bool schur_direct = getenv("OSG_SCHUR_DIRECT") && atoi(getenv("OSG_SCHUR_DIRECT")) != 0;
+    // OSG_POSE_RED_GATHER=1: k_pose_red gathers its edge inputs through hp_e (A/B runs), bit-identical
+    static const bool pose_red_gather = getenv("OSG_POSE_RED_GATHER") && atoi(getenv("OSG_POSE_RED_GATHER")) != 0;
+    // OSG_UPDATE_DIRECT=1: k_update reads each landmark's Hpl blocks per thread (A/B runs), bit-identical
+    // OSG_SCHUR_POINT=1: Dinv and Dinv b_l from a kernel of their own (A/B runs), bit-identical
+    static const bool schur_point = getenv("OSG_SCHUR_POINT") && atoi(getenv("OSG_SCHUR_POINT")) != 0;
+    static const bool update_direct = getenv("OSG_UPDATE_DIRECT") && atoi(getenv("OSG_UPDATE_DIRECT")) != 0;
     const auto tp0 = std::chrono::steady_clock::now();
     auto ms_since = [&](std::chrono::steady_clock::time_point t) {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
@@ -2408,6 +2533,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(din, pin, pk.total, hipMemcpyHostToDevice, ctx->stream));
     int mx_gll = 1;
     bool any_multi = false;
+    int mx_nhe = 0;
     int mx_ge = 0, mx_gl = 1, mx_gu = 0, mx_nblk = 0, mx_nhp = 0, mx_chunks = 0, mx_pairs = 0, mx_red = 0, mx_rs = 0;
     // XCD-aware graph placement (LBA_GRAPH) for batches of >= 8 graphs: OSG_LBA_XCD=1.  Off by
     // default: measured slower (64 C4 windows: k_schur_rows 10.4 vs 8.9 ms, k_linearize 5.4 vs 4.4 ms
@@ -2456,6 +2582,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         D.edge_blk = osg_dptr<int32_t>(din, o.eblk);
         D.hp_e_start = osg_dptr<int32_t>(din, o.hpes);
         D.hp_e = osg_dptr<int32_t>(din, o.hpe);
+        D.nhe = (int)h.hp_e.size();
         D.hp_b = osg_dptr<int32_t>(din, o.hpb);
         D.pair_b = osg_dptr<int32_t>(din, o.pairb);
         D.nchunks = h.nchunks;
@@ -2482,6 +2609,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         D.gu = h.gu;
         D.nblk_red = h.nblk_red;
         D.user_lambda = h.G->user_lambda_init;
+        D.dinv_inline = schur_point ? 0 : 1;
         size_t off = 0;
         carve_state(dst + st_off[a], off, h, &D, prof_ts);
         D.ctl = d_ctl + a;
@@ -2495,12 +2623,17 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         mx_gu = std::max(mx_gu, h.gu);
         mx_nblk = std::max(mx_nblk, h.nblk);
         mx_nhp = std::max(mx_nhp, h.nhp);
+        mx_nhe = std::max(mx_nhe, (int)h.hp_e.size());
         mx_chunks = std::max(mx_chunks, h.nchunks);
         mx_rs = std::max(mx_rs, h.n_rs);
         mx_pairs = std::max(mx_pairs, h.col_rows_start.empty() ? h.npairs : (int)h.live_pairs.size());
         mx_red = std::max(mx_red, h.nblk_red);
     }
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(d_dev, h_dev, dev_bytes, hipMemcpyHostToDevice, ctx->stream));
+    if (mx_nhe > 0 && !pose_red_gather) {
+        const dim3 g = xcd ? dim3(8 * ((mx_nhe + EB - 1) / EB), (NA + 7) / 8) : dim3((mx_nhe + EB - 1) / EB, NA);
+        hipLaunchKernelGGL(k_hp_rec, g, dim3(EB), 0, ctx->stream, d_dev);
+    }
     const double t_upload = ms_since(tp0) - t_struct;
     const auto tp1 = std::chrono::steady_clock::now();
 
@@ -2546,11 +2679,14 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         if (any_multi) hipLaunchKernelGGL(k_linearize<true>, gx(mx_gll), dim3(EB), 0, ctx->stream, d_dev);
         else hipLaunchKernelGGL(k_linearize<false>, gx(mx_gll), dim3(EB), 0, ctx->stream, d_dev);
         LBA_MARK(KT_POSE);
-        if (mx_nhp > 0) hipLaunchKernelGGL(k_pose_red, gx(mx_nhp), dim3(EB), 0, ctx->stream, d_dev);
+        if (mx_nhp > 0) {
+            if (pose_red_gather) hipLaunchKernelGGL(k_pose_red<false>, gx(mx_nhp), dim3(EB), 0, ctx->stream, d_dev);
+            else hipLaunchKernelGGL(k_pose_red<true>, gx(mx_nhp), dim3(EB), 0, ctx->stream, d_dev);
+        }
         LBA_MARK(KT_LINIT);
         hipLaunchKernelGGL(k_lambda_init, yb, dim3(64), 0, ctx->stream, d_dev);
         LBA_MARK(KT_SPOINT);
-        hipLaunchKernelGGL(k_schur_point, gx(mx_gl), dim3(EB), 0, ctx->stream, d_dev);
+        if (schur_point) hipLaunchKernelGGL(k_schur_point, gx(mx_gl), dim3(EB), 0, ctx->stream, d_dev);
         if (mx_nhp > 0) {
             LBA_MARK(KT_SROWS);
             if (schur_valu) hipLaunchKernelGGL(k_schur_rows<true>, gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
@@ -2594,7 +2730,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
             }
         }
         LBA_MARK(KT_UPD);
-        hipLaunchKernelGGL(k_update, gx(mx_gu), dim3(EB), 0, ctx->stream, d_dev);
+        if (update_direct) hipLaunchKernelGGL(k_update<false>, gx(mx_gu), dim3(EB), 0, ctx->stream, d_dev);
+        else hipLaunchKernelGGL(k_update<true>, gx(mx_gu), dim3(EB), 0, ctx->stream, d_dev);
         LBA_MARK(KT_ERR);
         hipLaunchKernelGGL(k_errors, gx(mx_ge), dim3(EB), 0, ctx->stream, d_dev, 0);
         LBA_MARK(KT_RED);

@@ -221,19 +221,30 @@ def _lba_batch_graphs():
     return graphs
 
 
-@pytest.mark.parametrize("env", [{"OSG_SCHUR_STAGE": "1"}, {"OSG_SCHUR_DIRECT": "1"}],
+def _gba_variant_graph():
+    rng = np.random.default_rng(3000 + 30)
+    return op.synth_gba_graph(rng, n_kf=30, n_points=3000, bRobust=False, stereo_frac=0.3)
+
+
+@pytest.mark.parametrize("env", [{"OSG_SCHUR_STAGE": "1"}, {"OSG_SCHUR_DIRECT": "1"}, {"OSG_POSE_RED_GATHER": "1"},
+                                 {"OSG_UPDATE_DIRECT": "1"}, {"OSG_SCHUR_POINT": "1"}],
                          ids=lambda e: "-".join(f"{k[4:]}={v}" for k, v in e.items()))
 def test_lba_schur_variants_bit_identical(ctx, env):
-    """The Schur product's two MFMA forms (read once per process, so run in a child): the LDS-staged
-    partner spans (k_schur_rows_st) and the per-group gathers (k_schur_rows) give the same results bit
-    for bit (the same products in the same order)."""
+    """Kernel variants that read their inputs differently but compute the same products in the same
+    order (read once per process, so run in a child) give the same results bit for bit: the Schur
+    product's LDS-staged partner spans (k_schur_rows_st) and per-lane loads against the per-group
+    gathers (k_schur_rows), k_pose_red's edge inputs gathered through hp_e against the pose-major
+    records (k_hp_rec), k_update's Hpl blocks read per thread against the LDS-staged pieces, and
+    Dinv from k_schur_point against Dinv formed by its readers.  The GBA graph has per-edge robust flags off (bRobust = false)."""
     import subprocess
     import sys
     out = f"/tmp/_osg_lba_variant_{os.getpid()}.npz"
     code = ("import numpy as np\n"
             "from orb_slam3_comments_ghr_amd import Context, optimizer as op\n"
             "from tests.test_ba_gpu import _lba_batch_graphs\n"
-            "res = op.Optimizer(Context(0)).LocalBundleAdjustmentBatch(_lba_batch_graphs())\n"
+            "from tests.test_ba_gpu import _gba_variant_graph\n"
+            "o = op.Optimizer(Context(0))\n"
+            "res = o.LocalBundleAdjustmentBatch(_lba_batch_graphs()) + [o.BundleAdjustment(_gba_variant_graph())]\n"
             f"np.savez('{out}', **{{f'p{{i}}': r.pose for i, r in enumerate(res)}},\n"
             "         **{f'q{i}': r.point for i, r in enumerate(res)},\n"
             "         it=np.array([[r.iterations, r.trials] for r in res]),\n"
@@ -244,7 +255,8 @@ def test_lba_schur_variants_bit_identical(ctx, env):
     assert r.returncode == 0, r.stderr[-2000:]
     got = np.load(out)
     os.remove(out)
-    res = op.Optimizer(ctx).LocalBundleAdjustmentBatch(_lba_batch_graphs())
+    o = op.Optimizer(ctx)
+    res = o.LocalBundleAdjustmentBatch(_lba_batch_graphs()) + [o.BundleAdjustment(_gba_variant_graph())]
     np.testing.assert_array_equal(got["it"], [[r.iterations, r.trials] for r in res])
     np.testing.assert_array_equal(got["chi"], [[r.chi2_initial, r.chi2_final] for r in res])
     for i, r in enumerate(res):
