@@ -512,8 +512,9 @@ def bench_lba(ctx, rank, world, dist, dev, args):
     blocks = sum(c["blocks"] for c in counts)
     lms = sum(c["landmarks"] for c in counts)
     # k_schur_rows per launch: S_ij products (36 x 3 FMA per contribution), BD = Hpl Dinv and the
-    # b_schur share per block (18 x 3 + 6 x 3 FMA); bytes: Hpl, Dinv and Dinv b_l read once, 12 B of
-    # (rank, block) per contribution, one 6x6 chunk partial per 64 contributions written
+    # b_schur share per block (18 x 3 + 6 x 3 FMA); bytes: Hpl, and Hll and b_l (Dinv and Dinv b_l are
+    # formed in the staging since late r04; the same bytes as reading them) once, 12 B of (rank, block)
+    # per contribution, one 6x6 chunk partial per 64 contributions written
     sr_flop = 2.0 * (contrib * 108 + blocks * 72)
     sr_bytes = blocks * 144 + lms * 96 + contrib * 12 + (contrib / 64.0) * 288
     sr_s = kt["schur_rows"][0] / 1e3 / steps

@@ -1,7 +1,7 @@
 """Batched LocalBundleAdjustment throughput (SURVEY.md §8d C4, B windows per GPU in lockstep):
 LM iterations per wall second for B = 1 .. 64, and with T host threads each driving its own context
 (own HIP stream) so that one thread's structure build / packing overlaps another's device steps.
-Run on the GPU box:  BS=1,64 TS=1,2,3 python tools/lba_batch_bench.py"""
+Run on the GPU box:  BS=1,64 TS=1,2,3 python tools/lba_batch_bench.py  (REPS: calls per thread)"""
 import os
 import sys
 import threading
@@ -25,7 +25,7 @@ def main():
             graphs = [pool[i % len(pool)] for i in range(B)]
             for o in opts[:T]:
                 o.LocalBundleAdjustmentBatch(graphs)
-            reps = max(2, 8 // B)
+            reps = int(os.environ.get("REPS", max(2, 8 // B)))
             its = [0] * T
 
             def run(t):
