@@ -15,9 +15,11 @@
 //   k_errors      per edge: error, Huber rho -> per-workgroup chi2 partials        (HBM/latency)
 //   k_linearize   per landmark: its edges' Jacobians -> Hll, b_l, the Hpl blocks   (FP64 VALU)
 //   k_pose_red    per pose: Hpp, b_p from its edges' pose Jacobians, recomputed in place (a
-//                 workgroup reduction; no per-edge contribution round trip through HBM)
+//                 workgroup reduction; no per-edge contribution round trip through HBM), its edge
+//                 inputs from pose-major records (k_hp_rec, once per call)
 // Per LM trial:
-//   k_schur_point  per landmark: Dinv = (Hll + lambda I)^-1, Dinv b_l
+//   (k_schur_point per landmark: Dinv = (Hll + lambda I)^-1, Dinv b_l; only with OSG_SCHUR_POINT=1:
+//                 by default k_schur_rows and k_update form Dinv from Hll themselves)
 //   k_schur_rows   per row segment (pose i, 200 of its blocks): BD = Hpl Dinv staged in LDS, the
 //                 segment's chunks of S_ij = sum_p BD_ip Hpl_jp^T on FP64 MFMA (v_mfma_f64_4x4x4f64,
 //                 one contribution per instruction; OSG_SCHUR_VALU=1: the VALU form) and its share
