@@ -1567,11 +1567,12 @@ __global__ __launch_bounds__(EB) void k_back_copy(const LbaDev *__restrict__ Ds)
     if (i < n) D.x[i] = D.bs[i];
 }
 
-// landmark back-substitution + new estimates + LM scale partials.  STAGE (default): the workgroup's
-// Hpl blocks (its EB landmarks' blocks are consecutive) come through LDS in UB-block pieces read with
-// coalesced 16-byte loads, instead of each thread walking its own blocks' 18 doubles (64 cache lines
-// per load instruction); the per-landmark sums are the same expressions in the same order.
-// OSG_UPDATE_DIRECT=1: the per-thread reads (A/B runs), bit-identical.
+// landmark back-substitution + new estimates + LM scale partials.  Each thread walks its landmark's
+// Hpl blocks (16-byte loads, many in flight per thread).  STAGE (OSG_UPDATE_STAGE=1, A/B runs,
+// bit-identical): the workgroup's Hpl blocks (its EB landmarks' blocks are consecutive) come through
+// LDS in UB-block pieces read with coalesced 16-byte loads; measured slower (2.34 against 2.08 ms per
+// 14 launches of 64 C4 windows, profiles/r04_lba_dinv_ab.txt): the pieces serialise load, barrier
+// and compute, where the per-thread walks keep more loads in flight.
 constexpr int UB = 256;  // blocks per staged piece: 36 KiB of LDS
 template <bool STAGE>
 __global__ __launch_bounds__(EB) void k_update(const LbaDev *__restrict__ Ds)
@@ -2400,10 +2401,10 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     static const bool schur_direct = getenv("OSG_SCHUR_DIRECT") && atoi(getenv("OSG_SCHUR_DIRECT")) != 0;
     // OSG_POSE_RED_GATHER=1: k_pose_red gathers its edge inputs through hp_e (A/B runs), bit-identical
     static const bool pose_red_gather = getenv("OSG_POSE_RED_GATHER") && atoi(getenv("OSG_POSE_RED_GATHER")) != 0;
-    // OSG_UPDATE_DIRECT=1: k_update reads each landmark's Hpl blocks per thread (A/B runs), bit-identical
+    // OSG_UPDATE_STAGE=1: k_update reads Hpl through LDS pieces (A/B runs), bit-identical
     // OSG_SCHUR_POINT=1: Dinv and Dinv b_l from a kernel of their own (A/B runs), bit-identical
     static const bool schur_point = getenv("OSG_SCHUR_POINT") && atoi(getenv("OSG_SCHUR_POINT")) != 0;
-    static const bool update_direct = getenv("OSG_UPDATE_DIRECT") && atoi(getenv("OSG_UPDATE_DIRECT")) != 0;
+    static const bool update_stage = getenv("OSG_UPDATE_STAGE") && atoi(getenv("OSG_UPDATE_STAGE")) != 0;
     const auto tp0 = std::chrono::steady_clock::now();
     auto ms_since = [&](std::chrono::steady_clock::time_point t) {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
@@ -2732,8 +2733,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
             }
         }
         LBA_MARK(KT_UPD);
-        if (update_direct) hipLaunchKernelGGL(k_update<false>, gx(mx_gu), dim3(EB), 0, ctx->stream, d_dev);
-        else hipLaunchKernelGGL(k_update<true>, gx(mx_gu), dim3(EB), 0, ctx->stream, d_dev);
+        if (update_stage) hipLaunchKernelGGL(k_update<true>, gx(mx_gu), dim3(EB), 0, ctx->stream, d_dev);
+        else hipLaunchKernelGGL(k_update<false>, gx(mx_gu), dim3(EB), 0, ctx->stream, d_dev);
         LBA_MARK(KT_ERR);
         hipLaunchKernelGGL(k_errors, gx(mx_ge), dim3(EB), 0, ctx->stream, d_dev, 0);
         LBA_MARK(KT_RED);
