@@ -108,7 +108,7 @@ def parse():
                     help="per-launch HBM traffic from the rocprofv3 PMC passes (tools/gpu/gpu_profile_r03.sh)")
     ap.add_argument("--valu-pmc", default=os.path.join(ROOT, "profiles", "r03_top2_valu_pmc.json"),
                     help="the headline kernel's VALU counters (tools/pmc_valu.py)")
-    ap.add_argument("--schur-pmc", default=os.path.join(ROOT, "profiles", "r04_schur_pmc.json"),
+    ap.add_argument("--schur-pmc", default=os.path.join(ROOT, "profiles", "r04b_lba_pmc.json"),
                     help="the LBA engine's SQ / MFMA / HBM counters (tools/pmc_kernel_summary.py)")
     return ap.parse_args()
 
@@ -521,7 +521,8 @@ def bench_lba(ctx, rank, world, dist, dev, args):
     kernels = {k: round(v[0] / max(1, v[1]), 4) for k, v in kt.items() if v[1]}
     dom = max(kernels, key=kernels.get)
     pmc = _load_json(args.schur_pmc)
-    pmc_sr = next((v for k, v in pmc.items() if k.startswith("k_schur_rows<false>")), {})
+    # the MFMA form: "k_schur_rows<false>" (r03 / r04 files) or "k_schur_rows<false, false>" (late r04)
+    pmc_sr = next((v for k, v in pmc.items() if k in ("k_schur_rows<false>", "k_schur_rows<false, false>")), {})
     flop_iter = 72.6e6
     res = {
         "metric": "LocalBA iters/s", "value": round(bval, 1), "unit": "LM iterations/s",
