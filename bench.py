@@ -52,6 +52,11 @@ PEAK_I8_TOPS = 256 * 4 * 1024 * 2 * 2.4e9 / 1e12
 I8_OPS_PER_PAIR = 512          # 256 MACs per (query, train row) pair
 MFMA_EPILOGUE_VALU_PER_PAIR = 2  # v_med3_i32 + v_min_i32 on the accumulator's packed key
 MFMA_MAX_ROWS = 8192           # the I8 kernel's 13-bit row field (osg_top2_mfma_max_rows)
+# OSG_TOP2_MFMA_SHAPE -> k_top2_mfma<NW, QT, CR, PIPE>, as osg_launch_top2_batch_mfma's switch
+# (csrc/hamming_mfma.hip); any other value takes the default
+MFMA_SHAPES = {"0": (16, 1, 256, 1), "1": (8, 2, 256, 1), "2": (16, 1, 256, 0), "3": (8, 2, 256, 0),
+               "4": (8, 1, 256, 1)}
+LINE_MAX_BYTES = 8192          # the stdout line's budget (the driver did not parse r04's 21 KB line)
 
 
 def job_totals(elapsed, units, world, dist=None, device="cpu"):
@@ -110,6 +115,8 @@ def parse():
                     help="the headline kernel's VALU counters (tools/pmc_valu.py)")
     ap.add_argument("--schur-pmc", default=os.path.join(ROOT, "profiles", "r04b_lba_pmc.json"),
                     help="the LBA engine's SQ / MFMA / HBM counters (tools/pmc_kernel_summary.py)")
+    ap.add_argument("--detail", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
+                    help="file for the full per-stage record (stdout carries the compact line); '' for none")
     return ap.parse_args()
 
 
@@ -229,10 +236,10 @@ def main():
     alg_bytes = B * ((nq + nt) * 32 + nq * 12)
     mfma = os.environ.get("OSG_TOP2_BATCH_MFMA", "1") != "0" and 1 <= nt <= MFMA_MAX_ROWS
     if mfma:
-        shape = {"0": (16, 1, 256), "1": (8, 2, 256), "2": (8, 1, 128), "3": (8, 2, 128)}[
-            os.environ.get("OSG_TOP2_MFMA_SHAPE", "0")]
+        shape = MFMA_SHAPES.get(os.environ.get("OSG_TOP2_MFMA_SHAPE", "0"), MFMA_SHAPES["0"])
         per_wg = shape[0] * shape[1] * 32
-        kname = f"k_top2_mfma<{shape[0]},{shape[1]},{shape[2]}> grid={(nq + per_wg - 1) // per_wg * B} x {shape[0] * 64}"
+        kname = (f"k_top2_mfma<{shape[0]},{shape[1]},{shape[2]},{shape[3]}> "
+                 f"grid={(nq + per_wg - 1) // per_wg * B} x {shape[0] * 64}")
         ksub = "k_top2_mfma"
         achieved = pairs_per_step * I8_OPS_PER_PAIR / (k_us * 1e-6) / 1e12
         epi = pairs_per_step * MFMA_EPILOGUE_VALU_PER_PAIR / (k_us * 1e-6) / 1e12
@@ -375,6 +382,10 @@ def main():
         except Exception as e:  # a failing secondary stage must not cost the headline line
             import traceback
             traceback.print_exc(file=sys.stderr)
+            if world > 1:
+                # the stages call collectives: a rank that skipped ahead would pair its next reduction
+                # with a peer still inside this stage, so a multi-rank run ends here
+                raise
             out[key] = {"error": f"{type(e).__name__}: {e}"[:500]}
 
     if not args.no_frames:
@@ -396,10 +407,75 @@ def main():
             stage("global_ba_loop", lambda *a: bench_gba_map(*a, loop=True))
 
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        # the full record goes to a file (mirrored under profiles/ by the GPU scripts); stdout carries
+        # one compact line the driver can parse (the 21 KB line was not parsed)
+        out["detail_file"] = os.path.relpath(args.detail, ROOT) if args.detail else None
+        if args.detail:
+            os.makedirs(os.path.dirname(os.path.abspath(args.detail)), exist_ok=True)
+            with open(args.detail, "w") as f:
+                json.dump(out, f, indent=1)
+        print(compact_line(out), flush=True)
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+_LINE_HEAD = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data")
+_LINE_ROOF = ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic", "kernel_us",
+              "algorithmic_ops_per_launch", "algorithmic_flop_per_launch", "algorithmic_bytes_per_launch",
+              "mfma_busy_frac_pmc")
+_LINE_CPU = ("value", "unit", "cores", "kind", "value_1thread", "sample")
+_LINE_STAGE = ("value", "unit", "speedup_vs_cpu", "speedup_vs_cpu_1thread", "kernel_frames_per_s",
+               "kernel_speedup_vs_cpu", "ms_per_call", "s_per_gba", "peak_device_bytes", "error")
+
+
+def _short(v, n):
+    return v[:n - 3] + "..." if isinstance(v, str) and len(v) > n else v
+
+
+def _pick(d, keys, n):
+    return {k: _short(d[k], n) for k in keys if isinstance(d, dict) and k in d}
+
+
+def compact_line(out, limit=LINE_MAX_BYTES):
+    """The one JSON line bench.py prints: the headline keys, the dominant kernel's roofline, the CPU
+    baseline, and per secondary stage its value, unit, speedup and (where it has one) its kernel's
+    roofline fraction -- at most `limit` bytes.  The full record is the --detail file.  Strings are
+    shortened first, then the stages' extras, until the line fits."""
+    for n, full in ((160, True), (72, True), (40, False)):
+        line = {k: _short(out[k], n) for k in _LINE_HEAD if k in out}
+        line["config"] = {k: _short(v, n) for k, v in out.get("config", {}).items()}
+        line["roofline"] = _pick(out.get("roofline", {}), _LINE_ROOF, n)
+        if "cpu_baseline" in out:
+            line["cpu_baseline"] = _pick(out["cpu_baseline"], _LINE_CPU, n)
+        for k in ("speedup_vs_cpu", "speedup_vs_cpu_1thread", "speedup_vs_cpu_node_estimate",
+                  "batch_frame0_equals_single"):
+            if k in out:
+                line[k] = out[k]
+        if full and "single_launch" in out:
+            line["single_launch"] = _pick(out["single_launch"], ("kernel", "kernel_us", "Mmatches_per_s_kernel"), n)
+        if "roofline_stream" in out:
+            line["roofline_stream"] = _pick(out["roofline_stream"], ("bound", "achieved", "peak", "unit", "frac",
+                                                                     "traffic", "kernel_us"), n)
+        if "stream_train_sharded" in out:
+            line["stream_train_sharded"] = _pick(out["stream_train_sharded"], ("value", "unit", "n_gpus"), n)
+        for key, st in out.items():
+            if not (isinstance(st, dict) and key.startswith(("frames_", "local_ba", "global_ba"))):
+                continue
+            s = _pick(st, _LINE_STAGE if full else ("value", "unit", "speedup_vs_cpu", "error"), n)
+            if "roofline" in st:
+                s["roofline"] = _pick(st["roofline"], ("frac", "kernel_us", "traffic", "mfma_busy_frac_pmc")
+                                      if full else ("frac", "kernel_us"), n)
+            if full and "cpu_baseline" in st:
+                s["cpu"] = _pick(st["cpu_baseline"], ("value", "cores", "kind"), n)
+            line[key] = s
+        if "detail_file" in out:
+            line["detail_file"] = out["detail_file"]
+        text = json.dumps(line, separators=(",", ":"))
+        if len(text.encode()) <= limit:
+            return text
+    raise ValueError(f"bench line of {len(text.encode())} B exceeds {limit} B")
 
 
 def bench_stream_sharded(ctx, dist, dev, stream, sq, st, world, rank, steps=20):
@@ -715,6 +791,12 @@ def bench_gba_map(ctx, rank, world, dist, dev, args, loop=False):
 _ORACLE = []
 
 
+def _ref_pattern():
+    """The reference's own BRIEF table (ref:src/ORBextractor.cc:212, data in tests/golden/)."""
+    from tests import golden_data
+    return golden_data.bit_pattern_31()
+
+
 def _oracle():
     """The CPU oracle (test infrastructure), loaded only by the cpu_baseline legs.  It times the
     reference's own arithmetic: the host libm's sin / cos / pow / atan2 (oracle_set_libm), not the
@@ -833,31 +915,45 @@ def _frame_batches(ctx, rank, world, dist, dev, args, steps, cpu_worker, label, 
     return res
 
 
-def _cpp_wall(res, workload, arrays, expect, args, rank, world):
+def _cpp_wall(res, workload, arrays, expect, args, rank, world, dist=None, dev=None):
     """The drop-in's wall rate as ORB-SLAM3 would see it: tools/adapter_wall_bench (C++) gathers mock
     Frames / KeyFrames / MapPoints through adapters/orbslam3/osg_orbslam3.h's batched entries, calls the
     C-ABI with host inputs and writes the results back into the objects, on --wall-threads host
     threads with one context each.  `arrays` is the problem pool (tools/adapter_arrays.py);
     `expect` maps each recorded per-frame result to the kernel-only path's values on the same pool,
-    and `equals_kernel_path` says whether the adapter run reproduced them.  Rank 0 at N = 1 only."""
-    if args.no_wall or rank != 0 or world != 1:
+    and `equals_kernel_path` says whether the adapter run reproduced them.  Every rank runs it on its
+    own GPU (HIP_VISIBLE_DEVICES = LOCAL_RANK for the child); the whole-job rate is all ranks' frames
+    over the slowest rank's wall time.  The one-frame latency runs on rank 0."""
+    if args.no_wall:
         return
     import subprocess
     import tempfile
     from tools.adapter_arrays import write_arrays
     exe = os.path.join(ROOT, "tools", "adapter_wall_bench")
-    if not os.path.exists(exe):
-        res["wall_cpp_adapter"] = {"error": "tools/adapter_wall_bench is not built (make)"}
+    env = dict(os.environ)
+    if world > 1:
+        env["HIP_VISIBLE_DEVICES"] = os.environ.get("LOCAL_RANK", "0")
+    ok = os.path.exists(exe)
+    if ok:
+        with tempfile.TemporaryDirectory() as d:
+            path = os.path.join(d, "pool.arrays")
+            write_arrays(path, arrays)
+            r = subprocess.run([exe, workload, path, str(args.wall_frames), str(args.wall_reps),
+                                str(args.wall_threads)], capture_output=True, text=True, timeout=300, env=env)
+        ok = r.returncode == 0
+    # every rank takes part in the reductions, whatever its own child did
+    w = json.loads(r.stdout.strip().splitlines()[-1]) if ok else {"frames": 0, "wall_s": 0.0}
+    bad_ranks = 1.0 - float(ok)
+    w_s, frames = job_totals(w["wall_s"], w["frames"], world, dist if world > 1 else None, dev)
+    if world > 1:
+        _, bad_ranks = job_totals(0.0, bad_ranks, world, dist, dev)
+    if not ok:
+        res["wall_cpp_adapter"] = {"error": "tools/adapter_wall_bench is not built (make)" if not os.path.exists(exe)
+                                   else (r.stdout + r.stderr)[-600:]}
         return
-    with tempfile.TemporaryDirectory() as d:
-        path = os.path.join(d, "pool.arrays")
-        write_arrays(path, arrays)
-        r = subprocess.run([exe, workload, path, str(args.wall_frames), str(args.wall_reps), str(args.wall_threads)],
-                           capture_output=True, text=True, timeout=300)
-    if r.returncode != 0:
-        res["wall_cpp_adapter"] = {"error": (r.stdout + r.stderr)[-600:]}
+    if bad_ranks:
+        res["wall_cpp_adapter"] = {"error": f"{int(bad_ranks)} rank(s) failed the adapter wall bench"}
         return
-    w = json.loads(r.stdout.strip().splitlines()[-1])
     n = min(args.wall_frames, w["distinct_problems"])
     first = w.pop("first_rep")
     bad = {}
@@ -871,15 +967,28 @@ def _cpp_wall(res, workload, arrays, expect, args, rank, world):
         w["mismatch"] = bad
     w["note"] = ("tools/adapter_wall_bench.cpp: gather from mock ORB-SLAM3 objects, C-ABI call with host inputs "
                  "(pack, PCIe, kernels, download), write-back; frames / wall second over all host threads")
-    res["wall_cpp_adapter_frames_per_s"] = w["frames_per_s"]
+    res["wall_cpp_adapter_frames_per_s"] = round(frames / w_s, 1)
     res["wall_cpp_adapter"] = w
+    # the drop-in's wall rate is the workload's value: what ORB-SLAM3 would see,
+    # host gather, packing, PCIe and write-back included; the batched launches' device time is beside it
+    res["kernel_frames_per_s"] = res["value"]
+    res["value"] = res["wall_cpp_adapter_frames_per_s"]
+    res["value_kind"] = ("C++ adapter wall rate (tools/adapter_wall_bench: mock ORB-SLAM3 objects -> C-ABI with host "
+                         f"buffers -> write-back, {args.wall_threads} host threads x {args.wall_frames} frames per call)")
     if "cpu_baseline" in res:
-        res["wall_cpp_adapter_speedup_vs_cpu"] = round(w["frames_per_s"] / res["cpu_baseline"]["value"], 2)
+        cb = res["cpu_baseline"]
+        res["kernel_speedup_vs_cpu"] = res["speedup_vs_cpu"]
+        res["speedup_vs_cpu"] = round(res["value"] / cb["value"], 2)
+        res["speedup_vs_cpu_1thread"] = round(res["value"] / cb["value_1thread"], 1)
+        res["speedup_vs_cpu_node_estimate"] = round(res["value"] / cb["node_estimate"]["value"], 2)
+    if rank != 0:
+        return
     # the drop-in as ORB-SLAM3 calls it: one frame per call, one thread, from C++ (no Python in the loop)
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "pool.arrays")
         write_arrays(path, arrays)
-        r1 = subprocess.run([exe, workload, path, "1", "200", "1"], capture_output=True, text=True, timeout=300)
+        r1 = subprocess.run([exe, workload, path, "1", "200", "1"], capture_output=True, text=True, timeout=300,
+                            env=env)
     if r1.returncode == 0:
         w1 = json.loads(r1.stdout.strip().splitlines()[-1])
         res["single_call_latency_cpp_adapter_us"] = {k: round(v / w1["reps"] * 1e6, 1)
@@ -948,7 +1057,7 @@ def bench_c3(ctx, rank, world, dist, dev, args):
                                           **pose_arrays(probs[i])}))
     _cpp_wall(res, "c3", arrays, {"SearchByBoW": nm, "PoseOptimization": [r.n_inliers for r in
                                                                           opt.PoseOptimization(probs)]},
-              args, rank, world)
+              args, rank, world, dist, dev)
     return res
 
 
@@ -1025,7 +1134,7 @@ def bench_c5(ctx, rank, world, dist, dev, args):
               "SearchByProjection(F,localMPs)": m_local.SearchByProjectionBatch(
                   F, Q, 3.0, False, 20.0, slot_mps=[x[0].copy() for x in S], slot_takens=[x[1] for x in S]),
               "PoseOptimization": [r.n_inliers for r in opt.PoseOptimization(probs)]}
-    _cpp_wall(res, "c5", arrays, expect, args, rank, world)
+    _cpp_wall(res, "c5", arrays, expect, args, rank, world, dist, dev)
     return res
 
 
@@ -1057,7 +1166,7 @@ def bench_dbow(ctx, rank, world, dist, dev, args):
     for i, d in enumerate(pool):
         arrays[f"p{i}.D.desc"] = np.ascontiguousarray(d, np.uint8).reshape(-1)
     _cpp_wall(res, "dbow", arrays, {"n_words": [len(r.word) for r in ref], "n_nodes": [len(r.node_id) for r in ref]},
-              args, rank, world)
+              args, rank, world, dist, dev)
     return res
 
 
@@ -1085,7 +1194,7 @@ def bench_stereo(ctx, rank, world, dist, dev, args):
     arrays = {"pool.n": np.array([n_pool], np.int32)}
     for i, f in enumerate(pool):
         arrays.update(prefixed(f"p{i}.", stereo_arrays(f)))
-    _cpp_wall(res, "stereo", arrays, {"ComputeStereoMatches": list(nm)}, args, rank, world)
+    _cpp_wall(res, "stereo", arrays, {"ComputeStereoMatches": list(nm)}, args, rank, world, dist, dev)
     return res
 
 
@@ -1099,7 +1208,7 @@ def bench_orb(ctx, rank, world, dist, dev, args):
     n_pool = 4
     rng = np.random.default_rng(0x0B5EED30 + rank)
     pool = [orb.synth_orb_frame(rng, n=1200, edge=16) for _ in range(n_pool)]
-    pat = orb.synth_pattern(rng)
+    pat = _ref_pattern()
     dpool = [(orb.ImagePyramid(f[0]).to_device(dev), orb.ImagePyramid(f[1]).to_device(dev)) + tuple(f[2:])
              for f in pool]
     for f in dpool:
@@ -1182,7 +1291,7 @@ def bench_orb_extract(ctx, rank, world, dist, dev, args):
     scaling of the keypoints (ref:src/ORBextractor.cc:1553-1690): ComputePyramid (8 levels x 1.2 with
     19-px reflect borders) and the per-level 7 x 7 GaussianBlur, ComputeKeyPointsOctTree (1000
     features), IC_Angle and steered BRIEF, for one EuRoC-shaped 752 x 480 image resident in HBM per
-    call (seeded synthetic images; a synthetic BRIEF pattern of the reference's shape).  value = frames
+    call (seeded synthetic images; the reference's own bit_pattern_31_ BRIEF table).  value = frames
     per wall second of the three calls with --ba-threads host threads on their own contexts."""
     import torch
     from orb_slam3_comments_ghr_amd import orb
@@ -1192,7 +1301,7 @@ def bench_orb_extract(ctx, rank, world, dist, dev, args):
     dimgs = [torch.from_numpy(im).to(dev) for im in imgs]
     inv, sc = orb.inv_scale_factors(8, 1.2), orb.scale_factors(8, 1.2)
     nf = orb.features_per_level(1000, 8, 1.2)
-    pattern = orb.synth_pattern(np.random.default_rng(5))
+    pattern = _ref_pattern()
     umax = orb.ic_umax()
     lv = np.arange(8, dtype=np.int32)
     torch.cuda.synchronize(dev)

@@ -8,7 +8,10 @@
 
 #include "osg_internal.h"
 
+#include <fcntl.h>
 #include <sched.h>
+#include <signal.h>
+#include <unistd.h>
 
 #include <condition_variable>
 #include <deque>
@@ -40,6 +43,9 @@ struct PoolJob {
     int n;
     std::atomic<int> next{0}, done{0}, active{0};
     int seats;  // workers that may still join (under the pool's mutex)
+    // the owner sleeps on this after a short spin; the thread that finishes the last index wakes it
+    std::mutex m;
+    std::condition_variable cv;
 };
 struct WorkerPool {
     std::mutex m;
@@ -55,7 +61,10 @@ struct WorkerPool {
     {
         for (int i = j->next++; i < j->n; i = j->next++) {
             j->fn(j->arg, i);
-            j->done++;
+            if (++j->done == j->n) {
+                std::lock_guard<std::mutex> lk(j->m);
+                j->cv.notify_all();
+            }
         }
     }
     void loop()
@@ -96,14 +105,20 @@ int osg_host_cpus()
     static const int n = [] {
         if (const char *e = getenv("OSG_HOST_THREADS"))
             if (atoi(e) > 0) return atoi(e);
-        int c = std::max(1, (int)std::thread::hardware_concurrency());
+        const int hw = std::max(1, (int)std::thread::hardware_concurrency());
+        int c = hw;
+        bool pinned = false;  // the launcher gave this process its own CPU set
         cpu_set_t set;
-        if (sched_getaffinity(0, sizeof(set), &set) == 0) c = std::min(c, std::max(1, CPU_COUNT(&set)));
+        if (sched_getaffinity(0, sizeof(set), &set) == 0) {
+            pinned = CPU_COUNT(&set) < hw;
+            c = std::min(c, std::max(1, CPU_COUNT(&set)));
+        }
         const int q = cgroup_cpus();
         if (q > 0) c = std::min(c, q);
-        // one process per GPU (torchrun): the node's share is split between the local ranks
+        // one process per GPU (torchrun): the node's share is split between the local ranks, unless
+        // the launcher already pinned each rank to its own share (not divided twice)
         if (const char *lw = getenv("LOCAL_WORLD_SIZE"))
-            if (atoi(lw) > 1) c = std::max(1, c / atoi(lw));
+            if (atoi(lw) > 1 && !pinned) c = std::max(1, c / atoi(lw));
         return c;
     }();
     return n;
@@ -128,7 +143,16 @@ void osg_parallel_run(int n, int max_threads, void (*fn)(void *, int), void *arg
     }
     WorkerPool::run(&j);
     if (queued) {  // the job lives on this stack: out of the queue and no worker inside before returning
-        while (j.done.load() < n) std::this_thread::yield();
+        // spin briefly (most loops end within it), then sleep until the last index is done, so a
+        // caller waiting on a long index does not burn a core beside the pool's workers
+        const auto t0 = std::chrono::steady_clock::now();
+        while (j.done.load() < n &&
+               std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() < 50.0)
+            std::this_thread::yield();
+        if (j.done.load() < n) {
+            std::unique_lock<std::mutex> lk(j.m);
+            j.cv.wait(lk, [&] { return j.done.load() >= n; });
+        }
         {
             std::lock_guard<std::mutex> lk(p->m);
             for (auto it = p->q.begin(); it != p->q.end(); ++it)
@@ -300,6 +324,57 @@ int osg_wait(osg_ctx *ctx)
     OSG_HIP_CHECK(ctx, hipEventSynchronize(ctx->ev_done));
     return OSG_OK;
 }
+
+// OSG_SEGV_MAPS=1: on SIGSEGV / SIGBUS, write the faulting address and /proc/self/maps to stderr, then
+// hand the signal to the handler installed before ours (e.g. a profiler's stack dumper), so a native
+// stack trace of unsymbolised frames can be mapped to libraries afterwards.  Only
+// open / read / write are used inside the handler (async-signal-safe).
+namespace {
+struct sigaction g_prev_segv, g_prev_bus;
+
+void write_all(int fd, const char *p, size_t n)
+{
+    while (n > 0) {
+        const ssize_t w = write(fd, p, n);
+        if (w <= 0) return;
+        p += w;
+        n -= (size_t)w;
+    }
+}
+
+void maps_handler(int sig, siginfo_t *si, void *uc)
+{
+    char hdr[96];
+    const int n = snprintf(hdr, sizeof hdr, "\n[osg] signal %d at %p; /proc/self/maps follows\n", sig,
+                           si ? si->si_addr : nullptr);
+    write_all(2, hdr, n > 0 ? (size_t)n : 0);
+    const int fd = open("/proc/self/maps", O_RDONLY);
+    if (fd >= 0) {
+        char buf[4096];
+        for (ssize_t r; (r = read(fd, buf, sizeof buf)) > 0;) write_all(2, buf, (size_t)r);
+        close(fd);
+    }
+    write_all(2, "[osg] end of maps\n", 18);
+    struct sigaction &prev = sig == SIGBUS ? g_prev_bus : g_prev_segv;
+    sigaction(sig, &prev, nullptr);  // the previous handler (or the default) takes the re-raised signal
+    if ((prev.sa_flags & SA_SIGINFO) && prev.sa_sigaction) prev.sa_sigaction(sig, si, uc);
+    else if (prev.sa_handler != SIG_IGN && prev.sa_handler != SIG_DFL) prev.sa_handler(sig);
+    else raise(sig);
+}
+
+__attribute__((constructor)) void install_maps_handler()
+{
+    const char *e = getenv("OSG_SEGV_MAPS");
+    if (!e || atoi(e) != 1) return;
+    struct sigaction sa;
+    memset(&sa, 0, sizeof sa);
+    sa.sa_sigaction = maps_handler;
+    sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+    sigemptyset(&sa.sa_mask);
+    sigaction(SIGSEGV, &sa, &g_prev_segv);
+    sigaction(SIGBUS, &sa, &g_prev_bus);
+}
+}  // namespace
 
 extern "C" {
 

@@ -13,8 +13,14 @@ import numpy as np
 import pytest
 
 from orb_slam3_comments_ghr_amd import orb
+from tests import golden_data
 from tests import oracle_calls as oc
 from tests import pyref_orb as po
+
+
+def pattern_of(kind, rng):
+    """"ref": the reference's own bit_pattern_31_ (tests/golden); "synth": a random pattern of its shape."""
+    return golden_data.bit_pattern_31() if kind == "ref" else orb.synth_pattern(rng)
 
 
 def small_frame(seed, n=40, fractional=True, edge=orb.EDGE_THRESHOLD):
@@ -41,10 +47,18 @@ def test_fast_atan2_accuracy(oracle):
             assert min(d, 360.0 - d) < 0.01
 
 
-@pytest.mark.parametrize("seed,edge", [(0, 19), (1, 19), (2, 16)])
-def test_oracle_vs_python(oracle, seed, edge):
+def test_reference_pattern_fixture():
+    pat = golden_data.bit_pattern_31()
+    assert pat.shape == (512, 2) and np.abs(pat).max() <= 13
+    # the table's first and last pairs (ref:src/ORBextractor.cc:214, :469)
+    assert pat[:2].tolist() == [[8, -3], [9, 5]] and pat[-2:].tolist() == [[-1, -6], [0, -11]]
+
+
+@pytest.mark.parametrize("seed,edge,kind", [(0, 19, "synth"), (1, 19, "synth"), (2, 16, "synth"), (3, 19, "ref"),
+                                            (4, 19, "ref")])
+def test_oracle_vs_python(oracle, seed, edge, kind):
     rng, raw, blur, x, y, level = small_frame(seed, edge=edge)
-    pat = orb.synth_pattern(rng)
+    pat = pattern_of(kind, rng)
     ang, desc, bad = oc.orb_describe(oracle, raw, blur, x, y, level, pat)
     assert bad == 0
     um = orb.ic_umax()
@@ -60,11 +74,12 @@ def test_oracle_vs_python(oracle, seed, edge):
         np.testing.assert_array_equal(d2[k], po.orb_descriptor(blur[level[k]], x[k], y[k], given[k], pat))
 
 
-def test_oracle_hand_cases(oracle):
+@pytest.mark.parametrize("kind", ["synth", "ref"])
+def test_oracle_hand_cases(oracle, kind):
     h, w = 64, 64
     ramp_x = np.tile(np.arange(w, dtype=np.uint8) * 3, (h, 1))
     ramp_y = np.ascontiguousarray(ramp_x.T)
-    pat = orb.synth_pattern(np.random.default_rng(9))
+    pat = pattern_of(kind, np.random.default_rng(9))
     x, y, lv = [32.0], [32.0], [0]
     a, d, bad = oc.orb_describe(oracle, [ramp_x], [ramp_x], x, y, lv, pat)
     assert bad == 0 and abs(a[0]) < 1e-3        # brighter to the right: angle 0
@@ -100,11 +115,14 @@ def same(a, b):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed,fractional,edge", [(0, False, 19), (1, True, 19), (2, False, 16), (3, True, 16)])
-def test_gpu_vs_oracle(ctx, oracle, seed, fractional, edge):
+@pytest.mark.parametrize("seed,fractional,edge,kind", [(0, False, 19, "synth"), (1, True, 19, "synth"),
+                                                       (2, False, 16, "synth"), (3, True, 16, "synth"),
+                                                       (4, False, 19, "ref"), (5, True, 19, "ref"),
+                                                       (6, True, 16, "ref")])
+def test_gpu_vs_oracle(ctx, oracle, seed, fractional, edge, kind):
     rng = np.random.default_rng(100 + seed)
     raw, blur, x, y, level = orb.synth_orb_frame(rng, n=1500, fractional=fractional, edge=edge)
-    pat = orb.synth_pattern(rng)
+    pat = pattern_of(kind, rng)
     ref = oc.orb_describe(oracle, raw, blur, x, y, level, pat)
     assert ref[2] >= 0
     got = orb.ORBDescribe(ctx, raw, blur, x, y, level, pat)

@@ -47,11 +47,14 @@ def _check_batch(ctx, imgs, pattern, dev, **kw):
 
 
 @pytest.mark.gpu
-def test_batch_equals_single_image_chain(ctx, oracle):
+@pytest.mark.parametrize("kind", ["synth", "ref"])
+def test_batch_equals_single_image_chain(ctx, oracle, kind):
+    """kind "ref": the reference's own bit_pattern_31_ (tests/golden/orb_bit_pattern_31.npz)."""
     import torch
+    from tests import golden_data
     imgs = [_image(100 + i, 480, 752) for i in range(6)]
     imgs[3] = np.full((480, 752), 128, np.uint8)  # blank: no corners anywhere
-    pattern = orb.synth_pattern(np.random.default_rng(7))
+    pattern = golden_data.bit_pattern_31() if kind == "ref" else orb.synth_pattern(np.random.default_rng(7))
     dev = torch.from_numpy(np.stack(imgs)).cuda()
     out = _check_batch(ctx, imgs, pattern, dev)
     assert out.counts[3] == 0 and min(out.counts[b] for b in (0, 1, 2, 4, 5)) > 500
