@@ -55,6 +55,18 @@ namespace osg_orbslam3 {
     T(const T &) = delete;  \
     T &operator=(const T &) = delete
 
+// The entry points keep their per-frame gathers in a per-thread pool reused call to call: the vectors
+// keep their capacity, so a 256-frame batch neither allocates nor pages in tens of MB of host memory
+// again, and a one-frame call touches warm buffers.  A pooled type has a default constructor and an
+// assign(...) that refills every member (measured: the allocation churn was half of the gather).
+template <class T>
+std::deque<T> &gather_pool(size_t n)
+{
+    thread_local std::deque<T> pool;
+    while (pool.size() < n) pool.emplace_back();
+    return pool;
+}
+
 // ------------------------------------------------------------------------------------ errors
 // Nothing in this adapter throws: ORB-SLAM3's Tracking, LocalMapping and LoopClosing
 // threads have no try / catch.  A failing ABI call (a negative OSG_E_* code) is logged once per
@@ -168,6 +180,27 @@ inline void push_kp(const KeyPointT &kp, std::vector<float> &x, std::vector<floa
     o.push_back(kp.octave);
 }
 
+// A MapPoint's 256-bit descriptor into dst.  MapPoint::GetDescriptor() returns a clone (a heap
+// allocation per call, ref:src/MapPoint.cc GetDescriptor); an integration that adds
+// `void GetDescriptorRow(unsigned char *dst) const` (the 32 bytes copied under mMutexFeatures,
+// INTEGRATION.md §2) is read through that instead -- measured 33 ns of the gather per MapPoint.
+template <class MapPointT>
+inline auto mp_descriptor_(const MapPointT *p, uint8_t *dst, int) -> decltype(p->GetDescriptorRow(dst), void())
+{
+    p->GetDescriptorRow(dst);
+}
+template <class MapPointT>
+inline void mp_descriptor_(const MapPointT *p, uint8_t *dst, long)
+{
+    const auto d = p->GetDescriptor();
+    std::memcpy(dst, d.template ptr<unsigned char>(0), 32);
+}
+template <class MapPointT>
+inline void mp_descriptor(const MapPointT *p, uint8_t *dst)
+{
+    mp_descriptor_(p, dst, 0);
+}
+
 template <class MatT>
 inline void copy_desc_rows(const MatT &m, int n, std::vector<uint8_t> &out)
 {
@@ -180,15 +213,25 @@ inline void copy_desc_rows(const MatT &m, int n, std::vector<uint8_t> &out)
 template <class GridT>
 inline void grid_csr(const GridT &grid, std::vector<int32_t> &gs, std::vector<int32_t> &gi)
 {
-    gs.assign(OSG_GRID_CELLS + 1, 0);
-    gi.clear();
+    // one pass: sizes and indices together (the cells are separate heap blocks; a second walk over
+    // them measured 30 % slower)
+    size_t total = 0;
     for (int ix = 0; ix < OSG_GRID_COLS; ix++)
+        for (int iy = 0; iy < OSG_GRID_ROWS; iy++) total += grid[ix][iy].size();
+    gs.resize(OSG_GRID_CELLS + 1);
+    gi.resize(total);
+    int32_t *g = gs.data(), *o = gi.data();
+    g[0] = 0;
+    for (int ix = 0; ix < OSG_GRID_COLS; ix++) {
+        const auto *col = &grid[ix][0];
         for (int iy = 0; iy < OSG_GRID_ROWS; iy++) {
-            const auto &cell = grid[ix][iy];
-            gs[ix * OSG_GRID_ROWS + iy + 1] = (int32_t)cell.size();
-            for (auto idx : cell) gi.push_back((int32_t)idx);
+            const auto *b = col[iy].data();
+            const int m = (int)col[iy].size();
+            for (int k = 0; k < m; k++) o[k] = (int32_t)b[k];
+            o += m;
+            g[ix * OSG_GRID_ROWS + iy + 1] = (int32_t)(o - gi.data());
         }
-    for (int c = 0; c < OSG_GRID_CELLS; c++) gs[c + 1] += gs[c];
+    }
 }
 
 // Frame::Nleft / KeyFrame::NLeft (ref:include/Frame.h, include/KeyFrame.h spell it differently)
@@ -214,14 +257,22 @@ struct FrameView {
     std::vector<uint8_t> desc;
     osg_frame v{};
 
-    explicit FrameView(const FrameT &F)
+    FrameView() = default;
+    explicit FrameView(const FrameT &F) { assign(F); }
+    void assign(const FrameT &F)
     {
         const int n = F.N, nleft = nleft_of(F, 0);
-        if (nleft == -1) {
-            for (int i = 0; i < n; i++) push_kp(F.mvKeysUn[i], kx, ky, ka, ko);
-        } else {
-            for (int i = 0; i < nleft; i++) push_kp(F.mvKeys[i], kx, ky, ka, ko);
-            for (int i = nleft; i < n; i++) push_kp(F.mvKeysRight[i - nleft], kx, ky, ka, ko);
+        v = osg_frame{};
+        kx.resize(n);
+        ky.resize(n);
+        ka.resize(n);
+        ko.resize(n);
+        for (int i = 0; i < n; i++) {
+            const auto &kp = nleft == -1 ? F.mvKeysUn[i] : (i < nleft ? F.mvKeys[i] : F.mvKeysRight[i - nleft]);
+            kx[i] = kp.pt.x;
+            ky[i] = kp.pt.y;
+            ka[i] = kp.angle;
+            ko[i] = kp.octave;
         }
         copy_desc_rows(F.mDescriptors, n, desc);
         ur.assign(F.mvuRight.begin(), F.mvuRight.end());
@@ -269,7 +320,9 @@ struct Slots {
     std::vector<int32_t> mp;
     std::vector<uint8_t> taken;
     std::vector<MapPointT *> occupant;
-    Slots(const std::vector<MapPointT *> &slots, int nq, bool need_obs)
+    Slots() = default;
+    Slots(const std::vector<MapPointT *> &slots, int nq, bool need_obs) { assign(slots, nq, need_obs); }
+    void assign(const std::vector<MapPointT *> &slots, int nq, bool need_obs)
     {
         const int n = (int)slots.size();
         mp.assign(n, -1);
@@ -313,20 +366,27 @@ struct MpsGather {
     std::vector<float> px, py, pxr, pyr, vc, vcr, depth;
     osg_mp_queries q{};
     Slots<MapPointT> slots;
-    MpsGather(FrameT &F, const std::vector<MapPointT *> &vpMapPoints)
-        : fv(F), slots(F.mvpMapPoints, (int)vpMapPoints.size(), true)
+    MpsGather() = default;
+    MpsGather(FrameT &F, const std::vector<MapPointT *> &vpMapPoints) { assign(F, vpMapPoints); }
+    void assign(FrameT &F, const std::vector<MapPointT *> &vpMapPoints)
     {
+        fv.assign(F);
+        slots.assign(F.mvpMapPoints, (int)vpMapPoints.size(), true);
         const int nq = (int)vpMapPoints.size();
-        id.resize(nq);
-        lvl.resize(nq);
-        lvl_r.resize(nq);
-        desc.resize((size_t)nq * 32);
-        usable.resize(nq);
-        has_obs.resize(nq);
-        in_view.resize(nq);
-        in_view_r.resize(nq);
-        for (auto *v : {&px, &py, &pxr, &pyr, &vc, &vcr, &depth}) v->resize(nq);
+        q = osg_mp_queries{};
+        id.assign(nq, 0);
+        lvl.assign(nq, 0);
+        lvl_r.assign(nq, 0);
+        desc.assign((size_t)nq * 32, 0);
+        usable.assign(nq, 0);
+        has_obs.assign(nq, 0);
+        in_view.assign(nq, 0);
+        in_view_r.assign(nq, 0);
+        for (auto *v : {&px, &py, &pxr, &pyr, &vc, &vcr, &depth}) v->assign(nq, 0.f);
+        constexpr int PF = 8;  // MapPoints are scattered heap objects: fetch a few ahead
+        for (int i = 0; i < std::min(PF, nq); i++) __builtin_prefetch(vpMapPoints[i]);
         for (int i = 0; i < nq; i++) {
+            if (i + PF < nq) __builtin_prefetch(vpMapPoints[i + PF]);
             MapPointT *p = vpMapPoints[i];
             id[i] = i;
             in_view[i] = p->mbTrackInView;
@@ -334,8 +394,7 @@ struct MpsGather {
             if (!in_view[i] && !in_view_r[i]) continue;  // the reference skips before any other read
             usable[i] = !p->isBad();
             has_obs[i] = p->Observations() > 0;
-            const auto d = p->GetDescriptor();
-            std::memcpy(&desc[(size_t)32 * i], d.template ptr<unsigned char>(0), 32);
+            mp_descriptor(p, &desc[(size_t)32 * i]);
             px[i] = p->mTrackProjX;
             py[i] = p->mTrackProjY;
             pxr[i] = p->mTrackProjXR;
@@ -370,7 +429,8 @@ int search_by_projection_mps(FrameT &F, const std::vector<MapPointT *> &vpMapPoi
                              float thFarPoints, float nnratio)
 {
     osg_ctx *ctx = thread_ctx();
-    MpsGather<FrameT, MapPointT> g(F, vpMapPoints);
+    MpsGather<FrameT, MapPointT> &g = gather_pool<MpsGather<FrameT, MapPointT>>(1)[0];
+    g.assign(F, vpMapPoints);
     const int nm = call(ctx, "osg_search_by_projection_mps", [&] {
         return osg_search_by_projection_mps(ctx, &g.fv.v, &g.q, nnratio, th, bFarPoints, thFarPoints, g.slots.mp.data(),
                                             g.slots.taken.data());
@@ -393,22 +453,29 @@ struct LastGather {
     std::vector<MapPointT *> queries;
     osg_last_queries q{};
     Slots<MapPointT> slots;
-    LastGather(FrameT &CF, const FrameT &LF) : fv(CF), slots(CF.mvpMapPoints, LF.N, true)
+    LastGather() = default;
+    LastGather(FrameT &CF, const FrameT &LF) { assign(CF, LF); }
+    void assign(FrameT &CF, const FrameT &LF)
     {
+        fv.assign(CF);
+        slots.assign(CF.mvpMapPoints, LF.N, true);
+        q = osg_last_queries{};
         const int n = LF.N;
         id.assign(n, -1);
         oct.assign(n, 0);
-        desc.resize((size_t)n * 32);
+        desc.assign((size_t)n * 32, 0);
         valid.assign(n, 0);
         has_obs.assign(n, 0);
-        for (auto *w : {&u, &v, &invz, &ang}) w->resize(n);
+        for (auto *w : {&u, &v, &invz, &ang}) w->assign(n, 0.f);
         queries.assign(n, nullptr);
         const bool two = CF.Nleft != -1;
         if (two) {
             ur.assign(n, 0.f);
             vr.assign(n, 0.f);
         }
+        constexpr int PF = 8;  // MapPoints are scattered heap objects: fetch a few ahead
         for (int i = 0; i < n; i++) {
+            if (i + PF < n && LF.mvpMapPoints[i + PF]) __builtin_prefetch(LF.mvpMapPoints[i + PF]);
             MapPointT *p = LF.mvpMapPoints[i];
             const auto &kp = (LF.Nleft == -1) ? LF.mvKeysUn[i]
                                               : (i < LF.Nleft ? LF.mvKeys[i] : LF.mvKeysRight[i - LF.Nleft]);
@@ -421,8 +488,7 @@ struct LastGather {
             id[i] = i;
             queries[i] = p;
             has_obs[i] = p->Observations() > 0;
-            const auto d = p->GetDescriptor();
-            std::memcpy(&desc[(size_t)32 * i], d.template ptr<unsigned char>(0), 32);
+            mp_descriptor(p, &desc[(size_t)32 * i]);
         }
         q.n = n;
         q.mp_id = id.data();
@@ -446,7 +512,8 @@ template <class H, class FrameT>
 int search_by_projection_last(FrameT &CF, const FrameT &LF, float th, bool bMono, bool checkOri)
 {
     osg_ctx *ctx = thread_ctx();
-    LastGather<H, FrameT> g(CF, LF);
+    LastGather<H, FrameT> &g = gather_pool<LastGather<H, FrameT>>(1)[0];
+    g.assign(CF, LF);
     const int nm = call(ctx, "osg_search_by_projection_last", [&] {
         return osg_search_by_projection_last(ctx, &g.fv.v, &g.q, th, bMono, checkOri, g.slots.mp.data(),
                                              g.slots.taken.data());
@@ -476,8 +543,7 @@ int search_by_projection_kf(FrameT &CF, KeyFrameT *pKF, const std::set<MapPointT
         if (!H::kf_query(CF, p, u[i], v[i], lvl[i])) continue;
         valid[i] = 1;
         id[i] = i;
-        const auto d = p->GetDescriptor();
-        std::memcpy(&desc[(size_t)32 * i], d.template ptr<unsigned char>(0), 32);
+        mp_descriptor(p, &desc[(size_t)32 * i]);
     }
     osg_kf_queries q{};
     q.n = n;
@@ -530,8 +596,7 @@ int fuse(KeyFrameT *pKF, const std::vector<MapPointT *> &vpMapPoints, float th, 
         if (!p || p->isBad() || p->IsInKeyFrame(pKF)) continue;  // ref:src/ORBmatcher.cc:1367-1382
         if (!H::fuse_query(pKF, p, bRight, u[i], v[i], ur[i], lvl[i])) continue;
         valid[i] = 1;
-        const auto d = p->GetDescriptor();
-        std::memcpy(&desc[(size_t)32 * i], d.template ptr<unsigned char>(0), 32);
+        mp_descriptor(p, &desc[(size_t)32 * i]);
     }
     std::vector<float> inv_s2(pKF->mvInvLevelSigma2.begin(), pKF->mvInvLevelSigma2.end());
     osg_fuse_queries q{};
@@ -592,8 +657,7 @@ int fuse_sim3(KeyFrameT *pKF, const Sim3T &Scw, const std::vector<MapPointT *> &
         if (p->isBad() || spAlreadyFound.count(p)) continue;  // ref:src/ORBmatcher.cc:1582
         if (!H::fuse_sim3_query(pKF, Scw, p, u[i], v[i], lvl[i])) continue;
         valid[i] = 1;
-        const auto d = p->GetDescriptor();
-        std::memcpy(&desc[(size_t)32 * i], d.template ptr<unsigned char>(0), 32);
+        mp_descriptor(p, &desc[(size_t)32 * i]);
     }
     osg_fuse_queries q{};
     q.n = n;
@@ -627,8 +691,13 @@ template <class FeatVecT>
 struct FeatVecCSR {
     std::vector<uint32_t> node;
     std::vector<int32_t> start, feat;
-    explicit FeatVecCSR(const FeatVecT &fvec)
+    FeatVecCSR() = default;
+    explicit FeatVecCSR(const FeatVecT &fvec) { assign(fvec); }
+    void assign(const FeatVecT &fvec)
     {
+        node.clear();
+        start.clear();
+        feat.clear();
         start.push_back(0);
         for (const auto &kv : fvec) {
             node.push_back((uint32_t)kv.first);
@@ -652,8 +721,13 @@ struct BowKfF {
     FeatVecCSR<decltype(std::declval<KeyFrameT &>().mFeatVec)> fk;
     FeatVecCSR<decltype(std::declval<FrameT &>().mFeatVec)> ff;
     osg_bow_side sk{}, sf{};
-    BowKfF(KeyFrameT *pKF, const FrameT &F) : vpMPsKF(pKF->GetMapPointMatches()), fk(pKF->mFeatVec), ff(F.mFeatVec)
+    BowKfF() = default;
+    BowKfF(KeyFrameT *pKF, const FrameT &F) { assign(pKF, F); }
+    void assign(KeyFrameT *pKF, const FrameT &F)
     {
+        vpMPsKF = pKF->GetMapPointMatches();
+        fk.assign(pKF->mFeatVec);
+        ff.assign(F.mFeatVec);
         const int nk = (int)vpMPsKF.size(), nf = F.N;
         good.resize(nk);
         ak.resize(nk);
@@ -688,7 +762,8 @@ int search_by_bow_kf_f(KeyFrameT *pKF, FrameT &F, std::vector<MapPointT *> &vpMa
                        bool checkOri)
 {
     osg_ctx *ctx = thread_ctx();
-    BowKfF<KeyFrameT, FrameT, MapPointT> g(pKF, F);
+    BowKfF<KeyFrameT, FrameT, MapPointT> &g = gather_pool<BowKfF<KeyFrameT, FrameT, MapPointT>>(1)[0];
+    g.assign(pKF, F);
     std::vector<int32_t> out(F.N, -1);
     const int nm = call(ctx, "osg_search_by_bow_kf_f",
                         [&] { return osg_search_by_bow_kf_f(ctx, &g.sk, &g.sf, nnratio, checkOri, out.data()); });
@@ -755,8 +830,7 @@ int search_by_projection_sim3(KeyFrameT *pKF, const Sim3T &Scw, const std::vecto
         if (p->isBad() || spAlreadyFound.count(p)) continue;  // :528, :647
         if (!H::sim3_query(pKF, Scw, p, vpPointsKFs != nullptr, u[i], v[i], lvl[i])) continue;
         valid[i] = 1;
-        const auto d = p->GetDescriptor();
-        std::memcpy(&desc[(size_t)32 * i], d.template ptr<unsigned char>(0), 32);
+        mp_descriptor(p, &desc[(size_t)32 * i]);
     }
     std::vector<int32_t> slot_query(pKF->N);
     for (int i = 0; i < pKF->N; i++) slot_query[i] = vpMatched[i] ? -2 : -1;
@@ -819,8 +893,7 @@ int search_by_sim3(KeyFrameT *pKF1, KeyFrameT *pKF2, std::vector<MapPointT *> &v
             if (!pMP || already[i] || pMP->isBad()) continue;  // :1737-1742 / :1813-1818
             if (!H::sim3_pair_query(pKF1, pKF2, pMP, S12, dir12, Qd.u[i], Qd.v[i], Qd.lvl[i])) continue;
             Qd.valid[i] = 1;
-            const auto d = pMP->GetDescriptor();
-            std::memcpy(&Qd.desc[(size_t)32 * i], d.template ptr<unsigned char>(0), 32);
+            mp_descriptor(pMP, &Qd.desc[(size_t)32 * i]);
         }
         Qd.q.n = n;
         Qd.q.desc = Qd.desc.data();
@@ -884,8 +957,18 @@ struct PyramidView {
     std::vector<int32_t> rows, cols, step;
     osg_image_pyramid v{};
 
+    PyramidView() = default;
     PyramidView(const std::vector<MatT> &pyr, int n_levels, const osg_image_pyramid *on_device = nullptr)
     {
+        assign(pyr, n_levels, on_device);
+    }
+    void assign(const std::vector<MatT> &pyr, int n_levels, const osg_image_pyramid *on_device = nullptr)
+    {
+        data.clear();
+        rows.clear();
+        cols.clear();
+        step.clear();
+        v = osg_image_pyramid{};
         if (on_device) {  // levels already in HBM: read in place, no pixels cross PCIe
             v = *on_device;
             return;
@@ -928,11 +1011,18 @@ struct StereoGather {
     std::vector<uint8_t> dl, dr;
     PyramidView<MatT> pl, pr;
     osg_stereo_frame s{};
-    explicit StereoGather(const FrameT &F)
-        : sc(F.mvScaleFactors.begin(), F.mvScaleFactors.end()), isc(F.mvInvScaleFactors.begin(), F.mvInvScaleFactors.end()),
-          pl(F.mpORBextractorLeft->mvImagePyramid, (int)F.mvScaleFactors.size(), device_levels(*F.mpORBextractorLeft, 0)),
-          pr(F.mpORBextractorRight->mvImagePyramid, (int)F.mvScaleFactors.size(), device_levels(*F.mpORBextractorRight, 0))
+    StereoGather() = default;
+    explicit StereoGather(const FrameT &F) { assign(F); }
+    void assign(const FrameT &F)
     {
+        sc.assign(F.mvScaleFactors.begin(), F.mvScaleFactors.end());
+        isc.assign(F.mvInvScaleFactors.begin(), F.mvInvScaleFactors.end());
+        pl.assign(F.mpORBextractorLeft->mvImagePyramid, (int)F.mvScaleFactors.size(), device_levels(*F.mpORBextractorLeft, 0));
+        pr.assign(F.mpORBextractorRight->mvImagePyramid, (int)F.mvScaleFactors.size(), device_levels(*F.mpORBextractorRight, 0));
+        for (auto *w : {&x, &y, &xr, &yr, &ang}) w->clear();
+        o.clear();
+        orr.clear();
+        s = osg_stereo_frame{};
         const int n = F.N, nr = (int)F.mvKeysRight.size();
         for (int i = 0; i < n; i++) push_kp(F.mvKeys[i], x, y, ang, o);
         for (int i = 0; i < nr; i++) push_kp(F.mvKeysRight[i], xr, yr, ang, orr);
@@ -1243,10 +1333,19 @@ struct PoseGather {
     std::vector<int> slot;
     std::vector<uint8_t> outl;
     osg_pose_problem p{};
+    PoseGather() = default;
     template <class MutexT>
-    PoseGather(FrameT *pFrame, MutexT *gather_mutex)
+    PoseGather(FrameT *pFrame, MutexT *gather_mutex) { assign(pFrame, gather_mutex); }
+    template <class MutexT>
+    void assign(FrameT *pFrame, MutexT *gather_mutex)
     {
         const int N = pFrame->N;
+        p = osg_pose_problem{};
+        kind.clear();
+        xw.clear();
+        obs.clear();
+        isig.clear();
+        slot.clear();
         const bool two = (bool)pFrame->mpCamera2;
         std::unique_lock<MutexT> gather_lock;
         if (gather_mutex) gather_lock = std::unique_lock<MutexT>(*gather_mutex);
@@ -1310,7 +1409,8 @@ template <class H, class FrameT, class MutexT = NoMutex>
 int pose_optimization(FrameT *pFrame, MutexT *gather_mutex = nullptr)
 {
     osg_ctx *ctx = thread_ctx();
-    PoseGather<H, FrameT> g(pFrame, gather_mutex);
+    PoseGather<H, FrameT> &g = gather_pool<PoseGather<H, FrameT>>(1)[0];
+    g.assign(pFrame, gather_mutex);
     osg_pose_result r{};
     r.outlier = g.outl.data();
     if (call(ctx, "osg_pose_optimization", [&] { return osg_pose_optimization(ctx, &g.p, &r); }) < 0) return 0;
@@ -1874,16 +1974,20 @@ int search_by_bow_kf_f_batch(const std::vector<KeyFrameT *> &kfs, const std::vec
 {
     osg_ctx *ctx = thread_ctx();
     const int B = (int)frames.size();
-    std::deque<BowKfF<KeyFrameT, FrameT, MapPointT>> g;
-    std::vector<osg_bow_side> sk(B), sf(B);
-    std::vector<size_t> off(B + 1, 0);
+    std::deque<BowKfF<KeyFrameT, FrameT, MapPointT>> &g = gather_pool<BowKfF<KeyFrameT, FrameT, MapPointT>>(B);
+    thread_local std::vector<osg_bow_side> sk, sf;
+    thread_local std::vector<size_t> off;
+    thread_local std::vector<int32_t> out;
+    sk.resize(B);
+    sf.resize(B);
+    off.assign(B + 1, 0);
     for (int b = 0; b < B; b++) {
-        g.emplace_back(kfs[b], *frames[b]);
-        sk[b] = g.back().sk;
-        sf[b] = g.back().sf;
+        g[b].assign(kfs[b], *frames[b]);
+        sk[b] = g[b].sk;
+        sf[b] = g[b].sf;
         off[b + 1] = off[b] + (size_t)frames[b]->N;
     }
-    std::vector<int32_t> out(off[B], -1);
+    out.assign(off[B], -1);
     const int rc = B == 0 ? OSG_OK : call(ctx, "osg_search_by_bow_kf_f_batch", [&] {
         return osg_search_by_bow_kf_f_batch(ctx, sk.data(), sf.data(), B, nnratio, checkOri, out.data(), nmatches);
     });
@@ -1900,14 +2004,16 @@ int pose_optimization_batch(const std::vector<FrameT *> &frames, int32_t *n_inli
 {
     osg_ctx *ctx = thread_ctx();
     const int B = (int)frames.size();
-    std::deque<PoseGather<H, FrameT>> g;
-    std::vector<osg_pose_problem> p(B);
-    std::vector<osg_pose_result> r(B);
+    std::deque<PoseGather<H, FrameT>> &g = gather_pool<PoseGather<H, FrameT>>(B);
+    thread_local std::vector<osg_pose_problem> p;
+    thread_local std::vector<osg_pose_result> r;
+    p.resize(B);
+    r.resize(B);
     for (int b = 0; b < B; b++) {
-        g.emplace_back(frames[b], gather_mutex);
-        p[b] = g.back().p;
+        g[b].assign(frames[b], gather_mutex);
+        p[b] = g[b].p;
         r[b] = osg_pose_result{};
-        r[b].outlier = g.back().outl.data();
+        r[b].outlier = g[b].outl.data();
     }
     const int rc = B == 0 ? OSG_OK : call(ctx, "osg_pose_optimization_batch",
                                           [&] { return osg_pose_optimization_batch(ctx, p.data(), B, r.data()); });
@@ -1921,18 +2027,23 @@ int search_by_projection_last_batch(const std::vector<FrameT *> &CFs, const std:
 {
     osg_ctx *ctx = thread_ctx();
     const int B = (int)CFs.size();
-    std::deque<LastGather<H, FrameT>> g;
-    std::vector<osg_frame> f(B);
-    std::vector<osg_last_queries> q(B);
-    std::vector<size_t> off(B + 1, 0);
+    std::deque<LastGather<H, FrameT>> &g = gather_pool<LastGather<H, FrameT>>(B);
+    thread_local std::vector<osg_frame> f;
+    thread_local std::vector<osg_last_queries> q;
+    thread_local std::vector<size_t> off;
+    thread_local std::vector<int32_t> mp;
+    thread_local std::vector<uint8_t> taken;
+    f.resize(B);
+    q.resize(B);
+    off.assign(B + 1, 0);
     for (int b = 0; b < B; b++) {
-        g.emplace_back(*CFs[b], *LFs[b]);
-        f[b] = g.back().fv.v;
-        q[b] = g.back().q;
+        g[b].assign(*CFs[b], *LFs[b]);
+        f[b] = g[b].fv.v;
+        q[b] = g[b].q;
         off[b + 1] = off[b] + (size_t)CFs[b]->N;
     }
-    std::vector<int32_t> mp(off[B]);
-    std::vector<uint8_t> taken(off[B]);
+    mp.resize(off[B]);
+    taken.resize(off[B]);
     for (int b = 0; b < B; b++) {
         std::copy(g[b].slots.mp.begin(), g[b].slots.mp.end(), mp.begin() + off[b]);
         std::copy(g[b].slots.taken.begin(), g[b].slots.taken.end(), taken.begin() + off[b]);
@@ -1958,18 +2069,23 @@ int search_by_projection_mps_batch(const std::vector<FrameT *> &Fs, const std::v
 {
     osg_ctx *ctx = thread_ctx();
     const int B = (int)Fs.size();
-    std::deque<MpsGather<FrameT, MapPointT>> g;
-    std::vector<osg_frame> f(B);
-    std::vector<osg_mp_queries> q(B);
-    std::vector<size_t> off(B + 1, 0);
+    std::deque<MpsGather<FrameT, MapPointT>> &g = gather_pool<MpsGather<FrameT, MapPointT>>(B);
+    thread_local std::vector<osg_frame> f;
+    thread_local std::vector<osg_mp_queries> q;
+    thread_local std::vector<size_t> off;
+    thread_local std::vector<int32_t> mp;
+    thread_local std::vector<uint8_t> taken;
+    f.resize(B);
+    q.resize(B);
+    off.assign(B + 1, 0);
     for (int b = 0; b < B; b++) {
-        g.emplace_back(*Fs[b], *mps[b]);
-        f[b] = g.back().fv.v;
-        q[b] = g.back().q;
+        g[b].assign(*Fs[b], *mps[b]);
+        f[b] = g[b].fv.v;
+        q[b] = g[b].q;
         off[b + 1] = off[b] + (size_t)Fs[b]->N;
     }
-    std::vector<int32_t> mp(off[B]);
-    std::vector<uint8_t> taken(off[B]);
+    mp.resize(off[B]);
+    taken.resize(off[B]);
     for (int b = 0; b < B; b++) {
         std::copy(g[b].slots.mp.begin(), g[b].slots.mp.end(), mp.begin() + off[b]);
         std::copy(g[b].slots.taken.begin(), g[b].slots.taken.end(), taken.begin() + off[b]);
@@ -1994,15 +2110,19 @@ int compute_stereo_matches_batch(const std::vector<FrameT *> &frames, int32_t *n
 {
     osg_ctx *ctx = thread_ctx();
     const int B = (int)frames.size();
-    std::deque<StereoGather<FrameT>> g;
-    std::vector<osg_stereo_frame> s(B);
-    std::vector<size_t> off(B + 1, 0);
+    std::deque<StereoGather<FrameT>> &g = gather_pool<StereoGather<FrameT>>(B);
+    thread_local std::vector<osg_stereo_frame> s;
+    thread_local std::vector<size_t> off;
+    thread_local std::vector<float> ur, depth;
+    s.resize(B);
+    off.assign(B + 1, 0);
     for (int b = 0; b < B; b++) {
-        g.emplace_back(*frames[b]);
-        s[b] = g.back().s;
+        g[b].assign(*frames[b]);
+        s[b] = g[b].s;
         off[b + 1] = off[b] + (size_t)frames[b]->N;
     }
-    std::vector<float> ur(off[B], -1.0f), depth(off[B], -1.0f);
+    ur.assign(off[B], -1.0f);
+    depth.assign(off[B], -1.0f);
     const int rc = B == 0 ? OSG_OK : call(ctx, "osg_compute_stereo_matches_batch", [&] {
         return osg_compute_stereo_matches_batch(ctx, s.data(), B, ur.data(), depth.data(), nmatches);
     });

@@ -107,8 +107,9 @@ def parse():
     ap.add_argument("--only", default="", help="comma-separated stage keys to run (A/B runs); default: all")
     ap.add_argument("--wall-frames", type=int, default=256, help="frames per batched adapter call (C++ wall bench)")
     ap.add_argument("--wall-reps", type=int, default=24, help="timed repetitions per host thread (C++ wall bench)")
-    ap.add_argument("--wall-threads", type=int, default=8,
-                    help="host threads of the C++ wall bench, each with its own context (Tracking threads)")
+    ap.add_argument("--wall-threads", type=int, default=0,
+                    help="host threads of the C++ wall bench, each with its own context (Tracking threads); 0: "
+                         "as many as the CPU baseline runs (the host CPUs this job may use, per rank)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-launch HBM traffic from the rocprofv3 PMC passes (tools/gpu/gpu_profile_r03.sh)")
     ap.add_argument("--valu-pmc", default=os.path.join(ROOT, "profiles", "r03_top2_valu_pmc.json"),
@@ -933,13 +934,17 @@ def _cpp_wall(res, workload, arrays, expect, args, rank, world, dist=None, dev=N
     env = dict(os.environ)
     if world > 1:
         env["HIP_VISIBLE_DEVICES"] = os.environ.get("LOCAL_RANK", "0")
+    threads = args.wall_threads
+    if threads <= 0:  # the same host cores as the CPU baseline (its `cores`), split between local ranks
+        from tests import cpu_mt
+        threads = max(1, min(64, cpu_mt.host_threads() // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))))
     ok = os.path.exists(exe)
     if ok:
         with tempfile.TemporaryDirectory() as d:
             path = os.path.join(d, "pool.arrays")
             write_arrays(path, arrays)
             r = subprocess.run([exe, workload, path, str(args.wall_frames), str(args.wall_reps),
-                                str(args.wall_threads)], capture_output=True, text=True, timeout=300, env=env)
+                                str(threads)], capture_output=True, text=True, timeout=300, env=env)
         ok = r.returncode == 0
     # every rank takes part in the reductions, whatever its own child did
     w = json.loads(r.stdout.strip().splitlines()[-1]) if ok else {"frames": 0, "wall_s": 0.0}
@@ -974,7 +979,7 @@ def _cpp_wall(res, workload, arrays, expect, args, rank, world, dist=None, dev=N
     res["kernel_frames_per_s"] = res["value"]
     res["value"] = res["wall_cpp_adapter_frames_per_s"]
     res["value_kind"] = ("C++ adapter wall rate (tools/adapter_wall_bench: mock ORB-SLAM3 objects -> C-ABI with host "
-                         f"buffers -> write-back, {args.wall_threads} host threads x {args.wall_frames} frames per call)")
+                         f"buffers -> write-back, {threads} host threads x {args.wall_frames} frames per call)")
     if "cpu_baseline" in res:
         cb = res["cpu_baseline"]
         res["kernel_speedup_vs_cpu"] = res["speedup_vs_cpu"]

@@ -120,9 +120,9 @@ int osg_local_bundle_adjustment(struct osg_ctx *ctx, const osg_ba_graph *g, osg_
 /* Optimizer::BundleAdjustment / GlobalBundleAdjustemnt (ref:src/Optimizer.cc:2831-3237): the same
  * engine on the whole map — every KeyFrame (only the map's init KeyFrame fixed), every MapPoint with
  * an edge, optimize(nIterations) with the caller's e_robust / Huber deltas, no outlier pass (edge_bad
- * is filled but the reference does not read it).  The reduced camera system is dense up to 1024 free
- * KeyFrames; past that it is factored on its envelope (banded maps), up to 7 723 free KeyFrames
- * (DESIGN.md §3.11). */
+ * is filled but the reference does not read it).  The reduced camera system is dense up to 64 free
+ * KeyFrames; past that it is stored and factored on its envelope (banded maps and their loop rows),
+ * up to 65 535 free KeyFrames (the pose-pair index is an int32_t). */
 int osg_bundle_adjustment(struct osg_ctx *ctx, const osg_ba_graph *g, osg_ba_result *r,
                           const volatile uint8_t *stop_flag);
 

@@ -145,11 +145,29 @@ struct LbaDev {
     // inside the envelope (the factorisation reads nothing else); null: every pair (n <= CMAX)
     const int32_t *live_pairs;
     int n_live;
+    const int32_t *live_chunk;           // per live pair: its chunk range [first, end) (past CMAX)
+    // past CMAX, Hs holds only the envelope's lower 32 x 32 tiles: row block t keeps column blocks
+    // blk_first[t] .. t, contiguous after env_off[t] tiles, each tile row-major; null: dense n x n
+    const int32_t *env_off;
     int *flag;                           // [0] cholesky ok
     unsigned long long *tstamp;          // phase timestamps (OSG_LBA_PROFILE=2), else null
 };
 
 __device__ inline double edge_w(const LbaDev &D, int e) { return (double)D.e_isig2[e]; }
+// Hs element (R, C): dense row-major up to CMAX, else its place in the envelope tile store (which
+// must hold it: hs_stored)
+__device__ inline size_t hs_at(const LbaDev &D, int n, int R, int C)
+{
+    if (!D.env_off) return (size_t)R * n + C;
+    const int t = R >> 5, u = C >> 5;
+    return ((size_t)(D.env_off[t] + u - D.blk_first[t]) << 10) + (size_t)((R & 31) << 5) + (size_t)(C & 31);
+}
+__device__ inline bool hs_stored(const LbaDev &D, int R, int C)
+{
+    if (!D.env_off) return true;
+    const int t = R >> 5, u = C >> 5;
+    return u <= t && u >= D.blk_first[t];
+}
 __device__ inline const double *cur_pose(const LbaDev &D) { return D.ctl->sel ? D.poseB : D.poseA; }
 __device__ inline const double *cur_point(const LbaDev &D) { return D.ctl->sel ? D.pointB : D.pointA; }
 __device__ inline double *new_pose(const LbaDev &D) { return D.ctl->sel ? D.poseA : D.poseB; }
@@ -946,14 +964,16 @@ __global__ __launch_bounds__(256) void k_schur_pairs(const LbaDev *__restrict__ 
     if (lane < 36) {
         const int r = lane / 6, c = lane % 6;
         double acc = 0.0;
-        for (int ch = D.pair_chunk[wave]; ch < D.pair_chunk[wave + 1]; ch++) acc += D.chunk_part[36 * (size_t)ch + lane];
+        const int ch0 = D.live_chunk ? D.live_chunk[2 * slot] : D.pair_chunk[wave];
+        const int ch1 = D.live_chunk ? D.live_chunk[2 * slot + 1] : D.pair_chunk[wave + 1];
+        for (int ch = ch0; ch < ch1; ch++) acc += D.chunk_part[36 * (size_t)ch + lane];
         double v = -acc;
         if (i == j) {
             v += D.Hpp[36 * (size_t)i + lane];
             if (r == c) v += lambda;
         }
-        D.Hs[(size_t)(6 * i + r) * n + 6 * j + c] = v;
-        if (i != j) D.Hs[(size_t)(6 * j + c) * n + 6 * i + r] = v;
+        if (hs_stored(D, 6 * i + r, 6 * j + c)) D.Hs[hs_at(D, n, 6 * i + r, 6 * j + c)] = v;
+        if (i != j && hs_stored(D, 6 * j + c, 6 * i + r)) D.Hs[hs_at(D, n, 6 * j + c, 6 * i + r)] = v;
     } else if (i == j && lane < 42) {  // b_schur_i = b_p,i - its row segments' sums, in segment order
         const int k = lane - 36;
         double t = 0.0;
@@ -985,7 +1005,7 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // read as zero; tile entries past n become the identity (keeps the padded factorisation finite).
 constexpr int LU_STEPS = CMAX / 64;  // 16-wide steps per wave at most
 
-__device__ __forceinline__ void tile_left_update2(const double *__restrict__ A, int n, int C0, int R0, int K,
+__device__ __forceinline__ void tile_left_update2(const LbaDev &D, const double *__restrict__ A, int n, int C0, int R0, int K,
                                                   const double *__restrict__ y,
                                                   double (*sT)[CB + 1], double (*sX)[CB + 1],
                                                   double (*sP)[CB][CB + 1], double (*s_rp)[CB])
@@ -997,8 +1017,8 @@ __device__ __forceinline__ void tile_left_update2(const double *__restrict__ A, 
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int e = threadIdx.x + 256 * q, r = e >> 5, c = e & 31;
-        aT[q] = (C0 + r < n && C0 + c < n) ? A[(size_t)(C0 + r) * n + C0 + c] : 0.0;
-        aX[q] = (two && R0 + r < n && C0 + c < n) ? A[(size_t)(R0 + r) * n + C0 + c] : 0.0;
+        aT[q] = (C0 + r < n && C0 + c < n) ? A[hs_at(D, n, C0 + r, C0 + c)] : 0.0;
+        aX[q] = (two && R0 + r < n && C0 + c < n) ? A[hs_at(D, n, R0 + r, C0 + c)] : 0.0;
     }
     const int g4 = 4 * (l >> 4);
     const int rj0 = C0 + (l & 15), rj1 = C0 + 16 + (l & 15);
@@ -1261,7 +1281,7 @@ __device__ __forceinline__ void chol_offdiag_out(const LbaDev &D, CholLds &L, in
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int r = qr + (l >> 4) + 4 * q;
-        if (R0 + r < n && c < nb) Aw[(size_t)(R0 + r) * n + k0 + c] = acc[q];
+        if (R0 + r < n && c < nb) Aw[hs_at(D, n, R0 + r, k0 + c)] = acc[q];
     }
 }
 
@@ -1296,7 +1316,7 @@ __global__ __launch_bounds__(256) void k_chol_col(const LbaDev *__restrict__ Ds,
     for (int e = tid; e < CB * (CB + 1); e += 256) (&L.sM[0][0])[e] = 0.0;
     // past CMAX the system is factored right-looking: k_chol_trail has already applied every earlier
     // column block to these tiles and to b, so nothing is left to subtract (K = 0)
-    tile_left_update2(A, n, k0, t > 0 ? R0 : -1, n > CMAX ? 0 : k0, t == 0 ? D.x : nullptr, L.sG, L.sX, L.sP, L.s_rp);
+    tile_left_update2(D, A, n, k0, t > 0 ? R0 : -1, n > CMAX ? 0 : k0, t == 0 ? D.x : nullptr, L.sG, L.sX, L.sP, L.s_rp);
     if (tid < CB) L.sM[tid][tid] = 1.0;
     __syncthreads();
     if (ts) ts[1] = wall_clock64();
@@ -1436,8 +1456,8 @@ __global__ __launch_bounds__(256) void k_chol_trail(const LbaDev *__restrict__ D
     const int tid = threadIdx.x;
     for (int e = tid; e < CB * CB; e += 256) {
         const int r = e >> 5, c = e & 31;
-        sLt[r][c] = (R0 + r < n) ? D.Hs[(size_t)(R0 + r) * n + K0 + c] : 0.0;
-        sLu[r][c] = (C0 + r < n) ? D.Hs[(size_t)(C0 + r) * n + K0 + c] : 0.0;
+        sLt[r][c] = (R0 + r < n) ? D.Hs[hs_at(D, n, R0 + r, K0 + c)] : 0.0;
+        sLu[r][c] = (C0 + r < n) ? D.Hs[hs_at(D, n, C0 + r, K0 + c)] : 0.0;
     }
     __syncthreads();
     const int w = tid >> 6, l = tid & 63;
@@ -1452,7 +1472,7 @@ __global__ __launch_bounds__(256) void k_chol_trail(const LbaDev *__restrict__ D
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int r = qr + (l >> 4) + 4 * q;
-        if (R0 + r < n && C0 + c < n) D.Hs[(size_t)(R0 + r) * n + C0 + c] -= acc[q];
+        if (R0 + r < n && C0 + c < n) D.Hs[hs_at(D, n, R0 + r, C0 + c)] -= acc[q];
     }
     if (t == u && tid < CB && R0 + tid < n) {  // block j is full (m > 0): y_j is 32 entries
         double s = 0.0;
@@ -1496,7 +1516,7 @@ __global__ __launch_bounds__(1024) void k_chol_back_large(const LbaDev *__restri
         if (c < nb) {
             for (int q = D.col_rows_start[bi]; q < D.col_rows_start[bi + 1]; q++) {
                 const int row = D.col_rows[q] * CB + g;
-                if (row < n) acc += A[(size_t)row * n + k0 + c] * s_x[row];
+                if (row < n) acc += A[hs_at(D, n, row, k0 + c)] * s_x[row];
             }
         }
         s_part[c][g] = acc;
@@ -1555,7 +1575,7 @@ __global__ __launch_bounds__(BSC) void k_back_step(const LbaDev *__restrict__ Ds
     const double *A = D.Hs;
     double acc = 0.0;
 #pragma unroll 8
-    for (int r = 0; r < nb; r++) acc += A[(size_t)(k0 + r) * n + u] * s_x[r];
+    for (int r = 0; r < nb; r++) acc += A[hs_at(D, n, k0 + r, u)] * s_x[r];
     D.x[u] -= acc;
 }
 __global__ __launch_bounds__(EB) void k_back_copy(const LbaDev *__restrict__ Ds)
@@ -1741,6 +1761,7 @@ struct LbaHost {
     bool multi = false;  // a block with several edges (k_linearize<true>)
     std::vector<int32_t> blk_first, blk_last;  // envelope of the reduced system by row block (see LbaDev)
     std::vector<int32_t> col_rows_start, col_rows, live_pairs;  // envelope rows per column block, live pairs
+    std::vector<int32_t> live_chunk, env_off;  // per live pair its chunk range; envelope tiles before each row block
     int max_col_rows = 0;
     bool trivial = false;  // nothing to optimise: the estimates are returned unchanged
     std::vector<int32_t> pose_h, hp_pose, point_h, hl_point, lm_e_start, lm_e, lg_start, lm_b_start, blk_pose, edge_blk, blk_lm,
@@ -1770,6 +1791,8 @@ struct LbaHost {
         col_rows_start.clear();
         col_rows.clear();
         live_pairs.clear();
+        live_chunk.clear();
+        env_off.clear();
         max_col_rows = 0;
         trivial = false;
         hp_pose.clear();
@@ -1888,8 +1911,9 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
         H.trivial = true;
         return OSG_OK;
     }
-    if (6 * (size_t)nhp * 6 * (size_t)nhp > (size_t(1) << 31))
-        return osg_set_error(ctx, OSG_E_INVALID, "%d free poses: the dense reduced system would exceed 2^31 entries", nhp);
+    // the pose-pair index (i <= j) is an int32_t; past CMAX the reduced system lives on its envelope
+    if ((size_t)nhp * ((size_t)nhp + 1) / 2 >= (size_t(1) << 31))
+        return osg_set_error(ctx, OSG_E_INVALID, "%d free poses: the pose-pair index would exceed 2^31", nhp);
     STRUCT_CP(1);
     const std::vector<int32_t> &pose_h = H.pose_h, &point_h = H.point_h;
     // edges per landmark (stable in edge order)
@@ -2165,6 +2189,9 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
                 for (int j = H.blk_first[t]; j < t; j++) H.col_rows[fill[j]++] = t;
             for (int j = 0; j < nb; j++)
                 H.max_col_rows = std::max(H.max_col_rows, H.col_rows_start[j + 1] - H.col_rows_start[j]);
+            // the envelope tile store (hs_at): row block t keeps tiles blk_first[t] .. t
+            H.env_off.assign(nb + 1, 0);
+            for (int t = 0; t < nb; t++) H.env_off[t + 1] = H.env_off[t] + (t - H.blk_first[t] + 1);
             // live pairs: (i <= j) with some entry (row in pose j, column in pose i) in a lower
             // envelope tile: row block of 6 j + r, column block of 6 i + c, blk_first[row blk] <= col blk
             std::vector<int32_t> fj(nhp);  // the smallest envelope start over pose j's two row blocks
@@ -2284,6 +2311,13 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
         for (int c = row_c0[i]; c < row_c0[i + 1]; c++) H.rs_chunk[fill[chunk_rs[c] - r0]++] = c;
     });
     }
+    if (!H.env_off.empty()) {  // past CMAX k_schur_pairs walks the live pairs only
+        H.live_chunk.resize(2 * std::max<size_t>(H.live_pairs.size(), 1));
+        for (size_t s = 0; s < H.live_pairs.size(); s++) {
+            H.live_chunk[2 * s] = H.pair_chunk[H.live_pairs[s]];
+            H.live_chunk[2 * s + 1] = H.pair_chunk[H.live_pairs[s] + 1];
+        }
+    }
     STRUCT_CP(9);
     H.rs_info.assign(8 * (size_t)std::max(H.n_rs, 1), 0);
     for (int w = 0; w < H.n_rs; w++) {
@@ -2348,7 +2382,8 @@ void carve_state(char *base, size_t &off, const LbaHost &H, LbaDev *D, bool prof
     double *bp = carve<double>(base, off, 6 * (size_t)nhp);
     double *Dinv = carve<double>(base, off, 9 * (size_t)nhl);
     double *bs_part = carve<double>(base, off, 6 * (size_t)std::max(H.n_rs, 1));
-    double *Hs = carve<double>(base, off, (size_t)sp * sp);
+    // dense up to CMAX; past it the envelope's tiles only (the dense n^2 capped maps at 7 723 free KeyFrames)
+    double *Hs = carve<double>(base, off, H.env_off.empty() ? (size_t)sp * sp : (size_t)H.env_off.back() * CB * CB);
     double *bs = carve<double>(base, off, (size_t)sp);
     double *x = carve<double>(base, off, (size_t)sp + 3 * (size_t)nhl);
     double *part = carve<double>(base, off, 4 * (size_t)H.npart + 64);
@@ -2460,7 +2495,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     struct InOff {
         size_t fixed, epose, epoint, ecam, ekind, eobs, eisig, cams, poseh, hppose, pointh, hlpoint, lmes, lme, lgs, lmbs,
             blkpose, eblk, hpes, hpe, hpb, pairb, chs, pch, pose0, point0, erob,
-            prank, rscs, rsc, hprs, bfirst, blast, rsinfo, hpblm, rscd, crs, cr, live;
+            prank, rscs, rsc, hprs, bfirst, blast, rsinfo, hpblm, rscd, crs, cr, live, envo;
     };
     std::vector<InOff> io(NA);
     for (int a = 0; a < NA; a++) {
@@ -2492,7 +2527,10 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         o.hpb = pk.add(h.hp_b.data(), 4 * (size_t)nblk);
         o.pairb = pk.add(h.pair_b.data(), 4 * h.pair_b.size());
         o.chs = pk.add(h.chunk_start.data(), 4 * h.chunk_start.size());
-        o.pch = pk.add(h.pair_chunk.data(), 4 * h.pair_chunk.size());
+        // past CMAX only the live pairs' chunk ranges (the pair-indexed table is nhp^2 / 2 entries)
+        o.pch = h.env_off.empty() ? pk.add(h.pair_chunk.data(), 4 * h.pair_chunk.size())
+                                  : pk.add(h.live_chunk.data(), 4 * h.live_chunk.size());
+        o.envo = h.env_off.empty() ? SIZE_MAX : pk.add(h.env_off.data(), 4 * h.env_off.size());
         o.prank = pk.add(h.pair_rank.data(), 4 * h.pair_rank.size());
         o.bfirst = pk.add(h.blk_first.data(), 4 * std::max<size_t>(h.blk_first.size(), 1));
         o.blast = pk.add(h.blk_last.data(), 4 * std::max<size_t>(h.blk_last.size(), 1));
@@ -2590,7 +2628,9 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         D.pair_b = osg_dptr<int32_t>(din, o.pairb);
         D.nchunks = h.nchunks;
         D.chunk_start = osg_dptr<int32_t>(din, o.chs);
-        D.pair_chunk = osg_dptr<int32_t>(din, o.pch);
+        D.pair_chunk = h.env_off.empty() ? osg_dptr<int32_t>(din, o.pch) : nullptr;
+        D.live_chunk = h.env_off.empty() ? nullptr : osg_dptr<int32_t>(din, o.pch);
+        D.env_off = o.envo == SIZE_MAX ? nullptr : osg_dptr<int32_t>(din, o.envo);
         D.pair_rank = osg_dptr<int32_t>(din, o.prank);
         D.blk_first = osg_dptr<int32_t>(din, o.bfirst);
         D.blk_last = osg_dptr<int32_t>(din, o.blast);

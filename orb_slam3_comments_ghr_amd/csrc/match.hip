@@ -1415,6 +1415,24 @@ struct Problem {
     std::vector<uint8_t> qdesc, slot_ok;
     std::vector<float> q_angle;
     int32_t *out_mp12 = nullptr;   // KF-KF: result indexed by KF1 keypoint
+    // a new call's problem: the arrays are emptied but keep their capacity (a 256-frame batch would
+    // otherwise allocate and page in tens of MB of host memory per call)
+    void reset()
+    {
+        A = {};
+        host_slot = nullptr;
+        n_slot = 0;
+        out_mp12 = nullptr;
+        for (auto *v : {&q_feat, &q_cb, &q_ce, &q_mp, &q_off}) v->clear();
+        qdesc.clear();
+        slot_ok.clear();
+        q_angle.clear();
+    }
+};
+// the context's problems and packer, reused call to call (one context per host thread)
+struct MatchCache {
+    std::deque<Problem> P;
+    osg_packer pk;
 };
 
 constexpr int STATUS_INTS = 16;
@@ -1423,9 +1441,8 @@ constexpr int STATUS_INTS = 16;
 // a problem's candidate buffer when its count pass reports more than the capacity), and download
 // the slot arrays / KF-KF results and the per-problem match counts.
 template <int MODE>
-int run_batch(osg_ctx *ctx, std::deque<Problem> &P, const osg_packer &pk, int32_t *nmatches)
+int run_batch(osg_ctx *ctx, std::deque<Problem> &P, int B, const osg_packer &pk, int32_t *nmatches)
 {
-    const int B = (int)P.size();
     if (B == 0) return OSG_OK;
     // host phase stamps for OSG_MATCH_PROFILE=2: setup, sync + pack, launches, wait, results
     using hclock = std::chrono::steady_clock;
@@ -1993,11 +2010,16 @@ int run_problems(osg_ctx *ctx, int B, int32_t *nmatches, Prep prep)
 {
     if (!ctx) return OSG_E_INVALID;
     OSG_REQUIRE(ctx, B >= 0 && (B == 0 || nmatches), "batch size / nmatches");
-    std::deque<Problem> P;
-    osg_packer pk;
+    if (!ctx->match_cache) ctx->match_cache = std::make_shared<MatchCache>();
+    MatchCache &mc = *static_cast<MatchCache *>(ctx->match_cache.get());
+    std::deque<Problem> &P = mc.P;
+    osg_packer &pk = mc.pk;
+    pk.items.clear();
+    pk.total = 0;
+    while ((int)P.size() < B) P.emplace_back();
     for (int b = 0; b < B; b++) {
-        P.emplace_back();
-        const int rc = prep(P.back(), pk, b);
+        P[b].reset();
+        const int rc = prep(P[b], pk, b);
         if (rc < 0) {
             if (B > 1) {
                 const std::string msg = ctx->last_error;
@@ -2006,7 +2028,7 @@ int run_problems(osg_ctx *ctx, int B, int32_t *nmatches, Prep prep)
             return rc;
         }
     }
-    return run_batch<MODE>(ctx, P, pk, nmatches);
+    return run_batch<MODE>(ctx, P, B, pk, nmatches);
 }
 
 template <int MODE, typename Prep>

@@ -47,6 +47,7 @@ struct osg_ctx {
     size_t lb_cap = 0;
     uint32_t lb_epoch = 0;
     std::shared_ptr<void> lba_cache;  // host structures of the last LBA batch, reused (ba.hip)
+    std::shared_ptr<void> match_cache;  // the matchers' per-problem host arrays, reused (match.hip)
     bool lba_ktime = false;           // osg_lba_kernel_times: per-kernel HIP-event timing of LBA steps
     double lba_kms[OSG_LBA_NK] = {};
     int64_t lba_kn[OSG_LBA_NK] = {};

@@ -502,7 +502,7 @@ def synth_gba_graph(rng, n_kf=120, n_points=20000, bRobust=False, iterations=10,
 
 
 def synth_map_graph(rng, n_kf=1500, n_points=150000, spacing=0.3, k_range=(2, 6), bRobust=False, iterations=10,
-                    stereo_frac=0.0, n_levels=8, loop=False):
+                    stereo_frac=0.0, n_levels=8, loop=False, vectorized=False):
     """A map-scale whole-map BA (GlobalBundleAdjustemnt on a long sequence): n_kf keyframes 'spacing'
     m apart along a 0.45 km path, looking sideways at points 4 .. 6 m away spread along it, so a
     keyframe shares points only with its neighbours (~27 on each side) and the reduced camera
@@ -513,7 +513,11 @@ def synth_map_graph(rng, n_kf=1500, n_points=150000, spacing=0.3, k_range=(2, 6)
     loop=True: the same path closed into a circle (radius n_kf spacing / 2 pi, cameras looking
     outwards at a ring of points), so the last keyframes share points with the first ones — the map
     LoopClosing hands to GlobalBundleAdjustemnt after closing a loop (ref:src/LoopClosing.cc:2436):
-    the reduced camera system is the band plus the two corner blocks that join its ends."""
+    the reduced camera system is the band plus the two corner blocks that join its ends.
+
+    vectorized=True draws each point's observing keyframes and levels array-wise (another random stream
+    than the per-point loop, the same distribution): the maps of many thousand keyframes build in
+    seconds."""
     cam = pinhole_camera()
     L = spacing * (n_kf - 1)
     cx = np.arange(n_kf) * spacing
@@ -557,6 +561,22 @@ def synth_map_graph(rng, n_kf=1500, n_points=150000, spacing=0.3, k_range=(2, 6)
         v = EUROC_FY * Xc[..., 1] / Xc[..., 2] + EUROC_CY
         vis = (Xc[..., 2] > 0.5) & (u > 0) & (u < EUROC_W) & (v > 0) & (v < EUROC_H)
         vis[:, 1:] &= cand[:, 1:] != cand[:, :-1]  # clipped duplicates
+        if vectorized:
+            nvis = vis.sum(1)
+            kk = np.minimum(nvis, rng.integers(k_range[0], k_range[1] + 1, len(Pc)))
+            kk[nvis < 2] = 0
+            key = np.where(vis, rng.random(vis.shape), 2.0)   # k uniformly chosen visible candidates
+            order = np.argsort(key, 1)
+            take = np.arange(vis.shape[1])[None, :] < kk[:, None]
+            mi, ji = np.nonzero(take)
+            jsel = order[mi, ji]
+            srt = np.lexsort((jsel, mi))                       # per point in candidate order, as np.sort
+            mi, jsel = mi[srt], jsel[srt]
+            e_point.extend((p0 + mi).tolist())
+            e_pose.extend(cand[mi, jsel].tolist())
+            e_obs.extend(np.stack([u[mi, jsel], v[mi, jsel], Xc[mi, jsel, 2]], 1).tolist())
+            e_lev.extend(rng.choice(n_levels, len(mi), p=lev_p).tolist())
+            continue
         for m in range(len(Pc)):
             idx = np.nonzero(vis[m])[0]
             if len(idx) < 2:

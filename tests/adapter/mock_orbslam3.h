@@ -96,6 +96,8 @@ struct MapPoint {
     bool isBad() const { return bad; }
     int Observations() const { return nobs; }
     cv::Mat GetDescriptor() const { return desc; }
+    // the integration's non-cloning accessor: the 32 bytes under the feature lock
+    void GetDescriptorRow(unsigned char *dst) const { std::memcpy(dst, desc.buf.data(), 32); }
     std::map<KeyFrame *, std::tuple<int, int>> GetObservations() const { return obs; }
     void EraseObservation(KeyFrame *k) { obs.erase(k); }
     bool IsInKeyFrame(KeyFrame *k) const { return obs.count(k) != 0; }

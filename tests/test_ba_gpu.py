@@ -331,6 +331,43 @@ def test_gba_map_loop_closed(ctx, oracle, n_kf, n_pts):
     assert got.chi2_final < 0.2 * got.chi2_initial and got.iterations >= 5
 
 
+def test_gba_loop_map_device_bytes_on_envelope():
+    """The 1500-KF loop-closed map's reduced system lives on its envelope tiles (hs_at), not as the
+    dense 8 994^2 matrix (647 MB): a fresh context's arena after one call stays under 0.5 GB."""
+    from orb_slam3_comments_ghr_amd import Context
+    G = op.synth_map_graph(np.random.default_rng(4200 + 1500), n_kf=1500, n_points=150000, loop=True)
+    c = Context(0)
+    try:
+        r = op.Optimizer(c).BundleAdjustment(G)
+        held = c.device_bytes()
+    finally:
+        c.close()
+    assert r.iterations >= 5 and r.chi2_final < 0.2 * r.chi2_initial
+    assert held <= 500e6, held
+
+
+def test_gba_9000_kf_loop_map_accepted():
+    """A 9 000-KeyFrame loop-closed map (n = 53 994, 3.6 M edges): past the old dense-matrix cap of 7 723
+    free KeyFrames.  No oracle at this size (its envelope LDL^T takes minutes): the call must converge
+    like the smaller maps, and the same map run twice gives the same result bit for bit."""
+    from orb_slam3_comments_ghr_amd import Context
+    G = op.synth_map_graph(np.random.default_rng(4900), n_kf=9000, n_points=900000, loop=True, vectorized=True)
+    G.iterations = 5
+    c = Context(0)
+    try:
+        opt = op.Optimizer(c)
+        r = opt.BundleAdjustment(G)
+        r2 = opt.BundleAdjustment(G)
+        held = c.device_bytes()
+    finally:
+        c.close()
+    assert r.iterations >= 3 and r.chi2_final < 0.5 * r.chi2_initial, (r.iterations, r.chi2_initial, r.chi2_final)
+    assert np.isfinite(r.pose).all() and np.isfinite(r.point).all()
+    assert (r.iterations, r.trials) == (r2.iterations, r2.trials)
+    np.testing.assert_array_equal(r.pose, r2.pose)
+    assert held < 8e9, held
+
+
 def test_gba_and_lba_in_one_batch(ctx, oracle):
     """A LocalBA window and a whole-map BA in one lockstep batch: each equals its own call."""
     rng = np.random.default_rng(3300)

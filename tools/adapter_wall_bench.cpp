@@ -59,6 +59,12 @@ struct Barrier {
 
 static std::string pre(int i) { return "p" + std::to_string(i) + "."; }
 
+// OSG_WALL_SPLIT=1 (probe runs only): before each repetition, thread 0 times the adapter's gathers of
+// the same frames alone, per stage, and the JSON line carries them as "thread0_gather_s"
+static const bool g_split = getenv("OSG_WALL_SPLIT") && atoi(getenv("OSG_WALL_SPLIT")) == 1;
+static thread_local double g_split_s[4] = {0, 0, 0, 0};
+static double g_split_t0[4] = {0, 0, 0, 0};
+
 // The per-thread work of one workload: the constructor builds the thread's B frames; rep() runs one
 // repetition of every stage, adds each stage's seconds to stage_s and, when `record` is given, keeps
 // the per-frame results.
@@ -106,6 +112,20 @@ struct C3 : Workload {
     }
     void rep(std::vector<double> &st, std::vector<std::vector<int32_t>> *rec) override
     {
+        if (g_split) {  // the adapter's gathers alone (no C-ABI call), timed apart from the stages
+            auto g0 = Clock::now();
+            {
+                std::deque<oa::BowKfF<KeyFrame, Frame, MapPoint>> g;
+                for (size_t b = 0; b < kfs.size(); b++) g.emplace_back(kfs[b], *fbp[b]);
+            }
+            auto g1 = Clock::now();
+            {
+                std::deque<oa::PoseGather<MockHooks, Frame>> g;
+                for (auto *f : fpp) g.emplace_back(f, (oa::NoMutex *)nullptr);
+            }
+            g_split_s[0] += secs(g0, g1);
+            g_split_s[1] += secs(g1, Clock::now());
+        }
         auto t0 = Clock::now();
         std::vector<std::vector<MapPoint *>> matches;
         oa::search_by_bow_kf_f_batch<MockHooks>(kfs, fbp, matches, 0.7f, true, nm.data());
@@ -166,6 +186,26 @@ struct C5 : Workload {
     void rep(std::vector<double> &st, std::vector<std::vector<int32_t>> *rec) override
     {
         const size_t B = fl.size();
+        if (g_split) {  // the adapter's gathers alone (no C-ABI call), timed apart from the stages
+            auto g0 = Clock::now();
+            {
+                std::deque<oa::LastGather<MockHooks, Frame>> g;
+                for (size_t b = 0; b < B; b++) g.emplace_back(*flp[b], *lfs[b]);
+            }
+            auto g1 = Clock::now();
+            {
+                std::deque<oa::MpsGather<Frame, MapPoint>> g;
+                for (size_t b = 0; b < B; b++) g.emplace_back(*fmp[b], *qs[b]);
+            }
+            auto g2 = Clock::now();
+            {
+                std::deque<oa::PoseGather<MockHooks, Frame>> g;
+                for (auto *f : fpp) g.emplace_back(f, (oa::NoMutex *)nullptr);
+            }
+            g_split_s[0] += secs(g0, g1);
+            g_split_s[1] += secs(g1, g2);
+            g_split_s[2] += secs(g2, Clock::now());
+        }
         auto t0 = Clock::now();
         for (size_t b = 0; b < B; b++) fl[b].mvpMapPoints = src_l[b]->mvpMapPoints;
         oa::search_by_projection_last_batch<MockHooks>(flp, lfs, 7.f, false, true, nl.data());
@@ -354,6 +394,8 @@ int main(int argc, char **argv)
                 if (err[t].empty())
                     for (int r = 0; r < reps; r++) w->rep(stage_s[t], nullptr);
                 end[t] = Clock::now();
+                if (t == 0)
+                    for (int k = 0; k < 4; k++) g_split_t0[k] = g_split_s[k];
             });
         ready.wait();
         const auto t0 = Clock::now();
@@ -370,7 +412,10 @@ int main(int argc, char **argv)
                     wl.c_str(), B, reps, T, n_pool, frames, wall, frames / wall);
         for (size_t s = 0; s < stages.size(); s++)
             std::printf("%s\"%s\": %.6f", s ? ", " : "", stages[s].c_str(), stage_s[0][s]);
-        std::printf("}, \"first_rep\": {");
+        std::printf("}");
+        if (g_split)
+            std::printf(", \"thread0_gather_s\": [%.6f, %.6f, %.6f]", g_split_t0[0], g_split_t0[1], g_split_t0[2]);
+        std::printf(", \"first_rep\": {");
         const int nrec = std::min(B, n_pool);
         for (size_t s = 0; s < first.size(); s++) {
             std::printf("%s\"%s\": [", s ? ", " : "", records[s].c_str());
