@@ -185,18 +185,18 @@ inline void push_kp(const KeyPointT &kp, std::vector<float> &x, std::vector<floa
 // `void GetDescriptorRow(unsigned char *dst) const` (the 32 bytes copied under mMutexFeatures,
 // INTEGRATION.md §2) is read through that instead -- measured 33 ns of the gather per MapPoint.
 template <class MapPointT>
-inline auto mp_descriptor_(const MapPointT *p, uint8_t *dst, int) -> decltype(p->GetDescriptorRow(dst), void())
+inline auto mp_descriptor_(MapPointT *p, uint8_t *dst, int) -> decltype(p->GetDescriptorRow(dst), void())
 {
     p->GetDescriptorRow(dst);
 }
 template <class MapPointT>
-inline void mp_descriptor_(const MapPointT *p, uint8_t *dst, long)
+inline void mp_descriptor_(MapPointT *p, uint8_t *dst, long)
 {
     const auto d = p->GetDescriptor();
     std::memcpy(dst, d.template ptr<unsigned char>(0), 32);
 }
 template <class MapPointT>
-inline void mp_descriptor(const MapPointT *p, uint8_t *dst)
+inline void mp_descriptor(MapPointT *p, uint8_t *dst)
 {
     mp_descriptor_(p, dst, 0);
 }

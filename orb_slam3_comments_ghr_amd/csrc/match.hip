@@ -2017,6 +2017,8 @@ int run_problems(osg_ctx *ctx, int B, int32_t *nmatches, Prep prep)
     pk.items.clear();
     pk.total = 0;
     while ((int)P.size() < B) P.emplace_back();
+    static const int prof_level = getenv("OSG_MATCH_PROFILE") ? atoi(getenv("OSG_MATCH_PROFILE")) : 0;
+    const auto tp = std::chrono::steady_clock::now();
     for (int b = 0; b < B; b++) {
         P[b].reset();
         const int rc = prep(P[b], pk, b);
@@ -2028,6 +2030,9 @@ int run_problems(osg_ctx *ctx, int B, int32_t *nmatches, Prep prep)
             return rc;
         }
     }
+    if (prof_level >= 2)
+        fprintf(stderr, "[osg match prep] mode %d B %d: %.1f us\n", MODE, B,
+                std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tp).count());
     return run_batch<MODE>(ctx, P, B, pk, nmatches);
 }
 

@@ -114,14 +114,14 @@ struct C3 : Workload {
     {
         if (g_split) {  // the adapter's gathers alone (no C-ABI call), timed apart from the stages
             auto g0 = Clock::now();
-            {
-                std::deque<oa::BowKfF<KeyFrame, Frame, MapPoint>> g;
-                for (size_t b = 0; b < kfs.size(); b++) g.emplace_back(kfs[b], *fbp[b]);
+            {  // the entry points' own per-thread pools (warm buffers, as the stage's gather)
+                auto &g = oa::gather_pool<oa::BowKfF<KeyFrame, Frame, MapPoint>>(kfs.size());
+                for (size_t b = 0; b < kfs.size(); b++) g[b].assign(kfs[b], *fbp[b]);
             }
             auto g1 = Clock::now();
             {
-                std::deque<oa::PoseGather<MockHooks, Frame>> g;
-                for (auto *f : fpp) g.emplace_back(f, (oa::NoMutex *)nullptr);
+                auto &g = oa::gather_pool<oa::PoseGather<MockHooks, Frame>>(fpp.size());
+                for (size_t b = 0; b < fpp.size(); b++) g[b].assign(fpp[b], (oa::NoMutex *)nullptr);
             }
             g_split_s[0] += secs(g0, g1);
             g_split_s[1] += secs(g1, Clock::now());
@@ -189,18 +189,18 @@ struct C5 : Workload {
         if (g_split) {  // the adapter's gathers alone (no C-ABI call), timed apart from the stages
             auto g0 = Clock::now();
             {
-                std::deque<oa::LastGather<MockHooks, Frame>> g;
-                for (size_t b = 0; b < B; b++) g.emplace_back(*flp[b], *lfs[b]);
+                auto &g = oa::gather_pool<oa::LastGather<MockHooks, Frame>>(B);
+                for (size_t b = 0; b < B; b++) g[b].assign(*flp[b], *lfs[b]);
             }
             auto g1 = Clock::now();
             {
-                std::deque<oa::MpsGather<Frame, MapPoint>> g;
-                for (size_t b = 0; b < B; b++) g.emplace_back(*fmp[b], *qs[b]);
+                auto &g = oa::gather_pool<oa::MpsGather<Frame, MapPoint>>(B);
+                for (size_t b = 0; b < B; b++) g[b].assign(*fmp[b], *qs[b]);
             }
             auto g2 = Clock::now();
             {
-                std::deque<oa::PoseGather<MockHooks, Frame>> g;
-                for (auto *f : fpp) g.emplace_back(f, (oa::NoMutex *)nullptr);
+                auto &g = oa::gather_pool<oa::PoseGather<MockHooks, Frame>>(fpp.size());
+                for (size_t b = 0; b < fpp.size(); b++) g[b].assign(fpp[b], (oa::NoMutex *)nullptr);
             }
             g_split_s[0] += secs(g0, g1);
             g_split_s[1] += secs(g1, g2);
