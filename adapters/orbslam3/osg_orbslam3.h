@@ -208,6 +208,17 @@ inline void copy_desc_rows(const MatT &m, int n, std::vector<uint8_t> &out)
     for (int i = 0; i < n; i++) std::memcpy(&out[(size_t)32 * i], m.template ptr<unsigned char>(i), 32);
 }
 
+// The n descriptor rows as one contiguous block: the Mat's own storage when its rows are packed (an
+// ORBextractor's N x 32 CV_8U output is), else a copy into `out`.  The ABI calls read it before they
+// return, so pointing into the Frame's Mat is safe.
+template <class MatT>
+inline const uint8_t *desc_rows(const MatT &m, int n, std::vector<uint8_t> &out)
+{
+    if (n > 0 && m.rows >= n && (size_t)m.step[0] == 32) return m.template ptr<unsigned char>(0);
+    copy_desc_rows(m, n, out);
+    return out.data();
+}
+
 // 64 x 48 grid of vectors as CSR in GetFeaturesInArea's enumeration order (ix outer, iy inner,
 // cell contents in insertion order)
 template <class GridT>
@@ -274,7 +285,7 @@ struct FrameView {
             ka[i] = kp.angle;
             ko[i] = kp.octave;
         }
-        copy_desc_rows(F.mDescriptors, n, desc);
+        const uint8_t *dp = desc_rows(F.mDescriptors, n, desc);
         ur.assign(F.mvuRight.begin(), F.mvuRight.end());
         ur.resize(n, -1.0f);
         grid_csr(F.mGrid, gs, gi);
@@ -292,7 +303,7 @@ struct FrameView {
         scale.assign(F.mvScaleFactors.begin(), F.mvScaleFactors.end());
         v.n = n;
         v.nleft = nleft;
-        v.desc = desc.data();
+        v.desc = dp;
         v.kp_x = kx.data();
         v.kp_y = ky.data();
         v.kp_angle = ka.data();
@@ -733,9 +744,10 @@ struct BowKfF {
         ak.resize(nk);
         af.resize(nf);
         idk.assign(nk, -1);
-        copy_desc_rows(pKF->mDescriptors, nk, dk);
-        copy_desc_rows(F.mDescriptors, nf, df);
+        const uint8_t *dkp = desc_rows(pKF->mDescriptors, nk, dk), *dfp = desc_rows(F.mDescriptors, nf, df);
+        constexpr int PF = 8;  // isBad() reads each MapPoint, scattered heap objects: fetch a few ahead
         for (int i = 0; i < nk; i++) {
+            if (i + PF < nk && vpMPsKF[i + PF]) __builtin_prefetch(vpMPsKF[i + PF]);
             // ref:src/ORBmatcher.cc:399-401
             ak[i] = (!pKF->mpCamera2) ? pKF->mvKeysUn[i].angle
                                       : (i >= pKF->NLeft ? pKF->mvKeysRight[i - pKF->NLeft].angle : pKF->mvKeys[i].angle);
@@ -744,8 +756,8 @@ struct BowKfF {
         }
         for (int i = 0; i < nf; i++)
             af[i] = (F.Nleft == -1) ? F.mvKeysUn[i].angle : (i < F.Nleft ? F.mvKeys[i].angle : F.mvKeysRight[i - F.Nleft].angle);
-        sk = osg_bow_side{nk, pKF->NLeft, dk.data(), ak.data(), idk.data(), good.data(), fk.view()};
-        sf = osg_bow_side{nf, F.Nleft, df.data(), af.data(), nullptr, nullptr, ff.view()};
+        sk = osg_bow_side{nk, pKF->NLeft, dkp, ak.data(), idk.data(), good.data(), fk.view()};
+        sf = osg_bow_side{nf, F.Nleft, dfp, af.data(), nullptr, nullptr, ff.view()};
     }
     // ref:src/ORBmatcher.cc:268 (the vector is re-initialised whatever happens) + the matches
     void apply(const int32_t *out, int nf, std::vector<MapPointT *> &vpMapPointMatches, bool ok) const
@@ -1026,18 +1038,17 @@ struct StereoGather {
         const int n = F.N, nr = (int)F.mvKeysRight.size();
         for (int i = 0; i < n; i++) push_kp(F.mvKeys[i], x, y, ang, o);
         for (int i = 0; i < nr; i++) push_kp(F.mvKeysRight[i], xr, yr, ang, orr);
-        copy_desc_rows(F.mDescriptors, n, dl);
-        copy_desc_rows(F.mDescriptorsRight, nr, dr);
+        const uint8_t *dlp = desc_rows(F.mDescriptors, n, dl), *drp = desc_rows(F.mDescriptorsRight, nr, dr);
         s.n = n;
         s.x = x.data();
         s.y = y.data();
         s.octave = o.data();
-        s.desc = dl.data();
+        s.desc = dlp;
         s.n_right = nr;
         s.xr = xr.data();
         s.yr = yr.data();
         s.octave_r = orr.data();
-        s.desc_r = dr.data();
+        s.desc_r = drp;
         s.scale_factors = sc.data();
         s.inv_scale_factors = isc.data();
         s.n_levels = (int)sc.size();

@@ -5,8 +5,8 @@
 
 Headline (BASELINE.json metric "Mmatches/s (256-bit Hamming) + LocalBA iters/s"), workload
 configs[1]: brute-force 256-bit Hamming top-2 of 2000 x 2000 descriptors (C2).  One step = one
-launch of 256 independent 2000 x 2000 problems (frames) through the C-ABI entry
-osg_hamming_top2_batch_dev (k_top2_batch) with inputs resident in HBM; the one-problem launch
+launch of 1024 independent 2000 x 2000 problems (frames) through the C-ABI entry
+osg_hamming_top2_batch_dev (k_top2_mfma, I8 matrix cores) with inputs resident in HBM; the one-problem launch
 (osg_hamming_top2_dev) is reported beside it as single_launch.  For N > 1 every rank matches its own
 independent frames (weak scaling; no collective in the data path); value = pairs of all ranks /
 max-over-ranks time.
@@ -15,11 +15,13 @@ Also reported (same run):
   * the dominant kernel's roofline (HIP events on its stream) and the C2' streaming kernel's HBM roofline
     (Q = 4 x M = 2^24);
   * the CPU restatement timed on this host (cpu_baseline);
-  * the frame-batched workloads: C3, C5, DBoW2, ComputeStereoMatches and the ORB extractor stages, with their
-    single-call latencies and the C++ adapter's wall rate (tools/adapter_wall_bench.cpp);
+  * the frame-batched workloads: C3, C5, DBoW2 and ComputeStereoMatches, each valued at the C++ adapter's wall
+    rate (tools/adapter_wall_bench.cpp: mock ORB-SLAM3 objects -> C-ABI -> write-back, as many host threads as
+    the CPU baseline) with the batched launches' device-time rate beside it, and the ORB extractor stages;
   * LocalBA iterations/s on C4 (64-window batches, --lba-threads host threads);
   * global BA on 150 KeyFrames and on the 1500-KeyFrame map.
 --only STAGE[,STAGE] runs a subset of those stages (A/B runs).
+stdout carries one compact JSON line (<= 8 KB, compact_line); the full record goes to --detail.
 """
 from __future__ import annotations
 
@@ -80,7 +82,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--nq", type=int, default=2000)
     ap.add_argument("--nt", type=int, default=2000)
-    ap.add_argument("--c2-batch", type=int, default=256,
+    ap.add_argument("--c2-batch", type=int, default=1024,
                     help="C2 frames per launch of the headline step (1: the single-problem launch)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")

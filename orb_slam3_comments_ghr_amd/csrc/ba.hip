@@ -120,6 +120,7 @@ struct LbaDev {
     double user_lambda;
     // state: estimate buffers A / B; ctl->sel says which one is current
     double *poseA, *poseB, *pointA, *pointB;
+    const double *pose0, *point0;        // the graph's input estimates (packed input), copied to A by k_init_state
     LbaCtl *ctl;                         // per-step control, written by the host each step
     double *out;                         // per-step results (k_step_reduce)
     uint8_t *bad;                        // classification
@@ -154,6 +155,7 @@ struct LbaDev {
 };
 
 __device__ inline double edge_w(const LbaDev &D, int e) { return (double)D.e_isig2[e]; }
+constexpr int CB_ROWS = 32;  // the envelope tile edge (= CB, the factorisation's block)
 // Hs element (R, C): dense row-major up to CMAX, else its place in the envelope tile store (which
 // must hold it: hs_stored)
 __device__ inline size_t hs_at(const LbaDev &D, int n, int R, int C)
@@ -161,6 +163,21 @@ __device__ inline size_t hs_at(const LbaDev &D, int n, int R, int C)
     if (!D.env_off) return (size_t)R * n + C;
     const int t = R >> 5, u = C >> 5;
     return ((size_t)(D.env_off[t] + u - D.blk_first[t]) << 10) + (size_t)((R & 31) << 5) + (size_t)(C & 31);
+}
+// Row block t of Hs (rows 32 t .. 32 t + 31): element (32 t + r, C) at hs_el(blk, r, C).  The kernels
+// that stay in one row block take this once instead of an envelope lookup per element.
+struct HsBlk {
+    long long base;
+    int rs, ts;  // row stride, tile stride (dense: n, 32; envelope: 32, 1024)
+};
+__device__ inline HsBlk hs_blk(const LbaDev &D, int n, int t)
+{
+    if (!D.env_off) return HsBlk{(long long)CB_ROWS * t * n, n, CB_ROWS};
+    return HsBlk{(long long)(D.env_off[t] - D.blk_first[t]) << 10, CB_ROWS, CB_ROWS * CB_ROWS};
+}
+__device__ inline size_t hs_el(const HsBlk &h, int r, int C)
+{
+    return (size_t)(h.base + (long long)r * h.rs + (long long)(C >> 5) * h.ts + (C & 31));
 }
 __device__ inline bool hs_stored(const LbaDev &D, int R, int C)
 {
@@ -362,6 +379,20 @@ __global__ __launch_bounds__(EB) void k_linearize(const LbaDev *__restrict__ Ds)
         for (int i = 0; i < EB / 64; i++) m = fmax(m, s_m[i]);
         D.part[2 * D.npart + bx] = m;
     }
+}
+
+// The input estimates into estimate buffer A, every graph of the batch in one launch (instead of two
+// copy-engine blits per graph: 128 dispatches of ~5 us each for a 64-window batch, r05a trace)
+__global__ __launch_bounds__(EB) void k_init_state(const LbaDev *__restrict__ Ds)
+{
+    const bool xcd_map_ = Ds[0].xcd_map;
+    const int by = xcd_map_ ? (int)(blockIdx.x & 7) + 8 * (int)blockIdx.y : (int)blockIdx.y;
+    const int bx = xcd_map_ ? (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+    if (by >= Ds[0].n_graphs) return;
+    const LbaDev &D = Ds[by];
+    const size_t i = (size_t)bx * EB + threadIdx.x, np7 = 7 * (size_t)D.np, npt3 = 3 * (size_t)D.npt;
+    if (i < np7) D.poseA[i] = D.pose0[i];
+    if (i < npt3) D.pointA[i] = D.point0[i];
 }
 
 // The static inputs k_pose_red reads per edge, gathered once per call into pose-major records: one
@@ -1014,11 +1045,12 @@ __device__ __forceinline__ void tile_left_update2(const LbaDev &D, const double 
     const bool two = R0 >= 0;
     // originals first: their latency overlaps the GEMM
     double aT[4], aX[4];
+    const HsBlk bT = hs_blk(D, n, C0 >> 5), bX = hs_blk(D, n, two ? R0 >> 5 : C0 >> 5);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int e = threadIdx.x + 256 * q, r = e >> 5, c = e & 31;
-        aT[q] = (C0 + r < n && C0 + c < n) ? A[hs_at(D, n, C0 + r, C0 + c)] : 0.0;
-        aX[q] = (two && R0 + r < n && C0 + c < n) ? A[hs_at(D, n, R0 + r, C0 + c)] : 0.0;
+        aT[q] = (C0 + r < n && C0 + c < n) ? A[hs_el(bT, r, C0 + c)] : 0.0;
+        aX[q] = (two && R0 + r < n && C0 + c < n) ? A[hs_el(bX, r, C0 + c)] : 0.0;
     }
     const int g4 = 4 * (l >> 4);
     const int rj0 = C0 + (l & 15), rj1 = C0 + 16 + (l & 15);
@@ -1278,10 +1310,11 @@ __device__ __forceinline__ void chol_offdiag_out(const LbaDev &D, CholLds &L, in
     }
     const int c = qc + (l & 15);
     double *Aw = D.Hs;
+    const HsBlk bR = hs_blk(D, n, R0 >> 5);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int r = qr + (l >> 4) + 4 * q;
-        if (R0 + r < n && c < nb) Aw[hs_at(D, n, R0 + r, k0 + c)] = acc[q];
+        if (R0 + r < n && c < nb) Aw[hs_el(bR, r, k0 + c)] = acc[q];
     }
 }
 
@@ -1454,10 +1487,11 @@ __global__ __launch_bounds__(256) void k_chol_trail(const LbaDev *__restrict__ D
     const int R0 = tb * CB, C0 = ub * CB, K0 = j * CB;
     __shared__ double sLt[CB][CB + 1], sLu[CB][CB + 1];
     const int tid = threadIdx.x;
+    const HsBlk bt = hs_blk(D, n, tb), bu = hs_blk(D, n, ub);
     for (int e = tid; e < CB * CB; e += 256) {
         const int r = e >> 5, c = e & 31;
-        sLt[r][c] = (R0 + r < n) ? D.Hs[hs_at(D, n, R0 + r, K0 + c)] : 0.0;
-        sLu[r][c] = (C0 + r < n) ? D.Hs[hs_at(D, n, C0 + r, K0 + c)] : 0.0;
+        sLt[r][c] = (R0 + r < n) ? D.Hs[hs_el(bt, r, K0 + c)] : 0.0;
+        sLu[r][c] = (C0 + r < n) ? D.Hs[hs_el(bu, r, K0 + c)] : 0.0;
     }
     __syncthreads();
     const int w = tid >> 6, l = tid & 63;
@@ -1472,7 +1506,7 @@ __global__ __launch_bounds__(256) void k_chol_trail(const LbaDev *__restrict__ D
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int r = qr + (l >> 4) + 4 * q;
-        if (R0 + r < n && C0 + c < n) D.Hs[hs_at(D, n, R0 + r, C0 + c)] -= acc[q];
+        if (R0 + r < n && C0 + c < n) D.Hs[hs_el(bt, r, C0 + c)] -= acc[q];
     }
     if (t == u && tid < CB && R0 + tid < n) {  // block j is full (m > 0): y_j is 32 entries
         double s = 0.0;
@@ -1515,8 +1549,8 @@ __global__ __launch_bounds__(1024) void k_chol_back_large(const LbaDev *__restri
         double acc = 0.0;
         if (c < nb) {
             for (int q = D.col_rows_start[bi]; q < D.col_rows_start[bi + 1]; q++) {
-                const int row = D.col_rows[q] * CB + g;
-                if (row < n) acc += A[hs_at(D, n, row, k0 + c)] * s_x[row];
+                const int rb = D.col_rows[q], row = rb * CB + g;
+                if (row < n) acc += A[hs_el(hs_blk(D, n, rb), g, k0 + c)] * s_x[row];
             }
         }
         s_part[c][g] = acc;
@@ -1574,8 +1608,9 @@ __global__ __launch_bounds__(BSC) void k_back_step(const LbaDev *__restrict__ Ds
     if (u >= k0) return;
     const double *A = D.Hs;
     double acc = 0.0;
+    const HsBlk bb = hs_blk(D, n, bi);
 #pragma unroll 8
-    for (int r = 0; r < nb; r++) acc += A[hs_at(D, n, k0 + r, u)] * s_x[r];
+    for (int r = 0; r < nb; r++) acc += A[hs_el(bb, r, u)] * s_x[r];
     D.x[u] -= acc;
 }
 __global__ __launch_bounds__(EB) void k_back_copy(const LbaDev *__restrict__ Ds)
@@ -2575,6 +2610,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     int mx_gll = 1;
     bool any_multi = false;
     int mx_nhe = 0;
+    size_t mx_init = 0;  // k_init_state's extent: the largest 7 np / 3 npt of the batch
     int mx_ge = 0, mx_gl = 1, mx_gu = 0, mx_nblk = 0, mx_nhp = 0, mx_chunks = 0, mx_pairs = 0, mx_red = 0, mx_rs = 0;
     // XCD-aware graph placement (LBA_GRAPH) for batches of >= 8 graphs: OSG_LBA_XCD=1.  Off by
     // default: measured slower (64 C4 windows: k_schur_rows 10.4 vs 8.9 ms, k_linearize 5.4 vs 4.4 ms
@@ -2657,8 +2693,9 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         carve_state(dst + st_off[a], off, h, &D, prof_ts);
         D.ctl = d_ctl + a;
         D.out = d_out + 8 * a;
-        OSG_HIP_CHECK(ctx, hipMemcpyAsync(D.poseA, din + o.pose0, 56 * (size_t)h.np, hipMemcpyDeviceToDevice, ctx->stream));
-        OSG_HIP_CHECK(ctx, hipMemcpyAsync(D.pointA, din + o.point0, 24 * (size_t)h.npt, hipMemcpyDeviceToDevice, ctx->stream));
+        D.pose0 = osg_dptr<double>(din, o.pose0);
+        D.point0 = osg_dptr<double>(din, o.point0);
+        mx_init = std::max(mx_init, std::max(7 * (size_t)h.np, 3 * (size_t)h.npt));
         mx_ge = std::max(mx_ge, h.ge);
         mx_gl = std::max(mx_gl, h.gl);
         mx_gll = std::max(mx_gll, h.gll);
@@ -2673,6 +2710,10 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         mx_red = std::max(mx_red, h.nblk_red);
     }
     OSG_HIP_CHECK(ctx, hipMemcpyAsync(d_dev, h_dev, dev_bytes, hipMemcpyHostToDevice, ctx->stream));
+    {
+        const int gi = (int)std::max<size_t>((mx_init + EB - 1) / EB, 1);
+        hipLaunchKernelGGL(k_init_state, xcd ? dim3(8 * gi, (NA + 7) / 8) : dim3(gi, NA), dim3(EB), 0, ctx->stream, d_dev);
+    }
     if (mx_nhe > 0 && !pose_red_gather) {
         const dim3 g = xcd ? dim3(8 * ((mx_nhe + EB - 1) / EB), (NA + 7) / 8) : dim3((mx_nhe + EB - 1) / EB, NA);
         hipLaunchKernelGGL(k_hp_rec, g, dim3(EB), 0, ctx->stream, d_dev);
@@ -2713,7 +2754,9 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
 
     // one lockstep step: every kernel once for all graphs, then 5 scalars per graph back
     auto run_step = [&]() -> int {
-        OSG_HIP_CHECK(ctx, hipMemcpyAsync(d_ctl, h_ctl, ctl_bytes, hipMemcpyHostToDevice, ctx->stream));
+        // the per-step control through a copy kernel in the stream's own queue (osg_upload), not the
+        // copy engine: the first kernel of the step then does not wait for an SDMA completion signal
+        OSG_RC(osg_upload(ctx, d_ctl, h_ctl, ctl_bytes));
         const dim3 yb = xcd ? dim3(8, (NA + 7) / 8) : dim3(1, NA);
         auto gx = [&](int n) { return xcd ? dim3(8 * std::max(n, 1), (NA + 7) / 8) : dim3(std::max(n, 1), NA); };
         LBA_MARK(KT_ERR);

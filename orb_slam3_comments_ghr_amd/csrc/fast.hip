@@ -337,12 +337,15 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
         score_off[l] = score_bytes;
         score_bytes += ((size_t)P->rows[l] * P->cols[l] * 2 + 255) & ~size_t(255);
     }
-    size_t max_keys = 0;  // one slot per tested pixel of every cell
+    // slots per cell: a kept pixel is a strict maximum of its 8 neighbours, so no two kept pixels are
+    // adjacent and an h x w cell holds at most ceil(h / 2) ceil(w / 2) of them (a quarter of the tested
+    // pixels, where one slot per pixel sized a 64-image batch's staging at ~2.4 GB: ADVICE r04)
+    size_t max_keys = 0;
     for (Cell &c : cells) {
         const int h = std::max(0, c.r1 - c.r0 - 6), w = std::max(0, c.c1 - c.c0 - 6);
         OSG_REQUIRE(ctx, h + 2 <= MAX_T && w + 2 <= MAX_T, "cell of %d x %d tested pixels", h, w);
         c.slot = (int)max_keys;
-        max_keys += (size_t)h * w;
+        max_keys += (size_t)((h + 1) / 2) * (size_t)((w + 1) / 2);
     }
     max_keys = (max_keys + 15) & ~size_t(15);
     OSG_REQUIRE(ctx, (size_t)B * max_keys < (size_t(1) << 31), "batch too large");
@@ -382,8 +385,8 @@ int detect_run(osg_ctx *ctx, const osg_image_pyramid *P, int ini_th, int min_th,
     // pinned: inputs, then the totals and counts, then the keys
     const size_t in_pad = (pk.total + 255) & ~size_t(255);
     const size_t cnt_pad = (sizeof(int32_t) * ((size_t)nc * B + B) + 255) & ~size_t(255);
-    // (a batch's keys get their own staging request once the totals are known: max_keys is every
-    // tested pixel of an image, ~100x the keypoints)
+    // (a batch's keys get their own staging request once the totals are known: max_keys is a quarter of
+    // an image's tested pixels, ~25x the keypoints)
     const size_t keys_pin = B == 1 ? sizeof(float4) * (max_keys + 1) : 0;
     char *pin = (char *)osg_pinned(ctx, in_pad + cnt_pad + keys_pin + 256);
     if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");

@@ -1,16 +1,14 @@
 #!/bin/bash
-# Global BA A/B between the current library and another build (OSG_LIB_PATH), two runs each (one gpurun call).
+# Global-BA A/B: tools/gba_kernel_probe.py with the current library and build/old (OSG_LIB_PATH),
+# alternating, two runs each.  Each GPU step has its own time limit; the chain stops at a failure.
 set -o pipefail
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-OUT=$R/gpurun_out/${1:-r03gbaab}
-OTHER=${2:-$R/build/old/liborbslam3_amd.so}
+OUT=$R/gpurun_out/${1:-gbaab}
 mkdir -p $OUT
 cd $R
-ARGS="--no-cpu --no-stream --no-ba --no-frames --no-gba-map --steps 3 --warmup 1"
-for v in cur other cur other; do
-  if [ $v = other ]; then export OSG_LIB_PATH=$OTHER; else unset OSG_LIB_PATH; fi
-  timeout -k 10 200 python3 bench.py $ARGS > $OUT/$v.json 2>> $OUT/err.log || exit 1
-  python3 -c "import json,sys; d=json.loads(open('$OUT/$v.json').read().strip().splitlines()[-1]); g=d['global_ba']; print('$v', g['value'], g['ms_per_gba'])" >> $OUT/ab.txt
+for v in cur old cur old; do
+  if [ $v = old ]; then export OSG_LIB_PATH=$R/build/old/liborbslam3_amd.so; else unset OSG_LIB_PATH; fi
+  timeout -k 10 240 python3 -u tools/gba_kernel_probe.py --label $v >> $OUT/ab.jsonl 2>> $OUT/err.log || exit 1
 done
-echo "exit=$?"
+echo "exit=0"

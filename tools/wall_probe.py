@@ -62,7 +62,8 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "wallp"))
     ap.add_argument("--threads", default="1,8,16")
     ap.add_argument("--workloads", default="c3,c5")
-    ap.add_argument("--frames", type=int, default=256)
+    ap.add_argument("--frames", default="256", help="frames per batched call, comma-separated list")
+    ap.add_argument("--no-split", action="store_true", help="skip the OSG_WALL_SPLIT runs")
     ap.add_argument("--reps", type=int, default=12)
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
@@ -70,14 +71,14 @@ def main():
     for wl in a.workloads.split(","):
         path = os.path.join(a.out, f"{wl}.arrays")
         write_arrays(path, c3_pool() if wl == "c3" else c5_pool())
-        for t in [int(x) for x in a.threads.split(",")]:
-            for split in (0, 1):
+        for t, fr in [(int(x), int(f)) for x in a.threads.split(",") for f in a.frames.split(",")]:
+            for split in ((0,) if a.no_split else (0, 1)):
                 env = dict(os.environ, OSG_WALL_SPLIT=str(split))
                 if t == 1 and split:
                     env["OSG_MATCH_PROFILE"] = "2"
-                errf = os.path.join(a.out, f"{wl}_t{t}_s{split}.err")
+                errf = os.path.join(a.out, f"{wl}_t{t}_f{fr}_s{split}.err")
                 with open(errf, "w") as ef:
-                    r = subprocess.run([exe, wl, path, str(a.frames), str(a.reps), str(t)], stdout=subprocess.PIPE,
+                    r = subprocess.run([exe, wl, path, str(fr), str(a.reps * 256 // fr), str(t)], stdout=subprocess.PIPE,
                                        stderr=ef, text=True, timeout=300, env=env)
                 if r.returncode != 0:
                     print(json.dumps({"workload": wl, "threads": t, "split": split, "rc": r.returncode}), flush=True)
