@@ -286,8 +286,10 @@ __global__ __launch_bounds__(EB) void k_errors(const LbaDev *__restrict__ Ds, in
 // The workgroup's max |diag Hll| goes to the computeLambdaInit partials.  The edges' pose parts
 // {Hpp upper 21, b_p 6} are not stored: k_pose_red recomputes them pose-major (27 doubles per edge
 // written and read back cost more HBM time than the recomputed Jacobian costs VALU time).
-template <bool MULTI>
-__global__ __launch_bounds__(EB) void k_linearize(const LbaDev *__restrict__ Ds)
+// WPE: the minimum waves per SIMD the register allocation must allow (1: the compiler's choice, 146
+// VGPRs = 3 waves; 4: 128 VGPRs with a few spills, OSG_LIN_WPE=4)
+template <bool MULTI, int WPE = 1>
+__global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_linearize(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_LIN);
     if (bx >= max(D.gll, 1)) return;
@@ -2474,6 +2476,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     // OSG_UPDATE_STAGE=1: k_update reads Hpl through LDS pieces (A/B runs), bit-identical
     // OSG_SCHUR_POINT=1: Dinv and Dinv b_l from a kernel of their own (A/B runs), bit-identical
     static const bool schur_point = getenv("OSG_SCHUR_POINT") && atoi(getenv("OSG_SCHUR_POINT")) != 0;
+    // OSG_LIN_WPE=4: k_linearize compiled for 4 waves per SIMD (A/B runs), bit-identical
+    static const bool lin_wpe4 = getenv("OSG_LIN_WPE") && atoi(getenv("OSG_LIN_WPE")) == 4;
     static const bool update_stage = getenv("OSG_UPDATE_STAGE") && atoi(getenv("OSG_UPDATE_STAGE")) != 0;
     const auto tp0 = std::chrono::steady_clock::now();
     auto ms_since = [&](std::chrono::steady_clock::time_point t) {
@@ -2763,6 +2767,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         hipLaunchKernelGGL(k_errors, gx(mx_ge), dim3(EB), 0, ctx->stream, d_dev, 1);
         LBA_MARK(KT_LIN);
         if (any_multi) hipLaunchKernelGGL(k_linearize<true>, gx(mx_gll), dim3(EB), 0, ctx->stream, d_dev);
+        else if (lin_wpe4) hipLaunchKernelGGL((k_linearize<false, 4>), gx(mx_gll), dim3(EB), 0, ctx->stream, d_dev);
         else hipLaunchKernelGGL(k_linearize<false>, gx(mx_gll), dim3(EB), 0, ctx->stream, d_dev);
         LBA_MARK(KT_POSE);
         if (mx_nhp > 0) {

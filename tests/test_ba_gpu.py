@@ -227,7 +227,8 @@ def _gba_variant_graph():
 
 
 @pytest.mark.parametrize("env", [{"OSG_SCHUR_STAGE": "1"}, {"OSG_SCHUR_DIRECT": "1"}, {"OSG_POSE_RED_GATHER": "1"},
-                                 {"OSG_UPDATE_STAGE": "1"}, {"OSG_SCHUR_POINT": "1"}],
+                                 {"OSG_UPDATE_STAGE": "1"}, {"OSG_SCHUR_POINT": "1"},
+                                 {"OSG_LIN_WPE": "4"}],
                          ids=lambda e: "-".join(f"{k[4:]}={v}" for k, v in e.items()))
 def test_lba_schur_variants_bit_identical(ctx, env):
     """Kernel variants that read their inputs differently but compute the same products in the same
@@ -235,7 +236,8 @@ def test_lba_schur_variants_bit_identical(ctx, env):
     product's LDS-staged partner spans (k_schur_rows_st) and per-lane loads against the per-group
     gathers (k_schur_rows), k_pose_red's edge inputs gathered through hp_e against the pose-major
     records (k_hp_rec), k_update's Hpl blocks through LDS pieces against per-thread reads, and
-    Dinv from k_schur_point against Dinv formed by its readers.  The GBA graph has per-edge robust flags off (bRobust = false)."""
+    Dinv from k_schur_point against Dinv formed by its readers, and k_linearize compiled for 4 waves
+    per SIMD against the compiler's register allocation.  The GBA graph has per-edge robust flags off (bRobust = false)."""
     import subprocess
     import sys
     out = f"/tmp/_osg_lba_variant_{os.getpid()}.npz"
