@@ -50,3 +50,29 @@ def test_structure_map_path_equals_window_path(harness, monkeypatch):
         monkeypatch.setenv("OSG_LBA_MAP_MODE", "1")
         h_map = harness.lba_host_struct_hash(C.byref(G.struct()))
         assert h_window != 0 and h_window == h_map
+
+
+def test_structure_build_concurrent_callers(harness, monkeypatch):
+    """8 host threads building structures at once (as bench.py's global_ba stage
+    drives lba_batch from 8 threads), each on its own graph, through the worker pool's map path with its
+    thread_local scratch vectors: every hash equals the same graph's single-threaded build."""
+    import threading
+    monkeypatch.setenv("OSG_LBA_MAP_MODE", "1")
+    graphs = [op.synth_map_graph(np.random.default_rng(70 + i), n_kf=150 + 40 * i, n_points=15000, loop=(i % 2 == 1))
+              for i in range(4)] + [op.synth_lba_graph(np.random.default_rng(80 + i), n_kf=50, n_points=10000)
+                                    for i in range(4)]
+    structs = [G.struct() for G in graphs]
+    want = [harness.lba_host_struct_hash(C.byref(s)) for s in structs]
+    assert all(want)
+    got = [[] for _ in graphs]
+
+    def run(i):
+        for _ in range(6):
+            got[i].append(harness.lba_host_struct_hash(C.byref(structs[i])))
+    th = [threading.Thread(target=run, args=(i,)) for i in range(len(graphs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for i in range(len(graphs)):
+        assert got[i] == [want[i]] * 6, i

@@ -47,7 +47,8 @@ extern "C" unsigned long long lba_host_struct_hash(const osg_ba_graph *G)
                     &H.point_h, &H.hl_point, &H.lm_e_start, &H.lm_e, &H.lg_start, &H.lm_b_start, &H.blk_pose,
                     &H.edge_blk, &H.blk_lm, &H.hp_e_start, &H.hp_e, &H.hp_b_start, &H.hp_b, &H.pair_start,
                     &pb, &H.chunk_start, &H.pair_chunk, &H.pair_rank, &H.rs_pose, &H.rs_rank0,
-                    &H.rs_chunk_start, &H.rs_chunk, &H.hp_rs_start, &H.rs_order, &H.rs_cdesc, &H.rs_info, &H.hp_b_lm})
+                    &H.rs_chunk_start, &H.rs_chunk, &H.hp_rs_start, &H.rs_order, &H.rs_cdesc, &H.rs_info, &H.hp_b_lm,
+                    &H.live_chunk, &H.env_off})
         mix(*v);
     const int sc[] = {H.np, H.npt, H.ne, H.nhp, H.nhl, H.nblk, H.npairs, H.nchunks, H.ge, H.gl, H.gll, H.gu,
                       H.nblk_red, H.npart, H.n_rs, H.max_col_rows, (int)H.multi};
