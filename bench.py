@@ -51,13 +51,11 @@ VALU_OPS_PER_PAIR = 19         # 8 v_xor + 8 v_bcnt(acc) + 1 v_lshl_or + v_med3 
 # I8 matrix cores: v_mfma_i32_32x32x32_i8 = 32 x 32 x 32 MACs per 32 cycles per SIMD (the cycles of the BF16
 # 32x32x16 form at twice the K, MI355X_MICROARCH.md "Matrix cores"): 256 CU x 4 SIMD x 1024 MAC x 2 ops x 2.4 GHz
 PEAK_I8_TOPS = 256 * 4 * 1024 * 2 * 2.4e9 / 1e12
+# FP4 (e2m1) block-scaled v_mfma_scale_f32_32x32x64_f8f6f4: the BF16 form's cycles at 4x K, twice the I8 rate
+PEAK_FP4_TOPS = 2 * PEAK_I8_TOPS
 I8_OPS_PER_PAIR = 512          # 256 MACs per (query, train row) pair
 MFMA_EPILOGUE_VALU_PER_PAIR = 2  # v_med3_i32 + v_min_i32 on the accumulator's packed key
 MFMA_MAX_ROWS = 8192           # the I8 kernel's 13-bit row field (osg_top2_mfma_max_rows)
-# OSG_TOP2_MFMA_SHAPE -> k_top2_mfma<NW, QT, CR, PIPE>, as osg_launch_top2_batch_mfma's switch
-# (csrc/hamming_mfma.hip); any other value takes the default
-MFMA_SHAPES = {"0": (16, 1, 256, 1), "1": (8, 2, 256, 1), "2": (16, 1, 256, 0), "3": (8, 2, 256, 0),
-               "4": (8, 1, 256, 1)}
 LINE_MAX_BYTES = 8192          # the stdout line's budget (the driver did not parse r04's 21 KB line)
 
 
@@ -237,21 +235,25 @@ def main():
     k1_us = kernel_us(step_single, max(50, min(args.steps, 500)))
     k_us = k_us_loop
     alg_bytes = B * ((nq + nt) * 32 + nq * 12)
-    mfma = os.environ.get("OSG_TOP2_BATCH_MFMA", "1") != "0" and 1 <= nt <= MFMA_MAX_ROWS
+    # the kernel the batched entry launches, named by the library itself
+    kname = ctx.hamming_top2_batch_plan(nq, nt, B)
+    mfma = kname.startswith(("k_top2_mfma", "k_top2_fp4"))
+    fp4 = kname.startswith("k_top2_fp4")
     if mfma:
-        shape = MFMA_SHAPES.get(os.environ.get("OSG_TOP2_MFMA_SHAPE", "0"), MFMA_SHAPES["0"])
-        per_wg = shape[0] * shape[1] * 32
-        kname = (f"k_top2_mfma<{shape[0]},{shape[1]},{shape[2]},{shape[3]}> "
-                 f"grid={(nq + per_wg - 1) // per_wg * B} x {shape[0] * 64}")
-        ksub = "k_top2_mfma"
+        ksub = kname.split("<")[0]
         achieved = pairs_per_step * I8_OPS_PER_PAIR / (k_us * 1e-6) / 1e12
         epi = pairs_per_step * MFMA_EPILOGUE_VALU_PER_PAIR / (k_us * 1e-6) / 1e12
+        peak = PEAK_FP4_TOPS if fp4 else PEAK_I8_TOPS
         roofline = {
-            "kernel": kname, "bound": "mfma", "achieved": round(achieved, 1), "peak": round(PEAK_I8_TOPS, 1),
-            "unit": "TOPS (i8 MFMA, 2 ops per MAC)",
-            "peak_source": "v_mfma_i32_32x32x32_i8: 32x32x32 MACs / 32 cycles / SIMD (MI355X_MICROARCH.md Matrix cores: "
-                           "I8 = the BF16 form's cycles at 2x K) x 1024 SIMDs x 2.4 GHz",
-            "frac": round(achieved / PEAK_I8_TOPS, 4),
+            "kernel": kname, "bound": "mfma", "achieved": round(achieved, 1), "peak": round(peak, 1),
+            "unit": "TOPS (fp4 e2m1 block-scaled MFMA, 2 ops per MAC)" if fp4 else "TOPS (i8 MFMA, 2 ops per MAC)",
+            "peak_source": ("v_mfma_scale_f32_32x32x64_f8f6f4 with fp4 operands: 32x32x64 MACs / 32 cycles / SIMD "
+                            "(MI355X_MICROARCH.md Matrix cores: FP4 = the BF16 form's cycles at 4x K) x 1024 SIMDs x "
+                            "2.4 GHz" if fp4 else
+                            "v_mfma_i32_32x32x32_i8: 32x32x32 MACs / 32 cycles / SIMD (MI355X_MICROARCH.md Matrix "
+                            "cores: I8 = the BF16 form's cycles at 2x K) x 1024 SIMDs x 2.4 GHz"),
+            "frac": round(achieved / peak, 4),
+            "frac_of_i8_peak": round(achieved / PEAK_I8_TOPS, 4),
             "algorithmic_ops_per_launch": pairs_per_step * I8_OPS_PER_PAIR,
             # the VALU side of the same kernel: the 2-op top-2 epilogue per pair against the measured 16-lane
             # ceiling and the guide's 32-lane figure
@@ -267,6 +269,7 @@ def main():
         ql = int(os.environ.get("OSG_TOP2_BATCH_QL", "2"))
         kname = (f"k_top2_batch<{ql},{int(os.environ.get('OSG_TOP2_BATCH_SCALAR', '1'))}> "
                  f"grid={(nq + 64 * ql - 1) // (64 * ql)} x {B} x 1024")
+        fp4 = False
         ksub = "k_top2_batch"
         achieved = pairs_per_step * VALU_OPS_PER_PAIR / (k_us * 1e-6) / 1e12
         vp = _load_json(args.valu_pmc)
@@ -319,7 +322,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "i8->i32" if mfma else "u32",
+        "dtype": ("fp4(e2m1)->f32" if fp4 else "i8->i32") if mfma else "u32",
         "data": "synthetic (SURVEY.md §8d C2 generator, seed 0x0B5EED01+rank; no EuRoC/ORBvoc in container)",
         "config": {"workload": f"C2: brute-force 256-bit Hamming top-2, 2000 x 2000 descriptors per frame, "
                                f"{B} independent frames per launch per GPU (headline; the one-frame launch is "

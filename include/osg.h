@@ -113,6 +113,11 @@ int osg_hamming_top2_batch_dev(osg_ctx *ctx, const void *d_query, int32_t nq, co
  * this process (the launch knobs are read once).  No reference counterpart. */
 int osg_hamming_top2_plan(osg_ctx *ctx, int32_t nq, int32_t nt, char *name, int32_t len);
 
+/* Diagnostics: name of the kernel osg_hamming_top2_batch_dev launches for (nq, nt, nb) in this process,
+ * with its template shape and grid (e.g. "k_top2_fp4<16,1,256,1> grid=1024 x 1024").  No reference
+ * counterpart. */
+int osg_hamming_top2_batch_plan(osg_ctx *ctx, int32_t nq, int32_t nt, int32_t nb, char *name, int32_t len);
+
 /* ---- frame view (SoA gather of ORB_SLAM3::Frame / KeyFrame fields) ----------------------------
  * Grid: ref:src/Frame.cc:469-507 (AssignFeaturesToGrid), cells in CSR with cell = ix*48 + iy and
  * items in insertion (ascending feature index) order, which is GetFeaturesInArea's candidate

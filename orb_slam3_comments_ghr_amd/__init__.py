@@ -136,6 +136,13 @@ class Context:
         self.check(self.lib.osg_hamming_top2_plan(self.handle, int(nq), int(nt), buf, 160), "osg_hamming_top2_plan")
         return buf.value.decode()
 
+    def hamming_top2_batch_plan(self, nq: int, nt: int, nb: int) -> str:
+        """The kernel osg_hamming_top2_batch_dev launches for (nq, nt, nb), with its shape and grid."""
+        buf = C.create_string_buffer(160)
+        self.check(self.lib.osg_hamming_top2_batch_plan(self.handle, int(nq), int(nt), int(nb), buf, 160),
+                   "osg_hamming_top2_batch_plan")
+        return buf.value.decode()
+
     def match_last_stats(self) -> dict:
         """Diagnostics of the last search call: candidates, Jacobi rounds, serial redo, nmatches."""
         out = np.zeros(4, np.int32)

@@ -184,7 +184,7 @@ EXPORTS = [
     "osg_ctx_create", "osg_ctx_destroy", "osg_ctx_set_stream", "osg_ctx_stream",
     "osg_ctx_synchronize", "osg_strerror", "osg_ctx_last_error", "osg_version",
     "osg_descriptor_distance", "osg_descriptor_distance_pairs", "osg_hamming_top2",
-    "osg_hamming_top2_dev", "osg_hamming_top2_batch_dev", "osg_hamming_top2_plan", "osg_search_by_projection_mps", "osg_search_by_projection_last",
+    "osg_hamming_top2_dev", "osg_hamming_top2_batch_dev", "osg_hamming_top2_plan", "osg_hamming_top2_batch_plan", "osg_search_by_projection_mps", "osg_search_by_projection_last",
     "osg_search_by_projection_kf", "osg_search_by_bow_kf_f", "osg_search_by_bow_kf_kf",
     "osg_search_by_projection_mps_batch", "osg_search_by_projection_last_batch",
     "osg_search_by_projection_kf_batch", "osg_search_by_bow_kf_f_batch", "osg_search_by_bow_kf_kf_batch",
@@ -224,6 +224,7 @@ def declare(lib: C.CDLL) -> C.CDLL:
     lib.osg_hamming_top2_dev.argtypes = [vp, vp, i32, vp, i32, vp]
     lib.osg_hamming_top2_batch_dev.argtypes = [vp, vp, i32, vp, i32, i32, vp]
     lib.osg_hamming_top2_plan.argtypes = [vp, i32, i32, C.c_char_p, i32]
+    lib.osg_hamming_top2_batch_plan.argtypes = [vp, i32, i32, i32, C.c_char_p, i32]
     lib.osg_search_by_projection_mps.argtypes = [vp, C.POINTER(OsgFrame), C.POINTER(OsgMpQueries),
                                                  f32, f32, C.c_int, f32, vp, vp]
     lib.osg_search_by_projection_last.argtypes = [vp, C.POINTER(OsgFrame),

@@ -327,6 +327,273 @@ __global__ __launch_bounds__(NW * 64) void k_top2_mfma(const uint32_t *__restric
     }
 }
 
+// ---- FP4 (e2m1) block-scaled form -------------------------------------------------------------
+// The same keys from v_mfma_scale_f32_32x32x64_f8f6f4 with FP4 operands (cbsz = blgp = 4): a query
+// bit is +1 (set) or -1 (clear), a train bit -2 (set) or 0 (clear), so
+//     sum_k q_k t_k = -2 (a - (|t| - a)) = 2 (H - |q|),
+// and the train operand's E8M0 block scale 2^12 makes it 8192 (H - |q|): the i8 path's key, exact in
+// the f32 accumulator (every product and partial sum is an integer multiple of 4096 of magnitude below
+// 2^22, plus the row < 2^13 from C), so the summation order inside the instruction cannot round.
+// C carries the bias 2^23 + 2^21 (plus the row in the tile), so every key the instruction produces lies in
+// [2^23, 2^24), the f32 binade whose ulp is 1: there the bit pattern is 0x4B000000 + (value - 2^23), an
+// affine map of the integer key.  The epilogue therefore runs on the bit patterns with the i8 path's
+// integer v_min3 / v_med3 / rebasing ops (as floats, fminf / fmaxf each cost a canonicalising v_max_f32
+// and the median no single instruction: 14 VALU ops per MFMA instead of 7).
+// K = 64 bits per instruction at the cycles of the i8 form's K = 32 (MI355X_MICROARCH.md "Matrix cores":
+// FP4 runs at 4x the BF16 rate per clock, I8 at 2x): 4 MFMAs per 32-row tile instead of 8, and an
+// expanded train row is 128 B (one nibble per bit) instead of 256.
+// Operand map: lane l carries row (A) / column (B) l & 31 and the K nibbles 32 (l >> 5) + j, j = 0..31,
+// nibble j at bit 4 (j & 7) of register j >> 3; K-step s of lane half h carries descriptor word 2 s + h on
+// both sides.  A dot product is unchanged by any K permutation applied to both operands alike, so the
+// exact-data probe (tools/micro/mfma_fp4_layout.hip, profiles/r05_mfma_fp4_layout.txt) passes for every
+// consistent map it tried; what it pins is the e2m1 codes, the E8M0 scaling and the C / D map.
+constexpr int MX_RS = 144;                  // LDS row stride: 128 B of nibbles + 16 B pad (16 distinct banks)
+constexpr int MX_SCALE_TRAIN = 127 + 12;    // E8M0 2^12 on the train operand
+constexpr int MX_SCALE_ONE = 127;           // E8M0 1.0
+constexpr float MX_BIAS = 10485760.0f;      // 2^23 + 2^21: keys of [-2^21, 2^21 + 32) land in [2^23, 2^24)
+constexpr int MX_KEY0 = 0x4B000000 + (1 << 21);   // bit pattern of MX_BIAS: bits = key + MX_KEY0
+constexpr float MX_PAD = 1073741824.0f;     // rows past nt: above every real key (2^30)
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// 8 bits -> bit y at bit 4 y
+__device__ __forceinline__ uint32_t spread_nib(uint32_t x)
+{
+    x &= 0xFFu;
+    x = (x | (x << 12)) & 0x000F000Fu;
+    x = (x | (x << 6)) & 0x03030303u;
+    return (x | (x << 3)) & 0x11111111u;
+}
+
+template <int NW, int QT, int CR, int PIPE>
+__global__ __launch_bounds__(NW * 64) void k_top2_fp4(const uint32_t *__restrict__ query, int nq,
+                                                       const uint32_t *__restrict__ train, int nt,
+                                                       int nqb, int32_t *__restrict__ out)
+{
+    constexpr int NT = NW * 64;
+    constexpr int BPT = CR * 32 / NT;        // packed bytes per thread per chunk
+    constexpr int WPT = BPT / 4;             // packed words per thread
+    constexpr int TPR = 32 / BPT;            // threads per row
+    constexpr int NTILE = CR / 32;           // 32-row tiles per chunk
+    static_assert(CR * 32 % NT == 0 && BPT % 4 == 0 && TPR >= 1, "chunk / workgroup shape");
+    __shared__ __attribute__((aligned(16))) unsigned char s_buf[2 * CR * MX_RS];   // [2][CR rows][144 B]
+    __shared__ uint32_t s_lut[256];          // train byte -> 8 nibbles (bit y -> nibble y: 0xC = -2 / 0)
+
+    const int t = threadIdx.x, lane = t & 63;
+    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int G = gridDim.x, L = blockIdx.x;
+    const int logical = (G % 8 == 0) ? (L % 8) * (G / 8) + L / 8 : L;
+    const int b = logical / nqb, qb = logical % nqb;
+    const uint32_t *qf = query + (size_t)b * nq * 8;
+    const uint32_t *tf = train + (size_t)b * nt * 8;
+    int32_t *of = out + (size_t)b * nq * 3;
+
+    for (int e = t; e < 256; e += NT) s_lut[e] = spread_nib((uint32_t)e) * 0xCu;
+
+    const int r = lane & 31, h = lane >> 5;
+    const int qw0 = qb * (NW * QT * 32) + w * (QT * 32);
+    const bool active = qw0 < nq;
+
+    // B fragments (the wave's queries, K-step s = descriptor word 2 s + h) and two running top-2
+    // pairs per query (accumulator elements 0-7 and 8-15)
+    i32x8 bq[QT][4];
+    int ka1[QT], ka2[QT], kb1[QT], kb2[QT];
+    int pq[QT];
+#pragma unroll
+    for (int j = 0; j < QT; j++) {
+        const int q = min(qw0 + 32 * j + r, nq - 1);
+        const uint4 lo = *(const uint4 *)(qf + (size_t)q * 8), hi = *(const uint4 *)(qf + (size_t)q * 8 + 4);
+        const uint32_t wd[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        int pc = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) pc += __popc(wd[k]);
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const uint32_t word = wd[2 * s + h];
+#pragma unroll
+            for (int d = 0; d < 4; d++)
+                bq[j][s][d] = (int)(0x22222222u | ((~spread_nib(word >> (8 * d)) & 0x11111111u) << 3));
+#pragma unroll
+            for (int d = 4; d < 8; d++) bq[j][s][d] = 0;
+        }
+        pq[j] = pc;
+        ka1[j] = ka2[j] = kb1[j] = kb2[j] = ((256 - pc) << MF_SHIFT) + MX_KEY0;
+    }
+    f32x16 crow;
+#pragma unroll
+    for (int i = 0; i < 16; i++) crow[i] = MX_BIAS + (float)((i & 3) + 8 * (i >> 2) + 4 * h);
+    const int lbase = r * MX_RS + h * 16;
+
+    const int erow = t / TPR, epart = t % TPR;
+    auto load_chunk = [&](int c0, uint32_t (&pw)[WPT]) {
+        const int row = c0 + erow;
+        if (row < nt) {
+            const uint32_t *src = tf + (size_t)row * 8 + epart * WPT;
+#pragma unroll
+            for (int i = 0; i < WPT; i += 2) {
+                const uint2 v = *(const uint2 *)(src + i);
+                pw[i] = v.x;
+                pw[i + 1] = v.y;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < WPT; i++) pw[i] = 0u;   // expands to zero nibbles: D = C exactly
+        }
+    };
+    auto store_chunk = [&](int buf, const uint32_t (&pw)[WPT]) {
+        unsigned char *dst = s_buf + ((size_t)buf * CR + erow) * MX_RS;
+#pragma unroll
+        for (int i = 0; i < WPT; i++) {
+            const uint32_t x = pw[i];
+            *(i32x4 *)(dst + 16 * (epart * WPT + i)) =
+                i32x4{(int)s_lut[x & 0xFFu], (int)s_lut[(x >> 8) & 0xFFu], (int)s_lut[(x >> 16) & 0xFFu],
+                      (int)s_lut[x >> 24]};
+        }
+    };
+
+    auto frag = [&](const unsigned char *tb, int s) -> i32x8 {
+        const i32x4 v = *(const i32x4 *)(tb + lbase + 32 * s);
+        return i32x8{v[0], v[1], v[2], v[3], 0, 0, 0, 0};
+    };
+    auto mfma = [&](const i32x8 &a, const i32x8 &bb, const f32x16 &c) {
+        return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, bb, c, 4, 4, 0, MX_SCALE_TRAIN, 0, MX_SCALE_ONE);
+    };
+    auto epi = [&](const f32x16 (&acc)[QT]) {
+#pragma unroll
+        for (int j = 0; j < QT; j++) {
+#pragma unroll
+            for (int i = 0; i < 8; i += 2) {
+                key_push2(ka1[j], ka2[j], __float_as_int(acc[j][i]), __float_as_int(acc[j][i + 1]));
+                key_push2(kb1[j], kb2[j], __float_as_int(acc[j][i + 8]), __float_as_int(acc[j][i + 9]));
+            }
+            ka1[j] -= 32;
+            ka2[j] -= 32;
+            kb1[j] -= 32;
+            kb2[j] -= 32;
+        }
+    };
+    auto tile = [&](const unsigned char *tb, const f32x16 &cin) {
+        i32x8 a[4];
+#pragma unroll
+        for (int s = 0; s < 4; s++) a[s] = frag(tb, s);
+        f32x16 acc[QT];
+#pragma unroll
+        for (int j = 0; j < QT; j++) acc[j] = mfma(a[0], bq[j][0], cin);
+#pragma unroll
+        for (int s = 1; s < 4; s++)
+#pragma unroll
+            for (int j = 0; j < QT; j++) acc[j] = mfma(a[s], bq[j][s], acc[j]);
+        epi(acc);
+    };
+
+    const int nch = (nt + CR - 1) / CR;
+    {
+        uint32_t pw[WPT];
+        load_chunk(0, pw);
+        __syncthreads();   // the table
+        store_chunk(0, pw);
+    }
+    __syncthreads();
+    for (int c = 0; c < nch; c++) {
+        const int c0 = c * CR;
+        uint32_t pw[WPT];
+        const bool more = c + 1 < nch;
+        if (more) load_chunk(c0 + CR, pw);
+        if (active) {
+            const unsigned char *sb = s_buf + (size_t)(c & 1) * CR * MX_RS;
+            const int nfull = min(NTILE, (nt - c0) / 32);
+            if (PIPE && nfull == NTILE) {
+                // K-step s of tile t issues its MFMAs, refills the A register it consumed with tile
+                // t + 1's granule, and performs key pairs 2 s, 2 s + 1 of tile t - 1 (as k_top2_mfma)
+                i32x8 a[4];
+                f32x16 accp[QT], acc[QT];
+#pragma unroll
+                for (int s = 0; s < 4; s++) a[s] = frag(sb, s);
+#pragma unroll
+                for (int s = 0; s < 4; s++) {
+#pragma unroll
+                    for (int j = 0; j < QT; j++) accp[j] = mfma(a[s], bq[j][s], s ? accp[j] : crow);
+                    a[s] = frag(sb + 32 * MX_RS, s);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#pragma unroll
+                for (int tt = 1; tt < NTILE; tt++) {
+#pragma unroll
+                    for (int s = 0; s < 4; s++) {
+#pragma unroll
+                        for (int j = 0; j < QT; j++) acc[j] = mfma(a[s], bq[j][s], s ? acc[j] : crow);
+                        if (tt + 1 < NTILE) a[s] = frag(sb + (tt + 1) * 32 * MX_RS, s);
+#pragma unroll
+                        for (int j = 0; j < QT; j++) {
+                            // pairs 2 s (chain A: elements 4 s, 4 s + 1 ... ) and 2 s + 1 (chain B)
+                            key_push2(ka1[j], ka2[j], __float_as_int(accp[j][2 * s]),
+                                      __float_as_int(accp[j][2 * s + 1]));
+                            key_push2(kb1[j], kb2[j], __float_as_int(accp[j][8 + 2 * s]),
+                                      __float_as_int(accp[j][9 + 2 * s]));
+                            if (s == 3) {
+                                ka1[j] -= 32;
+                                ka2[j] -= 32;
+                                kb1[j] -= 32;
+                                kb2[j] -= 32;
+                            }
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+#pragma unroll
+                    for (int j = 0; j < QT; j++) accp[j] = acc[j];
+                }
+                epi(accp);
+            } else {
+#pragma unroll
+                for (int tt = 0; tt < NTILE; tt++) {
+                    if (tt >= nfull) break;
+                    tile(sb + tt * 32 * MX_RS, crow);
+                }
+            }
+            const int lim = nt - (c0 + nfull * 32);
+            if (nfull < NTILE && lim > 0) {
+                f32x16 cin;
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    cin[i] = crow[i] + ((i & 3) + 8 * (i >> 2) + 4 * h >= lim ? MX_PAD : 0.f);
+                tile(sb + nfull * 32 * MX_RS, cin);
+            }
+        }
+        if (more) store_chunk((c + 1) & 1, pw);
+        __syncthreads();
+    }
+    if (!active) return;
+    const int base = 32 * ((nt + 31) / 32);
+#pragma unroll
+    for (int j = 0; j < QT; j++) {
+        int k1 = ka1[j], k2 = ka2[j];
+        key_merge(k1, k2, kb1[j], kb2[j]);
+        const int a1 = __shfl_xor(k1, 32), a2 = __shfl_xor(k2, 32);
+        key_merge(k1, k2, a1, a2);
+        const int q = qw0 + 32 * j + r;
+        if (h == 0 && q < nq) {
+            const int t1 = k1 - MX_KEY0 + base, t2 = k2 - MX_KEY0 + base;
+            const int d1 = (t1 >> MF_SHIFT) + pq[j], d2 = (t2 >> MF_SHIFT) + pq[j];
+            of[3 * q + 0] = d1 < 256 ? (t1 & (MF_MAX_ROWS - 1)) : -1;
+            of[3 * q + 1] = min(d1, 256);
+            of[3 * q + 2] = min(d2, 256);
+        }
+    }
+}
+
+template <int NW, int QT, int CR, int PIPE>
+int launch_fp4(osg_ctx *ctx, const void *d_query, int nq, const void *d_train, int nt, int nb, void *d_out)
+{
+    const int nqb = (nq + NW * QT * 32 - 1) / (NW * QT * 32);
+    const long long g = (long long)nqb * nb;
+    OSG_REQUIRE(ctx, g <= 0x7FFFFFFF, "grid too large");
+    hipLaunchKernelGGL((k_top2_fp4<NW, QT, CR, PIPE>), dim3((unsigned)g), dim3(NW * 64), 0, ctx->stream,
+                       (const uint32_t *)d_query, nq, (const uint32_t *)d_train, nt, nqb, (int32_t *)d_out);
+    OSG_HIP_CHECK(ctx, hipGetLastError());
+    return OSG_OK;
+}
+
 template <int NW, int QT, int CR, int PIPE>
 int launch(osg_ctx *ctx, const void *d_query, int nq, const void *d_train, int nt, int nb, void *d_out)
 {
@@ -343,12 +610,62 @@ int launch(osg_ctx *ctx, const void *d_query, int nq, const void *d_train, int n
 
 int osg_top2_mfma_max_rows() { return MF_MAX_ROWS; }
 
-// B problems of nq x nt on the I8 MFMA path; requires 1 <= nt <= 8192 (the key's row field)
+namespace {
+// the launch knobs, read once per process: OSG_TOP2_MFMA_SHAPE picks the workgroup shape,
+// OSG_TOP2_FP4=1 the FP4 block-scaled form (k_top2_fp4, same keys)
+int mfma_shape()
+{
+    static const int shape = getenv("OSG_TOP2_MFMA_SHAPE") ? atoi(getenv("OSG_TOP2_MFMA_SHAPE")) : 0;
+    return shape;
+}
+bool mfma_fp4()
+{
+    static const bool fp4 = getenv("OSG_TOP2_FP4") && atoi(getenv("OSG_TOP2_FP4")) == 1;
+    return fp4;
+}
+// {NW, QT, CR, PIPE} of the shape the switches below launch
+void mfma_shape_of(bool fp4, int shape, int *d)
+{
+    static const int i8[5][4] = {{16, 1, 256, 1}, {8, 2, 256, 1}, {16, 1, 256, 0}, {8, 2, 256, 0}, {8, 1, 256, 1}};
+    static const int f4[6][4] = {{16, 1, 256, 1}, {8, 2, 256, 1}, {16, 1, 256, 0}, {16, 1, 256, 1}, {8, 1, 256, 1},
+                                 {16, 2, 256, 1}};
+    const int *s = fp4 ? f4[(shape >= 1 && shape <= 5 && shape != 3) ? shape : 0]
+                       : i8[(shape >= 1 && shape <= 4) ? shape : 0];
+    for (int i = 0; i < 4; i++) d[i] = s[i];
+}
+}  // namespace
+
+int osg_hamming_top2_batch_plan(osg_ctx *ctx, int32_t nq, int32_t nt, int32_t nb, char *name, int32_t len)
+{
+    if (!ctx || !name || len <= 0) return OSG_E_INVALID;
+    const bool mf = getenv("OSG_TOP2_BATCH_MFMA") == nullptr || atoi(getenv("OSG_TOP2_BATCH_MFMA")) != 0;
+    if (nq <= 0 || nb <= 0 || nt <= 0 || !mf || nt > MF_MAX_ROWS) {
+        snprintf(name, (size_t)len, "%s", nq <= 0 || nb <= 0 ? "none" : "k_top2_batch");
+        return OSG_OK;
+    }
+    int d[4];
+    mfma_shape_of(mfma_fp4(), mfma_shape(), d);
+    const int per_wg = d[0] * d[1] * 32;
+    snprintf(name, (size_t)len, "%s<%d,%d,%d,%d> grid=%lld x %d", mfma_fp4() ? "k_top2_fp4" : "k_top2_mfma", d[0], d[1],
+             d[2], d[3], (long long)((nq + per_wg - 1) / per_wg) * nb, d[0] * 64);
+    return OSG_OK;
+}
+
+// B problems of nq x nt on the MFMA path; requires 1 <= nt <= 8192 (the key's row field)
 int osg_launch_top2_batch_mfma(osg_ctx *ctx, const void *d_query, int32_t nq, const void *d_train, int32_t nt,
                                int32_t nb, void *d_out)
 {
     OSG_REQUIRE(ctx, nt >= 1 && nt <= MF_MAX_ROWS, "nt=%d outside the MFMA path's 1..%d rows", nt, MF_MAX_ROWS);
-    static const int shape = getenv("OSG_TOP2_MFMA_SHAPE") ? atoi(getenv("OSG_TOP2_MFMA_SHAPE")) : 0;
+    const int shape = mfma_shape();
+    if (mfma_fp4()) {
+        switch (shape) {
+        case 1: return launch_fp4<8, 2, 256, 1>(ctx, d_query, nq, d_train, nt, nb, d_out);
+        case 2: return launch_fp4<16, 1, 256, 0>(ctx, d_query, nq, d_train, nt, nb, d_out);
+        case 4: return launch_fp4<8, 1, 256, 1>(ctx, d_query, nq, d_train, nt, nb, d_out);
+        case 5: return launch_fp4<16, 2, 256, 1>(ctx, d_query, nq, d_train, nt, nb, d_out);
+        default: return launch_fp4<16, 1, 256, 1>(ctx, d_query, nq, d_train, nt, nb, d_out);
+        }
+    }
     switch (shape) {
     case 1: return launch<8, 2, 256, 1>(ctx, d_query, nq, d_train, nt, nb, d_out);
     case 2: return launch<16, 1, 256, 0>(ctx, d_query, nq, d_train, nt, nb, d_out);

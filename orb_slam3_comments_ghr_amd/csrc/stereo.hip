@@ -15,6 +15,7 @@
 // Host pyramids are packed row-contiguous into the per-call upload; device-resident pyramids
 // (osg_image_pyramid.on_device) are read in place with their own row step.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <vector>
 
@@ -288,6 +289,10 @@ int stereo_run(osg_ctx *ctx, const osg_stereo_frame *F, int B, float *u_right, f
 {
     if (!ctx) return OSG_E_INVALID;
     OSG_REQUIRE(ctx, B >= 0 && B <= 65535 && (B == 0 || (F && nmatches)), "batch arguments");
+    // OSG_STEREO_PROFILE=1: host phase times per call on stderr (probe runs)
+    static const bool prof = getenv("OSG_STEREO_PROFILE") && atoi(getenv("OSG_STEREO_PROFILE")) == 1;
+    using hclock = std::chrono::steady_clock;
+    const hclock::time_point t0 = hclock::now();
     osg_packer pk;
     std::vector<StereoArgs> args(B);
     std::vector<Problem> P(B);
@@ -395,7 +400,9 @@ int stereo_run(osg_ctx *ctx, const osg_stereo_frame *F, int B, float *u_right, f
     char *pin = (char *)osg_pinned(ctx, in_bytes + args_bytes + out_bytes + 256);
     if (!pin) return osg_set_error(ctx, OSG_E_NOMEM, "pinned alloc failed");
     OSG_RC(osg_idle(ctx));  // the pinned block may still be in use
+    const hclock::time_point t1 = hclock::now();
     pk.fill_parallel(pin, 8);
+    const hclock::time_point t2 = hclock::now();
     StereoArgs *pin_args = (StereoArgs *)(pin + in_bytes);
     int32_t *pin_out = (int32_t *)((char *)pin_args + args_bytes);
     char *dev_in = nullptr;
@@ -440,13 +447,20 @@ int stereo_run(osg_ctx *ctx, const osg_stereo_frame *F, int B, float *u_right, f
     OSG_HIP_CHECK(ctx, hipGetLastError());
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[1], ctx->stream));
     OSG_RC(osg_download(ctx, pin_out, dev_out, out_bytes));
+    const hclock::time_point t3 = hclock::now();
     OSG_RC(osg_wait(ctx));
+    const hclock::time_point t4 = hclock::now();
     float ms = 0.f;
     OSG_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ev[0], ev[1]));
     ctx->last_kernel_ms = ms;
     std::memcpy(u_right, pin_out, sizeof(float) * N);
     std::memcpy(depth, pin_out + N, sizeof(float) * N);
     for (int b = 0; b < B; b++) nmatches[b] = pin_out[3 * N + b];
+    if (prof) {
+        auto us = [](hclock::time_point a, hclock::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+        fprintf(stderr, "[osg stereo host] B %d: prep %.1f | fill %.1f | launch %.1f | wait %.1f | results %.1f us (kernel %.3f ms, pack %zu B)\n",
+                B, us(t0, t1), us(t1, t2), us(t2, t3), us(t3, t4), us(t4, hclock::now()), ms, (size_t)pk.total);
+    }
     return OSG_OK;
 }
 

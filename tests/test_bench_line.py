@@ -95,15 +95,30 @@ def test_line_of_a_failed_stage():
     assert d["local_ba"]["error"].startswith("RuntimeError")
 
 
-def test_mfma_shape_table_matches_the_launcher():
-    """bench.MFMA_SHAPES mirrors osg_launch_top2_batch_mfma's switch (csrc/hamming_mfma.hip), PIPE
-    included."""
+def test_batch_plan_tables_match_the_launchers():
+    """osg_hamming_top2_batch_plan names the kernel bench.py prices: its shape tables in
+    csrc/hamming_mfma.hip (mfma_shape_of) mirror the launch switches of the I8 and the FP4 forms."""
     import os
     import re
     src = open(os.path.join(os.path.dirname(bench.__file__), "orb_slam3_comments_ghr_amd", "csrc",
                             "hamming_mfma.hip")).read()
     body = src[src.index("int osg_launch_top2_batch_mfma"):]
-    cases = dict(re.findall(r"case (\d+): return launch<(\d+, \d+, \d+, \d+)>", body))
-    default = re.search(r"default: return launch<(\d+, \d+, \d+, \d+)>", body).group(1)
-    cases["0"] = default
-    assert {k: tuple(int(x) for x in v.split(",")) for k, v in cases.items()} == bench.MFMA_SHAPES
+    split = body.index("\n    switch (shape)")  # the I8 switch; the FP4 one is nested under if (mfma_fp4())
+    fp4_sw, i8_sw = body[body.index("if (mfma_fp4())"):split], body[split:]
+
+    def switch(text, fn):
+        cases = {int(k): tuple(int(x) for x in v.split(","))
+                 for k, v in re.findall(r"case (\d+): return " + fn + r"<(\d+, \d+, \d+, \d+)>", text)}
+        cases[0] = tuple(int(x) for x in re.search(r"default: return " + fn + r"<(\d+, \d+, \d+, \d+)>",
+                                                   text).group(1).split(","))
+        return cases
+
+    def table(name, n):
+        t = re.search(r"static const int " + name + r"\[" + str(n) + r"\]\[4\] = \{(.*?)\};", src, re.S).group(1)
+        return [tuple(int(x) for x in row.split(",")) for row in re.findall(r"\{([^{}]*)\}", t)]
+
+    i8, f4 = table("i8", 5), table("f4", 6)
+    for k, v in switch(i8_sw, "launch").items():
+        assert i8[k] == v, (k, v)
+    for k, v in switch(fp4_sw, "launch_fp4").items():
+        assert f4[k] == v, (k, v)

@@ -185,12 +185,14 @@ def test_batch_empty_train(ctx):
 _VARIANTS = [{"OSG_TOP2_BATCH_MFMA": "0", "OSG_TOP2_BATCH_QL": ql, "OSG_TOP2_BATCH_SCALAR": sc}
              for ql, sc in [("1", "0"), ("2", "0"), ("4", "0"), ("1", "1"), ("4", "1")]]
 _VARIANTS += [{"OSG_TOP2_MFMA_SHAPE": sh} for sh in ("0", "1", "2", "3", "4")]
+_VARIANTS += [{"OSG_TOP2_FP4": "1", "OSG_TOP2_MFMA_SHAPE": sh} for sh in ("0", "1", "2", "4", "5")]
 
 
 @pytest.mark.parametrize("env", _VARIANTS, ids=lambda e: "-".join(f"{k[9:]}={v}" for k, v in e.items()))
 def test_batch_query_per_lane_variants(oracle, env):
     """The popcount kernel's queries-per-lane (OSG_TOP2_BATCH_QL) and scalar-load (OSG_TOP2_BATCH_SCALAR)
-    instantiations, and the I8-MFMA kernel's workgroup shapes (OSG_TOP2_MFMA_SHAPE), read once per process.
+    instantiations, the I8-MFMA kernel's workgroup shapes (OSG_TOP2_MFMA_SHAPE) and the FP4 block-scaled
+    kernel's (OSG_TOP2_FP4=1), read once per process.
     nt = 2100: a partial LDS chunk and a partial 32-row tile."""
     import subprocess
     import sys
@@ -243,3 +245,47 @@ def test_batch_mfma_edges(ctx, oracle):
         for b in range(2):
             for k, r in enumerate(otop2(oracle, qq, tt)):
                 np.testing.assert_array_equal(got[b, :, k], r)
+
+
+def _edge_problems():
+    """test_batch_mfma_edges' problems: duplicates across tiles / chunks, H = 0 and 256, |q| = 0 and 256,
+    nt = 8192 and nt = 1."""
+    rng = np.random.default_rng(2024)
+    q = rng.integers(0, 256, (96, 32), dtype=np.uint8)
+    t = rng.integers(0, 256, (600, 32), dtype=np.uint8)
+    for j, rows in enumerate([(31, 32), (255, 256, 257), (0, 511), (63, 64, 512)]):
+        for rr in rows:
+            t[rr] = q[j]
+    t[100] = ~q[10]
+    z = np.zeros((1, 32), np.uint8)
+    o = np.full((1, 32), 255, np.uint8)
+    probs = [(q, t), (np.concatenate([z, o, q[:94]]), np.concatenate([o, z, t[:598]]))]
+    probs += [synth.descriptors_c2(200, 8192, seed=77), synth.descriptors_c2(200, 1, seed=78)]
+    return probs
+
+
+@pytest.mark.parametrize("env", [{"OSG_TOP2_FP4": "1"}, {"OSG_TOP2_FP4": "1", "OSG_TOP2_MFMA_SHAPE": "1"}],
+                         ids=lambda e: "-".join(f"{k[9:]}={v}" for k, v in e.items()))
+def test_batch_fp4_edges(oracle, env):
+    """The FP4 block-scaled form (k_top2_fp4) on the I8 form's edge cases, each against the serial loop:
+    its keys are the same integers, carried in f32 (exact below 2^24)."""
+    import os
+    import subprocess
+    import sys
+    code = ("import numpy as np\n"
+            "from orb_slam3_comments_ghr_amd import Context\n"
+            "from tests.test_top2_gpu import _batch, _edge_problems\n"
+            "ctx = Context(0)\n"
+            "out = {}\n"
+            "for i, (q, t) in enumerate(_edge_problems()):\n"
+            "    out[f'p{i}'] = _batch(ctx, [q, q], [t, t])\n"
+            "np.savez('/tmp/_osg_fp4_edges.npz', **out)\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=dict(os.environ, **env), capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = np.load("/tmp/_osg_fp4_edges.npz")
+    for i, (q, t) in enumerate(_edge_problems()):
+        for b in range(2):
+            for k, ref in enumerate(otop2(oracle, q, t)):
+                np.testing.assert_array_equal(got[f"p{i}"][b, :, k], ref, err_msg=f"problem {i} column {k}")

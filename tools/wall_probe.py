@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 from tools.adapter_arrays import (bow_arrays, frame_arrays, last_arrays, mps_arrays, pose_arrays,  # noqa: E402
-                                  pose_for_mock, prefixed, slot_arrays, write_arrays)
+                                  pose_for_mock, prefixed, slot_arrays, stereo_arrays, write_arrays)
 
 
 def c3_pool(n_pool=32):
@@ -57,6 +57,19 @@ def c5_pool(n_pool=32):
     return arrays
 
 
+def stereo_pool(n_pool=16):
+    from orb_slam3_comments_ghr_amd import stereo as st
+    rng = np.random.default_rng(0x0B5EED20)
+    pool = [st.synth_stereo_frame(rng, n=1200) for _ in range(n_pool)]
+    arrays = {"pool.n": np.array([n_pool], np.int32)}
+    for i, f in enumerate(pool):
+        arrays.update(prefixed(f"p{i}.", stereo_arrays(f)))
+    return arrays
+
+
+POOLS = {"c3": c3_pool, "c5": c5_pool, "stereo": stereo_pool}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "wallp"))
@@ -70,12 +83,13 @@ def main():
     exe = os.path.join(ROOT, "tools", "adapter_wall_bench")
     for wl in a.workloads.split(","):
         path = os.path.join(a.out, f"{wl}.arrays")
-        write_arrays(path, c3_pool() if wl == "c3" else c5_pool())
+        write_arrays(path, POOLS[wl]())
         for t, fr in [(int(x), int(f)) for x in a.threads.split(",") for f in a.frames.split(",")]:
             for split in ((0,) if a.no_split else (0, 1)):
                 env = dict(os.environ, OSG_WALL_SPLIT=str(split))
                 if t == 1 and split:
                     env["OSG_MATCH_PROFILE"] = "2"
+                    env["OSG_STEREO_PROFILE"] = "1"
                 errf = os.path.join(a.out, f"{wl}_t{t}_f{fr}_s{split}.err")
                 with open(errf, "w") as ef:
                     r = subprocess.run([exe, wl, path, str(fr), str(a.reps * 256 // fr), str(t)], stdout=subprocess.PIPE,
