@@ -612,7 +612,8 @@ int osg_top2_mfma_max_rows() { return MF_MAX_ROWS; }
 
 namespace {
 // the launch knobs, read once per process: OSG_TOP2_MFMA_SHAPE picks the workgroup shape,
-// OSG_TOP2_FP4=1 the FP4 block-scaled form (k_top2_fp4, same keys)
+// OSG_TOP2_FP4=0 the I8 form (k_top2_mfma) instead of the FP4 block-scaled one (k_top2_fp4, same keys,
+// the default since late r05: 8.3 against 6.0 M Mmatches/s, profiles/r05_top2_fp4_ab.jsonl)
 int mfma_shape()
 {
     static const int shape = getenv("OSG_TOP2_MFMA_SHAPE") ? atoi(getenv("OSG_TOP2_MFMA_SHAPE")) : 0;
@@ -620,7 +621,7 @@ int mfma_shape()
 }
 bool mfma_fp4()
 {
-    static const bool fp4 = getenv("OSG_TOP2_FP4") && atoi(getenv("OSG_TOP2_FP4")) == 1;
+    static const bool fp4 = !(getenv("OSG_TOP2_FP4") && atoi(getenv("OSG_TOP2_FP4")) == 0);
     return fp4;
 }
 // {NW, QT, CR, PIPE} of the shape the switches below launch

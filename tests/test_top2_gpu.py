@@ -184,15 +184,15 @@ def test_batch_empty_train(ctx):
 
 _VARIANTS = [{"OSG_TOP2_BATCH_MFMA": "0", "OSG_TOP2_BATCH_QL": ql, "OSG_TOP2_BATCH_SCALAR": sc}
              for ql, sc in [("1", "0"), ("2", "0"), ("4", "0"), ("1", "1"), ("4", "1")]]
-_VARIANTS += [{"OSG_TOP2_MFMA_SHAPE": sh} for sh in ("0", "1", "2", "3", "4")]
+_VARIANTS += [{"OSG_TOP2_FP4": "0", "OSG_TOP2_MFMA_SHAPE": sh} for sh in ("0", "1", "2", "3", "4")]
 _VARIANTS += [{"OSG_TOP2_FP4": "1", "OSG_TOP2_MFMA_SHAPE": sh} for sh in ("0", "1", "2", "4", "5")]
 
 
 @pytest.mark.parametrize("env", _VARIANTS, ids=lambda e: "-".join(f"{k[9:]}={v}" for k, v in e.items()))
 def test_batch_query_per_lane_variants(oracle, env):
     """The popcount kernel's queries-per-lane (OSG_TOP2_BATCH_QL) and scalar-load (OSG_TOP2_BATCH_SCALAR)
-    instantiations, the I8-MFMA kernel's workgroup shapes (OSG_TOP2_MFMA_SHAPE) and the FP4 block-scaled
-    kernel's (OSG_TOP2_FP4=1), read once per process.
+    instantiations, the I8-MFMA kernel's workgroup shapes (OSG_TOP2_FP4=0, OSG_TOP2_MFMA_SHAPE) and the
+    FP4 block-scaled kernel's (the default), read once per process.
     nt = 2100: a partial LDS chunk and a partial 32-row tile."""
     import subprocess
     import sys
@@ -214,7 +214,7 @@ def test_batch_query_per_lane_variants(oracle, env):
 
 
 def test_batch_mfma_edges(ctx, oracle):
-    """The I8-MFMA form's edge cases, each problem against the serial loop:
+    """The matrix-core form's edge cases (the default, k_top2_fp4), each problem against the serial loop:
     * exact duplicates of the best row straddling the 32-row tiles and the 256-row LDS chunks (first index wins);
     * the query itself in the train set (H = 0), its complement (H = 256, never enters), all-zero and all-one
       descriptors (|q| = 0 and 256 shift the key by the most);
@@ -264,11 +264,13 @@ def _edge_problems():
     return probs
 
 
-@pytest.mark.parametrize("env", [{"OSG_TOP2_FP4": "1"}, {"OSG_TOP2_FP4": "1", "OSG_TOP2_MFMA_SHAPE": "1"}],
+@pytest.mark.parametrize("env", [{"OSG_TOP2_FP4": "0"}, {"OSG_TOP2_FP4": "0", "OSG_TOP2_MFMA_SHAPE": "1"},
+                                 {"OSG_TOP2_FP4": "1", "OSG_TOP2_MFMA_SHAPE": "1"}],
                          ids=lambda e: "-".join(f"{k[9:]}={v}" for k, v in e.items()))
 def test_batch_fp4_edges(oracle, env):
-    """The FP4 block-scaled form (k_top2_fp4) on the I8 form's edge cases, each against the serial loop:
-    its keys are the same integers, carried in f32 (exact below 2^24)."""
+    """The same edge cases on the other matrix-core forms, each against the serial loop: the I8 form
+    (k_top2_mfma, OSG_TOP2_FP4=0, integer keys) and a second FP4 shape (keys carried in f32 in [2^23, 2^24),
+    exact)."""
     import os
     import subprocess
     import sys

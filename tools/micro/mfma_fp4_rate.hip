@@ -3,7 +3,8 @@
 // dependent chain of 4 FP4 MFMAs (K = 64 each) against 8 I8 MFMAs (K = 32), optionally followed by the
 // top-2 update (float min3 / med3 / min on the FP4 path's float keys).
 //   mode 0: chains only;  1: + update on floats (fminf / med3 as written);  3: + update on the keys' bit
-//   patterns with integer min3 / med3 (the form k_top2_fp4 uses since late r05)
+//   patterns with integer min3 / med3 (the form k_top2_fp4 uses since late r05);  4: that update alone, no
+//   MFMA (the accumulators are opaque registers rewritten by an empty asm each iteration)
 // 1024-thread workgroups (16 waves, 4 per SIMD), G = 1024 workgroups.  Random-ish operands: the clock the
 // chip holds depends on the data, so both forms get nonzero patterns.
 // Build: hipcc --offload-arch=gfx950 -O3 mfma_fp4_rate.hip -o mfma_fp4_rate
@@ -36,11 +37,17 @@ __global__ __launch_bounds__(1024) void k_fp4(float *out, int iters)
     f32x16 accp = c;
     for (int it = 0; it < iters; it++) {
         for (int s = 0; s < 4; s++) asm volatile("" : "+v"(a[s]));
-        f32x16 acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a[0], b[0], c, 4, 4, 0, 139, 0, 127);
+        f32x16 acc;
+        if (MODE == 4) {
+            acc = accp;
+            asm volatile("" : "+v"(acc));
+        } else {
+            acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a[0], b[0], c, 4, 4, 0, 139, 0, 127);
 #pragma unroll
-        for (int s = 1; s < 4; s++)
-            acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a[s], b[s], acc, 4, 4, 0, 139, 0, 127);
-        if (MODE == 3) {
+            for (int s = 1; s < 4; s++)
+                acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a[s], b[s], acc, 4, 4, 0, 139, 0, 127);
+        }
+        if (MODE == 3 || MODE == 4) {
             int j1 = __float_as_int(k1), j2 = __float_as_int(k2), j3 = __float_as_int(k3), j4 = __float_as_int(k4);
 #pragma unroll
             for (int i = 0; i < 8; i += 2) {
@@ -137,11 +144,11 @@ int main()
     (void)hipMalloc(&d, sizeof(float) * G * 1024);
     // one tile = 32 rows x 32 queries x 256 bits: 262144 (query, row, bit) MACs
     const double tiles = (double)G * 16 * iters;
-    const double ms[5] = {run(k_i8<0>, d, iters, G), run(k_i8<1>, d, iters, G), run(k_fp4<0>, d, iters, G),
-                          run(k_fp4<1>, d, iters, G), run(k_fp4<3>, d, iters, G)};
-    const char *nm[5] = {"i8 chain", "i8 chain + update", "fp4 chain", "fp4 chain + float update",
-                         "fp4 chain + integer update on the bit patterns"};
-    for (int m = 0; m < 5; m++)
+    const double ms[6] = {run(k_i8<0>, d, iters, G), run(k_i8<1>, d, iters, G), run(k_fp4<0>, d, iters, G),
+                          run(k_fp4<1>, d, iters, G), run(k_fp4<3>, d, iters, G), run(k_fp4<4>, d, iters, G)};
+    const char *nm[6] = {"i8 chain", "i8 chain + update", "fp4 chain", "fp4 chain + float update",
+                         "fp4 chain + integer update on the bit patterns", "integer update alone (no MFMA)"};
+    for (int m = 0; m < 6; m++)
         printf("{\"mode\": \"%s\", \"ms\": %.4f, \"ns_per_tile_per_simd\": %.3f, \"Tmatch_bits_per_s\": %.1f}\n", nm[m],
                ms[m], ms[m] * 1e6 / (tiles / 1024), tiles * 262144 / (ms[m] * 1e-3) / 1e12);
     (void)hipFree(d);
