@@ -2,10 +2,14 @@
 //
 // Rectified stereo: every left keypoint looks for a right keypoint on its row, then refines the
 // disparity with an 11 x 11 SAD block match at its pyramid level and a parabola fit; matches whose
-// SAD is >= 1.5 * 1.4 * the median SAD are dropped.  Two kernels:
+// SAD is >= 1.5 * 1.4 * the median SAD are dropped.  Three kernels:
+//  * k_stereo_rows — one workgroup per frame builds vRowIndices (ref:src/Frame.cc:1150-1170) as CSR
+//    in HBM: per-row counts in LDS, a block scan, then an atomic fill.  The fill order within a row
+//    is free because the matcher breaks distance ties by the right index itself (since late r05;
+//    before, the host built the lists, 40 us per frame).
 //  * k_stereo_match — one wave per left keypoint (grid = (ceil(max n / 4), frames)).  The lanes
-//    take the row's candidates (vRowIndices order = ascending right index) and a wave min of
-//    (dist << 24 | position) gives the first minimum; then the left 11 x 11 patch and the right
+//    take the row's candidates and a wave min of (dist << 24 | right index) gives the reference's
+//    first minimum (its candidate vector is in ascending right index); then the left 11 x 11 patch and the right
 //    11 x 21 strip are staged in LDS, the 121 (offset, row) pairs are summed across the lanes and
 //    lanes 0..10 add the rows of one offset each; lane 0 finishes the reference's float arithmetic
 //    (built with -ffp-contract=off).
@@ -31,18 +35,19 @@ constexpr int PATCH = 2 * SW + 1;            // 11
 constexpr int STRIP = 2 * SW + 2 * SL + 1;   // 21
 constexpr int NOFF = 2 * SL + 1;             // 11 offsets incR = -L..L
 constexpr int MAX_LEVELS = 32;
-constexpr int MAX_ROW_LIST = 1 << 24;        // candidate position field of the wave-min key
+constexpr int MAX_ROW_LIST = 1 << 24;        // right-index field of the wave-min key
+constexpr int MAX_ROWS0 = 8192;              // level-0 image rows: k_stereo_rows' LDS counters
 
 struct StereoArgs {
-    int n, n_levels, rows0;
+    int n, n_levels, rows0, n_right;
     float mb, mbf;
     GLOBAL const float *x, *y;
     GLOBAL const int32_t *oct;
     GLOBAL const uint32_t *desc;
-    GLOBAL const float *xr;
+    GLOBAL const float *xr, *yr;
     GLOBAL const int32_t *oct_r;
     GLOBAL const uint32_t *desc_r;
-    GLOBAL const int32_t *row_start, *row_list;  // vRowIndices as CSR over rows0 rows
+    GLOBAL int32_t *row_start, *row_list;        // vRowIndices as CSR over rows0 rows (k_stereo_rows)
     GLOBAL const float *scale, *inv_scale;
     GLOBAL const uint8_t *img_l[MAX_LEVELS];
     GLOBAL const uint8_t *img_r[MAX_LEVELS];
@@ -66,6 +71,61 @@ __device__ __forceinline__ void wave_lds_sync()
 {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     __builtin_amdgcn_wave_barrier();
+}
+
+// rows floor(y - r) .. ceil(y + r) of right keypoint iR, r = 2 mvScaleFactors[octave], clipped to the
+// image (ref:src/Frame.cc:1158-1169; the reference would index past vRowIndices)
+__device__ __forceinline__ void right_rows(const StereoArgs &A, int iR, int &lo, int &hi)
+{
+    const float kpY = A.yr[iR];
+    const float r = 2.0f * A.scale[A.oct_r[iR]];
+    hi = min((int)ceilf(kpY + r), A.rows0 - 1);
+    lo = max((int)floorf(kpY - r), 0);
+}
+
+__global__ __launch_bounds__(1024) void k_stereo_rows(const StereoArgs *__restrict__ args)
+{
+    const StereoArgs &A = args[blockIdx.x];
+    __shared__ int s_cnt[MAX_ROWS0];
+    __shared__ int s_wave[16];
+    if (A.n == 0) return;
+    const int tid = threadIdx.x, R = A.rows0, nr = A.n_right;
+    for (int y = tid; y < R; y += 1024) s_cnt[y] = 0;
+    __syncthreads();
+    for (int iR = tid; iR < nr; iR += 1024) {
+        int lo, hi;
+        right_rows(A, iR, lo, hi);
+        for (int y = lo; y <= hi; y++) atomicAdd(&s_cnt[y], 1);
+    }
+    __syncthreads();
+    // exclusive scan: thread t owns rows [t seg, (t + 1) seg)
+    const int seg = (R + 1023) / 1024, y0 = min(tid * seg, R), y1 = min(y0 + seg, R);
+    int sum = 0;
+    for (int y = y0; y < y1; y++) sum += s_cnt[y];
+    int incl = sum;
+    const int lane = tid & 63, w = tid >> 6;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) s_wave[w] = incl;
+    __syncthreads();
+    int base = incl - sum;
+    for (int i = 0; i < w; i++) base += s_wave[i];
+    __syncthreads();   // every thread has read its rows' counts
+    for (int y = y0; y < y1; y++) {
+        const int c = s_cnt[y];
+        A.row_start[y] = base;
+        s_cnt[y] = base;   // the fill cursor
+        base += c;
+    }
+    if (tid == 1023) A.row_start[R] = base;
+    __syncthreads();
+    for (int iR = tid; iR < nr; iR += 1024) {
+        int lo, hi;
+        right_rows(A, iR, lo, hi);
+        for (int y = lo; y <= hi; y++) A.row_list[atomicAdd(&s_cnt[y], 1)] = iR;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_stereo_match(const StereoArgs *__restrict__ args)
@@ -94,7 +154,7 @@ __global__ __launch_bounds__(256) void k_stereo_match(const StereoArgs *__restri
         const u32x4 qa = *(GLOBAL const u32x4 *)(A.desc + 8 * iL), qb = *(GLOBAL const u32x4 *)(A.desc + 8 * iL + 4);
         uint32_t best = 0xFFFFFFFFu;
         for (int c = c0 + lane; c < c1; c += 64) {         // :1214-1245
-            const int iR = A.row_list[c];
+            const uint32_t iR = (uint32_t)A.row_list[c];
             const int o = A.oct_r[iR];
             if (o < levelL - 1 || o > levelL + 1) continue;
             const float uR = A.xr[iR];
@@ -108,12 +168,12 @@ __global__ __launch_bounds__(256) void k_stereo_match(const StereoArgs *__restri
             d = bcnt_acc(qb.y ^ kb.y, d);
             d = bcnt_acc(qb.z ^ kb.z, d);
             d = bcnt_acc(qb.w ^ kb.w, d);
-            if ((int)d < OSG_TH_HIGH) best = min(best, (d << 24) | (uint32_t)(c - c0));  // bestDist = TH_HIGH, '<'
+            if ((int)d < OSG_TH_HIGH) best = min(best, (d << 24) | iR);  // bestDist = TH_HIGH, '<'
         }
         for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor(best, o));
         const int thOrbDist = (OSG_TH_HIGH + OSG_TH_LOW) / 2;  // :1138
         if (best != 0xFFFFFFFFu && (int)(best >> 24) < thOrbDist) {  // :1248
-            const int bestIdxR = A.row_list[c0 + (best & 0xFFFFFF)];
+            const int bestIdxR = (int)(best & 0xFFFFFF);
             const float uR0 = A.xr[bestIdxR];
             const float scaleFactor = A.inv_scale[levelL];
             const float scaleduL = roundf(uL * scaleFactor);
@@ -270,9 +330,9 @@ void relocate(T *&field, char *base)
 }
 
 struct Problem {
-    std::vector<int32_t> row_start, row_list;
     std::vector<std::vector<uint8_t>> lv;  // packed host levels (left 0..L-1, right 0..L-1)
     bool dev[2] = {false, false};          // pyramid read in place (left, right)
+    size_t rs_off = 0, rl_off = 0;         // this frame's vRowIndices CSR in the device row buffer (ints)
 };
 
 int check_pyr(osg_ctx *ctx, const osg_image_pyramid &P, int n_levels, const char *which, int b)
@@ -297,6 +357,7 @@ int stereo_run(osg_ctx *ctx, const osg_stereo_frame *F, int B, float *u_right, f
     std::vector<StereoArgs> args(B);
     std::vector<Problem> P(B);
     std::vector<size_t> o_base(B + 1, 0);
+    size_t row_ints = 0;   // device vRowIndices of all frames (row_start + row_list capacity)
     int maxn = 0;
     for (int b = 0; b < B; b++) {
         const osg_stereo_frame &S = F[b];
@@ -322,41 +383,27 @@ int stereo_run(osg_ctx *ctx, const osg_stereo_frame *F, int B, float *u_right, f
             OSG_REQUIRE(ctx, S.octave[i] >= 0 && S.octave[i] < S.n_levels, "problem %d: octave[%d]", b, i);
         for (int i = 0; i < S.n_right; i++)
             OSG_REQUIRE(ctx, S.octave_r[i] >= 0 && S.octave_r[i] < S.n_levels, "problem %d: right octave[%d]", b, i);
-        // vRowIndices (ref:src/Frame.cc:1150-1170): right keypoint iR on rows floor(y - r) .. ceil(y + r),
-        // r = 2 mvScaleFactors[octave]; rows outside the image (the reference would index past
-        // vRowIndices) are dropped
+        // vRowIndices (ref:src/Frame.cc:1150-1170) is built on the device by k_stereo_rows; a right
+        // keypoint covers at most 2 r + 3 <= 4 max(mvScaleFactors) + 3 rows
         const int nRows = S.left.rows[0];
+        OSG_REQUIRE(ctx, nRows <= MAX_ROWS0, "problem %d: %d image rows above %d", b, nRows, MAX_ROWS0);
+        float smax = 1.0f;
+        for (int l = 0; l < S.n_levels; l++) smax = std::max(smax, S.scale_factors[l]);
+        OSG_REQUIRE(ctx, smax < 1e6f, "problem %d: scale factors", b);
         Problem &p = P[b];
-        p.row_start.assign(nRows + 1, 0);
-        for (int iR = 0; iR < S.n_right; iR++) {
-            const float kpY = S.yr[iR];
-            const float r = 2.0f * S.scale_factors[S.octave_r[iR]];
-            const int maxr = (int)std::ceil(kpY + r);
-            const int minr = (int)std::floor(kpY - r);
-            for (int yi = std::max(minr, 0); yi <= std::min(maxr, nRows - 1); yi++) p.row_start[yi + 1]++;
-        }
-        for (int yi = 0; yi < nRows; yi++) p.row_start[yi + 1] += p.row_start[yi];
-        p.row_list.assign(p.row_start[nRows], 0);
-        {
-            std::vector<int32_t> fill(p.row_start.begin(), p.row_start.end() - 1);
-            for (int iR = 0; iR < S.n_right; iR++) {
-                const float kpY = S.yr[iR];
-                const float r = 2.0f * S.scale_factors[S.octave_r[iR]];
-                const int maxr = (int)std::ceil(kpY + r);
-                const int minr = (int)std::floor(kpY - r);
-                for (int yi = std::max(minr, 0); yi <= std::min(maxr, nRows - 1); yi++) p.row_list[fill[yi]++] = iR;
-            }
-        }
+        p.rs_off = row_ints;
+        p.rl_off = row_ints + (size_t)nRows + 1;
+        row_ints = p.rl_off + (size_t)S.n_right * (size_t)((int)std::ceil(4.0f * smax) + 3);
         A.rows0 = nRows;
+        A.n_right = S.n_right;
         set_off(A.x, pk.add(S.x, sizeof(float) * S.n));
         set_off(A.y, pk.add(S.y, sizeof(float) * S.n));
         set_off(A.oct, pk.add(S.octave, sizeof(int32_t) * S.n));
         set_off(A.desc, pk.add(S.desc, (size_t)S.n * 32));
         set_off(A.xr, pk.add(S.xr, sizeof(float) * S.n_right));
+        set_off(A.yr, pk.add(S.yr, sizeof(float) * S.n_right));
         set_off(A.oct_r, pk.add(S.octave_r, sizeof(int32_t) * S.n_right));
         set_off(A.desc_r, pk.add(S.desc_r, (size_t)S.n_right * 32));
-        set_off(A.row_start, pk.add(p.row_start.data(), sizeof(int32_t) * (nRows + 1)));
-        set_off(A.row_list, pk.add(p.row_list.data(), sizeof(int32_t) * p.row_list.size()));
         set_off(A.scale, pk.add(S.scale_factors, sizeof(float) * S.n_levels));
         set_off(A.inv_scale, pk.add(S.inv_scale_factors, sizeof(float) * S.n_levels));
         p.lv.resize(2 * S.n_levels);
@@ -407,10 +454,11 @@ int stereo_run(osg_ctx *ctx, const osg_stereo_frame *F, int B, float *u_right, f
     int32_t *pin_out = (int32_t *)((char *)pin_args + args_bytes);
     char *dev_in = nullptr;
     StereoArgs *dev_args = nullptr;
-    int32_t *dev_out = nullptr;
+    int32_t *dev_out = nullptr, *dev_rows = nullptr;
     OSG_ALLOC(ctx, dev_in, SLOT_TMP0, pk.total + 256);
     OSG_ALLOC(ctx, dev_args, SLOT_TMP1, args_bytes);
     OSG_ALLOC(ctx, dev_out, SLOT_TMP2, out_bytes);
+    OSG_ALLOC(ctx, dev_rows, SLOT_TMP3, sizeof(int32_t) * row_ints + 256);
     const size_t N = o_base[B];
     for (int b = 0; b < B; b++) {
         StereoArgs &A = args[b];
@@ -419,10 +467,11 @@ int stereo_run(osg_ctx *ctx, const osg_stereo_frame *F, int B, float *u_right, f
         relocate(A.oct, dev_in);
         relocate(A.desc, dev_in);
         relocate(A.xr, dev_in);
+        relocate(A.yr, dev_in);
         relocate(A.oct_r, dev_in);
         relocate(A.desc_r, dev_in);
-        relocate(A.row_start, dev_in);
-        relocate(A.row_list, dev_in);
+        A.row_start = (GLOBAL int32_t *)(dev_rows + P[b].rs_off);
+        A.row_list = (GLOBAL int32_t *)(dev_rows + P[b].rl_off);
         relocate(A.scale, dev_in);
         relocate(A.inv_scale, dev_in);
         for (int l = 0; l < MAX_LEVELS; l++) {
@@ -441,6 +490,8 @@ int stereo_run(osg_ctx *ctx, const osg_stereo_frame *F, int B, float *u_right, f
     hipEvent_t *ev = osg_ctx_events(ctx);
     if (!ev) return osg_set_error(ctx, OSG_E_HIP, "event create failed");
     OSG_HIP_CHECK(ctx, hipEventRecord(ev[0], ctx->stream));
+    hipLaunchKernelGGL(k_stereo_rows, dim3(B), dim3(1024), 0, ctx->stream, dev_args);
+    OSG_HIP_CHECK(ctx, hipGetLastError());
     hipLaunchKernelGGL(k_stereo_match, dim3((maxn + 3) / 4, B), dim3(256), 0, ctx->stream, dev_args);
     OSG_HIP_CHECK(ctx, hipGetLastError());
     hipLaunchKernelGGL(k_stereo_filter, dim3(B), dim3(1024), 0, ctx->stream, dev_args);

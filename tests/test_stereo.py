@@ -126,3 +126,25 @@ def test_gpu_hand_cases_and_edges(ctx, oracle):
     ref = oc.stereo(oracle, D)
     same(st.ComputeStereoMatches(ctx, D), ref)
     assert ref[2] > 50
+
+
+@pytest.mark.gpu
+def test_gpu_device_row_index(ctx, oracle):
+    """vRowIndices built on the device (k_stereo_rows: LDS counts, block scan, atomic fill in any order):
+    * a 1100-row image (more rows than the workgroup's 1024 threads: two rows per scan segment);
+    * keypoints 2 px from the top and bottom, whose row bands the reference would index past (clipped);
+    * 30 % exact duplicates on the same row: Hamming ties resolve to the lowest right index, as the
+      reference's ascending candidate vector does."""
+    rng = np.random.default_rng(9995)
+    F = st.synth_stereo_frame(rng, n=900, width=800, height=1100, edge=2.0, dup=0.3)
+    yr = np.array(F.yr, np.float32)
+    yr[:20] = rng.uniform(0.0, 1.5, 20)
+    yr[20:40] = 1099.0 - rng.uniform(0.0, 1.5, 20)
+    F = st.StereoFrame(desc=F.desc, x=F.x, y=F.y, octave=F.octave, desc_r=F.desc_r, xr=F.xr, yr=yr,
+                       octave_r=F.octave_r, left=F.left, right=F.right)
+    ref = oc.stereo(oracle, F)
+    same(st.ComputeStereoMatches(ctx, F), ref)
+    assert ref[2] > 200
+    outs, nm = st.ComputeStereoMatchesBatch(ctx, [F, F])
+    for (ur, d), k in zip(outs, nm):
+        same((ur, d, k), ref)
