@@ -428,7 +428,7 @@ def main():
 
 _LINE_HEAD = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data")
-_LINE_ROOF = ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic", "kernel_us",
+_LINE_ROOF = ("kernel", "bound", "achieved", "peak", "unit", "frac", "frac_of_i8_peak", "traffic", "kernel_us",
               "algorithmic_ops_per_launch", "algorithmic_flop_per_launch", "algorithmic_bytes_per_launch",
               "mfma_busy_frac_pmc")
 _LINE_CPU = ("value", "unit", "cores", "kind", "value_1thread", "sample")
