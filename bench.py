@@ -54,7 +54,9 @@ PEAK_I8_TOPS = 256 * 4 * 1024 * 2 * 2.4e9 / 1e12
 # FP4 (e2m1) block-scaled v_mfma_scale_f32_32x32x64_f8f6f4: the BF16 form's cycles at 4x K, twice the I8 rate
 PEAK_FP4_TOPS = 2 * PEAK_I8_TOPS
 I8_OPS_PER_PAIR = 512          # 256 MACs per (query, train row) pair
-MFMA_EPILOGUE_VALU_PER_PAIR = 2  # v_med3_i32 + v_min_i32 on the accumulator's packed key
+# the matrix-core forms' top-2 epilogue per key: v_min3_i32 + v_med3_i32 + v_min_i32 per two keys, plus the
+# 4 rebasing subtractions per 16 keys of a 32-row tile (28 VALU ops per tile per wave)
+MFMA_EPILOGUE_VALU_PER_PAIR = 1.75
 MFMA_MAX_ROWS = 8192           # the I8 kernel's 13-bit row field (osg_top2_mfma_max_rows)
 LINE_MAX_BYTES = 8192          # the stdout line's budget (the driver did not parse r04's 21 KB line)
 
@@ -78,6 +80,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--ramp-s", type=float, default=0.5,
+                    help="untimed launches of the headline step for this long before the warmup (GPU clock ramp)")
     ap.add_argument("--nq", type=int, default=2000)
     ap.add_argument("--nt", type=int, default=2000)
     ap.add_argument("--c2-batch", type=int, default=1024,
@@ -190,6 +194,16 @@ def main():
     def step():
         ctx.hamming_top2_batch_dev(dqb, nq, dtb, nt, B, doutb)
 
+    # Clock ramp (untimed, before the W warmup steps): launches of the same step for --ramp-s seconds.
+    # A box that has been idle runs the first ~25 launches at a lower clock: with 20 timed steps after 5
+    # warmup steps the kernel read 561.7 us per launch, with 200 after 20 on the same box 482.3 us
+    # (gpurun_out/r05g).  The count is reported in config.
+    ramp_n, t_r = 0, time.perf_counter()
+    while time.perf_counter() - t_r < args.ramp_s:
+        for _ in range(8):
+            step()
+        torch.cuda.synchronize(dev)
+        ramp_n += 8
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -328,6 +342,7 @@ def main():
                                f"{B} independent frames per launch per GPU (headline; the one-frame launch is "
                                f"`single_launch`)",
                    "nq": nq, "nt": nt, "frames_per_step": B, "global_batch": world * B,
+                   "untimed_ramp_launches": ramp_n,
                    "parallelism": f"replicas x{world} (independent frames per GPU, no data-path collective)"},
         "roofline": roofline,
         "single_launch": single,
