@@ -150,6 +150,7 @@ struct LbaDev {
     // past CMAX, Hs holds only the envelope's lower 32 x 32 tiles: row block t keeps column blocks
     // blk_first[t] .. t, contiguous after env_off[t] tiles, each tile row-major; null: dense n x n
     const int32_t *env_off;
+    int chol_fused;                      // 0: column launches, 1: k_chol_dense, 2: k_chol_env (+ its own back solve)
     int *flag;                           // [0] cholesky ok
     unsigned long long *tstamp;          // phase timestamps (OSG_LBA_PROFILE=2), else null
 };
@@ -1209,14 +1210,22 @@ struct CholLds {
 //      m_c+1,m -= l10 m_c,m (m <= c): written one step later (other threads read row c + 1 now;
 //      nothing reads it in the next step).  Pivots go to s_d (the diagonal of G is read now).
 // An odd nb pairs its last column with padding column nb (identity: l10 = 0, d1 = 1).
-__device__ __forceinline__ int chol_factor_diag(CholLds &L, int nb)
+// GUARD: a workgroup of more than 256 threads (k_chol_dense), of which threads 0..255 eliminate and
+// every thread takes the barriers.
+template <bool GUARD = false, class LDS>
+__device__ __forceinline__ int chol_factor_diag(LDS &L, int nb)
 {
     const int tid = threadIdx.x;
-    const int jj = tid & 31, ib = tid >> 5;
+    const bool act = !GUARD || tid < 256;
+    const int jj = tid & 31, ib = (tid >> 5) & 7;
     int ok = 1;
     double defer_val = 0.0;
     int defer_at = -1;  // index into sM of the deferred row-(c+1) value
     for (int c = 0; c < nb; c += 2) {
+        if (!act) {
+            __syncthreads();
+            continue;
+        }
         if (defer_at >= 0) (&L.sM[0][0])[defer_at] = defer_val;
         defer_at = -1;
         const double d0 = L.sG[c][c], e = L.sG[c + 1][c], d1r = L.sG[c + 1][c + 1];
@@ -1258,7 +1267,7 @@ __device__ __forceinline__ int chol_factor_diag(CholLds &L, int nb)
         }
         __syncthreads();
     }
-    if (defer_at >= 0) (&L.sM[0][0])[defer_at] = defer_val;
+    if (act && defer_at >= 0) (&L.sM[0][0])[defer_at] = defer_val;
     __syncthreads();
     if (tid < CB) {
         const double d = L.s_d[tid];
@@ -1266,7 +1275,7 @@ __device__ __forceinline__ int chol_factor_diag(CholLds &L, int nb)
     }
     __syncthreads();
     // L_jj^-1 = D^-1/2 M (lower)
-    for (int e = tid; e < CB * CB; e += 256) {
+    for (int e = tid; e < CB * CB; e += blockDim.x) {
         const int i = e >> 5, m = e & 31;
         L.sM[i][m] = (m <= i) ? L.sM[i][m] * L.s_rsq[i] : 0.0;
     }
@@ -1331,6 +1340,7 @@ __global__ __launch_bounds__(256) void k_chol_col(const LbaDev *__restrict__ Ds,
 {
     LBA_GRAPH(M_ACT);
     if (j >= D.nblk_red || bx >= D.nblk_red - j) return;
+    if (D.chol_fused) return;  // factored by k_chol_dense / k_chol_env
     // past CMAX workgroup 0 is the diagonal block and workgroup b >= 1 the b-th envelope row of the
     // column (col_rows): a row block outside the envelope has an all-zero tile here, and its L_tj
     // stays zero
@@ -1360,6 +1370,317 @@ __global__ __launch_bounds__(256) void k_chol_col(const LbaDev *__restrict__ Ds,
     if (t == 0) chol_diag_out(D, L, k0, nb, n, bj, ok);
     else chol_offdiag_out(D, L, k0, R0, nb, n);
     if (ts) ts[3] = ts[4] = wall_clock64();
+}
+
+// The whole left-looking factorisation of a dense reduced system (n <= CMAX: LocalBundleAdjustment)
+// in one 1024-thread workgroup per graph, instead of one k_chol_col launch per column block: the
+// column steps' latency chains (operand loads, the elimination's barriers) then follow each other
+// without a launch boundary, and the diagonal tile is eliminated once per column instead of once per
+// row-block workgroup.  Per column block j (k0 = 32 j, row blocks j .. nblk - 1 held in LDS):
+//   1. tasks over the 16 waves: 16 x 16 quadrants X_t = A_tj - sum_{m < k0} L_tm L_jm^T (FP64 MFMA
+//      over the whole K; the diagonal tile's lower quadrants only), and b_j - sum_m L_jm y_m;
+//   2. chol_factor_diag on threads 0..255: L_jj^-1 = D^-1/2 Lt^-1;
+//   3. Linv and y_j out, then L_tj = X_t L_jj^-T per quadrant (FP64 MFMA) over A_tj.
+// The outputs are k_chol_col's (L below the diagonal in Hs, Linv, y in x), so k_chol_back follows
+// unchanged.  Its sums are ordered differently from k_chol_col's (one MFMA chain per quadrant
+// instead of four K slices), so the two agree to rounding (OSG_CHOL_DENSE=0 selects the column
+// launches, tests/test_ba_gpu.py compares them).
+constexpr int CD_T = 1024;
+__global__ __launch_bounds__(CD_T) void k_chol_dense(const LbaDev *__restrict__ Ds)
+{
+    LBA_GRAPH(M_ACT);
+    const int n = 6 * D.nhp;
+    if (n == 0 || n > CMAX || D.chol_fused != 1) return;
+    __shared__ double s_x[CMAX / CB][CB][CB + 1];
+    __shared__ double s_m[CB][CB + 1];
+    __shared__ double s_rsq[CB], s_d[CB], s_rhs[CB];
+    struct Lds {
+        double (&sG)[CB][CB + 1];
+        double (&sM)[CB][CB + 1];
+        double *s_rsq, *s_d;
+    } L{s_x[0], s_m, s_rsq, s_d};
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+    double *A = D.Hs;
+    const int nblk = (n + CB - 1) / CB;
+    const int g4 = 4 * (l >> 4);
+    for (int j = 0; j < nblk; j++) {
+        const int k0 = j * CB, nb = min(CB, n - k0), ntile = nblk - j;
+        const int ntask = 3 + 4 * (ntile - 1);  // the diagonal tile's lower quadrants, the row blocks' quadrants
+        for (int e = tid; e < CB * (CB + 1); e += CD_T) (&s_m[0][0])[e] = 0.0;
+        for (int task = w; task < ntask; task += CD_T / 64) {
+            int t, a, b;
+            if (task < 3) {
+                t = 0;
+                a = task > 0 ? 1 : 0;
+                b = task == 2 ? 1 : 0;
+            } else {
+                t = 1 + (task - 3) / 4;
+                a = ((task - 3) >> 1) & 1;
+                b = (task - 3) & 1;
+            }
+            const int R0 = k0 + t * CB + 16 * a, C0 = k0 + 16 * b;  // quadrant rows, columns
+            const int ra = R0 + (l & 15), rb = C0 + (l & 15);
+            const bool va = ra < n, vb = rb < n;
+            const double *pa = A + (size_t)(va ? ra : 0) * n + g4, *pb = A + (size_t)(vb ? rb : 0) * n + g4;
+            // the diagonal quadrants (0, 0) and (1, 1) also reduce b_j - sum_m L_jm y_m for their rows from
+            // the same A operands (rows of block j)
+            const bool rhs = t == 0 && a == b;
+            d4 acc = {0.0, 0.0, 0.0, 0.0};
+            double rp = 0.0;
+            // one 16-column step per iteration, the next step's operands loading while this one multiplies
+            double2 cur[4], nxt[4], ycur[2], ynxt[2];
+            auto load = [&](int m, double2 (&o)[4], double2 (&yo)[2]) {
+                o[0] = *(const double2 *)(pa + m);
+                o[1] = *(const double2 *)(pa + m + 2);
+                o[2] = *(const double2 *)(pb + m);
+                o[3] = *(const double2 *)(pb + m + 2);
+                if (rhs) {
+                    yo[0] = *(const double2 *)(D.x + g4 + m);
+                    yo[1] = *(const double2 *)(D.x + g4 + m + 2);
+                }
+            };
+            if (k0 > 0) load(0, cur, ycur);
+            for (int m = 0; m < k0; m += 16) {
+                if (m + 16 < k0) load(m + 16, nxt, ynxt);
+                const double av[4] = {va ? cur[0].x : 0.0, va ? cur[0].y : 0.0, va ? cur[1].x : 0.0, va ? cur[1].y : 0.0};
+                const double bv[4] = {vb ? cur[2].x : 0.0, vb ? cur[2].y : 0.0, vb ? cur[3].x : 0.0, vb ? cur[3].y : 0.0};
+#pragma unroll
+                for (int i = 0; i < 4; i++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[i], acc, 0, 0, 0);
+                if (rhs) {
+                    const double yv[4] = {ycur[0].x, ycur[0].y, ycur[1].x, ycur[1].y};
+#pragma unroll
+                    for (int i = 0; i < 4; i++) rp += av[i] * yv[i];
+                }
+#pragma unroll
+                for (int v = 0; v < 4; v++) cur[v] = nxt[v];
+                ycur[0] = ynxt[0];
+                ycur[1] = ynxt[1];
+            }
+            if (rhs) {  // the 4 k-groups of a row: lanes l, l ^ 16, l ^ 32, l ^ 48
+                rp += __shfl_xor(rp, 16);
+                rp += __shfl_xor(rp, 32);
+                const int r = 16 * a + (l & 15);
+                if (l < 16) s_rhs[r] = (k0 + r < n) ? D.bs[k0 + r] - rp : 0.0;
+            }
+            const int c = 16 * b + (l & 15);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int r = 16 * a + (l >> 4) + 4 * q;
+                const int gr = k0 + t * CB + r, gc = k0 + c;
+                double v;
+                if (gr < n && gc < n) v = A[(size_t)gr * n + gc] - acc[q];
+                else v = (t == 0 && r == c) ? 1.0 : 0.0;   // identity padding of the diagonal tile
+                s_x[t][r][c] = v;
+                if (t == 0 && a == 1 && b == 0) s_x[0][c][r] = 0.0;  // upper quadrant: read, never used
+            }
+        }
+        __syncthreads();
+        if (tid < CB) s_m[tid][tid] = 1.0;
+        __syncthreads();
+        const int ok = chol_factor_diag<true>(L, nb);
+        if (tid == 0 && !ok) D.flag[0] = 0;
+        for (int e = tid; e < CB * CB; e += CD_T) {
+            const int r = e >> 5, c = e & 31;
+            if (k0 + r < n) D.Linv[(size_t)(k0 + r) * CB + c] = s_m[r][c];
+        }
+        if (tid < 256) {  // y_j = L_jj^-1 rhs, 8 threads per row
+            const int i = tid >> 3, p = tid & 7;
+            double acc = 0.0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) acc += s_m[i][p + 8 * q] * s_rhs[p + 8 * q];
+            acc += __shfl_xor(acc, 1);
+            acc += __shfl_xor(acc, 2);
+            acc += __shfl_xor(acc, 4);
+            if (p == 0 && i < nb) D.x[k0 + i] = acc;
+        }
+        // L_tj = X_t L_jj^-T, quadrant (qr, qc) per task
+        for (int task = w; task < 4 * (ntile - 1); task += CD_T / 64) {
+            const int t = 1 + task / 4, qr = 16 * ((task >> 1) & 1), qc = 16 * (task & 1);
+            d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int ks = 0; ks < CB / 4; ks++) {
+                const int k = 4 * ks + (l >> 4);
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(s_x[t][qr + (l & 15)][k], s_m[qc + (l & 15)][k], acc, 0, 0, 0);
+            }
+            const int c = qc + (l & 15), R0 = k0 + t * CB;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int r = qr + (l >> 4) + 4 * q;
+                if (R0 + r < n && c < nb) A[(size_t)(R0 + r) * n + k0 + c] = acc[q];
+            }
+        }
+        __syncthreads();  // L_tj, Linv and y_j of this column before the next column reads them
+    }
+}
+
+// The right-looking envelope factorisation (past CMAX: BundleAdjustment) and its backward solve in one
+// 1024-thread workgroup per graph, for systems whose column blocks have at most ENV_T - 1 envelope rows
+// below the diagonal (a banded map: 7 for the 1500-KF open map, 13 closed into a loop) and n <= ENV_NX.
+// It replaces k_chol_col + k_chol_trail per column block (two launches of a few workgroups each) and
+// the backward solve's launches with one workgroup whose column steps follow each other in LDS:
+//   1. stage the diagonal tile and the column's envelope tiles (already trailing-updated) in LDS;
+//   2. chol_factor_diag; Linv and y_j out (y_j also kept in LDS);
+//   3. L_tj = X_t L_jj^-T per quadrant (FP64 MFMA), written over A_tj and kept in LDS;
+//   4. the trailing update A_tu -= L_tj L_uj^T of every envelope pair (t >= u) and b_t -= L_tj y_j.
+// The same products in the same order as k_chol_col (K = 0 past CMAX) and k_chol_trail, so the factor is
+// theirs bit for bit; the backward solve is k_chol_back_large's, with x in the tiles' LDS.
+constexpr int ENV_T = 16;                       // staged tiles: the diagonal + up to 15 envelope rows
+constexpr int ENV_NX = ENV_T * CB * (CB + 1);   // x of the backward solve in the same LDS (16 896)
+__global__ __launch_bounds__(CD_T) void k_chol_env(const LbaDev *__restrict__ Ds)
+{
+    LBA_GRAPH(M_ACT);
+    if (D.chol_fused != 2) return;
+    const int n = 6 * D.nhp;
+    __shared__ double s_x[ENV_T][CB][CB + 1];
+    __shared__ double s_m[CB][CB + 1];
+    __shared__ double s_part[CB][CB + 1];
+    __shared__ double s_rsq[CB], s_d[CB], s_rhs[CB], s_y[CB];
+    __shared__ int s_rb[ENV_T];
+    struct Lds {
+        double (&sG)[CB][CB + 1];
+        double (&sM)[CB][CB + 1];
+        double *s_rsq, *s_d;
+    } L{s_x[0], s_m, s_rsq, s_d};
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+    double *A = D.Hs;
+    const int nblk = D.nblk_red;
+    for (int j = 0; j < nblk; j++) {
+        const int k0 = j * CB, nb = min(CB, n - k0);
+        const int r0 = D.col_rows_start[j], m = D.col_rows_start[j + 1] - r0;
+        if (tid <= m) s_rb[tid] = tid == 0 ? j : D.col_rows[r0 + tid - 1];
+        for (int e = tid; e < CB * (CB + 1); e += CD_T) (&s_m[0][0])[e] = 0.0;
+        if (tid < CB) s_rhs[tid] = tid < nb ? D.bs[k0 + tid] - 0.0 : 0.0;
+        __syncthreads();
+        // 1. the tiles as k_chol_trail left them (K = 0: nothing left to subtract)
+        for (int e = tid; e < (m + 1) * CB * CB; e += CD_T) {
+            const int t = e >> 10, r = (e >> 5) & 31, c = e & 31, rb = s_rb[t], R = rb * CB + r;
+            double v;
+            if (t == 0) v = (R < n && k0 + c < n) ? (c <= r ? A[hs_el(hs_blk(D, n, rb), r, k0 + c)] : 0.0) : (r == c ? 1.0 : 0.0);
+            else v = (R < n && k0 + c < n) ? A[hs_el(hs_blk(D, n, rb), r, k0 + c)] : 0.0;
+            s_x[t][r][c] = v;
+        }
+        __syncthreads();
+        if (tid < CB) s_m[tid][tid] = 1.0;
+        __syncthreads();
+        // 2.
+        const int ok = chol_factor_diag<true>(L, nb);
+        if (tid == 0 && !ok) D.flag[0] = 0;
+        for (int e = tid; e < CB * CB; e += CD_T) {
+            const int r = e >> 5, c = e & 31;
+            if (k0 + r < n) D.Linv[(size_t)(k0 + r) * CB + c] = s_m[r][c];
+        }
+        if (tid < 256) {  // y_j = L_jj^-1 rhs, 8 threads per row (chol_diag_out's sums)
+            const int i = tid >> 3, p = tid & 7;
+            double acc = 0.0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) acc += s_m[i][p + 8 * q] * s_rhs[p + 8 * q];
+            acc += __shfl_xor(acc, 1);
+            acc += __shfl_xor(acc, 2);
+            acc += __shfl_xor(acc, 4);
+            if (p == 0 && i < nb) D.x[k0 + i] = acc;
+            if (p == 0) s_y[i] = i < nb ? acc : 0.0;
+        }
+        // 3. L_tj = X_t L_jj^-T (chol_offdiag_out's products), at most 4 quadrants per wave
+        d4 lt[(4 * (ENV_T - 1) + CD_T / 64 - 1) / (CD_T / 64)];
+#pragma unroll
+        for (int k = 0; k < (int)(sizeof(lt) / sizeof(lt[0])); k++) {
+            const int task = w + (CD_T / 64) * k;
+            if (task >= 4 * m) break;
+            const int t = 1 + task / 4, qr = 16 * ((task >> 1) & 1), qc = 16 * (task & 1);
+            d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int ks = 0; ks < CB / 4; ks++) {
+                const int kk = 4 * ks + (l >> 4);
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(s_x[t][qr + (l & 15)][kk], s_m[qc + (l & 15)][kk], acc, 0, 0, 0);
+            }
+            lt[k] = acc;
+            const int c = qc + (l & 15), rb = s_rb[t];
+            const HsBlk bR = hs_blk(D, n, rb);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int r = qr + (l >> 4) + 4 * q;
+                if (rb * CB + r < n && c < nb) A[hs_el(bR, r, k0 + c)] = acc[q];
+            }
+        }
+        __syncthreads();  // every read of the X tiles is done
+#pragma unroll
+        for (int k = 0; k < (int)(sizeof(lt) / sizeof(lt[0])); k++) {
+            const int task = w + (CD_T / 64) * k;
+            if (task >= 4 * m) break;
+            const int t = 1 + task / 4, qr = 16 * ((task >> 1) & 1), qc = 16 * (task & 1);
+            const int c = qc + (l & 15), rb = s_rb[t];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int r = qr + (l >> 4) + 4 * q;
+                s_x[t][r][c] = (rb * CB + r < n && c < nb) ? lt[k][q] : 0.0;  // k_chol_trail's staged L tile
+            }
+        }
+        __syncthreads();
+        // 4. trailing update of every envelope pair (a >= b) and the right-hand side
+        const int npr = m * (m + 1) / 2;
+        for (int task = w; task < 4 * npr; task += CD_T / 64) {
+            const int pr = task >> 2;
+            int a = (int)((sqrt(8.0 * pr + 1.0) - 1.0) * 0.5);  // pr = a (a + 1) / 2 + b, b <= a
+            while (a * (a + 1) / 2 > pr) a--;
+            while ((a + 1) * (a + 2) / 2 <= pr) a++;
+            const int b = pr - a * (a + 1) / 2;
+            const int ta = 1 + a, tb = 1 + b, qr = 16 * ((task >> 1) & 1), qc = 16 * (task & 1);
+            d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int ks = 0; ks < CB / 4; ks++) {
+                const int kk = 4 * ks + (l >> 4);
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(s_x[ta][qr + (l & 15)][kk], s_x[tb][qc + (l & 15)][kk], acc, 0, 0, 0);
+            }
+            const int R0 = s_rb[ta] * CB, C0 = s_rb[tb] * CB, c = qc + (l & 15);
+            const HsBlk bt = hs_blk(D, n, s_rb[ta]);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int r = qr + (l >> 4) + 4 * q;
+                if (R0 + r < n && C0 + c < n) A[hs_el(bt, r, C0 + c)] -= acc[q];
+            }
+        }
+        if (tid < m * CB) {  // b_t -= L_tj y_j (k_chol_trail's diagonal-pair sums)
+            const int t = 1 + (tid >> 5), r = tid & 31, R = s_rb[t] * CB + r;
+            double sacc = 0.0;
+#pragma unroll 8
+            for (int k = 0; k < CB; k++) sacc += s_x[t][r][k] * s_y[k];
+            if (R < n) D.bs[R] -= sacc;
+        }
+        __syncthreads();  // the updated tiles and b before the next column stages them
+    }
+    // backward solve L^T x = y (k_chol_back_large's blocks and sums), x over the tiles' LDS
+    double *xv = &s_x[0][0][0];
+    for (int i = tid; i < n; i += CD_T) xv[i] = 0.0;
+    const int c = tid & 31, g = tid >> 5;
+    for (int bi = nblk - 1; bi >= 0; bi--) {
+        const int k0 = bi * CB, nb = min(CB, n - k0);
+        (&s_m[0][0])[tid] = D.Linv[(size_t)min(k0 + (tid >> 5), n - 1) * CB + (tid & 31)];  // s_li[r * CB + c]
+        __syncthreads();
+        double acc = 0.0;
+        if (c < nb) {
+            for (int q = D.col_rows_start[bi]; q < D.col_rows_start[bi + 1]; q++) {
+                const int rb = D.col_rows[q], row = rb * CB + g;
+                if (row < n) acc += A[hs_el(hs_blk(D, n, rb), g, k0 + c)] * xv[row];
+            }
+        }
+        s_part[c][g] = acc;
+        __syncthreads();
+        if (tid < CB) {
+            double sp = 0.0;
+#pragma unroll
+            for (int gg = 0; gg < 32; gg++) sp += s_part[tid][gg];
+            s_rhs[tid] = (tid < nb) ? D.x[k0 + tid] - sp : 0.0;
+        }
+        __syncthreads();
+        if (tid < nb) {
+            double xs = 0.0;
+#pragma unroll
+            for (int r = 0; r < CB; r++) xs += (&s_m[0][0])[r * CB + tid] * s_rhs[r];
+            xv[k0 + tid] = xs;
+        }
+        __syncthreads();
+    }
+    for (int i = tid; i < n; i += CD_T) D.x[i] = xv[i];
 }
 
 // Backward substitution L^T x = y (y in x after the column launches), one 1024-thread
@@ -1475,7 +1796,7 @@ __global__ __launch_bounds__(256) void k_chol_trail(const LbaDev *__restrict__ D
 {
     LBA_GRAPH(M_ACT);
     const int n = 6 * D.nhp;
-    if (n <= CMAX) return;
+    if (n <= CMAX || D.chol_fused) return;
     if (j >= D.nblk_red) return;
     // the envelope rows of column j (L_tj nonzero): tile (t, u) for every pair of them, u <= t
     const int r0 = D.col_rows_start[j], m = D.col_rows_start[j + 1] - r0;
@@ -1527,7 +1848,7 @@ __global__ __launch_bounds__(1024) void k_chol_back_large(const LbaDev *__restri
 {
     LBA_GRAPH(M_ACT);
     const int n = 6 * D.nhp;
-    if (n <= CMAX || n > CMAX_LARGE) return;
+    if (n <= CMAX || n > CMAX_LARGE || D.chol_fused) return;
     __shared__ double s_x[CMAX_LARGE];
     __shared__ double s_y[CMAX_LARGE];
     __shared__ double s_li[CB * CB];
@@ -1587,7 +1908,7 @@ __global__ __launch_bounds__(BSC) void k_back_step(const LbaDev *__restrict__ Ds
 {
     LBA_GRAPH(M_ACT);
     const int n = 6 * D.nhp;
-    if (n <= CMAX_LARGE) return;
+    if (n <= CMAX_LARGE || D.chol_fused) return;
     const int bi = D.nblk_red - 1 - step;
     if (bi < 0) return;
     const int k0 = bi * CB, nb = min(CB, n - k0);
@@ -1619,7 +1940,7 @@ __global__ __launch_bounds__(EB) void k_back_copy(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT);
     const int n = 6 * D.nhp;
-    if (n <= CMAX_LARGE) return;
+    if (n <= CMAX_LARGE || D.chol_fused) return;
     const int i = bx * EB + threadIdx.x;
     if (i < n) D.x[i] = D.bs[i];
 }
@@ -2479,6 +2800,12 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     // OSG_LIN_WPE=4: k_linearize compiled for 4 waves per SIMD (A/B runs), bit-identical
     static const bool lin_wpe4 = getenv("OSG_LIN_WPE") && atoi(getenv("OSG_LIN_WPE")) == 4;
     static const bool update_stage = getenv("OSG_UPDATE_STAGE") && atoi(getenv("OSG_UPDATE_STAGE")) != 0;
+    // OSG_CHOL_DENSE=0: the per-column k_chol_col (+ k_chol_trail) launches for every system (A/B runs)
+    // instead of the one-workgroup factorisations k_chol_dense and k_chol_env
+    static const bool chol_dense = !(getenv("OSG_CHOL_DENSE") && atoi(getenv("OSG_CHOL_DENSE")) == 0);
+    // OSG_CHOL_ENV=1: k_chol_env for narrow-envelope maps (A/B runs; measured slower than the column launches:
+    // one workgroup serialises each column's trailing update, which k_chol_trail spreads over the chip)
+    static const bool chol_env = getenv("OSG_CHOL_ENV") && atoi(getenv("OSG_CHOL_ENV")) == 1;
     const auto tp0 = std::chrono::steady_clock::now();
     auto ms_since = [&](std::chrono::steady_clock::time_point t) {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
@@ -2622,6 +2949,10 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     static const bool xcd_env = getenv("OSG_LBA_XCD") && atoi(getenv("OSG_LBA_XCD")) == 1;
     const bool xcd = xcd_env && NA >= 8;
     bool large = false;  // some graph's reduced system is past CMAX
+    bool any_dense = false;  // some graph is factored by k_chol_dense (n <= CMAX, at least one free pose)
+    bool any_env = false;    // ... by k_chol_env (past CMAX, a narrow envelope)
+    bool any_col = false;    // ... by column launches (the others)
+    bool huge_col = false;   // ... and past CMAX_LARGE (k_back_step)
     bool huge = false;   // ... past CMAX_LARGE (k_back_step instead of k_chol_back_large)
     for (int a = 0; a < NA; a++) {
         const LbaHost &h = H[act[a]];
@@ -2651,6 +2982,12 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         D.hub_stereo = h.G->huber_stereo > 0.f ? h.G->huber_stereo : (float)std::sqrt(7.815);
         large |= 6 * h.nhp > CMAX;
         huge |= 6 * h.nhp > CMAX_LARGE;
+        if (chol_dense && h.nhp > 0 && 6 * h.nhp <= CMAX) D.chol_fused = 1;
+        else if (chol_env && 6 * h.nhp > CMAX && 6 * h.nhp <= ENV_NX && h.max_col_rows <= ENV_T - 1) D.chol_fused = 2;
+        any_dense |= D.chol_fused == 1;
+        any_env |= D.chol_fused == 2;
+        any_col |= h.nhp > 0 && D.chol_fused == 0;
+        huge_col |= 6 * h.nhp > CMAX_LARGE && D.chol_fused == 0;
         D.pose_h = osg_dptr<int32_t>(din, o.poseh);
         D.hp_pose = osg_dptr<int32_t>(din, o.hppose);
         D.point_h = osg_dptr<int32_t>(din, o.pointh);
@@ -2788,13 +3125,18 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
             LBA_MARK(KT_SPAIRS);
             hipLaunchKernelGGL(k_schur_pairs, gx((int)(((size_t)mx_pairs * 64 + 255) / 256)), dim3(256), 0, ctx->stream, d_dev);
             LBA_MARK(KT_CHOL);
-            for (int jb = 0; jb < mx_red; jb++) {  // row blocks at and below the diagonal block
+            // dense systems (n <= CMAX) in one k_chol_dense workgroup per graph, narrow envelopes in one
+            // k_chol_env workgroup (with its backward solve), the others by column launches
+            if (any_dense) hipLaunchKernelGGL(k_chol_dense, yb, dim3(CD_T), 0, ctx->stream, d_dev);
+            if (any_env) hipLaunchKernelGGL(k_chol_env, yb, dim3(CD_T), 0, ctx->stream, d_dev);
+            if (any_col) for (int jb = 0; jb < mx_red; jb++) {  // row blocks at and below the diagonal block
                 // past CMAX only the envelope's rows: grids sized by the largest reach of any graph
                 int rows = 0, m = 0;
                 for (int a = 0; a < NA; a++) {
                     const LbaHost &h = H[act[a]];
                     if (jb >= h.nblk_red) continue;
                     const bool big = 6 * h.nhp > CMAX;
+                    if (h_dev[a].chol_fused) continue;
                     const int nr = big ? h.col_rows_start[jb + 1] - h.col_rows_start[jb] : 0;
                     rows = std::max(rows, big ? 1 + nr : h.nblk_red - jb);
                     if (big) m = std::max(m, nr);
@@ -2806,8 +3148,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
             }
             LBA_MARK(KT_BACK);
             hipLaunchKernelGGL(k_chol_back, yb, dim3(1024), 0, ctx->stream, d_dev);
-            if (large) hipLaunchKernelGGL(k_chol_back_large, yb, dim3(1024), 0, ctx->stream, d_dev);
-            if (huge) {
+            if (any_col) hipLaunchKernelGGL(k_chol_back_large, yb, dim3(1024), 0, ctx->stream, d_dev);
+            if (huge_col) {
                 for (int step = 0; step < mx_red; step++) {
                     int cols = 0;
                     for (int a = 0; a < NA; a++) {

@@ -526,11 +526,26 @@ __global__ __launch_bounds__(NW * 64) void k_top2_fp4(const uint32_t *__restrict
                         if (tt + 1 < NTILE) a[s] = frag(sb + (tt + 1) * 32 * MX_RS, s);
 #pragma unroll
                         for (int j = 0; j < QT; j++) {
-                            // pairs 2 s (chain A: elements 4 s, 4 s + 1 ... ) and 2 s + 1 (chain B)
-                            key_push2(ka1[j], ka2[j], __float_as_int(accp[j][2 * s]),
-                                      __float_as_int(accp[j][2 * s + 1]));
-                            key_push2(kb1[j], kb2[j], __float_as_int(accp[j][8 + 2 * s]),
-                                      __float_as_int(accp[j][9 + 2 * s]));
+                            if (PIPE == 2) {
+                                // key pairs of tile tt - 1 from K-step 1 on: its last MFMA (issued just before
+                                // this tile's first) has completed once this tile's second one issues, so the
+                                // reads never wait on it (tools/micro/mfma_fp4_rate.hip: the update overlaps
+                                // the chains when it reads no fresh MFMA result).  Pairs p = 0..7 (chain A
+                                // pair p, then chain B pair p - 4) as 3 / 3 / 2 over steps 1..3.
+#pragma unroll
+                                for (int p = 0; p < 8; p++) {
+                                    if (p / 3 + 1 != s) continue;
+                                    const int e = (p & 3) * 2 + (p >> 2) * 8;
+                                    if (p < 4) key_push2(ka1[j], ka2[j], __float_as_int(accp[j][e]), __float_as_int(accp[j][e + 1]));
+                                    else key_push2(kb1[j], kb2[j], __float_as_int(accp[j][e]), __float_as_int(accp[j][e + 1]));
+                                }
+                            } else {
+                                // pairs 2 s (chain A: elements 4 s, 4 s + 1 ... ) and 2 s + 1 (chain B)
+                                key_push2(ka1[j], ka2[j], __float_as_int(accp[j][2 * s]),
+                                          __float_as_int(accp[j][2 * s + 1]));
+                                key_push2(kb1[j], kb2[j], __float_as_int(accp[j][8 + 2 * s]),
+                                          __float_as_int(accp[j][9 + 2 * s]));
+                            }
                             if (s == 3) {
                                 ka1[j] -= 32;
                                 ka2[j] -= 32;
@@ -628,9 +643,9 @@ bool mfma_fp4()
 void mfma_shape_of(bool fp4, int shape, int *d)
 {
     static const int i8[5][4] = {{16, 1, 256, 1}, {8, 2, 256, 1}, {16, 1, 256, 0}, {8, 2, 256, 0}, {8, 1, 256, 1}};
-    static const int f4[6][4] = {{16, 1, 256, 1}, {8, 2, 256, 1}, {16, 1, 256, 0}, {16, 1, 256, 1}, {8, 1, 256, 1},
-                                 {16, 2, 256, 1}};
-    const int *s = fp4 ? f4[(shape >= 1 && shape <= 5 && shape != 3) ? shape : 0]
+    static const int f4[7][4] = {{16, 1, 256, 1}, {8, 2, 256, 1}, {16, 1, 256, 0}, {16, 1, 256, 1}, {8, 1, 256, 1},
+                                 {16, 2, 256, 1}, {16, 1, 256, 2}};
+    const int *s = fp4 ? f4[(shape >= 1 && shape <= 6 && shape != 3) ? shape : 0]
                        : i8[(shape >= 1 && shape <= 4) ? shape : 0];
     for (int i = 0; i < 4; i++) d[i] = s[i];
 }
@@ -664,6 +679,7 @@ int osg_launch_top2_batch_mfma(osg_ctx *ctx, const void *d_query, int32_t nq, co
         case 2: return launch_fp4<16, 1, 256, 0>(ctx, d_query, nq, d_train, nt, nb, d_out);
         case 4: return launch_fp4<8, 1, 256, 1>(ctx, d_query, nq, d_train, nt, nb, d_out);
         case 5: return launch_fp4<16, 2, 256, 1>(ctx, d_query, nq, d_train, nt, nb, d_out);
+        case 6: return launch_fp4<16, 1, 256, 2>(ctx, d_query, nq, d_train, nt, nb, d_out);
         default: return launch_fp4<16, 1, 256, 1>(ctx, d_query, nq, d_train, nt, nb, d_out);
         }
     }

@@ -266,6 +266,61 @@ def test_lba_schur_variants_bit_identical(ctx, env):
         np.testing.assert_array_equal(got[f"q{i}"], r.point)
 
 
+def _env_map_graphs():
+    """Reduced systems past CMAX (n = 894) with narrow envelopes (k_chol_env): a 150-KF open map and one
+    closed into a loop (at most 7 envelope row blocks below a column block)."""
+    return [op.synth_map_graph(np.random.default_rng(71), n_kf=150, n_points=12000, loop=False),
+            op.synth_map_graph(np.random.default_rng(72), n_kf=150, n_points=12000, loop=True)]
+
+
+def _chol_child(env):
+    """LocalBundleAdjustmentBatch of _lba_batch_graphs and BundleAdjustment of _env_map_graphs in a child
+    process under `env` (the factorisation knobs are read once per process)."""
+    import subprocess
+    import sys
+    out = f"/tmp/_osg_chol_{os.getpid()}.npz"
+    code = ("import numpy as np\n"
+            "from orb_slam3_comments_ghr_amd import Context, optimizer as op\n"
+            "from tests.test_ba_gpu import _lba_batch_graphs, _env_map_graphs\n"
+            "o = op.Optimizer(Context(0))\n"
+            "res = o.LocalBundleAdjustmentBatch(_lba_batch_graphs()) + [o.BundleAdjustment(G) for G in _env_map_graphs()]\n"
+            f"np.savez('{out}', **{{f'p{{i}}': r.pose for i, r in enumerate(res)}},\n"
+            "         **{f'q{i}': r.point for i, r in enumerate(res)},\n"
+            "         it=np.array([[r.iterations, r.trials] for r in res]),\n"
+            "         chi=np.array([[r.chi2_initial, r.chi2_final] for r in res]))\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=dict(os.environ, **env), capture_output=True,
+                       text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = dict(np.load(out))
+    os.remove(out)
+    return got
+
+
+def test_lba_chol_fused_vs_column_launches(ctx):
+    """The one-workgroup factorisations against the per-column k_chol_col (+ k_chol_trail) launches:
+    * k_chol_dense (LocalBundleAdjustment windows, the default) against OSG_CHOL_DENSE=0: the same blocked
+      LL^T with its sums in another order, so identical iteration / trial counts and states equal to rounding;
+    * k_chol_env (OSG_CHOL_ENV=1: maps past CMAX with narrow envelopes, its own backward solve) against the
+      default column launches: the same products in the same order as k_chol_col / k_chol_trail /
+      k_chol_back_large, so bit-identical."""
+    o = op.Optimizer(ctx)
+    lba = o.LocalBundleAdjustmentBatch(_lba_batch_graphs())
+    maps = [o.BundleAdjustment(G) for G in _env_map_graphs()]
+    col = _chol_child({"OSG_CHOL_DENSE": "0"})
+    env = _chol_child({"OSG_CHOL_ENV": "1"})
+    for got in (col, env):
+        np.testing.assert_array_equal(got["it"], [[r.iterations, r.trials] for r in lba + maps])
+    np.testing.assert_allclose(col["chi"][:len(lba)], [[r.chi2_initial, r.chi2_final] for r in lba], rtol=1e-12, atol=0)
+    for i, r in enumerate(lba):
+        np.testing.assert_allclose(col[f"p{i}"], r.pose, atol=1e-9, rtol=0)
+        np.testing.assert_allclose(col[f"q{i}"], r.point, atol=1e-9, rtol=0)
+    for i, r in enumerate(lba + maps):  # k_chol_env's maps, and the dense windows under the same default
+        np.testing.assert_array_equal(env["chi"][i], [r.chi2_initial, r.chi2_final])
+        np.testing.assert_array_equal(env[f"p{i}"], r.pose)
+        np.testing.assert_array_equal(env[f"q{i}"], r.point)
+
+
 def test_lba_batch_c4_windows(ctx, oracle):
     """8 C4-sized windows (50 KF x 10k points) in one batch against the oracle."""
     rng = np.random.default_rng(0x0B5EED04 + 7)

@@ -84,3 +84,16 @@ extern "C" int pool_stress(int T, int loops, int n)
     for (auto &x : th) x.join();
     return bad.load();
 }
+
+// the reduced system's size and envelope reach of the last structure build: {n, blocks, max rows below a
+// column block inside the envelope}
+extern "C" void lba_host_envelope(const osg_ba_graph *G, int *out3)
+{
+    osg_ctx ctx;
+    LbaHost H;
+    out3[0] = out3[1] = out3[2] = -1;
+    if (build_structure(&ctx, G, H) != OSG_OK) return;
+    out3[0] = 6 * H.nhp;
+    out3[1] = H.nblk_red;
+    out3[2] = H.max_col_rows;
+}

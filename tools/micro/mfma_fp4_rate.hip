@@ -4,7 +4,9 @@
 // top-2 update (float min3 / med3 / min on the FP4 path's float keys).
 //   mode 0: chains only;  1: + update on floats (fminf / med3 as written);  3: + update on the keys' bit
 //   patterns with integer min3 / med3 (the form k_top2_fp4 uses since late r05);  4: that update alone, no
-//   MFMA (the accumulators are opaque registers rewritten by an empty asm each iteration)
+//   MFMA (the accumulators are opaque registers rewritten by an empty asm each iteration);  5: the chain with
+//   the update's 28 ops on registers no MFMA writes (does VALU issue overlap a wave's own MFMAs?);  6: waves
+//   specialised per SIMD, even waves the chain only, odd waves the update only (across waves?)
 // 1024-thread workgroups (16 waves, 4 per SIMD), G = 1024 workgroups.  Random-ish operands: the clock the
 // chip holds depends on the data, so both forms get nonzero patterns.
 // Build: hipcc --offload-arch=gfx950 -O3 mfma_fp4_rate.hip -o mfma_fp4_rate
@@ -38,7 +40,7 @@ __global__ __launch_bounds__(1024) void k_fp4(float *out, int iters)
     for (int it = 0; it < iters; it++) {
         for (int s = 0; s < 4; s++) asm volatile("" : "+v"(a[s]));
         f32x16 acc;
-        if (MODE == 4) {
+        if (MODE == 4 || (MODE == 6 && (threadIdx.x >> 6) % 2 == 1)) {
             acc = accp;
             asm volatile("" : "+v"(acc));
         } else {
@@ -47,7 +49,24 @@ __global__ __launch_bounds__(1024) void k_fp4(float *out, int iters)
             for (int s = 1; s < 4; s++)
                 acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a[s], b[s], acc, 4, 4, 0, 139, 0, 127);
         }
-        if (MODE == 3 || MODE == 4) {
+        if (MODE == 5) {
+            f32x16 z = c;
+            asm volatile("" : "+v"(z));
+            int j1 = __float_as_int(k1), j2 = __float_as_int(k2), j3 = __float_as_int(k3), j4 = __float_as_int(k4);
+#pragma unroll
+            for (int i = 0; i < 8; i += 2) {
+                const int x = __float_as_int(z[i]), y = __float_as_int(z[i + 1]);
+                const int u = __float_as_int(z[i + 8]), v = __float_as_int(z[i + 9]);
+                int m = med3(j1, x, y);
+                j1 = min(min(j1, x), y);
+                j2 = min(m, j2);
+                m = med3(j3, u, v);
+                j3 = min(min(j3, u), v);
+                j4 = min(m, j4);
+            }
+            k1 = __int_as_float(j1 - 32); k2 = __int_as_float(j2 - 32);
+            k3 = __int_as_float(j3 - 32); k4 = __int_as_float(j4 - 32);
+        } else if (MODE == 3 || MODE == 4 || (MODE == 6 && (threadIdx.x >> 6) % 2 == 1)) {
             int j1 = __float_as_int(k1), j2 = __float_as_int(k2), j3 = __float_as_int(k3), j4 = __float_as_int(k4);
 #pragma unroll
             for (int i = 0; i < 8; i += 2) {
@@ -144,11 +163,14 @@ int main()
     (void)hipMalloc(&d, sizeof(float) * G * 1024);
     // one tile = 32 rows x 32 queries x 256 bits: 262144 (query, row, bit) MACs
     const double tiles = (double)G * 16 * iters;
-    const double ms[6] = {run(k_i8<0>, d, iters, G), run(k_i8<1>, d, iters, G), run(k_fp4<0>, d, iters, G),
-                          run(k_fp4<1>, d, iters, G), run(k_fp4<3>, d, iters, G), run(k_fp4<4>, d, iters, G)};
-    const char *nm[6] = {"i8 chain", "i8 chain + update", "fp4 chain", "fp4 chain + float update",
-                         "fp4 chain + integer update on the bit patterns", "integer update alone (no MFMA)"};
-    for (int m = 0; m < 6; m++)
+    const double ms[8] = {run(k_i8<0>, d, iters, G), run(k_i8<1>, d, iters, G), run(k_fp4<0>, d, iters, G),
+                          run(k_fp4<1>, d, iters, G), run(k_fp4<3>, d, iters, G), run(k_fp4<4>, d, iters, G),
+                          run(k_fp4<5>, d, iters, G), run(k_fp4<6>, d, iters, G)};
+    const char *nm[8] = {"i8 chain", "i8 chain + update", "fp4 chain", "fp4 chain + float update",
+                         "fp4 chain + integer update on the bit patterns", "integer update alone (no MFMA)",
+                         "fp4 chain + the update on registers no MFMA writes",
+                         "even waves fp4 chain only, odd waves integer update only"};
+    for (int m = 0; m < 8; m++)
         printf("{\"mode\": \"%s\", \"ms\": %.4f, \"ns_per_tile_per_simd\": %.3f, \"Tmatch_bits_per_s\": %.1f}\n", nm[m],
                ms[m], ms[m] * 1e6 / (tiles / 1024), tiles * 262144 / (ms[m] * 1e-3) / 1e12);
     (void)hipFree(d);
