@@ -100,6 +100,68 @@ __global__ __launch_bounds__(1024) void k_fp4(float *out, int iters)
     out[blockIdx.x * 1024 + threadIdx.x] = k1 + k2 + k3 + k4 + accp[l & 15];
 }
 
+// 7: two tiles per iteration with two accumulator sets (no copy): the update of each tile's results runs
+//    while the other tile's chain is in flight, reading MFMA results one chain old;  8: 7 with each MFMA's
+//    A operand read from LDS (ds_read_b128 per MFMA, as k_top2_fp4's K-steps)
+__device__ __forceinline__ void upd_bits(int &j1, int &j2, int &j3, int &j4, const f32x16 &v)
+{
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+        const int x = __float_as_int(v[i]), y = __float_as_int(v[i + 1]);
+        const int u = __float_as_int(v[i + 8]), w = __float_as_int(v[i + 9]);
+        int m = med3(j1, x, y);
+        j1 = min(min(j1, x), y);
+        j2 = min(m, j2);
+        m = med3(j3, u, w);
+        j3 = min(min(j3, u), w);
+        j4 = min(m, j4);
+    }
+    j1 -= 32; j2 -= 32; j3 -= 32; j4 -= 32;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(1024) void k_fp4pp(float *out, int iters)
+{
+    const int l = threadIdx.x & 63;
+    __shared__ __attribute__((aligned(16))) int s_a[16][64][4];
+    i32x8 a[4], b[4];
+    for (int s = 0; s < 4; s++)
+        for (int r = 0; r < 8; r++) {
+            const unsigned x = (unsigned)(l * 2654435761u + s * 40503u + r * 977u);
+            a[s][r] = r < 4 ? (int)((x & 0x44444444u) * 3u) : 0;
+            b[s][r] = r < 4 ? (int)(0x22222222u | ((x >> 1) & 0x88888888u)) : 0;
+        }
+    for (int s = 0; s < 4; s++)
+        for (int r = 0; r < 4; r++) s_a[(threadIdx.x >> 6) % 16][l][r] = a[s][r];
+    __syncthreads();
+    const int *sa = &s_a[(threadIdx.x >> 6) % 16][l][0];
+    f32x16 c;
+    for (int i = 0; i < 16; i++) c[i] = (float)(8388608 + i + l);
+    int j1 = 0x7fffffff, j2 = j1, j3 = j1, j4 = j1;
+    f32x16 accA = c, accB = c;
+    auto chain = [&](f32x16 &acc) {
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            i32x8 av = a[s];
+            if (MODE == 8) {
+                const i32x4 v = *(const i32x4 *)(sa + 0);
+                av = i32x8{v[0], v[1], v[2], v[3], 0, 0, 0, 0};
+                asm volatile("" : "+v"(av));
+            }
+            acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, b[s], s ? acc : c, 4, 4, 0, 139, 0, 127);
+        }
+    };
+    for (int it = 0; it < iters; it += 2) {
+        for (int s = 0; s < 4; s++) asm volatile("" : "+v"(a[s]));
+        chain(accA);
+        upd_bits(j1, j2, j3, j4, accB);
+        for (int s = 0; s < 4; s++) asm volatile("" : "+v"(a[s]));
+        chain(accB);
+        upd_bits(j1, j2, j3, j4, accA);
+    }
+    out[blockIdx.x * 1024 + threadIdx.x] = (float)(j1 + j2 + j3 + j4) + accA[l & 15] + accB[l & 15];
+}
+
 template <int MODE>
 __global__ __launch_bounds__(1024) void k_i8(float *out, int iters)
 {
@@ -163,14 +225,17 @@ int main()
     (void)hipMalloc(&d, sizeof(float) * G * 1024);
     // one tile = 32 rows x 32 queries x 256 bits: 262144 (query, row, bit) MACs
     const double tiles = (double)G * 16 * iters;
-    const double ms[8] = {run(k_i8<0>, d, iters, G), run(k_i8<1>, d, iters, G), run(k_fp4<0>, d, iters, G),
-                          run(k_fp4<1>, d, iters, G), run(k_fp4<3>, d, iters, G), run(k_fp4<4>, d, iters, G),
-                          run(k_fp4<5>, d, iters, G), run(k_fp4<6>, d, iters, G)};
-    const char *nm[8] = {"i8 chain", "i8 chain + update", "fp4 chain", "fp4 chain + float update",
+    const double ms[10] = {run(k_i8<0>, d, iters, G), run(k_i8<1>, d, iters, G), run(k_fp4<0>, d, iters, G),
+                           run(k_fp4<1>, d, iters, G), run(k_fp4<3>, d, iters, G), run(k_fp4<4>, d, iters, G),
+                           run(k_fp4<5>, d, iters, G), run(k_fp4<6>, d, iters, G), run(k_fp4pp<7>, d, iters, G),
+                           run(k_fp4pp<8>, d, iters, G)};
+    const char *nm[10] = {"i8 chain", "i8 chain + update", "fp4 chain", "fp4 chain + float update",
                          "fp4 chain + integer update on the bit patterns", "integer update alone (no MFMA)",
                          "fp4 chain + the update on registers no MFMA writes",
-                         "even waves fp4 chain only, odd waves integer update only"};
-    for (int m = 0; m < 8; m++)
+                         "even waves fp4 chain only, odd waves integer update only",
+                         "two accumulator sets, the update one chain behind (no copies)",
+                         "two accumulator sets, + the A operand from LDS per MFMA"};
+    for (int m = 0; m < 10; m++)
         printf("{\"mode\": \"%s\", \"ms\": %.4f, \"ns_per_tile_per_simd\": %.3f, \"Tmatch_bits_per_s\": %.1f}\n", nm[m],
                ms[m], ms[m] * 1e6 / (tiles / 1024), tiles * 262144 / (ms[m] * 1e-3) / 1e12);
     (void)hipFree(d);
