@@ -706,14 +706,21 @@ struct FeatVecCSR {
     explicit FeatVecCSR(const FeatVecT &fvec) { assign(fvec); }
     void assign(const FeatVecT &fvec)
     {
-        node.clear();
-        start.clear();
-        feat.clear();
-        start.push_back(0);
+        // sized once, then written in place (push_back per feature measured ~2x slower)
+        const size_t nn = fvec.size();
+        size_t nf = 0;
+        for (const auto &kv : fvec) nf += kv.second.size();
+        node.resize(nn);
+        start.resize(nn + 1);
+        feat.resize(nf);
+        uint32_t *pn = node.data();
+        int32_t *ps = start.data(), *pf = feat.data();
+        int32_t k = 0;
+        ps[0] = 0;
         for (const auto &kv : fvec) {
-            node.push_back((uint32_t)kv.first);
-            for (auto f : kv.second) feat.push_back((int32_t)f);
-            start.push_back((int32_t)feat.size());
+            *pn++ = (uint32_t)kv.first;
+            for (auto f : kv.second) pf[k++] = (int32_t)f;
+            *++ps = k;
         }
     }
     osg_featvec view() const { return osg_featvec{(int32_t)node.size(), node.data(), start.data(), feat.data()}; }
