@@ -66,6 +66,9 @@ __global__ __launch_bounds__(1024) void k_fp4(float *out, int iters)
             }
             k1 = __int_as_float(j1 - 32); k2 = __int_as_float(j2 - 32);
             k3 = __int_as_float(j3 - 32); k4 = __int_as_float(j4 - 32);
+            // keep every iteration's chain live (r05's first build of this mode let the compiler sink the
+            // chain out of the loop, so it timed the update alone)
+            asm volatile("" : : "v"(acc));
         } else if (MODE == 3 || MODE == 4 || (MODE == 6 && (threadIdx.x >> 6) % 2 == 1)) {
             int j1 = __float_as_int(k1), j2 = __float_as_int(k2), j3 = __float_as_int(k3), j4 = __float_as_int(k4);
 #pragma unroll
