@@ -1385,7 +1385,8 @@ __global__ __launch_bounds__(256) void k_chol_col(const LbaDev *__restrict__ Ds,
 // unchanged.  Its sums are ordered differently from k_chol_col's (one MFMA chain per quadrant
 // instead of four K slices), so the two agree to rounding (OSG_CHOL_DENSE=0 selects the column
 // launches, tests/test_ba_gpu.py compares them).
-constexpr int CD_T = 1024;
+constexpr int CD_T = 1024;  // k_chol_env's workgroup; k_chol_dense takes its own as a template argument
+template <int CD_T, int RING>
 __global__ __launch_bounds__(CD_T) void k_chol_dense(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT);
@@ -1394,6 +1395,8 @@ __global__ __launch_bounds__(CD_T) void k_chol_dense(const LbaDev *__restrict__ 
     __shared__ double s_x[CMAX / CB][CB][CB + 1];
     __shared__ double s_m[CB][CB + 1];
     __shared__ double s_rsq[CB], s_d[CB], s_rhs[CB];
+    __shared__ double s_pq[CD_T / 64][16][17];   // K-slice partial quadrants (the last columns)
+    __shared__ double s_prp[CD_T / 64][16];      // ... and their b_j partials
     struct Lds {
         double (&sG)[CB][CB + 1];
         double (&sM)[CB][CB + 1];
@@ -1405,10 +1408,17 @@ __global__ __launch_bounds__(CD_T) void k_chol_dense(const LbaDev *__restrict__ 
     const int g4 = 4 * (l >> 4);
     for (int j = 0; j < nblk; j++) {
         const int k0 = j * CB, nb = min(CB, n - k0), ntile = nblk - j;
-        const int ntask = 3 + 4 * (ntile - 1);  // the diagonal tile's lower quadrants, the row blocks' quadrants
+        // the diagonal tile's lower quadrants (tasks 0..2) and the row blocks' quadrants; when they are few
+        // (the last columns, K largest), each quadrant's K is split over ks waves whose partial sums are
+        // added in slice order through LDS
+        // OSG_LBA_PROFILE=2: column phases of graph 0 (update | elimination | outputs), k_chol_col's slots
+        unsigned long long *ts = (D.tstamp && tid == 0 && j < 32) ? D.tstamp + 8 * (2 * j) : nullptr;
+        if (ts) ts[0] = wall_clock64();
+        const int ntask = 3 + 4 * (ntile - 1);
+        const int ks = ntask * 4 <= CD_T / 64 ? 4 : (ntask * 2 <= CD_T / 64 ? 2 : 1);
+        const int nst = k0 / 16, sps = (nst + ks - 1) / ks;  // 16-column steps in all, per slice
         for (int e = tid; e < CB * (CB + 1); e += CD_T) (&s_m[0][0])[e] = 0.0;
-        for (int task = w; task < ntask; task += CD_T / 64) {
-            int t, a, b;
+        auto decode = [&](int task, int &t, int &a, int &b) {
             if (task < 3) {
                 t = 0;
                 a = task > 0 ? 1 : 0;
@@ -1418,6 +1428,11 @@ __global__ __launch_bounds__(CD_T) void k_chol_dense(const LbaDev *__restrict__ 
                 a = ((task - 3) >> 1) & 1;
                 b = (task - 3) & 1;
             }
+        };
+        for (int item = w; item < ntask * ks; item += CD_T / 64) {
+            const int task = item / ks, sl = item - task * ks;
+            int t, a, b;
+            decode(task, t, a, b);
             const int R0 = k0 + t * CB + 16 * a, C0 = k0 + 16 * b;  // quadrant rows, columns
             const int ra = R0 + (l & 15), rb = C0 + (l & 15);
             const bool va = ra < n, vb = rb < n;
@@ -1427,9 +1442,11 @@ __global__ __launch_bounds__(CD_T) void k_chol_dense(const LbaDev *__restrict__ 
             const bool rhs = t == 0 && a == b;
             d4 acc = {0.0, 0.0, 0.0, 0.0};
             double rp = 0.0;
-            // one 16-column step per iteration, the next step's operands loading while this one multiplies
-            double2 cur[4], nxt[4], ycur[2], ynxt[2];
-            auto load = [&](int m, double2 (&o)[4], double2 (&yo)[2]) {
+            // a ring of RING 16-column steps in flight: the operand loads run RING - 1 steps ahead of the MFMAs
+            const int s0 = sl * sps, s1 = min(nst, s0 + sps);
+            double2 ring[RING][4], yring[RING][2];
+            auto load = [&](int st, double2 (&o)[4], double2 (&yo)[2]) {
+                const int m = 16 * st;
                 o[0] = *(const double2 *)(pa + m);
                 o[1] = *(const double2 *)(pa + m + 2);
                 o[2] = *(const double2 *)(pb + m);
@@ -1439,26 +1456,37 @@ __global__ __launch_bounds__(CD_T) void k_chol_dense(const LbaDev *__restrict__ 
                     yo[1] = *(const double2 *)(D.x + g4 + m + 2);
                 }
             };
-            if (k0 > 0) load(0, cur, ycur);
-            for (int m = 0; m < k0; m += 16) {
-                if (m + 16 < k0) load(m + 16, nxt, ynxt);
-                const double av[4] = {va ? cur[0].x : 0.0, va ? cur[0].y : 0.0, va ? cur[1].x : 0.0, va ? cur[1].y : 0.0};
-                const double bv[4] = {vb ? cur[2].x : 0.0, vb ? cur[2].y : 0.0, vb ? cur[3].x : 0.0, vb ? cur[3].y : 0.0};
 #pragma unroll
-                for (int i = 0; i < 4; i++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[i], acc, 0, 0, 0);
-                if (rhs) {
-                    const double yv[4] = {ycur[0].x, ycur[0].y, ycur[1].x, ycur[1].y};
+            for (int u = 0; u < RING; u++)
+                if (s0 + u < s1) load(s0 + u, ring[u], yring[u]);
+            for (int st = s0; st < s1; st += RING) {
 #pragma unroll
-                    for (int i = 0; i < 4; i++) rp += av[i] * yv[i];
+                for (int u = 0; u < RING; u++) {
+                    if (st + u >= s1) break;
+                    const double2 *c4 = ring[u];
+                    const double av[4] = {va ? c4[0].x : 0.0, va ? c4[0].y : 0.0, va ? c4[1].x : 0.0, va ? c4[1].y : 0.0};
+                    const double bv[4] = {vb ? c4[2].x : 0.0, vb ? c4[2].y : 0.0, vb ? c4[3].x : 0.0, vb ? c4[3].y : 0.0};
+#pragma unroll
+                    for (int i = 0; i < 4; i++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[i], acc, 0, 0, 0);
+                    if (rhs) {
+                        const double yv[4] = {yring[u][0].x, yring[u][0].y, yring[u][1].x, yring[u][1].y};
+#pragma unroll
+                        for (int i = 0; i < 4; i++) rp += av[i] * yv[i];
+                    }
+                    if (st + u + RING < s1) load(st + u + RING, ring[u], yring[u]);
                 }
-#pragma unroll
-                for (int v = 0; v < 4; v++) cur[v] = nxt[v];
-                ycur[0] = ynxt[0];
-                ycur[1] = ynxt[1];
             }
             if (rhs) {  // the 4 k-groups of a row: lanes l, l ^ 16, l ^ 32, l ^ 48
                 rp += __shfl_xor(rp, 16);
                 rp += __shfl_xor(rp, 32);
+            }
+            if (ks > 1) {  // partial sums, added below in slice order
+#pragma unroll
+                for (int q = 0; q < 4; q++) s_pq[item][(l >> 4) + 4 * q][l & 15] = acc[q];
+                if (rhs && l < 16) s_prp[item][l] = rp;
+                continue;
+            }
+            if (rhs) {
                 const int r = 16 * a + (l & 15);
                 if (l < 16) s_rhs[r] = (k0 + r < n) ? D.bs[k0 + r] - rp : 0.0;
             }
@@ -1474,10 +1502,34 @@ __global__ __launch_bounds__(CD_T) void k_chol_dense(const LbaDev *__restrict__ 
                 if (t == 0 && a == 1 && b == 0) s_x[0][c][r] = 0.0;  // upper quadrant: read, never used
             }
         }
+        if (ks > 1) {
+            __syncthreads();
+            for (int e = tid; e < ntask * 256; e += CD_T) {
+                const int task = e >> 8, r16 = (e >> 4) & 15, c16 = e & 15;
+                int t, a, b;
+                decode(task, t, a, b);
+                double sum = s_pq[task * ks][r16][c16];
+                for (int sl = 1; sl < ks; sl++) sum += s_pq[task * ks + sl][r16][c16];
+                const int r = 16 * a + r16, c = 16 * b + c16, gr = k0 + t * CB + r, gc = k0 + c;
+                double v;
+                if (gr < n && gc < n) v = A[(size_t)gr * n + gc] - sum;
+                else v = (t == 0 && r == c) ? 1.0 : 0.0;
+                s_x[t][r][c] = v;
+                if (t == 0 && a == 1 && b == 0) s_x[0][c][r] = 0.0;
+            }
+            if (tid < CB) {  // rows 0..15: task 0, rows 16..31: task 2
+                const int task = tid < 16 ? 0 : 2, r16 = tid & 15;
+                double sum = s_prp[task * ks][r16];
+                for (int sl = 1; sl < ks; sl++) sum += s_prp[task * ks + sl][r16];
+                s_rhs[tid] = (k0 + tid < n) ? D.bs[k0 + tid] - sum : 0.0;
+            }
+        }
         __syncthreads();
         if (tid < CB) s_m[tid][tid] = 1.0;
         __syncthreads();
+        if (ts) ts[1] = wall_clock64();
         const int ok = chol_factor_diag<true>(L, nb);
+        if (ts) ts[2] = wall_clock64();
         if (tid == 0 && !ok) D.flag[0] = 0;
         for (int e = tid; e < CB * CB; e += CD_T) {
             const int r = e >> 5, c = e & 31;
@@ -1510,6 +1562,7 @@ __global__ __launch_bounds__(CD_T) void k_chol_dense(const LbaDev *__restrict__ 
             }
         }
         __syncthreads();  // L_tj, Linv and y_j of this column before the next column reads them
+        if (ts) ts[3] = wall_clock64();
     }
 }
 
@@ -2806,6 +2859,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     // OSG_CHOL_ENV=1: k_chol_env for narrow-envelope maps (A/B runs; measured slower than the column launches:
     // one workgroup serialises each column's trailing update, which k_chol_trail spreads over the chip)
     static const bool chol_env = getenv("OSG_CHOL_ENV") && atoi(getenv("OSG_CHOL_ENV")) == 1;
+    // OSG_CHOL_DENSE_NT=512: k_chol_dense with 8 waves (256 VGPRs, a 3-step operand ring) instead of 16 (A/B)
+    static const int chol_dense_nt = getenv("OSG_CHOL_DENSE_NT") ? atoi(getenv("OSG_CHOL_DENSE_NT")) : 1024;
     const auto tp0 = std::chrono::steady_clock::now();
     auto ms_since = [&](std::chrono::steady_clock::time_point t) {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
@@ -3127,7 +3182,10 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
             LBA_MARK(KT_CHOL);
             // dense systems (n <= CMAX) in one k_chol_dense workgroup per graph, narrow envelopes in one
             // k_chol_env workgroup (with its backward solve), the others by column launches
-            if (any_dense) hipLaunchKernelGGL(k_chol_dense, yb, dim3(CD_T), 0, ctx->stream, d_dev);
+            if (any_dense) {
+                if (chol_dense_nt == 512) hipLaunchKernelGGL((k_chol_dense<512, 3>), yb, dim3(512), 0, ctx->stream, d_dev);
+                else hipLaunchKernelGGL((k_chol_dense<1024, 2>), yb, dim3(1024), 0, ctx->stream, d_dev);
+            }
             if (any_env) hipLaunchKernelGGL(k_chol_env, yb, dim3(CD_T), 0, ctx->stream, d_dev);
             if (any_col) for (int jb = 0; jb < mx_red; jb++) {  // row blocks at and below the diagonal block
                 // past CMAX only the envelope's rows: grids sized by the largest reach of any graph
