@@ -1283,6 +1283,101 @@ __device__ __forceinline__ int chol_factor_diag(LDS &L, int nb)
     return ok;
 }
 
+// chol_factor_diag four columns per barrier (OSG_CHOL_ELIM=4): the 4 x 4 pivot block P = LP DP LP^T is
+// factored redundantly in every thread (four reciprocals in sequence), a row's block entries B_i become
+// Y_i = B_i LP^-T by forward substitution, and then
+//   G: g_i,jj -= sum_p Y_ip Y_jj,p / d_p                           (c + 3 < jj <= i)
+//   M: m_i,m  -= sum_p Y_ip / d_p M'_p,m,  M'_blk = LP^-1 M_blk     (i > c + 3, m <= c + 3)
+// with the block rows M'_blk written one step later (other threads read M_blk now).  Eight barriers
+// instead of sixteen for a 32-column tile; the same factor to rounding.
+template <bool GUARD = false, class LDS>
+__device__ __forceinline__ int chol_factor_diag4(LDS &L, int nb)
+{
+    const int tid = threadIdx.x;
+    const bool act = !GUARD || tid < 256;
+    const int jj = tid & 31, ib = (tid >> 5) & 7;
+    int ok = 1;
+    double defer_val = 0.0;
+    int defer_at = -1;  // index into sM of the deferred block-row value
+    for (int c = 0; c < nb; c += 4) {
+        if (!act) {
+            __syncthreads();
+            continue;
+        }
+        if (defer_at >= 0) (&L.sM[0][0])[defer_at] = defer_val;
+        defer_at = -1;
+        const double P00 = L.sG[c][c], P10 = L.sG[c + 1][c], P20 = L.sG[c + 2][c], P30 = L.sG[c + 3][c];
+        const double P11 = L.sG[c + 1][c + 1], P21 = L.sG[c + 2][c + 1], P31 = L.sG[c + 3][c + 1];
+        const double P22 = L.sG[c + 2][c + 2], P32 = L.sG[c + 3][c + 2], P33 = L.sG[c + 3][c + 3];
+        const bool gcol = jj > c + 3;
+        double bj[4], gi[4][4], cur[4];
+        if (gcol) {
+#pragma unroll
+            for (int p = 0; p < 4; p++) bj[p] = L.sG[jj][c + p];
+        } else {
+#pragma unroll
+            for (int p = 0; p < 4; p++) bj[p] = L.sM[c + p][jj];
+        }
+        double *const base = gcol ? &L.sG[0][0] : &L.sM[0][0];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int i = ib + 8 * q;
+#pragma unroll
+            for (int p = 0; p < 4; p++) gi[q][p] = L.sG[i][c + p];
+            cur[q] = base[i * (CB + 1) + jj];
+        }
+        // LP DP LP^T of the pivot block
+        const double d0 = P00, r0 = rcp_nr(d0 > 0.0 ? d0 : 1.0);
+        const double l10 = P10 * r0, l20 = P20 * r0, l30 = P30 * r0;
+        const double d1 = P11 - P10 * l10, r1 = rcp_nr(d1 > 0.0 ? d1 : 1.0);
+        const double t21 = P21 - P20 * l10, t31 = P31 - P30 * l10;
+        const double l21 = t21 * r1, l31 = t31 * r1;
+        const double d2 = P22 - P20 * l20 - t21 * l21, r2 = rcp_nr(d2 > 0.0 ? d2 : 1.0);
+        const double t32 = P32 - P30 * l20 - t31 * l21;
+        const double l32 = t32 * r2;
+        const double d3 = P33 - P30 * l30 - t31 * l31 - t32 * l32, r3 = rcp_nr(d3 > 0.0 ? d3 : 1.0);
+        ok &= (d0 > 0.0) & (d1 > 0.0) & (d2 > 0.0) & (d3 > 0.0);
+        if (tid == 0) {
+            L.s_d[c] = d0;
+            L.s_d[c + 1] = d1;
+            L.s_d[c + 2] = d2;
+            L.s_d[c + 3] = d3;
+        }
+        // this column's coefficients: Y_jj / d (G) or M'_blk / d (M), both by forward substitution with LP
+        const double y0 = bj[0], y1 = bj[1] - y0 * l10, y2 = bj[2] - y0 * l20 - y1 * l21;
+        const double y3 = bj[3] - y0 * l30 - y1 * l31 - y2 * l32;
+        const double a0 = y0 * r0, a1 = y1 * r1, a2 = y2 * r2, a3 = y3 * r3;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int i = ib + 8 * q;
+            const double Y0 = gi[q][0], Y1 = gi[q][1] - Y0 * l10, Y2 = gi[q][2] - Y0 * l20 - Y1 * l21;
+            const double Y3 = gi[q][3] - Y0 * l30 - Y1 * l31 - Y2 * l32;
+            const double v = cur[q] - Y0 * a0 - Y1 * a1 - Y2 * a2 - Y3 * a3;
+            if (i < nb && i > c + 3 && (!gcol || jj <= i)) base[i * (CB + 1) + jj] = v;
+            if (!gcol && i >= c && i <= c + 3 && i < nb) {  // block row i of M' (deferred)
+                const int pi = i - c;
+                defer_val = pi == 0 ? y0 : (pi == 1 ? y1 : (pi == 2 ? y2 : y3));
+                defer_at = i * (CB + 1) + jj;
+            }
+        }
+        __syncthreads();
+    }
+    if (act && defer_at >= 0) (&L.sM[0][0])[defer_at] = defer_val;
+    __syncthreads();
+    if (tid < CB) {
+        const double d = L.s_d[tid];
+        L.s_rsq[tid] = (tid < nb && d > 0.0) ? 1.0 / sqrt(d) : 1.0;
+    }
+    __syncthreads();
+    // L_jj^-1 = D^-1/2 M (lower)
+    for (int e = tid; e < CB * CB; e += blockDim.x) {
+        const int i = e >> 5, m = e & 31;
+        L.sM[i][m] = (m <= i) ? L.sM[i][m] * L.s_rsq[i] : 0.0;
+    }
+    __syncthreads();
+    return ok;
+}
+
 // Step 3 of the diagonal role: L_jj^-1 -> Linv, y_j = L_jj^-1 (b_j - sum_m L_jm y_m) -> x
 __device__ __forceinline__ void chol_diag_out(const LbaDev &D, CholLds &L, int k0, int nb, int n, double bj, int ok)
 {
@@ -1336,6 +1431,7 @@ __device__ __forceinline__ void chol_offdiag_out(const LbaDev &D, CholLds &L, in
 //  2. chol_factor_diag: T = Lt D Lt^T, L_jj^-1 = D^-1/2 Lt^-1 without a triangular solve.
 //  3. workgroup 0: chol_diag_out;  workgroup t > 0: chol_offdiag_out.  A_jj itself is never
 //     written (nothing downstream needs L_jj).
+template <int ELIM>
 __global__ __launch_bounds__(256) void k_chol_col(const LbaDev *__restrict__ Ds, int j)
 {
     LBA_GRAPH(M_ACT);
@@ -1365,7 +1461,7 @@ __global__ __launch_bounds__(256) void k_chol_col(const LbaDev *__restrict__ Ds,
     if (tid < CB) L.sM[tid][tid] = 1.0;
     __syncthreads();
     if (ts) ts[1] = wall_clock64();
-    const int ok = chol_factor_diag(L, nb);
+    const int ok = ELIM == 4 ? chol_factor_diag4(L, nb) : chol_factor_diag(L, nb);
     if (ts) ts[2] = wall_clock64();
     if (t == 0) chol_diag_out(D, L, k0, nb, n, bj, ok);
     else chol_offdiag_out(D, L, k0, R0, nb, n);
@@ -1386,7 +1482,7 @@ __global__ __launch_bounds__(256) void k_chol_col(const LbaDev *__restrict__ Ds,
 // instead of four K slices), so the two agree to rounding (OSG_CHOL_DENSE=0 selects the column
 // launches, tests/test_ba_gpu.py compares them).
 constexpr int CD_T = 1024;  // k_chol_env's workgroup; k_chol_dense takes its own as a template argument
-template <int CD_T, int RING>
+template <int CD_T, int RING, int ELIM>
 __global__ __launch_bounds__(CD_T) void k_chol_dense(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT);
@@ -1528,7 +1624,7 @@ __global__ __launch_bounds__(CD_T) void k_chol_dense(const LbaDev *__restrict__ 
         if (tid < CB) s_m[tid][tid] = 1.0;
         __syncthreads();
         if (ts) ts[1] = wall_clock64();
-        const int ok = chol_factor_diag<true>(L, nb);
+        const int ok = ELIM == 4 ? chol_factor_diag4<true>(L, nb) : chol_factor_diag<true>(L, nb);
         if (ts) ts[2] = wall_clock64();
         if (tid == 0 && !ok) D.flag[0] = 0;
         for (int e = tid; e < CB * CB; e += CD_T) {
@@ -1579,6 +1675,7 @@ __global__ __launch_bounds__(CD_T) void k_chol_dense(const LbaDev *__restrict__ 
 // theirs bit for bit; the backward solve is k_chol_back_large's, with x in the tiles' LDS.
 constexpr int ENV_T = 16;                       // staged tiles: the diagonal + up to 15 envelope rows
 constexpr int ENV_NX = ENV_T * CB * (CB + 1);   // x of the backward solve in the same LDS (16 896)
+template <int ELIM>
 __global__ __launch_bounds__(CD_T) void k_chol_env(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT);
@@ -1616,7 +1713,7 @@ __global__ __launch_bounds__(CD_T) void k_chol_env(const LbaDev *__restrict__ Ds
         if (tid < CB) s_m[tid][tid] = 1.0;
         __syncthreads();
         // 2.
-        const int ok = chol_factor_diag<true>(L, nb);
+        const int ok = ELIM == 4 ? chol_factor_diag4<true>(L, nb) : chol_factor_diag<true>(L, nb);
         if (tid == 0 && !ok) D.flag[0] = 0;
         for (int e = tid; e < CB * CB; e += CD_T) {
             const int r = e >> 5, c = e & 31;
@@ -2861,6 +2958,11 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     static const bool chol_env = getenv("OSG_CHOL_ENV") && atoi(getenv("OSG_CHOL_ENV")) == 1;
     // OSG_CHOL_DENSE_NT=512: k_chol_dense with 8 waves (256 VGPRs, a 3-step operand ring) instead of 16 (A/B)
     static const int chol_dense_nt = getenv("OSG_CHOL_DENSE_NT") ? atoi(getenv("OSG_CHOL_DENSE_NT")) : 1024;
+    // the column launches' (and k_chol_env's) diagonal tiles eliminated four columns per barrier
+    // (chol_factor_diag4: 7.3-8.0 against 9.0 us per tile, global_ba_map +6 %); OSG_CHOL_ELIM=2 for the
+    // two-column form.  k_chol_dense keeps two: in its 1024-thread workgroup the four-column form spills
+    // (20-26 us per tile, gpurun_out/elim4).
+    static const int chol_elim = getenv("OSG_CHOL_ELIM") ? atoi(getenv("OSG_CHOL_ELIM")) : 4;
     const auto tp0 = std::chrono::steady_clock::now();
     auto ms_since = [&](std::chrono::steady_clock::time_point t) {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
@@ -3183,10 +3285,13 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
             // dense systems (n <= CMAX) in one k_chol_dense workgroup per graph, narrow envelopes in one
             // k_chol_env workgroup (with its backward solve), the others by column launches
             if (any_dense) {
-                if (chol_dense_nt == 512) hipLaunchKernelGGL((k_chol_dense<512, 3>), yb, dim3(512), 0, ctx->stream, d_dev);
-                else hipLaunchKernelGGL((k_chol_dense<1024, 2>), yb, dim3(1024), 0, ctx->stream, d_dev);
+                if (chol_dense_nt == 512) hipLaunchKernelGGL((k_chol_dense<512, 3, 2>), yb, dim3(512), 0, ctx->stream, d_dev);
+                else hipLaunchKernelGGL((k_chol_dense<1024, 2, 2>), yb, dim3(1024), 0, ctx->stream, d_dev);
             }
-            if (any_env) hipLaunchKernelGGL(k_chol_env, yb, dim3(CD_T), 0, ctx->stream, d_dev);
+            if (any_env) {
+                if (chol_elim == 4) hipLaunchKernelGGL(k_chol_env<4>, yb, dim3(CD_T), 0, ctx->stream, d_dev);
+                else hipLaunchKernelGGL(k_chol_env<2>, yb, dim3(CD_T), 0, ctx->stream, d_dev);
+            }
             if (any_col) for (int jb = 0; jb < mx_red; jb++) {  // row blocks at and below the diagonal block
                 // past CMAX only the envelope's rows: grids sized by the largest reach of any graph
                 int rows = 0, m = 0;
@@ -3200,7 +3305,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
                     if (big) m = std::max(m, nr);
                 }
                 if (rows == 0) continue;
-                hipLaunchKernelGGL(k_chol_col, gx(rows), dim3(256), 0, ctx->stream, d_dev, jb);
+                if (chol_elim == 4) hipLaunchKernelGGL(k_chol_col<4>, gx(rows), dim3(256), 0, ctx->stream, d_dev, jb);
+                else hipLaunchKernelGGL(k_chol_col<2>, gx(rows), dim3(256), 0, ctx->stream, d_dev, jb);
                 if (large && m > 0)
                     hipLaunchKernelGGL(k_chol_trail, gx(m * (m + 1) / 2), dim3(256), 0, ctx->stream, d_dev, jb);
             }

@@ -303,12 +303,20 @@ def test_lba_chol_fused_vs_column_launches(ctx):
       LL^T with its sums in another order, so identical iteration / trial counts and states equal to rounding;
     * k_chol_env (OSG_CHOL_ENV=1: maps past CMAX with narrow envelopes, its own backward solve) against the
       default column launches: the same products in the same order as k_chol_col / k_chol_trail /
-      k_chol_back_large, so bit-identical."""
+      k_chol_back_large, so bit-identical;
+    * the column launches with the two-column elimination (OSG_CHOL_ELIM=2) against the default four."""
     o = op.Optimizer(ctx)
     lba = o.LocalBundleAdjustmentBatch(_lba_batch_graphs())
     maps = [o.BundleAdjustment(G) for G in _env_map_graphs()]
     col = _chol_child({"OSG_CHOL_DENSE": "0"})
     env = _chol_child({"OSG_CHOL_ENV": "1"})
+    two = _chol_child({"OSG_CHOL_ELIM": "2"})
+    # the column launches' diagonal tiles eliminated two columns per barrier instead of four: the same
+    # factor to rounding
+    np.testing.assert_array_equal(two["it"], [[r.iterations, r.trials] for r in lba + maps])
+    for i, r in enumerate(lba + maps):
+        np.testing.assert_allclose(two[f"p{i}"], r.pose, atol=1e-8, rtol=0)
+        np.testing.assert_allclose(two[f"q{i}"], r.point, atol=1e-8, rtol=0)
     for got in (col, env):
         np.testing.assert_array_equal(got["it"], [[r.iterations, r.trials] for r in lba + maps])
     np.testing.assert_allclose(col["chi"][:len(lba)], [[r.chi2_initial, r.chi2_final] for r in lba], rtol=1e-12, atol=0)
