@@ -399,6 +399,13 @@ __global__ __launch_bounds__(NW * 64) void k_top2_fp4(const uint32_t *__restrict
     // pairs per query (accumulator elements 0-7 and 8-15)
     i32x8 bq[QT][4];
     int ka1[QT], ka2[QT], kb1[QT], kb2[QT];
+    // PIPE == 3 (the default shape): one running top-2 pair per query (both accumulator halves into ka):
+    // two fewer rebasing subtractions per tile and no merge of the halves, a longer dependent chain per
+    // lane; 852 -> 841 VALU ops, +1.8 % on the headline step (profiles/r05_top2_fp4_onechain.jsonl).
+    // The two-pair form stays as OSG_TOP2_MFMA_SHAPE=7.
+    constexpr bool ONE = PIPE == 3;
+    int(&kc1)[QT] = ONE ? ka1 : kb1;
+    int(&kc2)[QT] = ONE ? ka2 : kb2;
     int pq[QT];
 #pragma unroll
     for (int j = 0; j < QT; j++) {
@@ -465,12 +472,14 @@ __global__ __launch_bounds__(NW * 64) void k_top2_fp4(const uint32_t *__restrict
 #pragma unroll
             for (int i = 0; i < 8; i += 2) {
                 key_push2(ka1[j], ka2[j], __float_as_int(acc[j][i]), __float_as_int(acc[j][i + 1]));
-                key_push2(kb1[j], kb2[j], __float_as_int(acc[j][i + 8]), __float_as_int(acc[j][i + 9]));
+                key_push2(kc1[j], kc2[j], __float_as_int(acc[j][i + 8]), __float_as_int(acc[j][i + 9]));
             }
             ka1[j] -= 32;
             ka2[j] -= 32;
-            kb1[j] -= 32;
-            kb2[j] -= 32;
+            if (!ONE) {
+                kb1[j] -= 32;
+                kb2[j] -= 32;
+            }
         }
     };
     auto tile = [&](const unsigned char *tb, const f32x16 &cin) {
@@ -543,14 +552,16 @@ __global__ __launch_bounds__(NW * 64) void k_top2_fp4(const uint32_t *__restrict
                                 // pairs 2 s (chain A: elements 4 s, 4 s + 1 ... ) and 2 s + 1 (chain B)
                                 key_push2(ka1[j], ka2[j], __float_as_int(accp[j][2 * s]),
                                           __float_as_int(accp[j][2 * s + 1]));
-                                key_push2(kb1[j], kb2[j], __float_as_int(accp[j][8 + 2 * s]),
+                                key_push2(kc1[j], kc2[j], __float_as_int(accp[j][8 + 2 * s]),
                                           __float_as_int(accp[j][9 + 2 * s]));
                             }
                             if (s == 3) {
                                 ka1[j] -= 32;
                                 ka2[j] -= 32;
-                                kb1[j] -= 32;
-                                kb2[j] -= 32;
+                                if (!ONE) {
+                                    kb1[j] -= 32;
+                                    kb2[j] -= 32;
+                                }
                             }
                         }
                         __builtin_amdgcn_sched_barrier(0);
@@ -583,7 +594,7 @@ __global__ __launch_bounds__(NW * 64) void k_top2_fp4(const uint32_t *__restrict
 #pragma unroll
     for (int j = 0; j < QT; j++) {
         int k1 = ka1[j], k2 = ka2[j];
-        key_merge(k1, k2, kb1[j], kb2[j]);
+        if (!ONE) key_merge(k1, k2, kb1[j], kb2[j]);
         const int a1 = __shfl_xor(k1, 32), a2 = __shfl_xor(k2, 32);
         key_merge(k1, k2, a1, a2);
         const int q = qw0 + 32 * j + r;
@@ -643,9 +654,9 @@ bool mfma_fp4()
 void mfma_shape_of(bool fp4, int shape, int *d)
 {
     static const int i8[5][4] = {{16, 1, 256, 1}, {8, 2, 256, 1}, {16, 1, 256, 0}, {8, 2, 256, 0}, {8, 1, 256, 1}};
-    static const int f4[7][4] = {{16, 1, 256, 1}, {8, 2, 256, 1}, {16, 1, 256, 0}, {16, 1, 256, 1}, {8, 1, 256, 1},
-                                 {16, 2, 256, 1}, {16, 1, 256, 2}};
-    const int *s = fp4 ? f4[(shape >= 1 && shape <= 6 && shape != 3) ? shape : 0]
+    static const int f4[8][4] = {{16, 1, 256, 3}, {8, 2, 256, 1}, {16, 1, 256, 0}, {16, 1, 256, 3}, {8, 1, 256, 1},
+                                 {16, 2, 256, 1}, {16, 1, 256, 2}, {16, 1, 256, 1}};
+    const int *s = fp4 ? f4[(shape >= 1 && shape <= 7 && shape != 3) ? shape : 0]
                        : i8[(shape >= 1 && shape <= 4) ? shape : 0];
     for (int i = 0; i < 4; i++) d[i] = s[i];
 }
@@ -680,7 +691,8 @@ int osg_launch_top2_batch_mfma(osg_ctx *ctx, const void *d_query, int32_t nq, co
         case 4: return launch_fp4<8, 1, 256, 1>(ctx, d_query, nq, d_train, nt, nb, d_out);
         case 5: return launch_fp4<16, 2, 256, 1>(ctx, d_query, nq, d_train, nt, nb, d_out);
         case 6: return launch_fp4<16, 1, 256, 2>(ctx, d_query, nq, d_train, nt, nb, d_out);
-        default: return launch_fp4<16, 1, 256, 1>(ctx, d_query, nq, d_train, nt, nb, d_out);
+        case 7: return launch_fp4<16, 1, 256, 1>(ctx, d_query, nq, d_train, nt, nb, d_out);
+        default: return launch_fp4<16, 1, 256, 3>(ctx, d_query, nq, d_train, nt, nb, d_out);
         }
     }
     switch (shape) {

@@ -291,6 +291,41 @@ __device__ inline double seq_sum(double acc, const double *row, int cnt)
     return acc;
 }
 
+// sum of m >= 1 whole 64-entry LDS rows (row w at row0 + w * stride), in order, onto acc.  A row past
+// its chunk's last edge holds +0.0 (every lane writes its slot, zero when it has no active edge), and
+// adding +0.0 leaves acc unchanged (acc starts at +0.0, so it is never -0.0): summing rows whole is the
+// same chain as summing cnt entries.  The next 16 entries are always in flight: a block's loads are
+// issued before the previous block's adds (the scheduling barriers keep the compiler from sinking them
+// below the adds, which it did to seq_sum: every 16 adds then waited out a whole LDS round trip), and a
+// row's last block loads the next row's first.  The last row's look-ahead re-reads that row, unused.
+__device__ inline double seq_sum_rows(double acc, const double *row0, int stride, int m)
+{
+    const double2 *r = (const double2 *)row0;
+    double2 cur[8], nxt[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) cur[u] = r[u];
+    for (int w = 0; w < m; w++) {
+        const double2 *nr = (const double2 *)(row0 + (size_t)min(w + 1, m - 1) * stride);
+#pragma unroll
+        for (int blk = 0; blk < 4; blk++) {
+            const double2 *src = blk < 3 ? r + 8 * (blk + 1) : nr;
+#pragma unroll
+            for (int u = 0; u < 8; u++) nxt[u] = src[u];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                acc += cur[u].x;
+                acc += cur[u].y;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 8; u++) cur[u] = nxt[u];
+        }
+        r = nr;
+    }
+    return acc;
+}
+
 // frame constants and the cross-wave results (written by one wave, read by all after a barrier)
 struct PoseShared {
     osg_camera cam, cam2;
@@ -311,7 +346,9 @@ struct PoseWave {
 // wave w); the waves fill their LDS tiles in parallel, then wave 0 adds the tiles in edge order.
 // Outlier flags live in a register bitmask per lane (bit s <-> edge (s*NW+wave)*64+lane) and are
 // stored once at the end.
-template <int NW>
+// ROWSUM: the edge-order sums over whole rows with the loads kept ahead (seq_sum_rows); false is the
+// previous per-chunk seq_sum (OSG_POSE_ROWSUM=0, A/B runs; the same add chain, bit-identical)
+template <int NW, bool ROWSUM>
 __global__ __launch_bounds__(NW *PW) void k_pose_opt(const PoseProbDev *__restrict__ probs,
                                                      const int8_t *__restrict__ e_kind,
                                                      const double *__restrict__ e_xw,
@@ -375,6 +412,8 @@ __global__ __launch_bounds__(NW *PW) void k_pose_opt(const PoseProbDev *__restri
     auto active = [&](int s) { return edge_of(s) < n && !((om >> s) & 1); };
     // the edges of chunk w of superchunk s that exist
     auto chunk_cnt = [&](int s, int w) { return min(PW, n - (s * NW + w) * PW); };
+    // the chunks of superchunk s that exist (>= 1 for s < nsc)
+    auto n_rows = [&](int s) { return min(NW, (n - s * NW * PW + PW - 1) / PW); };
 
     // activeRobustChi2 at T, summed in edge order by wave 0 lane 0, broadcast through S.chi
     auto chi_pass = [&](const SE3 &T) -> double {
@@ -400,8 +439,11 @@ __global__ __launch_bounds__(NW *PW) void k_pose_opt(const PoseProbDev *__restri
             PROF_ADD(6, t_pc);
             __syncthreads();
             PROF_T(t_ps);
-            if (threadIdx.x == 0)
-                for (int w = 0; w < NW && chunk_cnt(s, w) > 0; w++) acc = seq_sum(acc, s_t + w * NT * ROW, chunk_cnt(s, w));
+            if (threadIdx.x == 0) {
+                if (ROWSUM) acc = seq_sum_rows(acc, s_t, NT * ROW, n_rows(s));
+                else
+                    for (int w = 0; w < NW && chunk_cnt(s, w) > 0; w++) acc = seq_sum(acc, s_t + w * NT * ROW, chunk_cnt(s, w));
+            }
             PROF_ADD(7, t_ps);
             __syncthreads();
         }
@@ -469,8 +511,10 @@ __global__ __launch_bounds__(NW *PW) void k_pose_opt(const PoseProbDev *__restri
             __syncthreads();
             if (wave == 0) {  // lane q < 28 adds stream q; the others repeat stream 27, unused
                 const int q = lane < NT ? lane : NT - 1;
-                for (int w = 0; w < NW && chunk_cnt(s, w) > 0; w++)
-                    acc = seq_sum(acc, s_t + (w * NT + q) * ROW, chunk_cnt(s, w));
+                if (ROWSUM) acc = seq_sum_rows(acc, s_t + q * ROW, NT * ROW, n_rows(s));
+                else
+                    for (int w = 0; w < NW && chunk_cnt(s, w) > 0; w++)
+                        acc = seq_sum(acc, s_t + (w * NT + q) * ROW, chunk_cnt(s, w));
             }
             __syncthreads();
         }
@@ -706,8 +750,15 @@ int osg_pose_optimization_batch(osg_ctx *ctx, const osg_pose_problem *p, int32_t
     const float *a4 = (const float *)(din + o_isig);
     uint8_t *a5 = (uint8_t *)(dio + o_outl);
     PoseOut *a6 = (PoseOut *)(dio + o_res);
-#define OSG_POSE_LAUNCH(W_) \
-    hipLaunchKernelGGL(k_pose_opt<W_>, dim3(nb), dim3(W_ * PW), 0, ctx->stream, a0, a1, a2, a3, a4, a5, a6)
+    const char *rs = getenv("OSG_POSE_ROWSUM");  // tests pin the variant
+    const bool rowsum = !(rs && atoi(rs) == 0);
+#define OSG_POSE_LAUNCH(W_)                                                                                    \
+    if (rowsum)                                                                                                \
+        hipLaunchKernelGGL((k_pose_opt<W_, true>), dim3(nb), dim3(W_ * PW), 0, ctx->stream, a0, a1, a2, a3, a4, a5, \
+                           a6);                                                                                \
+    else                                                                                                       \
+        hipLaunchKernelGGL((k_pose_opt<W_, false>), dim3(nb), dim3(W_ * PW), 0, ctx->stream, a0, a1, a2, a3, a4, \
+                           a5, a6)
     switch (nw) {
     case 1: OSG_POSE_LAUNCH(1); break;
     case 2: OSG_POSE_LAUNCH(2); break;

@@ -80,6 +80,20 @@ def test_pose_optimization_batch(ctx, oracle, monkeypatch, nw):
     assert_pose_equal(got, ref)
 
 
+@pytest.mark.parametrize("rowsum", ["0", "1"])
+@pytest.mark.parametrize("nw", ["1", "8"])
+def test_pose_optimization_rowsum_variants(ctx, oracle, monkeypatch, nw, rowsum):
+    """The edge-order sums over whole zero-padded rows (default) and the per-chunk sums
+    (OSG_POSE_ROWSUM=0): the same add chain, both bit-exact against the oracle, ragged last chunks."""
+    monkeypatch.setenv("OSG_POSE_NW", nw)
+    monkeypatch.setenv("OSG_POSE_ROWSUM", rowsum)
+    rng = np.random.default_rng(16)
+    probs = [op.synth_pose_problem(rng, n_edges=n, stereo_frac=0.4) for n in (3, 63, 64, 65, 191, 318, 513, 1100)]
+    assert_pose_equal(op.Optimizer(ctx).PoseOptimization(probs), oc.pose(oracle, probs))
+    for p in probs[-3:]:  # lone frames: the multi-wave layout the drop-in's one-frame call takes
+        assert_pose_equal([op.Optimizer(ctx).PoseOptimization(p)], oc.pose(oracle, [p]))
+
+
 @pytest.mark.parametrize("n_edges", [64, 65, 127, 129, 1000, 2500])
 def test_pose_optimization_single_frame_sizes(ctx, oracle, n_edges):
     """The drop-in's one-frame call (multi-wave variant) across chunk boundaries and large frames."""
