@@ -445,7 +445,7 @@ __global__ __launch_bounds__(NW *PW) void k_pose_opt(const PoseProbDev *__restri
                     for (int w = 0; w < NW && chunk_cnt(s, w) > 0; w++) acc = seq_sum(acc, s_t + w * NT * ROW, chunk_cnt(s, w));
             }
             PROF_ADD(7, t_ps);
-            __syncthreads();
+            if (s + 1 < nsc) __syncthreads();  // the last superchunk's tiles are next written after the barrier below
         }
         if (threadIdx.x == 0) S.chi = acc;
         __syncthreads();
@@ -516,7 +516,7 @@ __global__ __launch_bounds__(NW *PW) void k_pose_opt(const PoseProbDev *__restri
                     for (int w = 0; w < NW && chunk_cnt(s, w) > 0; w++)
                         acc = seq_sum(acc, s_t + (w * NT + q) * ROW, chunk_cnt(s, w));
             }
-            __syncthreads();
+            if (s + 1 < nsc) __syncthreads();  // as in chi_pass
         }
         if (wave == 0 && lane < NT) dst[lane] = acc;
         __syncthreads();
