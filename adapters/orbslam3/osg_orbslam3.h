@@ -1359,21 +1359,30 @@ struct PoseGather {
     {
         const int N = pFrame->N;
         p = osg_pose_problem{};
-        kind.clear();
-        xw.clear();
-        obs.clear();
-        isig.clear();
-        slot.clear();
+        // sized for every keypoint, written in place, trimmed to the edges found (push_back per edge
+        // measured slower)
+        kind.resize(N);
+        xw.resize(3 * (size_t)N);
+        obs.resize(3 * (size_t)N);
+        isig.resize(N);
+        slot.resize(N);
+        int m = 0;
         const bool two = (bool)pFrame->mpCamera2;
         std::unique_lock<MutexT> gather_lock;
         if (gather_mutex) gather_lock = std::unique_lock<MutexT>(*gather_mutex);
+        constexpr int PF = 8;  // world_pos reads scattered heap MapPoints: fetch a few ahead (two lines each)
         for (int i = 0; i < N; i++) {
+            if (i + PF < N)
+                if (const auto *q = pFrame->mvpMapPoints[i + PF]) {
+                    __builtin_prefetch(q);
+                    __builtin_prefetch((const char *)q + 64);
+                }
             auto *pMP = pFrame->mvpMapPoints[i];
             if (!pMP) continue;
-            double X[3];
+            double *X = &xw[3 * (size_t)m], *o = &obs[3 * (size_t)m];
             H::world_pos(pMP, X);
             int8_t k;
-            double o[3] = {0, 0, 0};
+            o[0] = o[1] = o[2] = 0.0;
             int oct;
             if (!two) {
                 const auto &kp = pFrame->mvKeysUn[i];
@@ -1396,12 +1405,16 @@ struct PoseGather {
                 oct = kp.octave;
             }
             pFrame->mvbOutlier[i] = false;
-            kind.push_back(k);
-            xw.insert(xw.end(), X, X + 3);
-            obs.insert(obs.end(), o, o + 3);
-            isig.push_back(pFrame->mvInvLevelSigma2[oct]);
-            slot.push_back(i);
+            kind[m] = k;
+            isig[m] = pFrame->mvInvLevelSigma2[oct];
+            slot[m] = i;
+            m++;
         }
+        kind.resize(m);
+        xw.resize(3 * (size_t)m);
+        obs.resize(3 * (size_t)m);
+        isig.resize(m);
+        slot.resize(m);
         if (gather_lock.owns_lock()) gather_lock.unlock();  // ref:src/Optimizer.cc:286, end of Step 3
         H::pose(*pFrame, p.pose);
         p.n_edges = (int32_t)kind.size();
