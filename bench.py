@@ -303,7 +303,7 @@ def main():
             "cycles_per_valu_inst_pmc": None if vk is None else round(vk["cycles_per_valu_inst"], 3),
             "valu_pmc_source": None if vk is None else os.path.relpath(args.valu_pmc, ROOT),
         }
-    tr = pmc_traffic(args.traffic, ksub)
+    tr = pmc_traffic_instance(args.traffic, kname) if ksub != "k_top2_batch" else pmc_traffic(args.traffic, ksub)
     roofline.update({
         "traffic": None if tr is None else round(tr[0]),
         "traffic_source": None if tr is None else f"{os.path.relpath(args.traffic, ROOT)}: {tr[1]}",
@@ -552,6 +552,21 @@ def pmc_traffic(path, kernel_substr):
             if best is None or v["launches_fetch_pass"] > best[1]["launches_fetch_pass"]:
                 best = (key, v)
     return None if best is None else (best[1]["traffic_bytes"], best[0])
+
+
+def pmc_traffic_instance(path, kname):
+    """pmc_traffic of the exact template instance `kname` ("k_top2_fp4<16,1,256,3>") when a pass for it
+    exists, else of any instance of its kernel."""
+    try:
+        data = json.load(open(path))
+    except (OSError, ValueError):
+        data = {}
+    kname = kname.split(" ")[0]  # the plan string carries " grid=..." after the instance
+    want = kname
+    for key, v in data.get("kernels", {}).items():
+        if want in key.split("|")[0].replace(" ", "") and v.get("traffic_bytes") is not None:
+            return pmc_traffic(path, key.split("|")[0])
+    return pmc_traffic(path, kname.split("<")[0])
 
 
 def bench_lba(ctx, rank, world, dist, dev, args):
