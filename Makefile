@@ -34,7 +34,7 @@ $(OBJDIR)/match.o: $(CSRC)/match.hip $(HDRS) $(CSRC)/match_common.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(EXACT) -c $< -o $@
 $(OBJDIR)/pose.o: $(CSRC)/pose.hip $(HDRS) $(CSRC)/ba_common.h $(CSRC)/exact_math.h $(CSRC)/glibc_math.h $(CSRC)/match_common.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(EXACT) -c $< -o $@
-$(OBJDIR)/ba.o: $(CSRC)/ba.hip $(HDRS) $(CSRC)/ba_common.h $(CSRC)/exact_math.h $(CSRC)/glibc_math.h | $(OBJDIR)
+$(OBJDIR)/ba.o: $(CSRC)/ba.hip $(HDRS) $(CSRC)/ba_common.h $(CSRC)/exact_math.h $(CSRC)/glibc_math.h $(CSRC)/match_common.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 $(OBJDIR)/dbow.o: $(CSRC)/dbow.hip $(HDRS) include/osg_dbow.h $(CSRC)/match_common.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(EXACT) -c $< -o $@

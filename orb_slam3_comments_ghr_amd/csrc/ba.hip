@@ -3110,7 +3110,6 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     bool any_env = false;    // ... by k_chol_env (past CMAX, a narrow envelope)
     bool any_col = false;    // ... by column launches (the others)
     bool huge_col = false;   // ... and past CMAX_LARGE (k_back_step)
-    bool huge = false;   // ... past CMAX_LARGE (k_back_step instead of k_chol_back_large)
     for (int a = 0; a < NA; a++) {
         const LbaHost &h = H[act[a]];
         const InOff &o = io[a];
@@ -3138,7 +3137,6 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         D.hub_mono = h.G->huber_mono > 0.f ? h.G->huber_mono : (float)std::sqrt(5.991);   // thHuberMono
         D.hub_stereo = h.G->huber_stereo > 0.f ? h.G->huber_stereo : (float)std::sqrt(7.815);
         large |= 6 * h.nhp > CMAX;
-        huge |= 6 * h.nhp > CMAX_LARGE;
         if (chol_dense && h.nhp > 0 && 6 * h.nhp <= CMAX) D.chol_fused = 1;
         else if (chol_env && 6 * h.nhp > CMAX && 6 * h.nhp <= ENV_NX && h.max_col_rows <= ENV_T - 1) D.chol_fused = 2;
         any_dense |= D.chol_fused == 1;

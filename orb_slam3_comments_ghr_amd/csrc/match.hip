@@ -1925,14 +1925,6 @@ int prep_bow_kf_f(osg_ctx *ctx, Problem &P, osg_packer &pk, const osg_bow_side *
     for (int i = 0; i < f->n; i++) out_mp[i] = -1;
     if (bow_queries(kf, f, false, P.q_feat, P.q_cb, P.q_ce) < 0) return osg_set_error(ctx, OSG_E_INVALID, "feature index");
     const int n = (int)P.q_feat.size();
-    P.qdesc.resize((size_t)n * 32);
-    P.q_mp.resize(n);
-    P.q_angle.resize(n);
-    for (int i = 0; i < n; i++) {
-        std::memcpy(&P.qdesc[(size_t)i * 32], kf->desc + (size_t)P.q_feat[i] * 32, 32);
-        P.q_mp[i] = kf->mp_id[P.q_feat[i]];
-        P.q_angle[i] = kf->angle[P.q_feat[i]];
-    }
     MatchArgs &A = P.A;
     A.nq = n;
     A.n_slots = f->n;
@@ -1944,9 +1936,11 @@ int prep_bow_kf_f(osg_ctx *ctx, Problem &P, osg_packer &pk, const osg_bow_side *
     if (n == 0) return OSG_OK;
     set_off(A.fdesc, pk.add(f->desc, (size_t)f->n * 32));
     set_off(A.slot_angle, pk.add(f->angle, sizeof(float) * f->n));
-    set_off(A.qdesc, pk.add(P.qdesc.data(), P.qdesc.size()));
-    set_off(A.q_mp, pk.add(P.q_mp.data(), sizeof(int32_t) * n));
-    set_off(A.q_angle, pk.add(P.q_angle.data(), sizeof(float) * n));
+    // the queries' descriptor rows, MapPoint ids and angles are gathered from the KeyFrame's arrays
+    // straight into the pinned block (P.q_feat lives until the fill)
+    set_off(A.qdesc, pk.add_rows(kf->desc, P.q_feat.data(), n, 32));
+    set_off(A.q_mp, pk.add_rows(kf->mp_id, P.q_feat.data(), n, sizeof(int32_t)));
+    set_off(A.q_angle, pk.add_rows(kf->angle, P.q_feat.data(), n, sizeof(float)));
     set_off(A.q_cb, pk.add(P.q_cb.data(), sizeof(int32_t) * n));
     set_off(A.q_ce, pk.add(P.q_ce.data(), sizeof(int32_t) * n));
     set_off(A.cand_list, pk.add(f->fv.feat, sizeof(int32_t) * f->fv.node_start[f->fv.n_nodes]));
@@ -1970,13 +1964,7 @@ int prep_bow_kf_kf(osg_ctx *ctx, Problem &P, osg_packer &pk, const osg_bow_side 
     for (int i = 0; i < kf1->n; i++) out_mp12[i] = -1;
     if (bow_queries(kf1, kf2, true, P.q_feat, P.q_cb, P.q_ce) < 0) return osg_set_error(ctx, OSG_E_INVALID, "feature index");
     const int n = (int)P.q_feat.size();
-    P.qdesc.resize((size_t)n * 32);
-    P.q_angle.resize(n);
     P.slot_ok.resize(kf2->n);
-    for (int i = 0; i < n; i++) {
-        std::memcpy(&P.qdesc[(size_t)i * 32], kf1->desc + (size_t)P.q_feat[i] * 32, 32);
-        P.q_angle[i] = kf1->angle[P.q_feat[i]];
-    }
     // right-camera keypoints of a two-camera KF2 are skipped (ref:src/ORBmatcher.cc:953-955)
     for (int s = 0; s < kf2->n; s++)
         P.slot_ok[s] = (kf2->mp_id[s] >= 0 && kf2->mp_good[s] && (kf2->nleft == -1 || s < kf2->nleft)) ? 1 : 0;
@@ -1992,8 +1980,9 @@ int prep_bow_kf_kf(osg_ctx *ctx, Problem &P, osg_packer &pk, const osg_bow_side 
     set_off(A.slot_angle, pk.add(kf2->angle, sizeof(float) * kf2->n));
     set_off(A.slot_mp2, pk.add(kf2->mp_id, sizeof(int32_t) * kf2->n));
     set_off(A.slot_ok, pk.add(P.slot_ok.data(), P.slot_ok.size()));
-    set_off(A.qdesc, pk.add(P.qdesc.data(), P.qdesc.size()));
-    set_off(A.q_angle, pk.add(P.q_angle.data(), sizeof(float) * n));
+    // KF1's query rows and angles gathered straight into the pinned block (as prep_bow_kf_f)
+    set_off(A.qdesc, pk.add_rows(kf1->desc, P.q_feat.data(), n, 32));
+    set_off(A.q_angle, pk.add_rows(kf1->angle, P.q_feat.data(), n, sizeof(float)));
     set_off(A.q_cb, pk.add(P.q_cb.data(), sizeof(int32_t) * n));
     set_off(A.q_ce, pk.add(P.q_ce.data(), sizeof(int32_t) * n));
     set_off(A.cand_list, pk.add(kf2->fv.feat, sizeof(int32_t) * kf2->fv.node_start[kf2->fv.n_nodes]));

@@ -35,6 +35,30 @@ def harness(tmp_path_factory):
     return lib
 
 
+@pytest.fixture(scope="module")
+def packer(tmp_path_factory):
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    out = str(tmp_path_factory.mktemp("pk") / "libpacker_check.so")
+    cmd = [hipcc, "--offload-arch=gfx950", "-O2", "-shared", "-fPIC", os.path.join(ROOT, "tools/micro/packer_check.hip"),
+           "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(LIBDIR, "csrc"), "-L" + LIBDIR, "-lorbslam3_amd",
+           "-Wl,-rpath," + LIBDIR, "-o", out]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lib = C.CDLL(out)
+    lib.packer_check.restype = C.c_int
+    lib.packer_check.argtypes = [C.c_uint, C.c_int, C.c_int]
+    return lib
+
+
+@pytest.mark.parametrize("seed,n_items,threads", [(1, 3, 1), (2, 12, 4), (3, 40, 8), (4, 25, 16)])
+def test_packer_row_gathers(packer, seed, n_items, threads):
+    """The matcher's pinned-block packer: row-gather items (SearchByBoW's query rows) and plain items, by
+    fill() and by fill_parallel()'s 4 MiB pieces (rows split across pieces), equal a reference pack."""
+    assert packer.packer_check(seed, n_items, threads) == 0
+
+
 @pytest.mark.parametrize("threads,loops,n", [(1, 500, 1), (1, 500, 37), (8, 300, 5), (8, 100, 1000), (24, 100, 33)])
 def test_worker_pool_concurrent_callers(harness, threads, loops, n):
     assert harness.pool_stress(threads, loops, n) == 0
