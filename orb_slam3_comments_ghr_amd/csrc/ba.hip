@@ -2101,8 +2101,12 @@ __global__ __launch_bounds__(EB) void k_back_copy(const LbaDev *__restrict__ Ds)
 // LDS in UB-block pieces read with coalesced 16-byte loads; measured slower (2.34 against 2.08 ms per
 // 14 launches of 64 C4 windows, profiles/r04_lba_dinv_ab.txt): the pieces serialise load, barrier
 // and compute, where the per-thread walks keep more loads in flight.
+// COOP (the default; OSG_UPDATE_COOP=0 for the walks, bit-identical): one thread per block, EB consecutive blocks of the
+// workgroup's landmarks at a time (coalesced 144-byte blocks, no LDS copy of them): each thread forms its
+// block's Hplᵀ(−x_p) in registers and leaves the 3 values in LDS, then each landmark's thread adds its
+// blocks' values in block order, the per-thread walk's sums.
 constexpr int UB = 256;  // blocks per staged piece: 36 KiB of LDS
-template <bool STAGE>
+template <bool STAGE, bool COOP = false>
 __global__ __launch_bounds__(EB) void k_update(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT);
@@ -2145,9 +2149,33 @@ __global__ __launch_bounds__(EB) void k_update(const LbaDev *__restrict__ Ds)
             __syncthreads();
         }
     }
+    if (COOP) {
+        __shared__ double s_v[3][EB];
+        const int l0 = bx * EB;
+        const int g0 = l0 < D.nhl ? D.lm_b_start[l0] : 0;
+        const int g1 = l0 < D.nhl ? D.lm_b_start[min(l0 + EB, D.nhl)] : 0;
+        const int mb0 = t < D.nhl ? D.lm_b_start[t] : 0, mb1 = t < D.nhl ? D.lm_b_start[t + 1] : 0;
+        for (int p0 = g0; p0 < g1; p0 += EB) {  // workgroup-uniform
+            const int blk = p0 + (int)threadIdx.x;
+            if (blk < g1) {
+                const int i1 = D.blk_pose[blk];
+                const double *B = D.Hpl + 18 * (size_t)blk;
+                for (int c = 0; c < 3; c++) {
+                    double s_ = 0;
+                    for (int r = 0; r < 6; r++) s_ += B[3 * r + c] * (-D.x[6 * i1 + r]);
+                    s_v[c][threadIdx.x] = s_;
+                }
+            }
+            __syncthreads();
+            const int a1 = min(mb1, p0 + EB);
+            for (int b2 = max(mb0, p0); b2 < a1; b2++)
+                for (int c = 0; c < 3; c++) cl[c] += s_v[c][b2 - p0];
+            __syncthreads();
+        }
+    }
     if (t < D.nhl) {
         const int l = t;
-        if (!STAGE)
+        if (!STAGE && !COOP)
             for (int blk = D.lm_b_start[l]; blk < D.lm_b_start[l + 1]; blk++) {
                 const int i1 = D.blk_pose[blk];
                 const double *B = D.Hpl + 18 * (size_t)blk;
@@ -2950,6 +2978,9 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     // OSG_LIN_WPE=4: k_linearize compiled for 4 waves per SIMD (A/B runs), bit-identical
     static const bool lin_wpe4 = getenv("OSG_LIN_WPE") && atoi(getenv("OSG_LIN_WPE")) == 4;
     static const bool update_stage = getenv("OSG_UPDATE_STAGE") && atoi(getenv("OSG_UPDATE_STAGE")) != 0;
+    // k_update with one thread per Hpl block (the default since the end of r05: 150 -> 143 us per 64-window
+    // step, profiles/r05_update_coop_ab.txt); OSG_UPDATE_COOP=0 restores the per-thread walks, bit-identical
+    static const bool update_coop = !(getenv("OSG_UPDATE_COOP") && atoi(getenv("OSG_UPDATE_COOP")) == 0);
     // OSG_CHOL_DENSE=0: the per-column k_chol_col (+ k_chol_trail) launches for every system (A/B runs)
     // instead of the one-workgroup factorisations k_chol_dense and k_chol_env
     static const bool chol_dense = !(getenv("OSG_CHOL_DENSE") && atoi(getenv("OSG_CHOL_DENSE")) == 0);
@@ -3326,6 +3357,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         }
         LBA_MARK(KT_UPD);
         if (update_stage) hipLaunchKernelGGL(k_update<true>, gx(mx_gu), dim3(EB), 0, ctx->stream, d_dev);
+        else if (update_coop) hipLaunchKernelGGL((k_update<false, true>), gx(mx_gu), dim3(EB), 0, ctx->stream, d_dev);
         else hipLaunchKernelGGL(k_update<false>, gx(mx_gu), dim3(EB), 0, ctx->stream, d_dev);
         LBA_MARK(KT_ERR);
         hipLaunchKernelGGL(k_errors, gx(mx_ge), dim3(EB), 0, ctx->stream, d_dev, 0);

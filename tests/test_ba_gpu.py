@@ -241,7 +241,7 @@ def _gba_variant_graph():
 
 
 @pytest.mark.parametrize("env", [{"OSG_SCHUR_STAGE": "1"}, {"OSG_SCHUR_DIRECT": "1"}, {"OSG_POSE_RED_GATHER": "1"},
-                                 {"OSG_UPDATE_STAGE": "1"}, {"OSG_SCHUR_POINT": "1"},
+                                 {"OSG_UPDATE_STAGE": "1"}, {"OSG_UPDATE_COOP": "0"}, {"OSG_SCHUR_POINT": "1"},
                                  {"OSG_LIN_WPE": "4"}],
                          ids=lambda e: "-".join(f"{k[4:]}={v}" for k, v in e.items()))
 def test_lba_schur_variants_bit_identical(ctx, env):
@@ -249,7 +249,8 @@ def test_lba_schur_variants_bit_identical(ctx, env):
     order (read once per process, so run in a child) give the same results bit for bit: the Schur
     product's LDS-staged partner spans (k_schur_rows_st) and per-lane loads against the per-group
     gathers (k_schur_rows), k_pose_red's edge inputs gathered through hp_e against the pose-major
-    records (k_hp_rec), k_update's Hpl blocks through LDS pieces against per-thread reads, and
+    records (k_hp_rec), k_update's Hpl blocks through LDS pieces or per-thread walks against one
+    thread per block, and
     Dinv from k_schur_point against Dinv formed by its readers, and k_linearize compiled for 4 waves
     per SIMD against the compiler's register allocation.  The GBA graph has per-edge robust flags off (bRobust = false)."""
     import subprocess
