@@ -222,27 +222,48 @@ inline const uint8_t *desc_rows(const MatT &m, int n, std::vector<uint8_t> &out)
 // 64 x 48 grid of vectors as CSR in GetFeaturesInArea's enumeration order (ix outer, iy inner,
 // cell contents in insertion order)
 template <class GridT>
-inline void grid_csr(const GridT &grid, std::vector<int32_t> &gs, std::vector<int32_t> &gi)
+inline void grid_csr(const GridT &grid, std::vector<int32_t> &gs, std::vector<int32_t> &gi, size_t cap)
 {
-    // one pass: sizes and indices together (the cells are separate heap blocks; a second walk over
-    // them measured 30 % slower)
-    size_t total = 0;
-    for (int ix = 0; ix < OSG_GRID_COLS; ix++)
-        for (int iy = 0; iy < OSG_GRID_ROWS; iy++) total += grid[ix][iy].size();
+    // one walk over the cells (separate heap blocks): sizes and indices together, into `gi` sized for
+    // `cap` indices (a Frame's grid holds each of its keypoints at most once), trimmed after; the
+    // two-walk form (count, then fill) below only if a grid holds more (a size walk first measured
+    // 30 % slower, and a walk that reads every cell header twice costs as much again)
     gs.resize(OSG_GRID_CELLS + 1);
-    gi.resize(total);
-    int32_t *g = gs.data(), *o = gi.data();
+    gi.resize(cap);
+    int32_t *g = gs.data(), *o = gi.data(), *const end = gi.data() + cap;
     g[0] = 0;
-    for (int ix = 0; ix < OSG_GRID_COLS; ix++) {
+    bool fits = true;
+    for (int ix = 0; ix < OSG_GRID_COLS && fits; ix++) {
         const auto *col = &grid[ix][0];
         for (int iy = 0; iy < OSG_GRID_ROWS; iy++) {
             const auto *b = col[iy].data();
             const int m = (int)col[iy].size();
+            if (m > end - o) {
+                fits = false;
+                break;
+            }
             for (int k = 0; k < m; k++) o[k] = (int32_t)b[k];
             o += m;
             g[ix * OSG_GRID_ROWS + iy + 1] = (int32_t)(o - gi.data());
         }
     }
+    if (fits) {
+        gi.resize((size_t)(o - gi.data()));
+        return;
+    }
+    size_t total = 0;
+    for (int ix = 0; ix < OSG_GRID_COLS; ix++)
+        for (int iy = 0; iy < OSG_GRID_ROWS; iy++) total += grid[ix][iy].size();
+    grid_csr(grid, gs, gi, total);
+}
+
+// The first `lines` 64-byte lines of a heap object (MapPoints: their state and the fields the hooks
+// read lie past the first line)
+template <class T>
+inline void prefetch_obj(const T *p, int lines = 4)
+{
+    if (!p) return;
+    for (int k = 0; k < lines; k++) __builtin_prefetch((const char *)p + 64 * k);
 }
 
 // Frame::Nleft / KeyFrame::NLeft (ref:include/Frame.h, include/KeyFrame.h spell it differently)
@@ -288,9 +309,9 @@ struct FrameView {
         const uint8_t *dp = desc_rows(F.mDescriptors, n, desc);
         ur.assign(F.mvuRight.begin(), F.mvuRight.end());
         ur.resize(n, -1.0f);
-        grid_csr(F.mGrid, gs, gi);
+        grid_csr(F.mGrid, gs, gi, (size_t)(nleft == -1 ? n : nleft));
         if (nleft != -1) {
-            grid_csr(F.mGridRight, gsr, gir);
+            grid_csr(F.mGridRight, gsr, gir, (size_t)(n - nleft));
             l2r.assign(F.mvLeftToRightMatch.begin(), F.mvLeftToRightMatch.end());
             r2l.assign(F.mvRightToLeftMatch.begin(), F.mvRightToLeftMatch.end());
             l2r.resize(nleft, -1);
@@ -397,7 +418,7 @@ struct MpsGather {
         constexpr int PF = 8;  // MapPoints are scattered heap objects: fetch a few ahead
         for (int i = 0; i < std::min(PF, nq); i++) __builtin_prefetch(vpMapPoints[i]);
         for (int i = 0; i < nq; i++) {
-            if (i + PF < nq) __builtin_prefetch(vpMapPoints[i + PF]);
+            if (i + PF < nq) prefetch_obj(vpMapPoints[i + PF]);
             MapPointT *p = vpMapPoints[i];
             id[i] = i;
             in_view[i] = p->mbTrackInView;
@@ -486,7 +507,7 @@ struct LastGather {
         }
         constexpr int PF = 8;  // MapPoints are scattered heap objects: fetch a few ahead
         for (int i = 0; i < n; i++) {
-            if (i + PF < n && LF.mvpMapPoints[i + PF]) __builtin_prefetch(LF.mvpMapPoints[i + PF]);
+            if (i + PF < n) prefetch_obj(LF.mvpMapPoints[i + PF]);
             MapPointT *p = LF.mvpMapPoints[i];
             const auto &kp = (LF.Nleft == -1) ? LF.mvKeysUn[i]
                                               : (i < LF.Nleft ? LF.mvKeys[i] : LF.mvKeysRight[i - LF.Nleft]);
