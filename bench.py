@@ -6,7 +6,8 @@
 Headline (BASELINE.json metric "Mmatches/s (256-bit Hamming) + LocalBA iters/s"), workload
 configs[1]: brute-force 256-bit Hamming top-2 of 2000 x 2000 descriptors (C2).  One step = one
 launch of 1024 independent 2000 x 2000 problems (frames) through the C-ABI entry
-osg_hamming_top2_batch_dev (k_top2_mfma, I8 matrix cores) with inputs resident in HBM; the one-problem launch
+osg_hamming_top2_batch_dev (k_top2_fp4, FP4 block-scaled matrix cores; OSG_TOP2_FP4=0 selects the I8 form
+k_top2_mfma) with inputs resident in HBM; the one-problem launch
 (osg_hamming_top2_dev) is reported beside it as single_launch.  For N > 1 every rank matches its own
 independent frames (weak scaling; no collective in the data path); value = pairs of all ranks /
 max-over-ranks time.
@@ -164,6 +165,8 @@ def main():
 
     from orb_slam3_comments_ghr_amd import Context, synth
 
+    if rank == 0 and world == 1 and not args.no_cpu:
+        _start_timing_build()  # the cpu_baseline legs' oracle, compiled for this host while the GPU runs
     ctx = Context(local_rank)
     # a dedicated (non-null) stream: the kernels and the HIP events below share it
     stream = torch.cuda.Stream(dev)
@@ -447,9 +450,9 @@ _LINE_HEAD = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_st
 _LINE_ROOF = ("kernel", "bound", "achieved", "peak", "unit", "frac", "frac_of_i8_peak", "traffic", "kernel_us",
               "algorithmic_ops_per_launch", "algorithmic_flop_per_launch", "algorithmic_bytes_per_launch",
               "mfma_busy_frac_pmc")
-_LINE_CPU = ("value", "unit", "cores", "kind", "value_1thread", "sample")
+_LINE_CPU = ("value", "unit", "cores", "kind", "flags", "value_1thread", "sample")
 _LINE_STAGE = ("value", "unit", "speedup_vs_cpu", "speedup_vs_cpu_1thread", "kernel_frames_per_s",
-               "kernel_speedup_vs_cpu", "ms_per_call", "s_per_gba", "peak_device_bytes", "error")
+               "kernel_speedup_vs_cpu", "equals_kernel_path", "ms_per_call", "s_per_gba", "peak_device_bytes", "error")
 
 
 def _short(v, n):
@@ -490,7 +493,7 @@ def compact_line(out, limit=LINE_MAX_BYTES):
                 s["roofline"] = _pick(st["roofline"], ("frac", "kernel_us", "traffic", "mfma_busy_frac_pmc")
                                       if full else ("frac", "kernel_us"), n)
             if full and "cpu_baseline" in st:
-                s["cpu"] = _pick(st["cpu_baseline"], ("value", "cores", "kind"), n)
+                s["cpu"] = _pick(st["cpu_baseline"], ("value", "cores", "kind", "flags"), n)
             line[key] = s
         if "detail_file" in out:
             line["detail_file"] = out["detail_file"]
@@ -813,11 +816,12 @@ def bench_gba_map(ctx, rank, world, dist, dev, args, loop=False):
            "n_gpus": world, "dtype": "f64", "scaling": "weak", "parallelism": f"replicas x{world} (one map per GPU)"}
     if rank == 0 and world == 1 and not args.no_cpu:
         orc, oc = _oracle()
+        from tests import cpu_mt
         t1 = time.perf_counter()
         rc = oc.lba(orc, G)
         tc = time.perf_counter() - t1
         res["cpu_baseline"] = {"value": round(rc.iterations / tc, 2), "unit": "LM iterations/s", "cores": 1,
-                               "kind": "port", "seconds_per_gba": round(tc, 2),
+                               "kind": "port", "flags": cpu_mt.ORACLE_FLAGS, "seconds_per_gba": round(tc, 2),
                                "sample": "one call of the oracle on the same map (envelope LDL^T; g2o's LM is "
                                          "single-threaded, so one map does not use more cores)"}
         res["speedup_vs_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
@@ -834,13 +838,46 @@ def _ref_pattern():
     return golden_data.bit_pattern_31()
 
 
+_TIMING_BUILD = {}
+
+
+def _start_timing_build():
+    """Compile the timing-only oracle (oracle/Makefile `timing`: -O3 -march=native, GCC's default
+    contraction -- the reference's release flags) for this host's CPU in a
+    background thread, so the ~2 s build overlaps the GPU stages.  -march=native means the box's own
+    CPU, so the build happens here, never in the container that cross-compiles the HIP library."""
+    import tempfile
+    import threading
+    d = tempfile.mkdtemp(prefix="osg_oracle_timing_")
+
+    def run():
+        from tests import oracle_calls
+        try:
+            _TIMING_BUILD["lib"] = oracle_calls.load_timing(d)
+        except Exception as e:  # noqa: BLE001 - the checker build stands in, and the line says so
+            _TIMING_BUILD["error"] = f"{type(e).__name__}: {e}"[:300]
+    th = threading.Thread(target=run, daemon=True)
+    th.start()
+    _TIMING_BUILD["thread"] = th
+
+
 def _oracle():
     """The CPU oracle (test infrastructure), loaded only by the cpu_baseline legs.  It times the
     reference's own arithmetic: the host libm's sin / cos / pow / atan2 (oracle_set_libm), not the
-    correctly rounded evaluations the parity tests hold both sides to."""
+    correctly rounded evaluations the parity tests hold both sides to, compiled with the reference's
+    release flags (the timing build) when that build succeeded on this host."""
     if not _ORACLE:
-        from tests import oracle_calls
-        lib = oracle_calls.load()
+        from tests import cpu_mt, oracle_calls
+        if "thread" not in _TIMING_BUILD:
+            _start_timing_build()
+        _TIMING_BUILD["thread"].join()
+        if "lib" in _TIMING_BUILD:
+            lib, flags = _TIMING_BUILD["lib"]
+            cpu_mt.ORACLE_FLAGS = flags + " (timing build)"
+        else:
+            lib = oracle_calls.load()
+            cpu_mt.ORACLE_FLAGS = ("-O3 -ffp-contract=off -fno-fast-math (the checker build: the timing build failed: "
+                                   + _TIMING_BUILD.get("error", "?") + ")")
         lib.oracle_set_libm(1)
         _ORACLE.append((lib, oracle_calls))
     return _ORACLE[0]
@@ -969,7 +1006,16 @@ def _cpp_wall(res, workload, arrays, expect, args, rank, world, dist=None, dev=N
     exe = os.path.join(ROOT, "tools", "adapter_wall_bench")
     env = dict(os.environ)
     if world > 1:
-        env["HIP_VISIBLE_DEVICES"] = os.environ.get("LOCAL_RANK", "0")
+        # this rank's GPU in the parent's own numbering: the LOCAL_RANK-th entry of a device list the
+        # launcher already set, else the ordinal itself
+        lr = int(os.environ.get("LOCAL_RANK", "0"))
+        for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+            vis = [x for x in os.environ.get(var, "").split(",") if x.strip()]
+            if vis:
+                env[var] = vis[lr % len(vis)]
+                break
+        else:
+            env["HIP_VISIBLE_DEVICES"] = str(lr)
     threads = args.wall_threads
     if threads <= 0:  # the same host cores as the CPU baseline (its `cores`), split between local ranks
         from tests import cpu_mt
@@ -1010,6 +1056,11 @@ def _cpp_wall(res, workload, arrays, expect, args, rank, world, dist=None, dev=N
                  "(pack, PCIe, kernels, download), write-back; frames / wall second over all host threads")
     res["wall_cpp_adapter_frames_per_s"] = round(frames / w_s, 1)
     res["wall_cpp_adapter"] = w
+    res["equals_kernel_path"] = not bad
+    if bad:
+        # a wrong-result adapter run is never the stage's value: the kernel rate stays, flagged
+        res["error"] = "C++ adapter results differ from the kernel path: " + json.dumps(bad)[:300]
+        return
     # the drop-in's wall rate is the workload's value: what ORB-SLAM3 would see,
     # host gather, packing, PCIe and write-back included; the batched launches' device time is beside it
     res["kernel_frames_per_s"] = res["value"]

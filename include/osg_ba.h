@@ -121,8 +121,12 @@ int osg_local_bundle_adjustment(struct osg_ctx *ctx, const osg_ba_graph *g, osg_
  * engine on the whole map — every KeyFrame (only the map's init KeyFrame fixed), every MapPoint with
  * an edge, optimize(nIterations) with the caller's e_robust / Huber deltas, no outlier pass (edge_bad
  * is filled but the reference does not read it).  The reduced camera system is dense up to 64 free
- * KeyFrames; past that it is stored and factored on its envelope (banded maps and their loop rows),
- * up to 65 535 free KeyFrames (the pose-pair index is an int32_t). */
+ * KeyFrames; past that it is stored and factored on its envelope (banded maps and their loop rows).
+ * Tested up to about 9 000 free KeyFrames (tests/test_ba_gpu.py::test_gba_9000_kf_loop_map_accepted,
+ * no parity check at that size; parity is checked on the 1 500-KF maps).  The host structure build
+ * still fills two dense pose-pair tables of nhp (nhp + 1) / 2 int32 entries each (about 160 MB each at
+ * 9 000 KF, 8.6 GB each at 65 535) and walks every pair, so host memory and build time grow with nhp^2
+ * (DESIGN.md §3.11). */
 int osg_bundle_adjustment(struct osg_ctx *ctx, const osg_ba_graph *g, osg_ba_result *r,
                           const volatile uint8_t *stop_flag);
 

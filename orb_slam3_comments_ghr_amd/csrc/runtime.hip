@@ -36,6 +36,35 @@ int cgroup_cpus()
     }
     return quota > 0 && period > 0 ? (int)((quota + period - 1) / period) : 0;
 }
+// CPUs of the cgroup's cpuset (v2 cpuset.cpus.effective, else v1 cpuset.effective_cpus, a cpulist such
+// as "0-15,32-47"); 0 when neither is readable
+int cpuset_cpus()
+{
+    const char *paths[] = {"/sys/fs/cgroup/cpuset.cpus.effective", "/sys/fs/cgroup/cpuset/cpuset.effective_cpus"};
+    for (const char *p : paths) {
+        FILE *f = fopen(p, "r");
+        if (!f) continue;
+        char buf[4096] = {};
+        const size_t len = fread(buf, 1, sizeof(buf) - 1, f);
+        fclose(f);
+        buf[len] = 0;
+        int n = 0;
+        for (char *s = buf; *s && *s != '\n';) {
+            char *e = nullptr;
+            const long a = strtol(s, &e, 10);
+            if (e == s) break;
+            long b = a;
+            if (*e == '-') {
+                s = e + 1;
+                b = strtol(s, &e, 10);
+            }
+            if (b >= a) n += (int)(b - a + 1);
+            s = (*e == ',') ? e + 1 : e;
+        }
+        if (n > 0) return n;
+    }
+    return 0;
+}
 // the worker pool behind osg_parallel_run
 struct PoolJob {
     void (*fn)(void *, int);
@@ -106,19 +135,28 @@ int osg_host_cpus()
         if (const char *e = getenv("OSG_HOST_THREADS"))
             if (atoi(e) > 0) return atoi(e);
         const int hw = std::max(1, (int)std::thread::hardware_concurrency());
-        int c = hw;
-        bool pinned = false;  // the launcher gave this process its own CPU set
+        int c = hw, aff = hw;
         cpu_set_t set;
         if (sched_getaffinity(0, sizeof(set), &set) == 0) {
-            pinned = CPU_COUNT(&set) < hw;
-            c = std::min(c, std::max(1, CPU_COUNT(&set)));
+            aff = std::max(1, CPU_COUNT(&set));
+            c = std::min(c, aff);
         }
         const int q = cgroup_cpus();
         if (q > 0) c = std::min(c, q);
         // one process per GPU (torchrun): the node's share is split between the local ranks, unless
-        // the launcher already pinned each rank to its own share (not divided twice)
-        if (const char *lw = getenv("LOCAL_WORLD_SIZE"))
-            if (atoi(lw) > 1 && !pinned) c = std::max(1, c / atoi(lw));
+        // the launcher already pinned each rank to its own share (not divided twice).  A rank
+        // counts as pinned only when its affinity set is at most its 1 / LOCAL_WORLD_SIZE part of the
+        // set all local ranks share (the cgroup's cpuset, else the machine): a container's cpuset that
+        // every rank inherits is smaller than the machine but is not a per-rank pinning
+        if (const char *lwe = getenv("LOCAL_WORLD_SIZE")) {
+            const int lw = atoi(lwe);
+            if (lw > 1) {
+                const int cs = cpuset_cpus();
+                const int shared = cs > 0 ? std::min(cs, hw) : hw;
+                const bool pinned = (long long)aff * lw <= shared;
+                if (!pinned) c = std::max(1, c / lw);
+            }
+        }
         return c;
     }();
     return n;

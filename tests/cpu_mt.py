@@ -16,6 +16,11 @@ import threading
 import time
 
 
+# the compiler flags of the oracle build the workers call (bench.py sets it when it loads the timing
+# build; every baseline object carries it as `flags`)
+ORACLE_FLAGS = "-O3 -ffp-contract=off -fno-fast-math (the checker build)"
+
+
 def cgroup_cpus():
     """The CPU quota of this process's cgroup (cpu.max quota / period), or None when unlimited."""
     try:
@@ -100,11 +105,11 @@ def baseline(make_worker, units_per_call, unit, seconds, label, threads=None):
     v1 = c1 * units_per_call / e1
     vn = cn * units_per_call / en
     host = os.cpu_count()
-    return {"value": round(vn, 2), "unit": unit, "cores": n, "kind": "port",
+    return {"value": round(vn, 2), "unit": unit, "cores": n, "kind": "port", "flags": ORACLE_FLAGS,
             "value_1thread": round(v1, 2), "thread_scaling": round(vn / v1, 2) if v1 else None,
             "host_cpus": host, "cgroup_cpu_quota": cgroup_cpus(), "cpu_model": cpu_model(),
             "node_estimate": {"threads": host, "value": round(vn * host / n, 1),
                               "note": "linear extrapolation of the N-thread rate to every hardware thread of "
                                       "the host (the box's cgroup caps this job at `cores`)"},
             "sample": f"{label}: {cn} calls on {n} threads in {en:.1f} s (+ {c1} calls on 1 thread in {e1:.1f} s), "
-                      f"oracle gcc -O3, one independent problem per thread"}
+                      f"oracle gcc {ORACLE_FLAGS}, one independent problem per thread"}

@@ -27,6 +27,15 @@ def load():
     return declare(C.CDLL(ORACLE_SO))
 
 
+def load_timing(out_dir):
+    """The timing-only oracle build (oracle/Makefile `timing`: the reference's -O3 -march=native with
+    GCC's default C++ contraction), compiled for THIS host's CPU into out_dir; bench.py's cpu_baseline
+    legs time it.  Returns (lib, flags).  The parity tests never load it: the checker is load()."""
+    subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "-j8", "timing", f"TIMING_DIR={out_dir}"],
+                   check=True, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+    with open(os.path.join(out_dir, "flags.txt")) as f:
+        flags = f.read().strip()
+    return declare(C.CDLL(os.path.join(out_dir, "liboracle_timing.so"))), flags
 
 
 def declare(lib: C.CDLL) -> C.CDLL:

@@ -267,7 +267,7 @@ def _edge_problems():
 @pytest.mark.parametrize("env", [{"OSG_TOP2_FP4": "0"}, {"OSG_TOP2_FP4": "0", "OSG_TOP2_MFMA_SHAPE": "1"},
                                  {"OSG_TOP2_FP4": "1", "OSG_TOP2_MFMA_SHAPE": "1"}],
                          ids=lambda e: "-".join(f"{k[9:]}={v}" for k, v in e.items()))
-def test_batch_fp4_edges(oracle, env):
+def test_batch_fp4_edges(oracle, env, tmp_path):
     """The same edge cases on the other matrix-core forms, each against the serial loop: the I8 form
     (k_top2_mfma, OSG_TOP2_FP4=0, integer keys) and a second FP4 shape (keys carried in f32 in [2^23, 2^24),
     exact)."""
@@ -281,12 +281,14 @@ def test_batch_fp4_edges(oracle, env):
             "out = {}\n"
             "for i, (q, t) in enumerate(_edge_problems()):\n"
             "    out[f'p{i}'] = _batch(ctx, [q, q], [t, t])\n"
-            "np.savez('/tmp/_osg_fp4_edges.npz', **out)\n")
+            "import sys\n"
+            "np.savez(sys.argv[1], **out)\n")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=dict(os.environ, **env), capture_output=True,
+    path = str(tmp_path / f"fp4_edges_{os.getpid()}.npz")
+    r = subprocess.run([sys.executable, "-c", code, path], cwd=root, env=dict(os.environ, **env), capture_output=True,
                        text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
-    got = np.load("/tmp/_osg_fp4_edges.npz")
+    got = np.load(path)
     for i, (q, t) in enumerate(_edge_problems()):
         for b in range(2):
             for k, ref in enumerate(otop2(oracle, q, t)):
