@@ -111,7 +111,8 @@ struct LbaDev {
                                          // pose, first rank, hp_b_start[pose], blocks, chunk range
     const int32_t *hp_b_lm;              // per hp_b entry: the block's landmark
     const int32_t *rs_chunk_start, *rs_chunk;  // chunks per row segment
-    const int32_t *rs_cdesc;             // per rs_chunk entry: {chunk, first contribution, count, 0}
+    const int32_t *rs_cdesc;             // per rs_chunk entry: {chunk, first contribution, count, partner
+                                         // hessian pose j}
     const int32_t *hp_rs_start;          // row segments per hessian pose
     double *chunk_part;                  // 36 per chunk
     double *bs_part;                     // 6 per row segment: sum of Hpl Dinv b_l
@@ -127,6 +128,11 @@ struct LbaDev {
     double *chi2o;                       // per edge chi2 of the last computed error (classification)
     double *err;                         // 3 per edge
     double *Hll, *bl, *Hpl, *Hpp, *bp;
+    // the compact per-block factor (the default; OSG_LBA_HPL=1 stores Hpl whole): 6 doubles per block,
+    // the symmetric M = sum over the block's edges of P^T rho' W P (see hpl_col), in Hpl's storage
+    int compact;
+    double *hp_Rt;                       // per hessian pose: R (row-major 9) and t (3) of the current
+                                         // estimate (k_pose_red, every linearisation)
     double *Dinv, *db;                   // k_schur_point's outputs (OSG_SCHUR_POINT=1 only)
     int dinv_inline;                     // 1: k_schur_rows / k_update form Dinv from Hll themselves
     double *Hs, *bs, *x;
@@ -275,6 +281,95 @@ __global__ __launch_bounds__(EB) void k_errors(const LbaDev *__restrict__ Ds, in
     if (threadIdx.x == 0) D.part[part_off + bx] = t;
 }
 
+// ---- the compact per-block factor ------------------------------------------
+// Every edge of the path has J_pose = P S(Xc) and J_point = P R with P = d(error)/d(Xc) (dim x 3), Xc the
+// point in the pose (body) frame, R the pose's rotation and S(Xc) = [-[Xc]x | I] (3 x 6, se3deriv):
+//   EdgeSE3ProjectXYZ           P = -projectJac(Xc)                  (ref:src/OptimizableTypes.cpp:107-141)
+//   EdgeSE3ProjectXYZToBody     P = -projectJac(Xr) Rrl, Xc = Xl     (ref:src/OptimizableTypes.cpp:231-265)
+//   EdgeStereoSE3ProjectXYZ     P = the explicit 3 x 3 of its two formulas
+//                                   (ref:Thirdparty/g2o/g2o/types/types_six_dof_expmap.cpp:318-372)
+// so a block's Hpl = sum_e J_pose^T rho' W J_point = S(Xc)^T M R with M = sum_e P^T rho' W P (3 x 3
+// symmetric; a two-camera rig's left and right edges share Xc = Xl and R, so their M add).  The block
+// keeps M (6 doubles, 48 B, against Hpl's 18); its readers rebuild Hpl from M, the pose's R, t and
+// the landmark's current position.  The rounding differs from the whole-Hpl form (BA parity is a
+// tolerance); every reader rebuilds with hpl_col, so all of them see the same Hpl.
+//
+// P and J_point of one edge (J_point exactly as edge_jacobians forms it, so Hll and b_l are the
+// whole-Hpl form's); dim-2 edges leave row 2 zero
+__device__ inline void edge_pjac(int kind, const osg_camera &cam, const SE3 &T, const double *X, double P[3][3],
+                                 double Jx[3][3])
+{
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            P[i][j] = 0.0;
+            Jx[i][j] = 0.0;
+        }
+    if (kind == OSG_EDGE_MONO) {
+        double Xc[3], PJ[2][3], R[3][3];
+        se3_map(T, X, Xc);
+        cam_project_jac(cam, Xc, PJ);
+        for (int i = 0; i < 2; i++)
+            for (int j = 0; j < 3; j++) P[i][j] = -PJ[i][j];
+        quat_to_R(T.q, R);
+        for (int i = 0; i < 2; i++)
+            for (int j = 0; j < 3; j++) Jx[i][j] = P[i][0] * R[0][j] + P[i][1] * R[1][j] + P[i][2] * R[2][j];
+    } else if (kind == OSG_EDGE_BODY) {
+        const SE3 Trl = se3_from7(cam.trl);
+        double Xl[3], Xr[3], PJ[2][3], Rrl[3][3];
+        se3_map(T, X, Xl);
+        se3_map(Trl, Xl, Xr);
+        cam_project_jac(cam, Xr, PJ);
+        for (int i = 0; i < 2; i++)
+            for (int j = 0; j < 3; j++) PJ[i][j] = -PJ[i][j];
+        quat_to_R(Trl.q, Rrl);
+        for (int i = 0; i < 2; i++)
+            for (int j = 0; j < 3; j++) P[i][j] = PJ[i][0] * Rrl[0][j] + PJ[i][1] * Rrl[1][j] + PJ[i][2] * Rrl[2][j];
+        const SE3 Trw = se3_mul(Trl, T);
+        double Rrw[3][3];
+        quat_to_R(Trw.q, Rrw);
+        for (int i = 0; i < 2; i++)
+            for (int j = 0; j < 3; j++) Jx[i][j] = PJ[i][0] * Rrw[0][j] + PJ[i][1] * Rrw[1][j] + PJ[i][2] * Rrw[2][j];
+    } else {  // STEREO
+        double Xc[3], R[3][3];
+        se3_map(T, X, Xc);
+        const double fx = cam.fx, fy = cam.fy, bf = cam.bf;
+        const double x = Xc[0], y = Xc[1], z = Xc[2];
+        quat_to_R(T.q, R);
+        const double z_2 = z * z;
+        for (int j = 0; j < 3; j++) {
+            Jx[0][j] = -fx * R[0][j] / z + fx * x * R[2][j] / z_2;
+            Jx[1][j] = -fy * R[1][j] / z + fy * y * R[2][j] / z_2;
+            Jx[2][j] = Jx[0][j] - bf * R[2][j] / z_2;
+        }
+        P[0][0] = -fx / z;
+        P[0][2] = fx * x / z_2;
+        P[1][1] = -fy / z;
+        P[1][2] = fy * y / z_2;
+        P[2][0] = P[0][0];
+        P[2][2] = P[0][2] - bf / z_2;
+    }
+}
+// the landmark in the pose frame from the pose's R (row-major) and t: one expression for every reader
+__device__ __forceinline__ double xc_coord(const double *Rrow, double tn, double X0, double X1, double X2)
+{
+    return Rrow[0] * X0 + Rrow[1] * X1 + Rrow[2] * X2 + tn;
+}
+// column c of Hpl = S(Xc)^T (M R) from column c of R: h[r] = Hpl(r, c), r = 0..5.  m = (m00, m01, m02,
+// m11, m12, m22); S(Xc)^T's rows 0..2 are (0, -z, y), (z, 0, -x), (-y, x, 0), rows 3..5 the identity
+__device__ __forceinline__ void hpl_col(const double *m, double x, double y, double z, double r0, double r1, double r2,
+                                        double h[6])
+{
+    const double q0 = m[0] * r0 + m[1] * r1 + m[2] * r2;
+    const double q1 = m[1] * r0 + m[3] * r1 + m[4] * r2;
+    const double q2 = m[2] * r0 + m[4] * r1 + m[5] * r2;
+    h[0] = y * q2 - z * q1;
+    h[1] = z * q0 - x * q2;
+    h[2] = x * q1 - y * q0;
+    h[3] = q0;
+    h[4] = q1;
+    h[5] = q2;
+}
+
 // Linearisation (ref:Thirdparty/g2o/g2o/core/base_binary_edge.hpp:55-120, robust branch), edge-parallel
 // with the landmark-major sums of a per-landmark loop.  Workgroup g takes the landmarks
 // [lg_start[g], lg_start[g + 1]) — at most EB edges, or one landmark with more — and their edges in
@@ -289,13 +384,15 @@ __global__ __launch_bounds__(EB) void k_errors(const LbaDev *__restrict__ Ds, in
 // written and read back cost more HBM time than the recomputed Jacobian costs VALU time).
 // WPE: the minimum waves per SIMD the register allocation must allow (1: the compiler's choice, 146
 // VGPRs = 3 waves; 4: 128 VGPRs with a few spills, OSG_LIN_WPE=4)
-template <bool MULTI, int WPE = 1>
+// COMPACT (the default): a block's M (6) instead of its Hpl (18), from edge_pjac
+template <bool MULTI, int WPE = 1, bool COMPACT = false>
 __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_linearize(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_LIN);
     if (bx >= max(D.gll, 1)) return;
+    constexpr int HN = COMPACT ? 6 : 18;          // doubles per block
     __shared__ double s_t[9][EB];                 // per edge: Hll upper 6 | b_l 3
-    __shared__ double s_h[MULTI ? 18 : 1][EB];    // per edge of a several-edge block: its Hpl terms
+    __shared__ double s_h[MULTI ? HN : 1][EB];    // per edge of a several-edge block: its Hpl / M terms
     __shared__ double s_m[EB / 64];
     double md = 0.0;
     if (D.nhl > 0) {
@@ -312,8 +409,9 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                 const int e = D.lm_e[q];
                 const int k = D.e_kind[e];
                 const SE3 T = se3_from7(poses + 7 * (size_t)D.e_pose[e]);
-                double Jp[3][6], Jx[3][3];
-                edge_jacobians(k, true, D.cams[D.e_cam[e]], T, points + 3 * (size_t)D.e_point[e], Jp, Jx);
+                double Jp[COMPACT ? 1 : 3][6], Jx[3][3], P[COMPACT ? 3 : 1][3];
+                if constexpr (COMPACT) edge_pjac(k, D.cams[D.e_cam[e]], T, points + 3 * (size_t)D.e_point[e], P, Jx);
+                else edge_jacobians(k, true, D.cams[D.e_cam[e]], T, points + 3 * (size_t)D.e_point[e], Jp, Jx);
                 const int dim = (k == OSG_EDGE_STEREO) ? 3 : 2;
                 const double w = edge_w(D, e);
                 const double ev[3] = {D.err[3 * e], D.err[3 * e + 1], D.err[3 * e + 2]};
@@ -325,19 +423,31 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                 double om[3];
                 for (int d = 0; d < 3; d++) om[d] = (d < dim) ? -(w * ev[d]) * rho1 : 0.0;
                 if (dim == 2) {
-                    for (int j = 0; j < 6; j++) Jp[2][j] = 0.0;
+                    if constexpr (!COMPACT)
+                        for (int j = 0; j < 6; j++) Jp[2][j] = 0.0;
                     for (int j = 0; j < 3; j++) Jx[2][j] = 0.0;
                 }
                 const int code = D.edge_blk[e];
                 if (code >= 0) {  // free pose: Hpl (the pose part is recomputed by k_pose_red)
                     const bool multi = MULTI && (code & 2);
-                    double *hp = D.Hpl + 18 * (size_t)(code >> 2);
-                    for (int a = 0; a < 6; a++)
-                        for (int bb = 0; bb < 3; bb++) {
-                            const double v = Jp[0][a] * ww * Jx[0][bb] + Jp[1][a] * ww * Jx[1][bb] + Jp[2][a] * ww * Jx[2][bb];
-                            if (multi) s_h[MULTI ? 3 * a + bb : 0][threadIdx.x] = v;
-                            else hp[3 * a + bb] = v;
+                    double *hp = D.Hpl + HN * (size_t)(code >> 2);
+                    if constexpr (COMPACT) {
+                        constexpr int MA[6] = {0, 0, 0, 1, 1, 2}, MB[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+                        for (int c = 0; c < 6; c++) {
+                            const int a = MA[c], bb = MB[c];
+                            const double v = P[0][a] * ww * P[0][bb] + P[1][a] * ww * P[1][bb] + P[2][a] * ww * P[2][bb];
+                            if (multi) s_h[MULTI ? c : 0][threadIdx.x] = v;
+                            else hp[c] = v;
                         }
+                    } else {
+                        for (int a = 0; a < 6; a++)
+                            for (int bb = 0; bb < 3; bb++) {
+                                const double v = Jp[0][a] * ww * Jx[0][bb] + Jp[1][a] * ww * Jx[1][bb] + Jp[2][a] * ww * Jx[2][bb];
+                                if (multi) s_h[MULTI ? 3 * a + bb : 0][threadIdx.x] = v;
+                                else hp[3 * a + bb] = v;
+                            }
+                    }
                 }
                 int c = 0;
                 for (int a = 0; a < 3; a++)
@@ -356,9 +466,9 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                     if (MULTI) {
                         const int code = D.edge_blk[D.lm_e[qq]];
                         if (code >= 0 && (code & 2)) {
-                            double *hp = D.Hpl + 18 * (size_t)(code >> 2);
+                            double *hp = D.Hpl + HN * (size_t)(code >> 2);
                             const bool first = !(code & 1);
-                            for (int i = 0; i < 18; i++) hp[i] = first ? s_h[MULTI ? i : 0][t] : hp[i] + s_h[MULTI ? i : 0][t];
+                            for (int i = 0; i < HN; i++) hp[i] = first ? s_h[MULTI ? i : 0][t] : hp[i] + s_h[MULTI ? i : 0][t];
                         }
                     }
                 }
@@ -496,6 +606,14 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(3, 8))) void
                 c++;
             }
         for (int k = 0; k < 36; k++) D.Hpp[36 * (size_t)i + k] = H[k];
+        if (D.hp_Rt) {  // the pose's R and t for the compact factor's readers (hpl_col, xc_coord)
+            double Rm[3][3];
+            quat_to_R(T.q, Rm);
+            double *o = D.hp_Rt + 12 * (size_t)i;
+            for (int r = 0; r < 3; r++)
+                for (int c = 0; c < 3; c++) o[3 * r + c] = Rm[r][c];
+            for (int r = 0; r < 3; r++) o[9 + r] = T.t[r];
+        }
         for (int a = 0; a < 6; a++) {
             D.bp[6 * (size_t)i + a] = s[0][21 + a];
             md = fmax(md, fabs(H[a * 7]));
@@ -797,6 +915,202 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__
             if (cnt == GC) {
                 // a full group: straight-line, so the LDS reads of later contributions issue while
                 // earlier MFMAs run (the guarded form below waits on each pair's reads)
+#pragma unroll
+                for (int v = 0; v < GC; v += 2) {
+                    const int r0 = __builtin_amdgcn_readlane(my_rank, u + v);
+                    const int r1 = __builtin_amdgcn_readlane(my_rank, u + v + 1);
+                    acc0 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[a_m * r0 + aoff], hb[18 * v + boff], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[a_m * r1 + aoff], hb[18 * (v + 1) + boff], acc1, 0, 0,
+                                                              0);
+                }
+            } else {
+#pragma unroll
+                for (int v = 0; v < GC; v += 2) {
+                    if (v < cnt) {
+                        const int rank = __builtin_amdgcn_readlane(my_rank, u + v);
+                        acc0 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[a_m * rank + aoff], hb[18 * v + boff], acc0, 0, 0,
+                                                                  0);
+                    }
+                    if (v + 1 < cnt) {
+                        const int rank = __builtin_amdgcn_readlane(my_rank, u + v + 1);
+                        acc1 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[a_m * rank + aoff], hb[18 * (v + 1) + boff], acc1,
+                                                                  0, 0, 0);
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (orow < 6 && ocol < 6) D.chunk_part[36 * (size_t)dc.x + 6 * orow + ocol] = acc0 + acc1;
+        dc = dn;
+        my_rank = n_rank;
+        my_b = n_b;
+        dn = d2;
+        contrib(dn, n_rank, n_b);
+    }
+}
+
+// The Schur product on the compact per-block factor (the default; see hpl_col).  The same row
+// segments, chunks, MFMA layout and accumulation order as k_schur_rows<false>; what changes is what a
+// contribution reads: the partner block's M (48 B) instead of its Hpl (144 B).
+//   * BD staging: each block's Hpl rows are rebuilt from its M, pose i's R, t and the landmark's
+//     current position X (kept in LDS per rank: a contribution's two blocks share the landmark).
+//   * Chunk loop: per group of GC contributions, lane 3 c + n (c < GC, n < 3) holds contribution c's
+//     M in registers (loaded one group ahead, as the granules before), forms coordinate n of its
+//     Xc = R_j X + t_j, takes the other two from its neighbours, and writes column n of Hpl_j
+//     (hpl_col) into the wave's LDS tile; pose j's R, t (the chunk's partner pose, rs_cdesc's fourth
+//     field) come one chunk ahead through a per-wave LDS slot.  The MFMAs then run as before.
+template <int UNUSED = 0>
+__global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict__ Ds)
+{
+    LBA_GRAPH(M_ACT);
+    if (bx >= D.n_rs) return;
+    typedef int i4 __attribute__((ext_vector_type(4)));
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    const i4 inf0 = ((const GLOBAL i4 *)gbl(D.rs_info))[2 * bx];
+    const i4 inf1 = ((const GLOBAL i4 *)gbl(D.rs_info))[2 * bx + 1];
+    const int rs = __builtin_amdgcn_readfirstlane(inf0.x), pi = __builtin_amdgcn_readfirstlane(inf0.y);
+    const int rb = __builtin_amdgcn_readfirstlane(inf0.z), hb0 = __builtin_amdgcn_readfirstlane(inf0.w);
+    const int nr = __builtin_amdgcn_readfirstlane(inf1.x);
+    const double lam = D.ctl->lambda;
+    constexpr int GC = 16;
+    __shared__ double s_bd[RS * 18 + 2];  // + a zero: the MFMA's K-padding lanes read it
+    __shared__ double s_xw[RS * 3];       // per rank: its landmark's current position
+    __shared__ double s_cf[RT / 64][6];
+    __shared__ __attribute__((aligned(16))) double s_hb[RT / 64][GC * 18];
+    __shared__ double s_pj[RT / 64][12];  // per wave: the current chunk's partner pose R (9), t (3)
+    if (threadIdx.x == 0) s_bd[RS * 18] = 0.0;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int kk = lane >> 4, beta = (lane >> 2) & 3, ri = lane & 3;
+    const int arow = 4 * (beta >> 1) + ri, bcol = 4 * (beta & 1) + ri;
+    const int a_m = kk < 3 ? 18 : 0;
+    const int aoff = kk < 3 ? 3 * min(arow, 5) + kk : RS * 18;
+    const int boff = 3 * min(bcol, 5) + min(kk, 2);
+    const int orow = 4 * (beta >> 1) + kk, ocol = 4 * (beta & 1) + ri;
+    const GLOBAL double *__restrict__ Mv = gbl(D.Hpl);
+    const GLOBAL double *__restrict__ Rt = gbl(D.hp_Rt);
+    const double *__restrict__ points = cur_point(D);
+    double *hb = s_hb[wv];
+    double *pj = s_pj[wv];
+    const int t1 = __builtin_amdgcn_readfirstlane(inf1.z);
+    int t = __builtin_amdgcn_readfirstlane(inf1.y) + wv;
+    const GLOBAL i4 *__restrict__ cd = (const GLOBAL i4 *)gbl(D.rs_cdesc);
+    auto desc = [&](int tt) -> i4 {
+        i4 d = tt < t1 ? cd[tt] : i4{0, 0, 0, 0};
+        return i4{__builtin_amdgcn_readfirstlane(d.x), __builtin_amdgcn_readfirstlane(d.y),
+                  __builtin_amdgcn_readfirstlane(d.z), __builtin_amdgcn_readfirstlane(d.w)};
+    };
+    auto contrib = [&](const i4 &d, int &mr, int &mb) {
+        mr = lane < d.z ? gbl(D.pair_rank)[d.y + lane] - rb : 0;
+        mb = lane < d.z ? gbl(D.pair_b)[d.y + lane] : 0;
+    };
+    // the rebuild roles: lane 3 rc + rn, rc < GC
+    const int rc = lane / 3, rn = lane - 3 * rc;
+    const bool rl = rc < GC;
+    auto load_m = [&](int u0, int cnt, int mb, u4 (&Mr)[3]) {
+        const int bj = __shfl(mb, (u0 + rc) & 63);
+        if (rl && rc < cnt) {
+#pragma unroll
+            for (int r = 0; r < 3; r++) Mr[r] = *(const GLOBAL u4 *)(Mv + 6 * (size_t)bj + 2 * r);
+        }
+    };
+    // one double of pose j's R, t per lane < 12, carried in registers to the chunk's start
+    auto load_pose = [&](int j) -> double { return lane < 12 ? Rt[12 * (size_t)j + lane] : 0.0; };
+    i4 dc = desc(t), dn = desc(t + RT / 64);
+    int my_rank = 0, my_b = 0, n_rank = 0, n_b = 0;
+    contrib(dc, my_rank, my_b);
+    contrib(dn, n_rank, n_b);
+    double pv = t < t1 ? load_pose(dc.w) : 0.0;
+    u4 Mr[3];
+    // pose i's R, t (uniform over the workgroup)
+    double Ri[12];
+#pragma unroll
+    for (int k = 0; k < 12; k++) Ri[k] = Rt[12 * (size_t)pi + k];
+    double cf[6] = {0, 0, 0, 0, 0, 0};
+    {
+        const int h = threadIdx.x & 1;  // two threads per block: rows 3h .. 3h + 2
+        double c3[3] = {0, 0, 0};
+        for (int r2 = threadIdx.x; r2 < 2 * nr; r2 += RT) {
+            const int r = r2 >> 1;
+            const int a = gbl(D.hp_b)[hb0 + rb + r];
+            const int l = gbl(D.hp_b_lm)[hb0 + rb + r];
+            const int p = gbl(D.hl_point)[l];
+            double Di[9], db[3], m[6], B[9];
+            if (D.dinv_inline) {
+                landmark_dinv(D, l, lam, Di, db);
+            } else {
+                for (int k = 0; k < 9; k++) Di[k] = gbl(D.Dinv)[9 * (size_t)l + k];
+                for (int k = 0; k < 3; k++) db[k] = gbl(D.db)[3 * (size_t)l + k];
+            }
+            for (int k = 0; k < 6; k++) m[k] = Mv[6 * (size_t)a + k];
+            const double X0 = points[3 * (size_t)p], X1 = points[3 * (size_t)p + 1], X2 = points[3 * (size_t)p + 2];
+            const double x = xc_coord(Ri, Ri[9], X0, X1, X2), y = xc_coord(Ri + 3, Ri[10], X0, X1, X2),
+                         z = xc_coord(Ri + 6, Ri[11], X0, X1, X2);
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                double hc[6];
+                hpl_col(m, x, y, z, Ri[c], Ri[3 + c], Ri[6 + c], hc);
+#pragma unroll
+                for (int rr = 0; rr < 3; rr++) B[3 * rr + c] = h ? hc[3 + rr] : hc[rr];
+            }
+            double *BD = s_bd + 18 * r + 9 * h;
+            for (int rr = 0; rr < 3; rr++) {
+                for (int c = 0; c < 3; c++)
+                    BD[3 * rr + c] = B[3 * rr] * Di[c] + B[3 * rr + 1] * Di[3 + c] + B[3 * rr + 2] * Di[6 + c];
+                c3[rr] += B[3 * rr] * db[0] + B[3 * rr + 1] * db[1] + B[3 * rr + 2] * db[2];
+            }
+            if (h == 0) {
+                s_xw[3 * r] = X0;
+                s_xw[3 * r + 1] = X1;
+                s_xw[3 * r + 2] = X2;
+            }
+        }
+        for (int k = 0; k < 6; k++) cf[k] = (k / 3 == h) ? c3[k % 3] : 0.0;
+    }
+    for (int k = 0; k < 6; k++) cf[k] = wave_sum(cf[k]);
+    if (lane == 0)
+        for (int k = 0; k < 6; k++) s_cf[wv][k] = cf[k];
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        double tt = 0.0;
+        for (int w = 0; w < RT / 64; w++) tt += s_cf[w][threadIdx.x];
+        D.bs_part[6 * (size_t)rs + threadIdx.x] = tt;
+    }
+    load_m(0, dc.z, my_b, Mr);
+    for (; t < t1; t += RT / 64) {
+        const i4 d2 = desc(t + 2 * (RT / 64));
+        const int nq = dc.z;
+        // this chunk's partner pose into the wave's slot, the next chunk's into registers
+        if (lane < 12) pj[lane] = pv;
+        pv = (t + RT / 64 < t1) ? load_pose(dn.w) : 0.0;
+        __builtin_amdgcn_wave_barrier();
+        double acc0 = 0.0, acc1 = 0.0;
+        for (int u = 0; u < nq; u += GC) {
+            const int cnt = min(GC, nq - u);
+            {
+                // rebuild Hpl_j of contributions u .. u + cnt - 1 into the wave's tile
+                const int rk = __shfl(my_rank, (u + rc) & 63);
+                const double X0 = s_xw[3 * rk], X1 = s_xw[3 * rk + 1], X2 = s_xw[3 * rk + 2];
+                const double xn = xc_coord(pj + 3 * rn, pj[9 + rn], X0, X1, X2);
+                const int l0 = 3 * rc;
+                const double x = __shfl(xn, l0 & 63), y = __shfl(xn, (l0 + 1) & 63), z = __shfl(xn, (l0 + 2) & 63);
+                double m[6];
+                m[0] = __builtin_bit_cast(double, (unsigned long long)Mr[0].x | ((unsigned long long)Mr[0].y << 32));
+                m[1] = __builtin_bit_cast(double, (unsigned long long)Mr[0].z | ((unsigned long long)Mr[0].w << 32));
+                m[2] = __builtin_bit_cast(double, (unsigned long long)Mr[1].x | ((unsigned long long)Mr[1].y << 32));
+                m[3] = __builtin_bit_cast(double, (unsigned long long)Mr[1].z | ((unsigned long long)Mr[1].w << 32));
+                m[4] = __builtin_bit_cast(double, (unsigned long long)Mr[2].x | ((unsigned long long)Mr[2].y << 32));
+                m[5] = __builtin_bit_cast(double, (unsigned long long)Mr[2].z | ((unsigned long long)Mr[2].w << 32));
+                double hc[6];
+                hpl_col(m, x, y, z, pj[rn], pj[3 + rn], pj[6 + rn], hc);
+                if (rl && rc < cnt) {
+#pragma unroll
+                    for (int r = 0; r < 6; r++) hb[18 * rc + 3 * r + rn] = hc[r];
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (u + GC < nq) load_m(u + GC, nq - u - GC, my_b, Mr);
+            else load_m(0, dn.z, n_b, Mr);
+            if (cnt == GC) {
 #pragma unroll
                 for (int v = 0; v < GC; v += 2) {
                     const int r0 = __builtin_amdgcn_readlane(my_rank, u + v);
@@ -2221,6 +2535,104 @@ __global__ __launch_bounds__(EB) void k_update(const LbaDev *__restrict__ Ds)
     if (threadIdx.x == 0) D.part[D.npart + bx] = tot;
 }
 
+// k_update on the compact per-block factor (the default): the COOP form's one thread per block, with
+// Hpl_j rebuilt in registers (hpl_col, as k_schur_rows_c) from the block's M, its pose's R, t and its
+// landmark's position; each workgroup's landmark positions and each piece's block -> landmark map come
+// through LDS from the landmarks' threads.  The per-landmark sums keep the COOP order.
+__global__ __launch_bounds__(EB) void k_update_c(const LbaDev *__restrict__ Ds)
+{
+    LBA_GRAPH(M_ACT);
+    if (bx >= D.gu) return;
+    const double lambda = D.ctl->lambda;
+    const double *pose_cur = cur_pose(D), *point_cur = cur_point(D);
+    double *pose_new = new_pose(D), *point_new = new_point(D);
+    __shared__ double s[EB / 64];
+    __shared__ double s_v[3][EB];
+    __shared__ double s_xw[3][EB];
+    __shared__ int s_lm[EB];
+    const int t = bx * EB + threadIdx.x;
+    const int sp = 6 * D.nhp;
+    double sc = 0.0;
+    double cl[3] = {0, 0, 0};
+    const int l0 = bx * EB;
+    const int g0 = l0 < D.nhl ? D.lm_b_start[l0] : 0;
+    const int g1 = l0 < D.nhl ? D.lm_b_start[min(l0 + EB, D.nhl)] : 0;
+    const int mb0 = t < D.nhl ? D.lm_b_start[t] : 0, mb1 = t < D.nhl ? D.lm_b_start[t + 1] : 0;
+    int p = -1;
+    if (t < D.nhl) {
+        cl[0] = D.bl[3 * (size_t)t];
+        cl[1] = D.bl[3 * (size_t)t + 1];
+        cl[2] = D.bl[3 * (size_t)t + 2];
+        p = D.hl_point[t];
+        for (int k = 0; k < 3; k++) s_xw[k][threadIdx.x] = point_cur[3 * (size_t)p + k];
+    }
+    for (int p0 = g0; p0 < g1; p0 += EB) {  // workgroup-uniform
+        // the piece's block -> landmark (local index) map, from the landmarks' threads
+        for (int b2 = max(mb0, p0); b2 < min(mb1, p0 + EB); b2++) s_lm[b2 - p0] = threadIdx.x;
+        __syncthreads();
+        const int blk = p0 + (int)threadIdx.x;
+        if (blk < g1) {
+            const int i1 = D.blk_pose[blk];
+            const int ll = s_lm[threadIdx.x];
+            const double *R = D.hp_Rt + 12 * (size_t)i1;
+            double m[6], Rv[12];
+            for (int k = 0; k < 6; k++) m[k] = D.Hpl[6 * (size_t)blk + k];
+            for (int k = 0; k < 12; k++) Rv[k] = R[k];
+            const double X0 = s_xw[0][ll], X1 = s_xw[1][ll], X2 = s_xw[2][ll];
+            const double x = xc_coord(Rv, Rv[9], X0, X1, X2), y = xc_coord(Rv + 3, Rv[10], X0, X1, X2),
+                         z = xc_coord(Rv + 6, Rv[11], X0, X1, X2);
+            double xp[6];
+            for (int r = 0; r < 6; r++) xp[r] = -D.x[6 * i1 + r];
+            for (int c = 0; c < 3; c++) {
+                double hc[6];
+                hpl_col(m, x, y, z, Rv[c], Rv[3 + c], Rv[6 + c], hc);
+                double s_ = 0;
+                for (int r = 0; r < 6; r++) s_ += hc[r] * xp[r];
+                s_v[c][threadIdx.x] = s_;
+            }
+        }
+        __syncthreads();
+        const int a1 = min(mb1, p0 + EB);
+        for (int b2 = max(mb0, p0); b2 < a1; b2++)
+            for (int c = 0; c < 3; c++) cl[c] += s_v[c][b2 - p0];
+        __syncthreads();
+    }
+    if (t < D.nhl) {
+        const int l = t;
+        double Dv[9];
+        const double *Di = D.Dinv + 9 * (size_t)l;
+        if (D.dinv_inline) {
+            landmark_dinv(D, l, lambda, Dv, nullptr);
+            Di = Dv;
+        }
+        for (int r = 0; r < 3; r++) {
+            const double xl = Di[3 * r] * cl[0] + Di[3 * r + 1] * cl[1] + Di[3 * r + 2] * cl[2];
+            D.x[sp + 3 * l + r] = xl;
+            point_new[3 * (size_t)p + r] = point_cur[3 * (size_t)p + r] + xl;
+            sc += xl * (lambda * xl + D.bl[3 * (size_t)l + r]);
+        }
+    }
+    if (t < D.np) {  // poses: exp(x) * T for free active poses, copy otherwise
+        const int hi = D.pose_h[t];
+        if (hi >= 0) {
+            SE3 T = se3_from7(pose_cur + 7 * (size_t)t);
+            double upd[6];
+            for (int k = 0; k < 6; k++) {
+                upd[k] = D.x[6 * hi + k];
+                sc += upd[k] * (lambda * upd[k] + D.bp[6 * (size_t)hi + k]);
+            }
+            se3_oplus(T, upd);
+            se3_to7(T, pose_new + 7 * (size_t)t);
+        } else {
+            for (int k = 0; k < 7; k++) pose_new[7 * (size_t)t + k] = pose_cur[7 * (size_t)t + k];
+        }
+    }
+    if (t < D.npt && D.point_h[t] < 0)
+        for (int k = 0; k < 3; k++) point_new[3 * (size_t)t + k] = point_cur[3 * (size_t)t + k];
+    const double tot = block_sum_d(sc, s);
+    if (threadIdx.x == 0) D.part[D.npart + bx] = tot;
+}
+
 __global__ __launch_bounds__(EB) void k_classify(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_FIN);
@@ -2875,6 +3287,7 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
         H.rs_cdesc[4 * (size_t)t] = c;
         H.rs_cdesc[4 * (size_t)t + 1] = H.chunk_start[c];
         H.rs_cdesc[4 * (size_t)t + 2] = H.chunk_start[c + 1] - H.chunk_start[c];
+        H.rs_cdesc[4 * (size_t)t + 3] = H.blk_pose[H.pair_b[H.chunk_start[c]]];  // the partner pose j
     }
     STRUCT_CP(10);
     H.ge = (ne + EB - 1) / EB;
@@ -2902,7 +3315,7 @@ int check_graph(osg_ctx *ctx, const osg_ba_graph *G, const osg_ba_result *R)
 }
 
 // device state of one graph (sizes only when base == nullptr)
-void carve_state(char *base, size_t &off, const LbaHost &H, LbaDev *D, bool prof_ts)
+void carve_state(char *base, size_t &off, const LbaHost &H, LbaDev *D, bool prof_ts, bool compact)
 {
     const int np = H.np, npt = H.npt, ne = H.ne, nhl = H.nhl, nhp = H.nhp, nblk = H.nblk;
     const int sp = 6 * nhp;
@@ -2913,7 +3326,8 @@ void carve_state(char *base, size_t &off, const LbaHost &H, LbaDev *D, bool prof
     double *err = carve<double>(base, off, 3 * (size_t)ne);
     double *Hll = carve<double>(base, off, 9 * (size_t)nhl);
     double *bl = carve<double>(base, off, 3 * (size_t)nhl);
-    double *Hpl = carve<double>(base, off, 18 * (size_t)nblk);
+    double *Hpl = carve<double>(base, off, (compact ? 6 : 18) * (size_t)nblk);  // the compact M, or Hpl
+    double *hp_Rt = carve<double>(base, off, 12 * (size_t)nhp);
     double *Hpp = carve<double>(base, off, 36 * (size_t)nhp);
     double *bp = carve<double>(base, off, 6 * (size_t)nhp);
     double *Dinv = carve<double>(base, off, 9 * (size_t)nhl);
@@ -2941,6 +3355,8 @@ void carve_state(char *base, size_t &off, const LbaHost &H, LbaDev *D, bool prof
     D->Hll = Hll;
     D->bl = bl;
     D->Hpl = Hpl;
+    D->hp_Rt = hp_Rt;
+    D->compact = compact ? 1 : 0;
     D->Hpp = Hpp;
     D->bp = bp;
     D->Dinv = Dinv;
@@ -2994,6 +3410,11 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     // two-column form.  k_chol_dense keeps two: in its 1024-thread workgroup the four-column form spills
     // (20-26 us per tile, gpurun_out/elim4).
     static const int chol_elim = getenv("OSG_CHOL_ELIM") ? atoi(getenv("OSG_CHOL_ELIM")) : 4;
+    // the compact per-block factor (k_linearize<.., true>, k_schur_rows_c, k_update_c) unless OSG_LBA_HPL=1
+    // stores Hpl whole; the Hpl-reading A/B variants above run on the whole-Hpl form
+    static const bool hpl_full = (getenv("OSG_LBA_HPL") && atoi(getenv("OSG_LBA_HPL")) == 1) || schur_valu ||
+                                 schur_stage || schur_direct || update_stage || !update_coop;
+    const bool compact = !hpl_full;
     const auto tp0 = std::chrono::steady_clock::now();
     auto ms_since = [&](std::chrono::steady_clock::time_point t) {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
@@ -3104,7 +3525,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     std::vector<size_t> st_off(NA + 1, 0);
     for (int a = 0; a < NA; a++) {
         size_t sz = 0;
-        carve_state(nullptr, sz, H[act[a]], nullptr, prof_ts);
+        carve_state(nullptr, sz, H[act[a]], nullptr, prof_ts, compact);
         st_off[a + 1] = st_off[a] + ((sz + 255) & ~size_t(255)) + 256;
     }
     const size_t in_pad = (pk.total + 255) & ~size_t(255);
@@ -3217,7 +3638,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         D.user_lambda = h.G->user_lambda_init;
         D.dinv_inline = schur_point ? 0 : 1;
         size_t off = 0;
-        carve_state(dst + st_off[a], off, h, &D, prof_ts);
+        carve_state(dst + st_off[a], off, h, &D, prof_ts, compact);
         D.ctl = d_ctl + a;
         D.out = d_out + 8 * a;
         D.pose0 = osg_dptr<double>(din, o.pose0);
@@ -3289,7 +3710,11 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         LBA_MARK(KT_ERR);
         hipLaunchKernelGGL(k_errors, gx(mx_ge), dim3(EB), 0, ctx->stream, d_dev, 1);
         LBA_MARK(KT_LIN);
-        if (any_multi) hipLaunchKernelGGL(k_linearize<true>, gx(mx_gll), dim3(EB), 0, ctx->stream, d_dev);
+        if (compact) {
+            if (any_multi) hipLaunchKernelGGL((k_linearize<true, 1, true>), gx(mx_gll), dim3(EB), 0, ctx->stream, d_dev);
+            else if (lin_wpe4) hipLaunchKernelGGL((k_linearize<false, 4, true>), gx(mx_gll), dim3(EB), 0, ctx->stream, d_dev);
+            else hipLaunchKernelGGL((k_linearize<false, 1, true>), gx(mx_gll), dim3(EB), 0, ctx->stream, d_dev);
+        } else if (any_multi) hipLaunchKernelGGL(k_linearize<true>, gx(mx_gll), dim3(EB), 0, ctx->stream, d_dev);
         else if (lin_wpe4) hipLaunchKernelGGL((k_linearize<false, 4>), gx(mx_gll), dim3(EB), 0, ctx->stream, d_dev);
         else hipLaunchKernelGGL(k_linearize<false>, gx(mx_gll), dim3(EB), 0, ctx->stream, d_dev);
         LBA_MARK(KT_POSE);
@@ -3303,7 +3728,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         if (schur_point) hipLaunchKernelGGL(k_schur_point, gx(mx_gl), dim3(EB), 0, ctx->stream, d_dev);
         if (mx_nhp > 0) {
             LBA_MARK(KT_SROWS);
-            if (schur_valu) hipLaunchKernelGGL(k_schur_rows<true>, gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
+            if (compact) hipLaunchKernelGGL(k_schur_rows_c<0>, gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
+            else if (schur_valu) hipLaunchKernelGGL(k_schur_rows<true>, gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
             else if (schur_stage) hipLaunchKernelGGL(k_schur_rows_st, gx(mx_rs), dim3(RT2), 0, ctx->stream, d_dev);
             else if (schur_direct)
                 hipLaunchKernelGGL((k_schur_rows<false, true>), gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
@@ -3356,7 +3782,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
             }
         }
         LBA_MARK(KT_UPD);
-        if (update_stage) hipLaunchKernelGGL(k_update<true>, gx(mx_gu), dim3(EB), 0, ctx->stream, d_dev);
+        if (compact) hipLaunchKernelGGL(k_update_c, gx(mx_gu), dim3(EB), 0, ctx->stream, d_dev);
+        else if (update_stage) hipLaunchKernelGGL(k_update<true>, gx(mx_gu), dim3(EB), 0, ctx->stream, d_dev);
         else if (update_coop) hipLaunchKernelGGL((k_update<false, true>), gx(mx_gu), dim3(EB), 0, ctx->stream, d_dev);
         else hipLaunchKernelGGL(k_update<false>, gx(mx_gu), dim3(EB), 0, ctx->stream, d_dev);
         LBA_MARK(KT_ERR);

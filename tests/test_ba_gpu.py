@@ -204,6 +204,51 @@ def test_lba_c4_full_size(ctx, oracle):
     assert got.iterations >= 1
 
 
+def _rig_graph(rng, n_kf, n_pts, body_frac=0.5, kb8=False):
+    """An LBA window of a two-camera rig (LocalBundleAdjustment's EdgeSE3ProjectXYZToBody, ref:src/
+    Optimizer.cc:2009-2032): body_frac of the left (mono) observations get a right-camera edge on the same
+    (KeyFrame, MapPoint), so those Hessian blocks carry two edges (k_linearize<true>; the compact factor
+    sums their M).  The right observation is the current estimate seen through Trl plus 1 px of noise;
+    with kb8 both cameras are KannalaBrandt8 and the left observations are re-projected through it."""
+    from orb_slam3_comments_ghr_amd import _abi
+    G = op.synth_lba_graph(rng, n_kf=n_kf, n_points=n_pts)
+    cam1 = op.kb8_camera() if kb8 else G.cams[0]
+    cam2 = (op.kb8_camera if kb8 else op.pinhole_camera)(trl=op.TUMVI_TRL)
+    R = np.array([op.quat_to_rot(q[:4]) for q in G.pose])
+    Xl = np.einsum("eij,ej->ei", R[G.e_pose], G.point[G.e_point]) + G.pose[G.e_pose, 4:]
+
+    def proj(cam, X):
+        if kb8:
+            return np.stack(op.kb8_project(cam, X), 1)
+        return np.stack([cam.fx * X[:, 0] / X[:, 2] + cam.cx, cam.fy * X[:, 1] / X[:, 2] + cam.cy], 1)
+    obs = G.e_obs.copy()
+    mono = G.e_kind == _abi.EDGE_MONO
+    if kb8:
+        obs[mono, :2] = proj(cam1, Xl[mono]) + rng.normal(size=(int(mono.sum()), 2))
+    add = np.nonzero(mono & (rng.random(len(G.e_point)) < body_frac))[0]
+    Rrl, trl = op.quat_to_rot(np.array(op.TUMVI_TRL[:4])), np.array(op.TUMVI_TRL[4:])
+    Xr = Xl[add] @ Rrl.T + trl
+    obs_r = np.zeros((len(add), 3))
+    obs_r[:, :2] = proj(cam2, Xr) + rng.normal(size=(len(add), 2))
+    return op.BAGraph(G.pose, G.pose_fixed, G.point,
+                      np.concatenate([G.e_point, G.e_point[add]]), np.concatenate([G.e_pose, G.e_pose[add]]),
+                      np.concatenate([G.e_kind, np.full(len(add), _abi.EDGE_BODY, np.int8)]),
+                      np.concatenate([G.e_cam, np.ones(len(add), np.int32)]),
+                      np.concatenate([obs, obs_r]).astype(np.float32).astype(np.float64),
+                      np.concatenate([G.e_inv_sigma2, G.e_inv_sigma2[add]]), [cam1, cam2])
+
+
+@pytest.mark.parametrize("n_kf,n_pts,kb8", [(8, 600, False), (20, 2500, False), (12, 1200, True)])
+def test_lba_two_camera_rig(ctx, oracle, n_kf, n_pts, kb8):
+    """Two-camera rig windows (left mono + right body edges on the same blocks, pinhole and KB8) against
+    the oracle: the blocks with several edges, in either Hessian-block form."""
+    rng = np.random.default_rng(4242 + n_kf)
+    G = _rig_graph(rng, n_kf, n_pts, kb8=kb8)
+    pairs = G.e_pose.astype(np.int64) * (len(G.point) + 1) + G.e_point
+    assert len(np.unique(pairs)) < len(pairs)  # some blocks carry two edges
+    check_lba(ctx, oracle, G)
+
+
 def test_lba_batch_equals_single_calls(ctx, oracle):
     """Lockstep batch of heterogeneous windows: every graph's result equals its own single call
     exactly (same kernels, per-graph deterministic reductions) and the oracle within tolerance."""
@@ -240,22 +285,12 @@ def _gba_variant_graph():
     return op.synth_gba_graph(rng, n_kf=30, n_points=3000, bRobust=False, stereo_frac=0.3)
 
 
-@pytest.mark.parametrize("env", [{"OSG_SCHUR_STAGE": "1"}, {"OSG_SCHUR_DIRECT": "1"}, {"OSG_POSE_RED_GATHER": "1"},
-                                 {"OSG_UPDATE_STAGE": "1"}, {"OSG_UPDATE_COOP": "0"}, {"OSG_SCHUR_POINT": "1"},
-                                 {"OSG_LIN_WPE": "4"}],
-                         ids=lambda e: "-".join(f"{k[4:]}={v}" for k, v in e.items()))
-def test_lba_schur_variants_bit_identical(ctx, env):
-    """Kernel variants that read their inputs differently but compute the same products in the same
-    order (read once per process, so run in a child) give the same results bit for bit: the Schur
-    product's LDS-staged partner spans (k_schur_rows_st) and per-lane loads against the per-group
-    gathers (k_schur_rows), k_pose_red's edge inputs gathered through hp_e against the pose-major
-    records (k_hp_rec), k_update's Hpl blocks through LDS pieces or per-thread walks against one
-    thread per block, and
-    Dinv from k_schur_point against Dinv formed by its readers, and k_linearize compiled for 4 waves
-    per SIMD against the compiler's register allocation.  The GBA graph has per-edge robust flags off (bRobust = false)."""
+def _variant_child(env):
+    """LocalBundleAdjustmentBatch of _lba_batch_graphs and BundleAdjustment of _gba_variant_graph in a
+    child process under `env` (the kernel knobs are read once per process)."""
     import subprocess
     import sys
-    out = f"/tmp/_osg_lba_variant_{os.getpid()}.npz"
+    out = f"/tmp/_osg_lba_variant_{os.getpid()}_{abs(hash(tuple(sorted(env.items()))))}.npz"
     code = ("import numpy as np\n"
             "from orb_slam3_comments_ghr_amd import Context, optimizer as op\n"
             "from tests.test_ba_gpu import _lba_batch_graphs\n"
@@ -270,15 +305,57 @@ def test_lba_schur_variants_bit_identical(ctx, env):
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=dict(os.environ, **env), capture_output=True,
                        text=True, timeout=180)
     assert r.returncode == 0, r.stderr[-2000:]
-    got = np.load(out)
+    got = dict(np.load(out))
     os.remove(out)
+    return got
+
+
+# variants of the whole-Hpl form (OSG_LBA_HPL=1): each against that form's default, in two children
+_HPL_VARIANTS = [{"OSG_SCHUR_STAGE": "1"}, {"OSG_SCHUR_DIRECT": "1"}, {"OSG_UPDATE_STAGE": "1"}, {"OSG_UPDATE_COOP": "0"}]
+
+
+@pytest.mark.parametrize("env", [{"OSG_POSE_RED_GATHER": "1"}, {"OSG_SCHUR_POINT": "1"}, {"OSG_LIN_WPE": "4"}]
+                         + _HPL_VARIANTS,
+                         ids=lambda e: "-".join(f"{k[4:]}={v}" for k, v in e.items()))
+def test_lba_schur_variants_bit_identical(ctx, env):
+    """Kernel variants that read their inputs differently but compute the same products in the same
+    order give the same results bit for bit.  On the default compact per-block factor: k_pose_red's edge
+    inputs gathered through hp_e against the pose-major records (k_hp_rec), Dinv from k_schur_point
+    against Dinv formed by its readers, and k_linearize compiled for 4 waves per SIMD.  On the whole-Hpl
+    form (OSG_LBA_HPL=1, which the Hpl-reading variants select): the Schur product's LDS-staged partner
+    spans (k_schur_rows_st) and per-lane loads against the per-group gathers (k_schur_rows), and
+    k_update's Hpl blocks through LDS pieces or per-thread walks against one thread per block.  The GBA
+    graph has per-edge robust flags off (bRobust = false)."""
+    got = _variant_child(env)
+    if env in _HPL_VARIANTS:
+        want = _variant_child({"OSG_LBA_HPL": "1"})
+    else:
+        o = op.Optimizer(ctx)
+        res = o.LocalBundleAdjustmentBatch(_lba_batch_graphs()) + [o.BundleAdjustment(_gba_variant_graph())]
+        want = {"it": np.array([[r.iterations, r.trials] for r in res]),
+                "chi": np.array([[r.chi2_initial, r.chi2_final] for r in res])}
+        for i, r in enumerate(res):
+            want[f"p{i}"], want[f"q{i}"] = r.pose, r.point
+    np.testing.assert_array_equal(got["it"], want["it"])
+    np.testing.assert_array_equal(got["chi"], want["chi"])
+    for i in range(len(got["it"])):
+        np.testing.assert_array_equal(got[f"p{i}"], want[f"p{i}"])
+        np.testing.assert_array_equal(got[f"q{i}"], want[f"q{i}"])
+
+
+def test_lba_compact_factor_vs_whole_hpl(ctx):
+    """The compact per-block factor (the default: M = P^T rho' W P per block, Hpl = S(Xc)^T M R rebuilt by
+    its readers) against the whole-Hpl form (OSG_LBA_HPL=1): the same Hessian in another rounding, so
+    identical iteration / trial counts, chi2 and states equal to rounding, on the LBA batch (mono, stereo,
+    and the 5- to 50-KF windows) and the bRobust = false GBA graph."""
     o = op.Optimizer(ctx)
     res = o.LocalBundleAdjustmentBatch(_lba_batch_graphs()) + [o.BundleAdjustment(_gba_variant_graph())]
-    np.testing.assert_array_equal(got["it"], [[r.iterations, r.trials] for r in res])
-    np.testing.assert_array_equal(got["chi"], [[r.chi2_initial, r.chi2_final] for r in res])
+    full = _variant_child({"OSG_LBA_HPL": "1"})
+    np.testing.assert_array_equal(full["it"], [[r.iterations, r.trials] for r in res])
+    np.testing.assert_allclose(full["chi"], [[r.chi2_initial, r.chi2_final] for r in res], rtol=1e-12, atol=0)
     for i, r in enumerate(res):
-        np.testing.assert_array_equal(got[f"p{i}"], r.pose)
-        np.testing.assert_array_equal(got[f"q{i}"], r.point)
+        np.testing.assert_allclose(full[f"p{i}"], r.pose, atol=1e-9, rtol=0)
+        np.testing.assert_allclose(full[f"q{i}"], r.point, atol=1e-9, rtol=0)
 
 
 def _env_map_graphs():
