@@ -926,12 +926,16 @@ def _pose_result(P):
     return r, o
 
 
-def _latency(gpu_call, cpu_call=None, reps=200):
+def _latency(gpu_call, cpu_call=None, reps=200, ctx=None):
     """Single-call latency of one drop-in call, the way Tracking issues them (one frame at a time,
     ref:src/Tracking.cc:3507): the C-ABI entry with host inputs and outputs (upload, kernels,
     download, stream sync), arguments packed beforehand as the C++ adapter packs them.  Median and
-    p90 over `reps` calls; beside it the oracle's 1-thread time for the same call."""
-    def timeit(call, n):
+    p90 over `reps` calls; beside it the oracle's 1-thread time for the same call.  With ctx, the
+    call's own kernel time (ctx.last_kernel_ms: HIP events around its launches) is recorded per call
+    too: kernel_us (median) and host_us = the median call minus it."""
+    ks = []
+
+    def timeit(call, n, k=None):
         for _ in range(5):
             call()
         ts = []
@@ -939,10 +943,16 @@ def _latency(gpu_call, cpu_call=None, reps=200):
             t0 = time.perf_counter()
             call()
             ts.append(time.perf_counter() - t0)
+            if k is not None:
+                k.append(ctx.last_kernel_ms() * 1e3)
         ts.sort()
         return ts[len(ts) // 2] * 1e6, ts[int(len(ts) * 0.9)] * 1e6
-    g50, g90 = timeit(gpu_call, reps)
+    g50, g90 = timeit(gpu_call, reps, ks if ctx is not None else None)
     out = {"gpu_us_median": round(g50, 1), "gpu_us_p90": round(g90, 1)}
+    if ks:
+        k50 = sorted(ks)[len(ks) // 2]
+        out["kernel_us_median"] = round(k50, 1)
+        out["host_us"] = round(g50 - k50, 1)
     if cpu_call is not None:
         c50, _ = timeit(cpu_call, max(10, reps // 10))
         out["cpu_1thread_us_median"] = round(c50, 1)
@@ -1135,7 +1145,8 @@ def bench_c3(ctx, rank, world, dist, dev, args):
                        C.byref(a), C.byref(b), 0.7, 1, o.ctypes.data)),
                f"PoseOptimization ({probs[0].n} edges)": _latency(
                    lambda: lib.osg_pose_optimization(h, C.byref(ps), C.byref(rs)),
-                   None if args.no_cpu else lambda: _oracle()[0].oracle_pose_optimization(C.byref(ps), C.byref(rs)))}
+                   None if args.no_cpu else lambda: _oracle()[0].oracle_pose_optimization(C.byref(ps), C.byref(rs)),
+                   ctx=ctx)}
 
     res = _frame_batches(ctx, rank, world, dist, dev, args,
                          [lambda: m.SearchByBoWBatch(KB, FB), lambda: opt.PoseOptimization(PB)], cpu,
@@ -1204,7 +1215,7 @@ def bench_c5(ctx, rank, world, dist, dev, args):
                                                           orc and mps(orc.oracle_search_by_projection_mps)),
                f"PoseOptimization KB8 ({probs[0].n} edges)": _latency(
                    lambda: lib.osg_pose_optimization(h, C.byref(ps), C.byref(rs)),
-                   orc and (lambda: orc.oracle_pose_optimization(C.byref(ps), C.byref(rs))))}
+                   orc and (lambda: orc.oracle_pose_optimization(C.byref(ps), C.byref(rs))), ctx=ctx)}
 
     res = _frame_batches(ctx, rank, world, dist, dev, args,
                          [lambda: m.SearchByProjectionBatch(FB, LB, 7.0, False, slot_mps=[S[i][0].copy() for i in idx],
