@@ -955,10 +955,11 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__
 //   * BD staging: each block's Hpl rows are rebuilt from its M, pose i's R, t and the landmark's
 //     current position X (kept in LDS per rank: a contribution's two blocks share the landmark).
 //   * Chunk loop: per group of GC contributions, lane 3 c + n (c < GC, n < 3) holds contribution c's
-//     M in registers (loaded one group ahead, as the granules before), forms coordinate n of its
-//     Xc = R_j X + t_j, takes the other two from its neighbours, and writes column n of Hpl_j
-//     (hpl_col) into the wave's LDS tile; pose j's R, t (the chunk's partner pose, rs_cdesc's fourth
-//     field) come one chunk ahead through a per-wave LDS slot.  The MFMAs then run as before.
+//     M in registers (loaded one group ahead, as the Hpl granules before), forms Xc = R_j X + t_j from
+//     the rank's X (LDS) and column n of Hpl_j (hpl_col), and writes it into the wave's LDS tile; the
+//     MFMAs then run as before.  Pose j's R, t (the chunk's partner pose, rs_cdesc's fourth field)
+//     come one chunk ahead through one double per lane < 12, into a per-wave LDS slot at the chunk's
+//     start (uniform reads; registers are what the MFMA section's operand reads need).
 template <int UNUSED = 0>
 __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict__ Ds)
 {
@@ -977,7 +978,7 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict
     __shared__ double s_xw[RS * 3];       // per rank: its landmark's current position
     __shared__ double s_cf[RT / 64][6];
     __shared__ __attribute__((aligned(16))) double s_hb[RT / 64][GC * 18];
-    __shared__ double s_pj[RT / 64][12];  // per wave: the current chunk's partner pose R (9), t (3)
+    __shared__ __attribute__((aligned(16))) double s_pj[RT / 64 + 1][12];  // per wave: pose j; [RT / 64]: pose i
     if (threadIdx.x == 0) s_bd[RS * 18] = 0.0;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int kk = lane >> 4, beta = (lane >> 2) & 3, ri = lane & 3;
@@ -1013,20 +1014,19 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict
             for (int r = 0; r < 3; r++) Mr[r] = *(const GLOBAL u4 *)(Mv + 6 * (size_t)bj + 2 * r);
         }
     };
-    // one double of pose j's R, t per lane < 12, carried in registers to the chunk's start
+    // one double of a pose's R, t per lane < 12
     auto load_pose = [&](int j) -> double { return lane < 12 ? Rt[12 * (size_t)j + lane] : 0.0; };
     i4 dc = desc(t), dn = desc(t + RT / 64);
     int my_rank = 0, my_b = 0, n_rank = 0, n_b = 0;
     contrib(dc, my_rank, my_b);
     contrib(dn, n_rank, n_b);
     double pv = t < t1 ? load_pose(dc.w) : 0.0;
+    if (threadIdx.x < 12) s_pj[RT / 64][threadIdx.x] = Rt[12 * (size_t)pi + threadIdx.x];
+    __syncthreads();
     u4 Mr[3];
-    // pose i's R, t (uniform over the workgroup)
-    double Ri[12];
-#pragma unroll
-    for (int k = 0; k < 12; k++) Ri[k] = Rt[12 * (size_t)pi + k];
     double cf[6] = {0, 0, 0, 0, 0, 0};
     {
+        const double *q = s_pj[RT / 64];  // pose i
         const int h = threadIdx.x & 1;  // two threads per block: rows 3h .. 3h + 2
         double c3[3] = {0, 0, 0};
         for (int r2 = threadIdx.x; r2 < 2 * nr; r2 += RT) {
@@ -1043,12 +1043,12 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict
             }
             for (int k = 0; k < 6; k++) m[k] = Mv[6 * (size_t)a + k];
             const double X0 = points[3 * (size_t)p], X1 = points[3 * (size_t)p + 1], X2 = points[3 * (size_t)p + 2];
-            const double x = xc_coord(Ri, Ri[9], X0, X1, X2), y = xc_coord(Ri + 3, Ri[10], X0, X1, X2),
-                         z = xc_coord(Ri + 6, Ri[11], X0, X1, X2);
+            const double x = xc_coord(q, q[9], X0, X1, X2), y = xc_coord(q + 3, q[10], X0, X1, X2),
+                         z = xc_coord(q + 6, q[11], X0, X1, X2);
 #pragma unroll
             for (int c = 0; c < 3; c++) {
                 double hc[6];
-                hpl_col(m, x, y, z, Ri[c], Ri[3 + c], Ri[6 + c], hc);
+                hpl_col(m, x, y, z, q[c], q[3 + c], q[6 + c], hc);
 #pragma unroll
                 for (int rr = 0; rr < 3; rr++) B[3 * rr + c] = h ? hc[3 + rr] : hc[rr];
             }
@@ -1079,7 +1079,7 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict
     for (; t < t1; t += RT / 64) {
         const i4 d2 = desc(t + 2 * (RT / 64));
         const int nq = dc.z;
-        // this chunk's partner pose into the wave's slot, the next chunk's into registers
+        // this chunk's partner pose into the wave's slot, the next chunk's into the register
         if (lane < 12) pj[lane] = pv;
         pv = (t + RT / 64 < t1) ? load_pose(dn.w) : 0.0;
         __builtin_amdgcn_wave_barrier();
@@ -1090,24 +1090,30 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict
                 // rebuild Hpl_j of contributions u .. u + cnt - 1 into the wave's tile
                 const int rk = __shfl(my_rank, (u + rc) & 63);
                 const double X0 = s_xw[3 * rk], X1 = s_xw[3 * rk + 1], X2 = s_xw[3 * rk + 2];
-                const double xn = xc_coord(pj + 3 * rn, pj[9 + rn], X0, X1, X2);
-                const int l0 = 3 * rc;
-                const double x = __shfl(xn, l0 & 63), y = __shfl(xn, (l0 + 1) & 63), z = __shfl(xn, (l0 + 2) & 63);
+                const double x = xc_coord(pj, pj[9], X0, X1, X2), y = xc_coord(pj + 3, pj[10], X0, X1, X2),
+                             z = xc_coord(pj + 6, pj[11], X0, X1, X2);
+                double Rc[3];
+#pragma unroll
+                for (int m = 0; m < 3; m++) {  // column rn: a selection between values
+                    const double a = pj[3 * m], b = pj[3 * m + 1], c = pj[3 * m + 2];
+                    const double bc = rn == 1 ? b : c;
+                    Rc[m] = rn == 0 ? a : bc;
+                }
                 double m[6];
-                m[0] = __builtin_bit_cast(double, (unsigned long long)Mr[0].x | ((unsigned long long)Mr[0].y << 32));
-                m[1] = __builtin_bit_cast(double, (unsigned long long)Mr[0].z | ((unsigned long long)Mr[0].w << 32));
-                m[2] = __builtin_bit_cast(double, (unsigned long long)Mr[1].x | ((unsigned long long)Mr[1].y << 32));
-                m[3] = __builtin_bit_cast(double, (unsigned long long)Mr[1].z | ((unsigned long long)Mr[1].w << 32));
-                m[4] = __builtin_bit_cast(double, (unsigned long long)Mr[2].x | ((unsigned long long)Mr[2].y << 32));
-                m[5] = __builtin_bit_cast(double, (unsigned long long)Mr[2].z | ((unsigned long long)Mr[2].w << 32));
+#pragma unroll
+                for (int r = 0; r < 3; r++) {
+                    m[2 * r] = __builtin_bit_cast(double, (unsigned long long)Mr[r].x | ((unsigned long long)Mr[r].y << 32));
+                    m[2 * r + 1] = __builtin_bit_cast(double, (unsigned long long)Mr[r].z | ((unsigned long long)Mr[r].w << 32));
+                }
                 double hc[6];
-                hpl_col(m, x, y, z, pj[rn], pj[3 + rn], pj[6 + rn], hc);
+                hpl_col(m, x, y, z, Rc[0], Rc[1], Rc[2], hc);
                 if (rl && rc < cnt) {
 #pragma unroll
                     for (int r = 0; r < 6; r++) hb[18 * rc + 3 * r + rn] = hc[r];
                 }
             }
             __builtin_amdgcn_wave_barrier();
+            // next group: the rest of this chunk, else the first group of the next chunk
             if (u + GC < nq) load_m(u + GC, nq - u - GC, my_b, Mr);
             else load_m(0, dn.z, n_b, Mr);
             if (cnt == GC) {
