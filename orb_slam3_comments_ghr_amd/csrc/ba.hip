@@ -133,6 +133,8 @@ struct LbaDev {
     int compact;
     double *hp_Rt;                       // per hessian pose: R (row-major 9) and t (3) of the current
                                          // estimate (k_pose_red, every linearisation)
+    double *lmX;                         // per landmark: its current position (k_linearize, compact form):
+                                         // one dependent load level less for the Schur staging
     double *Dinv, *db;                   // k_schur_point's outputs (OSG_SCHUR_POINT=1 only)
     int dinv_inline;                     // 1: k_schur_rows / k_update form Dinv from Hll themselves
     double *Hs, *bs, *x;
@@ -474,6 +476,10 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                 }
             }
             __syncthreads();
+        }
+        if (COMPACT && owner) {
+            const int p = D.hl_point[ol];
+            for (int k = 0; k < 3; k++) D.lmX[3 * (size_t)ol + k] = points[3 * (size_t)p + k];
         }
         if (owner) {
             const double H[9] = {H6[0], H6[1], H6[2], H6[1], H6[3], H6[4], H6[2], H6[4], H6[5]};
@@ -989,7 +995,6 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict
     const int orow = 4 * (beta >> 1) + kk, ocol = 4 * (beta & 1) + ri;
     const GLOBAL double *__restrict__ Mv = gbl(D.Hpl);
     const GLOBAL double *__restrict__ Rt = gbl(D.hp_Rt);
-    const double *__restrict__ points = cur_point(D);
     double *hb = s_hb[wv];
     double *pj = s_pj[wv];
     const int t1 = __builtin_amdgcn_readfirstlane(inf1.z);
@@ -1033,7 +1038,6 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict
             const int r = r2 >> 1;
             const int a = gbl(D.hp_b)[hb0 + rb + r];
             const int l = gbl(D.hp_b_lm)[hb0 + rb + r];
-            const int p = gbl(D.hl_point)[l];
             double Di[9], db[3], m[6], B[9];
             if (D.dinv_inline) {
                 landmark_dinv(D, l, lam, Di, db);
@@ -1042,7 +1046,7 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict
                 for (int k = 0; k < 3; k++) db[k] = gbl(D.db)[3 * (size_t)l + k];
             }
             for (int k = 0; k < 6; k++) m[k] = Mv[6 * (size_t)a + k];
-            const double X0 = points[3 * (size_t)p], X1 = points[3 * (size_t)p + 1], X2 = points[3 * (size_t)p + 2];
+            const double X0 = gbl(D.lmX)[3 * (size_t)l], X1 = gbl(D.lmX)[3 * (size_t)l + 1], X2 = gbl(D.lmX)[3 * (size_t)l + 2];
             const double x = xc_coord(q, q[9], X0, X1, X2), y = xc_coord(q + 3, q[10], X0, X1, X2),
                          z = xc_coord(q + 6, q[11], X0, X1, X2);
 #pragma unroll
@@ -3334,6 +3338,7 @@ void carve_state(char *base, size_t &off, const LbaHost &H, LbaDev *D, bool prof
     double *bl = carve<double>(base, off, 3 * (size_t)nhl);
     double *Hpl = carve<double>(base, off, (compact ? 6 : 18) * (size_t)nblk);  // the compact M, or Hpl
     double *hp_Rt = carve<double>(base, off, 12 * (size_t)nhp);
+    double *lmX = carve<double>(base, off, compact ? 3 * (size_t)nhl : 1);
     double *Hpp = carve<double>(base, off, 36 * (size_t)nhp);
     double *bp = carve<double>(base, off, 6 * (size_t)nhp);
     double *Dinv = carve<double>(base, off, 9 * (size_t)nhl);
@@ -3362,6 +3367,7 @@ void carve_state(char *base, size_t &off, const LbaHost &H, LbaDev *D, bool prof
     D->bl = bl;
     D->Hpl = Hpl;
     D->hp_Rt = hp_Rt;
+    D->lmX = lmX;
     D->compact = compact ? 1 : 0;
     D->Hpp = Hpp;
     D->bp = bp;

@@ -403,7 +403,7 @@ __global__ __launch_bounds__(NW * 64) void k_top2_fp4(const uint32_t *__restrict
     // two fewer rebasing subtractions per tile and no merge of the halves, a longer dependent chain per
     // lane; 852 -> 841 VALU ops, +1.8 % on the headline step (profiles/r05_top2_fp4_onechain.jsonl).
     // The two-pair form stays as OSG_TOP2_MFMA_SHAPE=7.
-    constexpr bool ONE = PIPE == 3;
+    constexpr bool ONE = PIPE == 3 || PIPE == 4;
     int(&kc1)[QT] = ONE ? ka1 : kb1;
     int(&kc2)[QT] = ONE ? ka2 : kb2;
     int pq[QT];
@@ -533,6 +533,42 @@ __global__ __launch_bounds__(NW * 64) void k_top2_fp4(const uint32_t *__restrict
 #pragma unroll
                         for (int j = 0; j < QT; j++) acc[j] = mfma(a[s], bq[j][s], s ? acc[j] : crow);
                         if (tt + 1 < NTILE) a[s] = frag(sb + (tt + 1) * 32 * MX_RS, s);
+                        if (PIPE == 4) {
+                            // the skip test: once a query's running pair has settled, a tile rarely holds a key
+                            // below its second key (a 32-row tile of random descriptors beats k2 in ~1 of 4
+                            // wave tiles at 2000 rows).  At K-step 1 (tile tt - 1's last MFMA has completed)
+                            // every lane takes the min of its 16 keys (8 VALU ops); only if some lane of the
+                            // wave has a key below its k2 does the wave run the 24-op update.  Keys are unique
+                            // (the row is in the key), so a tile whose minimum is above k2 changes neither k1
+                            // nor k2: the result is the update's, bit for bit.
+                            if (s == 1) {
+                                bool need = false;
+#pragma unroll
+                                for (int j = 0; j < QT; j++) {
+                                    int m = __float_as_int(accp[j][0]);
+#pragma unroll
+                                    for (int e = 1; e < 16; e += 2)
+                                        m = min(min(m, __float_as_int(accp[j][e])),
+                                                __float_as_int(accp[j][e + 1 < 16 ? e + 1 : e]));
+                                    need |= m < ka2[j];
+                                }
+                                if (__builtin_amdgcn_ballot_w64(need) != 0) {
+#pragma unroll
+                                    for (int j = 0; j < QT; j++)
+#pragma unroll
+                                        for (int e = 0; e < 16; e += 2)
+                                            key_push2(ka1[j], ka2[j], __float_as_int(accp[j][e]),
+                                                      __float_as_int(accp[j][e + 1]));
+                                }
+#pragma unroll
+                                for (int j = 0; j < QT; j++) {
+                                    ka1[j] -= 32;
+                                    ka2[j] -= 32;
+                                }
+                            }
+                            __builtin_amdgcn_sched_barrier(0);
+                            continue;
+                        }
 #pragma unroll
                         for (int j = 0; j < QT; j++) {
                             if (PIPE == 2) {
@@ -654,9 +690,9 @@ bool mfma_fp4()
 void mfma_shape_of(bool fp4, int shape, int *d)
 {
     static const int i8[5][4] = {{16, 1, 256, 1}, {8, 2, 256, 1}, {16, 1, 256, 0}, {8, 2, 256, 0}, {8, 1, 256, 1}};
-    static const int f4[8][4] = {{16, 1, 256, 3}, {8, 2, 256, 1}, {16, 1, 256, 0}, {16, 1, 256, 3}, {8, 1, 256, 1},
-                                 {16, 2, 256, 1}, {16, 1, 256, 2}, {16, 1, 256, 1}};
-    const int *s = fp4 ? f4[(shape >= 1 && shape <= 7 && shape != 3) ? shape : 0]
+    static const int f4[9][4] = {{16, 1, 256, 3}, {8, 2, 256, 1}, {16, 1, 256, 0}, {16, 1, 256, 3}, {8, 1, 256, 1},
+                                 {16, 2, 256, 1}, {16, 1, 256, 2}, {16, 1, 256, 1}, {16, 1, 256, 4}};
+    const int *s = fp4 ? f4[(shape >= 1 && shape <= 8 && shape != 3) ? shape : 0]
                        : i8[(shape >= 1 && shape <= 4) ? shape : 0];
     for (int i = 0; i < 4; i++) d[i] = s[i];
 }
@@ -692,6 +728,7 @@ int osg_launch_top2_batch_mfma(osg_ctx *ctx, const void *d_query, int32_t nq, co
         case 5: return launch_fp4<16, 2, 256, 1>(ctx, d_query, nq, d_train, nt, nb, d_out);
         case 6: return launch_fp4<16, 1, 256, 2>(ctx, d_query, nq, d_train, nt, nb, d_out);
         case 7: return launch_fp4<16, 1, 256, 1>(ctx, d_query, nq, d_train, nt, nb, d_out);
+        case 8: return launch_fp4<16, 1, 256, 4>(ctx, d_query, nq, d_train, nt, nb, d_out);
         default: return launch_fp4<16, 1, 256, 3>(ctx, d_query, nq, d_train, nt, nb, d_out);
         }
     }
