@@ -631,14 +631,18 @@ def bench_lba(ctx, rank, world, dist, dev, args):
     # b_schur share per block (18 x 3 + 6 x 3 FMA); bytes: Hpl, and Hll and b_l (Dinv and Dinv b_l are
     # formed in the staging since late r04; the same bytes as reading them) once, 12 B of (rank, block)
     # per contribution, one 6x6 chunk partial per 64 contributions written
+    # The compact per-block factor (the default, k_schur_rows_c): a block is its 48-B M (the Hpl rows are
+    # rebuilt from it, the pose's R, t and the landmark's position: + 24 B per landmark), not its 144-B Hpl
+    compact = os.environ.get("OSG_LBA_HPL", "0") != "1"
     sr_flop = 2.0 * (contrib * 108 + blocks * 72)
-    sr_bytes = blocks * 144 + lms * 96 + contrib * 12 + (contrib / 64.0) * 288
+    sr_bytes = blocks * (48 if compact else 144) + lms * (120 if compact else 96) + contrib * 12 + (contrib / 64.0) * 288
     sr_s = kt["schur_rows"][0] / 1e3 / steps
     kernels = {k: round(v[0] / max(1, v[1]), 4) for k, v in kt.items() if v[1]}
     dom = max(kernels, key=kernels.get)
     pmc = _load_json(args.schur_pmc)
     # the MFMA form: "k_schur_rows<false>" (r03 / r04 files) or "k_schur_rows<false, false>" (late r04)
-    pmc_sr = next((v for k, v in pmc.items() if k in ("k_schur_rows<false>", "k_schur_rows<false, false>")), {})
+    pmc_sr = next((v for k, v in pmc.items() if k in (("k_schur_rows_c<0>",) if compact else
+                                                      ("k_schur_rows<false>", "k_schur_rows<false, false>"))), {})
     flop_iter = 72.6e6
     res = {
         "metric": "LocalBA iters/s", "value": round(bval, 1), "unit": "LM iterations/s",
@@ -651,7 +655,8 @@ def bench_lba(ctx, rank, world, dist, dev, args):
         "n_gpus": world, "dtype": "f64",
         "scaling": "weak", "parallelism": f"replicas x{world} (independent windows per GPU)",
         "flop_per_iter_survey_formula": flop_iter,
-        "roofline": {"kernel": "k_schur_rows (Schur product S_ij -= sum BD_i Hpl_j^T on v_mfma_f64_4x4x4f64)",
+        "roofline": {"kernel": ("k_schur_rows_c (compact per-block factor; " if compact else "k_schur_rows (") +
+                               "Schur product S_ij -= sum BD_i Hpl_j^T on v_mfma_f64_4x4x4f64)",
                      "dominant_kernel": dom, "bound": "mfma", "achieved": round(sr_flop / sr_s / 1e12, 4),
                      "peak": 78.6, "unit": "TFLOP/s", "frac": round(sr_flop / sr_s / 1e12 / 78.6, 5),
                      "kernel_us": round(sr_s * 1e6, 2), "windows_per_launch": B,

@@ -51,6 +51,7 @@ using namespace osgba;
 namespace {
 
 constexpr int EB = 256;      // edge-parallel kernels
+constexpr int RT_STRIDE = 16;  // hp_Rt doubles per hessian pose: R (9), t (3), c = R^T t (3), pad
 
 // LbaDev's arrays are generic pointers; the hot gathers read them as global (address space 1) so
 // they issue global_load (counted by vmcnt alone) instead of flat loads, whose lgkmcnt share makes
@@ -129,10 +130,10 @@ struct LbaDev {
     double *err;                         // 3 per edge
     double *Hll, *bl, *Hpl, *Hpp, *bp;
     // the compact per-block factor (the default; OSG_LBA_HPL=1 stores Hpl whole): 6 doubles per block,
-    // the symmetric M = sum over the block's edges of P^T rho' W P (see hpl_col), in Hpl's storage
+    // the symmetric M' = sum over the block's edges of J_point^T rho' W J_point (see z_rows), in Hpl's storage
     int compact;
-    double *hp_Rt;                       // per hessian pose: R (row-major 9) and t (3) of the current
-                                         // estimate (k_pose_red, every linearisation)
+    double *hp_Rt;                       // per hessian pose: R (row-major 9), t (3), c = R^T t (3) of the
+                                         // current estimate (k_pose_red, every linearisation)
     double *lmX;                         // per landmark: its current position (k_linearize, compact form):
                                          // one dependent load level less for the Schur staging
     double *Dinv, *db;                   // k_schur_point's outputs (OSG_SCHUR_POINT=1 only)
@@ -284,92 +285,36 @@ __global__ __launch_bounds__(EB) void k_errors(const LbaDev *__restrict__ Ds, in
 }
 
 // ---- the compact per-block factor ------------------------------------------
-// Every edge of the path has J_pose = P S(Xc) and J_point = P R with P = d(error)/d(Xc) (dim x 3), Xc the
-// point in the pose (body) frame, R the pose's rotation and S(Xc) = [-[Xc]x | I] (3 x 6, se3deriv):
-//   EdgeSE3ProjectXYZ           P = -projectJac(Xc)                  (ref:src/OptimizableTypes.cpp:107-141)
-//   EdgeSE3ProjectXYZToBody     P = -projectJac(Xr) Rrl, Xc = Xl     (ref:src/OptimizableTypes.cpp:231-265)
-//   EdgeStereoSE3ProjectXYZ     P = the explicit 3 x 3 of its two formulas
-//                                   (ref:Thirdparty/g2o/g2o/types/types_six_dof_expmap.cpp:318-372)
-// so a block's Hpl = sum_e J_pose^T rho' W J_point = S(Xc)^T M R with M = sum_e P^T rho' W P (3 x 3
-// symmetric; a two-camera rig's left and right edges share Xc = Xl and R, so their M add).  The block
-// keeps M (6 doubles, 48 B, against Hpl's 18); its readers rebuild Hpl from M, the pose's R, t and
-// the landmark's current position.  The rounding differs from the whole-Hpl form (BA parity is a
-// tolerance); every reader rebuilds with hpl_col, so all of them see the same Hpl.
+// Every edge of the path has J_pose = P S(Xc) and J_point = P R, with P = d(error)/d(Xc), Xc = R X + t the
+// point in the pose (body) frame and S(Xc) = [-[Xc]x | I] (se3deriv): EdgeSE3ProjectXYZ, ...ToBody (P
+// through Trl) and EdgeStereoSE3ProjectXYZ alike (ref:src/OptimizableTypes.cpp:107-141, 231-265,
+// ref:Thirdparty/g2o/g2o/types/types_six_dof_expmap.cpp:318-372).  So a block's
+//     Hpl = sum_e J_pose^T rho' W J_point = S(Xc)^T M R,   M = sum_e P^T rho' W P,
+// and with M' = R^T M R = sum_e J_point^T rho' W J_point (the block's own Hll terms, 3 x 3 symmetric)
+// and c = R^T t ([R v]x = R [v]x R^T, so [Xc]x R = R [X + c]x):
+//     Hpl = D(R) Z,   D(R) = diag(R, R),   Z = [[X + c]x M' ; M']          (6 x 3)
+// A block keeps M' (6 doubles, 48 B, against Hpl's 18); X is its landmark's position, R, t, c its pose's.
+// The Schur product S_ij = sum Hpl_a Dinv Hpl_b^T = D(R_i) [sum (Z_a Dinv) Z_b^T] D(R_j)^T, and
+// Z_b^T = [-M'_b [X]x - M'_b [c_j]x | M'_b], so the chunks sum
+//     [B | A] = sum_p (Z_a Dinv)_p [-M'_p [X_p]x | M'_p]         (k_schur_rows_c: per contribution the
+//                                                                  partner's M' and the landmark's X)
+// and k_schur_pairs forms S_ij = D(R_i) [B - A [c_j]x | A] D(R_j)^T once per pose pair.  The rounding
+// differs from the whole-Hpl form's (BA parity is a tolerance).
 //
-// P and J_point of one edge (J_point exactly as edge_jacobians forms it, so Hll and b_l are the
-// whole-Hpl form's); dim-2 edges leave row 2 zero
-__device__ inline void edge_pjac(int kind, const osg_camera &cam, const SE3 &T, const double *X, double P[3][3],
-                                 double Jx[3][3])
+// rows of Z = [[v]x M' ; M'] for v = X + c (the tile operand uses c = 0): column k of [v]x M' is
+// v x (column k of M');  m = (m00, m01, m02, m11, m12, m22)
+__device__ __forceinline__ void z_rows(const double *m, double x, double y, double z, double Z[6][3])
 {
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) {
-            P[i][j] = 0.0;
-            Jx[i][j] = 0.0;
-        }
-    if (kind == OSG_EDGE_MONO) {
-        double Xc[3], PJ[2][3], R[3][3];
-        se3_map(T, X, Xc);
-        cam_project_jac(cam, Xc, PJ);
-        for (int i = 0; i < 2; i++)
-            for (int j = 0; j < 3; j++) P[i][j] = -PJ[i][j];
-        quat_to_R(T.q, R);
-        for (int i = 0; i < 2; i++)
-            for (int j = 0; j < 3; j++) Jx[i][j] = P[i][0] * R[0][j] + P[i][1] * R[1][j] + P[i][2] * R[2][j];
-    } else if (kind == OSG_EDGE_BODY) {
-        const SE3 Trl = se3_from7(cam.trl);
-        double Xl[3], Xr[3], PJ[2][3], Rrl[3][3];
-        se3_map(T, X, Xl);
-        se3_map(Trl, Xl, Xr);
-        cam_project_jac(cam, Xr, PJ);
-        for (int i = 0; i < 2; i++)
-            for (int j = 0; j < 3; j++) PJ[i][j] = -PJ[i][j];
-        quat_to_R(Trl.q, Rrl);
-        for (int i = 0; i < 2; i++)
-            for (int j = 0; j < 3; j++) P[i][j] = PJ[i][0] * Rrl[0][j] + PJ[i][1] * Rrl[1][j] + PJ[i][2] * Rrl[2][j];
-        const SE3 Trw = se3_mul(Trl, T);
-        double Rrw[3][3];
-        quat_to_R(Trw.q, Rrw);
-        for (int i = 0; i < 2; i++)
-            for (int j = 0; j < 3; j++) Jx[i][j] = PJ[i][0] * Rrw[0][j] + PJ[i][1] * Rrw[1][j] + PJ[i][2] * Rrw[2][j];
-    } else {  // STEREO
-        double Xc[3], R[3][3];
-        se3_map(T, X, Xc);
-        const double fx = cam.fx, fy = cam.fy, bf = cam.bf;
-        const double x = Xc[0], y = Xc[1], z = Xc[2];
-        quat_to_R(T.q, R);
-        const double z_2 = z * z;
-        for (int j = 0; j < 3; j++) {
-            Jx[0][j] = -fx * R[0][j] / z + fx * x * R[2][j] / z_2;
-            Jx[1][j] = -fy * R[1][j] / z + fy * y * R[2][j] / z_2;
-            Jx[2][j] = Jx[0][j] - bf * R[2][j] / z_2;
-        }
-        P[0][0] = -fx / z;
-        P[0][2] = fx * x / z_2;
-        P[1][1] = -fy / z;
-        P[1][2] = fy * y / z_2;
-        P[2][0] = P[0][0];
-        P[2][2] = P[0][2] - bf / z_2;
+    const double M[3][3] = {{m[0], m[1], m[2]}, {m[1], m[3], m[4]}, {m[2], m[4], m[5]}};
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        Z[0][k] = y * M[2][k] - z * M[1][k];
+        Z[1][k] = z * M[0][k] - x * M[2][k];
+        Z[2][k] = x * M[1][k] - y * M[0][k];
+        Z[3][k] = M[0][k];
+        Z[4][k] = M[1][k];
+        Z[5][k] = M[2][k];
     }
-}
-// the landmark in the pose frame from the pose's R (row-major) and t: one expression for every reader
-__device__ __forceinline__ double xc_coord(const double *Rrow, double tn, double X0, double X1, double X2)
-{
-    return Rrow[0] * X0 + Rrow[1] * X1 + Rrow[2] * X2 + tn;
-}
-// column c of Hpl = S(Xc)^T (M R) from column c of R: h[r] = Hpl(r, c), r = 0..5.  m = (m00, m01, m02,
-// m11, m12, m22); S(Xc)^T's rows 0..2 are (0, -z, y), (z, 0, -x), (-y, x, 0), rows 3..5 the identity
-__device__ __forceinline__ void hpl_col(const double *m, double x, double y, double z, double r0, double r1, double r2,
-                                        double h[6])
-{
-    const double q0 = m[0] * r0 + m[1] * r1 + m[2] * r2;
-    const double q1 = m[1] * r0 + m[3] * r1 + m[4] * r2;
-    const double q2 = m[2] * r0 + m[4] * r1 + m[5] * r2;
-    h[0] = y * q2 - z * q1;
-    h[1] = z * q0 - x * q2;
-    h[2] = x * q1 - y * q0;
-    h[3] = q0;
-    h[4] = q1;
-    h[5] = q2;
 }
 
 // Linearisation (ref:Thirdparty/g2o/g2o/core/base_binary_edge.hpp:55-120, robust branch), edge-parallel
@@ -386,7 +331,7 @@ __device__ __forceinline__ void hpl_col(const double *m, double x, double y, dou
 // written and read back cost more HBM time than the recomputed Jacobian costs VALU time).
 // WPE: the minimum waves per SIMD the register allocation must allow (1: the compiler's choice, 146
 // VGPRs = 3 waves; 4: 128 VGPRs with a few spills, OSG_LIN_WPE=4)
-// COMPACT (the default): a block's M (6) instead of its Hpl (18), from edge_pjac
+// COMPACT (the default): a block's M' (its Hll terms, 6) instead of its Hpl (18)
 template <bool MULTI, int WPE = 1, bool COMPACT = false>
 __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_linearize(const LbaDev *__restrict__ Ds)
 {
@@ -411,9 +356,8 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                 const int e = D.lm_e[q];
                 const int k = D.e_kind[e];
                 const SE3 T = se3_from7(poses + 7 * (size_t)D.e_pose[e]);
-                double Jp[COMPACT ? 1 : 3][6], Jx[3][3], P[COMPACT ? 3 : 1][3];
-                if constexpr (COMPACT) edge_pjac(k, D.cams[D.e_cam[e]], T, points + 3 * (size_t)D.e_point[e], P, Jx);
-                else edge_jacobians(k, true, D.cams[D.e_cam[e]], T, points + 3 * (size_t)D.e_point[e], Jp, Jx);
+                double Jp[3][6], Jx[3][3];
+                edge_jacobians(k, true, D.cams[D.e_cam[e]], T, points + 3 * (size_t)D.e_point[e], Jp, Jx);
                 const int dim = (k == OSG_EDGE_STEREO) ? 3 : 2;
                 const double w = edge_w(D, e);
                 const double ev[3] = {D.err[3 * e], D.err[3 * e + 1], D.err[3 * e + 2]};
@@ -425,22 +369,26 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                 double om[3];
                 for (int d = 0; d < 3; d++) om[d] = (d < dim) ? -(w * ev[d]) * rho1 : 0.0;
                 if (dim == 2) {
-                    if constexpr (!COMPACT)
-                        for (int j = 0; j < 6; j++) Jp[2][j] = 0.0;
+                    for (int j = 0; j < 6; j++) Jp[2][j] = 0.0;
                     for (int j = 0; j < 3; j++) Jx[2][j] = 0.0;
+                }
+                // the edge's Hll terms (upper 6): also the compact form's M' of a one-edge block
+                double hl6[6];
+                {
+                    int c = 0;
+                    for (int a = 0; a < 3; a++)
+                        for (int bb = a; bb < 3; bb++)
+                            hl6[c++] = Jx[0][a] * ww * Jx[0][bb] + Jx[1][a] * ww * Jx[1][bb] + Jx[2][a] * ww * Jx[2][bb];
                 }
                 const int code = D.edge_blk[e];
                 if (code >= 0) {  // free pose: Hpl (the pose part is recomputed by k_pose_red)
                     const bool multi = MULTI && (code & 2);
                     double *hp = D.Hpl + HN * (size_t)(code >> 2);
                     if constexpr (COMPACT) {
-                        constexpr int MA[6] = {0, 0, 0, 1, 1, 2}, MB[6] = {0, 1, 2, 1, 2, 2};
 #pragma unroll
                         for (int c = 0; c < 6; c++) {
-                            const int a = MA[c], bb = MB[c];
-                            const double v = P[0][a] * ww * P[0][bb] + P[1][a] * ww * P[1][bb] + P[2][a] * ww * P[2][bb];
-                            if (multi) s_h[MULTI ? c : 0][threadIdx.x] = v;
-                            else hp[c] = v;
+                            if (multi) s_h[MULTI ? c : 0][threadIdx.x] = hl6[c];
+                            else hp[c] = hl6[c];
                         }
                     } else {
                         for (int a = 0; a < 6; a++)
@@ -451,10 +399,7 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                             }
                     }
                 }
-                int c = 0;
-                for (int a = 0; a < 3; a++)
-                    for (int bb = a; bb < 3; bb++)
-                        s_t[c++][threadIdx.x] = Jx[0][a] * ww * Jx[0][bb] + Jx[1][a] * ww * Jx[1][bb] + Jx[2][a] * ww * Jx[2][bb];
+                for (int c = 0; c < 6; c++) s_t[c][threadIdx.x] = hl6[c];
                 for (int a = 0; a < 3; a++)
                     s_t[6 + a][threadIdx.x] = Jx[0][a] * om[0] + Jx[1][a] * om[1] + Jx[2][a] * om[2];
             }
@@ -612,13 +557,15 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(3, 8))) void
                 c++;
             }
         for (int k = 0; k < 36; k++) D.Hpp[36 * (size_t)i + k] = H[k];
-        if (D.hp_Rt) {  // the pose's R and t for the compact factor's readers (hpl_col, xc_coord)
+        if (D.hp_Rt) {  // the pose's R, t and c = R^T t for the compact factor's readers
             double Rm[3][3];
             quat_to_R(T.q, Rm);
-            double *o = D.hp_Rt + 12 * (size_t)i;
+            double *o = D.hp_Rt + RT_STRIDE * (size_t)i;
             for (int r = 0; r < 3; r++)
                 for (int c = 0; c < 3; c++) o[3 * r + c] = Rm[r][c];
             for (int r = 0; r < 3; r++) o[9 + r] = T.t[r];
+            for (int c = 0; c < 3; c++) o[12 + c] = Rm[0][c] * T.t[0] + Rm[1][c] * T.t[1] + Rm[2][c] * T.t[2];
+            o[15] = 0.0;
         }
         for (int a = 0; a < 6; a++) {
             D.bp[6 * (size_t)i + a] = s[0][21 + a];
@@ -955,17 +902,18 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__
     }
 }
 
-// The Schur product on the compact per-block factor (the default; see hpl_col).  The same row
-// segments, chunks, MFMA layout and accumulation order as k_schur_rows<false>; what changes is what a
-// contribution reads: the partner block's M (48 B) instead of its Hpl (144 B).
-//   * BD staging: each block's Hpl rows are rebuilt from its M, pose i's R, t and the landmark's
-//     current position X (kept in LDS per rank: a contribution's two blocks share the landmark).
-//   * Chunk loop: per group of GC contributions, lane 3 c + n (c < GC, n < 3) holds contribution c's
-//     M in registers (loaded one group ahead, as the Hpl granules before), forms Xc = R_j X + t_j from
-//     the rank's X (LDS) and column n of Hpl_j (hpl_col), and writes it into the wave's LDS tile; the
-//     MFMAs then run as before.  Pose j's R, t (the chunk's partner pose, rs_cdesc's fourth field)
-//     come one chunk ahead through one double per lane < 12, into a per-wave LDS slot at the chunk's
-//     start (uniform reads; registers are what the MFMA section's operand reads need).
+// The Schur product on the compact per-block factor (the default; see z_rows).  The same row segments,
+// chunks, MFMA layout and accumulation order as k_schur_rows<false>; what changes is what a contribution
+// reads (the partner block's M', 48 B, instead of its Hpl, 144 B) and that the products are summed in
+// the world frame, k_schur_pairs rotating each pose pair's sum once.
+//   * BD staging: BD' = Z_a Dinv with Z_a = [[X + c_i]x M'_a ; M'_a] (pose i's c, the landmark's X from
+//     lmX, landmark order), and the segment's share of b_schur as sum Z_a Dinv b_l (rotated later too);
+//     X is kept in LDS per rank for the chunks.
+//   * Chunks: lane v holds contribution v's M' (loaded one whole chunk ahead: up to 64 loads in flight
+//     per wave, where the whole-Hpl form keeps one group of 16 in flight) and its landmark's X.  Per
+//     group of GC contributions the group's lanes write [[X]x M' ; M'] (18 FMA, no pose) into the wave's
+//     LDS tile, the transposed operand [-M'[X]x | M'] of the product; the MFMAs then run as before and a
+//     chunk's partial is [B | A] of the comment above z_rows.
 template <int UNUSED = 0>
 __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict__ Ds)
 {
@@ -973,6 +921,7 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict
     if (bx >= D.n_rs) return;
     typedef int i4 __attribute__((ext_vector_type(4)));
     typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    typedef double d2v __attribute__((ext_vector_type(2)));
     const i4 inf0 = ((const GLOBAL i4 *)gbl(D.rs_info))[2 * bx];
     const i4 inf1 = ((const GLOBAL i4 *)gbl(D.rs_info))[2 * bx + 1];
     const int rs = __builtin_amdgcn_readfirstlane(inf0.x), pi = __builtin_amdgcn_readfirstlane(inf0.y);
@@ -984,7 +933,6 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict
     __shared__ double s_xw[RS * 3];       // per rank: its landmark's current position
     __shared__ double s_cf[RT / 64][6];
     __shared__ __attribute__((aligned(16))) double s_hb[RT / 64][GC * 18];
-    __shared__ __attribute__((aligned(16))) double s_pj[RT / 64 + 1][12];  // per wave: pose j; [RT / 64]: pose i
     if (threadIdx.x == 0) s_bd[RS * 18] = 0.0;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int kk = lane >> 4, beta = (lane >> 2) & 3, ri = lane & 3;
@@ -994,51 +942,42 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict
     const int boff = 3 * min(bcol, 5) + min(kk, 2);
     const int orow = 4 * (beta >> 1) + kk, ocol = 4 * (beta & 1) + ri;
     const GLOBAL double *__restrict__ Mv = gbl(D.Hpl);
-    const GLOBAL double *__restrict__ Rt = gbl(D.hp_Rt);
     double *hb = s_hb[wv];
-    double *pj = s_pj[wv];
     const int t1 = __builtin_amdgcn_readfirstlane(inf1.z);
     int t = __builtin_amdgcn_readfirstlane(inf1.y) + wv;
     const GLOBAL i4 *__restrict__ cd = (const GLOBAL i4 *)gbl(D.rs_cdesc);
     auto desc = [&](int tt) -> i4 {
         i4 d = tt < t1 ? cd[tt] : i4{0, 0, 0, 0};
         return i4{__builtin_amdgcn_readfirstlane(d.x), __builtin_amdgcn_readfirstlane(d.y),
-                  __builtin_amdgcn_readfirstlane(d.z), __builtin_amdgcn_readfirstlane(d.w)};
+                  __builtin_amdgcn_readfirstlane(d.z), 0};
     };
     auto contrib = [&](const i4 &d, int &mr, int &mb) {
         mr = lane < d.z ? gbl(D.pair_rank)[d.y + lane] - rb : 0;
         mb = lane < d.z ? gbl(D.pair_b)[d.y + lane] : 0;
     };
-    // the rebuild roles: lane 3 rc + rn, rc < GC
-    const int rc = lane / 3, rn = lane - 3 * rc;
-    const bool rl = rc < GC;
-    auto load_m = [&](int u0, int cnt, int mb, u4 (&Mr)[3]) {
-        const int bj = __shfl(mb, (u0 + rc) & 63);
-        if (rl && rc < cnt) {
+    // lane v: the M' of the chunk's contribution v
+    auto load_m = [&](const i4 &d, int mb, u4 (&Mr)[3]) {
+        if (lane < d.z) {
 #pragma unroll
-            for (int r = 0; r < 3; r++) Mr[r] = *(const GLOBAL u4 *)(Mv + 6 * (size_t)bj + 2 * r);
+            for (int r = 0; r < 3; r++) Mr[r] = *(const GLOBAL u4 *)(Mv + 6 * (size_t)mb + 2 * r);
         }
     };
-    // one double of a pose's R, t per lane < 12
-    auto load_pose = [&](int j) -> double { return lane < 12 ? Rt[12 * (size_t)j + lane] : 0.0; };
     i4 dc = desc(t), dn = desc(t + RT / 64);
     int my_rank = 0, my_b = 0, n_rank = 0, n_b = 0;
     contrib(dc, my_rank, my_b);
     contrib(dn, n_rank, n_b);
-    double pv = t < t1 ? load_pose(dc.w) : 0.0;
-    if (threadIdx.x < 12) s_pj[RT / 64][threadIdx.x] = Rt[12 * (size_t)pi + threadIdx.x];
-    __syncthreads();
-    u4 Mr[3];
+    u4 Mc[3], Mn[3];
     double cf[6] = {0, 0, 0, 0, 0, 0};
     {
-        const double *q = s_pj[RT / 64];  // pose i
+        const double *ci = D.hp_Rt + RT_STRIDE * (size_t)pi + 12;  // pose i's c = R^T t
+        const double c0 = ci[0], c1 = ci[1], c2 = ci[2];
         const int h = threadIdx.x & 1;  // two threads per block: rows 3h .. 3h + 2
         double c3[3] = {0, 0, 0};
         for (int r2 = threadIdx.x; r2 < 2 * nr; r2 += RT) {
             const int r = r2 >> 1;
             const int a = gbl(D.hp_b)[hb0 + rb + r];
             const int l = gbl(D.hp_b_lm)[hb0 + rb + r];
-            double Di[9], db[3], m[6], B[9];
+            double Di[9], db[3], m[6], Z[6][3];
             if (D.dinv_inline) {
                 landmark_dinv(D, l, lam, Di, db);
             } else {
@@ -1047,20 +986,13 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict
             }
             for (int k = 0; k < 6; k++) m[k] = Mv[6 * (size_t)a + k];
             const double X0 = gbl(D.lmX)[3 * (size_t)l], X1 = gbl(D.lmX)[3 * (size_t)l + 1], X2 = gbl(D.lmX)[3 * (size_t)l + 2];
-            const double x = xc_coord(q, q[9], X0, X1, X2), y = xc_coord(q + 3, q[10], X0, X1, X2),
-                         z = xc_coord(q + 6, q[11], X0, X1, X2);
-#pragma unroll
-            for (int c = 0; c < 3; c++) {
-                double hc[6];
-                hpl_col(m, x, y, z, q[c], q[3 + c], q[6 + c], hc);
-#pragma unroll
-                for (int rr = 0; rr < 3; rr++) B[3 * rr + c] = h ? hc[3 + rr] : hc[rr];
-            }
+            z_rows(m, X0 + c0, X1 + c1, X2 + c2, Z);
             double *BD = s_bd + 18 * r + 9 * h;
             for (int rr = 0; rr < 3; rr++) {
+                const double *B = Z[3 * h + rr];
                 for (int c = 0; c < 3; c++)
-                    BD[3 * rr + c] = B[3 * rr] * Di[c] + B[3 * rr + 1] * Di[3 + c] + B[3 * rr + 2] * Di[6 + c];
-                c3[rr] += B[3 * rr] * db[0] + B[3 * rr + 1] * db[1] + B[3 * rr + 2] * db[2];
+                    BD[3 * rr + c] = B[0] * Di[c] + B[1] * Di[3 + c] + B[2] * Di[6 + c];
+                c3[rr] += B[0] * db[0] + B[1] * db[1] + B[2] * db[2];
             }
             if (h == 0) {
                 s_xw[3 * r] = X0;
@@ -1070,6 +1002,7 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict
         }
         for (int k = 0; k < 6; k++) cf[k] = (k / 3 == h) ? c3[k % 3] : 0.0;
     }
+    load_m(dc, my_b, Mc);
     for (int k = 0; k < 6; k++) cf[k] = wave_sum(cf[k]);
     if (lane == 0)
         for (int k = 0; k < 6; k++) s_cf[wv][k] = cf[k];
@@ -1079,47 +1012,29 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict
         for (int w = 0; w < RT / 64; w++) tt += s_cf[w][threadIdx.x];
         D.bs_part[6 * (size_t)rs + threadIdx.x] = tt;
     }
-    load_m(0, dc.z, my_b, Mr);
     for (; t < t1; t += RT / 64) {
         const i4 d2 = desc(t + 2 * (RT / 64));
         const int nq = dc.z;
-        // this chunk's partner pose into the wave's slot, the next chunk's into the register
-        if (lane < 12) pj[lane] = pv;
-        pv = (t + RT / 64 < t1) ? load_pose(dn.w) : 0.0;
-        __builtin_amdgcn_wave_barrier();
+        load_m(dn, n_b, Mn);  // the next chunk's M', one chunk ahead
+        // lane v: the landmark position of contribution v
+        const double X0 = s_xw[3 * my_rank], X1 = s_xw[3 * my_rank + 1], X2 = s_xw[3 * my_rank + 2];
         double acc0 = 0.0, acc1 = 0.0;
         for (int u = 0; u < nq; u += GC) {
             const int cnt = min(GC, nq - u);
-            {
-                // rebuild Hpl_j of contributions u .. u + cnt - 1 into the wave's tile
-                const int rk = __shfl(my_rank, (u + rc) & 63);
-                const double X0 = s_xw[3 * rk], X1 = s_xw[3 * rk + 1], X2 = s_xw[3 * rk + 2];
-                const double x = xc_coord(pj, pj[9], X0, X1, X2), y = xc_coord(pj + 3, pj[10], X0, X1, X2),
-                             z = xc_coord(pj + 6, pj[11], X0, X1, X2);
-                double Rc[3];
-#pragma unroll
-                for (int m = 0; m < 3; m++) {  // column rn: a selection between values
-                    const double a = pj[3 * m], b = pj[3 * m + 1], c = pj[3 * m + 2];
-                    const double bc = rn == 1 ? b : c;
-                    Rc[m] = rn == 0 ? a : bc;
-                }
-                double m[6];
+            if (lane >= u && lane < u + cnt) {
+                // contribution `lane`'s operand rows [[X]x M' ; M'] (6 x 3, row-major) into the tile
+                double m[6], Z[6][3];
 #pragma unroll
                 for (int r = 0; r < 3; r++) {
-                    m[2 * r] = __builtin_bit_cast(double, (unsigned long long)Mr[r].x | ((unsigned long long)Mr[r].y << 32));
-                    m[2 * r + 1] = __builtin_bit_cast(double, (unsigned long long)Mr[r].z | ((unsigned long long)Mr[r].w << 32));
+                    m[2 * r] = __builtin_bit_cast(double, (unsigned long long)Mc[r].x | ((unsigned long long)Mc[r].y << 32));
+                    m[2 * r + 1] = __builtin_bit_cast(double, (unsigned long long)Mc[r].z | ((unsigned long long)Mc[r].w << 32));
                 }
-                double hc[6];
-                hpl_col(m, x, y, z, Rc[0], Rc[1], Rc[2], hc);
-                if (rl && rc < cnt) {
+                z_rows(m, X0, X1, X2, Z);
+                d2v *dst = (d2v *)(hb + 18 * (lane - u));
 #pragma unroll
-                    for (int r = 0; r < 6; r++) hb[18 * rc + 3 * r + rn] = hc[r];
-                }
+                for (int k = 0; k < 9; k++) dst[k] = d2v{Z[(2 * k) / 3][(2 * k) % 3], Z[(2 * k + 1) / 3][(2 * k + 1) % 3]};
             }
             __builtin_amdgcn_wave_barrier();
-            // next group: the rest of this chunk, else the first group of the next chunk
-            if (u + GC < nq) load_m(u + GC, nq - u - GC, my_b, Mr);
-            else load_m(0, dn.z, n_b, Mr);
             if (cnt == GC) {
 #pragma unroll
                 for (int v = 0; v < GC; v += 2) {
@@ -1150,6 +1065,8 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict
         dc = dn;
         my_rank = n_rank;
         my_b = n_b;
+#pragma unroll
+        for (int r = 0; r < 3; r++) Mc[r] = Mn[r];
         dn = d2;
         contrib(dn, n_rank, n_b);
     }
@@ -1319,6 +1236,55 @@ __global__ __launch_bounds__(256) void k_schur_pairs(const LbaDev *__restrict__ 
     while (i + 1 < m && start(i + 1) <= wave) i++;
     const int j = i + (int)(wave - start(i));
     const int n = 6 * D.nhp;
+    if (D.compact) {
+        // the compact factor's chunks summed [B | A] in the world frame (see z_rows): the pair's sum T,
+        // then S_ij = D(R_i) [B - A [c_j]x | A] D(R_j)^T; b_schur's share likewise D(R_i) v
+        __shared__ double s_T[4][48];
+        double *T = s_T[threadIdx.x >> 6];
+        if (lane < 36) {
+            double acc = 0.0;
+            const int ch0 = D.live_chunk ? D.live_chunk[2 * slot] : D.pair_chunk[wave];
+            const int ch1 = D.live_chunk ? D.live_chunk[2 * slot + 1] : D.pair_chunk[wave + 1];
+            for (int ch = ch0; ch < ch1; ch++) acc += D.chunk_part[36 * (size_t)ch + lane];
+            T[lane] = acc;
+        } else if (i == j && lane < 42) {
+            const int k = lane - 36;
+            double t = 0.0;
+            for (int rs = D.hp_rs_start[i]; rs < D.hp_rs_start[i + 1]; rs++) t += D.bs_part[6 * (size_t)rs + k];
+            T[lane] = t;
+        }
+        __builtin_amdgcn_wave_barrier();
+        const double *Ri = D.hp_Rt + RT_STRIDE * (size_t)i, *Rj = D.hp_Rt + RT_STRIDE * (size_t)j;
+        if (lane < 36) {
+            const int r = lane / 6, c = lane % 6, kb = 3 * (r / 3), mb = 3 * (c / 3);
+            const double cj0 = Rj[12], cj1 = Rj[13], cj2 = Rj[14];
+            double sv = 0.0;
+            for (int k2 = 0; k2 < 3; k2++) {
+                const int k = kb + k2;
+                const double a0 = T[6 * k + 3], a1 = T[6 * k + 4], a2 = T[6 * k + 5];
+                const double corr[3] = {a1 * cj2 - a2 * cj1, a2 * cj0 - a0 * cj2, a0 * cj1 - a1 * cj0};
+                double row = 0.0;  // (T' D(R_j)^T)[k][c]
+                for (int m2 = 0; m2 < 3; m2++) {
+                    const int m = mb + m2;
+                    const double tp = m < 3 ? T[6 * k + m] - corr[m] : T[6 * k + m];
+                    row += tp * Rj[3 * (c % 3) + m2];
+                }
+                sv += Ri[3 * (r % 3) + k2] * row;
+            }
+            double v = -sv;
+            if (i == j) {
+                v += D.Hpp[36 * (size_t)i + lane];
+                if (r == c) v += lambda;
+            }
+            if (hs_stored(D, 6 * i + r, 6 * j + c)) D.Hs[hs_at(D, n, 6 * i + r, 6 * j + c)] = v;
+            if (i != j && hs_stored(D, 6 * j + c, 6 * i + r)) D.Hs[hs_at(D, n, 6 * j + c, 6 * i + r)] = v;
+        } else if (i == j && lane < 42) {
+            const int k = lane - 36, kb = 36 + 3 * (k / 3);
+            const double rv = Ri[3 * (k % 3)] * T[kb] + Ri[3 * (k % 3) + 1] * T[kb + 1] + Ri[3 * (k % 3) + 2] * T[kb + 2];
+            D.bs[6 * i + k] = D.bp[6 * (size_t)i + k] - rv;
+        }
+        return;
+    }
     if (lane < 36) {
         const int r = lane / 6, c = lane % 6;
         double acc = 0.0;
@@ -2545,10 +2511,10 @@ __global__ __launch_bounds__(EB) void k_update(const LbaDev *__restrict__ Ds)
     if (threadIdx.x == 0) D.part[D.npart + bx] = tot;
 }
 
-// k_update on the compact per-block factor (the default): the COOP form's one thread per block, with
-// Hpl_j rebuilt in registers (hpl_col, as k_schur_rows_c) from the block's M, its pose's R, t and its
-// landmark's position; each workgroup's landmark positions and each piece's block -> landmark map come
-// through LDS from the landmarks' threads.  The per-landmark sums keep the COOP order.
+// k_update on the compact per-block factor (the default): the COOP form's one thread per block, forming
+// Hpl^T x_p from the block's M', its pose's R and c and its landmark's position (z_rows' algebra); each
+// workgroup's landmark positions and each piece's block -> landmark map come through LDS from the
+// landmarks' threads.  The per-landmark sums keep the COOP order.
 __global__ __launch_bounds__(EB) void k_update_c(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT);
@@ -2582,24 +2548,26 @@ __global__ __launch_bounds__(EB) void k_update_c(const LbaDev *__restrict__ Ds)
         __syncthreads();
         const int blk = p0 + (int)threadIdx.x;
         if (blk < g1) {
+            // Hpl^T x_p = Z^T D(R)^T x_p = M' (y2 - (X + c) x y1), y = (R^T x_p[0:3], R^T x_p[3:6]) (z_rows)
             const int i1 = D.blk_pose[blk];
             const int ll = s_lm[threadIdx.x];
-            const double *R = D.hp_Rt + 12 * (size_t)i1;
-            double m[6], Rv[12];
+            const double *R = D.hp_Rt + RT_STRIDE * (size_t)i1;
+            double m[6], Rv[15], xp[6];
             for (int k = 0; k < 6; k++) m[k] = D.Hpl[6 * (size_t)blk + k];
-            for (int k = 0; k < 12; k++) Rv[k] = R[k];
-            const double X0 = s_xw[0][ll], X1 = s_xw[1][ll], X2 = s_xw[2][ll];
-            const double x = xc_coord(Rv, Rv[9], X0, X1, X2), y = xc_coord(Rv + 3, Rv[10], X0, X1, X2),
-                         z = xc_coord(Rv + 6, Rv[11], X0, X1, X2);
-            double xp[6];
-            for (int r = 0; r < 6; r++) xp[r] = -D.x[6 * i1 + r];
+            for (int k = 0; k < 15; k++) Rv[k] = R[k];
+            for (int r = 0; r < 6; r++) xp[r] = D.x[6 * i1 + r];
+            const double w0 = s_xw[0][ll] + Rv[12], w1 = s_xw[1][ll] + Rv[13], w2 = s_xw[2][ll] + Rv[14];
+            double y1[3], y2[3];
             for (int c = 0; c < 3; c++) {
-                double hc[6];
-                hpl_col(m, x, y, z, Rv[c], Rv[3 + c], Rv[6 + c], hc);
-                double s_ = 0;
-                for (int r = 0; r < 6; r++) s_ += hc[r] * xp[r];
-                s_v[c][threadIdx.x] = s_;
+                y1[c] = Rv[c] * xp[0] + Rv[3 + c] * xp[1] + Rv[6 + c] * xp[2];
+                y2[c] = Rv[c] * xp[3] + Rv[3 + c] * xp[4] + Rv[6 + c] * xp[5];
             }
+            const double u0 = y2[0] - (w1 * y1[2] - w2 * y1[1]);
+            const double u1 = y2[1] - (w2 * y1[0] - w0 * y1[2]);
+            const double u2 = y2[2] - (w0 * y1[1] - w1 * y1[0]);
+            s_v[0][threadIdx.x] = -(m[0] * u0 + m[1] * u1 + m[2] * u2);
+            s_v[1][threadIdx.x] = -(m[1] * u0 + m[3] * u1 + m[4] * u2);
+            s_v[2][threadIdx.x] = -(m[2] * u0 + m[4] * u1 + m[5] * u2);
         }
         __syncthreads();
         const int a1 = min(mb1, p0 + EB);
@@ -3337,7 +3305,7 @@ void carve_state(char *base, size_t &off, const LbaHost &H, LbaDev *D, bool prof
     double *Hll = carve<double>(base, off, 9 * (size_t)nhl);
     double *bl = carve<double>(base, off, 3 * (size_t)nhl);
     double *Hpl = carve<double>(base, off, (compact ? 6 : 18) * (size_t)nblk);  // the compact M, or Hpl
-    double *hp_Rt = carve<double>(base, off, 12 * (size_t)nhp);
+    double *hp_Rt = carve<double>(base, off, RT_STRIDE * (size_t)nhp);
     double *lmX = carve<double>(base, off, compact ? 3 * (size_t)nhl : 1);
     double *Hpp = carve<double>(base, off, 36 * (size_t)nhp);
     double *bp = carve<double>(base, off, 6 * (size_t)nhp);
