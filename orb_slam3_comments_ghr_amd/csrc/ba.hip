@@ -903,25 +903,23 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__
 }
 
 // The Schur product on the compact per-block factor (the default; see z_rows).  The same row segments,
-// chunks, MFMA layout and accumulation order as k_schur_rows<false>; what changes is what a contribution
-// reads (the partner block's M', 48 B, instead of its Hpl, 144 B) and that the products are summed in
-// the world frame, k_schur_pairs rotating each pose pair's sum once.
+// chunks, MFMA layout, group pipeline and accumulation order as k_schur_rows<false>; what changes is what
+// a contribution reads (the partner block's M', 48 B, instead of its Hpl, 144 B) and that the products
+// are summed in the world frame, k_schur_pairs rotating each pose pair's sum once.
 //   * BD staging: BD' = Z_a Dinv with Z_a = [[X + c_i]x M'_a ; M'_a] (pose i's c, the landmark's X from
 //     lmX, landmark order), and the segment's share of b_schur as sum Z_a Dinv b_l (rotated later too);
 //     X is kept in LDS per rank for the chunks.
-//   * Chunks: lane v holds contribution v's M' (loaded one whole chunk ahead: up to 64 loads in flight
-//     per wave, where the whole-Hpl form keeps one group of 16 in flight) and its landmark's X.  Per
-//     group of GC contributions the group's lanes write [[X]x M' ; M'] (18 FMA, no pose) into the wave's
-//     LDS tile, the transposed operand [-M'[X]x | M'] of the product; the MFMAs then run as before and a
-//     chunk's partial is [B | A] of the comment above z_rows.
+//   * Chunks, per group of GC contributions: lane 3 c + k (c < GC) loads column k of contribution c's M'
+//     (three 8-byte loads inside one 48-byte block, shared lines across the contribution's three lanes;
+//     one group ahead, as the whole-Hpl form's granules) and, at the group, writes column k of
+//     [[X]x M' ; M'] (X from LDS, 6 FMA, no pose) into the wave's LDS tile: the transposed operand
+//     [-M'[X]x | M'] of the product.  A chunk's partial is [B | A] of the comment above z_rows.
 template <int UNUSED = 0>
 __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT);
     if (bx >= D.n_rs) return;
     typedef int i4 __attribute__((ext_vector_type(4)));
-    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-    typedef double d2v __attribute__((ext_vector_type(2)));
     const i4 inf0 = ((const GLOBAL i4 *)gbl(D.rs_info))[2 * bx];
     const i4 inf1 = ((const GLOBAL i4 *)gbl(D.rs_info))[2 * bx + 1];
     const int rs = __builtin_amdgcn_readfirstlane(inf0.x), pi = __builtin_amdgcn_readfirstlane(inf0.y);
@@ -955,18 +953,23 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict
         mr = lane < d.z ? gbl(D.pair_rank)[d.y + lane] - rb : 0;
         mb = lane < d.z ? gbl(D.pair_b)[d.y + lane] : 0;
     };
-    // lane v: the M' of the chunk's contribution v
-    auto load_m = [&](const i4 &d, int mb, u4 (&Mr)[3]) {
-        if (lane < d.z) {
-#pragma unroll
-            for (int r = 0; r < 3; r++) Mr[r] = *(const GLOBAL u4 *)(Mv + 6 * (size_t)mb + 2 * r);
+    // the column roles: lane 3 rc + rk, rc < GC; column rk of the symmetric M' = (m00 m01 m02 m11 m12 m22)
+    const int rc = lane / 3, rk = lane - 3 * rc;
+    const bool rl = rc < GC;
+    const int mo0 = rk, mo1 = rk == 0 ? 1 : (rk == 1 ? 3 : 4), mo2 = rk == 0 ? 2 : (rk == 1 ? 4 : 5);
+    auto load_col = [&](int u0, int cnt, int mb, double (&Mc)[3]) {
+        const int bj = __shfl(mb, (u0 + rc) & 63);
+        if (rl && rc < cnt) {
+            const GLOBAL double *src = Mv + 6 * (size_t)bj;
+            Mc[0] = src[mo0];
+            Mc[1] = src[mo1];
+            Mc[2] = src[mo2];
         }
     };
     i4 dc = desc(t), dn = desc(t + RT / 64);
     int my_rank = 0, my_b = 0, n_rank = 0, n_b = 0;
     contrib(dc, my_rank, my_b);
     contrib(dn, n_rank, n_b);
-    u4 Mc[3], Mn[3];
     double cf[6] = {0, 0, 0, 0, 0, 0};
     {
         const double *ci = D.hp_Rt + RT_STRIDE * (size_t)pi + 12;  // pose i's c = R^T t
@@ -1002,7 +1005,6 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict
         }
         for (int k = 0; k < 6; k++) cf[k] = (k / 3 == h) ? c3[k % 3] : 0.0;
     }
-    load_m(dc, my_b, Mc);
     for (int k = 0; k < 6; k++) cf[k] = wave_sum(cf[k]);
     if (lane == 0)
         for (int k = 0; k < 6; k++) s_cf[wv][k] = cf[k];
@@ -1012,29 +1014,32 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict
         for (int w = 0; w < RT / 64; w++) tt += s_cf[w][threadIdx.x];
         D.bs_part[6 * (size_t)rs + threadIdx.x] = tt;
     }
+    double Mc[3] = {0, 0, 0};
+    load_col(0, dc.z, my_b, Mc);
     for (; t < t1; t += RT / 64) {
         const i4 d2 = desc(t + 2 * (RT / 64));
         const int nq = dc.z;
-        load_m(dn, n_b, Mn);  // the next chunk's M', one chunk ahead
-        // lane v: the landmark position of contribution v
-        const double X0 = s_xw[3 * my_rank], X1 = s_xw[3 * my_rank + 1], X2 = s_xw[3 * my_rank + 2];
         double acc0 = 0.0, acc1 = 0.0;
         for (int u = 0; u < nq; u += GC) {
             const int cnt = min(GC, nq - u);
-            if (lane >= u && lane < u + cnt) {
-                // contribution `lane`'s operand rows [[X]x M' ; M'] (6 x 3, row-major) into the tile
-                double m[6], Z[6][3];
-#pragma unroll
-                for (int r = 0; r < 3; r++) {
-                    m[2 * r] = __builtin_bit_cast(double, (unsigned long long)Mc[r].x | ((unsigned long long)Mc[r].y << 32));
-                    m[2 * r + 1] = __builtin_bit_cast(double, (unsigned long long)Mc[r].z | ((unsigned long long)Mc[r].w << 32));
+            {
+                // column rk of contribution u + rc's operand rows [[X]x M' ; M'] into the tile
+                const int rank = __shfl(my_rank, (u + rc) & 63);
+                const double x = s_xw[3 * rank], y = s_xw[3 * rank + 1], z = s_xw[3 * rank + 2];
+                if (rl && rc < cnt) {
+                    double *dst = hb + 18 * rc + rk;
+                    dst[0] = y * Mc[2] - z * Mc[1];
+                    dst[3] = z * Mc[0] - x * Mc[2];
+                    dst[6] = x * Mc[1] - y * Mc[0];
+                    dst[9] = Mc[0];
+                    dst[12] = Mc[1];
+                    dst[15] = Mc[2];
                 }
-                z_rows(m, X0, X1, X2, Z);
-                d2v *dst = (d2v *)(hb + 18 * (lane - u));
-#pragma unroll
-                for (int k = 0; k < 9; k++) dst[k] = d2v{Z[(2 * k) / 3][(2 * k) % 3], Z[(2 * k + 1) / 3][(2 * k + 1) % 3]};
             }
             __builtin_amdgcn_wave_barrier();
+            // next group: the rest of this chunk, else the first group of the next chunk
+            if (u + GC < nq) load_col(u + GC, nq - u - GC, my_b, Mc);
+            else load_col(0, dn.z, n_b, Mc);
             if (cnt == GC) {
 #pragma unroll
                 for (int v = 0; v < GC; v += 2) {
@@ -1065,8 +1070,6 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict
         dc = dn;
         my_rank = n_rank;
         my_b = n_b;
-#pragma unroll
-        for (int r = 0; r < 3; r++) Mc[r] = Mn[r];
         dn = d2;
         contrib(dn, n_rank, n_b);
     }
@@ -1255,22 +1258,26 @@ __global__ __launch_bounds__(256) void k_schur_pairs(const LbaDev *__restrict__ 
         }
         __builtin_amdgcn_wave_barrier();
         const double *Ri = D.hp_Rt + RT_STRIDE * (size_t)i, *Rj = D.hp_Rt + RT_STRIDE * (size_t)j;
+        __shared__ double s_U[4][36];
+        double *Uw = s_U[threadIdx.x >> 6];
         if (lane < 36) {
-            const int r = lane / 6, c = lane % 6, kb = 3 * (r / 3), mb = 3 * (c / 3);
-            const double cj0 = Rj[12], cj1 = Rj[13], cj2 = Rj[14];
-            double sv = 0.0;
-            for (int k2 = 0; k2 < 3; k2++) {
-                const int k = kb + k2;
-                const double a0 = T[6 * k + 3], a1 = T[6 * k + 4], a2 = T[6 * k + 5];
-                const double corr[3] = {a1 * cj2 - a2 * cj1, a2 * cj0 - a0 * cj2, a0 * cj1 - a1 * cj0};
-                double row = 0.0;  // (T' D(R_j)^T)[k][c]
-                for (int m2 = 0; m2 < 3; m2++) {
-                    const int m = mb + m2;
-                    const double tp = m < 3 ? T[6 * k + m] - corr[m] : T[6 * k + m];
-                    row += tp * Rj[3 * (c % 3) + m2];
-                }
-                sv += Ri[3 * (r % 3) + k2] * row;
+            const int r = lane / 6, c = lane % 6, mb = 3 * (c / 3);
+            // T' = [B - A [c_j]x | A] (element (r, c) of it), then U = T' D(R_j)^T, S = D(R_i) U
+            double tp = T[lane];
+            if (c < 3) {
+                const double cj0 = Rj[12], cj1 = Rj[13], cj2 = Rj[14];
+                const double a0 = T[6 * r + 3], a1 = T[6 * r + 4], a2 = T[6 * r + 5];
+                tp -= c == 0 ? a1 * cj2 - a2 * cj1 : (c == 1 ? a2 * cj0 - a0 * cj2 : a0 * cj1 - a1 * cj0);
             }
+            __builtin_amdgcn_wave_barrier();
+            T[lane] = tp;
+            __builtin_amdgcn_wave_barrier();
+            const double *rj = Rj + 3 * (c % 3);
+            Uw[lane] = T[6 * r + mb] * rj[0] + T[6 * r + mb + 1] * rj[1] + T[6 * r + mb + 2] * rj[2];
+            __builtin_amdgcn_wave_barrier();
+            const int kb = 3 * (r / 3);
+            const double *ri = Ri + 3 * (r % 3);
+            const double sv = ri[0] * Uw[6 * kb + c] + ri[1] * Uw[6 * (kb + 1) + c] + ri[2] * Uw[6 * (kb + 2) + c];
             double v = -sv;
             if (i == j) {
                 v += D.Hpp[36 * (size_t)i + lane];
