@@ -980,19 +980,32 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict
             const int r = r2 >> 1;
             const int a = gbl(D.hp_b)[hb0 + rb + r];
             const int l = gbl(D.hp_b_lm)[hb0 + rb + r];
-            double Di[9], db[3], m[6], Z[6][3];
+            // this thread's half of Z_a first (rows 3h .. 3h + 2: [X + c_i]x M' for h = 0, M' for h = 1), so
+            // that M' is dead before Dinv is formed (the whole Z beside Dinv spilled)
+            double Zh[3][3];
+            const double X0 = gbl(D.lmX)[3 * (size_t)l], X1 = gbl(D.lmX)[3 * (size_t)l + 1], X2 = gbl(D.lmX)[3 * (size_t)l + 2];
+            {
+                const GLOBAL double *mp = Mv + 6 * (size_t)a;
+                const double m00 = mp[0], m01 = mp[1], m02 = mp[2], m11 = mp[3], m12 = mp[4], m22 = mp[5];
+                const double M[3][3] = {{m00, m01, m02}, {m01, m11, m12}, {m02, m12, m22}};
+                const double x = X0 + c0, y = X1 + c1, z = X2 + c2;
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    Zh[0][k] = h ? M[0][k] : y * M[2][k] - z * M[1][k];
+                    Zh[1][k] = h ? M[1][k] : z * M[0][k] - x * M[2][k];
+                    Zh[2][k] = h ? M[2][k] : x * M[1][k] - y * M[0][k];
+                }
+            }
+            double Di[9], db[3];
             if (D.dinv_inline) {
                 landmark_dinv(D, l, lam, Di, db);
             } else {
                 for (int k = 0; k < 9; k++) Di[k] = gbl(D.Dinv)[9 * (size_t)l + k];
                 for (int k = 0; k < 3; k++) db[k] = gbl(D.db)[3 * (size_t)l + k];
             }
-            for (int k = 0; k < 6; k++) m[k] = Mv[6 * (size_t)a + k];
-            const double X0 = gbl(D.lmX)[3 * (size_t)l], X1 = gbl(D.lmX)[3 * (size_t)l + 1], X2 = gbl(D.lmX)[3 * (size_t)l + 2];
-            z_rows(m, X0 + c0, X1 + c1, X2 + c2, Z);
             double *BD = s_bd + 18 * r + 9 * h;
             for (int rr = 0; rr < 3; rr++) {
-                const double *B = Z[3 * h + rr];
+                const double *B = Zh[rr];
                 for (int c = 0; c < 3; c++)
                     BD[3 * rr + c] = B[0] * Di[c] + B[1] * Di[3 + c] + B[2] * Di[6 + c];
                 c3[rr] += B[0] * db[0] + B[1] * db[1] + B[2] * db[2];
