@@ -120,7 +120,7 @@ def parse():
                     help="per-launch HBM traffic from the rocprofv3 PMC passes (tools/gpu/gpu_profile_r03.sh)")
     ap.add_argument("--valu-pmc", default=os.path.join(ROOT, "profiles", "r03_top2_valu_pmc.json"),
                     help="the headline kernel's VALU counters (tools/pmc_valu.py)")
-    ap.add_argument("--schur-pmc", default=os.path.join(ROOT, "profiles", "r05_lba_pmc.json"),
+    ap.add_argument("--schur-pmc", default=os.path.join(ROOT, "profiles", "r06_lba_pmc.json"),
                     help="the LBA engine's SQ / MFMA / HBM counters (tools/pmc_kernel_summary.py)")
     ap.add_argument("--detail", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
                     help="file for the full per-stage record (stdout carries the compact line); '' for none")
