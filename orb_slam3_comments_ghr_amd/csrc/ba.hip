@@ -914,7 +914,8 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__
 //     one group ahead, as the whole-Hpl form's granules) and, at the group, writes column k of
 //     [[X]x M' ; M'] (X from LDS, 6 FMA, no pose) into the wave's LDS tile: the transposed operand
 //     [-M'[X]x | M'] of the product.  A chunk's partial is [B | A] of the comment above z_rows.
-template <int UNUSED = 0>
+// PF = 2 (OSG_SCHUR_PF=2, A/B): the gathers two groups ahead, a group pair at a time (see the loop)
+template <int PF = 1>
 __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT);
@@ -1028,6 +1029,78 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict
         D.bs_part[6 * (size_t)rs + threadIdx.x] = tt;
     }
     double Mc[3] = {0, 0, 0};
+    // one group of GC contributions: its operand rows into the tile, then its MFMAs
+    auto run_group = [&](int u, int cnt, const double (&Mg)[3], double &acc0, double &acc1) {
+        {
+            const int rank = __shfl(my_rank, (u + rc) & 63);
+            const double x = s_xw[3 * rank], y = s_xw[3 * rank + 1], z = s_xw[3 * rank + 2];
+            if (rl && rc < cnt) {
+                double *dst = hb + 18 * rc + rk;
+                dst[0] = y * Mg[2] - z * Mg[1];
+                dst[3] = z * Mg[0] - x * Mg[2];
+                dst[6] = x * Mg[1] - y * Mg[0];
+                dst[9] = Mg[0];
+                dst[12] = Mg[1];
+                dst[15] = Mg[2];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (cnt == GC) {
+#pragma unroll
+            for (int v = 0; v < GC; v += 2) {
+                const int r0 = __builtin_amdgcn_readlane(my_rank, u + v);
+                const int r1 = __builtin_amdgcn_readlane(my_rank, u + v + 1);
+                acc0 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[a_m * r0 + aoff], hb[18 * v + boff], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[a_m * r1 + aoff], hb[18 * (v + 1) + boff], acc1, 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int v = 0; v < GC; v += 2) {
+                if (v < cnt) {
+                    const int rank = __builtin_amdgcn_readlane(my_rank, u + v);
+                    acc0 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[a_m * rank + aoff], hb[18 * v + boff], acc0, 0, 0, 0);
+                }
+                if (v + 1 < cnt) {
+                    const int rank = __builtin_amdgcn_readlane(my_rank, u + v + 1);
+                    acc1 = __builtin_amdgcn_mfma_f64_4x4x4f64(s_bd[a_m * rank + aoff], hb[18 * (v + 1) + boff], acc1, 0,
+                                                              0, 0);
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    };
+    if (PF == 2) {
+        // group pairs (u, u + GC) of a chunk: the next pair's gathers (the rest of this chunk, else the
+        // next chunk's first pair) are issued before this pair's first group, so 2 GC contributions'
+        // loads are in flight while a pair runs; the same products in the same order
+        double M0[3] = {0, 0, 0}, M1[3] = {0, 0, 0};
+        load_col(0, dc.z, my_b, M0);
+        load_col(GC, dc.z - GC, my_b, M1);
+        for (; t < t1; t += RT / 64) {
+            const i4 d2 = desc(t + 2 * (RT / 64));
+            const int nq = dc.z;
+            double acc0 = 0.0, acc1 = 0.0;
+            for (int u = 0; u < nq; u += 2 * GC) {
+                const double P0[3] = {M0[0], M0[1], M0[2]}, P1[3] = {M1[0], M1[1], M1[2]};
+                if (u + 2 * GC < nq) {
+                    load_col(u + 2 * GC, nq - u - 2 * GC, my_b, M0);
+                    load_col(u + 3 * GC, nq - u - 3 * GC, my_b, M1);
+                } else {
+                    load_col(0, dn.z, n_b, M0);
+                    load_col(GC, dn.z - GC, n_b, M1);
+                }
+                run_group(u, min(GC, nq - u), P0, acc0, acc1);
+                if (u + GC < nq) run_group(u + GC, min(GC, nq - u - GC), P1, acc0, acc1);
+            }
+            if (orow < 6 && ocol < 6) D.chunk_part[36 * (size_t)dc.x + 6 * orow + ocol] = acc0 + acc1;
+            dc = dn;
+            my_rank = n_rank;
+            my_b = n_b;
+            dn = d2;
+            contrib(dn, n_rank, n_b);
+        }
+        return;
+    }
     load_col(0, dc.z, my_b, Mc);
     for (; t < t1; t += RT / 64) {
         const i4 d2 = desc(t + 2 * (RT / 64));
@@ -3415,6 +3488,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     static const bool hpl_full = (getenv("OSG_LBA_HPL") && atoi(getenv("OSG_LBA_HPL")) == 1) || schur_valu ||
                                  schur_stage || schur_direct || update_stage || !update_coop;
     const bool compact = !hpl_full;
+    // OSG_SCHUR_PF=2: k_schur_rows_c with its gathers two groups ahead (A/B runs; the same sums)
+    static const bool schur_pf2 = getenv("OSG_SCHUR_PF") && atoi(getenv("OSG_SCHUR_PF")) == 2;
     const auto tp0 = std::chrono::steady_clock::now();
     auto ms_since = [&](std::chrono::steady_clock::time_point t) {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
@@ -3728,7 +3803,10 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         if (schur_point) hipLaunchKernelGGL(k_schur_point, gx(mx_gl), dim3(EB), 0, ctx->stream, d_dev);
         if (mx_nhp > 0) {
             LBA_MARK(KT_SROWS);
-            if (compact) hipLaunchKernelGGL(k_schur_rows_c<0>, gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
+            if (compact) {
+                if (schur_pf2) hipLaunchKernelGGL(k_schur_rows_c<2>, gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
+                else hipLaunchKernelGGL(k_schur_rows_c<1>, gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
+            }
             else if (schur_valu) hipLaunchKernelGGL(k_schur_rows<true>, gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
             else if (schur_stage) hipLaunchKernelGGL(k_schur_rows_st, gx(mx_rs), dim3(RT2), 0, ctx->stream, d_dev);
             else if (schur_direct)
