@@ -641,8 +641,9 @@ def bench_lba(ctx, rank, world, dist, dev, args):
     dom = max(kernels, key=kernels.get)
     pmc = _load_json(args.schur_pmc)
     # the MFMA form: "k_schur_rows<false>" (r03 / r04 files) or "k_schur_rows<false, false>" (late r04)
-    pmc_sr = next((v for k, v in pmc.items() if k in (("k_schur_rows_c<0>",) if compact else
-                                                      ("k_schur_rows<false>", "k_schur_rows<false, false>"))), {})
+    # compact form: "k_schur_rows_c<0>" (first r06 file) or "k_schur_rows_c<1>" / "<2>" (gather-ahead depth)
+    pmc_sr = next((v for k, v in pmc.items() if (k.startswith("k_schur_rows_c<") if compact else
+                                                 k in ("k_schur_rows<false>", "k_schur_rows<false, false>"))), {})
     flop_iter = 72.6e6
     res = {
         "metric": "LocalBA iters/s", "value": round(bval, 1), "unit": "LM iterations/s",

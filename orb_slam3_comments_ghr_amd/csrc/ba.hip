@@ -914,7 +914,8 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__
 //     one group ahead, as the whole-Hpl form's granules) and, at the group, writes column k of
 //     [[X]x M' ; M'] (X from LDS, 6 FMA, no pose) into the wave's LDS tile: the transposed operand
 //     [-M'[X]x | M'] of the product.  A chunk's partial is [B | A] of the comment above z_rows.
-// PF = 2 (OSG_SCHUR_PF=2, A/B): the gathers two groups ahead, a group pair at a time (see the loop)
+// PF = 2 (the default): the gathers two groups ahead, a group pair at a time (see the loop); PF = 1
+// (OSG_SCHUR_PF=1) one group ahead
 template <int PF = 1>
 __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict__ Ds)
 {
@@ -3488,8 +3489,9 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     static const bool hpl_full = (getenv("OSG_LBA_HPL") && atoi(getenv("OSG_LBA_HPL")) == 1) || schur_valu ||
                                  schur_stage || schur_direct || update_stage || !update_coop;
     const bool compact = !hpl_full;
-    // OSG_SCHUR_PF=2: k_schur_rows_c with its gathers two groups ahead (A/B runs; the same sums)
-    static const bool schur_pf2 = getenv("OSG_SCHUR_PF") && atoi(getenv("OSG_SCHUR_PF")) == 2;
+    // k_schur_rows_c with its gathers two groups ahead (the default since late r06: 6.40 against 6.47 ms per
+    // 14 launches, gpurun_out/r06k); OSG_SCHUR_PF=1 one group ahead (A/B runs; the same sums)
+    static const bool schur_pf2 = !(getenv("OSG_SCHUR_PF") && atoi(getenv("OSG_SCHUR_PF")) == 1);
     const auto tp0 = std::chrono::steady_clock::now();
     auto ms_since = [&](std::chrono::steady_clock::time_point t) {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();

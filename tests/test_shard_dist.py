@@ -90,19 +90,22 @@ def test_merge_top2_no_row_below_sentinel(oracle):
 
 
 # ---------------------------------------------------------------- world_size 2 over gloo (CPU)
-def _c5_units(n_seq, frames_per_seq=2):
-    """Small C5-style sequences: per frame, a two-camera KB8 frame with LastF and local-map queries
-    and a pose problem (seeded by sequence, SURVEY.md §8(d) C5: seeds 0x0B5EED10 + seq)."""
+def _c5_units(n_seq, frames_per_seq=2, full=False):
+    """C5-style sequences: per frame, a two-camera KB8 frame with LastF and local-map queries and a pose
+    problem (seeded by sequence, SURVEY.md §8(d) C5: seeds 0x0B5EED10 + seq).  Small frames for the CPU
+    gloo test; full=True the bench's C5 frame (2 x 1000 keypoints, 2000 LastF and 1500 local-map
+    queries, a 600-edge pose problem)."""
+    nk, nl, nm, ne = (1000, 2000, 1500, 600) if full else (150, 200, 200, 60)
     from orb_slam3_comments_ghr_amd import frames as fr, optimizer as op
     seqs = []
     for s in range(n_seq):
         rng = np.random.default_rng(0x0B5EED10 + s)
         frames = []
         for _ in range(frames_per_seq):
-            F = fr.synth_frame_two_cam(rng, n_left=150, n_right=150, stereo_frac=0.5, width=512, height=512)
-            frames.append((F, fr.synth_last_queries_two_cam(rng, F, n_last=200),
-                           fr.synth_mp_queries_two_cam(rng, F, m=200), fr.synth_slots(rng, F.n, frac_assigned=0.05),
-                           op.synth_pose_problem(rng, n_edges=60, cam=op.kb8_camera(), body_frac=0.4)))
+            F = fr.synth_frame_two_cam(rng, n_left=nk, n_right=nk, stereo_frac=0.5, width=512, height=512)
+            frames.append((F, fr.synth_last_queries_two_cam(rng, F, n_last=nl),
+                           fr.synth_mp_queries_two_cam(rng, F, m=nm), fr.synth_slots(rng, F.n, frac_assigned=0.05),
+                           op.synth_pose_problem(rng, n_edges=ne, cam=op.kb8_camera(), body_frac=0.4)))
         seqs.append(frames)
     return seqs
 
@@ -238,7 +241,8 @@ def _c5_gpu_sequence(ctx, frames):
     return out
 
 
-N_SEQ_GPU = 5
+N_SEQ_GPU = 6
+FRAMES_GPU = 4  # full-size C5 frames
 
 
 def _gpu_c5_worker(rank, world, port, q):
@@ -248,7 +252,7 @@ def _gpu_c5_worker(rank, world, port, q):
     from orb_slam3_comments_ghr_amd import Context
     dist.init_process_group("gloo", rank=rank, world_size=world)
     ctx = Context(0)
-    seqs = _c5_units(N_SEQ_GPU, frames_per_seq=3)
+    seqs = _c5_units(N_SEQ_GPU, frames_per_seq=FRAMES_GPU, full=True)
     local = shard.run_sharded(lambda fr_: _c5_gpu_sequence(ctx, fr_), seqs, dist)
     everything = shard.gather_results(local, dist)
     ctx.close()
@@ -259,8 +263,9 @@ def _gpu_c5_worker(rank, world, port, q):
 
 @pytest.mark.gpu
 def test_c5_sequences_sharded_gpu_two_ranks(oracle):
-    """BASELINE config 5 in its sharded form on the HIP path: C5 sequences (two-camera KB8,
-    SearchByProjection x2 + PoseOptimization per frame) round-robin over two processes sharing
+    """BASELINE config 5 in its sharded form on the HIP path: C5 sequences of full-size frames (two-camera
+    KB8 2 x 1000 keypoints, SearchByProjection x2 + a 600-edge PoseOptimization per frame, 6 sequences
+    x 4 frames) round-robin over two processes sharing
     cuda:0, each through the C-ABI kernels, gathered once at the end; every rank's gathered results
     equal the single-process oracle run, sequence by sequence, bit for bit."""
     world = 2
@@ -274,7 +279,7 @@ def test_c5_sequences_sharded_gpu_two_ranks(oracle):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    seqs = _c5_units(N_SEQ_GPU, frames_per_seq=3)
+    seqs = _c5_units(N_SEQ_GPU, frames_per_seq=FRAMES_GPU, full=True)
     want = {i: _c5_oracle_sequence(oracle, s) for i, s in enumerate(seqs)}
     owned = set()
     for rank, mine, everything in res:
