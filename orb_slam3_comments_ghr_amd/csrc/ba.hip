@@ -916,8 +916,9 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__
 //     [-M'[X]x | M'] of the product.  A chunk's partial is [B | A] of the comment above z_rows.
 // PF = 2 (the default): the gathers two groups ahead, a group pair at a time (see the loop); PF = 1
 // (OSG_SCHUR_PF=1) one group ahead
-template <int PF = 1>
-__global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict__ Ds)
+// WPE: the waves per SIMD the register allocation must allow (6: 80 VGPRs with a few spilled; 5: 92, none)
+template <int PF = 1, int WPE = 6>
+__global__ __launch_bounds__(RT, WPE) void k_schur_rows_c(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT);
     if (bx >= D.n_rs) return;
@@ -1070,15 +1071,26 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict
         }
         __builtin_amdgcn_wave_barrier();
     };
-    if (PF == 2) {
+    if (PF >= 2) {
         // group pairs (u, u + GC) of a chunk: the next pair's gathers (the rest of this chunk, else the
         // next chunk's first pair) are issued before this pair's first group, so 2 GC contributions'
         // loads are in flight while a pair runs; the same products in the same order
         double M0[3] = {0, 0, 0}, M1[3] = {0, 0, 0};
         load_col(0, dc.z, my_b, M0);
         load_col(GC, dc.z - GC, my_b, M1);
+        // PF == 3: a chunk is mostly one group, so the chain descriptor -> (rank, block) -> M' spans
+        // iterations: descriptors are loaded four chunks ahead (raw, in VGPRs) and made uniform three
+        // ahead, and a chunk's (rank, block) loads then never wait on a descriptor of the same iteration
+        auto desc_raw = [&](int tt) -> i4 { return tt < t1 ? cd[tt] : i4{0, 0, 0, 0}; };
+        auto uni = [&](const i4 &d) -> i4 {
+            return i4{__builtin_amdgcn_readfirstlane(d.x), __builtin_amdgcn_readfirstlane(d.y),
+                      __builtin_amdgcn_readfirstlane(d.z), 0};
+        };
+        i4 dn2 = PF == 3 ? desc(t + 2 * (RT / 64)) : i4{0, 0, 0, 0};
+        i4 raw1 = PF == 3 ? desc_raw(t + 3 * (RT / 64)) : i4{0, 0, 0, 0};
         for (; t < t1; t += RT / 64) {
-            const i4 d2 = desc(t + 2 * (RT / 64));
+            const i4 d2 = PF == 3 ? i4{0, 0, 0, 0} : desc(t + 2 * (RT / 64));
+            const i4 raw0 = PF == 3 ? desc_raw(t + 4 * (RT / 64)) : i4{0, 0, 0, 0};
             const int nq = dc.z;
             double acc0 = 0.0, acc1 = 0.0;
             for (int u = 0; u < nq; u += 2 * GC) {
@@ -1097,7 +1109,13 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows_c(const LbaDev *__restrict
             dc = dn;
             my_rank = n_rank;
             my_b = n_b;
-            dn = d2;
+            if (PF == 3) {
+                dn = dn2;
+                dn2 = uni(raw1);
+                raw1 = raw0;
+            } else {
+                dn = d2;
+            }
             contrib(dn, n_rank, n_b);
         }
         return;
@@ -3491,7 +3509,10 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     const bool compact = !hpl_full;
     // k_schur_rows_c with its gathers two groups ahead (the default since late r06: 6.40 against 6.47 ms per
     // 14 launches, gpurun_out/r06k); OSG_SCHUR_PF=1 one group ahead (A/B runs; the same sums)
-    static const bool schur_pf2 = !(getenv("OSG_SCHUR_PF") && atoi(getenv("OSG_SCHUR_PF")) == 1);
+    // OSG_SCHUR_PF=3: also the chunk descriptors four chunks ahead (A/B)
+    static const int schur_pf = getenv("OSG_SCHUR_PF") ? std::min(3, std::max(1, atoi(getenv("OSG_SCHUR_PF")))) : 2;
+    // OSG_SCHUR_WPE=5: k_schur_rows_c allocated for 5 waves per SIMD (92 VGPRs, no spills) instead of 6 (A/B)
+    static const bool schur_wpe5 = getenv("OSG_SCHUR_WPE") && atoi(getenv("OSG_SCHUR_WPE")) == 5;
     const auto tp0 = std::chrono::steady_clock::now();
     auto ms_since = [&](std::chrono::steady_clock::time_point t) {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
@@ -3806,8 +3827,10 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         if (mx_nhp > 0) {
             LBA_MARK(KT_SROWS);
             if (compact) {
-                if (schur_pf2) hipLaunchKernelGGL(k_schur_rows_c<2>, gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
-                else hipLaunchKernelGGL(k_schur_rows_c<1>, gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
+                auto sr = schur_pf == 3 ? (schur_wpe5 ? k_schur_rows_c<3, 5> : k_schur_rows_c<3, 6>)
+                          : schur_pf == 2 ? (schur_wpe5 ? k_schur_rows_c<2, 5> : k_schur_rows_c<2, 6>)
+                                          : k_schur_rows_c<1, 6>;
+                hipLaunchKernelGGL(sr, gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
             }
             else if (schur_valu) hipLaunchKernelGGL(k_schur_rows<true>, gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
             else if (schur_stage) hipLaunchKernelGGL(k_schur_rows_st, gx(mx_rs), dim3(RT2), 0, ctx->stream, d_dev);
