@@ -13,6 +13,10 @@ EXACT = -ffp-contract=off
 ifdef POSE_PROF
 HIPFLAGS += -DOSG_POSE_PROF
 endif
+# make SR_PROF=1: k_schur_rows_c's per-workgroup timeline (tools/sr_prof.py)
+ifdef SR_PROF
+HIPFLAGS += -DOSG_SR_PROF
+endif
 HDRS = include/osg.h include/osg_ba.h $(CSRC)/osg_internal.h
 
 OBJS = $(OBJDIR)/runtime.o $(OBJDIR)/hamming.o $(OBJDIR)/hamming_mfma.o $(OBJDIR)/match.o $(OBJDIR)/pose.o $(OBJDIR)/ba.o $(OBJDIR)/dbow.o $(OBJDIR)/fuse.o $(OBJDIR)/triang.o $(OBJDIR)/desc.o $(OBJDIR)/sim3.o $(OBJDIR)/init.o $(OBJDIR)/stereo.o $(OBJDIR)/orb.o $(OBJDIR)/fast.o $(OBJDIR)/pyramid.o

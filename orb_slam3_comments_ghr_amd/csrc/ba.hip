@@ -917,11 +917,22 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__
 // PF = 2 (the default): the gathers two groups ahead, a group pair at a time (see the loop); PF = 1
 // (OSG_SCHUR_PF=1) one group ahead
 // WPE: the waves per SIMD the register allocation must allow (6: 80 VGPRs with a few spilled; 5: 92, none)
+#ifdef OSG_SR_PROF
+// profiling builds only (make SR_PROF=1): per workgroup of graph 0, wall-clock ticks (100 MHz) at the start,
+// after the BD staging and at each wave's end, the segment's chunk count and blocks, the XCC / CU it ran on
+constexpr int SR_PROF_N = 1024;
+__device__ unsigned long long g_sr_prof[SR_PROF_N][13];
+#define SR_PROF_AT(slot) \
+    if (by == 0 && bx < SR_PROF_N && (threadIdx.x & 63) == 0) g_sr_prof[bx][slot] = wall_clock64()
+#else
+#define SR_PROF_AT(slot)
+#endif
 template <int PF = 1, int WPE = 6>
 __global__ __launch_bounds__(RT, WPE) void k_schur_rows_c(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT);
     if (bx >= D.n_rs) return;
+    if (threadIdx.x == 0) SR_PROF_AT(0);
     typedef int i4 __attribute__((ext_vector_type(4)));
     const i4 inf0 = ((const GLOBAL i4 *)gbl(D.rs_info))[2 * bx];
     const i4 inf1 = ((const GLOBAL i4 *)gbl(D.rs_info))[2 * bx + 1];
@@ -1025,6 +1036,7 @@ __global__ __launch_bounds__(RT, WPE) void k_schur_rows_c(const LbaDev *__restri
     if (lane == 0)
         for (int k = 0; k < 6; k++) s_cf[wv][k] = cf[k];
     __syncthreads();
+    if (threadIdx.x == 0) SR_PROF_AT(1);
     if (threadIdx.x < 6) {
         double tt = 0.0;
         for (int w = 0; w < RT / 64; w++) tt += s_cf[w][threadIdx.x];
@@ -1118,6 +1130,16 @@ __global__ __launch_bounds__(RT, WPE) void k_schur_rows_c(const LbaDev *__restri
             }
             contrib(dn, n_rank, n_b);
         }
+#ifdef OSG_SR_PROF
+        SR_PROF_AT(2 + wv);
+        if (by == 0 && bx < SR_PROF_N && threadIdx.x == 0) {
+            g_sr_prof[bx][10] = (unsigned long long)(t1 - __builtin_amdgcn_readfirstlane(inf1.y));
+            g_sr_prof[bx][11] = (unsigned long long)nr;
+            // XCC_ID (hardware register 20, bits 0..3) and HW_ID (4) bits 8..15 (CU, SH, SE)
+            g_sr_prof[bx][12] = (unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) |
+                                ((unsigned long long)__builtin_amdgcn_s_getreg((7 << 11) | (8 << 6) | 4) << 32);
+        }
+#endif
         return;
     }
     load_col(0, dc.z, my_b, Mc);
@@ -3940,6 +3962,17 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
             if (rc < 0) return rc;
         }
         steps++;
+#ifdef OSG_SR_PROF
+        // profiling builds: graph 0's k_schur_rows_c timeline of the third step to $OSG_SR_PROF_OUT (raw u64)
+        if (steps == 3 && getenv("OSG_SR_PROF_OUT")) {
+            std::vector<unsigned long long> hp((size_t)SR_PROF_N * 13);
+            OSG_HIP_CHECK(ctx, hipMemcpyFromSymbol(hp.data(), HIP_SYMBOL(g_sr_prof), hp.size() * sizeof(unsigned long long)));
+            if (FILE *f = fopen(getenv("OSG_SR_PROF_OUT"), "wb")) {
+                fwrite(hp.data(), sizeof(unsigned long long), hp.size(), f);
+                fclose(f);
+            }
+        }
+#endif
         if (prof_ts && !ts_printed && H[act[0]].nhp > 0) {
             ts_printed = true;
             const LbaDev &D0 = h_dev[0];
