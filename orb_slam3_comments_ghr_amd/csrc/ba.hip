@@ -129,6 +129,12 @@ struct LbaDev {
     double *chi2o;                       // per edge chi2 of the last computed error (classification)
     double *err;                         // 3 per edge
     double *Hll, *bl, *Hpl, *Hpp, *bp;
+    // per landmark: Hll (3 x 3), b_l (3) and, compact, its position (lmX) at strides ls_h / ls_b / ls_x: three
+    // arrays (strides 9, 3, 3) by default; OSG_LBA_LREC=1 one 128-byte record per landmark (stride 16: Hll at
+    // 0, b_l at 9, X at 12), one line per landmark for the Schur staging's scattered reads but strided for
+    // the landmark-parallel kernels: k_schur_rows_c 5.99 against 5.95-6.04 ms, k_linearize 1.82 against
+    // 1.70 and k_update_c 1.50 against 1.29 ms per 14 launches (A/B runs, the same values)
+    int ls_h, ls_b, ls_x;
     // the compact per-block factor (the default; OSG_LBA_HPL=1 stores Hpl whole): 6 doubles per block,
     // the symmetric M' = sum over the block's edges of J_point^T rho' W J_point (see z_rows), in Hpl's storage
     int compact;
@@ -424,12 +430,12 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
         }
         if (COMPACT && owner) {
             const int p = D.hl_point[ol];
-            for (int k = 0; k < 3; k++) D.lmX[3 * (size_t)ol + k] = points[3 * (size_t)p + k];
+            for (int k = 0; k < 3; k++) D.lmX[D.ls_x * (size_t)ol + k] = points[3 * (size_t)p + k];
         }
         if (owner) {
             const double H[9] = {H6[0], H6[1], H6[2], H6[1], H6[3], H6[4], H6[2], H6[4], H6[5]};
-            for (int i = 0; i < 9; i++) D.Hll[9 * (size_t)ol + i] = H[i];
-            for (int i = 0; i < 3; i++) D.bl[3 * (size_t)ol + i] = bl3[i];
+            for (int i = 0; i < 9; i++) D.Hll[D.ls_h * (size_t)ol + i] = H[i];
+            for (int i = 0; i < 3; i++) D.bl[D.ls_b * (size_t)ol + i] = bl3[i];
             md = fmax(fabs(H[0]), fmax(fabs(H[4]), fabs(H[8])));
         }
     }
@@ -610,13 +616,13 @@ __global__ void k_lambda_init(const LbaDev *__restrict__ Ds)
 __device__ inline void landmark_dinv(const LbaDev &D, int l, double lambda, double *Di, double *db)
 {
     double Dm[9];
-    for (int i = 0; i < 9; i++) Dm[i] = D.Hll[9 * (size_t)l + i];
+    for (int i = 0; i < 9; i++) Dm[i] = D.Hll[D.ls_h * (size_t)l + i];
     Dm[0] += lambda;
     Dm[4] += lambda;
     Dm[8] += lambda;
     inv3(Dm, Di);
     if (db) {
-        const double *b = D.bl + 3 * (size_t)l;
+        const double *b = D.bl + D.ls_b * (size_t)l;
         for (int r = 0; r < 3; r++) db[r] = Di[3 * r] * b[0] + Di[3 * r + 1] * b[1] + Di[3 * r + 2] * b[2];
     }
 }
@@ -916,7 +922,7 @@ __global__ __launch_bounds__(RT, 6) void k_schur_rows(const LbaDev *__restrict__
 //     [-M'[X]x | M'] of the product.  A chunk's partial is [B | A] of the comment above z_rows.
 // PF = 2 (the default): the gathers two groups ahead, a group pair at a time (see the loop); PF = 1
 // (OSG_SCHUR_PF=1) one group ahead
-// WPE: the waves per SIMD the register allocation must allow (6: 80 VGPRs with a few spilled; 5: 92, none)
+// WPE: the waves per SIMD the register allocation must allow (6: 80 VGPRs; 5: 92)
 #ifdef OSG_SR_PROF
 // profiling builds only (make SR_PROF=1): per workgroup of graph 0, wall-clock ticks (100 MHz) at the start,
 // after the BD staging and at each wave's end, the segment's chunk count and blocks, the XCC / CU it ran on
@@ -927,7 +933,10 @@ __device__ unsigned long long g_sr_prof[SR_PROF_N][13];
 #else
 #define SR_PROF_AT(slot)
 #endif
-template <int PF = 1, int WPE = 6>
+// HOIST (OSG_SCHUR_HOIST=1, A/B): the first group's gathers are issued between the staging's index loads and
+// its block loads, so their latency overlaps the staging instead of following it (15 VGPRs spilled in the
+// staging for it; without it the kernel allocates 80 VGPRs with none)
+template <int PF = 1, int WPE = 6, bool HOIST = false>
 __global__ __launch_bounds__(RT, WPE) void k_schur_rows_c(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT);
@@ -985,19 +994,24 @@ __global__ __launch_bounds__(RT, WPE) void k_schur_rows_c(const LbaDev *__restri
     contrib(dc, my_rank, my_b);
     contrib(dn, n_rank, n_b);
     double cf[6] = {0, 0, 0, 0, 0, 0};
+    double M0[3] = {0, 0, 0}, M1[3] = {0, 0, 0};  // PF >= 2: the gathers of the wave's first group pair
+    static_assert(2 * RS <= RT, "one block per thread pair in the staging");
     {
         const double *ci = D.hp_Rt + RT_STRIDE * (size_t)pi + 12;  // pose i's c = R^T t
         const double c0 = ci[0], c1 = ci[1], c2 = ci[2];
         const int h = threadIdx.x & 1;  // two threads per block: rows 3h .. 3h + 2
         double c3[3] = {0, 0, 0};
-        for (int r2 = threadIdx.x; r2 < 2 * nr; r2 += RT) {
-            const int r = r2 >> 1;
-            const int a = gbl(D.hp_b)[hb0 + rb + r];
-            const int l = gbl(D.hp_b_lm)[hb0 + rb + r];
+        const bool st = (int)threadIdx.x < 2 * nr;
+        const int r = threadIdx.x >> 1;
+        const int a = st ? gbl(D.hp_b)[hb0 + rb + r] : 0;
+        const int l = st ? gbl(D.hp_b_lm)[hb0 + rb + r] : 0;
+        if (HOIST) load_col(0, dc.z, my_b, M0);
+        if (st) {
             // this thread's half of Z_a first (rows 3h .. 3h + 2: [X + c_i]x M' for h = 0, M' for h = 1), so
             // that M' is dead before Dinv is formed (the whole Z beside Dinv spilled)
             double Zh[3][3];
-            const double X0 = gbl(D.lmX)[3 * (size_t)l], X1 = gbl(D.lmX)[3 * (size_t)l + 1], X2 = gbl(D.lmX)[3 * (size_t)l + 2];
+            const double X0 = gbl(D.lmX)[D.ls_x * (size_t)l], X1 = gbl(D.lmX)[D.ls_x * (size_t)l + 1],
+                         X2 = gbl(D.lmX)[D.ls_x * (size_t)l + 2];
             {
                 const GLOBAL double *mp = Mv + 6 * (size_t)a;
                 const double m00 = mp[0], m01 = mp[1], m02 = mp[2], m11 = mp[3], m12 = mp[4], m22 = mp[5];
@@ -1009,6 +1023,11 @@ __global__ __launch_bounds__(RT, WPE) void k_schur_rows_c(const LbaDev *__restri
                     Zh[1][k] = h ? M[1][k] : z * M[0][k] - x * M[2][k];
                     Zh[2][k] = h ? M[2][k] : x * M[1][k] - y * M[0][k];
                 }
+            }
+            if (h == 0) {  // X is dead from here on
+                s_xw[3 * r] = X0;
+                s_xw[3 * r + 1] = X1;
+                s_xw[3 * r + 2] = X2;
             }
             double Di[9], db[3];
             if (D.dinv_inline) {
@@ -1023,11 +1042,6 @@ __global__ __launch_bounds__(RT, WPE) void k_schur_rows_c(const LbaDev *__restri
                 for (int c = 0; c < 3; c++)
                     BD[3 * rr + c] = B[0] * Di[c] + B[1] * Di[3 + c] + B[2] * Di[6 + c];
                 c3[rr] += B[0] * db[0] + B[1] * db[1] + B[2] * db[2];
-            }
-            if (h == 0) {
-                s_xw[3 * r] = X0;
-                s_xw[3 * r + 1] = X1;
-                s_xw[3 * r + 2] = X2;
             }
         }
         for (int k = 0; k < 6; k++) cf[k] = (k / 3 == h) ? c3[k % 3] : 0.0;
@@ -1087,8 +1101,7 @@ __global__ __launch_bounds__(RT, WPE) void k_schur_rows_c(const LbaDev *__restri
         // group pairs (u, u + GC) of a chunk: the next pair's gathers (the rest of this chunk, else the
         // next chunk's first pair) are issued before this pair's first group, so 2 GC contributions'
         // loads are in flight while a pair runs; the same products in the same order
-        double M0[3] = {0, 0, 0}, M1[3] = {0, 0, 0};
-        load_col(0, dc.z, my_b, M0);
+        if (!HOIST) load_col(0, dc.z, my_b, M0);
         load_col(GC, dc.z - GC, my_b, M1);
         // PF == 3: a chunk is mostly one group, so the chain descriptor -> (rank, block) -> M' spans
         // iterations: descriptors are loaded four chunks ahead (raw, in VGPRs) and made uniform three
@@ -2544,9 +2557,9 @@ __global__ __launch_bounds__(EB) void k_update(const LbaDev *__restrict__ Ds)
     double sc = 0.0;
     double cl[3] = {0, 0, 0};
     if (t < D.nhl) {
-        cl[0] = D.bl[3 * (size_t)t];
-        cl[1] = D.bl[3 * (size_t)t + 1];
-        cl[2] = D.bl[3 * (size_t)t + 2];
+        cl[0] = D.bl[D.ls_b * (size_t)t];
+        cl[1] = D.bl[D.ls_b * (size_t)t + 1];
+        cl[2] = D.bl[D.ls_b * (size_t)t + 2];
     }
     if (STAGE) {
         __shared__ double s_b[UB * 18];
@@ -2620,7 +2633,7 @@ __global__ __launch_bounds__(EB) void k_update(const LbaDev *__restrict__ Ds)
             const double xl = Di[3 * r] * cl[0] + Di[3 * r + 1] * cl[1] + Di[3 * r + 2] * cl[2];
             D.x[sp + 3 * l + r] = xl;
             point_new[3 * (size_t)p + r] = point_cur[3 * (size_t)p + r] + xl;
-            sc += xl * (lambda * xl + D.bl[3 * (size_t)l + r]);
+            sc += xl * (lambda * xl + D.bl[D.ls_b * (size_t)l + r]);
         }
     }
     if (t < D.np) {  // poses: exp(x) * T for free active poses, copy otherwise
@@ -2670,9 +2683,9 @@ __global__ __launch_bounds__(EB) void k_update_c(const LbaDev *__restrict__ Ds)
     const int mb0 = t < D.nhl ? D.lm_b_start[t] : 0, mb1 = t < D.nhl ? D.lm_b_start[t + 1] : 0;
     int p = -1;
     if (t < D.nhl) {
-        cl[0] = D.bl[3 * (size_t)t];
-        cl[1] = D.bl[3 * (size_t)t + 1];
-        cl[2] = D.bl[3 * (size_t)t + 2];
+        cl[0] = D.bl[D.ls_b * (size_t)t];
+        cl[1] = D.bl[D.ls_b * (size_t)t + 1];
+        cl[2] = D.bl[D.ls_b * (size_t)t + 2];
         p = D.hl_point[t];
         for (int k = 0; k < 3; k++) s_xw[k][threadIdx.x] = point_cur[3 * (size_t)p + k];
     }
@@ -2721,7 +2734,7 @@ __global__ __launch_bounds__(EB) void k_update_c(const LbaDev *__restrict__ Ds)
             const double xl = Di[3 * r] * cl[0] + Di[3 * r + 1] * cl[1] + Di[3 * r + 2] * cl[2];
             D.x[sp + 3 * l + r] = xl;
             point_new[3 * (size_t)p + r] = point_cur[3 * (size_t)p + r] + xl;
-            sc += xl * (lambda * xl + D.bl[3 * (size_t)l + r]);
+            sc += xl * (lambda * xl + D.bl[D.ls_b * (size_t)l + r]);
         }
     }
     if (t < D.np) {  // poses: exp(x) * T for free active poses, copy otherwise
@@ -3436,11 +3449,12 @@ void carve_state(char *base, size_t &off, const LbaHost &H, LbaDev *D, bool prof
     double *qA = carve<double>(base, off, 3 * (size_t)npt);
     double *qB = carve<double>(base, off, 3 * (size_t)npt);
     double *err = carve<double>(base, off, 3 * (size_t)ne);
-    double *Hll = carve<double>(base, off, 9 * (size_t)nhl);
-    double *bl = carve<double>(base, off, 3 * (size_t)nhl);
+    static const bool lrec = getenv("OSG_LBA_LREC") && atoi(getenv("OSG_LBA_LREC")) == 1;
+    double *Hll = carve<double>(base, off, (lrec ? 16 : 9) * (size_t)nhl);
+    double *bl = lrec ? Hll + 9 : carve<double>(base, off, 3 * (size_t)nhl);
     double *Hpl = carve<double>(base, off, (compact ? 6 : 18) * (size_t)nblk);  // the compact M, or Hpl
     double *hp_Rt = carve<double>(base, off, RT_STRIDE * (size_t)nhp);
-    double *lmX = carve<double>(base, off, compact ? 3 * (size_t)nhl : 1);
+    double *lmX = lrec ? Hll + 12 : carve<double>(base, off, compact ? 3 * (size_t)nhl : 1);
     double *Hpp = carve<double>(base, off, 36 * (size_t)nhp);
     double *bp = carve<double>(base, off, 6 * (size_t)nhp);
     double *Dinv = carve<double>(base, off, 9 * (size_t)nhl);
@@ -3467,6 +3481,9 @@ void carve_state(char *base, size_t &off, const LbaHost &H, LbaDev *D, bool prof
     D->err = err;
     D->Hll = Hll;
     D->bl = bl;
+    D->ls_h = lrec ? 16 : 9;
+    D->ls_b = lrec ? 16 : 3;
+    D->ls_x = lrec ? 16 : 3;
     D->Hpl = Hpl;
     D->hp_Rt = hp_Rt;
     D->lmX = lmX;
@@ -3535,6 +3552,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     static const int schur_pf = getenv("OSG_SCHUR_PF") ? std::min(3, std::max(1, atoi(getenv("OSG_SCHUR_PF")))) : 2;
     // OSG_SCHUR_WPE=5: k_schur_rows_c allocated for 5 waves per SIMD (92 VGPRs, no spills) instead of 6 (A/B)
     static const bool schur_wpe5 = getenv("OSG_SCHUR_WPE") && atoi(getenv("OSG_SCHUR_WPE")) == 5;
+    // OSG_SCHUR_HOIST=1: k_schur_rows_c's first gathers issued inside the staging (A/B)
+    static const bool schur_hoist = getenv("OSG_SCHUR_HOIST") && atoi(getenv("OSG_SCHUR_HOIST")) == 1;
     const auto tp0 = std::chrono::steady_clock::now();
     auto ms_since = [&](std::chrono::steady_clock::time_point t) {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
@@ -3850,7 +3869,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
             LBA_MARK(KT_SROWS);
             if (compact) {
                 auto sr = schur_pf == 3 ? (schur_wpe5 ? k_schur_rows_c<3, 5> : k_schur_rows_c<3, 6>)
-                          : schur_pf == 2 ? (schur_wpe5 ? k_schur_rows_c<2, 5> : k_schur_rows_c<2, 6>)
+                          : schur_pf == 2 ? (schur_wpe5 ? k_schur_rows_c<2, 5>
+                                                        : (schur_hoist ? k_schur_rows_c<2, 6, true> : k_schur_rows_c<2, 6>))
                                           : k_schur_rows_c<1, 6>;
                 hipLaunchKernelGGL(sr, gx(mx_rs), dim3(RT), 0, ctx->stream, d_dev);
             }
