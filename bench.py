@@ -55,9 +55,10 @@ PEAK_I8_TOPS = 256 * 4 * 1024 * 2 * 2.4e9 / 1e12
 # FP4 (e2m1) block-scaled v_mfma_scale_f32_32x32x64_f8f6f4: the BF16 form's cycles at 4x K, twice the I8 rate
 PEAK_FP4_TOPS = 2 * PEAK_I8_TOPS
 I8_OPS_PER_PAIR = 512          # 256 MACs per (query, train row) pair
-# the matrix-core forms' top-2 epilogue per key: v_min3_i32 + v_med3_i32 + v_min_i32 per two keys, plus the
-# 4 rebasing subtractions per 16 keys of a 32-row tile (28 VALU ops per tile per wave)
-MFMA_EPILOGUE_VALU_PER_PAIR = 1.75
+# the FP4 top-2 epilogue per key, as compiled (r06): per two keys one v_med3_f32 and one v_min3_i32, the k2
+# chain merged into one v_min3_i32 per two pairs, plus 2 rebasing subtractions per tile: 22 VALU ops per
+# 32-row tile per wave (30 before r06's key_push2f, csrc/hamming_mfma.hip)
+MFMA_EPILOGUE_VALU_PER_PAIR = 22 / 16
 MFMA_MAX_ROWS = 8192           # the I8 kernel's 13-bit row field (osg_top2_mfma_max_rows)
 LINE_MAX_BYTES = 8192          # the stdout line's budget (the driver did not parse r04's 21 KB line)
 

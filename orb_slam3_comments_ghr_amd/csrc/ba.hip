@@ -2622,12 +2622,11 @@ __global__ __launch_bounds__(EB) void k_update(const LbaDev *__restrict__ Ds)
                     cl[c] += s_;
                 }
             }
-        double Dv[9];
-        const double *Di = D.Dinv + 9 * (size_t)l;
-        if (D.dinv_inline) {
-            landmark_dinv(D, l, lambda, Dv, nullptr);
-            Di = Dv;
-        }
+        // Dinv into registers from either source (a pointer to a local-or-global array put it in scratch)
+        double Di[9];
+        if (D.dinv_inline) landmark_dinv(D, l, lambda, Di, nullptr);
+        else
+            for (int k = 0; k < 9; k++) Di[k] = D.Dinv[9 * (size_t)l + k];
         const int p = D.hl_point[l];
         for (int r = 0; r < 3; r++) {
             const double xl = Di[3 * r] * cl[0] + Di[3 * r + 1] * cl[1] + Di[3 * r + 2] * cl[2];
@@ -2724,12 +2723,11 @@ __global__ __launch_bounds__(EB) void k_update_c(const LbaDev *__restrict__ Ds)
     }
     if (t < D.nhl) {
         const int l = t;
-        double Dv[9];
-        const double *Di = D.Dinv + 9 * (size_t)l;
-        if (D.dinv_inline) {
-            landmark_dinv(D, l, lambda, Dv, nullptr);
-            Di = Dv;
-        }
+        // Dinv into registers from either source (a pointer to a local-or-global array put it in scratch)
+        double Di[9];
+        if (D.dinv_inline) landmark_dinv(D, l, lambda, Di, nullptr);
+        else
+            for (int k = 0; k < 9; k++) Di[k] = D.Dinv[9 * (size_t)l + k];
         for (int r = 0; r < 3; r++) {
             const double xl = Di[3 * r] * cl[0] + Di[3 * r + 1] * cl[1] + Di[3 * r + 2] * cl[2];
             D.x[sp + 3 * l + r] = xl;

@@ -89,6 +89,19 @@ __device__ __forceinline__ void key_push2(int &k1, int &k2, int x, int y)
     k2 = min(m, k2);
 }
 
+// key_push2 for the FP4 path, whose keys are the bit patterns of positive normal floats (MX_BIAS, MX_KEY0
+// below): their float order is their integer order, so the median is taken as v_med3_f32 on the same bits.
+// Written this way the compiler selects one v_med3_f32 and one v_min3_i32 per pair and merges the k2 chain
+// into v_min3_i32 (22 VALU ops per 32-row tile against 30 for key_push2, whose med3 and min3 patterns share
+// the min(k1, x) node so that half the k1 updates become two v_min_i32).  Not for the I8 path: its keys can
+// be negative integers.
+__device__ __forceinline__ void key_push2f(int &k1, int &k2, int x, int y)
+{
+    const int m = __float_as_int(__builtin_amdgcn_fmed3f(__int_as_float(k1), __int_as_float(x), __int_as_float(y)));
+    k1 = min(min(x, y), k1);
+    k2 = min(m, k2);
+}
+
 __device__ __forceinline__ void key_merge(int &k1, int &k2, int a1, int a2)
 {
     const int hi = max(k1, a1);
@@ -471,8 +484,8 @@ __global__ __launch_bounds__(NW * 64) void k_top2_fp4(const uint32_t *__restrict
         for (int j = 0; j < QT; j++) {
 #pragma unroll
             for (int i = 0; i < 8; i += 2) {
-                key_push2(ka1[j], ka2[j], __float_as_int(acc[j][i]), __float_as_int(acc[j][i + 1]));
-                key_push2(kc1[j], kc2[j], __float_as_int(acc[j][i + 8]), __float_as_int(acc[j][i + 9]));
+                key_push2f(ka1[j], ka2[j], __float_as_int(acc[j][i]), __float_as_int(acc[j][i + 1]));
+                key_push2f(kc1[j], kc2[j], __float_as_int(acc[j][i + 8]), __float_as_int(acc[j][i + 9]));
             }
             ka1[j] -= 32;
             ka2[j] -= 32;
@@ -557,7 +570,7 @@ __global__ __launch_bounds__(NW * 64) void k_top2_fp4(const uint32_t *__restrict
                                     for (int j = 0; j < QT; j++)
 #pragma unroll
                                         for (int e = 0; e < 16; e += 2)
-                                            key_push2(ka1[j], ka2[j], __float_as_int(accp[j][e]),
+                                            key_push2f(ka1[j], ka2[j], __float_as_int(accp[j][e]),
                                                       __float_as_int(accp[j][e + 1]));
                                 }
 #pragma unroll
@@ -581,14 +594,14 @@ __global__ __launch_bounds__(NW * 64) void k_top2_fp4(const uint32_t *__restrict
                                 for (int p = 0; p < 8; p++) {
                                     if (p / 3 + 1 != s) continue;
                                     const int e = (p & 3) * 2 + (p >> 2) * 8;
-                                    if (p < 4) key_push2(ka1[j], ka2[j], __float_as_int(accp[j][e]), __float_as_int(accp[j][e + 1]));
-                                    else key_push2(kb1[j], kb2[j], __float_as_int(accp[j][e]), __float_as_int(accp[j][e + 1]));
+                                    if (p < 4) key_push2f(ka1[j], ka2[j], __float_as_int(accp[j][e]), __float_as_int(accp[j][e + 1]));
+                                    else key_push2f(kb1[j], kb2[j], __float_as_int(accp[j][e]), __float_as_int(accp[j][e + 1]));
                                 }
                             } else {
                                 // pairs 2 s (chain A: elements 4 s, 4 s + 1 ... ) and 2 s + 1 (chain B)
-                                key_push2(ka1[j], ka2[j], __float_as_int(accp[j][2 * s]),
+                                key_push2f(ka1[j], ka2[j], __float_as_int(accp[j][2 * s]),
                                           __float_as_int(accp[j][2 * s + 1]));
-                                key_push2(kc1[j], kc2[j], __float_as_int(accp[j][8 + 2 * s]),
+                                key_push2f(kc1[j], kc2[j], __float_as_int(accp[j][8 + 2 * s]),
                                           __float_as_int(accp[j][9 + 2 * s]));
                             }
                             if (s == 3) {
@@ -690,9 +703,9 @@ bool mfma_fp4()
 void mfma_shape_of(bool fp4, int shape, int *d)
 {
     static const int i8[5][4] = {{16, 1, 256, 1}, {8, 2, 256, 1}, {16, 1, 256, 0}, {8, 2, 256, 0}, {8, 1, 256, 1}};
-    static const int f4[9][4] = {{16, 1, 256, 3}, {8, 2, 256, 1}, {16, 1, 256, 0}, {16, 1, 256, 3}, {8, 1, 256, 1},
-                                 {16, 2, 256, 1}, {16, 1, 256, 2}, {16, 1, 256, 1}, {16, 1, 256, 4}};
-    const int *s = fp4 ? f4[(shape >= 1 && shape <= 8 && shape != 3) ? shape : 0]
+    static const int f4[10][4] = {{16, 1, 256, 3}, {8, 2, 256, 1}, {16, 1, 256, 0}, {16, 1, 256, 3}, {8, 1, 256, 1},
+                                  {16, 2, 256, 1}, {16, 1, 256, 2}, {16, 1, 256, 1}, {16, 1, 256, 4}, {8, 1, 256, 3}};
+    const int *s = fp4 ? f4[(shape >= 1 && shape <= 9 && shape != 3) ? shape : 0]
                        : i8[(shape >= 1 && shape <= 4) ? shape : 0];
     for (int i = 0; i < 4; i++) d[i] = s[i];
 }
@@ -729,6 +742,7 @@ int osg_launch_top2_batch_mfma(osg_ctx *ctx, const void *d_query, int32_t nq, co
         case 6: return launch_fp4<16, 1, 256, 2>(ctx, d_query, nq, d_train, nt, nb, d_out);
         case 7: return launch_fp4<16, 1, 256, 1>(ctx, d_query, nq, d_train, nt, nb, d_out);
         case 8: return launch_fp4<16, 1, 256, 4>(ctx, d_query, nq, d_train, nt, nb, d_out);
+        case 9: return launch_fp4<8, 1, 256, 3>(ctx, d_query, nq, d_train, nt, nb, d_out);
         default: return launch_fp4<16, 1, 256, 3>(ctx, d_query, nq, d_train, nt, nb, d_out);
         }
     }
