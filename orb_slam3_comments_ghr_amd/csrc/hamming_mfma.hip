@@ -416,7 +416,10 @@ __global__ __launch_bounds__(NW * 64) void k_top2_fp4(const uint32_t *__restrict
     // two fewer rebasing subtractions per tile and no merge of the halves, a longer dependent chain per
     // lane; 852 -> 841 VALU ops, +1.8 % on the headline step (profiles/r05_top2_fp4_onechain.jsonl).
     // The two-pair form stays as OSG_TOP2_MFMA_SHAPE=7.
-    constexpr bool ONE = PIPE == 3 || PIPE == 4;
+    constexpr bool ONE = PIPE == 3 || PIPE == 4 || PIPE == 5;
+    // PIPE == 5: PIPE 3, and a chunk with fewer full tiles (the last one) also runs the pipelined block,
+    // leaving it after its last full tile, instead of one unpipelined tile() per full tile
+    constexpr bool PART = PIPE == 5;
     int(&kc1)[QT] = ONE ? ka1 : kb1;
     int(&kc2)[QT] = ONE ? ka2 : kb2;
     int pq[QT];
@@ -525,7 +528,7 @@ __global__ __launch_bounds__(NW * 64) void k_top2_fp4(const uint32_t *__restrict
         if (active) {
             const unsigned char *sb = s_buf + (size_t)(c & 1) * CR * MX_RS;
             const int nfull = min(NTILE, (nt - c0) / 32);
-            if (PIPE && nfull == NTILE) {
+            if (PIPE && (nfull == NTILE || (PART && nfull >= 1))) {
                 // K-step s of tile t issues its MFMAs, refills the A register it consumed with tile
                 // t + 1's granule, and performs key pairs 2 s, 2 s + 1 of tile t - 1 (as k_top2_mfma)
                 i32x8 a[4];
@@ -541,6 +544,7 @@ __global__ __launch_bounds__(NW * 64) void k_top2_fp4(const uint32_t *__restrict
                 }
 #pragma unroll
                 for (int tt = 1; tt < NTILE; tt++) {
+                    if (PART && tt >= nfull) break;  // accp holds the last full tile (epi below)
 #pragma unroll
                     for (int s = 0; s < 4; s++) {
 #pragma unroll
@@ -703,9 +707,10 @@ bool mfma_fp4()
 void mfma_shape_of(bool fp4, int shape, int *d)
 {
     static const int i8[5][4] = {{16, 1, 256, 1}, {8, 2, 256, 1}, {16, 1, 256, 0}, {8, 2, 256, 0}, {8, 1, 256, 1}};
-    static const int f4[10][4] = {{16, 1, 256, 3}, {8, 2, 256, 1}, {16, 1, 256, 0}, {16, 1, 256, 3}, {8, 1, 256, 1},
-                                  {16, 2, 256, 1}, {16, 1, 256, 2}, {16, 1, 256, 1}, {16, 1, 256, 4}, {8, 1, 256, 3}};
-    const int *s = fp4 ? f4[(shape >= 1 && shape <= 9 && shape != 3) ? shape : 0]
+    static const int f4[13][4] = {{16, 1, 256, 3}, {8, 2, 256, 1}, {16, 1, 256, 0}, {16, 1, 256, 3}, {8, 1, 256, 1},
+                                  {16, 2, 256, 1}, {16, 1, 256, 2}, {16, 1, 256, 1}, {16, 1, 256, 4}, {8, 1, 256, 3},
+                                  {16, 1, 512, 3}, {16, 1, 256, 5}, {16, 1, 512, 5}};
+    const int *s = fp4 ? f4[(shape >= 1 && shape <= 12 && shape != 3) ? shape : 0]
                        : i8[(shape >= 1 && shape <= 4) ? shape : 0];
     for (int i = 0; i < 4; i++) d[i] = s[i];
 }
@@ -743,6 +748,9 @@ int osg_launch_top2_batch_mfma(osg_ctx *ctx, const void *d_query, int32_t nq, co
         case 7: return launch_fp4<16, 1, 256, 1>(ctx, d_query, nq, d_train, nt, nb, d_out);
         case 8: return launch_fp4<16, 1, 256, 4>(ctx, d_query, nq, d_train, nt, nb, d_out);
         case 9: return launch_fp4<8, 1, 256, 3>(ctx, d_query, nq, d_train, nt, nb, d_out);
+        case 10: return launch_fp4<16, 1, 512, 3>(ctx, d_query, nq, d_train, nt, nb, d_out);
+        case 11: return launch_fp4<16, 1, 256, 5>(ctx, d_query, nq, d_train, nt, nb, d_out);
+        case 12: return launch_fp4<16, 1, 512, 5>(ctx, d_query, nq, d_train, nt, nb, d_out);
         default: return launch_fp4<16, 1, 256, 3>(ctx, d_query, nq, d_train, nt, nb, d_out);
         }
     }
