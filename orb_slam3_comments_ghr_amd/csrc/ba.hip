@@ -501,13 +501,20 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(3, 8))) void
     // those of a stored-Jacobian reduction, without writing / reading EC doubles per edge)
     const SE3 T = se3_from7(cur_pose(D) + 7 * (size_t)D.hp_pose[i]);
     const double *points = cur_point(D);
-    for (int q = D.hp_e_start[i] + threadIdx.x; q < D.hp_e_start[i + 1]; q += EB) {
+    typedef int i4 __attribute__((ext_vector_type(4)));
+    // REC: the thread's next record is loaded one edge ahead, so an edge waits for its point and error
+    // (which the record indexes) but not for the record itself
+    const int q_end = D.hp_e_start[i + 1];
+    i4 rnext = i4{0, 0, 0, 0};
+    if (REC && D.hp_e_start[i] + (int)threadIdx.x < q_end)
+        rnext = *(const GLOBAL i4 *)(gbl(D.hp_rec) + 4 * (size_t)(D.hp_e_start[i] + threadIdx.x));
+    for (int q = D.hp_e_start[i] + threadIdx.x; q < q_end; q += EB) {
         int e, k, cam, pt;
         bool robust;
         double w;
         if (REC) {
-            typedef int i4 __attribute__((ext_vector_type(4)));
-            const i4 r = *(const i4 *)(D.hp_rec + 4 * (size_t)q);
+            const i4 r = rnext;
+            if (q + EB < q_end) rnext = *(const GLOBAL i4 *)(gbl(D.hp_rec) + 4 * (size_t)(q + EB));
             e = r.x;
             pt = r.y;
             cam = r.z & 0xffff;
@@ -1381,54 +1388,81 @@ __global__ __launch_bounds__(256) void k_schur_pairs(const LbaDev *__restrict__ 
     const int n = 6 * D.nhp;
     if (D.compact) {
         // the compact factor's chunks summed [B | A] in the world frame (see z_rows): the pair's sum T,
-        // then S_ij = D(R_i) [B - A [c_j]x | A] D(R_j)^T; b_schur's share likewise D(R_i) v
+        // then S_ij = D(R_i) [B - A [c_j]x | A] D(R_j)^T; b_schur's share likewise D(R_i) v.  A wave is a chain
+        // of memory round trips, so the lane's rotation operands (and Hpp on the diagonal) are loaded before
+        // the sums, and the sums load four partials at a time (added in the same order)
         __shared__ double s_T[4][48];
         double *T = s_T[threadIdx.x >> 6];
-        if (lane < 36) {
+        const GLOBAL double *Ri = gbl(D.hp_Rt) + RT_STRIDE * (size_t)i, *Rj = gbl(D.hp_Rt) + RT_STRIDE * (size_t)j;
+        const int r = lane / 6, c = lane % 6, k6 = lane - 36;
+        const bool prow = lane < 36, brow = !prow && i == j && lane < 42;
+        double ri[3] = {0, 0, 0}, rj[3] = {0, 0, 0}, cj[3] = {0, 0, 0}, hpp = 0.0;
+        if (prow) {
+            for (int q = 0; q < 3; q++) {
+                ri[q] = Ri[3 * (r % 3) + q];
+                rj[q] = Rj[3 * (c % 3) + q];
+                cj[q] = Rj[12 + q];
+            }
+            if (i == j) hpp = gbl(D.Hpp)[36 * (size_t)i + lane];
+        } else if (brow) {
+            for (int q = 0; q < 3; q++) ri[q] = Ri[3 * (k6 % 3) + q];
+        }
+        // sum_{t in [t0, t1)} src[stride t], in t order, four loads in flight
+        auto ordered_sum = [](const GLOBAL double *src, size_t stride, int t0, int t1) {
             double acc = 0.0;
+            int t = t0;
+            for (; t + 4 <= t1; t += 4) {
+                const double v0 = src[stride * t], v1 = src[stride * (t + 1)], v2 = src[stride * (t + 2)],
+                             v3 = src[stride * (t + 3)];
+                acc += v0;
+                acc += v1;
+                acc += v2;
+                acc += v3;
+            }
+            const int rem = t1 - t;
+            const double w0 = rem > 0 ? src[stride * t] : 0.0, w1 = rem > 1 ? src[stride * (t + 1)] : 0.0,
+                         w2 = rem > 2 ? src[stride * (t + 2)] : 0.0;
+            if (rem > 0) acc += w0;
+            if (rem > 1) acc += w1;
+            if (rem > 2) acc += w2;
+            return acc;
+        };
+        if (prow) {
             const int ch0 = D.live_chunk ? D.live_chunk[2 * slot] : D.pair_chunk[wave];
             const int ch1 = D.live_chunk ? D.live_chunk[2 * slot + 1] : D.pair_chunk[wave + 1];
-            for (int ch = ch0; ch < ch1; ch++) acc += D.chunk_part[36 * (size_t)ch + lane];
-            T[lane] = acc;
-        } else if (i == j && lane < 42) {
-            const int k = lane - 36;
-            double t = 0.0;
-            for (int rs = D.hp_rs_start[i]; rs < D.hp_rs_start[i + 1]; rs++) t += D.bs_part[6 * (size_t)rs + k];
-            T[lane] = t;
+            T[lane] = ordered_sum(gbl(D.chunk_part) + lane, 36, ch0, ch1);
+        } else if (brow) {
+            T[lane] = ordered_sum(gbl(D.bs_part) + k6, 6, D.hp_rs_start[i], D.hp_rs_start[i + 1]);
         }
         __builtin_amdgcn_wave_barrier();
-        const double *Ri = D.hp_Rt + RT_STRIDE * (size_t)i, *Rj = D.hp_Rt + RT_STRIDE * (size_t)j;
         __shared__ double s_U[4][36];
         double *Uw = s_U[threadIdx.x >> 6];
-        if (lane < 36) {
-            const int r = lane / 6, c = lane % 6, mb = 3 * (c / 3);
+        if (prow) {
+            const int mb = 3 * (c / 3);
             // T' = [B - A [c_j]x | A] (element (r, c) of it), then U = T' D(R_j)^T, S = D(R_i) U
             double tp = T[lane];
             if (c < 3) {
-                const double cj0 = Rj[12], cj1 = Rj[13], cj2 = Rj[14];
                 const double a0 = T[6 * r + 3], a1 = T[6 * r + 4], a2 = T[6 * r + 5];
-                tp -= c == 0 ? a1 * cj2 - a2 * cj1 : (c == 1 ? a2 * cj0 - a0 * cj2 : a0 * cj1 - a1 * cj0);
+                tp -= c == 0 ? a1 * cj[2] - a2 * cj[1] : (c == 1 ? a2 * cj[0] - a0 * cj[2] : a0 * cj[1] - a1 * cj[0]);
             }
             __builtin_amdgcn_wave_barrier();
             T[lane] = tp;
             __builtin_amdgcn_wave_barrier();
-            const double *rj = Rj + 3 * (c % 3);
             Uw[lane] = T[6 * r + mb] * rj[0] + T[6 * r + mb + 1] * rj[1] + T[6 * r + mb + 2] * rj[2];
             __builtin_amdgcn_wave_barrier();
             const int kb = 3 * (r / 3);
-            const double *ri = Ri + 3 * (r % 3);
             const double sv = ri[0] * Uw[6 * kb + c] + ri[1] * Uw[6 * (kb + 1) + c] + ri[2] * Uw[6 * (kb + 2) + c];
             double v = -sv;
             if (i == j) {
-                v += D.Hpp[36 * (size_t)i + lane];
+                v += hpp;
                 if (r == c) v += lambda;
             }
             if (hs_stored(D, 6 * i + r, 6 * j + c)) D.Hs[hs_at(D, n, 6 * i + r, 6 * j + c)] = v;
             if (i != j && hs_stored(D, 6 * j + c, 6 * i + r)) D.Hs[hs_at(D, n, 6 * j + c, 6 * i + r)] = v;
-        } else if (i == j && lane < 42) {
-            const int k = lane - 36, kb = 36 + 3 * (k / 3);
-            const double rv = Ri[3 * (k % 3)] * T[kb] + Ri[3 * (k % 3) + 1] * T[kb + 1] + Ri[3 * (k % 3) + 2] * T[kb + 2];
-            D.bs[6 * i + k] = D.bp[6 * (size_t)i + k] - rv;
+        } else if (brow) {
+            const int kb = 36 + 3 * (k6 / 3);
+            const double rv = ri[0] * T[kb] + ri[1] * T[kb + 1] + ri[2] * T[kb + 2];
+            D.bs[6 * i + k6] = D.bp[6 * (size_t)i + k6] - rv;
         }
         return;
     }
@@ -2688,18 +2722,32 @@ __global__ __launch_bounds__(EB) void k_update_c(const LbaDev *__restrict__ Ds)
         p = D.hl_point[t];
         for (int k = 0; k < 3; k++) s_xw[k][threadIdx.x] = point_cur[3 * (size_t)p + k];
     }
+    // the thread's block of the next piece (its pose and M') is loaded one piece ahead, so a piece waits
+    // for its pose's R, c and x_p only
+    int i1n = 0;
+    double mn[6] = {0, 0, 0, 0, 0, 0};
+    auto fetch = [&](int p) {
+        const int blk = p + (int)threadIdx.x;
+        if (blk < g1) {
+            i1n = gbl(D.blk_pose)[blk];
+            for (int k = 0; k < 6; k++) mn[k] = gbl(D.Hpl)[6 * (size_t)blk + k];
+        }
+    };
+    if (g0 < g1) fetch(g0);
     for (int p0 = g0; p0 < g1; p0 += EB) {  // workgroup-uniform
+        const int i1 = i1n;
+        double m[6];
+        for (int k = 0; k < 6; k++) m[k] = mn[k];
+        if (p0 + EB < g1) fetch(p0 + EB);
         // the piece's block -> landmark (local index) map, from the landmarks' threads
         for (int b2 = max(mb0, p0); b2 < min(mb1, p0 + EB); b2++) s_lm[b2 - p0] = threadIdx.x;
         __syncthreads();
         const int blk = p0 + (int)threadIdx.x;
         if (blk < g1) {
             // Hpl^T x_p = Z^T D(R)^T x_p = M' (y2 - (X + c) x y1), y = (R^T x_p[0:3], R^T x_p[3:6]) (z_rows)
-            const int i1 = D.blk_pose[blk];
             const int ll = s_lm[threadIdx.x];
             const double *R = D.hp_Rt + RT_STRIDE * (size_t)i1;
-            double m[6], Rv[15], xp[6];
-            for (int k = 0; k < 6; k++) m[k] = D.Hpl[6 * (size_t)blk + k];
+            double Rv[15], xp[6];
             for (int k = 0; k < 15; k++) Rv[k] = R[k];
             for (int r = 0; r < 6; r++) xp[r] = D.x[6 * i1 + r];
             const double w0 = s_xw[0][ll] + Rv[12], w1 = s_xw[1][ll] + Rv[13], w2 = s_xw[2][ll] + Rv[14];
