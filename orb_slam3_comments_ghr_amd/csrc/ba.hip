@@ -91,6 +91,8 @@ struct LbaDev {
     const int32_t *point_h;       // per point: landmark index or -1
     const int32_t *hl_point;      // per landmark: point index
     const int32_t *lm_e_start, *lm_e;    // edges per landmark
+    int lm_e_ident;                      // lm_e[q] == q for every q (edges given landmark by landmark, as
+                                         // LocalBundleAdjustment inserts them): k_linearize skips the lookup
     const int32_t *lg_start;             // k_linearize's landmark groups: <= EB edges, or one landmark
     const int32_t *lm_b_start;           // blocks per landmark (blocks are numbered landmark-major)
     const int32_t *blk_pose;             // per block: hessian pose index
@@ -359,7 +361,9 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
         for (int c0 = q0; c0 < q1; c0 += EB) {
             const int q = c0 + (int)threadIdx.x;
             if (q < q1) {
-                const int e = D.lm_e[q];
+                // the identity map saves the edge loads one dependent level
+                int e = q;
+                if (!D.lm_e_ident) e = D.lm_e[q];
                 const int k = D.e_kind[e];
                 const SE3 T = se3_from7(poses + 7 * (size_t)D.e_pose[e]);
                 double Jp[3][6], Jx[3][3];
@@ -417,7 +421,7 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                     for (int c = 0; c < 6; c++) H6[c] += s_t[c][t];
                     for (int a = 0; a < 3; a++) bl3[a] += s_t[6 + a][t];
                     if (MULTI) {
-                        const int code = D.edge_blk[D.lm_e[qq]];
+                        const int code = D.edge_blk[D.lm_e_ident ? qq : D.lm_e[qq]];
                         if (code >= 0 && (code & 2)) {
                             double *hp = D.Hpl + HN * (size_t)(code >> 2);
                             const bool first = !(code & 1);
@@ -997,6 +1001,11 @@ __global__ __launch_bounds__(RT, WPE) void k_schur_rows_c(const LbaDev *__restri
         }
     };
     i4 dc = desc(t), dn = desc(t + RT / 64);
+    // PF == 4: the wave's chunks t + 8 k, one descriptor per lane (k < 64), loaded before the staging, so no
+    // chunk waits for its descriptor (desc() of the chunk two ahead waited at the top of every iteration)
+    const int nchw = t < t1 ? (t1 - t + RT / 64 - 1) / (RT / 64) : 0;
+    i4 dl = i4{0, 0, 0, 0};
+    if (PF == 4 && lane < nchw) dl = cd[t + (RT / 64) * lane];
     int my_rank = 0, my_b = 0, n_rank = 0, n_b = 0;
     contrib(dc, my_rank, my_b);
     contrib(dn, n_rank, n_b);
@@ -1118,6 +1127,71 @@ __global__ __launch_bounds__(RT, WPE) void k_schur_rows_c(const LbaDev *__restri
             return i4{__builtin_amdgcn_readfirstlane(d.x), __builtin_amdgcn_readfirstlane(d.y),
                       __builtin_amdgcn_readfirstlane(d.z), 0};
         };
+        if (PF == 4) {
+            // the descriptors come from dl by readlane; the (rank, block) loads of chunk k + 2 are issued at
+            // the top of chunk k and hold raw values until its end (the "- rb" right after a load made it wait
+            // at once), so every load has a whole chunk to land
+            auto dsc = [&](int k) -> i4 {
+                if (k >= nchw) return i4{0, 0, 0, 0};
+                if (k < 64)
+                    return i4{__builtin_amdgcn_readlane(dl.x, k), __builtin_amdgcn_readlane(dl.y, k),
+                              __builtin_amdgcn_readlane(dl.z, k), 0};
+                return desc(t + (RT / 64) * k);  // past 64 chunks of one wave (rare): a direct load
+            };
+            // loads without branches: a load under a lane guard is skipped by a branch when no lane needs
+            // it, and across such branches the compiler cannot count the loads in flight, so it waits for
+            // all of them (vmcnt(0)); a clamped index keeps every load in the straight line
+            auto contrib_raw = [&](const i4 &d, int &mr, int &mb) {
+                const int qi = d.y + min(lane, max(d.z - 1, 0));
+                const int vr = gbl(D.pair_rank)[qi], vb = gbl(D.pair_b)[qi];
+                mr = lane < d.z ? vr : rb;
+                mb = lane < d.z ? vb : 0;
+            };
+            auto load_col_u = [&](int u0, int cnt, int mb, double (&Mc)[3]) {
+                const int bs = __shfl(mb, (u0 + rc) & 63);  // every lane takes part: bpermute reads
+                const int bj = (rl && rc < cnt) ? bs : 0;     // nothing from lanes outside EXEC
+                const GLOBAL double *src = Mv + 6 * (size_t)bj;
+                Mc[0] = src[mo0];
+                Mc[1] = src[mo1];
+                Mc[2] = src[mo2];
+            };
+            int nrr = n_rank + rb;  // chunk k + 1's raw rank (n_rank came through contrib)
+            // one chunk: dcur's contributions in (my_rank, my_b); the next chunk's in (nrr, n_b)
+            auto chunk = [&](int k, int &la, int &lb) {
+                const i4 dcur = dsc(k), dnext = dsc(k + 1), dnn = dsc(k + 2);
+                contrib_raw(dnn, la, lb);
+                const int nq = dcur.z;
+                double acc0 = 0.0, acc1 = 0.0;
+                for (int u = 0; u < nq; u += 2 * GC) {
+                    double N0[3], N1[3];
+                    const bool inner = u + 2 * GC < nq;
+                    const int u2 = inner ? u + 2 * GC : 0, c2 = inner ? nq - u - 2 * GC : dnext.z;
+                    const int mbn = inner ? my_b : n_b;
+                    load_col_u(u2, c2, mbn, N0);
+                    load_col_u(u2 + GC, c2 - GC, mbn, N1);
+                    run_group(u, min(GC, nq - u), M0, acc0, acc1);
+                    if (u + GC < nq) run_group(u + GC, min(GC, nq - u - GC), M1, acc0, acc1);
+#pragma unroll
+                    for (int q = 0; q < 3; q++) {
+                        M0[q] = N0[q];
+                        M1[q] = N1[q];
+                    }
+                }
+                if (orow < 6 && ocol < 6) D.chunk_part[36 * (size_t)dcur.x + 6 * orow + ocol] = acc0 + acc1;
+                my_rank = nrr - rb;
+                my_b = n_b;
+            };
+            for (int k = 0; k < nchw; k++) {
+                int la = rb, lb = 0;
+                chunk(k, la, lb);  // chunk k + 2's loads into (la, lb) at its top
+                nrr = la;          // ... the next chunk's "next"
+                n_b = lb;
+            }
+#ifdef OSG_SR_PROF
+            SR_PROF_AT(2 + wv);
+#endif
+            return;
+        }
         i4 dn2 = PF == 3 ? desc(t + 2 * (RT / 64)) : i4{0, 0, 0, 0};
         i4 raw1 = PF == 3 ? desc_raw(t + 3 * (RT / 64)) : i4{0, 0, 0, 0};
         for (; t < t1; t += RT / 64) {
@@ -1126,16 +1200,24 @@ __global__ __launch_bounds__(RT, WPE) void k_schur_rows_c(const LbaDev *__restri
             const int nq = dc.z;
             double acc0 = 0.0, acc1 = 0.0;
             for (int u = 0; u < nq; u += 2 * GC) {
-                const double P0[3] = {M0[0], M0[1], M0[2]}, P1[3] = {M1[0], M1[1], M1[2]};
+                // the next pair's gathers land in N0 / N1 and move into M0 / M1 after this pair's groups: a
+                // copy at the top (the loop-carried registers reused by the new loads) waited for the last
+                // pair's gathers before the next ones were even issued
+                double N0[3] = {0, 0, 0}, N1[3] = {0, 0, 0};
                 if (u + 2 * GC < nq) {
-                    load_col(u + 2 * GC, nq - u - 2 * GC, my_b, M0);
-                    load_col(u + 3 * GC, nq - u - 3 * GC, my_b, M1);
+                    load_col(u + 2 * GC, nq - u - 2 * GC, my_b, N0);
+                    load_col(u + 3 * GC, nq - u - 3 * GC, my_b, N1);
                 } else {
-                    load_col(0, dn.z, n_b, M0);
-                    load_col(GC, dn.z - GC, n_b, M1);
+                    load_col(0, dn.z, n_b, N0);
+                    load_col(GC, dn.z - GC, n_b, N1);
                 }
-                run_group(u, min(GC, nq - u), P0, acc0, acc1);
-                if (u + GC < nq) run_group(u + GC, min(GC, nq - u - GC), P1, acc0, acc1);
+                run_group(u, min(GC, nq - u), M0, acc0, acc1);
+                if (u + GC < nq) run_group(u + GC, min(GC, nq - u - GC), M1, acc0, acc1);
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    M0[k] = N0[k];
+                    M1[k] = N1[k];
+                }
             }
             if (orow < 6 && ocol < 6) D.chunk_part[36 * (size_t)dc.x + 6 * orow + ocol] = acc0 + acc1;
             dc = dn;
@@ -2883,6 +2965,7 @@ struct LbaHost {
     std::vector<int32_t> live_chunk, env_off;  // per live pair its chunk range; envelope tiles before each row block
     int max_col_rows = 0;
     bool trivial = false;  // nothing to optimise: the estimates are returned unchanged
+    int lm_e_ident = 0;
     std::vector<int32_t> pose_h, hp_pose, point_h, hl_point, lm_e_start, lm_e, lg_start, lm_b_start, blk_pose, edge_blk, blk_lm,
         hp_e_start, hp_e, hp_b_start, hp_b, pair_start, pair_b, chunk_start, pair_chunk,
         pair_rank, rs_pose, rs_rank0, rs_chunk_start, rs_chunk, hp_rs_start, rs_order, rs_cdesc, rs_info, hp_b_lm;
@@ -3043,6 +3126,10 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
     {
         std::vector<int32_t> fill(H.lm_e_start.begin(), H.lm_e_start.end() - 1);
         for (int e = 0; e < ne; e++) H.lm_e[fill[point_h[G->e_point[e]]]++] = e;
+        // OSG_LBA_LMIDENT=0: always through lm_e (A/B runs, the same values)
+        static const bool ident_ok = !(getenv("OSG_LBA_LMIDENT") && atoi(getenv("OSG_LBA_LMIDENT")) == 0);
+        H.lm_e_ident = ident_ok ? 1 : 0;
+        for (int q = 0; q < ne && H.lm_e_ident; q++) H.lm_e_ident = H.lm_e[q] == q;
         // k_linearize's landmark groups: consecutive landmarks with at most EB edges together, a
         // landmark with more alone
         H.lg_start.assign(1, 0);
@@ -3595,7 +3682,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
     // k_schur_rows_c with its gathers two groups ahead (the default since late r06: 6.40 against 6.47 ms per
     // 14 launches, gpurun_out/r06k); OSG_SCHUR_PF=1 one group ahead (A/B runs; the same sums)
     // OSG_SCHUR_PF=3: also the chunk descriptors four chunks ahead (A/B)
-    static const int schur_pf = getenv("OSG_SCHUR_PF") ? std::min(3, std::max(1, atoi(getenv("OSG_SCHUR_PF")))) : 2;
+    static const int schur_pf = getenv("OSG_SCHUR_PF") ? std::min(4, std::max(1, atoi(getenv("OSG_SCHUR_PF")))) : 2;
     // OSG_SCHUR_WPE=5: k_schur_rows_c allocated for 5 waves per SIMD (92 VGPRs, no spills) instead of 6 (A/B)
     static const bool schur_wpe5 = getenv("OSG_SCHUR_WPE") && atoi(getenv("OSG_SCHUR_WPE")) == 5;
     // OSG_SCHUR_HOIST=1: k_schur_rows_c's first gathers issued inside the staging (A/B)
@@ -3786,6 +3873,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         D.hl_point = osg_dptr<int32_t>(din, o.hlpoint);
         D.lm_e_start = osg_dptr<int32_t>(din, o.lmes);
         D.lm_e = osg_dptr<int32_t>(din, o.lme);
+        D.lm_e_ident = h.lm_e_ident;
         D.lg_start = osg_dptr<int32_t>(din, o.lgs);
         D.lm_b_start = osg_dptr<int32_t>(din, o.lmbs);
         D.blk_pose = osg_dptr<int32_t>(din, o.blkpose);
@@ -3914,7 +4002,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         if (mx_nhp > 0) {
             LBA_MARK(KT_SROWS);
             if (compact) {
-                auto sr = schur_pf == 3 ? (schur_wpe5 ? k_schur_rows_c<3, 5> : k_schur_rows_c<3, 6>)
+                auto sr = schur_pf == 4 ? k_schur_rows_c<4, 6>
+                          : schur_pf == 3 ? (schur_wpe5 ? k_schur_rows_c<3, 5> : k_schur_rows_c<3, 6>)
                           : schur_pf == 2 ? (schur_wpe5 ? k_schur_rows_c<2, 5>
                                                         : (schur_hoist ? k_schur_rows_c<2, 6, true> : k_schur_rows_c<2, 6>))
                                           : k_schur_rows_c<1, 6>;

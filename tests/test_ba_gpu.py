@@ -315,9 +315,9 @@ _HPL_VARIANTS = [{"OSG_SCHUR_STAGE": "1"}, {"OSG_SCHUR_DIRECT": "1"}, {"OSG_UPDA
 
 
 @pytest.mark.parametrize("env", [{"OSG_POSE_RED_GATHER": "1"}, {"OSG_SCHUR_POINT": "1"}, {"OSG_LIN_WPE": "4"},
-                                 {"OSG_SCHUR_PF": "1"}, {"OSG_SCHUR_PF": "3"},
+                                 {"OSG_SCHUR_PF": "1"}, {"OSG_SCHUR_PF": "3"}, {"OSG_SCHUR_PF": "4"},
                                  {"OSG_SCHUR_WPE": "5"}, {"OSG_LBA_LREC": "1"},
-                                 {"OSG_SCHUR_HOIST": "1"}]
+                                 {"OSG_SCHUR_HOIST": "1"}, {"OSG_LBA_LMIDENT": "0"}]
                          + _HPL_VARIANTS,
                          ids=lambda e: "-".join(f"{k[4:]}={v}" for k, v in e.items()))
 def test_lba_schur_variants_bit_identical(ctx, env):
@@ -326,9 +326,11 @@ def test_lba_schur_variants_bit_identical(ctx, env):
     inputs gathered through hp_e against the pose-major records (k_hp_rec), Dinv from k_schur_point
     against Dinv formed by its readers, k_linearize compiled for 4 waves per SIMD, and k_schur_rows_c with
     its gathers one group ahead (OSG_SCHUR_PF=1) against two (the default), with the chunk descriptors
-    four chunks ahead (OSG_SCHUR_PF=3), and allocated for 5 waves per SIMD (OSG_SCHUR_WPE=5); the landmark
+    four chunks ahead (OSG_SCHUR_PF=3), with its descriptors preloaded one per lane and branch-free loads
+    (OSG_SCHUR_PF=4), and allocated for 5 waves per SIMD (OSG_SCHUR_WPE=5); the landmark
     terms in one 128-byte record per landmark (OSG_LBA_LREC=1) against three arrays, and k_schur_rows_c's first
-    gathers issued inside its staging (OSG_SCHUR_HOIST=1).  On the whole-Hpl
+    gathers issued inside its staging (OSG_SCHUR_HOIST=1), and k_linearize through lm_e when the edges are in
+    landmark order (OSG_LBA_LMIDENT=0) against its identity shortcut.  On the whole-Hpl
     form (OSG_LBA_HPL=1, which the Hpl-reading variants select): the Schur product's LDS-staged partner
     spans (k_schur_rows_st) and per-lane loads against the per-group gathers (k_schur_rows), and
     k_update's Hpl blocks through LDS pieces or per-thread walks against one thread per block.  The GBA
