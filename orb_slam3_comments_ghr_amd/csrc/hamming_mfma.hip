@@ -661,6 +661,243 @@ __global__ __launch_bounds__(NW * 64) void k_top2_fp4(const uint32_t *__restrict
     }
 }
 
+// The PIPE 3 kernel, persistent (OSG_TOP2_MFMA_SHAPE=13, A/B): one workgroup per CU takes items (frame,
+// query block) item = blockIdx.x, + gridDim.x, ... (the same XCD-aware item -> (frame, block) map), keeps the
+// byte table, and loads the next item's first train chunk during the current item's last chunk, so the per
+// item start (table, first chunk, its barrier) is not paid 16 times per CU.  The same products and key
+// updates in the same order as k_top2_fp4<.., 3>: bit-exact.
+template <int NW, int QT, int CR>
+__global__ __launch_bounds__(NW * 64) void k_top2_fp4p(const uint32_t *__restrict__ query, int nq,
+                                                        const uint32_t *__restrict__ train, int nt,
+                                                        int nqb, int n_items, int32_t *__restrict__ out)
+{
+    constexpr int NT = NW * 64;
+    constexpr int BPT = CR * 32 / NT;
+    constexpr int WPT = BPT / 4;
+    constexpr int TPR = 32 / BPT;
+    constexpr int NTILE = CR / 32;
+    static_assert(CR * 32 % NT == 0 && BPT % 4 == 0 && TPR >= 1, "chunk / workgroup shape");
+    __shared__ __attribute__((aligned(16))) unsigned char s_buf[2 * CR * MX_RS];
+    __shared__ uint32_t s_lut[256];
+
+    const int t = threadIdx.x, lane = t & 63;
+    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int G = gridDim.x;
+    auto logical_of = [&](int item) { return (n_items % 8 == 0) ? (item % 8) * (n_items / 8) + item / 8 : item; };
+    int item = blockIdx.x;
+    if (item >= n_items) return;  // the whole workgroup
+    for (int e = t; e < 256; e += NT) s_lut[e] = spread_nib((uint32_t)e) * 0xCu;
+    const int r = lane & 31, h = lane >> 5;
+    const int lbase = r * MX_RS + h * 16;
+    const int erow = t / TPR, epart = t % TPR;
+    auto load_chunk = [&](const uint32_t *tfp, int c0, uint32_t (&pw)[WPT]) {
+        const int row = c0 + erow;
+        if (row < nt) {
+            const uint32_t *src = tfp + (size_t)row * 8 + epart * WPT;
+#pragma unroll
+            for (int i = 0; i < WPT; i += 2) {
+                const uint2 v = *(const uint2 *)(src + i);
+                pw[i] = v.x;
+                pw[i + 1] = v.y;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < WPT; i++) pw[i] = 0u;
+        }
+    };
+    auto store_chunk = [&](int buf, const uint32_t (&pw)[WPT]) {
+        unsigned char *dst = s_buf + ((size_t)buf * CR + erow) * MX_RS;
+#pragma unroll
+        for (int i = 0; i < WPT; i++) {
+            const uint32_t x = pw[i];
+            *(i32x4 *)(dst + 16 * (epart * WPT + i)) =
+                i32x4{(int)s_lut[x & 0xFFu], (int)s_lut[(x >> 8) & 0xFFu], (int)s_lut[(x >> 16) & 0xFFu],
+                      (int)s_lut[x >> 24]};
+        }
+    };
+    auto frag = [&](const unsigned char *tb, int s) -> i32x8 {
+        const i32x4 v = *(const i32x4 *)(tb + lbase + 32 * s);
+        return i32x8{v[0], v[1], v[2], v[3], 0, 0, 0, 0};
+    };
+    auto mfma = [&](const i32x8 &a, const i32x8 &bb, const f32x16 &c) {
+        return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, bb, c, 4, 4, 0, MX_SCALE_TRAIN, 0, MX_SCALE_ONE);
+    };
+    const int nch = (nt + CR - 1) / CR;
+    {
+        uint32_t pw[WPT];
+        load_chunk(train + (size_t)(logical_of(item) / nqb) * nt * 8, 0, pw);
+        __syncthreads();  // the table
+        store_chunk(0, pw);
+    }
+    __syncthreads();
+    int bufbase = 0;  // the LDS buffer of the item's chunk 0
+    for (; item < n_items; item += G) {
+        const int logical = logical_of(item);
+        const int b = logical / nqb, qb = logical % nqb;
+        const uint32_t *qf = query + (size_t)b * nq * 8;
+        const uint32_t *tf = train + (size_t)b * nt * 8;
+        int32_t *of = out + (size_t)b * nq * 3;
+        const int next = item + G;
+        const uint32_t *tfn = next < n_items ? train + (size_t)(logical_of(next) / nqb) * nt * 8 : nullptr;
+        const int qw0 = qb * (NW * QT * 32) + w * (QT * 32);
+        const bool active = qw0 < nq;
+        i32x8 bq[QT][4];
+        int ka1[QT], ka2[QT], pq[QT];
+#pragma unroll
+        for (int j = 0; j < QT; j++) {
+            const int q = min(qw0 + 32 * j + r, nq - 1);
+            const uint4 lo = *(const uint4 *)(qf + (size_t)q * 8), hi = *(const uint4 *)(qf + (size_t)q * 8 + 4);
+            const uint32_t wd[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+            int pc = 0;
+#pragma unroll
+            for (int k = 0; k < 8; k++) pc += __popc(wd[k]);
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                const uint32_t word = wd[2 * s + h];
+#pragma unroll
+                for (int d = 0; d < 4; d++)
+                    bq[j][s][d] = (int)(0x22222222u | ((~spread_nib(word >> (8 * d)) & 0x11111111u) << 3));
+#pragma unroll
+                for (int d = 4; d < 8; d++) bq[j][s][d] = 0;
+            }
+            pq[j] = pc;
+            ka1[j] = ka2[j] = ((256 - pc) << MF_SHIFT) + MX_KEY0;
+        }
+        // formed per item after the query fragments (held across items it pushed the setup past 128 VGPRs)
+        f32x16 crow;
+#pragma unroll
+        for (int i = 0; i < 16; i++) crow[i] = MX_BIAS + (float)((i & 3) + 8 * (i >> 2) + 4 * h);
+        auto epi = [&](const f32x16 (&acc)[QT]) {
+#pragma unroll
+            for (int j = 0; j < QT; j++) {
+#pragma unroll
+                for (int i = 0; i < 8; i += 2) {
+                    key_push2f(ka1[j], ka2[j], __float_as_int(acc[j][i]), __float_as_int(acc[j][i + 1]));
+                    key_push2f(ka1[j], ka2[j], __float_as_int(acc[j][i + 8]), __float_as_int(acc[j][i + 9]));
+                }
+                ka1[j] -= 32;
+                ka2[j] -= 32;
+            }
+        };
+        auto tile = [&](const unsigned char *tb, const f32x16 &cin) {
+            i32x8 a[4];
+#pragma unroll
+            for (int s = 0; s < 4; s++) a[s] = frag(tb, s);
+            f32x16 acc[QT];
+#pragma unroll
+            for (int j = 0; j < QT; j++) acc[j] = mfma(a[0], bq[j][0], cin);
+#pragma unroll
+            for (int s = 1; s < 4; s++)
+#pragma unroll
+                for (int j = 0; j < QT; j++) acc[j] = mfma(a[s], bq[j][s], acc[j]);
+            epi(acc);
+        };
+        for (int c = 0; c < nch; c++) {
+            const int c0 = c * CR;
+            uint32_t pw[WPT];
+            const bool more_in = c + 1 < nch, more = more_in || tfn != nullptr;
+            if (more_in) load_chunk(tf, c0 + CR, pw);
+            else if (tfn) load_chunk(tfn, 0, pw);  // the next item's first chunk
+            if (active) {
+                const unsigned char *sb = s_buf + (size_t)((c + bufbase) & 1) * CR * MX_RS;
+                const int nfull = min(NTILE, (nt - c0) / 32);
+                if (nfull == NTILE) {
+                    i32x8 a[4];
+                    f32x16 accp[QT], acc[QT];
+#pragma unroll
+                    for (int s = 0; s < 4; s++) a[s] = frag(sb, s);
+#pragma unroll
+                    for (int s = 0; s < 4; s++) {
+#pragma unroll
+                        for (int j = 0; j < QT; j++) accp[j] = mfma(a[s], bq[j][s], s ? accp[j] : crow);
+                        a[s] = frag(sb + 32 * MX_RS, s);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+#pragma unroll
+                    for (int tt = 1; tt < NTILE; tt++) {
+#pragma unroll
+                        for (int s = 0; s < 4; s++) {
+#pragma unroll
+                            for (int j = 0; j < QT; j++) acc[j] = mfma(a[s], bq[j][s], s ? acc[j] : crow);
+                            if (tt + 1 < NTILE) a[s] = frag(sb + (tt + 1) * 32 * MX_RS, s);
+#pragma unroll
+                            for (int j = 0; j < QT; j++) {
+                                key_push2f(ka1[j], ka2[j], __float_as_int(accp[j][2 * s]),
+                                           __float_as_int(accp[j][2 * s + 1]));
+                                key_push2f(ka1[j], ka2[j], __float_as_int(accp[j][8 + 2 * s]),
+                                           __float_as_int(accp[j][9 + 2 * s]));
+                                if (s == 3) {
+                                    ka1[j] -= 32;
+                                    ka2[j] -= 32;
+                                }
+                            }
+                            __builtin_amdgcn_sched_barrier(0);
+                        }
+#pragma unroll
+                        for (int j = 0; j < QT; j++) accp[j] = acc[j];
+                    }
+                    epi(accp);
+                } else {
+#pragma unroll
+                    for (int tt = 0; tt < NTILE; tt++) {
+                        if (tt >= nfull) break;
+                        tile(sb + tt * 32 * MX_RS, crow);
+                    }
+                }
+                const int lim = nt - (c0 + nfull * 32);
+                if (nfull < NTILE && lim > 0) {
+                    f32x16 cin;
+#pragma unroll
+                    for (int i = 0; i < 16; i++)
+                        cin[i] = crow[i] + ((i & 3) + 8 * (i >> 2) + 4 * h >= lim ? MX_PAD : 0.f);
+                    tile(sb + nfull * 32 * MX_RS, cin);
+                }
+            }
+            if (more) store_chunk((c + 1 + bufbase) & 1, pw);
+            __syncthreads();
+        }
+        bufbase = (bufbase + nch) & 1;
+        if (active) {
+            const int base = 32 * ((nt + 31) / 32);
+#pragma unroll
+            for (int j = 0; j < QT; j++) {
+                int k1 = ka1[j], k2 = ka2[j];
+                const int a1 = __shfl_xor(k1, 32), a2 = __shfl_xor(k2, 32);
+                key_merge(k1, k2, a1, a2);
+                const int q = qw0 + 32 * j + r;
+                if (h == 0 && q < nq) {
+                    const int t1 = k1 - MX_KEY0 + base, t2 = k2 - MX_KEY0 + base;
+                    const int d1 = (t1 >> MF_SHIFT) + pq[j], d2 = (t2 >> MF_SHIFT) + pq[j];
+                    of[3 * q + 0] = d1 < 256 ? (t1 & (MF_MAX_ROWS - 1)) : -1;
+                    of[3 * q + 1] = min(d1, 256);
+                    of[3 * q + 2] = min(d2, 256);
+                }
+            }
+        }
+    }
+}
+
+template <int NW, int QT, int CR>
+int launch_fp4p(osg_ctx *ctx, const void *d_query, int nq, const void *d_train, int nt, int nb, void *d_out)
+{
+    const int nqb = (nq + NW * QT * 32 - 1) / (NW * QT * 32);
+    const long long items = (long long)nqb * nb;
+    OSG_REQUIRE(ctx, items <= 0x7FFFFFFF, "grid too large");
+    static int ncu = 0;
+    if (ncu == 0) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+            ncu = n;
+        else
+            ncu = 256;
+    }
+    const int g = (int)std::min<long long>(items, ncu);  // one 16-wave workgroup per CU
+    hipLaunchKernelGGL((k_top2_fp4p<NW, QT, CR>), dim3((unsigned)std::max(g, 1)), dim3(NW * 64), 0, ctx->stream,
+                       (const uint32_t *)d_query, nq, (const uint32_t *)d_train, nt, nqb, (int)items, (int32_t *)d_out);
+    OSG_HIP_CHECK(ctx, hipGetLastError());
+    return OSG_OK;
+}
+
 template <int NW, int QT, int CR, int PIPE>
 int launch_fp4(osg_ctx *ctx, const void *d_query, int nq, const void *d_train, int nt, int nb, void *d_out)
 {
@@ -707,10 +944,10 @@ bool mfma_fp4()
 void mfma_shape_of(bool fp4, int shape, int *d)
 {
     static const int i8[5][4] = {{16, 1, 256, 1}, {8, 2, 256, 1}, {16, 1, 256, 0}, {8, 2, 256, 0}, {8, 1, 256, 1}};
-    static const int f4[13][4] = {{16, 1, 256, 3}, {8, 2, 256, 1}, {16, 1, 256, 0}, {16, 1, 256, 3}, {8, 1, 256, 1},
+    static const int f4[14][4] = {{16, 1, 256, 3}, {8, 2, 256, 1}, {16, 1, 256, 0}, {16, 1, 256, 3}, {8, 1, 256, 1},
                                   {16, 2, 256, 1}, {16, 1, 256, 2}, {16, 1, 256, 1}, {16, 1, 256, 4}, {8, 1, 256, 3},
-                                  {16, 1, 512, 3}, {16, 1, 256, 5}, {16, 1, 512, 5}};
-    const int *s = fp4 ? f4[(shape >= 1 && shape <= 12 && shape != 3) ? shape : 0]
+                                  {16, 1, 512, 3}, {16, 1, 256, 5}, {16, 1, 512, 5}, {16, 1, 256, 6}};
+    const int *s = fp4 ? f4[(shape >= 1 && shape <= 13 && shape != 3) ? shape : 0]
                        : i8[(shape >= 1 && shape <= 4) ? shape : 0];
     for (int i = 0; i < 4; i++) d[i] = s[i];
 }
@@ -751,6 +988,7 @@ int osg_launch_top2_batch_mfma(osg_ctx *ctx, const void *d_query, int32_t nq, co
         case 10: return launch_fp4<16, 1, 512, 3>(ctx, d_query, nq, d_train, nt, nb, d_out);
         case 11: return launch_fp4<16, 1, 256, 5>(ctx, d_query, nq, d_train, nt, nb, d_out);
         case 12: return launch_fp4<16, 1, 512, 5>(ctx, d_query, nq, d_train, nt, nb, d_out);
+        case 13: return launch_fp4p<16, 1, 256>(ctx, d_query, nq, d_train, nt, nb, d_out);
         default: return launch_fp4<16, 1, 256, 3>(ctx, d_query, nq, d_train, nt, nb, d_out);
         }
     }

@@ -117,7 +117,7 @@ def test_batch_plan_tables_match_the_launchers():
         t = re.search(r"static const int " + name + r"\[" + str(n) + r"\]\[4\] = \{(.*?)\};", src, re.S).group(1)
         return [tuple(int(x) for x in row.split(",")) for row in re.findall(r"\{([^{}]*)\}", t)]
 
-    i8, f4 = table("i8", 5), table("f4", 13)
+    i8, f4 = table("i8", 5), table("f4", 14)
     for k, v in switch(i8_sw, "launch").items():
         assert i8[k] == v, (k, v)
     for k, v in switch(fp4_sw, "launch_fp4").items():

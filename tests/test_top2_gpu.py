@@ -185,7 +185,7 @@ def test_batch_empty_train(ctx):
 _VARIANTS = [{"OSG_TOP2_BATCH_MFMA": "0", "OSG_TOP2_BATCH_QL": ql, "OSG_TOP2_BATCH_SCALAR": sc}
              for ql, sc in [("1", "0"), ("2", "0"), ("4", "0"), ("1", "1"), ("4", "1")]]
 _VARIANTS += [{"OSG_TOP2_FP4": "0", "OSG_TOP2_MFMA_SHAPE": sh} for sh in ("0", "1", "2", "3", "4")]
-_VARIANTS += [{"OSG_TOP2_FP4": "1", "OSG_TOP2_MFMA_SHAPE": sh} for sh in ("0", "1", "2", "4", "5", "6", "7", "8", "9", "10", "11", "12")]
+_VARIANTS += [{"OSG_TOP2_FP4": "1", "OSG_TOP2_MFMA_SHAPE": sh} for sh in ("0", "1", "2", "4", "5", "6", "7", "8", "9", "10", "11", "12", "13")]
 
 
 @pytest.mark.parametrize("env", _VARIANTS, ids=lambda e: "-".join(f"{k[9:]}={v}" for k, v in e.items()))
@@ -267,7 +267,8 @@ def _edge_problems():
 @pytest.mark.parametrize("env", [{"OSG_TOP2_FP4": "0"}, {"OSG_TOP2_FP4": "0", "OSG_TOP2_MFMA_SHAPE": "1"},
                                  {"OSG_TOP2_FP4": "1", "OSG_TOP2_MFMA_SHAPE": "1"}, {"OSG_TOP2_FP4": "1", "OSG_TOP2_MFMA_SHAPE": "8"},
                                  {"OSG_TOP2_FP4": "1", "OSG_TOP2_MFMA_SHAPE": "9"}, {"OSG_TOP2_FP4": "1", "OSG_TOP2_MFMA_SHAPE": "10"},
-                                 {"OSG_TOP2_FP4": "1", "OSG_TOP2_MFMA_SHAPE": "11"}, {"OSG_TOP2_FP4": "1", "OSG_TOP2_MFMA_SHAPE": "12"}],
+                                 {"OSG_TOP2_FP4": "1", "OSG_TOP2_MFMA_SHAPE": "11"}, {"OSG_TOP2_FP4": "1", "OSG_TOP2_MFMA_SHAPE": "12"},
+                                 {"OSG_TOP2_FP4": "1", "OSG_TOP2_MFMA_SHAPE": "13"}],
                          ids=lambda e: "-".join(f"{k[9:]}={v}" for k, v in e.items()))
 def test_batch_fp4_edges(oracle, env, tmp_path):
     """The same edge cases on the other matrix-core forms, each against the serial loop: the I8 form
