@@ -93,7 +93,9 @@ struct LbaDev {
     const int32_t *lm_e_start, *lm_e;    // edges per landmark
     int lm_e_ident;                      // lm_e[q] == q for every q (edges given landmark by landmark, as
                                          // LocalBundleAdjustment inserts them): k_linearize skips the lookup
-    const int32_t *lg_start;             // k_linearize's landmark groups: <= EB edges, or one landmark
+    const int32_t *lg_start;             // k_linearize's landmark groups: <= EB edges, or one landmark; on the
+                                         // device {first landmark, its first edge} per group boundary, so a
+                                         // workgroup's edge range is one load, not a load of a load
     const int32_t *lm_b_start;           // blocks per landmark (blocks are numbered landmark-major)
     const int32_t *blk_pose;             // per block: hessian pose index
     const int32_t *edge_blk;             // per edge: 4 block + 2 (block has several edges) + 1 (not its
@@ -351,8 +353,9 @@ __global__ __launch_bounds__(EB) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
     __shared__ double s_m[EB / 64];
     double md = 0.0;
     if (D.nhl > 0) {
-        const int l0 = D.lg_start[bx], l1 = D.lg_start[bx + 1];
-        const int q0 = D.lm_e_start[l0], q1 = D.lm_e_start[l1];
+        typedef int i2 __attribute__((ext_vector_type(2)));
+        const i2 g0 = *(const GLOBAL i2 *)(gbl(D.lg_start) + 2 * bx), g1 = *(const GLOBAL i2 *)(gbl(D.lg_start) + 2 * bx + 2);
+        const int l0 = g0.x, l1 = g1.x, q0 = g0.y, q1 = g1.y;
         const int ol = l0 + (int)threadIdx.x;  // the landmark this thread sums
         const bool owner = ol < l1;
         const int oq0 = owner ? D.lm_e_start[ol] : 0, oq1 = owner ? D.lm_e_start[ol + 1] : 0;
@@ -2966,7 +2969,7 @@ struct LbaHost {
     int max_col_rows = 0;
     bool trivial = false;  // nothing to optimise: the estimates are returned unchanged
     int lm_e_ident = 0;
-    std::vector<int32_t> pose_h, hp_pose, point_h, hl_point, lm_e_start, lm_e, lg_start, lm_b_start, blk_pose, edge_blk, blk_lm,
+    std::vector<int32_t> pose_h, hp_pose, point_h, hl_point, lm_e_start, lm_e, lg_start, lg_lq, lm_b_start, blk_pose, edge_blk, blk_lm,
         hp_e_start, hp_e, hp_b_start, hp_b, pair_start, pair_b, chunk_start, pair_chunk,
         pair_rank, rs_pose, rs_rank0, rs_chunk_start, rs_chunk, hp_rs_start, rs_order, rs_cdesc, rs_info, hp_b_lm;
     int n_rs = 0;
@@ -3140,6 +3143,11 @@ int build_structure(osg_ctx *ctx, const osg_ba_graph *G, LbaHost &H)
             l = l1;
         }
         if (nhl == 0) H.lg_start.push_back(0);
+        H.lg_lq.resize(2 * H.lg_start.size());
+        for (size_t g = 0; g < H.lg_start.size(); g++) {
+            H.lg_lq[2 * g] = H.lg_start[g];
+            H.lg_lq[2 * g + 1] = H.lm_e_start[H.lg_start[g]];
+        }
     }
     STRUCT_CP(2);
     // a map (one large graph per call) builds its structure on host workers; a window (many per batch,
@@ -3765,7 +3773,7 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
         o.hlpoint = pk.add(h.hl_point.data(), 4 * (size_t)nhl);
         o.lmes = pk.add(h.lm_e_start.data(), 4 * (size_t)(nhl + 1));
         o.lme = pk.add(h.lm_e.data(), 4 * (size_t)ne);
-        o.lgs = pk.add(h.lg_start.data(), 4 * h.lg_start.size());
+        o.lgs = pk.add(h.lg_lq.data(), 4 * h.lg_lq.size());
         o.lmbs = pk.add(h.lm_b_start.data(), 4 * (size_t)(nhl + 1));
         o.blkpose = pk.add(h.blk_pose.data(), 4 * (size_t)nblk);
         o.eblk = pk.add(h.edge_blk.data(), 4 * (size_t)ne);
