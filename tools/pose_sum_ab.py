@@ -2,7 +2,8 @@
 """A/B of PoseOptimization's edge-order sums (OSG_POSE_ROWSUM=1 whole rows with the loads kept ahead,
 =0 the per-chunk sums): single-call wall and kernel time of the drop-in's one-frame call (318-edge
 pinhole frame, 600-edge KB8 two-camera frame) and the kernel time of a 256-frame batch, the variants
-alternating.  One JSON line per (variant, repeat)."""
+alternating.  One JSON line per (variant, repeat).  argv[1] names another 0/1 switch to alternate
+instead (OSG_POSE_LANES: the solve and exp-map update spread over wave 0's lanes)."""
 import ctypes as C
 import json
 import os
@@ -40,14 +41,15 @@ def main():
         r = _abi.OsgPoseResult()
         ob = np.zeros(P.n, np.uint8)
         r.outlier = ob.ctypes.data
-        singles.append((n_edges, ps, r, ob))
+        singles.append((n_edges, ps, r, ob, P))  # P keeps the arrays ps points at alive
     batch = [op.synth_pose_problem(rng, n_edges=int(rng.integers(200, 600))) for _ in range(256)]
     opt = op.Optimizer(ctx)
-    for rep in range(2):
+    sw = sys.argv[1] if len(sys.argv) > 1 else "OSG_POSE_ROWSUM"
+    for rep in range(3 if len(sys.argv) > 1 else 2):
         for var in ["0", "1"]:
-            os.environ["OSG_POSE_ROWSUM"] = var
-            d = {"rowsum": var, "rep": rep}
-            for n_edges, ps, r, _ in singles:
+            os.environ[sw] = var
+            d = {sw: var, "rep": rep}
+            for n_edges, ps, r, *_ in singles:
                 w = med(lambda: lib.osg_pose_optimization(h, C.byref(ps), C.byref(r)))
                 ks = []
                 for _ in range(20):
@@ -62,7 +64,7 @@ def main():
                 ks.append(ctx.last_kernel_ms() * 1e3)
             d["batch256_kernel_us"] = round(float(np.median(ks)), 1)
             print(json.dumps(d), flush=True)
-    os.environ.pop("OSG_POSE_ROWSUM", None)
+    os.environ.pop(sw, None)
     ctx.close()
 
 
