@@ -196,17 +196,19 @@ def test_batch_query_per_lane_variants(oracle, env):
     nt = 2100: a partial LDS chunk and a partial 32-row tile."""
     import subprocess
     import sys
+    out = f"/tmp/_osg_batch_ql_{__import__('os').getpid()}.npy"  # per process: concurrent suites do not share it
     code = ("import numpy as np, torch\n"
             "from orb_slam3_comments_ghr_amd import Context, synth\n"
             "from tests.test_top2_gpu import _batch\n"
             "ctx = Context(0)\n"
             "qs, ts = zip(*[synth.descriptors_c2(333, 2100, seed=5 + b) for b in range(3)])\n"
-            "np.save('/tmp/_osg_batch_ql.npy', _batch(ctx, qs, ts))\n")
+            f"np.save({out!r}, _batch(ctx, qs, ts))\n")
     env = dict(__import__("os").environ, **env)
     root = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
-    got = np.load("/tmp/_osg_batch_ql.npy")
+    got = np.load(out)
+    __import__("os").remove(out)
     qs, ts = zip(*[synth.descriptors_c2(333, 2100, seed=5 + b) for b in range(3)])
     for b in range(3):
         for k, ref in enumerate(otop2(oracle, qs[b], ts[b])):
