@@ -2610,6 +2610,10 @@ __global__ __launch_bounds__(1024) void k_chol_back_large(const LbaDev *__restri
 // substitution) and k_back_copy moves it to x.  The work is the envelope's O(n bw), spread over the
 // chip, instead of one workgroup streaming the whole triangle through LDS.
 constexpr int BSC = 256;  // columns per workgroup of k_back_step
+// PRE (the default; OSG_BACK_PRE=0 for the previous order, bit-identical): the thread's 32 L entries and the
+// 32 x 32 Linv column are loaded before y'_bi, which the previous step wrote, so a step waits out one memory
+// round trip instead of three in a row (y', then Linv, then L); the sums are the same, in the same order.
+template <bool PRE>
 __global__ __launch_bounds__(BSC) void k_back_step(const LbaDev *__restrict__ Ds, int step)
 {
     LBA_GRAPH(M_ACT);
@@ -2622,24 +2626,46 @@ __global__ __launch_bounds__(BSC) void k_back_step(const LbaDev *__restrict__ Ds
     if (bx > 0 && c0 + (bx - 1) * BSC >= k0) return;
     __shared__ double s_rhs[CB], s_x[CB];
     const int tid = threadIdx.x;
+    const double *A = D.Hs;
+    const int u = c0 + (bx - 1) * BSC + tid;
+    double a[CB], li[CB];
+    if (PRE) {
+        if (bx > 0 && u < k0) {
+            const HsBlk bb = hs_blk(D, n, bi);
+#pragma unroll
+            for (int r = 0; r < CB; r++) a[r] = r < nb ? A[hs_el(bb, r, u)] : 0.0;
+        }
+        if (tid < CB)
+#pragma unroll
+            for (int r = 0; r < CB; r++) li[r] = D.Linv[(size_t)min(k0 + r, n - 1) * CB + tid];
+    }
     if (tid < CB) s_rhs[tid] = tid < nb ? D.x[k0 + tid] : 0.0;
     __syncthreads();
     if (tid < CB) {
         double xv = 0.0;
+        if (PRE) {
 #pragma unroll
-        for (int r = 0; r < CB; r++) xv += D.Linv[(size_t)min(k0 + r, n - 1) * CB + tid] * s_rhs[r];
+            for (int r = 0; r < CB; r++) xv += li[r] * s_rhs[r];
+        } else {
+#pragma unroll
+            for (int r = 0; r < CB; r++) xv += D.Linv[(size_t)min(k0 + r, n - 1) * CB + tid] * s_rhs[r];
+        }
         s_x[tid] = tid < nb ? xv : 0.0;
         if (bx == 0 && tid < nb) D.bs[k0 + tid] = xv;
     }
     __syncthreads();
     if (bx == 0) return;  // workgroup 0 solved the block; 1.. update the columns
-    const int u = c0 + (bx - 1) * BSC + tid;
     if (u >= k0) return;
-    const double *A = D.Hs;
     double acc = 0.0;
-    const HsBlk bb = hs_blk(D, n, bi);
+    if (PRE) {
+#pragma unroll
+        for (int r = 0; r < CB; r++)
+            if (r < nb) acc += a[r] * s_x[r];
+    } else {
+        const HsBlk bb = hs_blk(D, n, bi);
 #pragma unroll 8
-    for (int r = 0; r < nb; r++) acc += A[hs_el(bb, r, u)] * s_x[r];
+        for (int r = 0; r < nb; r++) acc += A[hs_el(bb, r, u)] * s_x[r];
+    }
     D.x[u] -= acc;
 }
 __global__ __launch_bounds__(EB) void k_back_copy(const LbaDev *__restrict__ Ds)
@@ -4057,6 +4083,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
             hipLaunchKernelGGL(k_chol_back, yb, dim3(1024), 0, ctx->stream, d_dev);
             if (any_col) hipLaunchKernelGGL(k_chol_back_large, yb, dim3(1024), 0, ctx->stream, d_dev);
             if (huge_col) {
+                const char *bp = getenv("OSG_BACK_PRE");  // tests pin the variant (read per call)
+                const bool back_pre = !(bp && atoi(bp) == 0);
                 for (int step = 0; step < mx_red; step++) {
                     int cols = 0;
                     for (int a = 0; a < NA; a++) {
@@ -4064,7 +4092,10 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
                         const int bi = h.nblk_red - 1 - step;
                         if (6 * h.nhp > CMAX_LARGE && bi >= 0) cols = std::max(cols, CB * (bi - h.blk_first[bi]));
                     }
-                    hipLaunchKernelGGL(k_back_step, gx(1 + (cols + BSC - 1) / BSC), dim3(BSC), 0, ctx->stream, d_dev, step);
+                    if (back_pre)
+                        hipLaunchKernelGGL(k_back_step<true>, gx(1 + (cols + BSC - 1) / BSC), dim3(BSC), 0, ctx->stream, d_dev, step);
+                    else
+                        hipLaunchKernelGGL(k_back_step<false>, gx(1 + (cols + BSC - 1) / BSC), dim3(BSC), 0, ctx->stream, d_dev, step);
                 }
                 hipLaunchKernelGGL(k_back_copy, gx((6 * mx_nhp + EB - 1) / EB), dim3(EB), 0, ctx->stream, d_dev);
             }

@@ -497,6 +497,23 @@ def test_gba_map_loop_closed(ctx, oracle, n_kf, n_pts):
     assert got.chi2_final < 0.2 * got.chi2_initial and got.iterations >= 5
 
 
+def test_gba_back_step_prefetch_bit_identical(ctx, monkeypatch):
+    """k_back_step (the back-substitution past 1024 free KeyFrames) with its L and Linv loads issued before
+    y' (default) and in the previous order (OSG_BACK_PRE=0): the same sums in the same order, so the
+    1500-KF loop-closed map ends bit for bit the same."""
+    G = op.synth_map_graph(np.random.default_rng(4200 + 1500), n_kf=1500, n_points=150000, loop=True)
+    res = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("OSG_BACK_PRE", v)
+        res[v] = op.Optimizer(ctx).BundleAdjustment(G)
+    a, b = res["0"], res["1"]
+    assert (a.iterations, a.trials) == (b.iterations, b.trials)
+    assert a.chi2_initial == b.chi2_initial and a.chi2_final == b.chi2_final
+    np.testing.assert_array_equal(a.pose, b.pose)
+    np.testing.assert_array_equal(a.point, b.point)
+    np.testing.assert_array_equal(a.edge_bad, b.edge_bad)
+
+
 def test_gba_loop_map_device_bytes_on_envelope():
     """The 1500-KF loop-closed map's reduced system lives on its envelope tiles (hs_at), not as the
     dense 8 994^2 matrix (647 MB): a fresh context's arena after one call stays under 0.5 GB."""
