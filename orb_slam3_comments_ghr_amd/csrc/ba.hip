@@ -2498,6 +2498,10 @@ __global__ __launch_bounds__(1024) void k_chol_back(const LbaDev *__restrict__ D
 // forward-substitution right-hand side b_t -= L_tj y_j.  The column launches then read their tiles as
 // they stand (K = 0): the O(n^3) work is spread over (nblk - j)^2 / 2 workgroups per step instead of
 // one K-long GEMM per row block (which left one CU per row block MFMA-bound at large n).
+// PRE (the default; OSG_TRAIL_PRE=0 for the previous order, bit-identical): the thread's four target
+// entries A_tu (and a diagonal tile's b_t / y_j) are loaded with the L tiles, before the MFMA, instead of
+// after it: one memory round trip per workgroup instead of two in a row.
+template <bool PRE>
 __global__ __launch_bounds__(256) void k_chol_trail(const LbaDev *__restrict__ Ds, int j)
 {
     LBA_GRAPH(M_ACT);
@@ -2517,14 +2521,28 @@ __global__ __launch_bounds__(256) void k_chol_trail(const LbaDev *__restrict__ D
     __shared__ double sLt[CB][CB + 1], sLu[CB][CB + 1];
     const int tid = threadIdx.x;
     const HsBlk bt = hs_blk(D, n, tb), bu = hs_blk(D, n, ub);
+    const int w = tid >> 6, l = tid & 63;
+    const int qr = (w >> 1) * 16, qc = (w & 1) * 16;
+    double old[4], bsv = 0.0, yv[CB];
+    if (PRE) {
+        const int c = qc + (l & 15);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int r = qr + (l >> 4) + 4 * q;
+            old[q] = (R0 + r < n && C0 + c < n) ? D.Hs[hs_el(bt, r, C0 + c)] : 0.0;
+        }
+        if (t == u && tid < CB && R0 + tid < n) {
+            bsv = D.bs[R0 + tid];
+#pragma unroll
+            for (int k = 0; k < CB; k++) yv[k] = D.x[K0 + k];
+        }
+    }
     for (int e = tid; e < CB * CB; e += 256) {
         const int r = e >> 5, c = e & 31;
         sLt[r][c] = (R0 + r < n) ? D.Hs[hs_el(bt, r, K0 + c)] : 0.0;
         sLu[r][c] = (C0 + r < n) ? D.Hs[hs_el(bu, r, K0 + c)] : 0.0;
     }
     __syncthreads();
-    const int w = tid >> 6, l = tid & 63;
-    const int qr = (w >> 1) * 16, qc = (w & 1) * 16;
     d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int ks = 0; ks < CB / 4; ks++) {
@@ -2535,13 +2553,22 @@ __global__ __launch_bounds__(256) void k_chol_trail(const LbaDev *__restrict__ D
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int r = qr + (l >> 4) + 4 * q;
-        if (R0 + r < n && C0 + c < n) D.Hs[hs_el(bt, r, C0 + c)] -= acc[q];
+        if (R0 + r < n && C0 + c < n) {
+            if (PRE) D.Hs[hs_el(bt, r, C0 + c)] = old[q] - acc[q];
+            else D.Hs[hs_el(bt, r, C0 + c)] -= acc[q];
+        }
     }
     if (t == u && tid < CB && R0 + tid < n) {  // block j is full (m > 0): y_j is 32 entries
         double s = 0.0;
+        if (PRE) {
+#pragma unroll
+            for (int k = 0; k < CB; k++) s += sLt[tid][k] * yv[k];
+            D.bs[R0 + tid] = bsv - s;
+        } else {
 #pragma unroll 8
-        for (int k = 0; k < CB; k++) s += sLt[tid][k] * D.x[K0 + k];
-        D.bs[R0 + tid] -= s;
+            for (int k = 0; k < CB; k++) s += sLt[tid][k] * D.x[K0 + k];
+            D.bs[R0 + tid] -= s;
+        }
     }
 }
 
@@ -4061,6 +4088,8 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
                 if (chol_elim == 4) hipLaunchKernelGGL(k_chol_env<4>, yb, dim3(CD_T), 0, ctx->stream, d_dev);
                 else hipLaunchKernelGGL(k_chol_env<2>, yb, dim3(CD_T), 0, ctx->stream, d_dev);
             }
+            const char *tp = getenv("OSG_TRAIL_PRE");  // tests pin the variant (read per call)
+            const bool trail_pre = !(tp && atoi(tp) == 0);
             if (any_col) for (int jb = 0; jb < mx_red; jb++) {  // row blocks at and below the diagonal block
                 // past CMAX only the envelope's rows: grids sized by the largest reach of any graph
                 int rows = 0, m = 0;
@@ -4076,8 +4105,12 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
                 if (rows == 0) continue;
                 if (chol_elim == 4) hipLaunchKernelGGL(k_chol_col<4>, gx(rows), dim3(256), 0, ctx->stream, d_dev, jb);
                 else hipLaunchKernelGGL(k_chol_col<2>, gx(rows), dim3(256), 0, ctx->stream, d_dev, jb);
-                if (large && m > 0)
-                    hipLaunchKernelGGL(k_chol_trail, gx(m * (m + 1) / 2), dim3(256), 0, ctx->stream, d_dev, jb);
+                if (large && m > 0) {
+                    if (trail_pre)
+                        hipLaunchKernelGGL(k_chol_trail<true>, gx(m * (m + 1) / 2), dim3(256), 0, ctx->stream, d_dev, jb);
+                    else
+                        hipLaunchKernelGGL(k_chol_trail<false>, gx(m * (m + 1) / 2), dim3(256), 0, ctx->stream, d_dev, jb);
+                }
             }
             LBA_MARK(KT_BACK);
             hipLaunchKernelGGL(k_chol_back, yb, dim3(1024), 0, ctx->stream, d_dev);

@@ -497,14 +497,16 @@ def test_gba_map_loop_closed(ctx, oracle, n_kf, n_pts):
     assert got.chi2_final < 0.2 * got.chi2_initial and got.iterations >= 5
 
 
-def test_gba_back_step_prefetch_bit_identical(ctx, monkeypatch):
+@pytest.mark.parametrize("var", ["OSG_BACK_PRE", "OSG_TRAIL_PRE"])
+def test_gba_back_step_prefetch_bit_identical(ctx, monkeypatch, var):
     """k_back_step (the back-substitution past 1024 free KeyFrames) with its L and Linv loads issued before
-    y' (default) and in the previous order (OSG_BACK_PRE=0): the same sums in the same order, so the
+    y' (default) and in the previous order (OSG_BACK_PRE=0); k_chol_trail with its target tile loaded
+    before the MFMA (default) and after it (OSG_TRAIL_PRE=0): the same sums in the same order, so the
     1500-KF loop-closed map ends bit for bit the same."""
     G = op.synth_map_graph(np.random.default_rng(4200 + 1500), n_kf=1500, n_points=150000, loop=True)
     res = {}
     for v in ("0", "1"):
-        monkeypatch.setenv("OSG_BACK_PRE", v)
+        monkeypatch.setenv(var, v)
         res[v] = op.Optimizer(ctx).BundleAdjustment(G)
     a, b = res["0"], res["1"]
     assert (a.iterations, a.trials) == (b.iterations, b.trials)
