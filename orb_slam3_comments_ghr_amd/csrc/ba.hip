@@ -2577,6 +2577,9 @@ __global__ __launch_bounds__(256) void k_chol_trail(const LbaDev *__restrict__ D
 // L_kk^-1 tile read from Linv when the block is reached instead of staged up front.
 constexpr int CMAX_LARGE = 6144;  // 1024 free poses
 
+// PRE (the default; OSG_BACKL_PRE=0 for the previous order, bit-identical): block bi - 1's Linv entry is
+// loaded while block bi is solved, so a block does not start with a global round trip.
+template <bool PRE>
 __global__ __launch_bounds__(1024) void k_chol_back_large(const LbaDev *__restrict__ Ds)
 {
     LBA_GRAPH(M_ACT);
@@ -2595,9 +2598,15 @@ __global__ __launch_bounds__(1024) void k_chol_back_large(const LbaDev *__restri
     }
     const int nblk = (n + CB - 1) / CB;
     const int c = tid & 31, g = tid >> 5;
+    double li_next = PRE ? D.Linv[(size_t)min((nblk - 1) * CB + (tid >> 5), n - 1) * CB + (tid & 31)] : 0.0;
     for (int bi = nblk - 1; bi >= 0; bi--) {
         const int k0 = bi * CB, nb = min(CB, n - k0);
-        s_li[tid] = D.Linv[(size_t)min(k0 + (tid >> 5), n - 1) * CB + (tid & 31)];
+        if (PRE) {
+            s_li[tid] = li_next;
+            if (bi > 0) li_next = D.Linv[(size_t)min(k0 - CB + (tid >> 5), n - 1) * CB + (tid & 31)];
+        } else {
+            s_li[tid] = D.Linv[(size_t)min(k0 + (tid >> 5), n - 1) * CB + (tid & 31)];
+        }
         __syncthreads();
         // the rows below the block inside the envelope only (column block bi's envelope rows, ascending):
         // every other L entry of this column is zero, and is not stored (k_schur_pairs writes only the
@@ -4114,7 +4123,11 @@ int lba_batch(osg_ctx *ctx, const osg_ba_graph *graphs, osg_ba_result *results, 
             }
             LBA_MARK(KT_BACK);
             hipLaunchKernelGGL(k_chol_back, yb, dim3(1024), 0, ctx->stream, d_dev);
-            if (any_col) hipLaunchKernelGGL(k_chol_back_large, yb, dim3(1024), 0, ctx->stream, d_dev);
+            if (any_col) {
+                const char *lp = getenv("OSG_BACKL_PRE");  // tests pin the variant (read per call)
+                if (!(lp && atoi(lp) == 0)) hipLaunchKernelGGL(k_chol_back_large<true>, yb, dim3(1024), 0, ctx->stream, d_dev);
+                else hipLaunchKernelGGL(k_chol_back_large<false>, yb, dim3(1024), 0, ctx->stream, d_dev);
+            }
             if (huge_col) {
                 const char *bp = getenv("OSG_BACK_PRE");  // tests pin the variant (read per call)
                 const bool back_pre = !(bp && atoi(bp) == 0);

@@ -497,13 +497,15 @@ def test_gba_map_loop_closed(ctx, oracle, n_kf, n_pts):
     assert got.chi2_final < 0.2 * got.chi2_initial and got.iterations >= 5
 
 
-@pytest.mark.parametrize("var", ["OSG_BACK_PRE", "OSG_TRAIL_PRE"])
-def test_gba_back_step_prefetch_bit_identical(ctx, monkeypatch, var):
+@pytest.mark.parametrize("var,n_kf,n_pts", [("OSG_BACK_PRE", 1500, 150000), ("OSG_TRAIL_PRE", 1500, 150000),
+                                           ("OSG_BACKL_PRE", 400, 40000)])
+def test_gba_back_step_prefetch_bit_identical(ctx, monkeypatch, var, n_kf, n_pts):
     """k_back_step (the back-substitution past 1024 free KeyFrames) with its L and Linv loads issued before
     y' (default) and in the previous order (OSG_BACK_PRE=0); k_chol_trail with its target tile loaded
     before the MFMA (default) and after it (OSG_TRAIL_PRE=0): the same sums in the same order, so the
-    1500-KF loop-closed map ends bit for bit the same."""
-    G = op.synth_map_graph(np.random.default_rng(4200 + 1500), n_kf=1500, n_points=150000, loop=True)
+    1500-KF loop-closed map ends bit for bit the same.  k_chol_back_large (400 KF) with the next block's Linv
+    loaded during the current block (default) and at the block's start (OSG_BACKL_PRE=0): likewise."""
+    G = op.synth_map_graph(np.random.default_rng(4200 + n_kf), n_kf=n_kf, n_points=n_pts, loop=True)
     res = {}
     for v in ("0", "1"):
         monkeypatch.setenv(var, v)
